@@ -1,0 +1,194 @@
+"""Torch binding of the C ABI with the reference's ``_C`` surface.
+
+Mirrors ``diff_gaussian_rasterization._C`` (ext.cpp:15-20) argument for
+argument, so the Python wrapper in ``dge_amd.diff_gaussian_rasterization``
+reads like the reference's:
+
+  rasterize_gaussians            <- RasterizeGaussiansCUDA          rasterize_points.cu:35-95
+  rasterize_gaussians_backward   <- RasterizeGaussiansBackwardCUDA  rasterize_points.cu:97-157
+  mark_visible                   <- markVisible                     rasterize_points.cu:159-175
+  apply_weights                  <- applyWeightsGaussiansCUDA       rasterize_points.cu:177-234
+
+Empty tensors mean "absent" and become NULL pointers, as in the reference.
+The opaque geometry/binning/image byte buffers are torch uint8 tensors
+allocated through the C ABI's allocator callback (the reference's resize
+functors, rasterize_points.cu:27-33) on the caller's current stream.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _native as N
+
+
+def _ptr(t):
+    """Device address of a tensor, or None for an absent (empty/None) one."""
+    if t is None or t.numel() == 0:
+        return None
+    return t.data_ptr()
+
+
+def _f32(t, name):
+    """contiguous float32 view (the reference's .contiguous().data<float>())."""
+    if t is None or t.numel() == 0:
+        return t
+    if t.dtype != torch.float32:
+        raise RuntimeError(f"{name} must be float32 (got {t.dtype})")
+    return t.contiguous()
+
+
+class _Allocator:
+    """gs_alloc_fn backed by the torch caching allocator."""
+
+    def __init__(self, device):
+        self.device = device
+        self.buffers = [torch.empty(0, dtype=torch.uint8, device=device) for _ in range(3)]
+
+        def cb(_ctx, which, nbytes):
+            buf = torch.empty(int(nbytes), dtype=torch.uint8, device=self.device)
+            self.buffers[which] = buf
+            return buf.data_ptr() if nbytes else None
+
+        self.fn = N.ALLOC_FN(cb)
+
+
+def _settings(bg, viewmatrix, projmatrix, campos, tanfovx, tanfovy, H, W, sh_degree, scale_modifier, prefiltered,
+              debug):
+    keep = [_f32(bg, "bg"), _f32(viewmatrix, "viewmatrix"), _f32(projmatrix, "projmatrix"), _f32(campos, "campos")]
+    s = N.GsSettings()
+    s.image_height = int(H)
+    s.image_width = int(W)
+    s.tanfovx = float(tanfovx)
+    s.tanfovy = float(tanfovy)
+    s.bg = _ptr(keep[0])
+    s.scale_modifier = float(scale_modifier)
+    s.viewmatrix = _ptr(keep[1])
+    s.projmatrix = _ptr(keep[2])
+    s.sh_degree = int(sh_degree)
+    s.campos = _ptr(keep[3])
+    s.prefiltered = int(bool(prefiltered))
+    s.debug = int(bool(debug))
+    return s, keep
+
+
+def _stream(device):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations, scale_modifier, cov3D_precomp,
+                        viewmatrix, projmatrix, tan_fovx, tan_fovy, image_height, image_width, sh, degree, campos,
+                        prefiltered, debug):
+    if means3D.ndimension() != 2 or means3D.size(1) != 3:
+        raise RuntimeError("means3D must have dimensions (num_points, 3)")
+    N.require_gpu(means3D)
+    dev = means3D.device
+    P = means3D.size(0)
+    H, W = int(image_height), int(image_width)
+    with torch.cuda.device(dev):
+        means3D = _f32(means3D, "means3D")
+        colors, opacity = _f32(colors, "colors"), _f32(opacity, "opacity")
+        scales, rotations = _f32(scales, "scales"), _f32(rotations, "rotations")
+        cov3D_precomp, sh = _f32(cov3D_precomp, "cov3D_precomp"), _f32(sh, "sh")
+        out_color = torch.empty((3, H, W), dtype=torch.float32, device=dev)
+        out_depth = torch.empty((1, H, W), dtype=torch.float32, device=dev)
+        radii = torch.empty((P,), dtype=torch.int32, device=dev)
+        M = sh.size(1) if sh is not None and sh.numel() != 0 else 0
+        s, keep = _settings(background, viewmatrix, projmatrix, campos, tan_fovx, tan_fovy, H, W, degree,
+                            scale_modifier, prefiltered, debug)
+        alloc = _Allocator(dev)
+        nr = ctypes.c_int(0)
+        rc = N.lib().gs_rasterize_forward(ctypes.byref(s), P, M, _ptr(means3D), _ptr(sh), _ptr(colors), _ptr(opacity),
+                                          _ptr(scales), _ptr(rotations), _ptr(cov3D_precomp), _ptr(out_color),
+                                          _ptr(out_depth), _ptr(radii), alloc.fn, None, _stream(dev), ctypes.byref(nr))
+        N.check(rc, "rasterize_gaussians")
+        if P == 0:
+            radii.zero_()
+        geom, binning, img = alloc.buffers
+        del keep
+        return nr.value, out_color, out_depth, radii, geom, binning, img
+
+
+def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rotations, scale_modifier, cov3D_precomp,
+                                 viewmatrix, projmatrix, tan_fovx, tan_fovy, dL_dout_color, sh, degree, campos,
+                                 geomBuffer, R, binningBuffer, imageBuffer, debug):
+    N.require_gpu(means3D)
+    dev = means3D.device
+    P = means3D.size(0)
+    H, W = int(dL_dout_color.size(1)), int(dL_dout_color.size(2))
+    M = sh.size(1) if sh is not None and sh.numel() != 0 else 0
+    with torch.cuda.device(dev):
+        opts = dict(dtype=torch.float32, device=dev)
+        out = (torch.empty((P, 3), **opts), torch.empty((P, 3), **opts), torch.empty((P, 1), **opts),
+               torch.empty((P, 3), **opts), torch.empty((P, 6), **opts), torch.empty((P, M, 3), **opts),
+               torch.empty((P, 3), **opts), torch.empty((P, 4), **opts))
+        if P == 0:
+            return out
+        means3D = _f32(means3D, "means3D")
+        colors, sh = _f32(colors, "colors"), _f32(sh, "sh")
+        scales, rotations = _f32(scales, "scales"), _f32(rotations, "rotations")
+        cov3D_precomp = _f32(cov3D_precomp, "cov3D_precomp")
+        radii = radii.contiguous()
+        if radii.dtype != torch.int32:
+            raise RuntimeError("radii must be int32")
+        grad = _f32(dL_dout_color, "dL_dout_color")
+        s, keep = _settings(background, viewmatrix, projmatrix, campos, tan_fovx, tan_fovy, H, W, degree,
+                            scale_modifier, False, debug)
+        dmeans2D, dcolors, dopac, dmeans3D, dcov, dsh, dscales, drot = out
+        rc = N.lib().gs_rasterize_backward(
+            ctypes.byref(s), P, M, int(R), _ptr(means3D), _ptr(sh), _ptr(colors), _ptr(scales), _ptr(rotations),
+            _ptr(cov3D_precomp), _ptr(radii), _ptr(geomBuffer), _ptr(binningBuffer), _ptr(imageBuffer), _ptr(grad),
+            _ptr(dmeans2D), _ptr(dcolors), _ptr(dopac), _ptr(dmeans3D), _ptr(dcov), _ptr(dsh), _ptr(dscales),
+            _ptr(drot), _stream(dev))
+        N.check(rc, "rasterize_gaussians_backward")
+        del keep
+        return out
+
+
+def mark_visible(means3D, viewmatrix, projmatrix):
+    N.require_gpu(means3D)
+    dev = means3D.device
+    P = means3D.size(0)
+    with torch.cuda.device(dev):
+        present = torch.zeros((P,), dtype=torch.bool, device=dev)
+        if P == 0:
+            return present
+        m = _f32(means3D, "means3D")
+        v = _f32(viewmatrix, "viewmatrix")
+        p = _f32(projmatrix, "projmatrix")
+        rc = N.lib().gs_mark_visible(P, _ptr(m), _ptr(v), _ptr(p), _ptr(present), _stream(dev))
+        N.check(rc, "mark_visible")
+        return present
+
+
+def apply_weights(background, means3D, weights, opacity, scales, rotations, scale_modifier, cov3D_precomp, viewmatrix,
+                  projmatrix, tan_fovx, tan_fovy, image_height, image_width, sh, degree, campos, prefiltered,
+                  image_weights, cnt, debug):
+    if means3D.ndimension() != 2 or means3D.size(1) != 3:
+        raise RuntimeError("means3D must have dimensions (num_points, 3)")
+    N.require_gpu(means3D)
+    dev = means3D.device
+    P = means3D.size(0)
+    C = int(image_weights.size(0))
+    if P == 0:
+        return None
+    if not (weights.is_contiguous() and cnt.is_contiguous()):
+        raise RuntimeError("apply_weights updates weights and cnt in place: they must be contiguous")
+    if weights.dtype != torch.float32 or cnt.dtype != torch.int32:
+        raise RuntimeError("weights must be float32 and cnt int32")
+    with torch.cuda.device(dev):
+        means3D, opacity = _f32(means3D, "means3D"), _f32(opacity, "opacity")
+        scales, rotations = _f32(scales, "scales"), _f32(rotations, "rotations")
+        cov3D_precomp, sh = _f32(cov3D_precomp, "cov3D_precomp"), _f32(sh, "sh")
+        iw = _f32(image_weights, "image_weights")
+        M = sh.size(1) if sh is not None and sh.numel() != 0 else 0
+        s, keep = _settings(background, viewmatrix, projmatrix, campos, tan_fovx, tan_fovy, image_height, image_width,
+                            degree, scale_modifier, prefiltered, debug)
+        alloc = _Allocator(dev)
+        rc = N.lib().gs_apply_weights(ctypes.byref(s), P, M, _ptr(means3D), _ptr(weights), C, _ptr(opacity),
+                                      _ptr(scales), _ptr(rotations), _ptr(cov3D_precomp), _ptr(sh), _ptr(iw),
+                                      _ptr(cnt), alloc.fn, None, _stream(dev))
+        N.check(rc, "apply_weights")
+        del keep, alloc
+        return None

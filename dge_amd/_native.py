@@ -1,0 +1,115 @@
+"""Loader for libgs_raster.so, the gfx950 kernels behind include/gs_raster.h.
+
+There is deliberately NO fallback: if the shared library is missing or no
+ROCm GPU is visible, every entry point raises.  (The CPU restatement under
+``oracle/`` is test infrastructure and is never imported from here.)
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libgs_raster.so")
+HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "gs_raster.h")
+
+GS_OK = 0
+GS_ERR_INVALID_ARG = 1
+GS_ERR_HIP = 2
+GS_ERR_ALLOC = 3
+GS_ERR_PREFILTERED = 4
+GS_ERR_UNSUPPORTED = 5
+
+_fp = ctypes.c_void_p  # device pointers travel as opaque addresses
+
+
+class GsSettings(ctypes.Structure):
+    """struct gs_settings (include/gs_raster.h)."""
+
+    _fields_ = [
+        ("image_height", ctypes.c_int),
+        ("image_width", ctypes.c_int),
+        ("tanfovx", ctypes.c_float),
+        ("tanfovy", ctypes.c_float),
+        ("bg", _fp),
+        ("scale_modifier", ctypes.c_float),
+        ("viewmatrix", _fp),
+        ("projmatrix", _fp),
+        ("sh_degree", ctypes.c_int),
+        ("campos", _fp),
+        ("prefiltered", ctypes.c_int),
+        ("debug", ctypes.c_int),
+    ]
+
+
+ALLOC_FN = ctypes.CFUNCTYPE(ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t)
+
+# Every symbol include/gs_raster.h declares, with its ctypes signature.
+SIGNATURES = {
+    "gs_rasterize_forward": (ctypes.c_int, [ctypes.POINTER(GsSettings), ctypes.c_int, ctypes.c_int] + [_fp] * 10
+                             + [ALLOC_FN, ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)]),
+    "gs_rasterize_backward": (ctypes.c_int, [ctypes.POINTER(GsSettings), ctypes.c_int, ctypes.c_int, ctypes.c_int]
+                              + [_fp] * 19 + [ctypes.c_void_p]),
+    "gs_mark_visible": (ctypes.c_int, [ctypes.c_int, _fp, _fp, _fp, _fp, ctypes.c_void_p]),
+    "gs_apply_weights": (ctypes.c_int, [ctypes.POINTER(GsSettings), ctypes.c_int, ctypes.c_int, _fp, _fp, ctypes.c_int]
+                         + [_fp] * 7 + [ALLOC_FN, ctypes.c_void_p, ctypes.c_void_p]),
+    "gs_geometry_buffer_size": (ctypes.c_size_t, [ctypes.c_int]),
+    "gs_image_buffer_size": (ctypes.c_size_t, [ctypes.c_int, ctypes.c_int]),
+    "gs_binning_buffer_size": (ctypes.c_size_t, [ctypes.c_int, ctypes.c_int]),
+    "gs_buffer_offset": (ctypes.c_longlong, [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_int,
+                                             ctypes.c_int, ctypes.c_int]),
+    "gs_last_error": (ctypes.c_char_p, []),
+    "gs_abi_version": (ctypes.c_int, []),
+}
+
+_lib = None
+_lock = threading.Lock()
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+def load_library(path: str = LIB_PATH):
+    """dlopen libgs_raster.so and bind every exported symbol (no GPU needed)."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(path):
+            raise ImportError(
+                f"dge_amd: {path} is missing. Build the HIP extension first "
+                "(python -c 'import __graft_entry__ as g; g.build()' or make -C dge_amd/csrc). "
+                "There is no CPU fallback.")
+        lib = ctypes.CDLL(path)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+        return lib
+
+
+def lib():
+    return _lib if _lib is not None else load_library()
+
+
+def last_error() -> str:
+    msg = lib().gs_last_error()
+    return msg.decode() if msg else ""
+
+
+def check(rc: int, what: str) -> None:
+    if rc != GS_OK:
+        raise NativeError(f"{what} failed (code {rc}): {last_error()}")
+
+
+def require_gpu(t) -> None:
+    """The product path runs only on a ROCm GPU; fail loudly otherwise."""
+    import torch
+
+    if not torch.cuda.is_available():
+        raise NativeError("dge_amd requires a ROCm GPU (torch.cuda.is_available() is False); no CPU fallback exists")
+    if not getattr(t, "is_cuda", False):
+        raise NativeError("dge_amd: tensors must live on the GPU")

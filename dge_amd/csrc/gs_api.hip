@@ -1,0 +1,455 @@
+// gs_api.hip — the C ABI (include/gs_raster.h): host orchestration of the
+// gfx950 kernels.  Replaces CudaRasterizer::Rasterizer::{forward, backward,
+// markVisible, apply_weights} (rasterizer_impl.cu:128-447) and the tensor glue
+// of rasterize_points.cu:35-234.
+//
+// Forward stream order (one stream, no device-wide sync):
+//   memset(counters, ranges, tile_last)
+//   k_preprocess                      -> geometry + depth keys + instance total
+//   D2H copy of {total, error} into pinned memory, event
+//   depth radix sort (4 x 8-bit passes over P keys)
+//   instance scan in depth order (reduce + top)
+//   --- host waits on the event only (the sort keeps the GPU busy) ---
+//   binning buffer allocation (caller's allocator, e.g. the torch caching allocator)
+//   k_scan_emit                       -> (tile, slot) instances, depth-ordered
+//   tile radix sort (1 pass up to 2048 tiles)
+//   k_ranges                          -> ranges, point_list, slot_to_pos
+//   k_render_fwd                      -> color, depth, final_T, n_contrib, tile_last
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <limits>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+
+#include "gs_common.h"
+#include "gs_internal.h"
+#include "gs_raster.h"
+
+using namespace gs;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int set_error(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_last_error = buf;
+    return code;
+}
+
+#define GS_HIP(call)                                                                                  \
+    do {                                                                                              \
+        hipError_t e_ = (call);                                                                       \
+        if (e_ != hipSuccess) return set_error(GS_ERR_HIP, "%s failed: %s", #call, hipGetErrorString(e_)); \
+    } while (0)
+
+// after a launch: surface launch errors; in debug mode also synchronise
+// (the reference's CHECK_CUDA, auxiliary.h:166-173)
+#define GS_LAUNCHED(what)                                                                                     \
+    do {                                                                                                      \
+        hipError_t e_ = hipGetLastError();                                                                    \
+        if (e_ != hipSuccess) return set_error(GS_ERR_HIP, "%s launch failed: %s", what, hipGetErrorString(e_)); \
+        if (debug) {                                                                                          \
+            e_ = hipStreamSynchronize(stream);                                                                \
+            if (e_ != hipSuccess) return set_error(GS_ERR_HIP, "%s failed: %s", what, hipGetErrorString(e_)); \
+        }                                                                                                     \
+    } while (0)
+
+// Per-(thread, device) pinned staging word + event for the num_rendered read-back.
+struct Staging {
+    uint32_t* host = nullptr;
+    hipEvent_t ev = nullptr;
+};
+
+int staging_for_device(Staging** out) {
+    static thread_local std::unordered_map<int, Staging> map;
+    int dev = 0;
+    GS_HIP(hipGetDevice(&dev));
+    Staging& s = map[dev];
+    if (!s.host) {
+        GS_HIP(hipHostMalloc((void**)&s.host, 16, hipHostMallocDefault));
+        GS_HIP(hipEventCreateWithFlags(&s.ev, hipEventDisableTiming));
+    }
+    *out = &s;
+    return GS_OK;
+}
+
+template <typename T>
+T* at(void* base, size_t off) {
+    return reinterpret_cast<T*>(static_cast<char*>(base) + off);
+}
+template <typename T>
+const T* at(const void* base, size_t off) {
+    return reinterpret_cast<const T*>(static_cast<const char*>(base) + off);
+}
+
+struct Grid {
+    int W, H, gx, gy, tiles;
+    float fx, fy;
+};
+
+Grid make_grid(const gs_settings* s) {
+    Grid g;
+    g.W = s->image_width;
+    g.H = s->image_height;
+    g.gx = (g.W + kTile - 1) / kTile;
+    g.gy = (g.H + kTile - 1) / kTile;
+    g.tiles = g.gx * g.gy;
+    // rasterizer_impl.cu:190-191
+    g.fy = g.H / (2.0f * s->tanfovy);
+    g.fx = g.W / (2.0f * s->tanfovx);
+    return g;
+}
+
+int sh_coeffs_needed(int D) { return D >= 3 ? 16 : (D + 1) * (D + 1); }
+
+int validate_common(const gs_settings* s, int P, int M, const float* means3D, const float* shs,
+                    const float* colors_precomp, const float* opacities, const float* scales, const float* rotations,
+                    const float* cov3D_precomp) {
+    if (!s) return set_error(GS_ERR_INVALID_ARG, "settings is NULL");
+    if (s->image_width <= 0 || s->image_height <= 0)
+        return set_error(GS_ERR_INVALID_ARG, "image size must be positive (got %dx%d)", s->image_width, s->image_height);
+    if (P < 0) return set_error(GS_ERR_INVALID_ARG, "P must be >= 0");
+    if (P == 0) return GS_OK;
+    if (!means3D) return set_error(GS_ERR_INVALID_ARG, "means3D must have dimensions (num_points, 3)");
+    if (!opacities) return set_error(GS_ERR_INVALID_ARG, "opacities are required");
+    if (!s->viewmatrix || !s->projmatrix || !s->bg || !s->campos)
+        return set_error(GS_ERR_INVALID_ARG, "viewmatrix, projmatrix, bg and campos are required");
+    if (!shs && !colors_precomp)
+        return set_error(GS_ERR_INVALID_ARG, "Please provide excatly one of either SHs or precomputed colors!");
+    if (shs && M < sh_coeffs_needed(s->sh_degree))
+        return set_error(GS_ERR_INVALID_ARG, "sh has %d coefficients per channel, degree %d needs %d", M, s->sh_degree,
+                         sh_coeffs_needed(s->sh_degree));
+    if (!cov3D_precomp && (!scales || !rotations))
+        return set_error(GS_ERR_INVALID_ARG,
+                         "Please provide exactly one of either scale/rotation pair or precomputed 3D covariance!");
+    return GS_OK;
+}
+
+// Everything of the forward up to (and including) tile ranges.  On success
+// *geom/*img/*bin hold the caller-owned buffers and *K the instance count.
+int bin_forward(const gs_settings* s, const Grid& g, int P, int M, const float* means3D, const float* shs,
+                const float* colors_precomp, const float* opacities, const float* scales, const float* rotations,
+                const float* cov3D_precomp, int* radii_out, int copy_colors, gs_alloc_fn alloc, void* ctx,
+                hipStream_t stream, void** geom_out, void** img_out, void** bin_out, int* K_out) {
+    const bool debug = s->debug != 0;
+    const GeomLayout gl = geom_layout(P);
+    const ImgLayout il = img_layout(g.W, g.H);
+    void* geom = alloc(ctx, 0, gl.total);
+    void* img = alloc(ctx, 2, il.total);
+    if (!geom || !img) return set_error(GS_ERR_ALLOC, "allocator returned NULL for the geometry/image buffer");
+    *geom_out = geom;
+    *img_out = img;
+
+    uint32_t* counters = at<uint32_t>(geom, gl.counters);
+    GS_HIP(hipMemsetAsync(counters, 0, 16, stream));
+    GS_HIP(hipMemsetAsync(at<char>(img, il.ranges), 0, il.total - il.ranges, stream));  // ranges + tile_last
+
+    PreprocessArgs pa;
+    pa.P = P; pa.D = s->sh_degree; pa.M = M; pa.W = g.W; pa.H = g.H; pa.gx = g.gx; pa.gy = g.gy;
+    pa.means3D = means3D; pa.shs = shs; pa.colors_precomp = colors_precomp; pa.opacities = opacities;
+    pa.scales = scales; pa.rotations = rotations; pa.cov3D_precomp = cov3D_precomp;
+    pa.view = s->viewmatrix; pa.proj = s->projmatrix; pa.campos = s->campos;
+    pa.tanfovx = s->tanfovx; pa.tanfovy = s->tanfovy; pa.fx = g.fx; pa.fy = g.fy;
+    pa.scale_modifier = s->scale_modifier;
+    pa.prefiltered = s->prefiltered; pa.copy_colors = copy_colors;
+    pa.radii_out = radii_out;
+    pa.radii = at<int>(geom, gl.radii);
+    pa.means2D = at<float2>(geom, gl.means2D);
+    pa.conic_opacity = at<float4>(geom, gl.conic_opacity);
+    pa.rgbd = at<float4>(geom, gl.rgbd);
+    pa.tiles_touched = at<uint32_t>(geom, gl.tiles_touched);
+    pa.clamped = at<uint8_t>(geom, gl.clamped);
+    pa.depth_key = at<uint32_t>(geom, gl.key0);
+    pa.depth_val = at<uint32_t>(geom, gl.val0);
+    pa.counters = counters;
+    launch_preprocess(pa, stream);
+    GS_LAUNCHED("preprocess");
+
+    Staging* st = nullptr;
+    int rc = staging_for_device(&st);
+    if (rc) return rc;
+    GS_HIP(hipMemcpyAsync(st->host, counters, 8, hipMemcpyDeviceToHost, stream));
+    GS_HIP(hipEventRecord(st->ev, stream));
+
+    // depth order of the Gaussians (stable: ties keep index order)
+    const int cur = radix_sort_pairs(at<uint32_t>(geom, gl.key0), at<uint32_t>(geom, gl.key1),
+                                     at<uint32_t>(geom, gl.val0), at<uint32_t>(geom, gl.val1), (uint32_t)P, 0, 32, 8,
+                                     false, at<uint32_t>(geom, gl.sort_hist), at<uint32_t>(geom, gl.sort_totals),
+                                     gl.sort_blocks, stream);
+    GS_LAUNCHED("depth sort");
+
+    EmitArgs ea;
+    ea.P = P; ea.gx = g.gx; ea.gy = g.gy;
+    ea.order = at<uint32_t>(geom, cur ? gl.val1 : gl.val0);
+    ea.tiles_touched = pa.tiles_touched;
+    ea.means2D = pa.means2D;
+    ea.radii = pa.radii;
+    ea.scan_sums = at<uint32_t>(geom, gl.scan_sums);
+    ea.first_slot = at<uint32_t>(geom, gl.first_slot);
+    ea.scan_blocks = gl.scan_blocks;
+    launch_scan_reduce(ea, stream);
+    GS_LAUNCHED("instance scan");
+
+    GS_HIP(hipEventSynchronize(st->ev));
+    const uint32_t K = st->host[0];
+    if (st->host[1]) return set_error(GS_ERR_PREFILTERED, "Point is filtered although prefiltered is set. This shouldn't happen!");
+    if (K > (uint32_t)std::numeric_limits<int>::max()) return set_error(GS_ERR_INVALID_ARG, "too many tile instances (%u)", K);
+    *K_out = (int)K;
+
+    const BinLayout bl = bin_layout((int)K, g.tiles);
+    void* bin = alloc(ctx, 1, bl.total);
+    if (!bin) return set_error(GS_ERR_ALLOC, "allocator returned NULL for the binning buffer");
+    *bin_out = bin;
+    if (K == 0) return GS_OK;
+
+    ea.tile_key = at<uint32_t>(bin, bl.key0);
+    ea.slot_gauss = at<uint32_t>(bin, bl.slot_gauss);
+    launch_scan_emit(ea, stream);
+    GS_LAUNCHED("emit");
+
+    const TileSortPlan plan = tile_sort_plan(g.tiles);
+    const int tc = radix_sort_pairs(at<uint32_t>(bin, bl.key0), at<uint32_t>(bin, bl.key1), at<uint32_t>(bin, bl.val0),
+                                    at<uint32_t>(bin, bl.val1), K, 0, plan.bits, kMaxSinglePassBits, true,
+                                    at<uint32_t>(bin, bl.sort_hist), at<uint32_t>(bin, bl.sort_totals), bl.sort_blocks,
+                                    stream);
+    GS_LAUNCHED("tile sort");
+    launch_ranges(at<uint32_t>(bin, tc ? bl.key1 : bl.key0), at<uint32_t>(bin, tc ? bl.val1 : bl.val0),
+                  at<uint32_t>(bin, bl.slot_gauss), (int)K, at<uint2>(img, il.ranges), at<uint32_t>(bin, bl.point_list),
+                  at<uint32_t>(bin, bl.slot_to_pos), stream);
+    GS_LAUNCHED("ranges");
+    return GS_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* gs_last_error(void) { return g_last_error.c_str(); }
+int gs_abi_version(void) { return GS_RASTER_ABI_VERSION; }
+
+size_t gs_geometry_buffer_size(int P) { return geom_layout(P).total; }
+size_t gs_image_buffer_size(int width, int height) { return img_layout(width, height).total; }
+size_t gs_binning_buffer_size(int num_rendered, int num_tiles) { return bin_layout(num_rendered, num_tiles).total; }
+
+long long gs_buffer_offset(const char* buffer, const char* field, int P, int width, int height, int num_rendered) {
+    if (!buffer || !field) return -1;
+    if (!strcmp(buffer, "geometry")) {
+        const GeomLayout L = geom_layout(P);
+        if (!strcmp(field, "means2D")) return (long long)L.means2D;
+        if (!strcmp(field, "conic_opacity")) return (long long)L.conic_opacity;
+        if (!strcmp(field, "rgbd")) return (long long)L.rgbd;
+        if (!strcmp(field, "tiles_touched")) return (long long)L.tiles_touched;
+        if (!strcmp(field, "clamped")) return (long long)L.clamped;
+        if (!strcmp(field, "radii")) return (long long)L.radii;
+        if (!strcmp(field, "first_slot")) return (long long)L.first_slot;
+    } else if (!strcmp(buffer, "image")) {
+        const ImgLayout L = img_layout(width, height);
+        if (!strcmp(field, "final_T")) return (long long)L.final_T;
+        if (!strcmp(field, "n_contrib")) return (long long)L.n_contrib;
+        if (!strcmp(field, "ranges")) return (long long)L.ranges;
+        if (!strcmp(field, "tile_last")) return (long long)L.tile_last;
+    } else if (!strcmp(buffer, "binning")) {
+        const int tiles = ((width + 15) / 16) * ((height + 15) / 16);
+        const BinLayout L = bin_layout(num_rendered, tiles);
+        if (!strcmp(field, "point_list")) return (long long)L.point_list;
+        if (!strcmp(field, "slot_gauss")) return (long long)L.slot_gauss;
+        if (!strcmp(field, "slot_to_pos")) return (long long)L.slot_to_pos;
+        if (!strcmp(field, "records")) return (long long)L.records;
+    }
+    return -1;
+}
+
+int gs_rasterize_forward(const gs_settings* s, int P, int M, const float* means3D, const float* shs,
+                         const float* colors_precomp, const float* opacities, const float* scales,
+                         const float* rotations, const float* cov3D_precomp, float* out_color, float* out_depth,
+                         int* radii, gs_alloc_fn alloc, void* alloc_ctx, gs_stream_t stream_, int* num_rendered) {
+    try {
+        hipStream_t stream = (hipStream_t)stream_;
+        if (!num_rendered || !alloc || !out_color || !out_depth)
+            return set_error(GS_ERR_INVALID_ARG, "num_rendered, alloc, out_color and out_depth are required");
+        *num_rendered = 0;
+        int rc = validate_common(s, P, M, means3D, shs, colors_precomp, opacities, scales, rotations, cov3D_precomp);
+        if (rc) return rc;
+        const bool debug = s->debug != 0;
+        const Grid g = make_grid(s);
+        if (P == 0) {  // rasterize_points.cu:57-72: zero outputs, empty buffers, no render
+            for (int w = 0; w < 3; ++w) alloc(alloc_ctx, w, 0);
+            GS_HIP(hipMemsetAsync(out_color, 0, sizeof(float) * 3 * (size_t)g.W * g.H, stream));
+            GS_HIP(hipMemsetAsync(out_depth, 0, sizeof(float) * (size_t)g.W * g.H, stream));
+            return GS_OK;
+        }
+        void *geom = nullptr, *img = nullptr, *bin = nullptr;
+        int K = 0;
+        rc = bin_forward(s, g, P, M, means3D, shs, colors_precomp, opacities, scales, rotations, cov3D_precomp, radii, 1,
+                         alloc, alloc_ctx, stream, &geom, &img, &bin, &K);
+        if (rc) return rc;
+        const GeomLayout gl = geom_layout(P);
+        const ImgLayout il = img_layout(g.W, g.H);
+        const BinLayout bl = bin_layout(K, g.tiles);
+        RenderArgs ra;
+        ra.W = g.W; ra.H = g.H; ra.gx = g.gx; ra.gy = g.gy;
+        ra.ranges = at<uint2>(img, il.ranges);
+        ra.point_list = at<uint32_t>(bin, bl.point_list);
+        ra.means2D = at<float2>(geom, gl.means2D);
+        ra.conic_opacity = at<float4>(geom, gl.conic_opacity);
+        ra.rgbd = at<float4>(geom, gl.rgbd);
+        ra.bg = s->bg;
+        ra.final_T = at<float>(img, il.final_T);
+        ra.n_contrib = at<uint32_t>(img, il.n_contrib);
+        ra.tile_last = at<uint32_t>(img, il.tile_last);
+        ra.out_color = out_color;
+        ra.out_depth = out_depth;
+        launch_render_forward(ra, stream);
+        GS_LAUNCHED("render");
+        *num_rendered = K;
+        return GS_OK;
+    } catch (const std::exception& e) {
+        return set_error(GS_ERR_INVALID_ARG, "exception: %s", e.what());
+    } catch (...) {
+        return set_error(GS_ERR_INVALID_ARG, "unknown exception");
+    }
+}
+
+int gs_rasterize_backward(const gs_settings* s, int P, int M, int R, const float* means3D, const float* shs,
+                          const float* colors_precomp, const float* scales, const float* rotations,
+                          const float* cov3D_precomp, const int* radii, const void* geom, const void* binning,
+                          const void* img, const float* dL_dpix, float* dL_dmeans2D, float* dL_dcolors,
+                          float* dL_dopacity, float* dL_dmeans3D, float* dL_dcov3D, float* dL_dsh, float* dL_dscales,
+                          float* dL_drotations, gs_stream_t stream_) {
+    try {
+        hipStream_t stream = (hipStream_t)stream_;
+        if (!s) return set_error(GS_ERR_INVALID_ARG, "settings is NULL");
+        if (P == 0) return GS_OK;
+        if (P < 0) return set_error(GS_ERR_INVALID_ARG, "P must be >= 0");
+        if (s->image_width <= 0 || s->image_height <= 0) return set_error(GS_ERR_INVALID_ARG, "image size must be positive");
+        if (!means3D || !s->viewmatrix || !s->projmatrix || !s->bg || !s->campos)
+            return set_error(GS_ERR_INVALID_ARG, "means3D, viewmatrix, projmatrix, bg and campos are required");
+        if (shs && M < sh_coeffs_needed(s->sh_degree))
+            return set_error(GS_ERR_INVALID_ARG, "sh has %d coefficients per channel, degree %d needs %d", M,
+                             s->sh_degree, sh_coeffs_needed(s->sh_degree));
+        if (!cov3D_precomp && (!scales || !rotations))
+            return set_error(GS_ERR_INVALID_ARG, "scales/rotations or cov3D_precomp are required");
+        (void)colors_precomp;  // colours were captured in the geometry buffer by the forward
+        if (!geom || !img || !radii || !dL_dpix)
+            return set_error(GS_ERR_INVALID_ARG, "geometry/image buffers, radii and dL_dpix are required");
+        if (!dL_dmeans2D || !dL_dcolors || !dL_dopacity || !dL_dmeans3D || !dL_dcov3D || !dL_dscales || !dL_drotations ||
+            (M > 0 && !dL_dsh))
+            return set_error(GS_ERR_INVALID_ARG, "gradient outputs are required");
+        if (R > 0 && !binning) return set_error(GS_ERR_INVALID_ARG, "binning buffer is required when num_rendered > 0");
+        const bool debug = s->debug != 0;
+        const Grid g = make_grid(s);
+        const GeomLayout gl = geom_layout(P);
+        const ImgLayout il = img_layout(g.W, g.H);
+        const BinLayout bl = bin_layout(R, g.tiles);
+        float4* records = R > 0 ? at<float4>(const_cast<void*>(binning), bl.records) : nullptr;
+        if (R > 0) {
+            RenderBwdArgs rb;
+            rb.W = g.W; rb.H = g.H; rb.gx = g.gx; rb.gy = g.gy;
+            rb.ranges = at<uint2>(img, il.ranges);
+            rb.point_list = at<uint32_t>(binning, bl.point_list);
+            rb.tile_last = at<uint32_t>(img, il.tile_last);
+            rb.means2D = at<float2>(geom, gl.means2D);
+            rb.conic_opacity = at<float4>(geom, gl.conic_opacity);
+            rb.rgbd = at<float4>(geom, gl.rgbd);
+            rb.bg = s->bg;
+            rb.final_T = at<float>(img, il.final_T);
+            rb.n_contrib = at<uint32_t>(img, il.n_contrib);
+            rb.dL_dpix = dL_dpix;
+            rb.records = records;
+            launch_render_backward(rb, stream);
+            GS_LAUNCHED("render backward");
+        }
+        GaussBwdArgs ga;
+        ga.P = P; ga.D = s->sh_degree; ga.M = shs ? M : (dL_dsh ? M : 0); ga.W = g.W; ga.H = g.H; ga.gx = g.gx; ga.gy = g.gy;
+        ga.means3D = means3D; ga.shs = shs; ga.scales = scales; ga.rotations = rotations; ga.cov3D_precomp = cov3D_precomp;
+        ga.view = s->viewmatrix; ga.proj = s->projmatrix; ga.campos = s->campos;
+        ga.tanfovx = s->tanfovx; ga.tanfovy = s->tanfovy; ga.fx = g.fx; ga.fy = g.fy;
+        ga.scale_modifier = s->scale_modifier;
+        ga.radii = radii;
+        ga.geom_radii = at<int>(geom, gl.radii);
+        ga.means2D = at<float2>(geom, gl.means2D);
+        ga.tiles_touched = at<uint32_t>(geom, gl.tiles_touched);
+        ga.first_slot = at<uint32_t>(geom, gl.first_slot);
+        ga.clamped = at<uint8_t>(geom, gl.clamped);
+        ga.slot_to_pos = R > 0 ? at<uint32_t>(binning, bl.slot_to_pos) : nullptr;
+        ga.ranges = at<uint2>(img, il.ranges);
+        ga.tile_last = at<uint32_t>(img, il.tile_last);
+        ga.records = records;
+        ga.dL_dmeans2D = dL_dmeans2D; ga.dL_dcolors = dL_dcolors; ga.dL_dopacity = dL_dopacity;
+        ga.dL_dmeans3D = dL_dmeans3D; ga.dL_dcov3D = dL_dcov3D; ga.dL_dsh = M > 0 ? dL_dsh : nullptr;
+        ga.dL_dscales = dL_dscales; ga.dL_drot = dL_drotations;
+        launch_gauss_backward(ga, stream);
+        GS_LAUNCHED("gaussian backward");
+        return GS_OK;
+    } catch (const std::exception& e) {
+        return set_error(GS_ERR_INVALID_ARG, "exception: %s", e.what());
+    } catch (...) {
+        return set_error(GS_ERR_INVALID_ARG, "unknown exception");
+    }
+}
+
+int gs_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix, uint8_t* present,
+                    gs_stream_t stream_) {
+    hipStream_t stream = (hipStream_t)stream_;
+    (void)projmatrix;
+    if (P < 0) return set_error(GS_ERR_INVALID_ARG, "P must be >= 0");
+    if (P == 0) return GS_OK;
+    if (!means3D || !viewmatrix || !present) return set_error(GS_ERR_INVALID_ARG, "means3D, viewmatrix, present required");
+    launch_mark_visible(P, means3D, viewmatrix, present, stream);
+    const bool debug = false;
+    GS_LAUNCHED("mark_visible");
+    return GS_OK;
+}
+
+int gs_apply_weights(const gs_settings* s, int P, int M, const float* means3D, float* weights, int num_channels,
+                     const float* opacities, const float* scales, const float* rotations, const float* cov3D_precomp,
+                     const float* shs, const float* image_weights, int* cnt, gs_alloc_fn alloc, void* alloc_ctx,
+                     gs_stream_t stream_) {
+    try {
+        hipStream_t stream = (hipStream_t)stream_;
+        if (num_channels < 1 || num_channels > 3)
+            return set_error(GS_ERR_UNSUPPORTED, "Unsupported number of channels: %d", num_channels);
+        if (!alloc || !weights || !image_weights || !cnt)
+            return set_error(GS_ERR_INVALID_ARG, "alloc, weights, image_weights and cnt are required");
+        int rc = validate_common(s, P, M, means3D, shs, weights, opacities, scales, rotations, cov3D_precomp);
+        if (rc) return rc;
+        if (P == 0) return GS_OK;
+        const bool debug = s->debug != 0;
+        const Grid g = make_grid(s);
+        void *geom = nullptr, *img = nullptr, *bin = nullptr;
+        int K = 0;
+        rc = bin_forward(s, g, P, M, means3D, shs, weights, opacities, scales, rotations, cov3D_precomp, nullptr, 0,
+                         alloc, alloc_ctx, stream, &geom, &img, &bin, &K);
+        if (rc) return rc;
+        if (K == 0) return GS_OK;
+        const GeomLayout gl = geom_layout(P);
+        const ImgLayout il = img_layout(g.W, g.H);
+        const BinLayout bl = bin_layout(K, g.tiles);
+        ApplyWeightsArgs aw;
+        aw.W = g.W; aw.H = g.H; aw.gx = g.gx; aw.gy = g.gy; aw.C = num_channels;
+        aw.ranges = at<uint2>(img, il.ranges);
+        aw.point_list = at<uint32_t>(bin, bl.point_list);
+        aw.means2D = at<float2>(geom, gl.means2D);
+        aw.conic_opacity = at<float4>(geom, gl.conic_opacity);
+        aw.image_weights = image_weights;
+        aw.weights = weights;
+        aw.cnt = cnt;
+        launch_render_apply_weights(aw, stream);
+        GS_LAUNCHED("apply_weights render");
+        return GS_OK;
+    } catch (const std::exception& e) {
+        return set_error(GS_ERR_INVALID_ARG, "exception: %s", e.what());
+    } catch (...) {
+        return set_error(GS_ERR_INVALID_ARG, "unknown exception");
+    }
+}
+
+}  // extern "C"

@@ -1,0 +1,284 @@
+// gs_backward.hip — per-Gaussian backward for gfx950, one thread per Gaussian.
+//
+// Fuses what the reference runs as three steps plus a memset:
+//   * torch::zeros of the 9 gradient tensors (rasterize_points.cu:120-128):
+//     not needed, every output element is written here;
+//   * the sum of the per-pixel atomics of renderCUDA bwd (backward.cu:523-554):
+//     here the sum of this Gaussian's per-tile records, read in tile order
+//     (deterministic);
+//   * computeCov2DCUDA (backward.cu:144-274) and preprocessCUDA bwd
+//     (backward.cu:346-396) with computeColorFromSH bwd (:20-139) and
+//     computeCov3D bwd (:278-341).
+// The 3D covariance is recomputed from (scale, rotation) with the forward's
+// own helper instead of being stored in the geometry buffer (-48 B/Gaussian
+// of HBM traffic).
+#include "gs_common.h"
+#include "gs_internal.h"
+
+namespace gs {
+
+// backward.cu:20-139 — writes dL_dsh for the (deg+1)^2 used coefficients and
+// returns the mean gradient through the normalised view direction.
+__device__ __forceinline__ f3 sh_backward(int deg, f3 pos, f3 campos, const float* __restrict__ sh, uint8_t clamp_bits,
+                                          f3 dL_dcolor, float* __restrict__ dsh) {
+    const f3 dir_orig = pos - campos;
+    const float len = sqrtf(dot3(dir_orig, dir_orig));
+    const f3 dir = mk3(dir_orig.x / len, dir_orig.y / len, dir_orig.z / len);
+    const f3 g = mk3(dL_dcolor.x * ((clamp_bits & 1) ? 0.f : 1.f), dL_dcolor.y * ((clamp_bits & 2) ? 0.f : 1.f),
+                     dL_dcolor.z * ((clamp_bits & 4) ? 0.f : 1.f));
+    auto put = [&](int k, f3 v) {
+        dsh[3 * k] = v.x;
+        dsh[3 * k + 1] = v.y;
+        dsh[3 * k + 2] = v.z;
+    };
+    f3 dx = mk3(0, 0, 0), dy = mk3(0, 0, 0), dz = mk3(0, 0, 0);
+    const float x = dir.x, y = dir.y, z = dir.z;
+    put(0, g * kSH_C0);
+    if (deg > 0) {
+        put(1, g * (-kSH_C1 * y));
+        put(2, g * (kSH_C1 * z));
+        put(3, g * (-kSH_C1 * x));
+        dx = ld3(sh + 9) * (-kSH_C1);
+        dy = ld3(sh + 3) * (-kSH_C1);
+        dz = ld3(sh + 6) * kSH_C1;
+        if (deg > 1) {
+            const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
+            put(4, g * (kSH_C2_0 * xy));
+            put(5, g * (kSH_C2_1 * yz));
+            put(6, g * (kSH_C2_2 * (2.f * zz - xx - yy)));
+            put(7, g * (kSH_C2_3 * xz));
+            put(8, g * (kSH_C2_4 * (xx - yy)));
+            dx = dx + (ld3(sh + 12) * (kSH_C2_0 * y) + ld3(sh + 18) * (kSH_C2_2 * 2.f * -x) +
+                       ld3(sh + 21) * (kSH_C2_3 * z) + ld3(sh + 24) * (kSH_C2_4 * 2.f * x));
+            dy = dy + (ld3(sh + 12) * (kSH_C2_0 * x) + ld3(sh + 15) * (kSH_C2_1 * z) +
+                       ld3(sh + 18) * (kSH_C2_2 * 2.f * -y) + ld3(sh + 24) * (kSH_C2_4 * 2.f * -y));
+            dz = dz + (ld3(sh + 15) * (kSH_C2_1 * y) + ld3(sh + 18) * (kSH_C2_2 * 2.f * 2.f * z) +
+                       ld3(sh + 21) * (kSH_C2_3 * x));
+            if (deg > 2) {
+                put(9, g * (kSH_C3_0 * y * (3.f * xx - yy)));
+                put(10, g * (kSH_C3_1 * xy * z));
+                put(11, g * (kSH_C3_2 * y * (4.f * zz - xx - yy)));
+                put(12, g * (kSH_C3_3 * z * (2.f * zz - 3.f * xx - 3.f * yy)));
+                put(13, g * (kSH_C3_4 * x * (4.f * zz - xx - yy)));
+                put(14, g * (kSH_C3_5 * z * (xx - yy)));
+                put(15, g * (kSH_C3_6 * x * (xx - 3.f * yy)));
+                dx = dx + (ld3(sh + 27) * (kSH_C3_0 * 3.f * 2.f * xy) + ld3(sh + 30) * (kSH_C3_1 * yz) +
+                           ld3(sh + 33) * (kSH_C3_2 * -2.f * xy) + ld3(sh + 36) * (kSH_C3_3 * -3.f * 2.f * xz) +
+                           ld3(sh + 39) * (kSH_C3_4 * (-3.f * xx + 4.f * zz - yy)) +
+                           ld3(sh + 42) * (kSH_C3_5 * 2.f * xz) + ld3(sh + 45) * (kSH_C3_6 * 3.f * (xx - yy)));
+                dy = dy + (ld3(sh + 27) * (kSH_C3_0 * 3.f * (xx - yy)) + ld3(sh + 30) * (kSH_C3_1 * xz) +
+                           ld3(sh + 33) * (kSH_C3_2 * (-3.f * yy + 4.f * zz - xx)) +
+                           ld3(sh + 36) * (kSH_C3_3 * -3.f * 2.f * yz) + ld3(sh + 39) * (kSH_C3_4 * -2.f * xy) +
+                           ld3(sh + 42) * (kSH_C3_5 * -2.f * yz) + ld3(sh + 45) * (kSH_C3_6 * -3.f * 2.f * xy));
+                dz = dz + (ld3(sh + 30) * (kSH_C3_1 * xy) + ld3(sh + 33) * (kSH_C3_2 * 4.f * 2.f * yz) +
+                           ld3(sh + 36) * (kSH_C3_3 * 3.f * (2.f * zz - xx - yy)) +
+                           ld3(sh + 39) * (kSH_C3_4 * 4.f * 2.f * xz) + ld3(sh + 42) * (kSH_C3_5 * (xx - yy)));
+            }
+        }
+    }
+    const f3 dL_ddir = mk3(dot3(dx, g), dot3(dy, g), dot3(dz, g));
+    // dnormvdv (auxiliary.h:107-117)
+    const f3 v = dir_orig;
+    const float sum2 = v.x * v.x + v.y * v.y + v.z * v.z;
+    const float invsum32 = 1.0f / sqrtf(sum2 * sum2 * sum2);
+    return mk3(((+sum2 - v.x * v.x) * dL_ddir.x - v.y * v.x * dL_ddir.y - v.z * v.x * dL_ddir.z) * invsum32,
+               (-v.x * v.y * dL_ddir.x + (sum2 - v.y * v.y) * dL_ddir.y - v.z * v.y * dL_ddir.z) * invsum32,
+               (-v.x * v.z * dL_ddir.x - v.y * v.z * dL_ddir.y + (sum2 - v.z * v.z) * dL_ddir.z) * invsum32);
+}
+
+// backward.cu:278-341 (gradient w.r.t. mod*scale and the unnormalised quaternion)
+__device__ __forceinline__ void cov3d_backward(f3 scale, float mod, float4 q, const float dc[6], float* dscale,
+                                               float* drot) {
+    const float r = q.x, x = q.y, y = q.z, z = q.w;
+    float R[3][3];  // glm R[c][r]
+    R[0][0] = 1.f - 2.f * (y * y + z * z); R[0][1] = 2.f * (x * y - r * z); R[0][2] = 2.f * (x * z + r * y);
+    R[1][0] = 2.f * (x * y + r * z); R[1][1] = 1.f - 2.f * (x * x + z * z); R[1][2] = 2.f * (y * z - r * x);
+    R[2][0] = 2.f * (x * z - r * y); R[2][1] = 2.f * (y * z + r * x); R[2][2] = 1.f - 2.f * (x * x + y * y);
+    const float s[3] = {mod * scale.x, mod * scale.y, mod * scale.z};
+    float S2M[3][3];  // (2 * M)[c][r] with M = S * R  ->  M[c][r] = s_r R[c][r]
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+#pragma unroll
+        for (int rr = 0; rr < 3; ++rr) S2M[c][rr] = 2.0f * (s[rr] * R[c][rr]);
+    float dS[3][3];  // dL_dSigma, glm column-major, symmetric
+    dS[0][0] = dc[0]; dS[0][1] = 0.5f * dc[1]; dS[0][2] = 0.5f * dc[2];
+    dS[1][0] = 0.5f * dc[1]; dS[1][1] = dc[3]; dS[1][2] = 0.5f * dc[4];
+    dS[2][0] = 0.5f * dc[2]; dS[2][1] = 0.5f * dc[4]; dS[2][2] = dc[5];
+    float dM[3][3];  // glm product (2M) * dSigma
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+#pragma unroll
+        for (int rr = 0; rr < 3; ++rr)
+            dM[c][rr] = S2M[0][rr] * dS[c][0] + S2M[1][rr] * dS[c][1] + S2M[2][rr] * dS[c][2];
+    // dL_dscale[i] = dot(Rt[i], dMt[i]) = sum_r R[r][i] dM[r][i]
+#pragma unroll
+    for (int i = 0; i < 3; ++i) dscale[i] = R[0][i] * dM[0][i] + R[1][i] * dM[1][i] + R[2][i] * dM[2][i];
+    float D[3][3];  // dMt[c][r] * s_c = dM[r][c] * s_c
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+#pragma unroll
+        for (int rr = 0; rr < 3; ++rr) D[c][rr] = dM[rr][c] * s[c];
+    drot[0] = 2 * z * (D[0][1] - D[1][0]) + 2 * y * (D[2][0] - D[0][2]) + 2 * x * (D[1][2] - D[2][1]);
+    drot[1] = 2 * y * (D[1][0] + D[0][1]) + 2 * z * (D[2][0] + D[0][2]) + 2 * r * (D[1][2] - D[2][1]) - 4 * x * (D[2][2] + D[1][1]);
+    drot[2] = 2 * x * (D[1][0] + D[0][1]) + 2 * r * (D[2][0] - D[0][2]) + 2 * z * (D[1][2] + D[2][1]) - 4 * y * (D[2][2] + D[0][0]);
+    drot[3] = 2 * r * (D[0][1] - D[1][0]) + 2 * x * (D[2][0] + D[0][2]) + 2 * y * (D[1][2] + D[2][1]) - 4 * z * (D[1][1] + D[0][0]);
+}
+
+__global__ __launch_bounds__(256) void k_gauss_bwd(GaussBwdArgs a) {
+    const int idx = blockIdx.x * 256 + threadIdx.x;
+    if (idx >= a.P) return;
+    const bool vis = a.radii[idx] > 0;
+    float acc[9];
+#pragma unroll
+    for (int f = 0; f < 9; ++f) acc[f] = 0.f;
+    const uint32_t n = vis ? a.tiles_touched[idx] : 0u;
+    if (n) {
+        const uint32_t first = a.first_slot[idx];
+        const float2 xy = a.means2D[idx];
+        // geometry radii (consistent with tiles_touched/first_slot): emission order is row-major over the rect
+        const int gr = a.geom_radii[idx];
+        const Rect q = tile_rect(xy.x, xy.y, gr, a.gx, a.gy);
+        const int wd = q.x1 - q.x0;
+        for (uint32_t k = 0; k < n; ++k) {
+            const int t = (q.y0 + (int)k / wd) * a.gx + q.x0 + (int)k % wd;
+            const uint32_t pos = a.slot_to_pos[first + k];
+            if (pos - a.ranges[t].x < a.tile_last[t]) {
+                const float4 r0 = a.records[3 * (size_t)pos];
+                const float4 r1 = a.records[3 * (size_t)pos + 1];
+                const float4 r2 = a.records[3 * (size_t)pos + 2];
+                acc[0] += r0.x; acc[1] += r0.y; acc[2] += r0.z; acc[3] += r0.w;
+                acc[4] += r1.x; acc[5] += r1.y; acc[6] += r1.z; acc[7] += r1.w;
+                acc[8] += r2.x;
+            }
+        }
+    }
+    a.dL_dmeans2D[3 * (size_t)idx] = acc[0];
+    a.dL_dmeans2D[3 * (size_t)idx + 1] = acc[1];
+    a.dL_dmeans2D[3 * (size_t)idx + 2] = 0.f;
+    a.dL_dopacity[idx] = acc[5];
+    a.dL_dcolors[3 * (size_t)idx] = acc[6];
+    a.dL_dcolors[3 * (size_t)idx + 1] = acc[7];
+    a.dL_dcolors[3 * (size_t)idx + 2] = acc[8];
+
+    float* dsh = a.dL_dsh ? a.dL_dsh + (size_t)idx * a.M * 3 : nullptr;
+    if (!vis) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) { a.dL_dmeans3D[3 * (size_t)idx + k] = 0.f; a.dL_dscales[3 * (size_t)idx + k] = 0.f; }
+#pragma unroll
+        for (int k = 0; k < 6; ++k) a.dL_dcov3D[6 * (size_t)idx + k] = 0.f;
+        *reinterpret_cast<float4*>(a.dL_drot + 4 * (size_t)idx) = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (dsh)
+            for (int k = 0; k < a.M * 3; ++k) dsh[k] = 0.f;
+        return;
+    }
+
+    const float* v = a.view;
+    const float* pm = a.proj;
+    const f3 m = ld3(a.means3D + 3 * (size_t)idx);
+    float cov3[6];
+    f3 scale = mk3(0, 0, 0);
+    float4 rot = make_float4(0, 0, 0, 0);
+    if (a.cov3D_precomp) {
+#pragma unroll
+        for (int k = 0; k < 6; ++k) cov3[k] = a.cov3D_precomp[6 * (size_t)idx + k];
+    } else {
+        scale = ld3(a.scales + 3 * (size_t)idx);
+        rot = *reinterpret_cast<const float4*>(a.rotations + 4 * (size_t)idx);
+        cov3d_from_scale_rot(scale, a.scale_modifier, rot, cov3);
+    }
+
+    // ---- computeCov2DCUDA (backward.cu:144-274) ----
+    Ewa e;
+    ewa_setup(m, a.fx, a.fy, a.tanfovx, a.tanfovy, cov3, v, e);
+    const float x_grad_mul = e.txtz < -e.limx || e.txtz > e.limx ? 0.f : 1.f;
+    const float y_grad_mul = e.tytz < -e.limy || e.tytz > e.limy ? 0.f : 1.f;
+    float ca, cb, cc;
+    ewa_cov2d(e, ca, cb, cc);
+    const float dcx = acc[2], dcy = acc[3], dcw = acc[4];  // dL_dconic x, y, w
+    const float denom = ca * cc - cb * cb;
+    float dL_da = 0.f, dL_db = 0.f, dL_dc = 0.f;
+    const float denom2inv = 1.0f / ((denom * denom) + 0.0000001f);
+    float dcov[6];
+    const float(&T)[2][3] = e.T;
+    if (denom2inv != 0) {
+        dL_da = denom2inv * (-cc * cc * dcx + 2 * cb * cc * dcy + (denom - ca * cc) * dcw);
+        dL_dc = denom2inv * (-ca * ca * dcw + 2 * ca * cb * dcy + (denom - ca * cc) * dcx);
+        dL_db = denom2inv * 2 * (cb * cc * dcx - (denom + 2 * cb * cb) * dcy + ca * cb * dcw);
+        dcov[0] = (T[0][0] * T[0][0] * dL_da + T[0][0] * T[1][0] * dL_db + T[1][0] * T[1][0] * dL_dc);
+        dcov[3] = (T[0][1] * T[0][1] * dL_da + T[0][1] * T[1][1] * dL_db + T[1][1] * T[1][1] * dL_dc);
+        dcov[5] = (T[0][2] * T[0][2] * dL_da + T[0][2] * T[1][2] * dL_db + T[1][2] * T[1][2] * dL_dc);
+        dcov[1] = 2 * T[0][0] * T[0][1] * dL_da + (T[0][0] * T[1][1] + T[0][1] * T[1][0]) * dL_db + 2 * T[1][0] * T[1][1] * dL_dc;
+        dcov[2] = 2 * T[0][0] * T[0][2] * dL_da + (T[0][0] * T[1][2] + T[0][2] * T[1][0]) * dL_db + 2 * T[1][0] * T[1][2] * dL_dc;
+        dcov[4] = 2 * T[0][2] * T[0][1] * dL_da + (T[0][1] * T[1][2] + T[0][2] * T[1][1]) * dL_db + 2 * T[1][1] * T[1][2] * dL_dc;
+    } else {
+#pragma unroll
+        for (int k = 0; k < 6; ++k) dcov[k] = 0.f;
+    }
+    float dT[2][3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        dT[0][j] = 2 * tv(e, 0, j) * dL_da + tv(e, 1, j) * dL_db;
+        dT[1][j] = 2 * tv(e, 1, j) * dL_dc + tv(e, 0, j) * dL_db;
+    }
+    // W[i][j] (glm) = v[i + 4j]
+    const float dL_dJ00 = v[0] * dT[0][0] + v[4] * dT[0][1] + v[8] * dT[0][2];
+    const float dL_dJ02 = v[2] * dT[0][0] + v[6] * dT[0][1] + v[10] * dT[0][2];
+    const float dL_dJ11 = v[1] * dT[1][0] + v[5] * dT[1][1] + v[9] * dT[1][2];
+    const float dL_dJ12 = v[2] * dT[1][0] + v[6] * dT[1][1] + v[10] * dT[1][2];
+    const f3 t = e.t;
+    const float tz = 1.f / t.z, tz2 = tz * tz, tz3 = tz2 * tz;
+    const float dL_dtx = x_grad_mul * -a.fx * tz2 * dL_dJ02;
+    const float dL_dty = y_grad_mul * -a.fy * tz2 * dL_dJ12;
+    const float dL_dtz = -a.fx * tz2 * dL_dJ00 - a.fy * tz2 * dL_dJ11 + (2 * a.fx * t.x) * tz3 * dL_dJ02 +
+                         (2 * a.fy * t.y) * tz3 * dL_dJ12;
+    // transformVec4x3Transpose (auxiliary.h:89-97)
+    f3 dmean = mk3(v[0] * dL_dtx + v[1] * dL_dty + v[2] * dL_dtz, v[4] * dL_dtx + v[5] * dL_dty + v[6] * dL_dtz,
+                   v[8] * dL_dtx + v[9] * dL_dty + v[10] * dL_dtz);
+
+    // ---- preprocessCUDA bwd: projection of the 2D mean (backward.cu:370-387) ----
+    {
+        const float4 mh = proj_point(pm, m);
+        const float m_w = 1.0f / (mh.w + 0.0000001f);
+        const float mul1 = (pm[0] * m.x + pm[4] * m.y + pm[8] * m.z + pm[12]) * m_w * m_w;
+        const float mul2 = (pm[1] * m.x + pm[5] * m.y + pm[9] * m.z + pm[13]) * m_w * m_w;
+        const float gx2 = acc[0], gy2 = acc[1];
+        const f3 d2 = mk3((pm[0] * m_w - pm[3] * mul1) * gx2 + (pm[1] * m_w - pm[3] * mul2) * gy2,
+                          (pm[4] * m_w - pm[7] * mul1) * gx2 + (pm[5] * m_w - pm[7] * mul2) * gy2,
+                          (pm[8] * m_w - pm[11] * mul1) * gx2 + (pm[9] * m_w - pm[11] * mul2) * gy2);
+        dmean = dmean + d2;
+    }
+    // ---- SH -> RGB backward ----
+    if (a.shs) {
+        const int used = a.D >= 3 ? 16 : (a.D + 1) * (a.D + 1);
+        dmean = dmean + sh_backward(a.D, m, ld3(a.campos), a.shs + (size_t)idx * a.M * 3, a.clamped[idx],
+                                    mk3(acc[6], acc[7], acc[8]), dsh);
+        for (int k = used * 3; k < a.M * 3; ++k) dsh[k] = 0.f;
+    } else if (dsh) {
+        for (int k = 0; k < a.M * 3; ++k) dsh[k] = 0.f;
+    }
+    a.dL_dmeans3D[3 * (size_t)idx] = dmean.x;
+    a.dL_dmeans3D[3 * (size_t)idx + 1] = dmean.y;
+    a.dL_dmeans3D[3 * (size_t)idx + 2] = dmean.z;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) a.dL_dcov3D[6 * (size_t)idx + k] = dcov[k];
+    // ---- scale / rotation ----
+    if (a.scales) {
+        float ds[3], dr[4];
+        cov3d_backward(scale, a.scale_modifier, rot, dcov, ds, dr);
+        a.dL_dscales[3 * (size_t)idx] = ds[0];
+        a.dL_dscales[3 * (size_t)idx + 1] = ds[1];
+        a.dL_dscales[3 * (size_t)idx + 2] = ds[2];
+        *reinterpret_cast<float4*>(a.dL_drot + 4 * (size_t)idx) = make_float4(dr[0], dr[1], dr[2], dr[3]);
+    } else {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) a.dL_dscales[3 * (size_t)idx + k] = 0.f;
+        *reinterpret_cast<float4*>(a.dL_drot + 4 * (size_t)idx) = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+}
+
+void launch_gauss_backward(const GaussBwdArgs& a, hipStream_t s) {
+    if (a.P <= 0) return;
+    hipLaunchKernelGGL(k_gauss_bwd, dim3(div_up(a.P, 256)), dim3(256), 0, s, a);
+}
+
+}  // namespace gs

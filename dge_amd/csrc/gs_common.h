@@ -1,0 +1,187 @@
+// gs_common.h — device-side building blocks shared by the gfx950 kernels.
+//
+// The per-Gaussian math restates the reference rasterizer
+// (gaussiansplatting/submodules/diff-gaussian-rasterization/cuda_rasterizer/
+//  forward.cu, backward.cu, auxiliary.h); every helper cites the lines whose
+// numerics it must reproduce.  Matrices are the reference's float[16]
+// (column-major transforms, auxiliary.h:58-97).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace gs {
+
+constexpr int kTile = 16;             // BLOCK_X = BLOCK_Y (config.h:15-16)
+constexpr int kTilePixels = kTile * kTile;
+constexpr int kWave = 64;             // CDNA wavefront
+constexpr int kQuad = 8;              // a wave rasterises one 8x8 quadrant of a tile
+
+// auxiliary.h:22-39
+__device__ constexpr float kSH_C0 = 0.28209479177387814f;
+__device__ constexpr float kSH_C1 = 0.4886025119029199f;
+__device__ constexpr float kSH_C2_0 = 1.0925484305920792f;
+__device__ constexpr float kSH_C2_1 = -1.0925484305920792f;
+__device__ constexpr float kSH_C2_2 = 0.31539156525252005f;
+__device__ constexpr float kSH_C2_3 = -1.0925484305920792f;
+__device__ constexpr float kSH_C2_4 = 0.5462742152960396f;
+__device__ constexpr float kSH_C3_0 = -0.5900435899266435f;
+__device__ constexpr float kSH_C3_1 = 2.890611442640554f;
+__device__ constexpr float kSH_C3_2 = -0.4570457994644658f;
+__device__ constexpr float kSH_C3_3 = 0.3731763325901154f;
+__device__ constexpr float kSH_C3_4 = -0.4570457994644658f;
+__device__ constexpr float kSH_C3_5 = 1.445305721320277f;
+__device__ constexpr float kSH_C3_6 = -0.5900435899266435f;
+
+struct f3 {
+    float x, y, z;
+};
+__device__ __forceinline__ f3 mk3(float x, float y, float z) { return f3{x, y, z}; }
+__device__ __forceinline__ f3 operator+(f3 a, f3 b) { return mk3(a.x + b.x, a.y + b.y, a.z + b.z); }
+__device__ __forceinline__ f3 operator-(f3 a, f3 b) { return mk3(a.x - b.x, a.y - b.y, a.z - b.z); }
+__device__ __forceinline__ f3 operator*(f3 a, float s) { return mk3(a.x * s, a.y * s, a.z * s); }
+__device__ __forceinline__ float dot3(f3 a, f3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+__device__ __forceinline__ f3 ld3(const float* p) { return mk3(p[0], p[1], p[2]); }
+
+// Camera constants, read once per thread from device memory (uniform ->
+// scalar loads).
+struct Camera {
+    float v[16];  // viewmatrix
+    float p[16];  // projmatrix
+};
+
+__device__ __forceinline__ void load_camera(const float* __restrict__ view, const float* __restrict__ proj, Camera& c) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        c.v[i] = view[i];
+        c.p[i] = proj[i];
+    }
+}
+
+// auxiliary.h:58-66
+__device__ __forceinline__ f3 view_point(const float* m, f3 p) {
+    return mk3(m[0] * p.x + m[4] * p.y + m[8] * p.z + m[12], m[1] * p.x + m[5] * p.y + m[9] * p.z + m[13],
+               m[2] * p.x + m[6] * p.y + m[10] * p.z + m[14]);
+}
+// auxiliary.h:68-77
+__device__ __forceinline__ float4 proj_point(const float* m, f3 p) {
+    return make_float4(m[0] * p.x + m[4] * p.y + m[8] * p.z + m[12], m[1] * p.x + m[5] * p.y + m[9] * p.z + m[13],
+                       m[2] * p.x + m[6] * p.y + m[10] * p.z + m[14], m[3] * p.x + m[7] * p.y + m[11] * p.z + m[15]);
+}
+
+// auxiliary.h:41-44 — the 1.0 literals make the reference evaluate in double.
+__device__ __forceinline__ float ndc_to_pixel(float v, int S) { return (float)((((double)v + 1.0) * S - 1.0) * 0.5); }
+
+// auxiliary.h:46-56 (float arithmetic, truncation toward zero, clamp to grid)
+struct Rect {
+    int x0, y0, x1, y1;
+};
+__device__ __forceinline__ Rect tile_rect(float px, float py, int r, int gx, int gy) {
+    Rect q;
+    q.x0 = min(gx, max(0, (int)((px - (float)r) / (float)kTile)));
+    q.y0 = min(gy, max(0, (int)((py - (float)r) / (float)kTile)));
+    q.x1 = min(gx, max(0, (int)((((px + (float)r) + (float)kTile) - 1.0f) / (float)kTile)));
+    q.y1 = min(gy, max(0, (int)((((py + (float)r) + (float)kTile) - 1.0f) / (float)kTile)));
+    return q;
+}
+
+// forward.cu:118-152 — Sigma = (S R)^T (S R) with R from the UNnormalised
+// quaternion (w,x,y,z).  Output: upper triangle [00,01,02,11,12,22].
+__device__ __forceinline__ void cov3d_from_scale_rot(f3 scale, float mod, float4 q, float cov[6]) {
+    const float r = q.x, x = q.y, y = q.z, z = q.w;
+    // rows of the rotation matrix in the reference's (column-major) layout:
+    // Rg[c][r] below is glm's R[c][r]
+    const float R00 = 1.f - 2.f * (y * y + z * z), R01 = 2.f * (x * y - r * z), R02 = 2.f * (x * z + r * y);
+    const float R10 = 2.f * (x * y + r * z), R11 = 1.f - 2.f * (x * x + z * z), R12 = 2.f * (y * z - r * x);
+    const float R20 = 2.f * (x * z - r * y), R21 = 2.f * (y * z + r * x), R22 = 1.f - 2.f * (x * x + y * y);
+    const float sx = mod * scale.x, sy = mod * scale.y, sz = mod * scale.z;
+    // M[c][r] = s_r * R[c][r]; Sigma[c][r] = sum_k M[r][k] * M[c][k]
+    const float M00 = sx * R00, M01 = sy * R01, M02 = sz * R02;
+    const float M10 = sx * R10, M11 = sy * R11, M12 = sz * R12;
+    const float M20 = sx * R20, M21 = sy * R21, M22 = sz * R22;
+    cov[0] = M00 * M00 + M01 * M01 + M02 * M02;
+    cov[1] = M10 * M00 + M11 * M01 + M12 * M02;
+    cov[2] = M20 * M00 + M21 * M01 + M22 * M02;
+    cov[3] = M10 * M10 + M11 * M11 + M12 * M12;
+    cov[4] = M20 * M10 + M21 * M11 + M22 * M12;
+    cov[5] = M20 * M20 + M21 * M21 + M22 * M22;
+}
+
+// The EWA projection of forward.cu:74-113 / backward.cu:160-199.
+// T holds the two non-zero rows of (J * W_rot) as T[i][j], i in {0,1}
+// (= glm T[i][j] in the reference); V is the symmetric 3D covariance.
+struct Ewa {
+    f3 t;                    // clamped camera-space mean
+    float txtz, tytz, limx, limy;
+    float J00, J02, J11, J12;
+    float T[2][3];
+    float V[3][3];
+};
+
+__device__ __forceinline__ void ewa_setup(f3 mean, float fx, float fy, float tanfovx, float tanfovy,
+                                          const float cov3D[6], const float* v, Ewa& e) {
+    f3 t = view_point(v, mean);
+    e.limx = 1.3f * tanfovx;
+    e.limy = 1.3f * tanfovy;
+    e.txtz = t.x / t.z;
+    e.tytz = t.y / t.z;
+    t.x = fminf(e.limx, fmaxf(-e.limx, e.txtz)) * t.z;
+    t.y = fminf(e.limy, fmaxf(-e.limy, e.tytz)) * t.z;
+    e.t = t;
+    e.J00 = fx / t.z;
+    e.J02 = -(fx * t.x) / (t.z * t.z);
+    e.J11 = fy / t.z;
+    e.J12 = -(fy * t.y) / (t.z * t.z);
+    // W (glm) = mat3(v0,v4,v8, v1,v5,v9, v2,v6,v10): W[k][r] = v[k + 4r]
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        e.T[0][j] = v[4 * j] * e.J00 + v[4 * j + 2] * e.J02;
+        e.T[1][j] = v[4 * j + 1] * e.J11 + v[4 * j + 2] * e.J12;
+    }
+    e.V[0][0] = cov3D[0]; e.V[0][1] = cov3D[1]; e.V[0][2] = cov3D[2];
+    e.V[1][0] = cov3D[1]; e.V[1][1] = cov3D[3]; e.V[1][2] = cov3D[4];
+    e.V[2][0] = cov3D[2]; e.V[2][1] = cov3D[4]; e.V[2][2] = cov3D[5];
+}
+
+// (T V)_i,k = sum_m T[i][m] V[k][m]
+__device__ __forceinline__ float tv(const Ewa& e, int i, int k) {
+    return e.T[i][0] * e.V[k][0] + e.T[i][1] * e.V[k][1] + e.T[i][2] * e.V[k][2];
+}
+
+// forward.cu:106-112: filtered 2D covariance (a, b, c)
+__device__ __forceinline__ void ewa_cov2d(const Ewa& e, float& a, float& b, float& c) {
+    const float B00 = tv(e, 0, 0), B01 = tv(e, 0, 1), B02 = tv(e, 0, 2);
+    const float B10 = tv(e, 1, 0), B11 = tv(e, 1, 1), B12 = tv(e, 1, 2);
+    a = (B00 * e.T[0][0] + B01 * e.T[0][1] + B02 * e.T[0][2]) + 0.3f;
+    b = B10 * e.T[0][0] + B11 * e.T[0][1] + B12 * e.T[0][2];
+    c = (B10 * e.T[1][0] + B11 * e.T[1][1] + B12 * e.T[1][2]) + 0.3f;
+}
+
+// ---------------------------------------------------------------------
+// wave-level primitives (64 lanes)
+// ---------------------------------------------------------------------
+__device__ __forceinline__ int lane_id() { return __lane_id(); }
+__device__ __forceinline__ uint64_t lanemask_lt() { return (1ull << lane_id()) - 1ull; }
+
+// Sum over the 64 lanes with DPP row ops; the total lands in lane 63.
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ float dpp_mov(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, ROW_MASK, 0xF, false));
+}
+__device__ __forceinline__ float wave_sum_to_lane63(float v) {
+    v += dpp_mov<0xB1, 0xF>(v);   // quad_perm [1,0,3,2]
+    v += dpp_mov<0x4E, 0xF>(v);   // quad_perm [2,3,0,1]
+    v += dpp_mov<0x141, 0xF>(v);  // row_half_mirror
+    v += dpp_mov<0x140, 0xF>(v);  // row_mirror
+    v += dpp_mov<0x142, 0xA>(v);  // row_bcast:15 into rows 1,3
+    v += dpp_mov<0x143, 0xC>(v);  // row_bcast:31 into rows 2,3
+    return v;
+}
+
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o));
+    return v;
+}
+
+}  // namespace gs

@@ -1,0 +1,239 @@
+// gs_internal.h — buffer layouts and kernel launchers shared by the HIP
+// translation units of libgs_raster.so.  Not part of the C ABI.
+//
+// Buffer design (MI355X-first; the reference's GeometryState / BinningState /
+// ImageState live in rasterizer_impl.h:21-73 and are NOT mirrored):
+//   geometry (per Gaussian, SoA, 256-B aligned arrays):
+//     means2D float2, conic_opacity float4, rgbd float4 (colour + depth, one
+//     16-B gather in the blend loop), tiles_touched u32, clamped u8 (3 bits),
+//     radii i32, first_slot u32 (first binning slot of the Gaussian),
+//     depth sort ping-pong (key u32 = depth bits, val u32 = index) and scratch.
+//   binning (per tile instance): tile-key sort ping-pong, slot_gauss (slot ->
+//     Gaussian), point_list (sorted position -> Gaussian), slot_to_pos, and the
+//     per-instance gradient records written by the backward blend.
+//   image (per pixel / tile): final_T, n_contrib, ranges uint2, tile_last
+//     (max n_contrib over the tile, the backward's start position).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace gs {
+
+constexpr int kSortIPT = 16;                    // keys per thread in the radix kernels
+constexpr int kSortTile = 256 * kSortIPT;       // keys per workgroup
+constexpr int kScanIPT = 16;
+constexpr int kScanTile = 256 * kScanIPT;
+constexpr int kMaxSinglePassBits = 11;          // tile keys up to 2048 tiles sort in one pass
+constexpr size_t kAlign = 256;
+
+__host__ __device__ inline size_t align_up(size_t x, size_t a = kAlign) { return (x + a - 1) / a * a; }
+inline int div_up(long long a, long long b) { return (int)((a + b - 1) / b); }
+
+inline int ceil_log2(uint32_t n) {
+    int b = 0;
+    while ((1u << b) < n) ++b;
+    return b;
+}
+
+// Radix pass plan for the tile-key sort.
+struct TileSortPlan {
+    int bits;          // total key bits
+    int passes;        // 1 or 2
+    int bits0, bits1;  // digit width of each pass
+};
+inline TileSortPlan tile_sort_plan(int num_tiles) {
+    TileSortPlan p;
+    p.bits = ceil_log2((uint32_t)(num_tiles > 1 ? num_tiles : 2));
+    if (p.bits <= kMaxSinglePassBits) {
+        p.passes = 1; p.bits0 = p.bits; p.bits1 = 0;
+    } else {
+        p.passes = 2; p.bits0 = (p.bits + 1) / 2; p.bits1 = p.bits - p.bits0;
+    }
+    return p;
+}
+
+struct GeomLayout {
+    size_t means2D, conic_opacity, rgbd, tiles_touched, clamped, radii, first_slot;
+    size_t key0, key1, val0, val1, sort_hist, sort_totals, scan_sums, counters, total;
+    int sort_blocks, scan_blocks;
+};
+inline GeomLayout geom_layout(int P) {
+    GeomLayout L;
+    size_t o = 0;
+    size_t p = (size_t)(P > 0 ? P : 1);
+    L.sort_blocks = div_up((long long)p, kSortTile);
+    L.scan_blocks = div_up((long long)p, kScanTile);
+    L.means2D = o; o = align_up(o + 8 * p);
+    L.conic_opacity = o; o = align_up(o + 16 * p);
+    L.rgbd = o; o = align_up(o + 16 * p);
+    L.tiles_touched = o; o = align_up(o + 4 * p);
+    L.clamped = o; o = align_up(o + 1 * p);
+    L.radii = o; o = align_up(o + 4 * p);
+    L.first_slot = o; o = align_up(o + 4 * p);
+    L.key0 = o; o = align_up(o + 4 * p);
+    L.key1 = o; o = align_up(o + 4 * p);
+    L.val0 = o; o = align_up(o + 4 * p);
+    L.val1 = o; o = align_up(o + 4 * p);
+    L.sort_hist = o; o = align_up(o + 4 * 256 * (size_t)L.sort_blocks);
+    L.sort_totals = o; o = align_up(o + 4 * 256);
+    L.scan_sums = o; o = align_up(o + 4 * (size_t)(L.scan_blocks + 1));
+    L.counters = o; o = align_up(o + 16);
+    L.total = o;
+    return L;
+}
+
+struct ImgLayout {
+    size_t final_T, n_contrib, ranges, tile_last, total;
+};
+inline ImgLayout img_layout(int W, int H) {
+    ImgLayout L;
+    size_t o = 0;
+    size_t n = (size_t)W * H;
+    size_t tiles = (size_t)div_up(W, 16) * div_up(H, 16);
+    L.final_T = o; o = align_up(o + 4 * n);
+    L.n_contrib = o; o = align_up(o + 4 * n);
+    L.ranges = o; o = align_up(o + 8 * tiles);
+    L.tile_last = o; o = align_up(o + 4 * tiles);
+    L.total = o;
+    return L;
+}
+
+struct BinLayout {
+    size_t key0, key1, val0, val1, slot_gauss, point_list, slot_to_pos, records, sort_hist, sort_totals, total;
+    int sort_blocks;
+};
+inline BinLayout bin_layout(int K, int num_tiles) {
+    BinLayout L;
+    size_t o = 0;
+    size_t k = (size_t)(K > 0 ? K : 1);
+    TileSortPlan plan = tile_sort_plan(num_tiles);
+    int maxbits = plan.bits0 > plan.bits1 ? plan.bits0 : plan.bits1;
+    L.sort_blocks = div_up((long long)k, kSortTile);
+    L.key0 = o; o = align_up(o + 4 * k);
+    L.key1 = o; o = align_up(o + 4 * k);
+    L.val0 = o; o = align_up(o + 4 * k);
+    L.val1 = o; o = align_up(o + 4 * k);
+    L.slot_gauss = o; o = align_up(o + 4 * k);
+    L.point_list = o; o = align_up(o + 4 * k);
+    L.slot_to_pos = o; o = align_up(o + 4 * k);
+    L.records = o; o = align_up(o + 48 * k);
+    L.sort_hist = o; o = align_up(o + 4 * ((size_t)1 << maxbits) * (size_t)L.sort_blocks);
+    L.sort_totals = o; o = align_up(o + 4 * ((size_t)1 << maxbits));
+    L.total = o;
+    return L;
+}
+
+// ---------------------------------------------------------------------
+// launchers (defined in the .hip translation units)
+// ---------------------------------------------------------------------
+struct PreprocessArgs {
+    int P, D, M, W, H, gx, gy;
+    const float *means3D, *shs, *colors_precomp, *opacities, *scales, *rotations, *cov3D_precomp;
+    const float *view, *proj, *campos;
+    float tanfovx, tanfovy, fx, fy, scale_modifier;
+    int prefiltered, copy_colors;
+    int* radii_out;
+    int* radii;
+    float2* means2D;
+    float4* conic_opacity;
+    float4* rgbd;
+    uint32_t* tiles_touched;
+    uint8_t* clamped;
+    uint32_t* depth_key;
+    uint32_t* depth_val;
+    uint32_t* counters;  // [0] instance total, [1] error flag
+};
+void launch_preprocess(const PreprocessArgs& a, hipStream_t s);
+void launch_mark_visible(int P, const float* means3D, const float* view, uint8_t* present, hipStream_t s);
+
+// LSD radix sort of (u32 key, u32 value).  Returns the buffer index (0/1)
+// holding the result.  identity_vals: values of the first pass are the
+// element indices (val0 is not read).
+int radix_sort_pairs(uint32_t* key0, uint32_t* key1, uint32_t* val0, uint32_t* val1, uint32_t n, int begin_bit,
+                     int end_bit, int max_pass_bits, bool identity_vals, uint32_t* hist, uint32_t* totals,
+                     int nblocks, hipStream_t s);
+
+struct EmitArgs {
+    int P, gx, gy;
+    const uint32_t* order;       // Gaussian ids by depth rank
+    const uint32_t* tiles_touched;
+    const float2* means2D;
+    const int* radii;
+    uint32_t* scan_sums;         // [scan_blocks + 1]
+    uint32_t* first_slot;
+    uint32_t* tile_key;          // K
+    uint32_t* slot_gauss;        // K
+    int scan_blocks;
+};
+void launch_scan_reduce(const EmitArgs& a, hipStream_t s);
+void launch_scan_emit(const EmitArgs& a, hipStream_t s);
+
+void launch_ranges(const uint32_t* sorted_tile, const uint32_t* sorted_slot, const uint32_t* slot_gauss, int K,
+                   uint2* ranges, uint32_t* point_list, uint32_t* slot_to_pos, hipStream_t s);
+
+struct RenderArgs {
+    int W, H, gx, gy;
+    const uint2* ranges;
+    const uint32_t* point_list;
+    const float2* means2D;
+    const float4* conic_opacity;
+    const float4* rgbd;
+    const float* bg;
+    float* final_T;
+    uint32_t* n_contrib;
+    uint32_t* tile_last;
+    float* out_color;
+    float* out_depth;
+};
+void launch_render_forward(const RenderArgs& a, hipStream_t s);
+
+struct ApplyWeightsArgs {
+    int W, H, gx, gy, C;
+    const uint2* ranges;
+    const uint32_t* point_list;
+    const float2* means2D;
+    const float4* conic_opacity;
+    const float* image_weights;
+    float* weights;
+    int* cnt;
+};
+void launch_render_apply_weights(const ApplyWeightsArgs& a, hipStream_t s);
+
+struct RenderBwdArgs {
+    int W, H, gx, gy;
+    const uint2* ranges;
+    const uint32_t* point_list;
+    const uint32_t* tile_last;
+    const float2* means2D;
+    const float4* conic_opacity;
+    const float4* rgbd;
+    const float* bg;
+    const float* final_T;
+    const uint32_t* n_contrib;
+    const float* dL_dpix;
+    float4* records;  // 3 float4 per instance
+};
+void launch_render_backward(const RenderBwdArgs& a, hipStream_t s);
+
+struct GaussBwdArgs {
+    int P, D, M, W, H, gx, gy;
+    const float *means3D, *shs, *scales, *rotations, *cov3D_precomp;
+    const float *view, *proj, *campos;
+    float tanfovx, tanfovy, fx, fy, scale_modifier;
+    const int* radii;       // caller's radii (the reference's visibility gate)
+    const int* geom_radii;  // radii stored by the forward (bin geometry)
+    const float2* means2D;
+    const uint32_t* tiles_touched;
+    const uint32_t* first_slot;
+    const uint8_t* clamped;
+    const uint32_t* slot_to_pos;
+    const uint2* ranges;
+    const uint32_t* tile_last;
+    const float4* records;
+    float *dL_dmeans2D, *dL_dcolors, *dL_dopacity, *dL_dmeans3D, *dL_dcov3D, *dL_dsh, *dL_dscales, *dL_drot;
+};
+void launch_gauss_backward(const GaussBwdArgs& a, hipStream_t s);
+
+}  // namespace gs

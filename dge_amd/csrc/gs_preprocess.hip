@@ -1,0 +1,142 @@
+// gs_preprocess.hip — per-Gaussian forward preprocessing for gfx950.
+//
+// Restates preprocessCUDA (forward.cu:155-256) with computeCov3D (:118-152),
+// computeCov2D (:74-113), computeColorFromSH (:20-71) and in_frustum
+// (auxiliary.h:139-164), and fuses three steps the reference runs separately:
+//   * the depth sort key (bits of the view-space depth, or 0xFFFFFFFF when the
+//     Gaussian is culled) that replaces the reference's (tile|depth) 64-bit key;
+//   * the instance total num_rendered (one atomic per workgroup), so the host
+//     read-back overlaps the depth sort instead of draining the stream;
+//   * colour and depth packed into one float4 (rgbd) for the blend loop.
+// One thread per Gaussian; 256-thread workgroups (4 waves).
+#include "gs_common.h"
+#include "gs_internal.h"
+
+namespace gs {
+
+// forward.cu:20-71
+__device__ __forceinline__ f3 sh_to_rgb(int deg, f3 pos, f3 campos, const float* __restrict__ sh, uint8_t& clamp_bits) {
+    f3 dir = pos - campos;
+    const float len = sqrtf(dot3(dir, dir));
+    dir = mk3(dir.x / len, dir.y / len, dir.z / len);
+    f3 res = ld3(sh) * kSH_C0;
+    if (deg > 0) {
+        const float x = dir.x, y = dir.y, z = dir.z;
+        res = res - ld3(sh + 3) * (kSH_C1 * y) + ld3(sh + 6) * (kSH_C1 * z) - ld3(sh + 9) * (kSH_C1 * x);
+        if (deg > 1) {
+            const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
+            res = res + ld3(sh + 12) * (kSH_C2_0 * xy) + ld3(sh + 15) * (kSH_C2_1 * yz) +
+                  ld3(sh + 18) * (kSH_C2_2 * (2.0f * zz - xx - yy)) + ld3(sh + 21) * (kSH_C2_3 * xz) +
+                  ld3(sh + 24) * (kSH_C2_4 * (xx - yy));
+            if (deg > 2) {
+                res = res + ld3(sh + 27) * (kSH_C3_0 * y * (3.0f * xx - yy)) + ld3(sh + 30) * (kSH_C3_1 * xy * z) +
+                      ld3(sh + 33) * (kSH_C3_2 * y * (4.0f * zz - xx - yy)) +
+                      ld3(sh + 36) * (kSH_C3_3 * z * (2.0f * zz - 3.0f * xx - 3.0f * yy)) +
+                      ld3(sh + 39) * (kSH_C3_4 * x * (4.0f * zz - xx - yy)) +
+                      ld3(sh + 42) * (kSH_C3_5 * z * (xx - yy)) + ld3(sh + 45) * (kSH_C3_6 * x * (xx - 3.0f * yy));
+            }
+        }
+    }
+    res = mk3(res.x + 0.5f, res.y + 0.5f, res.z + 0.5f);
+    clamp_bits = (res.x < 0 ? 1 : 0) | (res.y < 0 ? 2 : 0) | (res.z < 0 ? 4 : 0);
+    return mk3(fmaxf(res.x, 0.0f), fmaxf(res.y, 0.0f), fmaxf(res.z, 0.0f));
+}
+
+__global__ __launch_bounds__(256) void k_preprocess(PreprocessArgs a) {
+    const int idx = blockIdx.x * 256 + threadIdx.x;
+    uint32_t touched = 0;
+    if (idx < a.P) {
+        int radius_out = 0;
+        uint32_t key = 0xFFFFFFFFu;
+        uint8_t clamp_bits = 0;
+        const float* v = a.view;
+        const float* pm = a.proj;
+        const f3 p = ld3(a.means3D + 3 * (size_t)idx);
+        // in_frustum (auxiliary.h:139-164): only the near test is live
+        const float4 ph = proj_point(pm, p);
+        const float pw = 1.0f / (ph.w + 0.0000001f);
+        const f3 pv = view_point(v, p);
+        bool visible = pv.z > 0.2f;
+        if (!visible && a.prefiltered) atomicOr(&a.counters[1], 1u);
+        if (visible) {
+            float cov3[6];
+            if (a.cov3D_precomp) {
+#pragma unroll
+                for (int k = 0; k < 6; ++k) cov3[k] = a.cov3D_precomp[6 * (size_t)idx + k];
+            } else {
+                const float4 q = *reinterpret_cast<const float4*>(a.rotations + 4 * (size_t)idx);
+                cov3d_from_scale_rot(ld3(a.scales + 3 * (size_t)idx), a.scale_modifier, q, cov3);
+            }
+            Ewa e;
+            ewa_setup(p, a.fx, a.fy, a.tanfovx, a.tanfovy, cov3, v, e);
+            float ca, cb, cc;
+            ewa_cov2d(e, ca, cb, cc);
+            const float det = ca * cc - cb * cb;
+            if (det != 0.0f) {
+                const float det_inv = 1.f / det;
+                const float4 conic = make_float4(cc * det_inv, -cb * det_inv, ca * det_inv, a.opacities[idx]);
+                const float mid = 0.5f * (ca + cc);
+                const float l1 = mid + sqrtf(fmaxf(0.1f, mid * mid - det));
+                const float l2 = mid - sqrtf(fmaxf(0.1f, mid * mid - det));
+                const float rad = ceilf(3.f * sqrtf(fmaxf(l1, l2)));
+                const float px = ndc_to_pixel(ph.x * pw, a.W), py = ndc_to_pixel(ph.y * pw, a.H);
+                const Rect r = tile_rect(px, py, (int)rad, a.gx, a.gy);
+                const uint32_t area = (uint32_t)((r.y1 - r.y0) * (r.x1 - r.x0));
+                if (area != 0) {
+                    f3 rgb = mk3(0, 0, 0);
+                    if (a.copy_colors) {
+                        if (a.colors_precomp) {
+                            rgb = ld3(a.colors_precomp + 3 * (size_t)idx);
+                        } else {
+                            rgb = sh_to_rgb(a.D, p, ld3(a.campos), a.shs + (size_t)idx * a.M * 3, clamp_bits);
+                        }
+                    }
+                    a.means2D[idx] = make_float2(px, py);
+                    a.conic_opacity[idx] = conic;
+                    a.rgbd[idx] = make_float4(rgb.x, rgb.y, rgb.z, pv.z);
+                    radius_out = (int)rad;
+                    touched = area;
+                    key = __float_as_uint(pv.z);  // depth > 0.2: the bits sort as the value
+                }
+            }
+        }
+        a.radii[idx] = radius_out;
+        if (a.radii_out) a.radii_out[idx] = radius_out;
+        a.tiles_touched[idx] = touched;
+        a.clamped[idx] = clamp_bits;
+        a.depth_key[idx] = key;
+        a.depth_val[idx] = (uint32_t)idx;
+    }
+    // workgroup total of instances -> one atomic
+    __shared__ uint32_t part[4];
+    uint32_t s = touched;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) s += (uint32_t)__shfl_xor((int)s, o);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t t = part[0] + part[1] + part[2] + part[3];
+        if (t) atomicAdd(&a.counters[0], t);
+    }
+}
+
+void launch_preprocess(const PreprocessArgs& a, hipStream_t s) {
+    if (a.P <= 0) return;
+    hipLaunchKernelGGL(k_preprocess, dim3(div_up(a.P, 256)), dim3(256), 0, s, a);
+}
+
+// checkFrustum (rasterizer_impl.cu:53-63)
+__global__ __launch_bounds__(256) void k_mark_visible(int P, const float* __restrict__ means3D,
+                                                      const float* __restrict__ view, uint8_t* __restrict__ present) {
+    const int idx = blockIdx.x * 256 + threadIdx.x;
+    if (idx >= P) return;
+    const f3 pv = view_point(view, ld3(means3D + 3 * (size_t)idx));
+    present[idx] = pv.z > 0.2f ? 1 : 0;
+}
+
+void launch_mark_visible(int P, const float* means3D, const float* view, uint8_t* present, hipStream_t s) {
+    if (P <= 0) return;
+    hipLaunchKernelGGL(k_mark_visible, dim3(div_up(P, 256)), dim3(256), 0, s, P, means3D, view, present);
+}
+
+}  // namespace gs

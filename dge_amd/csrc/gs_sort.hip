@@ -1,0 +1,348 @@
+// gs_sort.hip — binning for gfx950: depth sort, instance scan + emission,
+// tile-key sort, tile ranges.
+//
+// The reference (rasterizer_impl.cu:227-270) scans tiles_touched in Gaussian
+// order, emits a 64-bit (tile << 32 | depth) key per instance
+// (duplicateWithKeys, :67-100) and radix-sorts all K instances on 32+log2(tiles)
+// bits with cub (:253-261).  Because that sort is stable and emission follows
+// Gaussian order, the result is: per tile, instances ordered by (depth bits,
+// Gaussian index).  This file produces the identical order with less traffic:
+//   1. stable LSD sort of the P visible depth keys (32-bit key, index value);
+//   2. exclusive scan of tiles_touched in depth order, then emission of one
+//      (tile, slot) instance per overlapped tile — instances are therefore
+//      already depth-ordered;
+//   3. stable LSD sort of the K instances on the tile id only (one pass for
+//      up to 2048 tiles);
+//   4. tile ranges + the slot -> Gaussian / slot -> position maps.
+// The radix kernels rank keys inside a workgroup with 64-lane ballots
+// (peer-mask match per digit), keep per-wave digit counters in LDS and never
+// use global atomics, so every pass is deterministic.
+#include "gs_common.h"
+#include "gs_internal.h"
+
+namespace gs {
+
+// ---------------------------------------------------------------------
+// helpers
+// ---------------------------------------------------------------------
+template <int BITS>
+__device__ __forceinline__ uint64_t match_digit(uint32_t d, uint64_t valid_mask) {
+    uint64_t m = valid_mask;
+#pragma unroll
+    for (int b = 0; b < BITS; ++b) {
+        const bool bit = (d >> b) & 1u;
+        const uint64_t bal = __ballot(bit);
+        m &= bit ? bal : ~bal;
+    }
+    return m;
+}
+
+// 256-thread exclusive scan; `total` receives the workgroup sum.
+__device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* lds4, uint32_t& total) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint32_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)x, o);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) lds4[w] = x;
+    __syncthreads();
+    uint32_t wbase = 0, t = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint32_t c = lds4[i];
+        wbase += (i < w) ? c : 0u;
+        t += c;
+    }
+    __syncthreads();
+    total = t;
+    return wbase + x - v;
+}
+
+// ---------------------------------------------------------------------
+// radix sort: histogram -> per-digit scan -> stable scatter
+// ---------------------------------------------------------------------
+template <int BITS>
+__global__ __launch_bounds__(256) void k_radix_hist(const uint32_t* __restrict__ keys, uint32_t n, int shift,
+                                                    uint32_t* __restrict__ hist, int nb) {
+    constexpr int NDIG = 1 << BITS;
+    __shared__ uint32_t cnt[4][NDIG];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    for (int i = tid; i < 4 * NDIG; i += 256) (&cnt[0][0])[i] = 0;
+    __syncthreads();
+    const uint32_t base = blockIdx.x * (uint32_t)kSortTile + w * 64u * kSortIPT;
+    uint32_t key[kSortIPT];
+#pragma unroll
+    for (int it = 0; it < kSortIPT; ++it) {
+        const uint32_t idx = base + it * 64 + lane;
+        key[it] = idx < n ? keys[idx] : 0u;
+    }
+#pragma unroll
+    for (int it = 0; it < kSortIPT; ++it) {
+        const uint32_t idx = base + it * 64 + lane;
+        const bool valid = idx < n;
+        const uint64_t vm = __ballot(valid);
+        if (vm == 0) break;
+        const uint32_t d = (key[it] >> shift) & (NDIG - 1);
+        const uint64_t peers = match_digit<BITS>(d, vm);
+        if (valid && (peers & lanemask_lt()) == 0) cnt[w][d] += (uint32_t)__popcll(peers);
+    }
+    __syncthreads();
+    for (int d = tid; d < NDIG; d += 256)
+        hist[(size_t)d * nb + blockIdx.x] = cnt[0][d] + cnt[1][d] + cnt[2][d] + cnt[3][d];
+}
+
+// One workgroup per digit: exclusive scan of hist[d][0..nb) in place,
+// totals[d] = digit count.
+__global__ __launch_bounds__(256) void k_radix_digit_scan(uint32_t* __restrict__ hist, int nb,
+                                                          uint32_t* __restrict__ totals) {
+    __shared__ uint32_t lds4[4];
+    uint32_t* row = hist + (size_t)blockIdx.x * nb;
+    const int per = (nb + 255) / 256;
+    const int beg = threadIdx.x * per;
+    uint32_t s = 0;
+    for (int i = 0; i < per; ++i) {
+        const int j = beg + i;
+        if (j < nb) s += row[j];
+    }
+    uint32_t total;
+    uint32_t run = block_exclusive_scan(s, lds4, total);
+    for (int i = 0; i < per; ++i) {
+        const int j = beg + i;
+        if (j < nb) {
+            const uint32_t c = row[j];
+            row[j] = run;
+            run += c;
+        }
+    }
+    if (threadIdx.x == 0) totals[blockIdx.x] = total;
+}
+
+template <int BITS, bool IDV>
+__global__ __launch_bounds__(256) void k_radix_scatter(const uint32_t* __restrict__ keys_in,
+                                                       const uint32_t* __restrict__ vals_in,
+                                                       uint32_t* __restrict__ keys_out, uint32_t* __restrict__ vals_out,
+                                                       uint32_t n, int shift, const uint32_t* __restrict__ hist,
+                                                       const uint32_t* __restrict__ totals, int nb) {
+    constexpr int NDIG = 1 << BITS;
+    constexpr int PER = NDIG >= 256 ? NDIG / 256 : 1;
+    __shared__ uint32_t cnt[4][NDIG];
+    __shared__ uint32_t dbase[NDIG];
+    __shared__ uint32_t lds4[4];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    for (int i = tid; i < 4 * NDIG; i += 256) (&cnt[0][0])[i] = 0;
+    {  // dbase = exclusive scan of the digit totals
+        uint32_t loc[PER];
+        uint32_t s = 0;
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const int d = tid * PER + i;
+            loc[i] = d < NDIG ? totals[d] : 0u;
+            s += loc[i];
+        }
+        uint32_t tot;
+        uint32_t run = block_exclusive_scan(s, lds4, tot);
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const int d = tid * PER + i;
+            if (d < NDIG) dbase[d] = run;
+            run += loc[i];
+        }
+    }
+    __syncthreads();
+    const uint32_t base = blockIdx.x * (uint32_t)kSortTile + w * 64u * kSortIPT;
+    uint32_t key[kSortIPT], val[kSortIPT], loc[kSortIPT];
+#pragma unroll
+    for (int it = 0; it < kSortIPT; ++it) {
+        const uint32_t idx = base + it * 64 + lane;
+        const bool valid = idx < n;
+        key[it] = valid ? keys_in[idx] : 0u;
+        val[it] = IDV ? idx : (valid ? vals_in[idx] : 0u);
+    }
+#pragma unroll
+    for (int it = 0; it < kSortIPT; ++it) {
+        const uint32_t idx = base + it * 64 + lane;
+        const bool valid = idx < n;
+        const uint64_t vm = __ballot(valid);
+        if (vm == 0) break;
+        const uint32_t d = (key[it] >> shift) & (NDIG - 1);
+        const uint64_t peers = match_digit<BITS>(d, vm);
+        const uint32_t rank = (uint32_t)__popcll(peers & lanemask_lt());
+        const uint32_t old = cnt[w][d];
+        loc[it] = old + rank;
+        if (valid && rank == 0) cnt[w][d] = old + (uint32_t)__popcll(peers);
+    }
+    __syncthreads();
+    for (int d = tid; d < NDIG; d += 256) {
+        const uint32_t c0 = cnt[0][d], c1 = cnt[1][d], c2 = cnt[2][d];
+        const uint32_t g = dbase[d] + hist[(size_t)d * nb + blockIdx.x];
+        cnt[0][d] = g;
+        cnt[1][d] = g + c0;
+        cnt[2][d] = g + c0 + c1;
+        cnt[3][d] = g + c0 + c1 + c2;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < kSortIPT; ++it) {
+        const uint32_t idx = base + it * 64 + lane;
+        if (idx < n) {
+            const uint32_t d = (key[it] >> shift) & (NDIG - 1);
+            const uint32_t pos = cnt[w][d] + loc[it];
+            keys_out[pos] = key[it];
+            vals_out[pos] = val[it];
+        }
+    }
+}
+
+template <int BITS>
+static void radix_pass(const uint32_t* kin, const uint32_t* vin, uint32_t* kout, uint32_t* vout, uint32_t n, int shift,
+                       bool idv, uint32_t* hist, uint32_t* totals, int nb, hipStream_t s) {
+    constexpr int NDIG = 1 << BITS;
+    hipLaunchKernelGGL(k_radix_hist<BITS>, dim3(nb), dim3(256), 0, s, kin, n, shift, hist, nb);
+    hipLaunchKernelGGL(k_radix_digit_scan, dim3(NDIG), dim3(256), 0, s, hist, nb, totals);
+    if (idv)
+        hipLaunchKernelGGL((k_radix_scatter<BITS, true>), dim3(nb), dim3(256), 0, s, kin, vin, kout, vout, n, shift,
+                           hist, totals, nb);
+    else
+        hipLaunchKernelGGL((k_radix_scatter<BITS, false>), dim3(nb), dim3(256), 0, s, kin, vin, kout, vout, n, shift,
+                           hist, totals, nb);
+}
+
+static void radix_pass_bits(int bits, const uint32_t* kin, const uint32_t* vin, uint32_t* kout, uint32_t* vout,
+                            uint32_t n, int shift, bool idv, uint32_t* hist, uint32_t* totals, int nb, hipStream_t s) {
+    switch (bits) {
+#define GS_CASE(B) \
+    case B: radix_pass<B>(kin, vin, kout, vout, n, shift, idv, hist, totals, nb, s); break;
+        GS_CASE(1) GS_CASE(2) GS_CASE(3) GS_CASE(4) GS_CASE(5) GS_CASE(6)
+        GS_CASE(7) GS_CASE(8) GS_CASE(9) GS_CASE(10) GS_CASE(11)
+#undef GS_CASE
+        default: break;
+    }
+}
+
+int radix_sort_pairs(uint32_t* key0, uint32_t* key1, uint32_t* val0, uint32_t* val1, uint32_t n, int begin_bit,
+                     int end_bit, int max_pass_bits, bool identity_vals, uint32_t* hist, uint32_t* totals, int nblocks,
+                     hipStream_t s) {
+    uint32_t* k[2] = {key0, key1};
+    uint32_t* v[2] = {val0, val1};
+    int cur = 0;
+    const int total_bits = end_bit - begin_bit;
+    const int passes = (total_bits + max_pass_bits - 1) / max_pass_bits;
+    int shift = begin_bit;
+    for (int p = 0; p < passes; ++p) {
+        // split the bits evenly over the passes
+        const int rem = end_bit - shift;
+        const int bits = (rem + (passes - p) - 1) / (passes - p);
+        radix_pass_bits(bits, k[cur], v[cur], k[cur ^ 1], v[cur ^ 1], n, shift, identity_vals && p == 0, hist, totals,
+                        nblocks, s);
+        cur ^= 1;
+        shift += bits;
+    }
+    return cur;
+}
+
+// ---------------------------------------------------------------------
+// instance scan in depth order + emission
+// ---------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_scan_reduce(EmitArgs a) {
+    __shared__ uint32_t lds4[4];
+    uint32_t s = 0;
+    const uint32_t base = blockIdx.x * (uint32_t)kScanTile;
+#pragma unroll
+    for (int it = 0; it < kScanIPT; ++it) {
+        const uint32_t r = base + it * 256 + threadIdx.x;
+        if (r < (uint32_t)a.P) s += a.tiles_touched[a.order[r]];
+    }
+    uint32_t total;
+    block_exclusive_scan(s, lds4, total);
+    if (threadIdx.x == 0) a.scan_sums[blockIdx.x] = total;
+}
+
+__global__ __launch_bounds__(256) void k_scan_top(uint32_t* __restrict__ sums, int nb) {
+    __shared__ uint32_t lds4[4];
+    uint32_t carry = 0;
+    for (int c = 0; c < nb; c += 256) {
+        const int j = c + threadIdx.x;
+        const uint32_t v = j < nb ? sums[j] : 0u;
+        uint32_t total;
+        const uint32_t ex = block_exclusive_scan(v, lds4, total);
+        if (j < nb) sums[j] = carry + ex;
+        carry += total;
+    }
+    if (threadIdx.x == 0) sums[nb] = carry;
+}
+
+__global__ __launch_bounds__(256) void k_scan_emit(EmitArgs a) {
+    __shared__ uint32_t lds4[4];
+    const uint32_t r0 = blockIdx.x * (uint32_t)kScanTile + threadIdx.x * kScanIPT;
+    uint32_t g[kScanIPT], c[kScanIPT];
+    uint32_t s = 0;
+#pragma unroll
+    for (int i = 0; i < kScanIPT; ++i) {
+        const uint32_t r = r0 + i;
+        g[i] = r < (uint32_t)a.P ? a.order[r] : 0u;
+        c[i] = r < (uint32_t)a.P ? a.tiles_touched[g[i]] : 0u;
+        s += c[i];
+    }
+    uint32_t total;
+    uint32_t slot = a.scan_sums[blockIdx.x] + block_exclusive_scan(s, lds4, total);
+#pragma unroll 1
+    for (int i = 0; i < kScanIPT; ++i) {
+        if (c[i] == 0) continue;
+        const uint32_t gi = g[i];
+        a.first_slot[gi] = slot;
+        const float2 xy = a.means2D[gi];
+        const Rect q = tile_rect(xy.x, xy.y, a.radii[gi], a.gx, a.gy);
+        for (int y = q.y0; y < q.y1; ++y)
+            for (int x = q.x0; x < q.x1; ++x) {
+                a.tile_key[slot] = (uint32_t)(y * a.gx + x);
+                a.slot_gauss[slot] = gi;
+                ++slot;
+            }
+    }
+}
+
+void launch_scan_reduce(const EmitArgs& a, hipStream_t s) {
+    if (a.P <= 0) return;
+    hipLaunchKernelGGL(k_scan_reduce, dim3(a.scan_blocks), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(256), 0, s, a.scan_sums, a.scan_blocks);
+}
+
+void launch_scan_emit(const EmitArgs& a, hipStream_t s) {
+    if (a.P <= 0) return;
+    hipLaunchKernelGGL(k_scan_emit, dim3(a.scan_blocks), dim3(256), 0, s, a);
+}
+
+// ---------------------------------------------------------------------
+// identifyTileRanges (rasterizer_impl.cu:105-125) + instance maps
+// ---------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_ranges(const uint32_t* __restrict__ tile, const uint32_t* __restrict__ slot,
+                                                const uint32_t* __restrict__ slot_gauss, int K, uint2* __restrict__ ranges,
+                                                uint32_t* __restrict__ point_list, uint32_t* __restrict__ slot_to_pos) {
+    const int pos = blockIdx.x * 256 + threadIdx.x;
+    if (pos >= K) return;
+    const uint32_t t = tile[pos];
+    const uint32_t sl = slot[pos];
+    point_list[pos] = slot_gauss[sl];
+    slot_to_pos[sl] = (uint32_t)pos;
+    if (pos == 0) {
+        ranges[t].x = 0;
+    } else {
+        const uint32_t prev = tile[pos - 1];
+        if (prev != t) {
+            ranges[prev].y = (uint32_t)pos;
+            ranges[t].x = (uint32_t)pos;
+        }
+    }
+    if (pos == K - 1) ranges[t].y = (uint32_t)K;
+}
+
+void launch_ranges(const uint32_t* sorted_tile, const uint32_t* sorted_slot, const uint32_t* slot_gauss, int K,
+                   uint2* ranges, uint32_t* point_list, uint32_t* slot_to_pos, hipStream_t s) {
+    if (K <= 0) return;
+    hipLaunchKernelGGL(k_ranges, dim3(div_up(K, 256)), dim3(256), 0, s, sorted_tile, sorted_slot, slot_gauss, K, ranges,
+                       point_list, slot_to_pos);
+}
+
+}  // namespace gs

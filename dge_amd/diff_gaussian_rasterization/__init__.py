@@ -1,0 +1,141 @@
+"""Drop-in ``diff_gaussian_rasterization`` package backed by the gfx950 kernels.
+
+Same public names, argument order, return tuples and errors as the
+reference wrapper (gaussiansplatting/submodules/diff-gaussian-rasterization/
+diff_gaussian_rasterization/__init__.py:26-364), so
+``gaussiansplatting/gaussian_renderer/__init__.py`` imports it unchanged once
+this package is on the import path under that name.
+
+Differences that are deliberate:
+  * the native calls go through the C ABI (include/gs_raster.h) on the
+    caller's current HIP stream, not the legacy default stream;
+  * the backward needs no zero-filled gradient tensors (every element is
+    written) and is bitwise reproducible (no float atomics).
+"""
+from __future__ import annotations
+
+from typing import NamedTuple
+
+import torch
+import torch.nn as nn
+
+from .. import _C
+
+
+def cpu_deep_copy_tuple(input_tuple):
+    return tuple(item.cpu().clone() if isinstance(item, torch.Tensor) else item for item in input_tuple)
+
+
+def rasterize_gaussians(means3D, means2D, sh, colors_precomp, opacities, scales, rotations, cov3Ds_precomp,
+                        raster_settings):
+    return _RasterizeGaussians.apply(means3D, means2D, sh, colors_precomp, opacities, scales, rotations,
+                                     cov3Ds_precomp, raster_settings)
+
+
+def _call_with_snapshot(fn, args, debug, dump_name, what):
+    """Debug mode keeps a CPU copy of the arguments and dumps it on failure (reference __init__.py:88-107)."""
+    if not debug:
+        return fn(*args)
+    cpu_args = cpu_deep_copy_tuple(args)
+    try:
+        return fn(*args)
+    except Exception:
+        torch.save(cpu_args, dump_name)
+        print(f"\nAn error occured in {what}. Please forward {dump_name} for debugging.")
+        raise
+
+
+class _RasterizeGaussians(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, means3D, means2D, sh, colors_precomp, opacities, scales, rotations, cov3Ds_precomp,
+                raster_settings):
+        rs = raster_settings
+        args = (rs.bg, means3D, colors_precomp, opacities, scales, rotations, rs.scale_modifier, cov3Ds_precomp,
+                rs.viewmatrix, rs.projmatrix, rs.tanfovx, rs.tanfovy, rs.image_height, rs.image_width, sh,
+                rs.sh_degree, rs.campos, rs.prefiltered, rs.debug)
+        num_rendered, color, depth, radii, geomBuffer, binningBuffer, imgBuffer = _call_with_snapshot(
+            _C.rasterize_gaussians, args, rs.debug, "snapshot_fw.dump", "forward")
+        ctx.raster_settings = rs
+        ctx.num_rendered = num_rendered
+        ctx.save_for_backward(colors_precomp, means3D, scales, rotations, cov3Ds_precomp, radii, sh, geomBuffer,
+                              binningBuffer, imgBuffer)
+        return color, radii, depth
+
+    @staticmethod
+    def backward(ctx, grad_out_color, grad_radii, grad_depth):
+        # depth is forward-only, as in the reference (__init__.py:137, 155-177)
+        rs = ctx.raster_settings
+        (colors_precomp, means3D, scales, rotations, cov3Ds_precomp, radii, sh, geomBuffer, binningBuffer,
+         imgBuffer) = ctx.saved_tensors
+        args = (rs.bg, means3D, radii, colors_precomp, scales, rotations, rs.scale_modifier, cov3Ds_precomp,
+                rs.viewmatrix, rs.projmatrix, rs.tanfovx, rs.tanfovy, grad_out_color, sh, rs.sh_degree, rs.campos,
+                geomBuffer, ctx.num_rendered, binningBuffer, imgBuffer, rs.debug)
+        (grad_means2D, grad_colors_precomp, grad_opacities, grad_means3D, grad_cov3Ds_precomp, grad_sh, grad_scales,
+         grad_rotations) = _call_with_snapshot(_C.rasterize_gaussians_backward, args, rs.debug, "snapshot_bw.dump",
+                                               "backward")
+        return (grad_means3D, grad_means2D, grad_sh, grad_colors_precomp, grad_opacities, grad_scales, grad_rotations,
+                grad_cov3Ds_precomp, None)
+
+
+class GaussianRasterizationSettings(NamedTuple):
+    image_height: int
+    image_width: int
+    tanfovx: float
+    tanfovy: float
+    bg: torch.Tensor
+    scale_modifier: float
+    viewmatrix: torch.Tensor
+    projmatrix: torch.Tensor
+    sh_degree: int
+    campos: torch.Tensor
+    prefiltered: bool
+    debug: bool
+
+
+def _absent(like):
+    return torch.empty(0, dtype=torch.float32, device=like.device)
+
+
+class GaussianRasterizer(nn.Module):
+    def __init__(self, raster_settings):
+        super().__init__()
+        self.raster_settings = raster_settings
+
+    def markVisible(self, positions):
+        with torch.no_grad():
+            rs = self.raster_settings
+            return _C.mark_visible(positions, rs.viewmatrix, rs.projmatrix)
+
+    def forward(self, means3D, means2D, opacities, shs=None, colors_precomp=None, scales=None, rotations=None,
+                cov3D_precomp=None):
+        rs = self.raster_settings
+        if (shs is None) == (colors_precomp is None):
+            raise Exception("Please provide excatly one of either SHs or precomputed colors!")
+        if ((scales is None or rotations is None) and cov3D_precomp is None) or (
+                (scales is not None or rotations is not None) and cov3D_precomp is not None):
+            raise Exception("Please provide exactly one of either scale/rotation pair or precomputed 3D covariance!")
+        shs = _absent(means3D) if shs is None else shs
+        colors_precomp = _absent(means3D) if colors_precomp is None else colors_precomp
+        scales = _absent(means3D) if scales is None else scales
+        rotations = _absent(means3D) if rotations is None else rotations
+        cov3D_precomp = _absent(means3D) if cov3D_precomp is None else cov3D_precomp
+        return rasterize_gaussians(means3D, means2D, shs, colors_precomp, opacities, scales, rotations, cov3D_precomp,
+                                   rs)
+
+    def apply_weights(self, means3D, means2D, opacities, shs=None, weights=None, scales=None, rotations=None,
+                      cov3Ds_precomp=None, cnt=None, image_weights=None):
+        assert weights is not None
+        assert cnt is not None
+        assert image_weights is not None
+        rs = self.raster_settings
+        shs = _absent(means3D) if shs is None else shs
+        scales = _absent(means3D) if scales is None else scales
+        rotations = _absent(means3D) if rotations is None else rotations
+        cov3Ds_precomp = _absent(means3D) if cov3Ds_precomp is None else cov3Ds_precomp
+        args = (rs.bg, means3D, weights, opacities, scales, rotations, rs.scale_modifier, cov3Ds_precomp,
+                rs.viewmatrix, rs.projmatrix, rs.tanfovx, rs.tanfovy, rs.image_height, rs.image_width, shs,
+                rs.sh_degree, rs.campos, rs.prefiltered, image_weights, cnt, rs.debug)
+        _C.apply_weights(*args)
+
+
+__all__ = ["GaussianRasterizationSettings", "GaussianRasterizer", "rasterize_gaussians", "_RasterizeGaussians"]

@@ -1,0 +1,109 @@
+"""render() entry points with the reference's signatures and return dicts.
+
+Restates gaussiansplatting/gaussian_renderer/__init__.py:
+  camera2rasterizer  (:21-42)
+  render             (:45-150)   -> {"render","viewspace_points","visibility_filter","radii","depth_3dgs"}
+  point_cloud_render (:156-250)
+on top of ``dge_amd.diff_gaussian_rasterization``.  Two reference paths are
+broken in the reference and work here: the
+``compute_cov3D_python`` path (scales.float() on None, :137) and the
+``convert_SHs_python`` path (shs.float() on None, :124).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from .diff_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer
+from .sh_utils import eval_sh
+
+
+class PipelineParams:
+    """arguments/__init__.py:63-68 defaults."""
+
+    def __init__(self, convert_SHs_python=False, compute_cov3D_python=False, debug=False):
+        self.convert_SHs_python = convert_SHs_python
+        self.compute_cov3D_python = compute_cov3D_python
+        self.debug = debug
+
+
+def _settings(cam, bg_color, scaling_modifier, sh_degree, debug=False):
+    return GaussianRasterizationSettings(
+        image_height=int(cam.image_height), image_width=int(cam.image_width),
+        tanfovx=math.tan(cam.FoVx * 0.5), tanfovy=math.tan(cam.FoVy * 0.5), bg=bg_color,
+        scale_modifier=scaling_modifier, viewmatrix=cam.world_view_transform, projmatrix=cam.full_proj_transform,
+        sh_degree=sh_degree, campos=cam.camera_center, prefiltered=False, debug=debug)
+
+
+def camera2rasterizer(viewpoint_camera, bg_color: torch.Tensor, sh_degree: int = 0):
+    return GaussianRasterizer(raster_settings=_settings(viewpoint_camera, bg_color, 1.0, sh_degree))
+
+
+def render(viewpoint_camera, pc, pipe, bg_color: torch.Tensor, scaling_modifier=1.0, override_color=None):
+    xyz = pc.get_xyz
+    screenspace_points = torch.zeros_like(xyz, dtype=xyz.dtype, requires_grad=True, device=xyz.device) + 0
+    try:
+        screenspace_points.retain_grad()
+    except Exception:
+        pass
+    rasterizer = GaussianRasterizer(
+        raster_settings=_settings(viewpoint_camera, bg_color, scaling_modifier, pc.active_sh_degree,
+                                  getattr(pipe, "debug", False)))
+    means3D, means2D, opacity = xyz, screenspace_points, pc.get_opacity
+
+    scales = rotations = cov3D_precomp = None
+    if pipe.compute_cov3D_python:
+        cov3D_precomp = pc.get_covariance(scaling_modifier)
+    else:
+        scales, rotations = pc.get_scaling, pc.get_rotation
+
+    shs = colors_precomp = None
+    if override_color is None:
+        if pipe.convert_SHs_python:
+            feats = pc.get_features
+            shs_view = feats.transpose(1, 2).reshape(-1, 3, (pc.max_sh_degree + 1) ** 2)
+            dir_pp = xyz - viewpoint_camera.camera_center.repeat(feats.shape[0], 1)
+            dir_pp = dir_pp / dir_pp.norm(dim=1, keepdim=True)
+            colors_precomp = torch.clamp_min(eval_sh(pc.active_sh_degree, shs_view, dir_pp) + 0.5, 0.0)
+        else:
+            shs = pc.get_features.float()
+    else:
+        colors_precomp = override_color
+
+    rendered_image, radii, depth = rasterizer(
+        means3D=means3D.float(), means2D=means2D.float(), shs=shs, colors_precomp=colors_precomp,
+        opacities=opacity.float(), scales=None if scales is None else scales.float(),
+        rotations=None if rotations is None else rotations.float(), cov3D_precomp=cov3D_precomp)
+    return {
+        "render": rendered_image,
+        "viewspace_points": screenspace_points,
+        "visibility_filter": radii > 0,
+        "radii": radii,
+        "depth_3dgs": depth,
+    }
+
+
+def point_cloud_render(viewpoint_camera, xyz, pipe, bg_color: torch.Tensor, scaling_modifier=1.0,
+                       override_color=None):
+    screenspace_points = torch.zeros_like(xyz, dtype=xyz.dtype, requires_grad=True, device=xyz.device) + 0
+    try:
+        screenspace_points.retain_grad()
+    except Exception:
+        pass
+    rasterizer = GaussianRasterizer(raster_settings=_settings(viewpoint_camera, bg_color, scaling_modifier, 0))
+    opacity = torch.ones_like(xyz[..., 0:1])
+    scales = torch.ones_like(xyz) * 0.005
+    rotations = torch.zeros([xyz.shape[0], 4], dtype=xyz.dtype, device=xyz.device)
+    rotations[..., 0] = 1.0
+    colors_precomp = torch.ones_like(xyz[..., 0:1]).repeat(1, 3)
+    rendered_image, radii, depth = rasterizer(
+        means3D=xyz.float(), means2D=screenspace_points.float(), shs=None, colors_precomp=colors_precomp,
+        opacities=opacity.float(), scales=scales.float(), rotations=rotations.float(), cov3D_precomp=None)
+    return {
+        "render": rendered_image,
+        "viewspace_points": screenspace_points,
+        "visibility_filter": radii > 0,
+        "radii": radii,
+        "depth_3dgs": depth,
+    }

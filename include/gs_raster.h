@@ -1,0 +1,136 @@
+/*
+ * gs_raster.h — C ABI of the MI355X-native differentiable 3D Gaussian
+ * Splatting rasterizer (libgs_raster.so, HIP kernels for gfx950).
+ *
+ * This is the drop-in boundary that replaces the reference's native surface
+ * (paths relative to gaussiansplatting/submodules/diff-gaussian-rasterization/):
+ *
+ *   gs_rasterize_forward   <- _C.rasterize_gaussians            ext.cpp:16
+ *                             RasterizeGaussiansCUDA             rasterize_points.cu:35-95
+ *                             CudaRasterizer::Rasterizer::forward rasterizer.h:30-57,
+ *                                                                rasterizer_impl.cu:179-285
+ *   gs_rasterize_backward  <- _C.rasterize_gaussians_backward   ext.cpp:17
+ *                             RasterizeGaussiansBackwardCUDA     rasterize_points.cu:97-157
+ *                             Rasterizer::backward               rasterizer_impl.cu:289-341
+ *   gs_mark_visible        <- _C.mark_visible                   ext.cpp:18
+ *                             markVisible / checkFrustum         rasterize_points.cu:159-175,
+ *                                                                rasterizer_impl.cu:53-63,128-133
+ *   gs_apply_weights       <- _C.apply_weights                  ext.cpp:19
+ *                             applyWeightsGaussiansCUDA          rasterize_points.cu:177-234
+ *                             Rasterizer::apply_weights          rasterizer_impl.cu:343-447
+ *
+ * Conventions (identical to the reference's tensors, so a binding passes
+ * data_ptr()s straight through):
+ *   - every pointer is DEVICE memory unless noted; float32, contiguous;
+ *   - means3D [P,3]; shs [P,M,3]; colors_precomp [P,3]; opacities [P];
+ *     scales [P,3]; rotations [P,4] as (w,x,y,z); cov3D_precomp [P,6];
+ *   - viewmatrix/projmatrix: the reference's 4x4 tensors (row-major memory
+ *     holding the column-major transform, auxiliary.h:58-97);
+ *   - "absent" inputs are NULL (the reference's empty tensors);
+ *   - out_color [3,H,W]; out_depth [1,H,W]; radii [P] int32;
+ *   - geometry/binning/image buffers are opaque bytes owned by the caller,
+ *     obtained through the gs_alloc_fn callback exactly like the reference's
+ *     std::function<char*(size_t)> resize functors (rasterize_points.cu:27-33);
+ *     only their round trip from forward to backward is contractual;
+ *   - all work is enqueued on `stream` (a hipStream_t); the only host
+ *     synchronisation is the read-back of num_rendered, as in the reference
+ *     (rasterizer_impl.cu:236-239), whose value the API returns;
+ *   - return 0 on success, a GS_ERR_* code otherwise; gs_last_error() holds
+ *     the message.  No C++ exception crosses this boundary.
+ */
+#ifndef GS_RASTER_H
+#define GS_RASTER_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GS_RASTER_ABI_VERSION 1
+
+#define GS_OK 0
+#define GS_ERR_INVALID_ARG 1   /* AT_ERROR / std::runtime_error in the reference */
+#define GS_ERR_HIP 2           /* HIP runtime error (CHECK_CUDA, auxiliary.h:166-173) */
+#define GS_ERR_ALLOC 3         /* allocator callback returned NULL */
+#define GS_ERR_PREFILTERED 4   /* prefiltered set but a point was culled (auxiliary.h:156-160) */
+#define GS_ERR_UNSUPPORTED 5   /* e.g. apply_weights channel count (apply_weights.cu:377-380) */
+
+typedef void *gs_stream_t; /* hipStream_t */
+
+/* Allocation callback: returns a device pointer to at least nbytes (16-byte
+ * aligned), or NULL.  `which` is 0 = geometry, 1 = binning, 2 = image. */
+typedef void *(*gs_alloc_fn)(void *ctx, int which, size_t nbytes);
+
+/* GaussianRasterizationSettings (diff_gaussian_rasterization/__init__.py:228-240). */
+typedef struct gs_settings {
+    int image_height;
+    int image_width;
+    float tanfovx;
+    float tanfovy;
+    const float *bg;         /* device [3] */
+    float scale_modifier;
+    const float *viewmatrix; /* device [16] */
+    const float *projmatrix; /* device [16] */
+    int sh_degree;
+    const float *campos;     /* device [3] */
+    int prefiltered;
+    int debug;               /* synchronise + check after every launch */
+} gs_settings;
+
+/* Forward render.  Replaces Rasterizer::forward (rasterizer_impl.cu:179-285).
+ * M = SH coefficients per channel (shs.size(1)), 0 when shs is NULL. */
+int gs_rasterize_forward(const gs_settings *s, int P, int M, const float *means3D, const float *shs,
+                         const float *colors_precomp, const float *opacities, const float *scales,
+                         const float *rotations, const float *cov3D_precomp, float *out_color,
+                         float *out_depth, int *radii, gs_alloc_fn alloc, void *alloc_ctx,
+                         gs_stream_t stream, int *num_rendered);
+
+/* Backward.  Replaces Rasterizer::backward (rasterizer_impl.cu:289-341).
+ * R = num_rendered from the forward.  Every output is fully written (the
+ * caller need not zero it): dL_dmeans2D [P,3] (z = 0), dL_dcolors [P,3],
+ * dL_dopacity [P], dL_dmeans3D [P,3], dL_dcov3D [P,6], dL_dsh [P,M,3]
+ * (may be NULL when M == 0), dL_dscales [P,3], dL_drotations [P,4]. */
+int gs_rasterize_backward(const gs_settings *s, int P, int M, int R, const float *means3D,
+                          const float *shs, const float *colors_precomp, const float *scales,
+                          const float *rotations, const float *cov3D_precomp, const int *radii,
+                          const void *geom_buffer, const void *binning_buffer, const void *img_buffer,
+                          const float *dL_dpix, float *dL_dmeans2D, float *dL_dcolors,
+                          float *dL_dopacity, float *dL_dmeans3D, float *dL_dcov3D, float *dL_dsh,
+                          float *dL_dscales, float *dL_drotations, gs_stream_t stream);
+
+/* present[i] = (view * means3D[i]).z > 0.2 (rasterizer_impl.cu:53-63). */
+int gs_mark_visible(int P, const float *means3D, const float *viewmatrix, const float *projmatrix,
+                    uint8_t *present, gs_stream_t stream);
+
+/* Back-projection of image weights onto Gaussians (apply_weights.cu:148-356).
+ * weights [P,C] (also the colors_precomp input, as in the reference) and
+ * cnt [P] int32 are accumulated in place; C = num_channels in {1,2,3}. */
+int gs_apply_weights(const gs_settings *s, int P, int M, const float *means3D, float *weights,
+                     int num_channels, const float *opacities, const float *scales,
+                     const float *rotations, const float *cov3D_precomp, const float *shs,
+                     const float *image_weights, int *cnt, gs_alloc_fn alloc, void *alloc_ctx,
+                     gs_stream_t stream);
+
+/* Byte sizes of the opaque buffers (host arithmetic, no device work). */
+size_t gs_geometry_buffer_size(int P);
+size_t gs_image_buffer_size(int width, int height);
+size_t gs_binning_buffer_size(int num_rendered, int num_tiles);
+
+/* Offsets (bytes) of the per-Gaussian arrays inside the geometry buffer, for
+ * field-by-field parity tests.  Names: "means2D" (float2), "conic_opacity"
+ * (float4), "rgbd" (float4 = r,g,b,depth), "tiles_touched" (u32),
+ * "clamped" (u8, bit c = channel c clamped), "radii" (int32).
+ * Image buffer: "final_T" (float), "n_contrib" (u32), "ranges" (uint2 per tile).
+ * Binning buffer: "point_list" (u32 per instance).  Returns -1 if unknown. */
+long long gs_buffer_offset(const char *buffer, const char *field, int P, int width, int height,
+                           int num_rendered);
+
+const char *gs_last_error(void);
+int gs_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GS_RASTER_H */

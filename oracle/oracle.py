@@ -1,0 +1,302 @@
+"""ctypes front-end of the CPU oracle (oracle/gs_oracle.c).
+
+TEST INFRASTRUCTURE ONLY.  The product package ``dge_amd`` never imports this
+module; only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s
+``cpu_baseline`` leg do, as the checker / CPU baseline.
+
+The oracle restates the reference rasterizer
+(gaussiansplatting/submodules/diff-gaussian-rasterization/cuda_rasterizer/
+forward.cu, backward.cu, rasterizer_impl.cu, apply_weights.cu) on the host.
+Inputs use the reference layouts: means3D [P,3], shs [P,M,3], rotations [P,4]
+(w,x,y,z), matrices as the reference's [4,4] tensors whose row-major memory is
+the column-major transform (auxiliary.h:58-97), colors [3,H,W].
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+from dataclasses import dataclass, field
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "liboracle.so")
+_lib = None
+
+_f32p = ctypes.POINTER(ctypes.c_float)
+_i32p = ctypes.POINTER(ctypes.c_int)
+_u8p = ctypes.POINTER(ctypes.c_uint8)
+
+
+class _Settings(ctypes.Structure):
+    _fields_ = [
+        ("image_width", ctypes.c_int),
+        ("image_height", ctypes.c_int),
+        ("tanfovx", ctypes.c_float),
+        ("tanfovy", ctypes.c_float),
+        ("bg", ctypes.c_float * 3),
+        ("scale_modifier", ctypes.c_float),
+        ("viewmatrix", ctypes.c_float * 16),
+        ("projmatrix", ctypes.c_float * 16),
+        ("sh_degree", ctypes.c_int),
+        ("campos", ctypes.c_float * 3),
+        ("prefiltered", ctypes.c_int),
+    ]
+
+
+class _Inputs(ctypes.Structure):
+    _fields_ = [
+        ("P", ctypes.c_int),
+        ("M", ctypes.c_int),
+        ("means3D", _f32p),
+        ("shs", _f32p),
+        ("colors_precomp", _f32p),
+        ("opacities", _f32p),
+        ("scales", _f32p),
+        ("rotations", _f32p),
+        ("cov3D_precomp", _f32p),
+    ]
+
+
+def build(force: bool = False) -> str:
+    """Compile liboracle.so with the committed Makefile (gcc, OpenMP)."""
+    src = os.path.join(_HERE, "gs_oracle.c")
+    if force or not os.path.exists(_LIB_PATH) or os.path.getmtime(_LIB_PATH) < os.path.getmtime(src):
+        subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return _LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        L = ctypes.CDLL(_LIB_PATH)
+        L.go_forward.restype = ctypes.c_void_p
+        L.go_forward.argtypes = [ctypes.POINTER(_Settings), ctypes.POINTER(_Inputs), _f32p, _f32p, _i32p, _i32p, _i32p]
+        L.go_backward.restype = ctypes.c_int
+        L.go_backward.argtypes = [ctypes.c_void_p, ctypes.POINTER(_Settings), ctypes.POINTER(_Inputs), _f32p] + [_f32p] * 9
+        L.go_state_get.restype = ctypes.c_long
+        L.go_state_get.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_void_p)]
+        L.go_free.argtypes = [ctypes.c_void_p]
+        L.go_mark_visible.argtypes = [ctypes.c_int, _f32p, _f32p, _f32p, _u8p]
+        L.go_apply_weights.restype = ctypes.c_int
+        L.go_apply_weights.argtypes = [ctypes.POINTER(_Settings), ctypes.POINTER(_Inputs), ctypes.c_int, _f32p, _f32p, _i32p]
+        L.go_set_threads.argtypes = [ctypes.c_int]
+        _lib = L
+    return _lib
+
+
+def set_threads(n: int) -> None:
+    lib().go_set_threads(int(n))
+
+
+def _np(x, dtype=np.float32):
+    if x is None:
+        return None
+    if hasattr(x, "detach"):
+        x = x.detach().cpu().numpy()
+    return np.ascontiguousarray(np.asarray(x, dtype=dtype))
+
+
+def _ptr(a, typ=_f32p):
+    return None if a is None or a.size == 0 else a.ctypes.data_as(typ)
+
+
+@dataclass
+class RasterSettings:
+    """Host copy of GaussianRasterizationSettings (diff_gaussian_rasterization/__init__.py:228-240)."""
+
+    image_height: int
+    image_width: int
+    tanfovx: float
+    tanfovy: float
+    bg: np.ndarray
+    scale_modifier: float
+    viewmatrix: np.ndarray
+    projmatrix: np.ndarray
+    sh_degree: int
+    campos: np.ndarray
+    prefiltered: bool = False
+
+    @classmethod
+    def from_any(cls, s) -> "RasterSettings":
+        return cls(
+            image_height=int(s.image_height),
+            image_width=int(s.image_width),
+            tanfovx=float(s.tanfovx),
+            tanfovy=float(s.tanfovy),
+            bg=_np(s.bg).reshape(3),
+            scale_modifier=float(s.scale_modifier),
+            viewmatrix=_np(s.viewmatrix).reshape(16),
+            projmatrix=_np(s.projmatrix).reshape(16),
+            sh_degree=int(s.sh_degree),
+            campos=_np(s.campos).reshape(3),
+            prefiltered=bool(getattr(s, "prefiltered", False)),
+        )
+
+    def c(self) -> _Settings:
+        c = _Settings()
+        c.image_width = self.image_width
+        c.image_height = self.image_height
+        c.tanfovx = self.tanfovx
+        c.tanfovy = self.tanfovy
+        c.bg[:] = [float(v) for v in self.bg]
+        c.scale_modifier = self.scale_modifier
+        c.viewmatrix[:] = [float(v) for v in self.viewmatrix]
+        c.projmatrix[:] = [float(v) for v in self.projmatrix]
+        c.sh_degree = self.sh_degree
+        c.campos[:] = [float(v) for v in self.campos]
+        c.prefiltered = int(self.prefiltered)
+        return c
+
+
+@dataclass
+class Inputs:
+    means3D: np.ndarray
+    opacities: np.ndarray
+    shs: np.ndarray | None = None
+    colors_precomp: np.ndarray | None = None
+    scales: np.ndarray | None = None
+    rotations: np.ndarray | None = None
+    cov3D_precomp: np.ndarray | None = None
+    _keep: list = field(default_factory=list)
+
+    @classmethod
+    def make(cls, means3D, opacities, shs=None, colors_precomp=None, scales=None, rotations=None, cov3D_precomp=None):
+        def nz(x):
+            a = _np(x)
+            return None if a is None or a.size == 0 else a
+
+        return cls(_np(means3D).reshape(-1, 3), _np(opacities).reshape(-1), nz(shs), nz(colors_precomp), nz(scales),
+                   nz(rotations), nz(cov3D_precomp))
+
+    @property
+    def P(self) -> int:
+        return int(self.means3D.shape[0])
+
+    @property
+    def M(self) -> int:
+        return 0 if self.shs is None else int(self.shs.shape[1])
+
+    def c(self) -> _Inputs:
+        c = _Inputs()
+        c.P = self.P
+        c.M = self.M
+        c.means3D = _ptr(self.means3D)
+        c.shs = _ptr(self.shs)
+        c.colors_precomp = _ptr(self.colors_precomp)
+        c.opacities = _ptr(self.opacities)
+        c.scales = _ptr(self.scales)
+        c.rotations = _ptr(self.rotations)
+        c.cov3D_precomp = _ptr(self.cov3D_precomp)
+        return c
+
+
+_STATE_DTYPES = {
+    "depths": np.float32, "clamped": np.uint8, "radii": np.int32, "means2D": np.float32, "cov3D": np.float32,
+    "conic_opacity": np.float32, "rgb": np.float32, "tiles_touched": np.uint32, "point_offsets": np.uint32,
+    "point_keys": np.uint64, "point_list": np.uint32, "ranges": np.uint32, "final_T": np.float32,
+    "n_contrib": np.uint32,
+}
+
+
+class State:
+    """Owns the oracle's forward intermediates (GeometryState/BinningState/ImageState analogue)."""
+
+    def __init__(self, handle, settings: RasterSettings, inputs: Inputs, num_rendered: int):
+        self.handle = handle
+        self.settings = settings
+        self.inputs = inputs
+        self.num_rendered = num_rendered
+
+    def get(self, name: str) -> np.ndarray:
+        p = ctypes.c_void_p()
+        n = lib().go_state_get(self.handle, name.encode(), ctypes.byref(p))
+        if n < 0:
+            raise KeyError(name)
+        dt = np.dtype(_STATE_DTYPES[name])
+        if n == 0 or not p.value:
+            return np.zeros(0, dt)
+        buf = (ctypes.c_char * (n * dt.itemsize)).from_address(p.value)
+        return np.frombuffer(buf, dtype=dt, count=n).copy()
+
+    def __del__(self):
+        try:
+            if getattr(self, "handle", None) and _lib is not None:
+                _lib.go_free(self.handle)
+        except Exception:  # interpreter shutdown
+            pass
+        self.handle = None
+
+
+def forward(settings, means3D, opacities, shs=None, colors_precomp=None, scales=None, rotations=None,
+            cov3D_precomp=None):
+    """rasterize_points.cu:35-95 semantics -> (num_rendered, color[3,H,W], depth[1,H,W], radii[P], state)."""
+    s = settings if isinstance(settings, RasterSettings) else RasterSettings.from_any(settings)
+    inp = Inputs.make(means3D, opacities, shs, colors_precomp, scales, rotations, cov3D_precomp)
+    H, W, P = s.image_height, s.image_width, inp.P
+    color = np.zeros((3, H, W), np.float32)
+    depth = np.zeros((1, H, W), np.float32)
+    radii = np.zeros(P, np.int32)
+    nr = ctypes.c_int(0)
+    err = ctypes.c_int(0)
+    cs, ci = s.c(), inp.c()
+    h = lib().go_forward(ctypes.byref(cs), ctypes.byref(ci), _ptr(color), _ptr(depth), _ptr(radii, _i32p),
+                         ctypes.byref(nr), ctypes.byref(err))
+    if err.value != 0 or not h:
+        raise RuntimeError(f"oracle forward failed with code {err.value}")
+    return nr.value, color, depth, radii, State(h, s, inp, nr.value)
+
+
+def backward(state: State, dL_dpix):
+    """rasterize_points.cu:97-157 semantics -> dict of the 8 reference grads (+ dL_dconic)."""
+    s, inp = state.settings, state.inputs
+    P, M = inp.P, inp.M
+    g = _np(dL_dpix).reshape(3, s.image_height, s.image_width)
+    out = {
+        "dL_dmeans2D": np.zeros((P, 3), np.float32),
+        "dL_dcolors": np.zeros((P, 3), np.float32),
+        "dL_dopacity": np.zeros((P, 1), np.float32),
+        "dL_dmeans3D": np.zeros((P, 3), np.float32),
+        "dL_dcov3D": np.zeros((P, 6), np.float32),
+        "dL_dsh": np.zeros((P, M, 3), np.float32),
+        "dL_dscales": np.zeros((P, 3), np.float32),
+        "dL_drotations": np.zeros((P, 4), np.float32),
+        "dL_dconic": np.zeros((P, 2, 2), np.float32),
+    }
+    cs, ci = s.c(), inp.c()
+    rc = lib().go_backward(state.handle, ctypes.byref(cs), ctypes.byref(ci), _ptr(g), *[
+        _ptr(out[k]) if out[k].size else None for k in
+        ("dL_dmeans2D", "dL_dcolors", "dL_dopacity", "dL_dmeans3D", "dL_dcov3D", "dL_dsh", "dL_dscales",
+         "dL_drotations", "dL_dconic")])
+    if rc != 0:
+        raise RuntimeError(f"oracle backward failed with code {rc}")
+    return out
+
+
+def mark_visible(means3D, viewmatrix, projmatrix):
+    m = _np(means3D).reshape(-1, 3)
+    v = _np(viewmatrix).reshape(16)
+    p = _np(projmatrix).reshape(16)
+    out = np.zeros(m.shape[0], np.uint8)
+    lib().go_mark_visible(m.shape[0], _ptr(m), _ptr(v), _ptr(p), _ptr(out, _u8p))
+    return out.astype(bool)
+
+
+def apply_weights(settings, means3D, opacities, weights, cnt, image_weights, scales=None, rotations=None,
+                  cov3D_precomp=None, shs=None):
+    """GaussianRasterizer.apply_weights semantics; returns updated (weights, cnt) copies."""
+    s = settings if isinstance(settings, RasterSettings) else RasterSettings.from_any(settings)
+    w = _np(weights).copy()
+    C = int(_np(image_weights).shape[0])
+    w2 = w.reshape(w.shape[0], -1)
+    c = _np(cnt, np.int32).reshape(-1).copy()
+    iw = _np(image_weights)
+    inp = Inputs.make(means3D, opacities, shs, None, scales, rotations, cov3D_precomp)
+    cs, ci = s.c(), inp.c()
+    rc = lib().go_apply_weights(ctypes.byref(cs), ctypes.byref(ci), C, _ptr(iw), _ptr(w2), _ptr(c, _i32p))
+    if rc != 0:
+        raise RuntimeError(f"oracle apply_weights failed with code {rc}")
+    return w2.reshape(w.shape), c.reshape(np.shape(_np(cnt, np.int32)))
