@@ -1,0 +1,240 @@
+#!/usr/bin/env python
+"""bench.py — forward+backward renders/s of the DGE 3DGS rasterizer hot path.
+
+Workload (BASELINE.json configs[1], "c2"): 1.0M Gaussians (SH degree 3),
+512x512, fp32, one render() forward + its backward per view, seeded synthetic
+scene and orbit cameras of SURVEY.md §8(d) (no network: data = synthetic).
+A step = every rank renders its `--views-per-rank` views (forward + backward
+through autograd, gradients accumulated into the shared parameters) and, for
+N > 1, ONE all-reduce of the flat parameter-gradient bucket (RCCL); per-GPU
+work is fixed, so scaling is weak and value = all views rendered / max-rank time.
+
+Prints ONE JSON line (rank 0) with the contract keys plus `roofline` (the
+dominant kernel, timed live with HIP events on its stream through the C ABI's
+stage profiler) and `cpu_baseline` (the oracle, a CPU restatement of the
+reference, timed on this host's cores on a bounded sample).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+
+METRIC = "forward+backward renders/sec @512×512, 1.0M Gaussians; achieved HBM GB/s"
+HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--points", type=int, default=1_000_000)
+    ap.add_argument("--width", type=int, default=512)
+    ap.add_argument("--height", type=int, default=512)
+    ap.add_argument("--sh-degree", type=int, default=3)
+    ap.add_argument("--views-per-rank", type=int, default=3)
+    ap.add_argument("--cpu-baseline-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-profile", action="store_true")
+    return ap.parse_args()
+
+
+def stage_bytes(stage, P, M, K, Kb, HW, tiles):
+    """Algorithmic bytes per launch of each stage."""
+    if stage == "preprocess":  # read xyz, scale, rot, opacity, SH; write the geometry record
+        return P * (12 + 12 + 16 + 4 + 12 * M) + P * (8 + 16 + 16 + 4 + 1 + 4 + 4 + 4 + 4)
+    if stage == "render_fwd":  # per instance: id + xy + conic/opacity + rgb/depth; per pixel: color, depth, T, n
+        return K * (4 + 8 + 16 + 16) + HW * 24 + tiles * 8
+    if stage == "render_bwd":  # per instance in the backward window: gather 44 B + 48-B record; per pixel 20 B
+        return Kb * (4 + 8 + 16 + 16 + 48) + HW * 20 + tiles * 12
+    if stage == "gauss_bwd":  # params + geometry + records in, 9 gradient tensors out
+        return P * (12 + 12 + 16 + 12 * M + 4 + 4 + 4 + 8 + 1) + Kb * (48 + 4) + P * 4 * (3 + 3 + 1 + 3 + 6 + 3 + 4) + P * 12 * M
+    return None
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"[bench] note: WORLD_SIZE={world} but --gpus={args.gpus}; using WORLD_SIZE", file=sys.stderr)
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from dge_amd import _native, _C
+    from dge_amd.cameras import orbit_camera
+    from dge_amd.gaussian_renderer import PipelineParams, render
+    from dge_amd.multiview import GradBucket
+    from dge_amd.scene import synthetic_scene
+
+    P, W, H, V = args.points, args.width, args.height, args.views_per_rank
+    scene = synthetic_scene(P, sh_degree=args.sh_degree, seed=0, device=dev).requires_grad_(True)
+    n_total = V * world
+    cams = [orbit_camera(k, n_total, W, H, device=dev) for k in range(rank * V, (rank + 1) * V)]
+    gen = torch.Generator(device="cpu").manual_seed(1)
+    seeds = [(torch.randn(3, H, W, generator=gen) * 1e-3).to(dev) for _ in range(V)]
+    bg = torch.zeros(3, device=dev)
+    pipe = PipelineParams()
+    bucket = GradBucket(scene.parameters())
+
+    def step():
+        bucket.zero()
+        for cam, g in zip(cams, seeds):
+            out = render(cam, scene, pipe, bg)["render"]
+            out.backward(g)
+        if world > 1:
+            bucket.allreduce()
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+
+    # instance counts of this rank's views (deterministic; outside the timed region)
+    Ks, Kbs = [], []
+    with torch.no_grad():
+        for cam in cams:
+            from dge_amd.gaussian_renderer import _settings
+            s = _settings(cam, bg, 1.0, scene.active_sh_degree)
+            K, color, depth, radii, geom, binning, img = _C.rasterize_gaussians(
+                s.bg, scene.get_xyz, torch.empty(0, device=dev), scene.get_opacity, scene.get_scaling,
+                scene.get_rotation, 1.0, torch.empty(0, device=dev), s.viewmatrix, s.projmatrix, s.tanfovx, s.tanfovy,
+                H, W, scene.get_features, scene.active_sh_degree, s.campos, False, False)
+            off = _native.lib().gs_buffer_offset(b"image", b"tile_last", P, W, H, K)
+            tiles = ((W + 15) // 16) * ((H + 15) // 16)
+            tl = img[off:off + 4 * tiles].view(torch.int32)
+            Ks.append(int(K))
+            Kbs.append(int(tl.sum().item()))
+    torch.cuda.synchronize()
+
+    if not args.no_profile:
+        _native.profile_enable(True)
+        _native.profile_collect()  # reset
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    prof = {}
+    if not args.no_profile:
+        prof = _native.profile_collect()
+        _native.profile_enable(False)
+    if world > 1:
+        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+
+    renders = args.steps * V * world
+    value = renders / dt
+    ms_per_step = 1000.0 * dt / args.steps
+
+    HW = W * H
+    tiles = ((W + 15) // 16) * ((H + 15) // 16)
+    M = (args.sh_degree + 1) ** 2
+    K = float(np.mean(Ks))
+    Kb = float(np.mean(Kbs))
+    # whole-render algorithmic bytes, SURVEY.md §8(d): B = 828 P + 200 K + 44 HW
+    B_render = 828.0 * P + 200.0 * K + 44.0 * HW
+    roofline = None
+    stages = {}
+    if prof:
+        for name, (ms, cnt) in prof.items():
+            if cnt:
+                stages[name] = {"avg_ms": ms / cnt, "launches": cnt,
+                                "share": ms / max(1e-9, sum(v[0] for v in prof.values()))}
+        dom = max(stages, key=lambda n: stages[n]["avg_ms"] * stages[n]["launches"])
+        b = stage_bytes(dom, P, M, K, Kb, HW, tiles)
+        if b is not None:
+            achieved = b / (stages[dom]["avg_ms"] * 1e-3) / 1e9
+            roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                        "frac": round(achieved / HBM_PEAK_GBPS, 5), "traffic": None, "kernel": dom,
+                        "algorithmic_bytes_per_launch": int(b), "avg_ms": round(stages[dom]["avg_ms"], 4)}
+            pmc = os.path.join(HERE, "profiles", "pmc_traffic.json")
+            if os.path.exists(pmc):
+                try:
+                    tr = json.load(open(pmc)).get(dom)
+                    if tr:
+                        roofline["traffic"] = tr.get("bytes_per_launch")
+                except Exception:
+                    pass
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(scene, cams[0], seeds[0], bg, args)
+
+    if rank == 0:
+        line = {
+            "metric": METRIC,
+            "value": round(value, 3),
+            "unit": "renders/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "fp32",
+            "data": "synthetic",
+            "config": {"workload": f"c2: {P / 1e6:.2f}M Gaussians (SH deg {args.sh_degree}), {W}x{H}, fp32 fwd+bwd",
+                       "gaussians": P, "width": W, "height": H, "views_per_rank": V,
+                       "parallelism": f"views sharded x{world}" + (", RCCL grad all-reduce" if world > 1 else "")},
+            "num_rendered_mean": int(K),
+            "backward_window_instances_mean": int(Kb),
+            "hbm_gbps_algorithmic_whole_render": round(B_render * value / world / 1e9, 2),
+            "stages_ms": {k: round(v["avg_ms"], 4) for k, v in stages.items()},
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(scene, cam, seed, bg, args):
+    """The oracle (CPU restatement of the reference) on the same scene/view, bounded to ~N seconds."""
+    try:
+        from oracle import oracle as O
+    except Exception as e:  # pragma: no cover
+        return {"error": f"oracle unavailable: {e}"}
+    threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+    O.set_threads(threads)
+    from dge_amd.gaussian_renderer import _settings
+    s = _settings(cam, bg, 1.0, scene.active_sh_degree)
+    with torch.no_grad():
+        xyz, op, sh = scene.get_xyz.cpu().numpy(), scene.get_opacity.cpu().numpy(), scene.get_features.cpu().numpy()
+        scl, rot = scene.get_scaling.cpu().numpy(), scene.get_rotation.cpu().numpy()
+    g = seed.cpu().numpy()
+    n, t0 = 0, time.perf_counter()
+    while True:
+        _, _, _, _, st = O.forward(s, xyz, op, shs=sh, scales=scl, rotations=rot)
+        O.backward(st, g)
+        del st
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= args.cpu_baseline_seconds or n >= 50:
+            break
+    return {"value": round(n / el, 4), "unit": "renders/s", "cores": threads, "kind": "port",
+            "sample": f"{n} fwd+bwd render(s) of the c2 scene, view 0, oracle/gs_oracle.c with {threads} OpenMP threads"}
+
+
+if __name__ == "__main__":
+    main()

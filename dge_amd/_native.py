@@ -59,6 +59,10 @@ SIGNATURES = {
     "gs_binning_buffer_size": (ctypes.c_size_t, [ctypes.c_int, ctypes.c_int]),
     "gs_buffer_offset": (ctypes.c_longlong, [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_int,
                                              ctypes.c_int, ctypes.c_int]),
+    "gs_profile_enable": (ctypes.c_int, [ctypes.c_int]),
+    "gs_profile_num_stages": (ctypes.c_int, []),
+    "gs_profile_stage_name": (ctypes.c_char_p, [ctypes.c_int]),
+    "gs_profile_collect": (ctypes.c_int, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int), ctypes.c_int]),
     "gs_last_error": (ctypes.c_char_p, []),
     "gs_abi_version": (ctypes.c_int, []),
 }
@@ -113,3 +117,17 @@ def require_gpu(t) -> None:
         raise NativeError("dge_amd requires a ROCm GPU (torch.cuda.is_available() is False); no CPU fallback exists")
     if not getattr(t, "is_cuda", False):
         raise NativeError("dge_amd: tensors must live on the GPU")
+
+
+def profile_enable(on: bool = True) -> None:
+    lib().gs_profile_enable(int(on))
+
+
+def profile_collect() -> dict:
+    """{stage: (total_ms, launches)} since the last collect (see gs_profile_collect)."""
+    L = lib()
+    n = L.gs_profile_num_stages()
+    ms = (ctypes.c_double * n)()
+    cnt = (ctypes.c_int * n)()
+    check(L.gs_profile_collect(ms, cnt, n), "gs_profile_collect")
+    return {L.gs_profile_stage_name(i).decode(): (ms[i], cnt[i]) for i in range(n)}

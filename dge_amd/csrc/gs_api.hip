@@ -20,9 +20,11 @@
 #include <string.h>
 
 #include <limits>
+#include <atomic>
 #include <mutex>
 #include <string>
 #include <unordered_map>
+#include <vector>
 
 #include "gs_common.h"
 #include "gs_internal.h"
@@ -80,6 +82,65 @@ int staging_for_device(Staging** out) {
     *out = &s;
     return GS_OK;
 }
+
+// ---------------------------------------------------------------------
+// stage profiler: HIP events recorded on the launch stream around each stage
+// (gs_profile_enable / gs_profile_collect); off by default.
+// ---------------------------------------------------------------------
+enum Stage {
+    ST_PREPROCESS = 0, ST_DEPTH_SORT, ST_SCAN, ST_EMIT, ST_TILE_SORT, ST_RANGES, ST_RENDER_FWD,
+    ST_RENDER_BWD, ST_GAUSS_BWD, ST_APPLY_WEIGHTS, ST_COUNT
+};
+const char* kStageNames[ST_COUNT] = {"preprocess", "depth_sort", "scan", "emit", "tile_sort", "ranges",
+                                     "render_fwd", "render_bwd", "gauss_bwd", "apply_weights"};
+struct ProfRecord {
+    int stage;
+    hipEvent_t a, b;
+};
+// Process-wide: torch's autograd runs the backward on its own device thread.
+struct Profiler {
+    std::atomic<bool> on{false};
+    std::mutex mu;
+    std::vector<ProfRecord> recs;
+    std::vector<hipEvent_t> pool;
+    hipEvent_t get() {
+        {
+            std::lock_guard<std::mutex> g(mu);
+            if (!pool.empty()) {
+                hipEvent_t e = pool.back();
+                pool.pop_back();
+                return e;
+            }
+        }
+        hipEvent_t e = nullptr;
+        if (hipEventCreate(&e) != hipSuccess) return nullptr;
+        return e;
+    }
+    void add(int stage, hipEvent_t a, hipEvent_t b) {
+        std::lock_guard<std::mutex> g(mu);
+        recs.push_back({stage, a, b});
+    }
+};
+Profiler& profiler() {
+    static Profiler p;
+    return p;
+}
+struct StageScope {
+    Profiler& p;
+    int stage;
+    hipStream_t s;
+    hipEvent_t a = nullptr;
+    StageScope(int st, hipStream_t stream) : p(profiler()), stage(st), s(stream) {
+        if (p.on.load(std::memory_order_relaxed) && (a = p.get())) (void)hipEventRecord(a, s);
+    }
+    ~StageScope() {
+        if (!a) return;
+        hipEvent_t b = p.get();
+        if (!b) return;
+        (void)hipEventRecord(b, s);
+        p.add(stage, a, b);
+    }
+};
 
 template <typename T>
 T* at(void* base, size_t off) {
@@ -170,7 +231,7 @@ int bin_forward(const gs_settings* s, const Grid& g, int P, int M, const float* 
     pa.depth_key = at<uint32_t>(geom, gl.key0);
     pa.depth_val = at<uint32_t>(geom, gl.val0);
     pa.counters = counters;
-    launch_preprocess(pa, stream);
+    { StageScope sc(ST_PREPROCESS, stream); launch_preprocess(pa, stream); }
     GS_LAUNCHED("preprocess");
 
     Staging* st = nullptr;
@@ -180,10 +241,12 @@ int bin_forward(const gs_settings* s, const Grid& g, int P, int M, const float* 
     GS_HIP(hipEventRecord(st->ev, stream));
 
     // depth order of the Gaussians (stable: ties keep index order)
-    const int cur = radix_sort_pairs(at<uint32_t>(geom, gl.key0), at<uint32_t>(geom, gl.key1),
+    int cur;
+    { StageScope sc(ST_DEPTH_SORT, stream);
+    cur = radix_sort_pairs(at<uint32_t>(geom, gl.key0), at<uint32_t>(geom, gl.key1),
                                      at<uint32_t>(geom, gl.val0), at<uint32_t>(geom, gl.val1), (uint32_t)P, 0, 32, 8,
                                      false, at<uint32_t>(geom, gl.sort_hist), at<uint32_t>(geom, gl.sort_totals),
-                                     gl.sort_blocks, stream);
+                                     gl.sort_blocks, stream); }
     GS_LAUNCHED("depth sort");
 
     EmitArgs ea;
@@ -195,7 +258,7 @@ int bin_forward(const gs_settings* s, const Grid& g, int P, int M, const float* 
     ea.scan_sums = at<uint32_t>(geom, gl.scan_sums);
     ea.first_slot = at<uint32_t>(geom, gl.first_slot);
     ea.scan_blocks = gl.scan_blocks;
-    launch_scan_reduce(ea, stream);
+    { StageScope sc(ST_SCAN, stream); launch_scan_reduce(ea, stream); }
     GS_LAUNCHED("instance scan");
 
     GS_HIP(hipEventSynchronize(st->ev));
@@ -212,18 +275,21 @@ int bin_forward(const gs_settings* s, const Grid& g, int P, int M, const float* 
 
     ea.tile_key = at<uint32_t>(bin, bl.key0);
     ea.slot_gauss = at<uint32_t>(bin, bl.slot_gauss);
-    launch_scan_emit(ea, stream);
+    { StageScope sc(ST_EMIT, stream); launch_scan_emit(ea, stream); }
     GS_LAUNCHED("emit");
 
     const TileSortPlan plan = tile_sort_plan(g.tiles);
-    const int tc = radix_sort_pairs(at<uint32_t>(bin, bl.key0), at<uint32_t>(bin, bl.key1), at<uint32_t>(bin, bl.val0),
+    int tc;
+    { StageScope sc(ST_TILE_SORT, stream);
+    tc = radix_sort_pairs(at<uint32_t>(bin, bl.key0), at<uint32_t>(bin, bl.key1), at<uint32_t>(bin, bl.val0),
                                     at<uint32_t>(bin, bl.val1), K, 0, plan.bits, kMaxSinglePassBits, true,
                                     at<uint32_t>(bin, bl.sort_hist), at<uint32_t>(bin, bl.sort_totals), bl.sort_blocks,
-                                    stream);
+                                    stream); }
     GS_LAUNCHED("tile sort");
+    { StageScope sc(ST_RANGES, stream);
     launch_ranges(at<uint32_t>(bin, tc ? bl.key1 : bl.key0), at<uint32_t>(bin, tc ? bl.val1 : bl.val0),
                   at<uint32_t>(bin, bl.slot_gauss), (int)K, at<uint2>(img, il.ranges), at<uint32_t>(bin, bl.point_list),
-                  at<uint32_t>(bin, bl.slot_to_pos), stream);
+                  at<uint32_t>(bin, bl.slot_to_pos), stream); }
     GS_LAUNCHED("ranges");
     return GS_OK;
 }
@@ -233,6 +299,34 @@ int bin_forward(const gs_settings* s, const Grid& g, int P, int M, const float* 
 extern "C" {
 
 const char* gs_last_error(void) { return g_last_error.c_str(); }
+
+int gs_profile_enable(int on) {
+    profiler().on.store(on != 0);
+    return GS_OK;
+}
+
+int gs_profile_num_stages(void) { return ST_COUNT; }
+const char* gs_profile_stage_name(int i) { return (i >= 0 && i < ST_COUNT) ? kStageNames[i] : ""; }
+
+int gs_profile_collect(double* total_ms, int* counts, int n) {
+    Profiler& p = profiler();
+    for (int i = 0; i < n; ++i) { total_ms[i] = 0.0; counts[i] = 0; }
+    std::vector<ProfRecord> recs;
+    {
+        std::lock_guard<std::mutex> g(p.mu);
+        recs.swap(p.recs);
+    }
+    for (const ProfRecord& r : recs) {
+        GS_HIP(hipEventSynchronize(r.b));
+        float ms = 0.f;
+        GS_HIP(hipEventElapsedTime(&ms, r.a, r.b));
+        if (r.stage < n) { total_ms[r.stage] += ms; counts[r.stage] += 1; }
+    }
+    std::lock_guard<std::mutex> g(p.mu);
+    for (const ProfRecord& r : recs) { p.pool.push_back(r.a); p.pool.push_back(r.b); }
+    return GS_OK;
+}
+
 int gs_abi_version(void) { return GS_RASTER_ABI_VERSION; }
 
 size_t gs_geometry_buffer_size(int P) { return geom_layout(P).total; }
@@ -307,7 +401,7 @@ int gs_rasterize_forward(const gs_settings* s, int P, int M, const float* means3
         ra.tile_last = at<uint32_t>(img, il.tile_last);
         ra.out_color = out_color;
         ra.out_depth = out_depth;
-        launch_render_forward(ra, stream);
+        { StageScope sc(ST_RENDER_FWD, stream); launch_render_forward(ra, stream); }
         GS_LAUNCHED("render");
         *num_rendered = K;
         return GS_OK;
@@ -364,7 +458,7 @@ int gs_rasterize_backward(const gs_settings* s, int P, int M, int R, const float
             rb.n_contrib = at<uint32_t>(img, il.n_contrib);
             rb.dL_dpix = dL_dpix;
             rb.records = records;
-            launch_render_backward(rb, stream);
+            { StageScope sc(ST_RENDER_BWD, stream); launch_render_backward(rb, stream); }
             GS_LAUNCHED("render backward");
         }
         GaussBwdArgs ga;
@@ -386,7 +480,7 @@ int gs_rasterize_backward(const gs_settings* s, int P, int M, int R, const float
         ga.dL_dmeans2D = dL_dmeans2D; ga.dL_dcolors = dL_dcolors; ga.dL_dopacity = dL_dopacity;
         ga.dL_dmeans3D = dL_dmeans3D; ga.dL_dcov3D = dL_dcov3D; ga.dL_dsh = M > 0 ? dL_dsh : nullptr;
         ga.dL_dscales = dL_dscales; ga.dL_drot = dL_drotations;
-        launch_gauss_backward(ga, stream);
+        { StageScope sc(ST_GAUSS_BWD, stream); launch_gauss_backward(ga, stream); }
         GS_LAUNCHED("gaussian backward");
         return GS_OK;
     } catch (const std::exception& e) {
@@ -442,7 +536,7 @@ int gs_apply_weights(const gs_settings* s, int P, int M, const float* means3D, f
         aw.image_weights = image_weights;
         aw.weights = weights;
         aw.cnt = cnt;
-        launch_render_apply_weights(aw, stream);
+        { StageScope sc(ST_APPLY_WEIGHTS, stream); launch_render_apply_weights(aw, stream); }
         GS_LAUNCHED("apply_weights render");
         return GS_OK;
     } catch (const std::exception& e) {

@@ -127,6 +127,15 @@ size_t gs_binning_buffer_size(int num_rendered, int num_tiles);
 long long gs_buffer_offset(const char *buffer, const char *field, int P, int width, int height,
                            int num_rendered);
 
+/* Stage profiler (bench / diagnostics): when enabled, every stage of the
+ * calls made on this host thread is bracketed by HIP events on its stream.
+ * gs_profile_collect synchronises on the recorded events, writes the summed
+ * milliseconds and launch counts per stage (n entries) and resets. */
+int gs_profile_enable(int on);
+int gs_profile_num_stages(void);
+const char *gs_profile_stage_name(int i);
+int gs_profile_collect(double *total_ms, int *counts, int n);
+
 const char *gs_last_error(void);
 int gs_abi_version(void);
 
