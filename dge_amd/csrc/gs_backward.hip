@@ -12,6 +12,12 @@
 // The 3D covariance is recomputed from (scale, rotation) with the forward's
 // own helper instead of being stored in the geometry buffer (-48 B/Gaussian
 // of HBM traffic).
+// Exact IEEE single-precision operations in the order written (no FMA
+// contraction): the per-Gaussian geometry, depth keys, radii and tile rects
+// then match the CPU restatement bit for bit, so the discrete outputs
+// (num_rendered, radii, sorted tile lists) are identical, not just close.
+// These kernels are HBM-bound; the extra multiplies cost nothing measurable.
+#pragma clang fp contract(off)
 #include "gs_common.h"
 #include "gs_internal.h"
 

@@ -9,6 +9,12 @@
 //     read-back overlaps the depth sort instead of draining the stream;
 //   * colour and depth packed into one float4 (rgbd) for the blend loop.
 // One thread per Gaussian; 256-thread workgroups (4 waves).
+// Exact IEEE single-precision operations in the order written (no FMA
+// contraction): the per-Gaussian geometry, depth keys, radii and tile rects
+// then match the CPU restatement bit for bit, so the discrete outputs
+// (num_rendered, radii, sorted tile lists) are identical, not just close.
+// These kernels are HBM-bound; the extra multiplies cost nothing measurable.
+#pragma clang fp contract(off)
 #include "gs_common.h"
 #include "gs_internal.h"
 

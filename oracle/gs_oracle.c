@@ -842,3 +842,12 @@ int go_apply_weights(const go_settings *s, const go_inputs *in, int C, const flo
     go_free(st);
     return GO_OK;
 }
+
+/* Test hook: forward.cu:20-71 for N points (pins the SH path against the
+ * reference's own eval_sh). pos/campos -> rgb [N,3] and clamped [N,3]. */
+void go_sh_to_rgb(int N, int deg, int M, const float *pos, const float *campos, const float *shs, float *rgb,
+                  unsigned char *clamped) {
+    for (int i = 0; i < N; ++i)
+        sh_to_rgb(deg, M, v3ld(pos + 3 * (size_t)i), v3ld(campos), shs + (size_t)i * M * 3, clamped + 3 * (size_t)i,
+                  rgb + 3 * (size_t)i);
+}

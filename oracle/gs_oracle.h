@@ -85,6 +85,10 @@ void go_mark_visible(int P, const float *means3D, const float *viewmatrix, const
 int go_apply_weights(const go_settings *s, const go_inputs *in, int C, const float *image_weights,
                      float *weights, int *cnt);
 
+/* forward.cu:20-71 for N points (test hook). */
+void go_sh_to_rgb(int N, int deg, int M, const float *pos, const float *campos, const float *shs, float *rgb,
+                  unsigned char *clamped);
+
 #ifdef __cplusplus
 }
 #endif

@@ -84,6 +84,7 @@ def lib():
         L.go_apply_weights.restype = ctypes.c_int
         L.go_apply_weights.argtypes = [ctypes.POINTER(_Settings), ctypes.POINTER(_Inputs), ctypes.c_int, _f32p, _f32p, _i32p]
         L.go_set_threads.argtypes = [ctypes.c_int]
+        L.go_sh_to_rgb.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, _f32p, _f32p, _f32p, _f32p, _u8p]
         _lib = L
     return _lib
 
@@ -300,3 +301,15 @@ def apply_weights(settings, means3D, opacities, weights, cnt, image_weights, sca
     if rc != 0:
         raise RuntimeError(f"oracle apply_weights failed with code {rc}")
     return w2.reshape(w.shape), c.reshape(np.shape(_np(cnt, np.int32)))
+
+
+def sh_to_rgb(deg, shs, pos, campos):
+    """forward.cu:20-71 for each point: (rgb [N,3], clamped [N,3] bool)."""
+    sh = _np(shs)
+    N, M = sh.shape[0], sh.shape[1]
+    p = _np(pos).reshape(N, 3)
+    c = _np(campos).reshape(3)
+    rgb = np.zeros((N, 3), np.float32)
+    cl = np.zeros((N, 3), np.uint8)
+    lib().go_sh_to_rgb(N, int(deg), M, _ptr(p), _ptr(c), _ptr(sh), _ptr(rgb), _ptr(cl, _u8p))
+    return rgb, cl.astype(bool)

@@ -1,0 +1,100 @@
+"""CPU tests of the host-side logic around the kernels: camera matrices,
+the GaussianModel-compatible getters, the Python wrapper's argument checks."""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from dge_amd import cameras as C
+from dge_amd.diff_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer
+from dge_amd.scene import build_covariance, synthetic_scene
+
+
+def test_projection_matrix_known_answer():
+    # graphics_utils.py:67-87 with symmetric frustum: P[0,0] = 1/tan(fovx/2), P[1,1] = 1/tan(fovy/2)
+    P = C.get_projection_matrix(0.01, 100.0, math.radians(60), math.radians(50)).numpy()
+    assert abs(P[0, 0] - 1 / math.tan(math.radians(30))) < 1e-6
+    assert abs(P[1, 1] - 1 / math.tan(math.radians(25))) < 1e-6
+    assert P[3, 2] == 1.0 and abs(P[2, 2] - 100 / 99.99) < 1e-6 and abs(P[2, 3] + 1.0 / 99.99) < 1e-6
+    assert P[0, 2] == 0 and P[1, 2] == 0 and P[3, 3] == 0
+
+
+def test_world2view_and_camera_center():
+    R, T = C.look_at_R_T([3.0, -4.0, 2.0])
+    Wv = C.get_world2view2(R, T)
+    np.testing.assert_allclose(Wv[:3, :3] @ Wv[:3, :3].T, np.eye(3), atol=1e-6)
+    cam = C.Camera(R, T, math.radians(60), math.radians(60), 64, 64, device="cpu")
+    np.testing.assert_allclose(cam.camera_center.numpy(), [3.0, -4.0, 2.0], atol=1e-5)
+    # the origin projects to the image centre (the camera looks at it)
+    p = torch.tensor([0.0, 0.0, 0.0, 1.0]) @ cam.full_proj_transform
+    assert abs(p[0] / p[3]) < 1e-6 and abs(p[1] / p[3]) < 1e-6 and p[3] > 0
+    # view-space z of the origin is the distance
+    v = torch.tensor([0.0, 0.0, 0.0, 1.0]) @ cam.world_view_transform
+    assert abs(float(v[2]) - math.sqrt(29.0)) < 1e-4
+
+
+def test_orbit_cameras_distinct_and_aimed():
+    cams = [C.orbit_camera(k, 8, 64, 48, device="cpu") for k in range(8)]
+    centers = np.stack([c.camera_center.numpy() for c in cams])
+    assert np.allclose(np.linalg.norm(centers, axis=1), 5.0, atol=1e-4)
+    assert len({tuple(np.round(c, 3)) for c in centers}) == 8
+    assert abs(cams[0].FoVy - 2 * math.atan(math.tan(math.radians(30)) * 48 / 64)) < 1e-9
+
+
+def test_scene_getters_follow_reference_activations():
+    sc = synthetic_scene(64, seed=1)
+    assert torch.allclose(sc.get_opacity, torch.sigmoid(sc._opacity))
+    assert torch.allclose(sc.get_scaling, torch.exp(sc._scaling))
+    assert torch.allclose(sc.get_rotation.norm(dim=1), torch.ones(64), atol=1e-6)
+    assert sc.get_features.shape == (64, 16, 3)
+    sc.localize, sc.mask = True, torch.arange(64) < 10
+    assert sc.get_xyz.shape == (10, 3) and sc.get_features.shape == (10, 16, 3)
+
+
+def test_build_covariance_matches_rasterizer_convention():
+    import torch_ref as TR
+
+    sc = synthetic_scene(32, seed=2)
+    cov = build_covariance(sc.get_scaling, sc.get_rotation)
+    # the dense reference builds Sigma = R diag(s)^2 R^T from the (normalised) quaternion
+    q = sc.get_rotation.double()
+    s = sc.get_scaling.double()
+    r, x, y, z = q[:, 0], q[:, 1], q[:, 2], q[:, 3]
+    R = torch.stack([1 - 2 * (y * y + z * z), 2 * (x * y - r * z), 2 * (x * z + r * y),
+                     2 * (x * y + r * z), 1 - 2 * (x * x + z * z), 2 * (y * z - r * x),
+                     2 * (x * z - r * y), 2 * (y * z + r * x), 1 - 2 * (x * x + y * y)], -1).reshape(-1, 3, 3)
+    S = R @ torch.diag_embed(s * s) @ R.transpose(1, 2)
+    ref = torch.stack([S[:, 0, 0], S[:, 0, 1], S[:, 0, 2], S[:, 1, 1], S[:, 1, 2], S[:, 2, 2]], -1)
+    assert torch.allclose(cov.double(), ref, rtol=1e-5, atol=1e-9)
+    assert TR is not None
+
+
+def _rs():
+    return GaussianRasterizationSettings(16, 16, 0.5, 0.5, torch.zeros(3), 1.0, torch.eye(4), torch.eye(4), 0,
+                                         torch.zeros(3), False, False)
+
+
+def test_wrapper_argument_checks_match_reference():
+    r = GaussianRasterizer(_rs())
+    m = torch.zeros(4, 3)
+    with pytest.raises(Exception, match="excatly one of either SHs or precomputed colors"):
+        r(m, m, torch.ones(4, 1))
+    with pytest.raises(Exception, match="excatly one of either SHs or precomputed colors"):
+        r(m, m, torch.ones(4, 1), shs=torch.zeros(4, 1, 3), colors_precomp=torch.zeros(4, 3))
+    with pytest.raises(Exception, match="scale/rotation pair or precomputed 3D covariance"):
+        r(m, m, torch.ones(4, 1), shs=torch.zeros(4, 1, 3))
+    with pytest.raises(Exception, match="scale/rotation pair or precomputed 3D covariance"):
+        r(m, m, torch.ones(4, 1), shs=torch.zeros(4, 1, 3), scales=torch.ones(4, 3), rotations=torch.ones(4, 4),
+          cov3D_precomp=torch.zeros(4, 6))
+
+
+def test_wrapper_rejects_bad_means_shape():
+    from dge_amd import _C
+
+    with pytest.raises(RuntimeError, match="means3D must have dimensions"):
+        _C.rasterize_gaussians(torch.zeros(3), torch.zeros(4, 2), torch.empty(0), torch.ones(4, 1), torch.ones(4, 3),
+                               torch.ones(4, 4), 1.0, torch.empty(0), torch.eye(4), torch.eye(4), 0.5, 0.5, 16, 16,
+                               torch.zeros(4, 1, 3), 0, torch.zeros(3), False, False)

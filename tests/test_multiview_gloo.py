@@ -1,0 +1,142 @@
+"""Multi-process (world_size 2, gloo, CPU) tests of the view-sharded step:
+the sharded gradient bucket all-reduce and the densification statistics
+reduce to exactly what the single-process loop over all views computes.
+
+The per-view render here is the dense PyTorch formulation (tests/torch_ref.py)
+so the data-parallel plumbing is checked end to end without a GPU; on the GPU
+box the same code path runs with dge_amd's render() and the nccl (RCCL)
+backend (bench.py --gpus N)."""
+from __future__ import annotations
+
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from dge_amd.multiview import GradBucket, multiview_step, reduce_view_stats, shard_views
+
+
+def test_shard_views_partition():
+    for n in (1, 5, 24, 25):
+        for w in (1, 2, 3, 8):
+            shards = [list(shard_views(n, w, r)) for r in range(w)]
+            flat = [i for s in shards for i in s]
+            assert flat == list(range(n))
+            assert max(map(len, shards)) - min(map(len, shards)) <= 1
+
+
+class _Scene:
+    """Minimal pc for the CPU render_fn: raw params + reference getters."""
+
+    def __init__(self, P, seed):
+        from dge_amd.scene import synthetic_scene
+
+        sc = synthetic_scene(P, seed=seed, radius=1.0, scale=0.1, sh_degree=1)
+        self.inner = sc.requires_grad_(True)
+
+    def parameters(self):
+        return self.inner.parameters()
+
+    def num_points(self):
+        return self.inner.num_points()
+
+
+def _render_fn(cam, pc, pipe, bg):
+    import torch_ref as TR
+    from dge_amd.gaussian_renderer import _settings
+
+    sc = pc.inner
+    s = _settings(cam, bg, 1.0, sc.active_sh_degree)
+    m2 = torch.zeros(sc.num_points(), 3, dtype=torch.float64, requires_grad=True)
+    m2.retain_grad()
+    c, _, radii, _ = TR.dense_render(sc.get_xyz, sc.get_opacity, s, shs=sc.get_features, scales=sc.get_scaling,
+                                     rotations=sc.get_rotation, means2D=m2, dtype=torch.float64)
+    return {"render": c.float(), "viewspace_points": _GradHolder(m2), "radii": torch.as_tensor(radii)}
+
+
+class _GradHolder:
+    def __init__(self, t):
+        self.t = t
+
+    @property
+    def grad(self):
+        return self.t.grad.float()
+
+
+def _setup(P=60, V=4, W=32, H=32):
+    from dge_amd.cameras import orbit_camera
+
+    cams = [orbit_camera(k, V, W, H, device="cpu") for k in range(V)]
+    g = torch.Generator().manual_seed(5)
+    targets = [torch.randn(3, H, W, generator=g) for _ in range(V)]
+    return cams, targets
+
+
+def _worker(rank, world, port, P, V, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.set_num_threads(1)
+        pc = _Scene(P, seed=4)
+        cams, targets = _setup(P, V)
+        mine = shard_views(V, world, rank)
+        bucket = GradBucket(pc.parameters())
+        vs, rmax = multiview_step(pc, [cams[i] for i in mine], _render_fn, None, torch.zeros(3),
+                                  [targets[i] for i in mine], bucket, V)
+        q.put((rank, bucket.flat.clone().numpy(), vs.numpy(), rmax.numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.slow
+def test_sharded_step_equals_single_process():
+    P, V = 60, 4
+    # single process reference: all views, plain autograd accumulation
+    pc = _Scene(P, seed=4)
+    cams, targets = _setup(P, V)
+    bucket = GradBucket(pc.parameters())
+    vs1, r1 = multiview_step(pc, cams, _render_fn, None, torch.zeros(3), targets, bucket, V)
+    ref = bucket.flat.clone().numpy()
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, P, V, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, flat, vs, rmax in res:
+        np.testing.assert_allclose(flat, ref, rtol=1e-5, atol=1e-6 * np.abs(ref).max())
+        np.testing.assert_allclose(vs, vs1.numpy(), rtol=1e-5, atol=1e-6 * np.abs(vs1.numpy()).max())
+        np.testing.assert_array_equal(rmax, r1.numpy())
+
+
+def test_grad_bucket_views_and_zero():
+    a = torch.zeros(3, 2, requires_grad=True)
+    b = torch.zeros(5, requires_grad=True)
+    bk = GradBucket([a, b])
+    (a.sum() * 2 + (b * torch.arange(5.0)).sum()).backward()
+    assert bk.check_attached()
+    np.testing.assert_allclose(bk.flat.numpy(), [2] * 6 + [0, 1, 2, 3, 4])
+    bk.zero()
+    assert not bk.flat.any() and bk.check_attached()
+    assert bk.allreduce() is None  # no process group: no-op
+    vs, rm = reduce_view_stats(torch.ones(2, 3), torch.tensor([1, 2], dtype=torch.int32))
+    assert vs.sum() == 6 and rm.tolist() == [1, 2]
