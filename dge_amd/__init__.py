@@ -13,3 +13,18 @@ surface on top:
 from . import _native  # noqa: F401
 
 __version__ = "0.1.0"
+
+
+def install_alias() -> None:
+    """Make ``import diff_gaussian_rasterization`` resolve to this package.
+
+    DGE's renderer (gaussiansplatting/gaussian_renderer/__init__.py:14-17)
+    imports the rasterizer under that name; after this call it gets the
+    gfx950 implementation with no change to DGE's code.
+    """
+    import sys
+
+    from . import _C, diff_gaussian_rasterization
+
+    sys.modules["diff_gaussian_rasterization"] = diff_gaussian_rasterization
+    sys.modules["diff_gaussian_rasterization._C"] = _C
