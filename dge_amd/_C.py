@@ -192,3 +192,107 @@ def apply_weights(background, means3D, weights, opacity, scales, rotations, scal
         N.check(rc, "apply_weights")
         del keep, alloc
         return None
+
+
+# ---------------------------------------------------------------------------
+# fused path: raw GaussianModel parameters, activations and SH split in-kernel
+# (gs_rasterize_forward_ex / gs_rasterize_backward_ex)
+# ---------------------------------------------------------------------------
+def _params(P, xyz, f_dc, f_rest, colors, raw_opacity, raw_scaling, raw_rotation):
+    g = N.GsParams()
+    g.P = P
+    have_sh = f_dc is not None and f_dc.numel() != 0
+    Mr = f_rest.size(1) if have_sh and f_rest is not None and f_rest.numel() != 0 else 0
+    g.M = (1 + Mr) if have_sh else 0
+    g.means3D = _ptr(xyz)
+    g.sh_dc = _ptr(f_dc) if have_sh else None
+    g.sh_rest = _ptr(f_rest) if Mr else None
+    g.sh_dc_stride = 3
+    g.sh_rest_stride = 3 * Mr
+    g.colors_precomp = None if have_sh else _ptr(colors)
+    g.opacities = _ptr(raw_opacity)
+    g.scales = _ptr(raw_scaling)
+    g.rotations = _ptr(raw_rotation)
+    g.cov3D_precomp = None
+    g.activation = 1
+    return g
+
+
+def rasterize_gaussians_fused(background, xyz, f_dc, f_rest, colors, raw_opacity, raw_scaling, raw_rotation,
+                              scale_modifier, viewmatrix, projmatrix, tan_fovx, tan_fovy, image_height, image_width,
+                              degree, campos, prefiltered, debug):
+    """Forward on raw parameters: opacity = sigmoid, scale = exp, rotation = normalize applied in-kernel,
+    SH read from _features_dc [P,1,3] and _features_rest [P,M-1,3] without concatenation."""
+    N.require_gpu(xyz)
+    dev = xyz.device
+    P = xyz.size(0)
+    H, W = int(image_height), int(image_width)
+    with torch.cuda.device(dev):
+        xyz = _f32(xyz, "xyz")
+        f_dc, f_rest, colors = _f32(f_dc, "features_dc"), _f32(f_rest, "features_rest"), _f32(colors, "colors")
+        raw_opacity, raw_scaling = _f32(raw_opacity, "opacity"), _f32(raw_scaling, "scaling")
+        raw_rotation = _f32(raw_rotation, "rotation")
+        out_color = torch.empty((3, H, W), dtype=torch.float32, device=dev)
+        out_depth = torch.empty((1, H, W), dtype=torch.float32, device=dev)
+        radii = torch.empty((P,), dtype=torch.int32, device=dev)
+        g = _params(P, xyz, f_dc, f_rest, colors, raw_opacity, raw_scaling, raw_rotation)
+        s, keep = _settings(background, viewmatrix, projmatrix, campos, tan_fovx, tan_fovy, H, W, degree,
+                            scale_modifier, prefiltered, debug)
+        alloc = _Allocator(dev)
+        nr = ctypes.c_int(0)
+        rc = N.lib().gs_rasterize_forward_ex(ctypes.byref(s), ctypes.byref(g), _ptr(out_color), _ptr(out_depth),
+                                             _ptr(radii), alloc.fn, None, _stream(dev), ctypes.byref(nr))
+        N.check(rc, "rasterize_gaussians_fused")
+        if P == 0:
+            radii.zero_()
+        geom, binning, img = alloc.buffers
+        del keep
+        return nr.value, out_color, out_depth, radii, geom, binning, img
+
+
+def rasterize_gaussians_fused_backward(background, xyz, f_dc, f_rest, colors, raw_opacity, raw_scaling, raw_rotation,
+                                       radii, scale_modifier, viewmatrix, projmatrix, tan_fovx, tan_fovy,
+                                       dL_dout_color, degree, campos, geomBuffer, R, binningBuffer, imageBuffer,
+                                       debug):
+    """-> (dL_dmeans2D [P,3], dL_dxyz, dL_dfeatures_dc, dL_dfeatures_rest, dL_dcolors, dL_dopacity_raw,
+    dL_dscaling_raw, dL_drotation_raw), gradients w.r.t. the raw tensors."""
+    N.require_gpu(xyz)
+    dev = xyz.device
+    P = xyz.size(0)
+    H, W = int(dL_dout_color.size(1)), int(dL_dout_color.size(2))
+    with torch.cuda.device(dev):
+        opts = dict(dtype=torch.float32, device=dev)
+        have_sh = f_dc is not None and f_dc.numel() != 0
+        d_m2 = torch.empty((P, 3), **opts)
+        d_xyz = torch.empty((P, 3), **opts)
+        d_dc = torch.empty_like(f_dc, **opts) if have_sh else None
+        d_rest = torch.empty_like(f_rest, **opts) if have_sh and f_rest is not None else None
+        d_col = torch.empty((P, 3), **opts)
+        d_op = torch.empty_like(raw_opacity, **opts)
+        d_sc = torch.empty((P, 3), **opts)
+        d_rot = torch.empty((P, 4), **opts)
+        out = (d_m2, d_xyz, d_dc, d_rest, d_col, d_op, d_sc, d_rot)
+        if P == 0:
+            return out
+        xyz = _f32(xyz, "xyz")
+        f_dc, f_rest, colors = _f32(f_dc, "features_dc"), _f32(f_rest, "features_rest"), _f32(colors, "colors")
+        raw_opacity, raw_scaling = _f32(raw_opacity, "opacity"), _f32(raw_scaling, "scaling")
+        raw_rotation = _f32(raw_rotation, "rotation")
+        g = _params(P, xyz, f_dc, f_rest, colors, raw_opacity, raw_scaling, raw_rotation)
+        o = N.GsGrads()
+        o.dL_dmeans2D, o.dL_dcolors, o.dL_dopacity = _ptr(d_m2), _ptr(d_col), _ptr(d_op)
+        o.dL_dmeans3D, o.dL_dcov3D = _ptr(d_xyz), None
+        o.dL_dsh_dc = _ptr(d_dc) if have_sh else None
+        o.dL_dsh_rest = _ptr(d_rest) if d_rest is not None else None
+        o.dsh_dc_stride = 3
+        o.dsh_rest_stride = 3 * (d_rest.size(1) if d_rest is not None else 0)
+        o.dL_dscales, o.dL_drotations = _ptr(d_sc), _ptr(d_rot)
+        grad = _f32(dL_dout_color, "dL_dout_color")
+        s, keep = _settings(background, viewmatrix, projmatrix, campos, tan_fovx, tan_fovy, H, W, degree,
+                            scale_modifier, False, debug)
+        rc = N.lib().gs_rasterize_backward_ex(ctypes.byref(s), ctypes.byref(g), int(R), _ptr(radii.contiguous()),
+                                              _ptr(geomBuffer), _ptr(binningBuffer), _ptr(imageBuffer), _ptr(grad),
+                                              ctypes.byref(o), _stream(dev))
+        N.check(rc, "rasterize_gaussians_fused_backward")
+        del keep
+        return out

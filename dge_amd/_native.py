@@ -43,6 +43,44 @@ class GsSettings(ctypes.Structure):
     ]
 
 
+class GsParams(ctypes.Structure):
+    """struct gs_params (include/gs_raster.h)."""
+
+    _fields_ = [
+        ("P", ctypes.c_int),
+        ("M", ctypes.c_int),
+        ("means3D", _fp),
+        ("sh_dc", _fp),
+        ("sh_rest", _fp),
+        ("sh_dc_stride", ctypes.c_int),
+        ("sh_rest_stride", ctypes.c_int),
+        ("colors_precomp", _fp),
+        ("opacities", _fp),
+        ("scales", _fp),
+        ("rotations", _fp),
+        ("cov3D_precomp", _fp),
+        ("activation", ctypes.c_int),
+    ]
+
+
+class GsGrads(ctypes.Structure):
+    """struct gs_grads (include/gs_raster.h)."""
+
+    _fields_ = [
+        ("dL_dmeans2D", _fp),
+        ("dL_dcolors", _fp),
+        ("dL_dopacity", _fp),
+        ("dL_dmeans3D", _fp),
+        ("dL_dcov3D", _fp),
+        ("dL_dsh_dc", _fp),
+        ("dL_dsh_rest", _fp),
+        ("dsh_dc_stride", ctypes.c_int),
+        ("dsh_rest_stride", ctypes.c_int),
+        ("dL_dscales", _fp),
+        ("dL_drotations", _fp),
+    ]
+
+
 ALLOC_FN = ctypes.CFUNCTYPE(ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t)
 
 # Every symbol include/gs_raster.h declares, with its ctypes signature.
@@ -51,6 +89,11 @@ SIGNATURES = {
                              + [ALLOC_FN, ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)]),
     "gs_rasterize_backward": (ctypes.c_int, [ctypes.POINTER(GsSettings), ctypes.c_int, ctypes.c_int, ctypes.c_int]
                               + [_fp] * 19 + [ctypes.c_void_p]),
+    "gs_rasterize_forward_ex": (ctypes.c_int, [ctypes.POINTER(GsSettings), ctypes.POINTER(GsParams), _fp, _fp, _fp,
+                                                ALLOC_FN, ctypes.c_void_p, ctypes.c_void_p,
+                                                ctypes.POINTER(ctypes.c_int)]),
+    "gs_rasterize_backward_ex": (ctypes.c_int, [ctypes.POINTER(GsSettings), ctypes.POINTER(GsParams), ctypes.c_int,
+                                                 _fp, _fp, _fp, _fp, _fp, ctypes.POINTER(GsGrads), ctypes.c_void_p]),
     "gs_mark_visible": (ctypes.c_int, [ctypes.c_int, _fp, _fp, _fp, _fp, ctypes.c_void_p]),
     "gs_apply_weights": (ctypes.c_int, [ctypes.POINTER(GsSettings), ctypes.c_int, ctypes.c_int, _fp, _fp, ctypes.c_int]
                          + [_fp] * 7 + [ALLOC_FN, ctypes.c_void_p, ctypes.c_void_p]),

@@ -171,35 +171,65 @@ Grid make_grid(const gs_settings* s) {
 
 int sh_coeffs_needed(int D) { return D >= 3 ? 16 : (D + 1) * (D + 1); }
 
-int validate_common(const gs_settings* s, int P, int M, const float* means3D, const float* shs,
-                    const float* colors_precomp, const float* opacities, const float* scales, const float* rotations,
-                    const float* cov3D_precomp) {
+gs_params make_params(int P, int M, const float* means3D, const float* shs, const float* colors_precomp,
+                      const float* opacities, const float* scales, const float* rotations,
+                      const float* cov3D_precomp) {
+    gs_params g;
+    g.P = P;
+    g.M = shs ? M : 0;
+    g.means3D = means3D;
+    g.sh_dc = shs;
+    g.sh_rest = shs ? shs + 3 : nullptr;
+    g.sh_dc_stride = g.sh_rest_stride = 3 * M;
+    g.colors_precomp = colors_precomp;
+    g.opacities = opacities;
+    g.scales = scales;
+    g.rotations = rotations;
+    g.cov3D_precomp = cov3D_precomp;
+    g.activation = 0;
+    return g;
+}
+
+int validate_params(const gs_settings* s, const gs_params* g, bool need_opacity = true) {
     if (!s) return set_error(GS_ERR_INVALID_ARG, "settings is NULL");
+    if (!g) return set_error(GS_ERR_INVALID_ARG, "params is NULL");
     if (s->image_width <= 0 || s->image_height <= 0)
         return set_error(GS_ERR_INVALID_ARG, "image size must be positive (got %dx%d)", s->image_width, s->image_height);
-    if (P < 0) return set_error(GS_ERR_INVALID_ARG, "P must be >= 0");
-    if (P == 0) return GS_OK;
-    if (!means3D) return set_error(GS_ERR_INVALID_ARG, "means3D must have dimensions (num_points, 3)");
-    if (!opacities) return set_error(GS_ERR_INVALID_ARG, "opacities are required");
+    if (g->P < 0) return set_error(GS_ERR_INVALID_ARG, "P must be >= 0");
+    if (g->P == 0) return GS_OK;
+    if (!g->means3D) return set_error(GS_ERR_INVALID_ARG, "means3D must have dimensions (num_points, 3)");
+    if (need_opacity && !g->opacities) return set_error(GS_ERR_INVALID_ARG, "opacities are required");
     if (!s->viewmatrix || !s->projmatrix || !s->bg || !s->campos)
         return set_error(GS_ERR_INVALID_ARG, "viewmatrix, projmatrix, bg and campos are required");
-    if (!shs && !colors_precomp)
+    if (!g->sh_dc && !g->colors_precomp)
         return set_error(GS_ERR_INVALID_ARG, "Please provide excatly one of either SHs or precomputed colors!");
-    if (shs && M < sh_coeffs_needed(s->sh_degree))
-        return set_error(GS_ERR_INVALID_ARG, "sh has %d coefficients per channel, degree %d needs %d", M, s->sh_degree,
-                         sh_coeffs_needed(s->sh_degree));
-    if (!cov3D_precomp && (!scales || !rotations))
+    if (g->sh_dc && g->M < sh_coeffs_needed(s->sh_degree))
+        return set_error(GS_ERR_INVALID_ARG, "sh has %d coefficients per channel, degree %d needs %d", g->M,
+                         s->sh_degree, sh_coeffs_needed(s->sh_degree));
+    if (g->sh_dc && g->M > 1 && !g->sh_rest) return set_error(GS_ERR_INVALID_ARG, "sh_rest is required when M > 1");
+    if (!g->cov3D_precomp && (!g->scales || !g->rotations))
         return set_error(GS_ERR_INVALID_ARG,
                          "Please provide exactly one of either scale/rotation pair or precomputed 3D covariance!");
+    if (g->activation && g->cov3D_precomp)
+        return set_error(GS_ERR_INVALID_ARG, "activation = 1 needs scales/rotations, not cov3D_precomp");
     return GS_OK;
+}
+
+ShView sh_view(const gs_params& g) {
+    ShView v;
+    v.dc = g.sh_dc;
+    v.rest = g.sh_rest ? g.sh_rest : g.sh_dc;
+    v.dc_stride = g.sh_dc_stride;
+    v.rest_stride = g.sh_rest_stride;
+    return v;
 }
 
 // Everything of the forward up to (and including) tile ranges.  On success
 // *geom/*img/*bin hold the caller-owned buffers and *K the instance count.
-int bin_forward(const gs_settings* s, const Grid& g, int P, int M, const float* means3D, const float* shs,
-                const float* colors_precomp, const float* opacities, const float* scales, const float* rotations,
-                const float* cov3D_precomp, int* radii_out, int copy_colors, gs_alloc_fn alloc, void* ctx,
-                hipStream_t stream, void** geom_out, void** img_out, void** bin_out, int* K_out) {
+int bin_forward(const gs_settings* s, const Grid& g, const gs_params& gp, int* radii_out, int copy_colors,
+                gs_alloc_fn alloc, void* ctx, hipStream_t stream, void** geom_out, void** img_out, void** bin_out,
+                int* K_out) {
+    const int P = gp.P;
     const bool debug = s->debug != 0;
     const GeomLayout gl = geom_layout(P);
     const ImgLayout il = img_layout(g.W, g.H);
@@ -214,9 +244,10 @@ int bin_forward(const gs_settings* s, const Grid& g, int P, int M, const float* 
     GS_HIP(hipMemsetAsync(at<char>(img, il.ranges), 0, il.total - il.ranges, stream));  // ranges + tile_last
 
     PreprocessArgs pa;
-    pa.P = P; pa.D = s->sh_degree; pa.M = M; pa.W = g.W; pa.H = g.H; pa.gx = g.gx; pa.gy = g.gy;
-    pa.means3D = means3D; pa.shs = shs; pa.colors_precomp = colors_precomp; pa.opacities = opacities;
-    pa.scales = scales; pa.rotations = rotations; pa.cov3D_precomp = cov3D_precomp;
+    pa.P = P; pa.D = s->sh_degree; pa.M = gp.M; pa.W = g.W; pa.H = g.H; pa.gx = g.gx; pa.gy = g.gy;
+    pa.means3D = gp.means3D; pa.sh = sh_view(gp); pa.colors_precomp = gp.colors_precomp;
+    pa.opacities = gp.opacities; pa.scales = gp.scales; pa.rotations = gp.rotations;
+    pa.cov3D_precomp = gp.cov3D_precomp; pa.activation = gp.activation;
     pa.view = s->viewmatrix; pa.proj = s->projmatrix; pa.campos = s->campos;
     pa.tanfovx = s->tanfovx; pa.tanfovy = s->tanfovy; pa.fx = g.fx; pa.fy = g.fy;
     pa.scale_modifier = s->scale_modifier;
@@ -364,14 +395,21 @@ long long gs_buffer_offset(const char* buffer, const char* field, int P, int wid
 int gs_rasterize_forward(const gs_settings* s, int P, int M, const float* means3D, const float* shs,
                          const float* colors_precomp, const float* opacities, const float* scales,
                          const float* rotations, const float* cov3D_precomp, float* out_color, float* out_depth,
-                         int* radii, gs_alloc_fn alloc, void* alloc_ctx, gs_stream_t stream_, int* num_rendered) {
+                         int* radii, gs_alloc_fn alloc, void* alloc_ctx, gs_stream_t stream, int* num_rendered) {
+    const gs_params g = make_params(P, M, means3D, shs, colors_precomp, opacities, scales, rotations, cov3D_precomp);
+    return gs_rasterize_forward_ex(s, &g, out_color, out_depth, radii, alloc, alloc_ctx, stream, num_rendered);
+}
+
+int gs_rasterize_forward_ex(const gs_settings* s, const gs_params* gp, float* out_color, float* out_depth, int* radii,
+                            gs_alloc_fn alloc, void* alloc_ctx, gs_stream_t stream_, int* num_rendered) {
     try {
         hipStream_t stream = (hipStream_t)stream_;
         if (!num_rendered || !alloc || !out_color || !out_depth)
             return set_error(GS_ERR_INVALID_ARG, "num_rendered, alloc, out_color and out_depth are required");
         *num_rendered = 0;
-        int rc = validate_common(s, P, M, means3D, shs, colors_precomp, opacities, scales, rotations, cov3D_precomp);
+        int rc = validate_params(s, gp);
         if (rc) return rc;
+        const int P = gp->P;
         const bool debug = s->debug != 0;
         const Grid g = make_grid(s);
         if (P == 0) {  // rasterize_points.cu:57-72: zero outputs, empty buffers, no render
@@ -382,8 +420,7 @@ int gs_rasterize_forward(const gs_settings* s, int P, int M, const float* means3
         }
         void *geom = nullptr, *img = nullptr, *bin = nullptr;
         int K = 0;
-        rc = bin_forward(s, g, P, M, means3D, shs, colors_precomp, opacities, scales, rotations, cov3D_precomp, radii, 1,
-                         alloc, alloc_ctx, stream, &geom, &img, &bin, &K);
+        rc = bin_forward(s, g, *gp, radii, 1, alloc, alloc_ctx, stream, &geom, &img, &bin, &K);
         if (rc) return rc;
         const GeomLayout gl = geom_layout(P);
         const ImgLayout il = img_layout(g.W, g.H);
@@ -417,25 +454,43 @@ int gs_rasterize_backward(const gs_settings* s, int P, int M, int R, const float
                           const float* cov3D_precomp, const int* radii, const void* geom, const void* binning,
                           const void* img, const float* dL_dpix, float* dL_dmeans2D, float* dL_dcolors,
                           float* dL_dopacity, float* dL_dmeans3D, float* dL_dcov3D, float* dL_dsh, float* dL_dscales,
-                          float* dL_drotations, gs_stream_t stream_) {
+                          float* dL_drotations, gs_stream_t stream) {
+    const gs_params g = make_params(P, M, means3D, shs, colors_precomp, nullptr, scales, rotations, cov3D_precomp);
+    gs_grads o;
+    o.dL_dmeans2D = dL_dmeans2D; o.dL_dcolors = dL_dcolors; o.dL_dopacity = dL_dopacity;
+    o.dL_dmeans3D = dL_dmeans3D; o.dL_dcov3D = dL_dcov3D;
+    o.dL_dsh_dc = (shs || M > 0) ? dL_dsh : nullptr;
+    o.dL_dsh_rest = o.dL_dsh_dc ? dL_dsh + 3 : nullptr;
+    o.dsh_dc_stride = o.dsh_rest_stride = 3 * M;
+    o.dL_dscales = dL_dscales; o.dL_drotations = dL_drotations;
+    gs_params g2 = g;
+    g2.M = M;  // dL_dsh is [P,M,3] even when shs is absent (then all zero)
+    return gs_rasterize_backward_ex(s, &g2, R, radii, geom, binning, img, dL_dpix, &o, stream);
+}
+
+int gs_rasterize_backward_ex(const gs_settings* s, const gs_params* gp, int R, const int* radii, const void* geom,
+                             const void* binning, const void* img, const float* dL_dpix, const gs_grads* o,
+                             gs_stream_t stream_) {
     try {
         hipStream_t stream = (hipStream_t)stream_;
-        if (!s) return set_error(GS_ERR_INVALID_ARG, "settings is NULL");
-        if (P == 0) return GS_OK;
+        if (!s || !gp || !o) return set_error(GS_ERR_INVALID_ARG, "settings, params and grads are required");
+        const int P = gp->P;
         if (P < 0) return set_error(GS_ERR_INVALID_ARG, "P must be >= 0");
+        if (P == 0) return GS_OK;
         if (s->image_width <= 0 || s->image_height <= 0) return set_error(GS_ERR_INVALID_ARG, "image size must be positive");
-        if (!means3D || !s->viewmatrix || !s->projmatrix || !s->bg || !s->campos)
+        if (!gp->means3D || !s->viewmatrix || !s->projmatrix || !s->bg || !s->campos)
             return set_error(GS_ERR_INVALID_ARG, "means3D, viewmatrix, projmatrix, bg and campos are required");
-        if (shs && M < sh_coeffs_needed(s->sh_degree))
-            return set_error(GS_ERR_INVALID_ARG, "sh has %d coefficients per channel, degree %d needs %d", M,
+        if (gp->sh_dc && gp->M < sh_coeffs_needed(s->sh_degree))
+            return set_error(GS_ERR_INVALID_ARG, "sh has %d coefficients per channel, degree %d needs %d", gp->M,
                              s->sh_degree, sh_coeffs_needed(s->sh_degree));
-        if (!cov3D_precomp && (!scales || !rotations))
+        if (!gp->cov3D_precomp && (!gp->scales || !gp->rotations))
             return set_error(GS_ERR_INVALID_ARG, "scales/rotations or cov3D_precomp are required");
-        (void)colors_precomp;  // colours were captured in the geometry buffer by the forward
+        if (gp->activation && !gp->opacities)
+            return set_error(GS_ERR_INVALID_ARG, "activation = 1 needs the raw opacities in the backward");
         if (!geom || !img || !radii || !dL_dpix)
             return set_error(GS_ERR_INVALID_ARG, "geometry/image buffers, radii and dL_dpix are required");
-        if (!dL_dmeans2D || !dL_dcolors || !dL_dopacity || !dL_dmeans3D || !dL_dcov3D || !dL_dscales || !dL_drotations ||
-            (M > 0 && !dL_dsh))
+        if (!o->dL_dmeans2D || !o->dL_dcolors || !o->dL_dopacity || !o->dL_dmeans3D || !o->dL_dscales ||
+            !o->dL_drotations || (gp->M > 1 && o->dL_dsh_dc && !o->dL_dsh_rest))
             return set_error(GS_ERR_INVALID_ARG, "gradient outputs are required");
         if (R > 0 && !binning) return set_error(GS_ERR_INVALID_ARG, "binning buffer is required when num_rendered > 0");
         const bool debug = s->debug != 0;
@@ -462,8 +517,15 @@ int gs_rasterize_backward(const gs_settings* s, int P, int M, int R, const float
             GS_LAUNCHED("render backward");
         }
         GaussBwdArgs ga;
-        ga.P = P; ga.D = s->sh_degree; ga.M = shs ? M : (dL_dsh ? M : 0); ga.W = g.W; ga.H = g.H; ga.gx = g.gx; ga.gy = g.gy;
-        ga.means3D = means3D; ga.shs = shs; ga.scales = scales; ga.rotations = rotations; ga.cov3D_precomp = cov3D_precomp;
+        ga.P = P; ga.D = s->sh_degree; ga.M = gp->M; ga.W = g.W; ga.H = g.H; ga.gx = g.gx; ga.gy = g.gy;
+        ga.means3D = gp->means3D; ga.scales = gp->scales; ga.rotations = gp->rotations;
+        ga.cov3D_precomp = gp->cov3D_precomp; ga.opacities = gp->opacities;
+        ga.sh = sh_view(*gp);
+        ga.dsh.dc = o->dL_dsh_dc;
+        ga.dsh.rest = o->dL_dsh_rest ? o->dL_dsh_rest : o->dL_dsh_dc;
+        ga.dsh.dc_stride = o->dsh_dc_stride;
+        ga.dsh.rest_stride = o->dsh_rest_stride;
+        ga.activation = gp->activation;
         ga.view = s->viewmatrix; ga.proj = s->projmatrix; ga.campos = s->campos;
         ga.tanfovx = s->tanfovx; ga.tanfovy = s->tanfovy; ga.fx = g.fx; ga.fy = g.fy;
         ga.scale_modifier = s->scale_modifier;
@@ -477,9 +539,9 @@ int gs_rasterize_backward(const gs_settings* s, int P, int M, int R, const float
         ga.ranges = at<uint2>(img, il.ranges);
         ga.tile_last = at<uint32_t>(img, il.tile_last);
         ga.records = records;
-        ga.dL_dmeans2D = dL_dmeans2D; ga.dL_dcolors = dL_dcolors; ga.dL_dopacity = dL_dopacity;
-        ga.dL_dmeans3D = dL_dmeans3D; ga.dL_dcov3D = dL_dcov3D; ga.dL_dsh = M > 0 ? dL_dsh : nullptr;
-        ga.dL_dscales = dL_dscales; ga.dL_drot = dL_drotations;
+        ga.dL_dmeans2D = o->dL_dmeans2D; ga.dL_dcolors = o->dL_dcolors; ga.dL_dopacity = o->dL_dopacity;
+        ga.dL_dmeans3D = o->dL_dmeans3D; ga.dL_dcov3D = o->dL_dcov3D;
+        ga.dL_dscales = o->dL_dscales; ga.dL_drot = o->dL_drotations;
         { StageScope sc(ST_GAUSS_BWD, stream); launch_gauss_backward(ga, stream); }
         GS_LAUNCHED("gaussian backward");
         return GS_OK;
@@ -513,15 +575,15 @@ int gs_apply_weights(const gs_settings* s, int P, int M, const float* means3D, f
             return set_error(GS_ERR_UNSUPPORTED, "Unsupported number of channels: %d", num_channels);
         if (!alloc || !weights || !image_weights || !cnt)
             return set_error(GS_ERR_INVALID_ARG, "alloc, weights, image_weights and cnt are required");
-        int rc = validate_common(s, P, M, means3D, shs, weights, opacities, scales, rotations, cov3D_precomp);
+        const gs_params gp = make_params(P, M, means3D, shs, weights, opacities, scales, rotations, cov3D_precomp);
+        int rc = validate_params(s, &gp);
         if (rc) return rc;
         if (P == 0) return GS_OK;
         const bool debug = s->debug != 0;
         const Grid g = make_grid(s);
         void *geom = nullptr, *img = nullptr, *bin = nullptr;
         int K = 0;
-        rc = bin_forward(s, g, P, M, means3D, shs, weights, opacities, scales, rotations, cov3D_precomp, nullptr, 0,
-                         alloc, alloc_ctx, stream, &geom, &img, &bin, &K);
+        rc = bin_forward(s, g, gp, nullptr, 0, alloc, alloc_ctx, stream, &geom, &img, &bin, &K);
         if (rc) return rc;
         if (K == 0) return GS_OK;
         const GeomLayout gl = geom_layout(P);

@@ -25,28 +25,34 @@ namespace gs {
 
 // backward.cu:20-139 — writes dL_dsh for the (deg+1)^2 used coefficients and
 // returns the mean gradient through the normalised view direction.
-__device__ __forceinline__ f3 sh_backward(int deg, f3 pos, f3 campos, const float* __restrict__ sh, uint8_t clamp_bits,
-                                          f3 dL_dcolor, float* __restrict__ dsh) {
+// c0/r: SH coefficient 0 / 1.. of this Gaussian; d0/dr: the same for dL_dsh.
+__device__ __forceinline__ f3 sh_backward(int deg, f3 pos, f3 campos, const float* __restrict__ c0,
+                                          const float* __restrict__ r, uint8_t clamp_bits, f3 dL_dcolor,
+                                          float* __restrict__ d0, float* __restrict__ dr) {
     const f3 dir_orig = pos - campos;
     const float len = sqrtf(dot3(dir_orig, dir_orig));
     const f3 dir = mk3(dir_orig.x / len, dir_orig.y / len, dir_orig.z / len);
     const f3 g = mk3(dL_dcolor.x * ((clamp_bits & 1) ? 0.f : 1.f), dL_dcolor.y * ((clamp_bits & 2) ? 0.f : 1.f),
                      dL_dcolor.z * ((clamp_bits & 4) ? 0.f : 1.f));
     auto put = [&](int k, f3 v) {
-        dsh[3 * k] = v.x;
-        dsh[3 * k + 1] = v.y;
-        dsh[3 * k + 2] = v.z;
+        float* o = k == 0 ? d0 : dr + 3 * (k - 1);
+        o[0] = v.x;
+        o[1] = v.y;
+        o[2] = v.z;
     };
+    // coefficient k >= 1 of the input
+#define SHK(k) ld3(r + 3 * ((k) - 1))
     f3 dx = mk3(0, 0, 0), dy = mk3(0, 0, 0), dz = mk3(0, 0, 0);
     const float x = dir.x, y = dir.y, z = dir.z;
     put(0, g * kSH_C0);
+    (void)c0;
     if (deg > 0) {
         put(1, g * (-kSH_C1 * y));
         put(2, g * (kSH_C1 * z));
         put(3, g * (-kSH_C1 * x));
-        dx = ld3(sh + 9) * (-kSH_C1);
-        dy = ld3(sh + 3) * (-kSH_C1);
-        dz = ld3(sh + 6) * kSH_C1;
+        dx = SHK(3) * (-kSH_C1);
+        dy = SHK(1) * (-kSH_C1);
+        dz = SHK(2) * kSH_C1;
         if (deg > 1) {
             const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
             put(4, g * (kSH_C2_0 * xy));
@@ -54,12 +60,11 @@ __device__ __forceinline__ f3 sh_backward(int deg, f3 pos, f3 campos, const floa
             put(6, g * (kSH_C2_2 * (2.f * zz - xx - yy)));
             put(7, g * (kSH_C2_3 * xz));
             put(8, g * (kSH_C2_4 * (xx - yy)));
-            dx = dx + (ld3(sh + 12) * (kSH_C2_0 * y) + ld3(sh + 18) * (kSH_C2_2 * 2.f * -x) +
-                       ld3(sh + 21) * (kSH_C2_3 * z) + ld3(sh + 24) * (kSH_C2_4 * 2.f * x));
-            dy = dy + (ld3(sh + 12) * (kSH_C2_0 * x) + ld3(sh + 15) * (kSH_C2_1 * z) +
-                       ld3(sh + 18) * (kSH_C2_2 * 2.f * -y) + ld3(sh + 24) * (kSH_C2_4 * 2.f * -y));
-            dz = dz + (ld3(sh + 15) * (kSH_C2_1 * y) + ld3(sh + 18) * (kSH_C2_2 * 2.f * 2.f * z) +
-                       ld3(sh + 21) * (kSH_C2_3 * x));
+            dx = dx + (SHK(4) * (kSH_C2_0 * y) + SHK(6) * (kSH_C2_2 * 2.f * -x) + SHK(7) * (kSH_C2_3 * z) +
+                       SHK(8) * (kSH_C2_4 * 2.f * x));
+            dy = dy + (SHK(4) * (kSH_C2_0 * x) + SHK(5) * (kSH_C2_1 * z) + SHK(6) * (kSH_C2_2 * 2.f * -y) +
+                       SHK(8) * (kSH_C2_4 * 2.f * -y));
+            dz = dz + (SHK(5) * (kSH_C2_1 * y) + SHK(6) * (kSH_C2_2 * 2.f * 2.f * z) + SHK(7) * (kSH_C2_3 * x));
             if (deg > 2) {
                 put(9, g * (kSH_C3_0 * y * (3.f * xx - yy)));
                 put(10, g * (kSH_C3_1 * xy * z));
@@ -68,20 +73,21 @@ __device__ __forceinline__ f3 sh_backward(int deg, f3 pos, f3 campos, const floa
                 put(13, g * (kSH_C3_4 * x * (4.f * zz - xx - yy)));
                 put(14, g * (kSH_C3_5 * z * (xx - yy)));
                 put(15, g * (kSH_C3_6 * x * (xx - 3.f * yy)));
-                dx = dx + (ld3(sh + 27) * (kSH_C3_0 * 3.f * 2.f * xy) + ld3(sh + 30) * (kSH_C3_1 * yz) +
-                           ld3(sh + 33) * (kSH_C3_2 * -2.f * xy) + ld3(sh + 36) * (kSH_C3_3 * -3.f * 2.f * xz) +
-                           ld3(sh + 39) * (kSH_C3_4 * (-3.f * xx + 4.f * zz - yy)) +
-                           ld3(sh + 42) * (kSH_C3_5 * 2.f * xz) + ld3(sh + 45) * (kSH_C3_6 * 3.f * (xx - yy)));
-                dy = dy + (ld3(sh + 27) * (kSH_C3_0 * 3.f * (xx - yy)) + ld3(sh + 30) * (kSH_C3_1 * xz) +
-                           ld3(sh + 33) * (kSH_C3_2 * (-3.f * yy + 4.f * zz - xx)) +
-                           ld3(sh + 36) * (kSH_C3_3 * -3.f * 2.f * yz) + ld3(sh + 39) * (kSH_C3_4 * -2.f * xy) +
-                           ld3(sh + 42) * (kSH_C3_5 * -2.f * yz) + ld3(sh + 45) * (kSH_C3_6 * -3.f * 2.f * xy));
-                dz = dz + (ld3(sh + 30) * (kSH_C3_1 * xy) + ld3(sh + 33) * (kSH_C3_2 * 4.f * 2.f * yz) +
-                           ld3(sh + 36) * (kSH_C3_3 * 3.f * (2.f * zz - xx - yy)) +
-                           ld3(sh + 39) * (kSH_C3_4 * 4.f * 2.f * xz) + ld3(sh + 42) * (kSH_C3_5 * (xx - yy)));
+                dx = dx + (SHK(9) * (kSH_C3_0 * 3.f * 2.f * xy) + SHK(10) * (kSH_C3_1 * yz) +
+                           SHK(11) * (kSH_C3_2 * -2.f * xy) + SHK(12) * (kSH_C3_3 * -3.f * 2.f * xz) +
+                           SHK(13) * (kSH_C3_4 * (-3.f * xx + 4.f * zz - yy)) + SHK(14) * (kSH_C3_5 * 2.f * xz) +
+                           SHK(15) * (kSH_C3_6 * 3.f * (xx - yy)));
+                dy = dy + (SHK(9) * (kSH_C3_0 * 3.f * (xx - yy)) + SHK(10) * (kSH_C3_1 * xz) +
+                           SHK(11) * (kSH_C3_2 * (-3.f * yy + 4.f * zz - xx)) + SHK(12) * (kSH_C3_3 * -3.f * 2.f * yz) +
+                           SHK(13) * (kSH_C3_4 * -2.f * xy) + SHK(14) * (kSH_C3_5 * -2.f * yz) +
+                           SHK(15) * (kSH_C3_6 * -3.f * 2.f * xy));
+                dz = dz + (SHK(10) * (kSH_C3_1 * xy) + SHK(11) * (kSH_C3_2 * 4.f * 2.f * yz) +
+                           SHK(12) * (kSH_C3_3 * 3.f * (2.f * zz - xx - yy)) + SHK(13) * (kSH_C3_4 * 4.f * 2.f * xz) +
+                           SHK(14) * (kSH_C3_5 * (xx - yy)));
             }
         }
     }
+#undef SHK
     const f3 dL_ddir = mk3(dot3(dx, g), dot3(dy, g), dot3(dz, g));
     // dnormvdv (auxiliary.h:107-117)
     const f3 v = dir_orig;
@@ -166,15 +172,20 @@ __global__ __launch_bounds__(256) void k_gauss_bwd(GaussBwdArgs a) {
     a.dL_dcolors[3 * (size_t)idx + 1] = acc[7];
     a.dL_dcolors[3 * (size_t)idx + 2] = acc[8];
 
-    float* dsh = a.dL_dsh ? a.dL_dsh + (size_t)idx * a.M * 3 : nullptr;
+    float* d0 = a.dsh.dc ? a.dsh.dc + (size_t)idx * a.dsh.dc_stride : nullptr;
+    float* dr = a.dsh.dc ? a.dsh.rest + (size_t)idx * a.dsh.rest_stride : nullptr;
     if (!vis) {
+        if (a.activation) a.dL_dopacity[idx] = 0.f;  // d sigmoid of a zero gradient
 #pragma unroll
         for (int k = 0; k < 3; ++k) { a.dL_dmeans3D[3 * (size_t)idx + k] = 0.f; a.dL_dscales[3 * (size_t)idx + k] = 0.f; }
+        if (a.dL_dcov3D)
 #pragma unroll
-        for (int k = 0; k < 6; ++k) a.dL_dcov3D[6 * (size_t)idx + k] = 0.f;
+            for (int k = 0; k < 6; ++k) a.dL_dcov3D[6 * (size_t)idx + k] = 0.f;
         *reinterpret_cast<float4*>(a.dL_drot + 4 * (size_t)idx) = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (dsh)
-            for (int k = 0; k < a.M * 3; ++k) dsh[k] = 0.f;
+        if (d0) {
+            d0[0] = d0[1] = d0[2] = 0.f;
+            for (int k = 0; k < (a.M - 1) * 3; ++k) dr[k] = 0.f;
+        }
         return;
     }
 
@@ -183,13 +194,19 @@ __global__ __launch_bounds__(256) void k_gauss_bwd(GaussBwdArgs a) {
     const f3 m = ld3(a.means3D + 3 * (size_t)idx);
     float cov3[6];
     f3 scale = mk3(0, 0, 0);
-    float4 rot = make_float4(0, 0, 0, 0);
+    float4 rot = make_float4(0, 0, 0, 0), rot_raw = rot;
+    float rot_len = 0.f;
     if (a.cov3D_precomp) {
 #pragma unroll
         for (int k = 0; k < 6; ++k) cov3[k] = a.cov3D_precomp[6 * (size_t)idx + k];
     } else {
         scale = ld3(a.scales + 3 * (size_t)idx);
         rot = *reinterpret_cast<const float4*>(a.rotations + 4 * (size_t)idx);
+        if (a.activation) {
+            rot_raw = rot;
+            rot = act_normalize(rot_raw, rot_len);
+            scale = mk3(expf(scale.x), expf(scale.y), expf(scale.z));
+        }
         cov3d_from_scale_rot(scale, a.scale_modifier, rot, cov3);
     }
 
@@ -254,27 +271,41 @@ __global__ __launch_bounds__(256) void k_gauss_bwd(GaussBwdArgs a) {
         dmean = dmean + d2;
     }
     // ---- SH -> RGB backward ----
-    if (a.shs) {
+    if (a.sh.dc) {
         const int used = a.D >= 3 ? 16 : (a.D + 1) * (a.D + 1);
-        dmean = dmean + sh_backward(a.D, m, ld3(a.campos), a.shs + (size_t)idx * a.M * 3, a.clamped[idx],
-                                    mk3(acc[6], acc[7], acc[8]), dsh);
-        for (int k = used * 3; k < a.M * 3; ++k) dsh[k] = 0.f;
-    } else if (dsh) {
-        for (int k = 0; k < a.M * 3; ++k) dsh[k] = 0.f;
+        dmean = dmean + sh_backward(a.D, m, ld3(a.campos), a.sh.dc + (size_t)idx * a.sh.dc_stride,
+                                    a.sh.rest + (size_t)idx * a.sh.rest_stride, a.clamped[idx],
+                                    mk3(acc[6], acc[7], acc[8]), d0, dr);
+        for (int k = (used - 1) * 3; k < (a.M - 1) * 3; ++k) dr[k] = 0.f;
+    } else if (d0) {
+        d0[0] = d0[1] = d0[2] = 0.f;
+        for (int k = 0; k < (a.M - 1) * 3; ++k) dr[k] = 0.f;
     }
     a.dL_dmeans3D[3 * (size_t)idx] = dmean.x;
     a.dL_dmeans3D[3 * (size_t)idx + 1] = dmean.y;
     a.dL_dmeans3D[3 * (size_t)idx + 2] = dmean.z;
+    if (a.dL_dcov3D)
 #pragma unroll
-    for (int k = 0; k < 6; ++k) a.dL_dcov3D[6 * (size_t)idx + k] = dcov[k];
+        for (int k = 0; k < 6; ++k) a.dL_dcov3D[6 * (size_t)idx + k] = dcov[k];
+    if (a.activation) {  // opacity = sigmoid(raw): torch's sigmoid backward g * (1 - y) * y
+        const float y = act_sigmoid(a.opacities[idx]);
+        a.dL_dopacity[idx] = acc[5] * ((1.0f - y) * y);
+    }
     // ---- scale / rotation ----
     if (a.scales) {
-        float ds[3], dr[4];
-        cov3d_backward(scale, a.scale_modifier, rot, dcov, ds, dr);
+        float ds[3], dq[4];
+        cov3d_backward(scale, a.scale_modifier, rot, dcov, ds, dq);
+        float4 g4 = make_float4(dq[0], dq[1], dq[2], dq[3]);
+        if (a.activation) {  // scale = exp(raw): g * y;  rotation = normalize(raw)
+            ds[0] *= scale.x;
+            ds[1] *= scale.y;
+            ds[2] *= scale.z;
+            g4 = act_normalize_bwd(rot, rot_len, g4);
+        }
         a.dL_dscales[3 * (size_t)idx] = ds[0];
         a.dL_dscales[3 * (size_t)idx + 1] = ds[1];
         a.dL_dscales[3 * (size_t)idx + 2] = ds[2];
-        *reinterpret_cast<float4*>(a.dL_drot + 4 * (size_t)idx) = make_float4(dr[0], dr[1], dr[2], dr[3]);
+        *reinterpret_cast<float4*>(a.dL_drot + 4 * (size_t)idx) = g4;
     } else {
 #pragma unroll
         for (int k = 0; k < 3; ++k) a.dL_dscales[3 * (size_t)idx + k] = 0.f;

@@ -157,6 +157,25 @@ __device__ __forceinline__ void ewa_cov2d(const Ewa& e, float& a, float& b, floa
     c = (B10 * e.T[1][0] + B11 * e.T[1][1] + B12 * e.T[1][2]) + 0.3f;
 }
 
+// GaussianModel activations (gaussian_model.py:42-57): sigmoid, exp,
+// F.normalize(q, dim=1, eps=1e-12) and their derivatives (what torch's
+// autograd applies to the getters in the reference's render()).
+__device__ __forceinline__ float act_sigmoid(float x) { return 1.0f / (1.0f + expf(-x)); }
+__device__ __forceinline__ float4 act_normalize(float4 q, float& norm_out) {
+    const float len = sqrtf(q.x * q.x + q.y * q.y + q.z * q.z + q.w * q.w);
+    const float n = fmaxf(len, 1e-12f);
+    norm_out = len;
+    return make_float4(q.x / n, q.y / n, q.z / n, q.w / n);
+}
+// d(q / max(|q|, eps)) / dq applied to g, given y = normalized q
+__device__ __forceinline__ float4 act_normalize_bwd(float4 y, float len, float4 g) {
+    if (len > 1e-12f) {
+        const float d = y.x * g.x + y.y * g.y + y.z * g.z + y.w * g.w;
+        return make_float4((g.x - y.x * d) / len, (g.y - y.y * d) / len, (g.z - y.z * d) / len, (g.w - y.w * d) / len);
+    }
+    return make_float4(g.x / 1e-12f, g.y / 1e-12f, g.z / 1e-12f, g.w / 1e-12f);
+}
+
 // ---------------------------------------------------------------------
 // wave-level primitives (64 lanes)
 // ---------------------------------------------------------------------

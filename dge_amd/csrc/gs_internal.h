@@ -128,9 +128,26 @@ inline BinLayout bin_layout(int K, int num_tiles) {
 // ---------------------------------------------------------------------
 // launchers (defined in the .hip translation units)
 // ---------------------------------------------------------------------
+// SH coefficient k of Gaussian i: k == 0 at sh_dc + i*dc_stride,
+// k >= 1 at sh_rest + i*rest_stride + 3*(k-1).  The reference's [P,M,3]
+// tensor is dc = shs, rest = shs + 3, both strides 3M; GaussianModel's raw
+// _features_dc [P,1,3] / _features_rest [P,M-1,3] are read in place (no cat).
+struct ShView {
+    const float* dc;
+    const float* rest;
+    int dc_stride, rest_stride;
+};
+struct ShGradView {
+    float* dc;
+    float* rest;
+    int dc_stride, rest_stride;
+};
+
 struct PreprocessArgs {
     int P, D, M, W, H, gx, gy;
-    const float *means3D, *shs, *colors_precomp, *opacities, *scales, *rotations, *cov3D_precomp;
+    const float *means3D, *colors_precomp, *opacities, *scales, *rotations, *cov3D_precomp;
+    ShView sh;         // sh.dc == nullptr: no SH
+    int activation;    // 1: opacities/scales/rotations are raw GaussianModel parameters
     const float *view, *proj, *campos;
     float tanfovx, tanfovy, fx, fy, scale_modifier;
     int prefiltered, copy_colors;
@@ -219,7 +236,10 @@ void launch_render_backward(const RenderBwdArgs& a, hipStream_t s);
 
 struct GaussBwdArgs {
     int P, D, M, W, H, gx, gy;
-    const float *means3D, *shs, *scales, *rotations, *cov3D_precomp;
+    const float *means3D, *scales, *rotations, *cov3D_precomp, *opacities;
+    ShView sh;
+    ShGradView dsh;    // dsh.dc == nullptr: no SH gradient output
+    int activation;    // 1: chain the gradients through sigmoid / exp / normalize
     const float *view, *proj, *campos;
     float tanfovx, tanfovy, fx, fy, scale_modifier;
     const int* radii;       // caller's radii (the reference's visibility gate)
@@ -232,7 +252,7 @@ struct GaussBwdArgs {
     const uint2* ranges;
     const uint32_t* tile_last;
     const float4* records;
-    float *dL_dmeans2D, *dL_dcolors, *dL_dopacity, *dL_dmeans3D, *dL_dcov3D, *dL_dsh, *dL_dscales, *dL_drot;
+    float *dL_dmeans2D, *dL_dcolors, *dL_dopacity, *dL_dmeans3D, *dL_dcov3D, *dL_dscales, *dL_drot;
 };
 void launch_gauss_backward(const GaussBwdArgs& a, hipStream_t s);
 

@@ -20,26 +20,27 @@
 
 namespace gs {
 
-// forward.cu:20-71
-__device__ __forceinline__ f3 sh_to_rgb(int deg, f3 pos, f3 campos, const float* __restrict__ sh, uint8_t& clamp_bits) {
+// forward.cu:20-71.  c0 = coefficient 0, r = coefficients 1.. (see ShView)
+__device__ __forceinline__ f3 sh_to_rgb(int deg, f3 pos, f3 campos, const float* __restrict__ c0,
+                                        const float* __restrict__ r, uint8_t& clamp_bits) {
     f3 dir = pos - campos;
     const float len = sqrtf(dot3(dir, dir));
     dir = mk3(dir.x / len, dir.y / len, dir.z / len);
-    f3 res = ld3(sh) * kSH_C0;
+    f3 res = ld3(c0) * kSH_C0;
     if (deg > 0) {
         const float x = dir.x, y = dir.y, z = dir.z;
-        res = res - ld3(sh + 3) * (kSH_C1 * y) + ld3(sh + 6) * (kSH_C1 * z) - ld3(sh + 9) * (kSH_C1 * x);
+        res = res - ld3(r) * (kSH_C1 * y) + ld3(r + 3) * (kSH_C1 * z) - ld3(r + 6) * (kSH_C1 * x);
         if (deg > 1) {
             const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
-            res = res + ld3(sh + 12) * (kSH_C2_0 * xy) + ld3(sh + 15) * (kSH_C2_1 * yz) +
-                  ld3(sh + 18) * (kSH_C2_2 * (2.0f * zz - xx - yy)) + ld3(sh + 21) * (kSH_C2_3 * xz) +
-                  ld3(sh + 24) * (kSH_C2_4 * (xx - yy));
+            res = res + ld3(r + 9) * (kSH_C2_0 * xy) + ld3(r + 12) * (kSH_C2_1 * yz) +
+                  ld3(r + 15) * (kSH_C2_2 * (2.0f * zz - xx - yy)) + ld3(r + 18) * (kSH_C2_3 * xz) +
+                  ld3(r + 21) * (kSH_C2_4 * (xx - yy));
             if (deg > 2) {
-                res = res + ld3(sh + 27) * (kSH_C3_0 * y * (3.0f * xx - yy)) + ld3(sh + 30) * (kSH_C3_1 * xy * z) +
-                      ld3(sh + 33) * (kSH_C3_2 * y * (4.0f * zz - xx - yy)) +
-                      ld3(sh + 36) * (kSH_C3_3 * z * (2.0f * zz - 3.0f * xx - 3.0f * yy)) +
-                      ld3(sh + 39) * (kSH_C3_4 * x * (4.0f * zz - xx - yy)) +
-                      ld3(sh + 42) * (kSH_C3_5 * z * (xx - yy)) + ld3(sh + 45) * (kSH_C3_6 * x * (xx - 3.0f * yy));
+                res = res + ld3(r + 24) * (kSH_C3_0 * y * (3.0f * xx - yy)) + ld3(r + 27) * (kSH_C3_1 * xy * z) +
+                      ld3(r + 30) * (kSH_C3_2 * y * (4.0f * zz - xx - yy)) +
+                      ld3(r + 33) * (kSH_C3_3 * z * (2.0f * zz - 3.0f * xx - 3.0f * yy)) +
+                      ld3(r + 36) * (kSH_C3_4 * x * (4.0f * zz - xx - yy)) +
+                      ld3(r + 39) * (kSH_C3_5 * z * (xx - yy)) + ld3(r + 42) * (kSH_C3_6 * x * (xx - 3.0f * yy));
             }
         }
     }
@@ -70,8 +71,14 @@ __global__ __launch_bounds__(256) void k_preprocess(PreprocessArgs a) {
 #pragma unroll
                 for (int k = 0; k < 6; ++k) cov3[k] = a.cov3D_precomp[6 * (size_t)idx + k];
             } else {
-                const float4 q = *reinterpret_cast<const float4*>(a.rotations + 4 * (size_t)idx);
-                cov3d_from_scale_rot(ld3(a.scales + 3 * (size_t)idx), a.scale_modifier, q, cov3);
+                float4 q = *reinterpret_cast<const float4*>(a.rotations + 4 * (size_t)idx);
+                f3 sc = ld3(a.scales + 3 * (size_t)idx);
+                if (a.activation) {  // get_rotation / get_scaling (gaussian_model.py:228-240)
+                    float len;
+                    q = act_normalize(q, len);
+                    sc = mk3(expf(sc.x), expf(sc.y), expf(sc.z));
+                }
+                cov3d_from_scale_rot(sc, a.scale_modifier, q, cov3);
             }
             Ewa e;
             ewa_setup(p, a.fx, a.fy, a.tanfovx, a.tanfovy, cov3, v, e);
@@ -80,7 +87,8 @@ __global__ __launch_bounds__(256) void k_preprocess(PreprocessArgs a) {
             const float det = ca * cc - cb * cb;
             if (det != 0.0f) {
                 const float det_inv = 1.f / det;
-                const float4 conic = make_float4(cc * det_inv, -cb * det_inv, ca * det_inv, a.opacities[idx]);
+                const float op = a.activation ? act_sigmoid(a.opacities[idx]) : a.opacities[idx];
+                const float4 conic = make_float4(cc * det_inv, -cb * det_inv, ca * det_inv, op);
                 const float mid = 0.5f * (ca + cc);
                 const float l1 = mid + sqrtf(fmaxf(0.1f, mid * mid - det));
                 const float l2 = mid - sqrtf(fmaxf(0.1f, mid * mid - det));
@@ -94,7 +102,8 @@ __global__ __launch_bounds__(256) void k_preprocess(PreprocessArgs a) {
                         if (a.colors_precomp) {
                             rgb = ld3(a.colors_precomp + 3 * (size_t)idx);
                         } else {
-                            rgb = sh_to_rgb(a.D, p, ld3(a.campos), a.shs + (size_t)idx * a.M * 3, clamp_bits);
+                            rgb = sh_to_rgb(a.D, p, ld3(a.campos), a.sh.dc + (size_t)idx * a.sh.dc_stride,
+                                            a.sh.rest + (size_t)idx * a.sh.rest_stride, clamp_bits);
                         }
                     }
                     a.means2D[idx] = make_float2(px, py);

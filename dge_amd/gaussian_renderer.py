@@ -12,10 +12,12 @@ broken in the reference and work here: the
 from __future__ import annotations
 
 import math
+import os
 
 import torch
+import torch.nn.functional as F
 
-from .diff_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer
+from .diff_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer, rasterize_gaussian_model
 from .sh_utils import eval_sh
 
 
@@ -40,7 +42,27 @@ def camera2rasterizer(viewpoint_camera, bg_color: torch.Tensor, sh_degree: int =
     return GaussianRasterizer(raster_settings=_settings(viewpoint_camera, bg_color, 1.0, sh_degree))
 
 
+def _fused_ok(pc, pipe) -> bool:
+    """The raw-parameter path applies when the model is a standard GaussianModel
+    (activations exp / sigmoid / F.normalize, no `localize` subset) and the
+    pipeline asks for the in-kernel SH and covariance (the defaults)."""
+    if os.environ.get("DGE_AMD_FUSED", "1") == "0":
+        return False
+    if pipe.compute_cov3D_python or pipe.convert_SHs_python or getattr(pc, "localize", False):
+        return False
+    need = ("_xyz", "_features_dc", "_features_rest", "_opacity", "_scaling", "_rotation")
+    if not all(isinstance(getattr(pc, n, None), torch.Tensor) for n in need):
+        return False
+    for attr, fn in (("scaling_activation", torch.exp), ("opacity_activation", torch.sigmoid),
+                     ("rotation_activation", F.normalize)):
+        if getattr(pc, attr, fn) is not fn:
+            return False
+    return all(getattr(pc, n).dtype == torch.float32 and getattr(pc, n).is_cuda for n in need)
+
+
 def render(viewpoint_camera, pc, pipe, bg_color: torch.Tensor, scaling_modifier=1.0, override_color=None):
+    if _fused_ok(pc, pipe):
+        return _render_fused(viewpoint_camera, pc, pipe, bg_color, scaling_modifier, override_color)
     xyz = pc.get_xyz
     screenspace_points = torch.zeros_like(xyz, dtype=xyz.dtype, requires_grad=True, device=xyz.device) + 0
     try:
@@ -75,6 +97,32 @@ def render(viewpoint_camera, pc, pipe, bg_color: torch.Tensor, scaling_modifier=
         means3D=means3D.float(), means2D=means2D.float(), shs=shs, colors_precomp=colors_precomp,
         opacities=opacity.float(), scales=None if scales is None else scales.float(),
         rotations=None if rotations is None else rotations.float(), cov3D_precomp=cov3D_precomp)
+    return {
+        "render": rendered_image,
+        "viewspace_points": screenspace_points,
+        "visibility_filter": radii > 0,
+        "radii": radii,
+        "depth_3dgs": depth,
+    }
+
+
+def _render_fused(viewpoint_camera, pc, pipe, bg_color, scaling_modifier=1.0, override_color=None):
+    """render() for a standard GaussianModel without the getters' torch kernels:
+    the rasterizer consumes _xyz, _features_dc, _features_rest, _opacity,
+    _scaling, _rotation directly and returns their gradients."""
+    xyz = pc._xyz
+    screenspace_points = torch.zeros_like(xyz, dtype=xyz.dtype, requires_grad=True, device=xyz.device)
+    try:
+        screenspace_points.retain_grad()
+    except Exception:
+        pass
+    rs = _settings(viewpoint_camera, bg_color, scaling_modifier, pc.active_sh_degree, getattr(pipe, "debug", False))
+    if override_color is None:
+        f_dc, f_rest, colors = pc._features_dc, pc._features_rest, None
+    else:
+        f_dc, f_rest, colors = None, None, override_color.float()
+    rendered_image, radii, depth = rasterize_gaussian_model(xyz, screenspace_points, f_dc, f_rest, colors,
+                                                            pc._opacity, pc._scaling, pc._rotation, rs)
     return {
         "render": rendered_image,
         "viewspace_points": screenspace_points,

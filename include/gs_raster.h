@@ -100,6 +100,52 @@ int gs_rasterize_backward(const gs_settings *s, int P, int M, int R, const float
                           float *dL_dopacity, float *dL_dmeans3D, float *dL_dcov3D, float *dL_dsh,
                           float *dL_dscales, float *dL_drotations, gs_stream_t stream);
 
+/* Extended entry points.  gs_params describes the Gaussians with split SH
+ * storage and optional in-kernel activations, so a GaussianModel's raw
+ * parameters (gaussian_model.py:42-57, 221-258: _xyz, _features_dc,
+ * _features_rest, _opacity, _scaling, _rotation) are consumed in place: no
+ * torch.cat of the SH, no separate sigmoid/exp/normalize kernels, and the
+ * backward returns gradients w.r.t. those raw tensors.  The reference-shaped
+ * gs_rasterize_forward/backward above are thin wrappers over these. */
+typedef struct gs_params {
+    int P;
+    int M;                        /* SH coefficients per channel, 0 when no SH */
+    const float *means3D;         /* [P,3] */
+    const float *sh_dc;           /* coefficient 0 of Gaussian i at sh_dc + i*sh_dc_stride (x3 floats) */
+    const float *sh_rest;         /* coefficient k>=1 at sh_rest + i*sh_rest_stride + 3*(k-1) */
+    int sh_dc_stride;             /* in floats; [P,M,3] SH: dc = shs, rest = shs + 3, both strides 3*M */
+    int sh_rest_stride;
+    const float *colors_precomp;  /* [P,3] or NULL */
+    const float *opacities;       /* [P] */
+    const float *scales;          /* [P,3] or NULL */
+    const float *rotations;       /* [P,4] or NULL */
+    const float *cov3D_precomp;   /* [P,6] or NULL */
+    int activation;               /* 0: values used as given (the reference's contract);
+                                     1: raw parameters: opacity = sigmoid(x), scale = exp(x),
+                                        rotation = x / max(|x|, 1e-12) (F.normalize) */
+} gs_params;
+
+typedef struct gs_grads {         /* backward outputs, every element written */
+    float *dL_dmeans2D;           /* [P,3], z = 0 */
+    float *dL_dcolors;            /* [P,3] */
+    float *dL_dopacity;           /* [P] (w.r.t. the raw opacity when activation = 1) */
+    float *dL_dmeans3D;           /* [P,3] */
+    float *dL_dcov3D;             /* [P,6] or NULL */
+    float *dL_dsh_dc;             /* same addressing as gs_params.sh_dc, or NULL */
+    float *dL_dsh_rest;
+    int dsh_dc_stride;
+    int dsh_rest_stride;
+    float *dL_dscales;            /* [P,3] (raw when activation = 1) */
+    float *dL_drotations;         /* [P,4] (raw when activation = 1) */
+} gs_grads;
+
+int gs_rasterize_forward_ex(const gs_settings *s, const gs_params *g, float *out_color, float *out_depth,
+                            int *radii, gs_alloc_fn alloc, void *alloc_ctx, gs_stream_t stream,
+                            int *num_rendered);
+int gs_rasterize_backward_ex(const gs_settings *s, const gs_params *g, int R, const int *radii,
+                             const void *geom_buffer, const void *binning_buffer, const void *img_buffer,
+                             const float *dL_dpix, const gs_grads *out, gs_stream_t stream);
+
 /* present[i] = (view * means3D[i]).z > 0.2 (rasterizer_impl.cu:53-63). */
 int gs_mark_visible(int P, const float *means3D, const float *viewmatrix, const float *projmatrix,
                     uint8_t *present, gs_stream_t stream);

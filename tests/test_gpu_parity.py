@@ -272,3 +272,38 @@ def test_backward_is_deterministic_and_linear(cuda_device):
     r12 = run_gpu(s, 2.0 * g1 - 0.5 * g2, intermediates=False, **kw)
     for n in GRAD_NAMES:
         assert_close(r12[n], 2.0 * r1[n] - 0.5 * r2[n], n + " linearity", 1e-4)
+
+
+@pytest.mark.parametrize("override", [False, True])
+def test_fused_raw_parameter_path_matches_getter_path(cuda_device, monkeypatch, override):
+    """render() on a standard GaussianModel reads the raw tensors in-kernel (activations fused);
+    image, screen-space and raw-parameter gradients equal the getter path's."""
+    from dge_amd.cameras import orbit_camera
+    from dge_amd.gaussian_renderer import PipelineParams, _fused_ok, render
+    from dge_amd.scene import synthetic_scene
+
+    dev = torch.device("cuda")
+    cam = orbit_camera(2, 5, 200, 136, device=dev)
+    G = torch.randn(3, 136, 200, generator=torch.Generator().manual_seed(11)).to(dev)
+    outs = []
+    for fused in (True, False):
+        monkeypatch.setenv("DGE_AMD_FUSED", "1" if fused else "0")
+        sc = synthetic_scene(20_000, seed=21, radius=1.5, scale=0.03, device=dev).requires_grad_(True)
+        assert _fused_ok(sc, PipelineParams()) == fused
+        oc = None
+        if override:
+            oc = torch.rand(20_000, 3, generator=torch.Generator().manual_seed(2)).to(dev)
+        pkg = render(cam, sc, PipelineParams(), torch.tensor([0.1, 0.0, 0.2], device=dev), override_color=oc)
+        (pkg["render"] * G).sum().backward()
+        grads = [None if p.grad is None else p.grad.cpu().numpy() for p in sc.parameters()]
+        outs.append((pkg["render"].detach().cpu().numpy(), pkg["radii"].cpu().numpy(),
+                     pkg["viewspace_points"].grad.cpu().numpy(), grads))
+    (img_f, r_f, vs_f, g_f), (img_r, r_r, vs_r, g_r) = outs
+    np.testing.assert_array_equal(r_f, r_r)
+    assert_close(img_f, img_r, "image", 1e-5)
+    assert_close(vs_f, vs_r, "viewspace grad", 1e-4)
+    for name, a, b in zip(["_xyz", "_features_dc", "_features_rest", "_opacity", "_scaling", "_rotation"], g_f, g_r):
+        if b is None:
+            assert a is None or not np.any(a), name
+            continue
+        assert_close(a, b, name, 1e-4)
