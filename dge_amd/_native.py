@@ -106,6 +106,8 @@ SIGNATURES = {
     "gs_profile_num_stages": (ctypes.c_int, []),
     "gs_profile_stage_name": (ctypes.c_char_p, [ctypes.c_int]),
     "gs_profile_collect": (ctypes.c_int, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int), ctypes.c_int]),
+    "gs_profile_diag_enable": (ctypes.c_int, [ctypes.c_int]),
+    "gs_profile_diag_read": (ctypes.c_longlong, [ctypes.c_int, ctypes.POINTER(ctypes.c_uint64), ctypes.c_longlong]),
     "gs_last_error": (ctypes.c_char_p, []),
     "gs_abi_version": (ctypes.c_int, []),
 }
@@ -174,3 +176,17 @@ def profile_collect() -> dict:
     cnt = (ctypes.c_int * n)()
     check(L.gs_profile_collect(ms, cnt, n), "gs_profile_collect")
     return {L.gs_profile_stage_name(i).decode(): (ms[i], cnt[i]) for i in range(n)}
+
+
+def diag_enable(on: bool = True) -> None:
+    lib().gs_profile_diag_enable(int(on))
+
+
+def diag_read(which: int, max_u64: int = 1 << 20):
+    """Per-wave (forward, which=0) / per-tile (backward, which=1) diagnostics of the last launch:
+    numpy [n, 4] of (start, end) in 10 ns ticks, kept entries, rounds."""
+    import numpy as np
+
+    buf = (ctypes.c_uint64 * max_u64)()
+    n = lib().gs_profile_diag_read(int(which), buf, max_u64)
+    return np.frombuffer(buf, dtype=np.uint64, count=n).reshape(-1, 4).copy()

@@ -142,6 +142,22 @@ struct StageScope {
     }
 };
 
+// ---------------------------------------------------------------------
+// blend-kernel diagnostics (off by default): device buffers with per-wave
+// timestamps, read back by gs_profile_diag_read.
+// ---------------------------------------------------------------------
+struct Diag {
+    std::atomic<bool> on{false};
+    std::mutex mu;
+    uint64_t* buf[2] = {nullptr, nullptr};
+    size_t cap[2] = {0, 0};
+    size_t used[2] = {0, 0};
+};
+Diag& diag() {
+    static Diag d;
+    return d;
+}
+
 template <typename T>
 T* at(void* base, size_t off) {
     return reinterpret_cast<T*>(static_cast<char*>(base) + off);
@@ -327,9 +343,40 @@ int bin_forward(const gs_settings* s, const Grid& g, const gs_params& gp, int* r
 
 }  // namespace
 
+namespace gs {
+uint64_t* diag_buffer(int which, size_t n_u64) {
+    Diag& d = diag();
+    if (!d.on.load()) return nullptr;
+    std::lock_guard<std::mutex> g(d.mu);
+    if (d.cap[which] < n_u64) {
+        if (d.buf[which]) (void)hipFree(d.buf[which]);
+        d.buf[which] = nullptr;
+        if (hipMalloc((void**)&d.buf[which], n_u64 * 8) != hipSuccess) return nullptr;
+        d.cap[which] = n_u64;
+    }
+    d.used[which] = n_u64;
+    return d.buf[which];
+}
+}  // namespace gs
+
 extern "C" {
 
 const char* gs_last_error(void) { return g_last_error.c_str(); }
+
+int gs_profile_diag_enable(int on) {
+    diag().on.store(on != 0);
+    return GS_OK;
+}
+
+long long gs_profile_diag_read(int which, uint64_t* host, long long max_u64) {
+    Diag& d = diag();
+    std::lock_guard<std::mutex> g(d.mu);
+    if (which < 0 || which > 1 || !d.buf[which]) return 0;
+    const size_t n = d.used[which] < (size_t)max_u64 ? d.used[which] : (size_t)max_u64;
+    GS_HIP(hipDeviceSynchronize());
+    GS_HIP(hipMemcpy(host, d.buf[which], n * 8, hipMemcpyDeviceToHost));
+    return (long long)n;
+}
 
 int gs_profile_enable(int on) {
     profiler().on.store(on != 0);
@@ -381,6 +428,7 @@ long long gs_buffer_offset(const char* buffer, const char* field, int P, int wid
         if (!strcmp(field, "n_contrib")) return (long long)L.n_contrib;
         if (!strcmp(field, "ranges")) return (long long)L.ranges;
         if (!strcmp(field, "tile_last")) return (long long)L.tile_last;
+        if (!strcmp(field, "quad_last")) return (long long)L.quad_last;
     } else if (!strcmp(buffer, "binning")) {
         const int tiles = ((width + 15) / 16) * ((height + 15) / 16);
         const BinLayout L = bin_layout(num_rendered, tiles);
@@ -436,8 +484,10 @@ int gs_rasterize_forward_ex(const gs_settings* s, const gs_params* gp, float* ou
         ra.final_T = at<float>(img, il.final_T);
         ra.n_contrib = at<uint32_t>(img, il.n_contrib);
         ra.tile_last = at<uint32_t>(img, il.tile_last);
+        ra.quad_last = at<uint32_t>(img, il.quad_last);
         ra.out_color = out_color;
         ra.out_depth = out_depth;
+        ra.diag = diag_buffer(0, 4 * (size_t)g.tiles * 4);
         { StageScope sc(ST_RENDER_FWD, stream); launch_render_forward(ra, stream); }
         GS_LAUNCHED("render");
         *num_rendered = K;
@@ -513,6 +563,7 @@ int gs_rasterize_backward_ex(const gs_settings* s, const gs_params* gp, int R, c
             rb.n_contrib = at<uint32_t>(img, il.n_contrib);
             rb.dL_dpix = dL_dpix;
             rb.records = records;
+            rb.diag = diag_buffer(1, 4 * (size_t)g.tiles);
             { StageScope sc(ST_RENDER_BWD, stream); launch_render_backward(rb, stream); }
             GS_LAUNCHED("render backward");
         }

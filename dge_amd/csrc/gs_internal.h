@@ -85,7 +85,7 @@ inline GeomLayout geom_layout(int P) {
 }
 
 struct ImgLayout {
-    size_t final_T, n_contrib, ranges, tile_last, total;
+    size_t final_T, n_contrib, ranges, tile_last, quad_last, total;
 };
 inline ImgLayout img_layout(int W, int H) {
     ImgLayout L;
@@ -96,6 +96,7 @@ inline ImgLayout img_layout(int W, int H) {
     L.n_contrib = o; o = align_up(o + 4 * n);
     L.ranges = o; o = align_up(o + 8 * tiles);
     L.tile_last = o; o = align_up(o + 4 * tiles);
+    L.quad_last = o; o = align_up(o + 16 * tiles);
     L.total = o;
     return L;
 }
@@ -201,8 +202,10 @@ struct RenderArgs {
     float* final_T;
     uint32_t* n_contrib;
     uint32_t* tile_last;
+    uint32_t* quad_last;  // [tiles*4] max n_contrib per 8x8 quadrant
     float* out_color;
     float* out_depth;
+    uint64_t* diag;       // optional [tiles*4][4]: start, end (s_memrealtime), kept, rounds
 };
 void launch_render_forward(const RenderArgs& a, hipStream_t s);
 
@@ -231,6 +234,7 @@ struct RenderBwdArgs {
     const uint32_t* n_contrib;
     const float* dL_dpix;
     float4* records;  // 3 float4 per instance
+    uint64_t* diag;   // optional [tiles][4]: start, end, kept (sum over waves), rounds
 };
 void launch_render_backward(const RenderBwdArgs& a, hipStream_t s);
 
@@ -255,5 +259,8 @@ struct GaussBwdArgs {
     float *dL_dmeans2D, *dL_dcolors, *dL_dopacity, *dL_dmeans3D, *dL_dcov3D, *dL_dscales, *dL_drot;
 };
 void launch_gauss_backward(const GaussBwdArgs& a, hipStream_t s);
+
+// diagnostics (gs_profile_diag_*): per-wave / per-block timestamps of the blend kernels
+uint64_t* diag_buffer(int which, size_t n_u64);  // which: 0 forward, 1 backward; nullptr when off
 
 }  // namespace gs

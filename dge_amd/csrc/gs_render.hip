@@ -36,7 +36,7 @@ __device__ __forceinline__ bool cull_keep(float2 xy, float4 co, float bx0, float
     if (o < 1.0f / 255.0f) return false;  // alpha <= o*G <= o   (NaN falls through: keep)
     const float a = co.x, b = co.y, c = co.z;
     if (!(a > 0.f && c > 0.f && a * c - b * b > 0.f)) return true;  // not positive definite: no bound
-    const float thr = 2.0f * logf(255.0f * o);
+    const float thr = 2.0f * __logf(255.0f * o);  // the slack below absorbs __logf's error
     const float X0 = xy.x - (bx0 + 7.0f), X1 = xy.x - bx0;
     const float Y0 = xy.y - (by0 + 7.0f), Y1 = xy.y - by0;
     if (X0 <= 0.f && X1 >= 0.f && Y0 <= 0.f && Y1 >= 0.f) return true;
@@ -46,14 +46,14 @@ __device__ __forceinline__ bool cull_keep(float2 xy, float4 co, float bx0, float
 #pragma unroll
     for (int e = 0; e < 2; ++e) {
         const float X = e ? X1 : X0;
-        const float dy = fminf(Y1, fmaxf(Y0, -b * X / c));
+        const float dy = fminf(Y1, fmaxf(Y0, __fdividef(-b * X, c)));
         const float t1 = a * X * X, t2 = 2.f * b * X * dy, t3 = c * dy * dy;
         keep |= (t1 + t2 + t3) - 1e-5f * (t1 + fabsf(t2) + t3) <= thr + slack;
     }
 #pragma unroll
     for (int e = 0; e < 2; ++e) {
         const float Y = e ? Y1 : Y0;
-        const float dx = fminf(X1, fmaxf(X0, -b * Y / a));
+        const float dx = fminf(X1, fmaxf(X0, __fdividef(-b * Y, a)));
         const float t1 = a * dx * dx, t2 = 2.f * b * dx * Y, t3 = c * Y * Y;
         keep |= (t1 + t2 + t3) - 1e-5f * (t1 + fabsf(t2) + t3) <= thr + slack;
     }
@@ -63,6 +63,27 @@ __device__ __forceinline__ bool cull_keep(float2 xy, float4 co, float bx0, float
 // =====================================================================
 // forward: one wave per 8x8 quadrant
 // =====================================================================
+// exp used by the blend loops: v_exp_f32 on the pre-scaled argument
+// (|rel. err| ~1e-7 over the live range power in [-5.6, 0], same order as
+// the CUDA expf the reference compiles to; see DESIGN.md §5 for the parity bar)
+__device__ __forceinline__ float blend_exp(float x) { return __expf(x); }
+
+// The per-(pixel, Gaussian) test shared by the forward, the backward replay
+// and apply_weights: identical code, hence identical skip decisions
+// (forward.cu:336-348, backward.cu:491-501).  Returns false when skipped.
+__device__ __forceinline__ bool pixel_alpha(float2 xy, float4 co, float pfx, float pfy, float& dx, float& dy,
+                                            float& G, float& alpha) {
+    dx = xy.x - pfx;
+    dy = xy.y - pfy;
+    const float power = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
+    if (power > 0.0f) return false;
+    G = blend_exp(power);
+    alpha = fminf(0.99f, co.w * G);
+    return alpha >= 1.0f / 255.0f;
+}
+
+constexpr int kRound = 256;  // list entries per round: 4 per lane, all loads in flight together
+
 __global__ __launch_bounds__(64) void k_render_fwd(RenderArgs a) {
     const int quad = blockIdx.x & 3, tile = blockIdx.x >> 2;
     const int tx = tile % a.gx, ty = tile / a.gx;
@@ -72,66 +93,86 @@ __global__ __launch_bounds__(64) void k_render_fwd(RenderArgs a) {
     const bool inside = px < a.W && py < a.H;
     const float pfx = (float)px, pfy = (float)py;
 
-    __shared__ float2 s_xy[64];
-    __shared__ float4 s_co[64];
-    __shared__ float4 s_rgbd[64];
-    __shared__ uint32_t s_pos[64];
+    __shared__ float2 s_xy[kRound];
+    __shared__ float4 s_co[kRound];
+    __shared__ float4 s_rgbd[kRound];
+    __shared__ uint32_t s_pos[kRound];
 
     const uint2 range = a.ranges[tile];
     float T = 1.0f, C0 = 0.f, C1 = 0.f, C2 = 0.f, D = 0.f;
     uint32_t last = 0;
     bool done = !inside;
+    const uint64_t t_start = a.diag ? __builtin_amdgcn_s_memrealtime() : 0;
+    uint32_t diag_kept = 0, diag_rounds = 0;
 
-    for (uint32_t b = range.x; b < range.y; b += 64) {
+    // prefetch the first round's ids
+    uint32_t ids[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint32_t k = range.x + 64 * i + lane;
+        ids[i] = k < range.y ? a.point_list[k] : 0u;
+    }
+    for (uint32_t b = range.x; b < range.y; b += kRound) {
         if (!__any(!done)) break;
-        const uint32_t k = b + lane;
-        bool keep = false;
-        float2 xy = make_float2(0.f, 0.f);
-        float4 co = make_float4(0.f, 0.f, 0.f, 0.f);
-        uint32_t id = 0;
-        if (k < range.y) {
-            id = a.point_list[k];
-            xy = a.means2D[id];
-            co = a.conic_opacity[id];
-            keep = cull_keep(xy, co, (float)bx0, (float)by0);
+        float2 xy[4];
+        float4 co[4], f[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const uint32_t k = b + 64 * i + lane;
+            if (k < range.y) {
+                xy[i] = a.means2D[ids[i]];
+                co[i] = a.conic_opacity[ids[i]];
+                f[i] = a.rgbd[ids[i]];
+            }
         }
-        const uint64_t km = __ballot(keep);
-        if (keep) {
-            const int slot = __popcll(km & lanemask_lt());
-            s_xy[slot] = xy;
-            s_co[slot] = co;
-            s_rgbd[slot] = a.rgbd[id];
-            s_pos[slot] = k - range.x + 1;  // 1-based contributor index (forward.cu:331)
+        // next round's ids, in flight during this round's blend
+        uint32_t nids[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const uint32_t k = b + kRound + 64 * i + lane;
+            nids[i] = k < range.y ? a.point_list[k] : 0u;
         }
+        // cull against the quadrant, compact survivors in list order (i-major, lane-minor)
+        int nk = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const uint32_t k = b + 64 * i + lane;
+            const bool keep = k < range.y && cull_keep(xy[i], co[i], (float)bx0, (float)by0);
+            const uint64_t km = __ballot(keep);
+            if (keep) {
+                const int slot = nk + __popcll(km & lanemask_lt());
+                s_xy[slot] = xy[i];
+                s_co[slot] = co[i];
+                s_rgbd[slot] = f[i];
+                s_pos[slot] = k - range.x + 1;  // 1-based contributor index (forward.cu:331)
+            }
+            nk += __popcll(km);
+        }
+        diag_kept += nk;
+        diag_rounds += 1;
         __syncthreads();
-        const int nk = __popcll(km);
         for (int j = 0; j < nk; ++j) {
             if (!__any(!done)) break;
-            if (!done) {
-                const float2 g = s_xy[j];
-                const float4 c = s_co[j];
-                const float dx = g.x - pfx, dy = g.y - pfy;
-                const float power = -0.5f * (c.x * dx * dx + c.z * dy * dy) - c.y * dx * dy;
-                if (power <= 0.0f) {
-                    const float alpha = fminf(0.99f, c.w * expf(power));
-                    if (alpha >= 1.0f / 255.0f) {
-                        const float test_T = T * (1 - alpha);
-                        if (test_T < 0.0001f) {
-                            done = true;
-                        } else {
-                            const float4 f = s_rgbd[j];
-                            C0 += f.x * alpha * T;
-                            C1 += f.y * alpha * T;
-                            C2 += f.z * alpha * T;
-                            D += f.w * alpha * T;
-                            T = test_T;
-                            last = s_pos[j];
-                        }
-                    }
+            float dx, dy, G, alpha;
+            if (!done && pixel_alpha(s_xy[j], s_co[j], pfx, pfy, dx, dy, G, alpha)) {
+                const float test_T = T * (1 - alpha);
+                if (test_T < 0.0001f) {
+                    done = true;
+                } else {
+                    const float4 fe = s_rgbd[j];
+                    const float w = alpha * T;
+                    C0 += fe.x * w;
+                    C1 += fe.y * w;
+                    C2 += fe.z * w;
+                    D += fe.w * w;
+                    T = test_T;
+                    last = s_pos[j];
                 }
             }
         }
         __syncthreads();
+#pragma unroll
+        for (int i = 0; i < 4; ++i) ids[i] = nids[i];
     }
 
     if (inside) {
@@ -145,7 +186,17 @@ __global__ __launch_bounds__(64) void k_render_fwd(RenderArgs a) {
         a.out_depth[pix] = D;
     }
     const uint32_t m = wave_max_u32(inside ? last : 0u);
-    if (lane == 0 && m) atomicMax(&a.tile_last[tile], m);
+    if (lane == 0) {
+        a.quad_last[blockIdx.x] = m;
+        if (m) atomicMax(&a.tile_last[tile], m);
+        if (a.diag) {
+            uint64_t* d = a.diag + 4 * (size_t)blockIdx.x;
+            d[0] = t_start;
+            d[1] = __builtin_amdgcn_s_memrealtime();
+            d[2] = diag_kept;
+            d[3] = diag_rounds;
+        }
+    }
 }
 
 void launch_render_forward(const RenderArgs& a, hipStream_t s) {
@@ -204,22 +255,14 @@ __global__ __launch_bounds__(64) void k_render_apply_weights(ApplyWeightsArgs a)
         for (int j = 0; j < nk; ++j) {
             if (!__any(!done)) break;
             bool blend = false;
-            if (!done) {
-                const float2 g = s_xy[j];
-                const float4 c = s_co[j];
-                const float dx = g.x - pfx, dy = g.y - pfy;
-                const float power = -0.5f * (c.x * dx * dx + c.z * dy * dy) - c.y * dx * dy;
-                if (power <= 0.0f) {
-                    const float alpha = fminf(0.99f, c.w * expf(power));
-                    if (alpha >= 1.0f / 255.0f) {
-                        const float test_T = T * (1 - alpha);
-                        if (test_T < 0.0001f) {
-                            done = true;
-                        } else {
-                            T = test_T;
-                            blend = true;
-                        }
-                    }
+            float dx, dy, G, alpha;
+            if (!done && pixel_alpha(s_xy[j], s_co[j], pfx, pfy, dx, dy, G, alpha)) {
+                const float test_T = T * (1 - alpha);
+                if (test_T < 0.0001f) {
+                    done = true;
+                } else {
+                    T = test_T;
+                    blend = true;
                 }
             }
             const uint64_t bm = __ballot(blend);
@@ -280,6 +323,8 @@ __global__ __launch_bounds__(256) void k_render_bwd(RenderBwdArgs a) {
     float last_alpha = 0.f;
     const float ddelx_dx = (float)(0.5 * a.W), ddely_dy = (float)(0.5 * a.H);
     const uint32_t wave_last = wave_max_u32(last_contributor);
+    const uint64_t t_start = a.diag ? __builtin_amdgcn_s_memrealtime() : 0;
+    uint32_t diag_kept = 0, diag_rounds = 0;
 
     for (int hi = (int)limit; hi > 0; hi -= 64) {
         const int lo = hi > 64 ? hi - 64 : 0;
@@ -297,21 +342,19 @@ __global__ __launch_bounds__(256) void k_render_bwd(RenderBwdArgs a) {
         bool keep = false;
         if (lane < n && (uint32_t)(lo + lane) < wave_last) keep = cull_keep(s_xy[lane], s_co[lane], (float)bx0, (float)by0);
         uint64_t km = __ballot(keep);
+        diag_kept += __popcll(km);
+        diag_rounds += 1;
         while (km) {
             const int j = 63 - __clzll(km);
             km &= ~(1ull << j);
             const uint32_t contributor = (uint32_t)(lo + j);  // 0-based position in the tile list
             float g0 = 0.f, g1 = 0.f, g2 = 0.f, g3 = 0.f, g4 = 0.f, g5 = 0.f, g6 = 0.f, g7 = 0.f, g8 = 0.f;
             bool hit = false;
-            if (contributor < last_contributor) {
-                const float2 xy = s_xy[j];
-                const float4 co = s_co[j];
-                const float dx = xy.x - pfx, dy = xy.y - pfy;
-                const float power = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
-                if (power <= 0.0f) {
-                    const float G = expf(power);
-                    const float alpha = fminf(0.99f, co.w * G);
-                    if (alpha >= 1.0f / 255.0f) {
+            float dx, dy, G, alpha;
+            const float4 co = s_co[j];
+            if (contributor < last_contributor && pixel_alpha(s_xy[j], co, pfx, pfy, dx, dy, G, alpha)) {
+                {
+                    {
                         hit = true;
                         T = T / (1.f - alpha);
                         const float dchannel_dcolor = alpha * T;
@@ -380,6 +423,18 @@ __global__ __launch_bounds__(256) void k_render_bwd(RenderBwdArgs a) {
             }
         }
         __syncthreads();
+    }
+    if (a.diag) {
+        __shared__ uint32_t s_kept[4];
+        if (lane == 0) s_kept[w] = diag_kept;
+        __syncthreads();
+        if (tid == 0) {
+            uint64_t* d = a.diag + 4 * (size_t)tile;
+            d[0] = t_start;
+            d[1] = __builtin_amdgcn_s_memrealtime();
+            d[2] = (uint64_t)s_kept[0] + s_kept[1] + s_kept[2] + s_kept[3];
+            d[3] = diag_rounds;
+        }
     }
 }
 

@@ -130,6 +130,7 @@ struct go_state {
     uint32_t *ranges;        /* 2 * tiles */
     float *final_T;          /* HW */
     uint32_t *n_contrib;     /* HW */
+    uint32_t *n_visited;     /* HW: list entries visited before stopping (diagnostic) */
     const float *features;   /* rgb or colors_precomp (borrowed) */
 };
 
@@ -139,6 +140,7 @@ void go_free(go_state *st) {
     free(st->conic_opacity); free(st->rgb); free(st->tiles_touched); free(st->point_offsets);
     free(st->point_keys); free(st->point_list); free(st->ranges); free(st->final_T);
     free(st->n_contrib);
+    free(st->n_visited);
     free(st);
 }
 
@@ -158,6 +160,7 @@ long go_state_get(go_state *st, const char *name, void **ptr) {
         {"ranges", st->ranges, 2L * st->gx * st->gy},
         {"final_T", st->final_T, (long)st->W * st->H},
         {"n_contrib", st->n_contrib, (long)st->W * st->H},
+        {"n_visited", st->n_visited, (long)st->W * st->H},
     };
     for (size_t i = 0; i < sizeof(t) / sizeof(t[0]); ++i)
         if (strcmp(t[i].n, name) == 0) { *ptr = t[i].p; return t[i].c; }
@@ -348,6 +351,7 @@ static go_state *state_alloc(int P, int W, int H) {
     st->ranges = (uint32_t *)calloc(2 * (size_t)st->gx * st->gy, sizeof(uint32_t));
     st->final_T = (float *)calloc((size_t)W * H, sizeof(float));
     st->n_contrib = (uint32_t *)calloc((size_t)W * H, sizeof(uint32_t));
+    st->n_visited = (uint32_t *)calloc((size_t)W * H, sizeof(uint32_t));
     return st;
 }
 
@@ -406,9 +410,10 @@ static void render_pixel(const go_state *st, const float *features, const float 
     const uint32_t r0 = st->ranges[2 * tile], r1 = st->ranges[2 * tile + 1];
     const float pfx = (float)px, pfy = (float)py;
     float T = 1.0f, C[3] = {0, 0, 0}, D = 0;
-    uint32_t contributor = 0, last = 0;
+    uint32_t contributor = 0, last = 0, visited_stop = 0;
     for (uint32_t k = r0; k < r1; ++k) {
         contributor++;
+        visited_stop = contributor;
         uint32_t id = st->point_list[k];
         float dx = st->means2D[2 * (size_t)id] - pfx, dy = st->means2D[2 * (size_t)id + 1] - pfy;
         const float *co = st->conic_opacity + 4 * (size_t)id;
@@ -426,6 +431,7 @@ static void render_pixel(const go_state *st, const float *features, const float 
     const size_t pix = (size_t)st->W * py + px;
     st->final_T[pix] = T;
     st->n_contrib[pix] = last;
+    st->n_visited[pix] = visited_stop;
     const size_t HW = (size_t)st->W * st->H;
     for (int ch = 0; ch < 3; ++ch) out_color[ch * HW + pix] = C[ch] + T * bg[ch];
     out_depth[pix] = D;

@@ -199,7 +199,7 @@ _STATE_DTYPES = {
     "depths": np.float32, "clamped": np.uint8, "radii": np.int32, "means2D": np.float32, "cov3D": np.float32,
     "conic_opacity": np.float32, "rgb": np.float32, "tiles_touched": np.uint32, "point_offsets": np.uint32,
     "point_keys": np.uint64, "point_list": np.uint32, "ranges": np.uint32, "final_T": np.float32,
-    "n_contrib": np.uint32,
+    "n_contrib": np.uint32, "n_visited": np.uint32,
 }
 
 
