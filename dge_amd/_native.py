@@ -183,10 +183,10 @@ def diag_enable(on: bool = True) -> None:
 
 
 def diag_read(which: int, max_u64: int = 1 << 20):
-    """Per-wave (forward, which=0) / per-tile (backward, which=1) diagnostics of the last launch:
-    numpy [n, 4] of (start, end) in 10 ns ticks, kept entries, rounds."""
+    """Per-wave diagnostics of the last forward (which=0) / backward (which=1) blend launch:
+    numpy [n, 8] of (start, end) in 10 ns ticks, kept entries, rounds, loop cycles, total cycles, 0, 0."""
     import numpy as np
 
     buf = (ctypes.c_uint64 * max_u64)()
     n = lib().gs_profile_diag_read(int(which), buf, max_u64)
-    return np.frombuffer(buf, dtype=np.uint64, count=n).reshape(-1, 4).copy()
+    return np.frombuffer(buf, dtype=np.uint64, count=n).reshape(-1, 8).copy()

@@ -487,7 +487,7 @@ int gs_rasterize_forward_ex(const gs_settings* s, const gs_params* gp, float* ou
         ra.quad_last = at<uint32_t>(img, il.quad_last);
         ra.out_color = out_color;
         ra.out_depth = out_depth;
-        ra.diag = diag_buffer(0, 4 * (size_t)g.tiles * 4);
+        ra.diag = diag_buffer(0, kDiagWords * (size_t)g.tiles * 4);
         { StageScope sc(ST_RENDER_FWD, stream); launch_render_forward(ra, stream); }
         GS_LAUNCHED("render");
         *num_rendered = K;
@@ -554,7 +554,7 @@ int gs_rasterize_backward_ex(const gs_settings* s, const gs_params* gp, int R, c
             rb.W = g.W; rb.H = g.H; rb.gx = g.gx; rb.gy = g.gy;
             rb.ranges = at<uint2>(img, il.ranges);
             rb.point_list = at<uint32_t>(binning, bl.point_list);
-            rb.tile_last = at<uint32_t>(img, il.tile_last);
+            rb.quad_last = at<uint32_t>(img, il.quad_last);
             rb.means2D = at<float2>(geom, gl.means2D);
             rb.conic_opacity = at<float4>(geom, gl.conic_opacity);
             rb.rgbd = at<float4>(geom, gl.rgbd);
@@ -563,7 +563,7 @@ int gs_rasterize_backward_ex(const gs_settings* s, const gs_params* gp, int R, c
             rb.n_contrib = at<uint32_t>(img, il.n_contrib);
             rb.dL_dpix = dL_dpix;
             rb.records = records;
-            rb.diag = diag_buffer(1, 4 * (size_t)g.tiles);
+            rb.diag = diag_buffer(1, kDiagWords * (size_t)g.tiles * 4);
             { StageScope sc(ST_RENDER_BWD, stream); launch_render_backward(rb, stream); }
             GS_LAUNCHED("render backward");
         }
@@ -583,12 +583,14 @@ int gs_rasterize_backward_ex(const gs_settings* s, const gs_params* gp, int R, c
         ga.radii = radii;
         ga.geom_radii = at<int>(geom, gl.radii);
         ga.means2D = at<float2>(geom, gl.means2D);
+        ga.conic_opacity = at<float4>(geom, gl.conic_opacity);
         ga.tiles_touched = at<uint32_t>(geom, gl.tiles_touched);
         ga.first_slot = at<uint32_t>(geom, gl.first_slot);
         ga.clamped = at<uint8_t>(geom, gl.clamped);
         ga.slot_to_pos = R > 0 ? at<uint32_t>(binning, bl.slot_to_pos) : nullptr;
         ga.ranges = at<uint2>(img, il.ranges);
         ga.tile_last = at<uint32_t>(img, il.tile_last);
+        ga.quad_last = at<uint32_t>(img, il.quad_last);
         ga.records = records;
         ga.dL_dmeans2D = o->dL_dmeans2D; ga.dL_dcolors = o->dL_dcolors; ga.dL_dopacity = o->dL_dopacity;
         ga.dL_dmeans3D = o->dL_dmeans3D; ga.dL_dcov3D = o->dL_dcov3D;

@@ -151,16 +151,24 @@ __global__ __launch_bounds__(256) void k_gauss_bwd(GaussBwdArgs a) {
         const int gr = a.geom_radii[idx];
         const Rect q = tile_rect(xy.x, xy.y, gr, a.gx, a.gy);
         const int wd = q.x1 - q.x0;
+        const float4 co = a.conic_opacity[idx];
         for (uint32_t k = 0; k < n; ++k) {
-            const int t = (q.y0 + (int)k / wd) * a.gx + q.x0 + (int)k % wd;
+            const int ty = q.y0 + (int)k / wd, tx = q.x0 + (int)k % wd;
+            const int t = ty * a.gx + tx;
             const uint32_t pos = a.slot_to_pos[first + k];
-            if (pos - a.ranges[t].x < a.tile_last[t]) {
-                const float4 r0 = a.records[3 * (size_t)pos];
-                const float4 r1 = a.records[3 * (size_t)pos + 1];
-                const float4 r2 = a.records[3 * (size_t)pos + 2];
-                acc[0] += r0.x; acc[1] += r0.y; acc[2] += r0.z; acc[3] += r0.w;
-                acc[4] += r1.x; acc[5] += r1.y; acc[6] += r1.z; acc[7] += r1.w;
-                acc[8] += r2.x;
+            const uint32_t lpos = pos - a.ranges[t].x;
+            if (lpos >= a.tile_last[t]) continue;  // behind every pixel's last contributor
+            // the quadrant waves that replayed this entry wrote a record at 4*pos+quad
+#pragma unroll
+            for (int qd = 0; qd < 4; ++qd) {
+                if (lpos < a.quad_last[4 * t + qd] &&
+                    cull_keep(xy, co, (float)(tx * kTile + (qd & 1) * kQuad), (float)(ty * kTile + (qd >> 1) * kQuad))) {
+                    const float4* rec = a.records + 3 * (4 * (size_t)pos + qd);
+                    const float4 r0 = rec[0], r1 = rec[1], r2 = rec[2];
+                    acc[0] += r0.x; acc[1] += r0.y; acc[2] += r0.z; acc[3] += r0.w;
+                    acc[4] += r1.x; acc[5] += r1.y; acc[6] += r1.z; acc[7] += r1.w;
+                    acc[8] += r2.x;
+                }
             }
         }
     }

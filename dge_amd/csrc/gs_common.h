@@ -182,6 +182,42 @@ __device__ __forceinline__ float4 act_normalize_bwd(float4 y, float len, float4 
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
 __device__ __forceinline__ uint64_t lanemask_lt() { return (1ull << lane_id()) - 1ull; }
 
+// Conservative test: can Gaussian (xy, conic, opacity) reach alpha >= 1/255
+// at any pixel of the box [bx0,bx0+7] x [by0,by0+7]?  alpha = min(.99, o*G),
+// G = exp(-q/2), q = a dx^2 + 2 b dx dy + c dy^2, d = xy - pixel.
+// Shared by the blend kernels and k_gauss_bwd (which re-derives from it which
+// quadrant records exist), so contraction is pinned: every caller evaluates
+// the identical instruction sequence and takes the identical decision.
+__device__ __forceinline__ bool cull_keep(float2 xy, float4 co, float bx0, float by0) {
+#pragma clang fp contract(off)
+    const float o = co.w;
+    if (o < 1.0f / 255.0f) return false;  // alpha <= o*G <= o   (NaN falls through: keep)
+    const float a = co.x, b = co.y, c = co.z;
+    if (!(a > 0.f && c > 0.f && a * c - b * b > 0.f)) return true;  // not positive definite: no bound
+    const float thr = 2.0f * __logf(255.0f * o);  // the slack below absorbs __logf's error
+    const float X0 = xy.x - (bx0 + 7.0f), X1 = xy.x - bx0;
+    const float Y0 = xy.y - (by0 + 7.0f), Y1 = xy.y - by0;
+    if (X0 <= 0.f && X1 >= 0.f && Y0 <= 0.f && Y1 >= 0.f) return true;
+    const float slack = 2e-3f * (1.0f + fabsf(thr));
+    bool keep = false;
+    // edges dx = X: minimise over dy
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+        const float X = e ? X1 : X0;
+        const float dy = fminf(Y1, fmaxf(Y0, __fdividef(-b * X, c)));
+        const float t1 = a * X * X, t2 = 2.f * b * X * dy, t3 = c * dy * dy;
+        keep |= (t1 + t2 + t3) - 1e-5f * (t1 + fabsf(t2) + t3) <= thr + slack;
+    }
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+        const float Y = e ? Y1 : Y0;
+        const float dx = fminf(X1, fmaxf(X0, __fdividef(-b * Y, a)));
+        const float t1 = a * dx * dx, t2 = 2.f * b * dx * Y, t3 = c * Y * Y;
+        keep |= (t1 + t2 + t3) - 1e-5f * (t1 + fabsf(t2) + t3) <= thr + slack;
+    }
+    return keep;
+}
+
 // Sum over the 64 lanes with DPP row ops; the total lands in lane 63.
 template <int CTRL, int ROW_MASK>
 __device__ __forceinline__ float dpp_mov(float v) {
@@ -195,6 +231,35 @@ __device__ __forceinline__ float wave_sum_to_lane63(float v) {
     v += dpp_mov<0x142, 0xA>(v);  // row_bcast:15 into rows 1,3
     v += dpp_mov<0x143, 0xC>(v);  // row_bcast:31 into rows 2,3
     return v;
+}
+
+// Sum over the 16 lanes of each row; every lane of the row gets the total.
+// (every lane has a source in these patterns, so no `old` value is needed
+// and each step folds into one v_add_f32_dpp)
+template <int CTRL>
+__device__ __forceinline__ float dpp_row(float v) {
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, true));
+}
+__device__ __forceinline__ float row_sum16(float v) {
+    v += dpp_row<0xB1>(v);   // quad_perm [1,0,3,2]
+    v += dpp_row<0x4E>(v);   // quad_perm [2,3,0,1]
+    v += dpp_row<0x141>(v);  // row_half_mirror
+    v += dpp_row<0x140>(v);  // row_mirror
+    return v;
+}
+
+// Reduce-scatter of four per-lane values over the 64 lanes with the gfx950
+// lane swaps (v_permlane32_swap / v_permlane16_swap) and one row reduction:
+// 3 swaps + 3 adds + 4 DPP adds for four sums instead of 4 x 6 DPP adds.
+// Result: every lane of row 0 holds sum(a), row 1 sum(c), row 2 sum(b),
+// row 3 sum(d).  Fixed summation order (deterministic).
+__device__ __forceinline__ float quad_reduce(float a, float b, float c, float d) {
+    const auto p = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+    const float ab = __uint_as_float(p[0]) + __uint_as_float(p[1]);  // lanes 0-31: a, 32-63: b
+    const auto q = __builtin_amdgcn_permlane32_swap(__float_as_uint(c), __float_as_uint(d), false, false);
+    const float cd = __uint_as_float(q[0]) + __uint_as_float(q[1]);  // lanes 0-31: c, 32-63: d
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(ab), __float_as_uint(cd), false, false);
+    return row_sum16(__uint_as_float(r[0]) + __uint_as_float(r[1]));  // rows: a, c, b, d
 }
 
 __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {

@@ -10,9 +10,12 @@
 //     depth sort ping-pong (key u32 = depth bits, val u32 = index) and scratch.
 //   binning (per tile instance): tile-key sort ping-pong, slot_gauss (slot ->
 //     Gaussian), point_list (sorted position -> Gaussian), slot_to_pos, and the
-//     per-instance gradient records written by the backward blend.
+//     gradient records written by the backward blend, one 48-B slot per
+//     (instance, 8x8 quadrant) at 4*pos+q, written only for entries the
+//     quadrant's cull kept (sized for HBM capacity, not touched otherwise).
 //   image (per pixel / tile): final_T, n_contrib, ranges uint2, tile_last
-//     (max n_contrib over the tile, the backward's start position).
+//     (max n_contrib over the tile) and quad_last (max n_contrib over each
+//     quadrant: the backward wave's start position).
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -119,7 +122,7 @@ inline BinLayout bin_layout(int K, int num_tiles) {
     L.slot_gauss = o; o = align_up(o + 4 * k);
     L.point_list = o; o = align_up(o + 4 * k);
     L.slot_to_pos = o; o = align_up(o + 4 * k);
-    L.records = o; o = align_up(o + 48 * k);
+    L.records = o; o = align_up(o + 4 * 48 * k);  // one record per (instance, quadrant)
     L.sort_hist = o; o = align_up(o + 4 * ((size_t)1 << maxbits) * (size_t)L.sort_blocks);
     L.sort_totals = o; o = align_up(o + 4 * ((size_t)1 << maxbits));
     L.total = o;
@@ -205,7 +208,7 @@ struct RenderArgs {
     uint32_t* quad_last;  // [tiles*4] max n_contrib per 8x8 quadrant
     float* out_color;
     float* out_depth;
-    uint64_t* diag;       // optional [tiles*4][4]: start, end (s_memrealtime), kept, rounds
+    uint64_t* diag;       // optional [tiles*4][kDiagWords] (see diag_buffer)
 };
 void launch_render_forward(const RenderArgs& a, hipStream_t s);
 
@@ -225,7 +228,7 @@ struct RenderBwdArgs {
     int W, H, gx, gy;
     const uint2* ranges;
     const uint32_t* point_list;
-    const uint32_t* tile_last;
+    const uint32_t* quad_last;  // [tiles*4] the replay window of each quadrant wave
     const float2* means2D;
     const float4* conic_opacity;
     const float4* rgbd;
@@ -233,8 +236,8 @@ struct RenderBwdArgs {
     const float* final_T;
     const uint32_t* n_contrib;
     const float* dL_dpix;
-    float4* records;  // 3 float4 per instance
-    uint64_t* diag;   // optional [tiles][4]: start, end, kept (sum over waves), rounds
+    float4* records;  // [4*K][3] float4: one record per (instance, quadrant), kept entries only
+    uint64_t* diag;   // optional [tiles*4][kDiagWords] (see diag_buffer)
 };
 void launch_render_backward(const RenderBwdArgs& a, hipStream_t s);
 
@@ -255,12 +258,17 @@ struct GaussBwdArgs {
     const uint32_t* slot_to_pos;
     const uint2* ranges;
     const uint32_t* tile_last;
+    const uint32_t* quad_last;
+    const float4* conic_opacity;
     const float4* records;
     float *dL_dmeans2D, *dL_dcolors, *dL_dopacity, *dL_dmeans3D, *dL_dcov3D, *dL_dscales, *dL_drot;
 };
 void launch_gauss_backward(const GaussBwdArgs& a, hipStream_t s);
 
-// diagnostics (gs_profile_diag_*): per-wave / per-block timestamps of the blend kernels
+// diagnostics (gs_profile_diag_*): per-wave records of the blend kernels,
+// kDiagWords u64 each: start, end (s_memrealtime, 100 MHz), kept entries,
+// rounds, cycles in the blend/replay loops, total cycles (s_memtime).
+constexpr int kDiagWords = 8;
 uint64_t* diag_buffer(int which, size_t n_u64);  // which: 0 forward, 1 backward; nullptr when off
 
 }  // namespace gs

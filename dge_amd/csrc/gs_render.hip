@@ -16,49 +16,18 @@
 //    quadrant, so the output (including n_contrib) is unchanged;
 //  * the forward waves are independent workgroups (no block barrier, a wave
 //    retires as soon as its 64 pixels saturate);
-//  * the backward keeps the 4 quadrant waves of a tile in one workgroup,
-//    starts at the tile's largest n_contrib instead of the list end, reduces
-//    each entry's 9 gradient terms across the wave with DPP, combines the 4
-//    waves in LDS and writes ONE 48-byte record per (Gaussian, tile) instance
-//    with plain stores.  No float atomics: the per-Gaussian sum happens in
-//    gs_backward.hip in a fixed order, so the backward is bitwise
+//  * the backward also runs one independent wave per quadrant, starting at
+//    the quadrant's largest n_contrib instead of the list end; it factors the
+//    reference's per-pixel gradient terms into nine per-pixel sums,
+//    reduce-scatters them across the wave four entries at a time with the
+//    gfx950 lane swaps, and writes ONE 48-byte record per (kept entry,
+//    quadrant) with plain stores.  No float atomics: the per-Gaussian sum
+//    happens in gs_backward.hip in a fixed order, so the backward is bitwise
 //    reproducible.
 #include "gs_common.h"
 #include "gs_internal.h"
 
 namespace gs {
-
-// Conservative test: can Gaussian (xy, conic, opacity) reach alpha >= 1/255
-// at any pixel of the box [bx0,bx0+7] x [by0,by0+7]?  alpha = min(.99, o*G),
-// G = exp(-q/2), q = a dx^2 + 2 b dx dy + c dy^2, d = xy - pixel.
-__device__ __forceinline__ bool cull_keep(float2 xy, float4 co, float bx0, float by0) {
-    const float o = co.w;
-    if (o < 1.0f / 255.0f) return false;  // alpha <= o*G <= o   (NaN falls through: keep)
-    const float a = co.x, b = co.y, c = co.z;
-    if (!(a > 0.f && c > 0.f && a * c - b * b > 0.f)) return true;  // not positive definite: no bound
-    const float thr = 2.0f * __logf(255.0f * o);  // the slack below absorbs __logf's error
-    const float X0 = xy.x - (bx0 + 7.0f), X1 = xy.x - bx0;
-    const float Y0 = xy.y - (by0 + 7.0f), Y1 = xy.y - by0;
-    if (X0 <= 0.f && X1 >= 0.f && Y0 <= 0.f && Y1 >= 0.f) return true;
-    const float slack = 2e-3f * (1.0f + fabsf(thr));
-    bool keep = false;
-    // edges dx = X: minimise over dy
-#pragma unroll
-    for (int e = 0; e < 2; ++e) {
-        const float X = e ? X1 : X0;
-        const float dy = fminf(Y1, fmaxf(Y0, __fdividef(-b * X, c)));
-        const float t1 = a * X * X, t2 = 2.f * b * X * dy, t3 = c * dy * dy;
-        keep |= (t1 + t2 + t3) - 1e-5f * (t1 + fabsf(t2) + t3) <= thr + slack;
-    }
-#pragma unroll
-    for (int e = 0; e < 2; ++e) {
-        const float Y = e ? Y1 : Y0;
-        const float dx = fminf(X1, fmaxf(X0, __fdividef(-b * Y, a)));
-        const float t1 = a * dx * dx, t2 = 2.f * b * dx * Y, t3 = c * Y * Y;
-        keep |= (t1 + t2 + t3) - 1e-5f * (t1 + fabsf(t2) + t3) <= thr + slack;
-    }
-    return keep;
-}
 
 // =====================================================================
 // forward: one wave per 8x8 quadrant
@@ -69,20 +38,60 @@ __device__ __forceinline__ bool cull_keep(float2 xy, float4 co, float bx0, float
 __device__ __forceinline__ float blend_exp(float x) { return __expf(x); }
 
 // The per-(pixel, Gaussian) test shared by the forward, the backward replay
-// and apply_weights: identical code, hence identical skip decisions
-// (forward.cu:336-348, backward.cu:491-501).  Returns false when skipped.
+// and apply_weights: identical code (contraction pinned), hence identical
+// skip decisions (forward.cu:336-348, backward.cu:491-501).  Branch-free:
+// G and alpha are always defined; the result is false where the reference
+// skips (`power > 0` or `alpha < 1/255`; NaN compares as the reference's).
 __device__ __forceinline__ bool pixel_alpha(float2 xy, float4 co, float pfx, float pfy, float& dx, float& dy,
                                             float& G, float& alpha) {
+#pragma clang fp contract(off)
     dx = xy.x - pfx;
     dy = xy.y - pfy;
     const float power = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
-    if (power > 0.0f) return false;
     G = blend_exp(power);
     alpha = fminf(0.99f, co.w * G);
-    return alpha >= 1.0f / 255.0f;
+    return !(power > 0.0f) && !(alpha < 1.0f / 255.0f);
 }
 
-constexpr int kRound = 256;  // list entries per round: 4 per lane, all loads in flight together
+constexpr int kRound = 256;  // list entries per round: 4 per lane
+constexpr int kGroup = 4;    // blend entries per unrolled step (LDS is padded to a multiple)
+
+// One list entry as gathered from the geometry buffer.
+struct Entry {
+    float2 xy;
+    float4 co;
+    float4 f;  // rgb + depth
+};
+
+__device__ __forceinline__ Entry gather_entry(const float2* means2D, const float4* conic_opacity, const float4* rgbd,
+                                              uint32_t id) {
+    Entry e;
+    e.xy = means2D[id];
+    e.co = conic_opacity[id];
+    e.f = rgbd[id];
+    return e;
+}
+
+// Blend one entry into the pixel state without branches: every lane evaluates
+// the reference's tests (forward.cu:336-358) and selects.  A pixel that is
+// done, skipped, or saturates on this entry keeps its state bit-for-bit.
+__device__ __forceinline__ void blend_step(float2 xy, float4 co, float4 fe, uint32_t pos, float pfx, float pfy,
+                                          bool& done, float& T, float& C0, float& C1, float& C2, float& D,
+                                          uint32_t& last) {
+    float dx, dy, G, alpha;
+    const bool hit = pixel_alpha(xy, co, pfx, pfy, dx, dy, G, alpha) && !done;
+    const float test_T = T * (1 - alpha);
+    const bool stop = hit && test_T < 0.0001f;
+    const bool use = hit && !stop;
+    done = done || stop;
+    const float w = alpha * T;
+    C0 = use ? C0 + fe.x * w : C0;
+    C1 = use ? C1 + fe.y * w : C1;
+    C2 = use ? C2 + fe.z * w : C2;
+    D = use ? D + fe.w * w : D;
+    T = use ? test_T : T;
+    last = use ? pos : last;
+}
 
 __global__ __launch_bounds__(64) void k_render_fwd(RenderArgs a) {
     const int quad = blockIdx.x & 3, tile = blockIdx.x >> 2;
@@ -93,86 +102,82 @@ __global__ __launch_bounds__(64) void k_render_fwd(RenderArgs a) {
     const bool inside = px < a.W && py < a.H;
     const float pfx = (float)px, pfy = (float)py;
 
-    __shared__ float2 s_xy[kRound];
-    __shared__ float4 s_co[kRound];
-    __shared__ float4 s_rgbd[kRound];
-    __shared__ uint32_t s_pos[kRound];
+    __shared__ float2 s_xy[kRound + kGroup];
+    __shared__ float4 s_co[kRound + kGroup];
+    __shared__ float4 s_rgbd[kRound + kGroup];
+    __shared__ uint32_t s_pos[kRound + kGroup];
 
     const uint2 range = a.ranges[tile];
     float T = 1.0f, C0 = 0.f, C1 = 0.f, C2 = 0.f, D = 0.f;
     uint32_t last = 0;
     bool done = !inside;
     const uint64_t t_start = a.diag ? __builtin_amdgcn_s_memrealtime() : 0;
+    const uint64_t c_start = a.diag ? __builtin_amdgcn_s_memtime() : 0;
+    uint64_t c_blend = 0;
     uint32_t diag_kept = 0, diag_rounds = 0;
 
-    // prefetch the first round's ids
-    uint32_t ids[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const uint32_t k = range.x + 64 * i + lane;
-        ids[i] = k < range.y ? a.point_list[k] : 0u;
-    }
-    for (uint32_t b = range.x; b < range.y; b += kRound) {
-        if (!__any(!done)) break;
-        float2 xy[4];
-        float4 co[4], f[4];
+    // Software pipeline over rounds of 256 entries: the ids run two rounds
+    // ahead and the geometry gathers one round ahead of the blend, so a
+    // round's loads are in flight while the previous round blends.
+    // Out-of-range slots load entry 0 (valid whenever the list is non-empty)
+    // and are dropped by the cull.
+    auto load_ids = [&](uint32_t b, uint32_t (&ids)[4]) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const uint32_t k = b + 64 * i + lane;
-            if (k < range.y) {
-                xy[i] = a.means2D[ids[i]];
-                co[i] = a.conic_opacity[ids[i]];
-                f[i] = a.rgbd[ids[i]];
-            }
+            ids[i] = k < range.y ? a.point_list[k] : 0u;
         }
-        // next round's ids, in flight during this round's blend
-        uint32_t nids[4];
+    };
+    uint32_t ids[4];
+    Entry cur[4];
+    load_ids(range.x, ids);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const uint32_t k = b + kRound + 64 * i + lane;
-            nids[i] = k < range.y ? a.point_list[k] : 0u;
-        }
+    for (int i = 0; i < 4; ++i) cur[i] = gather_entry(a.means2D, a.conic_opacity, a.rgbd, ids[i]);
+    load_ids(range.x + kRound, ids);
+
+    for (uint32_t b = range.x; b < range.y; b += kRound) {
+        if (!__any(!done)) break;
         // cull against the quadrant, compact survivors in list order (i-major, lane-minor)
         int nk = 0;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const uint32_t k = b + 64 * i + lane;
-            const bool keep = k < range.y && cull_keep(xy[i], co[i], (float)bx0, (float)by0);
+            const bool keep = k < range.y && cull_keep(cur[i].xy, cur[i].co, (float)bx0, (float)by0);
             const uint64_t km = __ballot(keep);
             if (keep) {
                 const int slot = nk + __popcll(km & lanemask_lt());
-                s_xy[slot] = xy[i];
-                s_co[slot] = co[i];
-                s_rgbd[slot] = f[i];
+                s_xy[slot] = cur[i].xy;
+                s_co[slot] = cur[i].co;
+                s_rgbd[slot] = cur[i].f;
                 s_pos[slot] = k - range.x + 1;  // 1-based contributor index (forward.cu:331)
             }
             nk += __popcll(km);
         }
+        // pad to a whole group with entries that fail alpha >= 1/255 everywhere
+        if (lane < kGroup) {
+            s_xy[nk + lane] = make_float2(0.f, 0.f);
+            s_co[nk + lane] = make_float4(0.f, 0.f, 0.f, 0.f);
+            s_rgbd[nk + lane] = make_float4(0.f, 0.f, 0.f, 0.f);
+            s_pos[nk + lane] = 0u;
+        }
         diag_kept += nk;
         diag_rounds += 1;
-        __syncthreads();
-        for (int j = 0; j < nk; ++j) {
-            if (!__any(!done)) break;
-            float dx, dy, G, alpha;
-            if (!done && pixel_alpha(s_xy[j], s_co[j], pfx, pfy, dx, dy, G, alpha)) {
-                const float test_T = T * (1 - alpha);
-                if (test_T < 0.0001f) {
-                    done = true;
-                } else {
-                    const float4 fe = s_rgbd[j];
-                    const float w = alpha * T;
-                    C0 += fe.x * w;
-                    C1 += fe.y * w;
-                    C2 += fe.z * w;
-                    D += fe.w * w;
-                    T = test_T;
-                    last = s_pos[j];
-                }
-            }
-        }
-        __syncthreads();
+        // next round's gathers and the round after's ids, in flight during the blend
 #pragma unroll
-        for (int i = 0; i < 4; ++i) ids[i] = nids[i];
+        for (int i = 0; i < 4; ++i) cur[i] = gather_entry(a.means2D, a.conic_opacity, a.rgbd, ids[i]);
+        load_ids(b + 2 * kRound, ids);
+        __syncthreads();
+
+        const uint64_t c0 = a.diag ? __builtin_amdgcn_s_memtime() : 0;
+        for (int j = 0; j < nk; j += kGroup) {
+            if (!__any(!done)) break;
+#pragma unroll
+            for (int u = 0; u < kGroup; ++u)
+                blend_step(s_xy[j + u], s_co[j + u], s_rgbd[j + u], s_pos[j + u], pfx, pfy, done, T, C0, C1, C2, D,
+                           last);
+        }
+        if (a.diag) c_blend += __builtin_amdgcn_s_memtime() - c0;
+        __syncthreads();
     }
 
     if (inside) {
@@ -190,11 +195,13 @@ __global__ __launch_bounds__(64) void k_render_fwd(RenderArgs a) {
         a.quad_last[blockIdx.x] = m;
         if (m) atomicMax(&a.tile_last[tile], m);
         if (a.diag) {
-            uint64_t* d = a.diag + 4 * (size_t)blockIdx.x;
+            uint64_t* d = a.diag + kDiagWords * (size_t)blockIdx.x;
             d[0] = t_start;
             d[1] = __builtin_amdgcn_s_memrealtime();
             d[2] = diag_kept;
             d[3] = diag_rounds;
+            d[4] = c_blend;
+            d[5] = __builtin_amdgcn_s_memtime() - c_start;
         }
     }
 }
@@ -289,27 +296,93 @@ void launch_render_apply_weights(const ApplyWeightsArgs& a, hipStream_t s) {
 // =====================================================================
 // backward: 4 quadrant waves per tile, records per instance
 // =====================================================================
-__global__ __launch_bounds__(256) void k_render_bwd(RenderBwdArgs a) {
-    const int tile = blockIdx.x;
-    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+// One entry of the back-to-front replay for one pixel, branch-free
+// (backward.cu:448-545).  State: T (transmittance in front of the entry) and
+// D, the colour composited behind the current position.  The reference's
+// accum_rec / last_alpha / last_color recurrence
+//     accum = last_alpha*last_color + (1-last_alpha)*accum;  last_* = (alpha, c)
+// hands every hit the value D had before it, with D <- alpha*c + (1-alpha)*D
+// after it; written as D += ae*(c - D) with ae = 0 for a skipped pixel, the
+// update is an exact no-op there and needs no select.  T is recovered with
+// v_rcp_f32 (<= 1 ulp per hit instead of the IEEE quotient's 0.5).
+// Instead of the reference's nine per-pixel gradient terms it emits the nine
+// per-pixel sums they factor into, with u = G * dL/dalpha:
+//   g = (u dx, u dy, u dx^2, u dx dy, u dy^2, u, aT dp0, aT dp1, aT dp2)
+// — the entry's conic, opacity and the ndc scale are constant over pixels
+// and are applied once per entry after the reduction (finish_record).
+__device__ __forceinline__ void bwd_step(float2 xy, float4 co, float4 c, bool in_list, float pfx, float pfy,
+                                        float dp0, float dp1, float dp2, float nbg, float& T, float& D0,
+                                        float& D1, float& D2, float (&g)[9]) {
+    float dx, dy, G, alpha;
+    const bool hit = pixel_alpha(xy, co, pfx, pfy, dx, dy, G, alpha) && in_list;
+    const float ae = hit ? alpha : 0.f;
+    const float r = __builtin_amdgcn_rcpf(1.f - ae);
+    T = hit ? T * r : T;
+    const float t0 = c.x - D0, t1 = c.y - D1, t2 = c.z - D2;
+    float dL_dalpha = t0 * dp0;
+    dL_dalpha += t1 * dp1;
+    dL_dalpha += t2 * dp2;
+    dL_dalpha = dL_dalpha * T + nbg * r;  // nbg = -T_final * (bg . dL/dpix)
+    const float u = hit ? G * dL_dalpha : 0.f;
+    const float wc = ae * T;  // dchannel_dcolor
+    const float udx = u * dx, udy = u * dy;
+    g[0] = udx;
+    g[1] = udy;
+    g[2] = udx * dx;
+    g[3] = udx * dy;
+    g[4] = udy * dy;
+    g[5] = u;
+    g[6] = wc * dp0;
+    g[7] = wc * dp1;
+    g[8] = wc * dp2;
+    D0 += ae * t0;
+    D1 += ae * t1;
+    D2 += ae * t2;
+}
+
+// The entry's record from the quadrant sums S: the reference's per-pixel
+// terms (backward.cu:524-545) with the per-entry constants factored out:
+//   dL/dmean2D = -(ddelx_dx, ddely_dy) * o * (a Sx + b Sy, c Sy + b Sx),
+//   dL/dconic  = -o/2 (Sxx, Sxy, Syy), dL/dopacity = Su, dL/dcolor = Sc.
+__device__ __forceinline__ void finish_record(float4 co, const float (&S)[9], float ddelx_dx, float ddely_dy,
+                                              float4* rec) {
+    const float h = -0.5f * co.w;
+    rec[0] = make_float4(-(co.x * S[0] + co.y * S[1]) * co.w * ddelx_dx,
+                         -(co.z * S[1] + co.y * S[0]) * co.w * ddely_dy, h * S[2], h * S[3]);
+    rec[1] = make_float4(h * S[4], S[5], S[6], S[7]);
+    rec[2] = make_float4(S[8], 0.f, 0.f, 0.f);
+}
+
+constexpr int kBwdGroup = 4;  // entries replayed between two reduce-scatters
+
+// One wave per 8x8 quadrant, independent workgroups (no block barrier):
+// the wave walks its own window [0, quad_last) of the tile list back to
+// front in rounds of 256 (ids two rounds, geometry one round ahead), culls
+// each round against its quadrant, replays the survivors in groups of four
+// and reduce-scatters their nine sums across the wave (quad_reduce).  Each
+// kept entry gets one 48-byte record at 4*pos + quadrant; k_gauss_bwd
+// re-derives with the same cull_keep which quadrant records exist.
+__global__ __launch_bounds__(64, 4) void k_render_bwd(RenderBwdArgs a) {
+    const int quad = blockIdx.x & 3, tile = blockIdx.x >> 2;
     const int tx = tile % a.gx, ty = tile / a.gx;
-    const int bx0 = tx * kTile + (w & 1) * kQuad, by0 = ty * kTile + (w >> 1) * kQuad;
+    const int lane = threadIdx.x;
+    const int bx0 = tx * kTile + (quad & 1) * kQuad, by0 = ty * kTile + (quad >> 1) * kQuad;
     const int px = bx0 + (lane & 7), py = by0 + (lane >> 3);
     const bool inside = px < a.W && py < a.H;
     const float pfx = (float)px, pfy = (float)py;
 
-    __shared__ float2 s_xy[64];
-    __shared__ float4 s_co[64];
-    __shared__ float4 s_rgb[64];
-    __shared__ float s_part[4][9][64];
+    // kept entries of a round, compacted back to front, + a group of padding
+    __shared__ float2 s_xy[kRound + kBwdGroup];
+    __shared__ float4 s_co[kRound + kBwdGroup];
+    __shared__ float4 s_rgb[kRound + kBwdGroup];
+    __shared__ uint32_t s_pos[kRound + kBwdGroup];
 
     const uint2 range = a.ranges[tile];
-    const uint32_t limit = a.tile_last[tile];
+    const int limit = (int)a.quad_last[blockIdx.x];
     const size_t HW = (size_t)a.W * a.H;
     const size_t pix = inside ? (size_t)a.W * py + px : 0;
 
     const float T_final = inside ? a.final_T[pix] : 0.f;
-    float T = T_final;
     const uint32_t last_contributor = inside ? a.n_contrib[pix] : 0u;
     float dp0 = 0.f, dp1 = 0.f, dp2 = 0.f;
     if (inside) {
@@ -317,131 +390,101 @@ __global__ __launch_bounds__(256) void k_render_bwd(RenderBwdArgs a) {
         dp1 = a.dL_dpix[HW + pix];
         dp2 = a.dL_dpix[2 * HW + pix];
     }
-    const float bg_dot = a.bg[0] * dp0 + a.bg[1] * dp1 + a.bg[2] * dp2;
-    float acc0 = 0.f, acc1 = 0.f, acc2 = 0.f;     // accum_rec
-    float lc0 = 0.f, lc1 = 0.f, lc2 = 0.f;        // last_color
-    float last_alpha = 0.f;
+    const float nbg = -T_final * (a.bg[0] * dp0 + a.bg[1] * dp1 + a.bg[2] * dp2);
+    float T = T_final, D0 = 0.f, D1 = 0.f, D2 = 0.f;
     const float ddelx_dx = (float)(0.5 * a.W), ddely_dy = (float)(0.5 * a.H);
-    const uint32_t wave_last = wave_max_u32(last_contributor);
     const uint64_t t_start = a.diag ? __builtin_amdgcn_s_memrealtime() : 0;
+    const uint64_t c_start = a.diag ? __builtin_amdgcn_s_memtime() : 0;
+    uint64_t c_replay = 0;
     uint32_t diag_kept = 0, diag_rounds = 0;
 
-    for (int hi = (int)limit; hi > 0; hi -= 64) {
-        const int lo = hi > 64 ? hi - 64 : 0;
-        const int n = hi - lo;
-        if (tid < n) {
-            const uint32_t id = a.point_list[range.x + lo + tid];
-            s_xy[tid] = a.means2D[id];
-            s_co[tid] = a.conic_opacity[id];
-            s_rgb[tid] = a.rgbd[id];
-        }
+    // the lane-row -> entry map of quad_reduce's result (rows hold e0, e0+2, e0+1, e0+3)
+    const int row = lane >> 4;
+    const int row_entry = row == 1 ? 2 : row == 2 ? 1 : row;
+    const bool row_writer = (lane & 15) == 0;
+
+    const int nr = (limit + kRound - 1) / kRound;
+    auto round_ids = [&](int r, uint32_t (&ids)[4]) {
+        const int hi = limit - kRound * r, lo = hi > kRound ? hi - kRound : 0;
 #pragma unroll
-        for (int f = 0; f < 9; ++f) s_part[w][f][lane] = 0.f;
+        for (int i = 0; i < 4; ++i) {
+            const int k = lo + 64 * i + lane;
+            ids[i] = r < nr && k < hi ? a.point_list[range.x + k] : 0u;
+        }
+    };
+    uint32_t ids[4];
+    Entry cur[4];
+    round_ids(0, ids);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) cur[i] = gather_entry(a.means2D, a.conic_opacity, a.rgbd, ids[i]);
+    round_ids(1, ids);
+
+    for (int r = 0; r < nr; ++r) {
+        const int hi = limit - kRound * r, lo = hi > kRound ? hi - kRound : 0;
+        const int n = hi - lo;
+        // cull this round (in registers) and compact the survivors back to front
+        int nk = 0;
+#pragma unroll
+        for (int i = 3; i >= 0; --i) {
+            const int j = 64 * i + lane;
+            const bool keep = j < n && cull_keep(cur[i].xy, cur[i].co, (float)bx0, (float)by0);
+            const uint64_t km = __ballot(keep);
+            if (keep) {
+                const int slot = nk + __popcll(km & ~lanemask_lt() & ~(1ull << lane));
+                s_xy[slot] = cur[i].xy;
+                s_co[slot] = cur[i].co;
+                s_rgb[slot] = cur[i].f;
+                s_pos[slot] = (uint32_t)(lo + j);
+            }
+            nk += __popcll(km);
+        }
+        if (lane < kBwdGroup) {  // padding: alpha = 0 everywhere, never in a pixel's list
+            s_xy[nk + lane] = make_float2(0.f, 0.f);
+            s_co[nk + lane] = make_float4(0.f, 0.f, 0.f, 0.f);
+            s_rgb[nk + lane] = make_float4(0.f, 0.f, 0.f, 0.f);
+            s_pos[nk + lane] = 0xFFFFFFFFu;
+        }
+        // next round's geometry and the round after's ids, in flight during the replay
+#pragma unroll
+        for (int i = 0; i < 4; ++i) cur[i] = gather_entry(a.means2D, a.conic_opacity, a.rgbd, ids[i]);
+        round_ids(r + 2, ids);
+        diag_kept += nk;
+        diag_rounds += 1;
         __syncthreads();
 
-        bool keep = false;
-        if (lane < n && (uint32_t)(lo + lane) < wave_last) keep = cull_keep(s_xy[lane], s_co[lane], (float)bx0, (float)by0);
-        uint64_t km = __ballot(keep);
-        diag_kept += __popcll(km);
-        diag_rounds += 1;
-        while (km) {
-            const int j = 63 - __clzll(km);
-            km &= ~(1ull << j);
-            const uint32_t contributor = (uint32_t)(lo + j);  // 0-based position in the tile list
-            float g0 = 0.f, g1 = 0.f, g2 = 0.f, g3 = 0.f, g4 = 0.f, g5 = 0.f, g6 = 0.f, g7 = 0.f, g8 = 0.f;
-            bool hit = false;
-            float dx, dy, G, alpha;
-            const float4 co = s_co[j];
-            if (contributor < last_contributor && pixel_alpha(s_xy[j], co, pfx, pfy, dx, dy, G, alpha)) {
-                {
-                    {
-                        hit = true;
-                        T = T / (1.f - alpha);
-                        const float dchannel_dcolor = alpha * T;
-                        const float4 c = s_rgb[j];
-                        float dL_dalpha = 0.0f;
-                        acc0 = last_alpha * lc0 + (1.f - last_alpha) * acc0;
-                        lc0 = c.x;
-                        dL_dalpha += (c.x - acc0) * dp0;
-                        g6 = dchannel_dcolor * dp0;
-                        acc1 = last_alpha * lc1 + (1.f - last_alpha) * acc1;
-                        lc1 = c.y;
-                        dL_dalpha += (c.y - acc1) * dp1;
-                        g7 = dchannel_dcolor * dp1;
-                        acc2 = last_alpha * lc2 + (1.f - last_alpha) * acc2;
-                        lc2 = c.z;
-                        dL_dalpha += (c.z - acc2) * dp2;
-                        g8 = dchannel_dcolor * dp2;
-                        dL_dalpha *= T;
-                        last_alpha = alpha;
-                        dL_dalpha += (-T_final / (1.f - alpha)) * bg_dot;
-                        const float dL_dG = co.w * dL_dalpha;
-                        const float gdx = G * dx, gdy = G * dy;
-                        const float dG_ddelx = -gdx * co.x - gdy * co.y;
-                        const float dG_ddely = -gdy * co.z - gdx * co.y;
-                        g0 = dL_dG * dG_ddelx * ddelx_dx;
-                        g1 = dL_dG * dG_ddely * ddely_dy;
-                        g2 = -0.5f * gdx * dx * dL_dG;
-                        g3 = -0.5f * gdx * dy * dL_dG;
-                        g4 = -0.5f * gdy * dy * dL_dG;
-                        g5 = G * dL_dalpha;
-                    }
-                }
-            }
-            if (__any(hit)) {
-                g0 = wave_sum_to_lane63(g0);
-                g1 = wave_sum_to_lane63(g1);
-                g2 = wave_sum_to_lane63(g2);
-                g3 = wave_sum_to_lane63(g3);
-                g4 = wave_sum_to_lane63(g4);
-                g5 = wave_sum_to_lane63(g5);
-                g6 = wave_sum_to_lane63(g6);
-                g7 = wave_sum_to_lane63(g7);
-                g8 = wave_sum_to_lane63(g8);
-                if (lane == 63) {
-                    s_part[w][0][j] = g0; s_part[w][1][j] = g1; s_part[w][2][j] = g2;
-                    s_part[w][3][j] = g3; s_part[w][4][j] = g4; s_part[w][5][j] = g5;
-                    s_part[w][6][j] = g6; s_part[w][7][j] = g7; s_part[w][8][j] = g8;
-                }
-            }
+        const uint64_t c0 = a.diag ? __builtin_amdgcn_s_memtime() : 0;
+        for (int k = 0; k < nk; k += kBwdGroup) {
+            float g[kBwdGroup][9];
+#pragma unroll
+            for (int e = 0; e < kBwdGroup; ++e)
+                bwd_step(s_xy[k + e], s_co[k + e], s_rgb[k + e], s_pos[k + e] < last_contributor, pfx, pfy, dp0, dp1,
+                         dp2, nbg, T, D0, D1, D2, g[e]);
+            float S[9];
+#pragma unroll
+            for (int f = 0; f < 9; ++f) S[f] = quad_reduce(g[0][f], g[1][f], g[2][f], g[3][f]);
+            const int kw = k + row_entry;
+            if (row_writer && kw < nk)
+                finish_record(s_co[kw], S, ddelx_dx, ddely_dy,
+                              a.records + 3 * (4 * ((size_t)range.x + s_pos[kw]) + quad));
         }
-        __syncthreads();
-        if (tid < 3 * 64) {
-            const int q = tid >> 6, j = tid & 63;
-            if (j < n) {
-                float4 r;
-                const int f0 = 4 * q;
-                r.x = (s_part[0][f0][j] + s_part[1][f0][j]) + (s_part[2][f0][j] + s_part[3][f0][j]);
-                if (q < 2) {
-                    r.y = (s_part[0][f0 + 1][j] + s_part[1][f0 + 1][j]) + (s_part[2][f0 + 1][j] + s_part[3][f0 + 1][j]);
-                    r.z = (s_part[0][f0 + 2][j] + s_part[1][f0 + 2][j]) + (s_part[2][f0 + 2][j] + s_part[3][f0 + 2][j]);
-                    r.w = (s_part[0][f0 + 3][j] + s_part[1][f0 + 3][j]) + (s_part[2][f0 + 3][j] + s_part[3][f0 + 3][j]);
-                } else {
-                    r.y = r.z = r.w = 0.f;
-                }
-                a.records[3 * ((size_t)range.x + lo + j) + q] = r;
-            }
-        }
+        if (a.diag) c_replay += __builtin_amdgcn_s_memtime() - c0;
         __syncthreads();
     }
-    if (a.diag) {
-        __shared__ uint32_t s_kept[4];
-        if (lane == 0) s_kept[w] = diag_kept;
-        __syncthreads();
-        if (tid == 0) {
-            uint64_t* d = a.diag + 4 * (size_t)tile;
-            d[0] = t_start;
-            d[1] = __builtin_amdgcn_s_memrealtime();
-            d[2] = (uint64_t)s_kept[0] + s_kept[1] + s_kept[2] + s_kept[3];
-            d[3] = diag_rounds;
-        }
+    if (a.diag && lane == 0) {
+        uint64_t* d = a.diag + kDiagWords * (size_t)blockIdx.x;
+        d[0] = t_start;
+        d[1] = __builtin_amdgcn_s_memrealtime();
+        d[2] = diag_kept;
+        d[3] = diag_rounds;
+        d[4] = c_replay;
+        d[5] = __builtin_amdgcn_s_memtime() - c_start;
     }
 }
 
 void launch_render_backward(const RenderBwdArgs& a, hipStream_t s) {
     const int tiles = a.gx * a.gy;
     if (tiles <= 0) return;
-    hipLaunchKernelGGL(k_render_bwd, dim3(tiles), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_render_bwd, dim3(tiles * 4), dim3(64), 0, s, a);
 }
 
 }  // namespace gs

@@ -182,9 +182,10 @@ int gs_profile_num_stages(void);
 const char *gs_profile_stage_name(int i);
 int gs_profile_collect(double *total_ms, int *counts, int n);
 
-/* Blend-kernel diagnostics: when enabled, the forward blend records per wave
- * (and the backward per tile) {start, end (s_memrealtime, 100 MHz), kept
- * entries, rounds}; gs_profile_diag_read copies the last launch's records
+/* Blend-kernel diagnostics: when enabled, the forward blend and the backward
+ * replay record per wave (8 u64) {start, end (s_memrealtime, 100 MHz), kept
+ * entries, rounds, cycles inside the blend/replay loops, total cycles
+ * (s_memtime), 0, 0}; gs_profile_diag_read copies the last launch's records
  * (which: 0 forward, 1 backward) to host memory and returns the u64 count. */
 int gs_profile_diag_enable(int on);
 long long gs_profile_diag_read(int which, uint64_t *host, long long max_u64);

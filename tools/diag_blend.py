@@ -18,30 +18,32 @@ from dge_amd.gaussian_renderer import PipelineParams, render  # noqa: E402
 from dge_amd.scene import synthetic_scene  # noqa: E402
 
 
-def summarize(name, d):
+def summarize(name, d, per_tile=False):
     if d.size == 0:
         print(name, "no data")
         return
-    start, end = d[:, 0].astype(np.int64), d[:, 1].astype(np.int64)
-    live = end > 0
-    start, end, kept, rounds = start[live], end[live], d[live, 2].astype(np.int64), d[live, 3].astype(np.int64)
+    d = d.astype(np.int64)
+    start, end, kept, rounds, cyc_loop, cyc_total = (d[:, i] for i in range(6))
     t0 = start.min()
     dur = (end - start) * 10e-3  # us (100 MHz)
     span = (end.max() - t0) * 10e-3
-    print(f"== {name}: {live.sum()} items, span {span:.1f} us, start spread {(start.max() - t0) * 10e-3:.1f} us")
-    for q in (50, 90, 99, 99.9, 100):
-        print(f"   dur p{q}: {np.percentile(dur, q):.2f} us")
-    print(f"   kept mean {kept.mean():.1f} max {kept.max()}  rounds mean {rounds.mean():.2f} max {rounds.max()}")
-    if kept.std() > 0:
-        A = np.stack([kept, rounds, np.ones_like(kept)], 1).astype(np.float64)
-        coef, *_ = np.linalg.lstsq(A, dur, rcond=None)
-        print(f"   fit dur ~ {coef[0] * 1e3:.2f} ns/kept + {coef[1]:.3f} us/round + {coef[2]:.2f} us")
-    order = np.argsort(-dur)[:5]
+    clk = cyc_total.sum() / max(1, (end - start).sum()) / 10e-3 / 1e3  # GHz
+    print(f"== {name}: {len(d)} waves, span {span:.1f} us, start spread {(start.max() - t0) * 10e-3:.1f} us, "
+          f"shader clock ~{clk:.2f} GHz")
+    for q in (50, 90, 99, 100):
+        print(f"   wave dur p{q}: {np.percentile(dur, q):.2f} us")
+    print(f"   kept/wave mean {kept.mean():.1f} max {kept.max()}  rounds mean {rounds.mean():.2f} max {rounds.max()}")
+    print(f"   loop share of cycles {cyc_loop.sum() / max(1, cyc_total.sum()):.3f}; "
+          f"loop cycles per kept entry (all) {cyc_loop.sum() / max(1, kept.sum()):.0f}")
+    order = np.argsort(-dur)[:6]
     for i in order:
-        print(f"   slowest: item {i} dur {dur[i]:.1f} kept {kept[i]} rounds {rounds[i]} start {(start[i] - t0) * 10e-3:.1f}")
+        extra = f" tile {i // 4} wave {i % 4} tile-kept {kept[4 * (i // 4):4 * (i // 4) + 4].tolist()}" if per_tile else ""
+        print(f"   slowest: wave {i} dur {dur[i]:.1f} us kept {kept[i]} rounds {rounds[i]} loop cyc/kept "
+              f"{cyc_loop[i] / max(1, kept[i]):.0f} loop share {cyc_loop[i] / max(1, cyc_total[i]):.2f} "
+              f"start {(start[i] - t0) * 10e-3:.1f}{extra}")
     ts = np.linspace(0, span, 11)
     alive = [int(((start - t0) * 10e-3 <= t).sum() - ((end - t0) * 10e-3 <= t).sum()) for t in ts]
-    print("   running over time:", " ".join(f"{t:.0f}:{a}" for t, a in zip(ts, alive)))
+    print("   waves running over time:", " ".join(f"{t:.0f}:{a}" for t, a in zip(ts, alive)))
 
 
 def main():
@@ -59,8 +61,8 @@ def main():
     render(cam, scene, PipelineParams(), bg)["render"].backward(g)
     torch.cuda.synchronize()
     _native.diag_enable(False)
-    summarize("render_fwd (per wave)", _native.diag_read(0))
-    summarize("render_bwd (per tile)", _native.diag_read(1))
+    summarize("render_fwd", _native.diag_read(0))
+    summarize("render_bwd", _native.diag_read(1), per_tile=True)
 
 
 if __name__ == "__main__":
