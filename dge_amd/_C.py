@@ -253,9 +253,13 @@ def rasterize_gaussians_fused(background, xyz, f_dc, f_rest, colors, raw_opacity
 def rasterize_gaussians_fused_backward(background, xyz, f_dc, f_rest, colors, raw_opacity, raw_scaling, raw_rotation,
                                        radii, scale_modifier, viewmatrix, projmatrix, tan_fovx, tan_fovy,
                                        dL_dout_color, degree, campos, geomBuffer, R, binningBuffer, imageBuffer,
-                                       debug):
+                                       debug, into=None):
     """-> (dL_dmeans2D [P,3], dL_dxyz, dL_dfeatures_dc, dL_dfeatures_rest, dL_dcolors, dL_dopacity_raw,
-    dL_dscaling_raw, dL_drotation_raw), gradients w.r.t. the raw tensors."""
+    dL_dscaling_raw, dL_drotation_raw), gradients w.r.t. the raw tensors.
+
+    into: optional {"xyz"|"sh"|"opacity"|"scaling"|"rotation": (dest, accumulate)} — write that gradient
+    into `dest` (for "sh" a (dc, rest) pair), adding to its contents when accumulate is true (the kernel's
+    fused gradient accumulation, gs_grads.accumulate); the returned tuple then holds `dest`."""
     N.require_gpu(xyz)
     dev = xyz.device
     P = xyz.size(0)
@@ -263,14 +267,30 @@ def rasterize_gaussians_fused_backward(background, xyz, f_dc, f_rest, colors, ra
     with torch.cuda.device(dev):
         opts = dict(dtype=torch.float32, device=dev)
         have_sh = f_dc is not None and f_dc.numel() != 0
+        into = into or {}
+        acc_bits = 0
+
+        def dest(name, make, bit):
+            nonlocal acc_bits
+            if name in into:
+                t, acc = into[name]
+                if acc:
+                    acc_bits |= bit
+                return t
+            return make()
+
         d_m2 = torch.empty((P, 3), **opts)
-        d_xyz = torch.empty((P, 3), **opts)
-        d_dc = torch.empty_like(f_dc, **opts) if have_sh else None
-        d_rest = torch.empty_like(f_rest, **opts) if have_sh and f_rest is not None else None
+        d_xyz = dest("xyz", lambda: torch.empty((P, 3), **opts), N.ACC_MEANS3D)
+        if have_sh and "sh" in into:
+            (d_dc, d_rest), acc = into["sh"]
+            acc_bits |= N.ACC_SH if acc else 0
+        else:
+            d_dc = torch.empty_like(f_dc, **opts) if have_sh else None
+            d_rest = torch.empty_like(f_rest, **opts) if have_sh and f_rest is not None else None
         d_col = torch.empty((P, 3), **opts)
-        d_op = torch.empty_like(raw_opacity, **opts)
-        d_sc = torch.empty((P, 3), **opts)
-        d_rot = torch.empty((P, 4), **opts)
+        d_op = dest("opacity", lambda: torch.empty_like(raw_opacity, **opts), N.ACC_OPACITY)
+        d_sc = dest("scaling", lambda: torch.empty((P, 3), **opts), N.ACC_SCALES)
+        d_rot = dest("rotation", lambda: torch.empty((P, 4), **opts), N.ACC_ROTATIONS)
         out = (d_m2, d_xyz, d_dc, d_rest, d_col, d_op, d_sc, d_rot)
         if P == 0:
             return out
@@ -287,6 +307,7 @@ def rasterize_gaussians_fused_backward(background, xyz, f_dc, f_rest, colors, ra
         o.dsh_dc_stride = 3
         o.dsh_rest_stride = 3 * (d_rest.size(1) if d_rest is not None else 0)
         o.dL_dscales, o.dL_drotations = _ptr(d_sc), _ptr(d_rot)
+        o.accumulate = acc_bits
         grad = _f32(dL_dout_color, "dL_dout_color")
         s, keep = _settings(background, viewmatrix, projmatrix, campos, tan_fovx, tan_fovy, H, W, degree,
                             scale_modifier, False, debug)

@@ -63,6 +63,11 @@ class GsParams(ctypes.Structure):
     ]
 
 
+# gs_grads.accumulate bits (include/gs_raster.h)
+ACC_MEANS2D, ACC_COLORS, ACC_OPACITY, ACC_MEANS3D, ACC_COV3D, ACC_SH = 1, 2, 4, 8, 16, 32
+ACC_SCALES, ACC_ROTATIONS = 128, 256
+
+
 class GsGrads(ctypes.Structure):
     """struct gs_grads (include/gs_raster.h)."""
 
@@ -78,6 +83,7 @@ class GsGrads(ctypes.Structure):
         ("dsh_rest_stride", ctypes.c_int),
         ("dL_dscales", _fp),
         ("dL_drotations", _fp),
+        ("accumulate", ctypes.c_uint),
     ]
 
 

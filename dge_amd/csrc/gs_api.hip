@@ -436,6 +436,7 @@ long long gs_buffer_offset(const char* buffer, const char* field, int P, int wid
         if (!strcmp(field, "slot_gauss")) return (long long)L.slot_gauss;
         if (!strcmp(field, "slot_to_pos")) return (long long)L.slot_to_pos;
         if (!strcmp(field, "records")) return (long long)L.records;
+        if (!strcmp(field, "rec_flags")) return (long long)L.rec_flags;
     }
     return -1;
 }
@@ -513,6 +514,7 @@ int gs_rasterize_backward(const gs_settings* s, int P, int M, int R, const float
     o.dL_dsh_rest = o.dL_dsh_dc ? dL_dsh + 3 : nullptr;
     o.dsh_dc_stride = o.dsh_rest_stride = 3 * M;
     o.dL_dscales = dL_dscales; o.dL_drotations = dL_drotations;
+    o.accumulate = 0;
     gs_params g2 = g;
     g2.M = M;  // dL_dsh is [P,M,3] even when shs is absent (then all zero)
     return gs_rasterize_backward_ex(s, &g2, R, radii, geom, binning, img, dL_dpix, &o, stream);
@@ -549,12 +551,16 @@ int gs_rasterize_backward_ex(const gs_settings* s, const gs_params* gp, int R, c
         const ImgLayout il = img_layout(g.W, g.H);
         const BinLayout bl = bin_layout(R, g.tiles);
         float4* records = R > 0 ? at<float4>(const_cast<void*>(binning), bl.records) : nullptr;
+        uint8_t* rec_flags = R > 0 ? at<uint8_t>(const_cast<void*>(binning), bl.rec_flags) : nullptr;
         if (R > 0) {
+            GS_HIP(hipMemsetAsync(rec_flags, 0, 4 * (size_t)R, stream));
+            const TileSortPlan plan = tile_sort_plan(g.tiles);  // the sort's values end in val1 after an odd pass count
             RenderBwdArgs rb;
             rb.W = g.W; rb.H = g.H; rb.gx = g.gx; rb.gy = g.gy;
             rb.ranges = at<uint2>(img, il.ranges);
             rb.point_list = at<uint32_t>(binning, bl.point_list);
             rb.quad_last = at<uint32_t>(img, il.quad_last);
+            rb.pos_slot = at<uint32_t>(binning, (plan.passes & 1) ? bl.val1 : bl.val0);
             rb.means2D = at<float2>(geom, gl.means2D);
             rb.conic_opacity = at<float4>(geom, gl.conic_opacity);
             rb.rgbd = at<float4>(geom, gl.rgbd);
@@ -563,6 +569,7 @@ int gs_rasterize_backward_ex(const gs_settings* s, const gs_params* gp, int R, c
             rb.n_contrib = at<uint32_t>(img, il.n_contrib);
             rb.dL_dpix = dL_dpix;
             rb.records = records;
+            rb.rec_flags = rec_flags;
             rb.diag = diag_buffer(1, kDiagWords * (size_t)g.tiles * 4);
             { StageScope sc(ST_RENDER_BWD, stream); launch_render_backward(rb, stream); }
             GS_LAUNCHED("render backward");
@@ -581,20 +588,15 @@ int gs_rasterize_backward_ex(const gs_settings* s, const gs_params* gp, int R, c
         ga.tanfovx = s->tanfovx; ga.tanfovy = s->tanfovy; ga.fx = g.fx; ga.fy = g.fy;
         ga.scale_modifier = s->scale_modifier;
         ga.radii = radii;
-        ga.geom_radii = at<int>(geom, gl.radii);
-        ga.means2D = at<float2>(geom, gl.means2D);
-        ga.conic_opacity = at<float4>(geom, gl.conic_opacity);
         ga.tiles_touched = at<uint32_t>(geom, gl.tiles_touched);
         ga.first_slot = at<uint32_t>(geom, gl.first_slot);
         ga.clamped = at<uint8_t>(geom, gl.clamped);
-        ga.slot_to_pos = R > 0 ? at<uint32_t>(binning, bl.slot_to_pos) : nullptr;
-        ga.ranges = at<uint2>(img, il.ranges);
-        ga.tile_last = at<uint32_t>(img, il.tile_last);
-        ga.quad_last = at<uint32_t>(img, il.quad_last);
+        ga.rec_flags = rec_flags;
         ga.records = records;
         ga.dL_dmeans2D = o->dL_dmeans2D; ga.dL_dcolors = o->dL_dcolors; ga.dL_dopacity = o->dL_dopacity;
         ga.dL_dmeans3D = o->dL_dmeans3D; ga.dL_dcov3D = o->dL_dcov3D;
         ga.dL_dscales = o->dL_dscales; ga.dL_drot = o->dL_drotations;
+        ga.acc = o->accumulate;
         { StageScope sc(ST_GAUSS_BWD, stream); launch_gauss_backward(ga, stream); }
         GS_LAUNCHED("gaussian backward");
         return GS_OK;

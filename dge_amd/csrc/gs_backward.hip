@@ -20,32 +20,31 @@
 #pragma clang fp contract(off)
 #include "gs_common.h"
 #include "gs_internal.h"
+#include "gs_raster.h"  // GS_ACC_*
 
 namespace gs {
 
-// backward.cu:20-139 — writes dL_dsh for the (deg+1)^2 used coefficients and
-// returns the mean gradient through the normalised view direction.
-// c0/r: SH coefficient 0 / 1.. of this Gaussian; d0/dr: the same for dL_dsh.
-__device__ __forceinline__ f3 sh_backward(int deg, f3 pos, f3 campos, const float* __restrict__ c0,
-                                          const float* __restrict__ r, uint8_t clamp_bits, f3 dL_dcolor,
-                                          float* __restrict__ d0, float* __restrict__ dr) {
+// backward.cu:20-139 — dL_dsh of the (deg+1)^2 used coefficients into
+// dsh[3*k..3*k+2] (registers; unused ones untouched) and the mean gradient
+// through the normalised view direction as the return value.
+// r: SH coefficients 1.. of this Gaussian (coefficient 0 has no direction term).
+__device__ __forceinline__ f3 sh_backward(int deg, f3 pos, f3 campos, const float* __restrict__ r,
+                                          uint8_t clamp_bits, f3 dL_dcolor, float (&dsh)[48]) {
     const f3 dir_orig = pos - campos;
     const float len = sqrtf(dot3(dir_orig, dir_orig));
     const f3 dir = mk3(dir_orig.x / len, dir_orig.y / len, dir_orig.z / len);
     const f3 g = mk3(dL_dcolor.x * ((clamp_bits & 1) ? 0.f : 1.f), dL_dcolor.y * ((clamp_bits & 2) ? 0.f : 1.f),
                      dL_dcolor.z * ((clamp_bits & 4) ? 0.f : 1.f));
     auto put = [&](int k, f3 v) {
-        float* o = k == 0 ? d0 : dr + 3 * (k - 1);
-        o[0] = v.x;
-        o[1] = v.y;
-        o[2] = v.z;
+        dsh[3 * k] = v.x;
+        dsh[3 * k + 1] = v.y;
+        dsh[3 * k + 2] = v.z;
     };
     // coefficient k >= 1 of the input
 #define SHK(k) ld3(r + 3 * ((k) - 1))
     f3 dx = mk3(0, 0, 0), dy = mk3(0, 0, 0), dz = mk3(0, 0, 0);
     const float x = dir.x, y = dir.y, z = dir.z;
     put(0, g * kSH_C0);
-    (void)c0;
     if (deg > 0) {
         put(1, g * (-kSH_C1 * y));
         put(2, g * (kSH_C1 * z));
@@ -136,80 +135,55 @@ __device__ __forceinline__ void cov3d_backward(f3 scale, float mod, float4 q, co
     drot[3] = 2 * r * (D[0][1] - D[1][0]) + 2 * x * (D[2][0] + D[0][2]) + 2 * y * (D[1][2] + D[2][1]) - 4 * z * (D[1][1] + D[0][0]);
 }
 
-__global__ __launch_bounds__(256) void k_gauss_bwd(GaussBwdArgs a) {
-    const int idx = blockIdx.x * 256 + threadIdx.x;
-    if (idx >= a.P) return;
-    const bool vis = a.radii[idx] > 0;
-    float acc[9];
-#pragma unroll
-    for (int f = 0; f < 9; ++f) acc[f] = 0.f;
-    const uint32_t n = vis ? a.tiles_touched[idx] : 0u;
-    if (n) {
-        const uint32_t first = a.first_slot[idx];
-        const float2 xy = a.means2D[idx];
-        // geometry radii (consistent with tiles_touched/first_slot): emission order is row-major over the rect
-        const int gr = a.geom_radii[idx];
-        const Rect q = tile_rect(xy.x, xy.y, gr, a.gx, a.gy);
-        const int wd = q.x1 - q.x0;
-        const float4 co = a.conic_opacity[idx];
-        for (uint32_t k = 0; k < n; ++k) {
-            const int ty = q.y0 + (int)k / wd, tx = q.x0 + (int)k % wd;
-            const int t = ty * a.gx + tx;
-            const uint32_t pos = a.slot_to_pos[first + k];
-            const uint32_t lpos = pos - a.ranges[t].x;
-            if (lpos >= a.tile_last[t]) continue;  // behind every pixel's last contributor
-            // the quadrant waves that replayed this entry wrote a record at 4*pos+quad
-#pragma unroll
-            for (int qd = 0; qd < 4; ++qd) {
-                if (lpos < a.quad_last[4 * t + qd] &&
-                    cull_keep(xy, co, (float)(tx * kTile + (qd & 1) * kQuad), (float)(ty * kTile + (qd >> 1) * kQuad))) {
-                    const float4* rec = a.records + 3 * (4 * (size_t)pos + qd);
-                    const float4 r0 = rec[0], r1 = rec[1], r2 = rec[2];
-                    acc[0] += r0.x; acc[1] += r0.y; acc[2] += r0.z; acc[3] += r0.w;
-                    acc[4] += r1.x; acc[5] += r1.y; acc[6] += r1.z; acc[7] += r1.w;
-                    acc[8] += r2.x;
-                }
-            }
-        }
-    }
-    a.dL_dmeans2D[3 * (size_t)idx] = acc[0];
-    a.dL_dmeans2D[3 * (size_t)idx + 1] = acc[1];
-    a.dL_dmeans2D[3 * (size_t)idx + 2] = 0.f;
-    a.dL_dopacity[idx] = acc[5];
-    a.dL_dcolors[3 * (size_t)idx] = acc[6];
-    a.dL_dcolors[3 * (size_t)idx + 1] = acc[7];
-    a.dL_dcolors[3 * (size_t)idx + 2] = acc[8];
+constexpr int kGB = 256;  // Gaussians per block
 
-    float* d0 = a.dsh.dc ? a.dsh.dc + (size_t)idx * a.dsh.dc_stride : nullptr;
-    float* dr = a.dsh.dc ? a.dsh.rest + (size_t)idx * a.dsh.rest_stride : nullptr;
-    if (!vis) {
-        if (a.activation) a.dL_dopacity[idx] = 0.f;  // d sigmoid of a zero gradient
-#pragma unroll
-        for (int k = 0; k < 3; ++k) { a.dL_dmeans3D[3 * (size_t)idx + k] = 0.f; a.dL_dscales[3 * (size_t)idx + k] = 0.f; }
-        if (a.dL_dcov3D)
-#pragma unroll
-            for (int k = 0; k < 6; ++k) a.dL_dcov3D[6 * (size_t)idx + k] = 0.f;
-        *reinterpret_cast<float4*>(a.dL_drot + 4 * (size_t)idx) = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (d0) {
-            d0[0] = d0[1] = d0[2] = 0.f;
-            for (int k = 0; k < (a.M - 1) * 3; ++k) dr[k] = 0.f;
-        }
-        return;
-    }
+// Per-Gaussian inputs, loaded at kernel entry so their latency overlaps the
+// SH staging and the record sums.
+struct GaussIn {
+    f3 m;
+    f3 scale;
+    float4 rot;
+    float cov[6];
+    float opacity;
+    uint8_t clamped;
+};
 
+__device__ __forceinline__ GaussIn load_gauss_in(const GaussBwdArgs& a, int idx) {
+    GaussIn g;
+    g.m = ld3(a.means3D + 3 * (size_t)idx);
+    g.scale = mk3(0, 0, 0);
+    g.rot = make_float4(0, 0, 0, 0);
+#pragma unroll
+    for (int k = 0; k < 6; ++k) g.cov[k] = 0.f;
+    if (a.cov3D_precomp) {
+#pragma unroll
+        for (int k = 0; k < 6; ++k) g.cov[k] = a.cov3D_precomp[6 * (size_t)idx + k];
+    } else {
+        g.scale = ld3(a.scales + 3 * (size_t)idx);
+        g.rot = *reinterpret_cast<const float4*>(a.rotations + 4 * (size_t)idx);
+    }
+    g.opacity = a.activation ? a.opacities[idx] : 0.f;
+    g.clamped = a.clamped[idx];
+    return g;
+}
+
+// The per-Gaussian chain of a visible Gaussian (geometry gradients written
+// here; SH gradients returned in dsh).
+__device__ __forceinline__ void gauss_bwd_visible(const GaussBwdArgs& a, int idx, const GaussIn& gin, const float (&acc)[9], float& dop,
+                                                  const float* my_sh, float (&dsh)[48]) {
     const float* v = a.view;
     const float* pm = a.proj;
-    const f3 m = ld3(a.means3D + 3 * (size_t)idx);
+    const f3 m = gin.m;
     float cov3[6];
     f3 scale = mk3(0, 0, 0);
     float4 rot = make_float4(0, 0, 0, 0), rot_raw = rot;
     float rot_len = 0.f;
     if (a.cov3D_precomp) {
 #pragma unroll
-        for (int k = 0; k < 6; ++k) cov3[k] = a.cov3D_precomp[6 * (size_t)idx + k];
+        for (int k = 0; k < 6; ++k) cov3[k] = gin.cov[k];
     } else {
-        scale = ld3(a.scales + 3 * (size_t)idx);
-        rot = *reinterpret_cast<const float4*>(a.rotations + 4 * (size_t)idx);
+        scale = gin.scale;
+        rot = gin.rot;
         if (a.activation) {
             rot_raw = rot;
             rot = act_normalize(rot_raw, rot_len);
@@ -279,25 +253,18 @@ __global__ __launch_bounds__(256) void k_gauss_bwd(GaussBwdArgs a) {
         dmean = dmean + d2;
     }
     // ---- SH -> RGB backward ----
-    if (a.sh.dc) {
-        const int used = a.D >= 3 ? 16 : (a.D + 1) * (a.D + 1);
-        dmean = dmean + sh_backward(a.D, m, ld3(a.campos), a.sh.dc + (size_t)idx * a.sh.dc_stride,
-                                    a.sh.rest + (size_t)idx * a.sh.rest_stride, a.clamped[idx],
-                                    mk3(acc[6], acc[7], acc[8]), d0, dr);
-        for (int k = (used - 1) * 3; k < (a.M - 1) * 3; ++k) dr[k] = 0.f;
-    } else if (d0) {
-        d0[0] = d0[1] = d0[2] = 0.f;
-        for (int k = 0; k < (a.M - 1) * 3; ++k) dr[k] = 0.f;
-    }
-    a.dL_dmeans3D[3 * (size_t)idx] = dmean.x;
-    a.dL_dmeans3D[3 * (size_t)idx + 1] = dmean.y;
-    a.dL_dmeans3D[3 * (size_t)idx + 2] = dmean.z;
+    if (a.sh.dc)
+        dmean = dmean + sh_backward(a.D, m, ld3(a.campos), my_sh, gin.clamped, mk3(acc[6], acc[7], acc[8]), dsh);
+    const bool am = a.acc & GS_ACC_MEANS3D;
+    put_out(a.dL_dmeans3D, 3 * (size_t)idx, dmean.x, am);
+    put_out(a.dL_dmeans3D, 3 * (size_t)idx + 1, dmean.y, am);
+    put_out(a.dL_dmeans3D, 3 * (size_t)idx + 2, dmean.z, am);
     if (a.dL_dcov3D)
 #pragma unroll
-        for (int k = 0; k < 6; ++k) a.dL_dcov3D[6 * (size_t)idx + k] = dcov[k];
+        for (int k = 0; k < 6; ++k) put_out(a.dL_dcov3D, 6 * (size_t)idx + k, dcov[k], a.acc & GS_ACC_COV3D);
     if (a.activation) {  // opacity = sigmoid(raw): torch's sigmoid backward g * (1 - y) * y
-        const float y = act_sigmoid(a.opacities[idx]);
-        a.dL_dopacity[idx] = acc[5] * ((1.0f - y) * y);
+        const float y = act_sigmoid(gin.opacity);
+        dop = acc[5] * ((1.0f - y) * y);
     }
     // ---- scale / rotation ----
     if (a.scales) {
@@ -310,20 +277,130 @@ __global__ __launch_bounds__(256) void k_gauss_bwd(GaussBwdArgs a) {
             ds[2] *= scale.z;
             g4 = act_normalize_bwd(rot, rot_len, g4);
         }
-        a.dL_dscales[3 * (size_t)idx] = ds[0];
-        a.dL_dscales[3 * (size_t)idx + 1] = ds[1];
-        a.dL_dscales[3 * (size_t)idx + 2] = ds[2];
-        *reinterpret_cast<float4*>(a.dL_drot + 4 * (size_t)idx) = g4;
+        const bool as = a.acc & GS_ACC_SCALES;
+        put_out(a.dL_dscales, 3 * (size_t)idx, ds[0], as);
+        put_out(a.dL_dscales, 3 * (size_t)idx + 1, ds[1], as);
+        put_out(a.dL_dscales, 3 * (size_t)idx + 2, ds[2], as);
+        float4* r4 = reinterpret_cast<float4*>(a.dL_drot + 4 * (size_t)idx);
+        if (a.acc & GS_ACC_ROTATIONS) {
+            const float4 o4 = *r4;
+            g4 = make_float4(o4.x + g4.x, o4.y + g4.y, o4.z + g4.z, o4.w + g4.w);
+        }
+        *r4 = g4;
     } else {
+        if (!(a.acc & GS_ACC_SCALES))
 #pragma unroll
-        for (int k = 0; k < 3; ++k) a.dL_dscales[3 * (size_t)idx + k] = 0.f;
-        *reinterpret_cast<float4*>(a.dL_drot + 4 * (size_t)idx) = make_float4(0.f, 0.f, 0.f, 0.f);
+            for (int k = 0; k < 3; ++k) a.dL_dscales[3 * (size_t)idx + k] = 0.f;
+        if (!(a.acc & GS_ACC_ROTATIONS))
+            *reinterpret_cast<float4*>(a.dL_drot + 4 * (size_t)idx) = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+}
+
+__global__ __launch_bounds__(kGB) void k_gauss_bwd(GaussBwdArgs a) {
+    __shared__ float s_sh[kGB * kShPitch];
+    const int idx0 = blockIdx.x * kGB;
+    const int idx = idx0 + threadIdx.x;
+    const int nrow = a.P - idx0 < kGB ? a.P - idx0 : kGB;
+    const bool in = idx < a.P;
+    const bool vis = in && a.radii[idx] > 0;
+    // rest floats staged per Gaussian: coefficients 1..15 (degree <= 3 never reads more)
+    const int ncol = (a.M - 1) * 3 < kShPitch ? (a.M - 1) * 3 : kShPitch;
+    float* const my_sh = s_sh + threadIdx.x * kShPitch;
+    GaussIn gin{};
+    if (vis) gin = load_gauss_in(a, idx);
+
+    // SH coefficients 1.. of the block, staged with coalesced loads
+    if (a.sh.dc && ncol > 0)
+        sh_rows_load<kGB>(a.sh.rest + (size_t)idx0 * a.sh.rest_stride, a.sh.rest_stride, s_sh, nrow, ncol);
+
+    // sum of this Gaussian's records: one per (slot, quadrant) the backward
+    // replay kept, flagged per slot; slots in emission order = tile order
+    float acc[9];
+#pragma unroll
+    for (int f = 0; f < 9; ++f) acc[f] = 0.f;
+    const uint32_t n = vis ? a.tiles_touched[idx] : 0u;
+    if (n) {
+        const uint32_t first = a.first_slot[idx];
+        const uint32_t* flags = reinterpret_cast<const uint32_t*>(a.rec_flags);
+        for (uint32_t k0 = 0; k0 < n; k0 += 8) {
+            uint32_t fl[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) fl[u] = k0 + u < n ? flags[first + k0 + u] : 0u;
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+#pragma unroll
+                for (int qd = 0; qd < 4; ++qd) {
+                    if ((fl[u] >> (8 * qd)) & 0xFFu) {
+                        const float4* rec = a.records + 3 * (4 * (size_t)(first + k0 + u) + qd);
+                        const float4 r0 = rec[0], r1 = rec[1], r2 = rec[2];
+                        acc[0] += r0.x; acc[1] += r0.y; acc[2] += r0.z; acc[3] += r0.w;
+                        acc[4] += r1.x; acc[5] += r1.y; acc[6] += r1.z; acc[7] += r1.w;
+                        acc[8] += r2.x;
+                    }
+                }
+            }
+        }
+    }
+    __syncthreads();  // SH staged
+
+    float dsh[48];
+#pragma unroll
+    for (int k = 0; k < 48; ++k) dsh[k] = 0.f;
+    float dop = acc[5];  // w.r.t. opacity; chained through the sigmoid below when activation = 1
+    if (in && !vis) {
+        if (a.activation) dop = 0.f;  // d sigmoid of a zero gradient
+        if (!(a.acc & GS_ACC_MEANS3D))
+#pragma unroll
+            for (int k = 0; k < 3; ++k) a.dL_dmeans3D[3 * (size_t)idx + k] = 0.f;
+        if (!(a.acc & GS_ACC_SCALES))
+#pragma unroll
+            for (int k = 0; k < 3; ++k) a.dL_dscales[3 * (size_t)idx + k] = 0.f;
+        if (a.dL_dcov3D && !(a.acc & GS_ACC_COV3D))
+#pragma unroll
+            for (int k = 0; k < 6; ++k) a.dL_dcov3D[6 * (size_t)idx + k] = 0.f;
+        if (!(a.acc & GS_ACC_ROTATIONS))
+            *reinterpret_cast<float4*>(a.dL_drot + 4 * (size_t)idx) = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    if (vis) gauss_bwd_visible(a, idx, gin, acc, dop, my_sh, dsh);
+    if (in) {
+        const bool a2 = a.acc & GS_ACC_MEANS2D, ac = a.acc & GS_ACC_COLORS;
+        put_out(a.dL_dmeans2D, 3 * (size_t)idx, acc[0], a2);
+        put_out(a.dL_dmeans2D, 3 * (size_t)idx + 1, acc[1], a2);
+        put_out(a.dL_dmeans2D, 3 * (size_t)idx + 2, 0.f, a2);
+        put_out(a.dL_dopacity, idx, dop, a.acc & GS_ACC_OPACITY);
+        put_out(a.dL_dcolors, 3 * (size_t)idx, acc[6], ac);
+        put_out(a.dL_dcolors, 3 * (size_t)idx + 1, acc[7], ac);
+        put_out(a.dL_dcolors, 3 * (size_t)idx + 2, acc[8], ac);
+    }
+
+    // dL_dsh: coefficient 0 per thread, 1.. through LDS (in place) with coalesced stores
+    if (a.dsh.dc) {
+        if (in) {
+            float* d0 = a.dsh.dc + (size_t)idx * a.dsh.dc_stride;
+            const bool ash = a.acc & GS_ACC_SH;
+            put_out(d0, 0, dsh[0], ash);
+            put_out(d0, 1, dsh[1], ash);
+            put_out(d0, 2, dsh[2], ash);
+            // coefficients beyond the 16 a degree-3 evaluation uses get zero gradient
+            float* dr = a.dsh.rest + (size_t)idx * a.dsh.rest_stride;
+            if (!ash)
+                for (int k = kShPitch; k < (a.M - 1) * 3; ++k) dr[k] = 0.f;
+        }
+        if (ncol > 0) {
+            __syncthreads();  // every row read before any row is overwritten
+#pragma unroll
+            for (int k = 0; k < 45; ++k)
+                if (k < ncol) my_sh[k] = dsh[3 + k];
+            __syncthreads();
+            sh_rows_store<kGB>(a.dsh.rest + (size_t)idx0 * a.dsh.rest_stride, a.dsh.rest_stride, s_sh, nrow, ncol,
+                          a.acc & GS_ACC_SH);
+        }
     }
 }
 
 void launch_gauss_backward(const GaussBwdArgs& a, hipStream_t s) {
     if (a.P <= 0) return;
-    hipLaunchKernelGGL(k_gauss_bwd, dim3(div_up(a.P, 256)), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_gauss_bwd, dim3(div_up(a.P, kGB)), dim3(kGB), 0, s, a);
 }
 
 }  // namespace gs

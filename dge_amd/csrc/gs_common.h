@@ -218,6 +218,116 @@ __device__ __forceinline__ bool cull_keep(float2 xy, float4 co, float bx0, float
     return keep;
 }
 
+// =====================================================================
+// SH coefficient rows staged through LDS (k_preprocess, k_gauss_bwd):
+// coalesced block-wide global transfers instead of 45 strided dword
+// accesses per lane.  NT = threads (= Gaussians) per block.
+// =====================================================================
+// Output store: out = v, or out += v when the output's GS_ACC_* bit is set
+// (fused gradient accumulation into an existing .grad buffer).
+__device__ __forceinline__ void put_out(float* p, size_t i, float v, bool acc) { p[i] = acc ? p[i] + v : v; }
+
+constexpr int kShPitch = 45;  // LDS floats per Gaussian row: (16-1)*3, odd -> conflict-free row access
+
+// Coalesced block transfer of the SH "rest" rows of Gaussians [idx0, idx0+nrow)
+// between global rows of `stride` floats and LDS rows of kShPitch floats;
+// only the first ncol floats of each row are moved (the tail of an
+// interleaved [P,16,3] row is the next Gaussian's DC term: never touched).
+// When the block's region is 16-B aligned (contiguous [P,15,3] parameters)
+// the global side moves float4s; every load of a thread is issued before
+// its first LDS store, so ~12 x 16 B per lane are in flight at once.
+__device__ __forceinline__ void sh_element_to_lds(float* __restrict__ lds, int e, float v, float inv, int stride,
+                                                  int ncol) {
+    const int row = (int)(((float)e + 0.5f) * inv);  // exact: e < 2^16, margin 0.5/stride
+    const int col = e - row * stride;
+    if (col < ncol) lds[row * kShPitch + col] = v;
+}
+
+template <int NT>
+__device__ __forceinline__ void sh_rows_load(const float* __restrict__ g, int stride, float* __restrict__ lds,
+                                             int nrow, int ncol) {
+    const int total = (nrow - 1) * stride + ncol;
+    const float inv = 1.0f / (float)stride;
+    if ((reinterpret_cast<uintptr_t>(g) & 15) == 0) {
+        constexpr int kV = 12;  // float4 per lane per batch: 256 x 45 floats = 2880 float4
+        const float4* g4 = reinterpret_cast<const float4*>(g);
+        const int n4 = total >> 2;
+        for (int b = 0; b < n4; b += kV * NT) {
+            float4 v[kV];
+#pragma unroll
+            for (int u = 0; u < kV; ++u) {
+                const int i = b + u * NT + (int)threadIdx.x;
+                v[u] = i < n4 ? g4[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+#pragma unroll
+            for (int u = 0; u < kV; ++u) {
+                const int i = b + u * NT + (int)threadIdx.x;
+                if (i < n4) {
+                    sh_element_to_lds(lds, 4 * i, v[u].x, inv, stride, ncol);
+                    sh_element_to_lds(lds, 4 * i + 1, v[u].y, inv, stride, ncol);
+                    sh_element_to_lds(lds, 4 * i + 2, v[u].z, inv, stride, ncol);
+                    sh_element_to_lds(lds, 4 * i + 3, v[u].w, inv, stride, ncol);
+                }
+            }
+        }
+        for (int e = 4 * n4 + (int)threadIdx.x; e < total; e += NT) sh_element_to_lds(lds, e, g[e], inv, stride, ncol);
+    } else {
+        constexpr int kV = 16;
+        for (int b = 0; b < total; b += kV * NT) {
+            float v[kV];
+#pragma unroll
+            for (int u = 0; u < kV; ++u) {
+                const int e = b + u * NT + (int)threadIdx.x;
+                v[u] = e < total ? g[e] : 0.f;
+            }
+#pragma unroll
+            for (int u = 0; u < kV; ++u) {
+                const int e = b + u * NT + (int)threadIdx.x;
+                if (e < total) sh_element_to_lds(lds, e, v[u], inv, stride, ncol);
+            }
+        }
+    }
+}
+
+template <int NT>
+__device__ __forceinline__ void sh_rows_store(float* __restrict__ g, int stride, const float* __restrict__ lds,
+                                              int nrow, int ncol, bool accumulate) {
+    const int total = (nrow - 1) * stride + ncol;
+    const float inv = 1.0f / (float)stride;
+    auto at = [&](int e, float& v) {
+        const int row = (int)(((float)e + 0.5f) * inv);
+        const int col = e - row * stride;
+        v = col < ncol ? lds[row * kShPitch + col] : 0.f;
+        return col < ncol;
+    };
+    if ((reinterpret_cast<uintptr_t>(g) & 15) == 0 && stride == ncol) {  // dense rows: float4 stores
+        float4* g4 = reinterpret_cast<float4*>(g);
+        const int n4 = total >> 2;
+        for (int i = threadIdx.x; i < n4; i += NT) {
+            float4 v;
+            at(4 * i, v.x);
+            at(4 * i + 1, v.y);
+            at(4 * i + 2, v.z);
+            at(4 * i + 3, v.w);
+            if (accumulate) {
+                const float4 o = g4[i];
+                v = make_float4(o.x + v.x, o.y + v.y, o.z + v.z, o.w + v.w);
+            }
+            g4[i] = v;
+        }
+        for (int e = 4 * n4 + (int)threadIdx.x; e < total; e += NT) {
+            float v;
+            at(e, v);
+            put_out(g, e, v, accumulate);
+        }
+    } else {
+        for (int e = threadIdx.x; e < total; e += NT) {
+            float v;
+            if (at(e, v)) put_out(g, e, v, accumulate);
+        }
+    }
+}
+
 // Sum over the 64 lanes with DPP row ops; the total lands in lane 63.
 template <int CTRL, int ROW_MASK>
 __device__ __forceinline__ float dpp_mov(float v) {

@@ -10,9 +10,10 @@
 //     depth sort ping-pong (key u32 = depth bits, val u32 = index) and scratch.
 //   binning (per tile instance): tile-key sort ping-pong, slot_gauss (slot ->
 //     Gaussian), point_list (sorted position -> Gaussian), slot_to_pos, and the
-//     gradient records written by the backward blend, one 48-B slot per
-//     (instance, 8x8 quadrant) at 4*pos+q, written only for entries the
-//     quadrant's cull kept (sized for HBM capacity, not touched otherwise).
+//     gradient records written by the backward blend, one 48-B record per
+//     (binning slot, 8x8 quadrant) at 4*slot+q, written only for entries the
+//     quadrant's cull kept (sized for HBM capacity, not touched otherwise),
+//     plus one flag byte per record (zeroed by each backward).
 //   image (per pixel / tile): final_T, n_contrib, ranges uint2, tile_last
 //     (max n_contrib over the tile) and quad_last (max n_contrib over each
 //     quadrant: the backward wave's start position).
@@ -105,7 +106,7 @@ inline ImgLayout img_layout(int W, int H) {
 }
 
 struct BinLayout {
-    size_t key0, key1, val0, val1, slot_gauss, point_list, slot_to_pos, records, sort_hist, sort_totals, total;
+    size_t key0, key1, val0, val1, slot_gauss, point_list, slot_to_pos, records, rec_flags, sort_hist, sort_totals, total;
     int sort_blocks;
 };
 inline BinLayout bin_layout(int K, int num_tiles) {
@@ -122,7 +123,8 @@ inline BinLayout bin_layout(int K, int num_tiles) {
     L.slot_gauss = o; o = align_up(o + 4 * k);
     L.point_list = o; o = align_up(o + 4 * k);
     L.slot_to_pos = o; o = align_up(o + 4 * k);
-    L.records = o; o = align_up(o + 4 * 48 * k);  // one record per (instance, quadrant)
+    L.records = o; o = align_up(o + 4 * 48 * k);  // one record per (slot, quadrant)
+    L.rec_flags = o; o = align_up(o + 4 * k);
     L.sort_hist = o; o = align_up(o + 4 * ((size_t)1 << maxbits) * (size_t)L.sort_blocks);
     L.sort_totals = o; o = align_up(o + 4 * ((size_t)1 << maxbits));
     L.total = o;
@@ -229,6 +231,7 @@ struct RenderBwdArgs {
     const uint2* ranges;
     const uint32_t* point_list;
     const uint32_t* quad_last;  // [tiles*4] the replay window of each quadrant wave
+    const uint32_t* pos_slot;   // sorted position -> binning slot (the tile sort's values)
     const float2* means2D;
     const float4* conic_opacity;
     const float4* rgbd;
@@ -236,7 +239,8 @@ struct RenderBwdArgs {
     const float* final_T;
     const uint32_t* n_contrib;
     const float* dL_dpix;
-    float4* records;  // [4*K][3] float4: one record per (instance, quadrant), kept entries only
+    float4* records;     // [4*K][3] float4: one record per (slot, quadrant), kept entries only
+    uint8_t* rec_flags;  // [4*K] set to 1 with each record (zeroed before the launch)
     uint64_t* diag;   // optional [tiles*4][kDiagWords] (see diag_buffer)
 };
 void launch_render_backward(const RenderBwdArgs& a, hipStream_t s);
@@ -250,18 +254,13 @@ struct GaussBwdArgs {
     const float *view, *proj, *campos;
     float tanfovx, tanfovy, fx, fy, scale_modifier;
     const int* radii;       // caller's radii (the reference's visibility gate)
-    const int* geom_radii;  // radii stored by the forward (bin geometry)
-    const float2* means2D;
     const uint32_t* tiles_touched;
     const uint32_t* first_slot;
     const uint8_t* clamped;
-    const uint32_t* slot_to_pos;
-    const uint2* ranges;
-    const uint32_t* tile_last;
-    const uint32_t* quad_last;
-    const float4* conic_opacity;
-    const float4* records;
+    const uint8_t* rec_flags;  // [4*K] nonzero: record (slot, quadrant) was written
+    const float4* records;     // [4*K][3] float4 by slot
     float *dL_dmeans2D, *dL_dcolors, *dL_dopacity, *dL_dmeans3D, *dL_dcov3D, *dL_dscales, *dL_drot;
+    uint32_t acc;  // GS_ACC_* bits: add into the output instead of overwriting
 };
 void launch_gauss_backward(const GaussBwdArgs& a, hipStream_t s);
 

@@ -50,15 +50,21 @@ __device__ __forceinline__ f3 sh_to_rgb(int deg, f3 pos, f3 campos, const float*
 }
 
 __global__ __launch_bounds__(256) void k_preprocess(PreprocessArgs a) {
-    const int idx = blockIdx.x * 256 + threadIdx.x;
+    __shared__ float s_sh[256 * kShPitch];
+    const int idx0 = blockIdx.x * 256;
+    const int idx = idx0 + threadIdx.x;
     uint32_t touched = 0;
+    int radius_out = 0;
+    uint32_t key = 0xFFFFFFFFu;
+    uint8_t clamp_bits = 0;
+    f3 p = mk3(0, 0, 0), rgb = mk3(0, 0, 0);
+    float2 pix = make_float2(0.f, 0.f);
+    float4 conic = make_float4(0.f, 0.f, 0.f, 0.f);
+    float depth = 0.f;
     if (idx < a.P) {
-        int radius_out = 0;
-        uint32_t key = 0xFFFFFFFFu;
-        uint8_t clamp_bits = 0;
         const float* v = a.view;
         const float* pm = a.proj;
-        const f3 p = ld3(a.means3D + 3 * (size_t)idx);
+        p = ld3(a.means3D + 3 * (size_t)idx);
         // in_frustum (auxiliary.h:139-164): only the near test is live
         const float4 ph = proj_point(pm, p);
         const float pw = 1.0f / (ph.w + 0.0000001f);
@@ -88,32 +94,43 @@ __global__ __launch_bounds__(256) void k_preprocess(PreprocessArgs a) {
             if (det != 0.0f) {
                 const float det_inv = 1.f / det;
                 const float op = a.activation ? act_sigmoid(a.opacities[idx]) : a.opacities[idx];
-                const float4 conic = make_float4(cc * det_inv, -cb * det_inv, ca * det_inv, op);
+                conic = make_float4(cc * det_inv, -cb * det_inv, ca * det_inv, op);
                 const float mid = 0.5f * (ca + cc);
                 const float l1 = mid + sqrtf(fmaxf(0.1f, mid * mid - det));
                 const float l2 = mid - sqrtf(fmaxf(0.1f, mid * mid - det));
                 const float rad = ceilf(3.f * sqrtf(fmaxf(l1, l2)));
-                const float px = ndc_to_pixel(ph.x * pw, a.W), py = ndc_to_pixel(ph.y * pw, a.H);
-                const Rect r = tile_rect(px, py, (int)rad, a.gx, a.gy);
+                pix = make_float2(ndc_to_pixel(ph.x * pw, a.W), ndc_to_pixel(ph.y * pw, a.H));
+                const Rect r = tile_rect(pix.x, pix.y, (int)rad, a.gx, a.gy);
                 const uint32_t area = (uint32_t)((r.y1 - r.y0) * (r.x1 - r.x0));
                 if (area != 0) {
-                    f3 rgb = mk3(0, 0, 0);
-                    if (a.copy_colors) {
-                        if (a.colors_precomp) {
-                            rgb = ld3(a.colors_precomp + 3 * (size_t)idx);
-                        } else {
-                            rgb = sh_to_rgb(a.D, p, ld3(a.campos), a.sh.dc + (size_t)idx * a.sh.dc_stride,
-                                            a.sh.rest + (size_t)idx * a.sh.rest_stride, clamp_bits);
-                        }
-                    }
-                    a.means2D[idx] = make_float2(px, py);
-                    a.conic_opacity[idx] = conic;
-                    a.rgbd[idx] = make_float4(rgb.x, rgb.y, rgb.z, pv.z);
                     radius_out = (int)rad;
                     touched = area;
+                    depth = pv.z;
                     key = __float_as_uint(pv.z);  // depth > 0.2: the bits sort as the value
                 }
             }
+        }
+    }
+    // colours: precomputed, or SH evaluated from rows staged through LDS (coalesced)
+    const bool need_sh = touched && a.copy_colors && !a.colors_precomp && a.sh.dc;
+    const int ncol = (a.M - 1) * 3 < kShPitch ? (a.M - 1) * 3 : kShPitch;
+    if (__syncthreads_count(need_sh) && ncol > 0) {
+        const int nrow = a.P - idx0 < 256 ? a.P - idx0 : 256;
+        sh_rows_load<256>(a.sh.rest + (size_t)idx0 * a.sh.rest_stride, a.sh.rest_stride, s_sh, nrow, ncol);
+        __syncthreads();
+    }
+    if (touched && a.copy_colors) {
+        if (a.colors_precomp)
+            rgb = ld3(a.colors_precomp + 3 * (size_t)idx);
+        else
+            rgb = sh_to_rgb(a.D, p, ld3(a.campos), a.sh.dc + (size_t)idx * a.sh.dc_stride, s_sh + threadIdx.x * kShPitch,
+                            clamp_bits);
+    }
+    if (idx < a.P) {
+        if (touched) {
+            a.means2D[idx] = pix;
+            a.conic_opacity[idx] = conic;
+            a.rgbd[idx] = make_float4(rgb.x, rgb.y, rgb.z, depth);
         }
         a.radii[idx] = radius_out;
         if (a.radii_out) a.radii_out[idx] = radius_out;

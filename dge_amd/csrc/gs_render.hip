@@ -360,8 +360,8 @@ constexpr int kBwdGroup = 4;  // entries replayed between two reduce-scatters
 // front in rounds of 256 (ids two rounds, geometry one round ahead), culls
 // each round against its quadrant, replays the survivors in groups of four
 // and reduce-scatters their nine sums across the wave (quad_reduce).  Each
-// kept entry gets one 48-byte record at 4*pos + quadrant; k_gauss_bwd
-// re-derives with the same cull_keep which quadrant records exist.
+// kept entry gets one 48-byte record at 4*slot + quadrant (slot: the binning
+// slot, so k_gauss_bwd reads a Gaussian's records contiguously) and a flag.
 __global__ __launch_bounds__(64, 4) void k_render_bwd(RenderBwdArgs a) {
     const int quad = blockIdx.x & 3, tile = blockIdx.x >> 2;
     const int tx = tile % a.gx, ty = tile / a.gx;
@@ -376,6 +376,7 @@ __global__ __launch_bounds__(64, 4) void k_render_bwd(RenderBwdArgs a) {
     __shared__ float4 s_co[kRound + kBwdGroup];
     __shared__ float4 s_rgb[kRound + kBwdGroup];
     __shared__ uint32_t s_pos[kRound + kBwdGroup];
+    __shared__ uint32_t s_slot[kRound + kBwdGroup];
 
     const uint2 range = a.ranges[tile];
     const int limit = (int)a.quad_last[blockIdx.x];
@@ -412,11 +413,21 @@ __global__ __launch_bounds__(64, 4) void k_render_bwd(RenderBwdArgs a) {
             ids[i] = r < nr && k < hi ? a.point_list[range.x + k] : 0u;
         }
     };
-    uint32_t ids[4];
+    // binning slot of each entry of round r (the record index), loaded with the geometry
+    auto round_slots = [&](int r, uint32_t (&sl)[4]) {
+        const int hi = limit - kRound * r, lo = hi > kRound ? hi - kRound : 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int k = lo + 64 * i + lane;
+            sl[i] = r < nr && k < hi ? a.pos_slot[range.x + k] : 0u;
+        }
+    };
+    uint32_t ids[4], slots[4];
     Entry cur[4];
     round_ids(0, ids);
 #pragma unroll
     for (int i = 0; i < 4; ++i) cur[i] = gather_entry(a.means2D, a.conic_opacity, a.rgbd, ids[i]);
+    round_slots(0, slots);
     round_ids(1, ids);
 
     for (int r = 0; r < nr; ++r) {
@@ -435,6 +446,7 @@ __global__ __launch_bounds__(64, 4) void k_render_bwd(RenderBwdArgs a) {
                 s_co[slot] = cur[i].co;
                 s_rgb[slot] = cur[i].f;
                 s_pos[slot] = (uint32_t)(lo + j);
+                s_slot[slot] = slots[i];
             }
             nk += __popcll(km);
         }
@@ -443,10 +455,12 @@ __global__ __launch_bounds__(64, 4) void k_render_bwd(RenderBwdArgs a) {
             s_co[nk + lane] = make_float4(0.f, 0.f, 0.f, 0.f);
             s_rgb[nk + lane] = make_float4(0.f, 0.f, 0.f, 0.f);
             s_pos[nk + lane] = 0xFFFFFFFFu;
+            s_slot[nk + lane] = 0u;
         }
         // next round's geometry and the round after's ids, in flight during the replay
 #pragma unroll
         for (int i = 0; i < 4; ++i) cur[i] = gather_entry(a.means2D, a.conic_opacity, a.rgbd, ids[i]);
+        round_slots(r + 1, slots);
         round_ids(r + 2, ids);
         diag_kept += nk;
         diag_rounds += 1;
@@ -463,9 +477,11 @@ __global__ __launch_bounds__(64, 4) void k_render_bwd(RenderBwdArgs a) {
 #pragma unroll
             for (int f = 0; f < 9; ++f) S[f] = quad_reduce(g[0][f], g[1][f], g[2][f], g[3][f]);
             const int kw = k + row_entry;
-            if (row_writer && kw < nk)
-                finish_record(s_co[kw], S, ddelx_dx, ddely_dy,
-                              a.records + 3 * (4 * ((size_t)range.x + s_pos[kw]) + quad));
+            if (row_writer && kw < nk) {
+                const size_t rec = 4 * (size_t)s_slot[kw] + quad;
+                finish_record(s_co[kw], S, ddelx_dx, ddely_dy, a.records + 3 * rec);
+                a.rec_flags[rec] = 1;
+            }
         }
         if (a.diag) c_replay += __builtin_amdgcn_s_memtime() - c0;
         __syncthreads();

@@ -16,6 +16,8 @@ from __future__ import annotations
 
 from typing import NamedTuple
 
+import os
+
 import torch
 import torch.nn as nn
 
@@ -104,16 +106,89 @@ class _RasterizeGaussiansFused(torch.autograd.Function):
         rs = ctx.raster_settings
         (xyz, f_dc, f_rest, colors, raw_opacity, raw_scaling, raw_rotation, radii, geomBuffer, binningBuffer,
          imgBuffer) = ctx.saved_tensors
+        # Fused gradient accumulation: where autograd would add this gradient into a parameter's .grad
+        # itself, the kernel writes (or adds) it there directly and autograd receives None — saving the
+        # separate read-modify-write pass over every parameter.
+        into, direct = {}, []
+        if _FUSED_GRAD_ACCUM and not torch.is_grad_enabled():
+            for name, p in (("xyz", xyz), ("opacity", raw_opacity), ("scaling", raw_scaling),
+                            ("rotation", raw_rotation)):
+                mode = _accumulation_mode(p)
+                if mode is not None:
+                    into[name] = _into_target(p, mode, direct)
+            if ctx.has_sh:
+                m_dc, m_rest = _accumulation_mode(f_dc), _accumulation_mode(f_rest)
+                if m_dc is not None and m_dc == m_rest:
+                    into["sh"] = ((_into_target(f_dc, m_dc, direct)[0], _into_target(f_rest, m_rest, direct)[0]),
+                                  m_dc == "add")
         args = (rs.bg, xyz, f_dc, f_rest, colors, raw_opacity, raw_scaling, raw_rotation, radii, rs.scale_modifier,
                 rs.viewmatrix, rs.projmatrix, rs.tanfovx, rs.tanfovy, grad_out_color, rs.sh_degree, rs.campos,
                 geomBuffer, ctx.num_rendered, binningBuffer, imgBuffer, rs.debug)
         d_m2, d_xyz, d_dc, d_rest, d_col, d_op, d_sc, d_rot = _call_with_snapshot(
-            _C.rasterize_gaussians_fused_backward, args, rs.debug, "snapshot_bw.dump", "backward")
+            lambda *a: _C.rasterize_gaussians_fused_backward(*a, into=into), args, rs.debug, "snapshot_bw.dump",
+            "backward")
+        for p, t in direct:  # parameters whose .grad was None: the kernel wrote it, hand it over
+            p.grad = t
         if ctx.has_sh:
             d_col = None
         else:
             d_dc = d_rest = None
+        if "xyz" in into:
+            d_xyz = None
+        if "opacity" in into:
+            d_op = None
+        if "scaling" in into:
+            d_sc = None
+        if "rotation" in into:
+            d_rot = None
+        if "sh" in into:
+            d_dc = d_rest = None
         return d_xyz, d_m2, d_dc, d_rest, d_col, d_op, d_sc, d_rot, None
+
+
+_FUSED_GRAD_ACCUM = os.environ.get("DGE_AMD_FUSED_GRAD_ACCUM", "1") != "0"
+
+
+def set_fused_grad_accumulation(enabled: bool) -> bool:
+    """Switch the fused gradient accumulation of the raw-parameter path on/off; returns the previous
+    setting (environment default: DGE_AMD_FUSED_GRAD_ACCUM, on unless "0")."""
+    global _FUSED_GRAD_ACCUM
+    prev, _FUSED_GRAD_ACCUM = _FUSED_GRAD_ACCUM, bool(enabled)
+    return prev
+
+
+def _accumulation_mode(p):
+    """"add" / "new" when this backward's gradient for leaf `p` may go straight into p.grad, else None.
+
+    Only where autograd itself would run p's AccumulateGrad in this backward (so torch.autograd.grad
+    callers, which capture instead, still get returned gradients), p has no tensor or post-accumulate
+    hooks, and an existing .grad is a plain contiguous fp32 buffer of p's shape."""
+    if not isinstance(p, torch.Tensor) or not p.requires_grad or p.grad_fn is not None or p.numel() == 0:
+        return None
+    if getattr(p, "_backward_hooks", None) or getattr(p, "_post_accumulate_grad_hooks", None):
+        return None
+    try:
+        with torch.enable_grad():
+            node = p.view_as(p).grad_fn.next_functions[0][0]
+        if not torch._C._will_engine_execute_node(node):
+            return None
+    except Exception:
+        return None
+    g = p.grad
+    if g is None:
+        return "new"
+    if (g.shape == p.shape and g.dtype == torch.float32 and g.device == p.device and g.is_contiguous()
+            and not g.requires_grad):
+        return "add"
+    return None
+
+
+def _into_target(p, mode, direct):
+    if mode == "add":
+        return (p.grad, True)
+    t = torch.empty_like(p, memory_format=torch.contiguous_format)
+    direct.append((p, t))
+    return (t, False)
 
 
 def rasterize_gaussian_model(xyz, means2D, features_dc, features_rest, colors_precomp, raw_opacity, raw_scaling,

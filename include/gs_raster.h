@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define GS_RASTER_ABI_VERSION 1
+#define GS_RASTER_ABI_VERSION 2
 
 #define GS_OK 0
 #define GS_ERR_INVALID_ARG 1   /* AT_ERROR / std::runtime_error in the reference */
@@ -125,6 +125,17 @@ typedef struct gs_params {
                                         rotation = x / max(|x|, 1e-12) (F.normalize) */
 } gs_params;
 
+/* gs_grads.accumulate bits: output i is ADDED to (out += grad) instead of
+ * overwritten — fused gradient accumulation into existing .grad buffers. */
+#define GS_ACC_MEANS2D   (1u << 0)
+#define GS_ACC_COLORS    (1u << 1)
+#define GS_ACC_OPACITY   (1u << 2)
+#define GS_ACC_MEANS3D   (1u << 3)
+#define GS_ACC_COV3D     (1u << 4)
+#define GS_ACC_SH        (1u << 5)   /* dL_dsh_dc and dL_dsh_rest */
+#define GS_ACC_SCALES    (1u << 7)
+#define GS_ACC_ROTATIONS (1u << 8)
+
 typedef struct gs_grads {         /* backward outputs, every element written */
     float *dL_dmeans2D;           /* [P,3], z = 0 */
     float *dL_dcolors;            /* [P,3] */
@@ -137,6 +148,7 @@ typedef struct gs_grads {         /* backward outputs, every element written */
     int dsh_rest_stride;
     float *dL_dscales;            /* [P,3] (raw when activation = 1) */
     float *dL_drotations;         /* [P,4] (raw when activation = 1) */
+    unsigned int accumulate;      /* GS_ACC_* bits; 0: overwrite every output (reference behaviour) */
 } gs_grads;
 
 int gs_rasterize_forward_ex(const gs_settings *s, const gs_params *g, float *out_color, float *out_depth,

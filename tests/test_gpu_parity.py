@@ -307,3 +307,62 @@ def test_fused_raw_parameter_path_matches_getter_path(cuda_device, monkeypatch, 
             assert a is None or not np.any(a), name
             continue
         assert_close(a, b, name, 1e-4)
+
+
+@pytest.mark.gpu
+def test_fused_gradient_accumulation(cuda_device):
+    """The raw-parameter path writes/adds gradients straight into .grad where autograd would; the
+    result is bitwise the autograd accumulation (same fp32 adds) over two views, a pre-existing .grad
+    and a multi-view batch, and torch.autograd.grad still receives returned gradients."""
+    from dge_amd.cameras import orbit_camera
+    from dge_amd.diff_gaussian_rasterization import set_fused_grad_accumulation
+    from dge_amd.gaussian_renderer import PipelineParams, render
+    from dge_amd.scene import synthetic_scene
+
+    dev = torch.device("cuda")
+    cams = [orbit_camera(k, 4, 160, 120, device=dev) for k in range(2)]
+    Gs = [torch.randn(3, 120, 160, generator=torch.Generator().manual_seed(30 + k)).to(dev) for k in range(2)]
+    bg = torch.zeros(3, device=dev)
+
+    def run(fused, pre_grad, batched):
+        prev = set_fused_grad_accumulation(fused)
+        try:
+            sc = synthetic_scene(15_000, seed=5, radius=1.5, scale=0.03, device=dev).requires_grad_(True)
+            if pre_grad:
+                for p in sc.parameters():
+                    p.grad = torch.full_like(p, 0.25)
+            outs = [render(c, sc, PipelineParams(), bg)["render"] for c in cams]
+            if batched:  # one backward through both views (autograd sums them)
+                sum((o * g).sum() for o, g in zip(outs, Gs)).backward()
+            else:
+                for o, g in zip(outs, Gs):
+                    (o * g).sum().backward()
+            return [p.grad.clone() for p in sc.parameters()]
+        finally:
+            set_fused_grad_accumulation(prev)
+
+    for pre_grad in (False, True):
+        for batched in (False, True):
+            a, b = run(True, pre_grad, batched), run(False, pre_grad, batched)
+            for x, y in zip(a, b):
+                if batched and pre_grad:
+                    # autograd sums the views first, pre + (g1 + g2); the fused path adds each view into
+                    # .grad, (pre + g1) + g2: one rounding apart
+                    torch.testing.assert_close(x, y, rtol=1e-6, atol=1e-6)
+                else:  # the same fp32 additions in the same (or a commutative) order
+                    assert torch.equal(x, y)
+
+    # torch.autograd.grad captures instead of accumulating: gradients come back, .grad stays untouched
+    sc = synthetic_scene(15_000, seed=5, radius=1.5, scale=0.03, device=dev).requires_grad_(True)
+    out = render(cams[0], sc, PipelineParams(), bg)["render"]
+    params = list(sc.parameters())
+    grads = torch.autograd.grad((out * Gs[0]).sum(), params)
+    assert all(p.grad is None for p in params)
+    sc2 = synthetic_scene(15_000, seed=5, radius=1.5, scale=0.03, device=dev).requires_grad_(True)
+    prev = set_fused_grad_accumulation(False)
+    try:
+        (render(cams[0], sc2, PipelineParams(), bg)["render"] * Gs[0]).sum().backward()
+    finally:
+        set_fused_grad_accumulation(prev)
+    for g, p in zip(grads, sc2.parameters()):
+        assert torch.equal(g, p.grad)

@@ -98,3 +98,54 @@ def test_wrapper_rejects_bad_means_shape():
         _C.rasterize_gaussians(torch.zeros(3), torch.zeros(4, 2), torch.empty(0), torch.ones(4, 1), torch.ones(4, 3),
                                torch.ones(4, 4), 1.0, torch.empty(0), torch.eye(4), torch.eye(4), 0.5, 0.5, 16, 16,
                                torch.zeros(4, 1, 3), 0, torch.zeros(3), False, False)
+
+
+# ---- fused gradient accumulation: the decision rules (pure autograd, CPU) ----
+def _modes_seen_in_backward(params, use_autograd_grad=False):
+    """Run a backward through a probe Function and record _accumulation_mode of every param."""
+    from dge_amd.diff_gaussian_rasterization import _accumulation_mode
+
+    seen = {}
+
+    class Probe(torch.autograd.Function):
+        @staticmethod
+        def forward(ctx, *xs):
+            ctx.xs = xs
+            return sum(x.sum() for x in xs)
+
+        @staticmethod
+        def backward(ctx, g):
+            for i, x in enumerate(ctx.xs):
+                seen[i] = _accumulation_mode(x)
+            return tuple(torch.ones_like(x) for x in ctx.xs)
+
+    out = Probe.apply(*params)
+    if use_autograd_grad:
+        torch.autograd.grad(out, params)
+    else:
+        out.backward()
+    return [seen[i] for i in range(len(params))]
+
+
+@pytest.mark.filterwarnings("ignore")
+def test_fused_accum_modes():
+    a = torch.zeros(4, requires_grad=True)
+    b = torch.zeros(4, requires_grad=True)
+    b.grad = torch.zeros(4)
+    c = torch.zeros(4, requires_grad=True)
+    c.register_hook(lambda g: g)  # hooked: autograd keeps the gradient
+    d = torch.zeros(4, requires_grad=True)
+    d.grad = torch.zeros(8)[::2]  # non-contiguous .grad
+    assert _modes_seen_in_backward([a, b, c, d]) == ["new", "add", None, None]
+
+
+def test_fused_accum_not_under_autograd_grad():
+    a = torch.zeros(4, requires_grad=True)
+    assert _modes_seen_in_backward([a], use_autograd_grad=True) == [None]
+
+
+def test_fused_accum_toggle():
+    from dge_amd.diff_gaussian_rasterization import set_fused_grad_accumulation
+
+    prev = set_fused_grad_accumulation(False)
+    assert set_fused_grad_accumulation(prev) is False

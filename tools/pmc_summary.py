@@ -1,0 +1,49 @@
+"""Summarise rocprofv3 --pmc passes per kernel (dev tool).
+
+Reads gpurun_out/pmc/p*/.../*counter_collection.csv, averages every counter
+per dispatch for each kernel, prints a table and writes
+gpurun_out/pmc/pmc_traffic.json (committed as profiles/pmc_traffic.json): per kernel the HBM bytes per launch from the
+memory-side counters, corrected as MI355X_MICROARCH.md §HBM prescribes
+(FETCH_SIZE reports half the bytes of wide coalesced reads on gfx950: x2;
+WRITE_SIZE is taken as reported; both are in KiB).
+"""
+import collections
+import csv
+import glob
+import json
+import os
+import sys
+
+STAGE = {"k_preprocess": "preprocess", "k_render_fwd": "render_fwd", "k_render_bwd": "render_bwd",
+         "k_gauss_bwd": "gauss_bwd", "k_render_apply_weights": "apply_weights", "k_ranges": "ranges",
+         "k_scan_emit": "emit"}
+
+
+def main(root):
+    vals = collections.defaultdict(lambda: collections.defaultdict(list))
+    for f in glob.glob(os.path.join(root, "p*", "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            name = r.get("Kernel_Name", r.get("Kernel-Name", ""))
+            short = name.split("(")[0].split("::")[-1].strip()
+            # one row per (dispatch, counter)
+            vals[short][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    out = {}
+    keys = sorted(vals, key=lambda k: -sum(vals[k].get("SQ_WAVE_CYCLES", [0])))
+    for k in keys:
+        c = {n: sum(v) / len(v) for n, v in vals[k].items()}
+        line = " ".join(f"{n}={c[n]:.4g}" for n in sorted(c))
+        print(f"{k}: {line}")
+        if k in STAGE and "FETCH_SIZE" in c and "WRITE_SIZE" in c:
+            rd = 2.0 * c["FETCH_SIZE"] * 1024.0
+            wr = c["WRITE_SIZE"] * 1024.0
+            out[STAGE[k]] = {"kernel": k, "read_bytes_per_launch": int(rd), "write_bytes_per_launch": int(wr),
+                             "bytes_per_launch": int(rd + wr),
+                             "method": "rocprofv3 --pmc FETCH_SIZE (x2, gfx950 correction) + WRITE_SIZE, separate passes"}
+    if out:
+        dst = os.path.join(root, "pmc_traffic.json")  # copied into profiles/ by hand after the run
+        json.dump(out, open(dst, "w"), indent=1)
+        print("wrote", dst)
+
+
+if __name__ == "__main__":
+    main(sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc")
