@@ -13,7 +13,7 @@
 //   binning buffer allocation (caller's allocator, e.g. the torch caching allocator)
 //   k_scan_emit                       -> (tile, slot) instances, depth-ordered
 //   tile radix sort (1 pass up to 2048 tiles)
-//   k_ranges                          -> ranges, point_list, slot_to_pos
+//   k_ranges                          -> ranges (point_list comes out of the tile sort)
 //   k_render_fwd                      -> color, depth, final_T, n_contrib, tile_last
 #include <stdarg.h>
 #include <stdio.h>
@@ -320,23 +320,25 @@ int bin_forward(const gs_settings* s, const Grid& g, const gs_params& gp, int* r
     *bin_out = bin;
     if (K == 0) return GS_OK;
 
+    // the tile sort carries (slot, Gaussian): the Gaussian ids are emitted into slot_gauss for a
+    // one-pass sort and into point_list for a two-pass one, so that they always end in point_list
+    const TileSortPlan plan = tile_sort_plan(g.tiles);
+    uint32_t* gsrc = at<uint32_t>(bin, plan.passes == 1 ? bl.slot_gauss : bl.point_list);
+    uint32_t* gdst = at<uint32_t>(bin, plan.passes == 1 ? bl.point_list : bl.slot_gauss);
     ea.tile_key = at<uint32_t>(bin, bl.key0);
-    ea.slot_gauss = at<uint32_t>(bin, bl.slot_gauss);
+    ea.slot_gauss = gsrc;
     { StageScope sc(ST_EMIT, stream); launch_scan_emit(ea, stream); }
     GS_LAUNCHED("emit");
 
-    const TileSortPlan plan = tile_sort_plan(g.tiles);
     int tc;
     { StageScope sc(ST_TILE_SORT, stream);
     tc = radix_sort_pairs(at<uint32_t>(bin, bl.key0), at<uint32_t>(bin, bl.key1), at<uint32_t>(bin, bl.val0),
                                     at<uint32_t>(bin, bl.val1), K, 0, plan.bits, kMaxSinglePassBits, true,
                                     at<uint32_t>(bin, bl.sort_hist), at<uint32_t>(bin, bl.sort_totals), bl.sort_blocks,
-                                    stream); }
+                                    stream, gsrc, gdst); }
     GS_LAUNCHED("tile sort");
     { StageScope sc(ST_RANGES, stream);
-    launch_ranges(at<uint32_t>(bin, tc ? bl.key1 : bl.key0), at<uint32_t>(bin, tc ? bl.val1 : bl.val0),
-                  at<uint32_t>(bin, bl.slot_gauss), (int)K, at<uint2>(img, il.ranges), at<uint32_t>(bin, bl.point_list),
-                  at<uint32_t>(bin, bl.slot_to_pos), stream); }
+    launch_ranges(at<uint32_t>(bin, tc ? bl.key1 : bl.key0), (int)K, at<uint2>(img, il.ranges), stream); }
     GS_LAUNCHED("ranges");
     return GS_OK;
 }
@@ -429,12 +431,12 @@ long long gs_buffer_offset(const char* buffer, const char* field, int P, int wid
         if (!strcmp(field, "ranges")) return (long long)L.ranges;
         if (!strcmp(field, "tile_last")) return (long long)L.tile_last;
         if (!strcmp(field, "quad_last")) return (long long)L.quad_last;
+        if (!strcmp(field, "ckpt")) return (long long)L.ckpt;
     } else if (!strcmp(buffer, "binning")) {
         const int tiles = ((width + 15) / 16) * ((height + 15) / 16);
         const BinLayout L = bin_layout(num_rendered, tiles);
         if (!strcmp(field, "point_list")) return (long long)L.point_list;
         if (!strcmp(field, "slot_gauss")) return (long long)L.slot_gauss;
-        if (!strcmp(field, "slot_to_pos")) return (long long)L.slot_to_pos;
         if (!strcmp(field, "records")) return (long long)L.records;
         if (!strcmp(field, "rec_flags")) return (long long)L.rec_flags;
     }
@@ -486,6 +488,7 @@ int gs_rasterize_forward_ex(const gs_settings* s, const gs_params* gp, float* ou
         ra.n_contrib = at<uint32_t>(img, il.n_contrib);
         ra.tile_last = at<uint32_t>(img, il.tile_last);
         ra.quad_last = at<uint32_t>(img, il.quad_last);
+        ra.ckpt = at<float4>(img, il.ckpt);
         ra.out_color = out_color;
         ra.out_depth = out_depth;
         ra.diag = diag_buffer(0, kDiagWords * (size_t)g.tiles * 4);
@@ -560,6 +563,7 @@ int gs_rasterize_backward_ex(const gs_settings* s, const gs_params* gp, int R, c
             rb.ranges = at<uint2>(img, il.ranges);
             rb.point_list = at<uint32_t>(binning, bl.point_list);
             rb.quad_last = at<uint32_t>(img, il.quad_last);
+            rb.ckpt = at<float4>(img, il.ckpt);
             rb.pos_slot = at<uint32_t>(binning, (plan.passes & 1) ? bl.val1 : bl.val0);
             rb.means2D = at<float2>(geom, gl.means2D);
             rb.conic_opacity = at<float4>(geom, gl.conic_opacity);
@@ -570,7 +574,7 @@ int gs_rasterize_backward_ex(const gs_settings* s, const gs_params* gp, int R, c
             rb.dL_dpix = dL_dpix;
             rb.records = records;
             rb.rec_flags = rec_flags;
-            rb.diag = diag_buffer(1, kDiagWords * (size_t)g.tiles * 4);
+            rb.diag = diag_buffer(1, kDiagWords * (size_t)g.tiles * 4 * kSegMax);
             { StageScope sc(ST_RENDER_BWD, stream); launch_render_backward(rb, stream); }
             GS_LAUNCHED("render backward");
         }

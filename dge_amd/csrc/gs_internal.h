@@ -8,8 +8,9 @@
 //     16-B gather in the blend loop), tiles_touched u32, clamped u8 (3 bits),
 //     radii i32, first_slot u32 (first binning slot of the Gaussian),
 //     depth sort ping-pong (key u32 = depth bits, val u32 = index) and scratch.
-//   binning (per tile instance): tile-key sort ping-pong, slot_gauss (slot ->
-//     Gaussian), point_list (sorted position -> Gaussian), slot_to_pos, and the
+//   binning (per tile instance): tile-key sort ping-pong (key = tile, value =
+//     slot, second value = Gaussian: slot_gauss / point_list), point_list
+//     (sorted position -> Gaussian), and the
 //     gradient records written by the backward blend, one 48-B record per
 //     (binning slot, 8x8 quadrant) at 4*slot+q, written only for entries the
 //     quadrant's cull kept (sized for HBM capacity, not touched otherwise),
@@ -27,7 +28,7 @@ namespace gs {
 
 constexpr int kSortIPT = 16;                    // keys per thread in the radix kernels
 constexpr int kSortTile = 256 * kSortIPT;       // keys per workgroup
-constexpr int kScanIPT = 16;
+constexpr int kScanIPT = 4;
 constexpr int kScanTile = 256 * kScanIPT;
 constexpr int kMaxSinglePassBits = 11;          // tile keys up to 2048 tiles sort in one pass
 constexpr size_t kAlign = 256;
@@ -88,8 +89,21 @@ inline GeomLayout geom_layout(int P) {
     return L;
 }
 
+// Segment-parallel backward replay: the forward checkpoints every quadrant's
+// per-pixel (T, C) at list positions k*L, k = 1..kSegMax-1 (slot 0 holds the
+// final state); the backward replays each segment [k*L, (k+1)*L) of a
+// quadrant window in its own wave.  L depends only on the tile's list length.
+constexpr int kSegMax = 8;        // segments (checkpoint slots) per quadrant
+constexpr int kSegMinLen = 512;   // shortest segment, list positions
+constexpr int kBlendRound = 256;  // list entries per blend round (segment lengths are multiples)
+__host__ __device__ inline int seg_len(uint32_t list_len) {
+    const uint32_t per = (list_len + kSegMax - 1) / kSegMax;
+    const uint32_t L = (per + kBlendRound - 1) / kBlendRound * kBlendRound;
+    return (int)(L > (uint32_t)kSegMinLen ? L : (uint32_t)kSegMinLen);
+}
+
 struct ImgLayout {
-    size_t final_T, n_contrib, ranges, tile_last, quad_last, total;
+    size_t final_T, n_contrib, ckpt, ranges, tile_last, quad_last, total;
 };
 inline ImgLayout img_layout(int W, int H) {
     ImgLayout L;
@@ -98,7 +112,8 @@ inline ImgLayout img_layout(int W, int H) {
     size_t tiles = (size_t)div_up(W, 16) * div_up(H, 16);
     L.final_T = o; o = align_up(o + 4 * n);
     L.n_contrib = o; o = align_up(o + 4 * n);
-    L.ranges = o; o = align_up(o + 8 * tiles);
+    L.ckpt = o; o = align_up(o + 16 * (size_t)kSegMax * 64 * 4 * tiles);  // [tiles*4][kSegMax][64] float4
+    L.ranges = o; o = align_up(o + 8 * tiles);  // ranges.. are zeroed per forward; ckpt is not
     L.tile_last = o; o = align_up(o + 4 * tiles);
     L.quad_last = o; o = align_up(o + 16 * tiles);
     L.total = o;
@@ -106,7 +121,7 @@ inline ImgLayout img_layout(int W, int H) {
 }
 
 struct BinLayout {
-    size_t key0, key1, val0, val1, slot_gauss, point_list, slot_to_pos, records, rec_flags, sort_hist, sort_totals, total;
+    size_t key0, key1, val0, val1, slot_gauss, point_list, records, rec_flags, sort_hist, sort_totals, total;
     int sort_blocks;
 };
 inline BinLayout bin_layout(int K, int num_tiles) {
@@ -122,7 +137,6 @@ inline BinLayout bin_layout(int K, int num_tiles) {
     L.val1 = o; o = align_up(o + 4 * k);
     L.slot_gauss = o; o = align_up(o + 4 * k);
     L.point_list = o; o = align_up(o + 4 * k);
-    L.slot_to_pos = o; o = align_up(o + 4 * k);
     L.records = o; o = align_up(o + 4 * 48 * k);  // one record per (slot, quadrant)
     L.rec_flags = o; o = align_up(o + 4 * k);
     L.sort_hist = o; o = align_up(o + 4 * ((size_t)1 << maxbits) * (size_t)L.sort_blocks);
@@ -171,12 +185,13 @@ struct PreprocessArgs {
 void launch_preprocess(const PreprocessArgs& a, hipStream_t s);
 void launch_mark_visible(int P, const float* means3D, const float* view, uint8_t* present, hipStream_t s);
 
-// LSD radix sort of (u32 key, u32 value).  Returns the buffer index (0/1)
-// holding the result.  identity_vals: values of the first pass are the
-// element indices (val0 is not read).
+// LSD radix sort of (u32 key, u32 value[, u32 second value]).  Returns the
+// buffer index (0/1) holding the result (for all arrays).  identity_vals:
+// values of the first pass are the element indices (val0 is not read).
+// v2a/v2b: optional ping-pong pair of a second value array (input in v2a).
 int radix_sort_pairs(uint32_t* key0, uint32_t* key1, uint32_t* val0, uint32_t* val1, uint32_t n, int begin_bit,
                      int end_bit, int max_pass_bits, bool identity_vals, uint32_t* hist, uint32_t* totals,
-                     int nblocks, hipStream_t s);
+                     int nblocks, hipStream_t s, uint32_t* v2a = nullptr, uint32_t* v2b = nullptr);
 
 struct EmitArgs {
     int P, gx, gy;
@@ -193,8 +208,7 @@ struct EmitArgs {
 void launch_scan_reduce(const EmitArgs& a, hipStream_t s);
 void launch_scan_emit(const EmitArgs& a, hipStream_t s);
 
-void launch_ranges(const uint32_t* sorted_tile, const uint32_t* sorted_slot, const uint32_t* slot_gauss, int K,
-                   uint2* ranges, uint32_t* point_list, uint32_t* slot_to_pos, hipStream_t s);
+void launch_ranges(const uint32_t* sorted_tile, int K, uint2* ranges, hipStream_t s);
 
 struct RenderArgs {
     int W, H, gx, gy;
@@ -208,6 +222,7 @@ struct RenderArgs {
     uint32_t* n_contrib;
     uint32_t* tile_last;
     uint32_t* quad_last;  // [tiles*4] max n_contrib per 8x8 quadrant
+    float4* ckpt;         // [tiles*4][kSegMax][64] (T, C) checkpoints for the segmented backward
     float* out_color;
     float* out_depth;
     uint64_t* diag;       // optional [tiles*4][kDiagWords] (see diag_buffer)
@@ -231,6 +246,7 @@ struct RenderBwdArgs {
     const uint2* ranges;
     const uint32_t* point_list;
     const uint32_t* quad_last;  // [tiles*4] the replay window of each quadrant wave
+    const float4* ckpt;         // the forward's (T, C) checkpoints
     const uint32_t* pos_slot;   // sorted position -> binning slot (the tile sort's values)
     const float2* means2D;
     const float4* conic_opacity;

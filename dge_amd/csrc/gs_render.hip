@@ -53,7 +53,7 @@ __device__ __forceinline__ bool pixel_alpha(float2 xy, float4 co, float pfx, flo
     return !(power > 0.0f) && !(alpha < 1.0f / 255.0f);
 }
 
-constexpr int kRound = 256;  // list entries per round: 4 per lane
+constexpr int kRound = kBlendRound;  // list entries per round: 4 per lane
 constexpr int kGroup = 4;    // blend entries per unrolled step (LDS is padded to a multiple)
 
 // One list entry as gathered from the geometry buffer.
@@ -135,8 +135,15 @@ __global__ __launch_bounds__(64) void k_render_fwd(RenderArgs a) {
     for (int i = 0; i < 4; ++i) cur[i] = gather_entry(a.means2D, a.conic_opacity, a.rgbd, ids[i]);
     load_ids(range.x + kRound, ids);
 
+    const int L = seg_len(range.y - range.x);
+    float4* ckpt = a.ckpt + (size_t)blockIdx.x * kSegMax * 64;
     for (uint32_t b = range.x; b < range.y; b += kRound) {
         if (!__any(!done)) break;
+        {  // (T, C) at the segment boundaries of the backward replay
+            const uint32_t rel = b - range.x;
+            if (rel > 0 && rel % (uint32_t)L == 0 && rel / (uint32_t)L < (uint32_t)kSegMax)
+                ckpt[(rel / L) * 64 + lane] = make_float4(T, C0, C1, C2);
+        }
         // cull against the quadrant, compact survivors in list order (i-major, lane-minor)
         int nk = 0;
 #pragma unroll
@@ -180,6 +187,7 @@ __global__ __launch_bounds__(64) void k_render_fwd(RenderArgs a) {
         __syncthreads();
     }
 
+    ckpt[lane] = make_float4(T, C0, C1, C2);  // slot 0: the final state
     if (inside) {
         const size_t pix = (size_t)a.W * py + px;
         const size_t HW = (size_t)a.W * a.H;
@@ -363,7 +371,11 @@ constexpr int kBwdGroup = 4;  // entries replayed between two reduce-scatters
 // kept entry gets one 48-byte record at 4*slot + quadrant (slot: the binning
 // slot, so k_gauss_bwd reads a Gaussian's records contiguously) and a flag.
 __global__ __launch_bounds__(64, 4) void k_render_bwd(RenderBwdArgs a) {
-    const int quad = blockIdx.x & 3, tile = blockIdx.x >> 2;
+    // block -> (segment, quadrant); segments >= 1 exist only for long windows: they launch first
+    const int nquads = 4 * a.gx * a.gy;
+    const int seg = kSegMax - 1 - (int)(blockIdx.x / (uint32_t)nquads);
+    const int qidx = (int)(blockIdx.x % (uint32_t)nquads);
+    const int quad = qidx & 3, tile = qidx >> 2;
     const int tx = tile % a.gx, ty = tile / a.gx;
     const int lane = threadIdx.x;
     const int bx0 = tx * kTile + (quad & 1) * kQuad, by0 = ty * kTile + (quad >> 1) * kQuad;
@@ -379,7 +391,13 @@ __global__ __launch_bounds__(64, 4) void k_render_bwd(RenderBwdArgs a) {
     __shared__ uint32_t s_slot[kRound + kBwdGroup];
 
     const uint2 range = a.ranges[tile];
-    const int limit = (int)a.quad_last[blockIdx.x];
+    const int window = (int)a.quad_last[qidx];  // the quadrant's last contributor (1-based)
+    const int L = seg_len(range.y - range.x);
+    const int nseg_q = (window + L - 1) / L < kSegMax ? (window + L - 1) / L : kSegMax;
+    if (seg >= nseg_q) return;
+    // this wave's segment [seg_lo, limit) of the window; the last segment takes any remainder
+    const int seg_lo = seg * L;
+    const int limit = seg == nseg_q - 1 ? window : seg_lo + L;
     const size_t HW = (size_t)a.W * a.H;
     const size_t pix = inside ? (size_t)a.W * py + px : 0;
 
@@ -393,6 +411,17 @@ __global__ __launch_bounds__(64, 4) void k_render_bwd(RenderBwdArgs a) {
     }
     const float nbg = -T_final * (a.bg[0] * dp0 + a.bg[1] * dp1 + a.bg[2] * dp2);
     float T = T_final, D0 = 0.f, D1 = 0.f, D2 = 0.f;
+    if (limit < window) {
+        // start inside the window: T and the colour behind position `limit` from the forward's
+        // checkpoints: D = (C_final - C_limit) / T_limit, the composite of entries >= limit
+        const float4* ck = a.ckpt + (size_t)qidx * kSegMax * 64;
+        const float4 cb = ck[(limit / L) * 64 + lane], cf = ck[lane];
+        T = cb.x;
+        const float inv = 1.0f / cb.x;
+        D0 = (cf.y - cb.y) * inv;
+        D1 = (cf.z - cb.z) * inv;
+        D2 = (cf.w - cb.w) * inv;
+    }
     const float ddelx_dx = (float)(0.5 * a.W), ddely_dy = (float)(0.5 * a.H);
     const uint64_t t_start = a.diag ? __builtin_amdgcn_s_memrealtime() : 0;
     const uint64_t c_start = a.diag ? __builtin_amdgcn_s_memtime() : 0;
@@ -404,9 +433,9 @@ __global__ __launch_bounds__(64, 4) void k_render_bwd(RenderBwdArgs a) {
     const int row_entry = row == 1 ? 2 : row == 2 ? 1 : row;
     const bool row_writer = (lane & 15) == 0;
 
-    const int nr = (limit + kRound - 1) / kRound;
+    const int nr = (limit - seg_lo + kRound - 1) / kRound;
     auto round_ids = [&](int r, uint32_t (&ids)[4]) {
-        const int hi = limit - kRound * r, lo = hi > kRound ? hi - kRound : 0;
+        const int hi = limit - kRound * r, lo = hi - kRound > seg_lo ? hi - kRound : seg_lo;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int k = lo + 64 * i + lane;
@@ -415,7 +444,7 @@ __global__ __launch_bounds__(64, 4) void k_render_bwd(RenderBwdArgs a) {
     };
     // binning slot of each entry of round r (the record index), loaded with the geometry
     auto round_slots = [&](int r, uint32_t (&sl)[4]) {
-        const int hi = limit - kRound * r, lo = hi > kRound ? hi - kRound : 0;
+        const int hi = limit - kRound * r, lo = hi - kRound > seg_lo ? hi - kRound : seg_lo;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int k = lo + 64 * i + lane;
@@ -431,7 +460,7 @@ __global__ __launch_bounds__(64, 4) void k_render_bwd(RenderBwdArgs a) {
     round_ids(1, ids);
 
     for (int r = 0; r < nr; ++r) {
-        const int hi = limit - kRound * r, lo = hi > kRound ? hi - kRound : 0;
+        const int hi = limit - kRound * r, lo = hi - kRound > seg_lo ? hi - kRound : seg_lo;
         const int n = hi - lo;
         // cull this round (in registers) and compact the survivors back to front
         int nk = 0;
@@ -487,7 +516,7 @@ __global__ __launch_bounds__(64, 4) void k_render_bwd(RenderBwdArgs a) {
         __syncthreads();
     }
     if (a.diag && lane == 0) {
-        uint64_t* d = a.diag + kDiagWords * (size_t)blockIdx.x;
+        uint64_t* d = a.diag + kDiagWords * (size_t)(seg * nquads + qidx);
         d[0] = t_start;
         d[1] = __builtin_amdgcn_s_memrealtime();
         d[2] = diag_kept;
@@ -500,7 +529,7 @@ __global__ __launch_bounds__(64, 4) void k_render_bwd(RenderBwdArgs a) {
 void launch_render_backward(const RenderBwdArgs& a, hipStream_t s) {
     const int tiles = a.gx * a.gy;
     if (tiles <= 0) return;
-    hipLaunchKernelGGL(k_render_bwd, dim3(tiles * 4), dim3(64), 0, s, a);
+    hipLaunchKernelGGL(k_render_bwd, dim3(tiles * 4 * kSegMax), dim3(64), 0, s, a);
 }
 
 }  // namespace gs

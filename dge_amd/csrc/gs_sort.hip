@@ -13,7 +13,8 @@
 //      already depth-ordered;
 //   3. stable LSD sort of the K instances on the tile id only (one pass for
 //      up to 2048 tiles);
-//   4. tile ranges + the slot -> Gaussian / slot -> position maps.
+//   4. tile ranges from the sorted tile ids; the sort carries the slot (the
+//      gradient-record index) and the Gaussian id (the point list) along.
 // The radix kernels rank keys inside a workgroup with 64-lane ballots
 // (peer-mask match per digit), keep per-wave digit counters in LDS and never
 // use global atomics, so every pass is deterministic.
@@ -119,11 +120,13 @@ __global__ __launch_bounds__(256) void k_radix_digit_scan(uint32_t* __restrict__
     if (threadIdx.x == 0) totals[blockIdx.x] = total;
 }
 
-template <int BITS, bool IDV>
+template <int BITS, bool IDV, bool V2>
 __global__ __launch_bounds__(256) void k_radix_scatter(const uint32_t* __restrict__ keys_in,
                                                        const uint32_t* __restrict__ vals_in,
                                                        uint32_t* __restrict__ keys_out, uint32_t* __restrict__ vals_out,
-                                                       uint32_t n, int shift, const uint32_t* __restrict__ hist,
+                                                       const uint32_t* __restrict__ vals2_in,
+                                                       uint32_t* __restrict__ vals2_out, uint32_t n, int shift,
+                                                       const uint32_t* __restrict__ hist,
                                                        const uint32_t* __restrict__ totals, int nb) {
     constexpr int NDIG = 1 << BITS;
     constexpr int PER = NDIG >= 256 ? NDIG / 256 : 1;
@@ -152,13 +155,14 @@ __global__ __launch_bounds__(256) void k_radix_scatter(const uint32_t* __restric
     }
     __syncthreads();
     const uint32_t base = blockIdx.x * (uint32_t)kSortTile + w * 64u * kSortIPT;
-    uint32_t key[kSortIPT], val[kSortIPT], loc[kSortIPT];
+    uint32_t key[kSortIPT], val[kSortIPT], val2[kSortIPT], loc[kSortIPT];
 #pragma unroll
     for (int it = 0; it < kSortIPT; ++it) {
         const uint32_t idx = base + it * 64 + lane;
         const bool valid = idx < n;
         key[it] = valid ? keys_in[idx] : 0u;
         val[it] = IDV ? idx : (valid ? vals_in[idx] : 0u);
+        val2[it] = V2 && valid ? vals2_in[idx] : 0u;
     }
 #pragma unroll
     for (int it = 0; it < kSortIPT; ++it) {
@@ -191,29 +195,35 @@ __global__ __launch_bounds__(256) void k_radix_scatter(const uint32_t* __restric
             const uint32_t pos = cnt[w][d] + loc[it];
             keys_out[pos] = key[it];
             vals_out[pos] = val[it];
+            if (V2) vals2_out[pos] = val2[it];
         }
     }
 }
 
 template <int BITS>
-static void radix_pass(const uint32_t* kin, const uint32_t* vin, uint32_t* kout, uint32_t* vout, uint32_t n, int shift,
-                       bool idv, uint32_t* hist, uint32_t* totals, int nb, hipStream_t s) {
+static void radix_pass(const uint32_t* kin, const uint32_t* vin, uint32_t* kout, uint32_t* vout, const uint32_t* v2in,
+                       uint32_t* v2out, uint32_t n, int shift, bool idv, uint32_t* hist, uint32_t* totals, int nb,
+                       hipStream_t s) {
     constexpr int NDIG = 1 << BITS;
     hipLaunchKernelGGL(k_radix_hist<BITS>, dim3(nb), dim3(256), 0, s, kin, n, shift, hist, nb);
     hipLaunchKernelGGL(k_radix_digit_scan, dim3(NDIG), dim3(256), 0, s, hist, nb, totals);
-    if (idv)
-        hipLaunchKernelGGL((k_radix_scatter<BITS, true>), dim3(nb), dim3(256), 0, s, kin, vin, kout, vout, n, shift,
-                           hist, totals, nb);
-    else
-        hipLaunchKernelGGL((k_radix_scatter<BITS, false>), dim3(nb), dim3(256), 0, s, kin, vin, kout, vout, n, shift,
-                           hist, totals, nb);
+#define GS_SCATTER(IDV, V2)                                                                                      \
+    hipLaunchKernelGGL((k_radix_scatter<BITS, IDV, V2>), dim3(nb), dim3(256), 0, s, kin, vin, kout, vout, v2in, \
+                       v2out, n, shift, hist, totals, nb)
+    if (v2in) {
+        if (idv) GS_SCATTER(true, true); else GS_SCATTER(false, true);
+    } else {
+        if (idv) GS_SCATTER(true, false); else GS_SCATTER(false, false);
+    }
+#undef GS_SCATTER
 }
 
 static void radix_pass_bits(int bits, const uint32_t* kin, const uint32_t* vin, uint32_t* kout, uint32_t* vout,
-                            uint32_t n, int shift, bool idv, uint32_t* hist, uint32_t* totals, int nb, hipStream_t s) {
+                            const uint32_t* v2in, uint32_t* v2out, uint32_t n, int shift, bool idv, uint32_t* hist,
+                            uint32_t* totals, int nb, hipStream_t s) {
     switch (bits) {
 #define GS_CASE(B) \
-    case B: radix_pass<B>(kin, vin, kout, vout, n, shift, idv, hist, totals, nb, s); break;
+    case B: radix_pass<B>(kin, vin, kout, vout, v2in, v2out, n, shift, idv, hist, totals, nb, s); break;
         GS_CASE(1) GS_CASE(2) GS_CASE(3) GS_CASE(4) GS_CASE(5) GS_CASE(6)
         GS_CASE(7) GS_CASE(8) GS_CASE(9) GS_CASE(10) GS_CASE(11)
 #undef GS_CASE
@@ -223,9 +233,10 @@ static void radix_pass_bits(int bits, const uint32_t* kin, const uint32_t* vin, 
 
 int radix_sort_pairs(uint32_t* key0, uint32_t* key1, uint32_t* val0, uint32_t* val1, uint32_t n, int begin_bit,
                      int end_bit, int max_pass_bits, bool identity_vals, uint32_t* hist, uint32_t* totals, int nblocks,
-                     hipStream_t s) {
+                     hipStream_t s, uint32_t* v2a, uint32_t* v2b) {
     uint32_t* k[2] = {key0, key1};
     uint32_t* v[2] = {val0, val1};
+    uint32_t* w[2] = {v2a, v2b};
     int cur = 0;
     const int total_bits = end_bit - begin_bit;
     const int passes = (total_bits + max_pass_bits - 1) / max_pass_bits;
@@ -234,8 +245,8 @@ int radix_sort_pairs(uint32_t* key0, uint32_t* key1, uint32_t* val0, uint32_t* v
         // split the bits evenly over the passes
         const int rem = end_bit - shift;
         const int bits = (rem + (passes - p) - 1) / (passes - p);
-        radix_pass_bits(bits, k[cur], v[cur], k[cur ^ 1], v[cur ^ 1], n, shift, identity_vals && p == 0, hist, totals,
-                        nblocks, s);
+        radix_pass_bits(bits, k[cur], v[cur], k[cur ^ 1], v[cur ^ 1], w[cur], w[cur ^ 1], n, shift,
+                        identity_vals && p == 0, hist, totals, nblocks, s);
         cur ^= 1;
         shift += bits;
     }
@@ -273,33 +284,52 @@ __global__ __launch_bounds__(256) void k_scan_top(uint32_t* __restrict__ sums, i
     if (threadIdx.x == 0) sums[nb] = carry;
 }
 
+// Emission in depth order: rounds of 256 Gaussians; a block scan of their
+// instance counts gives each its first slot, then the round's instances are
+// expanded cooperatively — thread j writes slot base+j, finding its Gaussian
+// by binary search over the round's start offsets in LDS — so every store of
+// a wave is coalesced (duplicateWithKeys, rasterizer_impl.cu:67-100, writes
+// per Gaussian instead).
 __global__ __launch_bounds__(256) void k_scan_emit(EmitArgs a) {
     __shared__ uint32_t lds4[4];
-    const uint32_t r0 = blockIdx.x * (uint32_t)kScanTile + threadIdx.x * kScanIPT;
-    uint32_t g[kScanIPT], c[kScanIPT];
-    uint32_t s = 0;
-#pragma unroll
-    for (int i = 0; i < kScanIPT; ++i) {
-        const uint32_t r = r0 + i;
-        g[i] = r < (uint32_t)a.P ? a.order[r] : 0u;
-        c[i] = r < (uint32_t)a.P ? a.tiles_touched[g[i]] : 0u;
-        s += c[i];
-    }
-    uint32_t total;
-    uint32_t slot = a.scan_sums[blockIdx.x] + block_exclusive_scan(s, lds4, total);
-#pragma unroll 1
-    for (int i = 0; i < kScanIPT; ++i) {
-        if (c[i] == 0) continue;
-        const uint32_t gi = g[i];
-        a.first_slot[gi] = slot;
-        const float2 xy = a.means2D[gi];
-        const Rect q = tile_rect(xy.x, xy.y, a.radii[gi], a.gx, a.gy);
-        for (int y = q.y0; y < q.y1; ++y)
-            for (int x = q.x0; x < q.x1; ++x) {
-                a.tile_key[slot] = (uint32_t)(y * a.gx + x);
-                a.slot_gauss[slot] = gi;
-                ++slot;
+    __shared__ uint32_t s_start[256];
+    __shared__ uint32_t s_gauss[256];
+    __shared__ int4 s_rect[256];  // x0, y0, width, -
+    uint32_t base = a.scan_sums[blockIdx.x];
+    const uint32_t r_block = blockIdx.x * (uint32_t)kScanTile;
+    for (int it = 0; it < kScanIPT; ++it) {
+        const uint32_t r = r_block + it * 256 + threadIdx.x;
+        const uint32_t g = r < (uint32_t)a.P ? a.order[r] : 0u;
+        const uint32_t c = r < (uint32_t)a.P ? a.tiles_touched[g] : 0u;
+        uint32_t total;
+        const uint32_t off = block_exclusive_scan(c, lds4, total);
+        if (c) {
+            a.first_slot[g] = base + off;
+            const float2 xy = a.means2D[g];
+            const Rect q = tile_rect(xy.x, xy.y, a.radii[g], a.gx, a.gy);
+            s_rect[threadIdx.x] = make_int4(q.x0, q.y0, q.x1 - q.x0, 0);
+        }
+        s_start[threadIdx.x] = off;
+        s_gauss[threadIdx.x] = g;
+        __syncthreads();
+        for (uint32_t j = threadIdx.x; j < total; j += 256) {
+            // owner: the last entry with start <= j.  Starts are an exclusive scan (non-decreasing); an
+            // empty entry shares its start with the later entry that owns that slot, so it is never last.
+            int lo = 0, hi = 255;
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (s_start[mid] <= j) lo = mid;
+                else hi = mid - 1;
             }
+            const int4 q = s_rect[lo];
+            const uint32_t k = j - s_start[lo];
+            const uint32_t ky = (uint32_t)(((float)k + 0.5f) / (float)q.z);  // exact: k < 2^20, margin 0.5/width
+            const uint32_t kx = k - ky * (uint32_t)q.z;
+            a.tile_key[base + j] = (uint32_t)((q.y + (int)ky) * a.gx + q.x + (int)kx);
+            a.slot_gauss[base + j] = s_gauss[lo];
+        }
+        base += total;
+        __syncthreads();
     }
 }
 
@@ -317,15 +347,10 @@ void launch_scan_emit(const EmitArgs& a, hipStream_t s) {
 // ---------------------------------------------------------------------
 // identifyTileRanges (rasterizer_impl.cu:105-125) + instance maps
 // ---------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_ranges(const uint32_t* __restrict__ tile, const uint32_t* __restrict__ slot,
-                                                const uint32_t* __restrict__ slot_gauss, int K, uint2* __restrict__ ranges,
-                                                uint32_t* __restrict__ point_list, uint32_t* __restrict__ slot_to_pos) {
+__global__ __launch_bounds__(256) void k_ranges(const uint32_t* __restrict__ tile, int K, uint2* __restrict__ ranges) {
     const int pos = blockIdx.x * 256 + threadIdx.x;
     if (pos >= K) return;
     const uint32_t t = tile[pos];
-    const uint32_t sl = slot[pos];
-    point_list[pos] = slot_gauss[sl];
-    slot_to_pos[sl] = (uint32_t)pos;
     if (pos == 0) {
         ranges[t].x = 0;
     } else {
@@ -338,11 +363,9 @@ __global__ __launch_bounds__(256) void k_ranges(const uint32_t* __restrict__ til
     if (pos == K - 1) ranges[t].y = (uint32_t)K;
 }
 
-void launch_ranges(const uint32_t* sorted_tile, const uint32_t* sorted_slot, const uint32_t* slot_gauss, int K,
-                   uint2* ranges, uint32_t* point_list, uint32_t* slot_to_pos, hipStream_t s) {
+void launch_ranges(const uint32_t* sorted_tile, int K, uint2* ranges, hipStream_t s) {
     if (K <= 0) return;
-    hipLaunchKernelGGL(k_ranges, dim3(div_up(K, 256)), dim3(256), 0, s, sorted_tile, sorted_slot, slot_gauss, K, ranges,
-                       point_list, slot_to_pos);
+    hipLaunchKernelGGL(k_ranges, dim3(div_up(K, 256)), dim3(256), 0, s, sorted_tile, K, ranges);
 }
 
 }  // namespace gs

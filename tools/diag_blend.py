@@ -18,11 +18,15 @@ from dge_amd.gaussian_renderer import PipelineParams, render  # noqa: E402
 from dge_amd.scene import synthetic_scene  # noqa: E402
 
 
-def summarize(name, d, per_tile=False):
+def summarize(name, d, nquads=None):
+    """d: per-wave records; for the backward, rows are indexed seg * nquads + quadrant."""
     if d.size == 0:
         print(name, "no data")
         return
     d = d.astype(np.int64)
+    ids = np.arange(len(d))
+    live = d[:, 1] > 0  # blocks that had work (segments past a window's end exit without a record)
+    d, ids = d[live], ids[live]
     start, end, kept, rounds, cyc_loop, cyc_total = (d[:, i] for i in range(6))
     t0 = start.min()
     dur = (end - start) * 10e-3  # us (100 MHz)
@@ -37,8 +41,8 @@ def summarize(name, d, per_tile=False):
           f"loop cycles per kept entry (all) {cyc_loop.sum() / max(1, kept.sum()):.0f}")
     order = np.argsort(-dur)[:6]
     for i in order:
-        extra = f" tile {i // 4} wave {i % 4} tile-kept {kept[4 * (i // 4):4 * (i // 4) + 4].tolist()}" if per_tile else ""
-        print(f"   slowest: wave {i} dur {dur[i]:.1f} us kept {kept[i]} rounds {rounds[i]} loop cyc/kept "
+        extra = f" seg {ids[i] // nquads} quad {ids[i] % nquads}" if nquads else ""
+        print(f"   slowest: wave {ids[i]} dur {dur[i]:.1f} us kept {kept[i]} rounds {rounds[i]} loop cyc/kept "
               f"{cyc_loop[i] / max(1, kept[i]):.0f} loop share {cyc_loop[i] / max(1, cyc_total[i]):.2f} "
               f"start {(start[i] - t0) * 10e-3:.1f}{extra}")
     ts = np.linspace(0, span, 11)
@@ -62,7 +66,7 @@ def main():
     torch.cuda.synchronize()
     _native.diag_enable(False)
     summarize("render_fwd", _native.diag_read(0))
-    summarize("render_bwd", _native.diag_read(1), per_tile=True)
+    summarize("render_bwd", _native.diag_read(1), nquads=4 * ((W + 15) // 16) * ((H + 15) // 16))
 
 
 if __name__ == "__main__":
