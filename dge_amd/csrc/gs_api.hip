@@ -13,7 +13,7 @@
 //   binning buffer allocation (caller's allocator, e.g. the torch caching allocator)
 //   k_scan_emit                       -> (tile, slot) instances, depth-ordered
 //   tile radix sort (1 pass up to 2048 tiles)
-//   k_ranges                          -> ranges (point_list comes out of the tile sort)
+//   k_ranges                          -> ranges (the per-tile lists come out of the tile sort)
 //   k_render_fwd                      -> color, depth, final_T, n_contrib, tile_last
 #include <stdarg.h>
 #include <stdio.h>
@@ -320,22 +320,17 @@ int bin_forward(const gs_settings* s, const Grid& g, const gs_params& gp, int* r
     *bin_out = bin;
     if (K == 0) return GS_OK;
 
-    // the tile sort carries (slot, Gaussian): the Gaussian ids are emitted into slot_gauss for a
-    // one-pass sort and into point_list for a two-pass one, so that they always end in point_list
     const TileSortPlan plan = tile_sort_plan(g.tiles);
-    uint32_t* gsrc = at<uint32_t>(bin, plan.passes == 1 ? bl.slot_gauss : bl.point_list);
-    uint32_t* gdst = at<uint32_t>(bin, plan.passes == 1 ? bl.point_list : bl.slot_gauss);
     ea.tile_key = at<uint32_t>(bin, bl.key0);
-    ea.slot_gauss = gsrc;
+    ea.slot_gauss = at<uint32_t>(bin, bl.slot_gauss);
     { StageScope sc(ST_EMIT, stream); launch_scan_emit(ea, stream); }
     GS_LAUNCHED("emit");
 
     int tc;
     { StageScope sc(ST_TILE_SORT, stream);
-    tc = radix_sort_pairs(at<uint32_t>(bin, bl.key0), at<uint32_t>(bin, bl.key1), at<uint32_t>(bin, bl.val0),
-                                    at<uint32_t>(bin, bl.val1), K, 0, plan.bits, kMaxSinglePassBits, true,
-                                    at<uint32_t>(bin, bl.sort_hist), at<uint32_t>(bin, bl.sort_totals), bl.sort_blocks,
-                                    stream, gsrc, gdst); }
+    tc = tile_sort(at<uint32_t>(bin, bl.key0), at<uint32_t>(bin, bl.key1), at<uint2>(bin, bl.pair0),
+                   at<uint2>(bin, bl.pair1), at<uint32_t>(bin, bl.slot_gauss), K, plan.bits,
+                   at<uint32_t>(bin, bl.sort_hist), at<uint32_t>(bin, bl.sort_totals), bl.sort_blocks, stream); }
     GS_LAUNCHED("tile sort");
     { StageScope sc(ST_RANGES, stream);
     launch_ranges(at<uint32_t>(bin, tc ? bl.key1 : bl.key0), (int)K, at<uint2>(img, il.ranges), stream); }
@@ -435,7 +430,7 @@ long long gs_buffer_offset(const char* buffer, const char* field, int P, int wid
     } else if (!strcmp(buffer, "binning")) {
         const int tiles = ((width + 15) / 16) * ((height + 15) / 16);
         const BinLayout L = bin_layout(num_rendered, tiles);
-        if (!strcmp(field, "point_list")) return (long long)L.point_list;
+        if (!strcmp(field, "point_pairs")) return (long long)L.point_pairs;
         if (!strcmp(field, "slot_gauss")) return (long long)L.slot_gauss;
         if (!strcmp(field, "records")) return (long long)L.records;
         if (!strcmp(field, "rec_flags")) return (long long)L.rec_flags;
@@ -479,7 +474,9 @@ int gs_rasterize_forward_ex(const gs_settings* s, const gs_params* gp, float* ou
         RenderArgs ra;
         ra.W = g.W; ra.H = g.H; ra.gx = g.gx; ra.gy = g.gy;
         ra.ranges = at<uint2>(img, il.ranges);
-        ra.point_list = at<uint32_t>(bin, bl.point_list);
+        ra.point_pairs = at<uint2>(bin, bl.point_pairs);
+        ra.bwd_items = at<uint32_t>(img, il.bwd_items);
+        ra.bwd_count = at<uint32_t>(img, il.bwd_count);
         ra.means2D = at<float2>(geom, gl.means2D);
         ra.conic_opacity = at<float4>(geom, gl.conic_opacity);
         ra.rgbd = at<float4>(geom, gl.rgbd);
@@ -557,14 +554,14 @@ int gs_rasterize_backward_ex(const gs_settings* s, const gs_params* gp, int R, c
         uint8_t* rec_flags = R > 0 ? at<uint8_t>(const_cast<void*>(binning), bl.rec_flags) : nullptr;
         if (R > 0) {
             GS_HIP(hipMemsetAsync(rec_flags, 0, 4 * (size_t)R, stream));
-            const TileSortPlan plan = tile_sort_plan(g.tiles);  // the sort's values end in val1 after an odd pass count
             RenderBwdArgs rb;
             rb.W = g.W; rb.H = g.H; rb.gx = g.gx; rb.gy = g.gy;
             rb.ranges = at<uint2>(img, il.ranges);
-            rb.point_list = at<uint32_t>(binning, bl.point_list);
+            rb.point_pairs = at<uint2>(binning, bl.point_pairs);
+            rb.bwd_items = at<uint32_t>(img, il.bwd_items);
+            rb.bwd_count = at<uint32_t>(img, il.bwd_count);
             rb.quad_last = at<uint32_t>(img, il.quad_last);
             rb.ckpt = at<float4>(img, il.ckpt);
-            rb.pos_slot = at<uint32_t>(binning, (plan.passes & 1) ? bl.val1 : bl.val0);
             rb.means2D = at<float2>(geom, gl.means2D);
             rb.conic_opacity = at<float4>(geom, gl.conic_opacity);
             rb.rgbd = at<float4>(geom, gl.rgbd);
@@ -651,7 +648,7 @@ int gs_apply_weights(const gs_settings* s, int P, int M, const float* means3D, f
         ApplyWeightsArgs aw;
         aw.W = g.W; aw.H = g.H; aw.gx = g.gx; aw.gy = g.gy; aw.C = num_channels;
         aw.ranges = at<uint2>(img, il.ranges);
-        aw.point_list = at<uint32_t>(bin, bl.point_list);
+        aw.point_pairs = at<uint2>(bin, bl.point_pairs);
         aw.means2D = at<float2>(geom, gl.means2D);
         aw.conic_opacity = at<float4>(geom, gl.conic_opacity);
         aw.image_weights = image_weights;

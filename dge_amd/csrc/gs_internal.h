@@ -8,9 +8,10 @@
 //     16-B gather in the blend loop), tiles_touched u32, clamped u8 (3 bits),
 //     radii i32, first_slot u32 (first binning slot of the Gaussian),
 //     depth sort ping-pong (key u32 = depth bits, val u32 = index) and scratch.
-//   binning (per tile instance): tile-key sort ping-pong (key = tile, value =
-//     slot, second value = Gaussian: slot_gauss / point_list), point_list
-//     (sorted position -> Gaussian), and the
+//   binning (per tile instance): slot_gauss (emitted Gaussian per slot), the
+//     tile sort's ping-pong keys (tile) and uint2 values (Gaussian, slot) —
+//     the result, point_pairs, is the per-tile list (x: Gaussian, y: slot, the
+//     gradient-record index) — and the
 //     gradient records written by the backward blend, one 48-B record per
 //     (binning slot, 8x8 quadrant) at 4*slot+q, written only for entries the
 //     quadrant's cull kept (sized for HBM capacity, not touched otherwise),
@@ -103,8 +104,12 @@ __host__ __device__ inline int seg_len(uint32_t list_len) {
 }
 
 struct ImgLayout {
-    size_t final_T, n_contrib, ckpt, ranges, tile_last, quad_last, total;
+    size_t final_T, n_contrib, ckpt, bwd_items, ranges, tile_last, quad_last, bwd_count, total;
 };
+// Backward work list, built by the forward: item = quadrant * kSegMax + segment.
+// Quadrants with more than one segment append theirs at the front (counter 0),
+// single-segment quadrants at the back (counter 1): the long replays dispatch first.
+__host__ __device__ inline size_t bwd_item_capacity(int tiles) { return (size_t)tiles * 4 * kSegMax; }
 inline ImgLayout img_layout(int W, int H) {
     ImgLayout L;
     size_t o = 0;
@@ -113,15 +118,17 @@ inline ImgLayout img_layout(int W, int H) {
     L.final_T = o; o = align_up(o + 4 * n);
     L.n_contrib = o; o = align_up(o + 4 * n);
     L.ckpt = o; o = align_up(o + 16 * (size_t)kSegMax * 64 * 4 * tiles);  // [tiles*4][kSegMax][64] float4
-    L.ranges = o; o = align_up(o + 8 * tiles);  // ranges.. are zeroed per forward; ckpt is not
+    L.bwd_items = o; o = align_up(o + 4 * bwd_item_capacity((int)tiles));
+    L.ranges = o; o = align_up(o + 8 * tiles);  // ranges.. are zeroed per forward; ckpt and items are not
     L.tile_last = o; o = align_up(o + 4 * tiles);
     L.quad_last = o; o = align_up(o + 16 * tiles);
+    L.bwd_count = o; o = align_up(o + 8);
     L.total = o;
     return L;
 }
 
 struct BinLayout {
-    size_t key0, key1, val0, val1, slot_gauss, point_list, records, rec_flags, sort_hist, sort_totals, total;
+    size_t key0, key1, pair0, pair1, slot_gauss, point_pairs, records, rec_flags, sort_hist, sort_totals, total;
     int sort_blocks;
 };
 inline BinLayout bin_layout(int K, int num_tiles) {
@@ -133,10 +140,10 @@ inline BinLayout bin_layout(int K, int num_tiles) {
     L.sort_blocks = div_up((long long)k, kSortTile);
     L.key0 = o; o = align_up(o + 4 * k);
     L.key1 = o; o = align_up(o + 4 * k);
-    L.val0 = o; o = align_up(o + 4 * k);
-    L.val1 = o; o = align_up(o + 4 * k);
+    L.pair0 = o; o = align_up(o + 8 * k);
+    L.pair1 = o; o = align_up(o + 8 * k);
+    L.point_pairs = plan.passes & 1 ? L.pair1 : L.pair0;  // where tile_sort leaves (Gaussian, slot)
     L.slot_gauss = o; o = align_up(o + 4 * k);
-    L.point_list = o; o = align_up(o + 4 * k);
     L.records = o; o = align_up(o + 4 * 48 * k);  // one record per (slot, quadrant)
     L.rec_flags = o; o = align_up(o + 4 * k);
     L.sort_hist = o; o = align_up(o + 4 * ((size_t)1 << maxbits) * (size_t)L.sort_blocks);
@@ -185,13 +192,17 @@ struct PreprocessArgs {
 void launch_preprocess(const PreprocessArgs& a, hipStream_t s);
 void launch_mark_visible(int P, const float* means3D, const float* view, uint8_t* present, hipStream_t s);
 
-// LSD radix sort of (u32 key, u32 value[, u32 second value]).  Returns the
-// buffer index (0/1) holding the result (for all arrays).  identity_vals:
-// values of the first pass are the element indices (val0 is not read).
-// v2a/v2b: optional ping-pong pair of a second value array (input in v2a).
+// LSD radix sort of (u32 key, u32 value).  Returns the buffer index (0/1)
+// holding the result.  identity_vals: values of the first pass are the
+// element indices (val0 is not read).
 int radix_sort_pairs(uint32_t* key0, uint32_t* key1, uint32_t* val0, uint32_t* val1, uint32_t n, int begin_bit,
                      int end_bit, int max_pass_bits, bool identity_vals, uint32_t* hist, uint32_t* totals,
-                     int nblocks, hipStream_t s, uint32_t* v2a = nullptr, uint32_t* v2b = nullptr);
+                     int nblocks, hipStream_t s);
+// Stable sort of the K emitted instances on their tile id (key0 in slot
+// order); the values are (Gaussian, slot) pairs built on the first pass from
+// gauss_by_slot.  Returns the buffer index (0/1) holding keys and pairs.
+int tile_sort(uint32_t* key0, uint32_t* key1, uint2* pair0, uint2* pair1, const uint32_t* gauss_by_slot, uint32_t n,
+              int bits, uint32_t* hist, uint32_t* totals, int nblocks, hipStream_t s);
 
 struct EmitArgs {
     int P, gx, gy;
@@ -213,7 +224,7 @@ void launch_ranges(const uint32_t* sorted_tile, int K, uint2* ranges, hipStream_
 struct RenderArgs {
     int W, H, gx, gy;
     const uint2* ranges;
-    const uint32_t* point_list;
+    const uint2* point_pairs;  // per-tile lists: (Gaussian, binning slot)
     const float2* means2D;
     const float4* conic_opacity;
     const float4* rgbd;
@@ -223,6 +234,8 @@ struct RenderArgs {
     uint32_t* tile_last;
     uint32_t* quad_last;  // [tiles*4] max n_contrib per 8x8 quadrant
     float4* ckpt;         // [tiles*4][kSegMax][64] (T, C) checkpoints for the segmented backward
+    uint32_t* bwd_items;  // backward work list (bwd_item_capacity) and its two counters
+    uint32_t* bwd_count;
     float* out_color;
     float* out_depth;
     uint64_t* diag;       // optional [tiles*4][kDiagWords] (see diag_buffer)
@@ -232,7 +245,7 @@ void launch_render_forward(const RenderArgs& a, hipStream_t s);
 struct ApplyWeightsArgs {
     int W, H, gx, gy, C;
     const uint2* ranges;
-    const uint32_t* point_list;
+    const uint2* point_pairs;  // per-tile lists: (Gaussian, binning slot)
     const float2* means2D;
     const float4* conic_opacity;
     const float* image_weights;
@@ -244,9 +257,11 @@ void launch_render_apply_weights(const ApplyWeightsArgs& a, hipStream_t s);
 struct RenderBwdArgs {
     int W, H, gx, gy;
     const uint2* ranges;
-    const uint32_t* point_list;
+    const uint2* point_pairs;  // per-tile lists: (Gaussian, binning slot)
     const uint32_t* quad_last;  // [tiles*4] the replay window of each quadrant wave
     const float4* ckpt;         // the forward's (T, C) checkpoints
+    const uint32_t* bwd_items;  // the forward's work list and counters
+    const uint32_t* bwd_count;
     const uint32_t* pos_slot;   // sorted position -> binning slot (the tile sort's values)
     const float2* means2D;
     const float4* conic_opacity;

@@ -125,7 +125,7 @@ __global__ __launch_bounds__(64) void k_render_fwd(RenderArgs a) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const uint32_t k = b + 64 * i + lane;
-            ids[i] = k < range.y ? a.point_list[k] : 0u;
+            ids[i] = k < range.y ? a.point_pairs[k].x : 0u;
         }
     };
     uint32_t ids[4];
@@ -199,6 +199,19 @@ __global__ __launch_bounds__(64) void k_render_fwd(RenderArgs a) {
         a.out_depth[pix] = D;
     }
     const uint32_t m = wave_max_u32(inside ? last : 0u);
+    if (m) {  // the backward replay's work items for this quadrant (see bwd_item_capacity)
+        const int nseg = (int)((m + L - 1) / L) < kSegMax ? (int)((m + L - 1) / L) : kSegMax;
+        const uint32_t item0 = blockIdx.x * (uint32_t)kSegMax;
+        if (nseg > 1) {
+            uint32_t base = 0;
+            if (lane == 0) base = atomicAdd(&a.bwd_count[0], (uint32_t)nseg);
+            base = __shfl(base, 0);
+            if (lane < nseg) a.bwd_items[base + lane] = item0 + lane;
+        } else if (lane == 0) {
+            const uint32_t b = atomicAdd(&a.bwd_count[1], 1u);
+            a.bwd_items[bwd_item_capacity(a.gx * a.gy) - 1 - b] = item0;
+        }
+    }
     if (lane == 0) {
         a.quad_last[blockIdx.x] = m;
         if (m) atomicMax(&a.tile_last[tile], m);
@@ -253,7 +266,7 @@ __global__ __launch_bounds__(64) void k_render_apply_weights(ApplyWeightsArgs a)
         float4 co = make_float4(0.f, 0.f, 0.f, 0.f);
         uint32_t id = 0;
         if (k < range.y) {
-            id = a.point_list[k];
+            id = a.point_pairs[k].x;
             xy = a.means2D[id];
             co = a.conic_opacity[id];
             keep = cull_keep(xy, co, (float)bx0, (float)by0);
@@ -371,10 +384,15 @@ constexpr int kBwdGroup = 4;  // entries replayed between two reduce-scatters
 // kept entry gets one 48-byte record at 4*slot + quadrant (slot: the binning
 // slot, so k_gauss_bwd reads a Gaussian's records contiguously) and a flag.
 __global__ __launch_bounds__(64, 4) void k_render_bwd(RenderBwdArgs a) {
-    // block -> (segment, quadrant); segments >= 1 exist only for long windows: they launch first
+    // block -> work item (quadrant, segment) of the forward's list: multi-segment windows first,
+    // blocks past the list's end exit (they dispatch after every real item)
     const int nquads = 4 * a.gx * a.gy;
-    const int seg = kSegMax - 1 - (int)(blockIdx.x / (uint32_t)nquads);
-    const int qidx = (int)(blockIdx.x % (uint32_t)nquads);
+    const uint32_t n_multi = a.bwd_count[0], n_single = a.bwd_count[1];
+    if (blockIdx.x >= n_multi + n_single) return;
+    const uint32_t item = blockIdx.x < n_multi ? a.bwd_items[blockIdx.x]
+                                               : a.bwd_items[bwd_item_capacity(a.gx * a.gy) - 1 - (blockIdx.x - n_multi)];
+    const int seg = (int)(item % kSegMax);
+    const int qidx = (int)(item / kSegMax);
     const int quad = qidx & 3, tile = qidx >> 2;
     const int tx = tile % a.gx, ty = tile / a.gx;
     const int lane = threadIdx.x;
@@ -394,7 +412,6 @@ __global__ __launch_bounds__(64, 4) void k_render_bwd(RenderBwdArgs a) {
     const int window = (int)a.quad_last[qidx];  // the quadrant's last contributor (1-based)
     const int L = seg_len(range.y - range.x);
     const int nseg_q = (window + L - 1) / L < kSegMax ? (window + L - 1) / L : kSegMax;
-    if (seg >= nseg_q) return;
     // this wave's segment [seg_lo, limit) of the window; the last segment takes any remainder
     const int seg_lo = seg * L;
     const int limit = seg == nseg_q - 1 ? window : seg_lo + L;
@@ -434,30 +451,25 @@ __global__ __launch_bounds__(64, 4) void k_render_bwd(RenderBwdArgs a) {
     const bool row_writer = (lane & 15) == 0;
 
     const int nr = (limit - seg_lo + kRound - 1) / kRound;
-    auto round_ids = [&](int r, uint32_t (&ids)[4]) {
+    // (Gaussian, slot) of each entry of round r; two rounds ahead of the replay
+    auto round_pairs = [&](int r, uint2 (&pr)[4]) {
         const int hi = limit - kRound * r, lo = hi - kRound > seg_lo ? hi - kRound : seg_lo;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int k = lo + 64 * i + lane;
-            ids[i] = r < nr && k < hi ? a.point_list[range.x + k] : 0u;
+            pr[i] = r < nr && k < hi ? a.point_pairs[range.x + k] : make_uint2(0u, 0u);
         }
     };
-    // binning slot of each entry of round r (the record index), loaded with the geometry
-    auto round_slots = [&](int r, uint32_t (&sl)[4]) {
-        const int hi = limit - kRound * r, lo = hi - kRound > seg_lo ? hi - kRound : seg_lo;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int k = lo + 64 * i + lane;
-            sl[i] = r < nr && k < hi ? a.pos_slot[range.x + k] : 0u;
-        }
-    };
-    uint32_t ids[4], slots[4];
+    uint2 pairs[4];
+    uint32_t slots[4];
     Entry cur[4];
-    round_ids(0, ids);
+    round_pairs(0, pairs);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) cur[i] = gather_entry(a.means2D, a.conic_opacity, a.rgbd, ids[i]);
-    round_slots(0, slots);
-    round_ids(1, ids);
+    for (int i = 0; i < 4; ++i) {
+        cur[i] = gather_entry(a.means2D, a.conic_opacity, a.rgbd, pairs[i].x);
+        slots[i] = pairs[i].y;
+    }
+    round_pairs(1, pairs);
 
     for (int r = 0; r < nr; ++r) {
         const int hi = limit - kRound * r, lo = hi - kRound > seg_lo ? hi - kRound : seg_lo;
@@ -488,9 +500,11 @@ __global__ __launch_bounds__(64, 4) void k_render_bwd(RenderBwdArgs a) {
         }
         // next round's geometry and the round after's ids, in flight during the replay
 #pragma unroll
-        for (int i = 0; i < 4; ++i) cur[i] = gather_entry(a.means2D, a.conic_opacity, a.rgbd, ids[i]);
-        round_slots(r + 1, slots);
-        round_ids(r + 2, ids);
+        for (int i = 0; i < 4; ++i) {
+            cur[i] = gather_entry(a.means2D, a.conic_opacity, a.rgbd, pairs[i].x);
+            slots[i] = pairs[i].y;  // the current round's slots are already staged
+        }
+        round_pairs(r + 2, pairs);
         diag_kept += nk;
         diag_rounds += 1;
         __syncthreads();
@@ -529,7 +543,7 @@ __global__ __launch_bounds__(64, 4) void k_render_bwd(RenderBwdArgs a) {
 void launch_render_backward(const RenderBwdArgs& a, hipStream_t s) {
     const int tiles = a.gx * a.gy;
     if (tiles <= 0) return;
-    hipLaunchKernelGGL(k_render_bwd, dim3(tiles * 4 * kSegMax), dim3(64), 0, s, a);
+    hipLaunchKernelGGL(k_render_bwd, dim3((unsigned)bwd_item_capacity(tiles)), dim3(64), 0, s, a);
 }
 
 }  // namespace gs

@@ -18,6 +18,8 @@
 // The radix kernels rank keys inside a workgroup with 64-lane ballots
 // (peer-mask match per digit), keep per-wave digit counters in LDS and never
 // use global atomics, so every pass is deterministic.
+#include <type_traits>
+
 #include "gs_common.h"
 #include "gs_internal.h"
 
@@ -120,14 +122,22 @@ __global__ __launch_bounds__(256) void k_radix_digit_scan(uint32_t* __restrict__
     if (threadIdx.x == 0) totals[blockIdx.x] = total;
 }
 
-template <int BITS, bool IDV, bool V2>
+// Value modes of the scatter: u32 values (IDV: the element index), or a packed
+// (Gaussian, slot) pair: built from the index and a Gaussian-per-slot array on
+// the first pass of the tile sort, then carried as one 8-byte value.
+enum ValMode { kValU32 = 0, kValPairFirst = 1, kValPair = 2 };
+
+template <int BITS, bool IDV, int VM>
 __global__ __launch_bounds__(256) void k_radix_scatter(const uint32_t* __restrict__ keys_in,
-                                                       const uint32_t* __restrict__ vals_in,
-                                                       uint32_t* __restrict__ keys_out, uint32_t* __restrict__ vals_out,
-                                                       const uint32_t* __restrict__ vals2_in,
-                                                       uint32_t* __restrict__ vals2_out, uint32_t n, int shift,
-                                                       const uint32_t* __restrict__ hist,
+                                                       const void* __restrict__ vals_in_,
+                                                       uint32_t* __restrict__ keys_out, void* __restrict__ vals_out_,
+                                                       const uint32_t* __restrict__ gauss_by_slot, uint32_t n,
+                                                       int shift, const uint32_t* __restrict__ hist,
                                                        const uint32_t* __restrict__ totals, int nb) {
+    using V = typename std::conditional<VM == kValU32, uint32_t, uint2>::type;
+    const uint32_t* vals_in = static_cast<const uint32_t*>(vals_in_);
+    const uint2* pairs_in = static_cast<const uint2*>(vals_in_);
+    V* vals_out = static_cast<V*>(vals_out_);
     constexpr int NDIG = 1 << BITS;
     constexpr int PER = NDIG >= 256 ? NDIG / 256 : 1;
     __shared__ uint32_t cnt[4][NDIG];
@@ -155,14 +165,16 @@ __global__ __launch_bounds__(256) void k_radix_scatter(const uint32_t* __restric
     }
     __syncthreads();
     const uint32_t base = blockIdx.x * (uint32_t)kSortTile + w * 64u * kSortIPT;
-    uint32_t key[kSortIPT], val[kSortIPT], val2[kSortIPT], loc[kSortIPT];
+    uint32_t key[kSortIPT], loc[kSortIPT];
+    V val[kSortIPT];
 #pragma unroll
     for (int it = 0; it < kSortIPT; ++it) {
         const uint32_t idx = base + it * 64 + lane;
         const bool valid = idx < n;
         key[it] = valid ? keys_in[idx] : 0u;
-        val[it] = IDV ? idx : (valid ? vals_in[idx] : 0u);
-        val2[it] = V2 && valid ? vals2_in[idx] : 0u;
+        if constexpr (VM == kValU32) val[it] = IDV ? idx : (valid ? vals_in[idx] : 0u);
+        else if constexpr (VM == kValPairFirst) val[it] = make_uint2(valid ? gauss_by_slot[idx] : 0u, idx);
+        else val[it] = valid ? pairs_in[idx] : make_uint2(0u, 0u);
     }
 #pragma unroll
     for (int it = 0; it < kSortIPT; ++it) {
@@ -195,35 +207,33 @@ __global__ __launch_bounds__(256) void k_radix_scatter(const uint32_t* __restric
             const uint32_t pos = cnt[w][d] + loc[it];
             keys_out[pos] = key[it];
             vals_out[pos] = val[it];
-            if (V2) vals2_out[pos] = val2[it];
         }
     }
 }
 
 template <int BITS>
-static void radix_pass(const uint32_t* kin, const uint32_t* vin, uint32_t* kout, uint32_t* vout, const uint32_t* v2in,
-                       uint32_t* v2out, uint32_t n, int shift, bool idv, uint32_t* hist, uint32_t* totals, int nb,
+static void radix_pass(const uint32_t* kin, const void* vin, uint32_t* kout, void* vout, const uint32_t* gauss_by_slot,
+                       uint32_t n, int shift, bool idv, int vm, uint32_t* hist, uint32_t* totals, int nb,
                        hipStream_t s) {
     constexpr int NDIG = 1 << BITS;
     hipLaunchKernelGGL(k_radix_hist<BITS>, dim3(nb), dim3(256), 0, s, kin, n, shift, hist, nb);
     hipLaunchKernelGGL(k_radix_digit_scan, dim3(NDIG), dim3(256), 0, s, hist, nb, totals);
-#define GS_SCATTER(IDV, V2)                                                                                      \
-    hipLaunchKernelGGL((k_radix_scatter<BITS, IDV, V2>), dim3(nb), dim3(256), 0, s, kin, vin, kout, vout, v2in, \
-                       v2out, n, shift, hist, totals, nb)
-    if (v2in) {
-        if (idv) GS_SCATTER(true, true); else GS_SCATTER(false, true);
-    } else {
-        if (idv) GS_SCATTER(true, false); else GS_SCATTER(false, false);
-    }
+#define GS_SCATTER(IDV, VM)                                                                                   \
+    hipLaunchKernelGGL((k_radix_scatter<BITS, IDV, VM>), dim3(nb), dim3(256), 0, s, kin, vin, kout, vout,     \
+                       gauss_by_slot, n, shift, hist, totals, nb)
+    if (vm == kValPairFirst) GS_SCATTER(true, kValPairFirst);
+    else if (vm == kValPair) GS_SCATTER(false, kValPair);
+    else if (idv) GS_SCATTER(true, kValU32);
+    else GS_SCATTER(false, kValU32);
 #undef GS_SCATTER
 }
 
-static void radix_pass_bits(int bits, const uint32_t* kin, const uint32_t* vin, uint32_t* kout, uint32_t* vout,
-                            const uint32_t* v2in, uint32_t* v2out, uint32_t n, int shift, bool idv, uint32_t* hist,
+static void radix_pass_bits(int bits, const uint32_t* kin, const void* vin, uint32_t* kout, void* vout,
+                            const uint32_t* gauss_by_slot, uint32_t n, int shift, bool idv, int vm, uint32_t* hist,
                             uint32_t* totals, int nb, hipStream_t s) {
     switch (bits) {
 #define GS_CASE(B) \
-    case B: radix_pass<B>(kin, vin, kout, vout, v2in, v2out, n, shift, idv, hist, totals, nb, s); break;
+    case B: radix_pass<B>(kin, vin, kout, vout, gauss_by_slot, n, shift, idv, vm, hist, totals, nb, s); break;
         GS_CASE(1) GS_CASE(2) GS_CASE(3) GS_CASE(4) GS_CASE(5) GS_CASE(6)
         GS_CASE(7) GS_CASE(8) GS_CASE(9) GS_CASE(10) GS_CASE(11)
 #undef GS_CASE
@@ -231,24 +241,45 @@ static void radix_pass_bits(int bits, const uint32_t* kin, const uint32_t* vin, 
     }
 }
 
+// passes over [begin_bit, end_bit) with at most max_pass_bits per pass, bits split evenly
+static int pass_bits(int begin_bit, int end_bit, int max_pass_bits, int p, int& shift) {
+    const int passes = (end_bit - begin_bit + max_pass_bits - 1) / max_pass_bits;
+    const int rem = end_bit - shift;
+    (void)begin_bit;
+    return (rem + (passes - p) - 1) / (passes - p);
+}
+
 int radix_sort_pairs(uint32_t* key0, uint32_t* key1, uint32_t* val0, uint32_t* val1, uint32_t n, int begin_bit,
                      int end_bit, int max_pass_bits, bool identity_vals, uint32_t* hist, uint32_t* totals, int nblocks,
-                     hipStream_t s, uint32_t* v2a, uint32_t* v2b) {
+                     hipStream_t s) {
     uint32_t* k[2] = {key0, key1};
     uint32_t* v[2] = {val0, val1};
-    uint32_t* w[2] = {v2a, v2b};
     int cur = 0;
-    const int total_bits = end_bit - begin_bit;
-    const int passes = (total_bits + max_pass_bits - 1) / max_pass_bits;
+    const int passes = (end_bit - begin_bit + max_pass_bits - 1) / max_pass_bits;
     int shift = begin_bit;
     for (int p = 0; p < passes; ++p) {
-        // split the bits evenly over the passes
-        const int rem = end_bit - shift;
-        const int bits = (rem + (passes - p) - 1) / (passes - p);
-        radix_pass_bits(bits, k[cur], v[cur], k[cur ^ 1], v[cur ^ 1], w[cur], w[cur ^ 1], n, shift,
-                        identity_vals && p == 0, hist, totals, nblocks, s);
+        const int bits = pass_bits(begin_bit, end_bit, max_pass_bits, p, shift);
+        radix_pass_bits(bits, k[cur], v[cur], k[cur ^ 1], v[cur ^ 1], nullptr, n, shift, identity_vals && p == 0,
+                        kValU32, hist, totals, nblocks, s);
         cur ^= 1;
         shift += bits;
+    }
+    return cur;
+}
+
+int tile_sort(uint32_t* key0, uint32_t* key1, uint2* pair0, uint2* pair1, const uint32_t* gauss_by_slot, uint32_t n,
+              int bits, uint32_t* hist, uint32_t* totals, int nblocks, hipStream_t s) {
+    uint32_t* k[2] = {key0, key1};
+    uint2* v[2] = {pair0, pair1};
+    int cur = 0;
+    const int passes = (bits + kMaxSinglePassBits - 1) / kMaxSinglePassBits;
+    int shift = 0;
+    for (int p = 0; p < passes; ++p) {
+        const int b = pass_bits(0, bits, kMaxSinglePassBits, p, shift);
+        radix_pass_bits(b, k[cur], v[cur], k[cur ^ 1], v[cur ^ 1], gauss_by_slot, n, shift, p == 0,
+                        p == 0 ? kValPairFirst : kValPair, hist, totals, nblocks, s);
+        cur ^= 1;
+        shift += b;
     }
     return cur;
 }

@@ -131,7 +131,8 @@ def run_gpu(settings, dL_dpix=None, means3D=None, opacities=None, shs=None, colo
         out["final_T"] = view(img, "image", "final_T", np.float32, W * H)
         out["n_contrib"] = view(img, "image", "n_contrib", np.uint32, W * H)
         out["ranges"] = view(img, "image", "ranges", np.uint32, 2 * tiles)
-        out["point_list"] = view(binning, "binning", "point_list", np.uint32, K) if K else np.zeros(0, np.uint32)
+        # per-tile lists: (Gaussian, slot) pairs; the Gaussian ids are the reference's point_list
+        out["point_list"] = view(binning, "binning", "point_pairs", np.uint32, 2 * K)[0::2] if K else np.zeros(0, np.uint32)
     if dL_dpix is not None:
         g = torch.as_tensor(np.asarray(dL_dpix, np.float32)).to(dev)
         grads = _C.rasterize_gaussians_backward(s.bg.to(dev), m, radii, T(colors_precomp), T(scales), T(rotations),

@@ -47,7 +47,7 @@ def test_buffer_offsets_are_aligned_and_distinct():
     assert geo[-1] < lib.gs_geometry_buffer_size(P)
     img = [lib.gs_buffer_offset(b"image", f, P, W, H, K) for f in (b"final_T", b"n_contrib", b"ranges", b"tile_last")]
     assert all(o >= 0 for o in img) and img[-1] < lib.gs_image_buffer_size(W, H)
-    assert lib.gs_buffer_offset(b"binning", b"point_list", P, W, H, K) >= 0
+    assert lib.gs_buffer_offset(b"binning", b"point_pairs", P, W, H, K) >= 0
     assert lib.gs_buffer_offset(b"geometry", b"nope", P, W, H, K) == -1
 
 
