@@ -287,7 +287,7 @@ def rasterize_gaussians_fused_backward(background, xyz, f_dc, f_rest, colors, ra
         else:
             d_dc = torch.empty_like(f_dc, **opts) if have_sh else None
             d_rest = torch.empty_like(f_rest, **opts) if have_sh and f_rest is not None else None
-        d_col = torch.empty((P, 3), **opts)
+        d_col = None if have_sh else torch.empty((P, 3), **opts)  # not needed when colours come from SH
         d_op = dest("opacity", lambda: torch.empty_like(raw_opacity, **opts), N.ACC_OPACITY)
         d_sc = dest("scaling", lambda: torch.empty((P, 3), **opts), N.ACC_SCALES)
         d_rot = dest("rotation", lambda: torch.empty((P, 4), **opts), N.ACC_ROTATIONS)

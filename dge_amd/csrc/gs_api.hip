@@ -541,7 +541,7 @@ int gs_rasterize_backward_ex(const gs_settings* s, const gs_params* gp, int R, c
             return set_error(GS_ERR_INVALID_ARG, "activation = 1 needs the raw opacities in the backward");
         if (!geom || !img || !radii || !dL_dpix)
             return set_error(GS_ERR_INVALID_ARG, "geometry/image buffers, radii and dL_dpix are required");
-        if (!o->dL_dmeans2D || !o->dL_dcolors || !o->dL_dopacity || !o->dL_dmeans3D || !o->dL_dscales ||
+        if (!o->dL_dmeans2D || !o->dL_dopacity || !o->dL_dmeans3D || !o->dL_dscales ||
             !o->dL_drotations || (gp->M > 1 && o->dL_dsh_dc && !o->dL_dsh_rest))
             return set_error(GS_ERR_INVALID_ARG, "gradient outputs are required");
         if (R > 0 && !binning) return set_error(GS_ERR_INVALID_ARG, "binning buffer is required when num_rendered > 0");

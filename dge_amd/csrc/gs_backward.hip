@@ -306,8 +306,15 @@ __global__ __launch_bounds__(kGB) void k_gauss_bwd(GaussBwdArgs a) {
     // rest floats staged per Gaussian: coefficients 1..15 (degree <= 3 never reads more)
     const int ncol = (a.M - 1) * 3 < kShPitch ? (a.M - 1) * 3 : kShPitch;
     float* const my_sh = s_sh + threadIdx.x * kShPitch;
+    // every independent load first: parameters, the first 8 record flags, then the SH staging
     GaussIn gin{};
     if (vis) gin = load_gauss_in(a, idx);
+    const uint32_t n = vis ? a.tiles_touched[idx] : 0u;
+    const uint32_t first = n ? a.first_slot[idx] : 0u;
+    const uint32_t* flags = reinterpret_cast<const uint32_t*>(a.rec_flags);
+    uint32_t fl[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) fl[u] = (uint32_t)u < n ? flags[first + u] : 0u;
 
     // SH coefficients 1.. of the block, staged with coalesced loads
     if (a.sh.dc && ncol > 0)
@@ -318,25 +325,21 @@ __global__ __launch_bounds__(kGB) void k_gauss_bwd(GaussBwdArgs a) {
     float acc[9];
 #pragma unroll
     for (int f = 0; f < 9; ++f) acc[f] = 0.f;
-    const uint32_t n = vis ? a.tiles_touched[idx] : 0u;
-    if (n) {
-        const uint32_t first = a.first_slot[idx];
-        const uint32_t* flags = reinterpret_cast<const uint32_t*>(a.rec_flags);
-        for (uint32_t k0 = 0; k0 < n; k0 += 8) {
-            uint32_t fl[8];
+    for (uint32_t k0 = 0; k0 < n; k0 += 8) {
+        if (k0) {
 #pragma unroll
             for (int u = 0; u < 8; ++u) fl[u] = k0 + u < n ? flags[first + k0 + u] : 0u;
+        }
 #pragma unroll
-            for (int u = 0; u < 8; ++u) {
+        for (int u = 0; u < 8; ++u) {
 #pragma unroll
-                for (int qd = 0; qd < 4; ++qd) {
-                    if ((fl[u] >> (8 * qd)) & 0xFFu) {
-                        const float4* rec = a.records + 3 * (4 * (size_t)(first + k0 + u) + qd);
-                        const float4 r0 = rec[0], r1 = rec[1], r2 = rec[2];
-                        acc[0] += r0.x; acc[1] += r0.y; acc[2] += r0.z; acc[3] += r0.w;
-                        acc[4] += r1.x; acc[5] += r1.y; acc[6] += r1.z; acc[7] += r1.w;
-                        acc[8] += r2.x;
-                    }
+            for (int qd = 0; qd < 4; ++qd) {
+                if ((fl[u] >> (8 * qd)) & 0xFFu) {
+                    const float4* rec = a.records + 3 * (4 * (size_t)(first + k0 + u) + qd);
+                    const float4 r0 = rec[0], r1 = rec[1], r2 = rec[2];
+                    acc[0] += r0.x; acc[1] += r0.y; acc[2] += r0.z; acc[3] += r0.w;
+                    acc[4] += r1.x; acc[5] += r1.y; acc[6] += r1.z; acc[7] += r1.w;
+                    acc[8] += r2.x;
                 }
             }
         }
@@ -368,9 +371,11 @@ __global__ __launch_bounds__(kGB) void k_gauss_bwd(GaussBwdArgs a) {
         put_out(a.dL_dmeans2D, 3 * (size_t)idx + 1, acc[1], a2);
         put_out(a.dL_dmeans2D, 3 * (size_t)idx + 2, 0.f, a2);
         put_out(a.dL_dopacity, idx, dop, a.acc & GS_ACC_OPACITY);
-        put_out(a.dL_dcolors, 3 * (size_t)idx, acc[6], ac);
-        put_out(a.dL_dcolors, 3 * (size_t)idx + 1, acc[7], ac);
-        put_out(a.dL_dcolors, 3 * (size_t)idx + 2, acc[8], ac);
+        if (a.dL_dcolors) {  // optional (the raw-parameter SH path does not need it)
+            put_out(a.dL_dcolors, 3 * (size_t)idx, acc[6], ac);
+            put_out(a.dL_dcolors, 3 * (size_t)idx + 1, acc[7], ac);
+            put_out(a.dL_dcolors, 3 * (size_t)idx + 2, acc[8], ac);
+        }
     }
 
     // dL_dsh: coefficient 0 per thread, 1.. through LDS (in place) with coalesced stores

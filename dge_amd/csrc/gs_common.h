@@ -248,7 +248,27 @@ __device__ __forceinline__ void sh_rows_load(const float* __restrict__ g, int st
                                              int nrow, int ncol) {
     const int total = (nrow - 1) * stride + ncol;
     const float inv = 1.0f / (float)stride;
-    if ((reinterpret_cast<uintptr_t>(g) & 15) == 0) {
+    if (stride == kShPitch && ncol == kShPitch && (reinterpret_cast<uintptr_t>(g) & 15) == 0) {
+        // dense [P,15,3] rows (the raw-parameter path): the LDS image is the global one
+        constexpr int kV = 12;
+        const float4* g4 = reinterpret_cast<const float4*>(g);
+        float4* l4 = reinterpret_cast<float4*>(lds);
+        const int n4 = total >> 2;
+        for (int b = 0; b < n4; b += kV * NT) {
+            float4 v[kV];
+#pragma unroll
+            for (int u = 0; u < kV; ++u) {
+                const int i = b + u * NT + (int)threadIdx.x;
+                v[u] = i < n4 ? g4[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+#pragma unroll
+            for (int u = 0; u < kV; ++u) {
+                const int i = b + u * NT + (int)threadIdx.x;
+                if (i < n4) l4[i] = v[u];
+            }
+        }
+        for (int e = 4 * n4 + (int)threadIdx.x; e < total; e += NT) lds[e] = g[e];
+    } else if ((reinterpret_cast<uintptr_t>(g) & 15) == 0) {
         constexpr int kV = 12;  // float4 per lane per batch: 256 x 45 floats = 2880 float4
         const float4* g4 = reinterpret_cast<const float4*>(g);
         const int n4 = total >> 2;
@@ -300,7 +320,21 @@ __device__ __forceinline__ void sh_rows_store(float* __restrict__ g, int stride,
         v = col < ncol ? lds[row * kShPitch + col] : 0.f;
         return col < ncol;
     };
-    if ((reinterpret_cast<uintptr_t>(g) & 15) == 0 && stride == ncol) {  // dense rows: float4 stores
+    if (stride == kShPitch && ncol == kShPitch && (reinterpret_cast<uintptr_t>(g) & 15) == 0) {
+        // dense [P,15,3] rows: the LDS image is the global one
+        float4* g4 = reinterpret_cast<float4*>(g);
+        const float4* l4 = reinterpret_cast<const float4*>(lds);
+        const int n4 = total >> 2;
+        for (int i = threadIdx.x; i < n4; i += NT) {
+            float4 v = l4[i];
+            if (accumulate) {
+                const float4 o = g4[i];
+                v = make_float4(o.x + v.x, o.y + v.y, o.z + v.z, o.w + v.w);
+            }
+            g4[i] = v;
+        }
+        for (int e = 4 * n4 + (int)threadIdx.x; e < total; e += NT) put_out(g, e, lds[e], accumulate);
+    } else if ((reinterpret_cast<uintptr_t>(g) & 15) == 0 && stride == ncol) {  // dense rows: float4 stores
         float4* g4 = reinterpret_cast<float4*>(g);
         const int n4 = total >> 2;
         for (int i = threadIdx.x; i < n4; i += NT) {

@@ -138,7 +138,7 @@ typedef struct gs_params {
 
 typedef struct gs_grads {         /* backward outputs, every element written */
     float *dL_dmeans2D;           /* [P,3], z = 0 */
-    float *dL_dcolors;            /* [P,3] */
+    float *dL_dcolors;            /* [P,3]; may be NULL in the _ex entry point (not written) */
     float *dL_dopacity;           /* [P] (w.r.t. the raw opacity when activation = 1) */
     float *dL_dmeans3D;           /* [P,3] */
     float *dL_dcov3D;             /* [P,6] or NULL */
