@@ -37,7 +37,7 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--points", type=int, default=1_000_000)
     ap.add_argument("--width", type=int, default=512)
     ap.add_argument("--height", type=int, default=512)
@@ -50,7 +50,7 @@ def parse():
     return ap.parse_args()
 
 
-def stage_bytes(stage, P, M, K, Kb, HW, tiles):
+def stage_bytes(stage, P, M, K, Kb, HW, tiles, live=None):
     """Algorithmic bytes per launch of each stage."""
     if stage == "preprocess":  # read xyz, scale, rot, opacity, SH; write the geometry record
         return P * (12 + 12 + 16 + 4 + 12 * M) + P * (8 + 16 + 16 + 4 + 1 + 4 + 4 + 4 + 4)
@@ -58,8 +58,15 @@ def stage_bytes(stage, P, M, K, Kb, HW, tiles):
         return K * (4 + 8 + 16 + 16) + HW * 24 + tiles * 8
     if stage == "render_bwd":  # per instance in the backward window: gather 44 B + 48-B record; per pixel 20 B
         return Kb * (4 + 8 + 16 + 16 + 48) + HW * 20 + tiles * 12
-    if stage == "gauss_bwd":  # params + geometry + records in, 9 gradient tensors out
-        return P * (12 + 12 + 16 + 12 * M + 4 + 4 + 4 + 8 + 1) + Kb * (48 + 4) + P * 4 * (3 + 3 + 1 + 3 + 6 + 3 + 4) + P * 12 * M
+    if stage == "gauss_bwd":
+        # every Gaussian: touched byte + radii (4), dL/dmean2D written (12, a fresh tensor);
+        # each live Gaussian (visible with >= 1 record; the others have exactly zero gradients):
+        # params in (xyz 12, scale 12, rot 16, opacity 4, SH 12 M), clamped 1, tiles/first slot 8,
+        # its slots' flags 4 n, its records 48 each, and the 59-float (3+3+4+1+3M) gradient
+        # read-modify-written into the shared .grad (fused accumulation: read + write)
+        L, F, R = live["live"], live["flag_words"], live["records"]
+        return P * (1 + 4 + 12) + L * (12 + 12 + 16 + 4 + 12 * M + 1 + 8) + 4 * F + 48 * R + \
+            L * 2 * 4 * (3 + 3 + 4 + 1 + 3 * M)
     return None
 
 
@@ -104,7 +111,7 @@ def main():
     torch.cuda.synchronize()
 
     # instance counts of this rank's views (deterministic; outside the timed region)
-    Ks, Kbs = [], []
+    Ks, Kbs, lives = [], [], []
     with torch.no_grad():
         for cam in cams:
             from dge_amd.gaussian_renderer import _settings
@@ -118,6 +125,19 @@ def main():
             tl = img[off:off + 4 * tiles].view(torch.int32)
             Ks.append(int(K))
             Kbs.append(int(tl.sum().item()))
+            # one reference-ABI backward: which Gaussians got records (gauss_bwd's live set)
+            _C.rasterize_gaussians_backward(
+                s.bg, scene.get_xyz, radii, torch.empty(0, device=dev), scene.get_scaling, scene.get_rotation, 1.0,
+                torch.empty(0, device=dev), s.viewmatrix, s.projmatrix, s.tanfovx, s.tanfovy, seeds[len(Ks) - 1],
+                scene.get_features, scene.active_sh_degree, s.campos, geom, K, binning, img, False)
+            toff = _native.lib().gs_buffer_offset(b"geometry", b"touched", P, W, H, K)
+            touched = geom[toff:toff + P]
+            toffs = _native.lib().gs_buffer_offset(b"geometry", b"tiles_touched", P, W, H, K)
+            tt = geom[toffs:toffs + 4 * P].view(torch.int32)
+            foff = _native.lib().gs_buffer_offset(b"binning", b"rec_flags", P, W, H, K)
+            recs = int((binning[foff:foff + 4 * K] != 0).sum().item()) if K else 0
+            lv = (touched != 0) & (radii > 0)
+            lives.append({"live": int(lv.sum().item()), "flag_words": int(tt[lv].sum().item()), "records": recs})
     torch.cuda.synchronize()
 
     if not args.no_profile:
@@ -161,7 +181,8 @@ def main():
                 stages[name] = {"avg_ms": ms / cnt, "launches": cnt,
                                 "share": ms / max(1e-9, sum(v[0] for v in prof.values()))}
         dom = max(stages, key=lambda n: stages[n]["avg_ms"] * stages[n]["launches"])
-        b = stage_bytes(dom, P, M, K, Kb, HW, tiles)
+        live = {k: float(np.mean([d[k] for d in lives])) for k in lives[0]}
+        b = stage_bytes(dom, P, M, K, Kb, HW, tiles, live)
         if b is not None:
             achieved = b / (stages[dom]["avg_ms"] * 1e-3) / 1e9
             roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
@@ -198,6 +219,8 @@ def main():
                        "gaussians": P, "width": W, "height": H, "views_per_rank": V,
                        "parallelism": f"views sharded x{world}" + (", RCCL grad all-reduce" if world > 1 else "")},
             "num_rendered_mean": int(K),
+            "live_gaussians_mean": int(np.mean([d["live"] for d in lives])),
+            "gradient_records_mean": int(np.mean([d["records"] for d in lives])),
             "backward_window_instances_mean": int(Kb),
             "hbm_gbps_algorithmic_whole_render": round(B_render * value / world / 1e9, 2),
             "stages_ms": {k: round(v["avg_ms"], 4) for k, v in stages.items()},

@@ -417,6 +417,7 @@ long long gs_buffer_offset(const char* buffer, const char* field, int P, int wid
         if (!strcmp(field, "rgbd")) return (long long)L.rgbd;
         if (!strcmp(field, "tiles_touched")) return (long long)L.tiles_touched;
         if (!strcmp(field, "clamped")) return (long long)L.clamped;
+        if (!strcmp(field, "touched")) return (long long)L.touched;
         if (!strcmp(field, "radii")) return (long long)L.radii;
         if (!strcmp(field, "first_slot")) return (long long)L.first_slot;
     } else if (!strcmp(buffer, "image")) {
@@ -552,6 +553,10 @@ int gs_rasterize_backward_ex(const gs_settings* s, const gs_params* gp, int R, c
         const BinLayout bl = bin_layout(R, g.tiles);
         float4* records = R > 0 ? at<float4>(const_cast<void*>(binning), bl.records) : nullptr;
         uint8_t* rec_flags = R > 0 ? at<uint8_t>(const_cast<void*>(binning), bl.rec_flags) : nullptr;
+        // per-Gaussian "has a record" bytes: k_gauss_bwd skips every Gaussian without one (all of
+        // its gradients are zero), which is most of them (occluded behind saturated pixels)
+        uint8_t* touched = at<uint8_t>(const_cast<void*>(geom), gl.touched);
+        GS_HIP(hipMemsetAsync(touched, 0, (size_t)P, stream));
         if (R > 0) {
             GS_HIP(hipMemsetAsync(rec_flags, 0, 4 * (size_t)R, stream));
             RenderBwdArgs rb;
@@ -571,6 +576,7 @@ int gs_rasterize_backward_ex(const gs_settings* s, const gs_params* gp, int R, c
             rb.dL_dpix = dL_dpix;
             rb.records = records;
             rb.rec_flags = rec_flags;
+            rb.touched = touched;
             rb.diag = diag_buffer(1, kDiagWords * (size_t)g.tiles * 4 * kSegMax);
             { StageScope sc(ST_RENDER_BWD, stream); launch_render_backward(rb, stream); }
             GS_LAUNCHED("render backward");
@@ -593,6 +599,9 @@ int gs_rasterize_backward_ex(const gs_settings* s, const gs_params* gp, int R, c
         ga.first_slot = at<uint32_t>(geom, gl.first_slot);
         ga.clamped = at<uint8_t>(geom, gl.clamped);
         ga.rec_flags = rec_flags;
+        ga.touched = touched;
+        ga.live_count = at<uint32_t>(const_cast<void*>(geom), gl.live_count);
+        ga.live_list = at<uint32_t>(const_cast<void*>(geom), gl.live_list);
         ga.records = records;
         ga.dL_dmeans2D = o->dL_dmeans2D; ga.dL_dcolors = o->dL_dcolors; ga.dL_dopacity = o->dL_dopacity;
         ga.dL_dmeans3D = o->dL_dmeans3D; ga.dL_dcov3D = o->dL_dcov3D;

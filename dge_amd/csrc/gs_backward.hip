@@ -167,10 +167,20 @@ __device__ __forceinline__ GaussIn load_gauss_in(const GaussBwdArgs& a, int idx)
     return g;
 }
 
-// The per-Gaussian chain of a visible Gaussian (geometry gradients written
-// here; SH gradients returned in dsh).
-__device__ __forceinline__ void gauss_bwd_visible(const GaussBwdArgs& a, int idx, const GaussIn& gin, const float (&acc)[9], float& dop,
-                                                  const float* my_sh, float (&dsh)[48]) {
+// Gradients of one live Gaussian w.r.t. its inputs, in registers: they are
+// committed afterwards with every load of an accumulated output issued before
+// the first store (see commit_outputs).
+struct GaussOut {
+    f3 dmean;
+    float dcov[6];
+    float dscale[3];
+    float4 drot;
+};
+
+// The per-Gaussian chain of a live Gaussian (geometry gradients into `o`,
+// SH gradients into dsh, opacity gradient chained into dop).
+__device__ __forceinline__ void gauss_bwd_visible(const GaussBwdArgs& a, const GaussIn& gin, const float (&acc)[9],
+                                                  float& dop, const float* my_sh, float (&dsh)[48], GaussOut& o) {
     const float* v = a.view;
     const float* pm = a.proj;
     const f3 m = gin.m;
@@ -255,13 +265,9 @@ __device__ __forceinline__ void gauss_bwd_visible(const GaussBwdArgs& a, int idx
     // ---- SH -> RGB backward ----
     if (a.sh.dc)
         dmean = dmean + sh_backward(a.D, m, ld3(a.campos), my_sh, gin.clamped, mk3(acc[6], acc[7], acc[8]), dsh);
-    const bool am = a.acc & GS_ACC_MEANS3D;
-    put_out(a.dL_dmeans3D, 3 * (size_t)idx, dmean.x, am);
-    put_out(a.dL_dmeans3D, 3 * (size_t)idx + 1, dmean.y, am);
-    put_out(a.dL_dmeans3D, 3 * (size_t)idx + 2, dmean.z, am);
-    if (a.dL_dcov3D)
+    o.dmean = dmean;
 #pragma unroll
-        for (int k = 0; k < 6; ++k) put_out(a.dL_dcov3D, 6 * (size_t)idx + k, dcov[k], a.acc & GS_ACC_COV3D);
+    for (int k = 0; k < 6; ++k) o.dcov[k] = dcov[k];
     if (a.activation) {  // opacity = sigmoid(raw): torch's sigmoid backward g * (1 - y) * y
         const float y = act_sigmoid(gin.opacity);
         dop = acc[5] * ((1.0f - y) * y);
@@ -277,135 +283,278 @@ __device__ __forceinline__ void gauss_bwd_visible(const GaussBwdArgs& a, int idx
             ds[2] *= scale.z;
             g4 = act_normalize_bwd(rot, rot_len, g4);
         }
-        const bool as = a.acc & GS_ACC_SCALES;
-        put_out(a.dL_dscales, 3 * (size_t)idx, ds[0], as);
-        put_out(a.dL_dscales, 3 * (size_t)idx + 1, ds[1], as);
-        put_out(a.dL_dscales, 3 * (size_t)idx + 2, ds[2], as);
-        float4* r4 = reinterpret_cast<float4*>(a.dL_drot + 4 * (size_t)idx);
-        if (a.acc & GS_ACC_ROTATIONS) {
-            const float4 o4 = *r4;
-            g4 = make_float4(o4.x + g4.x, o4.y + g4.y, o4.z + g4.z, o4.w + g4.w);
-        }
-        *r4 = g4;
+        o.dscale[0] = ds[0];
+        o.dscale[1] = ds[1];
+        o.dscale[2] = ds[2];
+        o.drot = g4;
     } else {
-        if (!(a.acc & GS_ACC_SCALES))
-#pragma unroll
-            for (int k = 0; k < 3; ++k) a.dL_dscales[3 * (size_t)idx + k] = 0.f;
-        if (!(a.acc & GS_ACC_ROTATIONS))
-            *reinterpret_cast<float4*>(a.dL_drot + 4 * (size_t)idx) = make_float4(0.f, 0.f, 0.f, 0.f);
+        o.dscale[0] = o.dscale[1] = o.dscale[2] = 0.f;
+        o.drot = make_float4(0.f, 0.f, 0.f, 0.f);
     }
 }
 
-__global__ __launch_bounds__(kGB) void k_gauss_bwd(GaussBwdArgs a) {
-    __shared__ float s_sh[kGB * kShPitch];
+// Writes (or adds, per GS_ACC_* bit) one live Gaussian's per-Gaussian outputs:
+// all loads of the accumulated ones first, then all stores, so the ~20
+// scattered read-modify-writes overlap instead of forming a dependent chain.
+__device__ __forceinline__ void commit_outputs(const GaussBwdArgs& a, int idx, const float (&acc)[9], float dop,
+                                               const float (&dsh)[48], const GaussOut& o) {
+    const uint32_t f = a.acc;
+    const size_t i3 = 3 * (size_t)idx;
+    float* d0 = a.dsh.dc ? a.dsh.dc + (size_t)idx * a.dsh.dc_stride : nullptr;
+    float4* r4 = reinterpret_cast<float4*>(a.dL_drot + 4 * (size_t)idx);
+    float om2[2] = {0.f, 0.f}, oop = 0.f, ocol[3] = {0.f, 0.f, 0.f}, om3[3] = {0.f, 0.f, 0.f};
+    float ocov[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, osc[3] = {0.f, 0.f, 0.f}, odc[3] = {0.f, 0.f, 0.f};
+    float4 orot = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (f & GS_ACC_MEANS2D) { om2[0] = a.dL_dmeans2D[i3]; om2[1] = a.dL_dmeans2D[i3 + 1]; }
+    if (f & GS_ACC_OPACITY) oop = a.dL_dopacity[idx];
+    if (a.dL_dcolors && (f & GS_ACC_COLORS))
+#pragma unroll
+        for (int k = 0; k < 3; ++k) ocol[k] = a.dL_dcolors[i3 + k];
+    if (f & GS_ACC_MEANS3D)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) om3[k] = a.dL_dmeans3D[i3 + k];
+    if (a.dL_dcov3D && (f & GS_ACC_COV3D))
+#pragma unroll
+        for (int k = 0; k < 6; ++k) ocov[k] = a.dL_dcov3D[6 * (size_t)idx + k];
+    if (f & GS_ACC_SCALES)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) osc[k] = a.dL_dscales[i3 + k];
+    if (f & GS_ACC_ROTATIONS) orot = *r4;
+    if (d0 && (f & GS_ACC_SH))
+#pragma unroll
+        for (int k = 0; k < 3; ++k) odc[k] = d0[k];
+
+    a.dL_dmeans2D[i3] = om2[0] + acc[0];
+    a.dL_dmeans2D[i3 + 1] = om2[1] + acc[1];
+    if (!(f & GS_ACC_MEANS2D)) a.dL_dmeans2D[i3 + 2] = 0.f;
+    a.dL_dopacity[idx] = oop + dop;
+    if (a.dL_dcolors)  // optional (the raw-parameter SH path does not need it)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) a.dL_dcolors[i3 + k] = ocol[k] + acc[6 + k];
+    a.dL_dmeans3D[i3] = om3[0] + o.dmean.x;
+    a.dL_dmeans3D[i3 + 1] = om3[1] + o.dmean.y;
+    a.dL_dmeans3D[i3 + 2] = om3[2] + o.dmean.z;
+    if (a.dL_dcov3D)
+#pragma unroll
+        for (int k = 0; k < 6; ++k) a.dL_dcov3D[6 * (size_t)idx + k] = ocov[k] + o.dcov[k];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) a.dL_dscales[i3 + k] = osc[k] + o.dscale[k];
+    *r4 = make_float4(orot.x + o.drot.x, orot.y + o.drot.y, orot.z + o.drot.z, orot.w + o.drot.w);
+    if (d0) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) d0[k] = odc[k] + dsh[k];
+        // coefficients beyond the 16 a degree-3 evaluation uses get zero gradient
+        if (!(f & GS_ACC_SH)) {
+            float* dr = a.dsh.rest + (size_t)idx * a.dsh.rest_stride;
+            for (int k = kShPitch; k < (a.M - 1) * 3; ++k) dr[k] = 0.f;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------
+// Pass 1 (all P, coalesced): the live set = visible Gaussians with at least
+// one gradient record.  Every other Gaussian has exactly zero gradients: its
+// overwritten outputs get zeros here, its accumulated ones are left alone.
+// Each 256-Gaussian block compacts its live indices in place (no atomics):
+// live_list[256 b + i], i < live_count[b].
+// ---------------------------------------------------------------------
+__global__ __launch_bounds__(kGB) void k_gauss_live(GaussBwdArgs a) {
+    __shared__ uint32_t s_wave[kGB / 64];
+    __shared__ uint8_t s_live[kGB];
     const int idx0 = blockIdx.x * kGB;
     const int idx = idx0 + threadIdx.x;
     const int nrow = a.P - idx0 < kGB ? a.P - idx0 : kGB;
     const bool in = idx < a.P;
-    const bool vis = in && a.radii[idx] > 0;
+    const bool live = in && a.touched[idx] && a.radii[idx] > 0;
+    s_live[threadIdx.x] = live;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint64_t bm = __ballot(live);
+    if (lane == 0) s_wave[wave] = (uint32_t)__popcll(bm);
+    __syncthreads();
+    uint32_t off = 0, total = 0;
+#pragma unroll
+    for (int w = 0; w < kGB / 64; ++w) {
+        off += w < wave ? s_wave[w] : 0u;
+        total += s_wave[w];
+    }
+    if (live) a.live_list[idx0 + off + (uint32_t)__popcll(bm & lanemask_lt())] = (uint32_t)idx;
+    if (threadIdx.x == 0) a.live_count[blockIdx.x] = total;
+
+    // zeros for the overwritten outputs of the dead Gaussians
+    const uint32_t acc = a.acc;
+    if (in && !live) {
+        if (!(acc & GS_ACC_MEANS2D))
+#pragma unroll
+            for (int k = 0; k < 3; ++k) a.dL_dmeans2D[3 * (size_t)idx + k] = 0.f;
+        if (!(acc & GS_ACC_OPACITY)) a.dL_dopacity[idx] = 0.f;
+        if (a.dL_dcolors && !(acc & GS_ACC_COLORS))
+#pragma unroll
+            for (int k = 0; k < 3; ++k) a.dL_dcolors[3 * (size_t)idx + k] = 0.f;
+        if (!(acc & GS_ACC_MEANS3D))
+#pragma unroll
+            for (int k = 0; k < 3; ++k) a.dL_dmeans3D[3 * (size_t)idx + k] = 0.f;
+        if (a.dL_dcov3D && !(acc & GS_ACC_COV3D))
+#pragma unroll
+            for (int k = 0; k < 6; ++k) a.dL_dcov3D[6 * (size_t)idx + k] = 0.f;
+        if (!(acc & GS_ACC_SCALES))
+#pragma unroll
+            for (int k = 0; k < 3; ++k) a.dL_dscales[3 * (size_t)idx + k] = 0.f;
+        if (!(acc & GS_ACC_ROTATIONS))
+            *reinterpret_cast<float4*>(a.dL_drot + 4 * (size_t)idx) = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (a.dsh.dc && !(acc & GS_ACC_SH)) {
+            float* d0 = a.dsh.dc + (size_t)idx * a.dsh.dc_stride;
+            d0[0] = 0.f; d0[1] = 0.f; d0[2] = 0.f;
+        }
+    }
+    if (a.dsh.dc && !(acc & GS_ACC_SH) && a.M > 1) {
+        // rest rows of the block's dead Gaussians, coalesced over the block's region
+        __syncthreads();  // s_live
+        const int ncol = (a.M - 1) * 3;
+        const int stride = a.dsh.rest_stride;
+        float* g = a.dsh.rest + (size_t)idx0 * stride;
+        const int total_f = (nrow - 1) * stride + ncol;
+        for (int e = threadIdx.x; e < total_f; e += kGB) {
+            const int row = e / stride, col = e - row * stride;
+            if (col < ncol && !s_live[row]) g[e] = 0.f;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------
+// Pass 2: the live Gaussians of kLiveGroup consecutive pass-1 blocks, one per
+// thread, in batches of 256.  Their rows are scattered, so the SH rows move
+// through LDS with a flat block-wide index (consecutive lanes touch
+// consecutive floats of one or two rows) instead of one 180-B row per lane,
+// and every read-modify-write batch issues its loads before its stores.
+// ---------------------------------------------------------------------
+constexpr int kLiveGroup = 8;
+
+__global__ __launch_bounds__(kGB) void k_gauss_bwd_live(GaussBwdArgs a) {
+    __shared__ float s_sh[kGB * kShPitch];
+    __shared__ uint32_t s_gid[kGB];
+    __shared__ uint32_t s_pre[kLiveGroup + 1];
+    const int nsrc = (a.P + kGB - 1) / kGB;
+    const int sb0 = blockIdx.x * kLiveGroup;
+    if (threadIdx.x < kLiveGroup) s_pre[threadIdx.x + 1] = sb0 + (int)threadIdx.x < nsrc ? a.live_count[sb0 + threadIdx.x] : 0u;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        s_pre[0] = 0;
+#pragma unroll
+        for (int g = 1; g <= kLiveGroup; ++g) s_pre[g] += s_pre[g - 1];
+    }
+    __syncthreads();
+    const uint32_t count = s_pre[kLiveGroup];
     // rest floats staged per Gaussian: coefficients 1..15 (degree <= 3 never reads more)
     const int ncol = (a.M - 1) * 3 < kShPitch ? (a.M - 1) * 3 : kShPitch;
+    const float inv_ncol = ncol > 0 ? 1.0f / (float)ncol : 0.f;
     float* const my_sh = s_sh + threadIdx.x * kShPitch;
-    // every independent load first: parameters, the first 8 record flags, then the SH staging
-    GaussIn gin{};
-    if (vis) gin = load_gauss_in(a, idx);
-    const uint32_t n = vis ? a.tiles_touched[idx] : 0u;
-    const uint32_t first = n ? a.first_slot[idx] : 0u;
-    const uint32_t* flags = reinterpret_cast<const uint32_t*>(a.rec_flags);
-    uint32_t fl[8];
+    const bool ash = a.acc & GS_ACC_SH;
+    for (uint32_t base = 0; base < count; base += kGB) {
+        const uint32_t j = base + threadIdx.x;
+        const int nrow = count - base < (uint32_t)kGB ? (int)(count - base) : kGB;
+        const bool ok = j < count;
+        int g = 0;
 #pragma unroll
-    for (int u = 0; u < 8; ++u) fl[u] = (uint32_t)u < n ? flags[first + u] : 0u;
-
-    // SH coefficients 1.. of the block, staged with coalesced loads
-    if (a.sh.dc && ncol > 0)
-        sh_rows_load<kGB>(a.sh.rest + (size_t)idx0 * a.sh.rest_stride, a.sh.rest_stride, s_sh, nrow, ncol);
-
-    // sum of this Gaussian's records: one per (slot, quadrant) the backward
-    // replay kept, flagged per slot; slots in emission order = tile order
-    float acc[9];
+        for (int q = 1; q < kLiveGroup; ++q) g += j >= s_pre[q] ? 1 : 0;
+        const int idx = ok ? (int)a.live_list[(size_t)(sb0 + g) * kGB + (j - s_pre[g])] : 0;
+        s_gid[threadIdx.x] = (uint32_t)idx;
+        // independent loads first: parameters, the first 8 record flags
+        GaussIn gin{};
+        if (ok) gin = load_gauss_in(a, idx);
+        const uint32_t n = ok ? a.tiles_touched[idx] : 0u;
+        const uint32_t first = n ? a.first_slot[idx] : 0u;
+        const uint32_t* flags = reinterpret_cast<const uint32_t*>(a.rec_flags);
+        uint32_t fl[8];
 #pragma unroll
-    for (int f = 0; f < 9; ++f) acc[f] = 0.f;
-    for (uint32_t k0 = 0; k0 < n; k0 += 8) {
-        if (k0) {
+        for (int u = 0; u < 8; ++u) fl[u] = (uint32_t)u < n ? flags[first + u] : 0u;
+        __syncthreads();  // s_gid
+        const int total = nrow * ncol;
+        constexpr int kV = 12;
+        if (a.sh.dc && ncol > 0) {
+            for (int b = 0; b < total; b += kV * kGB) {
+                float v[kV];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) fl[u] = k0 + u < n ? flags[first + k0 + u] : 0u;
-        }
+                for (int u = 0; u < kV; ++u) {
+                    const int e = b + u * kGB + (int)threadIdx.x;
+                    const int row = (int)(((float)e + 0.5f) * inv_ncol), col = e - row * ncol;
+                    v[u] = e < total ? a.sh.rest[(size_t)s_gid[row] * a.sh.rest_stride + col] : 0.f;
+                }
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
-#pragma unroll
-            for (int qd = 0; qd < 4; ++qd) {
-                if ((fl[u] >> (8 * qd)) & 0xFFu) {
-                    const float4* rec = a.records + 3 * (4 * (size_t)(first + k0 + u) + qd);
-                    const float4 r0 = rec[0], r1 = rec[1], r2 = rec[2];
-                    acc[0] += r0.x; acc[1] += r0.y; acc[2] += r0.z; acc[3] += r0.w;
-                    acc[4] += r1.x; acc[5] += r1.y; acc[6] += r1.z; acc[7] += r1.w;
-                    acc[8] += r2.x;
+                for (int u = 0; u < kV; ++u) {
+                    const int e = b + u * kGB + (int)threadIdx.x;
+                    const int row = (int)(((float)e + 0.5f) * inv_ncol), col = e - row * ncol;
+                    if (e < total) s_sh[row * kShPitch + col] = v[u];
                 }
             }
         }
-    }
-    __syncthreads();  // SH staged
-
-    float dsh[48];
+        // sum of this Gaussian's records: one per (slot, quadrant) the backward
+        // replay kept, flagged per slot; slots in emission order = tile order
+        float acc[9];
 #pragma unroll
-    for (int k = 0; k < 48; ++k) dsh[k] = 0.f;
-    float dop = acc[5];  // w.r.t. opacity; chained through the sigmoid below when activation = 1
-    if (in && !vis) {
-        if (a.activation) dop = 0.f;  // d sigmoid of a zero gradient
-        if (!(a.acc & GS_ACC_MEANS3D))
+        for (int f = 0; f < 9; ++f) acc[f] = 0.f;
+        for (uint32_t k0 = 0; k0 < n; k0 += 8) {
+            if (k0) {
 #pragma unroll
-            for (int k = 0; k < 3; ++k) a.dL_dmeans3D[3 * (size_t)idx + k] = 0.f;
-        if (!(a.acc & GS_ACC_SCALES))
+                for (int u = 0; u < 8; ++u) fl[u] = k0 + u < n ? flags[first + k0 + u] : 0u;
+            }
 #pragma unroll
-            for (int k = 0; k < 3; ++k) a.dL_dscales[3 * (size_t)idx + k] = 0.f;
-        if (a.dL_dcov3D && !(a.acc & GS_ACC_COV3D))
+            for (int u = 0; u < 8; ++u) {
 #pragma unroll
-            for (int k = 0; k < 6; ++k) a.dL_dcov3D[6 * (size_t)idx + k] = 0.f;
-        if (!(a.acc & GS_ACC_ROTATIONS))
-            *reinterpret_cast<float4*>(a.dL_drot + 4 * (size_t)idx) = make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-    if (vis) gauss_bwd_visible(a, idx, gin, acc, dop, my_sh, dsh);
-    if (in) {
-        const bool a2 = a.acc & GS_ACC_MEANS2D, ac = a.acc & GS_ACC_COLORS;
-        put_out(a.dL_dmeans2D, 3 * (size_t)idx, acc[0], a2);
-        put_out(a.dL_dmeans2D, 3 * (size_t)idx + 1, acc[1], a2);
-        put_out(a.dL_dmeans2D, 3 * (size_t)idx + 2, 0.f, a2);
-        put_out(a.dL_dopacity, idx, dop, a.acc & GS_ACC_OPACITY);
-        if (a.dL_dcolors) {  // optional (the raw-parameter SH path does not need it)
-            put_out(a.dL_dcolors, 3 * (size_t)idx, acc[6], ac);
-            put_out(a.dL_dcolors, 3 * (size_t)idx + 1, acc[7], ac);
-            put_out(a.dL_dcolors, 3 * (size_t)idx + 2, acc[8], ac);
+                for (int qd = 0; qd < 4; ++qd) {
+                    if ((fl[u] >> (8 * qd)) & 0xFFu) {
+                        const float4* rec = a.records + 3 * (4 * (size_t)(first + k0 + u) + qd);
+                        const float4 r0 = rec[0], r1 = rec[1], r2 = rec[2];
+                        acc[0] += r0.x; acc[1] += r0.y; acc[2] += r0.z; acc[3] += r0.w;
+                        acc[4] += r1.x; acc[5] += r1.y; acc[6] += r1.z; acc[7] += r1.w;
+                        acc[8] += r2.x;
+                    }
+                }
+            }
         }
-    }
+        __syncthreads();  // SH staged
 
-    // dL_dsh: coefficient 0 per thread, 1.. through LDS (in place) with coalesced stores
-    if (a.dsh.dc) {
-        if (in) {
-            float* d0 = a.dsh.dc + (size_t)idx * a.dsh.dc_stride;
-            const bool ash = a.acc & GS_ACC_SH;
-            put_out(d0, 0, dsh[0], ash);
-            put_out(d0, 1, dsh[1], ash);
-            put_out(d0, 2, dsh[2], ash);
-            // coefficients beyond the 16 a degree-3 evaluation uses get zero gradient
-            float* dr = a.dsh.rest + (size_t)idx * a.dsh.rest_stride;
-            if (!ash)
-                for (int k = kShPitch; k < (a.M - 1) * 3; ++k) dr[k] = 0.f;
-        }
-        if (ncol > 0) {
+        float dsh[48];
+#pragma unroll
+        for (int k = 0; k < 48; ++k) dsh[k] = 0.f;
+        float dop = acc[5];  // w.r.t. opacity; chained through the sigmoid when activation = 1
+        GaussOut o;
+        if (ok) gauss_bwd_visible(a, gin, acc, dop, my_sh, dsh, o);
+        if (a.dsh.dc && ncol > 0) {
             __syncthreads();  // every row read before any row is overwritten
 #pragma unroll
             for (int k = 0; k < 45; ++k)
                 if (k < ncol) my_sh[k] = dsh[3 + k];
-            __syncthreads();
-            sh_rows_store<kGB>(a.dsh.rest + (size_t)idx0 * a.dsh.rest_stride, a.dsh.rest_stride, s_sh, nrow, ncol,
-                          a.acc & GS_ACC_SH);
         }
+        if (ok) commit_outputs(a, idx, acc, dop, dsh, o);
+        // dL_dsh rest rows: through LDS (in place), flat block-wide batches, loads before stores
+        if (a.dsh.dc && ncol > 0) {
+            __syncthreads();
+            for (int b = 0; b < total; b += kV * kGB) {
+                float old[kV];
+#pragma unroll
+                for (int u = 0; u < kV; ++u) {
+                    const int e = b + u * kGB + (int)threadIdx.x;
+                    const int row = (int)(((float)e + 0.5f) * inv_ncol), col = e - row * ncol;
+                    old[u] = ash && e < total ? a.dsh.rest[(size_t)s_gid[row] * a.dsh.rest_stride + col] : 0.f;
+                }
+#pragma unroll
+                for (int u = 0; u < kV; ++u) {
+                    const int e = b + u * kGB + (int)threadIdx.x;
+                    const int row = (int)(((float)e + 0.5f) * inv_ncol), col = e - row * ncol;
+                    if (e < total)
+                        a.dsh.rest[(size_t)s_gid[row] * a.dsh.rest_stride + col] = old[u] + s_sh[row * kShPitch + col];
+                }
+            }
+        }
+        __syncthreads();  // s_gid / s_sh reused by the next batch
     }
 }
 
 void launch_gauss_backward(const GaussBwdArgs& a, hipStream_t s) {
     if (a.P <= 0) return;
-    hipLaunchKernelGGL(k_gauss_bwd, dim3(div_up(a.P, kGB)), dim3(kGB), 0, s, a);
+    const int blocks = div_up(a.P, kGB);
+    hipLaunchKernelGGL(k_gauss_live, dim3(blocks), dim3(kGB), 0, s, a);
+    hipLaunchKernelGGL(k_gauss_bwd_live, dim3(div_up(blocks, kLiveGroup)), dim3(kGB), 0, s, a);
 }
 
 }  // namespace gs

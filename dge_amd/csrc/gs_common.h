@@ -243,9 +243,18 @@ __device__ __forceinline__ void sh_element_to_lds(float* __restrict__ lds, int e
     if (col < ncol) lds[row * kShPitch + col] = v;
 }
 
+// Dense rows: does float4 i of the block's region hold a float of a live row?
+// (a float4 spans at most two rows of 45 floats)
+__device__ __forceinline__ bool dense_f4_live(const uint8_t* live, int i) {
+    return !live || (live[(4 * i) / kShPitch] | live[(4 * i + 3) / kShPitch]);
+}
+
+// `live` (LDS, one byte per row, nullable): rows whose Gaussian needs its SH;
+// the dense path skips the loads of the other rows (their LDS rows are left
+// undefined: the caller does not read them).
 template <int NT>
 __device__ __forceinline__ void sh_rows_load(const float* __restrict__ g, int stride, float* __restrict__ lds,
-                                             int nrow, int ncol) {
+                                             int nrow, int ncol, const uint8_t* live = nullptr) {
     const int total = (nrow - 1) * stride + ncol;
     const float inv = 1.0f / (float)stride;
     if (stride == kShPitch && ncol == kShPitch && (reinterpret_cast<uintptr_t>(g) & 15) == 0) {
@@ -259,7 +268,7 @@ __device__ __forceinline__ void sh_rows_load(const float* __restrict__ g, int st
 #pragma unroll
             for (int u = 0; u < kV; ++u) {
                 const int i = b + u * NT + (int)threadIdx.x;
-                v[u] = i < n4 ? g4[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+                v[u] = i < n4 && dense_f4_live(live, i) ? g4[i] : make_float4(0.f, 0.f, 0.f, 0.f);
             }
 #pragma unroll
             for (int u = 0; u < kV; ++u) {
@@ -309,9 +318,11 @@ __device__ __forceinline__ void sh_rows_load(const float* __restrict__ g, int st
     }
 }
 
+// With `accumulate`, the dense path skips float4s of rows that are not `live`
+// (their gradient is zero: adding it is a no-op).
 template <int NT>
 __device__ __forceinline__ void sh_rows_store(float* __restrict__ g, int stride, const float* __restrict__ lds,
-                                              int nrow, int ncol, bool accumulate) {
+                                              int nrow, int ncol, bool accumulate, const uint8_t* live = nullptr) {
     const int total = (nrow - 1) * stride + ncol;
     const float inv = 1.0f / (float)stride;
     auto at = [&](int e, float& v) {
@@ -326,6 +337,7 @@ __device__ __forceinline__ void sh_rows_store(float* __restrict__ g, int stride,
         const float4* l4 = reinterpret_cast<const float4*>(lds);
         const int n4 = total >> 2;
         for (int i = threadIdx.x; i < n4; i += NT) {
+            if (accumulate && !dense_f4_live(live, i)) continue;
             float4 v = l4[i];
             if (accumulate) {
                 const float4 o = g4[i];

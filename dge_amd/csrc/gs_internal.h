@@ -61,7 +61,8 @@ inline TileSortPlan tile_sort_plan(int num_tiles) {
 }
 
 struct GeomLayout {
-    size_t means2D, conic_opacity, rgbd, tiles_touched, clamped, radii, first_slot;
+    size_t means2D, conic_opacity, rgbd, tiles_touched, clamped, touched, live_count, live_list, radii, first_slot;
+    // live_count: one u32 per 256-Gaussian block (k_gauss_live); live_list: block-local compacted ids
     size_t key0, key1, val0, val1, sort_hist, sort_totals, scan_sums, counters, total;
     int sort_blocks, scan_blocks;
 };
@@ -76,6 +77,9 @@ inline GeomLayout geom_layout(int P) {
     L.rgbd = o; o = align_up(o + 16 * p);
     L.tiles_touched = o; o = align_up(o + 4 * p);
     L.clamped = o; o = align_up(o + 1 * p);
+    L.touched = o; o = align_up(o + 1 * p);
+    L.live_count = o; o = align_up(o + 4 * (size_t)div_up((long long)p, 256));
+    L.live_list = o; o = align_up(o + 4 * p);
     L.radii = o; o = align_up(o + 4 * p);
     L.first_slot = o; o = align_up(o + 4 * p);
     L.key0 = o; o = align_up(o + 4 * p);
@@ -272,6 +276,7 @@ struct RenderBwdArgs {
     const float* dL_dpix;
     float4* records;     // [4*K][3] float4: one record per (slot, quadrant), kept entries only
     uint8_t* rec_flags;  // [4*K] set to 1 with each record (zeroed before the launch)
+    uint8_t* touched;    // [P] set to 1 for every Gaussian that got a record (zeroed before the launch)
     uint64_t* diag;   // optional [tiles*4][kDiagWords] (see diag_buffer)
 };
 void launch_render_backward(const RenderBwdArgs& a, hipStream_t s);
@@ -289,6 +294,9 @@ struct GaussBwdArgs {
     const uint32_t* first_slot;
     const uint8_t* clamped;
     const uint8_t* rec_flags;  // [4*K] nonzero: record (slot, quadrant) was written
+    const uint8_t* touched;    // [P] nonzero: the Gaussian has at least one record
+    uint32_t* live_list;       // [P] k_gauss_live: block b's live Gaussians at [256 b, 256 b + live_count[b])
+    uint32_t* live_count;      // [P/256] live Gaussians per 256-Gaussian block
     const float4* records;     // [4*K][3] float4 by slot
     float *dL_dmeans2D, *dL_dcolors, *dL_dopacity, *dL_dmeans3D, *dL_dcov3D, *dL_dscales, *dL_drot;
     uint32_t acc;  // GS_ACC_* bits: add into the output instead of overwriting

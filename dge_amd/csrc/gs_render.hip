@@ -503,7 +503,7 @@ __global__ __launch_bounds__(64, 4) void k_render_bwd(RenderBwdArgs a) {
         for (int i = 0; i < 4; ++i) {
             cur[i] = gather_entry(a.means2D, a.conic_opacity, a.rgbd, pairs[i].x);
             slots[i] = pairs[i].y;  // the current round's slots are already staged
-        }
+            }
         round_pairs(r + 2, pairs);
         diag_kept += nk;
         diag_rounds += 1;
@@ -524,6 +524,7 @@ __global__ __launch_bounds__(64, 4) void k_render_bwd(RenderBwdArgs a) {
                 const size_t rec = 4 * (size_t)s_slot[kw] + quad;
                 finish_record(s_co[kw], S, ddelx_dx, ddely_dy, a.records + 3 * rec);
                 a.rec_flags[rec] = 1;
+                a.touched[a.point_pairs[range.x + s_pos[kw]].x] = 1;  // (an L2 hit: this round's ids)
             }
         }
         if (a.diag) c_replay += __builtin_amdgcn_s_memtime() - c0;
