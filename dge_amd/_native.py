@@ -109,6 +109,7 @@ SIGNATURES = {
     "gs_buffer_offset": (ctypes.c_longlong, [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_int,
                                              ctypes.c_int, ctypes.c_int]),
     "gs_profile_enable": (ctypes.c_int, [ctypes.c_int]),
+    "gs_profile_set_stages": (ctypes.c_int, [ctypes.c_uint]),
     "gs_profile_num_stages": (ctypes.c_int, []),
     "gs_profile_stage_name": (ctypes.c_char_p, [ctypes.c_int]),
     "gs_profile_collect": (ctypes.c_int, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int), ctypes.c_int]),
@@ -172,6 +173,16 @@ def require_gpu(t) -> None:
 
 def profile_enable(on: bool = True) -> None:
     lib().gs_profile_enable(int(on))
+
+
+def profile_stages(names=None) -> None:
+    """Profile only the named stages (None: all)."""
+    L = lib()
+    if names is None:
+        L.gs_profile_set_stages(0xFFFFFFFF)
+        return
+    all_names = [L.gs_profile_stage_name(i).decode() for i in range(L.gs_profile_num_stages())]
+    L.gs_profile_set_stages(sum(1 << all_names.index(n) for n in names))
 
 
 def profile_collect() -> dict:

@@ -100,6 +100,7 @@ struct ProfRecord {
 // Process-wide: torch's autograd runs the backward on its own device thread.
 struct Profiler {
     std::atomic<bool> on{false};
+    std::atomic<uint32_t> mask{0xFFFFFFFFu};  // stages bracketed while on (gs_profile_set_stages)
     std::mutex mu;
     std::vector<ProfRecord> recs;
     std::vector<hipEvent_t> pool;
@@ -112,8 +113,10 @@ struct Profiler {
                 return e;
             }
         }
+        // timing events without the system-scope release fence a plain event adds to the
+        // stream (the fence alone stalls the queue ~10 us per event between two kernels)
         hipEvent_t e = nullptr;
-        if (hipEventCreate(&e) != hipSuccess) return nullptr;
+        if (hipEventCreateWithFlags(&e, hipEventDisableSystemFence) != hipSuccess) return nullptr;
         return e;
     }
     void add(int stage, hipEvent_t a, hipEvent_t b) {
@@ -131,7 +134,9 @@ struct StageScope {
     hipStream_t s;
     hipEvent_t a = nullptr;
     StageScope(int st, hipStream_t stream) : p(profiler()), stage(st), s(stream) {
-        if (p.on.load(std::memory_order_relaxed) && (a = p.get())) (void)hipEventRecord(a, s);
+        if (p.on.load(std::memory_order_relaxed) && ((p.mask.load(std::memory_order_relaxed) >> st) & 1u) &&
+            (a = p.get()))
+            (void)hipEventRecord(a, s);
     }
     ~StageScope() {
         if (!a) return;
@@ -377,6 +382,11 @@ long long gs_profile_diag_read(int which, uint64_t* host, long long max_u64) {
 
 int gs_profile_enable(int on) {
     profiler().on.store(on != 0);
+    return GS_OK;
+}
+
+int gs_profile_set_stages(unsigned int mask) {
+    profiler().mask.store(mask);
     return GS_OK;
 }
 

@@ -190,6 +190,9 @@ long long gs_buffer_offset(const char *buffer, const char *field, int P, int wid
  * gs_profile_collect synchronises on the recorded events, writes the summed
  * milliseconds and launch counts per stage (n entries) and resets. */
 int gs_profile_enable(int on);
+/* Restrict the profiler to the stages whose bit (1 << stage index) is set
+ * (default: all): every bracketed stage costs two events on the stream. */
+int gs_profile_set_stages(unsigned int mask);
 int gs_profile_num_stages(void);
 const char *gs_profile_stage_name(int i);
 int gs_profile_collect(double *total_ms, int *counts, int n);
