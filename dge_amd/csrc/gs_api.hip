@@ -281,7 +281,8 @@ int bin_forward(const gs_settings* s, const Grid& g, const gs_params& gp, int* r
     pa.tiles_touched = at<uint32_t>(geom, gl.tiles_touched);
     pa.clamped = at<uint8_t>(geom, gl.clamped);
     pa.depth_key = at<uint32_t>(geom, gl.key0);
-    pa.depth_val = at<uint32_t>(geom, gl.val0);
+    pa.rect = at<uint32_t>(geom, gl.rect);
+    pa.rect_packed = rect_packable(g.gx, g.gy) ? 1 : 0;
     pa.counters = counters;
     { StageScope sc(ST_PREPROCESS, stream); launch_preprocess(pa, stream); }
     GS_LAUNCHED("preprocess");
@@ -295,15 +296,15 @@ int bin_forward(const gs_settings* s, const Grid& g, const gs_params& gp, int* r
     // depth order of the Gaussians (stable: ties keep index order)
     int cur;
     { StageScope sc(ST_DEPTH_SORT, stream);
-    cur = radix_sort_pairs(at<uint32_t>(geom, gl.key0), at<uint32_t>(geom, gl.key1),
-                                     at<uint32_t>(geom, gl.val0), at<uint32_t>(geom, gl.val1), (uint32_t)P, 0, 32, 8,
-                                     false, at<uint32_t>(geom, gl.sort_hist), at<uint32_t>(geom, gl.sort_totals),
-                                     gl.sort_blocks, stream); }
+    cur = radix_sort_aux(at<uint32_t>(geom, gl.key0), at<uint32_t>(geom, gl.key1), at<uint2>(geom, gl.val0),
+                         at<uint2>(geom, gl.val1), pa.rect, (uint32_t)P, 32, 8, at<uint32_t>(geom, gl.sort_hist),
+                         at<uint32_t>(geom, gl.sort_totals), gl.sort_blocks, stream); }
     GS_LAUNCHED("depth sort");
 
     EmitArgs ea;
     ea.P = P; ea.gx = g.gx; ea.gy = g.gy;
-    ea.order = at<uint32_t>(geom, cur ? gl.val1 : gl.val0);
+    ea.order = at<uint2>(geom, cur ? gl.val1 : gl.val0);
+    ea.rect_packed = pa.rect_packed;
     ea.tiles_touched = pa.tiles_touched;
     ea.means2D = pa.means2D;
     ea.radii = pa.radii;

@@ -63,7 +63,7 @@ inline TileSortPlan tile_sort_plan(int num_tiles) {
 struct GeomLayout {
     size_t means2D, conic_opacity, rgbd, tiles_touched, clamped, touched, live_count, live_list, radii, first_slot;
     // live_count: one u32 per 256-Gaussian block (k_gauss_live); live_list: block-local compacted ids
-    size_t key0, key1, val0, val1, sort_hist, sort_totals, scan_sums, counters, total;
+    size_t key0, key1, val0, val1, rect, sort_hist, sort_totals, scan_sums, counters, total;
     int sort_blocks, scan_blocks;
 };
 inline GeomLayout geom_layout(int P) {
@@ -84,8 +84,9 @@ inline GeomLayout geom_layout(int P) {
     L.first_slot = o; o = align_up(o + 4 * p);
     L.key0 = o; o = align_up(o + 4 * p);
     L.key1 = o; o = align_up(o + 4 * p);
-    L.val0 = o; o = align_up(o + 4 * p);
-    L.val1 = o; o = align_up(o + 4 * p);
+    L.val0 = o; o = align_up(o + 8 * p);  // depth sort values: uint2 (rect-or-count, Gaussian)
+    L.val1 = o; o = align_up(o + 8 * p);
+    L.rect = o; o = align_up(o + 4 * p);  // packed tile rect (pack_rect) or tiles_touched
     L.sort_hist = o; o = align_up(o + 4 * 256 * (size_t)L.sort_blocks);
     L.sort_totals = o; o = align_up(o + 4 * 256);
     L.scan_sums = o; o = align_up(o + 4 * (size_t)(L.scan_blocks + 1));
@@ -190,7 +191,8 @@ struct PreprocessArgs {
     uint32_t* tiles_touched;
     uint8_t* clamped;
     uint32_t* depth_key;
-    uint32_t* depth_val;
+    uint32_t* rect;          // pack_rect(tile rect) when the grid allows it, else tiles_touched
+    int rect_packed;
     uint32_t* counters;  // [0] instance total, [1] error flag
 };
 void launch_preprocess(const PreprocessArgs& a, hipStream_t s);
@@ -199,6 +201,10 @@ void launch_mark_visible(int P, const float* means3D, const float* view, uint8_t
 // LSD radix sort of (u32 key, u32 value).  Returns the buffer index (0/1)
 // holding the result.  identity_vals: values of the first pass are the
 // element indices (val0 is not read).
+// Stable LSD sort of (key, (aux[i], i)) pairs on key bits [0, bits), at most
+// max_pass_bits per pass; returns the ping-pong index holding the result.
+int radix_sort_aux(uint32_t* key0, uint32_t* key1, uint2* pair0, uint2* pair1, const uint32_t* aux, uint32_t n,
+                   int bits, int max_pass_bits, uint32_t* hist, uint32_t* totals, int nblocks, hipStream_t s);
 int radix_sort_pairs(uint32_t* key0, uint32_t* key1, uint32_t* val0, uint32_t* val1, uint32_t n, int begin_bit,
                      int end_bit, int max_pass_bits, bool identity_vals, uint32_t* hist, uint32_t* totals,
                      int nblocks, hipStream_t s);
@@ -208,9 +214,21 @@ int radix_sort_pairs(uint32_t* key0, uint32_t* key1, uint32_t* val0, uint32_t* v
 int tile_sort(uint32_t* key0, uint32_t* key1, uint2* pair0, uint2* pair1, const uint32_t* gauss_by_slot, uint32_t n,
               int bits, uint32_t* hist, uint32_t* totals, int nblocks, hipStream_t s);
 
+// Tile rect of a Gaussian in one u32 (x0, y0, x1, y1: 8 bits each, x1/y1
+// exclusive) — carried through the depth sort with the Gaussian id, so the
+// instance scan and the emission read it in depth order without gathers.
+// Grids wider or taller than 255 tiles carry tiles_touched instead and the
+// emission gathers the rect (rect_packed = 0).
+constexpr int kRectPackMax = 255;
+__host__ __device__ inline bool rect_packable(int gx, int gy) { return gx <= kRectPackMax && gy <= kRectPackMax; }
+__host__ __device__ inline uint32_t pack_rect(int x0, int y0, int x1, int y1) {
+    return (uint32_t)x0 | ((uint32_t)y0 << 8) | ((uint32_t)x1 << 16) | ((uint32_t)y1 << 24);
+}
+
 struct EmitArgs {
     int P, gx, gy;
-    const uint32_t* order;       // Gaussian ids by depth rank
+    int rect_packed;
+    const uint2* order;          // by depth rank: (packed rect or tiles_touched, Gaussian id)
     const uint32_t* tiles_touched;
     const float2* means2D;
     const int* radii;

@@ -54,6 +54,7 @@ __global__ __launch_bounds__(256) void k_preprocess(PreprocessArgs a) {
     const int idx0 = blockIdx.x * 256;
     const int idx = idx0 + threadIdx.x;
     uint32_t touched = 0;
+    uint32_t rect = 0;  // packed tile rect (or the count), 0 for a culled Gaussian
     int radius_out = 0;
     uint32_t key = 0xFFFFFFFFu;
     uint8_t clamp_bits = 0;
@@ -103,6 +104,7 @@ __global__ __launch_bounds__(256) void k_preprocess(PreprocessArgs a) {
                 const Rect r = tile_rect(pix.x, pix.y, (int)rad, a.gx, a.gy);
                 const uint32_t area = (uint32_t)((r.y1 - r.y0) * (r.x1 - r.x0));
                 if (area != 0) {
+                    rect = a.rect_packed ? pack_rect(r.x0, r.y0, r.x1, r.y1) : area;
                     radius_out = (int)rad;
                     touched = area;
                     depth = pv.z;
@@ -137,7 +139,7 @@ __global__ __launch_bounds__(256) void k_preprocess(PreprocessArgs a) {
         a.tiles_touched[idx] = touched;
         a.clamped[idx] = clamp_bits;
         a.depth_key[idx] = key;
-        a.depth_val[idx] = (uint32_t)idx;
+        a.rect[idx] = rect;
     }
     // workgroup total of instances -> one atomic
     __shared__ uint32_t part[4];

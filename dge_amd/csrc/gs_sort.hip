@@ -190,24 +190,57 @@ __global__ __launch_bounds__(256) void k_radix_scatter(const uint32_t* __restric
         if (valid && rank == 0) cnt[w][d] = old + (uint32_t)__popcll(peers);
     }
     __syncthreads();
-    for (int d = tid; d < NDIG; d += 256) {
-        const uint32_t c0 = cnt[0][d], c1 = cnt[1][d], c2 = cnt[2][d];
-        const uint32_t g = dbase[d] + hist[(size_t)d * nb + blockIdx.x];
-        cnt[0][d] = g;
-        cnt[1][d] = g + c0;
-        cnt[2][d] = g + c0 + c1;
-        cnt[3][d] = g + c0 + c1 + c2;
+    // block-local digit-major order: run of digit d starts at bstart[d] (scan of the block's digit
+    // totals); wave w's elements of digit d follow those of waves < w.  cnt[w][d] <- that start,
+    // dbase[d] <- global position of the block's run minus bstart[d].
+    {
+        uint32_t tot[PER];
+        uint32_t s = 0;
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const int d = tid * PER + i;
+            tot[i] = d < NDIG ? cnt[0][d] + cnt[1][d] + cnt[2][d] + cnt[3][d] : 0u;
+            s += tot[i];
+        }
+        uint32_t all;
+        uint32_t run = block_exclusive_scan(s, lds4, all);
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const int d = tid * PER + i;
+            if (d < NDIG) {
+                const uint32_t c0 = cnt[0][d], c1 = cnt[1][d], c2 = cnt[2][d];
+                cnt[0][d] = run;
+                cnt[1][d] = run + c0;
+                cnt[2][d] = run + c0 + c1;
+                cnt[3][d] = run + c0 + c1 + c2;
+                dbase[d] = dbase[d] + hist[(size_t)d * nb + blockIdx.x] - run;
+            }
+            run += tot[i];
+        }
     }
     __syncthreads();
+    // stage the block in digit-major order, then store it with consecutive lanes on consecutive
+    // positions of each digit run (coalesced) instead of one scattered element per lane
+    __shared__ uint32_t s_key[kSortTile];
+    __shared__ V s_val[kSortTile];
 #pragma unroll
     for (int it = 0; it < kSortIPT; ++it) {
         const uint32_t idx = base + it * 64 + lane;
         if (idx < n) {
             const uint32_t d = (key[it] >> shift) & (NDIG - 1);
-            const uint32_t pos = cnt[w][d] + loc[it];
-            keys_out[pos] = key[it];
-            vals_out[pos] = val[it];
+            const uint32_t lp = cnt[w][d] + loc[it];
+            s_key[lp] = key[it];
+            s_val[lp] = val[it];
         }
+    }
+    __syncthreads();
+    const uint32_t b0 = blockIdx.x * (uint32_t)kSortTile;
+    const int nvalid = n - b0 < (uint32_t)kSortTile ? (int)(n - b0) : kSortTile;
+    for (int i = tid; i < nvalid; i += 256) {
+        const uint32_t k = s_key[i];
+        const uint32_t pos = dbase[(k >> shift) & (NDIG - 1)] + (uint32_t)i;
+        keys_out[pos] = k;
+        vals_out[pos] = s_val[i];
     }
 }
 
@@ -267,16 +300,16 @@ int radix_sort_pairs(uint32_t* key0, uint32_t* key1, uint32_t* val0, uint32_t* v
     return cur;
 }
 
-int tile_sort(uint32_t* key0, uint32_t* key1, uint2* pair0, uint2* pair1, const uint32_t* gauss_by_slot, uint32_t n,
-              int bits, uint32_t* hist, uint32_t* totals, int nblocks, hipStream_t s) {
+int radix_sort_aux(uint32_t* key0, uint32_t* key1, uint2* pair0, uint2* pair1, const uint32_t* aux, uint32_t n,
+                   int bits, int max_pass_bits, uint32_t* hist, uint32_t* totals, int nblocks, hipStream_t s) {
     uint32_t* k[2] = {key0, key1};
     uint2* v[2] = {pair0, pair1};
     int cur = 0;
-    const int passes = (bits + kMaxSinglePassBits - 1) / kMaxSinglePassBits;
+    const int passes = (bits + max_pass_bits - 1) / max_pass_bits;
     int shift = 0;
     for (int p = 0; p < passes; ++p) {
-        const int b = pass_bits(0, bits, kMaxSinglePassBits, p, shift);
-        radix_pass_bits(b, k[cur], v[cur], k[cur ^ 1], v[cur ^ 1], gauss_by_slot, n, shift, p == 0,
+        const int b = pass_bits(0, bits, max_pass_bits, p, shift);
+        radix_pass_bits(b, k[cur], v[cur], k[cur ^ 1], v[cur ^ 1], aux, n, shift, p == 0,
                         p == 0 ? kValPairFirst : kValPair, hist, totals, nblocks, s);
         cur ^= 1;
         shift += b;
@@ -284,9 +317,21 @@ int tile_sort(uint32_t* key0, uint32_t* key1, uint2* pair0, uint2* pair1, const 
     return cur;
 }
 
+int tile_sort(uint32_t* key0, uint32_t* key1, uint2* pair0, uint2* pair1, const uint32_t* gauss_by_slot, uint32_t n,
+              int bits, uint32_t* hist, uint32_t* totals, int nblocks, hipStream_t s) {
+    return radix_sort_aux(key0, key1, pair0, pair1, gauss_by_slot, n, bits, kMaxSinglePassBits, hist, totals, nblocks,
+                          s);
+}
+
 // ---------------------------------------------------------------------
 // instance scan in depth order + emission
 // ---------------------------------------------------------------------
+// instances of a Gaussian from its depth-sort payload
+__device__ __forceinline__ uint32_t rect_count(uint32_t v, int packed) {
+    if (!packed) return v;
+    return ((v >> 16 & 0xFFu) - (v & 0xFFu)) * ((v >> 24) - (v >> 8 & 0xFFu));
+}
+
 __global__ __launch_bounds__(256) void k_scan_reduce(EmitArgs a) {
     __shared__ uint32_t lds4[4];
     uint32_t s = 0;
@@ -294,7 +339,7 @@ __global__ __launch_bounds__(256) void k_scan_reduce(EmitArgs a) {
 #pragma unroll
     for (int it = 0; it < kScanIPT; ++it) {
         const uint32_t r = base + it * 256 + threadIdx.x;
-        if (r < (uint32_t)a.P) s += a.tiles_touched[a.order[r]];
+        if (r < (uint32_t)a.P) s += rect_count(a.order[r].x, a.rect_packed);
     }
     uint32_t total;
     block_exclusive_scan(s, lds4, total);
@@ -330,14 +375,21 @@ __global__ __launch_bounds__(256) void k_scan_emit(EmitArgs a) {
     const uint32_t r_block = blockIdx.x * (uint32_t)kScanTile;
     for (int it = 0; it < kScanIPT; ++it) {
         const uint32_t r = r_block + it * 256 + threadIdx.x;
-        const uint32_t g = r < (uint32_t)a.P ? a.order[r] : 0u;
-        const uint32_t c = r < (uint32_t)a.P ? a.tiles_touched[g] : 0u;
+        const uint2 gr = r < (uint32_t)a.P ? a.order[r] : make_uint2(0u, 0u);
+        const uint32_t g = gr.y;
+        const uint32_t c = rect_count(gr.x, a.rect_packed);
         uint32_t total;
         const uint32_t off = block_exclusive_scan(c, lds4, total);
         if (c) {
             a.first_slot[g] = base + off;
-            const float2 xy = a.means2D[g];
-            const Rect q = tile_rect(xy.x, xy.y, a.radii[g], a.gx, a.gy);
+            Rect q;
+            if (a.rect_packed) {
+                q.x0 = (int)(gr.x & 0xFFu); q.y0 = (int)((gr.x >> 8) & 0xFFu);
+                q.x1 = (int)((gr.x >> 16) & 0xFFu); q.y1 = (int)(gr.x >> 24);
+            } else {
+                const float2 xy = a.means2D[g];
+                q = tile_rect(xy.x, xy.y, a.radii[g], a.gx, a.gy);
+            }
             s_rect[threadIdx.x] = make_int4(q.x0, q.y0, q.x1 - q.x0, 0);
         }
         s_start[threadIdx.x] = off;
