@@ -308,6 +308,12 @@ def rasterize_gaussians_fused_backward(background, xyz, f_dc, f_rest, colors, ra
         o.dsh_rest_stride = 3 * (d_rest.size(1) if d_rest is not None else 0)
         o.dL_dscales, o.dL_drotations = _ptr(d_sc), _ptr(d_rot)
         o.accumulate = acc_bits
+        gm = into.get("grad_mask")
+        if gm is not None:
+            mask_t, names = gm
+            o.grad_mask = mask_t.data_ptr()
+            o.mask_bits = sum({"xyz": N.ACC_MEANS3D, "sh": N.ACC_SH, "opacity": N.ACC_OPACITY,
+                               "scaling": N.ACC_SCALES, "rotation": N.ACC_ROTATIONS}[n] for n in names)
         grad = _f32(dL_dout_color, "dL_dout_color")
         s, keep = _settings(background, viewmatrix, projmatrix, campos, tan_fovx, tan_fovy, H, W, degree,
                             scale_modifier, False, debug)

@@ -84,6 +84,22 @@ class GsGrads(ctypes.Structure):
         ("dL_dscales", _fp),
         ("dL_drotations", _fp),
         ("accumulate", ctypes.c_uint),
+        ("grad_mask", ctypes.c_void_p),
+        ("mask_bits", ctypes.c_uint),
+    ]
+
+
+class AdamSegment(ctypes.Structure):
+    """struct gs_adam_segment (include/gs_raster.h)."""
+
+    _fields_ = [
+        ("param", ctypes.c_void_p),
+        ("grad", ctypes.c_void_p),
+        ("exp_avg", ctypes.c_void_p),
+        ("exp_avg_sq", ctypes.c_void_p),
+        ("n", ctypes.c_longlong),
+        ("step_size", ctypes.c_float),
+        ("bias_correction2_sqrt", ctypes.c_float),
     ]
 
 
@@ -115,6 +131,8 @@ SIGNATURES = {
     "gs_profile_collect": (ctypes.c_int, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int), ctypes.c_int]),
     "gs_profile_diag_enable": (ctypes.c_int, [ctypes.c_int]),
     "gs_profile_diag_read": (ctypes.c_longlong, [ctypes.c_int, ctypes.POINTER(ctypes.c_uint64), ctypes.c_longlong]),
+    "gs_adam_step": (ctypes.c_int, [ctypes.POINTER(AdamSegment), ctypes.c_int, ctypes.c_float, ctypes.c_float,
+                                    ctypes.c_float, ctypes.c_void_p]),
     "gs_last_error": (ctypes.c_char_p, []),
     "gs_abi_version": (ctypes.c_int, []),
 }

@@ -297,7 +297,7 @@ int bin_forward(const gs_settings* s, const Grid& g, const gs_params& gp, int* r
     int cur;
     { StageScope sc(ST_DEPTH_SORT, stream);
     cur = radix_sort_aux(at<uint32_t>(geom, gl.key0), at<uint32_t>(geom, gl.key1), at<uint2>(geom, gl.val0),
-                         at<uint2>(geom, gl.val1), pa.rect, (uint32_t)P, 32, 8, at<uint32_t>(geom, gl.sort_hist),
+                         at<uint2>(geom, gl.val1), pa.rect, (uint32_t)P, 32, 8, kDepthSortIPT, at<uint32_t>(geom, gl.sort_hist),
                          at<uint32_t>(geom, gl.sort_totals), gl.sort_blocks, stream); }
     GS_LAUNCHED("depth sort");
 
@@ -347,6 +347,8 @@ int bin_forward(const gs_settings* s, const Grid& g, const gs_params& gp, int* r
 }  // namespace
 
 namespace gs {
+int report_error(int code, const char* msg) { return set_error(code, "%s", msg); }
+
 uint64_t* diag_buffer(int which, size_t n_u64) {
     Diag& d = diag();
     if (!d.on.load()) return nullptr;
@@ -527,6 +529,8 @@ int gs_rasterize_backward(const gs_settings* s, int P, int M, int R, const float
     o.dsh_dc_stride = o.dsh_rest_stride = 3 * M;
     o.dL_dscales = dL_dscales; o.dL_drotations = dL_drotations;
     o.accumulate = 0;
+    o.grad_mask = nullptr;
+    o.mask_bits = 0;
     gs_params g2 = g;
     g2.M = M;  // dL_dsh is [P,M,3] even when shs is absent (then all zero)
     return gs_rasterize_backward_ex(s, &g2, R, radii, geom, binning, img, dL_dpix, &o, stream);
@@ -618,6 +622,8 @@ int gs_rasterize_backward_ex(const gs_settings* s, const gs_params* gp, int R, c
         ga.dL_dmeans3D = o->dL_dmeans3D; ga.dL_dcov3D = o->dL_dcov3D;
         ga.dL_dscales = o->dL_dscales; ga.dL_drot = o->dL_drotations;
         ga.acc = o->accumulate;
+        ga.grad_mask = o->grad_mask;
+        ga.mask_bits = o->grad_mask ? o->mask_bits : 0u;
         { StageScope sc(ST_GAUSS_BWD, stream); launch_gauss_backward(ga, stream); }
         GS_LAUNCHED("gaussian backward");
         return GS_OK;

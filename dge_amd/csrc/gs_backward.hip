@@ -293,6 +293,28 @@ __device__ __forceinline__ void gauss_bwd_visible(const GaussBwdArgs& a, const G
     }
 }
 
+// The grad-mask hooks of the reference's GaussianModel (gaussian_model.py:837-856:
+// grad * mask[:, None] on _xyz, _features_dc, _features_rest, _opacity,
+// _scaling — not _rotation), applied to the outputs named in mask_bits.
+__device__ __forceinline__ void apply_grad_mask(const GaussBwdArgs& a, float m, float (&acc)[9], float& dop,
+                                                float (&dsh)[48], GaussOut& o) {
+    const uint32_t b = a.mask_bits;
+    if (b & GS_ACC_MEANS2D) { acc[0] *= m; acc[1] *= m; }
+    if (b & GS_ACC_COLORS) { acc[6] *= m; acc[7] *= m; acc[8] *= m; }
+    if (b & GS_ACC_OPACITY) dop *= m;
+    if (b & GS_ACC_MEANS3D) o.dmean = o.dmean * m;
+    if (b & GS_ACC_COV3D)
+#pragma unroll
+        for (int k = 0; k < 6; ++k) o.dcov[k] *= m;
+    if (b & GS_ACC_SH)
+#pragma unroll
+        for (int k = 0; k < 48; ++k) dsh[k] *= m;
+    if (b & GS_ACC_SCALES)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) o.dscale[k] *= m;
+    if (b & GS_ACC_ROTATIONS) o.drot = make_float4(o.drot.x * m, o.drot.y * m, o.drot.z * m, o.drot.w * m);
+}
+
 // Writes (or adds, per GS_ACC_* bit) one live Gaussian's per-Gaussian outputs:
 // all loads of the accumulated ones first, then all stores, so the ~20
 // scattered read-modify-writes overlap instead of forming a dependent chain.
@@ -518,7 +540,10 @@ __global__ __launch_bounds__(kGB) void k_gauss_bwd_live(GaussBwdArgs a) {
         for (int k = 0; k < 48; ++k) dsh[k] = 0.f;
         float dop = acc[5];  // w.r.t. opacity; chained through the sigmoid when activation = 1
         GaussOut o;
-        if (ok) gauss_bwd_visible(a, gin, acc, dop, my_sh, dsh, o);
+        if (ok) {
+            gauss_bwd_visible(a, gin, acc, dop, my_sh, dsh, o);
+            if (a.grad_mask) apply_grad_mask(a, a.grad_mask[idx] ? 1.f : 0.f, acc, dop, dsh, o);
+        }
         if (a.dsh.dc && ncol > 0) {
             __syncthreads();  // every row read before any row is overwritten
 #pragma unroll

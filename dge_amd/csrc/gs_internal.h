@@ -27,8 +27,10 @@
 
 namespace gs {
 
-constexpr int kSortIPT = 16;                    // keys per thread in the radix kernels
+constexpr int kSortIPT = 16;                    // keys per thread in the tile-key radix kernels
 constexpr int kSortTile = 256 * kSortIPT;       // keys per workgroup
+constexpr int kDepthSortIPT = 8;                // depth sort: smaller tiles, >= 2 workgroups per CU at 1M
+constexpr int kDepthSortTile = 256 * kDepthSortIPT;
 constexpr int kScanIPT = 4;
 constexpr int kScanTile = 256 * kScanIPT;
 constexpr int kMaxSinglePassBits = 11;          // tile keys up to 2048 tiles sort in one pass
@@ -70,7 +72,7 @@ inline GeomLayout geom_layout(int P) {
     GeomLayout L;
     size_t o = 0;
     size_t p = (size_t)(P > 0 ? P : 1);
-    L.sort_blocks = div_up((long long)p, kSortTile);
+    L.sort_blocks = div_up((long long)p, kDepthSortTile);
     L.scan_blocks = div_up((long long)p, kScanTile);
     L.means2D = o; o = align_up(o + 8 * p);
     L.conic_opacity = o; o = align_up(o + 16 * p);
@@ -204,10 +206,7 @@ void launch_mark_visible(int P, const float* means3D, const float* view, uint8_t
 // Stable LSD sort of (key, (aux[i], i)) pairs on key bits [0, bits), at most
 // max_pass_bits per pass; returns the ping-pong index holding the result.
 int radix_sort_aux(uint32_t* key0, uint32_t* key1, uint2* pair0, uint2* pair1, const uint32_t* aux, uint32_t n,
-                   int bits, int max_pass_bits, uint32_t* hist, uint32_t* totals, int nblocks, hipStream_t s);
-int radix_sort_pairs(uint32_t* key0, uint32_t* key1, uint32_t* val0, uint32_t* val1, uint32_t n, int begin_bit,
-                     int end_bit, int max_pass_bits, bool identity_vals, uint32_t* hist, uint32_t* totals,
-                     int nblocks, hipStream_t s);
+                   int bits, int max_pass_bits, int ipt, uint32_t* hist, uint32_t* totals, int nblocks, hipStream_t s);
 // Stable sort of the K emitted instances on their tile id (key0 in slot
 // order); the values are (Gaussian, slot) pairs built on the first pass from
 // gauss_by_slot.  Returns the buffer index (0/1) holding keys and pairs.
@@ -318,6 +317,8 @@ struct GaussBwdArgs {
     const float4* records;     // [4*K][3] float4 by slot
     float *dL_dmeans2D, *dL_dcolors, *dL_dopacity, *dL_dmeans3D, *dL_dcov3D, *dL_dscales, *dL_drot;
     uint32_t acc;  // GS_ACC_* bits: add into the output instead of overwriting
+    const uint8_t* grad_mask;  // optional [P]: outputs in mask_bits are multiplied by it
+    uint32_t mask_bits;
 };
 void launch_gauss_backward(const GaussBwdArgs& a, hipStream_t s);
 
@@ -326,5 +327,6 @@ void launch_gauss_backward(const GaussBwdArgs& a, hipStream_t s);
 // rounds, cycles in the blend/replay loops, total cycles (s_memtime).
 constexpr int kDiagWords = 8;
 uint64_t* diag_buffer(int which, size_t n_u64);  // which: 0 forward, 1 backward; nullptr when off
+int report_error(int code, const char* msg);      // sets gs_last_error(), returns code
 
 }  // namespace gs

@@ -66,34 +66,29 @@ __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* l
 // ---------------------------------------------------------------------
 // radix sort: histogram -> per-digit scan -> stable scatter
 // ---------------------------------------------------------------------
-template <int BITS>
+// Per-block digit counts (integer LDS atomics: the counts do not depend on the order).
+template <int BITS, int IPT>
 __global__ __launch_bounds__(256) void k_radix_hist(const uint32_t* __restrict__ keys, uint32_t n, int shift,
                                                     uint32_t* __restrict__ hist, int nb) {
     constexpr int NDIG = 1 << BITS;
-    __shared__ uint32_t cnt[4][NDIG];
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    for (int i = tid; i < 4 * NDIG; i += 256) (&cnt[0][0])[i] = 0;
+    __shared__ uint32_t cnt[NDIG];
+    const int tid = threadIdx.x;
+    for (int i = tid; i < NDIG; i += 256) cnt[i] = 0;
     __syncthreads();
-    const uint32_t base = blockIdx.x * (uint32_t)kSortTile + w * 64u * kSortIPT;
-    uint32_t key[kSortIPT];
+    const uint32_t base = blockIdx.x * (uint32_t)(256 * IPT);
+    uint32_t key[IPT];
 #pragma unroll
-    for (int it = 0; it < kSortIPT; ++it) {
-        const uint32_t idx = base + it * 64 + lane;
+    for (int it = 0; it < IPT; ++it) {
+        const uint32_t idx = base + it * 256 + tid;
         key[it] = idx < n ? keys[idx] : 0u;
     }
 #pragma unroll
-    for (int it = 0; it < kSortIPT; ++it) {
-        const uint32_t idx = base + it * 64 + lane;
-        const bool valid = idx < n;
-        const uint64_t vm = __ballot(valid);
-        if (vm == 0) break;
-        const uint32_t d = (key[it] >> shift) & (NDIG - 1);
-        const uint64_t peers = match_digit<BITS>(d, vm);
-        if (valid && (peers & lanemask_lt()) == 0) cnt[w][d] += (uint32_t)__popcll(peers);
+    for (int it = 0; it < IPT; ++it) {
+        const uint32_t idx = base + it * 256 + tid;
+        if (idx < n) atomicAdd(&cnt[(key[it] >> shift) & (NDIG - 1)], 1u);
     }
     __syncthreads();
-    for (int d = tid; d < NDIG; d += 256)
-        hist[(size_t)d * nb + blockIdx.x] = cnt[0][d] + cnt[1][d] + cnt[2][d] + cnt[3][d];
+    for (int d = tid; d < NDIG; d += 256) hist[(size_t)d * nb + blockIdx.x] = cnt[d];
 }
 
 // One workgroup per digit: exclusive scan of hist[d][0..nb) in place,
@@ -127,7 +122,7 @@ __global__ __launch_bounds__(256) void k_radix_digit_scan(uint32_t* __restrict__
 // the first pass of the tile sort, then carried as one 8-byte value.
 enum ValMode { kValU32 = 0, kValPairFirst = 1, kValPair = 2 };
 
-template <int BITS, bool IDV, int VM>
+template <int BITS, int IPT, bool IDV, int VM>
 __global__ __launch_bounds__(256) void k_radix_scatter(const uint32_t* __restrict__ keys_in,
                                                        const void* __restrict__ vals_in_,
                                                        uint32_t* __restrict__ keys_out, void* __restrict__ vals_out_,
@@ -164,11 +159,11 @@ __global__ __launch_bounds__(256) void k_radix_scatter(const uint32_t* __restric
         }
     }
     __syncthreads();
-    const uint32_t base = blockIdx.x * (uint32_t)kSortTile + w * 64u * kSortIPT;
-    uint32_t key[kSortIPT], loc[kSortIPT];
-    V val[kSortIPT];
+    const uint32_t base = blockIdx.x * (uint32_t)(256 * IPT) + w * 64u * IPT;
+    uint32_t key[IPT], loc[IPT];
+    V val[IPT];
 #pragma unroll
-    for (int it = 0; it < kSortIPT; ++it) {
+    for (int it = 0; it < IPT; ++it) {
         const uint32_t idx = base + it * 64 + lane;
         const bool valid = idx < n;
         key[it] = valid ? keys_in[idx] : 0u;
@@ -177,7 +172,7 @@ __global__ __launch_bounds__(256) void k_radix_scatter(const uint32_t* __restric
         else val[it] = valid ? pairs_in[idx] : make_uint2(0u, 0u);
     }
 #pragma unroll
-    for (int it = 0; it < kSortIPT; ++it) {
+    for (int it = 0; it < IPT; ++it) {
         const uint32_t idx = base + it * 64 + lane;
         const bool valid = idx < n;
         const uint64_t vm = __ballot(valid);
@@ -221,10 +216,10 @@ __global__ __launch_bounds__(256) void k_radix_scatter(const uint32_t* __restric
     __syncthreads();
     // stage the block in digit-major order, then store it with consecutive lanes on consecutive
     // positions of each digit run (coalesced) instead of one scattered element per lane
-    __shared__ uint32_t s_key[kSortTile];
-    __shared__ V s_val[kSortTile];
+    __shared__ uint32_t s_key[256 * IPT];
+    __shared__ V s_val[256 * IPT];
 #pragma unroll
-    for (int it = 0; it < kSortIPT; ++it) {
+    for (int it = 0; it < IPT; ++it) {
         const uint32_t idx = base + it * 64 + lane;
         if (idx < n) {
             const uint32_t d = (key[it] >> shift) & (NDIG - 1);
@@ -234,8 +229,8 @@ __global__ __launch_bounds__(256) void k_radix_scatter(const uint32_t* __restric
         }
     }
     __syncthreads();
-    const uint32_t b0 = blockIdx.x * (uint32_t)kSortTile;
-    const int nvalid = n - b0 < (uint32_t)kSortTile ? (int)(n - b0) : kSortTile;
+    const uint32_t b0 = blockIdx.x * (uint32_t)(256 * IPT);
+    const int nvalid = n - b0 < (uint32_t)(256 * IPT) ? (int)(n - b0) : 256 * IPT;
     for (int i = tid; i < nvalid; i += 256) {
         const uint32_t k = s_key[i];
         const uint32_t pos = dbase[(k >> shift) & (NDIG - 1)] + (uint32_t)i;
@@ -244,15 +239,15 @@ __global__ __launch_bounds__(256) void k_radix_scatter(const uint32_t* __restric
     }
 }
 
-template <int BITS>
+template <int BITS, int IPT>
 static void radix_pass(const uint32_t* kin, const void* vin, uint32_t* kout, void* vout, const uint32_t* gauss_by_slot,
                        uint32_t n, int shift, bool idv, int vm, uint32_t* hist, uint32_t* totals, int nb,
                        hipStream_t s) {
     constexpr int NDIG = 1 << BITS;
-    hipLaunchKernelGGL(k_radix_hist<BITS>, dim3(nb), dim3(256), 0, s, kin, n, shift, hist, nb);
+    hipLaunchKernelGGL((k_radix_hist<BITS, IPT>), dim3(nb), dim3(256), 0, s, kin, n, shift, hist, nb);
     hipLaunchKernelGGL(k_radix_digit_scan, dim3(NDIG), dim3(256), 0, s, hist, nb, totals);
 #define GS_SCATTER(IDV, VM)                                                                                   \
-    hipLaunchKernelGGL((k_radix_scatter<BITS, IDV, VM>), dim3(nb), dim3(256), 0, s, kin, vin, kout, vout,     \
+    hipLaunchKernelGGL((k_radix_scatter<BITS, IPT, IDV, VM>), dim3(nb), dim3(256), 0, s, kin, vin, kout, vout,  \
                        gauss_by_slot, n, shift, hist, totals, nb)
     if (vm == kValPairFirst) GS_SCATTER(true, kValPairFirst);
     else if (vm == kValPair) GS_SCATTER(false, kValPair);
@@ -261,17 +256,22 @@ static void radix_pass(const uint32_t* kin, const void* vin, uint32_t* kout, voi
 #undef GS_SCATTER
 }
 
-static void radix_pass_bits(int bits, const uint32_t* kin, const void* vin, uint32_t* kout, void* vout,
+static void radix_pass_bits(int bits, int ipt, const uint32_t* kin, const void* vin, uint32_t* kout, void* vout,
                             const uint32_t* gauss_by_slot, uint32_t n, int shift, bool idv, int vm, uint32_t* hist,
                             uint32_t* totals, int nb, hipStream_t s) {
+#define GS_CASE(B)                                                                                              \
+    case B:                                                                                                     \
+        if (ipt == kDepthSortIPT)                                                                               \
+            radix_pass<B, kDepthSortIPT>(kin, vin, kout, vout, gauss_by_slot, n, shift, idv, vm, hist, totals, nb, s); \
+        else                                                                                                    \
+            radix_pass<B, kSortIPT>(kin, vin, kout, vout, gauss_by_slot, n, shift, idv, vm, hist, totals, nb, s); \
+        break;
     switch (bits) {
-#define GS_CASE(B) \
-    case B: radix_pass<B>(kin, vin, kout, vout, gauss_by_slot, n, shift, idv, vm, hist, totals, nb, s); break;
         GS_CASE(1) GS_CASE(2) GS_CASE(3) GS_CASE(4) GS_CASE(5) GS_CASE(6)
         GS_CASE(7) GS_CASE(8) GS_CASE(9) GS_CASE(10) GS_CASE(11)
-#undef GS_CASE
         default: break;
     }
+#undef GS_CASE
 }
 
 // passes over [begin_bit, end_bit) with at most max_pass_bits per pass, bits split evenly
@@ -282,26 +282,8 @@ static int pass_bits(int begin_bit, int end_bit, int max_pass_bits, int p, int& 
     return (rem + (passes - p) - 1) / (passes - p);
 }
 
-int radix_sort_pairs(uint32_t* key0, uint32_t* key1, uint32_t* val0, uint32_t* val1, uint32_t n, int begin_bit,
-                     int end_bit, int max_pass_bits, bool identity_vals, uint32_t* hist, uint32_t* totals, int nblocks,
-                     hipStream_t s) {
-    uint32_t* k[2] = {key0, key1};
-    uint32_t* v[2] = {val0, val1};
-    int cur = 0;
-    const int passes = (end_bit - begin_bit + max_pass_bits - 1) / max_pass_bits;
-    int shift = begin_bit;
-    for (int p = 0; p < passes; ++p) {
-        const int bits = pass_bits(begin_bit, end_bit, max_pass_bits, p, shift);
-        radix_pass_bits(bits, k[cur], v[cur], k[cur ^ 1], v[cur ^ 1], nullptr, n, shift, identity_vals && p == 0,
-                        kValU32, hist, totals, nblocks, s);
-        cur ^= 1;
-        shift += bits;
-    }
-    return cur;
-}
-
 int radix_sort_aux(uint32_t* key0, uint32_t* key1, uint2* pair0, uint2* pair1, const uint32_t* aux, uint32_t n,
-                   int bits, int max_pass_bits, uint32_t* hist, uint32_t* totals, int nblocks, hipStream_t s) {
+                   int bits, int max_pass_bits, int ipt, uint32_t* hist, uint32_t* totals, int nblocks, hipStream_t s) {
     uint32_t* k[2] = {key0, key1};
     uint2* v[2] = {pair0, pair1};
     int cur = 0;
@@ -309,7 +291,7 @@ int radix_sort_aux(uint32_t* key0, uint32_t* key1, uint2* pair0, uint2* pair1, c
     int shift = 0;
     for (int p = 0; p < passes; ++p) {
         const int b = pass_bits(0, bits, max_pass_bits, p, shift);
-        radix_pass_bits(b, k[cur], v[cur], k[cur ^ 1], v[cur ^ 1], aux, n, shift, p == 0,
+        radix_pass_bits(b, ipt, k[cur], v[cur], k[cur ^ 1], v[cur ^ 1], aux, n, shift, p == 0,
                         p == 0 ? kValPairFirst : kValPair, hist, totals, nblocks, s);
         cur ^= 1;
         shift += b;
@@ -319,8 +301,8 @@ int radix_sort_aux(uint32_t* key0, uint32_t* key1, uint2* pair0, uint2* pair1, c
 
 int tile_sort(uint32_t* key0, uint32_t* key1, uint2* pair0, uint2* pair1, const uint32_t* gauss_by_slot, uint32_t n,
               int bits, uint32_t* hist, uint32_t* totals, int nblocks, hipStream_t s) {
-    return radix_sort_aux(key0, key1, pair0, pair1, gauss_by_slot, n, bits, kMaxSinglePassBits, hist, totals, nblocks,
-                          s);
+    return radix_sort_aux(key0, key1, pair0, pair1, gauss_by_slot, n, bits, kMaxSinglePassBits, kSortIPT, hist, totals,
+                          nblocks, s);
 }
 
 // ---------------------------------------------------------------------

@@ -110,17 +110,41 @@ class _RasterizeGaussiansFused(torch.autograd.Function):
         # itself, the kernel writes (or adds) it there directly and autograd receives None — saving the
         # separate read-modify-write pass over every parameter.
         into, direct = {}, []
+        masked, owners = set(), set()
         if _FUSED_GRAD_ACCUM and not torch.is_grad_enabled():
             for name, p in (("xyz", xyz), ("opacity", raw_opacity), ("scaling", raw_scaling),
                             ("rotation", raw_rotation)):
-                mode = _accumulation_mode(p)
+                mode, owner = _accumulation_mode(p)
                 if mode is not None:
                     into[name] = _into_target(p, mode, direct)
+                    if owner is not None:
+                        masked.add(name)
+                        owners.add(owner)
             if ctx.has_sh:
-                m_dc, m_rest = _accumulation_mode(f_dc), _accumulation_mode(f_rest)
-                if m_dc is not None and m_dc == m_rest:
+                (m_dc, o_dc), (m_rest, o_rest) = _accumulation_mode(f_dc), _accumulation_mode(f_rest)
+                if m_dc is not None and m_dc == m_rest and o_dc is o_rest:
                     into["sh"] = ((_into_target(f_dc, m_dc, direct)[0], _into_target(f_rest, m_rest, direct)[0]),
                                   m_dc == "add")
+                    if o_dc is not None:
+                        masked.add("sh")
+                        owners.add(o_dc)
+        if masked:
+            # the GaussianModel's grad-mask hooks, applied in-kernel with the owner's current mask
+            mask = next(iter(owners)).mask if len(owners) == 1 else None
+            if (mask is None or mask.dtype != torch.bool or mask.shape != (xyz.shape[0],)
+                    or mask.device != xyz.device):
+                # not expressible in-kernel: hand those gradients back to autograd (which runs the hooks)
+                for name in masked:
+                    if name == "sh":
+                        tgt = (f_dc, f_rest)
+                    else:
+                        tgt = ({"xyz": xyz, "opacity": raw_opacity, "scaling": raw_scaling,
+                                "rotation": raw_rotation}[name],)
+                    direct[:] = [(p, t) for p, t in direct if all(p is not q for q in tgt)]
+                    del into[name]
+                masked = set()
+            else:
+                into["grad_mask"] = (mask.contiguous().view(torch.uint8), masked)
         args = (rs.bg, xyz, f_dc, f_rest, colors, raw_opacity, raw_scaling, raw_rotation, radii, rs.scale_modifier,
                 rs.viewmatrix, rs.projmatrix, rs.tanfovx, rs.tanfovy, grad_out_color, rs.sh_degree, rs.campos,
                 geomBuffer, ctx.num_rendered, binningBuffer, imgBuffer, rs.debug)
@@ -157,30 +181,48 @@ def set_fused_grad_accumulation(enabled: bool) -> bool:
     return prev
 
 
+def _mask_owner(p):
+    """(ok, owner): p's tensor hooks are none (owner None) or only GaussianModel grad-mask hooks of one
+    model (dge_amd/gaussian_model.py apply_grad_mask, tagged _dge_grad_mask_owner); ok False otherwise."""
+    hooks = getattr(p, "_backward_hooks", None)
+    if not hooks:
+        return True, None
+    owners = {id(getattr(h, "_dge_grad_mask_owner", None)): getattr(h, "_dge_grad_mask_owner", None)
+              for h in hooks.values()}
+    if len(owners) == 1:
+        owner = next(iter(owners.values()))
+        if owner is not None:
+            return True, owner
+    return False, None
+
+
 def _accumulation_mode(p):
-    """"add" / "new" when this backward's gradient for leaf `p` may go straight into p.grad, else None.
+    """("add" | "new" | None, mask owner): "add"/"new" when this backward's gradient for leaf `p` may go
+    straight into p.grad.
 
     Only where autograd itself would run p's AccumulateGrad in this backward (so torch.autograd.grad
-    callers, which capture instead, still get returned gradients), p has no tensor or post-accumulate
-    hooks, and an existing .grad is a plain contiguous fp32 buffer of p's shape."""
+    callers, which capture instead, still get returned gradients), p has no post-accumulate hooks and
+    no tensor hooks other than a GaussianModel's grad mask (applied in-kernel), and an existing .grad is
+    a plain contiguous fp32 buffer of p's shape."""
     if not isinstance(p, torch.Tensor) or not p.requires_grad or p.grad_fn is not None or p.numel() == 0:
-        return None
-    if getattr(p, "_backward_hooks", None) or getattr(p, "_post_accumulate_grad_hooks", None):
-        return None
+        return None, None
+    ok, owner = _mask_owner(p)
+    if not ok or getattr(p, "_post_accumulate_grad_hooks", None):
+        return None, None
     try:
         with torch.enable_grad():
             node = p.view_as(p).grad_fn.next_functions[0][0]
         if not torch._C._will_engine_execute_node(node):
-            return None
+            return None, None
     except Exception:
-        return None
+        return None, None
     g = p.grad
     if g is None:
-        return "new"
+        return "new", owner
     if (g.shape == p.shape and g.dtype == torch.float32 and g.device == p.device and g.is_contiguous()
             and not g.requires_grad):
-        return "add"
-    return None
+        return "add", owner
+    return None, None
 
 
 def _into_target(p, mode, direct):

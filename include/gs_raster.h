@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define GS_RASTER_ABI_VERSION 2
+#define GS_RASTER_ABI_VERSION 3
 
 #define GS_OK 0
 #define GS_ERR_INVALID_ARG 1   /* AT_ERROR / std::runtime_error in the reference */
@@ -149,6 +149,11 @@ typedef struct gs_grads {         /* backward outputs, every element written */
     float *dL_dscales;            /* [P,3] (raw when activation = 1) */
     float *dL_drotations;         /* [P,4] (raw when activation = 1) */
     unsigned int accumulate;      /* GS_ACC_* bits; 0: overwrite every output (reference behaviour) */
+    /* Optional per-Gaussian gradient mask (the GaussianModel's grad-mask hooks,
+     * gaussian_model.py:837-856: grad * mask[:, None]): outputs whose GS_ACC_*
+     * bit is set in mask_bits are multiplied by grad_mask[i] (0/1); NULL: none. */
+    const uint8_t *grad_mask;     /* [P] */
+    unsigned int mask_bits;
 } gs_grads;
 
 int gs_rasterize_forward_ex(const gs_settings *s, const gs_params *g, float *out_color, float *out_depth,
@@ -170,6 +175,26 @@ int gs_apply_weights(const gs_settings *s, int P, int M, const float *means3D, f
                      const float *rotations, const float *cov3D_precomp, const float *shs,
                      const float *image_weights, int *cnt, gs_alloc_fn alloc, void *alloc_ctx,
                      gs_stream_t stream);
+
+/* Fused Adam step over several parameter tensors in ONE launch — the
+ * optimizer of the training loop (gaussian_model.py:336-380:
+ * torch.optim.Adam(groups, lr=0.0, eps=1e-15), one group per parameter;
+ * torch/optim/adam.py _single_tensor_adam arithmetic).  Per segment the
+ * caller passes the group's step scalars (its own step count):
+ * step_size = lr / (1 - beta1^t), bias_correction2_sqrt = sqrt(1 - beta2^t).
+ * param, exp_avg, exp_avg_sq are updated in place; grad is read. */
+#define GS_ADAM_MAX_SEGMENTS 8    /* per launch; longer lists take several */
+typedef struct gs_adam_segment {
+    float *param;
+    const float *grad;
+    float *exp_avg;
+    float *exp_avg_sq;
+    long long n;                  /* elements */
+    float step_size;
+    float bias_correction2_sqrt;
+} gs_adam_segment;
+int gs_adam_step(const gs_adam_segment *segs, int nseg, float beta1, float beta2, float eps,
+                 gs_stream_t stream);
 
 /* Byte sizes of the opaque buffers (host arithmetic, no device work). */
 size_t gs_geometry_buffer_size(int P);

@@ -136,12 +136,33 @@ def test_fused_accum_modes():
     c.register_hook(lambda g: g)  # hooked: autograd keeps the gradient
     d = torch.zeros(4, requires_grad=True)
     d.grad = torch.zeros(8)[::2]  # non-contiguous .grad
-    assert _modes_seen_in_backward([a, b, c, d]) == ["new", "add", None, None]
+    modes = _modes_seen_in_backward([a, b, c, d])
+    assert [m for m, _ in modes] == ["new", "add", None, None]
+    assert all(o is None for _, o in modes)
+
+
+def test_fused_accum_with_model_grad_mask_hooks():
+    """GaussianModel.apply_grad_mask hooks (gaussian_model.py:837-856) keep the fused path: the mask is
+    applied in-kernel; a foreign hook next to them still disables it."""
+    from dge_amd.gaussian_model import GaussianModel
+
+    m = GaussianModel(1, device="cpu")
+    P = 5
+    m.set_parameters(torch.zeros(P, 3), torch.zeros(P, 1, 3), torch.zeros(P, 3, 3), torch.zeros(P, 1),
+                     torch.zeros(P, 3), torch.zeros(P, 4))
+    modes = _modes_seen_in_backward(m.parameters())
+    assert [md for md, _ in modes] == ["new"] * 6
+    # _xyz, _features_dc, _features_rest, _opacity, _scaling carry the hook; _rotation does not
+    assert [o is m for _, o in modes] == [True, True, True, True, True, False]
+    m._xyz.grad = None
+    m._xyz.register_hook(lambda g: g)
+    (md, o), = _modes_seen_in_backward([m._xyz])
+    assert md is None and o is None
 
 
 def test_fused_accum_not_under_autograd_grad():
     a = torch.zeros(4, requires_grad=True)
-    assert _modes_seen_in_backward([a], use_autograd_grad=True) == [None]
+    assert _modes_seen_in_backward([a], use_autograd_grad=True) == [(None, None)]
 
 
 def test_fused_accum_toggle():
