@@ -39,6 +39,31 @@ def _f32(t, name):
     return t.contiguous()
 
 
+def _sh_tensor(sh):
+    """SH as the kernels take them: contiguous fp32, or contiguous fp16 (upcast in-kernel)."""
+    if sh is None or sh.numel() == 0:
+        return sh
+    if sh.dtype == torch.float16:
+        return sh.contiguous()
+    return _f32(sh, "sh")
+
+
+def _half_sh_params(P, M, means3D, sh, colors, opacity, scales, rotations, cov3D_precomp):
+    """gs_params for the reference's (already activated) inputs with fp16 SH [P,M,3]."""
+    g = N.GsParams()
+    g.P, g.M = P, M
+    g.means3D = _ptr(means3D)
+    g.sh_dc = sh.data_ptr()
+    g.sh_rest = sh.data_ptr() + 6 if M > 1 else None  # coefficient 1: 3 halves in
+    g.sh_dc_stride = g.sh_rest_stride = 3 * M
+    g.colors_precomp = None
+    g.opacities = _ptr(opacity)
+    g.scales, g.rotations, g.cov3D_precomp = _ptr(scales), _ptr(rotations), _ptr(cov3D_precomp)
+    g.activation = 0
+    g.sh_half = 1
+    return g
+
+
 class _Allocator:
     """gs_alloc_fn backed by the torch caching allocator."""
 
@@ -90,7 +115,7 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
         means3D = _f32(means3D, "means3D")
         colors, opacity = _f32(colors, "colors"), _f32(opacity, "opacity")
         scales, rotations = _f32(scales, "scales"), _f32(rotations, "rotations")
-        cov3D_precomp, sh = _f32(cov3D_precomp, "cov3D_precomp"), _f32(sh, "sh")
+        cov3D_precomp, sh = _f32(cov3D_precomp, "cov3D_precomp"), _sh_tensor(sh)
         out_color = torch.empty((3, H, W), dtype=torch.float32, device=dev)
         out_depth = torch.empty((1, H, W), dtype=torch.float32, device=dev)
         radii = torch.empty((P,), dtype=torch.int32, device=dev)
@@ -99,9 +124,15 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
                             scale_modifier, prefiltered, debug)
         alloc = _Allocator(dev)
         nr = ctypes.c_int(0)
-        rc = N.lib().gs_rasterize_forward(ctypes.byref(s), P, M, _ptr(means3D), _ptr(sh), _ptr(colors), _ptr(opacity),
-                                          _ptr(scales), _ptr(rotations), _ptr(cov3D_precomp), _ptr(out_color),
-                                          _ptr(out_depth), _ptr(radii), alloc.fn, None, _stream(dev), ctypes.byref(nr))
+        if M and sh.dtype == torch.float16:  # fp16 SH storage: the _ex entry point upcasts in-kernel
+            g = _half_sh_params(P, M, means3D, sh, colors, opacity, scales, rotations, cov3D_precomp)
+            rc = N.lib().gs_rasterize_forward_ex(ctypes.byref(s), ctypes.byref(g), _ptr(out_color), _ptr(out_depth),
+                                                 _ptr(radii), alloc.fn, None, _stream(dev), ctypes.byref(nr))
+        else:
+            rc = N.lib().gs_rasterize_forward(ctypes.byref(s), P, M, _ptr(means3D), _ptr(sh), _ptr(colors),
+                                              _ptr(opacity), _ptr(scales), _ptr(rotations), _ptr(cov3D_precomp),
+                                              _ptr(out_color), _ptr(out_depth), _ptr(radii), alloc.fn, None,
+                                              _stream(dev), ctypes.byref(nr))
         N.check(rc, "rasterize_gaussians")
         if P == 0:
             radii.zero_()
@@ -126,7 +157,7 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
         if P == 0:
             return out
         means3D = _f32(means3D, "means3D")
-        colors, sh = _f32(colors, "colors"), _f32(sh, "sh")
+        colors, sh = _f32(colors, "colors"), _sh_tensor(sh)
         scales, rotations = _f32(scales, "scales"), _f32(rotations, "rotations")
         cov3D_precomp = _f32(cov3D_precomp, "cov3D_precomp")
         radii = radii.contiguous()
@@ -136,6 +167,21 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
         s, keep = _settings(background, viewmatrix, projmatrix, campos, tan_fovx, tan_fovy, H, W, degree,
                             scale_modifier, False, debug)
         dmeans2D, dcolors, dopac, dmeans3D, dcov, dsh, dscales, drot = out
+        if M and sh.dtype == torch.float16:  # fp16 SH: _ex entry point, fp32 SH gradients [P,M,3]
+            g = _half_sh_params(P, M, means3D, sh, colors, None, scales, rotations, cov3D_precomp)
+            o = N.GsGrads()
+            o.dL_dmeans2D, o.dL_dcolors, o.dL_dopacity = _ptr(dmeans2D), _ptr(dcolors), _ptr(dopac)
+            o.dL_dmeans3D, o.dL_dcov3D = _ptr(dmeans3D), _ptr(dcov)
+            o.dL_dsh_dc = _ptr(dsh)
+            o.dL_dsh_rest = dsh.data_ptr() + 12 if M > 1 else None
+            o.dsh_dc_stride = o.dsh_rest_stride = 3 * M
+            o.dL_dscales, o.dL_drotations = _ptr(dscales), _ptr(drot)
+            rc = N.lib().gs_rasterize_backward_ex(ctypes.byref(s), ctypes.byref(g), int(R), _ptr(radii),
+                                                  _ptr(geomBuffer), _ptr(binningBuffer), _ptr(imageBuffer),
+                                                  _ptr(grad), ctypes.byref(o), _stream(dev))
+            N.check(rc, "rasterize_gaussians_backward")
+            del keep
+            return out
         rc = N.lib().gs_rasterize_backward(
             ctypes.byref(s), P, M, int(R), _ptr(means3D), _ptr(sh), _ptr(colors), _ptr(scales), _ptr(rotations),
             _ptr(cov3D_precomp), _ptr(radii), _ptr(geomBuffer), _ptr(binningBuffer), _ptr(imageBuffer), _ptr(grad),

@@ -60,6 +60,7 @@ class GsParams(ctypes.Structure):
         ("rotations", _fp),
         ("cov3D_precomp", _fp),
         ("activation", ctypes.c_int),
+        ("sh_half", ctypes.c_int),
     ]
 
 

@@ -208,6 +208,7 @@ gs_params make_params(int P, int M, const float* means3D, const float* shs, cons
     g.rotations = rotations;
     g.cov3D_precomp = cov3D_precomp;
     g.activation = 0;
+    g.sh_half = 0;
     return g;
 }
 
@@ -242,6 +243,7 @@ ShView sh_view(const gs_params& g) {
     v.rest = g.sh_rest ? g.sh_rest : g.sh_dc;
     v.dc_stride = g.sh_dc_stride;
     v.rest_stride = g.sh_rest_stride;
+    v.half = g.sh_half;
     return v;
 }
 

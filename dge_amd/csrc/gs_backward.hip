@@ -499,7 +499,10 @@ __global__ __launch_bounds__(kGB) void k_gauss_bwd_live(GaussBwdArgs a) {
                 for (int u = 0; u < kV; ++u) {
                     const int e = b + u * kGB + (int)threadIdx.x;
                     const int row = (int)(((float)e + 0.5f) * inv_ncol), col = e - row * ncol;
-                    v[u] = e < total ? a.sh.rest[(size_t)s_gid[row] * a.sh.rest_stride + col] : 0.f;
+                    const size_t off = (size_t)s_gid[row] * a.sh.rest_stride + col;
+                    v[u] = e >= total ? 0.f
+                           : a.sh.half ? __half2float(reinterpret_cast<const __half*>(a.sh.rest)[off])
+                                       : a.sh.rest[off];
                 }
 #pragma unroll
                 for (int u = 0; u < kV; ++u) {

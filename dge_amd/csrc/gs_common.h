@@ -7,6 +7,7 @@
 // (column-major transforms, auxiliary.h:58-97).
 #pragma once
 
+#include <hip/hip_fp16.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -320,6 +321,40 @@ __device__ __forceinline__ void sh_rows_load(const float* __restrict__ g, int st
 
 // With `accumulate`, the dense path skips float4s of rows that are not `live`
 // (their gradient is zero: adding it is a no-op).
+// fp16 SH rows (the local-edit path's storage): the same block transfer with
+// 2-byte elements, upcast to fp32 in LDS.  Consecutive lanes read consecutive
+// halves (128 B per wave instruction); a thread's loads are all issued first.
+template <int NT>
+__device__ __forceinline__ void sh_rows_load_half(const __half* __restrict__ g, int stride, float* __restrict__ lds,
+                                                  int nrow, int ncol, const uint8_t* live = nullptr) {
+    const int total = (nrow - 1) * stride + ncol;
+    const float inv = 1.0f / (float)stride;
+    constexpr int kV = 16;
+    for (int b = 0; b < total; b += kV * NT) {
+        __half v[kV];
+#pragma unroll
+        for (int u = 0; u < kV; ++u) {
+            const int e = b + u * NT + (int)threadIdx.x;
+            const int row = (int)(((float)e + 0.5f) * inv);
+            v[u] = e < total && (!live || live[row]) ? g[e] : __float2half(0.f);
+        }
+#pragma unroll
+        for (int u = 0; u < kV; ++u) {
+            const int e = b + u * NT + (int)threadIdx.x;
+            if (e < total) sh_element_to_lds(lds, e, __half2float(v[u]), inv, stride, ncol);
+        }
+    }
+}
+
+// coefficient 0 (3 values) of an SH row, fp32 or fp16
+__device__ __forceinline__ f3 sh_dc3(const float* dc, int half, size_t off) {
+    if (half) {
+        const __half* h = reinterpret_cast<const __half*>(dc) + off;
+        return mk3(__half2float(h[0]), __half2float(h[1]), __half2float(h[2]));
+    }
+    return ld3(dc + off);
+}
+
 template <int NT>
 __device__ __forceinline__ void sh_rows_store(float* __restrict__ g, int stride, const float* __restrict__ lds,
                                               int nrow, int ncol, bool accumulate, const uint8_t* live = nullptr) {

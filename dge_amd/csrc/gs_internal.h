@@ -167,9 +167,10 @@ inline BinLayout bin_layout(int K, int num_tiles) {
 // tensor is dc = shs, rest = shs + 3, both strides 3M; GaussianModel's raw
 // _features_dc [P,1,3] / _features_rest [P,M-1,3] are read in place (no cat).
 struct ShView {
-    const float* dc;
+    const float* dc;    // fp32, or fp16 reinterpreted when `half`
     const float* rest;
-    int dc_stride, rest_stride;
+    int dc_stride, rest_stride;  // in elements
+    int half;
 };
 struct ShGradView {
     float* dc;

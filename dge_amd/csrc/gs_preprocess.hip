@@ -21,12 +21,12 @@
 namespace gs {
 
 // forward.cu:20-71.  c0 = coefficient 0, r = coefficients 1.. (see ShView)
-__device__ __forceinline__ f3 sh_to_rgb(int deg, f3 pos, f3 campos, const float* __restrict__ c0,
-                                        const float* __restrict__ r, uint8_t& clamp_bits) {
+__device__ __forceinline__ f3 sh_to_rgb(int deg, f3 pos, f3 campos, f3 c0, const float* __restrict__ r,
+                                        uint8_t& clamp_bits) {
     f3 dir = pos - campos;
     const float len = sqrtf(dot3(dir, dir));
     dir = mk3(dir.x / len, dir.y / len, dir.z / len);
-    f3 res = ld3(c0) * kSH_C0;
+    f3 res = c0 * kSH_C0;
     if (deg > 0) {
         const float x = dir.x, y = dir.y, z = dir.z;
         res = res - ld3(r) * (kSH_C1 * y) + ld3(r + 3) * (kSH_C1 * z) - ld3(r + 6) * (kSH_C1 * x);
@@ -118,15 +118,19 @@ __global__ __launch_bounds__(256) void k_preprocess(PreprocessArgs a) {
     const int ncol = (a.M - 1) * 3 < kShPitch ? (a.M - 1) * 3 : kShPitch;
     if (__syncthreads_count(need_sh) && ncol > 0) {
         const int nrow = a.P - idx0 < 256 ? a.P - idx0 : 256;
-        sh_rows_load<256>(a.sh.rest + (size_t)idx0 * a.sh.rest_stride, a.sh.rest_stride, s_sh, nrow, ncol);
+        if (a.sh.half)
+            sh_rows_load_half<256>(reinterpret_cast<const __half*>(a.sh.rest) + (size_t)idx0 * a.sh.rest_stride,
+                                   a.sh.rest_stride, s_sh, nrow, ncol);
+        else
+            sh_rows_load<256>(a.sh.rest + (size_t)idx0 * a.sh.rest_stride, a.sh.rest_stride, s_sh, nrow, ncol);
         __syncthreads();
     }
     if (touched && a.copy_colors) {
         if (a.colors_precomp)
             rgb = ld3(a.colors_precomp + 3 * (size_t)idx);
         else
-            rgb = sh_to_rgb(a.D, p, ld3(a.campos), a.sh.dc + (size_t)idx * a.sh.dc_stride, s_sh + threadIdx.x * kShPitch,
-                            clamp_bits);
+            rgb = sh_to_rgb(a.D, p, ld3(a.campos), sh_dc3(a.sh.dc, a.sh.half, (size_t)idx * a.sh.dc_stride),
+                            s_sh + threadIdx.x * kShPitch, clamp_bits);
     }
     if (idx < a.P) {
         if (touched) {

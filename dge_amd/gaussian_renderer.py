@@ -89,7 +89,10 @@ def render(viewpoint_camera, pc, pipe, bg_color: torch.Tensor, scaling_modifier=
             dir_pp = dir_pp / dir_pp.norm(dim=1, keepdim=True)
             colors_precomp = torch.clamp_min(eval_sh(pc.active_sh_degree, shs_view, dir_pp) + 0.5, 0.0)
         else:
-            shs = pc.get_features.float()
+            # fp16 SH storage (the local-edit path) goes to the kernels as is and is upcast there;
+            # the reference's .float() would materialise an fp32 copy first
+            feats = pc.get_features
+            shs = feats if feats.dtype == torch.float16 else feats.float()
     else:
         colors_precomp = override_color
 

@@ -123,6 +123,9 @@ typedef struct gs_params {
     int activation;               /* 0: values used as given (the reference's contract);
                                      1: raw parameters: opacity = sigmoid(x), scale = exp(x),
                                         rotation = x / max(|x|, 1e-12) (F.normalize) */
+    int sh_half;                  /* 1: sh_dc / sh_rest hold IEEE fp16 values (strides in elements),
+                                     upcast in-kernel (the local-edit path's fp16 SH storage);
+                                     the SH gradients stay fp32 */
 } gs_params;
 
 /* gs_grads.accumulate bits: output i is ADDED to (out += grad) instead of

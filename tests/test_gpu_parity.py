@@ -366,3 +366,47 @@ def test_fused_gradient_accumulation(cuda_device):
         set_fused_grad_accumulation(prev)
     for g, p in zip(grads, sc2.parameters()):
         assert torch.equal(g, p.grad)
+
+
+def test_c5_local_edit_fp16_sh_vs_oracle(cuda_device, oracle):
+    """configs[4]: 1.0M-Gaussian scene, localize=True on a fixed 200k mask (sorted by x, first 20%),
+    SH stored as fp16 and upcast in-kernel, fp32 covariance inputs, 512x512 fwd+bwd through render().
+    Oracle: the same subset with the fp16-rounded SH upcast to fp32."""
+    from dge_amd.cameras import orbit_camera
+    from dge_amd.gaussian_renderer import PipelineParams, _settings, render
+    from dge_amd.scene import synthetic_scene
+
+    dev = torch.device("cuda")
+    P, Psub, W, H = 1_000_000, 200_000, 512, 512
+    sc = synthetic_scene(P, seed=0, device=dev)
+    sc._features_dc = sc._features_dc.half()
+    sc._features_rest = sc._features_rest.half()
+    order = torch.argsort(sc._xyz[:, 0])
+    mask = torch.zeros(P, dtype=torch.bool, device=dev)
+    mask[order[:Psub]] = True
+    sc.mask, sc.localize = mask, True
+    sc.requires_grad_(True)
+    cam = orbit_camera(0, 1, W, H, device=dev)
+    G = (torch.randn(3, H, W, generator=torch.Generator().manual_seed(1)) * 1e-3).to(dev)
+    pkg = render(cam, sc, PipelineParams(), torch.zeros(3, device=dev))
+    assert pkg["radii"].shape == (Psub,)
+    (pkg["render"] * G).sum().backward()
+
+    s = _settings(orbit_camera(0, 1, W, H, device="cpu"), torch.zeros(3), 1.0, 3)
+    with torch.no_grad():
+        m = mask.cpu()
+        kw = dict(means3D=sc.get_xyz.cpu().numpy(), opacities=sc.get_opacity.cpu().numpy(),
+                  shs=sc.get_features.float().cpu().numpy(), scales=sc.get_scaling.cpu().numpy(),
+                  rotations=sc.get_rotation.cpu().numpy())
+    ref = run_oracle(oracle, s, G.cpu().numpy(), **kw)
+    np.testing.assert_array_equal(pkg["radii"].cpu().numpy(), ref["radii"])
+    assert_close(pkg["render"].detach().cpu().numpy(), ref["color"], "render", allow_frac=1e-4)
+    assert_close(pkg["viewspace_points"].grad.cpu().numpy(), ref["dL_dmeans2D"], "viewspace grad", allow_frac=1e-4)
+    # the fp16 parameters' gradients: the oracle's dL_dsh scattered to the subset rows, in fp16
+    gd = sc._features_dc.grad
+    assert gd.dtype == torch.float16 and gd.shape == (P, 1, 3)
+    full = np.zeros((P, 16, 3), np.float32)
+    full[m.numpy()] = ref["dL_dsh"].reshape(Psub, 16, 3)
+    got = torch.cat([gd, sc._features_rest.grad], dim=1).float().cpu().numpy()
+    assert_close(got, full.astype(np.float16).astype(np.float32), "dL_dsh (fp16)", rtol=2e-3, allow_frac=1e-4)
+    assert np.all(got[~m.numpy()] == 0)
