@@ -17,6 +17,7 @@ functors, rasterize_points.cu:27-33) on the caller's current stream.
 from __future__ import annotations
 
 import ctypes
+import weakref
 
 import torch
 
@@ -79,9 +80,28 @@ class _Allocator:
         self.fn = N.ALLOC_FN(cb)
 
 
+_CONTIG = {}  # id(tensor) -> (weakref, _version, contiguous copy)
+
+
+def _f32_cached(t, name):
+    """_f32 for the small per-camera tensors (the reference's cameras keep transposed, non-contiguous
+    matrices: .contiguous() would copy them on every forward and backward).  The copy is reused while
+    the source tensor is alive and unmodified (same object, same version counter)."""
+    if t is None or t.numel() == 0 or t.is_contiguous():
+        return _f32(t, name)
+    ent = _CONTIG.get(id(t))
+    if ent is not None and ent[0]() is t and ent[1] == t._version:
+        return ent[2]
+    c = _f32(t, name)
+    key = id(t)
+    _CONTIG[key] = (weakref.ref(t, lambda _r, k=key: _CONTIG.pop(k, None)), t._version, c)
+    return c
+
+
 def _settings(bg, viewmatrix, projmatrix, campos, tanfovx, tanfovy, H, W, sh_degree, scale_modifier, prefiltered,
               debug):
-    keep = [_f32(bg, "bg"), _f32(viewmatrix, "viewmatrix"), _f32(projmatrix, "projmatrix"), _f32(campos, "campos")]
+    keep = [_f32(bg, "bg"), _f32_cached(viewmatrix, "viewmatrix"), _f32_cached(projmatrix, "projmatrix"),
+            _f32_cached(campos, "campos")]
     s = N.GsSettings()
     s.image_height = int(H)
     s.image_width = int(W)

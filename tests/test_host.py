@@ -170,3 +170,18 @@ def test_fused_accum_toggle():
 
     prev = set_fused_grad_accumulation(False)
     assert set_fused_grad_accumulation(prev) is False
+
+
+def test_camera_matrix_contiguous_cache():
+    """Transposed camera matrices are made contiguous once per (tensor, version), not per call."""
+    from dge_amd._C import _f32_cached
+
+    base = torch.arange(16, dtype=torch.float32).reshape(4, 4)
+    t = base.transpose(0, 1)
+    a, b = _f32_cached(t, "viewmatrix"), _f32_cached(t, "viewmatrix")
+    assert a is b and a.is_contiguous() and torch.equal(a, t)
+    t.mul_(2)  # in-place edit bumps the version counter: a fresh copy
+    c = _f32_cached(t, "viewmatrix")
+    assert c is not a and torch.equal(c, t)
+    u = torch.eye(4)
+    assert _f32_cached(u, "projmatrix") is u  # contiguous input: no copy, no cache entry
