@@ -442,7 +442,6 @@ long long gs_buffer_offset(const char* buffer, const char* field, int P, int wid
         if (!strcmp(field, "ranges")) return (long long)L.ranges;
         if (!strcmp(field, "tile_last")) return (long long)L.tile_last;
         if (!strcmp(field, "quad_last")) return (long long)L.quad_last;
-        if (!strcmp(field, "ckpt")) return (long long)L.ckpt;
     } else if (!strcmp(buffer, "binning")) {
         const int tiles = ((width + 15) / 16) * ((height + 15) / 16);
         const BinLayout L = bin_layout(num_rendered, tiles);
@@ -491,8 +490,9 @@ int gs_rasterize_forward_ex(const gs_settings* s, const gs_params* gp, float* ou
         ra.W = g.W; ra.H = g.H; ra.gx = g.gx; ra.gy = g.gy;
         ra.ranges = at<uint2>(img, il.ranges);
         ra.point_pairs = at<uint2>(bin, bl.point_pairs);
-        ra.bwd_items = at<uint32_t>(img, il.bwd_items);
+        ra.bwd_items = at<uint2>(bin, bl.bwd_items);
         ra.bwd_count = at<uint32_t>(img, il.bwd_count);
+        ra.item_cap = (uint32_t)(4 * bl.nslots);
         ra.means2D = at<float2>(geom, gl.means2D);
         ra.conic_opacity = at<float4>(geom, gl.conic_opacity);
         ra.rgbd = at<float4>(geom, gl.rgbd);
@@ -501,7 +501,7 @@ int gs_rasterize_forward_ex(const gs_settings* s, const gs_params* gp, float* ou
         ra.n_contrib = at<uint32_t>(img, il.n_contrib);
         ra.tile_last = at<uint32_t>(img, il.tile_last);
         ra.quad_last = at<uint32_t>(img, il.quad_last);
-        ra.ckpt = at<float4>(img, il.ckpt);
+        ra.ckpt = at<float4>(bin, bl.ckpt);
         ra.out_color = out_color;
         ra.out_depth = out_depth;
         ra.diag = diag_buffer(0, kDiagWords * (size_t)g.tiles * 4);
@@ -576,14 +576,16 @@ int gs_rasterize_backward_ex(const gs_settings* s, const gs_params* gp, int R, c
         GS_HIP(hipMemsetAsync(touched, 0, (size_t)P, stream));
         if (R > 0) {
             GS_HIP(hipMemsetAsync(rec_flags, 0, 4 * (size_t)R, stream));
+            uint32_t* bwd_count = at<uint32_t>(const_cast<void*>(img), il.bwd_count);
             RenderBwdArgs rb;
             rb.W = g.W; rb.H = g.H; rb.gx = g.gx; rb.gy = g.gy;
             rb.ranges = at<uint2>(img, il.ranges);
             rb.point_pairs = at<uint2>(binning, bl.point_pairs);
-            rb.bwd_items = at<uint32_t>(img, il.bwd_items);
-            rb.bwd_count = at<uint32_t>(img, il.bwd_count);
+            rb.bwd_items = at<uint2>(binning, bl.bwd_items);
+            rb.bwd_count = bwd_count;
+            rb.item_cap = (uint32_t)(4 * bl.nslots);
             rb.quad_last = at<uint32_t>(img, il.quad_last);
-            rb.ckpt = at<float4>(img, il.ckpt);
+            rb.ckpt = at<float4>(binning, bl.ckpt);
             rb.means2D = at<float2>(geom, gl.means2D);
             rb.conic_opacity = at<float4>(geom, gl.conic_opacity);
             rb.rgbd = at<float4>(geom, gl.rgbd);
@@ -594,7 +596,7 @@ int gs_rasterize_backward_ex(const gs_settings* s, const gs_params* gp, int R, c
             rb.records = records;
             rb.rec_flags = rec_flags;
             rb.touched = touched;
-            rb.diag = diag_buffer(1, kDiagWords * (size_t)g.tiles * 4 * kSegMax);
+            rb.diag = diag_buffer(1, kDiagWords * 4 * bl.nslots);
             { StageScope sc(ST_RENDER_BWD, stream); launch_render_backward(rb, stream); }
             GS_LAUNCHED("render backward");
         }

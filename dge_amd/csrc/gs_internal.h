@@ -98,25 +98,21 @@ inline GeomLayout geom_layout(int P) {
 }
 
 // Segment-parallel backward replay: the forward checkpoints every quadrant's
-// per-pixel (T, C) at list positions k*L, k = 1..kSegMax-1 (slot 0 holds the
-// final state); the backward replays each segment [k*L, (k+1)*L) of a
-// quadrant window in its own wave.  L depends only on the tile's list length.
-constexpr int kSegMax = 8;        // segments (checkpoint slots) per quadrant
-constexpr int kSegMinLen = 512;   // shortest segment, list positions
-constexpr int kBlendRound = 256;  // list entries per blend round (segment lengths are multiples)
-__host__ __device__ inline int seg_len(uint32_t list_len) {
-    const uint32_t per = (list_len + kSegMax - 1) / kSegMax;
-    const uint32_t L = (per + kBlendRound - 1) / kBlendRound * kBlendRound;
-    return (int)(L > (uint32_t)kSegMinLen ? L : (uint32_t)kSegMinLen);
-}
+// per-pixel (T, C) at list positions k*kSegLen (k >= 1; slot 0 holds the final
+// state); the backward replays each segment [k*kSegLen, (k+1)*kSegLen) of a
+// quadrant window as its own work item.  Checkpoint slots are allocated per
+// tile from its list: tile t owns slots [ckpt_base(t), ckpt_base(t) + ceil(len/kSegLen)),
+// ckpt_base(t) = range.x / kSegLen + t (monotone and non-overlapping because
+// ranges are a prefix sum), each slot 4 quadrants x 64 pixels x float4.
+constexpr int kBlendRound = 256;  // list entries per blend round
+constexpr int kSegLen = kBlendRound;  // backward segment length (checkpoints at round boundaries)
+__host__ __device__ inline uint32_t ckpt_base(uint32_t range_x, int tile) { return range_x / kSegLen + (uint32_t)tile; }
+// checkpoint slots / work items for K instances over `tiles` tiles (upper bound)
+__host__ __device__ inline size_t ckpt_slots(size_t K, int tiles) { return K / kSegLen + (size_t)tiles + 2; }
 
 struct ImgLayout {
-    size_t final_T, n_contrib, ckpt, bwd_items, ranges, tile_last, quad_last, bwd_count, total;
+    size_t final_T, n_contrib, ranges, tile_last, quad_last, bwd_count, total;
 };
-// Backward work list, built by the forward: item = quadrant * kSegMax + segment.
-// Quadrants with more than one segment append theirs at the front (counter 0),
-// single-segment quadrants at the back (counter 1): the long replays dispatch first.
-__host__ __device__ inline size_t bwd_item_capacity(int tiles) { return (size_t)tiles * 4 * kSegMax; }
 inline ImgLayout img_layout(int W, int H) {
     ImgLayout L;
     size_t o = 0;
@@ -124,19 +120,19 @@ inline ImgLayout img_layout(int W, int H) {
     size_t tiles = (size_t)div_up(W, 16) * div_up(H, 16);
     L.final_T = o; o = align_up(o + 4 * n);
     L.n_contrib = o; o = align_up(o + 4 * n);
-    L.ckpt = o; o = align_up(o + 16 * (size_t)kSegMax * 64 * 4 * tiles);  // [tiles*4][kSegMax][64] float4
-    L.bwd_items = o; o = align_up(o + 4 * bwd_item_capacity((int)tiles));
-    L.ranges = o; o = align_up(o + 8 * tiles);  // ranges.. are zeroed per forward; ckpt and items are not
+    L.ranges = o; o = align_up(o + 8 * tiles);  // ranges.. are zeroed per forward
     L.tile_last = o; o = align_up(o + 4 * tiles);
     L.quad_last = o; o = align_up(o + 16 * tiles);
-    L.bwd_count = o; o = align_up(o + 8);
+    L.bwd_count = o; o = align_up(o + 16);  // [0] multi-segment items, [1] single
     L.total = o;
     return L;
 }
 
 struct BinLayout {
-    size_t key0, key1, pair0, pair1, slot_gauss, point_pairs, records, rec_flags, sort_hist, sort_totals, total;
+    size_t key0, key1, pair0, pair1, slot_gauss, point_pairs, records, rec_flags, sort_hist, sort_totals, ckpt,
+        bwd_items, total;
     int sort_blocks;
+    size_t nslots;  // checkpoint slots = work-item capacity / 4
 };
 inline BinLayout bin_layout(int K, int num_tiles) {
     BinLayout L;
@@ -155,6 +151,9 @@ inline BinLayout bin_layout(int K, int num_tiles) {
     L.rec_flags = o; o = align_up(o + 4 * k);
     L.sort_hist = o; o = align_up(o + 4 * ((size_t)1 << maxbits) * (size_t)L.sort_blocks);
     L.sort_totals = o; o = align_up(o + 4 * ((size_t)1 << maxbits));
+    L.nslots = ckpt_slots(k, num_tiles);
+    L.ckpt = o; o = align_up(o + 16 * 64 * 4 * L.nslots);  // [slot][quadrant][64] float4 (T, C)
+    L.bwd_items = o; o = align_up(o + 8 * 4 * L.nslots);   // uint2 (tile, seg << 2 | quadrant)
     L.total = o;
     return L;
 }
@@ -255,9 +254,10 @@ struct RenderArgs {
     uint32_t* n_contrib;
     uint32_t* tile_last;
     uint32_t* quad_last;  // [tiles*4] max n_contrib per 8x8 quadrant
-    float4* ckpt;         // [tiles*4][kSegMax][64] (T, C) checkpoints for the segmented backward
-    uint32_t* bwd_items;  // backward work list (bwd_item_capacity) and its two counters
+    float4* ckpt;         // (T, C) checkpoints for the segmented backward (see ckpt_base)
+    uint2* bwd_items;     // backward work list (4 * nslots) and its counters
     uint32_t* bwd_count;
+    uint32_t item_cap;
     float* out_color;
     float* out_depth;
     uint64_t* diag;       // optional [tiles*4][kDiagWords] (see diag_buffer)
@@ -282,9 +282,9 @@ struct RenderBwdArgs {
     const uint2* point_pairs;  // per-tile lists: (Gaussian, binning slot)
     const uint32_t* quad_last;  // [tiles*4] the replay window of each quadrant wave
     const float4* ckpt;         // the forward's (T, C) checkpoints
-    const uint32_t* bwd_items;  // the forward's work list and counters
-    const uint32_t* bwd_count;
-    const uint32_t* pos_slot;   // sorted position -> binning slot (the tile sort's values)
+    const uint2* bwd_items;     // the forward's work list (capacity item_cap)
+    const uint32_t* bwd_count;  // [0] multi, [1] single items
+    uint32_t item_cap;
     const float2* means2D;
     const float4* conic_opacity;
     const float4* rgbd;
@@ -295,7 +295,7 @@ struct RenderBwdArgs {
     float4* records;     // [4*K][3] float4: one record per (slot, quadrant), kept entries only
     uint8_t* rec_flags;  // [4*K] set to 1 with each record (zeroed before the launch)
     uint8_t* touched;    // [P] set to 1 for every Gaussian that got a record (zeroed before the launch)
-    uint64_t* diag;   // optional [tiles*4][kDiagWords] (see diag_buffer)
+    uint64_t* diag;   // optional [item_cap][kDiagWords], by queue position (see diag_buffer)
 };
 void launch_render_backward(const RenderBwdArgs& a, hipStream_t s);
 

@@ -135,14 +135,13 @@ __global__ __launch_bounds__(64) void k_render_fwd(RenderArgs a) {
     for (int i = 0; i < 4; ++i) cur[i] = gather_entry(a.means2D, a.conic_opacity, a.rgbd, ids[i]);
     load_ids(range.x + kRound, ids);
 
-    const int L = seg_len(range.y - range.x);
-    float4* ckpt = a.ckpt + (size_t)blockIdx.x * kSegMax * 64;
+    // checkpoint k of this quadrant: slot ckpt_base + k, quadrant `quad`
+    float4* ckpt = a.ckpt + ((size_t)ckpt_base(range.x, tile) * 4 + quad) * 64;
     for (uint32_t b = range.x; b < range.y; b += kRound) {
         if (!__any(!done)) break;
-        {  // (T, C) at the segment boundaries of the backward replay
-            const uint32_t rel = b - range.x;
-            if (rel > 0 && rel % (uint32_t)L == 0 && rel / (uint32_t)L < (uint32_t)kSegMax)
-                ckpt[(rel / L) * 64 + lane] = make_float4(T, C0, C1, C2);
+        {  // (T, C) at the segment boundaries of the backward replay (every round start)
+            const uint32_t k = (b - range.x) / kSegLen;
+            if (k > 0) ckpt[(size_t)k * 256 + lane] = make_float4(T, C0, C1, C2);
         }
         // cull against the quadrant, compact survivors in list order (i-major, lane-minor)
         int nk = 0;
@@ -187,7 +186,8 @@ __global__ __launch_bounds__(64) void k_render_fwd(RenderArgs a) {
         __syncthreads();
     }
 
-    ckpt[lane] = make_float4(T, C0, C1, C2);  // slot 0: the final state
+    // slot 0: the final state (an empty tile's range is (0, 0): it owns no slot and has no replay)
+    if (range.y > range.x) ckpt[lane] = make_float4(T, C0, C1, C2);
     if (inside) {
         const size_t pix = (size_t)a.W * py + px;
         const size_t HW = (size_t)a.W * a.H;
@@ -199,17 +199,16 @@ __global__ __launch_bounds__(64) void k_render_fwd(RenderArgs a) {
         a.out_depth[pix] = D;
     }
     const uint32_t m = wave_max_u32(inside ? last : 0u);
-    if (m) {  // the backward replay's work items for this quadrant (see bwd_item_capacity)
-        const int nseg = (int)((m + L - 1) / L) < kSegMax ? (int)((m + L - 1) / L) : kSegMax;
-        const uint32_t item0 = blockIdx.x * (uint32_t)kSegMax;
-        if (nseg > 1) {
+    if (m) {  // the backward replay's work items for this quadrant: (tile, segment << 2 | quadrant)
+        const uint32_t nseg = (m + kSegLen - 1) / kSegLen;
+        if (nseg > 1) {  // multi-segment windows at the front of the list: they dispatch first
             uint32_t base = 0;
-            if (lane == 0) base = atomicAdd(&a.bwd_count[0], (uint32_t)nseg);
+            if (lane == 0) base = atomicAdd(&a.bwd_count[0], nseg);
             base = __shfl(base, 0);
-            if (lane < nseg) a.bwd_items[base + lane] = item0 + lane;
+            for (uint32_t k = lane; k < nseg; k += 64) a.bwd_items[base + k] = make_uint2(tile, (k << 2) | quad);
         } else if (lane == 0) {
             const uint32_t b = atomicAdd(&a.bwd_count[1], 1u);
-            a.bwd_items[bwd_item_capacity(a.gx * a.gy) - 1 - b] = item0;
+            a.bwd_items[a.item_cap - 1 - b] = make_uint2(tile, quad);
         }
     }
     if (lane == 0) {
@@ -384,37 +383,35 @@ constexpr int kBwdGroup = 4;  // entries replayed between two reduce-scatters
 // kept entry gets one 48-byte record at 4*slot + quadrant (slot: the binning
 // slot, so k_gauss_bwd reads a Gaussian's records contiguously) and a flag.
 __global__ __launch_bounds__(64, 4) void k_render_bwd(RenderBwdArgs a) {
-    // block -> work item (quadrant, segment) of the forward's list: multi-segment windows first,
-    // blocks past the list's end exit (they dispatch after every real item)
-    const int nquads = 4 * a.gx * a.gy;
-    const uint32_t n_multi = a.bwd_count[0], n_single = a.bwd_count[1];
-    if (blockIdx.x >= n_multi + n_single) return;
-    const uint32_t item = blockIdx.x < n_multi ? a.bwd_items[blockIdx.x]
-                                               : a.bwd_items[bwd_item_capacity(a.gx * a.gy) - 1 - (blockIdx.x - n_multi)];
-    const int seg = (int)(item % kSegMax);
-    const int qidx = (int)(item / kSegMax);
-    const int quad = qidx & 3, tile = qidx >> 2;
-    const int tx = tile % a.gx, ty = tile / a.gx;
-    const int lane = threadIdx.x;
-    const int bx0 = tx * kTile + (quad & 1) * kQuad, by0 = ty * kTile + (quad >> 1) * kQuad;
-    const int px = bx0 + (lane & 7), py = by0 + (lane >> 3);
-    const bool inside = px < a.W && py < a.H;
-    const float pfx = (float)px, pfy = (float)py;
-
     // kept entries of a round, compacted back to front, + a group of padding
     __shared__ float2 s_xy[kRound + kBwdGroup];
     __shared__ float4 s_co[kRound + kBwdGroup];
     __shared__ float4 s_rgb[kRound + kBwdGroup];
     __shared__ uint32_t s_pos[kRound + kBwdGroup];
     __shared__ uint32_t s_slot[kRound + kBwdGroup];
+    const int lane = threadIdx.x;
+    // block -> work item (quadrant, segment) of the forward's list: multi-segment windows first;
+    // blocks past the list's end exit (they dispatch after every real item).  (A persistent-wave
+    // work queue measured slower than the hardware dispatcher here.)
+    const uint32_t n_multi = a.bwd_count[0], n_items = n_multi + a.bwd_count[1];
+    const uint32_t qi = blockIdx.x;
+    if (qi >= n_items) return;
+    {
+    const uint2 item = qi < n_multi ? a.bwd_items[qi] : a.bwd_items[a.item_cap - 1 - (qi - n_multi)];
+    const int tile = (int)item.x, quad = (int)(item.y & 3u), seg = (int)(item.y >> 2);
+    const int qidx = 4 * tile + quad;
+    const int tx = tile % a.gx, ty = tile / a.gx;
+    const int bx0 = tx * kTile + (quad & 1) * kQuad, by0 = ty * kTile + (quad >> 1) * kQuad;
+    const int px = bx0 + (lane & 7), py = by0 + (lane >> 3);
+    const bool inside = px < a.W && py < a.H;
+    const float pfx = (float)px, pfy = (float)py;
 
     const uint2 range = a.ranges[tile];
     const int window = (int)a.quad_last[qidx];  // the quadrant's last contributor (1-based)
-    const int L = seg_len(range.y - range.x);
-    const int nseg_q = (window + L - 1) / L < kSegMax ? (window + L - 1) / L : kSegMax;
-    // this wave's segment [seg_lo, limit) of the window; the last segment takes any remainder
-    const int seg_lo = seg * L;
-    const int limit = seg == nseg_q - 1 ? window : seg_lo + L;
+    const int nseg_q = (window + kSegLen - 1) / kSegLen;
+    // this wave's segment [seg_lo, limit) of the window; the last segment ends at the window
+    const int seg_lo = seg * kSegLen;
+    const int limit = seg == nseg_q - 1 ? window : seg_lo + kSegLen;
     const size_t HW = (size_t)a.W * a.H;
     const size_t pix = inside ? (size_t)a.W * py + px : 0;
 
@@ -431,8 +428,8 @@ __global__ __launch_bounds__(64, 4) void k_render_bwd(RenderBwdArgs a) {
     if (limit < window) {
         // start inside the window: T and the colour behind position `limit` from the forward's
         // checkpoints: D = (C_final - C_limit) / T_limit, the composite of entries >= limit
-        const float4* ck = a.ckpt + (size_t)qidx * kSegMax * 64;
-        const float4 cb = ck[(limit / L) * 64 + lane], cf = ck[lane];
+        const float4* ck = a.ckpt + ((size_t)ckpt_base(range.x, tile) * 4 + quad) * 64;
+        const float4 cb = ck[(size_t)(limit / kSegLen) * 256 + lane], cf = ck[lane];
         T = cb.x;
         const float inv = 1.0f / cb.x;
         D0 = (cf.y - cb.y) * inv;
@@ -531,20 +528,23 @@ __global__ __launch_bounds__(64, 4) void k_render_bwd(RenderBwdArgs a) {
         __syncthreads();
     }
     if (a.diag && lane == 0) {
-        uint64_t* d = a.diag + kDiagWords * (size_t)(seg * nquads + qidx);
+        uint64_t* d = a.diag + kDiagWords * (size_t)qi;
         d[0] = t_start;
         d[1] = __builtin_amdgcn_s_memrealtime();
         d[2] = diag_kept;
         d[3] = diag_rounds;
         d[4] = c_replay;
         d[5] = __builtin_amdgcn_s_memtime() - c_start;
+        d[6] = (uint64_t)seg << 32 | (uint32_t)qidx;
+    }
     }
 }
 
 void launch_render_backward(const RenderBwdArgs& a, hipStream_t s) {
     const int tiles = a.gx * a.gy;
     if (tiles <= 0) return;
-    hipLaunchKernelGGL(k_render_bwd, dim3((unsigned)bwd_item_capacity(tiles)), dim3(64), 0, s, a);
+    const unsigned grid = a.item_cap;
+    hipLaunchKernelGGL(k_render_bwd, dim3(grid), dim3(64), 0, s, a);
 }
 
 }  // namespace gs

@@ -19,7 +19,8 @@ from dge_amd.scene import synthetic_scene  # noqa: E402
 
 
 def summarize(name, d, nquads=None):
-    """d: per-wave records; for the backward, rows are indexed seg * nquads + quadrant."""
+    """d: per-wave records; for the backward, rows are work-queue positions and word 6 holds
+    (segment << 32 | quadrant index)."""
     if d.size == 0:
         print(name, "no data")
         return
@@ -41,7 +42,7 @@ def summarize(name, d, nquads=None):
           f"loop cycles per kept entry (all) {cyc_loop.sum() / max(1, kept.sum()):.0f}")
     order = np.argsort(-dur)[:6]
     for i in order:
-        extra = f" seg {ids[i] // nquads} quad {ids[i] % nquads}" if nquads else ""
+        extra = f" seg {int(d[i, 6]) >> 32} quad {int(d[i, 6]) & 0xFFFFFFFF}" if nquads else ""
         print(f"   slowest: wave {ids[i]} dur {dur[i]:.1f} us kept {kept[i]} rounds {rounds[i]} loop cyc/kept "
               f"{cyc_loop[i] / max(1, kept[i]):.0f} loop share {cyc_loop[i] / max(1, cyc_total[i]):.2f} "
               f"start {(start[i] - t0) * 10e-3:.1f}{extra}")
