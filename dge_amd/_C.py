@@ -17,6 +17,7 @@ functors, rasterize_points.cu:27-33) on the caller's current stream.
 from __future__ import annotations
 
 import ctypes
+import threading
 import weakref
 
 import torch
@@ -65,19 +66,32 @@ def _half_sh_params(P, M, means3D, sh, colors, opacity, scales, rotations, cov3D
     return g
 
 
+_TLS = threading.local()
+_EMPTY_U8 = {}  # device -> empty uint8 tensor (placeholder for buffers never allocated)
+
+
+def _alloc_cb(_ctx, which, nbytes):
+    a = _TLS.alloc
+    buf = torch.empty(int(nbytes), dtype=torch.uint8, device=a.device)
+    a.buffers[which] = buf
+    return buf.data_ptr() if nbytes else None
+
+
+_ALLOC_CB = N.ALLOC_FN(_alloc_cb)  # one ctypes thunk for the process (building one per call is slow)
+
+
 class _Allocator:
-    """gs_alloc_fn backed by the torch caching allocator."""
+    """gs_alloc_fn backed by the torch caching allocator.  The C call that receives `fn` runs on this
+    thread right after construction; the shared callback finds this object through a thread-local."""
 
     def __init__(self, device):
         self.device = device
-        self.buffers = [torch.empty(0, dtype=torch.uint8, device=device) for _ in range(3)]
-
-        def cb(_ctx, which, nbytes):
-            buf = torch.empty(int(nbytes), dtype=torch.uint8, device=self.device)
-            self.buffers[which] = buf
-            return buf.data_ptr() if nbytes else None
-
-        self.fn = N.ALLOC_FN(cb)
+        e = _EMPTY_U8.get(device)
+        if e is None:
+            e = _EMPTY_U8[device] = torch.empty(0, dtype=torch.uint8, device=device)
+        self.buffers = [e, e, e]
+        _TLS.alloc = self
+        self.fn = _ALLOC_CB
 
 
 _CONTIG = {}  # id(tensor) -> (weakref, _version, contiguous copy)

@@ -180,12 +180,19 @@ def check(rc: int, what: str) -> None:
         raise NativeError(f"{what} failed (code {rc}): {last_error()}")
 
 
+_gpu_ok = False
+
+
 def require_gpu(t) -> None:
     """The product path runs only on a ROCm GPU; fail loudly otherwise."""
-    import torch
+    global _gpu_ok
+    if not _gpu_ok:
+        import torch
 
-    if not torch.cuda.is_available():
-        raise NativeError("dge_amd requires a ROCm GPU (torch.cuda.is_available() is False); no CPU fallback exists")
+        if not torch.cuda.is_available():
+            raise NativeError("dge_amd requires a ROCm GPU (torch.cuda.is_available() is False); "
+                              "no CPU fallback exists")
+        _gpu_ok = True
     if not getattr(t, "is_cuda", False):
         raise NativeError("dge_amd: tensors must live on the GPU")
 

@@ -65,7 +65,20 @@ __global__ __launch_bounds__(256) void k_preprocess(PreprocessArgs a) {
     if (idx < a.P) {
         const float* v = a.view;
         const float* pm = a.proj;
+        // every per-Gaussian input is loaded up front, culled or not (one memory round trip
+        // instead of xyz -> frustum test -> scale/rotation -> opacity)
         p = ld3(a.means3D + 3 * (size_t)idx);
+        float cov3[6];
+        float4 q = make_float4(0.f, 0.f, 0.f, 0.f);
+        f3 sc = mk3(0.f, 0.f, 0.f);
+        if (a.cov3D_precomp) {
+#pragma unroll
+            for (int k = 0; k < 6; ++k) cov3[k] = a.cov3D_precomp[6 * (size_t)idx + k];
+        } else {
+            q = *reinterpret_cast<const float4*>(a.rotations + 4 * (size_t)idx);
+            sc = ld3(a.scales + 3 * (size_t)idx);
+        }
+        const float op_in = a.opacities[idx];
         // in_frustum (auxiliary.h:139-164): only the near test is live
         const float4 ph = proj_point(pm, p);
         const float pw = 1.0f / (ph.w + 0.0000001f);
@@ -73,13 +86,7 @@ __global__ __launch_bounds__(256) void k_preprocess(PreprocessArgs a) {
         bool visible = pv.z > 0.2f;
         if (!visible && a.prefiltered) atomicOr(&a.counters[1], 1u);
         if (visible) {
-            float cov3[6];
-            if (a.cov3D_precomp) {
-#pragma unroll
-                for (int k = 0; k < 6; ++k) cov3[k] = a.cov3D_precomp[6 * (size_t)idx + k];
-            } else {
-                float4 q = *reinterpret_cast<const float4*>(a.rotations + 4 * (size_t)idx);
-                f3 sc = ld3(a.scales + 3 * (size_t)idx);
+            if (!a.cov3D_precomp) {
                 if (a.activation) {  // get_rotation / get_scaling (gaussian_model.py:228-240)
                     float len;
                     q = act_normalize(q, len);
@@ -94,7 +101,7 @@ __global__ __launch_bounds__(256) void k_preprocess(PreprocessArgs a) {
             const float det = ca * cc - cb * cb;
             if (det != 0.0f) {
                 const float det_inv = 1.f / det;
-                const float op = a.activation ? act_sigmoid(a.opacities[idx]) : a.opacities[idx];
+                const float op = a.activation ? act_sigmoid(op_in) : op_in;
                 conic = make_float4(cc * det_inv, -cb * det_inv, ca * det_inv, op);
                 const float mid = 0.5f * (ca + cc);
                 const float l1 = mid + sqrtf(fmaxf(0.1f, mid * mid - det));
@@ -116,13 +123,17 @@ __global__ __launch_bounds__(256) void k_preprocess(PreprocessArgs a) {
     // colours: precomputed, or SH evaluated from rows staged through LDS (coalesced)
     const bool need_sh = touched && a.copy_colors && !a.colors_precomp && a.sh.dc;
     const int ncol = (a.M - 1) * 3 < kShPitch ? (a.M - 1) * 3 : kShPitch;
+    __shared__ uint8_t s_need[256];
+    s_need[threadIdx.x] = need_sh;
     if (__syncthreads_count(need_sh) && ncol > 0) {
         const int nrow = a.P - idx0 < 256 ? a.P - idx0 : 256;
+        // rows of culled Gaussians are not loaded (the dense path skips them)
         if (a.sh.half)
             sh_rows_load_half<256>(reinterpret_cast<const __half*>(a.sh.rest) + (size_t)idx0 * a.sh.rest_stride,
-                                   a.sh.rest_stride, s_sh, nrow, ncol);
+                                   a.sh.rest_stride, s_sh, nrow, ncol, s_need);
         else
-            sh_rows_load<256>(a.sh.rest + (size_t)idx0 * a.sh.rest_stride, a.sh.rest_stride, s_sh, nrow, ncol);
+            sh_rows_load<256>(a.sh.rest + (size_t)idx0 * a.sh.rest_stride, a.sh.rest_stride, s_sh, nrow, ncol,
+                              s_need);
         __syncthreads();
     }
     if (touched && a.copy_colors) {

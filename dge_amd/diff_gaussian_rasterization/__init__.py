@@ -112,16 +112,22 @@ class _RasterizeGaussiansFused(torch.autograd.Function):
         into, direct = {}, []
         masked, owners = set(), set()
         if _FUSED_GRAD_ACCUM and not torch.is_grad_enabled():
-            for name, p in (("xyz", xyz), ("opacity", raw_opacity), ("scaling", raw_scaling),
-                            ("rotation", raw_rotation)):
-                mode, owner = _accumulation_mode(p)
+            # forward inputs: xyz 0, means2D 1, f_dc 2, f_rest 3, colors 4, opacity 5, scaling 6, rotation 7
+            try:
+                nf = ctx.next_functions
+            except Exception:
+                nf = None
+            node = (lambda i: nf[i][0]) if nf is not None else (lambda i: None)
+            for name, p, i in (("xyz", xyz, 0), ("opacity", raw_opacity, 5), ("scaling", raw_scaling, 6),
+                               ("rotation", raw_rotation, 7)):
+                mode, owner = _accumulation_mode(p, node(i))
                 if mode is not None:
                     into[name] = _into_target(p, mode, direct)
                     if owner is not None:
                         masked.add(name)
                         owners.add(owner)
             if ctx.has_sh:
-                (m_dc, o_dc), (m_rest, o_rest) = _accumulation_mode(f_dc), _accumulation_mode(f_rest)
+                (m_dc, o_dc), (m_rest, o_rest) = _accumulation_mode(f_dc, node(2)), _accumulation_mode(f_rest, node(3))
                 if m_dc is not None and m_dc == m_rest and o_dc is o_rest:
                     into["sh"] = ((_into_target(f_dc, m_dc, direct)[0], _into_target(f_rest, m_rest, direct)[0]),
                                   m_dc == "add")
@@ -196,7 +202,7 @@ def _mask_owner(p):
     return False, None
 
 
-def _accumulation_mode(p):
+def _accumulation_mode(p, node=None):
     """("add" | "new" | None, mask owner): "add"/"new" when this backward's gradient for leaf `p` may go
     straight into p.grad.
 
@@ -210,8 +216,11 @@ def _accumulation_mode(p):
     if not ok or getattr(p, "_post_accumulate_grad_hooks", None):
         return None, None
     try:
-        with torch.enable_grad():
-            node = p.view_as(p).grad_fn.next_functions[0][0]
+        if node is None or getattr(node, "variable", None) is not p:
+            # the leaf's AccumulateGrad node (callers inside a backward pass the one from
+            # ctx.next_functions, which avoids building a view per parameter)
+            with torch.enable_grad():
+                node = p.view_as(p).grad_fn.next_functions[0][0]
         if not torch._C._will_engine_execute_node(node):
             return None, None
     except Exception:
