@@ -277,9 +277,7 @@ int bin_forward(const gs_settings* s, const Grid& g, const gs_params& gp, int* r
     pa.prefiltered = s->prefiltered; pa.copy_colors = copy_colors;
     pa.radii_out = radii_out;
     pa.radii = at<int>(geom, gl.radii);
-    pa.means2D = at<float2>(geom, gl.means2D);
-    pa.conic_opacity = at<float4>(geom, gl.conic_opacity);
-    pa.rgbd = at<float4>(geom, gl.rgbd);
+    pa.splat = at<Splat>(geom, gl.splat);
     pa.tiles_touched = at<uint32_t>(geom, gl.tiles_touched);
     pa.clamped = at<uint8_t>(geom, gl.clamped);
     pa.depth_key = at<uint32_t>(geom, gl.key0);
@@ -308,7 +306,7 @@ int bin_forward(const gs_settings* s, const Grid& g, const gs_params& gp, int* r
     ea.order = at<uint2>(geom, cur ? gl.val1 : gl.val0);
     ea.rect_packed = pa.rect_packed;
     ea.tiles_touched = pa.tiles_touched;
-    ea.means2D = pa.means2D;
+    ea.splat = pa.splat;
     ea.radii = pa.radii;
     ea.scan_sums = at<uint32_t>(geom, gl.scan_sums);
     ea.first_slot = at<uint32_t>(geom, gl.first_slot);
@@ -427,9 +425,10 @@ long long gs_buffer_offset(const char* buffer, const char* field, int P, int wid
     if (!buffer || !field) return -1;
     if (!strcmp(buffer, "geometry")) {
         const GeomLayout L = geom_layout(P);
-        if (!strcmp(field, "means2D")) return (long long)L.means2D;
-        if (!strcmp(field, "conic_opacity")) return (long long)L.conic_opacity;
-        if (!strcmp(field, "rgbd")) return (long long)L.rgbd;
+        // the per-Gaussian render record (64 B stride: means2D at +0, conic_opacity at +16, rgbd at +32)
+        if (!strcmp(field, "splat") || !strcmp(field, "means2D")) return (long long)L.splat;
+        if (!strcmp(field, "conic_opacity")) return (long long)(L.splat + offsetof(Splat, co));
+        if (!strcmp(field, "rgbd")) return (long long)(L.splat + offsetof(Splat, rgbd));
         if (!strcmp(field, "tiles_touched")) return (long long)L.tiles_touched;
         if (!strcmp(field, "clamped")) return (long long)L.clamped;
         if (!strcmp(field, "touched")) return (long long)L.touched;
@@ -493,9 +492,7 @@ int gs_rasterize_forward_ex(const gs_settings* s, const gs_params* gp, float* ou
         ra.bwd_items = at<uint2>(bin, bl.bwd_items);
         ra.bwd_count = at<uint32_t>(img, il.bwd_count);
         ra.item_cap = (uint32_t)(4 * bl.nslots);
-        ra.means2D = at<float2>(geom, gl.means2D);
-        ra.conic_opacity = at<float4>(geom, gl.conic_opacity);
-        ra.rgbd = at<float4>(geom, gl.rgbd);
+        ra.splat = at<Splat>(geom, gl.splat);
         ra.bg = s->bg;
         ra.final_T = at<float>(img, il.final_T);
         ra.n_contrib = at<uint32_t>(img, il.n_contrib);
@@ -586,9 +583,7 @@ int gs_rasterize_backward_ex(const gs_settings* s, const gs_params* gp, int R, c
             rb.item_cap = (uint32_t)(4 * bl.nslots);
             rb.quad_last = at<uint32_t>(img, il.quad_last);
             rb.ckpt = at<float4>(binning, bl.ckpt);
-            rb.means2D = at<float2>(geom, gl.means2D);
-            rb.conic_opacity = at<float4>(geom, gl.conic_opacity);
-            rb.rgbd = at<float4>(geom, gl.rgbd);
+            rb.splat = at<Splat>(geom, gl.splat);
             rb.bg = s->bg;
             rb.final_T = at<float>(img, il.final_T);
             rb.n_contrib = at<uint32_t>(img, il.n_contrib);
@@ -679,8 +674,7 @@ int gs_apply_weights(const gs_settings* s, int P, int M, const float* means3D, f
         aw.W = g.W; aw.H = g.H; aw.gx = g.gx; aw.gy = g.gy; aw.C = num_channels;
         aw.ranges = at<uint2>(img, il.ranges);
         aw.point_pairs = at<uint2>(bin, bl.point_pairs);
-        aw.means2D = at<float2>(geom, gl.means2D);
-        aw.conic_opacity = at<float4>(geom, gl.conic_opacity);
+        aw.splat = at<Splat>(geom, gl.splat);
         aw.image_weights = image_weights;
         aw.weights = weights;
         aw.cnt = cnt;

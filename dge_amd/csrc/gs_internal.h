@@ -4,8 +4,8 @@
 // Buffer design (MI355X-first; the reference's GeometryState / BinningState /
 // ImageState live in rasterizer_impl.h:21-73 and are NOT mirrored):
 //   geometry (per Gaussian, SoA, 256-B aligned arrays):
-//     means2D float2, conic_opacity float4, rgbd float4 (colour + depth, one
-//     16-B gather in the blend loop), tiles_touched u32, clamped u8 (3 bits),
+//     splat (64-B record: means2D, conic + opacity, colour + depth — one
+//     cache-line half per gather in the blend loops), tiles_touched u32, clamped u8 (3 bits),
 //     radii i32, first_slot u32 (first binning slot of the Gaussian),
 //     depth sort ping-pong (key u32 = depth bits, val u32 = index) and scratch.
 //   binning (per tile instance): slot_gauss (emitted Gaussian per slot), the
@@ -62,8 +62,19 @@ inline TileSortPlan tile_sort_plan(int num_tiles) {
     return p;
 }
 
+// What the blend kernels gather per list entry, one 64-B record per Gaussian
+// (one cache-line half per gather instead of three lines from three arrays):
+// 2D mean, conic + opacity, colour + depth (forward.cu:251-255 outputs).
+struct alignas(64) Splat {
+    float2 xy;
+    float2 pad0;
+    float4 co;    // conic (a, b, c) + opacity
+    float4 rgbd;  // colour + view depth
+    float4 pad1;
+};
+
 struct GeomLayout {
-    size_t means2D, conic_opacity, rgbd, tiles_touched, clamped, touched, live_count, live_list, radii, first_slot;
+    size_t splat, tiles_touched, clamped, touched, live_count, live_list, radii, first_slot;
     // live_count: one u32 per 256-Gaussian block (k_gauss_live); live_list: block-local compacted ids
     size_t key0, key1, val0, val1, rect, sort_hist, sort_totals, scan_sums, counters, total;
     int sort_blocks, scan_blocks;
@@ -74,9 +85,7 @@ inline GeomLayout geom_layout(int P) {
     size_t p = (size_t)(P > 0 ? P : 1);
     L.sort_blocks = div_up((long long)p, kDepthSortTile);
     L.scan_blocks = div_up((long long)p, kScanTile);
-    L.means2D = o; o = align_up(o + 8 * p);
-    L.conic_opacity = o; o = align_up(o + 16 * p);
-    L.rgbd = o; o = align_up(o + 16 * p);
+    L.splat = o; o = align_up(o + sizeof(Splat) * p);
     L.tiles_touched = o; o = align_up(o + 4 * p);
     L.clamped = o; o = align_up(o + 1 * p);
     L.touched = o; o = align_up(o + 1 * p);
@@ -187,9 +196,7 @@ struct PreprocessArgs {
     int prefiltered, copy_colors;
     int* radii_out;
     int* radii;
-    float2* means2D;
-    float4* conic_opacity;
-    float4* rgbd;
+    Splat* splat;
     uint32_t* tiles_touched;
     uint8_t* clamped;
     uint32_t* depth_key;
@@ -229,7 +236,7 @@ struct EmitArgs {
     int rect_packed;
     const uint2* order;          // by depth rank: (packed rect or tiles_touched, Gaussian id)
     const uint32_t* tiles_touched;
-    const float2* means2D;
+    const Splat* splat;
     const int* radii;
     uint32_t* scan_sums;         // [scan_blocks + 1]
     uint32_t* first_slot;
@@ -246,9 +253,7 @@ struct RenderArgs {
     int W, H, gx, gy;
     const uint2* ranges;
     const uint2* point_pairs;  // per-tile lists: (Gaussian, binning slot)
-    const float2* means2D;
-    const float4* conic_opacity;
-    const float4* rgbd;
+    const Splat* splat;
     const float* bg;
     float* final_T;
     uint32_t* n_contrib;
@@ -268,8 +273,7 @@ struct ApplyWeightsArgs {
     int W, H, gx, gy, C;
     const uint2* ranges;
     const uint2* point_pairs;  // per-tile lists: (Gaussian, binning slot)
-    const float2* means2D;
-    const float4* conic_opacity;
+    const Splat* splat;
     const float* image_weights;
     float* weights;
     int* cnt;
@@ -285,9 +289,7 @@ struct RenderBwdArgs {
     const uint2* bwd_items;     // the forward's work list (capacity item_cap)
     const uint32_t* bwd_count;  // [0] multi, [1] single items
     uint32_t item_cap;
-    const float2* means2D;
-    const float4* conic_opacity;
-    const float4* rgbd;
+    const Splat* splat;
     const float* bg;
     const float* final_T;
     const uint32_t* n_contrib;

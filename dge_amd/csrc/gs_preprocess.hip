@@ -145,9 +145,13 @@ __global__ __launch_bounds__(256) void k_preprocess(PreprocessArgs a) {
     }
     if (idx < a.P) {
         if (touched) {
-            a.means2D[idx] = pix;
-            a.conic_opacity[idx] = conic;
-            a.rgbd[idx] = make_float4(rgb.x, rgb.y, rgb.z, depth);
+            Splat sp;
+            sp.xy = pix;
+            sp.pad0 = make_float2(0.f, 0.f);
+            sp.co = conic;
+            sp.rgbd = make_float4(rgb.x, rgb.y, rgb.z, depth);
+            sp.pad1 = make_float4(0.f, 0.f, 0.f, 0.f);
+            a.splat[idx] = sp;
         }
         a.radii[idx] = radius_out;
         if (a.radii_out) a.radii_out[idx] = radius_out;

@@ -63,12 +63,12 @@ struct Entry {
     float4 f;  // rgb + depth
 };
 
-__device__ __forceinline__ Entry gather_entry(const float2* means2D, const float4* conic_opacity, const float4* rgbd,
-                                              uint32_t id) {
+__device__ __forceinline__ Entry gather_entry(const Splat* splat, uint32_t id) {
+    const Splat* sp = splat + id;
     Entry e;
-    e.xy = means2D[id];
-    e.co = conic_opacity[id];
-    e.f = rgbd[id];
+    e.xy = sp->xy;
+    e.co = sp->co;
+    e.f = sp->rgbd;
     return e;
 }
 
@@ -132,7 +132,7 @@ __global__ __launch_bounds__(64) void k_render_fwd(RenderArgs a) {
     Entry cur[4];
     load_ids(range.x, ids);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) cur[i] = gather_entry(a.means2D, a.conic_opacity, a.rgbd, ids[i]);
+    for (int i = 0; i < 4; ++i) cur[i] = gather_entry(a.splat, ids[i]);
     load_ids(range.x + kRound, ids);
 
     // checkpoint k of this quadrant: slot ckpt_base + k, quadrant `quad`
@@ -170,7 +170,7 @@ __global__ __launch_bounds__(64) void k_render_fwd(RenderArgs a) {
         diag_rounds += 1;
         // next round's gathers and the round after's ids, in flight during the blend
 #pragma unroll
-        for (int i = 0; i < 4; ++i) cur[i] = gather_entry(a.means2D, a.conic_opacity, a.rgbd, ids[i]);
+        for (int i = 0; i < 4; ++i) cur[i] = gather_entry(a.splat, ids[i]);
         load_ids(b + 2 * kRound, ids);
         __syncthreads();
 
@@ -266,8 +266,8 @@ __global__ __launch_bounds__(64) void k_render_apply_weights(ApplyWeightsArgs a)
         uint32_t id = 0;
         if (k < range.y) {
             id = a.point_pairs[k].x;
-            xy = a.means2D[id];
-            co = a.conic_opacity[id];
+            xy = a.splat[id].xy;
+            co = a.splat[id].co;
             keep = cull_keep(xy, co, (float)bx0, (float)by0);
         }
         const uint64_t km = __ballot(keep);
@@ -463,7 +463,7 @@ __global__ __launch_bounds__(64, 4) void k_render_bwd(RenderBwdArgs a) {
     round_pairs(0, pairs);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        cur[i] = gather_entry(a.means2D, a.conic_opacity, a.rgbd, pairs[i].x);
+        cur[i] = gather_entry(a.splat, pairs[i].x);
         slots[i] = pairs[i].y;
     }
     round_pairs(1, pairs);
@@ -498,7 +498,7 @@ __global__ __launch_bounds__(64, 4) void k_render_bwd(RenderBwdArgs a) {
         // next round's geometry and the round after's ids, in flight during the replay
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            cur[i] = gather_entry(a.means2D, a.conic_opacity, a.rgbd, pairs[i].x);
+            cur[i] = gather_entry(a.splat, pairs[i].x);
             slots[i] = pairs[i].y;  // the current round's slots are already staged
             }
         round_pairs(r + 2, pairs);

@@ -369,7 +369,7 @@ __global__ __launch_bounds__(256) void k_scan_emit(EmitArgs a) {
                 q.x0 = (int)(gr.x & 0xFFu); q.y0 = (int)((gr.x >> 8) & 0xFFu);
                 q.x1 = (int)((gr.x >> 16) & 0xFFu); q.y1 = (int)(gr.x >> 24);
             } else {
-                const float2 xy = a.means2D[g];
+                const float2 xy = a.splat[g].xy;
                 q = tile_rect(xy.x, xy.y, a.radii[g], a.gx, a.gy);
             }
             s_rect[threadIdx.x] = make_int4(q.x0, q.y0, q.x1 - q.x0, 0);

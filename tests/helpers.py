@@ -123,9 +123,10 @@ def run_gpu(settings, dL_dpix=None, means3D=None, opacities=None, shs=None, colo
             return buf[off:off + nbytes].cpu().numpy().view(dtype).copy()
 
         tiles = ((W + 15) // 16) * ((H + 15) // 16)
-        out["means2D"] = view(geom, "geometry", "means2D", np.float32, 2 * P).reshape(P, 2)
-        out["conic_opacity"] = view(geom, "geometry", "conic_opacity", np.float32, 4 * P).reshape(P, 4)
-        out["rgbd"] = view(geom, "geometry", "rgbd", np.float32, 4 * P).reshape(P, 4)
+        sp = view(geom, "geometry", "splat", np.float32, 16 * P).reshape(P, 16)  # 64-B records
+        out["means2D"] = np.ascontiguousarray(sp[:, 0:2])
+        out["conic_opacity"] = np.ascontiguousarray(sp[:, 4:8])
+        out["rgbd"] = np.ascontiguousarray(sp[:, 8:12])
         out["tiles_touched"] = view(geom, "geometry", "tiles_touched", np.uint32, P)
         out["clamped"] = view(geom, "geometry", "clamped", np.uint8, P)
         out["final_T"] = view(img, "image", "final_T", np.float32, W * H)

@@ -42,7 +42,7 @@ def test_buffer_offsets_are_aligned_and_distinct():
     lib = N.load_library()
     P, W, H, K = 12345, 100, 37, 5000
     geo = [lib.gs_buffer_offset(b"geometry", f, P, W, H, K) for f in
-           (b"means2D", b"conic_opacity", b"rgbd", b"tiles_touched", b"clamped", b"radii", b"first_slot")]
+           (b"splat", b"tiles_touched", b"clamped", b"radii", b"first_slot")]
     assert all(o >= 0 and o % 256 == 0 for o in geo) and len(set(geo)) == len(geo)
     assert geo[-1] < lib.gs_geometry_buffer_size(P)
     img = [lib.gs_buffer_offset(b"image", f, P, W, H, K) for f in (b"final_T", b"n_contrib", b"ranges", b"tile_last")]

@@ -15,8 +15,8 @@ import os
 import sys
 
 STAGE = {"k_preprocess": "preprocess", "k_render_fwd": "render_fwd", "k_render_bwd": "render_bwd",
-         "k_gauss_bwd": "gauss_bwd", "k_render_apply_weights": "apply_weights", "k_ranges": "ranges",
-         "k_scan_emit": "emit"}
+         "k_gauss_live": "gauss_bwd", "k_gauss_bwd_live": "gauss_bwd", "k_render_apply_weights": "apply_weights",
+         "k_ranges": "ranges", "k_scan_emit": "emit"}
 
 
 def main(root):
@@ -36,9 +36,14 @@ def main(root):
         if k in STAGE and "FETCH_SIZE" in c and "WRITE_SIZE" in c:
             rd = 2.0 * c["FETCH_SIZE"] * 1024.0
             wr = c["WRITE_SIZE"] * 1024.0
-            out[STAGE[k]] = {"kernel": k, "read_bytes_per_launch": int(rd), "write_bytes_per_launch": int(wr),
-                             "bytes_per_launch": int(rd + wr),
-                             "method": "rocprofv3 --pmc FETCH_SIZE (x2, gfx950 correction) + WRITE_SIZE, separate passes"}
+            e = out.setdefault(STAGE[k], {"kernel": [], "read_bytes_per_launch": 0, "write_bytes_per_launch": 0,
+                                          "bytes_per_launch": 0,
+                                          "method": "rocprofv3 --pmc FETCH_SIZE (x2, gfx950 correction) + "
+                                                    "WRITE_SIZE, separate passes; a stage's kernels summed"})
+            e["kernel"].append(k)
+            e["read_bytes_per_launch"] += int(rd)
+            e["write_bytes_per_launch"] += int(wr)
+            e["bytes_per_launch"] += int(rd + wr)
     if out:
         dst = os.path.join(root, "pmc_traffic.json")  # copied into profiles/ by hand after the run
         json.dump(out, open(dst, "w"), indent=1)
