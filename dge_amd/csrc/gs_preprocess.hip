@@ -62,6 +62,19 @@ __global__ __launch_bounds__(256) void k_preprocess(PreprocessArgs a) {
     float2 pix = make_float2(0.f, 0.f);
     float4 conic = make_float4(0.f, 0.f, 0.f, 0.f);
     float depth = 0.f;
+    // SH rows of the whole block staged first, in flight together with the per-Gaussian loads below
+    // (one memory phase instead of geometry -> compute -> SH rows); rows of Gaussians that turn out
+    // culled are read needlessly (180 B each), which object-centric views hardly have
+    const int ncol = (a.M - 1) * 3 < kShPitch ? (a.M - 1) * 3 : kShPitch;
+    const bool stage_sh = a.copy_colors && !a.colors_precomp && a.sh.dc && ncol > 0;
+    if (stage_sh) {
+        const int nrow = a.P - idx0 < 256 ? a.P - idx0 : 256;
+        if (a.sh.half)
+            sh_rows_load_half<256>(reinterpret_cast<const __half*>(a.sh.rest) + (size_t)idx0 * a.sh.rest_stride,
+                                   a.sh.rest_stride, s_sh, nrow, ncol);
+        else
+            sh_rows_load<256>(a.sh.rest + (size_t)idx0 * a.sh.rest_stride, a.sh.rest_stride, s_sh, nrow, ncol);
+    }
     if (idx < a.P) {
         const float* v = a.view;
         const float* pm = a.proj;
@@ -122,20 +135,8 @@ __global__ __launch_bounds__(256) void k_preprocess(PreprocessArgs a) {
     }
     // colours: precomputed, or SH evaluated from rows staged through LDS (coalesced)
     const bool need_sh = touched && a.copy_colors && !a.colors_precomp && a.sh.dc;
-    const int ncol = (a.M - 1) * 3 < kShPitch ? (a.M - 1) * 3 : kShPitch;
-    __shared__ uint8_t s_need[256];
-    s_need[threadIdx.x] = need_sh;
-    if (__syncthreads_count(need_sh) && ncol > 0) {
-        const int nrow = a.P - idx0 < 256 ? a.P - idx0 : 256;
-        // rows of culled Gaussians are not loaded (the dense path skips them)
-        if (a.sh.half)
-            sh_rows_load_half<256>(reinterpret_cast<const __half*>(a.sh.rest) + (size_t)idx0 * a.sh.rest_stride,
-                                   a.sh.rest_stride, s_sh, nrow, ncol, s_need);
-        else
-            sh_rows_load<256>(a.sh.rest + (size_t)idx0 * a.sh.rest_stride, a.sh.rest_stride, s_sh, nrow, ncol,
-                              s_need);
-        __syncthreads();
-    }
+    (void)need_sh;
+    if (stage_sh) __syncthreads();  // SH rows staged
     if (touched && a.copy_colors) {
         if (a.colors_precomp)
             rgb = ld3(a.colors_precomp + 3 * (size_t)idx);
