@@ -499,6 +499,7 @@ int gs_rasterize_forward_ex(const gs_settings* s, const gs_params* gp, float* ou
         ra.tile_last = at<uint32_t>(img, il.tile_last);
         ra.quad_last = at<uint32_t>(img, il.quad_last);
         ra.ckpt = at<float4>(bin, bl.ckpt);
+        ra.used = at<uint64_t>(bin, bl.used);
         ra.out_color = out_color;
         ra.out_depth = out_depth;
         ra.diag = diag_buffer(0, kDiagWords * (size_t)g.tiles * 4);
@@ -583,6 +584,7 @@ int gs_rasterize_backward_ex(const gs_settings* s, const gs_params* gp, int R, c
             rb.item_cap = (uint32_t)(4 * bl.nslots);
             rb.quad_last = at<uint32_t>(img, il.quad_last);
             rb.ckpt = at<float4>(binning, bl.ckpt);
+            rb.used = at<uint64_t>(binning, bl.used);
             rb.splat = at<Splat>(geom, gl.splat);
             rb.bg = s->bg;
             rb.final_T = at<float>(img, il.final_T);

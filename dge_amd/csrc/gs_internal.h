@@ -118,6 +118,13 @@ constexpr int kSegLen = kBlendRound;  // backward segment length (checkpoints at
 __host__ __device__ inline uint32_t ckpt_base(uint32_t range_x, int tile) { return range_x / kSegLen + (uint32_t)tile; }
 // checkpoint slots / work items for K instances over `tiles` tiles (upper bound)
 __host__ __device__ inline size_t ckpt_slots(size_t K, int tiles) { return K / kSegLen + (size_t)tiles + 2; }
+// Per (quadrant, list position) "blended by some pixel" bits, written by the forward
+// and read by the backward instead of re-running the quadrant cull (exact: the
+// backward's per-pixel hits are the forward's).  Tile t's words start at
+// used_base(t) (64 positions per word), 4 quadrants interleaved: word w of
+// quadrant q is used[(used_base + w) * 4 + q].
+__host__ __device__ inline uint32_t used_base(uint32_t range_x, int tile) { return range_x / 64 + (uint32_t)tile; }
+__host__ __device__ inline size_t used_words(size_t K, int tiles) { return 4 * (K / 64 + (size_t)tiles + 2); }
 
 struct ImgLayout {
     size_t final_T, n_contrib, ranges, tile_last, quad_last, bwd_count, total;
@@ -139,7 +146,7 @@ inline ImgLayout img_layout(int W, int H) {
 
 struct BinLayout {
     size_t key0, key1, pair0, pair1, slot_gauss, point_pairs, records, rec_flags, sort_hist, sort_totals, ckpt,
-        bwd_items, total;
+        bwd_items, used, total;
     int sort_blocks;
     size_t nslots;  // checkpoint slots = work-item capacity / 4
 };
@@ -163,6 +170,7 @@ inline BinLayout bin_layout(int K, int num_tiles) {
     L.nslots = ckpt_slots(k, num_tiles);
     L.ckpt = o; o = align_up(o + 16 * 64 * 4 * L.nslots);  // [slot][quadrant][64] float4 (T, C)
     L.bwd_items = o; o = align_up(o + 8 * 4 * L.nslots);   // uint2 (tile, seg << 2 | quadrant)
+    L.used = o; o = align_up(o + 8 * used_words(k, num_tiles));
     L.total = o;
     return L;
 }
@@ -260,6 +268,7 @@ struct RenderArgs {
     uint32_t* tile_last;
     uint32_t* quad_last;  // [tiles*4] max n_contrib per 8x8 quadrant
     float4* ckpt;         // (T, C) checkpoints for the segmented backward (see ckpt_base)
+    uint64_t* used;       // per (quadrant, position) blended bits (see used_base)
     uint2* bwd_items;     // backward work list (4 * nslots) and its counters
     uint32_t* bwd_count;
     uint32_t item_cap;
@@ -286,6 +295,7 @@ struct RenderBwdArgs {
     const uint2* point_pairs;  // per-tile lists: (Gaussian, binning slot)
     const uint32_t* quad_last;  // [tiles*4] the replay window of each quadrant wave
     const float4* ckpt;         // the forward's (T, C) checkpoints
+    const uint64_t* used;       // the forward's blended bits: the backward's exact cull
     const uint2* bwd_items;     // the forward's work list (capacity item_cap)
     const uint32_t* bwd_count;  // [0] multi, [1] single items
     uint32_t item_cap;

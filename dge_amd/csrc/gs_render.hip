@@ -75,7 +75,7 @@ __device__ __forceinline__ Entry gather_entry(const Splat* splat, uint32_t id) {
 // Blend one entry into the pixel state without branches: every lane evaluates
 // the reference's tests (forward.cu:336-358) and selects.  A pixel that is
 // done, skipped, or saturates on this entry keeps its state bit-for-bit.
-__device__ __forceinline__ void blend_step(float2 xy, float4 co, float4 fe, uint32_t pos, float pfx, float pfy,
+__device__ __forceinline__ bool blend_step(float2 xy, float4 co, float4 fe, uint32_t pos, float pfx, float pfy,
                                           bool& done, float& T, float& C0, float& C1, float& C2, float& D,
                                           uint32_t& last) {
     float dx, dy, G, alpha;
@@ -91,6 +91,7 @@ __device__ __forceinline__ void blend_step(float2 xy, float4 co, float4 fe, uint
     D = use ? D + fe.w * w : D;
     T = use ? test_T : T;
     last = use ? pos : last;
+    return use;
 }
 
 __global__ __launch_bounds__(64) void k_render_fwd(RenderArgs a) {
@@ -106,8 +107,10 @@ __global__ __launch_bounds__(64) void k_render_fwd(RenderArgs a) {
     __shared__ float4 s_co[kRound + kGroup];
     __shared__ float4 s_rgbd[kRound + kGroup];
     __shared__ uint32_t s_pos[kRound + kGroup];
+    __shared__ uint32_t s_gused[kRound / kGroup + 1];  // per blend group: bit u = entry u was blended
 
     const uint2 range = a.ranges[tile];
+    uint64_t* used = a.used + (size_t)used_base(range.x, tile) * 4 + quad;
     float T = 1.0f, C0 = 0.f, C1 = 0.f, C2 = 0.f, D = 0.f;
     uint32_t last = 0;
     bool done = !inside;
@@ -145,13 +148,15 @@ __global__ __launch_bounds__(64) void k_render_fwd(RenderArgs a) {
         }
         // cull against the quadrant, compact survivors in list order (i-major, lane-minor)
         int nk = 0;
+        int kslot[4];  // compacted slot of this lane's entry i (-1: culled)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const uint32_t k = b + 64 * i + lane;
             const bool keep = k < range.y && cull_keep(cur[i].xy, cur[i].co, (float)bx0, (float)by0);
             const uint64_t km = __ballot(keep);
+            kslot[i] = keep ? nk + __popcll(km & lanemask_lt()) : -1;
             if (keep) {
-                const int slot = nk + __popcll(km & lanemask_lt());
+                const int slot = kslot[i];
                 s_xy[slot] = cur[i].xy;
                 s_co[slot] = cur[i].co;
                 s_rgbd[slot] = cur[i].f;
@@ -172,18 +177,35 @@ __global__ __launch_bounds__(64) void k_render_fwd(RenderArgs a) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) cur[i] = gather_entry(a.splat, ids[i]);
         load_ids(b + 2 * kRound, ids);
+        if (lane <= kRound / kGroup) s_gused[lane] = 0u;  // (groups past an early exit stay 0)
         __syncthreads();
 
         const uint64_t c0 = a.diag ? __builtin_amdgcn_s_memtime() : 0;
         for (int j = 0; j < nk; j += kGroup) {
             if (!__any(!done)) break;
+            uint32_t gm = 0u;  // (uniform: scalar ops beside the blend's vector ones)
 #pragma unroll
-            for (int u = 0; u < kGroup; ++u)
-                blend_step(s_xy[j + u], s_co[j + u], s_rgbd[j + u], s_pos[j + u], pfx, pfy, done, T, C0, C1, C2, D,
-                           last);
+            for (int u = 0; u < kGroup; ++u) {
+                const bool use = blend_step(s_xy[j + u], s_co[j + u], s_rgbd[j + u], s_pos[j + u], pfx, pfy, done, T,
+                                            C0, C1, C2, D, last);
+                gm |= (__ballot(use) != 0ull ? 1u : 0u) << u;
+            }
+            s_gused[j / kGroup] = gm;
         }
         if (a.diag) c_blend += __builtin_amdgcn_s_memtime() - c0;
         __syncthreads();
+        // the round's blended bits in list order, one ballot per word (words of rounds the wave
+        // never reaches stay unwritten: past every pixel's last contributor, outside every replay)
+        uint64_t words[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int sl = kslot[i];
+            words[i] = __ballot(sl >= 0 && ((s_gused[sl / kGroup] >> (sl % kGroup)) & 1u));
+        }
+        const uint32_t rel = b - range.x;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)  // (the list's own words only: the next tile's start here)
+            if (lane == i && rel + 64 * i < range.y - range.x) used[(size_t)(rel / 64 + i) * 4] = words[i];
     }
 
     // slot 0: the final state (an empty tile's range is (0, 0): it owns no slot and has no replay)
@@ -388,7 +410,6 @@ __global__ __launch_bounds__(64, 4) void k_render_bwd(RenderBwdArgs a) {
     __shared__ float4 s_co[kRound + kBwdGroup];
     __shared__ float4 s_rgb[kRound + kBwdGroup];
     __shared__ uint32_t s_pos[kRound + kBwdGroup];
-    __shared__ uint32_t s_slot[kRound + kBwdGroup];
     const int lane = threadIdx.x;
     // block -> work item (quadrant, segment) of the forward's list: multi-segment windows first;
     // blocks past the list's end exit (they dispatch after every real item).  (A persistent-wave
@@ -448,35 +469,50 @@ __global__ __launch_bounds__(64, 4) void k_render_bwd(RenderBwdArgs a) {
     const bool row_writer = (lane & 15) == 0;
 
     const int nr = (limit - seg_lo + kRound - 1) / kRound;
-    // (Gaussian, slot) of each entry of round r; two rounds ahead of the replay
-    auto round_pairs = [&](int r, uint2 (&pr)[4]) {
+    const uint64_t* used = a.used + (size_t)used_base(range.x, tile) * 4 + quad;
+    // (Gaussian, slot) and the forward's blended bit of each entry of round r, two rounds ahead
+    // of the replay.  An entry no pixel of the quadrant blended has an all-zero gradient: the
+    // bit is the exact cull (the forward's `use` is the replay's `hit && pos < n_contrib`).
+    // (the 32-bit half of the word holding each entry's bit; decoded where the pairs are consumed)
+    const uint32_t* used32 = reinterpret_cast<const uint32_t*>(used);
+    auto round_pairs = [&](int r, uint2 (&pr)[4], uint32_t (&ub)[4]) {
         const int hi = limit - kRound * r, lo = hi - kRound > seg_lo ? hi - kRound : seg_lo;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int k = lo + 64 * i + lane;
-            pr[i] = r < nr && k < hi ? a.point_pairs[range.x + k] : make_uint2(0u, 0u);
+            const bool in = r < nr && k < hi;
+            pr[i] = in ? a.point_pairs[range.x + k] : make_uint2(0u, 0u);
+            ub[i] = in ? used32[(size_t)(k >> 6) * 8 + ((k >> 5) & 1)] : 0u;
         }
     };
-    uint2 pairs[4];
-    uint32_t slots[4];
-    Entry cur[4];
-    round_pairs(0, pairs);
+    // the round's kept bits (bit i: entry lo + 64 i + lane) from its loaded halves
+    auto kept_bits = [&](int r, const uint32_t (&ub)[4]) {
+        const int hi = limit - kRound * r, lo = hi - kRound > seg_lo ? hi - kRound : seg_lo;
+        uint32_t kb = 0u;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        cur[i] = gather_entry(a.splat, pairs[i].x);
-        slots[i] = pairs[i].y;
+        for (int i = 0; i < 4; ++i) kb |= ((ub[i] >> ((lo + 64 * i + lane) & 31)) & 1u) << i;
+        return kb;
+    };
+    uint2 pairs[4];
+    uint32_t ubits[4], kb_cur;
+    Entry cur[4];
+    round_pairs(0, pairs, ubits);
+    kb_cur = kept_bits(0, ubits);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {  // (dropped entries gather Gaussian 0: one shared line)
+        cur[i] = gather_entry(a.splat, (kb_cur >> i) & 1u ? pairs[i].x : 0u);
     }
-    round_pairs(1, pairs);
+    round_pairs(1, pairs, ubits);
 
     for (int r = 0; r < nr; ++r) {
         const int hi = limit - kRound * r, lo = hi - kRound > seg_lo ? hi - kRound : seg_lo;
         const int n = hi - lo;
-        // cull this round (in registers) and compact the survivors back to front
+        // compact the forward's blended entries back to front
         int nk = 0;
 #pragma unroll
         for (int i = 3; i >= 0; --i) {
             const int j = 64 * i + lane;
-            const bool keep = j < n && cull_keep(cur[i].xy, cur[i].co, (float)bx0, (float)by0);
+            const bool keep = j < n && ((kb_cur >> i) & 1u);
             const uint64_t km = __ballot(keep);
             if (keep) {
                 const int slot = nk + __popcll(km & ~lanemask_lt() & ~(1ull << lane));
@@ -484,7 +520,6 @@ __global__ __launch_bounds__(64, 4) void k_render_bwd(RenderBwdArgs a) {
                 s_co[slot] = cur[i].co;
                 s_rgb[slot] = cur[i].f;
                 s_pos[slot] = (uint32_t)(lo + j);
-                s_slot[slot] = slots[i];
             }
             nk += __popcll(km);
         }
@@ -493,15 +528,14 @@ __global__ __launch_bounds__(64, 4) void k_render_bwd(RenderBwdArgs a) {
             s_co[nk + lane] = make_float4(0.f, 0.f, 0.f, 0.f);
             s_rgb[nk + lane] = make_float4(0.f, 0.f, 0.f, 0.f);
             s_pos[nk + lane] = 0xFFFFFFFFu;
-            s_slot[nk + lane] = 0u;
         }
         // next round's geometry and the round after's ids, in flight during the replay
+        kb_cur = kept_bits(r + 1, ubits);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            cur[i] = gather_entry(a.splat, pairs[i].x);
-            slots[i] = pairs[i].y;  // the current round's slots are already staged
-            }
-        round_pairs(r + 2, pairs);
+            cur[i] = gather_entry(a.splat, (kb_cur >> i) & 1u ? pairs[i].x : 0u);
+        }
+        round_pairs(r + 2, pairs, ubits);
         diag_kept += nk;
         diag_rounds += 1;
         __syncthreads();
@@ -518,10 +552,11 @@ __global__ __launch_bounds__(64, 4) void k_render_bwd(RenderBwdArgs a) {
             for (int f = 0; f < 9; ++f) S[f] = quad_reduce(g[0][f], g[1][f], g[2][f], g[3][f]);
             const int kw = k + row_entry;
             if (row_writer && kw < nk) {
-                const size_t rec = 4 * (size_t)s_slot[kw] + quad;
+                const uint2 pr = a.point_pairs[range.x + s_pos[kw]];  // (an L2 hit: this round's pairs)
+                const size_t rec = 4 * (size_t)pr.y + quad;
                 finish_record(s_co[kw], S, ddelx_dx, ddely_dy, a.records + 3 * rec);
                 a.rec_flags[rec] = 1;
-                a.touched[a.point_pairs[range.x + s_pos[kw]].x] = 1;  // (an L2 hit: this round's ids)
+                a.touched[pr.x] = 1;
             }
         }
         if (a.diag) c_replay += __builtin_amdgcn_s_memtime() - c0;

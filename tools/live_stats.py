@@ -49,3 +49,11 @@ mx = np.zeros_like(cnt)
 np.maximum.at(mx, grp, n)
 print("per block: live mean %.1f max %d; max n per block p50 %d p90 %d max %d" %
       (cnt.mean(), cnt.max(), np.percentile(mx, 50), np.percentile(mx, 90), mx.max()))
+
+# records whose nine sums are all zero (kept by the quadrant cull, no pixel contributed)
+roff = off(b"binning", b"records")
+rec = binning[roff:roff + 4 * K * 48].view(torch.float32).view(4 * K, 12)
+flags = binning[off(b"binning", b"rec_flags"):][:4 * K] != 0
+r = rec[flags]
+nz = (r[:, :9].abs().sum(dim=1) != 0)
+print("records", int(flags.sum()), "all-zero", int((~nz).sum()), "frac %.3f" % float((~nz).float().mean()))
