@@ -4,10 +4,16 @@
 Workload (BASELINE.json configs[1], "c2"): 1.0M Gaussians (SH degree 3),
 512x512, fp32, one render() forward + its backward per view, seeded synthetic
 scene and orbit cameras of SURVEY.md §8(d) (no network: data = synthetic).
-A step = every rank renders its `--views-per-rank` views (forward + backward
-through autograd, gradients accumulated into the shared parameters) and, for
-N > 1, ONE all-reduce of the flat parameter-gradient bucket (RCCL); per-GPU
-work is fixed, so scaling is weak and value = all views rendered / max-rank time.
+A step = every rank renders its `--views-per-rank` views, forward + backward
+each (the gradients of the reference's batch step — threestudio/systems/DGE.py
+renders the batch's views and back-propagates the summed loss — up to float
+summation order), accumulated into the shared parameters, and, for N > 1, ONE
+all-reduce of the flat parameter-gradient bucket (RCCL).  `--streams N`
+alternates the views over N HIP streams (dge_amd.multiview.render_backward_views:
+one view's backward overlapping the next view's forward; default 1) and
+`--batch-backward` runs all forwards first, then one backward, as the
+reference orders it.  Per-GPU work
+is fixed, so scaling is weak and value = all views rendered / max-rank time.
 
 Prints ONE JSON line (rank 0) with the contract keys plus `roofline` (the
 dominant kernel, timed live with HIP events on its stream through the C ABI's
@@ -43,6 +49,12 @@ def parse():
     ap.add_argument("--height", type=int, default=512)
     ap.add_argument("--sh-degree", type=int, default=3)
     ap.add_argument("--views-per-rank", type=int, default=3)
+    ap.add_argument("--streams", type=int, default=1,
+                    help="HIP streams the views alternate over (2 measured slower at c2: the host side, one "
+                         "blocking instance-count read-back per forward, is then the limit)")
+    ap.add_argument("--batch-backward", action="store_true",
+                    help="all forwards, then one backward (default: each view's backward right after its "
+                         "forward, overlapping the next view's forward on the other stream)")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -91,7 +103,7 @@ def main():
     from dge_amd import _native, _C
     from dge_amd.cameras import orbit_camera
     from dge_amd.gaussian_renderer import PipelineParams, render
-    from dge_amd.multiview import GradBucket
+    from dge_amd.multiview import GradBucket, render_backward_views, render_views
     from dge_amd.scene import synthetic_scene
 
     P, W, H, V = args.points, args.width, args.height, args.views_per_rank
@@ -106,9 +118,11 @@ def main():
 
     def step():
         bucket.zero()
-        for cam, g in zip(cams, seeds):
-            out = render(cam, scene, pipe, bg)["render"]
-            out.backward(g)
+        if args.batch_backward:
+            outs = render_views(cams, scene, pipe, bg, streams=args.streams)
+            torch.autograd.backward([o["render"] for o in outs], seeds)
+        else:
+            render_backward_views(cams, scene, pipe, bg, seeds, streams=args.streams)
         if world > 1:
             bucket.allreduce()
 
@@ -236,7 +250,7 @@ def main():
             "dtype": "fp32",
             "data": "synthetic",
             "config": {"workload": f"c2: {P / 1e6:.2f}M Gaussians (SH deg {args.sh_degree}), {W}x{H}, fp32 fwd+bwd",
-                       "gaussians": P, "width": W, "height": H, "views_per_rank": V,
+                       "gaussians": P, "width": W, "height": H, "views_per_rank": V, "streams": args.streams,
                        "parallelism": f"views sharded x{world}" + (", RCCL grad all-reduce" if world > 1 else "")},
             "num_rendered_mean": int(K),
             "live_gaussians_mean": int(np.mean([d["live"] for d in lives])),

@@ -262,9 +262,8 @@ int bin_forward(const gs_settings* s, const Grid& g, const gs_params& gp, int* r
     *geom_out = geom;
     *img_out = img;
 
-    uint32_t* counters = at<uint32_t>(geom, gl.counters);
-    GS_HIP(hipMemsetAsync(counters, 0, 16, stream));
-    GS_HIP(hipMemsetAsync(at<char>(img, il.ranges), 0, il.total - il.ranges, stream));  // ranges + tile_last
+    uint32_t* counters = at<uint32_t>(img, il.counters);
+    GS_HIP(hipMemsetAsync(counters, 0, il.total - il.counters, stream));  // counters, ranges, tile_last, ...
 
     PreprocessArgs pa;
     pa.P = P; pa.D = s->sh_degree; pa.M = gp.M; pa.W = g.W; pa.H = g.H; pa.gx = g.gx; pa.gy = g.gy;
@@ -284,6 +283,7 @@ int bin_forward(const gs_settings* s, const Grid& g, const gs_params& gp, int* r
     pa.rect = at<uint32_t>(geom, gl.rect);
     pa.rect_packed = rect_packable(g.gx, g.gy) ? 1 : 0;
     pa.counters = counters;
+    pa.touched = at<uint8_t>(geom, gl.touched);
     { StageScope sc(ST_PREPROCESS, stream); launch_preprocess(pa, stream); }
     GS_LAUNCHED("preprocess");
 
@@ -339,7 +339,8 @@ int bin_forward(const gs_settings* s, const Grid& g, const gs_params& gp, int* r
                    at<uint32_t>(bin, bl.sort_hist), at<uint32_t>(bin, bl.sort_totals), bl.sort_blocks, stream); }
     GS_LAUNCHED("tile sort");
     { StageScope sc(ST_RANGES, stream);
-    launch_ranges(at<uint32_t>(bin, tc ? bl.key1 : bl.key0), (int)K, at<uint2>(img, il.ranges), stream); }
+    launch_ranges(at<uint32_t>(bin, tc ? bl.key1 : bl.key0), (int)K, at<uint2>(img, il.ranges),
+                  at<uint32_t>(bin, bl.rec_flags), stream); }
     GS_LAUNCHED("ranges");
     return GS_OK;
 }
@@ -570,10 +571,11 @@ int gs_rasterize_backward_ex(const gs_settings* s, const gs_params* gp, int R, c
         uint8_t* rec_flags = R > 0 ? at<uint8_t>(const_cast<void*>(binning), bl.rec_flags) : nullptr;
         // per-Gaussian "has a record" bytes: k_gauss_bwd skips every Gaussian without one (all of
         // its gradients are zero), which is most of them (occluded behind saturated pixels)
+        // (both zeroed by the forward: `touched` in preprocess, the flags with the tile ranges.  A
+        // second backward of the same forward finds the bytes of the first, which it sets again: the
+        // entries that get records depend on the forward alone)
         uint8_t* touched = at<uint8_t>(const_cast<void*>(geom), gl.touched);
-        GS_HIP(hipMemsetAsync(touched, 0, (size_t)P, stream));
         if (R > 0) {
-            GS_HIP(hipMemsetAsync(rec_flags, 0, 4 * (size_t)R, stream));
             uint32_t* bwd_count = at<uint32_t>(const_cast<void*>(img), il.bwd_count);
             RenderBwdArgs rb;
             rb.W = g.W; rb.H = g.H; rb.gx = g.gx; rb.gy = g.gy;

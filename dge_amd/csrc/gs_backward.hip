@@ -443,21 +443,26 @@ __global__ __launch_bounds__(kGB) void k_gauss_live(GaussBwdArgs a) {
 }
 
 // ---------------------------------------------------------------------
-// Pass 2: the live Gaussians of kLiveGroup consecutive pass-1 blocks, one per
+// Pass 2: the live Gaussians of `group` consecutive pass-1 blocks (group =
+// ceil(blocks / 512), at most 8: about 512 workgroups whatever P is, so a small
+// or densely visible scene is not funnelled through a few workgroups), one per
 // thread, in batches of 256.  Their rows are scattered, so the SH rows move
 // through LDS with a flat block-wide index (consecutive lanes touch
 // consecutive floats of one or two rows) instead of one 180-B row per lane,
 // and every read-modify-write batch issues its loads before its stores.
 // ---------------------------------------------------------------------
-constexpr int kLiveGroup = 8;
+constexpr int kLiveGroup = 8;    // most pass-1 blocks per workgroup
+constexpr int kLiveGrid = 512;   // target workgroups (2 per CU at 190 VGPRs)
 
 __global__ __launch_bounds__(kGB) void k_gauss_bwd_live(GaussBwdArgs a) {
     __shared__ float s_sh[kGB * kShPitch];
     __shared__ uint32_t s_gid[kGB];
     __shared__ uint32_t s_pre[kLiveGroup + 1];
     const int nsrc = (a.P + kGB - 1) / kGB;
-    const int sb0 = blockIdx.x * kLiveGroup;
-    if (threadIdx.x < kLiveGroup) s_pre[threadIdx.x + 1] = sb0 + (int)threadIdx.x < nsrc ? a.live_count[sb0 + threadIdx.x] : 0u;
+    const int group = (nsrc + kLiveGrid - 1) / kLiveGrid < kLiveGroup ? (nsrc + kLiveGrid - 1) / kLiveGrid : kLiveGroup;
+    const int sb0 = blockIdx.x * group;
+    if (threadIdx.x < kLiveGroup)
+        s_pre[threadIdx.x + 1] = (int)threadIdx.x < group && sb0 + (int)threadIdx.x < nsrc ? a.live_count[sb0 + threadIdx.x] : 0u;
     __syncthreads();
     if (threadIdx.x == 0) {
         s_pre[0] = 0;
@@ -582,7 +587,8 @@ void launch_gauss_backward(const GaussBwdArgs& a, hipStream_t s) {
     if (a.P <= 0) return;
     const int blocks = div_up(a.P, kGB);
     hipLaunchKernelGGL(k_gauss_live, dim3(blocks), dim3(kGB), 0, s, a);
-    hipLaunchKernelGGL(k_gauss_bwd_live, dim3(div_up(blocks, kLiveGroup)), dim3(kGB), 0, s, a);
+    const int group = std::min(div_up(blocks, kLiveGrid), kLiveGroup);  // (the kernel derives the same)
+    hipLaunchKernelGGL(k_gauss_bwd_live, dim3(div_up(blocks, group)), dim3(kGB), 0, s, a);
 }
 
 }  // namespace gs

@@ -76,7 +76,7 @@ struct alignas(64) Splat {
 struct GeomLayout {
     size_t splat, tiles_touched, clamped, touched, live_count, live_list, radii, first_slot;
     // live_count: one u32 per 256-Gaussian block (k_gauss_live); live_list: block-local compacted ids
-    size_t key0, key1, val0, val1, rect, sort_hist, sort_totals, scan_sums, counters, total;
+    size_t key0, key1, val0, val1, rect, sort_hist, sort_totals, scan_sums, total;
     int sort_blocks, scan_blocks;
 };
 inline GeomLayout geom_layout(int P) {
@@ -101,7 +101,6 @@ inline GeomLayout geom_layout(int P) {
     L.sort_hist = o; o = align_up(o + 4 * 256 * (size_t)L.sort_blocks);
     L.sort_totals = o; o = align_up(o + 4 * 256);
     L.scan_sums = o; o = align_up(o + 4 * (size_t)(L.scan_blocks + 1));
-    L.counters = o; o = align_up(o + 16);
     L.total = o;
     return L;
 }
@@ -127,7 +126,7 @@ __host__ __device__ inline uint32_t used_base(uint32_t range_x, int tile) { retu
 __host__ __device__ inline size_t used_words(size_t K, int tiles) { return 4 * (K / 64 + (size_t)tiles + 2); }
 
 struct ImgLayout {
-    size_t final_T, n_contrib, ranges, tile_last, quad_last, bwd_count, total;
+    size_t final_T, n_contrib, counters, ranges, tile_last, quad_last, bwd_count, total;
 };
 inline ImgLayout img_layout(int W, int H) {
     ImgLayout L;
@@ -136,7 +135,8 @@ inline ImgLayout img_layout(int W, int H) {
     size_t tiles = (size_t)div_up(W, 16) * div_up(H, 16);
     L.final_T = o; o = align_up(o + 4 * n);
     L.n_contrib = o; o = align_up(o + 4 * n);
-    L.ranges = o; o = align_up(o + 8 * tiles);  // ranges.. are zeroed per forward
+    L.counters = o; o = align_up(o + 16);        // counters.. are zeroed per forward (one memset)
+    L.ranges = o; o = align_up(o + 8 * tiles);
     L.tile_last = o; o = align_up(o + 4 * tiles);
     L.quad_last = o; o = align_up(o + 16 * tiles);
     L.bwd_count = o; o = align_up(o + 16);  // [0] multi-segment items, [1] single
@@ -211,6 +211,7 @@ struct PreprocessArgs {
     uint32_t* rect;          // pack_rect(tile rect) when the grid allows it, else tiles_touched
     int rect_packed;
     uint32_t* counters;  // [0] instance total, [1] error flag
+    uint8_t* touched;    // zeroed here: k_render_bwd sets the bytes of Gaussians that get a record
 };
 void launch_preprocess(const PreprocessArgs& a, hipStream_t s);
 void launch_mark_visible(int P, const float* means3D, const float* view, uint8_t* present, hipStream_t s);
@@ -255,7 +256,8 @@ struct EmitArgs {
 void launch_scan_reduce(const EmitArgs& a, hipStream_t s);
 void launch_scan_emit(const EmitArgs& a, hipStream_t s);
 
-void launch_ranges(const uint32_t* sorted_tile, int K, uint2* ranges, hipStream_t s);
+// tile ranges; also zeroes the backward's per-slot record flags (u32 per slot)
+void launch_ranges(const uint32_t* sorted_tile, int K, uint2* ranges, uint32_t* rec_flags32, hipStream_t s);
 
 struct RenderArgs {
     int W, H, gx, gy;

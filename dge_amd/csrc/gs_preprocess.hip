@@ -160,6 +160,7 @@ __global__ __launch_bounds__(256) void k_preprocess(PreprocessArgs a) {
         a.clamped[idx] = clamp_bits;
         a.depth_key[idx] = key;
         a.rect[idx] = rect;
+        if (a.touched) a.touched[idx] = 0;
     }
     // workgroup total of instances -> one atomic
     __shared__ uint32_t part[4];

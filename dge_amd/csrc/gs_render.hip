@@ -53,6 +53,13 @@ __device__ __forceinline__ bool pixel_alpha(float2 xy, float4 co, float pfx, flo
     return !(power > 0.0f) && !(alpha < 1.0f / 255.0f);
 }
 
+// (diagnostics) where this wave runs: HW_ID (wave slot, SIMD, CU, SH, SE) | XCC_ID << 32
+__device__ __forceinline__ uint64_t wave_location() {
+    const uint32_t hw = __builtin_amdgcn_s_getreg(4 | (31 << 11));   // HW_REG_HW_ID, bits [31:0]
+    const uint32_t xcc = __builtin_amdgcn_s_getreg(20 | (15 << 11)); // HW_REG_XCC_ID, bits [15:0]
+    return (uint64_t)xcc << 32 | hw;
+}
+
 constexpr int kRound = kBlendRound;  // list entries per round: 4 per lane
 constexpr int kGroup = 4;    // blend entries per unrolled step (LDS is padded to a multiple)
 
@@ -84,18 +91,24 @@ __device__ __forceinline__ bool blend_step(float2 xy, float4 co, float4 fe, uint
     const bool stop = hit && test_T < 0.0001f;
     const bool use = hit && !stop;
     done = done || stop;
-    const float w = alpha * T;
-    C0 = use ? C0 + fe.x * w : C0;
-    C1 = use ? C1 + fe.y * w : C1;
-    C2 = use ? C2 + fe.z * w : C2;
-    D = use ? D + fe.w * w : D;
+    // one select on the weight instead of four on the sums: C + f * 0 == C (f finite)
+    const float w = use ? alpha * T : 0.0f;
+    C0 = C0 + fe.x * w;
+    C1 = C1 + fe.y * w;
+    C2 = C2 + fe.z * w;
+    D = D + fe.w * w;
     T = use ? test_T : T;
     last = use ? pos : last;
     return use;
 }
 
 __global__ __launch_bounds__(64) void k_render_fwd(RenderArgs a) {
-    const int quad = blockIdx.x & 3, tile = blockIdx.x >> 2;
+    // XCD-aware: blocks b, b+8, b+16, b+24 (one XCD under the round-robin dealing) take the four
+    // quadrants of one tile, so the tile's list and its Splat gathers are fetched into one L2
+    const int x8 = blockIdx.x & 7, j8 = blockIdx.x >> 3;
+    const int quad = j8 & 3, tile = (j8 >> 2) * 8 + x8;
+    if (tile >= a.gx * a.gy) return;
+    const int qidx = 4 * tile + quad;
     const int tx = tile % a.gx, ty = tile / a.gx;
     const int lane = threadIdx.x;
     const int bx0 = tx * kTile + (quad & 1) * kQuad, by0 = ty * kTile + (quad >> 1) * kQuad;
@@ -124,11 +137,15 @@ __global__ __launch_bounds__(64) void k_render_fwd(RenderArgs a) {
     // round's loads are in flight while the previous round blends.
     // Out-of-range slots load entry 0 (valid whenever the list is non-empty)
     // and are dropped by the cull.
+    // (unconditional loads, clamped into the list: the compiler can then count them in vmcnt
+    // waits instead of draining every outstanding access; a non-empty list's last entry, or
+    // entry 0 of the binning buffer, which always exists)
+    const uint32_t k_last = range.y > range.x ? range.y - 1 : 0u;
     auto load_ids = [&](uint32_t b, uint32_t (&ids)[4]) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const uint32_t k = b + 64 * i + lane;
-            ids[i] = k < range.y ? a.point_pairs[k].x : 0u;
+            ids[i] = a.point_pairs[k < range.y ? k : k_last].x;
         }
     };
     uint32_t ids[4];
@@ -140,12 +157,19 @@ __global__ __launch_bounds__(64) void k_render_fwd(RenderArgs a) {
 
     // checkpoint k of this quadrant: slot ckpt_base + k, quadrant `quad`
     float4* ckpt = a.ckpt + ((size_t)ckpt_base(range.x, tile) * 4 + quad) * 64;
+    uint64_t c_cull = 0;
+    // The round's global stores (checkpoint, the previous round's blended bits) are issued after
+    // the next round's gathers: stores count in vmcnt, and one issued just before the cull would
+    // make the cull's wait for the gathers wait for the store too.
+    uint64_t pend_word = 0;    // lane i < 4: word i of the previous round's blended bits
+    int pend_rel = -1;         // that round's first list position (-1: none)
+    auto store_words = [&]() {
+        if (pend_rel >= 0 && lane < kRound / 64 && pend_rel + 64 * lane < (int)(range.y - range.x))
+            used[(size_t)(pend_rel / 64 + lane) * 4] = pend_word;  // (the list's own words only)
+    };
     for (uint32_t b = range.x; b < range.y; b += kRound) {
         if (!__any(!done)) break;
-        {  // (T, C) at the segment boundaries of the backward replay (every round start)
-            const uint32_t k = (b - range.x) / kSegLen;
-            if (k > 0) ckpt[(size_t)k * 256 + lane] = make_float4(T, C0, C1, C2);
-        }
+        const uint64_t r0 = a.diag ? __builtin_amdgcn_s_memtime() : 0;
         // cull against the quadrant, compact survivors in list order (i-major, lane-minor)
         int nk = 0;
         int kslot[4];  // compacted slot of this lane's entry i (-1: culled)
@@ -173,10 +197,16 @@ __global__ __launch_bounds__(64) void k_render_fwd(RenderArgs a) {
         }
         diag_kept += nk;
         diag_rounds += 1;
+        if (a.diag) c_cull += __builtin_amdgcn_s_memtime() - r0;
         // next round's gathers and the round after's ids, in flight during the blend
 #pragma unroll
         for (int i = 0; i < 4; ++i) cur[i] = gather_entry(a.splat, ids[i]);
         load_ids(b + 2 * kRound, ids);
+        {  // (T, C) at the segment boundaries of the backward replay (every round start)
+            const uint32_t k = (b - range.x) / kSegLen;
+            if (k > 0) ckpt[(size_t)k * 256 + lane] = make_float4(T, C0, C1, C2);
+        }
+        store_words();
         if (lane <= kRound / kGroup) s_gused[lane] = 0u;  // (groups past an early exit stay 0)
         __syncthreads();
 
@@ -196,17 +226,15 @@ __global__ __launch_bounds__(64) void k_render_fwd(RenderArgs a) {
         __syncthreads();
         // the round's blended bits in list order, one ballot per word (words of rounds the wave
         // never reaches stay unwritten: past every pixel's last contributor, outside every replay)
-        uint64_t words[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int sl = kslot[i];
-            words[i] = __ballot(sl >= 0 && ((s_gused[sl / kGroup] >> (sl % kGroup)) & 1u));
+            const uint64_t wd = __ballot(sl >= 0 && ((s_gused[sl / kGroup] >> (sl % kGroup)) & 1u));
+            pend_word = lane == i ? wd : pend_word;
         }
-        const uint32_t rel = b - range.x;
-#pragma unroll
-        for (int i = 0; i < 4; ++i)  // (the list's own words only: the next tile's start here)
-            if (lane == i && rel + 64 * i < range.y - range.x) used[(size_t)(rel / 64 + i) * 4] = words[i];
+        pend_rel = (int)(b - range.x);
     }
+    store_words();
 
     // slot 0: the final state (an empty tile's range is (0, 0): it owns no slot and has no replay)
     if (range.y > range.x) ckpt[lane] = make_float4(T, C0, C1, C2);
@@ -234,16 +262,18 @@ __global__ __launch_bounds__(64) void k_render_fwd(RenderArgs a) {
         }
     }
     if (lane == 0) {
-        a.quad_last[blockIdx.x] = m;
+        a.quad_last[qidx] = m;
         if (m) atomicMax(&a.tile_last[tile], m);
         if (a.diag) {
-            uint64_t* d = a.diag + kDiagWords * (size_t)blockIdx.x;
+            uint64_t* d = a.diag + kDiagWords * (size_t)qidx;
             d[0] = t_start;
             d[1] = __builtin_amdgcn_s_memrealtime();
             d[2] = diag_kept;
             d[3] = diag_rounds;
             d[4] = c_blend;
             d[5] = __builtin_amdgcn_s_memtime() - c_start;
+            d[6] = c_cull;
+            d[7] = wave_location();
         }
     }
 }
@@ -251,7 +281,7 @@ __global__ __launch_bounds__(64) void k_render_fwd(RenderArgs a) {
 void launch_render_forward(const RenderArgs& a, hipStream_t s) {
     const int tiles = a.gx * a.gy;
     if (tiles <= 0) return;
-    hipLaunchKernelGGL(k_render_fwd, dim3(tiles * 4), dim3(64), 0, s, a);
+    hipLaunchKernelGGL(k_render_fwd, dim3(div_up(tiles, 8) * 32), dim3(64), 0, s, a);
 }
 
 // =====================================================================
@@ -571,6 +601,7 @@ __global__ __launch_bounds__(64, 4) void k_render_bwd(RenderBwdArgs a) {
         d[4] = c_replay;
         d[5] = __builtin_amdgcn_s_memtime() - c_start;
         d[6] = (uint64_t)seg << 32 | (uint32_t)qidx;
+        d[7] = wave_location();
     }
     }
 }

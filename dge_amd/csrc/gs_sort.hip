@@ -412,9 +412,11 @@ void launch_scan_emit(const EmitArgs& a, hipStream_t s) {
 // ---------------------------------------------------------------------
 // identifyTileRanges (rasterizer_impl.cu:105-125) + instance maps
 // ---------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_ranges(const uint32_t* __restrict__ tile, int K, uint2* __restrict__ ranges) {
+__global__ __launch_bounds__(256) void k_ranges(const uint32_t* __restrict__ tile, int K, uint2* __restrict__ ranges,
+                                                uint32_t* __restrict__ rec_flags32) {
     const int pos = blockIdx.x * 256 + threadIdx.x;
     if (pos >= K) return;
+    if (rec_flags32) rec_flags32[pos] = 0u;  // (slot `pos`: the four quadrant flags; no memset launch)
     const uint32_t t = tile[pos];
     if (pos == 0) {
         ranges[t].x = 0;
@@ -428,9 +430,9 @@ __global__ __launch_bounds__(256) void k_ranges(const uint32_t* __restrict__ til
     if (pos == K - 1) ranges[t].y = (uint32_t)K;
 }
 
-void launch_ranges(const uint32_t* sorted_tile, int K, uint2* ranges, hipStream_t s) {
+void launch_ranges(const uint32_t* sorted_tile, int K, uint2* ranges, uint32_t* rec_flags32, hipStream_t s) {
     if (K <= 0) return;
-    hipLaunchKernelGGL(k_ranges, dim3(div_up(K, 256)), dim3(256), 0, s, sorted_tile, K, ranges);
+    hipLaunchKernelGGL(k_ranges, dim3(div_up(K, 256)), dim3(256), 0, s, sorted_tile, K, ranges, rec_flags32);
 }
 
 }  // namespace gs

@@ -154,9 +154,13 @@ class _RasterizeGaussiansFused(torch.autograd.Function):
         args = (rs.bg, xyz, f_dc, f_rest, colors, raw_opacity, raw_scaling, raw_rotation, radii, rs.scale_modifier,
                 rs.viewmatrix, rs.projmatrix, rs.tanfovx, rs.tanfovy, grad_out_color, rs.sh_degree, rs.campos,
                 geomBuffer, ctx.num_rendered, binningBuffer, imgBuffer, rs.debug)
+        ordered = bool(into) and _SIDE_STREAMS
+        stream = _order_grad_writes_begin(xyz.device) if ordered else None
         d_m2, d_xyz, d_dc, d_rest, d_col, d_op, d_sc, d_rot = _call_with_snapshot(
             lambda *a: _C.rasterize_gaussians_fused_backward(*a, into=into), args, rs.debug, "snapshot_bw.dump",
             "backward")
+        if ordered:
+            _order_grad_writes_end(xyz.device, stream, [t for _, t in direct])
         for p, t in direct:  # parameters whose .grad was None: the kernel wrote it, hand it over
             p.grad = t
         if ctx.has_sh:
@@ -177,6 +181,33 @@ class _RasterizeGaussiansFused(torch.autograd.Function):
 
 
 _FUSED_GRAD_ACCUM = os.environ.get("DGE_AMD_FUSED_GRAD_ACCUM", "1") != "0"
+
+# In-kernel .grad writes of backward calls that autograd runs on different streams (views rendered
+# concurrently, dge_amd.multiview.render_views: each view's backward runs on its forward's stream)
+# are chained with events, and the default stream waits for them, so an optimizer step or an
+# all-reduce issued there sees the gradients.  Backward calls on the default stream need nothing.
+_GRAD_WRITES = {}  # device index -> (stream, event) of the last side-stream .grad write
+_SIDE_STREAMS = False  # set once dge_amd.multiview.stream_pool hands out streams
+
+
+def _order_grad_writes_begin(dev):
+    cur = torch.cuda.current_stream(dev)
+    last = _GRAD_WRITES.get(dev.index)
+    if last is not None and last[0] != cur:
+        cur.wait_event(last[1])
+    return cur
+
+
+def _order_grad_writes_end(dev, cur, fresh):
+    dflt = torch.cuda.default_stream(dev)
+    if cur == dflt:
+        _GRAD_WRITES.pop(dev.index, None)
+        return
+    ev = cur.record_event()
+    dflt.wait_event(ev)
+    for t in fresh:  # new .grad tensors allocated on the side stream, used on the default one
+        t.record_stream(dflt)
+    _GRAD_WRITES[dev.index] = (cur, ev)
 
 
 def set_fused_grad_accumulation(enabled: bool) -> bool:

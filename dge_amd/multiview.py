@@ -71,6 +71,85 @@ class GradBucket:
         return dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=group, async_op=async_op)
 
 
+_STREAM_POOLS = {}
+
+
+def stream_pool(device, n: int):
+    """n HIP streams of `device`, created once and reused."""
+    dev = torch.device(device)
+    key = (dev.index, n)
+    pool = _STREAM_POOLS.get(key)
+    if pool is None:
+        from . import diff_gaussian_rasterization as _r
+
+        _r._SIDE_STREAMS = True  # backward calls may now run off the default stream: order .grad writes
+        pool = _STREAM_POOLS[key] = [torch.cuda.Stream(device=dev) for _ in range(n)]
+    return pool
+
+
+def render_views(cameras, pc, pipe, bg_color, streams: int = 2, **kw):
+    """render() of every camera, the views spread round-robin over `streams` HIP streams.
+
+    The reference renders a batch's views one after another (threestudio/systems/DGE.py:179-239) on
+    one stream; here consecutive views run on different streams, so one view's latency-bound phases
+    (binning launches, the blend tail) overlap the next view's HBM-bound preprocessing.  Outputs are
+    the same dicts render() returns, usable on the caller's stream (it waits for every view); autograd
+    runs each view's backward on that view's stream and the in-kernel gradient accumulation orders
+    itself across them (diff_gaussian_rasterization._order_grad_writes_*)."""
+    from .gaussian_renderer import render
+
+    if streams <= 1 or len(cameras) <= 1:
+        return [render(c, pc, pipe, bg_color, **kw) for c in cameras]
+    dev = bg_color.device
+    main = torch.cuda.current_stream(dev)
+    pool = stream_pool(dev, streams)
+    ready = main.record_event()
+    outs = []
+    for i, cam in enumerate(cameras):
+        s = pool[i % len(pool)]
+        s.wait_event(ready)
+        with torch.cuda.stream(s):
+            out = render(cam, pc, pipe, bg_color, **kw)
+        for v in out.values():
+            if isinstance(v, torch.Tensor) and v.is_cuda:
+                v.record_stream(main)
+        outs.append(out)
+    for s in pool[:min(len(pool), len(cameras))]:
+        main.wait_stream(s)
+    return outs
+
+
+def render_backward_views(cameras, pc, pipe, bg_color, grads, streams: int = 2, **kw):
+    """Forward + backward of every view (d(image)/d(params) contracted with `grads[i]`, accumulated into
+    the parameters' .grad), view i on stream i % `streams`: view i's backward overlaps view i+1's
+    forward.  The gradients equal the reference's batch step (all views rendered, one backward of the
+    summed loss) up to float summation order.  Returns the render() dicts with the images detached."""
+    from .gaussian_renderer import render
+
+    dev = bg_color.device
+    main = torch.cuda.current_stream(dev)
+    pool = stream_pool(dev, streams) if streams > 1 else [main]
+    ready = main.record_event()
+    outs = []
+    for i, (cam, g) in enumerate(zip(cameras, grads)):
+        s = pool[i % len(pool)]
+        if s != main:
+            s.wait_event(ready)
+        with torch.cuda.stream(s):
+            out = render(cam, pc, pipe, bg_color, **kw)
+            out["render"].backward(g)
+        out = {k: (v.detach() if isinstance(v, torch.Tensor) else v) for k, v in out.items()}
+        if s != main:
+            for v in out.values():
+                if isinstance(v, torch.Tensor) and v.is_cuda:
+                    v.record_stream(main)
+        outs.append(out)
+    for s in pool[:min(len(pool), len(cameras))]:
+        if s != main:
+            main.wait_stream(s)
+    return outs
+
+
 def reduce_view_stats(viewspace_grad_sum: torch.Tensor, radii_max: torch.Tensor, group=None):
     """SUM of the view-space gradient accumulator, MAX of radii across ranks (in place)."""
     if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:

@@ -136,3 +136,45 @@ def test_edit_step_render_adam_densify(cuda_device):
     assert m.num_points() != n0
     pkg = render(orbit_camera(0, 2, 128, 128, device=cuda_device), m, PipelineParams(), bg)
     assert torch.isfinite(pkg["render"]).all()
+
+
+@pytest.mark.parametrize("grads_exist", [False, True])
+def test_render_views_on_streams_matches_sequential(cuda_device, grads_exist):
+    """render_views over a 2-stream pool + ONE backward (each view's backward on its stream, the fused
+    .grad writes ordered across them) gives the gradients of the sequential per-view loop, and the
+    default stream sees them (read there right after backward returns)."""
+    from dge_amd.cameras import orbit_camera
+    from dge_amd.gaussian_renderer import PipelineParams, render
+    from dge_amd.multiview import render_backward_views, render_views
+    from dge_amd.scene import synthetic_scene
+
+    cams = [orbit_camera(k, 4, 160, 128, device=cuda_device) for k in range(4)]
+    G = [torch.randn(3, 128, 160, generator=torch.Generator().manual_seed(30 + k)).to(cuda_device) * 1e-2
+         for k in range(4)]
+    bg = torch.zeros(3, device=cuda_device)
+    res = {}
+    for mode in ("sequential", "streams", "interleaved"):
+        sc = synthetic_scene(20_000, seed=4, device=cuda_device).requires_grad_(True)
+        if grads_exist:
+            for p in sc.parameters():
+                p.grad = torch.full_like(p, 0.25)
+        if mode == "sequential":
+            imgs = []
+            for c, g in zip(cams, G):
+                out = render(c, sc, PipelineParams(), bg)
+                out["render"].backward(g)
+                imgs.append(out["render"].detach())
+        elif mode == "streams":
+            outs = render_views(cams, sc, PipelineParams(), bg, streams=2)
+            torch.autograd.backward([o["render"] for o in outs], G)
+            imgs = [o["render"].detach() for o in outs]
+        else:
+            outs = render_backward_views(cams, sc, PipelineParams(), bg, G, streams=2)
+            imgs = [o["render"] for o in outs]
+        res[mode] = ([p.grad.clone() for p in sc.parameters()], [i.clone() for i in imgs])
+    torch.cuda.synchronize()
+    for mode in ("streams", "interleaved"):
+        for a, b in zip(res["sequential"][1], res[mode][1]):
+            torch.testing.assert_close(a, b, rtol=0, atol=0)
+        for a, b in zip(res["sequential"][0], res[mode][0]):
+            torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-7)

@@ -42,10 +42,25 @@ def summarize(name, d, nquads=None):
           f"loop cycles per kept entry (all) {cyc_loop.sum() / max(1, kept.sum()):.0f}")
     order = np.argsort(-dur)[:6]
     for i in order:
-        extra = f" seg {int(d[i, 6]) >> 32} quad {int(d[i, 6]) & 0xFFFFFFFF}" if nquads else ""
+        extra = f" seg {int(d[i, 6]) >> 32} quad {int(d[i, 6]) & 0xFFFFFFFF}" if nquads else \
+            f" cull+wait share {d[i, 6] / max(1, cyc_total[i]):.2f}"
         print(f"   slowest: wave {ids[i]} dur {dur[i]:.1f} us kept {kept[i]} rounds {rounds[i]} loop cyc/kept "
               f"{cyc_loop[i] / max(1, kept[i]):.0f} loop share {cyc_loop[i] / max(1, cyc_total[i]):.2f} "
               f"start {(start[i] - t0) * 10e-3:.1f}{extra}")
+    # SIMD sharing: waves of one SIMD (word 7: HW_ID | XCC_ID << 32) compete for its issue slots
+    loc = d[:, 7]
+    simd = (loc >> 32) * 4096 + ((loc >> 8) & 0xF) * 256 + ((loc >> 12) & 0x1) * 128 + ((loc >> 13) & 0x7) * 16 \
+        + ((loc >> 4) & 0x3)
+    if loc.any():
+        u, inv = np.unique(simd, return_inverse=True)
+        busy = np.bincount(inv, weights=dur)
+        print(f"   SIMDs used {len(u)}; summed wave-us per SIMD p50 {np.percentile(busy, 50):.0f} "
+              f"p99 {np.percentile(busy, 99):.0f} max {busy.max():.0f}")
+        for i in order[:3]:
+            mates = np.nonzero((inv == inv[i]) & (np.arange(len(d)) != i))[0]
+            ov = [min(end[i], end[j]) - max(start[i], start[j]) for j in mates]
+            print(f"   slowest wave {ids[i]}: {len(mates)} SIMD mates, overlap-us {[round(o * 10e-3, 1) for o in ov]}, "
+                  f"their durations {[round(float(dur[j]), 1) for j in mates]}")
     ts = np.linspace(0, span, 11)
     alive = [int(((start - t0) * 10e-3 <= t).sum() - ((end - t0) * 10e-3 <= t).sum()) for t in ts]
     print("   waves running over time:", " ".join(f"{t:.0f}:{a}" for t, a in zip(ts, alive)))
