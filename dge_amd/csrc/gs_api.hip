@@ -489,6 +489,7 @@ int gs_rasterize_forward_ex(const gs_settings* s, const gs_params* gp, float* ou
         RenderArgs ra;
         ra.W = g.W; ra.H = g.H; ra.gx = g.gx; ra.gy = g.gy;
         ra.ranges = at<uint2>(img, il.ranges);
+        ra.tile_order = at<uint32_t>(img, il.tile_order);
         ra.point_pairs = at<uint2>(bin, bl.point_pairs);
         ra.bwd_items = at<uint2>(bin, bl.bwd_items);
         ra.bwd_count = at<uint32_t>(img, il.bwd_count);

@@ -24,54 +24,35 @@
 
 namespace gs {
 
-// backward.cu:20-139 — dL_dsh of the (deg+1)^2 used coefficients into
-// dsh[3*k..3*k+2] (registers; unused ones untouched) and the mean gradient
-// through the normalised view direction as the return value.
+// backward.cu:20-139 — the mean gradient through the normalised view direction
+// (return value) and dL_dsh of the (deg+1)^2 used coefficients, times `msk`
+// (the grad mask, 1 when none): coefficient 0 into ddc, coefficients 1..
+// written over the input row r in place (after every read of it; ncol floats,
+// zeros beyond the degree) — no 48-float register array.
 // r: SH coefficients 1.. of this Gaussian (coefficient 0 has no direction term).
-__device__ __forceinline__ f3 sh_backward(int deg, f3 pos, f3 campos, const float* __restrict__ r,
-                                          uint8_t clamp_bits, f3 dL_dcolor, float (&dsh)[48]) {
+__device__ __forceinline__ f3 sh_backward(int deg, f3 pos, f3 campos, float* r, int ncol, uint8_t clamp_bits,
+                                          f3 dL_dcolor, float msk, float (&ddc)[3]) {
     const f3 dir_orig = pos - campos;
     const float len = sqrtf(dot3(dir_orig, dir_orig));
     const f3 dir = mk3(dir_orig.x / len, dir_orig.y / len, dir_orig.z / len);
     const f3 g = mk3(dL_dcolor.x * ((clamp_bits & 1) ? 0.f : 1.f), dL_dcolor.y * ((clamp_bits & 2) ? 0.f : 1.f),
                      dL_dcolor.z * ((clamp_bits & 4) ? 0.f : 1.f));
-    auto put = [&](int k, f3 v) {
-        dsh[3 * k] = v.x;
-        dsh[3 * k + 1] = v.y;
-        dsh[3 * k + 2] = v.z;
-    };
     // coefficient k >= 1 of the input
 #define SHK(k) ld3(r + 3 * ((k) - 1))
     f3 dx = mk3(0, 0, 0), dy = mk3(0, 0, 0), dz = mk3(0, 0, 0);
     const float x = dir.x, y = dir.y, z = dir.z;
-    put(0, g * kSH_C0);
     if (deg > 0) {
-        put(1, g * (-kSH_C1 * y));
-        put(2, g * (kSH_C1 * z));
-        put(3, g * (-kSH_C1 * x));
         dx = SHK(3) * (-kSH_C1);
         dy = SHK(1) * (-kSH_C1);
         dz = SHK(2) * kSH_C1;
         if (deg > 1) {
             const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
-            put(4, g * (kSH_C2_0 * xy));
-            put(5, g * (kSH_C2_1 * yz));
-            put(6, g * (kSH_C2_2 * (2.f * zz - xx - yy)));
-            put(7, g * (kSH_C2_3 * xz));
-            put(8, g * (kSH_C2_4 * (xx - yy)));
             dx = dx + (SHK(4) * (kSH_C2_0 * y) + SHK(6) * (kSH_C2_2 * 2.f * -x) + SHK(7) * (kSH_C2_3 * z) +
                        SHK(8) * (kSH_C2_4 * 2.f * x));
             dy = dy + (SHK(4) * (kSH_C2_0 * x) + SHK(5) * (kSH_C2_1 * z) + SHK(6) * (kSH_C2_2 * 2.f * -y) +
                        SHK(8) * (kSH_C2_4 * 2.f * -y));
             dz = dz + (SHK(5) * (kSH_C2_1 * y) + SHK(6) * (kSH_C2_2 * 2.f * 2.f * z) + SHK(7) * (kSH_C2_3 * x));
             if (deg > 2) {
-                put(9, g * (kSH_C3_0 * y * (3.f * xx - yy)));
-                put(10, g * (kSH_C3_1 * xy * z));
-                put(11, g * (kSH_C3_2 * y * (4.f * zz - xx - yy)));
-                put(12, g * (kSH_C3_3 * z * (2.f * zz - 3.f * xx - 3.f * yy)));
-                put(13, g * (kSH_C3_4 * x * (4.f * zz - xx - yy)));
-                put(14, g * (kSH_C3_5 * z * (xx - yy)));
-                put(15, g * (kSH_C3_6 * x * (xx - 3.f * yy)));
                 dx = dx + (SHK(9) * (kSH_C3_0 * 3.f * 2.f * xy) + SHK(10) * (kSH_C3_1 * yz) +
                            SHK(11) * (kSH_C3_2 * -2.f * xy) + SHK(12) * (kSH_C3_3 * -3.f * 2.f * xz) +
                            SHK(13) * (kSH_C3_4 * (-3.f * xx + 4.f * zz - yy)) + SHK(14) * (kSH_C3_5 * 2.f * xz) +
@@ -87,6 +68,40 @@ __device__ __forceinline__ f3 sh_backward(int deg, f3 pos, f3 campos, const floa
         }
     }
 #undef SHK
+    // every read of r is done: the coefficient gradients overwrite it
+    auto put = [&](int k, f3 v) {
+        v = v * msk;
+        if (k == 0) {
+            ddc[0] = v.x;
+            ddc[1] = v.y;
+            ddc[2] = v.z;
+            return;
+        }
+        const int c = 3 * (k - 1);
+        if (c < ncol) r[c] = v.x;
+        if (c + 1 < ncol) r[c + 1] = v.y;
+        if (c + 2 < ncol) r[c + 2] = v.z;
+    };
+    const f3 zero = mk3(0.f, 0.f, 0.f);
+    put(0, g * kSH_C0);
+    put(1, deg > 0 ? g * (-kSH_C1 * y) : zero);
+    put(2, deg > 0 ? g * (kSH_C1 * z) : zero);
+    put(3, deg > 0 ? g * (-kSH_C1 * x) : zero);
+    {
+        const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
+        put(4, deg > 1 ? g * (kSH_C2_0 * xy) : zero);
+        put(5, deg > 1 ? g * (kSH_C2_1 * yz) : zero);
+        put(6, deg > 1 ? g * (kSH_C2_2 * (2.f * zz - xx - yy)) : zero);
+        put(7, deg > 1 ? g * (kSH_C2_3 * xz) : zero);
+        put(8, deg > 1 ? g * (kSH_C2_4 * (xx - yy)) : zero);
+        put(9, deg > 2 ? g * (kSH_C3_0 * y * (3.f * xx - yy)) : zero);
+        put(10, deg > 2 ? g * (kSH_C3_1 * xy * z) : zero);
+        put(11, deg > 2 ? g * (kSH_C3_2 * y * (4.f * zz - xx - yy)) : zero);
+        put(12, deg > 2 ? g * (kSH_C3_3 * z * (2.f * zz - 3.f * xx - 3.f * yy)) : zero);
+        put(13, deg > 2 ? g * (kSH_C3_4 * x * (4.f * zz - xx - yy)) : zero);
+        put(14, deg > 2 ? g * (kSH_C3_5 * z * (xx - yy)) : zero);
+        put(15, deg > 2 ? g * (kSH_C3_6 * x * (xx - 3.f * yy)) : zero);
+    }
     const f3 dL_ddir = mk3(dot3(dx, g), dot3(dy, g), dot3(dz, g));
     // dnormvdv (auxiliary.h:107-117)
     const f3 v = dir_orig;
@@ -180,7 +195,8 @@ struct GaussOut {
 // The per-Gaussian chain of a live Gaussian (geometry gradients into `o`,
 // SH gradients into dsh, opacity gradient chained into dop).
 __device__ __forceinline__ void gauss_bwd_visible(const GaussBwdArgs& a, const GaussIn& gin, const float (&acc)[9],
-                                                  float& dop, const float* my_sh, float (&dsh)[48], GaussOut& o) {
+                                                  float& dop, float* my_sh, int ncol, float sh_msk, float (&ddc)[3],
+                                                  GaussOut& o) {
     const float* v = a.view;
     const float* pm = a.proj;
     const f3 m = gin.m;
@@ -264,7 +280,8 @@ __device__ __forceinline__ void gauss_bwd_visible(const GaussBwdArgs& a, const G
     }
     // ---- SH -> RGB backward ----
     if (a.sh.dc)
-        dmean = dmean + sh_backward(a.D, m, ld3(a.campos), my_sh, gin.clamped, mk3(acc[6], acc[7], acc[8]), dsh);
+        dmean = dmean + sh_backward(a.D, m, ld3(a.campos), my_sh, ncol, gin.clamped, mk3(acc[6], acc[7], acc[8]),
+                                    sh_msk, ddc);
     o.dmean = dmean;
 #pragma unroll
     for (int k = 0; k < 6; ++k) o.dcov[k] = dcov[k];
@@ -296,8 +313,9 @@ __device__ __forceinline__ void gauss_bwd_visible(const GaussBwdArgs& a, const G
 // The grad-mask hooks of the reference's GaussianModel (gaussian_model.py:837-856:
 // grad * mask[:, None] on _xyz, _features_dc, _features_rest, _opacity,
 // _scaling — not _rotation), applied to the outputs named in mask_bits.
+// (the SH part is applied inside sh_backward)
 __device__ __forceinline__ void apply_grad_mask(const GaussBwdArgs& a, float m, float (&acc)[9], float& dop,
-                                                float (&dsh)[48], GaussOut& o) {
+                                                GaussOut& o) {
     const uint32_t b = a.mask_bits;
     if (b & GS_ACC_MEANS2D) { acc[0] *= m; acc[1] *= m; }
     if (b & GS_ACC_COLORS) { acc[6] *= m; acc[7] *= m; acc[8] *= m; }
@@ -306,9 +324,6 @@ __device__ __forceinline__ void apply_grad_mask(const GaussBwdArgs& a, float m, 
     if (b & GS_ACC_COV3D)
 #pragma unroll
         for (int k = 0; k < 6; ++k) o.dcov[k] *= m;
-    if (b & GS_ACC_SH)
-#pragma unroll
-        for (int k = 0; k < 48; ++k) dsh[k] *= m;
     if (b & GS_ACC_SCALES)
 #pragma unroll
         for (int k = 0; k < 3; ++k) o.dscale[k] *= m;
@@ -319,7 +334,7 @@ __device__ __forceinline__ void apply_grad_mask(const GaussBwdArgs& a, float m, 
 // all loads of the accumulated ones first, then all stores, so the ~20
 // scattered read-modify-writes overlap instead of forming a dependent chain.
 __device__ __forceinline__ void commit_outputs(const GaussBwdArgs& a, int idx, const float (&acc)[9], float dop,
-                                               const float (&dsh)[48], const GaussOut& o) {
+                                               const float (&ddc)[3], const GaussOut& o) {
     const uint32_t f = a.acc;
     const size_t i3 = 3 * (size_t)idx;
     float* d0 = a.dsh.dc ? a.dsh.dc + (size_t)idx * a.dsh.dc_stride : nullptr;
@@ -364,7 +379,7 @@ __device__ __forceinline__ void commit_outputs(const GaussBwdArgs& a, int idx, c
     *r4 = make_float4(orot.x + o.drot.x, orot.y + o.drot.y, orot.z + o.drot.z, orot.w + o.drot.w);
     if (d0) {
 #pragma unroll
-        for (int k = 0; k < 3; ++k) d0[k] = odc[k] + dsh[k];
+        for (int k = 0; k < 3; ++k) d0[k] = odc[k] + ddc[k];
         // coefficients beyond the 16 a degree-3 evaluation uses get zero gradient
         if (!(f & GS_ACC_SH)) {
             float* dr = a.dsh.rest + (size_t)idx * a.dsh.rest_stride;
@@ -543,22 +558,16 @@ __global__ __launch_bounds__(kGB) void k_gauss_bwd_live(GaussBwdArgs a) {
         }
         __syncthreads();  // SH staged
 
-        float dsh[48];
-#pragma unroll
-        for (int k = 0; k < 48; ++k) dsh[k] = 0.f;
+        float ddc[3] = {0.f, 0.f, 0.f};
         float dop = acc[5];  // w.r.t. opacity; chained through the sigmoid when activation = 1
         GaussOut o;
         if (ok) {
-            gauss_bwd_visible(a, gin, acc, dop, my_sh, dsh, o);
-            if (a.grad_mask) apply_grad_mask(a, a.grad_mask[idx] ? 1.f : 0.f, acc, dop, dsh, o);
+            const float gm = a.grad_mask ? (a.grad_mask[idx] ? 1.f : 0.f) : 1.f;
+            // (each thread reads and then overwrites only its own LDS row: no barrier in between)
+            gauss_bwd_visible(a, gin, acc, dop, my_sh, ncol, (a.mask_bits & GS_ACC_SH) ? gm : 1.f, ddc, o);
+            if (a.grad_mask) apply_grad_mask(a, gm, acc, dop, o);
         }
-        if (a.dsh.dc && ncol > 0) {
-            __syncthreads();  // every row read before any row is overwritten
-#pragma unroll
-            for (int k = 0; k < 45; ++k)
-                if (k < ncol) my_sh[k] = dsh[3 + k];
-        }
-        if (ok) commit_outputs(a, idx, acc, dop, dsh, o);
+        if (ok) commit_outputs(a, idx, acc, dop, ddc, o);
         // dL_dsh rest rows: through LDS (in place), flat block-wide batches, loads before stores
         if (a.dsh.dc && ncol > 0) {
             __syncthreads();

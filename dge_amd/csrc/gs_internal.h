@@ -126,7 +126,7 @@ __host__ __device__ inline uint32_t used_base(uint32_t range_x, int tile) { retu
 __host__ __device__ inline size_t used_words(size_t K, int tiles) { return 4 * (K / 64 + (size_t)tiles + 2); }
 
 struct ImgLayout {
-    size_t final_T, n_contrib, counters, ranges, tile_last, quad_last, bwd_count, total;
+    size_t final_T, n_contrib, tile_order, counters, ranges, tile_last, quad_last, bwd_count, total;
 };
 inline ImgLayout img_layout(int W, int H) {
     ImgLayout L;
@@ -135,6 +135,7 @@ inline ImgLayout img_layout(int W, int H) {
     size_t tiles = (size_t)div_up(W, 16) * div_up(H, 16);
     L.final_T = o; o = align_up(o + 4 * n);
     L.n_contrib = o; o = align_up(o + 4 * n);
+    L.tile_order = o; o = align_up(o + 4 * tiles);  // tiles by list length, longest first
     L.counters = o; o = align_up(o + 16);        // counters.. are zeroed per forward (one memset)
     L.ranges = o; o = align_up(o + 8 * tiles);
     L.tile_last = o; o = align_up(o + 4 * tiles);
@@ -262,6 +263,7 @@ void launch_ranges(const uint32_t* sorted_tile, int K, uint2* ranges, uint32_t* 
 struct RenderArgs {
     int W, H, gx, gy;
     const uint2* ranges;
+    uint32_t* tile_order;      // written by launch_render_forward's ordering pass
     const uint2* point_pairs;  // per-tile lists: (Gaussian, binning slot)
     const Splat* splat;
     const float* bg;

@@ -102,12 +102,85 @@ __device__ __forceinline__ bool blend_step(float2 xy, float4 co, float4 fe, uint
     return use;
 }
 
+// pixel_alpha for two consecutive entries at once: the same IEEE operations in
+// the same order (contraction pinned), on float2 so the compiler issues packed
+// v_pk_add/v_pk_mul (two entries per instruction); results bit-identical to
+// two pixel_alpha calls.
+typedef float f2v __attribute__((ext_vector_type(2)));  // built-in vector ops: the pragma below holds
+__device__ __forceinline__ void pixel_alpha2(f2v x, f2v y, f2v cx, f2v cy, f2v cz, f2v op, float pfx, float pfy,
+                                             f2v& alpha, bool& ok0, bool& ok1) {
+#pragma clang fp contract(off)
+    const f2v dx = x - pfx;
+    const f2v dy = y - pfy;
+    const f2v power = -0.5f * (cx * dx * dx + cz * dy * dy) - cy * dx * dy;
+    f2v G;
+    G.x = blend_exp(power.x);
+    G.y = blend_exp(power.y);
+    const f2v oG = op * G;
+    alpha.x = fminf(0.99f, oG.x);
+    alpha.y = fminf(0.99f, oG.y);
+    ok0 = !(power.x > 0.0f) && !(alpha.x < 1.0f / 255.0f);
+    ok1 = !(power.y > 0.0f) && !(alpha.y < 1.0f / 255.0f);
+}
+
+// The sequential part of blend_step once the entry's alpha test is done.
+__device__ __forceinline__ bool blend_chain(bool ok, float alpha, float4 fe, uint32_t pos, bool& done, float& T,
+                                           float& C0, float& C1, float& C2, float& D, uint32_t& last) {
+    const bool hit = ok && !done;
+    const float test_T = T * (1 - alpha);
+    const bool stop = hit && test_T < 0.0001f;
+    const bool use = hit && !stop;
+    done = done || stop;
+    const float w = use ? alpha * T : 0.0f;
+    C0 = C0 + fe.x * w;
+    C1 = C1 + fe.y * w;
+    C2 = C2 + fe.z * w;
+    D = D + fe.w * w;
+    T = use ? test_T : T;
+    last = use ? pos : last;
+    return use;
+}
+
+// Dispatch order of the blend: tiles by list length, longest first (coarse
+// log-scale classes; the order inside a class is whatever the LDS atomics give
+// — it only decides placement).  The longest lists are then dealt first, one
+// per SIMD, instead of landing next to each other (they cluster in the image).
+__global__ __launch_bounds__(1024) void k_tile_order(const uint2* __restrict__ ranges, int tiles,
+                                                     uint32_t* __restrict__ order) {
+    constexpr int kClasses = 64;
+    __shared__ uint32_t cnt[kClasses];
+    const int tid = threadIdx.x;
+    if (tid < kClasses) cnt[tid] = 0u;
+    __syncthreads();
+    auto cls = [](uint32_t len) { return min(kClasses - 1, (int)(__log2f((float)len + 1.0f) * 3.0f)); };
+    for (int t = tid; t < tiles; t += 1024) {
+        const uint2 r = ranges[t];
+        atomicAdd(&cnt[cls(r.y - r.x)], 1u);
+    }
+    __syncthreads();
+    if (tid == 0) {  // start of each class, longest class first
+        uint32_t run = 0;
+        for (int c = kClasses - 1; c >= 0; --c) {
+            const uint32_t n = cnt[c];
+            cnt[c] = run;
+            run += n;
+        }
+    }
+    __syncthreads();
+    for (int t = tid; t < tiles; t += 1024) {
+        const uint2 r = ranges[t];
+        order[atomicAdd(&cnt[cls(r.y - r.x)], 1u)] = (uint32_t)t;
+    }
+}
+
 __global__ __launch_bounds__(64) void k_render_fwd(RenderArgs a) {
     // XCD-aware: blocks b, b+8, b+16, b+24 (one XCD under the round-robin dealing) take the four
-    // quadrants of one tile, so the tile's list and its Splat gathers are fetched into one L2
+    // quadrants of one tile, so the tile's list and its Splat gathers are fetched into one L2;
+    // tiles in k_tile_order's order, longest list first
     const int x8 = blockIdx.x & 7, j8 = blockIdx.x >> 3;
-    const int quad = j8 & 3, tile = (j8 >> 2) * 8 + x8;
-    if (tile >= a.gx * a.gy) return;
+    const int quad = j8 & 3, rank = (j8 >> 2) * 8 + x8;
+    if (rank >= a.gx * a.gy) return;
+    const int tile = (int)a.tile_order[rank];
     const int qidx = 4 * tile + quad;
     const int tx = tile % a.gx, ty = tile / a.gx;
     const int lane = threadIdx.x;
@@ -116,8 +189,10 @@ __global__ __launch_bounds__(64) void k_render_fwd(RenderArgs a) {
     const bool inside = px < a.W && py < a.H;
     const float pfx = (float)px, pfy = (float)py;
 
-    __shared__ float2 s_xy[kRound + kGroup];
-    __shared__ float4 s_co[kRound + kGroup];
+    // the round's kept entries, one array per field: a pair of consecutive entries' field is one
+    // 8-B read, the operand of a packed instruction (pixel_alpha2)
+    __shared__ float s_x[kRound + kGroup], s_y[kRound + kGroup];
+    __shared__ float s_cx[kRound + kGroup], s_cy[kRound + kGroup], s_cz[kRound + kGroup], s_op[kRound + kGroup];
     __shared__ float4 s_rgbd[kRound + kGroup];
     __shared__ uint32_t s_pos[kRound + kGroup];
     __shared__ uint32_t s_gused[kRound / kGroup + 1];  // per blend group: bit u = entry u was blended
@@ -181,8 +256,12 @@ __global__ __launch_bounds__(64) void k_render_fwd(RenderArgs a) {
             kslot[i] = keep ? nk + __popcll(km & lanemask_lt()) : -1;
             if (keep) {
                 const int slot = kslot[i];
-                s_xy[slot] = cur[i].xy;
-                s_co[slot] = cur[i].co;
+                s_x[slot] = cur[i].xy.x;
+                s_y[slot] = cur[i].xy.y;
+                s_cx[slot] = cur[i].co.x;
+                s_cy[slot] = cur[i].co.y;
+                s_cz[slot] = cur[i].co.z;
+                s_op[slot] = cur[i].co.w;
                 s_rgbd[slot] = cur[i].f;
                 s_pos[slot] = k - range.x + 1;  // 1-based contributor index (forward.cu:331)
             }
@@ -190,8 +269,12 @@ __global__ __launch_bounds__(64) void k_render_fwd(RenderArgs a) {
         }
         // pad to a whole group with entries that fail alpha >= 1/255 everywhere
         if (lane < kGroup) {
-            s_xy[nk + lane] = make_float2(0.f, 0.f);
-            s_co[nk + lane] = make_float4(0.f, 0.f, 0.f, 0.f);
+            s_x[nk + lane] = 0.f;
+            s_y[nk + lane] = 0.f;
+            s_cx[nk + lane] = 0.f;
+            s_cy[nk + lane] = 0.f;
+            s_cz[nk + lane] = 0.f;
+            s_op[nk + lane] = 0.f;
             s_rgbd[nk + lane] = make_float4(0.f, 0.f, 0.f, 0.f);
             s_pos[nk + lane] = 0u;
         }
@@ -215,10 +298,16 @@ __global__ __launch_bounds__(64) void k_render_fwd(RenderArgs a) {
             if (!__any(!done)) break;
             uint32_t gm = 0u;  // (uniform: scalar ops beside the blend's vector ones)
 #pragma unroll
-            for (int u = 0; u < kGroup; ++u) {
-                const bool use = blend_step(s_xy[j + u], s_co[j + u], s_rgbd[j + u], s_pos[j + u], pfx, pfy, done, T,
-                                            C0, C1, C2, D, last);
-                gm |= (__ballot(use) != 0ull ? 1u : 0u) << u;
+            for (int u = 0; u < kGroup; u += 2) {
+                f2v al;
+                bool ok0, ok1;
+                const auto ld2 = [&](const float* f) { return *reinterpret_cast<const f2v*>(f + j + u); };
+                pixel_alpha2(ld2(s_x), ld2(s_y), ld2(s_cx), ld2(s_cy), ld2(s_cz), ld2(s_op), pfx, pfy, al, ok0, ok1);
+                const bool use0 = blend_chain(ok0, al.x, s_rgbd[j + u], s_pos[j + u], done, T, C0, C1, C2, D, last);
+                gm |= (__ballot(use0) != 0ull ? 1u : 0u) << u;
+                const bool use1 =
+                    blend_chain(ok1, al.y, s_rgbd[j + u + 1], s_pos[j + u + 1], done, T, C0, C1, C2, D, last);
+                gm |= (__ballot(use1) != 0ull ? 1u : 0u) << (u + 1);
             }
             s_gused[j / kGroup] = gm;
         }
@@ -281,6 +370,7 @@ __global__ __launch_bounds__(64) void k_render_fwd(RenderArgs a) {
 void launch_render_forward(const RenderArgs& a, hipStream_t s) {
     const int tiles = a.gx * a.gy;
     if (tiles <= 0) return;
+    hipLaunchKernelGGL(k_tile_order, dim3(1), dim3(1024), 0, s, a.ranges, tiles, a.tile_order);
     hipLaunchKernelGGL(k_render_fwd, dim3(div_up(tiles, 8) * 32), dim3(64), 0, s, a);
 }
 
