@@ -108,12 +108,11 @@ __device__ __forceinline__ bool blend_step(float2 xy, float4 co, float4 fe, uint
 // two pixel_alpha calls.
 typedef float f2v __attribute__((ext_vector_type(2)));  // built-in vector ops: the pragma below holds
 __device__ __forceinline__ void pixel_alpha2(f2v x, f2v y, f2v cx, f2v cy, f2v cz, f2v op, float pfx, float pfy,
-                                             f2v& alpha, bool& ok0, bool& ok1) {
+                                             f2v& dx, f2v& dy, f2v& G, f2v& alpha, bool& ok0, bool& ok1) {
 #pragma clang fp contract(off)
-    const f2v dx = x - pfx;
-    const f2v dy = y - pfy;
+    dx = x - pfx;
+    dy = y - pfy;
     const f2v power = -0.5f * (cx * dx * dx + cz * dy * dy) - cy * dx * dy;
-    f2v G;
     G.x = blend_exp(power.x);
     G.y = blend_exp(power.y);
     const f2v oG = op * G;
@@ -299,10 +298,11 @@ __global__ __launch_bounds__(64) void k_render_fwd(RenderArgs a) {
             uint32_t gm = 0u;  // (uniform: scalar ops beside the blend's vector ones)
 #pragma unroll
             for (int u = 0; u < kGroup; u += 2) {
-                f2v al;
+                f2v al, dx2, dy2, G2;
                 bool ok0, ok1;
                 const auto ld2 = [&](const float* f) { return *reinterpret_cast<const f2v*>(f + j + u); };
-                pixel_alpha2(ld2(s_x), ld2(s_y), ld2(s_cx), ld2(s_cy), ld2(s_cz), ld2(s_op), pfx, pfy, al, ok0, ok1);
+                pixel_alpha2(ld2(s_x), ld2(s_y), ld2(s_cx), ld2(s_cy), ld2(s_cz), ld2(s_op), pfx, pfy, dx2, dy2, G2,
+                             al, ok0, ok1);
                 const bool use0 = blend_chain(ok0, al.x, s_rgbd[j + u], s_pos[j + u], done, T, C0, C1, C2, D, last);
                 gm |= (__ballot(use0) != 0ull ? 1u : 0u) << u;
                 const bool use1 =
@@ -472,11 +472,12 @@ void launch_render_apply_weights(const ApplyWeightsArgs& a, hipStream_t s) {
 //   g = (u dx, u dy, u dx^2, u dx dy, u dy^2, u, aT dp0, aT dp1, aT dp2)
 // — the entry's conic, opacity and the ndc scale are constant over pixels
 // and are applied once per entry after the reduction (finish_record).
-__device__ __forceinline__ void bwd_step(float2 xy, float4 co, float4 c, bool in_list, float pfx, float pfy,
-                                        float dp0, float dp1, float dp2, float nbg, float& T, float& D0,
-                                        float& D1, float& D2, float (&g)[9]) {
-    float dx, dy, G, alpha;
-    const bool hit = pixel_alpha(xy, co, pfx, pfy, dx, dy, G, alpha) && in_list;
+//
+// Two consecutive entries of the replay: the alpha tests packed (pixel_alpha2),
+// the back-to-front chain (T, D) entry by entry (bwd_chain), the per-pixel
+// products of the nine sums packed again.
+__device__ __forceinline__ float bwd_chain(bool hit, float alpha, float G, float4 c, float dp0, float dp1, float dp2,
+                                           float nbg, float& T, float& D0, float& D1, float& D2, float& wc) {
     const float ae = hit ? alpha : 0.f;
     const float r = __builtin_amdgcn_rcpf(1.f - ae);
     T = hit ? T * r : T;
@@ -484,22 +485,38 @@ __device__ __forceinline__ void bwd_step(float2 xy, float4 co, float4 c, bool in
     float dL_dalpha = t0 * dp0;
     dL_dalpha += t1 * dp1;
     dL_dalpha += t2 * dp2;
-    dL_dalpha = dL_dalpha * T + nbg * r;  // nbg = -T_final * (bg . dL/dpix)
-    const float u = hit ? G * dL_dalpha : 0.f;
-    const float wc = ae * T;  // dchannel_dcolor
-    const float udx = u * dx, udy = u * dy;
-    g[0] = udx;
-    g[1] = udy;
-    g[2] = udx * dx;
-    g[3] = udx * dy;
-    g[4] = udy * dy;
-    g[5] = u;
-    g[6] = wc * dp0;
-    g[7] = wc * dp1;
-    g[8] = wc * dp2;
+    dL_dalpha = dL_dalpha * T + nbg * r;
+    wc = ae * T;
     D0 += ae * t0;
     D1 += ae * t1;
     D2 += ae * t2;
+    return hit ? G * dL_dalpha : 0.f;
+}
+
+__device__ __forceinline__ void bwd_pair(f2v x, f2v y, f2v cx, f2v cy, f2v cz, f2v op, float4 c0, float4 c1, bool in0,
+                                         bool in1, float pfx, float pfy, float dp0, float dp1, float dp2, float nbg,
+                                         float& T, float& D0, float& D1, float& D2, float (&g0)[9], float (&g1)[9]) {
+    f2v dx, dy, G, alpha;
+    bool ok0, ok1;
+    pixel_alpha2(x, y, cx, cy, cz, op, pfx, pfy, dx, dy, G, alpha, ok0, ok1);
+    float wc0, wc1;
+    f2v u, wc;
+    u.x = bwd_chain(ok0 && in0, alpha.x, G.x, c0, dp0, dp1, dp2, nbg, T, D0, D1, D2, wc0);
+    u.y = bwd_chain(ok1 && in1, alpha.y, G.y, c1, dp0, dp1, dp2, nbg, T, D0, D1, D2, wc1);
+    wc.x = wc0;
+    wc.y = wc1;
+    const f2v udx = u * dx, udy = u * dy;
+    const f2v gxx = udx * dx, gxy = udx * dy, gyy = udy * dy;
+    const f2v w0 = wc * dp0, w1 = wc * dp1, w2 = wc * dp2;
+    g0[0] = udx.x; g1[0] = udx.y;
+    g0[1] = udy.x; g1[1] = udy.y;
+    g0[2] = gxx.x; g1[2] = gxx.y;
+    g0[3] = gxy.x; g1[3] = gxy.y;
+    g0[4] = gyy.x; g1[4] = gyy.y;
+    g0[5] = u.x;   g1[5] = u.y;
+    g0[6] = w0.x;  g1[6] = w0.y;
+    g0[7] = w1.x;  g1[7] = w1.y;
+    g0[8] = w2.x;  g1[8] = w2.y;
 }
 
 // The entry's record from the quadrant sums S: the reference's per-pixel
@@ -526,8 +543,10 @@ constexpr int kBwdGroup = 4;  // entries replayed between two reduce-scatters
 // slot, so k_gauss_bwd reads a Gaussian's records contiguously) and a flag.
 __global__ __launch_bounds__(64, 4) void k_render_bwd(RenderBwdArgs a) {
     // kept entries of a round, compacted back to front, + a group of padding
-    __shared__ float2 s_xy[kRound + kBwdGroup];
-    __shared__ float4 s_co[kRound + kBwdGroup];
+    // (one array per field: a pair of consecutive entries' field is one 8-B read, see bwd_pair)
+    __shared__ float s_x[kRound + kBwdGroup], s_y[kRound + kBwdGroup];
+    __shared__ float s_cx[kRound + kBwdGroup], s_cy[kRound + kBwdGroup], s_cz[kRound + kBwdGroup],
+        s_op[kRound + kBwdGroup];
     __shared__ float4 s_rgb[kRound + kBwdGroup];
     __shared__ uint32_t s_pos[kRound + kBwdGroup];
     const int lane = threadIdx.x;
@@ -636,16 +655,24 @@ __global__ __launch_bounds__(64, 4) void k_render_bwd(RenderBwdArgs a) {
             const uint64_t km = __ballot(keep);
             if (keep) {
                 const int slot = nk + __popcll(km & ~lanemask_lt() & ~(1ull << lane));
-                s_xy[slot] = cur[i].xy;
-                s_co[slot] = cur[i].co;
+                s_x[slot] = cur[i].xy.x;
+                s_y[slot] = cur[i].xy.y;
+                s_cx[slot] = cur[i].co.x;
+                s_cy[slot] = cur[i].co.y;
+                s_cz[slot] = cur[i].co.z;
+                s_op[slot] = cur[i].co.w;
                 s_rgb[slot] = cur[i].f;
                 s_pos[slot] = (uint32_t)(lo + j);
             }
             nk += __popcll(km);
         }
         if (lane < kBwdGroup) {  // padding: alpha = 0 everywhere, never in a pixel's list
-            s_xy[nk + lane] = make_float2(0.f, 0.f);
-            s_co[nk + lane] = make_float4(0.f, 0.f, 0.f, 0.f);
+            s_x[nk + lane] = 0.f;
+            s_y[nk + lane] = 0.f;
+            s_cx[nk + lane] = 0.f;
+            s_cy[nk + lane] = 0.f;
+            s_cz[nk + lane] = 0.f;
+            s_op[nk + lane] = 0.f;
             s_rgb[nk + lane] = make_float4(0.f, 0.f, 0.f, 0.f);
             s_pos[nk + lane] = 0xFFFFFFFFu;
         }
@@ -664,9 +691,12 @@ __global__ __launch_bounds__(64, 4) void k_render_bwd(RenderBwdArgs a) {
         for (int k = 0; k < nk; k += kBwdGroup) {
             float g[kBwdGroup][9];
 #pragma unroll
-            for (int e = 0; e < kBwdGroup; ++e)
-                bwd_step(s_xy[k + e], s_co[k + e], s_rgb[k + e], s_pos[k + e] < last_contributor, pfx, pfy, dp0, dp1,
-                         dp2, nbg, T, D0, D1, D2, g[e]);
+            for (int e = 0; e < kBwdGroup; e += 2) {
+                const auto ld2 = [&](const float* f) { return *reinterpret_cast<const f2v*>(f + k + e); };
+                bwd_pair(ld2(s_x), ld2(s_y), ld2(s_cx), ld2(s_cy), ld2(s_cz), ld2(s_op), s_rgb[k + e],
+                         s_rgb[k + e + 1], s_pos[k + e] < last_contributor, s_pos[k + e + 1] < last_contributor, pfx,
+                         pfy, dp0, dp1, dp2, nbg, T, D0, D1, D2, g[e], g[e + 1]);
+            }
             float S[9];
 #pragma unroll
             for (int f = 0; f < 9; ++f) S[f] = quad_reduce(g[0][f], g[1][f], g[2][f], g[3][f]);
@@ -674,7 +704,8 @@ __global__ __launch_bounds__(64, 4) void k_render_bwd(RenderBwdArgs a) {
             if (row_writer && kw < nk) {
                 const uint2 pr = a.point_pairs[range.x + s_pos[kw]];  // (an L2 hit: this round's pairs)
                 const size_t rec = 4 * (size_t)pr.y + quad;
-                finish_record(s_co[kw], S, ddelx_dx, ddely_dy, a.records + 3 * rec);
+                finish_record(make_float4(s_cx[kw], s_cy[kw], s_cz[kw], s_op[kw]), S, ddelx_dx, ddely_dy,
+                              a.records + 3 * rec);
                 a.rec_flags[rec] = 1;
                 a.touched[pr.x] = 1;
             }
