@@ -20,12 +20,17 @@
 
 namespace gs {
 
-// forward.cu:20-71.  c0 = coefficient 0, r = coefficients 1.. (see ShView)
-__device__ __forceinline__ f3 sh_to_rgb(int deg, f3 pos, f3 campos, f3 c0, const float* __restrict__ r,
-                                        uint8_t& clamp_bits) {
+// forward.cu:20-71, in two parts so the coefficient rows can be staged in two
+// halves: sh_rgb_head = bands 0-2 (c0 = coefficient 0, rA = coefficients 1..8),
+// sh_rgb_tail = band 3 (rB = coefficients 9..15) + the offset and clamp.  The
+// sum is accumulated in the reference's order either way.
+__device__ __forceinline__ f3 sh_dir(f3 pos, f3 campos) {
     f3 dir = pos - campos;
     const float len = sqrtf(dot3(dir, dir));
-    dir = mk3(dir.x / len, dir.y / len, dir.z / len);
+    return mk3(dir.x / len, dir.y / len, dir.z / len);
+}
+
+__device__ __forceinline__ f3 sh_rgb_head(int deg, f3 dir, f3 c0, const float* __restrict__ r) {
     f3 res = c0 * kSH_C0;
     if (deg > 0) {
         const float x = dir.x, y = dir.y, z = dir.z;
@@ -35,22 +40,42 @@ __device__ __forceinline__ f3 sh_to_rgb(int deg, f3 pos, f3 campos, f3 c0, const
             res = res + ld3(r + 9) * (kSH_C2_0 * xy) + ld3(r + 12) * (kSH_C2_1 * yz) +
                   ld3(r + 15) * (kSH_C2_2 * (2.0f * zz - xx - yy)) + ld3(r + 18) * (kSH_C2_3 * xz) +
                   ld3(r + 21) * (kSH_C2_4 * (xx - yy));
-            if (deg > 2) {
-                res = res + ld3(r + 24) * (kSH_C3_0 * y * (3.0f * xx - yy)) + ld3(r + 27) * (kSH_C3_1 * xy * z) +
-                      ld3(r + 30) * (kSH_C3_2 * y * (4.0f * zz - xx - yy)) +
-                      ld3(r + 33) * (kSH_C3_3 * z * (2.0f * zz - 3.0f * xx - 3.0f * yy)) +
-                      ld3(r + 36) * (kSH_C3_4 * x * (4.0f * zz - xx - yy)) +
-                      ld3(r + 39) * (kSH_C3_5 * z * (xx - yy)) + ld3(r + 42) * (kSH_C3_6 * x * (xx - 3.0f * yy));
-            }
         }
+    }
+    return res;
+}
+
+__device__ __forceinline__ f3 sh_rgb_tail(int deg, f3 dir, f3 res, const float* __restrict__ r, uint8_t& clamp_bits) {
+    if (deg > 2) {
+        const float x = dir.x, y = dir.y, z = dir.z;
+        const float xx = x * x, yy = y * y, zz = z * z, xy = x * y;
+        res = res + ld3(r) * (kSH_C3_0 * y * (3.0f * xx - yy)) + ld3(r + 3) * (kSH_C3_1 * xy * z) +
+              ld3(r + 6) * (kSH_C3_2 * y * (4.0f * zz - xx - yy)) +
+              ld3(r + 9) * (kSH_C3_3 * z * (2.0f * zz - 3.0f * xx - 3.0f * yy)) +
+              ld3(r + 12) * (kSH_C3_4 * x * (4.0f * zz - xx - yy)) + ld3(r + 15) * (kSH_C3_5 * z * (xx - yy)) +
+              ld3(r + 18) * (kSH_C3_6 * x * (xx - 3.0f * yy));
     }
     res = mk3(res.x + 0.5f, res.y + 0.5f, res.z + 0.5f);
     clamp_bits = (res.x < 0 ? 1 : 0) | (res.y < 0 ? 2 : 0) | (res.z < 0 ? 4 : 0);
     return mk3(fmaxf(res.x, 0.0f), fmaxf(res.y, 0.0f), fmaxf(res.z, 0.0f));
 }
 
+// fp16 SH rows (kSplit): coefficient rows 1..15 of the block's Gaussians are
+// staged through LDS in two halves (coefficients 1..8 = 24 values, then 9..15
+// = 21) in one 25-float-pitch buffer: 25.6 KB instead of 46 KB per block, 6
+// waves per SIMD instead of 3 (c5: 48 -> 34 us).  Both halves are loaded at
+// kernel start — the second into registers, written to LDS once the first
+// half is consumed.  Element f of a half: row f / n, column f % n.  fp32 rows
+// keep the one-pass float4 staging (measured faster there: 93 vs 95 us at c2).
+constexpr int kShA = 24, kShB = 21, kShPitchAB = 25;
+constexpr int kShBPer = (256 * kShB + 255) / 256;  // = 21 register values per thread
+
+
+
+template <bool kSplit>
 __global__ __launch_bounds__(256) void k_preprocess(PreprocessArgs a) {
-    __shared__ float s_sh[256 * kShPitch];
+    constexpr int kPitch = kSplit ? kShPitchAB : kShPitch;
+    __shared__ float s_sh[256 * kPitch];
     const int idx0 = blockIdx.x * 256;
     const int idx = idx0 + threadIdx.x;
     uint32_t touched = 0;
@@ -67,13 +92,38 @@ __global__ __launch_bounds__(256) void k_preprocess(PreprocessArgs a) {
     // culled are read needlessly (180 B each), which object-centric views hardly have
     const int ncol = (a.M - 1) * 3 < kShPitch ? (a.M - 1) * 3 : kShPitch;
     const bool stage_sh = a.copy_colors && !a.colors_precomp && a.sh.dc && ncol > 0;
-    if (stage_sh) {
-        const int nrow = a.P - idx0 < 256 ? a.P - idx0 : 256;
-        if (a.sh.half)
-            sh_rows_load_half<256>(reinterpret_cast<const __half*>(a.sh.rest) + (size_t)idx0 * a.sh.rest_stride,
-                                   a.sh.rest_stride, s_sh, nrow, ncol);
-        else
-            sh_rows_load<256>(a.sh.rest + (size_t)idx0 * a.sh.rest_stride, a.sh.rest_stride, s_sh, nrow, ncol);
+    const int nrow = a.P - idx0 < 256 ? a.P - idx0 : 256;
+    const int ncolA = ncol < kShA ? ncol : kShA, ncolB = ncol - ncolA;
+    float shB[kShBPer];
+    if (stage_sh && !kSplit) {
+        sh_rows_load<256>(a.sh.rest + (size_t)idx0 * a.sh.rest_stride, a.sh.rest_stride, s_sh, nrow, ncol);
+    } else if (stage_sh) {
+        // both halves' loads issued together (32-bit offsets from the block's uniform base): the first
+        // half is stored to LDS as it arrives, the second stays in registers
+        const int stride = a.sh.rest_stride;
+        const float invA = 1.0f / (float)ncolA, invB = ncolB > 0 ? 1.0f / (float)ncolB : 0.f;
+        const float* baseF = a.sh.rest + (size_t)idx0 * stride;
+        const __half* baseH = reinterpret_cast<const __half*>(a.sh.rest) + (size_t)idx0 * stride;
+        auto ld = [&](uint32_t off) { return a.sh.half ? __half2float(baseH[off]) : baseF[off]; };
+        float shA[kShA];
+#pragma unroll
+        for (int i = 0; i < kShA; ++i) {
+            const int f = threadIdx.x + 256 * i;
+            const int row = (int)(((float)f + 0.5f) * invA), col = f - row * ncolA;
+            shA[i] = row < nrow ? ld((uint32_t)(row * stride + col)) : 0.f;
+        }
+#pragma unroll
+        for (int i = 0; i < kShBPer; ++i) {
+            const int f = threadIdx.x + 256 * i;
+            const int row = (int)(((float)f + 0.5f) * invB), col = f - row * ncolB;
+            shB[i] = ncolB > 0 && row < nrow ? ld((uint32_t)(row * stride + kShA + col)) : 0.f;
+        }
+#pragma unroll
+        for (int i = 0; i < kShA; ++i) {
+            const int f = threadIdx.x + 256 * i;
+            const int row = (int)(((float)f + 0.5f) * invA), col = f - row * ncolA;
+            if (row < nrow) s_sh[row * kShPitchAB + col] = shA[i];
+        }
     }
     if (idx < a.P) {
         const float* v = a.view;
@@ -136,14 +186,27 @@ __global__ __launch_bounds__(256) void k_preprocess(PreprocessArgs a) {
     // colours: precomputed, or SH evaluated from rows staged through LDS (coalesced)
     const bool need_sh = touched && a.copy_colors && !a.colors_precomp && a.sh.dc;
     (void)need_sh;
-    if (stage_sh) __syncthreads();  // SH rows staged
-    if (touched && a.copy_colors) {
-        if (a.colors_precomp)
-            rgb = ld3(a.colors_precomp + 3 * (size_t)idx);
-        else
-            rgb = sh_to_rgb(a.D, p, ld3(a.campos), sh_dc3(a.sh.dc, a.sh.half, (size_t)idx * a.sh.dc_stride),
-                            s_sh + threadIdx.x * kShPitch, clamp_bits);
+    if (stage_sh) __syncthreads();  // first half staged
+    f3 dir = mk3(0.f, 0.f, 0.f), head = mk3(0.f, 0.f, 0.f);
+    const bool sh_color = touched && a.copy_colors && !a.colors_precomp;
+    if (touched && a.copy_colors && a.colors_precomp) rgb = ld3(a.colors_precomp + 3 * (size_t)idx);
+    if (sh_color) {
+        dir = sh_dir(p, ld3(a.campos));
+        head = sh_rgb_head(a.D, dir, sh_dc3(a.sh.dc, a.sh.half, (size_t)idx * a.sh.dc_stride),
+                           s_sh + threadIdx.x * kPitch);
     }
+    if (kSplit && stage_sh && ncolB > 0) {
+        __syncthreads();  // every row's first half read
+        const float invB = 1.0f / (float)ncolB;
+#pragma unroll
+        for (int i = 0; i < kShBPer; ++i) {
+            const int f = threadIdx.x + 256 * i;
+            const int row = (int)(((float)f + 0.5f) * invB), col = f - row * ncolB;
+            if (row < nrow) s_sh[row * kShPitchAB + col] = shB[i];
+        }
+        __syncthreads();  // second half staged
+    }
+    if (sh_color) rgb = sh_rgb_tail(a.D, dir, head, s_sh + threadIdx.x * kPitch + (kSplit ? 0 : kShA), clamp_bits);
     if (idx < a.P) {
         if (touched) {
             Splat sp;
@@ -177,7 +240,10 @@ __global__ __launch_bounds__(256) void k_preprocess(PreprocessArgs a) {
 
 void launch_preprocess(const PreprocessArgs& a, hipStream_t s) {
     if (a.P <= 0) return;
-    hipLaunchKernelGGL(k_preprocess, dim3(div_up(a.P, 256)), dim3(256), 0, s, a);
+    if (a.sh.half)
+        hipLaunchKernelGGL(k_preprocess<true>, dim3(div_up(a.P, 256)), dim3(256), 0, s, a);
+    else
+        hipLaunchKernelGGL(k_preprocess<false>, dim3(div_up(a.P, 256)), dim3(256), 0, s, a);
 }
 
 // checkFrustum (rasterizer_impl.cu:53-63)
