@@ -278,9 +278,13 @@ def apply_weights(background, means3D, weights, opacity, scales, rotations, scal
 # fused path: raw GaussianModel parameters, activations and SH split in-kernel
 # (gs_rasterize_forward_ex / gs_rasterize_backward_ex)
 # ---------------------------------------------------------------------------
-def _params(P, xyz, f_dc, f_rest, colors, raw_opacity, raw_scaling, raw_rotation):
+def _params(P, xyz, f_dc, f_rest, colors, raw_opacity, raw_scaling, raw_rotation, index=None):
+    """gs_params of the raw-parameter path; `index` (int32 [P], ascending): the localize subset's rows
+    (gathered in-kernel); fp16 features are read as such (sh_half)."""
     g = N.GsParams()
     g.P = P
+    g.index = _ptr(index)
+    g.sh_half = 1 if f_dc is not None and f_dc.dtype == torch.float16 else 0
     have_sh = f_dc is not None and f_dc.numel() != 0
     Mr = f_rest.size(1) if have_sh and f_rest is not None and f_rest.numel() != 0 else 0
     g.M = (1 + Mr) if have_sh else 0
@@ -298,24 +302,42 @@ def _params(P, xyz, f_dc, f_rest, colors, raw_opacity, raw_scaling, raw_rotation
     return g
 
 
+def _index32(index):
+    if index is None:
+        return None
+    if index.dtype != torch.int32 or index.dim() != 1:
+        raise RuntimeError("index must be a 1-D int32 tensor of parameter rows")
+    return index.contiguous()
+
+
+def _features(t, name):
+    """fp32, or fp16 read as such (gs_params.sh_half); contiguous."""
+    if t is None or t.numel() == 0 or t.dtype != torch.float16:
+        return _f32(t, name)
+    return t.contiguous()
+
+
 def rasterize_gaussians_fused(background, xyz, f_dc, f_rest, colors, raw_opacity, raw_scaling, raw_rotation,
                               scale_modifier, viewmatrix, projmatrix, tan_fovx, tan_fovy, image_height, image_width,
-                              degree, campos, prefiltered, debug):
+                              degree, campos, prefiltered, debug, index=None):
     """Forward on raw parameters: opacity = sigmoid, scale = exp, rotation = normalize applied in-kernel,
-    SH read from _features_dc [P,1,3] and _features_rest [P,M-1,3] without concatenation."""
+    SH read from _features_dc [P,1,3] and _features_rest [P,M-1,3] without concatenation (fp32 or fp16).
+    index: optional int32 rows — render only those Gaussians (the `localize` subset), P = len(index)."""
     N.require_gpu(xyz)
     dev = xyz.device
-    P = xyz.size(0)
+    index = _index32(index)
+    P = index.numel() if index is not None else xyz.size(0)
     H, W = int(image_height), int(image_width)
     with torch.cuda.device(dev):
         xyz = _f32(xyz, "xyz")
-        f_dc, f_rest, colors = _f32(f_dc, "features_dc"), _f32(f_rest, "features_rest"), _f32(colors, "colors")
+        f_dc, f_rest = _features(f_dc, "features_dc"), _features(f_rest, "features_rest")
+        colors = _f32(colors, "colors")
         raw_opacity, raw_scaling = _f32(raw_opacity, "opacity"), _f32(raw_scaling, "scaling")
         raw_rotation = _f32(raw_rotation, "rotation")
         out_color = torch.empty((3, H, W), dtype=torch.float32, device=dev)
         out_depth = torch.empty((1, H, W), dtype=torch.float32, device=dev)
         radii = torch.empty((P,), dtype=torch.int32, device=dev)
-        g = _params(P, xyz, f_dc, f_rest, colors, raw_opacity, raw_scaling, raw_rotation)
+        g = _params(P, xyz, f_dc, f_rest, colors, raw_opacity, raw_scaling, raw_rotation, index)
         s, keep = _settings(background, viewmatrix, projmatrix, campos, tan_fovx, tan_fovy, H, W, degree,
                             scale_modifier, prefiltered, debug)
         alloc = _Allocator(dev)
@@ -333,16 +355,19 @@ def rasterize_gaussians_fused(background, xyz, f_dc, f_rest, colors, raw_opacity
 def rasterize_gaussians_fused_backward(background, xyz, f_dc, f_rest, colors, raw_opacity, raw_scaling, raw_rotation,
                                        radii, scale_modifier, viewmatrix, projmatrix, tan_fovx, tan_fovy,
                                        dL_dout_color, degree, campos, geomBuffer, R, binningBuffer, imageBuffer,
-                                       debug, into=None):
+                                       debug, into=None, index=None):
     """-> (dL_dmeans2D [P,3], dL_dxyz, dL_dfeatures_dc, dL_dfeatures_rest, dL_dcolors, dL_dopacity_raw,
     dL_dscaling_raw, dL_drotation_raw), gradients w.r.t. the raw tensors.
 
     into: optional {"xyz"|"sh"|"opacity"|"scaling"|"rotation": (dest, accumulate)} — write that gradient
     into `dest` (for "sh" a (dc, rest) pair), adding to its contents when accumulate is true (the kernel's
-    fused gradient accumulation, gs_grads.accumulate); the returned tuple then holds `dest`."""
+    fused gradient accumulation, gs_grads.accumulate); the returned tuple then holds `dest`.
+    index: the forward's rows; the parameter-shaped gradients are then full-size, zero outside them."""
     N.require_gpu(xyz)
     dev = xyz.device
-    P = xyz.size(0)
+    index = _index32(index)
+    Pp = xyz.size(0)  # parameter rows
+    P = index.numel() if index is not None else Pp
     H, W = int(dL_dout_color.size(1)), int(dL_dout_color.size(2))
     with torch.cuda.device(dev):
         opts = dict(dtype=torch.float32, device=dev)
@@ -359,26 +384,30 @@ def rasterize_gaussians_fused_backward(background, xyz, f_dc, f_rest, colors, ra
                 return t
             return make()
 
+        # parameter-shaped outputs: only the index rows are written, so fresh ones start at zero
+        new = torch.zeros if index is not None else torch.empty
+        new_like = torch.zeros_like if index is not None else torch.empty_like
         d_m2 = torch.empty((P, 3), **opts)
-        d_xyz = dest("xyz", lambda: torch.empty((P, 3), **opts), N.ACC_MEANS3D)
+        d_xyz = dest("xyz", lambda: new((Pp, 3), **opts), N.ACC_MEANS3D)
         if have_sh and "sh" in into:
             (d_dc, d_rest), acc = into["sh"]
             acc_bits |= N.ACC_SH if acc else 0
         else:
-            d_dc = torch.empty_like(f_dc, **opts) if have_sh else None
-            d_rest = torch.empty_like(f_rest, **opts) if have_sh and f_rest is not None else None
+            d_dc = new_like(f_dc, **opts) if have_sh else None
+            d_rest = new_like(f_rest, **opts) if have_sh and f_rest is not None else None
         d_col = None if have_sh else torch.empty((P, 3), **opts)  # not needed when colours come from SH
-        d_op = dest("opacity", lambda: torch.empty_like(raw_opacity, **opts), N.ACC_OPACITY)
-        d_sc = dest("scaling", lambda: torch.empty((P, 3), **opts), N.ACC_SCALES)
-        d_rot = dest("rotation", lambda: torch.empty((P, 4), **opts), N.ACC_ROTATIONS)
+        d_op = dest("opacity", lambda: new_like(raw_opacity, **opts), N.ACC_OPACITY)
+        d_sc = dest("scaling", lambda: new((Pp, 3), **opts), N.ACC_SCALES)
+        d_rot = dest("rotation", lambda: new((Pp, 4), **opts), N.ACC_ROTATIONS)
         out = (d_m2, d_xyz, d_dc, d_rest, d_col, d_op, d_sc, d_rot)
         if P == 0:
             return out
         xyz = _f32(xyz, "xyz")
-        f_dc, f_rest, colors = _f32(f_dc, "features_dc"), _f32(f_rest, "features_rest"), _f32(colors, "colors")
+        f_dc, f_rest = _features(f_dc, "features_dc"), _features(f_rest, "features_rest")
+        colors = _f32(colors, "colors")
         raw_opacity, raw_scaling = _f32(raw_opacity, "opacity"), _f32(raw_scaling, "scaling")
         raw_rotation = _f32(raw_rotation, "rotation")
-        g = _params(P, xyz, f_dc, f_rest, colors, raw_opacity, raw_scaling, raw_rotation)
+        g = _params(P, xyz, f_dc, f_rest, colors, raw_opacity, raw_scaling, raw_rotation, index)
         o = N.GsGrads()
         o.dL_dmeans2D, o.dL_dcolors, o.dL_dopacity = _ptr(d_m2), _ptr(d_col), _ptr(d_op)
         o.dL_dmeans3D, o.dL_dcov3D = _ptr(d_xyz), None

@@ -61,6 +61,7 @@ class GsParams(ctypes.Structure):
         ("cov3D_precomp", _fp),
         ("activation", ctypes.c_int),
         ("sh_half", ctypes.c_int),
+        ("index", ctypes.c_void_p),
     ]
 
 

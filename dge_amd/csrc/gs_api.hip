@@ -209,6 +209,7 @@ gs_params make_params(int P, int M, const float* means3D, const float* shs, cons
     g.cov3D_precomp = cov3D_precomp;
     g.activation = 0;
     g.sh_half = 0;
+    g.index = nullptr;
     return g;
 }
 
@@ -269,6 +270,7 @@ int bin_forward(const gs_settings* s, const Grid& g, const gs_params& gp, int* r
     pa.P = P; pa.D = s->sh_degree; pa.M = gp.M; pa.W = g.W; pa.H = g.H; pa.gx = g.gx; pa.gy = g.gy;
     pa.means3D = gp.means3D; pa.sh = sh_view(gp); pa.colors_precomp = gp.colors_precomp;
     pa.opacities = gp.opacities; pa.scales = gp.scales; pa.rotations = gp.rotations;
+    pa.index = gp.index;
     pa.cov3D_precomp = gp.cov3D_precomp; pa.activation = gp.activation;
     pa.view = s->viewmatrix; pa.proj = s->projmatrix; pa.campos = s->campos;
     pa.tanfovx = s->tanfovx; pa.tanfovy = s->tanfovy; pa.fx = g.fx; pa.fy = g.fy;
@@ -604,6 +606,7 @@ int gs_rasterize_backward_ex(const gs_settings* s, const gs_params* gp, int R, c
         ga.P = P; ga.D = s->sh_degree; ga.M = gp->M; ga.W = g.W; ga.H = g.H; ga.gx = g.gx; ga.gy = g.gy;
         ga.means3D = gp->means3D; ga.scales = gp->scales; ga.rotations = gp->rotations;
         ga.cov3D_precomp = gp->cov3D_precomp; ga.opacities = gp->opacities;
+        ga.index = gp->index;
         ga.sh = sh_view(*gp);
         ga.dsh.dc = o->dL_dsh_dc;
         ga.dsh.rest = o->dL_dsh_rest ? o->dL_dsh_rest : o->dL_dsh_dc;

@@ -163,21 +163,22 @@ struct GaussIn {
     uint8_t clamped;
 };
 
-__device__ __forceinline__ GaussIn load_gauss_in(const GaussBwdArgs& a, int idx) {
+// idx: the Gaussian in the render (its clamp bits); src: its parameter row (gs_params.index)
+__device__ __forceinline__ GaussIn load_gauss_in(const GaussBwdArgs& a, int idx, int src) {
     GaussIn g;
-    g.m = ld3(a.means3D + 3 * (size_t)idx);
+    g.m = ld3(a.means3D + 3 * (size_t)src);
     g.scale = mk3(0, 0, 0);
     g.rot = make_float4(0, 0, 0, 0);
 #pragma unroll
     for (int k = 0; k < 6; ++k) g.cov[k] = 0.f;
     if (a.cov3D_precomp) {
 #pragma unroll
-        for (int k = 0; k < 6; ++k) g.cov[k] = a.cov3D_precomp[6 * (size_t)idx + k];
+        for (int k = 0; k < 6; ++k) g.cov[k] = a.cov3D_precomp[6 * (size_t)src + k];
     } else {
-        g.scale = ld3(a.scales + 3 * (size_t)idx);
-        g.rot = *reinterpret_cast<const float4*>(a.rotations + 4 * (size_t)idx);
+        g.scale = ld3(a.scales + 3 * (size_t)src);
+        g.rot = *reinterpret_cast<const float4*>(a.rotations + 4 * (size_t)src);
     }
-    g.opacity = a.activation ? a.opacities[idx] : 0.f;
+    g.opacity = a.activation ? a.opacities[src] : 0.f;
     g.clamped = a.clamped[idx];
     return g;
 }
@@ -333,29 +334,30 @@ __device__ __forceinline__ void apply_grad_mask(const GaussBwdArgs& a, float m, 
 // Writes (or adds, per GS_ACC_* bit) one live Gaussian's per-Gaussian outputs:
 // all loads of the accumulated ones first, then all stores, so the ~20
 // scattered read-modify-writes overlap instead of forming a dependent chain.
-__device__ __forceinline__ void commit_outputs(const GaussBwdArgs& a, int idx, const float (&acc)[9], float dop,
-                                               const float (&ddc)[3], const GaussOut& o) {
+// (means2D and colors are per rendered Gaussian `idx`; the parameter-shaped outputs go to row `src`)
+__device__ __forceinline__ void commit_outputs(const GaussBwdArgs& a, int idx, int src, const float (&acc)[9],
+                                               float dop, const float (&ddc)[3], const GaussOut& o) {
     const uint32_t f = a.acc;
-    const size_t i3 = 3 * (size_t)idx;
-    float* d0 = a.dsh.dc ? a.dsh.dc + (size_t)idx * a.dsh.dc_stride : nullptr;
-    float4* r4 = reinterpret_cast<float4*>(a.dL_drot + 4 * (size_t)idx);
+    const size_t i3 = 3 * (size_t)idx, s3 = 3 * (size_t)src;
+    float* d0 = a.dsh.dc ? a.dsh.dc + (size_t)src * a.dsh.dc_stride : nullptr;
+    float4* r4 = reinterpret_cast<float4*>(a.dL_drot + 4 * (size_t)src);
     float om2[2] = {0.f, 0.f}, oop = 0.f, ocol[3] = {0.f, 0.f, 0.f}, om3[3] = {0.f, 0.f, 0.f};
     float ocov[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, osc[3] = {0.f, 0.f, 0.f}, odc[3] = {0.f, 0.f, 0.f};
     float4 orot = make_float4(0.f, 0.f, 0.f, 0.f);
     if (f & GS_ACC_MEANS2D) { om2[0] = a.dL_dmeans2D[i3]; om2[1] = a.dL_dmeans2D[i3 + 1]; }
-    if (f & GS_ACC_OPACITY) oop = a.dL_dopacity[idx];
+    if (f & GS_ACC_OPACITY) oop = a.dL_dopacity[src];
     if (a.dL_dcolors && (f & GS_ACC_COLORS))
 #pragma unroll
         for (int k = 0; k < 3; ++k) ocol[k] = a.dL_dcolors[i3 + k];
     if (f & GS_ACC_MEANS3D)
 #pragma unroll
-        for (int k = 0; k < 3; ++k) om3[k] = a.dL_dmeans3D[i3 + k];
+        for (int k = 0; k < 3; ++k) om3[k] = a.dL_dmeans3D[s3 + k];
     if (a.dL_dcov3D && (f & GS_ACC_COV3D))
 #pragma unroll
-        for (int k = 0; k < 6; ++k) ocov[k] = a.dL_dcov3D[6 * (size_t)idx + k];
+        for (int k = 0; k < 6; ++k) ocov[k] = a.dL_dcov3D[6 * (size_t)src + k];
     if (f & GS_ACC_SCALES)
 #pragma unroll
-        for (int k = 0; k < 3; ++k) osc[k] = a.dL_dscales[i3 + k];
+        for (int k = 0; k < 3; ++k) osc[k] = a.dL_dscales[s3 + k];
     if (f & GS_ACC_ROTATIONS) orot = *r4;
     if (d0 && (f & GS_ACC_SH))
 #pragma unroll
@@ -364,25 +366,25 @@ __device__ __forceinline__ void commit_outputs(const GaussBwdArgs& a, int idx, c
     a.dL_dmeans2D[i3] = om2[0] + acc[0];
     a.dL_dmeans2D[i3 + 1] = om2[1] + acc[1];
     if (!(f & GS_ACC_MEANS2D)) a.dL_dmeans2D[i3 + 2] = 0.f;
-    a.dL_dopacity[idx] = oop + dop;
+    a.dL_dopacity[src] = oop + dop;
     if (a.dL_dcolors)  // optional (the raw-parameter SH path does not need it)
 #pragma unroll
         for (int k = 0; k < 3; ++k) a.dL_dcolors[i3 + k] = ocol[k] + acc[6 + k];
-    a.dL_dmeans3D[i3] = om3[0] + o.dmean.x;
-    a.dL_dmeans3D[i3 + 1] = om3[1] + o.dmean.y;
-    a.dL_dmeans3D[i3 + 2] = om3[2] + o.dmean.z;
+    a.dL_dmeans3D[s3] = om3[0] + o.dmean.x;
+    a.dL_dmeans3D[s3 + 1] = om3[1] + o.dmean.y;
+    a.dL_dmeans3D[s3 + 2] = om3[2] + o.dmean.z;
     if (a.dL_dcov3D)
 #pragma unroll
-        for (int k = 0; k < 6; ++k) a.dL_dcov3D[6 * (size_t)idx + k] = ocov[k] + o.dcov[k];
+        for (int k = 0; k < 6; ++k) a.dL_dcov3D[6 * (size_t)src + k] = ocov[k] + o.dcov[k];
 #pragma unroll
-    for (int k = 0; k < 3; ++k) a.dL_dscales[i3 + k] = osc[k] + o.dscale[k];
+    for (int k = 0; k < 3; ++k) a.dL_dscales[s3 + k] = osc[k] + o.dscale[k];
     *r4 = make_float4(orot.x + o.drot.x, orot.y + o.drot.y, orot.z + o.drot.z, orot.w + o.drot.w);
     if (d0) {
 #pragma unroll
         for (int k = 0; k < 3; ++k) d0[k] = odc[k] + ddc[k];
         // coefficients beyond the 16 a degree-3 evaluation uses get zero gradient
         if (!(f & GS_ACC_SH)) {
-            float* dr = a.dsh.rest + (size_t)idx * a.dsh.rest_stride;
+            float* dr = a.dsh.rest + (size_t)src * a.dsh.rest_stride;
             for (int k = kShPitch; k < (a.M - 1) * 3; ++k) dr[k] = 0.f;
         }
     }
@@ -417,33 +419,38 @@ __global__ __launch_bounds__(kGB) void k_gauss_live(GaussBwdArgs a) {
     if (live) a.live_list[idx0 + off + (uint32_t)__popcll(bm & lanemask_lt())] = (uint32_t)idx;
     if (threadIdx.x == 0) a.live_count[blockIdx.x] = total;
 
-    // zeros for the overwritten outputs of the dead Gaussians
+    // zeros for the overwritten outputs of the dead Gaussians (parameter-shaped ones at row src)
     const uint32_t acc = a.acc;
+    const int src = in && a.index ? a.index[idx] : idx;
     if (in && !live) {
         if (!(acc & GS_ACC_MEANS2D))
 #pragma unroll
             for (int k = 0; k < 3; ++k) a.dL_dmeans2D[3 * (size_t)idx + k] = 0.f;
-        if (!(acc & GS_ACC_OPACITY)) a.dL_dopacity[idx] = 0.f;
+        if (!(acc & GS_ACC_OPACITY)) a.dL_dopacity[src] = 0.f;
         if (a.dL_dcolors && !(acc & GS_ACC_COLORS))
 #pragma unroll
             for (int k = 0; k < 3; ++k) a.dL_dcolors[3 * (size_t)idx + k] = 0.f;
         if (!(acc & GS_ACC_MEANS3D))
 #pragma unroll
-            for (int k = 0; k < 3; ++k) a.dL_dmeans3D[3 * (size_t)idx + k] = 0.f;
+            for (int k = 0; k < 3; ++k) a.dL_dmeans3D[3 * (size_t)src + k] = 0.f;
         if (a.dL_dcov3D && !(acc & GS_ACC_COV3D))
 #pragma unroll
-            for (int k = 0; k < 6; ++k) a.dL_dcov3D[6 * (size_t)idx + k] = 0.f;
+            for (int k = 0; k < 6; ++k) a.dL_dcov3D[6 * (size_t)src + k] = 0.f;
         if (!(acc & GS_ACC_SCALES))
 #pragma unroll
-            for (int k = 0; k < 3; ++k) a.dL_dscales[3 * (size_t)idx + k] = 0.f;
+            for (int k = 0; k < 3; ++k) a.dL_dscales[3 * (size_t)src + k] = 0.f;
         if (!(acc & GS_ACC_ROTATIONS))
-            *reinterpret_cast<float4*>(a.dL_drot + 4 * (size_t)idx) = make_float4(0.f, 0.f, 0.f, 0.f);
+            *reinterpret_cast<float4*>(a.dL_drot + 4 * (size_t)src) = make_float4(0.f, 0.f, 0.f, 0.f);
         if (a.dsh.dc && !(acc & GS_ACC_SH)) {
-            float* d0 = a.dsh.dc + (size_t)idx * a.dsh.dc_stride;
+            float* d0 = a.dsh.dc + (size_t)src * a.dsh.dc_stride;
             d0[0] = 0.f; d0[1] = 0.f; d0[2] = 0.f;
+            if (a.index && a.M > 1) {  // (scattered rows: per thread)
+                float* dr = a.dsh.rest + (size_t)src * a.dsh.rest_stride;
+                for (int k = 0; k < (a.M - 1) * 3; ++k) dr[k] = 0.f;
+            }
         }
     }
-    if (a.dsh.dc && !(acc & GS_ACC_SH) && a.M > 1) {
+    if (a.dsh.dc && !(acc & GS_ACC_SH) && a.M > 1 && !a.index) {
         // rest rows of the block's dead Gaussians, coalesced over the block's region
         __syncthreads();  // s_live
         const int ncol = (a.M - 1) * 3;
@@ -499,12 +506,13 @@ __global__ __launch_bounds__(kGB) void k_gauss_bwd_live(GaussBwdArgs a) {
 #pragma unroll
         for (int q = 1; q < kLiveGroup; ++q) g += j >= s_pre[q] ? 1 : 0;
         const int idx = ok ? (int)a.live_list[(size_t)(sb0 + g) * kGB + (j - s_pre[g])] : 0;
-        s_gid[threadIdx.x] = (uint32_t)idx;
-        // independent loads first: parameters, the first 8 record flags
+        // independent loads first: parameters, slot range, the first 8 record flags
         GaussIn gin{};
-        if (ok) gin = load_gauss_in(a, idx);
+        const int src = ok && a.index ? a.index[idx] : idx;  // parameter row
+        s_gid[threadIdx.x] = (uint32_t)src;  // (SH rows are parameter rows)
+        if (ok) gin = load_gauss_in(a, idx, src);
         const uint32_t n = ok ? a.tiles_touched[idx] : 0u;
-        const uint32_t first = n ? a.first_slot[idx] : 0u;
+        const uint32_t first = ok ? a.first_slot[idx] : 0u;  // (a live Gaussian has slots)
         const uint32_t* flags = reinterpret_cast<const uint32_t*>(a.rec_flags);
         uint32_t fl[8];
 #pragma unroll
@@ -562,12 +570,12 @@ __global__ __launch_bounds__(kGB) void k_gauss_bwd_live(GaussBwdArgs a) {
         float dop = acc[5];  // w.r.t. opacity; chained through the sigmoid when activation = 1
         GaussOut o;
         if (ok) {
-            const float gm = a.grad_mask ? (a.grad_mask[idx] ? 1.f : 0.f) : 1.f;
+            const float gm = a.grad_mask ? (a.grad_mask[src] ? 1.f : 0.f) : 1.f;
             // (each thread reads and then overwrites only its own LDS row: no barrier in between)
             gauss_bwd_visible(a, gin, acc, dop, my_sh, ncol, (a.mask_bits & GS_ACC_SH) ? gm : 1.f, ddc, o);
             if (a.grad_mask) apply_grad_mask(a, gm, acc, dop, o);
         }
-        if (ok) commit_outputs(a, idx, acc, dop, ddc, o);
+        if (ok) commit_outputs(a, idx, src, acc, dop, ddc, o);
         // dL_dsh rest rows: through LDS (in place), flat block-wide batches, loads before stores
         if (a.dsh.dc && ncol > 0) {
             __syncthreads();

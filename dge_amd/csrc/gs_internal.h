@@ -198,6 +198,7 @@ struct ShGradView {
 struct PreprocessArgs {
     int P, D, M, W, H, gx, gy;
     const float *means3D, *colors_precomp, *opacities, *scales, *rotations, *cov3D_precomp;
+    const int* index;  // gs_params.index: parameter row of Gaussian i (NULL: i)
     ShView sh;         // sh.dc == nullptr: no SH
     int activation;    // 1: opacities/scales/rotations are raw GaussianModel parameters
     const float *view, *proj, *campos;
@@ -318,6 +319,7 @@ void launch_render_backward(const RenderBwdArgs& a, hipStream_t s);
 struct GaussBwdArgs {
     int P, D, M, W, H, gx, gy;
     const float *means3D, *scales, *rotations, *cov3D_precomp, *opacities;
+    const int* index;  // gs_params.index: parameter row (inputs and parameter-shaped gradients)
     ShView sh;
     ShGradView dsh;    // dsh.dc == nullptr: no SH gradient output
     int activation;    // 1: chain the gradients through sigmoid / exp / normalize

@@ -95,6 +95,13 @@ __global__ __launch_bounds__(256) void k_preprocess(PreprocessArgs a) {
     const int nrow = a.P - idx0 < 256 ? a.P - idx0 : 256;
     const int ncolA = ncol < kShA ? ncol : kShA, ncolB = ncol - ncolA;
     float shB[kShBPer];
+    // parameter rows of the block's Gaussians (gs_params.index: the localize subset, gathered here)
+    __shared__ int s_src[256];
+    if (a.index) {
+        s_src[threadIdx.x] = (int)threadIdx.x < nrow ? a.index[idx0 + threadIdx.x] : 0;
+        __syncthreads();
+    }
+    const int src = a.index ? s_src[threadIdx.x] : idx;
     if (stage_sh && !kSplit) {
         sh_rows_load<256>(a.sh.rest + (size_t)idx0 * a.sh.rest_stride, a.sh.rest_stride, s_sh, nrow, ncol);
     } else if (stage_sh) {
@@ -102,21 +109,23 @@ __global__ __launch_bounds__(256) void k_preprocess(PreprocessArgs a) {
         // half is stored to LDS as it arrives, the second stays in registers
         const int stride = a.sh.rest_stride;
         const float invA = 1.0f / (float)ncolA, invB = ncolB > 0 ? 1.0f / (float)ncolB : 0.f;
-        const float* baseF = a.sh.rest + (size_t)idx0 * stride;
-        const __half* baseH = reinterpret_cast<const __half*>(a.sh.rest) + (size_t)idx0 * stride;
+        const int rbase = a.index ? 0 : idx0;  // rows: s_src[row] (gathered) or idx0 + row
+        const float* baseF = a.sh.rest + (size_t)rbase * stride;
+        const __half* baseH = reinterpret_cast<const __half*>(a.sh.rest) + (size_t)rbase * stride;
         auto ld = [&](uint32_t off) { return a.sh.half ? __half2float(baseH[off]) : baseF[off]; };
+        auto srow = [&](int row) { return a.index ? s_src[row] : row; };
         float shA[kShA];
 #pragma unroll
         for (int i = 0; i < kShA; ++i) {
             const int f = threadIdx.x + 256 * i;
             const int row = (int)(((float)f + 0.5f) * invA), col = f - row * ncolA;
-            shA[i] = row < nrow ? ld((uint32_t)(row * stride + col)) : 0.f;
+            shA[i] = row < nrow ? ld((uint32_t)(srow(row) * stride + col)) : 0.f;
         }
 #pragma unroll
         for (int i = 0; i < kShBPer; ++i) {
             const int f = threadIdx.x + 256 * i;
             const int row = (int)(((float)f + 0.5f) * invB), col = f - row * ncolB;
-            shB[i] = ncolB > 0 && row < nrow ? ld((uint32_t)(row * stride + kShA + col)) : 0.f;
+            shB[i] = ncolB > 0 && row < nrow ? ld((uint32_t)(srow(row) * stride + kShA + col)) : 0.f;
         }
 #pragma unroll
         for (int i = 0; i < kShA; ++i) {
@@ -130,18 +139,18 @@ __global__ __launch_bounds__(256) void k_preprocess(PreprocessArgs a) {
         const float* pm = a.proj;
         // every per-Gaussian input is loaded up front, culled or not (one memory round trip
         // instead of xyz -> frustum test -> scale/rotation -> opacity)
-        p = ld3(a.means3D + 3 * (size_t)idx);
+        p = ld3(a.means3D + 3 * (size_t)src);
         float cov3[6];
         float4 q = make_float4(0.f, 0.f, 0.f, 0.f);
         f3 sc = mk3(0.f, 0.f, 0.f);
         if (a.cov3D_precomp) {
 #pragma unroll
-            for (int k = 0; k < 6; ++k) cov3[k] = a.cov3D_precomp[6 * (size_t)idx + k];
+            for (int k = 0; k < 6; ++k) cov3[k] = a.cov3D_precomp[6 * (size_t)src + k];
         } else {
-            q = *reinterpret_cast<const float4*>(a.rotations + 4 * (size_t)idx);
-            sc = ld3(a.scales + 3 * (size_t)idx);
+            q = *reinterpret_cast<const float4*>(a.rotations + 4 * (size_t)src);
+            sc = ld3(a.scales + 3 * (size_t)src);
         }
-        const float op_in = a.opacities[idx];
+        const float op_in = a.opacities[src];
         // in_frustum (auxiliary.h:139-164): only the near test is live
         const float4 ph = proj_point(pm, p);
         const float pw = 1.0f / (ph.w + 0.0000001f);
@@ -192,7 +201,7 @@ __global__ __launch_bounds__(256) void k_preprocess(PreprocessArgs a) {
     if (touched && a.copy_colors && a.colors_precomp) rgb = ld3(a.colors_precomp + 3 * (size_t)idx);
     if (sh_color) {
         dir = sh_dir(p, ld3(a.campos));
-        head = sh_rgb_head(a.D, dir, sh_dc3(a.sh.dc, a.sh.half, (size_t)idx * a.sh.dc_stride),
+        head = sh_rgb_head(a.D, dir, sh_dc3(a.sh.dc, a.sh.half, (size_t)src * a.sh.dc_stride),
                            s_sh + threadIdx.x * kPitch);
     }
     if (kSplit && stage_sh && ncolB > 0) {
@@ -240,7 +249,7 @@ __global__ __launch_bounds__(256) void k_preprocess(PreprocessArgs a) {
 
 void launch_preprocess(const PreprocessArgs& a, hipStream_t s) {
     if (a.P <= 0) return;
-    if (a.sh.half)
+    if (a.sh.half || a.index)  // (the one-pass staging needs the block's rows contiguous)
         hipLaunchKernelGGL(k_preprocess<true>, dim3(div_up(a.P, 256)), dim3(256), 0, s, a);
     else
         hipLaunchKernelGGL(k_preprocess<false>, dim3(div_up(a.P, 256)), dim3(256), 0, s, a);

@@ -87,14 +87,16 @@ class _RasterizeGaussiansFused(torch.autograd.Function):
     the getters would produce), without the getters' separate torch kernels."""
 
     @staticmethod
-    def forward(ctx, xyz, means2D, f_dc, f_rest, colors, raw_opacity, raw_scaling, raw_rotation, raster_settings):
+    def forward(ctx, xyz, means2D, f_dc, f_rest, colors, raw_opacity, raw_scaling, raw_rotation, raster_settings,
+                index=None):
         rs = raster_settings
         args = (rs.bg, xyz, f_dc, f_rest, colors, raw_opacity, raw_scaling, raw_rotation, rs.scale_modifier,
                 rs.viewmatrix, rs.projmatrix, rs.tanfovx, rs.tanfovy, rs.image_height, rs.image_width, rs.sh_degree,
                 rs.campos, rs.prefiltered, rs.debug)
         num_rendered, color, depth, radii, geomBuffer, binningBuffer, imgBuffer = _call_with_snapshot(
-            _C.rasterize_gaussians_fused, args, rs.debug, "snapshot_fw.dump", "forward")
+            lambda *a: _C.rasterize_gaussians_fused(*a, index=index), args, rs.debug, "snapshot_fw.dump", "forward")
         ctx.raster_settings = rs
+        ctx.index = index
         ctx.num_rendered = num_rendered
         ctx.has_sh = f_dc is not None and f_dc.numel() != 0
         ctx.save_for_backward(xyz, f_dc, f_rest, colors, raw_opacity, raw_scaling, raw_rotation, radii, geomBuffer,
@@ -122,15 +124,16 @@ class _RasterizeGaussiansFused(torch.autograd.Function):
                                ("rotation", raw_rotation, 7)):
                 mode, owner = _accumulation_mode(p, node(i))
                 if mode is not None:
-                    into[name] = _into_target(p, mode, direct)
+                    into[name] = _into_target(p, mode, direct, ctx.index is not None)
                     if owner is not None:
                         masked.add(name)
                         owners.add(owner)
             if ctx.has_sh:
                 (m_dc, o_dc), (m_rest, o_rest) = _accumulation_mode(f_dc, node(2)), _accumulation_mode(f_rest, node(3))
                 if m_dc is not None and m_dc == m_rest and o_dc is o_rest:
-                    into["sh"] = ((_into_target(f_dc, m_dc, direct)[0], _into_target(f_rest, m_rest, direct)[0]),
-                                  m_dc == "add")
+                    zi = ctx.index is not None
+                    into["sh"] = ((_into_target(f_dc, m_dc, direct, zi)[0],
+                                   _into_target(f_rest, m_rest, direct, zi)[0]), m_dc == "add")
                     if o_dc is not None:
                         masked.add("sh")
                         owners.add(o_dc)
@@ -157,8 +160,8 @@ class _RasterizeGaussiansFused(torch.autograd.Function):
         ordered = bool(into) and _SIDE_STREAMS
         stream = _order_grad_writes_begin(xyz.device) if ordered else None
         d_m2, d_xyz, d_dc, d_rest, d_col, d_op, d_sc, d_rot = _call_with_snapshot(
-            lambda *a: _C.rasterize_gaussians_fused_backward(*a, into=into), args, rs.debug, "snapshot_bw.dump",
-            "backward")
+            lambda *a: _C.rasterize_gaussians_fused_backward(*a, into=into, index=ctx.index), args, rs.debug,
+            "snapshot_bw.dump", "backward")
         if ordered:
             _order_grad_writes_end(xyz.device, stream, [t for _, t in direct])
         for p, t in direct:  # parameters whose .grad was None: the kernel wrote it, hand it over
@@ -177,7 +180,7 @@ class _RasterizeGaussiansFused(torch.autograd.Function):
             d_rot = None
         if "sh" in into:
             d_dc = d_rest = None
-        return d_xyz, d_m2, d_dc, d_rest, d_col, d_op, d_sc, d_rot, None
+        return d_xyz, d_m2, d_dc, d_rest, d_col, d_op, d_sc, d_rot, None, None
 
 
 _FUSED_GRAD_ACCUM = os.environ.get("DGE_AMD_FUSED_GRAD_ACCUM", "1") != "0"
@@ -241,7 +244,8 @@ def _accumulation_mode(p, node=None):
     callers, which capture instead, still get returned gradients), p has no post-accumulate hooks and
     no tensor hooks other than a GaussianModel's grad mask (applied in-kernel), and an existing .grad is
     a plain contiguous fp32 buffer of p's shape."""
-    if not isinstance(p, torch.Tensor) or not p.requires_grad or p.grad_fn is not None or p.numel() == 0:
+    if (not isinstance(p, torch.Tensor) or not p.requires_grad or p.grad_fn is not None or p.numel() == 0
+            or p.dtype != torch.float32):  # (the kernels write fp32 gradients)
         return None, None
     ok, owner = _mask_owner(p)
     if not ok or getattr(p, "_post_accumulate_grad_hooks", None):
@@ -265,22 +269,26 @@ def _accumulation_mode(p, node=None):
     return None, None
 
 
-def _into_target(p, mode, direct):
+def _into_target(p, mode, direct, zero=False):
+    """zero: the kernel writes only some rows (the index path), so a fresh .grad starts at zero."""
     if mode == "add":
         return (p.grad, True)
-    t = torch.empty_like(p, memory_format=torch.contiguous_format)
+    t = (torch.zeros_like if zero else torch.empty_like)(p, memory_format=torch.contiguous_format)
     direct.append((p, t))
     return (t, False)
 
 
 def rasterize_gaussian_model(xyz, means2D, features_dc, features_rest, colors_precomp, raw_opacity, raw_scaling,
-                             raw_rotation, raster_settings):
+                             raw_rotation, raster_settings, index=None):
     """(color, radii, depth) of a GaussianModel given its raw tensors (_xyz, _features_dc, _features_rest or
-    colors_precomp, _opacity, _scaling, _rotation); activations are applied in-kernel."""
+    colors_precomp, _opacity, _scaling, _rotation); activations are applied in-kernel.  `index` (int32,
+    ascending): render only those rows — the model's `localize` subset pc[mask] — gathering them
+    in-kernel; the gradients land in the full-size tensors' rows (means2D/radii are per subset entry)."""
     empty = torch.empty(0, dtype=torch.float32, device=xyz.device)
     return _RasterizeGaussiansFused.apply(
         xyz, means2D, empty if features_dc is None else features_dc, empty if features_rest is None else features_rest,
-        empty if colors_precomp is None else colors_precomp, raw_opacity, raw_scaling, raw_rotation, raster_settings)
+        empty if colors_precomp is None else colors_precomp, raw_opacity, raw_scaling, raw_rotation, raster_settings,
+        index)
 
 
 class GaussianRasterizationSettings(NamedTuple):

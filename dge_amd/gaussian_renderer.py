@@ -13,6 +13,7 @@ from __future__ import annotations
 
 import math
 import os
+import weakref
 
 import torch
 import torch.nn.functional as F
@@ -44,11 +45,12 @@ def camera2rasterizer(viewpoint_camera, bg_color: torch.Tensor, sh_degree: int =
 
 def _fused_ok(pc, pipe) -> bool:
     """The raw-parameter path applies when the model is a standard GaussianModel
-    (activations exp / sigmoid / F.normalize, no `localize` subset) and the
+    (activations exp / sigmoid / F.normalize; fp32 parameters, features fp32 or
+    fp16; a `localize` subset given by a boolean mask over the rows) and the
     pipeline asks for the in-kernel SH and covariance (the defaults)."""
     if os.environ.get("DGE_AMD_FUSED", "1") == "0":
         return False
-    if pipe.compute_cov3D_python or pipe.convert_SHs_python or getattr(pc, "localize", False):
+    if pipe.compute_cov3D_python or pipe.convert_SHs_python:
         return False
     need = ("_xyz", "_features_dc", "_features_rest", "_opacity", "_scaling", "_rotation")
     if not all(isinstance(getattr(pc, n, None), torch.Tensor) for n in need):
@@ -57,7 +59,30 @@ def _fused_ok(pc, pipe) -> bool:
                      ("rotation_activation", F.normalize)):
         if getattr(pc, attr, fn) is not fn:
             return False
-    return all(getattr(pc, n).dtype == torch.float32 and getattr(pc, n).is_cuda for n in need)
+    if getattr(pc, "localize", False):
+        m = getattr(pc, "mask", None)
+        if not (isinstance(m, torch.Tensor) and m.dtype == torch.bool and m.shape == (pc._xyz.shape[0],)
+                and m.device == pc._xyz.device):
+            return False
+    feats = (pc._features_dc.dtype, pc._features_rest.dtype)
+    if feats not in ((torch.float32, torch.float32), (torch.float16, torch.float16)):
+        return False
+    return all(getattr(pc, n).is_cuda for n in need) and all(
+        getattr(pc, n).dtype == torch.float32 for n in ("_xyz", "_opacity", "_scaling", "_rotation"))
+
+
+_MASK_INDEX = {}  # id(mask) -> (weakref(mask), version, int32 rows)
+
+
+def _mask_rows(mask):
+    """Ascending int32 rows of a boolean mask (the order of pc[mask]); one host sync per mask change."""
+    key = id(mask)
+    ent = _MASK_INDEX.get(key)
+    if ent is not None and ent[0]() is mask and ent[1] == mask._version:
+        return ent[2]
+    rows = torch.nonzero(mask.detach()).squeeze(1).to(torch.int32)
+    _MASK_INDEX[key] = (weakref.ref(mask, lambda _r, k=key: _MASK_INDEX.pop(k, None)), mask._version, rows)
+    return rows
 
 
 def render(viewpoint_camera, pc, pipe, bg_color: torch.Tensor, scaling_modifier=1.0, override_color=None):
@@ -114,7 +139,9 @@ def _render_fused(viewpoint_camera, pc, pipe, bg_color, scaling_modifier=1.0, ov
     the rasterizer consumes _xyz, _features_dc, _features_rest, _opacity,
     _scaling, _rotation directly and returns their gradients."""
     xyz = pc._xyz
-    screenspace_points = torch.zeros_like(xyz, dtype=xyz.dtype, requires_grad=True, device=xyz.device)
+    index = _mask_rows(pc.mask) if getattr(pc, "localize", False) else None
+    n = index.numel() if index is not None else xyz.shape[0]
+    screenspace_points = torch.zeros((n, 3), dtype=xyz.dtype, requires_grad=True, device=xyz.device)
     try:
         screenspace_points.retain_grad()
     except Exception:
@@ -125,7 +152,7 @@ def _render_fused(viewpoint_camera, pc, pipe, bg_color, scaling_modifier=1.0, ov
     else:
         f_dc, f_rest, colors = None, None, override_color.float()
     rendered_image, radii, depth = rasterize_gaussian_model(xyz, screenspace_points, f_dc, f_rest, colors,
-                                                            pc._opacity, pc._scaling, pc._rotation, rs)
+                                                            pc._opacity, pc._scaling, pc._rotation, rs, index)
     return {
         "render": rendered_image,
         "viewspace_points": screenspace_points,

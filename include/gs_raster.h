@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define GS_RASTER_ABI_VERSION 3
+#define GS_RASTER_ABI_VERSION 4
 
 #define GS_OK 0
 #define GS_ERR_INVALID_ARG 1   /* AT_ERROR / std::runtime_error in the reference */
@@ -126,6 +126,12 @@ typedef struct gs_params {
     int sh_half;                  /* 1: sh_dc / sh_rest hold IEEE fp16 values (strides in elements),
                                      upcast in-kernel (the local-edit path's fp16 SH storage);
                                      the SH gradients stay fp32 */
+    const int *index;             /* NULL, or [P] ascending rows: Gaussian i of the render is row
+                                     index[i] of means3D/sh/opacities/scales/rotations/cov3D_precomp
+                                     (the GaussianModel's `localize` subset pc[mask], gathered
+                                     in-kernel).  The backward then writes the parameter-shaped
+                                     gradients (means3D, sh, opacity, scales, rotations, cov3D) at
+                                     those rows only; means2D / colors / radii stay [P]. */
 } gs_params;
 
 /* gs_grads.accumulate bits: output i is ADDED to (out += grad) instead of
@@ -154,7 +160,8 @@ typedef struct gs_grads {         /* backward outputs, every element written */
     unsigned int accumulate;      /* GS_ACC_* bits; 0: overwrite every output (reference behaviour) */
     /* Optional per-Gaussian gradient mask (the GaussianModel's grad-mask hooks,
      * gaussian_model.py:837-856: grad * mask[:, None]): outputs whose GS_ACC_*
-     * bit is set in mask_bits are multiplied by grad_mask[i] (0/1); NULL: none. */
+     * bit is set in mask_bits are multiplied by grad_mask[i] (0/1; grad_mask[index[i]] with
+     * gs_params.index); NULL: none. */
     const uint8_t *grad_mask;     /* [P] */
     unsigned int mask_bits;
 } gs_grads;

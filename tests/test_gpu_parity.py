@@ -410,3 +410,49 @@ def test_c5_local_edit_fp16_sh_vs_oracle(cuda_device, oracle):
     got = torch.cat([gd, sc._features_rest.grad], dim=1).float().cpu().numpy()
     assert_close(got, full.astype(np.float16).astype(np.float32), "dL_dsh (fp16)", rtol=2e-3, allow_frac=1e-4)
     assert np.all(got[~m.numpy()] == 0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("half", [False, True], ids=["fp32_sh", "fp16_sh"])
+@pytest.mark.parametrize("preexisting_grads", [False, True], ids=["fresh_grads", "accumulate"])
+def test_fused_localize_index_path_matches_getter_path(cuda_device, monkeypatch, half, preexisting_grads):
+    """`localize` on a boolean mask (the local-edit render, c5): the fused path gathers the subset's rows
+    in-kernel (gs_params.index) and scatters the gradients into the full tensors' rows; image, radii,
+    screen-space and full-size raw-parameter gradients equal the getter path's (t[mask] gathers +
+    autograd scatter), rows outside the mask untouched."""
+    from dge_amd.cameras import orbit_camera
+    from dge_amd.gaussian_renderer import PipelineParams, _fused_ok, render
+    from dge_amd.scene import synthetic_scene
+
+    dev = torch.device("cuda")
+    cam = orbit_camera(1, 5, 200, 136, device=dev)
+    G = torch.randn(3, 136, 200, generator=torch.Generator().manual_seed(12)).to(dev)
+    outs = []
+    for fused in (True, False):
+        monkeypatch.setenv("DGE_AMD_FUSED", "1" if fused else "0")
+        sc = synthetic_scene(30_000, seed=23, radius=1.5, scale=0.03, device=dev)
+        if half:
+            sc._features_dc = sc._features_dc.half()
+            sc._features_rest = sc._features_rest.half()
+        sc.requires_grad_(True)
+        mask = torch.zeros(30_000, dtype=torch.bool, device=dev)
+        mask[torch.argsort(sc._xyz[:, 0])[:9_000]] = True
+        sc.mask, sc.localize = mask, True
+        if preexisting_grads:
+            for p in sc.parameters():
+                p.grad = torch.full_like(p, 0.5)
+        assert _fused_ok(sc, PipelineParams()) == fused
+        pkg = render(cam, sc, PipelineParams(), torch.tensor([0.1, 0.0, 0.2], device=dev))
+        (pkg["render"] * G).sum().backward()
+        grads = [p.grad.float().cpu().numpy() for p in sc.parameters()]
+        outs.append((pkg["render"].detach().cpu().numpy(), pkg["radii"].cpu().numpy(),
+                     pkg["viewspace_points"].grad.cpu().numpy(), grads, mask.cpu().numpy()))
+    (img_f, r_f, vs_f, g_f, m), (img_r, r_r, vs_r, g_r, _) = outs
+    assert r_f.shape == (9_000,)
+    np.testing.assert_array_equal(r_f, r_r)
+    assert_close(img_f, img_r, "image", 1e-5)
+    assert_close(vs_f, vs_r, "viewspace grad", 1e-4)
+    for name, a, b in zip(["_xyz", "_features_dc", "_features_rest", "_opacity", "_scaling", "_rotation"], g_f, g_r):
+        # (fp16 feature grads are rounded to fp16 by autograd on both paths)
+        assert_close(a, b, name, 2e-3 if half and "features" in name else 1e-4)
+        np.testing.assert_array_equal(a[~m], 0.5 if preexisting_grads else 0.0, err_msg=name)
