@@ -24,7 +24,7 @@ def main(root):
     for f in glob.glob(os.path.join(root, "p*", "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
             name = r.get("Kernel_Name", r.get("Kernel-Name", ""))
-            short = name.split("(")[0].split("::")[-1].strip()
+            short = name.split("(")[0].split("::")[-1].split("<")[0].strip()  # (template arguments dropped)
             # one row per (dispatch, counter)
             vals[short][r["Counter_Name"]].append(float(r["Counter_Value"]))
     out = {}
