@@ -217,7 +217,7 @@ __global__ __launch_bounds__(256) void k_preprocess(PreprocessArgs a) {
     }
     if (sh_color) rgb = sh_rgb_tail(a.D, dir, head, s_sh + threadIdx.x * kPitch + (kSplit ? 0 : kShA), clamp_bits);
     if (idx < a.P) {
-        if (touched) {
+        if (touched) {  // (whole 64-B records: writing only the used 40 B measured slower — partial lines)
             Splat sp;
             sp.xy = pix;
             sp.pad0 = make_float2(0.f, 0.f);
@@ -226,7 +226,9 @@ __global__ __launch_bounds__(256) void k_preprocess(PreprocessArgs a) {
             sp.pad1 = make_float4(0.f, 0.f, 0.f, 0.f);
             a.splat[idx] = sp;
         }
-        a.radii[idx] = radius_out;
+        // the geometry buffer's radii feed only the emission of grids too large to pack a rect
+        // (and layout queries); the caller's radii serve everything else
+        if (!a.rect_packed || !a.radii_out) a.radii[idx] = radius_out;
         if (a.radii_out) a.radii_out[idx] = radius_out;
         a.tiles_touched[idx] = touched;
         a.clamped[idx] = clamp_bits;

@@ -212,9 +212,11 @@ size_t gs_image_buffer_size(int width, int height);
 size_t gs_binning_buffer_size(int num_rendered, int num_tiles);
 
 /* Offsets (bytes) of the per-Gaussian arrays inside the geometry buffer, for
- * field-by-field parity tests.  Names: "means2D" (float2), "conic_opacity"
- * (float4), "rgbd" (float4 = r,g,b,depth), "tiles_touched" (u32),
- * "clamped" (u8, bit c = channel c clamped), "radii" (int32).
+ * field-by-field parity tests.  Names: "splat" (64-B records: "means2D" float2
+ * at +0, "conic_opacity" float4 at +16, "rgbd" float4 = r,g,b,depth at +32),
+ * "tiles_touched" (u32), "clamped" (u8, bit c = channel c clamped), "radii"
+ * (int32; a copy of the caller's radii, kept only when the caller passes none
+ * or the tile grid exceeds 255 x 255).
  * Image buffer: "final_T" (float), "n_contrib" (u32), "ranges" (uint2 per tile).
  * Binning buffer: "point_list" (u32 per instance).  Returns -1 if unknown. */
 long long gs_buffer_offset(const char *buffer, const char *field, int P, int width, int height,
