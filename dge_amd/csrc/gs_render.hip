@@ -549,6 +549,11 @@ __global__ __launch_bounds__(64, 4) void k_render_bwd(RenderBwdArgs a) {
         s_op[kRound + kBwdGroup];
     __shared__ float4 s_rgb[kRound + kBwdGroup];
     __shared__ uint32_t s_pos[kRound + kBwdGroup];
+    // (Gaussian, slot) of the next round's entries by round position, stashed when their gathers are
+    // issued, then of the kept entries by compacted slot: the record writes read them from LDS
+    // instead of re-loading point_pairs (a dependent global round trip per group of four)
+    __shared__ uint2 s_stash[kRound];
+    __shared__ uint2 s_pair[kRound + kBwdGroup];
     const int lane = threadIdx.x;
     // block -> work item (quadrant, segment) of the forward's list: multi-segment windows first;
     // blocks past the list's end exit (they dispatch after every real item).  (A persistent-wave
@@ -640,6 +645,7 @@ __global__ __launch_bounds__(64, 4) void k_render_bwd(RenderBwdArgs a) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {  // (dropped entries gather Gaussian 0: one shared line)
         cur[i] = gather_entry(a.splat, (kb_cur >> i) & 1u ? pairs[i].x : 0u);
+        s_stash[64 * i + lane] = pairs[i];
     }
     round_pairs(1, pairs, ubits);
 
@@ -663,6 +669,7 @@ __global__ __launch_bounds__(64, 4) void k_render_bwd(RenderBwdArgs a) {
                 s_op[slot] = cur[i].co.w;
                 s_rgb[slot] = cur[i].f;
                 s_pos[slot] = (uint32_t)(lo + j);
+                s_pair[slot] = s_stash[j];
             }
             nk += __popcll(km);
         }
@@ -681,6 +688,7 @@ __global__ __launch_bounds__(64, 4) void k_render_bwd(RenderBwdArgs a) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             cur[i] = gather_entry(a.splat, (kb_cur >> i) & 1u ? pairs[i].x : 0u);
+            s_stash[64 * i + lane] = pairs[i];  // (after this round's compaction read its stash)
         }
         round_pairs(r + 2, pairs, ubits);
         diag_kept += nk;
@@ -702,7 +710,7 @@ __global__ __launch_bounds__(64, 4) void k_render_bwd(RenderBwdArgs a) {
             for (int f = 0; f < 9; ++f) S[f] = quad_reduce(g[0][f], g[1][f], g[2][f], g[3][f]);
             const int kw = k + row_entry;
             if (row_writer && kw < nk) {
-                const uint2 pr = a.point_pairs[range.x + s_pos[kw]];  // (an L2 hit: this round's pairs)
+                const uint2 pr = s_pair[kw];
                 const size_t rec = 4 * (size_t)pr.y + quad;
                 finish_record(make_float4(s_cx[kw], s_cy[kw], s_cz[kw], s_op[kw]), S, ddelx_dx, ddely_dy,
                               a.records + 3 * rec);
