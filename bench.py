@@ -8,7 +8,8 @@ A step = every rank renders its `--views-per-rank` views, forward + backward
 each (the gradients of the reference's batch step — threestudio/systems/DGE.py
 renders the batch's views and back-propagates the summed loss — up to float
 summation order), accumulated into the shared parameters, and, for N > 1, ONE
-all-reduce of the flat parameter-gradient bucket (RCCL).  `--streams N`
+all-reduce of the flat parameter-gradient bucket (RCCL) — of the rows nonzero
+on some rank only (GradBucket.allreduce: ~24% of the 236 MB for 24 views).  `--streams N`
 alternates the views over N HIP streams (dge_amd.multiview.render_backward_views:
 one view's backward overlapping the next view's forward; default 1) and
 `--batch-backward` runs all forwards first, then one backward, as the
@@ -251,7 +252,9 @@ def main():
             "data": "synthetic",
             "config": {"workload": f"c2: {P / 1e6:.2f}M Gaussians (SH deg {args.sh_degree}), {W}x{H}, fp32 fwd+bwd",
                        "gaussians": P, "width": W, "height": H, "views_per_rank": V, "streams": args.streams,
-                       "parallelism": f"views sharded x{world}" + (", RCCL grad all-reduce" if world > 1 else "")},
+                       "parallelism": f"views sharded x{world}" + (
+                           f", {os.environ.get('DGE_AMD_BENCH_BACKEND', 'nccl').replace('nccl', 'RCCL')} "
+                           "sparse-row grad all-reduce" if world > 1 else "")},
             "num_rendered_mean": int(K),
             "live_gaussians_mean": int(np.mean([d["live"] for d in lives])),
             "gradient_records_mean": int(np.mean([d["records"] for d in lives])),

@@ -60,7 +60,14 @@ class GradBucket:
     def check_attached(self) -> bool:
         return all(p.grad is not None and p.grad.data_ptr() == v.data_ptr() for p, v in zip(self.params, self.views))
 
-    def allreduce(self, group=None, async_op: bool = False):
+    def allreduce(self, group=None, async_op: bool = False, sparse: bool = True):
+        """SUM of the bucket over the ranks.  sparse (when every parameter has the same number of rows,
+        as a GaussianModel's do): only rows that are nonzero on some rank travel — the union of the
+        ranks' nonzero rows is agreed with one MAX all-reduce of a byte per row, those rows are packed,
+        all-reduced and copied back.  A Gaussian behind saturated pixels in every view of every rank
+        gets exactly zero gradient, so at c2 the union of 24 views is ~24% of the rows (~4x fewer
+        bytes over xGMI than the dense 236 MB).  Rows outside the union are zero on every rank, so the
+        result is the dense all-reduce's up to the float summation order inside RCCL."""
         if not dist.is_available() or not dist.is_initialized() or dist.get_world_size(group) == 1:
             return None
         if not self.check_attached():  # autograd replaced a grad: fold it back into the bucket
@@ -68,7 +75,26 @@ class GradBucket:
                 if p.grad is not None and p.grad.data_ptr() != v.data_ptr():
                     v.copy_(p.grad)
             self.attach()
-        return dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=group, async_op=async_op)
+        rows = {v.shape[0] if v.dim() else -1 for v in self.views}
+        if not sparse or async_op or len(rows) != 1 or -1 in rows:
+            return dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=group, async_op=async_op)
+        n = rows.pop()
+        mats = [v.reshape(n, -1) for v in self.views]
+        live = torch.zeros(n, dtype=torch.uint8, device=self.flat.device)
+        for m in mats:
+            live |= (m != 0).any(1).to(torch.uint8)
+        dist.all_reduce(live, op=dist.ReduceOp.MAX, group=group)
+        idx = torch.nonzero(live).squeeze(1)
+        if 2 * idx.numel() > n:  # mostly dense: packing would not pay
+            return dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=group)
+        packed = torch.cat([m.index_select(0, idx) for m in mats], 1)
+        dist.all_reduce(packed, op=dist.ReduceOp.SUM, group=group)
+        off = 0
+        for m in mats:
+            w = m.shape[1]
+            m.index_copy_(0, idx, packed[:, off:off + w])
+            off += w
+        return None
 
 
 _STREAM_POOLS = {}

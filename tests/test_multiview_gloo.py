@@ -140,3 +140,44 @@ def test_grad_bucket_views_and_zero():
     assert bk.allreduce() is None  # no process group: no-op
     vs, rm = reduce_view_stats(torch.ones(2, 3), torch.tensor([1, 2], dtype=torch.int32))
     assert vs.sum() == 6 and rm.tolist() == [1, 2]
+
+
+def _sparse_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.set_num_threads(1)
+        out = {}
+        for sparse in (True, False):
+            g = torch.Generator().manual_seed(100 + rank)
+            ps = [torch.zeros(400, 3, requires_grad=True), torch.zeros(400, 1, 15, requires_grad=True),
+                  torch.zeros(400, 1, requires_grad=True)]
+            bk = GradBucket(ps)
+            rows = torch.randperm(400, generator=g)[: 30 + 20 * rank]  # each rank: its own live rows
+            for p in ps:
+                p.grad[rows] = torch.randn(p.grad[rows].shape, generator=g)
+            bk.allreduce(sparse=sparse)
+            out[sparse] = bk.flat.clone().numpy()
+        q.put((rank, out[True], out[False]))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.slow
+def test_sparse_bucket_allreduce_equals_dense():
+    """GradBucket.allreduce(sparse=True) (union of nonzero rows, packed) == the dense all-reduce."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_sparse_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, sp, de in res:
+        np.testing.assert_array_equal(sp, de)
+        assert np.count_nonzero(de) > 0
+    np.testing.assert_array_equal(res[0][1], res[1][1])
