@@ -105,6 +105,14 @@ class AdamSegment(ctypes.Structure):
     ]
 
 
+class RowsRegion(ctypes.Structure):
+    """struct gs_rows_region (include/gs_raster.h)."""
+
+    _fields_ = [("base", ctypes.c_void_p), ("width", ctypes.c_int)]
+
+
+ROWS_MAX_REGIONS = 8
+
 ALLOC_FN = ctypes.CFUNCTYPE(ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t)
 
 # Every symbol include/gs_raster.h declares, with its ctypes signature.
@@ -135,6 +143,12 @@ SIGNATURES = {
     "gs_profile_diag_read": (ctypes.c_longlong, [ctypes.c_int, ctypes.POINTER(ctypes.c_uint64), ctypes.c_longlong]),
     "gs_adam_step": (ctypes.c_int, [ctypes.POINTER(AdamSegment), ctypes.c_int, ctypes.c_float, ctypes.c_float,
                                     ctypes.c_float, ctypes.c_void_p]),
+    "gs_rows_live": (ctypes.c_int, [ctypes.POINTER(RowsRegion), ctypes.c_int, ctypes.c_longlong, ctypes.c_void_p,
+                                    ctypes.c_void_p]),
+    "gs_rows_gather": (ctypes.c_int, [ctypes.POINTER(RowsRegion), ctypes.c_int, ctypes.c_void_p, ctypes.c_longlong,
+                                      ctypes.c_void_p, ctypes.c_void_p]),
+    "gs_rows_scatter": (ctypes.c_int, [ctypes.POINTER(RowsRegion), ctypes.c_int, ctypes.c_void_p, ctypes.c_longlong,
+                                       ctypes.c_void_p, ctypes.c_void_p]),
     "gs_last_error": (ctypes.c_char_p, []),
     "gs_abi_version": (ctypes.c_int, []),
 }

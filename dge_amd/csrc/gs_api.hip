@@ -16,6 +16,7 @@
 //   k_ranges                          -> ranges (the per-tile lists come out of the tile sort)
 //   k_render_fwd                      -> color, depth, final_T, n_contrib, tile_last
 #include <stdarg.h>
+#include <stdlib.h>
 #include <stdio.h>
 #include <string.h>
 
@@ -65,6 +66,12 @@ int set_error(int code, const char* fmt, ...) {
     } while (0)
 
 // Per-(thread, device) pinned staging word + event for the num_rendered read-back.
+// DGE_AMD_DEPTH_KEYS32=1 forces the 32-bit depth-key fallback (tests compare both orders)
+bool force_depth_keys32() {
+    const char* e = getenv("DGE_AMD_DEPTH_KEYS32");
+    return e && e[0] == '1';
+}
+
 struct Staging {
     uint32_t* host = nullptr;
     hipEvent_t ev = nullptr;
@@ -292,15 +299,15 @@ int bin_forward(const gs_settings* s, const Grid& g, const gs_params& gp, int* r
     Staging* st = nullptr;
     int rc = staging_for_device(&st);
     if (rc) return rc;
-    GS_HIP(hipMemcpyAsync(st->host, counters, 8, hipMemcpyDeviceToHost, stream));
+    GS_HIP(hipMemcpyAsync(st->host, counters, 12, hipMemcpyDeviceToHost, stream));
     GS_HIP(hipEventRecord(st->ev, stream));
 
     // depth order of the Gaussians (stable: ties keep index order)
     int cur;
     { StageScope sc(ST_DEPTH_SORT, stream);
     cur = radix_sort_aux(at<uint32_t>(geom, gl.key0), at<uint32_t>(geom, gl.key1), at<uint2>(geom, gl.val0),
-                         at<uint2>(geom, gl.val1), pa.rect, (uint32_t)P, 32, 8, kDepthSortIPT, at<uint32_t>(geom, gl.sort_hist),
-                         at<uint32_t>(geom, gl.sort_totals), gl.sort_blocks, stream); }
+                         at<uint2>(geom, gl.val1), pa.rect, (uint32_t)P, kDepthKeyBits, kDepthPassBits, kDepthSortIPT,
+                         at<uint32_t>(geom, gl.sort_hist), at<uint32_t>(geom, gl.sort_totals), gl.sort_blocks, stream); }
     GS_LAUNCHED("depth sort");
 
     EmitArgs ea;
@@ -319,6 +326,18 @@ int bin_forward(const gs_settings* s, const Grid& g, const gs_params& gp, int* r
     GS_HIP(hipEventSynchronize(st->ev));
     const uint32_t K = st->host[0];
     if (st->host[1]) return set_error(GS_ERR_PREFILTERED, "Point is filtered although prefiltered is set. This shouldn't happen!");
+    if (st->host[2] || force_depth_keys32()) {
+        // a depth outside the 30-bit key range: redo the depth order on the full 32-bit keys
+        { StageScope sc(ST_DEPTH_SORT, stream);
+        launch_depth_keys32(P, pa.rect, pa.splat, at<uint32_t>(geom, gl.key0), stream);
+        cur = radix_sort_aux(at<uint32_t>(geom, gl.key0), at<uint32_t>(geom, gl.key1), at<uint2>(geom, gl.val0),
+                             at<uint2>(geom, gl.val1), pa.rect, (uint32_t)P, 32, 8, kDepthSortIPT,
+                             at<uint32_t>(geom, gl.sort_hist), at<uint32_t>(geom, gl.sort_totals), gl.sort_blocks,
+                             stream); }
+        ea.order = at<uint2>(geom, cur ? gl.val1 : gl.val0);
+        { StageScope sc(ST_SCAN, stream); launch_scan_reduce(ea, stream); }
+        GS_LAUNCHED("depth sort (32-bit keys)");
+    }
     if (K > (uint32_t)std::numeric_limits<int>::max()) return set_error(GS_ERR_INVALID_ARG, "too many tile instances (%u)", K);
     *K_out = (int)K;
 
@@ -331,6 +350,7 @@ int bin_forward(const gs_settings* s, const Grid& g, const gs_params& gp, int* r
     const TileSortPlan plan = tile_sort_plan(g.tiles);
     ea.tile_key = at<uint32_t>(bin, bl.key0);
     ea.slot_gauss = at<uint32_t>(bin, bl.slot_gauss);
+    ea.rec_flags32 = at<uint32_t>(bin, bl.rec_flags);
     { StageScope sc(ST_EMIT, stream); launch_scan_emit(ea, stream); }
     GS_LAUNCHED("emit");
 
@@ -338,12 +358,14 @@ int bin_forward(const gs_settings* s, const Grid& g, const gs_params& gp, int* r
     { StageScope sc(ST_TILE_SORT, stream);
     tc = tile_sort(at<uint32_t>(bin, bl.key0), at<uint32_t>(bin, bl.key1), at<uint2>(bin, bl.pair0),
                    at<uint2>(bin, bl.pair1), at<uint32_t>(bin, bl.slot_gauss), K, plan.bits,
-                   at<uint32_t>(bin, bl.sort_hist), at<uint32_t>(bin, bl.sort_totals), bl.sort_blocks, stream); }
+                   at<uint32_t>(bin, bl.sort_hist), at<uint32_t>(bin, bl.sort_totals), bl.sort_blocks, stream,
+                   at<uint2>(img, il.ranges)); }
     GS_LAUNCHED("tile sort");
-    { StageScope sc(ST_RANGES, stream);
-    launch_ranges(at<uint32_t>(bin, tc ? bl.key1 : bl.key0), (int)K, at<uint2>(img, il.ranges),
-                  at<uint32_t>(bin, bl.rec_flags), stream); }
-    GS_LAUNCHED("ranges");
+    if (!tile_sort_writes_ranges(g.tiles)) {
+        StageScope sc(ST_RANGES, stream);
+        launch_ranges(at<uint32_t>(bin, tc ? bl.key1 : bl.key0), (int)K, at<uint2>(img, il.ranges), nullptr, stream);
+        GS_LAUNCHED("ranges");
+    }
     return GS_OK;
 }
 

@@ -1,0 +1,190 @@
+// gs_bucket.hip — the sparse-row gradient exchange of the multi-view step, for gfx950.
+//
+// DGE sums the parameter gradients of a batch of views before the optimizer
+// step (threestudio/systems/DGE.py:170-296).  Sharded over ranks, that sum is an
+// all-reduce of the GaussianModel's six .grad tensors (59 floats per Gaussian,
+// 236 MB at 1M).  A Gaussian no view of a rank blends has exactly zero gradient
+// there, so dge_amd/multiview.py GradBucket moves only the rows that are
+// nonzero on some rank.  These kernels are its bookkeeping, each one pass at the
+// HBM roofline instead of torch's per-tensor compare / any / index_select / cat /
+// index_copy chain (~680 us at c3 on one MI355X, tools/probes/bucket_cost.py):
+//   k_rows_live    live[r] = row r of some region has an element != 0   (reads 4·W·n B)
+//   k_rows_gather  packed[i, :] = row rows[i] of every region           (4·W·m B each way)
+//   k_rows_scatter row rows[i] of every region = packed[i, :]
+#include "gs_internal.h"
+#include "gs_raster.h"
+
+namespace gs {
+
+struct RowsLaunch {
+    int nreg, width;                               // regions, total floats per row
+    float* base[GS_ROWS_MAX_REGIONS];
+    int w[GS_ROWS_MAX_REGIONS];
+    int col0[GS_ROWS_MAX_REGIONS + 1];             // first packed column of each region
+};
+
+constexpr int kRowsBlock = 256;  // rows per workgroup of k_rows_live
+
+// One workgroup per 256 rows: each region's rows [r0, r0 + nr) are one contiguous span, read
+// coalesced (float4 when the span is 16-B aligned, four in flight per thread); a nonzero element
+// marks its row in LDS (benign same-value stores).
+__device__ __forceinline__ int row_of(int j, int w, float inv_w) {
+    int r = (int)((float)j * inv_w);  // exact after the correction: j < 2^24
+    r -= (r * w > j);
+    r += ((r + 1) * w <= j);
+    return r;
+}
+
+__global__ __launch_bounds__(kRowsBlock) void k_rows_live(RowsLaunch a, long long n, uint8_t* __restrict__ live) {
+    __shared__ uint32_t flag[kRowsBlock];
+    const long long r0 = (long long)blockIdx.x * kRowsBlock;
+    const int nr = n - r0 < kRowsBlock ? (int)(n - r0) : kRowsBlock;
+    flag[threadIdx.x] = 0u;
+    __syncthreads();
+    for (int k = 0; k < a.nreg; ++k) {
+        const int w = a.w[k];
+        const float* __restrict__ src = a.base[k] + r0 * w;
+        const int span = nr * w;
+        const float inv_w = 1.f / (float)w;
+        int e = 0;  // elements below e are done
+        if ((reinterpret_cast<uintptr_t>(src) & 15) == 0) {
+            const float4* __restrict__ s4 = reinterpret_cast<const float4*>(src);
+            const int n4 = span >> 2;
+            int q = threadIdx.x;
+            for (; q + 3 * kRowsBlock < n4; q += 4 * kRowsBlock) {
+                float4 v[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) v[u] = s4[q + u * kRowsBlock];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int j = 4 * (q + u * kRowsBlock);
+                    if (v[u].x != 0.f) flag[row_of(j, w, inv_w)] = 1u;  // (NaN counts, as torch's `!= 0`)
+                    if (v[u].y != 0.f) flag[row_of(j + 1, w, inv_w)] = 1u;
+                    if (v[u].z != 0.f) flag[row_of(j + 2, w, inv_w)] = 1u;
+                    if (v[u].w != 0.f) flag[row_of(j + 3, w, inv_w)] = 1u;
+                }
+            }
+            for (; q < n4; q += kRowsBlock) {
+                const float4 v = s4[q];
+                const int j = 4 * q;
+                if (v.x != 0.f) flag[row_of(j, w, inv_w)] = 1u;
+                if (v.y != 0.f) flag[row_of(j + 1, w, inv_w)] = 1u;
+                if (v.z != 0.f) flag[row_of(j + 2, w, inv_w)] = 1u;
+                if (v.w != 0.f) flag[row_of(j + 3, w, inv_w)] = 1u;
+            }
+            e = n4 << 2;
+        }
+        for (int j = e + threadIdx.x; j < span; j += kRowsBlock) {
+            if (src[j] != 0.f) flag[row_of(j, w, inv_w)] = 1u;
+        }
+    }
+    __syncthreads();
+    if ((int)threadIdx.x < nr) live[r0 + threadIdx.x] = (uint8_t)flag[threadIdx.x];
+}
+
+// A 64-lane wave moves kRowsPerWave packed rows, lane = column (rows wider than 64 loop): all of a
+// wave's loads are issued before its stores; no index division.
+constexpr int kRowsPerWave = 8;
+
+template <bool GATHER>
+__global__ __launch_bounds__(256) void k_rows_move(RowsLaunch a, const long long* __restrict__ rows, long long m,
+                                                   float* __restrict__ packed) {
+    const long long i0 = ((long long)blockIdx.x * 4 + (threadIdx.x >> 6)) * kRowsPerWave;
+    if (i0 >= m) return;
+    const int nrow = m - i0 < kRowsPerWave ? (int)(m - i0) : kRowsPerWave;
+    long long row[kRowsPerWave];
+#pragma unroll
+    for (int u = 0; u < kRowsPerWave; ++u) row[u] = rows[i0 + (u < nrow ? u : 0)];
+    for (int c = threadIdx.x & 63; c < a.width; c += 64) {
+        int k = 0;
+#pragma unroll
+        for (int q = 1; q < GS_ROWS_MAX_REGIONS; ++q) k += (c >= a.col0[q]);
+        float* __restrict__ col = a.base[k] + (c - a.col0[k]);
+        const int w = a.w[k];
+        float* __restrict__ out = packed + i0 * a.width + c;
+        float v[kRowsPerWave];
+        if (GATHER) {
+#pragma unroll
+            for (int u = 0; u < kRowsPerWave; ++u) v[u] = col[row[u] * w];
+#pragma unroll
+            for (int u = 0; u < kRowsPerWave; ++u)
+                if (u < nrow) out[(long long)u * a.width] = v[u];
+        } else {
+#pragma unroll
+            for (int u = 0; u < kRowsPerWave; ++u) v[u] = out[(long long)(u < nrow ? u : 0) * a.width];
+#pragma unroll
+            for (int u = 0; u < kRowsPerWave; ++u)
+                if (u < nrow) col[row[u] * w] = v[u];
+        }
+    }
+}
+
+static int rows_launch(const gs_rows_region* regions, int nreg, RowsLaunch& a, const char* fn) {
+    if (nreg < 1 || nreg > GS_ROWS_MAX_REGIONS || !regions)
+        return report_error(GS_ERR_INVALID_ARG, fn);
+    a.nreg = nreg;
+    a.col0[0] = 0;
+    for (int k = 0; k < nreg; ++k) {
+        if (!regions[k].base || regions[k].width < 1) return report_error(GS_ERR_INVALID_ARG, fn);
+        a.base[k] = regions[k].base;
+        a.w[k] = regions[k].width;
+        a.col0[k + 1] = a.col0[k] + regions[k].width;
+    }
+    for (int k = nreg; k < GS_ROWS_MAX_REGIONS; ++k) {
+        a.base[k] = nullptr;
+        a.w[k] = 1;
+        a.col0[k + 1] = a.col0[k];
+    }
+    a.width = a.col0[nreg];
+    return GS_OK;
+}
+
+static int launched() {
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? GS_OK : report_error(GS_ERR_HIP, hipGetErrorString(e));
+}
+
+}  // namespace gs
+
+extern "C" int gs_rows_live(const gs_rows_region* regions, int nreg, long long n, uint8_t* live, gs_stream_t stream) {
+    using namespace gs;
+    RowsLaunch a;
+    if (int rc = rows_launch(regions, nreg, a, "gs_rows_live: bad region list")) return rc;
+    if (n < 0 || (n > 0 && !live)) return report_error(GS_ERR_INVALID_ARG, "gs_rows_live: bad row count / mask");
+    for (int k = 0; k < nreg; ++k)
+        if ((long long)kRowsBlock * a.w[k] >= (1ll << 24))
+            return report_error(GS_ERR_INVALID_ARG, "gs_rows_live: region too wide");
+    if (n == 0) return GS_OK;
+    hipLaunchKernelGGL(k_rows_live, dim3((unsigned)((n + kRowsBlock - 1) / kRowsBlock)), dim3(kRowsBlock), 0,
+                       (hipStream_t)stream, a, n, live);
+    return launched();
+}
+
+static int rows_move(const gs_rows_region* regions, int nreg, const long long* rows, long long m, float* packed,
+                     gs_stream_t stream, bool gather, const char* fn) {
+    using namespace gs;
+    RowsLaunch a;
+    if (int rc = rows_launch(regions, nreg, a, fn)) return rc;
+    if (m < 0 || (m > 0 && (!rows || !packed))) return report_error(GS_ERR_INVALID_ARG, fn);
+    if (m == 0) return GS_OK;
+    const long long blocks = (m + 4 * kRowsPerWave - 1) / (4 * kRowsPerWave);
+    if (blocks > 0x7FFFFFFF) return report_error(GS_ERR_INVALID_ARG, fn);
+    if (gather)
+        hipLaunchKernelGGL(k_rows_move<true>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, a, rows, m,
+                           packed);
+    else
+        hipLaunchKernelGGL(k_rows_move<false>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, a, rows, m,
+                           packed);
+    return launched();
+}
+
+extern "C" int gs_rows_gather(const gs_rows_region* regions, int nreg, const long long* rows, long long m,
+                              float* packed, gs_stream_t stream) {
+    return rows_move(regions, nreg, rows, m, packed, stream, true, "gs_rows_gather: bad arguments");
+}
+
+extern "C" int gs_rows_scatter(const gs_rows_region* regions, int nreg, const long long* rows, long long m,
+                               const float* packed, gs_stream_t stream) {
+    return rows_move(regions, nreg, rows, m, const_cast<float*>(packed), stream, false,
+                     "gs_rows_scatter: bad arguments");
+}

@@ -33,6 +33,12 @@ constexpr int kDepthSortIPT = 8;                // depth sort: smaller tiles, >=
 constexpr int kDepthSortTile = 256 * kDepthSortIPT;
 constexpr int kScanIPT = 4;
 constexpr int kScanTile = 256 * kScanIPT;
+// Depth sort keys: the bits of a view depth d > 0.2 (the near plane) minus 0x3E000000 fit 30 bits
+// for d < 2^125, so three 10-bit passes sort them; culled Gaussians get the largest key.
+constexpr uint32_t kDepthKeyBase = 0x3E000000u;
+constexpr uint32_t kDepthKeyCulled = 0x3FFFFFFFu;
+constexpr int kDepthKeyBits = 30;
+constexpr int kDepthPassBits = 10;
 constexpr int kMaxSinglePassBits = 11;          // tile keys up to 2048 tiles sort in one pass
 constexpr size_t kAlign = 256;
 
@@ -98,8 +104,8 @@ inline GeomLayout geom_layout(int P) {
     L.val0 = o; o = align_up(o + 8 * p);  // depth sort values: uint2 (rect-or-count, Gaussian)
     L.val1 = o; o = align_up(o + 8 * p);
     L.rect = o; o = align_up(o + 4 * p);  // packed tile rect (pack_rect) or tiles_touched
-    L.sort_hist = o; o = align_up(o + 4 * 256 * (size_t)L.sort_blocks);
-    L.sort_totals = o; o = align_up(o + 4 * 256);
+    L.sort_hist = o; o = align_up(o + 4 * (1u << kDepthPassBits) * (size_t)L.sort_blocks);
+    L.sort_totals = o; o = align_up(o + 4 * (1u << kDepthPassBits));
     L.scan_sums = o; o = align_up(o + 4 * (size_t)(L.scan_blocks + 1));
     L.total = o;
     return L;
@@ -216,6 +222,7 @@ struct PreprocessArgs {
     uint8_t* touched;    // zeroed here: k_render_bwd sets the bytes of Gaussians that get a record
 };
 void launch_preprocess(const PreprocessArgs& a, hipStream_t s);
+void launch_depth_keys32(int P, const uint32_t* rect, const Splat* splat, uint32_t* key, hipStream_t s);
 void launch_mark_visible(int P, const float* means3D, const float* view, uint8_t* present, hipStream_t s);
 
 // LSD radix sort of (u32 key, u32 value).  Returns the buffer index (0/1)
@@ -224,12 +231,15 @@ void launch_mark_visible(int P, const float* means3D, const float* view, uint8_t
 // Stable LSD sort of (key, (aux[i], i)) pairs on key bits [0, bits), at most
 // max_pass_bits per pass; returns the ping-pong index holding the result.
 int radix_sort_aux(uint32_t* key0, uint32_t* key1, uint2* pair0, uint2* pair1, const uint32_t* aux, uint32_t n,
-                   int bits, int max_pass_bits, int ipt, uint32_t* hist, uint32_t* totals, int nblocks, hipStream_t s);
+                   int bits, int max_pass_bits, int ipt, uint32_t* hist, uint32_t* totals, int nblocks, hipStream_t s,
+                   uint2* ranges = nullptr);
 // Stable sort of the K emitted instances on their tile id (key0 in slot
 // order); the values are (Gaussian, slot) pairs built on the first pass from
 // gauss_by_slot.  Returns the buffer index (0/1) holding keys and pairs.
 int tile_sort(uint32_t* key0, uint32_t* key1, uint2* pair0, uint2* pair1, const uint32_t* gauss_by_slot, uint32_t n,
-              int bits, uint32_t* hist, uint32_t* totals, int nblocks, hipStream_t s);
+              int bits, uint32_t* hist, uint32_t* totals, int nblocks, hipStream_t s, uint2* ranges);
+// the single-pass tile sort writes the tile ranges itself (and no sorted keys); two passes need k_ranges
+inline bool tile_sort_writes_ranges(int num_tiles) { return tile_sort_plan(num_tiles).passes == 1; }
 
 // Tile rect of a Gaussian in one u32 (x0, y0, x1, y1: 8 bits each, x1/y1
 // exclusive) — carried through the depth sort with the Gaussian id, so the
@@ -253,6 +263,7 @@ struct EmitArgs {
     uint32_t* first_slot;
     uint32_t* tile_key;          // K
     uint32_t* slot_gauss;        // K
+    uint32_t* rec_flags32 = nullptr;  // K: zeroed by the emission (the backward's per-slot record flags)
     int scan_blocks;
 };
 void launch_scan_reduce(const EmitArgs& a, hipStream_t s);

@@ -81,7 +81,7 @@ __global__ __launch_bounds__(256) void k_preprocess(PreprocessArgs a) {
     uint32_t touched = 0;
     uint32_t rect = 0;  // packed tile rect (or the count), 0 for a culled Gaussian
     int radius_out = 0;
-    uint32_t key = 0xFFFFFFFFu;
+    uint32_t key = kDepthKeyCulled;
     uint8_t clamp_bits = 0;
     f3 p = mk3(0, 0, 0), rgb = mk3(0, 0, 0);
     float2 pix = make_float2(0.f, 0.f);
@@ -187,7 +187,16 @@ __global__ __launch_bounds__(256) void k_preprocess(PreprocessArgs a) {
                     radius_out = (int)rad;
                     touched = area;
                     depth = pv.z;
-                    key = __float_as_uint(pv.z);  // depth > 0.2: the bits sort as the value
+                    // depth > 0.2: its bits sort as the value; offset into 30 bits (3 radix passes).
+                    // A depth of 2^125 or more (or NaN) is clamped and flagged: the host then redoes the
+                    // depth sort on the full 32-bit keys (k_depth_keys32), so the order stays exact.
+                    const uint32_t kb = __float_as_uint(pv.z);
+                    if (kb - kDepthKeyBase < kDepthKeyCulled) {
+                        key = kb - kDepthKeyBase;
+                    } else {
+                        key = kDepthKeyCulled - 1u;
+                        atomicOr(&a.counters[2], 1u);
+                    }
                 }
             }
         }
@@ -255,6 +264,20 @@ void launch_preprocess(const PreprocessArgs& a, hipStream_t s) {
         hipLaunchKernelGGL(k_preprocess<true>, dim3(div_up(a.P, 256)), dim3(256), 0, s, a);
     else
         hipLaunchKernelGGL(k_preprocess<false>, dim3(div_up(a.P, 256)), dim3(256), 0, s, a);
+}
+
+// Full 32-bit depth keys (the reference's key, rasterizer_impl.cu:86-92) from what preprocess left:
+// the fallback for scenes with a depth outside the 30-bit key range (rare; flagged in counters[2]).
+__global__ __launch_bounds__(256) void k_depth_keys32(int P, const uint32_t* __restrict__ rect,
+                                                      const Splat* __restrict__ splat, uint32_t* __restrict__ key) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= P) return;
+    key[i] = rect[i] ? __float_as_uint(splat[i].rgbd.w) : 0xFFFFFFFFu;
+}
+
+void launch_depth_keys32(int P, const uint32_t* rect, const Splat* splat, uint32_t* key, hipStream_t s) {
+    if (P <= 0) return;
+    hipLaunchKernelGGL(k_depth_keys32, dim3(div_up(P, 256)), dim3(256), 0, s, P, rect, splat, key);
 }
 
 // checkFrustum (rasterizer_impl.cu:53-63)

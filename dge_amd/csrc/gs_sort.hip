@@ -128,7 +128,8 @@ __global__ __launch_bounds__(256) void k_radix_scatter(const uint32_t* __restric
                                                        uint32_t* __restrict__ keys_out, void* __restrict__ vals_out_,
                                                        const uint32_t* __restrict__ gauss_by_slot, uint32_t n,
                                                        int shift, const uint32_t* __restrict__ hist,
-                                                       const uint32_t* __restrict__ totals, int nb) {
+                                                       const uint32_t* __restrict__ totals, int nb,
+                                                       uint2* __restrict__ ranges) {
     using V = typename std::conditional<VM == kValU32, uint32_t, uint2>::type;
     const uint32_t* vals_in = static_cast<const uint32_t*>(vals_in_);
     const uint2* pairs_in = static_cast<const uint2*>(vals_in_);
@@ -155,6 +156,10 @@ __global__ __launch_bounds__(256) void k_radix_scatter(const uint32_t* __restric
         for (int i = 0; i < PER; ++i) {
             const int d = tid * PER + i;
             if (d < NDIG) dbase[d] = run;
+            // single-pass tile sort: the digit is the tile, so its run is the tile's range
+            // (identifyTileRanges, rasterizer_impl.cu:105-125; empty tiles keep (0, 0))
+            if (ranges && blockIdx.x == 0 && d < NDIG)
+                ranges[d] = loc[i] ? make_uint2(run, run + loc[i]) : make_uint2(0u, 0u);
             run += loc[i];
         }
     }
@@ -234,7 +239,7 @@ __global__ __launch_bounds__(256) void k_radix_scatter(const uint32_t* __restric
     for (int i = tid; i < nvalid; i += 256) {
         const uint32_t k = s_key[i];
         const uint32_t pos = dbase[(k >> shift) & (NDIG - 1)] + (uint32_t)i;
-        keys_out[pos] = k;
+        if (keys_out) keys_out[pos] = k;  // (not needed after the last tile-sort pass)
         vals_out[pos] = s_val[i];
     }
 }
@@ -242,13 +247,13 @@ __global__ __launch_bounds__(256) void k_radix_scatter(const uint32_t* __restric
 template <int BITS, int IPT>
 static void radix_pass(const uint32_t* kin, const void* vin, uint32_t* kout, void* vout, const uint32_t* gauss_by_slot,
                        uint32_t n, int shift, bool idv, int vm, uint32_t* hist, uint32_t* totals, int nb,
-                       hipStream_t s) {
+                       uint2* ranges, hipStream_t s) {
     constexpr int NDIG = 1 << BITS;
     hipLaunchKernelGGL((k_radix_hist<BITS, IPT>), dim3(nb), dim3(256), 0, s, kin, n, shift, hist, nb);
     hipLaunchKernelGGL(k_radix_digit_scan, dim3(NDIG), dim3(256), 0, s, hist, nb, totals);
 #define GS_SCATTER(IDV, VM)                                                                                   \
     hipLaunchKernelGGL((k_radix_scatter<BITS, IPT, IDV, VM>), dim3(nb), dim3(256), 0, s, kin, vin, kout, vout,  \
-                       gauss_by_slot, n, shift, hist, totals, nb)
+                       gauss_by_slot, n, shift, hist, totals, nb, ranges)
     if (vm == kValPairFirst) GS_SCATTER(true, kValPairFirst);
     else if (vm == kValPair) GS_SCATTER(false, kValPair);
     else if (idv) GS_SCATTER(true, kValU32);
@@ -258,13 +263,13 @@ static void radix_pass(const uint32_t* kin, const void* vin, uint32_t* kout, voi
 
 static void radix_pass_bits(int bits, int ipt, const uint32_t* kin, const void* vin, uint32_t* kout, void* vout,
                             const uint32_t* gauss_by_slot, uint32_t n, int shift, bool idv, int vm, uint32_t* hist,
-                            uint32_t* totals, int nb, hipStream_t s) {
+                            uint32_t* totals, int nb, uint2* ranges, hipStream_t s) {
 #define GS_CASE(B)                                                                                              \
     case B:                                                                                                     \
         if (ipt == kDepthSortIPT)                                                                               \
-            radix_pass<B, kDepthSortIPT>(kin, vin, kout, vout, gauss_by_slot, n, shift, idv, vm, hist, totals, nb, s); \
+            radix_pass<B, kDepthSortIPT>(kin, vin, kout, vout, gauss_by_slot, n, shift, idv, vm, hist, totals, nb, ranges, s); \
         else                                                                                                    \
-            radix_pass<B, kSortIPT>(kin, vin, kout, vout, gauss_by_slot, n, shift, idv, vm, hist, totals, nb, s); \
+            radix_pass<B, kSortIPT>(kin, vin, kout, vout, gauss_by_slot, n, shift, idv, vm, hist, totals, nb, ranges, s); \
         break;
     switch (bits) {
         GS_CASE(1) GS_CASE(2) GS_CASE(3) GS_CASE(4) GS_CASE(5) GS_CASE(6)
@@ -283,7 +288,8 @@ static int pass_bits(int begin_bit, int end_bit, int max_pass_bits, int p, int& 
 }
 
 int radix_sort_aux(uint32_t* key0, uint32_t* key1, uint2* pair0, uint2* pair1, const uint32_t* aux, uint32_t n,
-                   int bits, int max_pass_bits, int ipt, uint32_t* hist, uint32_t* totals, int nblocks, hipStream_t s) {
+                   int bits, int max_pass_bits, int ipt, uint32_t* hist, uint32_t* totals, int nblocks, hipStream_t s,
+                   uint2* ranges) {
     uint32_t* k[2] = {key0, key1};
     uint2* v[2] = {pair0, pair1};
     int cur = 0;
@@ -291,8 +297,11 @@ int radix_sort_aux(uint32_t* key0, uint32_t* key1, uint2* pair0, uint2* pair1, c
     int shift = 0;
     for (int p = 0; p < passes; ++p) {
         const int b = pass_bits(0, bits, max_pass_bits, p, shift);
-        radix_pass_bits(b, ipt, k[cur], v[cur], k[cur ^ 1], v[cur ^ 1], aux, n, shift, p == 0,
-                        p == 0 ? kValPairFirst : kValPair, hist, totals, nblocks, s);
+        // a single pass given `ranges` writes the tile ranges and no sorted keys
+        const bool ranges_here = ranges && passes == 1;
+        radix_pass_bits(b, ipt, k[cur], v[cur], ranges_here ? nullptr : k[cur ^ 1], v[cur ^ 1], aux, n, shift,
+                        p == 0, p == 0 ? kValPairFirst : kValPair, hist, totals, nblocks,
+                        ranges_here ? ranges : nullptr, s);
         cur ^= 1;
         shift += b;
     }
@@ -300,9 +309,9 @@ int radix_sort_aux(uint32_t* key0, uint32_t* key1, uint2* pair0, uint2* pair1, c
 }
 
 int tile_sort(uint32_t* key0, uint32_t* key1, uint2* pair0, uint2* pair1, const uint32_t* gauss_by_slot, uint32_t n,
-              int bits, uint32_t* hist, uint32_t* totals, int nblocks, hipStream_t s) {
+              int bits, uint32_t* hist, uint32_t* totals, int nblocks, hipStream_t s, uint2* ranges) {
     return radix_sort_aux(key0, key1, pair0, pair1, gauss_by_slot, n, bits, kMaxSinglePassBits, kSortIPT, hist, totals,
-                          nblocks, s);
+                          nblocks, s, ranges);
 }
 
 // ---------------------------------------------------------------------
@@ -392,6 +401,7 @@ __global__ __launch_bounds__(256) void k_scan_emit(EmitArgs a) {
             const uint32_t kx = k - ky * (uint32_t)q.z;
             a.tile_key[base + j] = (uint32_t)((q.y + (int)ky) * a.gx + q.x + (int)kx);
             a.slot_gauss[base + j] = s_gauss[lo];
+            if (a.rec_flags32) a.rec_flags32[base + j] = 0u;  // slot's four quadrant flags (no memset launch)
         }
         base += total;
         __syncthreads();

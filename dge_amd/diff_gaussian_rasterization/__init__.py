@@ -47,6 +47,13 @@ def _call_with_snapshot(fn, args, debug, dump_name, what):
         raise
 
 
+def _no_grad_materialization(ctx, radii):
+    """radii are integer and depth is forward-only: without this autograd would zero-fill a P-element
+    int32 and an HxW fp32 gradient for them before every backward (two kernels per view)."""
+    ctx.mark_non_differentiable(radii)
+    ctx.set_materialize_grads(False)
+
+
 class _RasterizeGaussians(torch.autograd.Function):
     @staticmethod
     def forward(ctx, means3D, means2D, sh, colors_precomp, opacities, scales, rotations, cov3Ds_precomp,
@@ -61,11 +68,14 @@ class _RasterizeGaussians(torch.autograd.Function):
         ctx.num_rendered = num_rendered
         ctx.save_for_backward(colors_precomp, means3D, scales, rotations, cov3Ds_precomp, radii, sh, geomBuffer,
                               binningBuffer, imgBuffer)
+        _no_grad_materialization(ctx, radii)
         return color, radii, depth
 
     @staticmethod
     def backward(ctx, grad_out_color, grad_radii, grad_depth):
         # depth is forward-only, as in the reference (__init__.py:137, 155-177)
+        if grad_out_color is None:  # the image took no part in the loss: every gradient is zero
+            return (None,) * 9
         rs = ctx.raster_settings
         (colors_precomp, means3D, scales, rotations, cov3Ds_precomp, radii, sh, geomBuffer, binningBuffer,
          imgBuffer) = ctx.saved_tensors
@@ -101,10 +111,13 @@ class _RasterizeGaussiansFused(torch.autograd.Function):
         ctx.has_sh = f_dc is not None and f_dc.numel() != 0
         ctx.save_for_backward(xyz, f_dc, f_rest, colors, raw_opacity, raw_scaling, raw_rotation, radii, geomBuffer,
                               binningBuffer, imgBuffer)
+        _no_grad_materialization(ctx, radii)
         return color, radii, depth
 
     @staticmethod
     def backward(ctx, grad_out_color, grad_radii, grad_depth):
+        if grad_out_color is None:
+            return (None,) * 10
         rs = ctx.raster_settings
         (xyz, f_dc, f_rest, colors, raw_opacity, raw_scaling, raw_rotation, radii, geomBuffer, binningBuffer,
          imgBuffer) = ctx.saved_tensors

@@ -134,6 +134,24 @@ def render(viewpoint_camera, pc, pipe, bg_color: torch.Tensor, scaling_modifier=
     }
 
 
+_VIEWSPACE_ZEROS = {}  # device -> (zero buffer, its version when last known zero)
+
+
+def _viewspace_zeros(n, dtype, device):
+    """A fresh leaf of n x 3 zeros (the means2D placeholder whose .grad receives dL/dmeans2D) without a fill
+    kernel per view: every call returns a new leaf over one cached zero buffer, re-zeroed only if
+    someone wrote into it (its version counter moved)."""
+    ent = _VIEWSPACE_ZEROS.get(device)
+    if ent is None or ent[0].shape[0] < n or ent[0].dtype != dtype:
+        buf = torch.zeros((max(n, 1), 3), dtype=dtype, device=device)
+        ent = _VIEWSPACE_ZEROS[device] = (buf, buf._version)
+    buf, ver = ent
+    if buf._version != ver:
+        buf.zero_()
+        _VIEWSPACE_ZEROS[device] = (buf, buf._version)
+    return buf[:n].detach().requires_grad_(True)
+
+
 def _render_fused(viewpoint_camera, pc, pipe, bg_color, scaling_modifier=1.0, override_color=None):
     """render() for a standard GaussianModel without the getters' torch kernels:
     the rasterizer consumes _xyz, _features_dc, _features_rest, _opacity,
@@ -141,11 +159,7 @@ def _render_fused(viewpoint_camera, pc, pipe, bg_color, scaling_modifier=1.0, ov
     xyz = pc._xyz
     index = _mask_rows(pc.mask) if getattr(pc, "localize", False) else None
     n = index.numel() if index is not None else xyz.shape[0]
-    screenspace_points = torch.zeros((n, 3), dtype=xyz.dtype, requires_grad=True, device=xyz.device)
-    try:
-        screenspace_points.retain_grad()
-    except Exception:
-        pass
+    screenspace_points = _viewspace_zeros(n, xyz.dtype, xyz.device)
     rs = _settings(viewpoint_camera, bg_color, scaling_modifier, pc.active_sh_degree, getattr(pipe, "debug", False))
     if override_color is None:
         f_dc, f_rest, colors = pc._features_dc, pc._features_rest, None

@@ -22,6 +22,8 @@ from __future__ import annotations
 
 from typing import Sequence
 
+import ctypes
+
 import torch
 import torch.distributed as dist
 
@@ -80,21 +82,73 @@ class GradBucket:
             return dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=group, async_op=async_op)
         n = rows.pop()
         mats = [v.reshape(n, -1) for v in self.views]
-        live = torch.zeros(n, dtype=torch.uint8, device=self.flat.device)
-        for m in mats:
-            live |= (m != 0).any(1).to(torch.uint8)
+        live = _rows_live(mats, n)
         dist.all_reduce(live, op=dist.ReduceOp.MAX, group=group)
         idx = torch.nonzero(live).squeeze(1)
         if 2 * idx.numel() > n:  # mostly dense: packing would not pay
             return dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=group)
-        packed = torch.cat([m.index_select(0, idx) for m in mats], 1)
+        packed = _rows_gather(mats, idx)
         dist.all_reduce(packed, op=dist.ReduceOp.SUM, group=group)
-        off = 0
-        for m in mats:
-            w = m.shape[1]
-            m.index_copy_(0, idx, packed[:, off:off + w])
-            off += w
+        _rows_scatter(mats, idx, packed)
         return None
+
+
+# Sparse-row bookkeeping: one gfx950 kernel each on the GPU (gs_rows_live / gs_rows_gather /
+# gs_rows_scatter, dge_amd/csrc/gs_bucket.hip); torch ops for CPU buckets (the gloo tests).
+def _native_rows(mats):
+    from . import _native as N
+
+    regs = (N.RowsRegion * len(mats))(*[N.RowsRegion(m.data_ptr(), m.shape[1]) for m in mats])
+    return N, regs, ctypes.c_void_p(torch.cuda.current_stream(mats[0].device).cuda_stream)
+
+
+def _native_ok(mats):
+    from . import _native as N
+
+    return (mats[0].is_cuda and len(mats) <= N.ROWS_MAX_REGIONS
+            and all(m.dtype == torch.float32 and m.is_contiguous() for m in mats))
+
+
+def _rows_live(mats, n):
+    """uint8 [n]: 1 where row r of some matrix has an element != 0."""
+    live = torch.empty(n, dtype=torch.uint8, device=mats[0].device)
+    if _native_ok(mats):
+        N, regs, stream = _native_rows(mats)
+        N.check(N.lib().gs_rows_live(regs, len(mats), n, live.data_ptr(), stream), "gs_rows_live")
+        return live
+    live.zero_()
+    for m in mats:
+        live |= (m != 0).any(1).to(torch.uint8)
+    return live
+
+
+def _rows_gather(mats, idx):
+    """[len(idx), sum(widths)]: the rows idx of every matrix, side by side."""
+    if _native_ok(mats):
+        N, regs, stream = _native_rows(mats)
+        packed = torch.empty((idx.numel(), sum(m.shape[1] for m in mats)), dtype=torch.float32,
+                             device=mats[0].device)
+        idx = idx.to(torch.int64).contiguous()
+        N.check(N.lib().gs_rows_gather(regs, len(mats), idx.data_ptr(), idx.numel(), packed.data_ptr(), stream),
+                "gs_rows_gather")
+        return packed
+    return torch.cat([m.index_select(0, idx) for m in mats], 1)
+
+
+def _rows_scatter(mats, idx, packed):
+    """The inverse of _rows_gather: rows idx of every matrix = their columns of packed."""
+    if _native_ok(mats):
+        N, regs, stream = _native_rows(mats)
+        idx = idx.to(torch.int64).contiguous()
+        packed = packed.contiguous()
+        N.check(N.lib().gs_rows_scatter(regs, len(mats), idx.data_ptr(), idx.numel(), packed.data_ptr(), stream),
+                "gs_rows_scatter")
+        return
+    off = 0
+    for m in mats:
+        w = m.shape[1]
+        m.index_copy_(0, idx, packed[:, off:off + w])
+        off += w
 
 
 _STREAM_POOLS = {}

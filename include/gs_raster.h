@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define GS_RASTER_ABI_VERSION 4
+#define GS_RASTER_ABI_VERSION 5
 
 #define GS_OK 0
 #define GS_ERR_INVALID_ARG 1   /* AT_ERROR / std::runtime_error in the reference */
@@ -205,6 +205,26 @@ typedef struct gs_adam_segment {
 } gs_adam_segment;
 int gs_adam_step(const gs_adam_segment *segs, int nseg, float beta1, float beta2, float eps,
                  gs_stream_t stream);
+
+/* Sparse-row gradient exchange of the multi-view step (not in the reference,
+ * whose loop is single-GPU: threestudio/systems/DGE.py:170-296 sums the views'
+ * gradients in one process).  dge_amd/multiview.py GradBucket all-reduces only
+ * the rows that are nonzero on some rank.  A bucket is up to
+ * GS_ROWS_MAX_REGIONS row-major fp32 matrices sharing the row count (a
+ * GaussianModel's six .grad tensors: 3 + 3 + 45 + 1 + 3 + 4 floats per row). */
+#define GS_ROWS_MAX_REGIONS 8
+typedef struct gs_rows_region {
+    float *base;                  /* [n, width] row-major */
+    int width;
+} gs_rows_region;
+/* live[r] = 1 if row r of some region holds an element != 0 (NaN included), else 0. */
+int gs_rows_live(const gs_rows_region *regions, int nreg, long long n, uint8_t *live, gs_stream_t stream);
+/* packed[i, :] = row rows[i] of region 0, then of region 1, ... (m x sum(width)). */
+int gs_rows_gather(const gs_rows_region *regions, int nreg, const long long *rows, long long m, float *packed,
+                   gs_stream_t stream);
+/* the inverse: row rows[i] of every region = its columns of packed[i, :]. */
+int gs_rows_scatter(const gs_rows_region *regions, int nreg, const long long *rows, long long m,
+                    const float *packed, gs_stream_t stream);
 
 /* Byte sizes of the opaque buffers (host arithmetic, no device work). */
 size_t gs_geometry_buffer_size(int P);

@@ -456,3 +456,58 @@ def test_fused_localize_index_path_matches_getter_path(cuda_device, monkeypatch,
         # (fp16 feature grads are rounded to fp16 by autograd on both paths)
         assert_close(a, b, name, 2e-3 if half and "features" in name else 1e-4)
         np.testing.assert_array_equal(a[~m], 0.5 if preexisting_grads else 0.0, err_msg=name)
+
+
+def _axis_camera(W, H, fov_deg=60.0, device="cpu"):
+    """Camera at the origin looking down +z (identity view): view-space points are exact."""
+    from dge_amd.cameras import get_projection_matrix
+    from helpers import settings_from
+
+    fov = math.radians(fov_deg)
+    proj = get_projection_matrix(0.01, 100.0, fov, fov).transpose(0, 1).numpy()
+    return settings_from(W, H, math.tan(fov / 2), math.tan(fov / 2), (0.0, 0.0, 0.0), np.eye(4, dtype=np.float32),
+                         proj, (0.0, 0.0, 0.0), 3, device=device)
+
+
+def _far_depth_scene():
+    rng = np.random.default_rng(11)
+    P = 4000
+    xyz = np.stack([rng.uniform(-1, 1, P), rng.uniform(-1, 1, P), rng.uniform(3, 6, P)], 1).astype(np.float32)
+    # Gaussians beyond the 30-bit depth key (>= 2^125 ~ 4.25e37), on the axis (centre tile), in reverse
+    # index order of depth, plus a tie: the order must still be the reference's (depth bits, index)
+    far = np.array([[0, 0, 9e37], [0, 0, 6e37], [0, 0, 6e37], [0, 0, 5e37], [0.01, 0, 7e37]], np.float32)
+    xyz = np.concatenate([xyz, far])
+    n = xyz.shape[0]
+    rot = rng.standard_normal((n, 4)).astype(np.float32)
+    rot /= np.linalg.norm(rot, axis=1, keepdims=True)
+    return dict(means3D=xyz, opacities=rng.uniform(0.2, 0.9, (n, 1)).astype(np.float32),
+                shs=(rng.standard_normal((n, 16, 3)) * 0.3).astype(np.float32),
+                scales=rng.uniform(0.01, 0.05, (n, 3)).astype(np.float32), rotations=rot)
+
+
+def test_depth_beyond_30bit_key_range_keeps_reference_order(cuda_device, oracle):
+    """Depth keys are the view depth's float bits offset into 30 bits (three 10-bit radix passes); a
+    depth >= 2^125 is flagged by preprocess and the depth order is redone on the full 32-bit keys."""
+    kw = _far_depth_scene()
+    g = np.random.default_rng(3).standard_normal((3, 96, 96)).astype(np.float32) * 1e-3
+    ref = run_oracle(oracle, _axis_camera(96, 96), g, **kw)
+    got = run_gpu(_axis_camera(96, 96, device="cuda"), g, **kw)
+    assert (ref["radii"][-5:] > 0).sum() >= 4  # the far Gaussians are rendered
+    assert got["num_rendered"] == ref["num_rendered"]
+    np.testing.assert_array_equal(got["radii"], ref["radii"])
+    np.testing.assert_array_equal(got["ranges"], ref["ranges"])
+    np.testing.assert_array_equal(got["point_list"], ref["point_list"])
+    compare_forward(got, ref)
+    compare_grads(got, ref)
+
+
+def test_forced_32bit_depth_keys_match_30bit_path(cuda_device, monkeypatch):
+    """The 32-bit fallback (DGE_AMD_DEPTH_KEYS32=1) and the 30-bit path give the same lists and images."""
+    a = scene_arrays(100_000, seed=4, radius=2.0, scale=0.02)
+    kw = _sh_kw(a)
+    s = camera_settings(256, 256, device="cuda")
+    base = run_gpu(s, **kw)
+    monkeypatch.setenv("DGE_AMD_DEPTH_KEYS32", "1")
+    forced = run_gpu(s, **kw)
+    for k in ("radii", "ranges", "point_list", "n_contrib", "color", "final_T"):
+        np.testing.assert_array_equal(forced[k], base[k], err_msg=k)
