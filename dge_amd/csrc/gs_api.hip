@@ -72,6 +72,27 @@ bool force_depth_keys32() {
     return e && e[0] == '1';
 }
 
+// depth-sort bits (three passes of kDepthPassBits; DGE_AMD_DEPTH_SORT_BITS overrides, for probes)
+int depth_sort_bits() {
+    static const int bits = [] {
+        const char* e = getenv("DGE_AMD_DEPTH_SORT_BITS");
+        const int b = e ? atoi(e) : 0;
+        return (b >= 3 && b <= 30) ? b : kDepthSortBits;
+    }();
+    return bits;
+}
+
+// per-pass digit bits of the depth sort (DGE_AMD_DEPTH_PASS_BITS overrides; negative: low passes of
+// that width, the remainder in the last)
+int depth_pass_bits() {
+    static const int bits = [] {
+        const char* e = getenv("DGE_AMD_DEPTH_PASS_BITS");
+        const int b = e ? atoi(e) : 0;
+        return (b != 0 && b >= -10 && b <= 11) ? b : kDepthPassBits;
+    }();
+    return bits;
+}
+
 struct Staging {
     uint32_t* host = nullptr;
     hipEvent_t ev = nullptr;
@@ -83,7 +104,7 @@ int staging_for_device(Staging** out) {
     GS_HIP(hipGetDevice(&dev));
     Staging& s = map[dev];
     if (!s.host) {
-        GS_HIP(hipHostMalloc((void**)&s.host, 16, hipHostMallocDefault));
+        GS_HIP(hipHostMalloc((void**)&s.host, 4 * kCounterSlots * kCounterStride, hipHostMallocDefault));
         GS_HIP(hipEventCreateWithFlags(&s.ev, hipEventDisableTiming));
     }
     *out = &s;
@@ -299,15 +320,17 @@ int bin_forward(const gs_settings* s, const Grid& g, const gs_params& gp, int* r
     Staging* st = nullptr;
     int rc = staging_for_device(&st);
     if (rc) return rc;
-    GS_HIP(hipMemcpyAsync(st->host, counters, 12, hipMemcpyDeviceToHost, stream));
+    GS_HIP(hipMemcpyAsync(st->host, counters, 4 * kCounterSlots * kCounterStride, hipMemcpyDeviceToHost, stream));
     GS_HIP(hipEventRecord(st->ev, stream));
 
     // depth order of the Gaussians (stable: ties keep index order)
     int cur;
     { StageScope sc(ST_DEPTH_SORT, stream);
     cur = radix_sort_aux(at<uint32_t>(geom, gl.key0), at<uint32_t>(geom, gl.key1), at<uint2>(geom, gl.val0),
-                         at<uint2>(geom, gl.val1), pa.rect, (uint32_t)P, kDepthKeyBits, kDepthPassBits, kDepthSortIPT,
-                         at<uint32_t>(geom, gl.sort_hist), at<uint32_t>(geom, gl.sort_totals), gl.sort_blocks, stream); }
+                         at<uint2>(geom, gl.val1), pa.rect, (uint32_t)P, depth_sort_bits(), depth_pass_bits(),
+                         kDepthSortIPT, at<uint32_t>(geom, gl.sort_hist), at<uint32_t>(geom, gl.sort_totals),
+                         gl.sort_blocks, stream, nullptr, counters + 2); }
+    if (cur < 0) return set_error(GS_ERR_INVALID_ARG, "depth sort: bad digit layout");
     GS_LAUNCHED("depth sort");
 
     EmitArgs ea;
@@ -324,10 +347,20 @@ int bin_forward(const gs_settings* s, const Grid& g, const gs_params& gp, int* r
     GS_LAUNCHED("instance scan");
 
     GS_HIP(hipEventSynchronize(st->ev));
-    const uint32_t K = st->host[0];
-    if (st->host[1]) return set_error(GS_ERR_PREFILTERED, "Point is filtered although prefiltered is set. This shouldn't happen!");
-    if (st->host[2] || force_depth_keys32()) {
-        // a depth outside the 30-bit key range: redo the depth order on the full 32-bit keys
+    uint64_t K64 = 0;
+    uint32_t kmax = 0, kmin_not = 0;
+    for (int i = 0; i < kCounterSlots; ++i) {
+        const uint32_t* c = st->host + kCounterStride * i;
+        K64 += c[0];
+        kmax = c[1] > kmax ? c[1] : kmax;
+        kmin_not = c[2] > kmin_not ? c[2] : kmin_not;
+    }
+    if (st->host[3]) return set_error(GS_ERR_PREFILTERED, "Point is filtered although prefiltered is set. This shouldn't happen!");
+    if (K64 > (uint64_t)std::numeric_limits<int>::max()) return set_error(GS_ERR_INVALID_ARG, "too many tile instances (%llu)", (unsigned long long)K64);
+    const uint32_t K = (uint32_t)K64;
+    if ((K && kmax - ~kmin_not >= (1u << depth_sort_bits())) || force_depth_keys32()) {
+        // the visible depth keys span more bits than the short sort covered: redo the depth order
+        // on the full 32-bit keys
         { StageScope sc(ST_DEPTH_SORT, stream);
         launch_depth_keys32(P, pa.rect, pa.splat, at<uint32_t>(geom, gl.key0), stream);
         cur = radix_sort_aux(at<uint32_t>(geom, gl.key0), at<uint32_t>(geom, gl.key1), at<uint2>(geom, gl.val0),
@@ -338,7 +371,6 @@ int bin_forward(const gs_settings* s, const Grid& g, const gs_params& gp, int* r
         { StageScope sc(ST_SCAN, stream); launch_scan_reduce(ea, stream); }
         GS_LAUNCHED("depth sort (32-bit keys)");
     }
-    if (K > (uint32_t)std::numeric_limits<int>::max()) return set_error(GS_ERR_INVALID_ARG, "too many tile instances (%u)", K);
     *K_out = (int)K;
 
     const BinLayout bl = bin_layout((int)K, g.tiles);

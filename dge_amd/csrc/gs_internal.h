@@ -33,12 +33,13 @@ constexpr int kDepthSortIPT = 8;                // depth sort: smaller tiles, >=
 constexpr int kDepthSortTile = 256 * kDepthSortIPT;
 constexpr int kScanIPT = 4;
 constexpr int kScanTile = 256 * kScanIPT;
-// Depth sort keys: the bits of a view depth d > 0.2 (the near plane) minus 0x3E000000 fit 30 bits
-// for d < 2^125, so three 10-bit passes sort them; culled Gaussians get the largest key.
-constexpr uint32_t kDepthKeyBase = 0x3E000000u;
-constexpr uint32_t kDepthKeyCulled = 0x3FFFFFFFu;
-constexpr int kDepthKeyBits = 30;
-constexpr int kDepthPassBits = 10;
+// Depth sort: keys are the bits of the view depth (d > 0.2), sorted as key - min(visible keys) on
+// kDepthSortBits bits in three passes — a depth ratio up to 2^(27-23) = 65536 between the farthest
+// and nearest visible Gaussian; wider (or NaN) ranges take the full 32-bit sort (4 x 8 bits).
+constexpr int kCounterSlots = 16;   // preprocess counters: copies in separate 64-B lines
+constexpr int kCounterStride = 16;  // u32 per slot
+constexpr int kDepthPassBits = 9;
+constexpr int kDepthSortBits = 3 * kDepthPassBits;
 constexpr int kMaxSinglePassBits = 11;          // tile keys up to 2048 tiles sort in one pass
 constexpr size_t kAlign = 256;
 
@@ -104,8 +105,8 @@ inline GeomLayout geom_layout(int P) {
     L.val0 = o; o = align_up(o + 8 * p);  // depth sort values: uint2 (rect-or-count, Gaussian)
     L.val1 = o; o = align_up(o + 8 * p);
     L.rect = o; o = align_up(o + 4 * p);  // packed tile rect (pack_rect) or tiles_touched
-    L.sort_hist = o; o = align_up(o + 4 * (1u << kDepthPassBits) * (size_t)L.sort_blocks);
-    L.sort_totals = o; o = align_up(o + 4 * (1u << kDepthPassBits));
+    L.sort_hist = o; o = align_up(o + 4 * (1u << kMaxSinglePassBits) * (size_t)L.sort_blocks);  // any digit width
+    L.sort_totals = o; o = align_up(o + 4 * (1u << kMaxSinglePassBits));
     L.scan_sums = o; o = align_up(o + 4 * (size_t)(L.scan_blocks + 1));
     L.total = o;
     return L;
@@ -133,6 +134,8 @@ __host__ __device__ inline size_t used_words(size_t K, int tiles) { return 4 * (
 
 struct ImgLayout {
     size_t final_T, n_contrib, tile_order, counters, ranges, tile_last, quad_last, bwd_count, total;
+    // counters: kCounterSlots slots of kCounterStride u32: [0] instances, [1] max depth key,
+    // [2] ~min depth key (summed / maxed over the slots by the host); slot 0 [3]: prefiltered error
 };
 inline ImgLayout img_layout(int W, int H) {
     ImgLayout L;
@@ -142,7 +145,7 @@ inline ImgLayout img_layout(int W, int H) {
     L.final_T = o; o = align_up(o + 4 * n);
     L.n_contrib = o; o = align_up(o + 4 * n);
     L.tile_order = o; o = align_up(o + 4 * tiles);  // tiles by list length, longest first
-    L.counters = o; o = align_up(o + 16);        // counters.. are zeroed per forward (one memset)
+    L.counters = o; o = align_up(o + 4 * kCounterSlots * kCounterStride);  // counters.. zeroed per forward (one memset)
     L.ranges = o; o = align_up(o + 8 * tiles);
     L.tile_last = o; o = align_up(o + 4 * tiles);
     L.quad_last = o; o = align_up(o + 16 * tiles);
@@ -218,7 +221,7 @@ struct PreprocessArgs {
     uint32_t* depth_key;
     uint32_t* rect;          // pack_rect(tile rect) when the grid allows it, else tiles_touched
     int rect_packed;
-    uint32_t* counters;  // [0] instance total, [1] error flag
+    uint32_t* counters;  // kCounterSlots x kCounterStride (ImgLayout)
     uint8_t* touched;    // zeroed here: k_render_bwd sets the bytes of Gaussians that get a record
 };
 void launch_preprocess(const PreprocessArgs& a, hipStream_t s);
@@ -232,7 +235,9 @@ void launch_mark_visible(int P, const float* means3D, const float* view, uint8_t
 // max_pass_bits per pass; returns the ping-pong index holding the result.
 int radix_sort_aux(uint32_t* key0, uint32_t* key1, uint2* pair0, uint2* pair1, const uint32_t* aux, uint32_t n,
                    int bits, int max_pass_bits, int ipt, uint32_t* hist, uint32_t* totals, int nblocks, hipStream_t s,
-                   uint2* ranges = nullptr);
+                   uint2* ranges = nullptr, const uint32_t* key_bias_not = nullptr);
+// key_bias_not: the preprocess counter slots' ~min key (kCounterStride apart); the first pass sorts
+// (and writes) key - min
 // Stable sort of the K emitted instances on their tile id (key0 in slot
 // order); the values are (Gaussian, slot) pairs built on the first pass from
 // gauss_by_slot.  Returns the buffer index (0/1) holding keys and pairs.

@@ -81,7 +81,7 @@ __global__ __launch_bounds__(256) void k_preprocess(PreprocessArgs a) {
     uint32_t touched = 0;
     uint32_t rect = 0;  // packed tile rect (or the count), 0 for a culled Gaussian
     int radius_out = 0;
-    uint32_t key = kDepthKeyCulled;
+    uint32_t key = 0xFFFFFFFFu;
     uint8_t clamp_bits = 0;
     f3 p = mk3(0, 0, 0), rgb = mk3(0, 0, 0);
     float2 pix = make_float2(0.f, 0.f);
@@ -156,7 +156,7 @@ __global__ __launch_bounds__(256) void k_preprocess(PreprocessArgs a) {
         const float pw = 1.0f / (ph.w + 0.0000001f);
         const f3 pv = view_point(v, p);
         bool visible = pv.z > 0.2f;
-        if (!visible && a.prefiltered) atomicOr(&a.counters[1], 1u);
+        if (!visible && a.prefiltered) atomicOr(&a.counters[3], 1u);  // (slot 0, word 3)
         if (visible) {
             if (!a.cov3D_precomp) {
                 if (a.activation) {  // get_rotation / get_scaling (gaussian_model.py:228-240)
@@ -187,16 +187,7 @@ __global__ __launch_bounds__(256) void k_preprocess(PreprocessArgs a) {
                     radius_out = (int)rad;
                     touched = area;
                     depth = pv.z;
-                    // depth > 0.2: its bits sort as the value; offset into 30 bits (3 radix passes).
-                    // A depth of 2^125 or more (or NaN) is clamped and flagged: the host then redoes the
-                    // depth sort on the full 32-bit keys (k_depth_keys32), so the order stays exact.
-                    const uint32_t kb = __float_as_uint(pv.z);
-                    if (kb - kDepthKeyBase < kDepthKeyCulled) {
-                        key = kb - kDepthKeyBase;
-                    } else {
-                        key = kDepthKeyCulled - 1u;
-                        atomicOr(&a.counters[2], 1u);
-                    }
+                    key = __float_as_uint(pv.z);  // depth > 0.2: the bits sort as the value
                 }
             }
         }
@@ -245,16 +236,33 @@ __global__ __launch_bounds__(256) void k_preprocess(PreprocessArgs a) {
         a.rect[idx] = rect;
         if (a.touched) a.touched[idx] = 0;
     }
-    // workgroup total of instances -> one atomic
-    __shared__ uint32_t part[4];
-    uint32_t s = touched;
+    // workgroup total of instances and the range of the visible depth keys -> three atomics
+    // (per slot: [0] instances, [1] max key, [2] ~min key: all start at 0).  The depth sort orders
+    // key - min on kDepthSortBits bits; the host redoes it on all 32 when the range is wider.
+    __shared__ uint32_t part[4][3];
+    uint32_t s = touched, kmax = touched ? key : 0u, kmin_n = touched ? ~key : 0u;
 #pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) s += (uint32_t)__shfl_xor((int)s, o);
-    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = s;
+    for (int o = 32; o >= 1; o >>= 1) {
+        s += (uint32_t)__shfl_xor((int)s, o);
+        kmax = max(kmax, (uint32_t)__shfl_xor((int)kmax, o));
+        kmin_n = max(kmin_n, (uint32_t)__shfl_xor((int)kmin_n, o));
+    }
+    if ((threadIdx.x & 63) == 0) {
+        part[threadIdx.x >> 6][0] = s;
+        part[threadIdx.x >> 6][1] = kmax;
+        part[threadIdx.x >> 6][2] = kmin_n;
+    }
     __syncthreads();
     if (threadIdx.x == 0) {
-        const uint32_t t = part[0] + part[1] + part[2] + part[3];
-        if (t) atomicAdd(&a.counters[0], t);
+        const uint32_t t = part[0][0] + part[1][0] + part[2][0] + part[3][0];
+        if (t) {
+            // kCounterSlots copies in separate 64-B lines: same-address device atomics from every
+            // workgroup serialise (one slot: +35 us per counter at 1M Gaussians); the host sums them
+            uint32_t* c = a.counters + kCounterStride * (blockIdx.x % kCounterSlots);
+            atomicAdd(&c[0], t);
+            atomicMax(&c[1], max(max(part[0][1], part[1][1]), max(part[2][1], part[3][1])));
+            atomicMax(&c[2], max(max(part[0][2], part[1][2]), max(part[2][2], part[3][2])));
+        }
     }
 }
 
@@ -267,7 +275,8 @@ void launch_preprocess(const PreprocessArgs& a, hipStream_t s) {
 }
 
 // Full 32-bit depth keys (the reference's key, rasterizer_impl.cu:86-92) from what preprocess left:
-// the fallback for scenes with a depth outside the 30-bit key range (rare; flagged in counters[2]).
+// the fallback for scenes whose visible depth keys span more than kDepthSortBits (the 3-pass sort
+// has overwritten the originals by then).
 __global__ __launch_bounds__(256) void k_depth_keys32(int P, const uint32_t* __restrict__ rect,
                                                       const Splat* __restrict__ splat, uint32_t* __restrict__ key) {
     const int i = blockIdx.x * 256 + threadIdx.x;

@@ -63,24 +63,36 @@ __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* l
     return wbase + x - v;
 }
 
+// The depth sort's bias: the minimum visible key, kept as ~min in the preprocess counter slots
+// (max over the slots; kCounterStride apart).
+__device__ __forceinline__ uint32_t key_bias(const uint32_t* __restrict__ bias_not) {
+    if (!bias_not) return 0u;
+    uint32_t m = 0u;
+#pragma unroll
+    for (int i = 0; i < kCounterSlots; ++i) m = max(m, bias_not[i * kCounterStride]);
+    return ~m;
+}
+
 // ---------------------------------------------------------------------
 // radix sort: histogram -> per-digit scan -> stable scatter
 // ---------------------------------------------------------------------
 // Per-block digit counts (integer LDS atomics: the counts do not depend on the order).
 template <int BITS, int IPT>
 __global__ __launch_bounds__(256) void k_radix_hist(const uint32_t* __restrict__ keys, uint32_t n, int shift,
-                                                    uint32_t* __restrict__ hist, int nb) {
+                                                    uint32_t* __restrict__ hist, int nb,
+                                                    const uint32_t* __restrict__ bias_not) {
     constexpr int NDIG = 1 << BITS;
     __shared__ uint32_t cnt[NDIG];
     const int tid = threadIdx.x;
     for (int i = tid; i < NDIG; i += 256) cnt[i] = 0;
     __syncthreads();
     const uint32_t base = blockIdx.x * (uint32_t)(256 * IPT);
+    const uint32_t bias = key_bias(bias_not);
     uint32_t key[IPT];
 #pragma unroll
     for (int it = 0; it < IPT; ++it) {
         const uint32_t idx = base + it * 256 + tid;
-        key[it] = idx < n ? keys[idx] : 0u;
+        key[it] = idx < n ? keys[idx] - bias : 0u;
     }
 #pragma unroll
     for (int it = 0; it < IPT; ++it) {
@@ -129,7 +141,8 @@ __global__ __launch_bounds__(256) void k_radix_scatter(const uint32_t* __restric
                                                        const uint32_t* __restrict__ gauss_by_slot, uint32_t n,
                                                        int shift, const uint32_t* __restrict__ hist,
                                                        const uint32_t* __restrict__ totals, int nb,
-                                                       uint2* __restrict__ ranges) {
+                                                       uint2* __restrict__ ranges,
+                                                       const uint32_t* __restrict__ bias_not) {
     using V = typename std::conditional<VM == kValU32, uint32_t, uint2>::type;
     const uint32_t* vals_in = static_cast<const uint32_t*>(vals_in_);
     const uint2* pairs_in = static_cast<const uint2*>(vals_in_);
@@ -165,13 +178,14 @@ __global__ __launch_bounds__(256) void k_radix_scatter(const uint32_t* __restric
     }
     __syncthreads();
     const uint32_t base = blockIdx.x * (uint32_t)(256 * IPT) + w * 64u * IPT;
+    const uint32_t bias = key_bias(bias_not);
     uint32_t key[IPT], loc[IPT];
     V val[IPT];
 #pragma unroll
     for (int it = 0; it < IPT; ++it) {
         const uint32_t idx = base + it * 64 + lane;
         const bool valid = idx < n;
-        key[it] = valid ? keys_in[idx] : 0u;
+        key[it] = valid ? keys_in[idx] - bias : 0u;
         if constexpr (VM == kValU32) val[it] = IDV ? idx : (valid ? vals_in[idx] : 0u);
         else if constexpr (VM == kValPairFirst) val[it] = make_uint2(valid ? gauss_by_slot[idx] : 0u, idx);
         else val[it] = valid ? pairs_in[idx] : make_uint2(0u, 0u);
@@ -247,13 +261,13 @@ __global__ __launch_bounds__(256) void k_radix_scatter(const uint32_t* __restric
 template <int BITS, int IPT>
 static void radix_pass(const uint32_t* kin, const void* vin, uint32_t* kout, void* vout, const uint32_t* gauss_by_slot,
                        uint32_t n, int shift, bool idv, int vm, uint32_t* hist, uint32_t* totals, int nb,
-                       uint2* ranges, hipStream_t s) {
+                       uint2* ranges, const uint32_t* bias_not, hipStream_t s) {
     constexpr int NDIG = 1 << BITS;
-    hipLaunchKernelGGL((k_radix_hist<BITS, IPT>), dim3(nb), dim3(256), 0, s, kin, n, shift, hist, nb);
+    hipLaunchKernelGGL((k_radix_hist<BITS, IPT>), dim3(nb), dim3(256), 0, s, kin, n, shift, hist, nb, bias_not);
     hipLaunchKernelGGL(k_radix_digit_scan, dim3(NDIG), dim3(256), 0, s, hist, nb, totals);
 #define GS_SCATTER(IDV, VM)                                                                                   \
     hipLaunchKernelGGL((k_radix_scatter<BITS, IPT, IDV, VM>), dim3(nb), dim3(256), 0, s, kin, vin, kout, vout,  \
-                       gauss_by_slot, n, shift, hist, totals, nb, ranges)
+                       gauss_by_slot, n, shift, hist, totals, nb, ranges, bias_not)
     if (vm == kValPairFirst) GS_SCATTER(true, kValPairFirst);
     else if (vm == kValPair) GS_SCATTER(false, kValPair);
     else if (idv) GS_SCATTER(true, kValU32);
@@ -263,13 +277,13 @@ static void radix_pass(const uint32_t* kin, const void* vin, uint32_t* kout, voi
 
 static void radix_pass_bits(int bits, int ipt, const uint32_t* kin, const void* vin, uint32_t* kout, void* vout,
                             const uint32_t* gauss_by_slot, uint32_t n, int shift, bool idv, int vm, uint32_t* hist,
-                            uint32_t* totals, int nb, uint2* ranges, hipStream_t s) {
+                            uint32_t* totals, int nb, uint2* ranges, const uint32_t* bias_not, hipStream_t s) {
 #define GS_CASE(B)                                                                                              \
     case B:                                                                                                     \
         if (ipt == kDepthSortIPT)                                                                               \
-            radix_pass<B, kDepthSortIPT>(kin, vin, kout, vout, gauss_by_slot, n, shift, idv, vm, hist, totals, nb, ranges, s); \
+            radix_pass<B, kDepthSortIPT>(kin, vin, kout, vout, gauss_by_slot, n, shift, idv, vm, hist, totals, nb, ranges, bias_not, s); \
         else                                                                                                    \
-            radix_pass<B, kSortIPT>(kin, vin, kout, vout, gauss_by_slot, n, shift, idv, vm, hist, totals, nb, ranges, s); \
+            radix_pass<B, kSortIPT>(kin, vin, kout, vout, gauss_by_slot, n, shift, idv, vm, hist, totals, nb, ranges, bias_not, s); \
         break;
     switch (bits) {
         GS_CASE(1) GS_CASE(2) GS_CASE(3) GS_CASE(4) GS_CASE(5) GS_CASE(6)
@@ -289,19 +303,23 @@ static int pass_bits(int begin_bit, int end_bit, int max_pass_bits, int p, int& 
 
 int radix_sort_aux(uint32_t* key0, uint32_t* key1, uint2* pair0, uint2* pair1, const uint32_t* aux, uint32_t n,
                    int bits, int max_pass_bits, int ipt, uint32_t* hist, uint32_t* totals, int nblocks, hipStream_t s,
-                   uint2* ranges) {
+                   uint2* ranges, const uint32_t* key_bias_not) {
     uint32_t* k[2] = {key0, key1};
     uint2* v[2] = {pair0, pair1};
     int cur = 0;
-    const int passes = (bits + max_pass_bits - 1) / max_pass_bits;
+    // max_pass_bits < 0: |max_pass_bits|-bit low passes, the remainder (<= 11 bits) in the last
+    const int low = max_pass_bits < 0 ? -max_pass_bits : 0;
+    const int passes = low ? 1 + (bits - kMaxSinglePassBits + low - 1) / low
+                           : (bits + max_pass_bits - 1) / max_pass_bits;
     int shift = 0;
     for (int p = 0; p < passes; ++p) {
-        const int b = pass_bits(0, bits, max_pass_bits, p, shift);
+        const int b = low ? (p + 1 < passes ? low : bits - shift) : pass_bits(0, bits, max_pass_bits, p, shift);
+        if (b < 1 || b > kMaxSinglePassBits) return -1;  // (histograms are sized for <= 11-bit digits)
         // a single pass given `ranges` writes the tile ranges and no sorted keys
         const bool ranges_here = ranges && passes == 1;
         radix_pass_bits(b, ipt, k[cur], v[cur], ranges_here ? nullptr : k[cur ^ 1], v[cur ^ 1], aux, n, shift,
                         p == 0, p == 0 ? kValPairFirst : kValPair, hist, totals, nblocks,
-                        ranges_here ? ranges : nullptr, s);
+                        ranges_here ? ranges : nullptr, p == 0 ? key_bias_not : nullptr, s);
         cur ^= 1;
         shift += b;
     }
