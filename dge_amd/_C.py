@@ -278,7 +278,7 @@ def apply_weights(background, means3D, weights, opacity, scales, rotations, scal
 # fused path: raw GaussianModel parameters, activations and SH split in-kernel
 # (gs_rasterize_forward_ex / gs_rasterize_backward_ex)
 # ---------------------------------------------------------------------------
-def _params(P, xyz, f_dc, f_rest, colors, raw_opacity, raw_scaling, raw_rotation, index=None):
+def _params(P, xyz, f_dc, f_rest, colors, raw_opacity, raw_scaling, raw_rotation, index=None, visible=None):
     """gs_params of the raw-parameter path; `index` (int32 [P], ascending): the localize subset's rows
     (gathered in-kernel); fp16 features are read as such (sh_half)."""
     g = N.GsParams()
@@ -299,6 +299,10 @@ def _params(P, xyz, f_dc, f_rest, colors, raw_opacity, raw_scaling, raw_rotation
     g.rotations = _ptr(raw_rotation)
     g.cov3D_precomp = None
     g.activation = 1
+    if visible is not None:
+        if visible.dtype != torch.bool or visible.numel() != P or not visible.is_contiguous():
+            raise ValueError("visible must be a contiguous bool tensor of P elements")
+        g.visible_out = visible.data_ptr()
     return g
 
 
@@ -319,10 +323,11 @@ def _features(t, name):
 
 def rasterize_gaussians_fused(background, xyz, f_dc, f_rest, colors, raw_opacity, raw_scaling, raw_rotation,
                               scale_modifier, viewmatrix, projmatrix, tan_fovx, tan_fovy, image_height, image_width,
-                              degree, campos, prefiltered, debug, index=None):
+                              degree, campos, prefiltered, debug, index=None, visible=None):
     """Forward on raw parameters: opacity = sigmoid, scale = exp, rotation = normalize applied in-kernel,
     SH read from _features_dc [P,1,3] and _features_rest [P,M-1,3] without concatenation (fp32 or fp16).
-    index: optional int32 rows — render only those Gaussians (the `localize` subset), P = len(index)."""
+    index: optional int32 rows — render only those Gaussians (the `localize` subset), P = len(index).
+    visible: optional bool [P] output, set to radii > 0 by the preprocess kernel."""
     N.require_gpu(xyz)
     dev = xyz.device
     index = _index32(index)
@@ -337,7 +342,7 @@ def rasterize_gaussians_fused(background, xyz, f_dc, f_rest, colors, raw_opacity
         out_color = torch.empty((3, H, W), dtype=torch.float32, device=dev)
         out_depth = torch.empty((1, H, W), dtype=torch.float32, device=dev)
         radii = torch.empty((P,), dtype=torch.int32, device=dev)
-        g = _params(P, xyz, f_dc, f_rest, colors, raw_opacity, raw_scaling, raw_rotation, index)
+        g = _params(P, xyz, f_dc, f_rest, colors, raw_opacity, raw_scaling, raw_rotation, index, visible)
         s, keep = _settings(background, viewmatrix, projmatrix, campos, tan_fovx, tan_fovy, H, W, degree,
                             scale_modifier, prefiltered, debug)
         alloc = _Allocator(dev)

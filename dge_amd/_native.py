@@ -62,6 +62,7 @@ class GsParams(ctypes.Structure):
         ("activation", ctypes.c_int),
         ("sh_half", ctypes.c_int),
         ("index", ctypes.c_void_p),
+        ("visible_out", ctypes.c_void_p),
     ]
 
 

@@ -238,6 +238,7 @@ gs_params make_params(int P, int M, const float* means3D, const float* shs, cons
     g.activation = 0;
     g.sh_half = 0;
     g.index = nullptr;
+    g.visible_out = nullptr;
     return g;
 }
 
@@ -305,6 +306,7 @@ int bin_forward(const gs_settings* s, const Grid& g, const gs_params& gp, int* r
     pa.scale_modifier = s->scale_modifier;
     pa.prefiltered = s->prefiltered; pa.copy_colors = copy_colors;
     pa.radii_out = radii_out;
+    pa.visible_out = gp.visible_out;
     pa.radii = at<int>(geom, gl.radii);
     pa.splat = at<Splat>(geom, gl.splat);
     pa.tiles_touched = at<uint32_t>(geom, gl.tiles_touched);

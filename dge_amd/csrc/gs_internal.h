@@ -214,6 +214,7 @@ struct PreprocessArgs {
     float tanfovx, tanfovy, fx, fy, scale_modifier;
     int prefiltered, copy_colors;
     int* radii_out;
+    uint8_t* visible_out;  // optional (radii > 0) bytes
     int* radii;
     Splat* splat;
     uint32_t* tiles_touched;

@@ -230,6 +230,7 @@ __global__ __launch_bounds__(256) void k_preprocess(PreprocessArgs a) {
         // (and layout queries); the caller's radii serve everything else
         if (!a.rect_packed || !a.radii_out) a.radii[idx] = radius_out;
         if (a.radii_out) a.radii_out[idx] = radius_out;
+        if (a.visible_out) a.visible_out[idx] = radius_out > 0;
         a.tiles_touched[idx] = touched;
         a.clamped[idx] = clamp_bits;
         a.depth_key[idx] = key;

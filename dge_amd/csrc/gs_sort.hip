@@ -134,7 +134,10 @@ __global__ __launch_bounds__(256) void k_radix_digit_scan(uint32_t* __restrict__
 // the first pass of the tile sort, then carried as one 8-byte value.
 enum ValMode { kValU32 = 0, kValPairFirst = 1, kValPair = 2 };
 
-template <int BITS, int IPT, bool IDV, int VM>
+// WK: the sorted keys are written (every pass but the last tile-sort pass).  Without them the block
+// stages only the digit (u16), and the per-wave digit counters are u16 throughout (<= 256*IPT), so
+// the single-pass tile sort fits three workgroups per CU (52 KB of LDS instead of 68).
+template <int BITS, int IPT, bool IDV, int VM, bool WK = true>
 __global__ __launch_bounds__(256) void k_radix_scatter(const uint32_t* __restrict__ keys_in,
                                                        const void* __restrict__ vals_in_,
                                                        uint32_t* __restrict__ keys_out, void* __restrict__ vals_out_,
@@ -149,7 +152,9 @@ __global__ __launch_bounds__(256) void k_radix_scatter(const uint32_t* __restric
     V* vals_out = static_cast<V*>(vals_out_);
     constexpr int NDIG = 1 << BITS;
     constexpr int PER = NDIG >= 256 ? NDIG / 256 : 1;
-    __shared__ uint32_t cnt[4][NDIG];
+    using C = uint16_t;
+    static_assert(256 * IPT <= 65535, "u16 digit counters");
+    __shared__ C cnt[4][NDIG];
     __shared__ uint32_t dbase[NDIG];
     __shared__ uint32_t lds4[4];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -201,7 +206,7 @@ __global__ __launch_bounds__(256) void k_radix_scatter(const uint32_t* __restric
         const uint32_t rank = (uint32_t)__popcll(peers & lanemask_lt());
         const uint32_t old = cnt[w][d];
         loc[it] = old + rank;
-        if (valid && rank == 0) cnt[w][d] = old + (uint32_t)__popcll(peers);
+        if (valid && rank == 0) cnt[w][d] = (C)(old + (uint32_t)__popcll(peers));
     }
     __syncthreads();
     // block-local digit-major order: run of digit d starts at bstart[d] (scan of the block's digit
@@ -223,10 +228,10 @@ __global__ __launch_bounds__(256) void k_radix_scatter(const uint32_t* __restric
             const int d = tid * PER + i;
             if (d < NDIG) {
                 const uint32_t c0 = cnt[0][d], c1 = cnt[1][d], c2 = cnt[2][d];
-                cnt[0][d] = run;
-                cnt[1][d] = run + c0;
-                cnt[2][d] = run + c0 + c1;
-                cnt[3][d] = run + c0 + c1 + c2;
+                cnt[0][d] = (C)run;
+                cnt[1][d] = (C)(run + c0);
+                cnt[2][d] = (C)(run + c0 + c1);
+                cnt[3][d] = (C)(run + c0 + c1 + c2);
                 dbase[d] = dbase[d] + hist[(size_t)d * nb + blockIdx.x] - run;
             }
             run += tot[i];
@@ -235,7 +240,8 @@ __global__ __launch_bounds__(256) void k_radix_scatter(const uint32_t* __restric
     __syncthreads();
     // stage the block in digit-major order, then store it with consecutive lanes on consecutive
     // positions of each digit run (coalesced) instead of one scattered element per lane
-    __shared__ uint32_t s_key[256 * IPT];
+    using SK = typename std::conditional<WK, uint32_t, uint16_t>::type;  // staged key, or its digit
+    __shared__ SK s_key[256 * IPT];
     __shared__ V s_val[256 * IPT];
 #pragma unroll
     for (int it = 0; it < IPT; ++it) {
@@ -243,7 +249,7 @@ __global__ __launch_bounds__(256) void k_radix_scatter(const uint32_t* __restric
         if (idx < n) {
             const uint32_t d = (key[it] >> shift) & (NDIG - 1);
             const uint32_t lp = cnt[w][d] + loc[it];
-            s_key[lp] = key[it];
+            s_key[lp] = WK ? (SK)key[it] : (SK)d;
             s_val[lp] = val[it];
         }
     }
@@ -252,8 +258,8 @@ __global__ __launch_bounds__(256) void k_radix_scatter(const uint32_t* __restric
     const int nvalid = n - b0 < (uint32_t)(256 * IPT) ? (int)(n - b0) : 256 * IPT;
     for (int i = tid; i < nvalid; i += 256) {
         const uint32_t k = s_key[i];
-        const uint32_t pos = dbase[(k >> shift) & (NDIG - 1)] + (uint32_t)i;
-        if (keys_out) keys_out[pos] = k;  // (not needed after the last tile-sort pass)
+        const uint32_t pos = dbase[WK ? (k >> shift) & (NDIG - 1) : k] + (uint32_t)i;
+        if (WK) keys_out[pos] = k;
         vals_out[pos] = s_val[i];
     }
 }
@@ -268,7 +274,10 @@ static void radix_pass(const uint32_t* kin, const void* vin, uint32_t* kout, voi
 #define GS_SCATTER(IDV, VM)                                                                                   \
     hipLaunchKernelGGL((k_radix_scatter<BITS, IPT, IDV, VM>), dim3(nb), dim3(256), 0, s, kin, vin, kout, vout,  \
                        gauss_by_slot, n, shift, hist, totals, nb, ranges, bias_not)
-    if (vm == kValPairFirst) GS_SCATTER(true, kValPairFirst);
+    if (vm == kValPairFirst && !kout)  // the last tile-sort pass: no sorted keys
+        hipLaunchKernelGGL((k_radix_scatter<BITS, IPT, true, kValPairFirst, false>), dim3(nb), dim3(256), 0, s, kin,
+                           vin, kout, vout, gauss_by_slot, n, shift, hist, totals, nb, ranges, bias_not);
+    else if (vm == kValPairFirst) GS_SCATTER(true, kValPairFirst);
     else if (vm == kValPair) GS_SCATTER(false, kValPair);
     else if (idv) GS_SCATTER(true, kValU32);
     else GS_SCATTER(false, kValU32);

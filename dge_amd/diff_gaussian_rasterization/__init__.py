@@ -98,13 +98,14 @@ class _RasterizeGaussiansFused(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, xyz, means2D, f_dc, f_rest, colors, raw_opacity, raw_scaling, raw_rotation, raster_settings,
-                index=None):
+                index=None, visible=None):
         rs = raster_settings
         args = (rs.bg, xyz, f_dc, f_rest, colors, raw_opacity, raw_scaling, raw_rotation, rs.scale_modifier,
                 rs.viewmatrix, rs.projmatrix, rs.tanfovx, rs.tanfovy, rs.image_height, rs.image_width, rs.sh_degree,
                 rs.campos, rs.prefiltered, rs.debug)
         num_rendered, color, depth, radii, geomBuffer, binningBuffer, imgBuffer = _call_with_snapshot(
-            lambda *a: _C.rasterize_gaussians_fused(*a, index=index), args, rs.debug, "snapshot_fw.dump", "forward")
+            lambda *a: _C.rasterize_gaussians_fused(*a, index=index, visible=visible), args, rs.debug,
+            "snapshot_fw.dump", "forward")
         ctx.raster_settings = rs
         ctx.index = index
         ctx.num_rendered = num_rendered
@@ -117,7 +118,7 @@ class _RasterizeGaussiansFused(torch.autograd.Function):
     @staticmethod
     def backward(ctx, grad_out_color, grad_radii, grad_depth):
         if grad_out_color is None:
-            return (None,) * 10
+            return (None,) * 11
         rs = ctx.raster_settings
         (xyz, f_dc, f_rest, colors, raw_opacity, raw_scaling, raw_rotation, radii, geomBuffer, binningBuffer,
          imgBuffer) = ctx.saved_tensors
@@ -193,7 +194,7 @@ class _RasterizeGaussiansFused(torch.autograd.Function):
             d_rot = None
         if "sh" in into:
             d_dc = d_rest = None
-        return d_xyz, d_m2, d_dc, d_rest, d_col, d_op, d_sc, d_rot, None, None
+        return d_xyz, d_m2, d_dc, d_rest, d_col, d_op, d_sc, d_rot, None, None, None
 
 
 _FUSED_GRAD_ACCUM = os.environ.get("DGE_AMD_FUSED_GRAD_ACCUM", "1") != "0"
@@ -292,7 +293,7 @@ def _into_target(p, mode, direct, zero=False):
 
 
 def rasterize_gaussian_model(xyz, means2D, features_dc, features_rest, colors_precomp, raw_opacity, raw_scaling,
-                             raw_rotation, raster_settings, index=None):
+                             raw_rotation, raster_settings, index=None, visible=None):
     """(color, radii, depth) of a GaussianModel given its raw tensors (_xyz, _features_dc, _features_rest or
     colors_precomp, _opacity, _scaling, _rotation); activations are applied in-kernel.  `index` (int32,
     ascending): render only those rows — the model's `localize` subset pc[mask] — gathering them
@@ -301,7 +302,7 @@ def rasterize_gaussian_model(xyz, means2D, features_dc, features_rest, colors_pr
     return _RasterizeGaussiansFused.apply(
         xyz, means2D, empty if features_dc is None else features_dc, empty if features_rest is None else features_rest,
         empty if colors_precomp is None else colors_precomp, raw_opacity, raw_scaling, raw_rotation, raster_settings,
-        index)
+        index, visible)
 
 
 class GaussianRasterizationSettings(NamedTuple):

@@ -165,12 +165,14 @@ def _render_fused(viewpoint_camera, pc, pipe, bg_color, scaling_modifier=1.0, ov
         f_dc, f_rest, colors = pc._features_dc, pc._features_rest, None
     else:
         f_dc, f_rest, colors = None, None, override_color.float()
+    visible = torch.empty(n, dtype=torch.bool, device=xyz.device)  # radii > 0, written by the preprocess
     rendered_image, radii, depth = rasterize_gaussian_model(xyz, screenspace_points, f_dc, f_rest, colors,
-                                                            pc._opacity, pc._scaling, pc._rotation, rs, index)
+                                                            pc._opacity, pc._scaling, pc._rotation, rs, index,
+                                                            visible)
     return {
         "render": rendered_image,
         "viewspace_points": screenspace_points,
-        "visibility_filter": radii > 0,
+        "visibility_filter": visible,
         "radii": radii,
         "depth_3dgs": depth,
     }

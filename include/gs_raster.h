@@ -132,6 +132,8 @@ typedef struct gs_params {
                                      in-kernel).  The backward then writes the parameter-shaped
                                      gradients (means3D, sh, opacity, scales, rotations, cov3D) at
                                      those rows only; means2D / colors / radii stay [P]. */
+    uint8_t *visible_out;         /* forward only: NULL, or [P] bytes set to (radii > 0) — render()'s
+                                     visibility_filter as a bool tensor, without a separate pass */
 } gs_params;
 
 /* gs_grads.accumulate bits: output i is ADDED to (out += grad) instead of

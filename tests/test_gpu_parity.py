@@ -294,6 +294,8 @@ def test_fused_raw_parameter_path_matches_getter_path(cuda_device, monkeypatch, 
         if override:
             oc = torch.rand(20_000, 3, generator=torch.Generator().manual_seed(2)).to(dev)
         pkg = render(cam, sc, PipelineParams(), torch.tensor([0.1, 0.0, 0.2], device=dev), override_color=oc)
+        assert torch.equal(pkg["visibility_filter"], pkg["radii"] > 0)  # (fused: written by the preprocess)
+        assert pkg["visibility_filter"].dtype == torch.bool
         (pkg["render"] * G).sum().backward()
         grads = [None if p.grad is None else p.grad.cpu().numpy() for p in sc.parameters()]
         outs.append((pkg["render"].detach().cpu().numpy(), pkg["radii"].cpu().numpy(),
