@@ -62,6 +62,7 @@ __device__ __forceinline__ uint64_t wave_location() {
 
 constexpr int kRound = kBlendRound;  // list entries per round: 4 per lane
 constexpr int kGroup = 4;    // blend entries per unrolled step (LDS is padded to a multiple)
+constexpr int kFcmpOGT = 2;  // llvm::CmpInst::FCMP_OGT, the predicate of __builtin_amdgcn_fcmpf
 
 // One list entry as gathered from the geometry buffer.
 struct Entry {
@@ -122,22 +123,33 @@ __device__ __forceinline__ void pixel_alpha2(f2v x, f2v y, f2v cx, f2v cy, f2v c
     ok1 = !(power.y > 0.0f) && !(alpha.y < 1.0f / 255.0f);
 }
 
-// The sequential part of blend_step once the entry's alpha test is done.
-__device__ __forceinline__ bool blend_chain(bool ok, float alpha, float4 fe, uint32_t pos, bool& done, float& T,
-                                           float& C0, float& C1, float& C2, float& D, uint32_t& last) {
-    const bool hit = ok && !done;
-    const float test_T = T * (1 - alpha);
-    const bool stop = hit && test_T < 0.0001f;
-    const bool use = hit && !stop;
-    done = done || stop;
-    const float w = use ? alpha * T : 0.0f;
-    C0 = C0 + fe.x * w;
-    C1 = C1 + fe.y * w;
-    C2 = C2 + fe.z * w;
-    D = D + fe.w * w;
-    T = use ? test_T : T;
-    last = use ? pos : last;
-    return use;
+// The sequential part of blend_step once the entry's alpha test is done, on a
+// signed transmittance: Ts = T while the pixel is live, Ts = -T once it has
+// saturated (the reference's `done`), so the whole per-entry chain is VALU:
+//   a' = ok ? alpha : 0                 (a skipped entry multiplies T by 1, exactly)
+//   tT = Ts * (1 - a')                  (<= 0 once saturated: 1 - a' >= 0.01)
+//   use-or-skip <=> tT >= 1e-4          (live and !stop, forward.cu:350-354)
+//   Ts = (tT >= 1e-4) ? tT : -|Ts|       (a stop keeps T and marks the pixel done)
+//   w  = (tT >= 1e-4) ? a' * Ts : 0     (w > 0 exactly when the entry is blended:
+//                                         a' >= 1/255, T >= 1e-4 then)
+// T, the colour sums and `last` are bit-identical to blend_step's; |Ts| is the
+// pixel's T.  The colour and depth sums are two packed pairs (C0, C1), (C2, D):
+// one v_pk_fma each against the entry's (r, g) and (b, depth), aligned register
+// pairs after the 16-B LDS read; fused multiply-adds, as `C + f * w` contracts
+// to (forward.cu:355-356 under nvcc's default fmad).  A skipped entry adds
+// f * 0 (f finite).  Returns w, so the caller's "blended by some pixel" vote is
+// one compare.
+__device__ __forceinline__ float blend_chain(float a, float4 fe, uint32_t pos, float& Ts, f2v& C01, f2v& C2D,
+                                           uint32_t& last) {
+    const float tT = Ts * (1.0f - a);
+    const bool go = tT >= 0.0001f;
+    const float w = go ? a * Ts : 0.0f;
+    Ts = go ? tT : -fabsf(Ts);
+    const f2v w2 = {w, w};
+    C01 = __builtin_elementwise_fma(f2v{fe.x, fe.y}, w2, C01);
+    C2D = __builtin_elementwise_fma(f2v{fe.z, fe.w}, w2, C2D);
+    last = w > 0.0f ? pos : last;
+    return w;
 }
 
 // Dispatch order of the blend: tiles by list length, longest first (coarse
@@ -198,9 +210,9 @@ __global__ __launch_bounds__(64) void k_render_fwd(RenderArgs a) {
 
     const uint2 range = a.ranges[tile];
     uint64_t* used = a.used + (size_t)used_base(range.x, tile) * 4 + quad;
-    float T = 1.0f, C0 = 0.f, C1 = 0.f, C2 = 0.f, D = 0.f;
+    float Ts = inside ? 1.0f : -1.0f;  // signed transmittance (blend_chain): < 0 once done
+    f2v C01 = {0.f, 0.f}, C2D = {0.f, 0.f};  // (C0, C1), (C2, depth)
     uint32_t last = 0;
-    bool done = !inside;
     const uint64_t t_start = a.diag ? __builtin_amdgcn_s_memrealtime() : 0;
     const uint64_t c_start = a.diag ? __builtin_amdgcn_s_memtime() : 0;
     uint64_t c_blend = 0;
@@ -242,7 +254,7 @@ __global__ __launch_bounds__(64) void k_render_fwd(RenderArgs a) {
             used[(size_t)(pend_rel / 64 + lane) * 4] = pend_word;  // (the list's own words only)
     };
     for (uint32_t b = range.x; b < range.y; b += kRound) {
-        if (!__any(!done)) break;
+        if (!__any(Ts > 0.0f)) break;
         const uint64_t r0 = a.diag ? __builtin_amdgcn_s_memtime() : 0;
         // cull against the quadrant, compact survivors in list order (i-major, lane-minor)
         int nk = 0;
@@ -286,7 +298,7 @@ __global__ __launch_bounds__(64) void k_render_fwd(RenderArgs a) {
         load_ids(b + 2 * kRound, ids);
         {  // (T, C) at the segment boundaries of the backward replay (every round start)
             const uint32_t k = (b - range.x) / kSegLen;
-            if (k > 0) ckpt[(size_t)k * 256 + lane] = make_float4(T, C0, C1, C2);
+            if (k > 0) ckpt[(size_t)k * 256 + lane] = make_float4(fabsf(Ts), C01.x, C01.y, C2D.x);
         }
         store_words();
         if (lane <= kRound / kGroup) s_gused[lane] = 0u;  // (groups past an early exit stay 0)
@@ -294,7 +306,7 @@ __global__ __launch_bounds__(64) void k_render_fwd(RenderArgs a) {
 
         const uint64_t c0 = a.diag ? __builtin_amdgcn_s_memtime() : 0;
         for (int j = 0; j < nk; j += kGroup) {
-            if (!__any(!done)) break;
+            if (!__any(Ts > 0.0f)) break;
             uint32_t gm = 0u;  // (uniform: scalar ops beside the blend's vector ones)
 #pragma unroll
             for (int u = 0; u < kGroup; u += 2) {
@@ -303,11 +315,10 @@ __global__ __launch_bounds__(64) void k_render_fwd(RenderArgs a) {
                 const auto ld2 = [&](const float* f) { return *reinterpret_cast<const f2v*>(f + j + u); };
                 pixel_alpha2(ld2(s_x), ld2(s_y), ld2(s_cx), ld2(s_cy), ld2(s_cz), ld2(s_op), pfx, pfy, dx2, dy2, G2,
                              al, ok0, ok1);
-                const bool use0 = blend_chain(ok0, al.x, s_rgbd[j + u], s_pos[j + u], done, T, C0, C1, C2, D, last);
-                gm |= (__ballot(use0) != 0ull ? 1u : 0u) << u;
-                const bool use1 =
-                    blend_chain(ok1, al.y, s_rgbd[j + u + 1], s_pos[j + u + 1], done, T, C0, C1, C2, D, last);
-                gm |= (__ballot(use1) != 0ull ? 1u : 0u) << (u + 1);
+                const float w0 = blend_chain(ok0 ? al.x : 0.0f, s_rgbd[j + u], s_pos[j + u], Ts, C01, C2D, last);
+                gm |= (__builtin_amdgcn_fcmpf(w0, 0.0f, kFcmpOGT) != 0ull ? 1u : 0u) << u;
+                const float w1 = blend_chain(ok1 ? al.y : 0.0f, s_rgbd[j + u + 1], s_pos[j + u + 1], Ts, C01, C2D, last);
+                gm |= (__builtin_amdgcn_fcmpf(w1, 0.0f, kFcmpOGT) != 0ull ? 1u : 0u) << (u + 1);
             }
             s_gused[j / kGroup] = gm;
         }
@@ -326,16 +337,17 @@ __global__ __launch_bounds__(64) void k_render_fwd(RenderArgs a) {
     store_words();
 
     // slot 0: the final state (an empty tile's range is (0, 0): it owns no slot and has no replay)
-    if (range.y > range.x) ckpt[lane] = make_float4(T, C0, C1, C2);
+    const float T = fabsf(Ts);
+    if (range.y > range.x) ckpt[lane] = make_float4(T, C01.x, C01.y, C2D.x);
     if (inside) {
         const size_t pix = (size_t)a.W * py + px;
         const size_t HW = (size_t)a.W * a.H;
         a.final_T[pix] = T;
         a.n_contrib[pix] = last;
-        a.out_color[pix] = C0 + T * a.bg[0];
-        a.out_color[HW + pix] = C1 + T * a.bg[1];
-        a.out_color[2 * HW + pix] = C2 + T * a.bg[2];
-        a.out_depth[pix] = D;
+        a.out_color[pix] = C01.x + T * a.bg[0];
+        a.out_color[HW + pix] = C01.y + T * a.bg[1];
+        a.out_color[2 * HW + pix] = C2D.x + T * a.bg[2];
+        a.out_depth[pix] = C2D.y;
     }
     const uint32_t m = wave_max_u32(inside ? last : 0u);
     if (m) {  // the backward replay's work items for this quadrant: (tile, segment << 2 | quadrant)
