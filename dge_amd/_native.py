@@ -11,7 +11,8 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libgs_raster.so")
+# DGE_AMD_LIB: an alternative in-tree build of the same ABI (A/B kernel experiments)
+LIB_PATH = os.environ.get("DGE_AMD_LIB") or os.path.join(_HERE, "lib", "libgs_raster.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "gs_raster.h")
 
 GS_OK = 0

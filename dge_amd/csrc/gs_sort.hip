@@ -76,7 +76,9 @@ __device__ __forceinline__ uint32_t key_bias(const uint32_t* __restrict__ bias_n
 // ---------------------------------------------------------------------
 // radix sort: histogram -> per-digit scan -> stable scatter
 // ---------------------------------------------------------------------
-// Per-block digit counts (integer LDS atomics: the counts do not depend on the order).
+// Per-block digit counts (integer LDS atomics: the counts do not depend on the order),
+// stored block-major: hist[b * NDIG + d], one coalesced row per block (a digit-major
+// table made every block write NDIG scattered words, one cache line each).
 template <int BITS, int IPT>
 __global__ __launch_bounds__(256) void k_radix_hist(const uint32_t* __restrict__ keys, uint32_t n, int shift,
                                                     uint32_t* __restrict__ hist, int nb,
@@ -100,33 +102,46 @@ __global__ __launch_bounds__(256) void k_radix_hist(const uint32_t* __restrict__
         if (idx < n) atomicAdd(&cnt[(key[it] >> shift) & (NDIG - 1)], 1u);
     }
     __syncthreads();
-    for (int d = tid; d < NDIG; d += 256) hist[(size_t)d * nb + blockIdx.x] = cnt[d];
+    for (int d = tid; d < NDIG; d += 256) hist[(size_t)blockIdx.x * NDIG + d] = cnt[d];
 }
 
-// One workgroup per digit: exclusive scan of hist[d][0..nb) in place,
-// totals[d] = digit count.
-__global__ __launch_bounds__(256) void k_radix_digit_scan(uint32_t* __restrict__ hist, int nb,
-                                                          uint32_t* __restrict__ totals) {
-    __shared__ uint32_t lds4[4];
-    uint32_t* row = hist + (size_t)blockIdx.x * nb;
-    const int per = (nb + 255) / 256;
-    const int beg = threadIdx.x * per;
+// Exclusive scan of every digit's column hist[0..nb)[d] in place, totals[d] =
+// digit count.  One 1024-thread workgroup per 16 digits: thread (row group g,
+// digit dl) sums rows [g*per, (g+1)*per) of its digit (a wave load covers 4 rows
+// x 64 B), the 64 row-group sums are scanned in LDS, then the rows are
+// rewritten.  (c2: 880 tile-sort rows -> 14 per thread.)
+constexpr int kScanDigits = 16, kScanGroups = 64;
+__global__ __launch_bounds__(1024) void k_radix_digit_scan(uint32_t* __restrict__ hist, int nb, int ndig,
+                                                           uint32_t* __restrict__ totals) {
+    __shared__ uint32_t part[kScanGroups][kScanDigits];
+    const int dl = threadIdx.x & (kScanDigits - 1), g = threadIdx.x / kScanDigits;
+    const int d = blockIdx.x * kScanDigits + dl;
+    const int per = (nb + kScanGroups - 1) / kScanGroups;
+    const int r0 = g * per, r1 = min(nb, r0 + per);
     uint32_t s = 0;
-    for (int i = 0; i < per; ++i) {
-        const int j = beg + i;
-        if (j < nb) s += row[j];
+    if (d < ndig) {
+#pragma unroll 4
+        for (int r = r0; r < r1; ++r) s += hist[(size_t)r * ndig + d];
     }
-    uint32_t total;
-    uint32_t run = block_exclusive_scan(s, lds4, total);
-    for (int i = 0; i < per; ++i) {
-        const int j = beg + i;
-        if (j < nb) {
-            const uint32_t c = row[j];
-            row[j] = run;
+    part[g][dl] = s;
+    __syncthreads();
+    uint32_t run = 0, total = 0;
+#pragma unroll 8
+    for (int i = 0; i < kScanGroups; ++i) {
+        const uint32_t v = part[i][dl];
+        run += i < g ? v : 0u;
+        total += v;
+    }
+    if (d < ndig) {
+#pragma unroll 4
+        for (int r = r0; r < r1; ++r) {
+            const size_t at = (size_t)r * ndig + d;
+            const uint32_t c = hist[at];
+            hist[at] = run;
             run += c;
         }
+        if (g == 0) totals[d] = total;
     }
-    if (threadIdx.x == 0) totals[blockIdx.x] = total;
 }
 
 // Value modes of the scatter: u32 values (IDV: the element index), or a packed
@@ -232,7 +247,7 @@ __global__ __launch_bounds__(256) void k_radix_scatter(const uint32_t* __restric
                 cnt[1][d] = (C)(run + c0);
                 cnt[2][d] = (C)(run + c0 + c1);
                 cnt[3][d] = (C)(run + c0 + c1 + c2);
-                dbase[d] = dbase[d] + hist[(size_t)d * nb + blockIdx.x] - run;
+                dbase[d] = dbase[d] + hist[(size_t)blockIdx.x * NDIG + d] - run;
             }
             run += tot[i];
         }
@@ -270,7 +285,7 @@ static void radix_pass(const uint32_t* kin, const void* vin, uint32_t* kout, voi
                        uint2* ranges, const uint32_t* bias_not, hipStream_t s) {
     constexpr int NDIG = 1 << BITS;
     hipLaunchKernelGGL((k_radix_hist<BITS, IPT>), dim3(nb), dim3(256), 0, s, kin, n, shift, hist, nb, bias_not);
-    hipLaunchKernelGGL(k_radix_digit_scan, dim3(NDIG), dim3(256), 0, s, hist, nb, totals);
+    hipLaunchKernelGGL(k_radix_digit_scan, dim3(div_up(NDIG, kScanDigits)), dim3(1024), 0, s, hist, nb, NDIG, totals);
 #define GS_SCATTER(IDV, VM)                                                                                   \
     hipLaunchKernelGGL((k_radix_scatter<BITS, IPT, IDV, VM>), dim3(nb), dim3(256), 0, s, kin, vin, kout, vout,  \
                        gauss_by_slot, n, shift, hist, totals, nb, ranges, bias_not)
