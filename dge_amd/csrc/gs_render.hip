@@ -305,22 +305,73 @@ __global__ __launch_bounds__(64) void k_render_fwd(RenderArgs a) {
         __syncthreads();
 
         const uint64_t c0 = a.diag ? __builtin_amdgcn_s_memtime() : 0;
-        for (int j = 0; j < nk; j += kGroup) {
-            if (!__any(Ts > 0.0f)) break;
+        // The alpha-test operands of a group are read one group ahead (ping-pong A/B, no register
+        // copies), so their LDS latency overlaps the previous group's blend.  A group's colour and
+        // position reads are issued before the next group's prefetch: LDS reads retire in order, so
+        // waiting for them does not wait for the prefetch.  Reads past nk land in the padding or
+        // stale slots (index < kRound + kGroup) and are never used.
+        struct AlphaOps { f2v x[2], y[2], cx[2], cy[2], cz[2], op[2]; };
+        struct ColourOps { float4 rgbd[kGroup]; uint32_t pos[kGroup]; };
+        const auto load_alpha = [&](int j, AlphaOps& g) {
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const auto ld2 = [&](const float* f) { return *reinterpret_cast<const f2v*>(f + j + 2 * h); };
+                g.x[h] = ld2(s_x);
+                g.y[h] = ld2(s_y);
+                g.cx[h] = ld2(s_cx);
+                g.cy[h] = ld2(s_cy);
+                g.cz[h] = ld2(s_cz);
+                g.op[h] = ld2(s_op);
+            }
+        };
+        const auto load_colour = [&](int j, ColourOps& c) {
+#pragma unroll
+            for (int u = 0; u < kGroup; ++u) {
+                c.rgbd[u] = s_rgbd[j + u];
+                c.pos[u] = s_pos[j + u];
+            }
+        };
+        const auto blend_group = [&](int j, const AlphaOps& g, const ColourOps& c) {
             uint32_t gm = 0u;  // (uniform: scalar ops beside the blend's vector ones)
 #pragma unroll
             for (int u = 0; u < kGroup; u += 2) {
                 f2v al, dx2, dy2, G2;
                 bool ok0, ok1;
-                const auto ld2 = [&](const float* f) { return *reinterpret_cast<const f2v*>(f + j + u); };
-                pixel_alpha2(ld2(s_x), ld2(s_y), ld2(s_cx), ld2(s_cy), ld2(s_cz), ld2(s_op), pfx, pfy, dx2, dy2, G2,
-                             al, ok0, ok1);
-                const float w0 = blend_chain(ok0 ? al.x : 0.0f, s_rgbd[j + u], s_pos[j + u], Ts, C01, C2D, last);
+                const int h = u / 2;
+                pixel_alpha2(g.x[h], g.y[h], g.cx[h], g.cy[h], g.cz[h], g.op[h], pfx, pfy, dx2, dy2, G2, al, ok0,
+                             ok1);
+                const float w0 = blend_chain(ok0 ? al.x : 0.0f, c.rgbd[u], c.pos[u], Ts, C01, C2D, last);
                 gm |= (__builtin_amdgcn_fcmpf(w0, 0.0f, kFcmpOGT) != 0ull ? 1u : 0u) << u;
-                const float w1 = blend_chain(ok1 ? al.y : 0.0f, s_rgbd[j + u + 1], s_pos[j + u + 1], Ts, C01, C2D, last);
+                const float w1 = blend_chain(ok1 ? al.y : 0.0f, c.rgbd[u + 1], c.pos[u + 1], Ts, C01, C2D, last);
                 gm |= (__builtin_amdgcn_fcmpf(w1, 0.0f, kFcmpOGT) != 0ull ? 1u : 0u) << (u + 1);
             }
             s_gused[j / kGroup] = gm;
+        };
+        AlphaOps ga, gb;
+        ColourOps cc;
+        // lgkmcnt(0) only (vmcnt 63, expcnt 7: the next round's gathers stay in flight): at the loop
+        // head nothing is outstanding in LDS, so the compiler's waits inside count the colour reads
+        // exactly instead of draining the prefetch (its loop-carried state is conservative)
+        constexpr unsigned kWaitLds = 0xC07F;
+        load_alpha(0, ga);
+        __builtin_amdgcn_s_waitcnt(kWaitLds);
+        // (scheduling barriers keep the compiler from merging or reordering the reads across them)
+        for (int j = 0; j < nk; j += 2 * kGroup) {
+            if (!__any(Ts > 0.0f)) break;
+            load_colour(j, cc);
+            __builtin_amdgcn_sched_barrier(0);
+            load_alpha(j + kGroup, gb);
+            __builtin_amdgcn_sched_barrier(0);
+            blend_group(j, ga, cc);
+            __builtin_amdgcn_sched_barrier(0);
+            if (j + kGroup >= nk || !__any(Ts > 0.0f)) break;
+            load_colour(j + kGroup, cc);
+            __builtin_amdgcn_sched_barrier(0);
+            load_alpha(j + 2 * kGroup, ga);
+            __builtin_amdgcn_sched_barrier(0);
+            blend_group(j + kGroup, gb, cc);
+            __builtin_amdgcn_sched_barrier(0);
+            __builtin_amdgcn_s_waitcnt(kWaitLds);  // (the prefetch of ga: issued a whole group ago)
         }
         if (a.diag) c_blend += __builtin_amdgcn_s_memtime() - c0;
         __syncthreads();
