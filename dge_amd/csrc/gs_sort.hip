@@ -118,27 +118,48 @@ __global__ __launch_bounds__(1024) void k_radix_digit_scan(uint32_t* __restrict_
     const int d = blockIdx.x * kScanDigits + dl;
     const int per = (nb + kScanGroups - 1) / kScanGroups;
     const int r0 = g * per, r1 = min(nb, r0 + per);
+    // up to kScanRegs rows per thread are held in registers: every load in flight at once, one
+    // read and one write per element (c2: 14 tile-sort rows, 8 depth-sort rows); longer columns loop
+    constexpr int kScanRegs = 16;
+    const bool in_regs = per <= kScanRegs;
+    uint32_t v[kScanRegs];
     uint32_t s = 0;
     if (d < ndig) {
+        if (in_regs) {
+#pragma unroll
+            for (int i = 0; i < kScanRegs; ++i) {
+                v[i] = r0 + i < r1 ? hist[(size_t)(r0 + i) * ndig + d] : 0u;
+                s += v[i];
+            }
+        } else {
 #pragma unroll 4
-        for (int r = r0; r < r1; ++r) s += hist[(size_t)r * ndig + d];
+            for (int r = r0; r < r1; ++r) s += hist[(size_t)r * ndig + d];
+        }
     }
     part[g][dl] = s;
     __syncthreads();
     uint32_t run = 0, total = 0;
 #pragma unroll 8
     for (int i = 0; i < kScanGroups; ++i) {
-        const uint32_t v = part[i][dl];
-        run += i < g ? v : 0u;
-        total += v;
+        const uint32_t pv = part[i][dl];
+        run += i < g ? pv : 0u;
+        total += pv;
     }
     if (d < ndig) {
+        if (in_regs) {
+#pragma unroll
+            for (int i = 0; i < kScanRegs; ++i) {
+                if (r0 + i < r1) hist[(size_t)(r0 + i) * ndig + d] = run;
+                run += v[i];
+            }
+        } else {
 #pragma unroll 4
-        for (int r = r0; r < r1; ++r) {
-            const size_t at = (size_t)r * ndig + d;
-            const uint32_t c = hist[at];
-            hist[at] = run;
-            run += c;
+            for (int r = r0; r < r1; ++r) {
+                const size_t at = (size_t)r * ndig + d;
+                const uint32_t c = hist[at];
+                hist[at] = run;
+                run += c;
+            }
         }
         if (g == 0) totals[d] = total;
     }
@@ -369,10 +390,18 @@ __global__ __launch_bounds__(256) void k_scan_reduce(EmitArgs a) {
     __shared__ uint32_t lds4[4];
     uint32_t s = 0;
     const uint32_t base = blockIdx.x * (uint32_t)kScanTile;
+    // (clamped loads, all issued before the first use: a guarded load per iteration was waited
+    // for one at a time)
+    uint32_t v[kScanIPT];
 #pragma unroll
     for (int it = 0; it < kScanIPT; ++it) {
         const uint32_t r = base + it * 256 + threadIdx.x;
-        if (r < (uint32_t)a.P) s += rect_count(a.order[r].x, a.rect_packed);
+        v[it] = a.order[r < (uint32_t)a.P ? r : (uint32_t)a.P - 1u].x;
+    }
+#pragma unroll
+    for (int it = 0; it < kScanIPT; ++it) {
+        const uint32_t r = base + it * 256 + threadIdx.x;
+        s += r < (uint32_t)a.P ? rect_count(v[it], a.rect_packed) : 0u;
     }
     uint32_t total;
     block_exclusive_scan(s, lds4, total);
