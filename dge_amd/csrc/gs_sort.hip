@@ -77,11 +77,17 @@ __device__ __forceinline__ uint32_t key_bias(const uint32_t* __restrict__ bias_n
 // radix sort: histogram -> per-digit scan -> stable scatter
 // ---------------------------------------------------------------------
 // Per-block digit counts (integer LDS atomics: the counts do not depend on the order),
-// stored block-major: hist[b * NDIG + d], one coalesced row per block (a digit-major
-// table made every block write NDIG scattered words, one cache line each).
+// stored block-major (bm: hist[b * NDIG + d], one coalesced row per block; a
+// digit-major table makes every block write NDIG scattered words, one cache line
+// each) while the column scan stays short — up to kScanBmRows blocks; longer sorts
+// (c4's 10k-block tile sort) keep the digit-major table, whose scan is one
+// workgroup per digit over a contiguous row.
+__host__ __device__ __forceinline__ size_t hist_at(int bm, uint32_t b, uint32_t d, int nb, int ndig) {
+    return bm ? (size_t)b * ndig + d : (size_t)d * nb + b;
+}
 template <int BITS, int IPT>
 __global__ __launch_bounds__(256) void k_radix_hist(const uint32_t* __restrict__ keys, uint32_t n, int shift,
-                                                    uint32_t* __restrict__ hist, int nb,
+                                                    uint32_t* __restrict__ hist, int nb, int bm,
                                                     const uint32_t* __restrict__ bias_not) {
     constexpr int NDIG = 1 << BITS;
     __shared__ uint32_t cnt[NDIG];
@@ -102,7 +108,7 @@ __global__ __launch_bounds__(256) void k_radix_hist(const uint32_t* __restrict__
         if (idx < n) atomicAdd(&cnt[(key[it] >> shift) & (NDIG - 1)], 1u);
     }
     __syncthreads();
-    for (int d = tid; d < NDIG; d += 256) hist[(size_t)blockIdx.x * NDIG + d] = cnt[d];
+    for (int d = tid; d < NDIG; d += 256) hist[hist_at(bm, blockIdx.x, d, nb, NDIG)] = cnt[d];
 }
 
 // Exclusive scan of every digit's column hist[0..nb)[d] in place, totals[d] =
@@ -110,7 +116,8 @@ __global__ __launch_bounds__(256) void k_radix_hist(const uint32_t* __restrict__
 // digit dl) sums rows [g*per, (g+1)*per) of its digit (a wave load covers 4 rows
 // x 64 B), the 64 row-group sums are scanned in LDS, then the rows are
 // rewritten.  (c2: 880 tile-sort rows -> 14 per thread.)
-constexpr int kScanDigits = 16, kScanGroups = 64;
+constexpr int kScanDigits = 16, kScanGroups = 64, kScanRegs = 16;
+constexpr int kScanBmRows = kScanGroups * kScanRegs;  // block-major tables up to this many blocks
 __global__ __launch_bounds__(1024) void k_radix_digit_scan(uint32_t* __restrict__ hist, int nb, int ndig,
                                                            uint32_t* __restrict__ totals) {
     __shared__ uint32_t part[kScanGroups][kScanDigits];
@@ -120,7 +127,6 @@ __global__ __launch_bounds__(1024) void k_radix_digit_scan(uint32_t* __restrict_
     const int r0 = g * per, r1 = min(nb, r0 + per);
     // up to kScanRegs rows per thread are held in registers: every load in flight at once, one
     // read and one write per element (c2: 14 tile-sort rows, 8 depth-sort rows); longer columns loop
-    constexpr int kScanRegs = 16;
     const bool in_regs = per <= kScanRegs;
     uint32_t v[kScanRegs];
     uint32_t s = 0;
@@ -165,6 +171,32 @@ __global__ __launch_bounds__(1024) void k_radix_digit_scan(uint32_t* __restrict_
     }
 }
 
+// One workgroup per digit (digit-major table): exclusive scan of hist[d][0..nb)
+// in place, totals[d] = digit count.
+__global__ __launch_bounds__(256) void k_radix_digit_scan_dm(uint32_t* __restrict__ hist, int nb,
+                                                             uint32_t* __restrict__ totals) {
+    __shared__ uint32_t lds4[4];
+    uint32_t* row = hist + (size_t)blockIdx.x * nb;
+    const int per = (nb + 255) / 256;
+    const int beg = threadIdx.x * per;
+    uint32_t s = 0;
+    for (int i = 0; i < per; ++i) {
+        const int j = beg + i;
+        if (j < nb) s += row[j];
+    }
+    uint32_t total;
+    uint32_t run = block_exclusive_scan(s, lds4, total);
+    for (int i = 0; i < per; ++i) {
+        const int j = beg + i;
+        if (j < nb) {
+            const uint32_t c = row[j];
+            row[j] = run;
+            run += c;
+        }
+    }
+    if (threadIdx.x == 0) totals[blockIdx.x] = total;
+}
+
 // Value modes of the scatter: u32 values (IDV: the element index), or a packed
 // (Gaussian, slot) pair: built from the index and a Gaussian-per-slot array on
 // the first pass of the tile sort, then carried as one 8-byte value.
@@ -179,7 +211,7 @@ __global__ __launch_bounds__(256) void k_radix_scatter(const uint32_t* __restric
                                                        uint32_t* __restrict__ keys_out, void* __restrict__ vals_out_,
                                                        const uint32_t* __restrict__ gauss_by_slot, uint32_t n,
                                                        int shift, const uint32_t* __restrict__ hist,
-                                                       const uint32_t* __restrict__ totals, int nb,
+                                                       const uint32_t* __restrict__ totals, int nb, int bm,
                                                        uint2* __restrict__ ranges,
                                                        const uint32_t* __restrict__ bias_not) {
     using V = typename std::conditional<VM == kValU32, uint32_t, uint2>::type;
@@ -268,7 +300,7 @@ __global__ __launch_bounds__(256) void k_radix_scatter(const uint32_t* __restric
                 cnt[1][d] = (C)(run + c0);
                 cnt[2][d] = (C)(run + c0 + c1);
                 cnt[3][d] = (C)(run + c0 + c1 + c2);
-                dbase[d] = dbase[d] + hist[(size_t)blockIdx.x * NDIG + d] - run;
+                dbase[d] = dbase[d] + hist[hist_at(bm, blockIdx.x, d, nb, NDIG)] - run;
             }
             run += tot[i];
         }
@@ -305,14 +337,19 @@ static void radix_pass(const uint32_t* kin, const void* vin, uint32_t* kout, voi
                        uint32_t n, int shift, bool idv, int vm, uint32_t* hist, uint32_t* totals, int nb,
                        uint2* ranges, const uint32_t* bias_not, hipStream_t s) {
     constexpr int NDIG = 1 << BITS;
-    hipLaunchKernelGGL((k_radix_hist<BITS, IPT>), dim3(nb), dim3(256), 0, s, kin, n, shift, hist, nb, bias_not);
-    hipLaunchKernelGGL(k_radix_digit_scan, dim3(div_up(NDIG, kScanDigits)), dim3(1024), 0, s, hist, nb, NDIG, totals);
+    const int bm = nb <= kScanBmRows ? 1 : 0;
+    hipLaunchKernelGGL((k_radix_hist<BITS, IPT>), dim3(nb), dim3(256), 0, s, kin, n, shift, hist, nb, bm, bias_not);
+    if (bm)
+        hipLaunchKernelGGL(k_radix_digit_scan, dim3(div_up(NDIG, kScanDigits)), dim3(1024), 0, s, hist, nb, NDIG,
+                           totals);
+    else
+        hipLaunchKernelGGL(k_radix_digit_scan_dm, dim3(NDIG), dim3(256), 0, s, hist, nb, totals);
 #define GS_SCATTER(IDV, VM)                                                                                   \
     hipLaunchKernelGGL((k_radix_scatter<BITS, IPT, IDV, VM>), dim3(nb), dim3(256), 0, s, kin, vin, kout, vout,  \
-                       gauss_by_slot, n, shift, hist, totals, nb, ranges, bias_not)
+                       gauss_by_slot, n, shift, hist, totals, nb, bm, ranges, bias_not)
     if (vm == kValPairFirst && !kout)  // the last tile-sort pass: no sorted keys
         hipLaunchKernelGGL((k_radix_scatter<BITS, IPT, true, kValPairFirst, false>), dim3(nb), dim3(256), 0, s, kin,
-                           vin, kout, vout, gauss_by_slot, n, shift, hist, totals, nb, ranges, bias_not);
+                           vin, kout, vout, gauss_by_slot, n, shift, hist, totals, nb, bm, ranges, bias_not);
     else if (vm == kValPairFirst) GS_SCATTER(true, kValPairFirst);
     else if (vm == kValPair) GS_SCATTER(false, kValPair);
     else if (idv) GS_SCATTER(true, kValU32);
