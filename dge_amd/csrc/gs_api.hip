@@ -393,7 +393,7 @@ int bin_forward(const gs_settings* s, const Grid& g, const gs_params& gp, int* r
     tc = tile_sort(at<uint32_t>(bin, bl.key0), at<uint32_t>(bin, bl.key1), at<uint2>(bin, bl.pair0),
                    at<uint2>(bin, bl.pair1), at<uint32_t>(bin, bl.slot_gauss), K, plan.bits,
                    at<uint32_t>(bin, bl.sort_hist), at<uint32_t>(bin, bl.sort_totals), bl.sort_blocks, stream,
-                   at<uint2>(img, il.ranges)); }
+                   at<uint2>(img, il.ranges), at<uint32_t>(img, il.tile_order), g.tiles); }
     GS_LAUNCHED("tile sort");
     if (!tile_sort_writes_ranges(g.tiles)) {
         StageScope sc(ST_RANGES, stream);
@@ -548,6 +548,7 @@ int gs_rasterize_forward_ex(const gs_settings* s, const gs_params* gp, float* ou
         ra.W = g.W; ra.H = g.H; ra.gx = g.gx; ra.gy = g.gy;
         ra.ranges = at<uint2>(img, il.ranges);
         ra.tile_order = at<uint32_t>(img, il.tile_order);
+        ra.order_ready = K > 0 && tile_sort_writes_ranges(g.tiles) ? 1 : 0;
         ra.point_pairs = at<uint2>(bin, bl.point_pairs);
         ra.bwd_items = at<uint2>(bin, bl.bwd_items);
         ra.bwd_count = at<uint32_t>(img, il.bwd_count);

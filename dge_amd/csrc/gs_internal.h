@@ -236,14 +236,16 @@ void launch_mark_visible(int P, const float* means3D, const float* view, uint8_t
 // max_pass_bits per pass; returns the ping-pong index holding the result.
 int radix_sort_aux(uint32_t* key0, uint32_t* key1, uint2* pair0, uint2* pair1, const uint32_t* aux, uint32_t n,
                    int bits, int max_pass_bits, int ipt, uint32_t* hist, uint32_t* totals, int nblocks, hipStream_t s,
-                   uint2* ranges = nullptr, const uint32_t* key_bias_not = nullptr);
+                   uint2* ranges = nullptr, const uint32_t* key_bias_not = nullptr, uint32_t* tile_order = nullptr,
+                   int ntiles = 0);
 // key_bias_not: the preprocess counter slots' ~min key (kCounterStride apart); the first pass sorts
 // (and writes) key - min
 // Stable sort of the K emitted instances on their tile id (key0 in slot
 // order); the values are (Gaussian, slot) pairs built on the first pass from
 // gauss_by_slot.  Returns the buffer index (0/1) holding keys and pairs.
 int tile_sort(uint32_t* key0, uint32_t* key1, uint2* pair0, uint2* pair1, const uint32_t* gauss_by_slot, uint32_t n,
-              int bits, uint32_t* hist, uint32_t* totals, int nblocks, hipStream_t s, uint2* ranges);
+              int bits, uint32_t* hist, uint32_t* totals, int nblocks, hipStream_t s, uint2* ranges,
+              uint32_t* tile_order, int ntiles);  // tile_order: the forward's dispatch order (single pass only)
 // the single-pass tile sort writes the tile ranges itself (and no sorted keys); two passes need k_ranges
 inline bool tile_sort_writes_ranges(int num_tiles) { return tile_sort_plan(num_tiles).passes == 1; }
 
@@ -281,7 +283,8 @@ void launch_ranges(const uint32_t* sorted_tile, int K, uint2* ranges, uint32_t* 
 struct RenderArgs {
     int W, H, gx, gy;
     const uint2* ranges;
-    uint32_t* tile_order;      // written by launch_render_forward's ordering pass
+    uint32_t* tile_order;      // tiles longest list first: by the single-pass tile sort, else k_tile_order
+    int order_ready;           // tile_order already written (the single-pass tile sort did it)
     const uint2* point_pairs;  // per-tile lists: (Gaussian, binning slot)
     const Splat* splat;
     const float* bg;

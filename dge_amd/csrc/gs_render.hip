@@ -433,7 +433,7 @@ __global__ __launch_bounds__(64) void k_render_fwd(RenderArgs a) {
 void launch_render_forward(const RenderArgs& a, hipStream_t s) {
     const int tiles = a.gx * a.gy;
     if (tiles <= 0) return;
-    hipLaunchKernelGGL(k_tile_order, dim3(1), dim3(1024), 0, s, a.ranges, tiles, a.tile_order);
+    if (!a.order_ready) hipLaunchKernelGGL(k_tile_order, dim3(1), dim3(1024), 0, s, a.ranges, tiles, a.tile_order);
     hipLaunchKernelGGL(k_render_fwd, dim3(div_up(tiles, 8) * 32), dim3(64), 0, s, a);
 }
 

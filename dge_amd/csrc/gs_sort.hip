@@ -197,6 +197,16 @@ __global__ __launch_bounds__(256) void k_radix_digit_scan_dm(uint32_t* __restric
     if (threadIdx.x == 0) totals[blockIdx.x] = total;
 }
 
+// What a single-pass tile sort writes besides the permutation: the tile ranges
+// (the digit IS the tile) and, when tile_order is set, the forward's dispatch
+// order — tiles by list length, longest first (the former k_tile_order launch;
+// block 0 has every tile's count in registers when it writes the ranges).
+struct RangeOut {
+    uint2* ranges;
+    uint32_t* tile_order;
+    int ntiles;
+};
+
 // Value modes of the scatter: u32 values (IDV: the element index), or a packed
 // (Gaussian, slot) pair: built from the index and a Gaussian-per-slot array on
 // the first pass of the tile sort, then carried as one 8-byte value.
@@ -212,7 +222,7 @@ __global__ __launch_bounds__(256) void k_radix_scatter(const uint32_t* __restric
                                                        const uint32_t* __restrict__ gauss_by_slot, uint32_t n,
                                                        int shift, const uint32_t* __restrict__ hist,
                                                        const uint32_t* __restrict__ totals, int nb, int bm,
-                                                       uint2* __restrict__ ranges,
+                                                       RangeOut ro,
                                                        const uint32_t* __restrict__ bias_not) {
     using V = typename std::conditional<VM == kValU32, uint32_t, uint2>::type;
     const uint32_t* vals_in = static_cast<const uint32_t*>(vals_in_);
@@ -244,9 +254,36 @@ __global__ __launch_bounds__(256) void k_radix_scatter(const uint32_t* __restric
             if (d < NDIG) dbase[d] = run;
             // single-pass tile sort: the digit is the tile, so its run is the tile's range
             // (identifyTileRanges, rasterizer_impl.cu:105-125; empty tiles keep (0, 0))
-            if (ranges && blockIdx.x == 0 && d < NDIG)
-                ranges[d] = loc[i] ? make_uint2(run, run + loc[i]) : make_uint2(0u, 0u);
+            if (ro.ranges && blockIdx.x == 0 && d < NDIG)
+                ro.ranges[d] = loc[i] ? make_uint2(run, run + loc[i]) : make_uint2(0u, 0u);
             run += loc[i];
+        }
+        if (ro.tile_order && blockIdx.x == 0) {  // (uniform per block: the barriers below are safe)
+            constexpr int kClasses = 64;
+            __shared__ uint32_t s_cls[kClasses];
+            auto cls = [](uint32_t len) { return min(kClasses - 1, (int)(__log2f((float)len + 1.0f) * 3.0f)); };
+            if (tid < kClasses) s_cls[tid] = 0u;
+            __syncthreads();
+#pragma unroll
+            for (int i = 0; i < PER; ++i) {
+                const int d = tid * PER + i;
+                if (d < ro.ntiles) atomicAdd(&s_cls[cls(loc[i])], 1u);
+            }
+            __syncthreads();
+            if (tid == 0) {  // start of each class, longest class first
+                uint32_t acc = 0;
+                for (int c = kClasses - 1; c >= 0; --c) {
+                    const uint32_t m = s_cls[c];
+                    s_cls[c] = acc;
+                    acc += m;
+                }
+            }
+            __syncthreads();
+#pragma unroll
+            for (int i = 0; i < PER; ++i) {
+                const int d = tid * PER + i;
+                if (d < ro.ntiles) ro.tile_order[atomicAdd(&s_cls[cls(loc[i])], 1u)] = (uint32_t)d;
+            }
         }
     }
     __syncthreads();
@@ -335,7 +372,7 @@ __global__ __launch_bounds__(256) void k_radix_scatter(const uint32_t* __restric
 template <int BITS, int IPT>
 static void radix_pass(const uint32_t* kin, const void* vin, uint32_t* kout, void* vout, const uint32_t* gauss_by_slot,
                        uint32_t n, int shift, bool idv, int vm, uint32_t* hist, uint32_t* totals, int nb,
-                       uint2* ranges, const uint32_t* bias_not, hipStream_t s) {
+                       RangeOut ro, const uint32_t* bias_not, hipStream_t s) {
     constexpr int NDIG = 1 << BITS;
     const int bm = nb <= kScanBmRows ? 1 : 0;
     hipLaunchKernelGGL((k_radix_hist<BITS, IPT>), dim3(nb), dim3(256), 0, s, kin, n, shift, hist, nb, bm, bias_not);
@@ -346,10 +383,10 @@ static void radix_pass(const uint32_t* kin, const void* vin, uint32_t* kout, voi
         hipLaunchKernelGGL(k_radix_digit_scan_dm, dim3(NDIG), dim3(256), 0, s, hist, nb, totals);
 #define GS_SCATTER(IDV, VM)                                                                                   \
     hipLaunchKernelGGL((k_radix_scatter<BITS, IPT, IDV, VM>), dim3(nb), dim3(256), 0, s, kin, vin, kout, vout,  \
-                       gauss_by_slot, n, shift, hist, totals, nb, bm, ranges, bias_not)
+                       gauss_by_slot, n, shift, hist, totals, nb, bm, ro, bias_not)
     if (vm == kValPairFirst && !kout)  // the last tile-sort pass: no sorted keys
         hipLaunchKernelGGL((k_radix_scatter<BITS, IPT, true, kValPairFirst, false>), dim3(nb), dim3(256), 0, s, kin,
-                           vin, kout, vout, gauss_by_slot, n, shift, hist, totals, nb, bm, ranges, bias_not);
+                           vin, kout, vout, gauss_by_slot, n, shift, hist, totals, nb, bm, ro, bias_not);
     else if (vm == kValPairFirst) GS_SCATTER(true, kValPairFirst);
     else if (vm == kValPair) GS_SCATTER(false, kValPair);
     else if (idv) GS_SCATTER(true, kValU32);
@@ -359,13 +396,13 @@ static void radix_pass(const uint32_t* kin, const void* vin, uint32_t* kout, voi
 
 static void radix_pass_bits(int bits, int ipt, const uint32_t* kin, const void* vin, uint32_t* kout, void* vout,
                             const uint32_t* gauss_by_slot, uint32_t n, int shift, bool idv, int vm, uint32_t* hist,
-                            uint32_t* totals, int nb, uint2* ranges, const uint32_t* bias_not, hipStream_t s) {
+                            uint32_t* totals, int nb, RangeOut ro, const uint32_t* bias_not, hipStream_t s) {
 #define GS_CASE(B)                                                                                              \
     case B:                                                                                                     \
         if (ipt == kDepthSortIPT)                                                                               \
-            radix_pass<B, kDepthSortIPT>(kin, vin, kout, vout, gauss_by_slot, n, shift, idv, vm, hist, totals, nb, ranges, bias_not, s); \
+            radix_pass<B, kDepthSortIPT>(kin, vin, kout, vout, gauss_by_slot, n, shift, idv, vm, hist, totals, nb, ro, bias_not, s); \
         else                                                                                                    \
-            radix_pass<B, kSortIPT>(kin, vin, kout, vout, gauss_by_slot, n, shift, idv, vm, hist, totals, nb, ranges, bias_not, s); \
+            radix_pass<B, kSortIPT>(kin, vin, kout, vout, gauss_by_slot, n, shift, idv, vm, hist, totals, nb, ro, bias_not, s); \
         break;
     switch (bits) {
         GS_CASE(1) GS_CASE(2) GS_CASE(3) GS_CASE(4) GS_CASE(5) GS_CASE(6)
@@ -385,7 +422,7 @@ static int pass_bits(int begin_bit, int end_bit, int max_pass_bits, int p, int& 
 
 int radix_sort_aux(uint32_t* key0, uint32_t* key1, uint2* pair0, uint2* pair1, const uint32_t* aux, uint32_t n,
                    int bits, int max_pass_bits, int ipt, uint32_t* hist, uint32_t* totals, int nblocks, hipStream_t s,
-                   uint2* ranges, const uint32_t* key_bias_not) {
+                   uint2* ranges, const uint32_t* key_bias_not, uint32_t* tile_order, int ntiles) {
     uint32_t* k[2] = {key0, key1};
     uint2* v[2] = {pair0, pair1};
     int cur = 0;
@@ -401,7 +438,8 @@ int radix_sort_aux(uint32_t* key0, uint32_t* key1, uint2* pair0, uint2* pair1, c
         const bool ranges_here = ranges && passes == 1;
         radix_pass_bits(b, ipt, k[cur], v[cur], ranges_here ? nullptr : k[cur ^ 1], v[cur ^ 1], aux, n, shift,
                         p == 0, p == 0 ? kValPairFirst : kValPair, hist, totals, nblocks,
-                        ranges_here ? ranges : nullptr, p == 0 ? key_bias_not : nullptr, s);
+                        RangeOut{ranges_here ? ranges : nullptr, ranges_here ? tile_order : nullptr, ntiles},
+                        p == 0 ? key_bias_not : nullptr, s);
         cur ^= 1;
         shift += b;
     }
@@ -409,9 +447,10 @@ int radix_sort_aux(uint32_t* key0, uint32_t* key1, uint2* pair0, uint2* pair1, c
 }
 
 int tile_sort(uint32_t* key0, uint32_t* key1, uint2* pair0, uint2* pair1, const uint32_t* gauss_by_slot, uint32_t n,
-              int bits, uint32_t* hist, uint32_t* totals, int nblocks, hipStream_t s, uint2* ranges) {
+              int bits, uint32_t* hist, uint32_t* totals, int nblocks, hipStream_t s, uint2* ranges,
+              uint32_t* tile_order, int ntiles) {
     return radix_sort_aux(key0, key1, pair0, pair1, gauss_by_slot, n, bits, kMaxSinglePassBits, kSortIPT, hist, totals,
-                          nblocks, s, ranges);
+                          nblocks, s, ranges, nullptr, tile_order, ntiles);
 }
 
 // ---------------------------------------------------------------------
