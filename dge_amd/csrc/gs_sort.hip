@@ -462,6 +462,8 @@ __device__ __forceinline__ uint32_t rect_count(uint32_t v, int packed) {
     return ((v >> 16 & 0xFFu) - (v & 0xFFu)) * ((v >> 24) - (v >> 8 & 0xFFu));
 }
 
+// Block sums of the instance counts in depth order (k_scan_emit derives each
+// block's first slot from them).
 __global__ __launch_bounds__(256) void k_scan_reduce(EmitArgs a) {
     __shared__ uint32_t lds4[4];
     uint32_t s = 0;
@@ -484,20 +486,6 @@ __global__ __launch_bounds__(256) void k_scan_reduce(EmitArgs a) {
     if (threadIdx.x == 0) a.scan_sums[blockIdx.x] = total;
 }
 
-__global__ __launch_bounds__(256) void k_scan_top(uint32_t* __restrict__ sums, int nb) {
-    __shared__ uint32_t lds4[4];
-    uint32_t carry = 0;
-    for (int c = 0; c < nb; c += 256) {
-        const int j = c + threadIdx.x;
-        const uint32_t v = j < nb ? sums[j] : 0u;
-        uint32_t total;
-        const uint32_t ex = block_exclusive_scan(v, lds4, total);
-        if (j < nb) sums[j] = carry + ex;
-        carry += total;
-    }
-    if (threadIdx.x == 0) sums[nb] = carry;
-}
-
 // Emission in depth order: rounds of 256 Gaussians; a block scan of their
 // instance counts gives each its first slot, then the round's instances are
 // expanded cooperatively — thread j writes slot base+j, finding its Gaussian
@@ -509,7 +497,14 @@ __global__ __launch_bounds__(256) void k_scan_emit(EmitArgs a) {
     __shared__ uint32_t s_start[256];
     __shared__ uint32_t s_gauss[256];
     __shared__ int4 s_rect[256];  // x0, y0, width, -
-    uint32_t base = a.scan_sums[blockIdx.x];
+    // the block's first slot: the sum of the block sums before it (k_scan_reduce's, read from L2:
+    // at most scan_blocks words; this replaced a one-workgroup top-level scan launch)
+    uint32_t base;
+    {
+        uint32_t part = 0;
+        for (uint32_t j = threadIdx.x; j < blockIdx.x; j += 256) part += a.scan_sums[j];
+        block_exclusive_scan(part, lds4, base);
+    }
     const uint32_t r_block = blockIdx.x * (uint32_t)kScanTile;
     for (int it = 0; it < kScanIPT; ++it) {
         const uint32_t r = r_block + it * 256 + threadIdx.x;
@@ -558,7 +553,6 @@ __global__ __launch_bounds__(256) void k_scan_emit(EmitArgs a) {
 void launch_scan_reduce(const EmitArgs& a, hipStream_t s) {
     if (a.P <= 0) return;
     hipLaunchKernelGGL(k_scan_reduce, dim3(a.scan_blocks), dim3(256), 0, s, a);
-    hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(256), 0, s, a.scan_sums, a.scan_blocks);
 }
 
 void launch_scan_emit(const EmitArgs& a, hipStream_t s) {
