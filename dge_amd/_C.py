@@ -50,19 +50,21 @@ def _sh_tensor(sh):
     return _f32(sh, "sh")
 
 
-def _half_sh_params(P, M, means3D, sh, colors, opacity, scales, rotations, cov3D_precomp):
-    """gs_params for the reference's (already activated) inputs with fp16 SH [P,M,3]."""
+def _sh_params(P, M, means3D, sh, colors, opacity, scales, rotations, cov3D_precomp):
+    """gs_params for the reference's (already activated) inputs, SH [P,M,3] in fp32 or fp16."""
     g = N.GsParams()
     g.P, g.M = P, M
     g.means3D = _ptr(means3D)
-    g.sh_dc = sh.data_ptr()
-    g.sh_rest = sh.data_ptr() + 6 if M > 1 else None  # coefficient 1: 3 halves in
-    g.sh_dc_stride = g.sh_rest_stride = 3 * M
-    g.colors_precomp = None
+    half = M > 0 and sh.dtype == torch.float16
+    if M:
+        g.sh_dc = sh.data_ptr()
+        g.sh_rest = sh.data_ptr() + 3 * sh.element_size() if M > 1 else None  # coefficient 1
+        g.sh_dc_stride = g.sh_rest_stride = 3 * M
+    g.colors_precomp = _ptr(colors)
     g.opacities = _ptr(opacity)
     g.scales, g.rotations, g.cov3D_precomp = _ptr(scales), _ptr(rotations), _ptr(cov3D_precomp)
     g.activation = 0
-    g.sh_half = 1
+    g.sh_half = 1 if half else 0
     return g
 
 
@@ -159,7 +161,7 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
         alloc = _Allocator(dev)
         nr = ctypes.c_int(0)
         if M and sh.dtype == torch.float16:  # fp16 SH storage: the _ex entry point upcasts in-kernel
-            g = _half_sh_params(P, M, means3D, sh, colors, opacity, scales, rotations, cov3D_precomp)
+            g = _sh_params(P, M, means3D, sh, colors, opacity, scales, rotations, cov3D_precomp)
             rc = N.lib().gs_rasterize_forward_ex(ctypes.byref(s), ctypes.byref(g), _ptr(out_color), _ptr(out_depth),
                                                  _ptr(radii), alloc.fn, None, _stream(dev), ctypes.byref(nr))
         else:
@@ -177,7 +179,10 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
 
 def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rotations, scale_modifier, cov3D_precomp,
                                  viewmatrix, projmatrix, tan_fovx, tan_fovy, dL_dout_color, sh, degree, campos,
-                                 geomBuffer, R, binningBuffer, imageBuffer, debug):
+                                 geomBuffer, R, binningBuffer, imageBuffer, debug, dL_dconic=None):
+    """rasterize_points.cu:97-157.  `dL_dconic` (not in the reference's API; parity tests): a [P,3]
+    float32 tensor that receives each Gaussian's summed conic gradient (x, y, w of the reference's
+    [P,2,2] dL_dconic2D)."""
     N.require_gpu(means3D)
     dev = means3D.device
     P = means3D.size(0)
@@ -201,8 +206,9 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
         s, keep = _settings(background, viewmatrix, projmatrix, campos, tan_fovx, tan_fovy, H, W, degree,
                             scale_modifier, False, debug)
         dmeans2D, dcolors, dopac, dmeans3D, dcov, dsh, dscales, drot = out
-        if M and sh.dtype == torch.float16:  # fp16 SH: _ex entry point, fp32 SH gradients [P,M,3]
-            g = _half_sh_params(P, M, means3D, sh, colors, None, scales, rotations, cov3D_precomp)
+        if (M and sh.dtype == torch.float16) or dL_dconic is not None:
+            # _ex entry point: fp16 SH (fp32 SH gradients [P,M,3]) or the conic-gradient output
+            g = _sh_params(P, M, means3D, sh, colors, None, scales, rotations, cov3D_precomp)
             o = N.GsGrads()
             o.dL_dmeans2D, o.dL_dcolors, o.dL_dopacity = _ptr(dmeans2D), _ptr(dcolors), _ptr(dopac)
             o.dL_dmeans3D, o.dL_dcov3D = _ptr(dmeans3D), _ptr(dcov)
@@ -210,6 +216,10 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
             o.dL_dsh_rest = dsh.data_ptr() + 12 if M > 1 else None
             o.dsh_dc_stride = o.dsh_rest_stride = 3 * M
             o.dL_dscales, o.dL_drotations = _ptr(dscales), _ptr(drot)
+            if dL_dconic is not None:
+                if dL_dconic.shape != (P, 3) or dL_dconic.dtype != torch.float32 or not dL_dconic.is_contiguous():
+                    raise RuntimeError("dL_dconic must be a contiguous float32 [P,3] tensor")
+                o.dL_dconic = _ptr(dL_dconic)
             rc = N.lib().gs_rasterize_backward_ex(ctypes.byref(s), ctypes.byref(g), int(R), _ptr(radii),
                                                   _ptr(geomBuffer), _ptr(binningBuffer), _ptr(imageBuffer),
                                                   _ptr(grad), ctypes.byref(o), _stream(dev))

@@ -90,6 +90,7 @@ class GsGrads(ctypes.Structure):
         ("accumulate", ctypes.c_uint),
         ("grad_mask", ctypes.c_void_p),
         ("mask_bits", ctypes.c_uint),
+        ("dL_dconic", _fp),
     ]
 
 
@@ -151,6 +152,7 @@ SIGNATURES = {
                                       ctypes.c_void_p, ctypes.c_void_p]),
     "gs_rows_scatter": (ctypes.c_int, [ctypes.POINTER(RowsRegion), ctypes.c_int, ctypes.c_void_p, ctypes.c_longlong,
                                        ctypes.c_void_p, ctypes.c_void_p]),
+    "gs_blend_exp": (ctypes.c_int, [ctypes.c_longlong, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "gs_last_error": (ctypes.c_char_p, []),
     "gs_abi_version": (ctypes.c_int, []),
 }

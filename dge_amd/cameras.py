@@ -54,13 +54,16 @@ def focal2fov(focal: float, pixels: int) -> float:
 class Camera:
     """The attributes render() reads from a Simple_Camera (cameras.py:59-96)."""
 
-    def __init__(self, R, T, FoVx, FoVy, height, width, device="cuda", znear=0.01, zfar=100.0, uid=0):
+    def __init__(self, R, T, FoVx, FoVy, height, width, device="cuda", znear=0.01, zfar=100.0, uid=0,
+                 trans=np.array([0.0, 0.0, 0.0]), scale=1.0):
         self.R, self.T = np.asarray(R, np.float64), np.asarray(T, np.float64)
+        self.trans, self.scale = np.asarray(trans, np.float64), float(scale)
         self.FoVx, self.FoVy = float(FoVx), float(FoVy)
         self.image_height, self.image_width = int(height), int(width)
         self.znear, self.zfar = znear, zfar
         self.uid = uid
-        self.world_view_transform = torch.tensor(get_world2view2(self.R, self.T)).transpose(0, 1).to(device)
+        self.world_view_transform = torch.tensor(get_world2view2(self.R, self.T, self.trans, self.scale)).transpose(
+            0, 1).to(device)
         self.projection_matrix = get_projection_matrix(znear, zfar, self.FoVx, self.FoVy).transpose(0, 1).to(device)
         self.full_proj_transform = (self.world_view_transform.unsqueeze(0).bmm(
             self.projection_matrix.unsqueeze(0))).squeeze(0).float()
@@ -68,7 +71,7 @@ class Camera:
 
     def to(self, device):
         return Camera(self.R, self.T, self.FoVx, self.FoVy, self.image_height, self.image_width, device, self.znear,
-                      self.zfar, self.uid)
+                      self.zfar, self.uid, self.trans, self.scale)
 
 
 def look_at_R_T(position, target=(0.0, 0.0, 0.0), world_up=(0.0, 0.0, 1.0)):

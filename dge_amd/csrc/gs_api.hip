@@ -476,6 +476,15 @@ int gs_profile_collect(double* total_ms, int* counts, int n) {
 
 int gs_abi_version(void) { return GS_RASTER_ABI_VERSION; }
 
+int gs_blend_exp(long long n, const float* x, float* y, gs_stream_t stream) {
+    if (n < 0 || (n > 0 && (!x || !y))) return set_error(GS_ERR_INVALID_ARG, "gs_blend_exp: bad arguments");
+    if (n == 0) return GS_OK;
+    if ((n + 1) / 2 > 255ll * 0x7FFFFFFF) return set_error(GS_ERR_INVALID_ARG, "gs_blend_exp: n too large");
+    gs::launch_blend_exp(n, x, y, (hipStream_t)stream);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? GS_OK : set_error(GS_ERR_HIP, "gs_blend_exp launch failed: %s", hipGetErrorString(e));
+}
+
 size_t gs_geometry_buffer_size(int P) { return geom_layout(P).total; }
 size_t gs_image_buffer_size(int width, int height) { return img_layout(width, height).total; }
 size_t gs_binning_buffer_size(int num_rendered, int num_tiles) { return bin_layout(num_rendered, num_tiles).total; }
@@ -592,6 +601,7 @@ int gs_rasterize_backward(const gs_settings* s, int P, int M, int R, const float
     o.accumulate = 0;
     o.grad_mask = nullptr;
     o.mask_bits = 0;
+    o.dL_dconic = nullptr;
     gs_params g2 = g;
     g2.M = M;  // dL_dsh is [P,M,3] even when shs is absent (then all zero)
     return gs_rasterize_backward_ex(s, &g2, R, radii, geom, binning, img, dL_dpix, &o, stream);
@@ -688,6 +698,7 @@ int gs_rasterize_backward_ex(const gs_settings* s, const gs_params* gp, int R, c
         ga.acc = o->accumulate;
         ga.grad_mask = o->grad_mask;
         ga.mask_bits = o->grad_mask ? o->mask_bits : 0u;
+        ga.dL_dconic = o->dL_dconic;
         { StageScope sc(ST_GAUSS_BWD, stream); launch_gauss_backward(ga, stream); }
         GS_LAUNCHED("gaussian backward");
         return GS_OK;

@@ -344,6 +344,9 @@ __device__ __forceinline__ void commit_outputs(const GaussBwdArgs& a, int idx, i
     float om2[2] = {0.f, 0.f}, oop = 0.f, ocol[3] = {0.f, 0.f, 0.f}, om3[3] = {0.f, 0.f, 0.f};
     float ocov[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, osc[3] = {0.f, 0.f, 0.f}, odc[3] = {0.f, 0.f, 0.f};
     float4 orot = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (a.dL_dconic)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) a.dL_dconic[i3 + k] = acc[2 + k];
     if (f & GS_ACC_MEANS2D) { om2[0] = a.dL_dmeans2D[i3]; om2[1] = a.dL_dmeans2D[i3 + 1]; }
     if (f & GS_ACC_OPACITY) oop = a.dL_dopacity[src];
     if (a.dL_dcolors && (f & GS_ACC_COLORS))
@@ -423,6 +426,9 @@ __global__ __launch_bounds__(kGB) void k_gauss_live(GaussBwdArgs a) {
     const uint32_t acc = a.acc;
     const int src = in && a.index ? a.index[idx] : idx;
     if (in && !live) {
+        if (a.dL_dconic)
+#pragma unroll
+            for (int k = 0; k < 3; ++k) a.dL_dconic[3 * (size_t)idx + k] = 0.f;
         if (!(acc & GS_ACC_MEANS2D))
 #pragma unroll
             for (int k = 0; k < 3; ++k) a.dL_dmeans2D[3 * (size_t)idx + k] = 0.f;

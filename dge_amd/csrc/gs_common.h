@@ -158,6 +158,69 @@ __device__ __forceinline__ void ewa_cov2d(const Ewa& e, float& a, float& b, floa
     c = (B10 * e.T[1][0] + B11 * e.T[1][1] + B12 * e.T[1][2]) + 0.3f;
 }
 
+// ---------------------------------------------------------------------
+// The blend's exp (forward.cu:345 `exp(power)`, backward.cu:495).
+// The reference compiles CUDA's expf (<= 2 ulp, not reproducible off an
+// NVIDIA GPU); the skip / stop decisions of the blend (alpha >= 1/255,
+// T (1 - alpha) >= 1e-4) and therefore n_contrib, the per-pixel lists and the
+// whole T chain depend on the last bit of every G.  So the exp here is a fixed
+// sequence of IEEE single operations — clamp, round-to-integer by the 1.5*2^23
+// shifter, one-constant Cody-Waite reduction, degree-7 Taylor/Horner with
+// fma, exponent built from the shifter's bits — that the CPU oracle
+// (oracle/gs_oracle.c gs_expf) evaluates identically: G, alpha, T and every
+// blend decision are bit-identical between the two.  Accuracy: <= 0.97 ulp
+// against exp over [-10, 1] (99.67% correctly rounded).  NaN -> NaN (the
+// reference then blends the entry at alpha = min(0.99, NaN) = 0.99, and so
+// do we); -inf -> -inf (alpha < 1/255: skipped, as exp(-inf) = 0 is).
+// ---------------------------------------------------------------------
+typedef float f2v __attribute__((ext_vector_type(2)));  // two entries per packed instruction
+
+constexpr float kExpLog2e = 1.44269504f;
+constexpr float kExpShifter = 12582912.0f;  // 1.5 * 2^23: t + S rounds t to an integer (ties to even)
+constexpr float kExpLn2 = 0.693147182f;
+constexpr float kExpC7 = 1.98412698e-4f, kExpC6 = 1.38888889e-3f, kExpC5 = 8.33333377e-3f,
+                kExpC4 = 4.16666679e-2f, kExpC3 = 1.66666672e-1f;
+
+__device__ __forceinline__ float exp_scale(float u) {  // 2^n from the shifter sum u = S + n
+    return __uint_as_float((__float_as_uint(u) << 23) + 0x3F800000u);
+}
+
+__device__ __forceinline__ float gs_exp(float x) {
+#pragma clang fp contract(off)
+    float t = x * kExpLog2e;
+    t = fminf(fmaxf(t, -120.0f), 120.0f);
+    const float u = t + kExpShifter;
+    const float n = u - kExpShifter;
+    const float r = __builtin_fmaf(n, -kExpLn2, x);
+    float p = __builtin_fmaf(kExpC7, r, kExpC6);
+    p = __builtin_fmaf(p, r, kExpC5);
+    p = __builtin_fmaf(p, r, kExpC4);
+    p = __builtin_fmaf(p, r, kExpC3);
+    p = __builtin_fmaf(p, r, 0.5f);
+    p = __builtin_fmaf(p, r, 1.0f);
+    p = __builtin_fmaf(p, r, 1.0f);
+    return p * exp_scale(u);
+}
+
+// gs_exp of two values: the same operations, packed (v_pk_mul / v_pk_add / v_pk_fma_f32)
+__device__ __forceinline__ f2v gs_exp2(f2v x) {
+#pragma clang fp contract(off)
+    f2v t = x * kExpLog2e;
+    t.x = fminf(fmaxf(t.x, -120.0f), 120.0f);
+    t.y = fminf(fmaxf(t.y, -120.0f), 120.0f);
+    const f2v u = t + kExpShifter;
+    const f2v n = u - kExpShifter;
+    const f2v r = __builtin_elementwise_fma(n, f2v{-kExpLn2, -kExpLn2}, x);
+    f2v p = __builtin_elementwise_fma(f2v{kExpC7, kExpC7}, r, f2v{kExpC6, kExpC6});
+    p = __builtin_elementwise_fma(p, r, f2v{kExpC5, kExpC5});
+    p = __builtin_elementwise_fma(p, r, f2v{kExpC4, kExpC4});
+    p = __builtin_elementwise_fma(p, r, f2v{kExpC3, kExpC3});
+    p = __builtin_elementwise_fma(p, r, f2v{0.5f, 0.5f});
+    p = __builtin_elementwise_fma(p, r, f2v{1.0f, 1.0f});
+    p = __builtin_elementwise_fma(p, r, f2v{1.0f, 1.0f});
+    return p * f2v{exp_scale(u.x), exp_scale(u.y)};
+}
+
 // GaussianModel activations (gaussian_model.py:42-57): sigmoid, exp,
 // F.normalize(q, dim=1, eps=1e-12) and their derivatives (what torch's
 // autograd applies to the getters in the reference's render()).

@@ -112,10 +112,15 @@ inline GeomLayout geom_layout(int P) {
     return L;
 }
 
-// Segment-parallel backward replay: the forward checkpoints every quadrant's
-// per-pixel (T, C) at list positions k*kSegLen (k >= 1; slot 0 holds the final
-// state); the backward replays each segment [k*kSegLen, (k+1)*kSegLen) of a
-// quadrant window as its own work item.  Checkpoint slots are allocated per
+// Segment-parallel backward replay: for every segment k = [k*kSegLen,
+// (k+1)*kSegLen) of a tile list it blends, the forward stores per quadrant pixel
+// slot k = (T after the segment, S_k), S_k = the segment's own colour sum
+// sum f alpha T (a separate accumulator, reset per segment).  The backward
+// replays each segment of a quadrant window as its own work item, starting
+// from T = slot k.T and the colour composited behind the segment
+// D = (S_{k+1} + ... + S_last) / T: a sum of later segments' local sums, so its
+// rounding is relative to D itself (a difference of prefix sums,
+// (C_final - C_k) / T_k, would carry the whole prefix's rounding / T_k).  Checkpoint slots are allocated per
 // tile from its list: tile t owns slots [ckpt_base(t), ckpt_base(t) + ceil(len/kSegLen)),
 // ckpt_base(t) = range.x / kSegLen + t (monotone and non-overlapping because
 // ranges are a prefix sum), each slot 4 quadrants x 64 pixels x float4.
@@ -313,6 +318,7 @@ struct ApplyWeightsArgs {
     int* cnt;
 };
 void launch_render_apply_weights(const ApplyWeightsArgs& a, hipStream_t s);
+void launch_blend_exp(long long n, const float* x, float* y, hipStream_t s);
 
 struct RenderBwdArgs {
     int W, H, gx, gy;
@@ -358,6 +364,7 @@ struct GaussBwdArgs {
     uint32_t acc;  // GS_ACC_* bits: add into the output instead of overwriting
     const uint8_t* grad_mask;  // optional [P]: outputs in mask_bits are multiplied by it
     uint32_t mask_bits;
+    float* dL_dconic;          // optional [P,3]: the summed conic gradient (parity tests)
 };
 void launch_gauss_backward(const GaussBwdArgs& a, hipStream_t s);
 

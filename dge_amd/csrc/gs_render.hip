@@ -32,10 +32,21 @@ namespace gs {
 // =====================================================================
 // forward: one wave per 8x8 quadrant
 // =====================================================================
-// exp used by the blend loops: v_exp_f32 on the pre-scaled argument
-// (|rel. err| ~1e-7 over the live range power in [-5.6, 0], same order as
-// the CUDA expf the reference compiles to; see DESIGN.md §5 for the parity bar)
-__device__ __forceinline__ float blend_exp(float x) { return __expf(x); }
+// exp used by the blend loops: gs_exp (gs_common.h), the fixed IEEE sequence the
+// oracle evaluates bit for bit, so every alpha and blend decision is the oracle's
+__device__ __forceinline__ float blend_exp(float x) { return gs_exp(x); }
+
+// test hook (gs_blend_exp): the blend exp over an array, packed as the blend loops use it
+__global__ __launch_bounds__(256) void k_blend_exp(long long n, const float* __restrict__ x, float* __restrict__ y) {
+    const long long i = 2 * ((long long)blockIdx.x * 256 + threadIdx.x);
+    if (i + 1 < n) {
+        const f2v r = gs_exp2(f2v{x[i], x[i + 1]});
+        y[i] = r.x;
+        y[i + 1] = r.y;
+    } else if (i < n) {
+        y[i] = gs_exp(x[i]);
+    }
+}
 
 // The per-(pixel, Gaussian) test shared by the forward, the backward replay
 // and apply_weights: identical code (contraction pinned), hence identical
@@ -80,42 +91,17 @@ __device__ __forceinline__ Entry gather_entry(const Splat* splat, uint32_t id) {
     return e;
 }
 
-// Blend one entry into the pixel state without branches: every lane evaluates
-// the reference's tests (forward.cu:336-358) and selects.  A pixel that is
-// done, skipped, or saturates on this entry keeps its state bit-for-bit.
-__device__ __forceinline__ bool blend_step(float2 xy, float4 co, float4 fe, uint32_t pos, float pfx, float pfy,
-                                          bool& done, float& T, float& C0, float& C1, float& C2, float& D,
-                                          uint32_t& last) {
-    float dx, dy, G, alpha;
-    const bool hit = pixel_alpha(xy, co, pfx, pfy, dx, dy, G, alpha) && !done;
-    const float test_T = T * (1 - alpha);
-    const bool stop = hit && test_T < 0.0001f;
-    const bool use = hit && !stop;
-    done = done || stop;
-    // one select on the weight instead of four on the sums: C + f * 0 == C (f finite)
-    const float w = use ? alpha * T : 0.0f;
-    C0 = C0 + fe.x * w;
-    C1 = C1 + fe.y * w;
-    C2 = C2 + fe.z * w;
-    D = D + fe.w * w;
-    T = use ? test_T : T;
-    last = use ? pos : last;
-    return use;
-}
-
 // pixel_alpha for two consecutive entries at once: the same IEEE operations in
 // the same order (contraction pinned), on float2 so the compiler issues packed
 // v_pk_add/v_pk_mul (two entries per instruction); results bit-identical to
 // two pixel_alpha calls.
-typedef float f2v __attribute__((ext_vector_type(2)));  // built-in vector ops: the pragma below holds
 __device__ __forceinline__ void pixel_alpha2(f2v x, f2v y, f2v cx, f2v cy, f2v cz, f2v op, float pfx, float pfy,
                                              f2v& dx, f2v& dy, f2v& G, f2v& alpha, bool& ok0, bool& ok1) {
 #pragma clang fp contract(off)
     dx = x - pfx;
     dy = y - pfy;
     const f2v power = -0.5f * (cx * dx * dx + cz * dy * dy) - cy * dx * dy;
-    G.x = blend_exp(power.x);
-    G.y = blend_exp(power.y);
+    G = gs_exp2(power);
     const f2v oG = op * G;
     alpha.x = fminf(0.99f, oG.x);
     alpha.y = fminf(0.99f, oG.y);
@@ -130,24 +116,28 @@ __device__ __forceinline__ void pixel_alpha2(f2v x, f2v y, f2v cx, f2v cy, f2v c
 //   tT = Ts * (1 - a')                  (<= 0 once saturated: 1 - a' >= 0.01)
 //   use-or-skip <=> tT >= 1e-4          (live and !stop, forward.cu:350-354)
 //   Ts = (tT >= 1e-4) ? tT : -|Ts|       (a stop keeps T and marks the pixel done)
-//   w  = (tT >= 1e-4) ? a' * Ts : 0     (w > 0 exactly when the entry is blended:
-//                                         a' >= 1/255, T >= 1e-4 then)
-// T, the colour sums and `last` are bit-identical to blend_step's; |Ts| is the
-// pixel's T.  The colour and depth sums are two packed pairs (C0, C1), (C2, D):
-// one v_pk_fma each against the entry's (r, g) and (b, depth), aligned register
-// pairs after the 16-B LDS read; fused multiply-adds, as `C + f * w` contracts
-// to (forward.cu:355-356 under nvcc's default fmad).  A skipped entry adds
-// f * 0 (f finite).  Returns w, so the caller's "blended by some pixel" vote is
-// one compare.
+//   Tw = (tT >= 1e-4) ? Ts : 0          (the T a use blends with; 0 for stop/done)
+// and the sums in the reference's association, `C += f * alpha * T` as nvcc's
+// default fmad contracts it (forward.cu:355-357): C = fma(f * a', Tw, C), two
+// packed pairs (C0, C1), (C2, D) against the entry's (r, g), (b, depth); the
+// same products go into the segment-local sums (L01, L2) of the checkpoints.  A
+// skipped entry adds (f * 0) * T = 0, a stopped or saturated one f a' * 0.
+// T, the sums and `last` are bit-identical to the oracle's.  Returns
+// w = a' Tw, > 0 exactly when the entry is blended (the caller's vote).
 __device__ __forceinline__ float blend_chain(float a, float4 fe, uint32_t pos, float& Ts, f2v& C01, f2v& C2D,
-                                           uint32_t& last) {
+                                           f2v& L01, float& L2, uint32_t& last) {
+#pragma clang fp contract(off)
     const float tT = Ts * (1.0f - a);
     const bool go = tT >= 0.0001f;
-    const float w = go ? a * Ts : 0.0f;
+    const float Tw = go ? Ts : 0.0f;
     Ts = go ? tT : -fabsf(Ts);
-    const f2v w2 = {w, w};
-    C01 = __builtin_elementwise_fma(f2v{fe.x, fe.y}, w2, C01);
-    C2D = __builtin_elementwise_fma(f2v{fe.z, fe.w}, w2, C2D);
+    const f2v a2 = {a, a}, T2 = {Tw, Tw};
+    const f2v fa01 = f2v{fe.x, fe.y} * a2, fa2d = f2v{fe.z, fe.w} * a2;
+    C01 = __builtin_elementwise_fma(fa01, T2, C01);
+    C2D = __builtin_elementwise_fma(fa2d, T2, C2D);
+    L01 = __builtin_elementwise_fma(fa01, T2, L01);  // the segment's own colour sum (backward start)
+    L2 = __builtin_fmaf(fa2d.x, Tw, L2);
+    const float w = a * Tw;
     last = w > 0.0f ? pos : last;
     return w;
 }
@@ -212,6 +202,8 @@ __global__ __launch_bounds__(64) void k_render_fwd(RenderArgs a) {
     uint64_t* used = a.used + (size_t)used_base(range.x, tile) * 4 + quad;
     float Ts = inside ? 1.0f : -1.0f;  // signed transmittance (blend_chain): < 0 once done
     f2v C01 = {0.f, 0.f}, C2D = {0.f, 0.f};  // (C0, C1), (C2, depth)
+    f2v L01 = {0.f, 0.f};                    // this segment's own colour sum (C0, C1), C2
+    float L2 = 0.f;
     uint32_t last = 0;
     const uint64_t t_start = a.diag ? __builtin_amdgcn_s_memrealtime() : 0;
     const uint64_t c_start = a.diag ? __builtin_amdgcn_s_memtime() : 0;
@@ -241,8 +233,9 @@ __global__ __launch_bounds__(64) void k_render_fwd(RenderArgs a) {
     for (int i = 0; i < 4; ++i) cur[i] = gather_entry(a.splat, ids[i]);
     load_ids(range.x + kRound, ids);
 
-    // checkpoint k of this quadrant: slot ckpt_base + k, quadrant `quad`
+    // checkpoint of segment k of this quadrant: slot ckpt_base + k, quadrant `quad`
     float4* ckpt = a.ckpt + ((size_t)ckpt_base(range.x, tile) * 4 + quad) * 64;
+    int seg_done = -1;  // last segment whose checkpoint is pending (the round just blended)
     uint64_t c_cull = 0;
     // The round's global stores (checkpoint, the previous round's blended bits) are issued after
     // the next round's gathers: stores count in vmcnt, and one issued just before the cull would
@@ -296,10 +289,12 @@ __global__ __launch_bounds__(64) void k_render_fwd(RenderArgs a) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) cur[i] = gather_entry(a.splat, ids[i]);
         load_ids(b + 2 * kRound, ids);
-        {  // (T, C) at the segment boundaries of the backward replay (every round start)
-            const uint32_t k = (b - range.x) / kSegLen;
-            if (k > 0) ckpt[(size_t)k * 256 + lane] = make_float4(fabsf(Ts), C01.x, C01.y, C2D.x);
+        if (seg_done >= 0) {  // the previous segment's (T after it, own colour sum): the replay's start
+            ckpt[(size_t)seg_done * 256 + lane] = make_float4(fabsf(Ts), L01.x, L01.y, L2);
+            L01 = f2v{0.f, 0.f};
+            L2 = 0.f;
         }
+        seg_done = (int)((b - range.x) / kSegLen);
         store_words();
         if (lane <= kRound / kGroup) s_gused[lane] = 0u;  // (groups past an early exit stay 0)
         __syncthreads();
@@ -340,9 +335,10 @@ __global__ __launch_bounds__(64) void k_render_fwd(RenderArgs a) {
                 const int h = u / 2;
                 pixel_alpha2(g.x[h], g.y[h], g.cx[h], g.cy[h], g.cz[h], g.op[h], pfx, pfy, dx2, dy2, G2, al, ok0,
                              ok1);
-                const float w0 = blend_chain(ok0 ? al.x : 0.0f, c.rgbd[u], c.pos[u], Ts, C01, C2D, last);
+                const float w0 = blend_chain(ok0 ? al.x : 0.0f, c.rgbd[u], c.pos[u], Ts, C01, C2D, L01, L2, last);
                 gm |= (__builtin_amdgcn_fcmpf(w0, 0.0f, kFcmpOGT) != 0ull ? 1u : 0u) << u;
-                const float w1 = blend_chain(ok1 ? al.y : 0.0f, c.rgbd[u + 1], c.pos[u + 1], Ts, C01, C2D, last);
+                const float w1 =
+                    blend_chain(ok1 ? al.y : 0.0f, c.rgbd[u + 1], c.pos[u + 1], Ts, C01, C2D, L01, L2, last);
                 gm |= (__builtin_amdgcn_fcmpf(w1, 0.0f, kFcmpOGT) != 0ull ? 1u : 0u) << (u + 1);
             }
             s_gused[j / kGroup] = gm;
@@ -387,17 +383,18 @@ __global__ __launch_bounds__(64) void k_render_fwd(RenderArgs a) {
     }
     store_words();
 
-    // slot 0: the final state (an empty tile's range is (0, 0): it owns no slot and has no replay)
+    // the last blended segment's checkpoint (an empty tile's range is (0, 0): no slot, no replay)
     const float T = fabsf(Ts);
-    if (range.y > range.x) ckpt[lane] = make_float4(T, C01.x, C01.y, C2D.x);
+    if (seg_done >= 0) ckpt[(size_t)seg_done * 256 + lane] = make_float4(T, L01.x, L01.y, L2);
     if (inside) {
         const size_t pix = (size_t)a.W * py + px;
         const size_t HW = (size_t)a.W * a.H;
         a.final_T[pix] = T;
         a.n_contrib[pix] = last;
-        a.out_color[pix] = C01.x + T * a.bg[0];
-        a.out_color[HW + pix] = C01.y + T * a.bg[1];
-        a.out_color[2 * HW + pix] = C2D.x + T * a.bg[2];
+        // forward.cu:376 `C + T * bg`, contracted (as the oracle): fma(T, bg, C)
+        a.out_color[pix] = __builtin_fmaf(T, a.bg[0], C01.x);
+        a.out_color[HW + pix] = __builtin_fmaf(T, a.bg[1], C01.y);
+        a.out_color[2 * HW + pix] = __builtin_fmaf(T, a.bg[2], C2D.x);
         a.out_depth[pix] = C2D.y;
     }
     const uint32_t m = wave_max_u32(inside ? last : 0u);
@@ -510,6 +507,11 @@ __global__ __launch_bounds__(64) void k_render_apply_weights(ApplyWeightsArgs a)
         }
         __syncthreads();
     }
+}
+
+void launch_blend_exp(long long n, const float* x, float* y, hipStream_t s) {
+    const long long pairs = (n + 1) / 2;
+    hipLaunchKernelGGL(k_blend_exp, dim3((unsigned)((pairs + 255) / 256)), dim3(256), 0, s, n, x, y);
 }
 
 void launch_render_apply_weights(const ApplyWeightsArgs& a, hipStream_t s) {
@@ -654,15 +656,22 @@ __global__ __launch_bounds__(64, 4) void k_render_bwd(RenderBwdArgs a) {
     const float nbg = -T_final * (a.bg[0] * dp0 + a.bg[1] * dp1 + a.bg[2] * dp2);
     float T = T_final, D0 = 0.f, D1 = 0.f, D2 = 0.f;
     if (limit < window) {
-        // start inside the window: T and the colour behind position `limit` from the forward's
-        // checkpoints: D = (C_final - C_limit) / T_limit, the composite of entries >= limit
+        // start inside the window: T after this segment (its checkpoint) and the colour composited
+        // behind position `limit`, D = (S_{seg+1} + ... + S_last) / T from the later segments' own
+        // colour sums (summed back to front)
         const float4* ck = a.ckpt + ((size_t)ckpt_base(range.x, tile) * 4 + quad) * 64;
-        const float4 cb = ck[(size_t)(limit / kSegLen) * 256 + lane], cf = ck[lane];
-        T = cb.x;
-        const float inv = 1.0f / cb.x;
-        D0 = (cf.y - cb.y) * inv;
-        D1 = (cf.z - cb.z) * inv;
-        D2 = (cf.w - cb.w) * inv;
+        T = ck[(size_t)seg * 256 + lane].x;
+        float S0 = 0.f, S1 = 0.f, S2 = 0.f;
+        for (int k = nseg_q - 1; k > seg; --k) {
+            const float4 c = ck[(size_t)k * 256 + lane];
+            S0 += c.y;
+            S1 += c.z;
+            S2 += c.w;
+        }
+        const float inv = 1.0f / T;
+        D0 = S0 * inv;
+        D1 = S1 * inv;
+        D2 = S2 * inv;
     }
     const float ddelx_dx = (float)(0.5 * a.W), ddely_dy = (float)(0.5 * a.H);
     const uint64_t t_start = a.diag ? __builtin_amdgcn_s_memrealtime() : 0;

@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define GS_RASTER_ABI_VERSION 5
+#define GS_RASTER_ABI_VERSION 6
 
 #define GS_OK 0
 #define GS_ERR_INVALID_ARG 1   /* AT_ERROR / std::runtime_error in the reference */
@@ -166,6 +166,10 @@ typedef struct gs_grads {         /* backward outputs, every element written */
      * gs_params.index); NULL: none. */
     const uint8_t *grad_mask;     /* [P] */
     unsigned int mask_bits;
+    /* Optional [P,3] output (not in the reference's API; parity tests): each
+     * Gaussian's summed conic gradient (x, y, w of backward.cu's dL_dconic2D),
+     * the input of the per-Gaussian chain; NULL: not written. */
+    float *dL_dconic;
 } gs_grads;
 
 int gs_rasterize_forward_ex(const gs_settings *s, const gs_params *g, float *out_color, float *out_depth,
@@ -263,6 +267,11 @@ int gs_profile_collect(double *total_ms, int *counts, int n);
  * (which: 0 forward, 1 backward) to host memory and returns the u64 count. */
 int gs_profile_diag_enable(int on);
 long long gs_profile_diag_read(int which, uint64_t *host, long long max_u64);
+
+/* Test hook: the blend's exp (forward.cu:345 `exp(power)`) over n floats on the
+ * device, evaluated exactly as the blend kernels do (packed pairs); bit-identical
+ * to the oracle's gs_expf.  Returns GS_OK or an error code. */
+int gs_blend_exp(long long n, const float *x, float *y, gs_stream_t stream);
 
 const char *gs_last_error(void);
 int gs_abi_version(void);

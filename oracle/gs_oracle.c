@@ -99,6 +99,39 @@ static v3 xform_vec43_T(v3 p, const float *m) {
                   m[8] * p.x + m[9] * p.y + m[10] * p.z);
 }
 
+/* The blend's exp (forward.cu:345, backward.cu:495, apply_weights.cu): the
+ * reference calls CUDA's expf (<= 2 ulp, unavailable here).  The oracle fixes
+ * ONE exp as a sequence of IEEE single operations (<= 0.97 ulp vs exp over
+ * [-10, 1], 99.67% correctly rounded; NaN -> NaN, -inf -> -inf) that the HIP
+ * path (dge_amd/csrc/gs_common.h gs_exp) evaluates identically, so every
+ * alpha, every skip/stop decision, T and n_contrib can be compared bit for
+ * bit.  fmaf is the correctly rounded fused multiply-add (built -mfma). */
+static float gs_expf(float x) {
+    float t = x * 1.44269504f;
+    t = fminf(fmaxf(t, -120.0f), 120.0f);
+    const float u = t + 12582912.0f; /* 1.5 * 2^23: rounds t to an integer, ties to even */
+    const float n = u - 12582912.0f;
+    const float r = fmaf(n, -0.693147182f, x);
+    float p = fmaf(1.98412698e-4f, r, 1.38888889e-3f);
+    p = fmaf(p, r, 8.33333377e-3f);
+    p = fmaf(p, r, 4.16666679e-2f);
+    p = fmaf(p, r, 1.66666672e-1f);
+    p = fmaf(p, r, 0.5f);
+    p = fmaf(p, r, 1.0f);
+    p = fmaf(p, r, 1.0f);
+    uint32_t ub, sb;
+    memcpy(&ub, &u, 4);
+    sb = (ub << 23) + 0x3F800000u; /* 2^n */
+    float sc;
+    memcpy(&sc, &sb, 4);
+    return p * sc;
+}
+
+/* Test hook: gs_expf over an array (bit-compared with the GPU's gs_exp). */
+void go_expf(int n, const float *x, float *y) {
+    for (int i = 0; i < n; ++i) y[i] = gs_expf(x[i]);
+}
+
 /* auxiliary.h:41-44 — evaluated in double because of the 1.0 literals */
 static float ndc_to_pixel(float v, int S) { return (float)((((double)v + 1.0) * S - 1.0) * 0.5); }
 
@@ -419,12 +452,14 @@ static void render_pixel(const go_state *st, const float *features, const float 
         const float *co = st->conic_opacity + 4 * (size_t)id;
         float power = -0.5f * (co[0] * dx * dx + co[2] * dy * dy) - co[1] * dx * dy;
         if (power > 0.0f) continue;
-        float alpha = fminf(0.99f, co[3] * expf(power));
+        float alpha = fminf(0.99f, co[3] * gs_expf(power));
         if (alpha < 1.0f / 255.0f) continue;
         float test_T = T * (1 - alpha);
         if (test_T < 0.0001f) break;
-        for (int ch = 0; ch < 3; ++ch) C[ch] += features[3 * (size_t)id + ch] * alpha * T;
-        D += st->depths[id] * alpha * T;
+        /* forward.cu:355-357 `C += f * alpha * T` as nvcc's default fmad contracts it:
+         * fma(f * alpha, T, C) (the HIP blend evaluates the same operations) */
+        for (int ch = 0; ch < 3; ++ch) C[ch] = fmaf(features[3 * (size_t)id + ch] * alpha, T, C[ch]);
+        D = fmaf(st->depths[id] * alpha, T, D);
         T = test_T;
         last = contributor;
     }
@@ -433,7 +468,8 @@ static void render_pixel(const go_state *st, const float *features, const float 
     st->n_contrib[pix] = last;
     st->n_visited[pix] = visited_stop;
     const size_t HW = (size_t)st->W * st->H;
-    for (int ch = 0; ch < 3; ++ch) out_color[ch * HW + pix] = C[ch] + T * bg[ch];
+    /* forward.cu:376 `C + T * bg`, contracted: fma(T, bg, C) */
+    for (int ch = 0; ch < 3; ++ch) out_color[ch * HW + pix] = fmaf(T, bg[ch], C[ch]);
     out_depth[pix] = D;
 }
 
@@ -474,8 +510,14 @@ go_state *go_forward(const go_settings *s, const go_inputs *in, float *out_color
 
 /* backward.cu:399-557, one pixel.  Per-(instance) gradient records are kept
  * in double at the instance's sorted position: rec[9*k + {mx,my,cx,cy,cw,op,r,g,b}] */
+/* mag (nullable): per instance, the same 9 fields of sum |sub-term|, the scale
+ * against which a different summation order or factoring is judged (a
+ * cancellation-aware tolerance: see tests/helpers.py raster_grads_close).  Each
+ * gradient term is bounded by the absolute values of the products it adds:
+ * dL_dalpha by sum_ch (|c| + |accum|) |dL_dch| T + |T_final/(1-alpha) bg.dL_dpix|,
+ * dG/d(delx) by |G dx a| + |G dy b|, and so on. */
 static void render_pixel_bwd(const go_state *st, const float *colors, const float *bg, const float *dL_dpix, int tile,
-                             int px, int py, double *rec) {
+                             int px, int py, double *rec, double *mag) {
     const uint32_t r0 = st->ranges[2 * tile], r1 = st->ranges[2 * tile + 1];
     const float pfx = (float)px, pfy = (float)py;
     const size_t pix = (size_t)st->W * py + px, HW = (size_t)st->W * st->H;
@@ -494,7 +536,7 @@ static void render_pixel_bwd(const go_state *st, const float *colors, const floa
         const float *co = st->conic_opacity + 4 * (size_t)id;
         float power = -0.5f * (co[0] * dx * dx + co[2] * dy * dy) - co[1] * dx * dy;
         if (power > 0.0f) continue;
-        float G = expf(power);
+        float G = gs_expf(power);
         float alpha = fminf(0.99f, co[3] * G);
         if (alpha < 1.0f / 255.0f) continue;
         T = T / (1.f - alpha);
@@ -524,6 +566,24 @@ static void render_pixel_bwd(const go_state *st, const float *colors, const floa
         r[3] += (double)(-0.5f * gdx * dy * dL_dG);
         r[4] += (double)(-0.5f * gdy * dy * dL_dG);
         r[5] += (double)(G * dL_dalpha);
+        if (mag) {
+            double ma = 0, bgm = 0;
+            for (int ch = 0; ch < 3; ++ch) {
+                double c = fabs((double)colors[3 * (size_t)id + ch]);
+                ma += (c + fabs((double)accum_rec[ch])) * fabs((double)dL_dpixel[ch]);
+                bgm += fabs((double)bg[ch] * dL_dpixel[ch]);
+            }
+            ma = ma * T + fabs((double)T_final / (1.0 - alpha)) * bgm; /* bounds |dL_dalpha| */
+            const double mG = fabs((double)co[3]) * ma;                   /* bounds |dL_dG| */
+            double *m = mag + 9 * (size_t)k;
+            m[0] += mG * (fabs((double)gdx * co[0]) + fabs((double)gdy * co[1])) * ddelx_dx;
+            m[1] += mG * (fabs((double)gdy * co[2]) + fabs((double)gdx * co[1])) * ddely_dy;
+            m[2] += 0.5 * fabs((double)gdx * dx) * mG;
+            m[3] += 0.5 * fabs((double)gdx * dy) * mG;
+            m[4] += 0.5 * fabs((double)gdy * dy) * mG;
+            m[5] += fabs((double)G) * ma;
+            for (int ch = 0; ch < 3; ++ch) m[6 + ch] += fabs((double)dchannel_dcolor * dL_dpixel[ch]);
+        }
     }
 }
 
@@ -699,23 +759,70 @@ static void cov3d_bwd(const float *scale, float mod, const float *rot, const flo
 #undef D
 }
 
-int go_backward(go_state *st, const go_settings *s, const go_inputs *in, const float *dL_dpix, float *dL_dmeans2D,
-                float *dL_dcolors, float *dL_dopacity, float *dL_dmeans3D, float *dL_dcov3D, float *dL_dsh,
-                float *dL_dscales, float *dL_drotations, float *dL_dconic) {
+/* computeCov2DCUDA + preprocessCUDA bwd (backward.cu:144-396) of Gaussian i from
+ * its summed rasterizer gradients g9 = (dL_dmean2D x, y, dL_dconic x, y, w,
+ * dL_dopacity, dL_dcolor r, g, b) in float. */
+static void gauss_chain(const go_state *st, const go_settings *s, const go_inputs *in, int i, const float g9[9],
+                        float *dL_dmeans3D, float *dL_dcov3D, float *dL_dsh, float *dL_dscales, float *dL_drotations) {
+    const int M = in->M;
+    if (!(st->radii[i] > 0)) return;
+    const float fy = s->image_height / (2.0f * s->tanfovy);
+    const float fx = s->image_width / (2.0f * s->tanfovx);
+    const float *proj = s->projmatrix;
+    const float g2x = g9[0], g2y = g9[1];
+    const float gcon[3] = {g9[2], g9[3], g9[4]};
+    v3 m = v3ld(in->means3D + 3 * (size_t)i);
+    const float *cov3 = in->cov3D_precomp ? in->cov3D_precomp + 6 * (size_t)i : st->cov3D + 6 * (size_t)i;
+    /* computeCov2DCUDA: assignment (backward.cu:273) */
+    v3 gm = cov2d_bwd(m, fx, fy, s->tanfovx, s->tanfovy, cov3, s->viewmatrix, gcon, dL_dcov3D + 6 * (size_t)i);
+    /* preprocessCUDA bwd (backward.cu:370-387) */
+    float mh[4];
+    xform_point44(m, proj, mh);
+    float m_w = 1.0f / (mh[3] + 0.0000001f);
+    float mul1 = (proj[0] * m.x + proj[4] * m.y + proj[8] * m.z + proj[12]) * m_w * m_w;
+    float mul2 = (proj[1] * m.x + proj[5] * m.y + proj[9] * m.z + proj[13]) * m_w * m_w;
+    v3 dm;
+    dm.x = (proj[0] * m_w - proj[3] * mul1) * g2x + (proj[1] * m_w - proj[3] * mul2) * g2y;
+    dm.y = (proj[4] * m_w - proj[7] * mul1) * g2x + (proj[5] * m_w - proj[7] * mul2) * g2y;
+    dm.z = (proj[8] * m_w - proj[11] * mul1) * g2x + (proj[9] * m_w - proj[11] * mul2) * g2y;
+    gm = v3add(gm, dm);
+    if (in->shs) {
+        v3 gdir = sh_bwd(s->sh_degree, m, v3ld(s->campos), in->shs + (size_t)i * M * 3, st->clamped + 3 * (size_t)i,
+                         g9 + 6, dL_dsh + (size_t)i * M * 3);
+        gm = v3add(gm, gdir);
+    }
+    dL_dmeans3D[3 * (size_t)i] = gm.x;
+    dL_dmeans3D[3 * (size_t)i + 1] = gm.y;
+    dL_dmeans3D[3 * (size_t)i + 2] = gm.z;
+    if (in->scales)
+        cov3d_bwd(in->scales + 3 * (size_t)i, s->scale_modifier, in->rotations + 4 * (size_t)i,
+                  dL_dcov3D + 6 * (size_t)i, dL_dscales + 3 * (size_t)i, dL_drotations + 4 * (size_t)i);
+}
+
+static void zero_param_grads(const go_inputs *in, float *dL_dmeans3D, float *dL_dcov3D, float *dL_dsh,
+                             float *dL_dscales, float *dL_drotations) {
     const int P = in->P, M = in->M;
-    if (P == 0) return GO_OK;
-    memset(dL_dmeans2D, 0, 3 * (size_t)P * sizeof(float));
-    memset(dL_dcolors, 0, 3 * (size_t)P * sizeof(float));
-    memset(dL_dopacity, 0, (size_t)P * sizeof(float));
     memset(dL_dmeans3D, 0, 3 * (size_t)P * sizeof(float));
     memset(dL_dcov3D, 0, 6 * (size_t)P * sizeof(float));
     if (M > 0 && dL_dsh) memset(dL_dsh, 0, (size_t)P * M * 3 * sizeof(float));
     memset(dL_dscales, 0, 3 * (size_t)P * sizeof(float));
     memset(dL_drotations, 0, 4 * (size_t)P * sizeof(float));
+}
+
+int go_backward(go_state *st, const go_settings *s, const go_inputs *in, const float *dL_dpix, float *dL_dmeans2D,
+                float *dL_dcolors, float *dL_dopacity, float *dL_dmeans3D, float *dL_dcov3D, float *dL_dsh,
+                float *dL_dscales, float *dL_drotations, float *dL_dconic, float *mag9) {
+    const int P = in->P;
+    if (P == 0) return GO_OK;
+    memset(dL_dmeans2D, 0, 3 * (size_t)P * sizeof(float));
+    memset(dL_dcolors, 0, 3 * (size_t)P * sizeof(float));
+    memset(dL_dopacity, 0, (size_t)P * sizeof(float));
+    zero_param_grads(in, dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales, dL_drotations);
     if (dL_dconic) memset(dL_dconic, 0, 4 * (size_t)P * sizeof(float));
 
     const size_t K = (size_t)st->K;
     double *rec = (double *)calloc((K ? K : 1) * 9, sizeof(double));
+    double *mrec = mag9 ? (double *)calloc((K ? K : 1) * 9, sizeof(double)) : NULL;
     const float *colors = in->colors_precomp ? in->colors_precomp : st->rgb;
     const int ntiles = st->gx * st->gy, W = st->W, H = st->H;
 #pragma omp parallel for schedule(dynamic, 4)
@@ -724,65 +831,59 @@ int go_backward(go_state *st, const go_settings *s, const go_inputs *in, const f
         for (int yy = 0; yy < TILE_Y; ++yy)
             for (int xx = 0; xx < TILE_X; ++xx) {
                 int px = tx * TILE_X + xx, py = ty * TILE_Y + yy;
-                if (px < W && py < H) render_pixel_bwd(st, colors, s->bg, dL_dpix, t, px, py, rec);
+                if (px < W && py < H) render_pixel_bwd(st, colors, s->bg, dL_dpix, t, px, py, rec, mrec);
             }
     }
     /* per-Gaussian sums over its instances, in sorted order (deterministic) */
     double *acc = (double *)calloc((size_t)P * 9, sizeof(double));
+    double *macc = mag9 ? (double *)calloc((size_t)P * 9, sizeof(double)) : NULL;
     for (size_t k = 0; k < K; ++k) {
         double *a = acc + 9 * (size_t)st->point_list[k];
         const double *r = rec + 9 * k;
         for (int j = 0; j < 9; ++j) a[j] += r[j];
+        if (macc) {
+            double *ma = macc + 9 * (size_t)st->point_list[k];
+            for (int j = 0; j < 9; ++j) ma[j] += mrec[9 * k + j];
+        }
     }
     free(rec);
+    free(mrec);
+    if (macc) {
+        for (size_t j = 0; j < (size_t)P * 9; ++j) mag9[j] = (float)macc[j];
+        free(macc);
+    }
 
-    const float fy = s->image_height / (2.0f * s->tanfovy);
-    const float fx = s->image_width / (2.0f * s->tanfovx);
-    const float *proj = s->projmatrix;
 #pragma omp parallel for schedule(static)
     for (int i = 0; i < P; ++i) {
         const double *a = acc + 9 * (size_t)i;
-        float g2x = (float)a[0], g2y = (float)a[1];
-        float gcon[3] = {(float)a[2], (float)a[3], (float)a[4]};
-        dL_dmeans2D[3 * (size_t)i] = g2x;
-        dL_dmeans2D[3 * (size_t)i + 1] = g2y;
-        dL_dopacity[i] = (float)a[5];
-        for (int ch = 0; ch < 3; ++ch) dL_dcolors[3 * (size_t)i + ch] = (float)a[6 + ch];
+        float g9[9];
+        for (int j = 0; j < 9; ++j) g9[j] = (float)a[j];
+        dL_dmeans2D[3 * (size_t)i] = g9[0];
+        dL_dmeans2D[3 * (size_t)i + 1] = g9[1];
+        dL_dopacity[i] = g9[5];
+        for (int ch = 0; ch < 3; ++ch) dL_dcolors[3 * (size_t)i + ch] = g9[6 + ch];
         if (dL_dconic) {
-            dL_dconic[4 * (size_t)i] = gcon[0];
-            dL_dconic[4 * (size_t)i + 1] = gcon[1];
-            dL_dconic[4 * (size_t)i + 3] = gcon[2];
+            dL_dconic[4 * (size_t)i] = g9[2];
+            dL_dconic[4 * (size_t)i + 1] = g9[3];
+            dL_dconic[4 * (size_t)i + 3] = g9[4];
         }
-        if (!(st->radii[i] > 0)) continue;
-        v3 m = v3ld(in->means3D + 3 * (size_t)i);
-        const float *cov3 = in->cov3D_precomp ? in->cov3D_precomp + 6 * (size_t)i : st->cov3D + 6 * (size_t)i;
-        /* computeCov2DCUDA: assignment (backward.cu:273) */
-        v3 gm = cov2d_bwd(m, fx, fy, s->tanfovx, s->tanfovy, cov3, s->viewmatrix, gcon, dL_dcov3D + 6 * (size_t)i);
-        /* preprocessCUDA bwd (backward.cu:370-387) */
-        float mh[4];
-        xform_point44(m, proj, mh);
-        float m_w = 1.0f / (mh[3] + 0.0000001f);
-        float mul1 = (proj[0] * m.x + proj[4] * m.y + proj[8] * m.z + proj[12]) * m_w * m_w;
-        float mul2 = (proj[1] * m.x + proj[5] * m.y + proj[9] * m.z + proj[13]) * m_w * m_w;
-        v3 dm;
-        dm.x = (proj[0] * m_w - proj[3] * mul1) * g2x + (proj[1] * m_w - proj[3] * mul2) * g2y;
-        dm.y = (proj[4] * m_w - proj[7] * mul1) * g2x + (proj[5] * m_w - proj[7] * mul2) * g2y;
-        dm.z = (proj[8] * m_w - proj[11] * mul1) * g2x + (proj[9] * m_w - proj[11] * mul2) * g2y;
-        gm = v3add(gm, dm);
-        if (in->shs) {
-            float dcol[3] = {dL_dcolors[3 * (size_t)i], dL_dcolors[3 * (size_t)i + 1], dL_dcolors[3 * (size_t)i + 2]};
-            v3 gdir = sh_bwd(s->sh_degree, m, v3ld(s->campos), in->shs + (size_t)i * M * 3, st->clamped + 3 * (size_t)i,
-                             dcol, dL_dsh + (size_t)i * M * 3);
-            gm = v3add(gm, gdir);
-        }
-        dL_dmeans3D[3 * (size_t)i] = gm.x;
-        dL_dmeans3D[3 * (size_t)i + 1] = gm.y;
-        dL_dmeans3D[3 * (size_t)i + 2] = gm.z;
-        if (in->scales)
-            cov3d_bwd(in->scales + 3 * (size_t)i, s->scale_modifier, in->rotations + 4 * (size_t)i,
-                      dL_dcov3D + 6 * (size_t)i, dL_dscales + 3 * (size_t)i, dL_drotations + 4 * (size_t)i);
+        gauss_chain(st, s, in, i, g9, dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales, dL_drotations);
     }
     free(acc);
+    return GO_OK;
+}
+
+/* The per-Gaussian chain alone, from given float sums g9 [P,9] (the layout of
+ * gauss_chain): isolates the rasterizer's summation (order-dependent) from the
+ * chain rule after it (fixed IEEE operations, comparable bit for bit). */
+int go_backward_chain(go_state *st, const go_settings *s, const go_inputs *in, const float *g9, float *dL_dmeans3D,
+                      float *dL_dcov3D, float *dL_dsh, float *dL_dscales, float *dL_drotations) {
+    const int P = in->P;
+    if (P == 0) return GO_OK;
+    zero_param_grads(in, dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales, dL_drotations);
+#pragma omp parallel for schedule(static)
+    for (int i = 0; i < P; ++i)
+        gauss_chain(st, s, in, i, g9 + 9 * (size_t)i, dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales, dL_drotations);
     return GO_OK;
 }
 
@@ -829,7 +930,7 @@ int go_apply_weights(const go_settings *s, const go_inputs *in, int C, const flo
                     const float *co = st->conic_opacity + 4 * (size_t)id;
                     float power = -0.5f * (co[0] * dx * dx + co[2] * dy * dy) - co[1] * dx * dy;
                     if (power > 0.0f) continue;
-                    float alpha = fminf(0.99f, co[3] * expf(power));
+                    float alpha = fminf(0.99f, co[3] * gs_expf(power));
                     if (alpha < 1.0f / 255.0f) continue;
                     float test_T = T * (1 - alpha);
                     if (test_T < 0.0001f) break;

@@ -66,11 +66,21 @@ go_state *go_forward(const go_settings *s, const go_inputs *in, float *out_color
                      int *radii, int *num_rendered, int *err);
 
 /* Backward.  All outputs are fully written (no pre-zeroing needed).
- * dL_dconic (optional, [P,4] x,y,_,w as the reference's [P,2,2]). */
+ * dL_dconic (optional, [P,4] x,y,_,w as the reference's [P,2,2]).
+ * mag9 (optional, [P,9]): per Gaussian, sum over its (pixel, instance) terms of
+ * the absolute sub-products of (dL_dmean2D x, y, dL_dconic x, y, w, dL_dopacity,
+ * dL_dcolor r, g, b) — the scale a summation-order difference is judged by. */
 int go_backward(go_state *st, const go_settings *s, const go_inputs *in, const float *dL_dpix,
                 float *dL_dmeans2D, float *dL_dcolors, float *dL_dopacity, float *dL_dmeans3D,
                 float *dL_dcov3D, float *dL_dsh, float *dL_dscales, float *dL_drotations,
-                float *dL_dconic);
+                float *dL_dconic, float *mag9);
+
+/* The per-Gaussian chain (computeCov2DCUDA + preprocessCUDA bwd) alone, from
+ * float rasterizer sums g9 [P,9] = (dL_dmean2D x, y, dL_dconic x, y, w,
+ * dL_dopacity, dL_dcolor r, g, b); st from go_forward. */
+int go_backward_chain(go_state *st, const go_settings *s, const go_inputs *in, const float *g9,
+                      float *dL_dmeans3D, float *dL_dcov3D, float *dL_dsh, float *dL_dscales,
+                      float *dL_drotations);
 
 /* Access an intermediate array by name; returns element count or -1. */
 long go_state_get(go_state *st, const char *name, void **ptr);
@@ -86,6 +96,8 @@ int go_apply_weights(const go_settings *s, const go_inputs *in, int C, const flo
                      float *weights, int *cnt);
 
 /* forward.cu:20-71 for N points (test hook). */
+/* the blend exp (bit-identical to the HIP gs_exp), elementwise */
+void go_expf(int n, const float *x, float *y);
 void go_sh_to_rgb(int N, int deg, int M, const float *pos, const float *campos, const float *shs, float *rgb,
                   unsigned char *clamped);
 

@@ -76,7 +76,10 @@ def lib():
         L.go_forward.restype = ctypes.c_void_p
         L.go_forward.argtypes = [ctypes.POINTER(_Settings), ctypes.POINTER(_Inputs), _f32p, _f32p, _i32p, _i32p, _i32p]
         L.go_backward.restype = ctypes.c_int
-        L.go_backward.argtypes = [ctypes.c_void_p, ctypes.POINTER(_Settings), ctypes.POINTER(_Inputs), _f32p] + [_f32p] * 9
+        L.go_backward.argtypes = [ctypes.c_void_p, ctypes.POINTER(_Settings), ctypes.POINTER(_Inputs), _f32p] + [_f32p] * 10
+        L.go_backward_chain.restype = ctypes.c_int
+        L.go_backward_chain.argtypes = [ctypes.c_void_p, ctypes.POINTER(_Settings), ctypes.POINTER(_Inputs),
+                                        _f32p] + [_f32p] * 5
         L.go_state_get.restype = ctypes.c_long
         L.go_state_get.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_void_p)]
         L.go_free.argtypes = [ctypes.c_void_p]
@@ -85,6 +88,7 @@ def lib():
         L.go_apply_weights.argtypes = [ctypes.POINTER(_Settings), ctypes.POINTER(_Inputs), ctypes.c_int, _f32p, _f32p, _i32p]
         L.go_set_threads.argtypes = [ctypes.c_int]
         L.go_sh_to_rgb.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, _f32p, _f32p, _f32p, _f32p, _u8p]
+        L.go_expf.argtypes = [ctypes.c_int, _f32p, _f32p]
         _lib = L
     return _lib
 
@@ -251,8 +255,10 @@ def forward(settings, means3D, opacities, shs=None, colors_precomp=None, scales=
     return nr.value, color, depth, radii, State(h, s, inp, nr.value)
 
 
-def backward(state: State, dL_dpix):
-    """rasterize_points.cu:97-157 semantics -> dict of the 8 reference grads (+ dL_dconic)."""
+def backward(state: State, dL_dpix, magnitudes: bool = True):
+    """rasterize_points.cu:97-157 semantics -> dict of the 8 reference grads (+ dL_dconic, and with
+    `magnitudes` "mag9" [P,9]: the per-Gaussian sum of absolute sub-terms of (dL_dmean2D x, y,
+    dL_dconic x, y, w, dL_dopacity, dL_dcolor r, g, b), the cancellation-aware scale of each sum)."""
     s, inp = state.settings, state.inputs
     P, M = inp.P, inp.M
     g = _np(dL_dpix).reshape(3, s.image_height, s.image_width)
@@ -267,13 +273,37 @@ def backward(state: State, dL_dpix):
         "dL_drotations": np.zeros((P, 4), np.float32),
         "dL_dconic": np.zeros((P, 2, 2), np.float32),
     }
+    if magnitudes:
+        out["mag9"] = np.zeros((P, 9), np.float32)
     cs, ci = s.c(), inp.c()
     rc = lib().go_backward(state.handle, ctypes.byref(cs), ctypes.byref(ci), _ptr(g), *[
         _ptr(out[k]) if out[k].size else None for k in
         ("dL_dmeans2D", "dL_dcolors", "dL_dopacity", "dL_dmeans3D", "dL_dcov3D", "dL_dsh", "dL_dscales",
-         "dL_drotations", "dL_dconic")])
+         "dL_drotations", "dL_dconic")], _ptr(out["mag9"]) if magnitudes and P else None)
     if rc != 0:
         raise RuntimeError(f"oracle backward failed with code {rc}")
+    return out
+
+
+def backward_chain(state: State, g9):
+    """The per-Gaussian chain of the backward (backward.cu:144-396) from float rasterizer sums
+    g9 [P,9] = (dL_dmean2D x, y, dL_dconic x, y, w, dL_dopacity, dL_dcolor r, g, b)."""
+    s, inp = state.settings, state.inputs
+    P, M = inp.P, inp.M
+    g = np.ascontiguousarray(np.asarray(g9, np.float32).reshape(P, 9))
+    out = {
+        "dL_dmeans3D": np.zeros((P, 3), np.float32),
+        "dL_dcov3D": np.zeros((P, 6), np.float32),
+        "dL_dsh": np.zeros((P, M, 3), np.float32),
+        "dL_dscales": np.zeros((P, 3), np.float32),
+        "dL_drotations": np.zeros((P, 4), np.float32),
+    }
+    cs, ci = s.c(), inp.c()
+    rc = lib().go_backward_chain(state.handle, ctypes.byref(cs), ctypes.byref(ci), _ptr(g), *[
+        _ptr(out[k]) if out[k].size else None for k in
+        ("dL_dmeans3D", "dL_dcov3D", "dL_dsh", "dL_dscales", "dL_drotations")])
+    if rc != 0:
+        raise RuntimeError(f"oracle backward_chain failed with code {rc}")
     return out
 
 
@@ -313,3 +343,12 @@ def sh_to_rgb(deg, shs, pos, campos):
     cl = np.zeros((N, 3), np.uint8)
     lib().go_sh_to_rgb(N, int(deg), M, _ptr(p), _ptr(c), _ptr(sh), _ptr(rgb), _ptr(cl, _u8p))
     return rgb, cl.astype(bool)
+
+
+def expf(x):
+    """The blend's exp (gs_oracle.c gs_expf) elementwise: float32 in, float32 out."""
+    a = _np(x).reshape(-1)
+    y = np.empty_like(a)
+    if a.size:
+        lib().go_expf(int(a.size), _ptr(a), _ptr(y))
+    return y.reshape(np.shape(x))

@@ -5,6 +5,8 @@
                     (gaussiansplatting/utils/sh_utils.py:57-112), imported read-only
                     from /root/reference with bytecode writing disabled.  Pins the
                     oracle's and the kernels' SH->RGB (forward.cu:20-71 restates it).
+  cameras_ref.npz   the REFERENCE's getWorld2View2 / getProjectionMatrix outputs (and the
+                    Simple_Camera composition) for the c1-c5 cameras and random poses.
   scene_*.npz       seeded scenes (inputs) with the oracle's outputs and gradients:
                     the GPU parity tests compare the HIP path against them.
 
@@ -39,6 +41,72 @@ def sh_fixture():
         out[f"rgb_deg{deg}"] = eval_sh(deg, sh, d).numpy()
     np.savez_compressed(os.path.join(OUT, "sh_eval_ref.npz"), **out)
     sys.path.remove("/root/reference")
+
+
+def camera_fixture():
+    """The reference's camera matrices (gaussiansplatting/utils/graphics_utils.py:40-51 getWorld2View2,
+    :67-87 getProjectionMatrix), imported read-only with a `kornia` stand-in module in sys.modules
+    (graphics_utils imports kornia.core at module level, :109-110, for functions this path never
+    calls; kornia is not installed — SURVEY.md §8(c)(ii)).  The Simple_Camera composition
+    (scene/cameras.py:90-94) is evaluated on the CPU with those outputs (the class itself
+    moves every tensor to CUDA).  Cameras: the c1-c5 orbit cameras and seeded random poses with
+    trans/scale."""
+    import math
+    import types
+
+    from dge_amd.cameras import look_at_R_T
+
+    sys.dont_write_bytecode = True
+    stub = types.ModuleType("kornia")
+    core = types.ModuleType("kornia.core")
+    core.Tensor = torch.Tensor
+    core.concatenate, core.stack, core.zeros_like = torch.cat, torch.stack, torch.zeros_like
+    stub.core = core
+    saved = {k: sys.modules.get(k) for k in ("kornia", "kornia.core")}
+    sys.modules["kornia"], sys.modules["kornia.core"] = stub, core
+    sys.path.insert(0, "/root/reference")
+    try:
+        from gaussiansplatting.utils.graphics_utils import getProjectionMatrix, getWorld2View2
+        cams = []
+        for (k, n, W, H) in [(0, 1, 256, 256), (0, 1, 512, 512), (5, 24, 512, 512), (17, 24, 512, 512),
+                             (0, 1, 1920, 1080)]:
+            az, el = 2.0 * math.pi * k / n, math.radians(15.0)
+            pos = 5.0 * np.array([math.cos(el) * math.cos(az), math.cos(el) * math.sin(az), math.sin(el)])
+            R, T = look_at_R_T(pos)
+            fx = math.radians(60.0)
+            cams.append((R, T, np.zeros(3), 1.0, fx, 2.0 * math.atan(math.tan(fx / 2) * H / W)))
+        rng = np.random.default_rng(3)
+        for _ in range(4):
+            q = rng.standard_normal(4)
+            q /= np.linalg.norm(q)
+            w, x, y, z = q
+            R = np.array([[1 - 2 * (y * y + z * z), 2 * (x * y - w * z), 2 * (x * z + w * y)],
+                          [2 * (x * y + w * z), 1 - 2 * (x * x + z * z), 2 * (y * z - w * x)],
+                          [2 * (x * z - w * y), 2 * (y * z + w * x), 1 - 2 * (x * x + y * y)]])
+            cams.append((R, rng.uniform(-3, 3, 3), rng.uniform(-1, 1, 3), float(rng.uniform(0.5, 2.0)),
+                         float(rng.uniform(0.6, 1.6)), float(rng.uniform(0.6, 1.6))))
+        out = {"n": len(cams)}
+        for i, (R, T, trans, scale, fovx, fovy) in enumerate(cams):
+            w2v = getWorld2View2(R, T, trans, scale)
+            proj = getProjectionMatrix(znear=0.01, zfar=100.0, fovX=fovx, fovY=fovy)
+            wv = torch.tensor(w2v).transpose(0, 1)
+            pt = proj.transpose(0, 1)
+            full = wv.unsqueeze(0).bmm(pt.unsqueeze(0)).squeeze(0).float()
+            out.update({f"R{i}": R, f"T{i}": T, f"trans{i}": trans, f"scale{i}": scale, f"fovx{i}": fovx,
+                        f"fovy{i}": fovy, f"w2v{i}": w2v, f"proj{i}": proj.numpy(),
+                        f"world_view{i}": wv.numpy(), f"full_proj{i}": full.numpy(),
+                        f"center{i}": wv.inverse()[3, :3].numpy()})
+        np.savez_compressed(os.path.join(OUT, "cameras_ref.npz"), **out)
+        print("cameras", len(cams))
+    finally:
+        sys.path.remove("/root/reference")
+        for k, v in saved.items():
+            if v is None:
+                sys.modules.pop(k, None)
+            else:
+                sys.modules[k] = v
+        for k in [m for m in sys.modules if m.startswith("gaussiansplatting")]:
+            sys.modules.pop(k)
 
 
 def scene_fixture(name, P, W, H, seed, radius=1.5, scale=0.05, sh_degree=3, bg=(0.0, 0.0, 0.0), mode="sh",
@@ -84,6 +152,7 @@ def scene_fixture(name, P, W, H, seed, radius=1.5, scale=0.05, sh_degree=3, bg=(
 def main():
     os.makedirs(OUT, exist_ok=True)
     sh_fixture()
+    camera_fixture()
     scene_fixture("sh3_96x80", 1500, 96, 80, seed=11)
     scene_fixture("sh1_bg_64", 800, 64, 64, seed=12, sh_degree=1, bg=(0.2, 0.5, 0.9), scale=0.08)
     scene_fixture("colors_120x72", 1000, 120, 72, seed=13, mode="colors", scale=0.06, view=1, nviews=3)
