@@ -245,7 +245,8 @@ def diag_enable(on: bool = True) -> None:
 
 
 def diag_read(which: int, max_u64: int = 1 << 20):
-    """Per-wave diagnostics of the last forward (which=0) / backward (which=1) blend launch:
+    """Per-wave diagnostics of the last forward (which=0) / backward (which=1) blend launch
+    (which=2: k_gauss_bwd_live phase stamps, see gs_backward.hip):
     numpy [n, 8] of (start, end) in 10 ns ticks, kept entries, rounds, loop cycles, total cycles, 0, 0."""
     import numpy as np
 

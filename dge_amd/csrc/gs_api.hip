@@ -182,9 +182,9 @@ struct StageScope {
 struct Diag {
     std::atomic<bool> on{false};
     std::mutex mu;
-    uint64_t* buf[2] = {nullptr, nullptr};
-    size_t cap[2] = {0, 0};
-    size_t used[2] = {0, 0};
+    uint64_t* buf[3] = {nullptr, nullptr, nullptr};
+    size_t cap[3] = {0, 0, 0};
+    size_t used[3] = {0, 0, 0};
 };
 Diag& diag() {
     static Diag d;
@@ -435,7 +435,7 @@ int gs_profile_diag_enable(int on) {
 long long gs_profile_diag_read(int which, uint64_t* host, long long max_u64) {
     Diag& d = diag();
     std::lock_guard<std::mutex> g(d.mu);
-    if (which < 0 || which > 1 || !d.buf[which]) return 0;
+    if (which < 0 || which > 2 || !d.buf[which]) return 0;
     const size_t n = d.used[which] < (size_t)max_u64 ? d.used[which] : (size_t)max_u64;
     GS_HIP(hipDeviceSynchronize());
     GS_HIP(hipMemcpy(host, d.buf[which], n * 8, hipMemcpyDeviceToHost));
@@ -479,7 +479,7 @@ int gs_abi_version(void) { return GS_RASTER_ABI_VERSION; }
 int gs_blend_exp(long long n, const float* x, float* y, gs_stream_t stream) {
     if (n < 0 || (n > 0 && (!x || !y))) return set_error(GS_ERR_INVALID_ARG, "gs_blend_exp: bad arguments");
     if (n == 0) return GS_OK;
-    if ((n + 1) / 2 > 255ll * 0x7FFFFFFF) return set_error(GS_ERR_INVALID_ARG, "gs_blend_exp: n too large");
+    if ((n + 3) / 4 > 255ll * 0x7FFFFFFF) return set_error(GS_ERR_INVALID_ARG, "gs_blend_exp: n too large");
     gs::launch_blend_exp(n, x, y, (hipStream_t)stream);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? GS_OK : set_error(GS_ERR_HIP, "gs_blend_exp launch failed: %s", hipGetErrorString(e));
@@ -699,6 +699,7 @@ int gs_rasterize_backward_ex(const gs_settings* s, const gs_params* gp, int R, c
         ga.grad_mask = o->grad_mask;
         ga.mask_bits = o->grad_mask ? o->mask_bits : 0u;
         ga.dL_dconic = o->dL_dconic;
+        ga.diag = diag_buffer(2, kDiagWords * 4 * (size_t)(P / 256 + 1));
         { StageScope sc(ST_GAUSS_BWD, stream); launch_gauss_backward(ga, stream); }
         GS_LAUNCHED("gaussian backward");
         return GS_OK;

@@ -499,6 +499,9 @@ __global__ __launch_bounds__(kGB) void k_gauss_bwd_live(GaussBwdArgs a) {
     }
     __syncthreads();
     const uint32_t count = s_pre[kLiveGroup];
+    // (diagnostics) per wave, s_memrealtime at: start, the ids/params barrier, records summed, SH staged,
+    // chain computed, outputs committed; then the workgroup's live count and the end
+    uint64_t st[8] = {a.diag ? __builtin_amdgcn_s_memrealtime() : 0, 0, 0, 0, 0, 0, 0, 0};
     // rest floats staged per Gaussian: coefficients 1..15 (degree <= 3 never reads more)
     const int ncol = (a.M - 1) * 3 < kShPitch ? (a.M - 1) * 3 : kShPitch;
     const float inv_ncol = ncol > 0 ? 1.0f / (float)ncol : 0.f;
@@ -524,6 +527,7 @@ __global__ __launch_bounds__(kGB) void k_gauss_bwd_live(GaussBwdArgs a) {
 #pragma unroll
         for (int u = 0; u < 8; ++u) fl[u] = (uint32_t)u < n ? flags[first + u] : 0u;
         __syncthreads();  // s_gid
+        if (a.diag && base == 0) st[1] = __builtin_amdgcn_s_memrealtime();
         const int total = nrow * ncol;
         constexpr int kV = 12;
         if (a.sh.dc && ncol > 0) {
@@ -570,7 +574,9 @@ __global__ __launch_bounds__(kGB) void k_gauss_bwd_live(GaussBwdArgs a) {
                 }
             }
         }
+        if (a.diag && base == 0) st[2] = __builtin_amdgcn_s_memrealtime();
         __syncthreads();  // SH staged
+        if (a.diag && base == 0) st[3] = __builtin_amdgcn_s_memrealtime();
 
         float ddc[3] = {0.f, 0.f, 0.f};
         float dop = acc[5];  // w.r.t. opacity; chained through the sigmoid when activation = 1
@@ -581,7 +587,9 @@ __global__ __launch_bounds__(kGB) void k_gauss_bwd_live(GaussBwdArgs a) {
             gauss_bwd_visible(a, gin, acc, dop, my_sh, ncol, (a.mask_bits & GS_ACC_SH) ? gm : 1.f, ddc, o);
             if (a.grad_mask) apply_grad_mask(a, gm, acc, dop, o);
         }
+        if (a.diag && base == 0) st[4] = __builtin_amdgcn_s_memrealtime();
         if (ok) commit_outputs(a, idx, src, acc, dop, ddc, o);
+        if (a.diag && base == 0) st[5] = __builtin_amdgcn_s_memrealtime();
         // dL_dsh rest rows: through LDS (in place), flat block-wide batches, loads before stores
         if (a.dsh.dc && ncol > 0) {
             __syncthreads();
@@ -603,6 +611,13 @@ __global__ __launch_bounds__(kGB) void k_gauss_bwd_live(GaussBwdArgs a) {
             }
         }
         __syncthreads();  // s_gid / s_sh reused by the next batch
+    }
+    if (a.diag && (threadIdx.x & 63) == 0) {
+        st[7] = __builtin_amdgcn_s_memrealtime();
+        st[6] = count;  // live Gaussians of the workgroup
+        uint64_t* d = a.diag + kDiagWords * ((size_t)blockIdx.x * 4 + (threadIdx.x >> 6));
+#pragma unroll
+        for (int i = 0; i < 8; ++i) d[i] = st[i];
     }
 }
 

@@ -202,23 +202,29 @@ __device__ __forceinline__ float gs_exp(float x) {
     return p * exp_scale(u);
 }
 
-// gs_exp of two values: the same operations, packed (v_pk_mul / v_pk_add / v_pk_fma_f32)
-__device__ __forceinline__ f2v gs_exp2(f2v x) {
+// gs_exp of four values: two independent packed streams, so each dependent
+// v_pk_fma of one stream issues behind the other's (no hazard nops between the
+// Horner steps, which a single packed chain needs on gfx950)
+typedef float f4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ f4v gs_exp4(f4v x) {
 #pragma clang fp contract(off)
-    f2v t = x * kExpLog2e;
+    f4v t = x * kExpLog2e;
     t.x = fminf(fmaxf(t.x, -120.0f), 120.0f);
     t.y = fminf(fmaxf(t.y, -120.0f), 120.0f);
-    const f2v u = t + kExpShifter;
-    const f2v n = u - kExpShifter;
-    const f2v r = __builtin_elementwise_fma(n, f2v{-kExpLn2, -kExpLn2}, x);
-    f2v p = __builtin_elementwise_fma(f2v{kExpC7, kExpC7}, r, f2v{kExpC6, kExpC6});
-    p = __builtin_elementwise_fma(p, r, f2v{kExpC5, kExpC5});
-    p = __builtin_elementwise_fma(p, r, f2v{kExpC4, kExpC4});
-    p = __builtin_elementwise_fma(p, r, f2v{kExpC3, kExpC3});
-    p = __builtin_elementwise_fma(p, r, f2v{0.5f, 0.5f});
-    p = __builtin_elementwise_fma(p, r, f2v{1.0f, 1.0f});
-    p = __builtin_elementwise_fma(p, r, f2v{1.0f, 1.0f});
-    return p * f2v{exp_scale(u.x), exp_scale(u.y)};
+    t.z = fminf(fmaxf(t.z, -120.0f), 120.0f);
+    t.w = fminf(fmaxf(t.w, -120.0f), 120.0f);
+    const f4v u = t + kExpShifter;
+    const f4v n = u - kExpShifter;
+    const f4v c = {1.0f, 1.0f, 1.0f, 1.0f};
+    const f4v r = __builtin_elementwise_fma(n, -kExpLn2 * c, x);
+    f4v p = __builtin_elementwise_fma(kExpC7 * c, r, kExpC6 * c);
+    p = __builtin_elementwise_fma(p, r, kExpC5 * c);
+    p = __builtin_elementwise_fma(p, r, kExpC4 * c);
+    p = __builtin_elementwise_fma(p, r, kExpC3 * c);
+    p = __builtin_elementwise_fma(p, r, 0.5f * c);
+    p = __builtin_elementwise_fma(p, r, c);
+    p = __builtin_elementwise_fma(p, r, c);
+    return p * f4v{exp_scale(u.x), exp_scale(u.y), exp_scale(u.z), exp_scale(u.w)};
 }
 
 // GaussianModel activations (gaussian_model.py:42-57): sigmoid, exp,

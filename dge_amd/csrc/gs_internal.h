@@ -365,6 +365,7 @@ struct GaussBwdArgs {
     const uint8_t* grad_mask;  // optional [P]: outputs in mask_bits are multiplied by it
     uint32_t mask_bits;
     float* dL_dconic;          // optional [P,3]: the summed conic gradient (parity tests)
+    uint64_t* diag;            // optional per-wave phase stamps of k_gauss_bwd_live (see diag_buffer)
 };
 void launch_gauss_backward(const GaussBwdArgs& a, hipStream_t s);
 
@@ -372,7 +373,7 @@ void launch_gauss_backward(const GaussBwdArgs& a, hipStream_t s);
 // kDiagWords u64 each: start, end (s_memrealtime, 100 MHz), kept entries,
 // rounds, cycles in the blend/replay loops, total cycles (s_memtime).
 constexpr int kDiagWords = 8;
-uint64_t* diag_buffer(int which, size_t n_u64);  // which: 0 forward, 1 backward; nullptr when off
+uint64_t* diag_buffer(int which, size_t n_u64);  // which: 0 forward, 1 backward, 2 gauss_bwd; nullptr when off
 int report_error(int code, const char* msg);      // sets gs_last_error(), returns code
 
 }  // namespace gs

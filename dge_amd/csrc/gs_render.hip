@@ -36,15 +36,17 @@ namespace gs {
 // oracle evaluates bit for bit, so every alpha and blend decision is the oracle's
 __device__ __forceinline__ float blend_exp(float x) { return gs_exp(x); }
 
-// test hook (gs_blend_exp): the blend exp over an array, packed as the blend loops use it
+// test hook (gs_blend_exp): the blend exp over an array, four-wide as the blend loops use it
 __global__ __launch_bounds__(256) void k_blend_exp(long long n, const float* __restrict__ x, float* __restrict__ y) {
-    const long long i = 2 * ((long long)blockIdx.x * 256 + threadIdx.x);
-    if (i + 1 < n) {
-        const f2v r = gs_exp2(f2v{x[i], x[i + 1]});
+    const long long i = 4 * ((long long)blockIdx.x * 256 + threadIdx.x);
+    if (i + 3 < n) {
+        const f4v r = gs_exp4(f4v{x[i], x[i + 1], x[i + 2], x[i + 3]});
         y[i] = r.x;
         y[i + 1] = r.y;
-    } else if (i < n) {
-        y[i] = gs_exp(x[i]);
+        y[i + 2] = r.z;
+        y[i + 3] = r.w;
+    } else {
+        for (long long k = i; k < n; ++k) y[k] = gs_exp(x[k]);
     }
 }
 
@@ -91,22 +93,25 @@ __device__ __forceinline__ Entry gather_entry(const Splat* splat, uint32_t id) {
     return e;
 }
 
-// pixel_alpha for two consecutive entries at once: the same IEEE operations in
-// the same order (contraction pinned), on float2 so the compiler issues packed
-// v_pk_add/v_pk_mul (two entries per instruction); results bit-identical to
-// two pixel_alpha calls.
-__device__ __forceinline__ void pixel_alpha2(f2v x, f2v y, f2v cx, f2v cy, f2v cz, f2v op, float pfx, float pfy,
-                                             f2v& dx, f2v& dy, f2v& G, f2v& alpha, bool& ok0, bool& ok1) {
+// pixel_alpha for four consecutive entries: two packed streams (f4v ops split
+// into pairs of v_pk_* instructions), bit-identical to four pixel_alpha calls.
+// Operands arrive pre-negated where a subtraction would otherwise not pack
+// (v_pk_add_f32 has no subtract form): ncy = -conic.y, (npx, npy) = -pixel, and
+//   x + npx == x - px,   (-0.5 (a dx^2 + c dy^2)) + (ncy dx) dy == ... - (b dx) dy
+// exactly (negation is exact, a - b == a + (-b) in IEEE arithmetic).
+__device__ __forceinline__ void pixel_alpha4(f4v x, f4v y, f4v cx, f4v ncy, f4v cz, f4v op, float npx, float npy,
+                                             f4v& dx, f4v& dy, f4v& G, f4v& alpha, bool (&ok)[4]) {
 #pragma clang fp contract(off)
-    dx = x - pfx;
-    dy = y - pfy;
-    const f2v power = -0.5f * (cx * dx * dx + cz * dy * dy) - cy * dx * dy;
-    G = gs_exp2(power);
-    const f2v oG = op * G;
-    alpha.x = fminf(0.99f, oG.x);
-    alpha.y = fminf(0.99f, oG.y);
-    ok0 = !(power.x > 0.0f) && !(alpha.x < 1.0f / 255.0f);
-    ok1 = !(power.y > 0.0f) && !(alpha.y < 1.0f / 255.0f);
+    dx = x + npx;
+    dy = y + npy;
+    const f4v power = -0.5f * (cx * dx * dx + cz * dy * dy) + ncy * dx * dy;
+    G = gs_exp4(power);
+    const f4v oG = op * G;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        alpha[u] = fminf(0.99f, oG[u]);
+        ok[u] = !(power[u] > 0.0f) && !(alpha[u] < 1.0f / 255.0f);
+    }
 }
 
 // The sequential part of blend_step once the entry's alpha test is done, on a
@@ -174,7 +179,7 @@ __global__ __launch_bounds__(1024) void k_tile_order(const uint2* __restrict__ r
     }
 }
 
-__global__ __launch_bounds__(64) void k_render_fwd(RenderArgs a) {
+__global__ __launch_bounds__(64, 3) void k_render_fwd(RenderArgs a) {
     // XCD-aware: blocks b, b+8, b+16, b+24 (one XCD under the round-robin dealing) take the four
     // quadrants of one tile, so the tile's list and its Splat gathers are fetched into one L2;
     // tiles in k_tile_order's order, longest list first
@@ -191,7 +196,7 @@ __global__ __launch_bounds__(64) void k_render_fwd(RenderArgs a) {
     const float pfx = (float)px, pfy = (float)py;
 
     // the round's kept entries, one array per field: a pair of consecutive entries' field is one
-    // 8-B read, the operand of a packed instruction (pixel_alpha2)
+    // 16-B read, the operands of two packed instructions (pixel_alpha4)
     __shared__ float s_x[kRound + kGroup], s_y[kRound + kGroup];
     __shared__ float s_cx[kRound + kGroup], s_cy[kRound + kGroup], s_cz[kRound + kGroup], s_op[kRound + kGroup];
     __shared__ float4 s_rgbd[kRound + kGroup];
@@ -263,7 +268,7 @@ __global__ __launch_bounds__(64) void k_render_fwd(RenderArgs a) {
                 s_x[slot] = cur[i].xy.x;
                 s_y[slot] = cur[i].xy.y;
                 s_cx[slot] = cur[i].co.x;
-                s_cy[slot] = cur[i].co.y;
+                s_cy[slot] = -cur[i].co.y;  // (negated: pixel_alpha4)
                 s_cz[slot] = cur[i].co.z;
                 s_op[slot] = cur[i].co.w;
                 s_rgbd[slot] = cur[i].f;
@@ -305,19 +310,16 @@ __global__ __launch_bounds__(64) void k_render_fwd(RenderArgs a) {
         // position reads are issued before the next group's prefetch: LDS reads retire in order, so
         // waiting for them does not wait for the prefetch.  Reads past nk land in the padding or
         // stale slots (index < kRound + kGroup) and are never used.
-        struct AlphaOps { f2v x[2], y[2], cx[2], cy[2], cz[2], op[2]; };
+        struct AlphaOps { f4v x, y, cx, cy, cz, op; };
         struct ColourOps { float4 rgbd[kGroup]; uint32_t pos[kGroup]; };
         const auto load_alpha = [&](int j, AlphaOps& g) {
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const auto ld2 = [&](const float* f) { return *reinterpret_cast<const f2v*>(f + j + 2 * h); };
-                g.x[h] = ld2(s_x);
-                g.y[h] = ld2(s_y);
-                g.cx[h] = ld2(s_cx);
-                g.cy[h] = ld2(s_cy);
-                g.cz[h] = ld2(s_cz);
-                g.op[h] = ld2(s_op);
-            }
+            const auto ld4 = [&](const float* f) { return *reinterpret_cast<const f4v*>(f + j); };
+            g.x = ld4(s_x);
+            g.y = ld4(s_y);
+            g.cx = ld4(s_cx);
+            g.cy = ld4(s_cy);
+            g.cz = ld4(s_cz);
+            g.op = ld4(s_op);
         };
         const auto load_colour = [&](int j, ColourOps& c) {
 #pragma unroll
@@ -327,21 +329,17 @@ __global__ __launch_bounds__(64) void k_render_fwd(RenderArgs a) {
             }
         };
         const auto blend_group = [&](int j, const AlphaOps& g, const ColourOps& c) {
-            uint32_t gm = 0u;  // (uniform: scalar ops beside the blend's vector ones)
+            f4v dx4, dy4, G4, al;
+            bool ok[4];
+            pixel_alpha4(g.x, g.y, g.cx, g.cy, g.cz, g.op, -pfx, -pfy, dx4, dy4, G4, al, ok);
+            uint64_t vm[kGroup];  // per entry: the lanes that blended it (uniform masks, SALU)
 #pragma unroll
-            for (int u = 0; u < kGroup; u += 2) {
-                f2v al, dx2, dy2, G2;
-                bool ok0, ok1;
-                const int h = u / 2;
-                pixel_alpha2(g.x[h], g.y[h], g.cx[h], g.cy[h], g.cz[h], g.op[h], pfx, pfy, dx2, dy2, G2, al, ok0,
-                             ok1);
-                const float w0 = blend_chain(ok0 ? al.x : 0.0f, c.rgbd[u], c.pos[u], Ts, C01, C2D, L01, L2, last);
-                gm |= (__builtin_amdgcn_fcmpf(w0, 0.0f, kFcmpOGT) != 0ull ? 1u : 0u) << u;
-                const float w1 =
-                    blend_chain(ok1 ? al.y : 0.0f, c.rgbd[u + 1], c.pos[u + 1], Ts, C01, C2D, L01, L2, last);
-                gm |= (__builtin_amdgcn_fcmpf(w1, 0.0f, kFcmpOGT) != 0ull ? 1u : 0u) << (u + 1);
+            for (int u = 0; u < kGroup; ++u) {
+                const float w = blend_chain(ok[u] ? al[u] : 0.0f, c.rgbd[u], c.pos[u], Ts, C01, C2D, L01, L2, last);
+                vm[u] = __builtin_amdgcn_fcmpf(w, 0.0f, kFcmpOGT);
             }
-            s_gused[j / kGroup] = gm;
+            const uint32_t gm = (vm[0] ? 1u : 0u) | (vm[1] ? 2u : 0u) | (vm[2] ? 4u : 0u) | (vm[3] ? 8u : 0u);
+            s_gused[j / kGroup] = __builtin_amdgcn_readfirstlane(gm);
         };
         AlphaOps ga, gb;
         ColourOps cc;
@@ -510,8 +508,8 @@ __global__ __launch_bounds__(64) void k_render_apply_weights(ApplyWeightsArgs a)
 }
 
 void launch_blend_exp(long long n, const float* x, float* y, hipStream_t s) {
-    const long long pairs = (n + 1) / 2;
-    hipLaunchKernelGGL(k_blend_exp, dim3((unsigned)((pairs + 255) / 256)), dim3(256), 0, s, n, x, y);
+    const long long quads = (n + 3) / 4;
+    hipLaunchKernelGGL(k_blend_exp, dim3((unsigned)((quads + 255) / 256)), dim3(256), 0, s, n, x, y);
 }
 
 void launch_render_apply_weights(const ApplyWeightsArgs& a, hipStream_t s) {
@@ -538,7 +536,7 @@ void launch_render_apply_weights(const ApplyWeightsArgs& a, hipStream_t s) {
 // — the entry's conic, opacity and the ndc scale are constant over pixels
 // and are applied once per entry after the reduction (finish_record).
 //
-// Two consecutive entries of the replay: the alpha tests packed (pixel_alpha2),
+// Four consecutive entries of the replay: the alpha tests packed (pixel_alpha4),
 // the back-to-front chain (T, D) entry by entry (bwd_chain), the per-pixel
 // products of the nine sums packed again.
 __device__ __forceinline__ float bwd_chain(bool hit, float alpha, float G, float4 c, float dp0, float dp1, float dp2,
@@ -558,30 +556,34 @@ __device__ __forceinline__ float bwd_chain(bool hit, float alpha, float G, float
     return hit ? G * dL_dalpha : 0.f;
 }
 
-__device__ __forceinline__ void bwd_pair(f2v x, f2v y, f2v cx, f2v cy, f2v cz, f2v op, float4 c0, float4 c1, bool in0,
-                                         bool in1, float pfx, float pfy, float dp0, float dp1, float dp2, float nbg,
-                                         float& T, float& D0, float& D1, float& D2, float (&g0)[9], float (&g1)[9]) {
-    f2v dx, dy, G, alpha;
-    bool ok0, ok1;
-    pixel_alpha2(x, y, cx, cy, cz, op, pfx, pfy, dx, dy, G, alpha, ok0, ok1);
-    float wc0, wc1;
-    f2v u, wc;
-    u.x = bwd_chain(ok0 && in0, alpha.x, G.x, c0, dp0, dp1, dp2, nbg, T, D0, D1, D2, wc0);
-    u.y = bwd_chain(ok1 && in1, alpha.y, G.y, c1, dp0, dp1, dp2, nbg, T, D0, D1, D2, wc1);
-    wc.x = wc0;
-    wc.y = wc1;
-    const f2v udx = u * dx, udy = u * dy;
-    const f2v gxx = udx * dx, gxy = udx * dy, gyy = udy * dy;
-    const f2v w0 = wc * dp0, w1 = wc * dp1, w2 = wc * dp2;
-    g0[0] = udx.x; g1[0] = udx.y;
-    g0[1] = udy.x; g1[1] = udy.y;
-    g0[2] = gxx.x; g1[2] = gxx.y;
-    g0[3] = gxy.x; g1[3] = gxy.y;
-    g0[4] = gyy.x; g1[4] = gyy.y;
-    g0[5] = u.x;   g1[5] = u.y;
-    g0[6] = w0.x;  g1[6] = w0.y;
-    g0[7] = w1.x;  g1[7] = w1.y;
-    g0[8] = w2.x;  g1[8] = w2.y;
+__device__ __forceinline__ void bwd_quad(f4v x, f4v y, f4v cx, f4v ncy, f4v cz, f4v op, const float4 (&c)[4],
+                                         const bool (&in)[4], float pfx, float pfy, float dp0, float dp1, float dp2,
+                                         float nbg, float& T, float& D0, float& D1, float& D2, float (&g)[4][9]) {
+    f4v dx, dy, G, alpha;
+    bool ok[4];
+    pixel_alpha4(x, y, cx, ncy, cz, op, -pfx, -pfy, dx, dy, G, alpha, ok);
+    f4v u, wc;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        float w;
+        u[e] = bwd_chain(ok[e] && in[e], alpha[e], G[e], c[e], dp0, dp1, dp2, nbg, T, D0, D1, D2, w);
+        wc[e] = w;
+    }
+    const f4v udx = u * dx, udy = u * dy;
+    const f4v gxx = udx * dx, gxy = udx * dy, gyy = udy * dy;
+    const f4v w0 = wc * dp0, w1 = wc * dp1, w2 = wc * dp2;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        g[e][0] = udx[e];
+        g[e][1] = udy[e];
+        g[e][2] = gxx[e];
+        g[e][3] = gxy[e];
+        g[e][4] = gyy[e];
+        g[e][5] = u[e];
+        g[e][6] = w0[e];
+        g[e][7] = w1[e];
+        g[e][8] = w2[e];
+    }
 }
 
 // The entry's record from the quadrant sums S: the reference's per-pixel
@@ -597,28 +599,27 @@ __device__ __forceinline__ void finish_record(float4 co, const float (&S)[9], fl
     rec[2] = make_float4(S[8], 0.f, 0.f, 0.f);
 }
 
-constexpr int kBwdGroup = 4;  // entries replayed between two reduce-scatters
+constexpr int kBwdGroup = 4;            // entries replayed between two reduce-scatters
+constexpr int kBwdHalf = kSegLen / 2;   // list positions per half-segment (LDS staging unit)
 
-// One wave per 8x8 quadrant, independent workgroups (no block barrier):
-// the wave walks its own window [0, quad_last) of the tile list back to
-// front in rounds of 256 (ids two rounds, geometry one round ahead), culls
-// each round against its quadrant, replays the survivors in groups of four
-// and reduce-scatters their nine sums across the wave (quad_reduce).  Each
-// kept entry gets one 48-byte record at 4*slot + quadrant (slot: the binning
-// slot, so k_gauss_bwd reads a Gaussian's records contiguously) and a flag.
+// One wave per work item = (8x8 quadrant, segment of its window), independent
+// 64-thread workgroups.  A segment is at most kSegLen = 256 list positions: the
+// wave loads their (Gaussian, slot) pairs and the forward's blended bits (4 per
+// lane), gathers the Splats of the blended ones, and replays the segment back
+// to front in two halves of 128 positions staged through LDS (6.9 KB: with
+// <= 128 VGPRs, 4 waves per SIMD), each in groups of four entries whose nine
+// sums are reduce-scattered across the wave (quad_reduce).  Each kept entry gets
+// one record at 4*slot + quadrant (slot: the binning slot, so k_gauss_bwd reads
+// a Gaussian's records contiguously) and a flag.
 __global__ __launch_bounds__(64, 4) void k_render_bwd(RenderBwdArgs a) {
-    // kept entries of a round, compacted back to front, + a group of padding
-    // (one array per field: a pair of consecutive entries' field is one 8-B read, see bwd_pair)
-    __shared__ float s_x[kRound + kBwdGroup], s_y[kRound + kBwdGroup];
-    __shared__ float s_cx[kRound + kBwdGroup], s_cy[kRound + kBwdGroup], s_cz[kRound + kBwdGroup],
-        s_op[kRound + kBwdGroup];
-    __shared__ float4 s_rgb[kRound + kBwdGroup];
-    __shared__ uint32_t s_pos[kRound + kBwdGroup];
-    // (Gaussian, slot) of the next round's entries by round position, stashed when their gathers are
-    // issued, then of the kept entries by compacted slot: the record writes read them from LDS
-    // instead of re-loading point_pairs (a dependent global round trip per group of four)
-    __shared__ uint2 s_stash[kRound];
-    __shared__ uint2 s_pair[kRound + kBwdGroup];
+    // kept entries of a half-segment, compacted back to front, + a group of padding
+    // (one array per field: four consecutive entries' field is one 16-B read, see bwd_quad)
+    __shared__ float s_x[kBwdHalf + kBwdGroup], s_y[kBwdHalf + kBwdGroup];
+    __shared__ float s_cx[kBwdHalf + kBwdGroup], s_cy[kBwdHalf + kBwdGroup], s_cz[kBwdHalf + kBwdGroup],
+        s_op[kBwdHalf + kBwdGroup];
+    __shared__ float4 s_rgb[kBwdHalf + kBwdGroup];
+    __shared__ uint32_t s_pos[kBwdHalf + kBwdGroup];
+    __shared__ uint2 s_pair[kBwdHalf + kBwdGroup];  // (Gaussian, slot) of the kept entries: the record writes
     const int lane = threadIdx.x;
     // block -> work item (quadrant, segment) of the forward's list: multi-segment windows first;
     // blocks past the list's end exit (they dispatch after every real item).  (A persistent-wave
@@ -626,7 +627,6 @@ __global__ __launch_bounds__(64, 4) void k_render_bwd(RenderBwdArgs a) {
     const uint32_t n_multi = a.bwd_count[0], n_items = n_multi + a.bwd_count[1];
     const uint32_t qi = blockIdx.x;
     if (qi >= n_items) return;
-    {
     const uint2 item = qi < n_multi ? a.bwd_items[qi] : a.bwd_items[a.item_cap - 1 - (qi - n_multi)];
     const int tile = (int)item.x, quad = (int)(item.y & 3u), seg = (int)(item.y >> 2);
     const int qidx = 4 * tile + quad;
@@ -639,12 +639,32 @@ __global__ __launch_bounds__(64, 4) void k_render_bwd(RenderBwdArgs a) {
     const uint2 range = a.ranges[tile];
     const int window = (int)a.quad_last[qidx];  // the quadrant's last contributor (1-based)
     const int nseg_q = (window + kSegLen - 1) / kSegLen;
-    // this wave's segment [seg_lo, limit) of the window; the last segment ends at the window
-    const int seg_lo = seg * kSegLen;
-    const int limit = seg == nseg_q - 1 ? window : seg_lo + kSegLen;
+    // this wave's segment [lo, limit) of the window; the last segment ends at the window
+    const int lo = seg * kSegLen;
+    const int limit = seg == nseg_q - 1 ? window : lo + kSegLen;
+    const int n = limit - lo;
+
+    // (Gaussian, slot) and the forward's blended bit of the segment's entries (entry lo + 64 i + lane).
+    // An entry no pixel of the quadrant blended has an all-zero gradient: the bit is the exact cull
+    // (the forward's `use` is the replay's `hit && pos < n_contrib`).
+    const uint32_t* used32 = reinterpret_cast<const uint32_t*>(a.used + (size_t)used_base(range.x, tile) * 4 + quad);
+    uint2 pairs[4];
+    uint32_t kb = 0u;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int j = 64 * i + lane, k = lo + j;
+        const bool in = j < n;
+        pairs[i] = in ? a.point_pairs[range.x + k] : make_uint2(0u, 0u);
+        const uint32_t ub = in ? used32[(size_t)(k >> 6) * 8 + ((k >> 5) & 1)] : 0u;
+        kb |= ((ub >> (k & 31)) & 1u) << i;
+    }
+    Entry cur[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)  // (dropped entries gather Gaussian 0: one shared line)
+        cur[i] = gather_entry(a.splat, (kb >> i) & 1u ? pairs[i].x : 0u);
+
     const size_t HW = (size_t)a.W * a.H;
     const size_t pix = inside ? (size_t)a.W * py + px : 0;
-
     const float T_final = inside ? a.final_T[pix] : 0.f;
     const uint32_t last_contributor = inside ? a.n_contrib[pix] : 0u;
     float dp0 = 0.f, dp1 = 0.f, dp2 = 0.f;
@@ -677,71 +697,33 @@ __global__ __launch_bounds__(64, 4) void k_render_bwd(RenderBwdArgs a) {
     const uint64_t t_start = a.diag ? __builtin_amdgcn_s_memrealtime() : 0;
     const uint64_t c_start = a.diag ? __builtin_amdgcn_s_memtime() : 0;
     uint64_t c_replay = 0;
-    uint32_t diag_kept = 0, diag_rounds = 0;
+    uint32_t diag_kept = 0;
 
     // the lane-row -> entry map of quad_reduce's result (rows hold e0, e0+2, e0+1, e0+3)
     const int row = lane >> 4;
     const int row_entry = row == 1 ? 2 : row == 2 ? 1 : row;
     const bool row_writer = (lane & 15) == 0;
 
-    const int nr = (limit - seg_lo + kRound - 1) / kRound;
-    const uint64_t* used = a.used + (size_t)used_base(range.x, tile) * 4 + quad;
-    // (Gaussian, slot) and the forward's blended bit of each entry of round r, two rounds ahead
-    // of the replay.  An entry no pixel of the quadrant blended has an all-zero gradient: the
-    // bit is the exact cull (the forward's `use` is the replay's `hit && pos < n_contrib`).
-    // (the 32-bit half of the word holding each entry's bit; decoded where the pairs are consumed)
-    const uint32_t* used32 = reinterpret_cast<const uint32_t*>(used);
-    auto round_pairs = [&](int r, uint2 (&pr)[4], uint32_t (&ub)[4]) {
-        const int hi = limit - kRound * r, lo = hi - kRound > seg_lo ? hi - kRound : seg_lo;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int k = lo + 64 * i + lane;
-            const bool in = r < nr && k < hi;
-            pr[i] = in ? a.point_pairs[range.x + k] : make_uint2(0u, 0u);
-            ub[i] = in ? used32[(size_t)(k >> 6) * 8 + ((k >> 5) & 1)] : 0u;
-        }
-    };
-    // the round's kept bits (bit i: entry lo + 64 i + lane) from its loaded halves
-    auto kept_bits = [&](int r, const uint32_t (&ub)[4]) {
-        const int hi = limit - kRound * r, lo = hi - kRound > seg_lo ? hi - kRound : seg_lo;
-        uint32_t kb = 0u;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) kb |= ((ub[i] >> ((lo + 64 * i + lane) & 31)) & 1u) << i;
-        return kb;
-    };
-    uint2 pairs[4];
-    uint32_t ubits[4], kb_cur;
-    Entry cur[4];
-    round_pairs(0, pairs, ubits);
-    kb_cur = kept_bits(0, ubits);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {  // (dropped entries gather Gaussian 0: one shared line)
-        cur[i] = gather_entry(a.splat, (kb_cur >> i) & 1u ? pairs[i].x : 0u);
-        s_stash[64 * i + lane] = pairs[i];
-    }
-    round_pairs(1, pairs, ubits);
-
-    for (int r = 0; r < nr; ++r) {
-        const int hi = limit - kRound * r, lo = hi - kRound > seg_lo ? hi - kRound : seg_lo;
-        const int n = hi - lo;
-        // compact the forward's blended entries back to front
+    for (int h = 1; h >= 0; --h) {  // back half (positions 128..255) first
+        // compact the forward's blended entries of this half back to front
         int nk = 0;
 #pragma unroll
-        for (int i = 3; i >= 0; --i) {
+        for (int i = 2 * h + 1; i >= 2 * h; --i) {
             const int j = 64 * i + lane;
-            const bool keep = j < n && ((kb_cur >> i) & 1u);
+            const bool keep = j < n && ((kb >> i) & 1u);
             const uint64_t km = __ballot(keep);
             if (keep) {
                 const int slot = nk + __popcll(km & ~lanemask_lt() & ~(1ull << lane));
                 s_x[slot] = cur[i].xy.x;
                 s_y[slot] = cur[i].xy.y;
                 s_cx[slot] = cur[i].co.x;
-                s_cy[slot] = cur[i].co.y;
+                s_cy[slot] = -cur[i].co.y;  // (negated: pixel_alpha4; finish_record negates back)
                 s_cz[slot] = cur[i].co.z;
                 s_op[slot] = cur[i].co.w;
                 s_rgb[slot] = cur[i].f;
                 s_pos[slot] = (uint32_t)(lo + j);
-                s_pair[slot] = s_stash[j];
+                s_pair[slot] = pairs[i];
             }
             nk += __popcll(km);
         }
@@ -755,36 +737,30 @@ __global__ __launch_bounds__(64, 4) void k_render_bwd(RenderBwdArgs a) {
             s_rgb[nk + lane] = make_float4(0.f, 0.f, 0.f, 0.f);
             s_pos[nk + lane] = 0xFFFFFFFFu;
         }
-        // next round's geometry and the round after's ids, in flight during the replay
-        kb_cur = kept_bits(r + 1, ubits);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            cur[i] = gather_entry(a.splat, (kb_cur >> i) & 1u ? pairs[i].x : 0u);
-            s_stash[64 * i + lane] = pairs[i];  // (after this round's compaction read its stash)
-        }
-        round_pairs(r + 2, pairs, ubits);
         diag_kept += nk;
-        diag_rounds += 1;
         __syncthreads();
 
         const uint64_t c0 = a.diag ? __builtin_amdgcn_s_memtime() : 0;
         for (int k = 0; k < nk; k += kBwdGroup) {
             float g[kBwdGroup][9];
-#pragma unroll
-            for (int e = 0; e < kBwdGroup; e += 2) {
-                const auto ld2 = [&](const float* f) { return *reinterpret_cast<const f2v*>(f + k + e); };
-                bwd_pair(ld2(s_x), ld2(s_y), ld2(s_cx), ld2(s_cy), ld2(s_cz), ld2(s_op), s_rgb[k + e],
-                         s_rgb[k + e + 1], s_pos[k + e] < last_contributor, s_pos[k + e + 1] < last_contributor, pfx,
-                         pfy, dp0, dp1, dp2, nbg, T, D0, D1, D2, g[e], g[e + 1]);
+            {
+                const auto ld4 = [&](const float* f) { return *reinterpret_cast<const f4v*>(f + k); };
+                const float4 c4[4] = {s_rgb[k], s_rgb[k + 1], s_rgb[k + 2], s_rgb[k + 3]};
+                const bool in4[4] = {s_pos[k] < last_contributor, s_pos[k + 1] < last_contributor,
+                                     s_pos[k + 2] < last_contributor, s_pos[k + 3] < last_contributor};
+                bwd_quad(ld4(s_x), ld4(s_y), ld4(s_cx), ld4(s_cy), ld4(s_cz), ld4(s_op), c4, in4, pfx, pfy, dp0, dp1,
+                         dp2, nbg, T, D0, D1, D2, g);
             }
+            __builtin_amdgcn_sched_barrier(0);  // (every product first: the lane swaps clobber their operands)
             float S[9];
 #pragma unroll
             for (int f = 0; f < 9; ++f) S[f] = quad_reduce(g[0][f], g[1][f], g[2][f], g[3][f]);
+            __builtin_amdgcn_sched_barrier(0);
             const int kw = k + row_entry;
             if (row_writer && kw < nk) {
                 const uint2 pr = s_pair[kw];
                 const size_t rec = 4 * (size_t)pr.y + quad;
-                finish_record(make_float4(s_cx[kw], s_cy[kw], s_cz[kw], s_op[kw]), S, ddelx_dx, ddely_dy,
+                finish_record(make_float4(s_cx[kw], -s_cy[kw], s_cz[kw], s_op[kw]), S, ddelx_dx, ddely_dy,
                               a.records + 3 * rec);
                 a.rec_flags[rec] = 1;
                 a.touched[pr.x] = 1;
@@ -798,12 +774,11 @@ __global__ __launch_bounds__(64, 4) void k_render_bwd(RenderBwdArgs a) {
         d[0] = t_start;
         d[1] = __builtin_amdgcn_s_memrealtime();
         d[2] = diag_kept;
-        d[3] = diag_rounds;
+        d[3] = 1;
         d[4] = c_replay;
         d[5] = __builtin_amdgcn_s_memtime() - c_start;
         d[6] = (uint64_t)seg << 32 | (uint32_t)qidx;
         d[7] = wave_location();
-    }
     }
 }
 

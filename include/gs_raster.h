@@ -264,7 +264,8 @@ int gs_profile_collect(double *total_ms, int *counts, int n);
  * replay record per wave (8 u64) {start, end (s_memrealtime, 100 MHz), kept
  * entries, rounds, cycles inside the blend/replay loops, total cycles
  * (s_memtime), 0, 0}; gs_profile_diag_read copies the last launch's records
- * (which: 0 forward, 1 backward) to host memory and returns the u64 count. */
+ * (which: 0 forward, 1 backward, 2 the per-Gaussian backward's phase stamps) to host memory and
+ * returns the u64 count. */
 int gs_profile_diag_enable(int on);
 long long gs_profile_diag_read(int which, uint64_t *host, long long max_u64);
 

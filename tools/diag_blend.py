@@ -83,6 +83,19 @@ def main():
     _native.diag_enable(False)
     summarize("render_fwd", _native.diag_read(0))
     summarize("render_bwd", _native.diag_read(1), nquads=4 * ((W + 15) // 16) * ((H + 15) // 16))
+    g = _native.diag_read(2).astype(np.int64)
+    g = g[g[:, 0] > 0]
+    if len(g):
+        t0 = g[:, 0].min()
+        names = ["params+ids", "records", "SH staged", "chain", "commit", "SH store+end"]
+        cols = [1, 2, 3, 4, 5, 7]
+        prev = g[:, 0]
+        print(f"== gauss_bwd_live: {len(g)} waves, span {(g[:, 7].max() - t0) * 1e-2:.1f} us, "
+              f"start spread {(g[:, 0].max() - t0) * 1e-2:.1f} us, live/workgroup mean {g[:, 6].mean():.0f}")
+        for n, c in zip(names, cols):
+            d = (g[:, c] - prev) * 1e-2
+            print(f"   {n:>13}: mean {d.mean():6.2f} us  p90 {np.percentile(d, 90):6.2f}  max {d.max():6.2f}")
+            prev = g[:, c]
 
 
 if __name__ == "__main__":
