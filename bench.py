@@ -38,6 +38,8 @@ sys.path.insert(0, HERE)
 
 METRIC = "forward+backward renders/sec @512×512, 1.0M Gaussians; achieved HBM GB/s"
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+CLOCK_HZ = 2.4e9        # MI355X peak engine clock
+N_SIMDS = 256 * 4       # 256 CUs x 4 SIMDs
 
 
 def parse():
@@ -60,6 +62,8 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
+    ap.add_argument("--no-side-legs", action="store_true",
+                    help="skip the extra legs (unchanged-DGE render() path, high-live-fraction scene)")
     return ap.parse_args()
 
 
@@ -161,9 +165,10 @@ def main():
             lives.append({"live": int(lv.sum().item()), "flag_words": int(tt[lv].sum().item()), "records": recs})
     torch.cuda.synchronize()
 
-    # stage calibration (untimed): every stage bracketed by events, to find the dominant kernel;
-    # the timed region then brackets only that stage (two events per launch, no other overhead)
+    # stage calibration (untimed): every stage bracketed by events, for the per-stage times of the line;
+    # the timed region then brackets only the two blend kernels (two events per launch each)
     calib = {}
+    blend = ["render_fwd", "render_bwd"]
     if not args.no_profile:
         _native.profile_stages(None)
         _native.profile_enable(True)
@@ -172,8 +177,7 @@ def main():
             step()
         torch.cuda.synchronize()
         calib = {n: (ms, c) for n, (ms, c) in _native.profile_collect().items() if c}
-        dom_calib = max(calib, key=lambda n: calib[n][0])
-        _native.profile_stages([dom_calib])
+        _native.profile_stages(blend)
         _native.profile_collect()
     if world > 1:
         dist.barrier()
@@ -204,33 +208,45 @@ def main():
     M = (args.sh_degree + 1) ** 2
     K = float(np.mean(Ks))
     Kb = float(np.mean(Kbs))
-    # whole-render algorithmic bytes, SURVEY.md §8(d): B = 828 P + 200 K + 44 HW
-    B_render = 828.0 * P + 200.0 * K + 44.0 * HW
-    roofline = None
-    stages = {}
-    if calib:
-        for name, (ms, cnt) in calib.items():
-            stages[name] = {"avg_ms": ms / cnt, "launches": cnt,
-                            "share": ms / max(1e-9, sum(v[0] for v in calib.values()))}
-        dom = dom_calib
-        ms, cnt = prof.get(dom, (0.0, 0))
-        if cnt:  # the dominant stage as timed inside the timed region
-            stages[dom]["avg_ms"] = ms / cnt
-        live = {k: float(np.mean([d[k] for d in lives])) for k in lives[0]}
-        b = stage_bytes(dom, P, M, K, Kb, HW, tiles, live)
-        if b is not None:
-            achieved = b / (stages[dom]["avg_ms"] * 1e-3) / 1e9
-            roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                        "frac": round(achieved / HBM_PEAK_GBPS, 5), "traffic": None, "kernel": dom,
-                        "algorithmic_bytes_per_launch": int(b), "avg_ms": round(stages[dom]["avg_ms"], 4)}
-            pmc = os.path.join(HERE, "profiles", "pmc_traffic.json")
-            if os.path.exists(pmc):
-                try:
-                    tr = json.load(open(pmc)).get(dom)
-                    if tr:
-                        roofline["traffic"] = tr.get("bytes_per_launch")
-                except Exception:
-                    pass
+    live = {k: float(np.mean([d[k] for d in lives])) for k in lives[0]}
+    stages = {n: ms / cnt for n, (ms, cnt) in calib.items()}
+    rooflines = {}
+    pmc = {}
+    pmc_path = os.path.join(HERE, "profiles", "pmc_traffic.json")
+    if os.path.exists(pmc_path):
+        try:
+            pmc = json.load(open(pmc_path))
+        except Exception:
+            pmc = {}
+    for name in blend:  # both blend kernels, timed live inside the timed region
+        ms, cnt = prof.get(name, (0.0, 0))
+        if not cnt:
+            continue
+        avg = ms / cnt
+        stages[name] = avg
+        b = stage_bytes(name, P, M, K, Kb, HW, tiles, live)
+        achieved = b / (avg * 1e-3) / 1e9
+        r = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+             "frac": round(achieved / HBM_PEAK_GBPS, 5), "traffic": None, "kernel": name,
+             "algorithmic_bytes_per_launch": int(b), "avg_ms": round(avg, 4)}
+        tr = pmc.get(name) or {}
+        if tr.get("bytes_per_launch"):
+            r["traffic"] = tr["bytes_per_launch"]
+            r["traffic_over_algorithmic"] = round(tr["bytes_per_launch"] / b, 3)
+        if tr.get("valu_insts_per_launch"):
+            # VALU issue fraction: wave64 VALU instructions x 2 SIMD cycles / (kernel cycles at the 2.4 GHz
+            # peak clock x 1024 SIMDs) -- what bounds these kernels instead of HBM
+            vf = tr["valu_insts_per_launch"] * 2.0 / (avg * 1e-3 * CLOCK_HZ * N_SIMDS)
+            r["valu_issue_frac"] = round(vf, 4)
+            r["limit"] = "valu/latency" if vf > r["frac"] else "hbm"
+        if tr.get("build"):
+            r["pmc_build"] = tr["build"]
+        rooflines[name] = r
+    roofline = max(rooflines.values(), key=lambda r: r["avg_ms"]) if rooflines else None
+
+    legs = {}
+    if not args.no_side_legs and world == 1:
+        legs = side_legs(args, scene, cams, seeds, bg, pipe, bucket, step, dev)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -256,17 +272,87 @@ def main():
                            f", {os.environ.get('DGE_AMD_BENCH_BACKEND', 'nccl').replace('nccl', 'RCCL')} "
                            "sparse-row grad all-reduce" if world > 1 else "")},
             "num_rendered_mean": int(K),
-            "live_gaussians_mean": int(np.mean([d["live"] for d in lives])),
-            "gradient_records_mean": int(np.mean([d["records"] for d in lives])),
+            "live_gaussians_mean": int(live["live"]),
+            "gradient_records_mean": int(live["records"]),
             "backward_window_instances_mean": int(Kb),
-            "hbm_gbps_algorithmic_whole_render": round(B_render * value / world / 1e9, 2),
-            "stages_ms": {k: round(v["avg_ms"], 4) for k, v in stages.items()},
+            # a MODEL, not measured traffic: SURVEY.md §8(d)'s B = 828 P + 200 K + 44 HW bytes per render
+            # (the reference's traffic) x renders/s per GPU
+            "modeled_gbps_survey_bytes_whole_render": round((828.0 * P + 200.0 * K + 44.0 * HW) * value / world / 1e9, 2),
+            "stages_ms": {k: round(v, 4) for k, v in stages.items()},
             "roofline": roofline,
+            "rooflines": rooflines,
+            "legs": legs,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def _time(fn, steps):
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    torch.cuda.synchronize()
+    return time.perf_counter() - t0
+
+
+def side_legs(args, scene, cams, seeds, bg, pipe, bucket, step, dev):
+    """Extra legs, timed after the main region on the same box (not the headline value):
+    * dge_unchanged_render: the path DGE takes with only install_alias() -- its own render()
+      (gaussian_renderer/__init__.py:90-140: the torch getters, torch.cat of the SH, GaussianRasterizer /
+      _RasterizeGaussians) -- reproduced by render() with the fused raw-parameter path off;
+    * c2_high_live: c2 with raw opacity N(-2, 1) instead of N(0, 1.5): most Gaussians translucent, so far
+      more of them reach the backward (the live-set backward is not only judged at ~7% live)."""
+    from dge_amd.cameras import orbit_camera
+    from dge_amd.multiview import GradBucket, render_backward_views
+    from dge_amd.scene import synthetic_scene
+
+    legs = {}
+    steps = max(5, min(args.steps, 20))
+    V = len(cams)
+    prev = os.environ.get("DGE_AMD_FUSED")
+    os.environ["DGE_AMD_FUSED"] = "0"
+    try:
+        for _ in range(3):
+            step()
+        dt = _time(step, steps)
+    finally:
+        if prev is None:
+            os.environ.pop("DGE_AMD_FUSED", None)
+        else:
+            os.environ["DGE_AMD_FUSED"] = prev
+    legs["dge_unchanged_render"] = {"value": round(steps * V / dt, 3), "unit": "renders/s",
+                                    "path": "torch getters + cat + _RasterizeGaussians (fused path off)"}
+
+    hl = synthetic_scene(args.points, sh_degree=args.sh_degree, seed=0, device=dev, opacity_mean=-2.0,
+                         opacity_std=1.0).requires_grad_(True)
+    hb = GradBucket(hl.parameters())
+
+    def hstep():
+        hb.zero()
+        render_backward_views(cams, hl, pipe, bg, seeds, streams=args.streams)
+
+    for _ in range(3):
+        hstep()
+    from dge_amd import _native
+    _native.profile_stages(None)
+    _native.profile_enable(True)
+    _native.profile_collect()
+    hstep()
+    torch.cuda.synchronize()
+    st = {n: round(ms / c, 4) for n, (ms, c) in _native.profile_collect().items() if c}
+    _native.profile_enable(False)
+    dt = _time(hstep, steps)
+    # live fraction of view 0 (Gaussians with a gradient: nonzero opacity gradient after one backward)
+    hb.zero()
+    render_backward_views(cams[:1], hl, pipe, bg, seeds[:1], streams=1)
+    live = float((hl._opacity.grad != 0).float().mean().item())
+    legs["c2_high_live"] = {"value": round(steps * V / dt, 3), "unit": "renders/s", "live_fraction": round(live, 4),
+                            "opacity": "raw N(-2, 1)", "stages_ms": st}
+    del hl, hb
+    return legs
 
 
 def cpu_baseline(scene, cam, seed, bg, args):
@@ -286,13 +372,21 @@ def cpu_baseline(scene, cam, seed, bg, args):
     n, t0 = 0, time.perf_counter()
     while True:
         _, _, _, _, st = O.forward(s, xyz, op, shs=sh, scales=scl, rotations=rot)
-        O.backward(st, g)
+        O.backward(st, g, magnitudes=False)
         del st
         n += 1
         el = time.perf_counter() - t0
         if el >= args.cpu_baseline_seconds or n >= 50:
             break
-    return {"value": round(n / el, 4), "unit": "renders/s", "cores": threads, "kind": "port",
+    model = ""
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                model = ln.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"value": round(n / el, 4), "unit": "renders/s", "cores": threads, "kind": "port", "cpu_model": model,
             "sample": f"{n} fwd+bwd render(s) of the c2 scene, view 0, oracle/gs_oracle.c with {threads} OpenMP threads"}
 
 

@@ -15,16 +15,42 @@ from . import _native  # noqa: F401
 __version__ = "0.1.0"
 
 
-def install_alias() -> None:
+def install_alias(fused_render: bool = False) -> None:
     """Make ``import diff_gaussian_rasterization`` resolve to this package.
 
     DGE's renderer (gaussiansplatting/gaussian_renderer/__init__.py:14-17)
     imports the rasterizer under that name; after this call it gets the
     gfx950 implementation with no change to DGE's code.
+    Its own render() then runs unchanged: the torch getters, the torch.cat of
+    the SH and _RasterizeGaussians (bench.py leg "dge_unchanged_render").
+
+    fused_render=True also rebinds ``gaussiansplatting.gaussian_renderer``'s
+    render / camera2rasterizer / point_cloud_render to this package's, which
+    read a GaussianModel's raw tensors in-kernel (no getters, no cat) and
+    return the same dict — in that module and in every already-imported module
+    that did ``from gaussiansplatting.gaussian_renderer import render``
+    (threestudio/systems/DGE.py:15), so DGE's loop takes the fused path with no
+    code edit.  Needs the reference package importable.
     """
+    import importlib
     import sys
 
     from . import _C, diff_gaussian_rasterization
 
     sys.modules["diff_gaussian_rasterization"] = diff_gaussian_rasterization
     sys.modules["diff_gaussian_rasterization._C"] = _C
+    if not fused_render:
+        return
+    from . import gaussian_renderer as ours
+
+    ref = importlib.import_module("gaussiansplatting.gaussian_renderer")
+    for name in ("render", "camera2rasterizer", "point_cloud_render"):
+        orig, new = getattr(ref, name, None), getattr(ours, name)
+        if orig is None or orig is new:
+            continue
+        for mod in list(sys.modules.values()):
+            try:
+                if getattr(mod, name, None) is orig:
+                    setattr(mod, name, new)
+            except Exception:  # modules with exotic attribute access
+                continue

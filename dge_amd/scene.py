@@ -89,8 +89,10 @@ def build_covariance(scaling, rotation):
 
 
 def synthetic_scene(P: int, sh_degree: int = 3, seed: int = 0, radius: float = 2.0, scale: float = 0.02,
-                    device="cpu") -> GaussianScene:
-    """Seeded scene of SURVEY.md §8(d): uniform ball, log-normal scales, random quaternions."""
+                    device="cpu", opacity_mean: float = 0.0, opacity_std: float = 1.5) -> GaussianScene:
+    """Seeded scene of SURVEY.md §8(d): uniform ball, log-normal scales, random quaternions; raw opacity
+    N(opacity_mean, opacity_std) (the survey's N(0, 1.5) by default; N(-2, 1) is the bench's high-live
+    side config: mostly translucent Gaussians, so most of them reach the backward)."""
     g = torch.Generator(device="cpu").manual_seed(seed)
     d = torch.randn(P, 3, generator=g, dtype=torch.float64)
     d = d / d.norm(dim=1, keepdim=True).clamp_min(1e-12)
@@ -98,7 +100,7 @@ def synthetic_scene(P: int, sh_degree: int = 3, seed: int = 0, radius: float = 2
     xyz = (d * r).float()
     scaling = (math.log(scale) + 0.3 * torch.randn(P, 3, generator=g)).float()
     rotation = torch.randn(P, 4, generator=g).float()
-    opacity = (1.5 * torch.randn(P, 1, generator=g)).float()
+    opacity = (opacity_mean + opacity_std * torch.randn(P, 1, generator=g)).float()
     n_rest = (sh_degree + 1) ** 2 - 1
     features_dc = (0.5 * torch.randn(P, 1, 3, generator=g)).float()
     features_rest = (0.1 * torch.randn(P, n_rest, 3, generator=g)).float()

@@ -207,3 +207,36 @@ def test_cameras_match_reference_graphics_utils():
         np.testing.assert_array_equal(cam.world_view_transform.numpy(), rec[f"world_view{i}"])
         np.testing.assert_array_equal(cam.full_proj_transform.numpy(), rec[f"full_proj{i}"])
         np.testing.assert_array_equal(cam.camera_center.numpy(), rec[f"center{i}"])
+
+
+def test_install_alias_rebinds_reference_render(monkeypatch):
+    """install_alias(fused_render=True): DGE's `from gaussiansplatting.gaussian_renderer import render`
+    (threestudio/systems/DGE.py:15) ends up calling dge_amd's render, in the renderer module and in
+    modules that imported the name before the call; the rasterizer package alias is installed too.
+    (Stand-in modules with the reference's module names: the reference package is not importable here.)"""
+    import sys
+    import types
+
+    import dge_amd
+    from dge_amd import gaussian_renderer as ours
+
+    def ref_render(*a, **k):
+        raise AssertionError("reference render called")
+
+    pkg = types.ModuleType("gaussiansplatting")
+    rend = types.ModuleType("gaussiansplatting.gaussian_renderer")
+    rend.render, rend.camera2rasterizer = ref_render, lambda *a, **k: None
+    pkg.gaussian_renderer = rend
+    system = types.ModuleType("threestudio_dge_standin")
+    system.render = ref_render  # as `from gaussiansplatting.gaussian_renderer import render` leaves it
+    for name, mod in (("gaussiansplatting", pkg), ("gaussiansplatting.gaussian_renderer", rend),
+                      ("threestudio_dge_standin", system)):
+        monkeypatch.setitem(sys.modules, name, mod)
+    monkeypatch.delitem(sys.modules, "diff_gaussian_rasterization", raising=False)
+    monkeypatch.delitem(sys.modules, "diff_gaussian_rasterization._C", raising=False)
+    dge_amd.install_alias(fused_render=True)
+    assert rend.render is ours.render and system.render is ours.render
+    assert rend.camera2rasterizer is ours.camera2rasterizer
+    import diff_gaussian_rasterization
+
+    assert diff_gaussian_rasterization is dge_amd.diff_gaussian_rasterization

@@ -7,7 +7,7 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT" 2>/dev/null || cd /root/repo
 mkdir -p gpurun_out/pmc
 export TMPDIR=/tmp
-CMD="python bench.py --steps 3 --warmup 2 --no-cpu-baseline --no-profile ${PMC_BENCH_ARGS:-}"
+CMD="python bench.py --steps 3 --warmup 2 --no-cpu-baseline --no-profile --no-side-legs ${PMC_BENCH_ARGS:-}"
 i=0
 while read -r group; do
   [ -z "$group" ] && continue

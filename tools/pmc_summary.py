@@ -44,6 +44,10 @@ def main(root):
             e["read_bytes_per_launch"] += int(rd)
             e["write_bytes_per_launch"] += int(wr)
             e["bytes_per_launch"] += int(rd + wr)
+            if "SQ_INSTS_VALU" in c:
+                e["valu_insts_per_launch"] = int(e.get("valu_insts_per_launch", 0) + c["SQ_INSTS_VALU"])
+            if os.environ.get("PMC_BUILD"):
+                e["build"] = os.environ["PMC_BUILD"]
     if out:
         dst = os.path.join(root, "pmc_traffic.json")  # copied into profiles/ by hand after the run
         json.dump(out, open(dst, "w"), indent=1)
