@@ -238,23 +238,66 @@ def reduce_view_stats(viewspace_grad_sum: torch.Tensor, radii_max: torch.Tensor,
     return viewspace_grad_sum, radii_max
 
 
-def multiview_step(scene, cameras, render_fn, pipe, bg, targets, bucket: GradBucket, total_views: int, group=None):
-    """One data-parallel step: render this rank's views, backprop, all-reduce.
+def found_inf_allreduce(bucket: GradBucket, group=None) -> torch.Tensor:
+    """1 if any gradient of this rank's bucket is inf/NaN on SOME rank, else 0 (a MAX all-reduce of one
+    flag), computed before the gradient all-reduce: Lightning's 16-mixed GradScaler (configs/dge.yaml:81)
+    skips the optimizer step on overflow, and every replica must skip the same steps or their
+    parameters diverge.  (The SUM all-reduce would spread an inf/NaN to every rank anyway — for the
+    rows it carries; this flag makes the decision explicit and independent of the sparse packing.)"""
+    flag = (~torch.isfinite(bucket.flat)).any().to(torch.float32).reshape(1)
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+        dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=group)
+    return flag
 
-    ``targets[i]`` is the per-view gradient seed dL/dimage (the edited-frame
-    loss gradient).  Returns (viewspace_grad_sum [P,3], radii_max [P]) after
-    the cross-rank reductions, matching DGE.py:190-193 / :269-276.
+
+def multiview_step(scene, cameras, render_fn, pipe, bg, bucket: GradBucket, total_views: int, targets=None,
+                   gt_images=None, masks=None, lambda_l1: float = 1.0, loss_scale: float = 1.0,
+                   semantic: bool = False, group=None):
+    """One data-parallel step of DGE's edit loop over this rank's views (threestudio/systems/DGE.py
+    forward :170-239, training_step :617-699, on_before_optimizer_step :266-296).
+
+    The per-view loss is either a given gradient seed (``targets[i]`` = dL/dimage, [3,H,W]) or DGE's
+    l1 term: ``F.l1_loss(images * mask, gt * mask)`` is a mean over all B views' elements
+    (DGE.py:672), so this rank's share is its views' absolute-error SUM over (B * H * W * 3) — the
+    local mean times B_local / B — and the ranks' gradients add up to the single-GPU loop's.
+    (The perceptual term, :673-676, is a per-view ``.sum()``: unchanged under sharding; its network is
+    out of scope.)  ``loss_scale`` is the GradScaler's scale (16-mixed); ``semantic`` also runs DGE's
+    mask render per view (:198-204, override_color = the Gaussian mask) — gradient-free, so here
+    without autograd, its boolean ``norm > 0.8`` map returned in ``masks``.
+
+    Then one (sparse-row) SUM all-reduce of the gradient bucket, the overflow flag MAX-reduced before it
+    (found_inf_allreduce), and the densification statistics: the SUM of the view-space gradients and the
+    MAX of the radii across views and ranks.  Returns a dict: viewspace_grad_sum [P,3], radii_max [P],
+    found_inf (float tensor [1]), semantic_masks (list of [H,W] bool, when ``semantic``).
     """
     P = scene.num_points()
     dev = bucket.flat.device
     vs_sum = torch.zeros((P, 3), dtype=torch.float32, device=dev)
     radii_max = torch.zeros((P,), dtype=torch.int32, device=dev)
-    for cam, g in zip(cameras, targets):
+    sem = []
+    for i, cam in enumerate(cameras):
         pkg = render_fn(cam, scene, pipe, bg)
-        loss = (pkg["render"] * g).sum()
+        img = pkg["render"]
+        if targets is not None:
+            loss = (img * targets[i]).sum()
+        else:
+            m = masks[i] if masks is not None else torch.ones_like(img[:1])
+            loss = torch.abs(img * m - gt_images[i] * m).sum() * (lambda_l1 / (total_views * img.numel()))
+        if loss_scale != 1.0:
+            loss = loss * loss_scale
         loss.backward()
         vs_sum += pkg["viewspace_points"].grad
         radii_max = torch.maximum(radii_max, pkg["radii"])
+        if semantic:
+            with torch.no_grad():
+                gm = getattr(scene, "mask", None)
+                gm = gm if gm is not None else torch.ones(P, dtype=torch.bool, device=dev)
+                sm = render_fn(cam, scene, pipe, bg, override_color=gm[..., None].float().repeat(1, 3))["render"]
+                sem.append(torch.norm(sm, dim=0) > 0.8)
+    found_inf = found_inf_allreduce(bucket, group)
     bucket.allreduce(group)
     reduce_view_stats(vs_sum, radii_max, group)
-    return vs_sum, radii_max
+    out = {"viewspace_grad_sum": vs_sum, "radii_max": radii_max, "found_inf": found_inf}
+    if semantic:
+        out["semantic_masks"] = sem
+    return out

@@ -1,0 +1,153 @@
+"""GPU tests of the multi-view step (SURVEY.md §8(f) F1, configs[2] c3 as far as one card allows):
+the 3-view step reductions against the oracle fixture, and the view-sharded step with two ranks
+sharing one card (gloo) against the single-process loop."""
+from __future__ import annotations
+
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from helpers import assert_close
+
+pytestmark = pytest.mark.gpu
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+class _Activated:
+    """A model whose getters return leaf tensors (the activated values the oracle fixture holds): the
+    reference-shaped render() path, gradients land in the leaves."""
+
+    def __init__(self, rec, dev):
+        t = lambda k: torch.from_numpy(np.ascontiguousarray(rec[k])).to(dev).requires_grad_(True)
+        self.xyz, self.op, self.sh = t("means3D"), t("opacities"), t("shs")
+        self.sc, self.rot = t("scales"), t("rotations")
+        self.active_sh_degree = self.max_sh_degree = 3
+        self.mask = None
+
+    get_xyz = property(lambda self: self.xyz)
+    get_opacity = property(lambda self: self.op)
+    get_features = property(lambda self: self.sh)
+    get_scaling = property(lambda self: self.sc)
+    get_rotation = property(lambda self: self.rot)
+
+    def parameters(self):
+        return [self.xyz, self.op, self.sh, self.sc, self.rot]
+
+    def num_points(self):
+        return int(self.xyz.shape[0])
+
+
+def test_multiview_step_vs_oracle_3views(cuda_device):
+    """multiview_step over 3 views (render + backward per view, gradients summed in the shared bucket):
+    radii max identical, the view-space gradient sum within 1e-4 x its terms' magnitude, the summed
+    parameter gradients against the oracle's sum (DGE.py:170-296)."""
+    from dge_amd.cameras import orbit_camera
+    from dge_amd.gaussian_renderer import PipelineParams, render
+    from dge_amd.multiview import GradBucket, multiview_step
+
+    rec = np.load(os.path.join(GOLDEN, "multiview_3views.npz"))
+    dev = torch.device("cuda")
+    P, W, H, V = (int(rec[k]) for k in ("P", "W", "H", "V"))
+    pc = _Activated(rec, dev)
+    cams = [orbit_camera(k, V, W, H, device=dev) for k in range(V)]
+    seeds = [torch.from_numpy(rec["dL_dpix"][k]).to(dev) for k in range(V)]
+    bucket = GradBucket(pc.parameters())
+    out = multiview_step(pc, cams, render, PipelineParams(), torch.zeros(3, device=dev), bucket, V, targets=seeds)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(out["radii_max"].cpu().numpy(), rec["radii_max"])
+    vs = out["viewspace_grad_sum"].cpu().numpy().astype(np.float64)
+    err = np.abs(vs[:, :2] - rec["viewspace_grad_sum"][:, :2])
+    nbad = int((err > 1e-4 * rec["mag9_sum"][:, :2] + 1e-30).sum())
+    print(f"[parity F1] view-space sum elements beyond 1e-4 x magnitude: {nbad}; "
+          f"max err/mag {float((err / (rec['mag9_sum'][:, :2] + 1e-30)).max()):.2e}")
+    assert nbad == 0 and not vs[:, 2].any()
+    for name, p in zip(["means3D", "opacity", "sh", "scales", "rotations"], pc.parameters()):
+        assert_close(p.grad.cpu().numpy(), rec[f"dL_d{name}_sum"].reshape(p.shape), f"summed dL_d{name}")
+    assert out["found_inf"].item() == 0.0
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _c3_setup(dev, P, V, W, H):
+    from dge_amd.cameras import orbit_camera
+    from dge_amd.scene import synthetic_scene
+
+    sc = synthetic_scene(P, seed=0, device=dev).requires_grad_(True)
+    cams = [orbit_camera(k, 24, W, H, device=dev) for k in range(V)]
+    g = torch.Generator().manual_seed(7)
+    seeds = [(torch.randn(3, H, W, generator=g) * 1e-3).to(dev) for _ in range(V)]
+    return sc, cams, seeds
+
+
+def _c3_worker(rank, world, port, P, V, W, H, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    try:
+        torch.cuda.set_device(0)
+        dev = torch.device("cuda", 0)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from dge_amd.gaussian_renderer import PipelineParams, render
+        from dge_amd.multiview import GradBucket, multiview_step, shard_views
+
+        sc, cams, seeds = _c3_setup(dev, P, V, W, H)
+        mine = list(shard_views(V, world, rank))
+        bucket = GradBucket(sc.parameters())
+        out = multiview_step(sc, [cams[i] for i in mine], render, PipelineParams(), torch.zeros(3, device=dev),
+                             bucket, V, targets=[seeds[i] for i in mine])
+        torch.cuda.synchronize()
+        q.put((rank, bucket.flat.cpu().numpy() if rank == 0 else None, out["viewspace_grad_sum"].cpu().numpy(),
+               out["radii_max"].cpu().numpy(), None))
+    except Exception as e:  # report instead of hanging the parent
+        q.put((rank, None, None, None, repr(e)))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def test_c3_two_ranks_share_one_card(cuda_device):
+    """configs[2]'s per-rank workload (1M Gaussians, the c3 orbit cameras, 3 views per rank) with two
+    ranks on one card over gloo: the sparse-row bucket all-reduce, the view-space SUM and radii MAX
+    give the single-process 6-view step's results (up to float summation order)."""
+    from dge_amd.gaussian_renderer import PipelineParams, render
+    from dge_amd.multiview import GradBucket, multiview_step
+
+    P, V, W, H = 1_000_000, 6, 512, 512
+    dev = torch.device("cuda", 0)
+    sc, cams, seeds = _c3_setup(dev, P, V, W, H)
+    bucket = GradBucket(sc.parameters())
+    out = multiview_step(sc, cams, render, PipelineParams(), torch.zeros(3, device=dev), bucket, V, targets=seeds)
+    torch.cuda.synchronize()
+    ref, vs1, r1 = bucket.flat.cpu().numpy(), out["viewspace_grad_sum"].cpu().numpy(), out["radii_max"].cpu().numpy()
+    del sc, bucket, out
+    torch.cuda.empty_cache()
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_c3_worker, args=(r, 2, port, P, V, W, H, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    for rank, flat, vs, rmax, err in res:
+        assert err is None, f"rank {rank}: {err}"
+        if flat is not None:
+            nz = int(np.count_nonzero(ref))
+            print(f"[parity c3x2] bucket nonzero {nz} of {ref.size}; max |d| {float(np.abs(flat - ref).max()):.3e}")
+            np.testing.assert_allclose(flat, ref, rtol=1e-5, atol=1e-6 * np.abs(ref).max())
+        np.testing.assert_allclose(vs, vs1, rtol=1e-5, atol=1e-6 * np.abs(vs1).max())
+        np.testing.assert_array_equal(rmax, r1)
+    for p in procs:
+        assert p.exitcode == 0

@@ -18,7 +18,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from dge_amd.multiview import GradBucket, multiview_step, reduce_view_stats, shard_views
+from dge_amd.multiview import GradBucket, found_inf_allreduce, multiview_step, reduce_view_stats, shard_views
 
 
 def test_shard_views_partition():
@@ -77,7 +77,24 @@ def _setup(P=60, V=4, W=32, H=32):
     return cams, targets
 
 
-def _worker(rank, world, port, P, V, q):
+def _step(pc, cams, targets, idx, V, mode):
+    """multiview_step over views idx: gradient seeds (mode "seed") or DGE's masked l1 mean (mode "l1",
+    targets = (gt images [3,H,W], masks [1,H,W]))."""
+    bucket = GradBucket(pc.parameters())
+    kw = dict(targets=[targets[i] for i in idx]) if mode == "seed" else dict(
+        gt_images=[targets[0][i] for i in idx], masks=[targets[1][i] for i in idx], lambda_l1=10.0)
+    out = multiview_step(pc, [cams[i] for i in idx], _render_fn, None, torch.zeros(3), bucket, V, **kw)
+    return bucket, out
+
+
+def _l1_targets(V, W=32, H=32):
+    g = torch.Generator().manual_seed(9)
+    gts = [torch.rand(3, H, W, generator=g) for _ in range(V)]
+    masks = [(torch.rand(1, H, W, generator=g) > 0.3).float() for _ in range(V)]
+    return gts, masks
+
+
+def _worker(rank, world, port, P, V, mode, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -85,11 +102,15 @@ def _worker(rank, world, port, P, V, q):
         torch.set_num_threads(1)
         pc = _Scene(P, seed=4)
         cams, targets = _setup(P, V)
-        mine = shard_views(V, world, rank)
-        bucket = GradBucket(pc.parameters())
-        vs, rmax = multiview_step(pc, [cams[i] for i in mine], _render_fn, None, torch.zeros(3),
-                                  [targets[i] for i in mine], bucket, V)
-        q.put((rank, bucket.flat.clone().numpy(), vs.numpy(), rmax.numpy()))
+        if mode == "l1":
+            targets = _l1_targets(V)
+        bucket, out = _step(pc, cams, targets, list(shard_views(V, world, rank)), V, mode)
+        # overflow on one rank only: every rank must see it (the GradScaler skip is collective)
+        if rank == 1:
+            bucket.flat[7] = float("nan")
+        fi = found_inf_allreduce(bucket)
+        q.put((rank, bucket.flat.clone().numpy() if rank == 0 else None, out["viewspace_grad_sum"].numpy(),
+               out["radii_max"].numpy(), float(out["found_inf"].item()), float(fi.item())))
     finally:
         dist.destroy_process_group()
 
@@ -103,29 +124,37 @@ def _free_port():
 
 
 @pytest.mark.slow
-def test_sharded_step_equals_single_process():
+@pytest.mark.parametrize("mode", ["seed", "l1"])
+def test_sharded_step_equals_single_process(mode):
+    """2 ranks x 2 views == 1 process x 4 views: the summed parameter gradients (sparse-row bucket
+    all-reduce), the view-space gradient sum and the radii max; for DGE's masked l1 (a mean over all
+    views, DGE.py:672) through the B_local / B share of each rank.  found_inf is collective."""
     P, V = 60, 4
-    # single process reference: all views, plain autograd accumulation
     pc = _Scene(P, seed=4)
     cams, targets = _setup(P, V)
-    bucket = GradBucket(pc.parameters())
-    vs1, r1 = multiview_step(pc, cams, _render_fn, None, torch.zeros(3), targets, bucket, V)
+    if mode == "l1":
+        targets = _l1_targets(V)
+    bucket, out = _step(pc, cams, targets, list(range(V)), V, mode)
     ref = bucket.flat.clone().numpy()
+    vs1, r1 = out["viewspace_grad_sum"].numpy(), out["radii_max"].numpy()
+    assert out["found_inf"].item() == 0.0 and np.abs(ref).max() > 0
 
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, P, V, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, P, V, mode, q)) for r in range(2)]
     for p in procs:
         p.start()
     res = [q.get(timeout=300) for _ in procs]
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    for rank, flat, vs, rmax in res:
-        np.testing.assert_allclose(flat, ref, rtol=1e-5, atol=1e-6 * np.abs(ref).max())
-        np.testing.assert_allclose(vs, vs1.numpy(), rtol=1e-5, atol=1e-6 * np.abs(vs1.numpy()).max())
-        np.testing.assert_array_equal(rmax, r1.numpy())
+    for rank, flat, vs, rmax, fi_step, fi_nan in res:
+        if flat is not None:
+            np.testing.assert_allclose(flat, ref, rtol=1e-5, atol=1e-6 * np.abs(ref).max())
+        np.testing.assert_allclose(vs, vs1, rtol=1e-5, atol=1e-6 * np.abs(vs1).max())
+        np.testing.assert_array_equal(rmax, r1)
+        assert fi_step == 0.0 and fi_nan == 1.0
 
 
 def test_grad_bucket_views_and_zero():

@@ -7,6 +7,8 @@
                     oracle's and the kernels' SH->RGB (forward.cu:20-71 restates it).
   cameras_ref.npz   the REFERENCE's getWorld2View2 / getProjectionMatrix outputs (and the
                     Simple_Camera composition) for the c1-c5 cameras and random poses.
+  multiview_3views.npz  the oracle's 3-view step reductions (summed parameter and view-space
+                    gradients, max radii) for the F1 multi-view step test.
   scene_*.npz       seeded scenes (inputs) with the oracle's outputs and gradients:
                     the GPU parity tests compare the HIP path against them.
 
@@ -149,6 +151,49 @@ def scene_fixture(name, P, W, H, seed, radius=1.5, scale=0.05, sh_degree=3, bg=(
     print(name, "P", P, "K", nr, "bytes", os.path.getsize(os.path.join(OUT, f"scene_{name}.npz")))
 
 
+def multiview_fixture():
+    """F1: DGE's per-step reductions over a 3-view batch, from the oracle: the
+    parameter gradients summed over the views (one backward of the summed loss, DGE.py:617-699), the
+    view-space gradient sum and the radii max (DGE.py:190-193, 269-281), with each view's oracle
+    magnitudes (mag9) summed for the view-space tolerance."""
+    from oracle import oracle as O
+    from dge_amd.cameras import orbit_camera
+    from dge_amd.gaussian_renderer import _settings
+    from dge_amd.scene import synthetic_scene
+
+    P, W, H, V = 2500, 112, 96, 3
+    sc = synthetic_scene(P, sh_degree=3, seed=21, radius=1.5, scale=0.04)
+    with torch.no_grad():
+        kw = dict(shs=sc.get_features.numpy(), scales=sc.get_scaling.numpy(), rotations=sc.get_rotation.numpy())
+        xyz, op = sc.get_xyz.numpy(), sc.get_opacity.numpy()
+    rng = np.random.default_rng(31)
+    acc = {k: np.zeros(v.shape, np.float64) for k, v in dict(means3D=xyz, opacity=op, sh=kw["shs"],
+                                                              scales=kw["scales"], rotations=kw["rotations"]).items()}
+    vs = np.zeros((P, 3), np.float64)
+    mag = np.zeros((P, 9), np.float64)
+    rmax = np.zeros(P, np.int32)
+    seeds = []
+    for k in range(V):
+        s = _settings(orbit_camera(k, V, W, H, device="cpu"), torch.zeros(3), 1.0, 3)
+        g = (rng.standard_normal((3, H, W)) * 1e-2).astype(np.float32)
+        seeds.append(g)
+        nr, color, depth, radii, st = O.forward(s, xyz, op, **kw)
+        gr = O.backward(st, g)
+        acc["means3D"] += gr["dL_dmeans3D"]
+        acc["opacity"] += gr["dL_dopacity"]
+        acc["sh"] += gr["dL_dsh"]
+        acc["scales"] += gr["dL_dscales"]
+        acc["rotations"] += gr["dL_drotations"]
+        vs += gr["dL_dmeans2D"]
+        mag += gr["mag9"]
+        rmax = np.maximum(rmax, radii)
+    rec = dict(P=P, W=W, H=H, V=V, means3D=xyz, opacities=op, **kw, dL_dpix=np.stack(seeds),
+               viewspace_grad_sum=vs.astype(np.float32), mag9_sum=mag.astype(np.float32), radii_max=rmax,
+               **{f"dL_d{k}_sum": v.astype(np.float32) for k, v in acc.items()})
+    np.savez_compressed(os.path.join(OUT, "multiview_3views.npz"), **rec)
+    print("multiview_3views", os.path.getsize(os.path.join(OUT, "multiview_3views.npz")))
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
     sh_fixture()
@@ -157,6 +202,7 @@ def main():
     scene_fixture("sh1_bg_64", 800, 64, 64, seed=12, sh_degree=1, bg=(0.2, 0.5, 0.9), scale=0.08)
     scene_fixture("colors_120x72", 1000, 120, 72, seed=13, mode="colors", scale=0.06, view=1, nviews=3)
     scene_fixture("cov3d_mod_80", 900, 80, 80, seed=14, mode="cov3d", scale_modifier=0.8, scale=0.07)
+    multiview_fixture()
 
 
 if __name__ == "__main__":
