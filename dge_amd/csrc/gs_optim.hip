@@ -8,12 +8,13 @@
 // per element read p, g, m, v and write p, m, v (28 B) — the HBM roofline of
 // the step (~1.65 GB per step at 1M Gaussians).
 //
-// Arithmetic follows torch's single-tensor Adam (torch/optim/adam.py,
-// _single_tensor_adam) in its operation order:
-//   m = m + (1 - b1) * (g - m)                   exp_avg.lerp_(grad, 1 - b1)
-//   v = v * b2 + (1 - b2) * g * g                exp_avg_sq.mul_(b2).addcmul_(g, g, value=1 - b2)
-//   d = sqrt(v) / bc2_sqrt + eps                 (exp_avg_sq.sqrt() / bc2_sqrt).add_(eps)
-//   p = p + (-step_size) * m / d                 param.addcdiv_(exp_avg, denom, value=-step_size)
+// Arithmetic follows the Adam DGE runs — torch.optim.Adam on CUDA/ROCm tensors,
+// i.e. the foreach implementation (torch/optim/adam.py, _multi_tensor_adam) —
+// in its operation order:
+//   m = m + (1 - b1) * (g - m)        _foreach_lerp_(exp_avgs, grads, 1 - b1)  (weight < 0.5 branch)
+//   v = v * b2 + ((1 - b2) * g) * g   _foreach_mul_(exp_avg_sqs, b2); _foreach_addcmul_(.., g, g, 1 - b2)
+//   d = sqrt(v) / bc2_sqrt + eps      _foreach_sqrt; _foreach_div_(.., bc2_sqrt); _foreach_add_(.., eps)
+//   p = p + (-step_size) * (m / d)    _foreach_addcdiv_(params, exp_avgs, denom, -step_size)
 // with step_size = lr / (1 - b1^t) and bc2_sqrt = sqrt(1 - b2^t) computed on
 // the host in double, as torch does with Python floats.
 #pragma clang fp contract(off)
@@ -38,7 +39,7 @@ __device__ __forceinline__ void adam_one(float& p, float g, float& m, float& v, 
     m = m + a.one_minus_b1 * (g - m);
     v = v * a.b2 + a.one_minus_b2 * g * g;
     const float d = sqrtf(v) / bc2s + a.eps;
-    p = p + nstep * m / d;
+    p = p + nstep * (m / d);
 }
 
 __global__ __launch_bounds__(kAdamThreads) void k_adam(AdamLaunch a) {

@@ -54,6 +54,19 @@ def _no_grad_materialization(ctx, radii):
     ctx.set_materialize_grads(False)
 
 
+def _serialize_scratch(ctx, dev):
+    """The backward reuses scratch inside the forward's buffers (gradient records and flags, the live
+    list, counters: gs_raster.h, gs_rasterize_backward), so two backward calls of ONE forward
+    (retain_graph=True, or torch.autograd.grad then .backward) must not overlap.  On one stream they
+    cannot; when a later call runs on another stream than the previous one, it first waits for that
+    stream."""
+    cur = torch.cuda.current_stream(dev)
+    prev = getattr(ctx, "_bwd_stream", None)
+    if prev is not None and prev != cur:
+        cur.wait_stream(prev)
+    ctx._bwd_stream = cur
+
+
 class _RasterizeGaussians(torch.autograd.Function):
     @staticmethod
     def forward(ctx, means3D, means2D, sh, colors_precomp, opacities, scales, rotations, cov3Ds_precomp,
@@ -79,6 +92,7 @@ class _RasterizeGaussians(torch.autograd.Function):
         rs = ctx.raster_settings
         (colors_precomp, means3D, scales, rotations, cov3Ds_precomp, radii, sh, geomBuffer, binningBuffer,
          imgBuffer) = ctx.saved_tensors
+        _serialize_scratch(ctx, means3D.device)
         args = (rs.bg, means3D, radii, colors_precomp, scales, rotations, rs.scale_modifier, cov3Ds_precomp,
                 rs.viewmatrix, rs.projmatrix, rs.tanfovx, rs.tanfovy, grad_out_color, sh, rs.sh_degree, rs.campos,
                 geomBuffer, ctx.num_rendered, binningBuffer, imgBuffer, rs.debug)
@@ -171,6 +185,7 @@ class _RasterizeGaussiansFused(torch.autograd.Function):
         args = (rs.bg, xyz, f_dc, f_rest, colors, raw_opacity, raw_scaling, raw_rotation, radii, rs.scale_modifier,
                 rs.viewmatrix, rs.projmatrix, rs.tanfovx, rs.tanfovy, grad_out_color, rs.sh_degree, rs.campos,
                 geomBuffer, ctx.num_rendered, binningBuffer, imgBuffer, rs.debug)
+        _serialize_scratch(ctx, xyz.device)
         ordered = bool(into) and _SIDE_STREAMS
         stream = _order_grad_writes_begin(xyz.device) if ordered else None
         d_m2, d_xyz, d_dc, d_rest, d_col, d_op, d_sc, d_rot = _call_with_snapshot(

@@ -91,7 +91,11 @@ int gs_rasterize_forward(const gs_settings *s, int P, int M, const float *means3
  * R = num_rendered from the forward.  Every output is fully written (the
  * caller need not zero it): dL_dmeans2D [P,3] (z = 0), dL_dcolors [P,3],
  * dL_dopacity [P], dL_dmeans3D [P,3], dL_dcov3D [P,6], dL_dsh [P,M,3]
- * (may be NULL when M == 0), dL_dscales [P,3], dL_drotations [P,4]. */
+ * (may be NULL when M == 0), dL_dscales [P,3], dL_drotations [P,4].
+ * The backward writes scratch inside the forward's geometry/binning/image
+ * buffers (gradient records and flags, the live list, counters): calls for ONE
+ * forward must be ordered (same stream, or the later one waits for the earlier
+ * one); calls for different forwards may run concurrently. */
 int gs_rasterize_backward(const gs_settings *s, int P, int M, int R, const float *means3D,
                           const float *shs, const float *colors_precomp, const float *scales,
                           const float *rotations, const float *cov3D_precomp, const int *radii,
