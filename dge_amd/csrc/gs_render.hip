@@ -197,10 +197,11 @@ __global__ __launch_bounds__(64, 3) void k_render_fwd(RenderArgs a) {
 
     // the round's kept entries, one array per field: a pair of consecutive entries' field is one
     // 16-B read, the operands of two packed instructions (pixel_alpha4)
-    __shared__ float s_x[kRound + kGroup], s_y[kRound + kGroup];
-    __shared__ float s_cx[kRound + kGroup], s_cy[kRound + kGroup], s_cz[kRound + kGroup], s_op[kRound + kGroup];
+    __shared__ __attribute__((aligned(16))) float s_x[kRound + kGroup], s_y[kRound + kGroup];
+    __shared__ __attribute__((aligned(16))) float s_cx[kRound + kGroup], s_cy[kRound + kGroup], s_cz[kRound + kGroup],
+        s_op[kRound + kGroup];
     __shared__ float4 s_rgbd[kRound + kGroup];
-    __shared__ uint32_t s_pos[kRound + kGroup];
+    __shared__ __attribute__((aligned(16))) uint32_t s_pos[kRound + kGroup];
     __shared__ uint32_t s_gused[kRound / kGroup + 1];  // per blend group: bit u = entry u was blended
 
     const uint2 range = a.ranges[tile];
@@ -218,17 +219,18 @@ __global__ __launch_bounds__(64, 3) void k_render_fwd(RenderArgs a) {
     // Software pipeline over rounds of 256 entries: the ids run two rounds
     // ahead and the geometry gathers one round ahead of the blend, so a
     // round's loads are in flight while the previous round blends.
-    // Out-of-range slots load entry 0 (valid whenever the list is non-empty)
-    // and are dropped by the cull.
+    // Out-of-range slots load the list's last entry and are dropped by the cull
     // (unconditional loads, clamped into the list: the compiler can then count them in vmcnt
-    // waits instead of draining every outstanding access; a non-empty list's last entry, or
-    // entry 0 of the binning buffer, which always exists)
+    // waits instead of draining every outstanding access).
     const uint32_t k_last = range.y > range.x ? range.y - 1 : 0u;
+    // (an empty list reads nothing: its slot of the binning buffer need not hold a valid id; Gaussian 0
+    // is gathered instead, P > 0 whenever the blend runs)
+    const bool list_empty = range.y <= range.x;
     auto load_ids = [&](uint32_t b, uint32_t (&ids)[4]) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const uint32_t k = b + 64 * i + lane;
-            ids[i] = a.point_pairs[k < range.y ? k : k_last].x;
+            ids[i] = list_empty ? 0u : a.point_pairs[k < range.y ? k : k_last].x;
         }
     };
     uint32_t ids[4];
@@ -614,8 +616,9 @@ constexpr int kBwdHalf = kSegLen / 2;   // list positions per half-segment (LDS 
 __global__ __launch_bounds__(64, 4) void k_render_bwd(RenderBwdArgs a) {
     // kept entries of a half-segment, compacted back to front, + a group of padding
     // (one array per field: four consecutive entries' field is one 16-B read, see bwd_quad)
-    __shared__ float s_x[kBwdHalf + kBwdGroup], s_y[kBwdHalf + kBwdGroup];
-    __shared__ float s_cx[kBwdHalf + kBwdGroup], s_cy[kBwdHalf + kBwdGroup], s_cz[kBwdHalf + kBwdGroup],
+    __shared__ __attribute__((aligned(16))) float s_x[kBwdHalf + kBwdGroup], s_y[kBwdHalf + kBwdGroup];
+    __shared__ __attribute__((aligned(16))) float s_cx[kBwdHalf + kBwdGroup], s_cy[kBwdHalf + kBwdGroup],
+        s_cz[kBwdHalf + kBwdGroup],
         s_op[kBwdHalf + kBwdGroup];
     __shared__ float4 s_rgb[kBwdHalf + kBwdGroup];
     __shared__ uint32_t s_pos[kBwdHalf + kBwdGroup];
