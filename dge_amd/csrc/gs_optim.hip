@@ -10,11 +10,13 @@
 //
 // Arithmetic follows the Adam DGE runs — torch.optim.Adam on CUDA/ROCm tensors,
 // i.e. the foreach implementation (torch/optim/adam.py, _multi_tensor_adam) —
-// in its operation order:
-//   m = m + (1 - b1) * (g - m)        _foreach_lerp_(exp_avgs, grads, 1 - b1)  (weight < 0.5 branch)
-//   v = v * b2 + ((1 - b2) * g) * g   _foreach_mul_(exp_avg_sqs, b2); _foreach_addcmul_(.., g, g, 1 - b2)
-//   d = sqrt(v) / bc2_sqrt + eps      _foreach_sqrt; _foreach_div_(.., bc2_sqrt); _foreach_add_(.., eps)
-//   p = p + (-step_size) * (m / d)    _foreach_addcdiv_(params, exp_avgs, denom, -step_size)
+// in the float32 operation order its kernels compile to on ROCm (ATen's
+// elementwise kernels are built with fp contraction on; the order was
+// measured bitwise against torch on an MI355X, tools/probes/adam_order.py):
+//   m = fma(1 - b1, g - m, m)          _foreach_lerp_(exp_avgs, grads, 1 - b1)  (weight < 0.5 branch)
+//   v = fma(1 - b2, g * g, v * b2)     _foreach_mul_(exp_avg_sqs, b2); _foreach_addcmul_(.., g, g, 1 - b2)
+//   d = sqrt(v) / bc2_sqrt + eps       _foreach_sqrt; _foreach_div_(.., bc2_sqrt); _foreach_add_(.., eps)
+//   p = fma(-step_size, m / d, p)      _foreach_addcdiv_(params, exp_avgs, denom, -step_size)
 // with step_size = lr / (1 - b1^t) and bc2_sqrt = sqrt(1 - b2^t) computed on
 // the host in double, as torch does with Python floats.
 #pragma clang fp contract(off)
@@ -36,10 +38,10 @@ constexpr long long kAdamBlockElems = (long long)kAdamThreads * kAdamVec * 4;  /
 
 __device__ __forceinline__ void adam_one(float& p, float g, float& m, float& v, const AdamLaunch& a, float nstep,
                                          float bc2s) {
-    m = m + a.one_minus_b1 * (g - m);
-    v = v * a.b2 + a.one_minus_b2 * g * g;
+    m = __builtin_fmaf(a.one_minus_b1, g - m, m);
+    v = __builtin_fmaf(a.one_minus_b2, g * g, v * a.b2);
     const float d = sqrtf(v) / bc2s + a.eps;
-    p = p + nstep * (m / d);
+    p = __builtin_fmaf(nstep, m / d, p);
 }
 
 __global__ __launch_bounds__(kAdamThreads) void k_adam(AdamLaunch a) {
