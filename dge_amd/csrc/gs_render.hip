@@ -147,6 +147,29 @@ __device__ __forceinline__ float blend_chain(float a, float4 fe, uint32_t pos, f
     return w;
 }
 
+// blend_chain split at Tw (identical operations): the transmittance step, then the sums
+__device__ __forceinline__ float blend_t(float a, float& Ts) {
+#pragma clang fp contract(off)
+    const float tT = Ts * (1.0f - a);
+    const bool go = tT >= 0.0001f;
+    const float Tw = go ? Ts : 0.0f;
+    Ts = go ? tT : -fabsf(Ts);
+    return Tw;
+}
+__device__ __forceinline__ float blend_sums(float a, float Tw, float4 fe, uint32_t pos, f2v& C01, f2v& C2D, f2v& L01,
+                                            float& L2, uint32_t& last) {
+#pragma clang fp contract(off)
+    const f2v a2 = {a, a}, T2 = {Tw, Tw};
+    const f2v fa01 = f2v{fe.x, fe.y} * a2, fa2d = f2v{fe.z, fe.w} * a2;
+    C01 = __builtin_elementwise_fma(fa01, T2, C01);
+    C2D = __builtin_elementwise_fma(fa2d, T2, C2D);
+    L01 = __builtin_elementwise_fma(fa01, T2, L01);
+    L2 = __builtin_fmaf(fa2d.x, Tw, L2);
+    const float w = a * Tw;
+    last = w > 0.0f ? pos : last;
+    return w;
+}
+
 // Dispatch order of the blend: tiles by list length, longest first (coarse
 // log-scale classes; the order inside a class is whatever the LDS atomics give
 // — it only decides placement).  The longest lists are then dealt first, one
@@ -190,6 +213,9 @@ __global__ __launch_bounds__(64, 3) void k_render_fwd(RenderArgs a) {
     const int qidx = 4 * tile + quad;
     const int tx = tile % a.gx, ty = tile / a.gx;
     const int lane = threadIdx.x;
+#ifdef GS_FWD_PRIO_RANKS
+    if (rank < GS_FWD_PRIO_RANKS) __builtin_amdgcn_s_setprio(3);
+#endif
     const int bx0 = tx * kTile + (quad & 1) * kQuad, by0 = ty * kTile + (quad >> 1) * kQuad;
     const int px = bx0 + (lane & 7), py = by0 + (lane >> 3);
     const bool inside = px < a.W && py < a.H;
@@ -427,11 +453,419 @@ __global__ __launch_bounds__(64, 3) void k_render_fwd(RenderArgs a) {
     }
 }
 
+// =====================================================================
+// forward, pipelined: one 128-thread workgroup (two waves) per 8x8 quadrant
+// =====================================================================
+// The blend of a quadrant is sequential only in its per-pixel transmittance
+// chain; the cull and the alpha test of an entry (~60% of k_render_fwd's VALU
+// work per kept entry) are independent of it.  A lone wave running all of it
+// spends ~260 cycles per kept entry (tools/probes/chain_latency.hip: a
+// dependent VALU result costs ~10 cycles, and every VALU -> SALU hand-off —
+// a ballot vote read by scalar code, a readfirstlane, a branch on __any — ~40),
+// so the heaviest quadrants (~650 kept entries over ~2800 list positions at
+// c2) set k_render_fwd's span while most of the chip idles.  Here the work of
+// one quadrant is split over two waves (on two SIMDs), stepped by one block
+// barrier per chunk of <= kPcChunk kept entries of one 256-position segment:
+//   wave 1 (producer): turns the previous chunk's votes into the backward's
+//                      blended-bit words (LDS atomics, list order), runs the
+//                      alpha test of chunk t for the 64 pixels, a' = ok ? alpha
+//                      : 0 into an LDS buffer (pixel_alpha4, the identical
+//                      instruction sequence, hence identical bits), then
+//                      gathers, culls against the quadrant and compacts the list
+//                      into the chunk ring (rounds of 128 positions, gathers one
+//                      round and ids two rounds ahead) until chunk t+1 is closed;
+//   wave 0 (chain):    blend_chain over chunk t-1 — T, colour, depth,
+//                      n_contrib, the checkpoint of every finished segment —
+//                      with no scalar hand-off per entry: the per-entry votes
+//                      stay in a lane mask, OR-reduced once per chunk.
+// Outputs are those of k_render_fwd bit for bit (same arithmetic per entry,
+// same entry order).  Checkpoints and blended-bit words are written for every
+// segment/word up to the last chained chunk (the backward reads none past the
+// last contributor).  ~20 KB of LDS and <= 128 VGPRs: 8 workgroups per CU
+// (2048 quadrants in flight chip-wide).
+constexpr int kPcChunk = 16;                  // kept entries per chunk (one pipeline step)
+constexpr int kPcCull = 128;                  // list positions per cull round (2 per lane)
+constexpr int kPcChunks = 16;                 // chunk slots in the ring
+constexpr int kPcRing = kPcChunk * kPcChunks;
+constexpr int kPcWords = 32;                  // blended-bit words being assembled (window)
+static_assert(kSegLen % kPcCull == 0, "a cull round lies inside one segment");
+// live chunk slots: chain t-1 .. producer t+1 plus one cull round's overshoot (<= 9 chunks)
+static_assert(kPcChunks >= 3 + (kPcChunk - 1 + kPcCull) / kPcChunk + 1, "chunk ring size");
+
+__device__ __forceinline__ uint32_t hw_simd_id() { return (__builtin_amdgcn_s_getreg(4 | (31 << 11)) >> 4) & 3u; }
+
+// OR over the 64 lanes with DPP row ops (the wave_sum_to_lane63 pattern); the result lands in lane 63
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ uint32_t dpp_u32(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROW_MASK, 0xF, false);
+}
+__device__ __forceinline__ uint32_t wave_or_to_lane63(uint32_t v) {
+    v |= dpp_u32<0xB1, 0xF>(v);
+    v |= dpp_u32<0x4E, 0xF>(v);
+    v |= dpp_u32<0x141, 0xF>(v);
+    v |= dpp_u32<0x140, 0xF>(v);
+    v |= dpp_u32<0x142, 0xA>(v);
+    v |= dpp_u32<0x143, 0xC>(v);
+    return v;
+}
+
+__global__ __launch_bounds__(128, 4) void k_render_fwd_pc(RenderArgs a) {
+    __shared__ __attribute__((aligned(16))) float r_x[kPcRing], r_y[kPcRing], r_cx[kPcRing], r_cy[kPcRing],
+        r_cz[kPcRing], r_op[kPcRing];
+    __shared__ float4 r_rgbd[kPcRing];
+    __shared__ __attribute__((aligned(16))) uint32_t r_pos[kPcRing];  // 1-based list position
+    __shared__ uint32_t s_meta[kPcChunks];        // chunk slot: entries | segment << 5
+    __shared__ uint32_t s_votes[kPcChunks];       // chunk slot: bit e = some pixel blended entry e
+    __shared__ f4v s_alpha[2][kPcChunk / 4][64];  // [chunk parity][group of 4 entries][pixel]
+    __shared__ unsigned long long s_words[kPcWords];
+    __shared__ uint32_t s_count[2];               // [step parity]: chunks closed | list culled << 31
+    __shared__ uint32_t s_stop[2];                // [step parity]: every pixel saturated
+    __shared__ uint32_t s_simd[2];
+    __shared__ uint64_t s_pstat;
+
+    // (wave index made uniform for the compiler: the role branches below are scalar branches)
+    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)), lane = (int)(threadIdx.x & 63);
+    // XCD-aware as k_render_fwd: blocks b, b+8, b+16, b+24 take the four quadrants of one tile
+    const int x8 = blockIdx.x & 7, j8 = blockIdx.x >> 3;
+    const int quad = j8 & 3, rank = (j8 >> 2) * 8 + x8;
+    if (rank >= a.gx * a.gy) return;
+    const int tile = (int)a.tile_order[rank];
+    const int qidx = 4 * tile + quad;
+    const int tx = tile % a.gx, ty = tile / a.gx;
+    const int bx0 = tx * kTile + (quad & 1) * kQuad, by0 = ty * kTile + (quad >> 1) * kQuad;
+    const int px = bx0 + (lane & 7), py = by0 + (lane >> 3);
+    const bool inside = px < a.W && py < a.H;
+    const float pfx = (float)px, pfy = (float)py;
+    const uint2 range = a.ranges[tile];
+    const bool list_empty = range.y <= range.x;
+    const uint32_t k_last = list_empty ? 0u : range.y - 1;
+#ifdef GS_FWD_PRIO_RANKS
+    if (rank < GS_FWD_PRIO_RANKS) __builtin_amdgcn_s_setprio(3);
+#endif
+    if (a.diag && lane == 0) s_simd[wave] = hw_simd_id();
+    const uint64_t t_entry = a.diag ? __builtin_amdgcn_s_memrealtime() : 0;
+
+    if (threadIdx.x < 2) s_stop[threadIdx.x] = 0u;
+    // Step control, evaluated identically by both waves after each barrier (the published words are
+    // double-buffered by step parity, so no wave can see a later step's value): the loop ends when
+    // the chain wave saw every pixel saturate, or when the list is culled and its last chunk chained.
+    // Each role runs its own loop (disjoint register live ranges) with one barrier per step.
+    const auto step_go = [&](int t, uint32_t& nch, bool& done) {
+        const uint32_t cw = s_count[t & 1];
+        nch = cw & 0x7FFFFFFFu;
+        done = (cw >> 31) != 0;
+        return !(s_stop[t & 1] || (done && t - 1 >= (int)nch));
+    };
+
+    if (wave == 1) {
+        // ================= producer =================
+        if (lane < kPcWords) s_words[lane] = 0ull;
+        uint32_t cb = range.x;    // first list position of the next cull round
+        uint32_t n_closed = 0;    // chunks closed (their entries and meta are final)
+        uint32_t fill = 0;        // entries of the open chunk (index n_closed)
+        uint32_t open_seg = 0;    // segment of the open chunk
+        uint32_t ids[2];
+        Entry cur[2], nxt[2];  // gathered entries of the round being culled and of the next one
+        const auto load_ids = [&](uint32_t b) {
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const uint32_t k = b + 64 * i + lane;
+                ids[i] = list_empty ? 0u : a.point_pairs[k < range.y ? k : k_last].x;
+            }
+        };
+        const auto close_open = [&]() {  // a partial chunk: its pad slots blend nothing (zero opacity, colour)
+            const uint32_t cs = n_closed % kPcChunks;
+            if (lane == 0) s_meta[cs] = fill | open_seg << 5;
+            if (lane >= (int)fill && lane < kPcChunk) {
+                const uint32_t slot = cs * kPcChunk + lane;
+                r_x[slot] = r_y[slot] = r_cx[slot] = r_cy[slot] = r_cz[slot] = r_op[slot] = 0.f;
+                r_rgbd[slot] = make_float4(0.f, 0.f, 0.f, 0.f);
+                r_pos[slot] = 0u;
+            }
+            ++n_closed;
+            fill = 0;
+        };
+        const auto cull_round = [&]() {
+            const uint32_t seg = (cb - range.x) / kSegLen;
+            if (fill > 0 && seg != open_seg) close_open();  // a chunk holds one segment's entries
+            open_seg = seg;
+            uint32_t nk = 0;
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const uint32_t k = cb + 64 * i + lane;
+                const bool keep = k < range.y && cull_keep(cur[i].xy, cur[i].co, (float)bx0, (float)by0);
+                const uint64_t km = __ballot(keep);
+                if (keep) {
+                    const uint32_t j = fill + nk + __popcll(km & lanemask_lt());
+                    const uint32_t slot = ((n_closed + j / kPcChunk) % kPcChunks) * kPcChunk + j % kPcChunk;
+                    r_x[slot] = cur[i].xy.x;
+                    r_y[slot] = cur[i].xy.y;
+                    r_cx[slot] = cur[i].co.x;
+                    r_cy[slot] = -cur[i].co.y;  // (negated: pixel_alpha4)
+                    r_cz[slot] = cur[i].co.z;
+                    r_op[slot] = cur[i].co.w;
+                    r_rgbd[slot] = cur[i].f;
+                    r_pos[slot] = k - range.x + 1;  // 1-based contributor index (forward.cu:331)
+                }
+                nk += (uint32_t)__popcll(km);
+            }
+            const uint32_t total = fill + nk, full = total / kPcChunk;
+            if (lane < (int)full) s_meta[(n_closed + lane) % kPcChunks] = kPcChunk | seg << 5;
+            n_closed += full;
+            fill = total % kPcChunk;
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                cur[i] = nxt[i];
+                nxt[i] = gather_entry(a.splat, ids[i]);
+            }
+            load_ids(cb + 3 * kPcCull);
+            cb += kPcCull;
+            if (cb >= range.y && fill > 0) close_open();
+        };
+        const auto cull_until = [&](uint32_t target) {
+            while (n_closed < target && cb < range.y) cull_round();
+        };
+        const auto publish = [&](int slot) {
+            if (lane == 0) s_count[slot] = n_closed | (cb >= range.y ? 0x80000000u : 0u);
+        };
+        // blended-bit words: those below word `wnew` are final (later chunks lie past them)
+        uint32_t wlo = 0, w_end = 0;  // first unwritten word; one past the last word owed
+        uint64_t* used = a.used + (size_t)used_base(range.x, tile) * 4 + quad;
+        const auto flush_below = [&](uint32_t wnew) {
+            for (; wlo < wnew; wlo += kPcWords) {
+                const uint32_t w = wlo + (uint32_t)lane;
+                if (lane < kPcWords && w < wnew) {
+                    used[(size_t)w * 4] = s_words[w % kPcWords];
+                    s_words[w % kPcWords] = 0ull;
+                }
+            }
+            wlo = wnew;
+        };
+        const auto convert = [&](int c) {  // the chain's votes of chunk c -> words
+            const int cs = c % kPcChunks;
+            const uint32_t nc = s_meta[cs] & 31u, votes = s_votes[cs];
+            const uint32_t p_first = __builtin_amdgcn_readfirstlane(r_pos[cs * kPcChunk]) - 1u;
+            const uint32_t p_last = __builtin_amdgcn_readfirstlane(r_pos[cs * kPcChunk + nc - 1]) - 1u;
+            flush_below(p_first >> 6);
+            if (lane < (int)nc && ((votes >> lane) & 1u)) {
+                const uint32_t p = r_pos[cs * kPcChunk + lane] - 1u;
+                atomicOr(&s_words[(p >> 6) % kPcWords], 1ull << (p & 63u));
+            }
+            w_end = (p_last >> 6) + 1;
+        };
+        if (!list_empty) {  // gathers two rounds ahead, ids three
+            load_ids(range.x);
+#pragma unroll
+            for (int i = 0; i < 2; ++i) cur[i] = gather_entry(a.splat, ids[i]);
+            load_ids(range.x + kPcCull);
+#pragma unroll
+            for (int i = 0; i < 2; ++i) nxt[i] = gather_entry(a.splat, ids[i]);
+            load_ids(range.x + 2 * kPcCull);
+        }
+        // a quadrant without a pixel inside the image blends nothing (k_render_fwd's first-round exit)
+        if (__any(inside)) cull_until(1);
+        else cb = range.y;
+        publish(0);
+        __syncthreads();
+        uint64_t p_alpha = 0, p_cull = 0;
+        int pending = -1;  // the chunk the chain wave took in the previous step: its votes are final
+        for (int t = 0;; ++t) {
+            uint32_t nch;
+            bool done;
+            if (!step_go(t, nch, done)) break;
+            const uint64_t q0 = a.diag ? __builtin_amdgcn_s_memtime() : 0;
+            if (pending >= 0) convert(pending);
+            pending = (t >= 1 && t - 1 < (int)nch) ? t - 1 : -1;  // (the chain wave's test, same words)
+            const uint64_t q1 = a.diag ? __builtin_amdgcn_s_memtime() : 0;
+            if (t < (int)nch) {          // alpha test of chunk t: a' = ok ? alpha : 0 (blend_chain's operand)
+                const int cs = t % kPcChunks;
+                const int nc = (int)(s_meta[cs] & 31u);
+                // two groups of four at a time (four independent packed streams); a group past the chunk's
+                // end computes an unused slot
+                for (int g = 0; 4 * g < nc; g += 2) {
+                    f4v ap[2];
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        const int ri = cs * kPcChunk + 4 * (g + h);
+                        const auto ld4 = [&](const float* f) { return *reinterpret_cast<const f4v*>(f + ri); };
+                        f4v dx4, dy4, G4, al;
+                        bool ok[4];
+                        pixel_alpha4(ld4(r_x), ld4(r_y), ld4(r_cx), ld4(r_cy), ld4(r_cz), ld4(r_op), -pfx, -pfy,
+                                     dx4, dy4, G4, al, ok);
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) ap[h][u] = ok[u] ? al[u] : 0.0f;
+                    }
+                    s_alpha[t & 1][g][lane] = ap[0];
+                    s_alpha[t & 1][g + 1][lane] = ap[1];
+                }
+            }
+            const uint64_t q2 = a.diag ? __builtin_amdgcn_s_memtime() : 0;
+            if (!done) cull_until((uint32_t)(t + 2));  // chunk t+1 closed for the next step
+            publish((t + 1) & 1);
+            if (a.diag) {
+                p_alpha += q2 - q1;
+                p_cull += __builtin_amdgcn_s_memtime() - q2;
+            }
+            __syncthreads();
+        }
+        if (pending >= 0) convert(pending);  // the last chunk the chain wave took
+        flush_below(w_end);
+        if (a.diag) {  // (diagnostics) the producer's cycles in the alpha tests and the cull, for wave 0's record
+            if (lane == 0) s_pstat = p_alpha | p_cull << 32;
+            __syncthreads();
+        }
+        return;
+    }
+    __syncthreads();  // (the producer's prologue)
+
+    // ================= chain wave (wave 0) =================
+    float Ts = inside ? 1.0f : -1.0f;  // signed transmittance (blend_chain)
+    f2v C01 = {0.f, 0.f}, C2D = {0.f, 0.f}, L01 = {0.f, 0.f};
+    float L2 = 0.f;
+    uint32_t last = 0;
+    uint32_t cur_seg = 0;  // segment of the chain position (its checkpoint is owed)
+    bool chained = false;  // any chunk chained
+    uint32_t diag_kept = 0;
+    float4* ckpt = a.ckpt + ((size_t)ckpt_base(range.x, tile) * 4 + quad) * 64;
+    const uint64_t t_start = a.diag ? __builtin_amdgcn_s_memrealtime() : 0;
+    const uint64_t c_start = a.diag ? __builtin_amdgcn_s_memtime() : 0;
+    uint64_t c_chain = 0;
+    struct Ops {  // a group's operands: alpha of this lane's pixel, colours, positions
+        f4v a4;
+        float4 f[4];
+        uint4 p4;
+    };
+    for (int t = 0;; ++t) {
+        uint32_t nch;
+        bool done;
+        if (!step_go(t, nch, done)) break;
+        const int c = t - 1;
+        if (c >= 0 && c < (int)nch) {
+            const uint64_t c0 = a.diag ? __builtin_amdgcn_s_memtime() : 0;
+            const int cs = c % kPcChunks;
+            const uint32_t meta = __builtin_amdgcn_readfirstlane(s_meta[cs]);
+            const int nc = (int)(meta & 31u);
+            const uint32_t seg = meta >> 5;
+            if (!__any(Ts > 0.0f)) {  // every pixel saturated: nothing more to blend
+                if (lane == 0) {
+                    s_stop[(t + 1) & 1] = 1u;
+                    s_votes[cs] = 0u;
+                }
+            } else {
+                if (seg != cur_seg) {  // the checkpoints of the segments before this chunk's
+                    ckpt[(size_t)cur_seg * 256 + lane] = make_float4(fabsf(Ts), L01.x, L01.y, L2);
+                    L01 = f2v{0.f, 0.f};
+                    L2 = 0.f;
+                    for (uint32_t s2 = cur_seg + 1; s2 < seg; ++s2)
+                        ckpt[(size_t)s2 * 256 + lane] = make_float4(fabsf(Ts), 0.f, 0.f, 0.f);
+                    cur_seg = seg;
+                }
+                const f4v* al = s_alpha[c & 1][0];
+                const auto load_ops = [&](int g, Ops& o) {
+                    const int ri = cs * kPcChunk + 4 * g;
+                    o.a4 = al[g * 64 + lane];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) o.f[u] = r_rgbd[ri + u];
+                    o.p4 = *reinterpret_cast<const uint4*>(&r_pos[ri]);
+                };
+                uint32_t lv = 0;  // this pixel's votes: bit e = entry e of the chunk blended here
+                // four entries: the transmittance chain first (the critical path), then the sums, which
+                // only need each entry's Tw; pad entries (a' = 0, zero colour) change nothing
+                const auto group = [&](int g, const Ops& o) {
+                    const uint32_t pu[4] = {o.p4.x, o.p4.y, o.p4.z, o.p4.w};
+                    float tw[4];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) tw[u] = blend_t(o.a4[u], Ts);
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const float w = blend_sums(o.a4[u], tw[u], o.f[u], pu[u], C01, C2D, L01, L2, last);
+                        lv |= w > 0.0f ? 1u << (4 * g + u) : 0u;
+                    }
+                };
+                Ops oa, ob;  // ping-pong: a group's operands are read while the previous group blends
+                load_ops(0, oa);
+                if (4 < nc) load_ops(1, ob);
+                group(0, oa);
+                if (4 < nc) {
+                    if (8 < nc) load_ops(2, oa);
+                    group(1, ob);
+                    if (8 < nc) {
+                        if (12 < nc) load_ops(3, ob);
+                        group(2, oa);
+                        if (12 < nc) group(3, ob);
+                    }
+                }
+                const uint32_t votes = wave_or_to_lane63(lv);
+                if (lane == 63) s_votes[cs] = votes;
+                chained = true;
+                diag_kept += nc;
+            }
+            if (a.diag) c_chain += __builtin_amdgcn_s_memtime() - c0;
+        }
+        __syncthreads();
+    }
+
+    if (a.diag) __syncthreads();  // (diagnostics: the producer's s_pstat)
+    // the owed checkpoint of the last chained segment
+    const float T = fabsf(Ts);
+    if (chained) ckpt[(size_t)cur_seg * 256 + lane] = make_float4(T, L01.x, L01.y, L2);
+    if (inside) {
+        const size_t pix = (size_t)a.W * py + px;
+        const size_t HW = (size_t)a.W * a.H;
+        a.final_T[pix] = T;
+        a.n_contrib[pix] = last;
+        a.out_color[pix] = __builtin_fmaf(T, a.bg[0], C01.x);
+        a.out_color[HW + pix] = __builtin_fmaf(T, a.bg[1], C01.y);
+        a.out_color[2 * HW + pix] = __builtin_fmaf(T, a.bg[2], C2D.x);
+        a.out_depth[pix] = C2D.y;
+    }
+    const uint32_t m = wave_max_u32(inside ? last : 0u);
+    if (m) {  // the backward replay's work items for this quadrant (as k_render_fwd)
+        const uint32_t nseg = (m + kSegLen - 1) / kSegLen;
+        if (nseg > 1) {
+            uint32_t base = 0;
+            if (lane == 0) base = atomicAdd(&a.bwd_count[0], nseg);
+            base = __shfl(base, 0);
+            for (uint32_t k = lane; k < nseg; k += 64) a.bwd_items[base + k] = make_uint2(tile, (k << 2) | quad);
+        } else if (lane == 0) {
+            const uint32_t b = atomicAdd(&a.bwd_count[1], 1u);
+            a.bwd_items[a.item_cap - 1 - b] = make_uint2(tile, quad);
+        }
+    }
+    if (lane == 0) {
+        a.quad_last[qidx] = m;
+        if (m) atomicMax(&a.tile_last[tile], m);
+        if (a.diag) {
+            uint64_t* d = a.diag + kDiagWords * (size_t)qidx;
+            d[0] = t_entry;
+            d[1] = __builtin_amdgcn_s_memrealtime();
+            d[2] = diag_kept;
+            d[3] = s_pstat;  // producer cycles: alpha tests | cull << 32
+            d[4] = c_chain;
+            d[5] = __builtin_amdgcn_s_memtime() - c_start;
+            d[6] = s_simd[0] | s_simd[1] << 2 | (uint64_t)(t_start - t_entry) << 8 | (uint64_t)rank << 40;
+            d[7] = wave_location();
+        }
+    }
+}
+
+static int fwd_variant() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("DGE_AMD_FWD");
+        v = (e && e[0] == '1') ? 1 : 0;  // 0: one wave per quadrant (k_render_fwd), 1: pipelined (experiment)
+    }
+    return v;
+}
+
 void launch_render_forward(const RenderArgs& a, hipStream_t s) {
     const int tiles = a.gx * a.gy;
     if (tiles <= 0) return;
     if (!a.order_ready) hipLaunchKernelGGL(k_tile_order, dim3(1), dim3(1024), 0, s, a.ranges, tiles, a.tile_order);
-    hipLaunchKernelGGL(k_render_fwd, dim3(div_up(tiles, 8) * 32), dim3(64), 0, s, a);
+    if (fwd_variant() == 1)
+        hipLaunchKernelGGL(k_render_fwd_pc, dim3(div_up(tiles, 8) * 32), dim3(128), 0, s, a);
+    else
+        hipLaunchKernelGGL(k_render_fwd, dim3(div_up(tiles, 8) * 32), dim3(64), 0, s, a);
 }
 
 // =====================================================================
