@@ -144,7 +144,7 @@ SIGNATURES = {
     "gs_profile_collect": (ctypes.c_int, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int), ctypes.c_int]),
     "gs_profile_diag_enable": (ctypes.c_int, [ctypes.c_int]),
     "gs_profile_diag_read": (ctypes.c_longlong, [ctypes.c_int, ctypes.POINTER(ctypes.c_uint64), ctypes.c_longlong]),
-    "gs_adam_step": (ctypes.c_int, [ctypes.POINTER(AdamSegment), ctypes.c_int, ctypes.c_float, ctypes.c_float,
+    "gs_adam_step": (ctypes.c_int, [ctypes.POINTER(AdamSegment), ctypes.c_int, ctypes.c_double, ctypes.c_double,
                                     ctypes.c_float, ctypes.c_void_p]),
     "gs_rows_live": (ctypes.c_int, [ctypes.POINTER(RowsRegion), ctypes.c_int, ctypes.c_longlong, ctypes.c_void_p,
                                     ctypes.c_void_p]),

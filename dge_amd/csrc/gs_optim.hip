@@ -105,7 +105,7 @@ __global__ __launch_bounds__(kAdamThreads) void k_adam(AdamLaunch a) {
 
 }  // namespace gs
 
-extern "C" int gs_adam_step(const gs_adam_segment* segs, int nseg, float beta1, float beta2, float eps,
+extern "C" int gs_adam_step(const gs_adam_segment* segs, int nseg, double beta1, double beta2, float eps,
                             gs_stream_t stream) {
     using namespace gs;
     if (nseg < 0 || (nseg > 0 && !segs)) return report_error(GS_ERR_INVALID_ARG, "gs_adam_step: bad segment list");
@@ -113,10 +113,10 @@ extern "C" int gs_adam_step(const gs_adam_segment* segs, int nseg, float beta1, 
     int i = 0;
     while (i < nseg) {  // launches of up to GS_ADAM_MAX_SEGMENTS non-empty segments
         AdamLaunch a{};
-        a.b1 = beta1;
-        a.b2 = beta2;
-        a.one_minus_b1 = (float)(1.0 - (double)beta1);
-        a.one_minus_b2 = (float)(1.0 - (double)beta2);
+        a.b1 = (float)beta1;
+        a.b2 = (float)beta2;
+        a.one_minus_b1 = (float)(1.0 - beta1);  // (torch: the Python float 1 - beta, rounded once)
+        a.one_minus_b2 = (float)(1.0 - beta2);
         a.eps = eps;
         long long blocks = 0;
         int k = 0;

@@ -10,8 +10,10 @@ per-parameter state ``step`` / ``exp_avg`` / ``exp_avg_sq`` — but its step is
 ONE gfx950 kernel over every group (``gs_adam_step``, dge_amd/csrc/gs_optim.hip)
 instead of torch's per-tensor chain of elementwise kernels.
 
-Arithmetic: torch's single-tensor Adam (torch/optim/adam.py) in its operation
-order, with the bias corrections computed in double on the host as torch does.
+Arithmetic: torch's foreach Adam (torch/optim/adam.py, the path torch.optim.Adam
+takes for GPU tensors) in the float32 operation order its kernels compile to,
+with the bias corrections and 1 - beta computed in double on the host as torch
+does with Python floats: bit-identical to it (tests/test_gpu_model.py).
 Only the configuration the reference uses is supported (weight_decay = 0, no
 amsgrad/maximize); anything else raises, as does a CPU tensor: there is no
 fallback path.

@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define GS_RASTER_ABI_VERSION 6
+#define GS_RASTER_ABI_VERSION 7
 
 #define GS_OK 0
 #define GS_ERR_INVALID_ARG 1   /* AT_ERROR / std::runtime_error in the reference */
@@ -199,9 +199,11 @@ int gs_apply_weights(const gs_settings *s, int P, int M, const float *means3D, f
 /* Fused Adam step over several parameter tensors in ONE launch — the
  * optimizer of the training loop (gaussian_model.py:336-380:
  * torch.optim.Adam(groups, lr=0.0, eps=1e-15), one group per parameter;
- * torch/optim/adam.py _single_tensor_adam arithmetic).  Per segment the
- * caller passes the group's step scalars (its own step count):
+ * the float32 operation order of torch's foreach Adam on the GPU).  Per
+ * segment the caller passes the group's step scalars (its own step count):
  * step_size = lr / (1 - beta1^t), bias_correction2_sqrt = sqrt(1 - beta2^t).
+ * beta1/beta2 are doubles, as torch's Python floats: 1 - beta is formed in
+ * double before the one rounding to float (ABI 7; a float beta rounds twice).
  * param, exp_avg, exp_avg_sq are updated in place; grad is read. */
 #define GS_ADAM_MAX_SEGMENTS 8    /* per launch; longer lists take several */
 typedef struct gs_adam_segment {
@@ -213,7 +215,7 @@ typedef struct gs_adam_segment {
     float step_size;
     float bias_correction2_sqrt;
 } gs_adam_segment;
-int gs_adam_step(const gs_adam_segment *segs, int nseg, float beta1, float beta2, float eps,
+int gs_adam_step(const gs_adam_segment *segs, int nseg, double beta1, double beta2, float eps,
                  gs_stream_t stream);
 
 /* Sparse-row gradient exchange of the multi-view step (not in the reference,
