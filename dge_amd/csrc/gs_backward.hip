@@ -551,7 +551,12 @@ __global__ __launch_bounds__(kGB) void k_gauss_bwd_live(GaussBwdArgs a) {
             }
         }
         // sum of this Gaussian's records: one per (slot, quadrant) the backward
-        // replay kept, flagged per slot; slots in emission order = tile order
+        // replay kept, flagged per slot; slots in emission order = tile order,
+        // quadrants in order within a slot.  The flagged records are taken four at
+        // a time from a bit mask (bit 4u + quadrant), all twelve loads of a batch
+        // issued before its sums: one memory round trip per four records instead
+        // of one per record (a batch's unused places re-read its first record and
+        // add nothing; acc is never -0, so the skipped +0 changes no bit).
         float acc[9];
 #pragma unroll
         for (int f = 0; f < 9; ++f) acc[f] = 0.f;
@@ -560,16 +565,32 @@ __global__ __launch_bounds__(kGB) void k_gauss_bwd_live(GaussBwdArgs a) {
 #pragma unroll
                 for (int u = 0; u < 8; ++u) fl[u] = k0 + u < n ? flags[first + k0 + u] : 0u;
             }
+            uint32_t m = 0;
 #pragma unroll
-            for (int u = 0; u < 8; ++u) {
+            for (int u = 0; u < 8; ++u)
 #pragma unroll
-                for (int qd = 0; qd < 4; ++qd) {
-                    if ((fl[u] >> (8 * qd)) & 0xFFu) {
-                        const float4* rec = a.records + 3 * (4 * (size_t)(first + k0 + u) + qd);
-                        const float4 r0 = rec[0], r1 = rec[1], r2 = rec[2];
-                        acc[0] += r0.x; acc[1] += r0.y; acc[2] += r0.z; acc[3] += r0.w;
-                        acc[4] += r1.x; acc[5] += r1.y; acc[6] += r1.z; acc[7] += r1.w;
-                        acc[8] += r2.x;
+                for (int qd = 0; qd < 4; ++qd) m |= ((fl[u] >> (8 * qd)) & 0xFFu) ? 1u << (4 * u + qd) : 0u;
+            const float4* recs = a.records + 3 * (4 * (size_t)(first + k0));
+            while (m) {
+                int bi[4];
+                bool use[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    use[i] = m != 0u;
+                    bi[i] = use[i] ? __builtin_ctz(m) : bi[0];
+                    m &= m - 1u;
+                }
+                float4 r[4][3];
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int c = 0; c < 3; ++c) r[i][c] = recs[3 * bi[i] + c];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    if (use[i]) {
+                        acc[0] += r[i][0].x; acc[1] += r[i][0].y; acc[2] += r[i][0].z; acc[3] += r[i][0].w;
+                        acc[4] += r[i][1].x; acc[5] += r[i][1].y; acc[6] += r[i][1].z; acc[7] += r[i][1].w;
+                        acc[8] += r[i][2].x;
                     }
                 }
             }
