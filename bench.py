@@ -98,7 +98,11 @@ def main():
     gpu = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(gpu)
     dev = torch.device("cuda", gpu)
-    if world > 1:
+    # DGE_AMD_BENCH_DIST=1: a process group (and the full sparse all-reduce protocol) even for one rank,
+    # to rehearse the RCCL path on a one-GPU box under torch.distributed.run --nproc-per-node 1
+    rehearse = os.environ.get("DGE_AMD_BENCH_DIST") == "1"
+    distributed = world > 1 or rehearse
+    if distributed:
         backend = os.environ.get("DGE_AMD_BENCH_BACKEND", "nccl")  # nccl = RCCL on ROCm; gloo for rehearsals
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
@@ -128,8 +132,8 @@ def main():
             torch.autograd.backward([o["render"] for o in outs], seeds)
         else:
             render_backward_views(cams, scene, pipe, bg, seeds, streams=args.streams)
-        if world > 1:
-            bucket.allreduce()
+        if distributed:
+            bucket.allreduce(min_world=1 if rehearse else 2)
 
     for _ in range(args.warmup):
         step()
@@ -179,14 +183,14 @@ def main():
         calib = {n: (ms, c) for n, (ms, c) in _native.profile_collect().items() if c}
         _native.profile_stages(blend)
         _native.profile_collect()
-    if world > 1:
+    if distributed:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
     torch.cuda.synchronize()
-    if world > 1:
+    if distributed:
         dist.barrier()
     dt = time.perf_counter() - t0
     prof = {}
@@ -194,7 +198,7 @@ def main():
         prof = _native.profile_collect()
         _native.profile_enable(False)
         _native.profile_stages(None)
-    if world > 1:
+    if distributed:
         t = torch.tensor([dt], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
@@ -285,7 +289,7 @@ def main():
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if distributed:
         dist.destroy_process_group()
 
 

@@ -62,15 +62,17 @@ class GradBucket:
     def check_attached(self) -> bool:
         return all(p.grad is not None and p.grad.data_ptr() == v.data_ptr() for p, v in zip(self.params, self.views))
 
-    def allreduce(self, group=None, async_op: bool = False, sparse: bool = True):
+    def allreduce(self, group=None, async_op: bool = False, sparse: bool = True, min_world: int = 2):
         """SUM of the bucket over the ranks.  sparse (when every parameter has the same number of rows,
         as a GaussianModel's do): only rows that are nonzero on some rank travel — the union of the
         ranks' nonzero rows is agreed with one MAX all-reduce of a byte per row, those rows are packed,
         all-reduced and copied back.  A Gaussian behind saturated pixels in every view of every rank
         gets exactly zero gradient, so at c2 the union of 24 views is ~24% of the rows (~4x fewer
         bytes over xGMI than the dense 236 MB).  Rows outside the union are zero on every rank, so the
-        result is the dense all-reduce's up to the float summation order inside RCCL."""
-        if not dist.is_available() or not dist.is_initialized() or dist.get_world_size(group) == 1:
+        result is the dense all-reduce's up to the float summation order inside RCCL.
+        min_world: smallest group that communicates (1 runs the whole protocol on a one-rank group: the
+        bench's RCCL rehearsal on a one-GPU box)."""
+        if not dist.is_available() or not dist.is_initialized() or dist.get_world_size(group) < min_world:
             return None
         if not self.check_attached():  # autograd replaced a grad: fold it back into the bucket
             for p, v in zip(self.params, self.views):
