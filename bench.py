@@ -242,7 +242,9 @@ def main():
             # peak clock x 1024 SIMDs) -- what bounds these kernels instead of HBM
             vf = tr["valu_insts_per_launch"] * 2.0 / (avg * 1e-3 * CLOCK_HZ * N_SIMDS)
             r["valu_issue_frac"] = round(vf, 4)
-            r["limit"] = "valu/latency" if vf > r["frac"] else "hbm"
+            # what bounds the kernel: a resource it keeps over half busy, else latency (dependent chains,
+            # the tail of the longest quadrants) -- the blend kernels' case, DESIGN.md §4.3-4.4
+            r["limit"] = "hbm" if r["frac"] > 0.5 else "valu" if vf > 0.5 else "latency"
         if tr.get("build"):
             r["pmc_build"] = tr["build"]
         rooflines[name] = r
