@@ -4,16 +4,19 @@
 Workload (BASELINE.json configs[1], "c2"): 1.0M Gaussians (SH degree 3),
 512x512, fp32, one render() forward + its backward per view, seeded synthetic
 scene and orbit cameras of SURVEY.md §8(d) (no network: data = synthetic).
-A step = every rank renders its `--views-per-rank` views, forward + backward
-each (the gradients of the reference's batch step — threestudio/systems/DGE.py
-renders the batch's views and back-propagates the summed loss — up to float
-summation order), accumulated into the shared parameters, and, for N > 1, ONE
+A step = every rank renders its `--views-per-rank` views, then runs one
+backward of their summed loss (the reference's batch step: threestudio/systems/
+DGE.py renders the batch's views and back-propagates the summed loss), the
+gradients accumulated into the shared parameters, and, for N > 1, ONE
 all-reduce of the flat parameter-gradient bucket (RCCL) — of the rows nonzero
-on some rank only (GradBucket.allreduce: ~24% of the 236 MB for 24 views).  `--streams N`
-alternates the views over N HIP streams (dge_amd.multiview.render_backward_views:
-one view's backward overlapping the next view's forward; default 1) and
-`--batch-backward` runs all forwards first, then one backward, as the
-reference orders it.  Per-GPU work
+on some rank only (GradBucket.allreduce: ~24% of the 236 MB for 24 views).  The
+views run on `--streams` HIP streams (default 3, dge_amd.multiview.render_views:
+one view's latency-bound blend tails overlap the others' work; the in-kernel
+gradient accumulation orders only the per-Gaussian passes across streams) and the
+bucket's zero fill overlaps the forwards (GradBucket.zero(overlap=True), issued
+after them);
+`--per-view-backward` runs each view's backward right after its forward
+instead.  Per-GPU work
 is fixed, so scaling is weak and value = all views rendered / max-rank time.
 
 Prints ONE JSON line (rank 0) with the contract keys plus `roofline` (the
@@ -52,12 +55,17 @@ def parse():
     ap.add_argument("--height", type=int, default=512)
     ap.add_argument("--sh-degree", type=int, default=3)
     ap.add_argument("--views-per-rank", type=int, default=3)
-    ap.add_argument("--streams", type=int, default=1,
-                    help="HIP streams the views alternate over (2 measured slower at c2: the host side, one "
-                         "blocking instance-count read-back per forward, is then the limit)")
-    ap.add_argument("--batch-backward", action="store_true",
-                    help="all forwards, then one backward (default: each view's backward right after its "
-                         "forward, overlapping the next view's forward on the other stream)")
+    ap.add_argument("--streams", type=int, default=3,
+                    help="HIP streams the views alternate over (default 3: one per view of a 3-view step, so "
+                         "one view's latency-bound blend tails overlap the others' work)")
+    ap.add_argument("--per-view-backward", dest="batch_backward", action="store_false",
+                    help="each view's backward right after its forward (default: all forwards, then one "
+                         "backward of the summed loss -- the reference's order, DGE.py:170-239, 617-699)")
+    ap.add_argument("--batch-backward", dest="batch_backward", action="store_true", help=argparse.SUPPRESS)
+    ap.set_defaults(batch_backward=True)
+    ap.add_argument("--serial-zero", action="store_true",
+                    help="zero the gradient bucket before the forwards (default with streams: after enqueueing "
+                         "them, only the gradient writes wait for it: GradBucket.zero(overlap=True))")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -112,7 +120,7 @@ def main():
     from dge_amd import _native, _C
     from dge_amd.cameras import orbit_camera
     from dge_amd.gaussian_renderer import PipelineParams, render
-    from dge_amd.multiview import GradBucket, render_backward_views, render_views
+    from dge_amd.multiview import GradBucket
     from dge_amd.scene import synthetic_scene
 
     P, W, H, V = args.points, args.width, args.height, args.views_per_rank
@@ -126,12 +134,7 @@ def main():
     bucket = GradBucket(scene.parameters())
 
     def step():
-        bucket.zero()
-        if args.batch_backward:
-            outs = render_views(cams, scene, pipe, bg, streams=args.streams)
-            torch.autograd.backward([o["render"] for o in outs], seeds)
-        else:
-            render_backward_views(cams, scene, pipe, bg, seeds, streams=args.streams)
+        run_views(args, cams, scene, pipe, bg, seeds, bucket)
         if distributed:
             bucket.allreduce(min_world=1 if rehearse else 2)
 
@@ -295,6 +298,25 @@ def main():
         dist.destroy_process_group()
 
 
+def run_views(args, cams, scene, pipe, bg, seeds, bucket):
+    """One step's renders: zero the bucket, forward every view, backward (see the module docstring)."""
+    from dge_amd.multiview import render_backward_views, render_views
+
+    # the overlapped zero (fused path only: its gradient writes wait for the fill in-kernel) is issued after
+    # the forwards are enqueued on the side streams, so they do not queue behind the 236-MB fill
+    overlap = (not args.serial_zero and args.batch_backward and args.streams > 1
+               and os.environ.get("DGE_AMD_FUSED", "1") != "0")
+    if not overlap:
+        bucket.zero()
+    if args.batch_backward:
+        outs = render_views(cams, scene, pipe, bg, streams=args.streams)
+        if overlap:
+            bucket.zero(overlap=True)
+        torch.autograd.backward([o["render"] for o in outs], seeds)
+    else:
+        render_backward_views(cams, scene, pipe, bg, seeds, streams=args.streams)
+
+
 def _time(fn, steps):
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -337,8 +359,7 @@ def side_legs(args, scene, cams, seeds, bg, pipe, bucket, step, dev):
     hb = GradBucket(hl.parameters())
 
     def hstep():
-        hb.zero()
-        render_backward_views(cams, hl, pipe, bg, seeds, streams=args.streams)
+        run_views(args, cams, hl, pipe, bg, seeds, hb)
 
     for _ in range(3):
         hstep()

@@ -370,14 +370,16 @@ def rasterize_gaussians_fused(background, xyz, f_dc, f_rest, colors, raw_opacity
 def rasterize_gaussians_fused_backward(background, xyz, f_dc, f_rest, colors, raw_opacity, raw_scaling, raw_rotation,
                                        radii, scale_modifier, viewmatrix, projmatrix, tan_fovx, tan_fovy,
                                        dL_dout_color, degree, campos, geomBuffer, R, binningBuffer, imageBuffer,
-                                       debug, into=None, index=None):
+                                       debug, into=None, index=None, writes_after=None):
     """-> (dL_dmeans2D [P,3], dL_dxyz, dL_dfeatures_dc, dL_dfeatures_rest, dL_dcolors, dL_dopacity_raw,
     dL_dscaling_raw, dL_drotation_raw), gradients w.r.t. the raw tensors.
 
     into: optional {"xyz"|"sh"|"opacity"|"scaling"|"rotation": (dest, accumulate)} — write that gradient
     into `dest` (for "sh" a (dc, rest) pair), adding to its contents when accumulate is true (the kernel's
     fused gradient accumulation, gs_grads.accumulate); the returned tuple then holds `dest`.
-    index: the forward's rows; the parameter-shaped gradients are then full-size, zero outside them."""
+    index: the forward's rows; the parameter-shaped gradients are then full-size, zero outside them.
+    writes_after: optional torch.cuda.Event the stream waits for before the first accumulated write
+    (gs_grads.writes_after: after the replay, before the per-Gaussian pass)."""
     N.require_gpu(xyz)
     dev = xyz.device
     index = _index32(index)
@@ -432,6 +434,8 @@ def rasterize_gaussians_fused_backward(background, xyz, f_dc, f_rest, colors, ra
         o.dsh_rest_stride = 3 * (d_rest.size(1) if d_rest is not None else 0)
         o.dL_dscales, o.dL_drotations = _ptr(d_sc), _ptr(d_rot)
         o.accumulate = acc_bits
+        if writes_after is not None:
+            o.writes_after = writes_after.cuda_event
         gm = into.get("grad_mask")
         if gm is not None:
             mask_t, names = gm

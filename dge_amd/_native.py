@@ -91,6 +91,7 @@ class GsGrads(ctypes.Structure):
         ("grad_mask", ctypes.c_void_p),
         ("mask_bits", ctypes.c_uint),
         ("dL_dconic", _fp),
+        ("writes_after", ctypes.c_void_p),
     ]
 
 

@@ -602,6 +602,7 @@ int gs_rasterize_backward(const gs_settings* s, int P, int M, int R, const float
     o.grad_mask = nullptr;
     o.mask_bits = 0;
     o.dL_dconic = nullptr;
+    o.writes_after = nullptr;
     gs_params g2 = g;
     g2.M = M;  // dL_dsh is [P,M,3] even when shs is absent (then all zero)
     return gs_rasterize_backward_ex(s, &g2, R, radii, geom, binning, img, dL_dpix, &o, stream);
@@ -700,7 +701,8 @@ int gs_rasterize_backward_ex(const gs_settings* s, const gs_params* gp, int R, c
         ga.mask_bits = o->grad_mask ? o->mask_bits : 0u;
         ga.dL_dconic = o->dL_dconic;
         ga.diag = diag_buffer(2, kDiagWords * 4 * (size_t)(P / 256 + 1));
-        { StageScope sc(ST_GAUSS_BWD, stream); launch_gauss_backward(ga, stream); }
+        { StageScope sc(ST_GAUSS_BWD, stream);
+        launch_gauss_backward(ga, stream, (hipEvent_t)o->writes_after); }
         GS_LAUNCHED("gaussian backward");
         return GS_OK;
     } catch (const std::exception& e) {

@@ -642,10 +642,12 @@ __global__ __launch_bounds__(kGB) void k_gauss_bwd_live(GaussBwdArgs a) {
     }
 }
 
-void launch_gauss_backward(const GaussBwdArgs& a, hipStream_t s) {
+void launch_gauss_backward(const GaussBwdArgs& a, hipStream_t s, hipEvent_t writes_after) {
     if (a.P <= 0) return;
     const int blocks = div_up(a.P, kGB);
     hipLaunchKernelGGL(k_gauss_live, dim3(blocks), dim3(kGB), 0, s, a);
+    // k_gauss_live writes only overwritten (per-call) outputs; the accumulated ones start here
+    if (writes_after) (void)hipStreamWaitEvent(s, writes_after, 0);
     const int group = std::min(div_up(blocks, kLiveGrid), kLiveGroup);  // (the kernel derives the same)
     hipLaunchKernelGGL(k_gauss_bwd_live, dim3(div_up(blocks, group)), dim3(kGB), 0, s, a);
 }

@@ -367,7 +367,7 @@ struct GaussBwdArgs {
     float* dL_dconic;          // optional [P,3]: the summed conic gradient (parity tests)
     uint64_t* diag;            // optional per-wave phase stamps of k_gauss_bwd_live (see diag_buffer)
 };
-void launch_gauss_backward(const GaussBwdArgs& a, hipStream_t s);
+void launch_gauss_backward(const GaussBwdArgs& a, hipStream_t s, hipEvent_t writes_after = nullptr);
 
 // diagnostics (gs_profile_diag_*): per-wave records of the blend kernels,
 // kDiagWords u64 each: start, end (s_memrealtime, 100 MHz), kept entries,

@@ -187,10 +187,10 @@ class _RasterizeGaussiansFused(torch.autograd.Function):
                 geomBuffer, ctx.num_rendered, binningBuffer, imgBuffer, rs.debug)
         _serialize_scratch(ctx, xyz.device)
         ordered = bool(into) and _SIDE_STREAMS
-        stream = _order_grad_writes_begin(xyz.device) if ordered else None
+        stream, after = _order_grad_writes_begin(xyz.device) if ordered else (None, None)
         d_m2, d_xyz, d_dc, d_rest, d_col, d_op, d_sc, d_rot = _call_with_snapshot(
-            lambda *a: _C.rasterize_gaussians_fused_backward(*a, into=into, index=ctx.index), args, rs.debug,
-            "snapshot_bw.dump", "backward")
+            lambda *a: _C.rasterize_gaussians_fused_backward(*a, into=into, index=ctx.index, writes_after=after),
+            args, rs.debug, "snapshot_bw.dump", "backward")
         if ordered:
             _order_grad_writes_end(xyz.device, stream, [t for _, t in direct])
         for p, t in direct:  # parameters whose .grad was None: the kernel wrote it, hand it over
@@ -223,11 +223,14 @@ _SIDE_STREAMS = False  # set once dge_amd.multiview.stream_pool hands out stream
 
 
 def _order_grad_writes_begin(dev):
+    """(current stream, the event its .grad writes must wait for or None).  The wait is placed by the
+    backward itself right before its per-Gaussian pass (gs_grads.writes_after), so this view's gradient
+    replay still overlaps the previous view's gradient writes on the other stream."""
     cur = torch.cuda.current_stream(dev)
     last = _GRAD_WRITES.get(dev.index)
     if last is not None and last[0] != cur:
-        cur.wait_event(last[1])
-    return cur
+        return cur, last[1]
+    return cur, None
 
 
 def _order_grad_writes_end(dev, cur, fresh):

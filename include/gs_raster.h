@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define GS_RASTER_ABI_VERSION 7
+#define GS_RASTER_ABI_VERSION 8
 
 #define GS_OK 0
 #define GS_ERR_INVALID_ARG 1   /* AT_ERROR / std::runtime_error in the reference */
@@ -174,6 +174,12 @@ typedef struct gs_grads {         /* backward outputs, every element written */
      * Gaussian's summed conic gradient (x, y, w of backward.cu's dL_dconic2D),
      * the input of the per-Gaussian chain; NULL: not written. */
     float *dL_dconic;
+    /* Optional hipEvent_t (NULL: none): the stream waits for it right before
+     * the first write of an ACCUMULATED output (the per-Gaussian pass), not
+     * before the gradient replay.  Backward calls of different views that add
+     * into the same .grad buffers from different streams are ordered by it
+     * while the replay of one overlaps the per-Gaussian pass of the other. */
+    void *writes_after;
 } gs_grads;
 
 int gs_rasterize_forward_ex(const gs_settings *s, const gs_params *g, float *out_color, float *out_depth,

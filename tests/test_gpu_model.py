@@ -187,12 +187,26 @@ def test_render_views_on_streams_matches_sequential(cuda_device, grads_exist):
          for k in range(4)]
     bg = torch.zeros(3, device=cuda_device)
     res = {}
-    for mode in ("sequential", "streams", "interleaved"):
+    for mode in ("sequential", "streams", "interleaved", "bucket"):
         sc = synthetic_scene(20_000, seed=4, device=cuda_device).requires_grad_(True)
         if grads_exist:
             for p in sc.parameters():
                 p.grad = torch.full_like(p, 0.25)
-        if mode == "sequential":
+        if mode == "bucket":
+            # the bench's step: forwards on 3 streams, then a dirty flat bucket zeroed on the default stream
+            # (only the in-kernel gradient writes wait for it), one backward; grads_exist: 0.25 added after
+            from dge_amd.multiview import GradBucket
+
+            bucket = GradBucket(sc.parameters())
+            bucket.flat.fill_(7.0)
+            outs = render_views(cams, sc, PipelineParams(), bg, streams=3)
+            bucket.zero(overlap=True)
+            torch.autograd.backward([o["render"] for o in outs], G)
+            imgs = [o["render"].detach() for o in outs]
+            if grads_exist:
+                for p in sc.parameters():
+                    p.grad += 0.25
+        elif mode == "sequential":
             imgs = []
             for c, g in zip(cams, G):
                 out = render(c, sc, PipelineParams(), bg)
@@ -207,7 +221,7 @@ def test_render_views_on_streams_matches_sequential(cuda_device, grads_exist):
             imgs = [o["render"] for o in outs]
         res[mode] = ([p.grad.clone() for p in sc.parameters()], [i.clone() for i in imgs])
     torch.cuda.synchronize()
-    for mode in ("streams", "interleaved"):
+    for mode in ("streams", "interleaved", "bucket"):
         for a, b in zip(res["sequential"][1], res[mode][1]):
             torch.testing.assert_close(a, b, rtol=0, atol=0)
         for a, b in zip(res["sequential"][0], res[mode][0]):
