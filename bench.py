@@ -63,6 +63,9 @@ def parse():
                          "backward of the summed loss -- the reference's order, DGE.py:170-239, 617-699)")
     ap.add_argument("--batch-backward", dest="batch_backward", action="store_true", help=argparse.SUPPRESS)
     ap.set_defaults(batch_backward=True)
+    ap.add_argument("--view-threads", action="store_true",
+                    help="issue each view's forward from its own host thread (dge_amd.multiview.render_views("
+                         "threads=True); measured no faster and far noisier at c2)")
     ap.add_argument("--serial-zero", action="store_true",
                     help="zero the gradient bucket before the forwards (default with streams: after enqueueing "
                          "them, only the gradient writes wait for it: GradBucket.zero(overlap=True))")
@@ -309,7 +312,7 @@ def run_views(args, cams, scene, pipe, bg, seeds, bucket):
     if not overlap:
         bucket.zero()
     if args.batch_backward:
-        outs = render_views(cams, scene, pipe, bg, streams=args.streams)
+        outs = render_views(cams, scene, pipe, bg, streams=args.streams, threads=args.view_threads)
         if overlap:
             bucket.zero(overlap=True)
         torch.autograd.backward([o["render"] for o in outs], seeds)

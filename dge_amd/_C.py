@@ -331,13 +331,25 @@ def _features(t, name):
     return t.contiguous()
 
 
-def rasterize_gaussians_fused(background, xyz, f_dc, f_rest, colors, raw_opacity, raw_scaling, raw_rotation,
-                              scale_modifier, viewmatrix, projmatrix, tan_fovx, tan_fovy, image_height, image_width,
-                              degree, campos, prefiltered, debug, index=None, visible=None):
-    """Forward on raw parameters: opacity = sigmoid, scale = exp, rotation = normalize applied in-kernel,
-    SH read from _features_dc [P,1,3] and _features_rest [P,M-1,3] without concatenation (fp32 or fp16).
-    index: optional int32 rows — render only those Gaussians (the `localize` subset), P = len(index).
-    visible: optional bool [P] output, set to radii > 0 by the preprocess kernel."""
+class Prepared:
+    """A raw-parameter forward between gs_rasterize_forward_begin and _end (see rasterize_gaussians_fused_begin):
+    the native handle, the allocator that holds its buffers, its outputs so far and every input it reads."""
+
+    def __init__(self, handle, alloc, radii, keep, H, W, P, dev):
+        self.handle, self.alloc, self.radii, self.keep = handle, alloc, radii, keep
+        self.H, self.W, self.P, self.dev = H, W, P, dev
+        # a handle that is never ended gives back its read-back slot when this object goes away
+        self._fin = weakref.finalize(self, N.lib().gs_rasterize_forward_release, handle)
+
+
+def rasterize_gaussians_fused_begin(background, xyz, f_dc, f_rest, colors, raw_opacity, raw_scaling, raw_rotation,
+                                    scale_modifier, viewmatrix, projmatrix, tan_fovx, tan_fovy, image_height,
+                                    image_width, degree, campos, prefiltered, debug, index=None, visible=None):
+    """First half of rasterize_gaussians_fused (gs_rasterize_forward_begin): enqueues the preprocess, the
+    depth sort and the instance scan on the current stream without waiting; returns a Prepared for
+    rasterize_gaussians_fused_end.  Rendering several views, begin them all first, then end each: the
+    host then waits once for the first view's instance count instead of once per view with the GPU
+    idle behind it."""
     N.require_gpu(xyz)
     dev = xyz.device
     index = _index32(index)
@@ -349,22 +361,50 @@ def rasterize_gaussians_fused(background, xyz, f_dc, f_rest, colors, raw_opacity
         colors = _f32(colors, "colors")
         raw_opacity, raw_scaling = _f32(raw_opacity, "opacity"), _f32(raw_scaling, "scaling")
         raw_rotation = _f32(raw_rotation, "rotation")
-        out_color = torch.empty((3, H, W), dtype=torch.float32, device=dev)
-        out_depth = torch.empty((1, H, W), dtype=torch.float32, device=dev)
         radii = torch.empty((P,), dtype=torch.int32, device=dev)
         g = _params(P, xyz, f_dc, f_rest, colors, raw_opacity, raw_scaling, raw_rotation, index, visible)
         s, keep = _settings(background, viewmatrix, projmatrix, campos, tan_fovx, tan_fovy, H, W, degree,
                             scale_modifier, prefiltered, debug)
+        keep += [xyz, f_dc, f_rest, colors, raw_opacity, raw_scaling, raw_rotation, index, visible]
         alloc = _Allocator(dev)
-        nr = ctypes.c_int(0)
-        rc = N.lib().gs_rasterize_forward_ex(ctypes.byref(s), ctypes.byref(g), _ptr(out_color), _ptr(out_depth),
-                                             _ptr(radii), alloc.fn, None, _stream(dev), ctypes.byref(nr))
+        h = ctypes.c_void_p(None)
+        rc = N.lib().gs_rasterize_forward_begin(ctypes.byref(s), ctypes.byref(g), _ptr(radii), alloc.fn, None,
+                                                _stream(dev), ctypes.byref(h))
         N.check(rc, "rasterize_gaussians_fused")
-        if P == 0:
+        return Prepared(h.value, alloc, radii, keep, H, W, P, dev)
+
+
+def rasterize_gaussians_fused_end(prep):
+    """Second half (gs_rasterize_forward_end) on the current stream (the begin stream or one ordered after
+    it): -> the (num_rendered, color, depth, radii, geom, binning, img) of rasterize_gaussians_fused."""
+    dev = prep.dev
+    with torch.cuda.device(dev):
+        out_color = torch.empty((3, prep.H, prep.W), dtype=torch.float32, device=dev)
+        out_depth = torch.empty((1, prep.H, prep.W), dtype=torch.float32, device=dev)
+        _TLS.alloc = prep.alloc  # the binning buffer joins the geometry/image buffers of the begin
+        nr = ctypes.c_int(0)
+        prep._fin.detach()  # _end consumes the handle, also on error
+        rc = N.lib().gs_rasterize_forward_end(prep.handle, _ptr(out_color), _ptr(out_depth), prep.alloc.fn, None,
+                                              _stream(dev), ctypes.byref(nr))
+        N.check(rc, "rasterize_gaussians_fused")
+        radii = prep.radii
+        if prep.P == 0:
             radii.zero_()
-        geom, binning, img = alloc.buffers
-        del keep
+        geom, binning, img = prep.alloc.buffers
         return nr.value, out_color, out_depth, radii, geom, binning, img
+
+
+def rasterize_gaussians_fused(background, xyz, f_dc, f_rest, colors, raw_opacity, raw_scaling, raw_rotation,
+                              scale_modifier, viewmatrix, projmatrix, tan_fovx, tan_fovy, image_height, image_width,
+                              degree, campos, prefiltered, debug, index=None, visible=None):
+    """Forward on raw parameters: opacity = sigmoid, scale = exp, rotation = normalize applied in-kernel,
+    SH read from _features_dc [P,1,3] and _features_rest [P,M-1,3] without concatenation (fp32 or fp16).
+    index: optional int32 rows — render only those Gaussians (the `localize` subset), P = len(index).
+    visible: optional bool [P] output, set to radii > 0 by the preprocess kernel."""
+    return rasterize_gaussians_fused_end(rasterize_gaussians_fused_begin(
+        background, xyz, f_dc, f_rest, colors, raw_opacity, raw_scaling, raw_rotation, scale_modifier, viewmatrix,
+        projmatrix, tan_fovx, tan_fovy, image_height, image_width, degree, campos, prefiltered, debug, index=index,
+        visible=visible))
 
 
 def rasterize_gaussians_fused_backward(background, xyz, f_dc, f_rest, colors, raw_opacity, raw_scaling, raw_rotation,

@@ -128,6 +128,11 @@ SIGNATURES = {
     "gs_rasterize_forward_ex": (ctypes.c_int, [ctypes.POINTER(GsSettings), ctypes.POINTER(GsParams), _fp, _fp, _fp,
                                                 ALLOC_FN, ctypes.c_void_p, ctypes.c_void_p,
                                                 ctypes.POINTER(ctypes.c_int)]),
+    "gs_rasterize_forward_begin": (ctypes.c_int, [ctypes.POINTER(GsSettings), ctypes.POINTER(GsParams), _fp, ALLOC_FN,
+                                                   ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p)]),
+    "gs_rasterize_forward_end": (ctypes.c_int, [ctypes.c_void_p, _fp, _fp, ALLOC_FN, ctypes.c_void_p, ctypes.c_void_p,
+                                                 ctypes.POINTER(ctypes.c_int)]),
+    "gs_rasterize_forward_release": (None, [ctypes.c_void_p]),
     "gs_rasterize_backward_ex": (ctypes.c_int, [ctypes.POINTER(GsSettings), ctypes.POINTER(GsParams), ctypes.c_int,
                                                  _fp, _fp, _fp, _fp, _fp, ctypes.POINTER(GsGrads), ctypes.c_void_p]),
     "gs_mark_visible": (ctypes.c_int, [ctypes.c_int, _fp, _fp, _fp, _fp, ctypes.c_void_p]),

@@ -21,6 +21,7 @@
 #include <string.h>
 
 #include <limits>
+#include <memory>
 #include <atomic>
 #include <mutex>
 #include <string>
@@ -93,22 +94,52 @@ int depth_pass_bits() {
     return bits;
 }
 
+// Pinned read-back slot of one forward's preprocess counters + its event.  A
+// pool per device: several forwards may be between begin and end at once
+// (gs_rasterize_forward_begin / _end), each holding its own slot.
 struct Staging {
     uint32_t* host = nullptr;
     hipEvent_t ev = nullptr;
+    int dev = 0;
 };
+struct StagingPool {
+    std::mutex mu;
+    std::unordered_map<int, std::vector<Staging*>> free;
+};
+StagingPool& staging_pool() {
+    static StagingPool p;
+    return p;
+}
 
-int staging_for_device(Staging** out) {
-    static thread_local std::unordered_map<int, Staging> map;
+int staging_acquire(Staging** out) {
     int dev = 0;
     GS_HIP(hipGetDevice(&dev));
-    Staging& s = map[dev];
-    if (!s.host) {
-        GS_HIP(hipHostMalloc((void**)&s.host, 4 * kCounterSlots * kCounterStride, hipHostMallocDefault));
-        GS_HIP(hipEventCreateWithFlags(&s.ev, hipEventDisableTiming));
+    StagingPool& p = staging_pool();
+    {
+        std::lock_guard<std::mutex> g(p.mu);
+        std::vector<Staging*>& v = p.free[dev];
+        if (!v.empty()) {
+            *out = v.back();
+            v.pop_back();
+            return GS_OK;
+        }
     }
-    *out = &s;
+    Staging* s = new Staging();
+    s->dev = dev;
+    if (hipHostMalloc((void**)&s->host, 4 * kCounterSlots * kCounterStride, hipHostMallocDefault) != hipSuccess ||
+        hipEventCreateWithFlags(&s->ev, hipEventDisableTiming) != hipSuccess) {
+        delete s;
+        return set_error(GS_ERR_HIP, "could not create the counter read-back slot");
+    }
+    *out = s;
     return GS_OK;
+}
+
+void staging_release(Staging* s) {
+    if (!s) return;
+    StagingPool& p = staging_pool();
+    std::lock_guard<std::mutex> g(p.mu);
+    p.free[s->dev].push_back(s);
 }
 
 // ---------------------------------------------------------------------
@@ -277,11 +308,27 @@ ShView sh_view(const gs_params& g) {
     return v;
 }
 
-// Everything of the forward up to (and including) tile ranges.  On success
-// *geom/*img/*bin hold the caller-owned buffers and *K the instance count.
-int bin_forward(const gs_settings* s, const Grid& g, const gs_params& gp, int* radii_out, int copy_colors,
-                gs_alloc_fn alloc, void* ctx, hipStream_t stream, void** geom_out, void** img_out, void** bin_out,
-                int* K_out) {
+// A forward between its two halves: everything enqueued up to the instance
+// count's read-back (bin_begin), the rest once the count is on the host (bin_end).
+struct FwdState {
+    gs_settings s;
+    gs_params gp;
+    Grid g;
+    int* radii = nullptr;
+    void* geom = nullptr;
+    void* img = nullptr;
+    Staging* st = nullptr;
+    PreprocessArgs pa;
+    EmitArgs ea;
+    ~FwdState() { staging_release(st); }
+};
+
+// First half of the forward: buffers, preprocess, counter read-back, depth
+// sort, instance scan (rasterizer_impl.cu:179-239 up to the num_rendered copy).
+int bin_begin(FwdState& f, int copy_colors, gs_alloc_fn alloc, void* ctx, hipStream_t stream) {
+    const gs_settings* s = &f.s;
+    const Grid& g = f.g;
+    const gs_params& gp = f.gp;
     const int P = gp.P;
     const bool debug = s->debug != 0;
     const GeomLayout gl = geom_layout(P);
@@ -289,13 +336,13 @@ int bin_forward(const gs_settings* s, const Grid& g, const gs_params& gp, int* r
     void* geom = alloc(ctx, 0, gl.total);
     void* img = alloc(ctx, 2, il.total);
     if (!geom || !img) return set_error(GS_ERR_ALLOC, "allocator returned NULL for the geometry/image buffer");
-    *geom_out = geom;
-    *img_out = img;
+    f.geom = geom;
+    f.img = img;
 
     uint32_t* counters = at<uint32_t>(img, il.counters);
     GS_HIP(hipMemsetAsync(counters, 0, il.total - il.counters, stream));  // counters, ranges, tile_last, ...
 
-    PreprocessArgs pa;
+    PreprocessArgs& pa = f.pa;
     pa.P = P; pa.D = s->sh_degree; pa.M = gp.M; pa.W = g.W; pa.H = g.H; pa.gx = g.gx; pa.gy = g.gy;
     pa.means3D = gp.means3D; pa.sh = sh_view(gp); pa.colors_precomp = gp.colors_precomp;
     pa.opacities = gp.opacities; pa.scales = gp.scales; pa.rotations = gp.rotations;
@@ -305,7 +352,7 @@ int bin_forward(const gs_settings* s, const Grid& g, const gs_params& gp, int* r
     pa.tanfovx = s->tanfovx; pa.tanfovy = s->tanfovy; pa.fx = g.fx; pa.fy = g.fy;
     pa.scale_modifier = s->scale_modifier;
     pa.prefiltered = s->prefiltered; pa.copy_colors = copy_colors;
-    pa.radii_out = radii_out;
+    pa.radii_out = f.radii;
     pa.visible_out = gp.visible_out;
     pa.radii = at<int>(geom, gl.radii);
     pa.splat = at<Splat>(geom, gl.splat);
@@ -319,11 +366,10 @@ int bin_forward(const gs_settings* s, const Grid& g, const gs_params& gp, int* r
     { StageScope sc(ST_PREPROCESS, stream); launch_preprocess(pa, stream); }
     GS_LAUNCHED("preprocess");
 
-    Staging* st = nullptr;
-    int rc = staging_for_device(&st);
+    int rc = staging_acquire(&f.st);
     if (rc) return rc;
-    GS_HIP(hipMemcpyAsync(st->host, counters, 4 * kCounterSlots * kCounterStride, hipMemcpyDeviceToHost, stream));
-    GS_HIP(hipEventRecord(st->ev, stream));
+    GS_HIP(hipMemcpyAsync(f.st->host, counters, 4 * kCounterSlots * kCounterStride, hipMemcpyDeviceToHost, stream));
+    GS_HIP(hipEventRecord(f.st->ev, stream));
 
     // depth order of the Gaussians (stable: ties keep index order)
     int cur;
@@ -335,7 +381,7 @@ int bin_forward(const gs_settings* s, const Grid& g, const gs_params& gp, int* r
     if (cur < 0) return set_error(GS_ERR_INVALID_ARG, "depth sort: bad digit layout");
     GS_LAUNCHED("depth sort");
 
-    EmitArgs ea;
+    EmitArgs& ea = f.ea;
     ea.P = P; ea.gx = g.gx; ea.gy = g.gy;
     ea.order = at<uint2>(geom, cur ? gl.val1 : gl.val0);
     ea.rect_packed = pa.rect_packed;
@@ -347,6 +393,24 @@ int bin_forward(const gs_settings* s, const Grid& g, const gs_params& gp, int* r
     ea.scan_blocks = gl.scan_blocks;
     { StageScope sc(ST_SCAN, stream); launch_scan_reduce(ea, stream); }
     GS_LAUNCHED("instance scan");
+    return GS_OK;
+}
+
+// Second half: wait for the instance count (the reference's one host sync,
+// rasterizer_impl.cu:236-239), then emission, tile sort and tile ranges.  On
+// success *bin_out holds the binning buffer and *K_out the instance count.
+int bin_end(FwdState& f, gs_alloc_fn alloc, void* ctx, hipStream_t stream, void** bin_out, int* K_out) {
+    const gs_settings* s = &f.s;
+    const Grid& g = f.g;
+    const int P = f.gp.P;
+    const bool debug = s->debug != 0;
+    const GeomLayout gl = geom_layout(P);
+    const ImgLayout il = img_layout(g.W, g.H);
+    void* geom = f.geom;
+    void* img = f.img;
+    Staging* st = f.st;
+    PreprocessArgs& pa = f.pa;
+    EmitArgs& ea = f.ea;
 
     GS_HIP(hipEventSynchronize(st->ev));
     uint64_t K64 = 0;
@@ -357,12 +421,16 @@ int bin_forward(const gs_settings* s, const Grid& g, const gs_params& gp, int* r
         kmax = c[1] > kmax ? c[1] : kmax;
         kmin_not = c[2] > kmin_not ? c[2] : kmin_not;
     }
-    if (st->host[3]) return set_error(GS_ERR_PREFILTERED, "Point is filtered although prefiltered is set. This shouldn't happen!");
+    const bool prefilter_fail = st->host[3] != 0;
+    staging_release(st);
+    f.st = nullptr;
+    if (prefilter_fail) return set_error(GS_ERR_PREFILTERED, "Point is filtered although prefiltered is set. This shouldn't happen!");
     if (K64 > (uint64_t)std::numeric_limits<int>::max()) return set_error(GS_ERR_INVALID_ARG, "too many tile instances (%llu)", (unsigned long long)K64);
     const uint32_t K = (uint32_t)K64;
     if ((K && kmax - ~kmin_not >= (1u << depth_sort_bits())) || force_depth_keys32()) {
         // the visible depth keys span more bits than the short sort covered: redo the depth order
         // on the full 32-bit keys
+        int cur;
         { StageScope sc(ST_DEPTH_SORT, stream);
         launch_depth_keys32(P, pa.rect, pa.splat, at<uint32_t>(geom, gl.key0), stream);
         cur = radix_sort_aux(at<uint32_t>(geom, gl.key0), at<uint32_t>(geom, gl.key1), at<uint2>(geom, gl.val0),
@@ -403,7 +471,27 @@ int bin_forward(const gs_settings* s, const Grid& g, const gs_params& gp, int* r
     return GS_OK;
 }
 
+// Everything of the forward up to (and including) tile ranges, in one call.
+int bin_forward(const gs_settings* s, const Grid& g, const gs_params& gp, int* radii_out, int copy_colors,
+                gs_alloc_fn alloc, void* ctx, hipStream_t stream, void** geom_out, void** img_out, void** bin_out,
+                int* K_out) {
+    FwdState f;
+    f.s = *s;
+    f.gp = gp;
+    f.g = g;
+    f.radii = radii_out;
+    int rc = bin_begin(f, copy_colors, alloc, ctx, stream);
+    *geom_out = f.geom;
+    *img_out = f.img;
+    if (rc) return rc;
+    return bin_end(f, alloc, ctx, stream, bin_out, K_out);
+}
+
 }  // namespace
+
+struct gs_forward_state {
+    FwdState f;
+};
 
 namespace gs {
 int report_error(int code, const char* msg) { return set_error(code, "%s", msg); }
@@ -528,27 +616,61 @@ int gs_rasterize_forward(const gs_settings* s, int P, int M, const float* means3
     return gs_rasterize_forward_ex(s, &g, out_color, out_depth, radii, alloc, alloc_ctx, stream, num_rendered);
 }
 
-int gs_rasterize_forward_ex(const gs_settings* s, const gs_params* gp, float* out_color, float* out_depth, int* radii,
-                            gs_alloc_fn alloc, void* alloc_ctx, gs_stream_t stream_, int* num_rendered) {
+int gs_rasterize_forward_begin(const gs_settings* s, const gs_params* gp, int* radii, gs_alloc_fn alloc,
+                               void* alloc_ctx, gs_stream_t stream_, gs_forward_state** state) {
     try {
         hipStream_t stream = (hipStream_t)stream_;
+        if (!state || !alloc) return set_error(GS_ERR_INVALID_ARG, "state and alloc are required");
+        *state = nullptr;
+        int rc = validate_params(s, gp);
+        if (rc) return rc;
+        std::unique_ptr<gs_forward_state> st(new gs_forward_state());
+        FwdState& f = st->f;
+        f.s = *s;
+        f.gp = *gp;
+        f.g = make_grid(s);
+        f.radii = radii;
+        if (gp->P == 0) {  // rasterize_points.cu:57-72: empty buffers (the outputs are zeroed by _end)
+            alloc(alloc_ctx, 0, 0);
+            alloc(alloc_ctx, 2, 0);
+        } else {
+            rc = bin_begin(f, 1, alloc, alloc_ctx, stream);
+            if (rc) return rc;
+        }
+        *state = st.release();
+        return GS_OK;
+    } catch (const std::exception& e) {
+        return set_error(GS_ERR_INVALID_ARG, "exception: %s", e.what());
+    } catch (...) {
+        return set_error(GS_ERR_INVALID_ARG, "unknown exception");
+    }
+}
+
+int gs_rasterize_forward_end(gs_forward_state* state, float* out_color, float* out_depth, gs_alloc_fn alloc,
+                             void* alloc_ctx, gs_stream_t stream_, int* num_rendered) {
+    std::unique_ptr<gs_forward_state> own(state);
+    try {
+        hipStream_t stream = (hipStream_t)stream_;
+        if (!state) return set_error(GS_ERR_INVALID_ARG, "state is NULL");
         if (!num_rendered || !alloc || !out_color || !out_depth)
             return set_error(GS_ERR_INVALID_ARG, "num_rendered, alloc, out_color and out_depth are required");
         *num_rendered = 0;
-        int rc = validate_params(s, gp);
-        if (rc) return rc;
-        const int P = gp->P;
+        FwdState& f = state->f;
+        const gs_settings* s = &f.s;
+        const int P = f.gp.P;
         const bool debug = s->debug != 0;
-        const Grid g = make_grid(s);
+        const Grid g = f.g;
         if (P == 0) {  // rasterize_points.cu:57-72: zero outputs, empty buffers, no render
-            for (int w = 0; w < 3; ++w) alloc(alloc_ctx, w, 0);
+            alloc(alloc_ctx, 1, 0);
             GS_HIP(hipMemsetAsync(out_color, 0, sizeof(float) * 3 * (size_t)g.W * g.H, stream));
             GS_HIP(hipMemsetAsync(out_depth, 0, sizeof(float) * (size_t)g.W * g.H, stream));
             return GS_OK;
         }
-        void *geom = nullptr, *img = nullptr, *bin = nullptr;
+        void* geom = f.geom;
+        void* img = f.img;
+        void* bin = nullptr;
         int K = 0;
-        rc = bin_forward(s, g, *gp, radii, 1, alloc, alloc_ctx, stream, &geom, &img, &bin, &K);
+        int rc = bin_end(f, alloc, alloc_ctx, stream, &bin, &K);
         if (rc) return rc;
         const GeomLayout gl = geom_layout(P);
         const ImgLayout il = img_layout(g.W, g.H);
@@ -582,6 +704,19 @@ int gs_rasterize_forward_ex(const gs_settings* s, const gs_params* gp, float* ou
     } catch (...) {
         return set_error(GS_ERR_INVALID_ARG, "unknown exception");
     }
+}
+
+void gs_rasterize_forward_release(gs_forward_state* state) { delete state; }
+
+int gs_rasterize_forward_ex(const gs_settings* s, const gs_params* gp, float* out_color, float* out_depth, int* radii,
+                            gs_alloc_fn alloc, void* alloc_ctx, gs_stream_t stream, int* num_rendered) {
+    if (num_rendered) *num_rendered = 0;
+    if (!num_rendered || !alloc || !out_color || !out_depth)
+        return set_error(GS_ERR_INVALID_ARG, "num_rendered, alloc, out_color and out_depth are required");
+    gs_forward_state* st = nullptr;
+    const int rc = gs_rasterize_forward_begin(s, gp, radii, alloc, alloc_ctx, stream, &st);
+    if (rc) return rc;
+    return gs_rasterize_forward_end(st, out_color, out_depth, alloc, alloc_ctx, stream, num_rendered);
 }
 
 int gs_rasterize_backward(const gs_settings* s, int P, int M, int R, const float* means3D, const float* shs,

@@ -112,14 +112,20 @@ class _RasterizeGaussiansFused(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, xyz, means2D, f_dc, f_rest, colors, raw_opacity, raw_scaling, raw_rotation, raster_settings,
-                index=None, visible=None):
+                index=None, visible=None, prepared=None):
+        # prepared: the first half of this very forward, already enqueued by rasterize_gaussians_fused_begin
+        # with these inputs (dge_amd.multiview.render_views begins every view before ending any)
         rs = raster_settings
-        args = (rs.bg, xyz, f_dc, f_rest, colors, raw_opacity, raw_scaling, raw_rotation, rs.scale_modifier,
-                rs.viewmatrix, rs.projmatrix, rs.tanfovx, rs.tanfovy, rs.image_height, rs.image_width, rs.sh_degree,
-                rs.campos, rs.prefiltered, rs.debug)
-        num_rendered, color, depth, radii, geomBuffer, binningBuffer, imgBuffer = _call_with_snapshot(
-            lambda *a: _C.rasterize_gaussians_fused(*a, index=index, visible=visible), args, rs.debug,
-            "snapshot_fw.dump", "forward")
+        if prepared is not None:
+            num_rendered, color, depth, radii, geomBuffer, binningBuffer, imgBuffer = \
+                _C.rasterize_gaussians_fused_end(prepared)
+        else:
+            args = (rs.bg, xyz, f_dc, f_rest, colors, raw_opacity, raw_scaling, raw_rotation, rs.scale_modifier,
+                    rs.viewmatrix, rs.projmatrix, rs.tanfovx, rs.tanfovy, rs.image_height, rs.image_width,
+                    rs.sh_degree, rs.campos, rs.prefiltered, rs.debug)
+            num_rendered, color, depth, radii, geomBuffer, binningBuffer, imgBuffer = _call_with_snapshot(
+                lambda *a: _C.rasterize_gaussians_fused(*a, index=index, visible=visible), args, rs.debug,
+                "snapshot_fw.dump", "forward")
         ctx.raster_settings = rs
         ctx.index = index
         ctx.num_rendered = num_rendered
@@ -132,7 +138,7 @@ class _RasterizeGaussiansFused(torch.autograd.Function):
     @staticmethod
     def backward(ctx, grad_out_color, grad_radii, grad_depth):
         if grad_out_color is None:
-            return (None,) * 11
+            return (None,) * 12
         rs = ctx.raster_settings
         (xyz, f_dc, f_rest, colors, raw_opacity, raw_scaling, raw_rotation, radii, geomBuffer, binningBuffer,
          imgBuffer) = ctx.saved_tensors
@@ -209,7 +215,7 @@ class _RasterizeGaussiansFused(torch.autograd.Function):
             d_rot = None
         if "sh" in into:
             d_dc = d_rest = None
-        return d_xyz, d_m2, d_dc, d_rest, d_col, d_op, d_sc, d_rot, None, None, None
+        return d_xyz, d_m2, d_dc, d_rest, d_col, d_op, d_sc, d_rot, None, None, None, None
 
 
 _FUSED_GRAD_ACCUM = os.environ.get("DGE_AMD_FUSED_GRAD_ACCUM", "1") != "0"
@@ -311,16 +317,17 @@ def _into_target(p, mode, direct, zero=False):
 
 
 def rasterize_gaussian_model(xyz, means2D, features_dc, features_rest, colors_precomp, raw_opacity, raw_scaling,
-                             raw_rotation, raster_settings, index=None, visible=None):
+                             raw_rotation, raster_settings, index=None, visible=None, prepared=None):
     """(color, radii, depth) of a GaussianModel given its raw tensors (_xyz, _features_dc, _features_rest or
     colors_precomp, _opacity, _scaling, _rotation); activations are applied in-kernel.  `index` (int32,
     ascending): render only those rows — the model's `localize` subset pc[mask] — gathering them
-    in-kernel; the gradients land in the full-size tensors' rows (means2D/radii are per subset entry)."""
+    in-kernel; the gradients land in the full-size tensors' rows (means2D/radii are per subset entry).
+    prepared: this forward's first half from _C.rasterize_gaussians_fused_begin (same inputs)."""
     empty = torch.empty(0, dtype=torch.float32, device=xyz.device)
     return _RasterizeGaussiansFused.apply(
         xyz, means2D, empty if features_dc is None else features_dc, empty if features_rest is None else features_rest,
         empty if colors_precomp is None else colors_precomp, raw_opacity, raw_scaling, raw_rotation, raster_settings,
-        index, visible)
+        index, visible, prepared)
 
 
 class GaussianRasterizationSettings(NamedTuple):

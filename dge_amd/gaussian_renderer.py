@@ -156,23 +156,47 @@ def _render_fused(viewpoint_camera, pc, pipe, bg_color, scaling_modifier=1.0, ov
     """render() for a standard GaussianModel without the getters' torch kernels:
     the rasterizer consumes _xyz, _features_dc, _features_rest, _opacity,
     _scaling, _rotation directly and returns their gradients."""
+    return _fused_end(_fused_begin(viewpoint_camera, pc, pipe, bg_color, scaling_modifier, override_color), pc)
+
+
+def _fused_begin(viewpoint_camera, pc, pipe, bg_color, scaling_modifier=1.0, override_color=None):
+    """The first half of _render_fused: settings, the visibility output and the native forward's first half
+    (preprocess, depth sort, instance scan) enqueued on the current stream without a host wait."""
+    from . import _C
+
     xyz = pc._xyz
     index = _mask_rows(pc.mask) if getattr(pc, "localize", False) else None
     n = index.numel() if index is not None else xyz.shape[0]
-    screenspace_points = _viewspace_zeros(n, xyz.dtype, xyz.device)
     rs = _settings(viewpoint_camera, bg_color, scaling_modifier, pc.active_sh_degree, getattr(pipe, "debug", False))
     if override_color is None:
         f_dc, f_rest, colors = pc._features_dc, pc._features_rest, None
     else:
         f_dc, f_rest, colors = None, None, override_color.float()
     visible = torch.empty(n, dtype=torch.bool, device=xyz.device)  # radii > 0, written by the preprocess
-    rendered_image, radii, depth = rasterize_gaussian_model(xyz, screenspace_points, f_dc, f_rest, colors,
-                                                            pc._opacity, pc._scaling, pc._rotation, rs, index,
-                                                            visible)
+    st = {"rs": rs, "index": index, "n": n, "f_dc": f_dc, "f_rest": f_rest, "colors": colors, "visible": visible,
+          "prepared": None}
+    if rs.debug:  # debug mode: the one-call forward, which keeps the reference's failure snapshot
+        return st
+    empty = torch.empty(0, dtype=torch.float32, device=xyz.device)
+    st["prepared"] = _C.rasterize_gaussians_fused_begin(
+        rs.bg, xyz, empty if f_dc is None else f_dc, empty if f_rest is None else f_rest,
+        empty if colors is None else colors, pc._opacity, pc._scaling, pc._rotation, rs.scale_modifier,
+        rs.viewmatrix, rs.projmatrix, rs.tanfovx, rs.tanfovy, rs.image_height, rs.image_width, rs.sh_degree,
+        rs.campos, rs.prefiltered, rs.debug, index=index, visible=visible)
+    return st
+
+
+def _fused_end(st, pc):
+    """The second half: the autograd node over the native forward's second half; render()'s dict."""
+    xyz = pc._xyz
+    screenspace_points = _viewspace_zeros(st["n"], xyz.dtype, xyz.device)
+    rendered_image, radii, depth = rasterize_gaussian_model(
+        xyz, screenspace_points, st["f_dc"], st["f_rest"], st["colors"], pc._opacity, pc._scaling, pc._rotation,
+        st["rs"], st["index"], st["visible"], prepared=st["prepared"])
     return {
         "render": rendered_image,
         "viewspace_points": screenspace_points,
-        "visibility_filter": visible,
+        "visibility_filter": st["visible"],
         "radii": radii,
         "depth_3dgs": depth,
     }

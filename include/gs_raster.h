@@ -185,6 +185,26 @@ typedef struct gs_grads {         /* backward outputs, every element written */
 int gs_rasterize_forward_ex(const gs_settings *s, const gs_params *g, float *out_color, float *out_depth,
                             int *radii, gs_alloc_fn alloc, void *alloc_ctx, gs_stream_t stream,
                             int *num_rendered);
+/* gs_rasterize_forward_ex in two halves, so a caller rendering several views
+ * can enqueue every view's first half before it waits for any instance count
+ * (the reference's one host sync per forward, rasterizer_impl.cu:236-239:
+ * num_rendered sizes the binning buffer).
+ *   _begin: allocates the geometry/image buffers (alloc which = 0, 2) and
+ *           enqueues the preprocess, the counter read-back, the depth sort and
+ *           the instance scan; *state receives an opaque handle.  Does not wait.
+ *   _end:   waits for that view's instance count, allocates the binning buffer
+ *           (which = 1), enqueues the rest and writes out_color/out_depth;
+ *           always consumes the handle (also on error).  `stream` must be the
+ *           begin stream or one ordered after it.
+ *   _release: drops a handle that will not be ended.
+ * The inputs named by s and g must stay valid and unmodified until _end. */
+typedef struct gs_forward_state gs_forward_state;
+int gs_rasterize_forward_begin(const gs_settings *s, const gs_params *g, int *radii, gs_alloc_fn alloc,
+                               void *alloc_ctx, gs_stream_t stream, gs_forward_state **state);
+int gs_rasterize_forward_end(gs_forward_state *state, float *out_color, float *out_depth, gs_alloc_fn alloc,
+                             void *alloc_ctx, gs_stream_t stream, int *num_rendered);
+void gs_rasterize_forward_release(gs_forward_state *state);
+
 int gs_rasterize_backward_ex(const gs_settings *s, const gs_params *g, int R, const int *radii,
                              const void *geom_buffer, const void *binning_buffer, const void *img_buffer,
                              const float *dL_dpix, const gs_grads *out, gs_stream_t stream);

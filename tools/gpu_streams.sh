@@ -6,7 +6,7 @@ cd "$GRAFT_REPO_ROOT" 2>/dev/null || cd /root/repo
 mkdir -p gpurun_out
 : > gpurun_out/streams.log
 run() {
-    timeout -k 10 240 python bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-side-legs --no-profile "$@" \
+    timeout -k 10 240 python bench.py --steps ${STEPS:-60} --warmup 5 --no-cpu-baseline --no-side-legs --no-profile "$@" \
         > gpurun_out/streams_one.json 2> gpurun_out/streams_one.err || { echo "bench $* failed"; tail -20 gpurun_out/streams_one.err; exit 1; }
     python - "$*" <<'PY' >> gpurun_out/streams.log
 import json, sys
@@ -14,10 +14,9 @@ d = json.loads(open("gpurun_out/streams_one.json").read().strip().splitlines()[-
 print(f"{sys.argv[1] or 'default':40s} {d['value']:9.1f} renders/s  {d['ms_per_step']:.4f} ms/step")
 PY
 }
+for rep in 1 2; do
 run ${EXTRA_ARGS:-}
 run --serial-zero ${EXTRA_ARGS:-}
 run --streams 1 --per-view-backward --serial-zero ${EXTRA_ARGS:-}
-run --streams 2 ${EXTRA_ARGS:-}
-run --streams 1 ${EXTRA_ARGS:-}
-run ${EXTRA_ARGS:-}
+done
 cat gpurun_out/streams.log
