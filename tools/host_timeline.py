@@ -55,6 +55,10 @@ def _wrap(mod, name, tag):
 
 
 _wrap(_C, "rasterize_gaussians_fused", "C fwd")
+_wrap(_C, "rasterize_gaussians_fused_begin", "C begin")
+_wrap(_C, "rasterize_gaussians_fused_end", "C end")
+_wrap(GR, "_fused_begin", "py begin")
+_wrap(GR, "_fused_end", "py end")
 _wrap(_C, "rasterize_gaussians_fused_backward", "C bwd")
 _bw = DR._RasterizeGaussiansFused.backward
 
@@ -73,7 +77,7 @@ def step():
     t0 = time.perf_counter()
     outs = render_views(cams, scene, pipe, bg, streams=streams)
     t1 = time.perf_counter()
-    bucket.zero(overlap=streams > 1)
+    bucket.zero(overlap=streams > 1 and not os.environ.get("SERIAL_ZERO"))
     t2 = time.perf_counter()
     torch.autograd.backward([o["render"] for o in outs], seeds)
     t3 = time.perf_counter()
@@ -95,8 +99,11 @@ torch.cuda.synchronize()
 tw = time.perf_counter() - t0
 print(f"streams {streams}: host loop {1e3 * th / n:.3f} ms/step, wall {1e3 * tw / n:.3f} ms/step "
       f"({n * V / tw:.0f} renders/s)")
-for name in ("render", "C fwd", "views", "zero", "backward", "py bwd", "C bwd"):
+for name in ("render", "C fwd", "py begin", "C begin", "py end", "C end", "views", "zero", "backward", "py bwd",
+             "C bwd"):
     v = [d for k, d in stamps if k == name]
+    if not v:
+        continue
     print(f"  {name:9s} median {1e6 * statistics.median(v):8.1f} us  p90 {1e6 * sorted(v)[int(0.9 * len(v))]:8.1f} us"
           f"  x{len(v) / n:.0f}/step")
 
