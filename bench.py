@@ -141,6 +141,11 @@ def main():
         if distributed:
             bucket.allreduce(min_world=1 if rehearse else 2)
 
+    def step_one_stream():
+        # the kernels in isolation (one stream, nothing concurrent): what the per-stage and roofline
+        # durations are taken from -- on several streams an event pair also times the other streams' work
+        run_views(args, cams, scene, pipe, bg, seeds, bucket, streams=1)
+
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -175,8 +180,7 @@ def main():
             lives.append({"live": int(lv.sum().item()), "flag_words": int(tt[lv].sum().item()), "records": recs})
     torch.cuda.synchronize()
 
-    # stage calibration (untimed): every stage bracketed by events, for the per-stage times of the line;
-    # the timed region then brackets only the two blend kernels (two events per launch each)
+    # stage calibration (untimed, one stream): every stage bracketed by events, for the per-stage times
     calib = {}
     blend = ["render_fwd", "render_bwd"]
     if not args.no_profile:
@@ -184,11 +188,10 @@ def main():
         _native.profile_enable(True)
         _native.profile_collect()  # reset
         for _ in range(2):
-            step()
+            step_one_stream()
         torch.cuda.synchronize()
         calib = {n: (ms, c) for n, (ms, c) in _native.profile_collect().items() if c}
-        _native.profile_stages(blend)
-        _native.profile_collect()
+        _native.profile_enable(False)
     if distributed:
         dist.barrier()
     torch.cuda.synchronize()
@@ -199,8 +202,20 @@ def main():
     if distributed:
         dist.barrier()
     dt = time.perf_counter() - t0
-    prof = {}
+    # roofline leg (timed, one stream): the two blend kernels bracketed by HIP events on their launch
+    # stream, live, over iso_steps steps of the same workload with the views on one stream
+    prof, iso = {}, None
     if not args.no_profile:
+        iso_steps = max(5, min(args.steps, 20))
+        _native.profile_stages(blend)
+        _native.profile_enable(True)
+        _native.profile_collect()
+        torch.cuda.synchronize()
+        ti = time.perf_counter()
+        for _ in range(iso_steps):
+            step_one_stream()
+        torch.cuda.synchronize()
+        iso = {"steps": iso_steps, "renders_per_s": round(iso_steps * V / (time.perf_counter() - ti), 3)}
         prof = _native.profile_collect()
         _native.profile_enable(False)
         _native.profile_stages(None)
@@ -228,7 +243,7 @@ def main():
             pmc = json.load(open(pmc_path))
         except Exception:
             pmc = {}
-    for name in blend:  # both blend kernels, timed live inside the timed region
+    for name in blend:  # both blend kernels, timed live in the one-stream roofline leg
         ms, cnt = prof.get(name, (0.0, 0))
         if not cnt:
             continue
@@ -293,6 +308,8 @@ def main():
             "stages_ms": {k: round(v, 4) for k, v in stages.items()},
             "roofline": roofline,
             "rooflines": rooflines,
+            # the leg the rooflines and stages_ms come from: the same step with the views on one stream
+            "roofline_leg": iso,
             "legs": legs,
             "cpu_baseline": cpu,
         }
@@ -301,23 +318,24 @@ def main():
         dist.destroy_process_group()
 
 
-def run_views(args, cams, scene, pipe, bg, seeds, bucket):
+def run_views(args, cams, scene, pipe, bg, seeds, bucket, streams=None):
     """One step's renders: zero the bucket, forward every view, backward (see the module docstring)."""
     from dge_amd.multiview import render_backward_views, render_views
 
+    streams = args.streams if streams is None else streams
     # the overlapped zero (fused path only: its gradient writes wait for the fill in-kernel) is issued after
     # the forwards are enqueued on the side streams, so they do not queue behind the 236-MB fill
-    overlap = (not args.serial_zero and args.batch_backward and args.streams > 1
+    overlap = (not args.serial_zero and args.batch_backward and streams > 1
                and os.environ.get("DGE_AMD_FUSED", "1") != "0")
     if not overlap:
         bucket.zero()
     if args.batch_backward:
-        outs = render_views(cams, scene, pipe, bg, streams=args.streams, threads=args.view_threads)
+        outs = render_views(cams, scene, pipe, bg, streams=streams, threads=args.view_threads)
         if overlap:
             bucket.zero(overlap=True)
         torch.autograd.backward([o["render"] for o in outs], seeds)
     else:
-        render_backward_views(cams, scene, pipe, bg, seeds, streams=args.streams)
+        render_backward_views(cams, scene, pipe, bg, seeds, streams=streams)
 
 
 def _time(fn, steps):
@@ -370,7 +388,7 @@ def side_legs(args, scene, cams, seeds, bg, pipe, bucket, step, dev):
     _native.profile_stages(None)
     _native.profile_enable(True)
     _native.profile_collect()
-    hstep()
+    run_views(args, cams, hl, pipe, bg, seeds, hb, streams=1)  # (stage times in isolation: one stream)
     torch.cuda.synchronize()
     st = {n: round(ms / c, 4) for n, (ms, c) in _native.profile_collect().items() if c}
     _native.profile_enable(False)
