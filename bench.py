@@ -66,6 +66,9 @@ def parse():
     ap.add_argument("--view-threads", action="store_true",
                     help="issue each view's forward from its own host thread (dge_amd.multiview.render_views("
                          "threads=True); measured no faster and far noisier at c2)")
+    ap.add_argument("--scan-live", action="store_true",
+                    help="N > 1: find the all-reduce's live rows by reading the gradient bucket after the backward "
+                         "(GradBucket.allreduce) instead of agreeing on the forwards' blended Gaussians before it")
     ap.add_argument("--serial-zero", action="store_true",
                     help="zero the gradient bucket before the forwards (default with streams: after enqueueing "
                          "them, only the gradient writes wait for it: GradBucket.zero(overlap=True))")
@@ -136,10 +139,15 @@ def main():
     pipe = PipelineParams()
     bucket = GradBucket(scene.parameters())
 
+    min_world = 1 if rehearse else 2
+
     def step():
-        run_views(args, cams, scene, pipe, bg, seeds, bucket)
+        run_views(args, cams, scene, pipe, bg, seeds, bucket, min_world=min_world if distributed else None)
         if distributed:
-            bucket.allreduce(min_world=1 if rehearse else 2)
+            if args.batch_backward and not args.scan_live:
+                bucket.allreduce_end()
+            else:
+                bucket.allreduce(min_world=min_world)
 
     def step_one_stream():
         # the kernels in isolation (one stream, nothing concurrent): what the per-stage and roofline
@@ -318,8 +326,10 @@ def main():
         dist.destroy_process_group()
 
 
-def run_views(args, cams, scene, pipe, bg, seeds, bucket, streams=None):
-    """One step's renders: zero the bucket, forward every view, backward (see the module docstring)."""
+def run_views(args, cams, scene, pipe, bg, seeds, bucket, streams=None, min_world=None):
+    """One step's renders: zero the bucket, forward every view, backward (see the module docstring).
+    min_world (distributed steps): the sparse all-reduce's union of live rows is agreed on between the
+    forwards and the backward (GradBucket.allreduce_begin; the caller runs allreduce_end)."""
     from dge_amd.multiview import render_backward_views, render_views
 
     streams = args.streams if streams is None else streams
@@ -333,6 +343,8 @@ def run_views(args, cams, scene, pipe, bg, seeds, bucket, streams=None):
         outs = render_views(cams, scene, pipe, bg, streams=streams, threads=args.view_threads)
         if overlap:
             bucket.zero(overlap=True)
+        if min_world is not None and not args.scan_live:
+            bucket.allreduce_begin([o.get("_live_rows") for o in outs], min_world=min_world)
         torch.autograd.backward([o["render"] for o in outs], seeds)
     else:
         render_backward_views(cams, scene, pipe, bg, seeds, streams=streams)

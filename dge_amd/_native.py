@@ -158,6 +158,8 @@ SIGNATURES = {
                                       ctypes.c_void_p, ctypes.c_void_p]),
     "gs_rows_scatter": (ctypes.c_int, [ctypes.POINTER(RowsRegion), ctypes.c_int, ctypes.c_void_p, ctypes.c_longlong,
                                        ctypes.c_void_p, ctypes.c_void_p]),
+    "gs_rows_compact": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_longlong, ctypes.c_void_p, ctypes.c_void_p,
+                                       ctypes.c_void_p]),
     "gs_blend_exp": (ctypes.c_int, [ctypes.c_longlong, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "gs_last_error": (ctypes.c_char_p, []),
     "gs_abi_version": (ctypes.c_int, []),

@@ -694,6 +694,7 @@ int gs_rasterize_forward_end(gs_forward_state* state, float* out_color, float* o
         ra.used = at<uint64_t>(bin, bl.used);
         ra.out_color = out_color;
         ra.out_depth = out_depth;
+        ra.touched = at<uint8_t>(geom, gl.touched);
         ra.diag = diag_buffer(0, kDiagWords * (size_t)g.tiles * 4);
         { StageScope sc(ST_RENDER_FWD, stream); launch_render_forward(ra, stream); }
         GS_LAUNCHED("render");

@@ -228,7 +228,7 @@ struct PreprocessArgs {
     uint32_t* rect;          // pack_rect(tile rect) when the grid allows it, else tiles_touched
     int rect_packed;
     uint32_t* counters;  // kCounterSlots x kCounterStride (ImgLayout)
-    uint8_t* touched;    // zeroed here: k_render_bwd sets the bytes of Gaussians that get a record
+    uint8_t* touched;    // zeroed here: k_render_fwd sets the bytes of Gaussians some pixel blends
 };
 void launch_preprocess(const PreprocessArgs& a, hipStream_t s);
 void launch_depth_keys32(int P, const uint32_t* rect, const Splat* splat, uint32_t* key, hipStream_t s);
@@ -304,6 +304,8 @@ struct RenderArgs {
     uint32_t item_cap;
     float* out_color;
     float* out_depth;
+    uint8_t* touched;     // [P] set to 1 for every Gaussian some pixel blends (zeroed by the preprocess):
+                          // exactly the Gaussians the backward gives a record, known after the forward
     uint64_t* diag;       // optional [tiles*4][kDiagWords] (see diag_buffer)
 };
 void launch_render_forward(const RenderArgs& a, hipStream_t s);
@@ -337,7 +339,7 @@ struct RenderBwdArgs {
     const float* dL_dpix;
     float4* records;     // [4*K][3] float4: one record per (slot, quadrant), kept entries only
     uint8_t* rec_flags;  // [4*K] set to 1 with each record (zeroed before the launch)
-    uint8_t* touched;    // [P] set to 1 for every Gaussian that got a record (zeroed before the launch)
+    uint8_t* touched;    // [P] set to 1 for every Gaussian that got a record, or NULL: the forward set them
     uint64_t* diag;   // optional [item_cap][kDiagWords], by queue position (see diag_buffer)
 };
 void launch_render_backward(const RenderBwdArgs& a, hipStream_t s);

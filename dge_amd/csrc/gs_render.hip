@@ -229,6 +229,7 @@ __global__ __launch_bounds__(64, 3) void k_render_fwd(RenderArgs a) {
     __shared__ float4 s_rgbd[kRound + kGroup];
     __shared__ __attribute__((aligned(16))) uint32_t s_pos[kRound + kGroup];
     __shared__ uint32_t s_gused[kRound / kGroup + 1];  // per blend group: bit u = entry u was blended
+    __shared__ uint32_t s_id[kRound];                  // the kept entries' Gaussians (the touched bytes)
 
     const uint2 range = a.ranges[tile];
     uint64_t* used = a.used + (size_t)used_base(range.x, tile) * 4 + quad;
@@ -259,11 +260,14 @@ __global__ __launch_bounds__(64, 3) void k_render_fwd(RenderArgs a) {
             ids[i] = list_empty ? 0u : a.point_pairs[k < range.y ? k : k_last].x;
         }
     };
-    uint32_t ids[4];
+    uint32_t ids[4], cid[4];  // cid: the ids of the entries in `cur` (the touched bytes at the round's end)
     Entry cur[4];
     load_ids(range.x, ids);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) cur[i] = gather_entry(a.splat, ids[i]);
+    for (int i = 0; i < 4; ++i) {
+        cur[i] = gather_entry(a.splat, ids[i]);
+        cid[i] = ids[i];
+    }
     load_ids(range.x + kRound, ids);
 
     // checkpoint of segment k of this quadrant: slot ckpt_base + k, quadrant `quad`
@@ -301,6 +305,7 @@ __global__ __launch_bounds__(64, 3) void k_render_fwd(RenderArgs a) {
                 s_op[slot] = cur[i].co.w;
                 s_rgbd[slot] = cur[i].f;
                 s_pos[slot] = k - range.x + 1;  // 1-based contributor index (forward.cu:331)
+                s_id[slot] = cid[i];
             }
             nk += __popcll(km);
         }
@@ -320,7 +325,10 @@ __global__ __launch_bounds__(64, 3) void k_render_fwd(RenderArgs a) {
         if (a.diag) c_cull += __builtin_amdgcn_s_memtime() - r0;
         // next round's gathers and the round after's ids, in flight during the blend
 #pragma unroll
-        for (int i = 0; i < 4; ++i) cur[i] = gather_entry(a.splat, ids[i]);
+        for (int i = 0; i < 4; ++i) {
+            cur[i] = gather_entry(a.splat, ids[i]);
+            cid[i] = ids[i];
+        }
         load_ids(b + 2 * kRound, ids);
         if (seg_done >= 0) {  // the previous segment's (T after it, own colour sum): the replay's start
             ckpt[(size_t)seg_done * 256 + lane] = make_float4(fabsf(Ts), L01.x, L01.y, L2);
@@ -402,8 +410,10 @@ __global__ __launch_bounds__(64, 3) void k_render_fwd(RenderArgs a) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int sl = kslot[i];
-            const uint64_t wd = __ballot(sl >= 0 && ((s_gused[sl / kGroup] >> (sl % kGroup)) & 1u));
+            const bool blended = sl >= 0 && ((s_gused[sl / kGroup] >> (sl % kGroup)) & 1u);
+            const uint64_t wd = __ballot(blended);
             pend_word = lane == i ? wd : pend_word;
+            if (blended) a.touched[s_id[sl]] = 1;  // (same-value byte stores: no atomics needed)
         }
         pend_rel = (int)(b - range.x);
     }
@@ -1200,7 +1210,7 @@ __global__ __launch_bounds__(64, 4) void k_render_bwd(RenderBwdArgs a) {
                 finish_record(make_float4(s_cx[kw], -s_cy[kw], s_cz[kw], s_op[kw]), S, ddelx_dx, ddely_dy,
                               a.records + 3 * rec);
                 a.rec_flags[rec] = 1;
-                a.touched[pr.x] = 1;
+                if (a.touched) a.touched[pr.x] = 1;
             }
         }
         if (a.diag) c_replay += __builtin_amdgcn_s_memtime() - c0;
@@ -1223,7 +1233,9 @@ void launch_render_backward(const RenderBwdArgs& a, hipStream_t s) {
     const int tiles = a.gx * a.gy;
     if (tiles <= 0) return;
     const unsigned grid = a.item_cap;
-    hipLaunchKernelGGL(k_render_bwd, dim3(grid), dim3(64), 0, s, a);
+    RenderBwdArgs b = a;
+    if (fwd_variant() == 0) b.touched = nullptr;  // k_render_fwd set them (the pipelined variant does not)
+    hipLaunchKernelGGL(k_render_bwd, dim3(grid), dim3(64), 0, s, b);
 }
 
 }  // namespace gs

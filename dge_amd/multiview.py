@@ -81,6 +81,70 @@ class GradBucket:
         if ev is not None:
             torch.cuda.current_stream(self.flat.device).wait_event(ev)
 
+    def allreduce_begin(self, live_hint, group=None, min_world: int = 2):
+        """First half of a sparse allreduce() whose union of live rows is agreed on BEFORE the backward runs,
+        so the one host wait of the protocol (the union's size, which shapes the packed collective) waits
+        for the forwards, not for the backward: call it after the views' forwards are enqueued and before
+        backward(); allreduce_end() after the backward.
+
+        live_hint: uint8 [rows] tensors, one per view rendered this step — render_views()' "_live_rows",
+        the Gaussians some pixel of the view blends (set by the forward kernel), which are exactly the ones
+        the backward gives a nonzero gradient row.  Valid only when the bucket was zeroed this step and
+        these views' fused backward is the only writer of the gradients (the multi-view step); otherwise
+        use allreduce(), which finds the nonzero rows by reading the bucket."""
+        self._pending = None
+        if not dist.is_available() or not dist.is_initialized() or dist.get_world_size(group) < min_world:
+            return
+        rows = {v.shape[0] if v.dim() else -1 for v in self.views}
+        n = next(iter(rows))
+        mats = [v.reshape(n, -1) for v in self.views] if len(rows) == 1 and n >= 0 else None
+        hints = list(live_hint or [])
+        if (mats is None or not hints or not _native_ok(mats)
+                or any(h is None or h.dtype != torch.uint8 or h.shape != (n,) for h in hints)):
+            self._pending = ("scan", group)  # no usable hint: allreduce() in allreduce_end
+            return
+        live = hints[0].clone()
+        for h in hints[1:]:
+            live |= h
+        dist.all_reduce(live, op=dist.ReduceOp.MAX, group=group)
+        from . import _native as N
+
+        dev = self.flat.device
+        idx = torch.empty(n, dtype=torch.int64, device=dev)
+        cs = torch.empty(1 + (n + 1023) // 1024, dtype=torch.int64, device=dev)
+        stream = torch.cuda.current_stream(dev)
+        N.check(N.lib().gs_rows_compact(live.data_ptr(), n, idx.data_ptr(), cs.data_ptr(),
+                                        ctypes.c_void_p(stream.cuda_stream)), "gs_rows_compact")
+        pinned = getattr(self, "_count_host", None)
+        if pinned is None:
+            pinned = self._count_host = torch.empty(1, dtype=torch.int64, pin_memory=True)
+        pinned.copy_(cs[:1], non_blocking=True)
+        self._pending = ("hint", group, idx, pinned, stream.record_event(), n, mats)
+
+    def allreduce_end(self):
+        """Second half of allreduce_begin (after the backward): the packed SUM of the agreed rows."""
+        pend, self._pending = getattr(self, "_pending", None), None
+        if pend is None:
+            return None
+        if pend[0] == "scan":
+            return self.allreduce(pend[1], min_world=1)
+        _, group, idx, pinned, ev, n, mats = pend
+        ev.synchronize()  # the forwards' union is agreed: no wait for the backward
+        m = int(pinned.item())
+        self.wait_zero()
+        if not self.check_attached():
+            for p, v in zip(self.params, self.views):
+                if p.grad is not None and p.grad.data_ptr() != v.data_ptr():
+                    v.copy_(p.grad)
+            self.attach()
+        if 2 * m > n:  # mostly dense: packing would not pay
+            return dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=group)
+        rows = idx[:m]
+        packed = _rows_gather(mats, rows)
+        dist.all_reduce(packed, op=dist.ReduceOp.SUM, group=group)
+        _rows_scatter(mats, rows, packed)
+        return None
+
     def check_attached(self) -> bool:
         return all(p.grad is not None and p.grad.data_ptr() == v.data_ptr() for p, v in zip(self.params, self.views))
 
@@ -211,6 +275,15 @@ def _render_on(stream, ready, grad_enabled, render, cam, pc, pipe, bg_color, kw)
         return render(cam, pc, pipe, bg_color, **kw)
 
 
+def _touched_rows(prep):
+    """uint8 [P] view of a finished forward's `touched` bytes (the Gaussians some pixel blended)."""
+    from . import _native as N
+
+    geom = prep.alloc.buffers[0]
+    off = N.lib().gs_buffer_offset(b"geometry", b"touched", prep.P, prep.W, prep.H, 0)
+    return geom[off:off + prep.P]
+
+
 def render_views(cameras, pc, pipe, bg_color, streams: int = 2, threads: bool = False, **kw):
     """render() of every camera, the views spread round-robin over `streams` HIP streams.
 
@@ -264,6 +337,8 @@ def render_views(cameras, pc, pipe, bg_color, streams: int = 2, threads: bool = 
             s.wait_event(ready)
         with torch.cuda.stream(s):
             out = render(cam, pc, pipe, bg_color, **kw) if begun is None else _fused_end(begun[i], pc)
+            if begun is not None and begun[i]["index"] is None and begun[i]["prepared"] is not None:
+                out["_live_rows"] = _touched_rows(begun[i]["prepared"])
         for v in out.values():
             if isinstance(v, torch.Tensor) and v.is_cuda:
                 v.record_stream(main)

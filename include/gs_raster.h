@@ -263,6 +263,11 @@ int gs_rows_gather(const gs_rows_region *regions, int nreg, const long long *row
 /* the inverse: row rows[i] of every region = its columns of packed[i, :]. */
 int gs_rows_scatter(const gs_rows_region *regions, int nreg, const long long *rows, long long m,
                     const float *packed, gs_stream_t stream);
+/* rows[0..count) = the ascending indices r < n with live[r] != 0, count_scratch[0] = count (int64),
+ * with no host round trip (the sparse all-reduce's union of live rows, agreed on before the backward
+ * runs: dge_amd/multiview.py GradBucket.allreduce_begin).  count_scratch holds 1 + ceil(n / 1024)
+ * int64 (the rest is scratch); rows holds up to n. */
+int gs_rows_compact(const uint8_t *live, long long n, long long *rows, long long *count_scratch, gs_stream_t stream);
 
 /* Byte sizes of the opaque buffers (host arithmetic, no device work). */
 size_t gs_geometry_buffer_size(int P);

@@ -59,3 +59,65 @@ def test_rows_live_gather_scatter_match_torch(cuda_device, n, widths, density):
         exp = torch.zeros(n, m.shape[1])
         exp[idx.cpu()] = m.cpu()[idx.cpu()] * 2
         assert torch.equal(m2.cpu().nan_to_num(7.0), exp.nan_to_num(7.0))
+
+
+@pytest.mark.parametrize("n,density", [(1_000_003, 0.1), (1, 1.0), (2047, 0.0), (4096, 1.0), (70_000, 0.5)])
+def test_rows_compact_matches_nonzero(cuda_device, n, density):
+    """gs_rows_compact: the ascending live rows and their count, no host round trip (vs torch.nonzero)."""
+    from dge_amd import _native as N
+
+    g = torch.Generator(device="cpu").manual_seed(n)
+    live = ((torch.rand(n, generator=g) < density).to(torch.uint8) * torch.randint(1, 255, (n,), generator=g,
+                                                                                     dtype=torch.uint8)).cuda()
+    rows = torch.full((n,), -7, dtype=torch.int64, device="cuda")
+    cs = torch.empty(1 + (n + 1023) // 1024, dtype=torch.int64, device="cuda")
+    N.check(N.lib().gs_rows_compact(live.data_ptr(), n, rows.data_ptr(), cs.data_ptr(),
+                                    torch.cuda.current_stream().cuda_stream), "gs_rows_compact")
+    ref = torch.nonzero(live).squeeze(1)
+    m = int(cs[0].item())
+    assert m == ref.numel()
+    assert torch.equal(rows[:m], ref)
+
+
+def test_allreduce_begin_end_one_rank(cuda_device):
+    """The hinted protocol on a one-rank RCCL group (the bench's multi-GPU step): the forwards' blended
+    Gaussians cover every nonzero gradient row, and the packed SUM leaves the bucket unchanged (one rank);
+    the union it agreed on equals the rows the bucket scan finds nonzero."""
+    import os
+
+    import torch.distributed as dist
+
+    from dge_amd.cameras import orbit_camera
+    from dge_amd.gaussian_renderer import PipelineParams
+    from dge_amd.scene import synthetic_scene
+
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29531")
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=cuda_device)
+    try:
+        sc = synthetic_scene(50_000, seed=9, device=cuda_device).requires_grad_(True)
+        cams = [orbit_camera(k, 3, 192, 160, device=cuda_device) for k in range(3)]
+        G = [torch.randn(3, 160, 192, generator=torch.Generator().manual_seed(k)).to(cuda_device) for k in range(3)]
+        bucket = mv.GradBucket(sc.parameters())
+        bucket.flat.fill_(3.0)
+        outs = mv.render_views(cams, sc, PipelineParams(), torch.zeros(3, device=cuda_device), streams=3)
+        bucket.zero(overlap=True)
+        hints = [o["_live_rows"] for o in outs]
+        bucket.allreduce_begin(hints, min_world=1)
+        assert bucket._pending[0] == "hint"
+        torch.autograd.backward([o["render"] for o in outs], G)
+        torch.cuda.synchronize()
+        before = bucket.flat.clone()
+        n = sc._xyz.shape[0]
+        mats = [v.reshape(n, -1) for v in bucket.views]
+        nonzero = mv._rows_live(mats, n).bool()
+        union = torch.zeros(n, dtype=torch.bool, device=cuda_device)
+        for h in hints:
+            union |= h.bool()
+        assert not (nonzero & ~union).any()  # every nonzero gradient row is in the agreed union
+        assert torch.equal(union, nonzero)   # ... and the union is exactly the backward's live set
+        bucket.allreduce_end()
+        torch.cuda.synchronize()
+        assert torch.equal(bucket.flat, before)
+    finally:
+        dist.destroy_process_group()
