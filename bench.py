@@ -63,6 +63,8 @@ def parse():
                          "backward of the summed loss -- the reference's order, DGE.py:170-239, 617-699)")
     ap.add_argument("--batch-backward", dest="batch_backward", action="store_true", help=argparse.SUPPRESS)
     ap.set_defaults(batch_backward=True)
+    ap.add_argument("--stagger", action="store_true",
+                    help="start each view's first half after the previous view's (render_views(stagger=True))")
     ap.add_argument("--view-threads", action="store_true",
                     help="issue each view's forward from its own host thread (dge_amd.multiview.render_views("
                          "threads=True); measured no faster and far noisier at c2)")
@@ -340,7 +342,7 @@ def run_views(args, cams, scene, pipe, bg, seeds, bucket, streams=None, min_worl
     if not overlap:
         bucket.zero()
     if args.batch_backward:
-        outs = render_views(cams, scene, pipe, bg, streams=streams, threads=args.view_threads)
+        outs = render_views(cams, scene, pipe, bg, streams=streams, threads=args.view_threads, stagger=args.stagger)
         if overlap:
             bucket.zero(overlap=True)
         if min_world is not None and not args.scan_live:

@@ -1057,7 +1057,8 @@ constexpr int kBwdHalf = kSegLen / 2;   // list positions per half-segment (LDS 
 // sums are reduce-scattered across the wave (quad_reduce).  Each kept entry gets
 // one record at 4*slot + quadrant (slot: the binning slot, so k_gauss_bwd reads
 // a Gaussian's records contiguously) and a flag.
-__global__ __launch_bounds__(64, 4) void k_render_bwd(RenderBwdArgs a) {
+template <bool LOOP>
+__global__ __launch_bounds__(64, 4) void k_render_bwd(RenderBwdArgs a, uint32_t first_item) {
     // kept entries of a half-segment, compacted back to front, + a group of padding
     // (one array per field: four consecutive entries' field is one 16-B read, see bwd_quad)
     __shared__ __attribute__((aligned(16))) float s_x[kBwdHalf + kBwdGroup], s_y[kBwdHalf + kBwdGroup];
@@ -1068,12 +1069,14 @@ __global__ __launch_bounds__(64, 4) void k_render_bwd(RenderBwdArgs a) {
     __shared__ uint32_t s_pos[kBwdHalf + kBwdGroup];
     __shared__ uint2 s_pair[kBwdHalf + kBwdGroup];  // (Gaussian, slot) of the kept entries: the record writes
     const int lane = threadIdx.x;
-    // block -> work item (quadrant, segment) of the forward's list: multi-segment windows first;
-    // blocks past the list's end exit (they dispatch after every real item).  (A persistent-wave
-    // work queue measured slower than the hardware dispatcher here.)
+    // block -> work item (quadrant, segment) of the forward's list, multi-segment windows first:
+    // first_item + blockIdx.x (LOOP: then + gridDim.x while items remain).  The host cannot know the
+    // item count; the bound (4 x slots) is ~7x the c2 count, and launching it whole put ~50k
+    // immediately-exiting workgroups at the end of the kernel.  launch_render_backward covers the
+    // first kBwdGridCap items with one workgroup each and the rest, if any, with a small looping grid.
+    // (A persistent-wave work queue measured slower than the hardware dispatcher here.)
     const uint32_t n_multi = a.bwd_count[0], n_items = n_multi + a.bwd_count[1];
-    const uint32_t qi = blockIdx.x;
-    if (qi >= n_items) return;
+    for (uint32_t qi = first_item + blockIdx.x; qi < n_items; qi += gridDim.x) {
     const uint2 item = qi < n_multi ? a.bwd_items[qi] : a.bwd_items[a.item_cap - 1 - (qi - n_multi)];
     const int tile = (int)item.x, quad = (int)(item.y & 3u), seg = (int)(item.y >> 2);
     const int qidx = 4 * tile + quad;
@@ -1227,15 +1230,35 @@ __global__ __launch_bounds__(64, 4) void k_render_bwd(RenderBwdArgs a) {
         d[6] = (uint64_t)seg << 32 | (uint32_t)qidx;
         d[7] = wave_location();
     }
+    if (!LOOP) break;
+    }
+}
+
+constexpr unsigned kBwdGridCap = 16384;  // items with a workgroup of their own (c2: ~7-9k items)
+constexpr unsigned kBwdLoopGrid = 2048;  // the looping grid over any items beyond
+
+static unsigned bwd_grid_cap() {  // DGE_AMD_BWD_GRID_CAP: a smaller cap (tests of the looping grid)
+    static unsigned v = 0;
+    if (!v) {
+        const char* e = getenv("DGE_AMD_BWD_GRID_CAP");
+        const long c = e ? atol(e) : 0;
+        v = (c > 0 && c < (long)kBwdGridCap) ? (unsigned)c : kBwdGridCap;
+    }
+    return v;
 }
 
 void launch_render_backward(const RenderBwdArgs& a, hipStream_t s) {
     const int tiles = a.gx * a.gy;
     if (tiles <= 0) return;
-    const unsigned grid = a.item_cap;
     RenderBwdArgs b = a;
     if (fwd_variant() == 0) b.touched = nullptr;  // k_render_fwd set them (the pipelined variant does not)
-    hipLaunchKernelGGL(k_render_bwd, dim3(grid), dim3(64), 0, s, b);
+    const unsigned cap = bwd_grid_cap();
+    const unsigned grid = a.item_cap < cap ? a.item_cap : cap;
+    hipLaunchKernelGGL(k_render_bwd<false>, dim3(grid), dim3(64), 0, s, b, 0u);
+    if (a.item_cap > cap) {
+        const unsigned rest = a.item_cap - cap;
+        hipLaunchKernelGGL(k_render_bwd<true>, dim3(rest < kBwdLoopGrid ? rest : kBwdLoopGrid), dim3(64), 0, s, b, cap);
+    }
 }
 
 }  // namespace gs

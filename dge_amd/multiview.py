@@ -284,7 +284,8 @@ def _touched_rows(prep):
     return geom[off:off + prep.P]
 
 
-def render_views(cameras, pc, pipe, bg_color, streams: int = 2, threads: bool = False, **kw):
+def render_views(cameras, pc, pipe, bg_color, streams: int = 2, threads: bool = False, stagger: bool = False,
+                 **kw):
     """render() of every camera, the views spread round-robin over `streams` HIP streams.
 
     The reference renders a batch's views one after another (threestudio/systems/DGE.py:179-239) on
@@ -296,7 +297,9 @@ def render_views(cameras, pc, pipe, bg_color, streams: int = 2, threads: bool = 
     release the GIL).  Off by default: at c2 it measured no faster than one issuing thread and far
     noisier (1413-2274 vs 1902-2052 renders/s over repeated runs).  Outputs are the same dicts render() returns, usable on the caller's stream (it
     waits for every view); autograd runs each view's backward on that view's stream and the in-kernel
-    gradient accumulation orders itself across them (diff_gaussian_rasterization._order_grad_writes_*)."""
+    gradient accumulation orders itself across them (diff_gaussian_rasterization._order_grad_writes_*).
+    stagger: view i's first half (preprocess, depth sort, instance scan) starts after view i-1's, so the
+    views reach their HBM-bound and latency-bound phases at different times instead of all at once."""
     from .gaussian_renderer import render
 
     if streams <= 1 or len(cameras) <= 1:
@@ -326,11 +329,14 @@ def render_views(cameras, pc, pipe, bg_color, streams: int = 2, threads: bool = 
     begun = None
     if _fused_ok(pc, pipe):
         begun = []
+        prev = ready
         for i, cam in enumerate(cameras):
             s = pool[i % len(pool)]
-            s.wait_event(ready)
+            s.wait_event(prev)
             with torch.cuda.stream(s):
                 begun.append(_fused_begin(cam, pc, pipe, bg_color, **kw))
+            if stagger:
+                prev = s.record_event()
     for i, cam in enumerate(cameras):
         s = pool[i % len(pool)]
         if begun is None:
@@ -401,7 +407,7 @@ def found_inf_allreduce(bucket: GradBucket, group=None) -> torch.Tensor:
 
 def multiview_step(scene, cameras, render_fn, pipe, bg, bucket: GradBucket, total_views: int, targets=None,
                    gt_images=None, masks=None, lambda_l1: float = 1.0, loss_scale: float = 1.0,
-                   semantic: bool = False, group=None):
+                   semantic: bool = False, group=None, streams: int = 1, bucket_zeroed: bool = False):
     """One data-parallel step of DGE's edit loop over this rank's views (threestudio/systems/DGE.py
     forward :170-239, training_step :617-699, on_before_optimizer_step :266-296).
 
@@ -418,14 +424,26 @@ def multiview_step(scene, cameras, render_fn, pipe, bg, bucket: GradBucket, tota
     (found_inf_allreduce), and the densification statistics: the SUM of the view-space gradients and the
     MAX of the radii across views and ranks.  Returns a dict: viewspace_grad_sum [P,3], radii_max [P],
     found_inf (float tensor [1]), semantic_masks (list of [H,W] bool, when ``semantic``).
+
+    streams > 1 with this package's render (dge_amd.gaussian_renderer.render): the views are rendered
+    together on that many HIP streams (render_views) and ONE backward of their summed loss follows — the
+    reference's order (DGE.py renders the batch, then back-propagates); with ``bucket_zeroed`` (the caller
+    zeroed the bucket this step and these losses are the only gradient source) the all-reduce's union of
+    live rows is agreed on between the forwards and that backward (GradBucket.allreduce_begin), so the
+    host does not wait for the backward before the collective is shaped.
     """
+    from .gaussian_renderer import render as _render
+
     P = scene.num_points()
     dev = bucket.flat.device
     vs_sum = torch.zeros((P, 3), dtype=torch.float32, device=dev)
     radii_max = torch.zeros((P,), dtype=torch.int32, device=dev)
     sem = []
+    batched = streams > 1 and render_fn is _render and len(cameras) > 1
+    pkgs = render_views(cameras, scene, pipe, bg, streams=streams) if batched else None
+    losses = []
     for i, cam in enumerate(cameras):
-        pkg = render_fn(cam, scene, pipe, bg)
+        pkg = pkgs[i] if batched else render_fn(cam, scene, pipe, bg)
         img = pkg["render"]
         if targets is not None:
             loss = (img * targets[i]).sum()
@@ -434,9 +452,21 @@ def multiview_step(scene, cameras, render_fn, pipe, bg, bucket: GradBucket, tota
             loss = torch.abs(img * m - gt_images[i] * m).sum() * (lambda_l1 / (total_views * img.numel()))
         if loss_scale != 1.0:
             loss = loss * loss_scale
+        if batched:
+            losses.append(loss)
+            continue
         loss.backward()
         vs_sum += pkg["viewspace_points"].grad
         radii_max = torch.maximum(radii_max, pkg["radii"])
+    hinted = batched and bucket_zeroed and all("_live_rows" in pkg for pkg in pkgs)
+    if batched:
+        if hinted:
+            bucket.allreduce_begin([pkg["_live_rows"] for pkg in pkgs], group)
+        torch.autograd.backward(losses)
+        for pkg in pkgs:
+            vs_sum += pkg["viewspace_points"].grad
+            radii_max = torch.maximum(radii_max, pkg["radii"])
+    for i, cam in enumerate(cameras):
         if semantic:
             with torch.no_grad():
                 gm = getattr(scene, "mask", None)
@@ -444,7 +474,10 @@ def multiview_step(scene, cameras, render_fn, pipe, bg, bucket: GradBucket, tota
                 sm = render_fn(cam, scene, pipe, bg, override_color=gm[..., None].float().repeat(1, 3))["render"]
                 sem.append(torch.norm(sm, dim=0) > 0.8)
     found_inf = found_inf_allreduce(bucket, group)
-    bucket.allreduce(group)
+    if hinted:
+        bucket.allreduce_end()
+    else:
+        bucket.allreduce(group)
     reduce_view_stats(vs_sum, radii_max, group)
     out = {"viewspace_grad_sum": vs_sum, "radii_max": radii_max, "found_inf": found_inf}
     if semantic:

@@ -151,3 +151,39 @@ def test_c3_two_ranks_share_one_card(cuda_device):
         np.testing.assert_array_equal(rmax, r1)
     for p in procs:
         assert p.exitcode == 0
+
+
+def test_multiview_step_batched_streams_hinted_one_rank(cuda_device):
+    """multiview_step(streams=3, bucket_zeroed=True) on a one-rank RCCL group — views rendered together on
+    3 streams, one backward of the summed loss, the all-reduce's live rows agreed on before it — gives the
+    per-view loop's gradients, view-space sums and radii."""
+    import torch.distributed as dist
+
+    from dge_amd.gaussian_renderer import PipelineParams, render
+    from dge_amd.multiview import GradBucket, multiview_step
+
+    dev = torch.device("cuda")
+    P, V, W, H = 60_000, 3, 160, 128
+    res = {}
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ["MASTER_PORT"] = str(_free_port())
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    try:
+        for mode in ("loop", "batched"):
+            sc, cams, seeds = _c3_setup(dev, P, V, W, H)
+            bucket = GradBucket(sc.parameters())
+            bucket.zero()
+            if mode == "loop":
+                out = multiview_step(sc, cams, render, PipelineParams(), torch.zeros(3, device=dev), bucket, V,
+                                     targets=seeds)
+            else:
+                out = multiview_step(sc, cams, render, PipelineParams(), torch.zeros(3, device=dev), bucket, V,
+                                     targets=seeds, streams=3, bucket_zeroed=True)
+            torch.cuda.synchronize()
+            res[mode] = (bucket.flat.clone(), out["viewspace_grad_sum"].clone(), out["radii_max"].clone())
+    finally:
+        dist.destroy_process_group()
+    (g0, v0, r0), (g1, v1, r1) = res["loop"], res["batched"]
+    assert torch.equal(r0, r1)
+    torch.testing.assert_close(v1, v0, rtol=1e-5, atol=1e-9)
+    torch.testing.assert_close(g1, g0, rtol=1e-5, atol=1e-9)

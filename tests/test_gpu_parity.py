@@ -579,3 +579,33 @@ def test_forced_32bit_depth_keys_match_30bit_path(cuda_device, monkeypatch):
     forced = run_gpu(s, **kw)
     for k in ("radii", "ranges", "point_list", "n_contrib", "color", "final_T"):
         np.testing.assert_array_equal(forced[k], base[k], err_msg=k)
+
+
+def test_backward_looping_grid_is_bitwise_identical(cuda_device, tmp_path):
+    """k_render_bwd's work items beyond the per-item grid (kBwdGridCap; c4-sized item counts) run on a
+    looping grid: with the cap forced down to 3 items (DGE_AMD_BWD_GRID_CAP, read once per process: a
+    child process), every gradient is bitwise the default launch's."""
+    import subprocess
+    import sys
+
+    script = tmp_path / "bwd_cap.py"
+    script.write_text(f'''
+import sys, numpy as np
+sys.path.insert(0, {repr(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))})
+sys.path.insert(0, {repr(os.path.dirname(os.path.abspath(__file__)))})
+from helpers import scene_arrays, camera_settings, run_gpu, GRAD_NAMES
+from test_gpu_parity import _sh_kw
+a = scene_arrays(200_000, seed=5, radius=2.0, scale=0.02)
+g = np.random.default_rng(7).standard_normal((3, 256, 384)).astype(np.float32)
+r = run_gpu(camera_settings(384, 256, device="cuda"), g, intermediates=False, **_sh_kw(a))
+np.savez(sys.argv[1], **{{n: r[n] for n in GRAD_NAMES}})
+''')
+    out = tmp_path / "capped.npz"
+    env = dict(os.environ, DGE_AMD_BWD_GRID_CAP="3")
+    subprocess.run([sys.executable, str(script), str(out)], env=env, check=True, timeout=300)
+    a = scene_arrays(200_000, seed=5, radius=2.0, scale=0.02)
+    g = np.random.default_rng(7).standard_normal((3, 256, 384)).astype(np.float32)
+    ref = run_gpu(camera_settings(384, 256, device="cuda"), g, intermediates=False, **_sh_kw(a))
+    capped = np.load(out)
+    for n in GRAD_NAMES:
+        np.testing.assert_array_equal(capped[n], ref[n], err_msg=f"{n} differs with the looping grid")

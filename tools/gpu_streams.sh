@@ -16,7 +16,7 @@ PY
 }
 for rep in 1 2; do
 run ${EXTRA_ARGS:-}
+run --stagger ${EXTRA_ARGS:-}
 run --serial-zero ${EXTRA_ARGS:-}
-run --streams 1 --per-view-backward --serial-zero ${EXTRA_ARGS:-}
 done
 cat gpurun_out/streams.log
