@@ -12,9 +12,7 @@ all-reduce of the flat parameter-gradient bucket (RCCL) — of the rows nonzero
 on some rank only (GradBucket.allreduce: ~24% of the 236 MB for 24 views).  The
 views run on `--streams` HIP streams (default 3, dge_amd.multiview.render_views:
 one view's latency-bound blend tails overlap the others' work; the in-kernel
-gradient accumulation orders only the per-Gaussian passes across streams) and the
-bucket's zero fill overlaps the forwards (GradBucket.zero(overlap=True), issued
-after them);
+gradient accumulation orders only the per-Gaussian passes across streams);
 `--per-view-backward` runs each view's backward right after its forward
 instead.  Per-GPU work
 is fixed, so scaling is weak and value = all views rendered / max-rank time.
@@ -71,9 +69,11 @@ def parse():
     ap.add_argument("--scan-live", action="store_true",
                     help="N > 1: find the all-reduce's live rows by reading the gradient bucket after the backward "
                          "(GradBucket.allreduce) instead of agreeing on the forwards' blended Gaussians before it")
-    ap.add_argument("--serial-zero", action="store_true",
-                    help="zero the gradient bucket before the forwards (default with streams: after enqueueing "
-                         "them, only the gradient writes wait for it: GradBucket.zero(overlap=True))")
+    ap.add_argument("--overlap-zero", dest="serial_zero", action="store_false",
+                    help="zero the gradient bucket after enqueueing the forwards, only the gradient writes waiting "
+                         "for it (GradBucket.zero(overlap=True)); measured no faster than zeroing first (default)")
+    ap.add_argument("--serial-zero", dest="serial_zero", action="store_true", help=argparse.SUPPRESS)
+    ap.set_defaults(serial_zero=True)
     ap.add_argument("--cpu-baseline-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -205,6 +205,7 @@ def main():
     if distributed:
         dist.barrier()
     torch.cuda.synchronize()
+    m0 = torch.cuda.memory_stats(dev)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
@@ -212,6 +213,11 @@ def main():
     if distributed:
         dist.barrier()
     dt = time.perf_counter() - t0
+    m1 = torch.cuda.memory_stats(dev)
+    # caching-allocator activity inside the timed region (device allocations there cost a hipMalloc each)
+    alloc_stats = {k: int(m1.get(k, 0) - m0.get(k, 0)) for k in ("num_device_alloc", "num_device_free",
+                                                                   "num_alloc_retries")}
+    alloc_stats["reserved_gb"] = round(m1.get("reserved_bytes.all.current", 0) / 2**30, 2)
     # roofline leg (timed, one stream): the two blend kernels bracketed by HIP events on their launch
     # stream, live, over iso_steps steps of the same workload with the views on one stream
     prof, iso = {}, None
@@ -320,6 +326,7 @@ def main():
             "rooflines": rooflines,
             # the leg the rooflines and stages_ms come from: the same step with the views on one stream
             "roofline_leg": iso,
+            "allocator_timed_region": alloc_stats,
             "legs": legs,
             "cpu_baseline": cpu,
         }

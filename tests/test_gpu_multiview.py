@@ -162,7 +162,7 @@ def test_multiview_step_batched_streams_hinted_one_rank(cuda_device):
     from dge_amd.gaussian_renderer import PipelineParams, render
     from dge_amd.multiview import GradBucket, multiview_step
 
-    dev = torch.device("cuda")
+    dev = torch.device("cuda", 0)
     P, V, W, H = 60_000, 3, 160, 128
     res = {}
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
