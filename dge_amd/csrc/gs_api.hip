@@ -790,6 +790,7 @@ int gs_rasterize_backward_ex(const gs_settings* s, const gs_params* gp, int R, c
             rb.point_pairs = at<uint2>(binning, bl.point_pairs);
             rb.bwd_items = at<uint2>(binning, bl.bwd_items);
             rb.bwd_count = bwd_count;
+            rb.tile_last = at<uint32_t>(img, il.tile_last);
             rb.item_cap = (uint32_t)(4 * bl.nslots);
             rb.quad_last = at<uint32_t>(img, il.quad_last);
             rb.ckpt = at<float4>(binning, bl.ckpt);
@@ -829,6 +830,7 @@ int gs_rasterize_backward_ex(const gs_settings* s, const gs_params* gp, int R, c
         ga.live_count = at<uint32_t>(const_cast<void*>(geom), gl.live_count);
         ga.live_list = at<uint32_t>(const_cast<void*>(geom), gl.live_list);
         ga.records = records;
+        ga.merged = render_backward_merged();
         ga.dL_dmeans2D = o->dL_dmeans2D; ga.dL_dcolors = o->dL_dcolors; ga.dL_dopacity = o->dL_dopacity;
         ga.dL_dmeans3D = o->dL_dmeans3D; ga.dL_dcov3D = o->dL_dcov3D;
         ga.dL_dscales = o->dL_dscales; ga.dL_drot = o->dL_drotations;

@@ -566,11 +566,18 @@ __global__ __launch_bounds__(kGB) void k_gauss_bwd_live(GaussBwdArgs a) {
                 for (int u = 0; u < 8; ++u) fl[u] = k0 + u < n ? flags[first + k0 + u] : 0u;
             }
             uint32_t m = 0;
+            const float4* recs;
+            if (a.merged) {  // one record per flagged slot
 #pragma unroll
-            for (int u = 0; u < 8; ++u)
+                for (int u = 0; u < 8; ++u) m |= fl[u] ? 1u << u : 0u;
+                recs = a.records + 3 * (size_t)(first + k0);
+            } else {
 #pragma unroll
-                for (int qd = 0; qd < 4; ++qd) m |= ((fl[u] >> (8 * qd)) & 0xFFu) ? 1u << (4 * u + qd) : 0u;
-            const float4* recs = a.records + 3 * (4 * (size_t)(first + k0));
+                for (int u = 0; u < 8; ++u)
+#pragma unroll
+                    for (int qd = 0; qd < 4; ++qd) m |= ((fl[u] >> (8 * qd)) & 0xFFu) ? 1u << (4 * u + qd) : 0u;
+                recs = a.records + 3 * (4 * (size_t)(first + k0));
+            }
             while (m) {
                 int bi[4];
                 bool use[4];

@@ -330,7 +330,8 @@ struct RenderBwdArgs {
     const float4* ckpt;         // the forward's (T, C) checkpoints
     const uint64_t* used;       // the forward's blended bits: the backward's exact cull
     const uint2* bwd_items;     // the forward's work list (capacity item_cap)
-    const uint32_t* bwd_count;  // [0] multi, [1] single items
+    const uint32_t* bwd_count;  // [0] multi, [1] single items; [2], [3] the per-tile list's (k_bwd_tile_items)
+    const uint32_t* tile_last;  // [tiles] the tile's last contributor (the per-tile replay's window)
     uint32_t item_cap;
     const Splat* splat;
     const float* bg;
@@ -343,6 +344,7 @@ struct RenderBwdArgs {
     uint64_t* diag;   // optional [item_cap][kDiagWords], by queue position (see diag_buffer)
 };
 void launch_render_backward(const RenderBwdArgs& a, hipStream_t s);
+int render_backward_merged();  // 1: one record per slot (k_render_bwd_tile), 0: per (slot, quadrant)
 
 struct GaussBwdArgs {
     int P, D, M, W, H, gx, gy;
@@ -362,6 +364,8 @@ struct GaussBwdArgs {
     uint32_t* live_list;       // [P] k_gauss_live: block b's live Gaussians at [256 b, 256 b + live_count[b])
     uint32_t* live_count;      // [P/256] live Gaussians per 256-Gaussian block
     const float4* records;     // [4*K][3] float4 by slot
+    int merged;                // records per slot (k_render_bwd_tile: flag u32 != 0, record at 3*slot) instead of
+                               // per (slot, quadrant) (k_render_bwd: flag byte 4*slot + q, record 3*(4*slot + q))
     float *dL_dmeans2D, *dL_dcolors, *dL_dopacity, *dL_dmeans3D, *dL_dcov3D, *dL_dscales, *dL_drot;
     uint32_t acc;  // GS_ACC_* bits: add into the output instead of overwriting
     const uint8_t* grad_mask;  // optional [P]: outputs in mask_bits are multiplied by it

@@ -24,6 +24,8 @@
 //    quadrant) with plain stores.  No float atomics: the per-Gaussian sum
 //    happens in gs_backward.hip in a fixed order, so the backward is bitwise
 //    reproducible.
+#include <string.h>
+
 #include "gs_common.h"
 #include "gs_internal.h"
 
@@ -1234,6 +1236,216 @@ __global__ __launch_bounds__(64, 4) void k_render_bwd(RenderBwdArgs a, uint32_t 
     }
 }
 
+// =====================================================================
+// backward, merged per tile: one 256-thread workgroup per (tile, segment)
+// =====================================================================
+// The four quadrant waves of a tile replay the same 256 list positions (each
+// its own window, pixel state and blended bits, exactly as k_render_bwd), in
+// quarters of 64 positions.  A wave's finished per-(entry, quadrant) record
+// goes to an LDS table instead of HBM; after each quarter one wave adds the
+// tile's four quadrant records of every kept position in quadrant order and
+// writes ONE record per (slot) with a u32 flag: a quarter of k_render_bwd's
+// record and flag stores, whole-record writes, one (Gaussian, slot) list read
+// and one Splat gather per position for the tile instead of one per quadrant,
+// and k_gauss_bwd reads a quarter of the records.  Fixed summation order:
+// bitwise reproducible.  Work items (tile, segment << 2) come from
+// k_bwd_tile_items (multi-segment tiles first).
+constexpr int kBwdQuarter = 64;  // list positions per replay round
+
+__global__ __launch_bounds__(1024) void k_bwd_tile_items(RenderBwdArgs a, int tiles) {
+    __shared__ uint32_t cnt[2];
+    if (threadIdx.x < 2) cnt[threadIdx.x] = 0u;
+    __syncthreads();
+    uint2* items = const_cast<uint2*>(a.bwd_items);
+    for (int t = threadIdx.x; t < tiles; t += 1024) {
+        const uint32_t last = a.tile_last[t];
+        const uint32_t nseg = (last + kSegLen - 1) / kSegLen;
+        if (nseg > 1) {  // multi-segment tiles at the front: they dispatch first
+            const uint32_t b = atomicAdd(&cnt[0], nseg);
+            for (uint32_t k = 0; k < nseg; ++k) items[b + k] = make_uint2((uint32_t)t, k << 2);
+        } else if (nseg == 1) {
+            const uint32_t b = atomicAdd(&cnt[1], 1u);
+            items[a.item_cap - 1 - b] = make_uint2((uint32_t)t, 0u);
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < 2) const_cast<uint32_t*>(a.bwd_count)[2 + threadIdx.x] = cnt[threadIdx.x];
+}
+
+template <bool LOOP>
+__global__ __launch_bounds__(256, 3) void k_render_bwd_tile(RenderBwdArgs a, uint32_t first_item) {
+    constexpr int QS = kBwdQuarter + kBwdGroup;  // staged entries per wave (+ a group of padding)
+    __shared__ __attribute__((aligned(16))) float s_x[4][QS], s_y[4][QS], s_cx[4][QS], s_cy[4][QS], s_cz[4][QS],
+        s_op[4][QS];
+    __shared__ float4 s_rgb[4][QS];
+    __shared__ uint32_t s_pos[4][QS];
+    __shared__ float s_rec[4][kSegLen][9];  // finished quadrant records by position in the segment
+    __shared__ uint64_t s_kept[4][4];       // kept positions of each quadrant, per quarter
+    const int q = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint32_t n_multi = a.bwd_count[2], n_items = n_multi + a.bwd_count[3];
+    for (uint32_t qi = first_item + blockIdx.x; qi < n_items; qi += gridDim.x) {
+    const uint2 item = qi < n_multi ? a.bwd_items[qi] : a.bwd_items[a.item_cap - 1 - (qi - n_multi)];
+    const int tile = (int)item.x, seg = (int)(item.y >> 2);
+    const int qidx = 4 * tile + q;
+    const int tx = tile % a.gx, ty = tile / a.gx;
+    const int bx0 = tx * kTile + (q & 1) * kQuad, by0 = ty * kTile + (q >> 1) * kQuad;
+    const int px = bx0 + (lane & 7), py = by0 + (lane >> 3);
+    const bool inside = px < a.W && py < a.H;
+    const float pfx = (float)px, pfy = (float)py;
+
+    const uint2 range = a.ranges[tile];
+    const int lo = seg * kSegLen;
+    const int tile_n = min(kSegLen, (int)a.tile_last[tile] - lo);  // the tile's positions in this segment
+    const int window = (int)a.quad_last[qidx];
+    const int nseg_q = (window + kSegLen - 1) / kSegLen;
+    // this quadrant's part [lo, limit) of the segment (empty when its window ends before it)
+    const int limit = seg >= nseg_q ? lo : seg == nseg_q - 1 ? window : lo + kSegLen;
+    const int n = limit - lo;
+
+    const uint32_t* used32 = reinterpret_cast<const uint32_t*>(a.used + (size_t)used_base(range.x, tile) * 4 + q);
+    uint2 pairs[4];
+    uint32_t kb = 0u;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int j = 64 * i + lane, k = lo + j;
+        pairs[i] = j < tile_n ? a.point_pairs[range.x + k] : make_uint2(0u, 0u);
+        const uint32_t ub = j < n ? used32[(size_t)(k >> 6) * 8 + ((k >> 5) & 1)] : 0u;
+        kb |= ((ub >> (k & 31)) & 1u) << i;
+    }
+    // the kept entries' Splats one quarter ahead: quarter i-1's gathers are in flight during quarter i
+    Entry cur = gather_entry(a.splat, (kb >> 3) & 1u ? pairs[3].x : 0u);
+
+    const size_t HW = (size_t)a.W * a.H;
+    const size_t pix = inside ? (size_t)a.W * py + px : 0;
+    const float T_final = inside && n > 0 ? a.final_T[pix] : 0.f;
+    const uint32_t last_contributor = inside && n > 0 ? a.n_contrib[pix] : 0u;
+    float dp0 = 0.f, dp1 = 0.f, dp2 = 0.f;
+    if (inside && n > 0) {
+        dp0 = a.dL_dpix[pix];
+        dp1 = a.dL_dpix[HW + pix];
+        dp2 = a.dL_dpix[2 * HW + pix];
+    }
+    const float nbg = -T_final * (a.bg[0] * dp0 + a.bg[1] * dp1 + a.bg[2] * dp2);
+    float T = T_final, D0 = 0.f, D1 = 0.f, D2 = 0.f;
+    if (n > 0 && limit < window) {  // start inside the window (see k_render_bwd)
+        const float4* ck = a.ckpt + ((size_t)ckpt_base(range.x, tile) * 4 + q) * 64;
+        T = ck[(size_t)seg * 256 + lane].x;
+        float S0 = 0.f, S1 = 0.f, S2 = 0.f;
+        for (int k = nseg_q - 1; k > seg; --k) {
+            const float4 c = ck[(size_t)k * 256 + lane];
+            S0 += c.y;
+            S1 += c.z;
+            S2 += c.w;
+        }
+        const float inv = 1.0f / T;
+        D0 = S0 * inv;
+        D1 = S1 * inv;
+        D2 = S2 * inv;
+    }
+    const float ddelx_dx = (float)(0.5 * a.W), ddely_dy = (float)(0.5 * a.H);
+    const int row = lane >> 4;
+    const int row_entry = row == 1 ? 2 : row == 2 ? 1 : row;
+    const bool row_writer = (lane & 15) == 0;
+    float* xs = s_x[q];
+    float* ys = s_y[q];
+    float* cxs = s_cx[q];
+    float* cys = s_cy[q];
+    float* czs = s_cz[q];
+    float* ops = s_op[q];
+
+#pragma unroll
+    for (int i = 3; i >= 0; --i) {  // quarters back to front
+        const int qlo = lo + 64 * i;
+        const bool keep = 64 * i + lane < n && ((kb >> i) & 1u);
+        const uint64_t km = __ballot(keep);
+        const int nk = __popcll(km);
+        if (keep) {  // compacted back to front
+            const int slot = __popcll(km & ~lanemask_lt() & ~(1ull << lane));
+            xs[slot] = cur.xy.x;
+            ys[slot] = cur.xy.y;
+            cxs[slot] = cur.co.x;
+            cys[slot] = -cur.co.y;  // (negated: pixel_alpha4; finish_record negates back)
+            czs[slot] = cur.co.z;
+            ops[slot] = cur.co.w;
+            s_rgb[q][slot] = cur.f;
+            s_pos[q][slot] = (uint32_t)(qlo + lane);
+            if (a.touched) a.touched[pairs[i].x] = 1;
+        }
+        if (i > 0) cur = gather_entry(a.splat, (kb >> (i - 1)) & 1u ? pairs[i - 1].x : 0u);
+        if (lane < kBwdGroup) {  // padding: alpha = 0 everywhere, never in a pixel's list
+            xs[nk + lane] = 0.f;
+            ys[nk + lane] = 0.f;
+            cxs[nk + lane] = 0.f;
+            cys[nk + lane] = 0.f;
+            czs[nk + lane] = 0.f;
+            ops[nk + lane] = 0.f;
+            s_rgb[q][nk + lane] = make_float4(0.f, 0.f, 0.f, 0.f);
+            s_pos[q][nk + lane] = 0xFFFFFFFFu;
+        }
+        if (lane == 0) s_kept[q][i] = km;
+        // (the staging is this wave's own: a wave-level barrier, not a block one)
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        for (int k = 0; k < nk; k += kBwdGroup) {
+            float g[kBwdGroup][9];
+            {
+                const auto ld4 = [&](const float* f) { return *reinterpret_cast<const f4v*>(f + k); };
+                const float4 c4[4] = {s_rgb[q][k], s_rgb[q][k + 1], s_rgb[q][k + 2], s_rgb[q][k + 3]};
+                const bool in4[4] = {s_pos[q][k] < last_contributor, s_pos[q][k + 1] < last_contributor,
+                                     s_pos[q][k + 2] < last_contributor, s_pos[q][k + 3] < last_contributor};
+                bwd_quad(ld4(xs), ld4(ys), ld4(cxs), ld4(cys), ld4(czs), ld4(ops), c4, in4, pfx, pfy, dp0, dp1,
+                         dp2, nbg, T, D0, D1, D2, g);
+            }
+            __builtin_amdgcn_sched_barrier(0);  // (every product first: the lane swaps clobber their operands)
+            float S[9];
+#pragma unroll
+            for (int f = 0; f < 9; ++f) S[f] = quad_reduce(g[0][f], g[1][f], g[2][f], g[3][f]);
+            __builtin_amdgcn_sched_barrier(0);
+            const int kw = k + row_entry;
+            if (row_writer && kw < nk) {
+                float4 r[3];
+                finish_record(make_float4(cxs[kw], -cys[kw], czs[kw], ops[kw]), S, ddelx_dx, ddely_dy, r);
+                float* t = s_rec[q][s_pos[q][kw] - (uint32_t)lo];
+                t[0] = r[0].x; t[1] = r[0].y; t[2] = r[0].z; t[3] = r[0].w;
+                t[4] = r[1].x; t[5] = r[1].y; t[6] = r[1].z; t[7] = r[1].w;
+                t[8] = r[2].x;
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // (the next quarter restages)
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    __syncthreads();
+    {   // the tile's record of each kept position of the segment: quadrants added in order
+        const int p = threadIdx.x, i = p >> 6;
+        const uint64_t bit = 1ull << (p & 63);
+        const bool kk[4] = {(s_kept[0][i] & bit) != 0, (s_kept[1][i] & bit) != 0, (s_kept[2][i] & bit) != 0,
+                            (s_kept[3][i] & bit) != 0};
+        if (p < tile_n && (kk[0] | kk[1] | kk[2] | kk[3])) {
+            float acc[9];
+#pragma unroll
+            for (int f = 0; f < 9; ++f) acc[f] = 0.f;
+#pragma unroll
+            for (int qq = 0; qq < 4; ++qq) {
+                if (kk[qq]) {
+#pragma unroll
+                    for (int f = 0; f < 9; ++f) acc[f] += s_rec[qq][p][f];
+                }
+            }
+            const size_t rec = a.point_pairs[range.x + lo + p].y;
+            float4* dst = a.records + 3 * rec;
+            dst[0] = make_float4(acc[0], acc[1], acc[2], acc[3]);
+            dst[1] = make_float4(acc[4], acc[5], acc[6], acc[7]);
+            dst[2] = make_float4(acc[8], 0.f, 0.f, 0.f);
+            reinterpret_cast<uint32_t*>(a.rec_flags)[rec] = 1u;
+        }
+    }
+    __syncthreads();  // (a next item reuses the table)
+    if (!LOOP) break;
+    }
+}
+
 constexpr unsigned kBwdGridCap = 16384;  // items with a workgroup of their own (c2: ~7-9k items)
 constexpr unsigned kBwdLoopGrid = 2048;  // the looping grid over any items beyond
 
@@ -1247,11 +1459,35 @@ static unsigned bwd_grid_cap() {  // DGE_AMD_BWD_GRID_CAP: a smaller cap (tests 
     return v;
 }
 
+// DGE_AMD_BWD=tile: k_render_bwd_tile (one record per slot), else k_render_bwd (one per quadrant).  The
+// per-tile merge cuts the record traffic and gauss_bwd (65 -> 59 us at c2) but its four quadrant waves
+// wait for one another (render_bwd 105 -> 122 us): measured 2113-2130 vs 2155-2175 renders/s, off by default.
+int render_backward_merged() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("DGE_AMD_BWD");
+        v = (e && !strcmp(e, "tile")) ? 1 : 0;
+    }
+    return v;
+}
+
 void launch_render_backward(const RenderBwdArgs& a, hipStream_t s) {
     const int tiles = a.gx * a.gy;
     if (tiles <= 0) return;
     RenderBwdArgs b = a;
     if (fwd_variant() == 0) b.touched = nullptr;  // k_render_fwd set them (the pipelined variant does not)
+    if (render_backward_merged()) {
+        hipLaunchKernelGGL(k_bwd_tile_items, dim3(1), dim3(1024), 0, s, b, tiles);
+        const unsigned items = a.item_cap / 4;  // per-tile segments <= slots
+        const unsigned cap = bwd_grid_cap() / 4 > 0 ? bwd_grid_cap() / 4 : 1u;
+        hipLaunchKernelGGL(k_render_bwd_tile<false>, dim3(items < cap ? items : cap), dim3(256), 0, s, b, 0u);
+        if (items > cap) {
+            const unsigned rest = items - cap;
+            hipLaunchKernelGGL(k_render_bwd_tile<true>, dim3(rest < kBwdLoopGrid / 4 ? rest : kBwdLoopGrid / 4),
+                               dim3(256), 0, s, b, cap);
+        }
+        return;
+    }
     const unsigned cap = bwd_grid_cap();
     const unsigned grid = a.item_cap < cap ? a.item_cap : cap;
     hipLaunchKernelGGL(k_render_bwd<false>, dim3(grid), dim3(64), 0, s, b, 0u);
