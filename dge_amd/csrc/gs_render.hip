@@ -1072,11 +1072,9 @@ __global__ __launch_bounds__(64, 4) void k_render_bwd(RenderBwdArgs a, uint32_t 
     __shared__ uint2 s_pair[kBwdHalf + kBwdGroup];  // (Gaussian, slot) of the kept entries: the record writes
     const int lane = threadIdx.x;
     // block -> work item (quadrant, segment) of the forward's list, multi-segment windows first:
-    // first_item + blockIdx.x (LOOP: then + gridDim.x while items remain).  The host cannot know the
-    // item count; the bound (4 x slots) is ~7x the c2 count, and launching it whole put ~50k
-    // immediately-exiting workgroups at the end of the kernel.  launch_render_backward covers the
-    // first kBwdGridCap items with one workgroup each and the rest, if any, with a small looping grid.
-    // (A persistent-wave work queue measured slower than the hardware dispatcher here.)
+    // first_item + blockIdx.x (LOOP: then + gridDim.x while items remain); blocks past the list's end
+    // exit (they dispatch after every real item; see launch_render_backward for the grid).  (A
+    // persistent-wave work queue measured slower than the hardware dispatcher here.)
     const uint32_t n_multi = a.bwd_count[0], n_items = n_multi + a.bwd_count[1];
     for (uint32_t qi = first_item + blockIdx.x; qi < n_items; qi += gridDim.x) {
     const uint2 item = qi < n_multi ? a.bwd_items[qi] : a.bwd_items[a.item_cap - 1 - (qi - n_multi)];
@@ -1446,15 +1444,18 @@ __global__ __launch_bounds__(256, 3) void k_render_bwd_tile(RenderBwdArgs a, uin
     }
 }
 
-constexpr unsigned kBwdGridCap = 16384;  // items with a workgroup of their own (c2: ~7-9k items)
-constexpr unsigned kBwdLoopGrid = 2048;  // the looping grid over any items beyond
+// One workgroup per possible item (the bound, 4 x checkpoint slots, is ~7x the c2 count): the surplus
+// workgroups exit at once and cost nothing measurable (render_bwd 104 us either way), while capping the
+// grid needs a second, looping launch for the overflow whose empty dispatch alone measured ~5 us.
+// DGE_AMD_BWD_GRID_CAP=n caps it anyway (the test of the looping path).
+constexpr unsigned kBwdLoopGrid = 2048;  // the looping grid over items beyond a cap
 
-static unsigned bwd_grid_cap() {  // DGE_AMD_BWD_GRID_CAP: a smaller cap (tests of the looping grid)
+static unsigned bwd_grid_cap() {
     static unsigned v = 0;
     if (!v) {
         const char* e = getenv("DGE_AMD_BWD_GRID_CAP");
         const long c = e ? atol(e) : 0;
-        v = (c > 0 && c < (long)kBwdGridCap) ? (unsigned)c : kBwdGridCap;
+        v = c > 0 ? (unsigned)c : 0xFFFFFFFFu;
     }
     return v;
 }
