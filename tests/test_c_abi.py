@@ -30,8 +30,12 @@ def test_library_exports_every_header_symbol():
 
 
 def test_abi_version_and_sizes():
+    import re
+
     lib = N.load_library()
-    assert lib.gs_abi_version() == 8
+    assert lib.gs_abi_version() == N.ABI_VERSION
+    hdr = open(N.HEADER_PATH).read()
+    assert int(re.search(r"#define GS_RASTER_ABI_VERSION (\d+)", hdr).group(1)) == N.ABI_VERSION
     g1, g2 = lib.gs_geometry_buffer_size(1000), lib.gs_geometry_buffer_size(2000)
     assert 0 < g1 < g2 and g1 % 256 == 0
     assert lib.gs_image_buffer_size(512, 512) >= 512 * 512 * 8
