@@ -73,6 +73,13 @@ bool force_depth_keys32() {
     return e && e[0] == '1';
 }
 
+// DGE_AMD_TILE_SORT=2pass: the emission + two full tile-sort passes + k_ranges even where the
+// two-level binning applies (tests compare both; read per forward)
+bool tile_sort_unfused() {
+    const char* e = getenv("DGE_AMD_TILE_SORT");
+    return e && !strcmp(e, "2pass");
+}
+
 // depth-sort bits (three passes of kDepthPassBits; DGE_AMD_DEPTH_SORT_BITS overrides, for probes)
 int depth_sort_bits() {
     static const int bits = [] {
@@ -391,6 +398,8 @@ int bin_begin(FwdState& f, int copy_colors, gs_alloc_fn alloc, void* ctx, hipStr
     ea.scan_sums = at<uint32_t>(geom, gl.scan_sums);
     ea.first_slot = at<uint32_t>(geom, gl.first_slot);
     ea.scan_blocks = gl.scan_blocks;
+    ea.xhist = tile_sort_fused(g.gx, g.gy) && pa.rect_packed && !tile_sort_unfused() ? at<uint32_t>(geom, gl.emit_hist)
+                                                                                    : nullptr;
     { StageScope sc(ST_SCAN, stream); launch_scan_reduce(ea, stream); }
     GS_LAUNCHED("instance scan");
     return GS_OK;
@@ -450,6 +459,20 @@ int bin_end(FwdState& f, gs_alloc_fn alloc, void* ctx, hipStream_t stream, void*
     if (K == 0) return GS_OK;
 
     const TileSortPlan plan = tile_sort_plan(g.tiles);
+    if (ea.xhist) {  // two-level binning (tile_sort_fused): column-ordered emission, row pass, ranges
+        ea.tile_key = at<uint32_t>(bin, bl.key1);
+        ea.pairs_out = at<uint2>(bin, bl.pair1);
+        ea.xtotals = at<uint32_t>(bin, bl.sort_totals);
+        ea.tile_count = at<uint32_t>(bin, bl.tile_count);
+        ea.ntiles = g.tiles;
+        ea.rec_flags32 = at<uint32_t>(bin, bl.rec_flags);
+        { StageScope sc(ST_EMIT, stream); launch_emit_fused(ea, stream); }
+        { StageScope sc(ST_TILE_SORT, stream);
+        launch_row_pass(ea, K, at<uint2>(bin, bl.point_pairs), at<uint32_t>(bin, bl.sort_hist), bl.sort_blocks,
+                        at<uint2>(img, il.ranges), stream); }
+        GS_LAUNCHED("two-level binning");
+        return GS_OK;
+    }
     ea.tile_key = at<uint32_t>(bin, bl.key0);
     ea.slot_gauss = at<uint32_t>(bin, bl.slot_gauss);
     ea.rec_flags32 = at<uint32_t>(bin, bl.rec_flags);

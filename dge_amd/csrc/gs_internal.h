@@ -52,6 +52,14 @@ inline int ceil_log2(uint32_t n) {
     return b;
 }
 
+// Two-level binning for grids of more than 2048 tiles and at most 128 x 128 (c4: 120 x 68): the
+// emission itself does the first, column pass (k_scan_emit_x: instances written ordered by tile
+// column, stable, with the key y << 7 | x), one 7-bit row pass follows, and the tile ranges come
+// from per-tile counts taken during that pass — instead of an emission, two full sort passes and a
+// ranges pass over the K instances.
+constexpr int kXBits = 7, kXDigits = 1 << kXBits;
+inline bool tile_sort_fused(int gx, int gy) { return gx * gy > (1 << 11) && gx <= kXDigits && gy <= kXDigits; }
+
 // Radix pass plan for the tile-key sort.
 struct TileSortPlan {
     int bits;          // total key bits
@@ -83,7 +91,7 @@ struct alignas(64) Splat {
 struct GeomLayout {
     size_t splat, tiles_touched, clamped, touched, live_count, live_list, radii, first_slot;
     // live_count: one u32 per 256-Gaussian block (k_gauss_live); live_list: block-local compacted ids
-    size_t key0, key1, val0, val1, rect, sort_hist, sort_totals, scan_sums, total;
+    size_t key0, key1, val0, val1, rect, sort_hist, sort_totals, scan_sums, emit_hist, total;
     int sort_blocks, scan_blocks;
 };
 inline GeomLayout geom_layout(int P) {
@@ -108,6 +116,7 @@ inline GeomLayout geom_layout(int P) {
     L.sort_hist = o; o = align_up(o + 4 * (1u << kMaxSinglePassBits) * (size_t)L.sort_blocks);  // any digit width
     L.sort_totals = o; o = align_up(o + 4 * (1u << kMaxSinglePassBits));
     L.scan_sums = o; o = align_up(o + 4 * (size_t)(L.scan_blocks + 1));
+    L.emit_hist = o; o = align_up(o + 4 * (size_t)kXDigits * L.scan_blocks);  // two-level binning: columns per block
     L.total = o;
     return L;
 }
@@ -125,7 +134,11 @@ inline GeomLayout geom_layout(int P) {
 // ckpt_base(t) = range.x / kSegLen + t (monotone and non-overlapping because
 // ranges are a prefix sum), each slot 4 quadrants x 64 pixels x float4.
 constexpr int kBlendRound = 256;  // list entries per blend round
-constexpr int kSegLen = kBlendRound;  // backward segment length (checkpoints at round boundaries)
+// backward segment length: checkpoints at every round boundary and mid-round, so a replay work item
+// covers at most 128 positions (half the per-item work of round-long segments: the replay's wave
+// durations pack onto the SIMDs instead of leaving a tail of long items)
+constexpr int kSegLen = 128;
+static_assert(kBlendRound == 2 * kSegLen, "k_render_fwd writes two checkpoints per round");
 __host__ __device__ inline uint32_t ckpt_base(uint32_t range_x, int tile) { return range_x / kSegLen + (uint32_t)tile; }
 // checkpoint slots / work items for K instances over `tiles` tiles (upper bound)
 __host__ __device__ inline size_t ckpt_slots(size_t K, int tiles) { return K / kSegLen + (size_t)tiles + 2; }
@@ -161,7 +174,7 @@ inline ImgLayout img_layout(int W, int H) {
 
 struct BinLayout {
     size_t key0, key1, pair0, pair1, slot_gauss, point_pairs, records, rec_flags, sort_hist, sort_totals, ckpt,
-        bwd_items, used, total;
+        bwd_items, used, tile_count, total;
     int sort_blocks;
     size_t nslots;  // checkpoint slots = work-item capacity / 4
 };
@@ -186,6 +199,7 @@ inline BinLayout bin_layout(int K, int num_tiles) {
     L.ckpt = o; o = align_up(o + 16 * 64 * 4 * L.nslots);  // [slot][quadrant][64] float4 (T, C)
     L.bwd_items = o; o = align_up(o + 8 * 4 * L.nslots);   // uint2 (tile, seg << 2 | quadrant)
     L.used = o; o = align_up(o + 8 * used_words(k, num_tiles));
+    L.tile_count = o; o = align_up(o + 4 * (size_t)num_tiles);  // two-level binning: instances per tile
     L.total = o;
     return L;
 }
@@ -278,9 +292,21 @@ struct EmitArgs {
     uint32_t* slot_gauss;        // K
     uint32_t* rec_flags32 = nullptr;  // K: zeroed by the emission (the backward's per-slot record flags)
     int scan_blocks;
+    // two-level binning (tile_sort_fused): per-block column counts (k_scan_reduce), their scanned
+    // form and totals, the column-ordered (Gaussian, slot) pairs, per-tile counts zeroed by block 0
+    uint32_t* xhist = nullptr;
+    uint32_t* xtotals = nullptr;
+    uint2* pairs_out = nullptr;
+    uint32_t* tile_count = nullptr;
+    int ntiles = 0;
 };
 void launch_scan_reduce(const EmitArgs& a, hipStream_t s);
 void launch_scan_emit(const EmitArgs& a, hipStream_t s);
+// two-level binning after the instance count is known: column scan + k_scan_emit_x, the row pass
+// (pairs_out/tile_key -> point_pairs, per-tile counts), ranges from the counts
+void launch_emit_fused(const EmitArgs& a, hipStream_t s);
+void launch_row_pass(const EmitArgs& a, uint32_t K, uint2* point_pairs, uint32_t* hist, int sort_blocks,
+                     uint2* ranges, hipStream_t s);
 
 // tile ranges; also zeroes the backward's per-slot record flags (u32 per slot)
 void launch_ranges(const uint32_t* sorted_tile, int K, uint2* ranges, uint32_t* rec_flags32, hipStream_t s);

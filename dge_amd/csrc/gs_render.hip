@@ -76,6 +76,7 @@ __device__ __forceinline__ uint64_t wave_location() {
 }
 
 constexpr int kRound = kBlendRound;  // list entries per round: 4 per lane
+
 constexpr int kGroup = 4;    // blend entries per unrolled step (LDS is padded to a multiple)
 constexpr int kFcmpOGT = 2;  // llvm::CmpInst::FCMP_OGT, the predicate of __builtin_amdgcn_fcmpf
 
@@ -225,13 +226,15 @@ __global__ __launch_bounds__(64, 3) void k_render_fwd(RenderArgs a) {
 
     // the round's kept entries, one array per field: a pair of consecutive entries' field is one
     // 16-B read, the operands of two packed instructions (pixel_alpha4)
-    __shared__ __attribute__((aligned(16))) float s_x[kRound + kGroup], s_y[kRound + kGroup];
-    __shared__ __attribute__((aligned(16))) float s_cx[kRound + kGroup], s_cy[kRound + kGroup], s_cz[kRound + kGroup],
-        s_op[kRound + kGroup];
-    __shared__ float4 s_rgbd[kRound + kGroup];
-    __shared__ __attribute__((aligned(16))) uint32_t s_pos[kRound + kGroup];
-    __shared__ uint32_t s_gused[kRound / kGroup + 1];  // per blend group: bit u = entry u was blended
-    __shared__ uint32_t s_id[kRound];                  // the kept entries' Gaussians (the touched bytes)
+    // (kRoundLds: the round's kept entries, the <= 7 pad slots that start its second segment on a
+    // whole blend step, the end padding and the prefetch's overshoot)
+    constexpr int kRoundLds = kRound + 4 * kGroup;
+    __shared__ __attribute__((aligned(16))) float s_x[kRoundLds], s_y[kRoundLds];
+    __shared__ __attribute__((aligned(16))) float s_cx[kRoundLds], s_cy[kRoundLds], s_cz[kRoundLds], s_op[kRoundLds];
+    __shared__ float4 s_rgbd[kRoundLds];
+    __shared__ __attribute__((aligned(16))) uint32_t s_pos[kRoundLds];
+    __shared__ uint32_t s_gused[kRoundLds / kGroup];  // per blend group: bit u = entry u was blended
+    __shared__ uint32_t s_id[kRoundLds];              // the kept entries' Gaussians (the touched bytes)
 
     const uint2 range = a.ranges[tile];
     uint64_t* used = a.used + (size_t)used_base(range.x, tile) * 4 + quad;
@@ -288,11 +291,29 @@ __global__ __launch_bounds__(64, 3) void k_render_fwd(RenderArgs a) {
     for (uint32_t b = range.x; b < range.y; b += kRound) {
         if (!__any(Ts > 0.0f)) break;
         const uint64_t r0 = a.diag ? __builtin_amdgcn_s_memtime() : 0;
-        // cull against the quadrant, compact survivors in list order (i-major, lane-minor)
-        int nk = 0;
+        // cull against the quadrant, compact survivors in list order (i-major, lane-minor); the
+        // round's second segment (positions kSegLen..) starts at slot n_mid, on a whole group, behind
+        // <= 3 pad slots that blend nothing — the checkpoint between the two segments is taken between
+        // the blend loops over them
+        int nk = 0, n_mid = 0;
         int kslot[4];  // compacted slot of this lane's entry i (-1: culled)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
+            if (i == kSegLen / 64) {
+                n_mid = (nk + kGroup - 1) & ~(kGroup - 1);
+                if (lane < n_mid - nk) {
+                    const int slot = nk + lane;
+                    s_x[slot] = 0.f;
+                    s_y[slot] = 0.f;
+                    s_cx[slot] = 0.f;
+                    s_cy[slot] = 0.f;
+                    s_cz[slot] = 0.f;
+                    s_op[slot] = 0.f;
+                    s_rgbd[slot] = make_float4(0.f, 0.f, 0.f, 0.f);
+                    s_pos[slot] = 0u;
+                }
+                nk = n_mid;
+            }
             const uint32_t k = b + 64 * i + lane;
             const bool keep = k < range.y && cull_keep(cur[i].xy, cur[i].co, (float)bx0, (float)by0);
             const uint64_t km = __ballot(keep);
@@ -337,9 +358,21 @@ __global__ __launch_bounds__(64, 3) void k_render_fwd(RenderArgs a) {
             L01 = f2v{0.f, 0.f};
             L2 = 0.f;
         }
-        seg_done = (int)((b - range.x) / kSegLen);
+        seg_done = (int)((b - range.x) / kSegLen);  // the round's first segment
+        // the round's second segment exists: its checkpoint follows the first one's at n_mid (-1: none,
+        // or taken)
+        const int n_mid_slot = n_mid;
+        if (range.y - b <= (uint32_t)kSegLen) n_mid = -1;
+        const auto take_mid = [&]() {
+            ckpt[(size_t)seg_done * 256 + lane] = make_float4(fabsf(Ts), L01.x, L01.y, L2);
+            L01 = f2v{0.f, 0.f};
+            L2 = 0.f;
+            ++seg_done;
+            n_mid = -1;
+        };
         store_words();
-        if (lane <= kRound / kGroup) s_gused[lane] = 0u;  // (groups past an early exit stay 0)
+        s_gused[lane] = 0u;  // (groups past an early exit stay 0)
+        if (lane < kRoundLds / kGroup - 64) s_gused[64 + lane] = 0u;
         __syncthreads();
 
         const uint64_t c0 = a.diag ? __builtin_amdgcn_s_memtime() : 0;
@@ -385,25 +418,34 @@ __global__ __launch_bounds__(64, 3) void k_render_fwd(RenderArgs a) {
         // head nothing is outstanding in LDS, so the compiler's waits inside count the colour reads
         // exactly instead of draining the prefetch (its loop-carried state is conservative)
         constexpr unsigned kWaitLds = 0xC07F;
-        load_alpha(0, ga);
-        __builtin_amdgcn_s_waitcnt(kWaitLds);
         // (scheduling barriers keep the compiler from merging or reordering the reads across them)
-        for (int j = 0; j < nk; j += 2 * kGroup) {
-            if (!__any(Ts > 0.0f)) break;
-            load_colour(j, cc);
-            __builtin_amdgcn_sched_barrier(0);
-            load_alpha(j + kGroup, gb);
-            __builtin_amdgcn_sched_barrier(0);
-            blend_group(j, ga, cc);
-            __builtin_amdgcn_sched_barrier(0);
-            if (j + kGroup >= nk || !__any(Ts > 0.0f)) break;
-            load_colour(j + kGroup, cc);
-            __builtin_amdgcn_sched_barrier(0);
-            load_alpha(j + 2 * kGroup, ga);
-            __builtin_amdgcn_sched_barrier(0);
-            blend_group(j + kGroup, gb, cc);
-            __builtin_amdgcn_sched_barrier(0);
-            __builtin_amdgcn_s_waitcnt(kWaitLds);  // (the prefetch of ga: issued a whole group ago)
+        const auto blend_range = [&](int j0, int j1) {
+            load_alpha(j0, ga);
+            __builtin_amdgcn_s_waitcnt(kWaitLds);
+            for (int j = j0; j < j1; j += 2 * kGroup) {
+                if (!__any(Ts > 0.0f)) break;
+                load_colour(j, cc);
+                __builtin_amdgcn_sched_barrier(0);
+                load_alpha(j + kGroup, gb);
+                __builtin_amdgcn_sched_barrier(0);
+                blend_group(j, ga, cc);
+                __builtin_amdgcn_sched_barrier(0);
+                if (j + kGroup >= j1 || !__any(Ts > 0.0f)) break;
+                load_colour(j + kGroup, cc);
+                __builtin_amdgcn_sched_barrier(0);
+                load_alpha(j + 2 * kGroup, ga);
+                __builtin_amdgcn_sched_barrier(0);
+                blend_group(j + kGroup, gb, cc);
+                __builtin_amdgcn_sched_barrier(0);
+                __builtin_amdgcn_s_waitcnt(kWaitLds);  // (the prefetch of ga: issued a whole group ago)
+            }
+        };
+        // the round's first segment, its checkpoint, the second segment: two copies of the loop, so the
+        // checkpoint costs nothing inside it (an early exit leaves the state at the first segment's end)
+        blend_range(0, n_mid >= 0 ? n_mid : nk);
+        if (n_mid >= 0) {
+            take_mid();
+            blend_range(n_mid_slot, nk);
         }
         if (a.diag) c_blend += __builtin_amdgcn_s_memtime() - c0;
         __syncthreads();
@@ -1048,19 +1090,25 @@ __device__ __forceinline__ void finish_record(float4 co, const float (&S)[9], fl
 }
 
 constexpr int kBwdGroup = 4;            // entries replayed between two reduce-scatters
-constexpr int kBwdHalf = kSegLen / 2;   // list positions per half-segment (LDS staging unit)
+constexpr int kBwdHalf = 128;           // list positions per LDS staging unit
+constexpr int kBwdNI = kSegLen / 64;    // list positions per lane
+static_assert(kSegLen % kBwdHalf == 0, "whole staging units per segment");
 
 // One wave per work item = (8x8 quadrant, segment of its window), independent
-// 64-thread workgroups.  A segment is at most kSegLen = 256 list positions: the
-// wave loads their (Gaussian, slot) pairs and the forward's blended bits (4 per
+// 64-thread workgroups.  A segment is at most kSegLen = 128 list positions: the
+// wave loads their (Gaussian, slot) pairs and the forward's blended bits (2 per
 // lane), gathers the Splats of the blended ones, and replays the segment back
-// to front in two halves of 128 positions staged through LDS (6.9 KB: with
+// to front in units of 128 positions staged through LDS (6.9 KB: with
 // <= 128 VGPRs, 4 waves per SIMD), each in groups of four entries whose nine
 // sums are reduce-scattered across the wave (quad_reduce).  Each kept entry gets
 // one record at 4*slot + quadrant (slot: the binning slot, so k_gauss_bwd reads
 // a Gaussian's records contiguously) and a flag.
 template <bool LOOP>
-__global__ __launch_bounds__(64, 4) void k_render_bwd(RenderBwdArgs a, uint32_t first_item) {
+// 5 waves per SIMD: the 128-position items need <= 96 VGPRs (no spill)
+#ifndef GS_BWD_WAVES
+#define GS_BWD_WAVES 5
+#endif
+__global__ __launch_bounds__(64, GS_BWD_WAVES) void k_render_bwd(RenderBwdArgs a, uint32_t first_item) {
     // kept entries of a half-segment, compacted back to front, + a group of padding
     // (one array per field: four consecutive entries' field is one 16-B read, see bwd_quad)
     __shared__ __attribute__((aligned(16))) float s_x[kBwdHalf + kBwdGroup], s_y[kBwdHalf + kBwdGroup];
@@ -1098,19 +1146,19 @@ __global__ __launch_bounds__(64, 4) void k_render_bwd(RenderBwdArgs a, uint32_t 
     // An entry no pixel of the quadrant blended has an all-zero gradient: the bit is the exact cull
     // (the forward's `use` is the replay's `hit && pos < n_contrib`).
     const uint32_t* used32 = reinterpret_cast<const uint32_t*>(a.used + (size_t)used_base(range.x, tile) * 4 + quad);
-    uint2 pairs[4];
+    uint2 pairs[kBwdNI];
     uint32_t kb = 0u;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < kBwdNI; ++i) {
         const int j = 64 * i + lane, k = lo + j;
         const bool in = j < n;
         pairs[i] = in ? a.point_pairs[range.x + k] : make_uint2(0u, 0u);
         const uint32_t ub = in ? used32[(size_t)(k >> 6) * 8 + ((k >> 5) & 1)] : 0u;
         kb |= ((ub >> (k & 31)) & 1u) << i;
     }
-    Entry cur[4];
+    Entry cur[kBwdNI];
 #pragma unroll
-    for (int i = 0; i < 4; ++i)  // (dropped entries gather Gaussian 0: one shared line)
+    for (int i = 0; i < kBwdNI; ++i)  // (dropped entries gather Gaussian 0: one shared line)
         cur[i] = gather_entry(a.splat, (kb >> i) & 1u ? pairs[i].x : 0u);
 
     const size_t HW = (size_t)a.W * a.H;
@@ -1155,7 +1203,7 @@ __global__ __launch_bounds__(64, 4) void k_render_bwd(RenderBwdArgs a, uint32_t 
     const bool row_writer = (lane & 15) == 0;
 
 #pragma unroll
-    for (int h = 1; h >= 0; --h) {  // back half (positions 128..255) first
+    for (int h = kSegLen / kBwdHalf - 1; h >= 0; --h) {  // back unit first
         // compact the forward's blended entries of this half back to front
         int nk = 0;
 #pragma unroll

@@ -205,7 +205,12 @@ struct RangeOut {
     uint2* ranges;
     uint32_t* tile_order;
     int ntiles;
+    // two-level binning's row pass: instances per tile (key y << 7 | x, input ordered by column x),
+    // counted in LDS for the block's first kTcCols columns, global atomics beyond
+    uint32_t* tile_count = nullptr;
+    int gx = 0;
 };
+constexpr int kTcCols = 4;
 
 // Value modes of the scatter: u32 values (IDV: the element index), or a packed
 // (Gaussian, slot) pair: built from the index and a Gaussian-per-slot array on
@@ -215,7 +220,7 @@ enum ValMode { kValU32 = 0, kValPairFirst = 1, kValPair = 2 };
 // WK: the sorted keys are written (every pass but the last tile-sort pass).  Without them the block
 // stages only the digit (u16), and the per-wave digit counters are u16 throughout (<= 256*IPT), so
 // the single-pass tile sort fits three workgroups per CU (52 KB of LDS instead of 68).
-template <int BITS, int IPT, bool IDV, int VM, bool WK = true>
+template <int BITS, int IPT, bool IDV, int VM, bool WK = true, bool TC = false>
 __global__ __launch_bounds__(256) void k_radix_scatter(const uint32_t* __restrict__ keys_in,
                                                        const void* __restrict__ vals_in_,
                                                        uint32_t* __restrict__ keys_out, void* __restrict__ vals_out_,
@@ -237,6 +242,9 @@ __global__ __launch_bounds__(256) void k_radix_scatter(const uint32_t* __restric
     __shared__ uint32_t lds4[4];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     for (int i = tid; i < 4 * NDIG; i += 256) (&cnt[0][0])[i] = 0;
+    __shared__ uint32_t s_tc[TC ? kTcCols * kXDigits : 1];  // TC: the row pass's tile counts
+    if (TC)
+        for (int i = tid; i < kTcCols * kXDigits; i += 256) s_tc[i] = 0u;
     {  // dbase = exclusive scan of the digit totals
         uint32_t loc[PER];
         uint32_t s = 0;
@@ -348,6 +356,8 @@ __global__ __launch_bounds__(256) void k_radix_scatter(const uint32_t* __restric
     using SK = typename std::conditional<WK, uint32_t, uint16_t>::type;  // staged key, or its digit
     __shared__ SK s_key[256 * IPT];
     __shared__ V s_val[256 * IPT];
+    const uint32_t b0 = blockIdx.x * (uint32_t)(256 * IPT);
+    const uint32_t x_first = TC ? keys_in[b0] & (kXDigits - 1) : 0u;  // the block's first column
 #pragma unroll
     for (int it = 0; it < IPT; ++it) {
         const uint32_t idx = base + it * 64 + lane;
@@ -356,10 +366,20 @@ __global__ __launch_bounds__(256) void k_radix_scatter(const uint32_t* __restric
             const uint32_t lp = cnt[w][d] + loc[it];
             s_key[lp] = WK ? (SK)key[it] : (SK)d;
             s_val[lp] = val[it];
+            if (TC) {
+                const uint32_t x = key[it] & (kXDigits - 1), y = key[it] >> kXBits, c = x - x_first;
+                if (c < (uint32_t)kTcCols) atomicAdd(&s_tc[c * kXDigits + y], 1u);
+                else atomicAdd(&ro.tile_count[y * (uint32_t)ro.gx + x], 1u);
+            }
         }
     }
     __syncthreads();
-    const uint32_t b0 = blockIdx.x * (uint32_t)(256 * IPT);
+    if (TC) {  // integer sums: the counts do not depend on the order
+        for (int i = tid; i < kTcCols * kXDigits; i += 256) {
+            const uint32_t v = s_tc[i];
+            if (v) atomicAdd(&ro.tile_count[(uint32_t)(i % kXDigits) * ro.gx + x_first + i / kXDigits], v);
+        }
+    }
     const int nvalid = n - b0 < (uint32_t)(256 * IPT) ? (int)(n - b0) : 256 * IPT;
     for (int i = tid; i < nvalid; i += 256) {
         const uint32_t k = s_key[i];
@@ -384,7 +404,10 @@ static void radix_pass(const uint32_t* kin, const void* vin, uint32_t* kout, voi
 #define GS_SCATTER(IDV, VM)                                                                                   \
     hipLaunchKernelGGL((k_radix_scatter<BITS, IPT, IDV, VM>), dim3(nb), dim3(256), 0, s, kin, vin, kout, vout,  \
                        gauss_by_slot, n, shift, hist, totals, nb, bm, ro, bias_not)
-    if (vm == kValPairFirst && !kout)  // the last tile-sort pass: no sorted keys
+    if (vm == kValPair && !kout)  // the two-level binning's row pass: no sorted keys
+        hipLaunchKernelGGL((k_radix_scatter<BITS, IPT, false, kValPair, false, true>), dim3(nb), dim3(256), 0, s, kin,
+                           vin, kout, vout, gauss_by_slot, n, shift, hist, totals, nb, bm, ro, bias_not);
+    else if (vm == kValPairFirst && !kout)  // the last tile-sort pass: no sorted keys
         hipLaunchKernelGGL((k_radix_scatter<BITS, IPT, true, kValPairFirst, false>), dim3(nb), dim3(256), 0, s, kin,
                            vin, kout, vout, gauss_by_slot, n, shift, hist, totals, nb, bm, ro, bias_not);
     else if (vm == kValPairFirst) GS_SCATTER(true, kValPairFirst);
@@ -484,6 +507,21 @@ __global__ __launch_bounds__(256) void k_scan_reduce(EmitArgs a) {
     uint32_t total;
     block_exclusive_scan(s, lds4, total);
     if (threadIdx.x == 0) a.scan_sums[blockIdx.x] = total;
+    if (a.xhist) {  // two-level binning: the block's instances per tile column (rect height per column)
+        __shared__ uint32_t h[kXDigits];
+        if (threadIdx.x < kXDigits) h[threadIdx.x] = 0u;
+        __syncthreads();
+#pragma unroll
+        for (int it = 0; it < kScanIPT; ++it) {
+            const uint32_t r = base + it * 256 + threadIdx.x;
+            const uint32_t q = v[it];
+            const uint32_t x0 = q & 0xFFu, y0 = (q >> 8) & 0xFFu, x1 = (q >> 16) & 0xFFu, y1 = q >> 24;
+            if (r < (uint32_t)a.P && y1 > y0)
+                for (uint32_t x = x0; x < x1; ++x) atomicAdd(&h[x], y1 - y0);
+        }
+        __syncthreads();
+        if (threadIdx.x < kXDigits) a.xhist[(size_t)blockIdx.x * kXDigits + threadIdx.x] = h[threadIdx.x];
+    }
 }
 
 // Emission in depth order: rounds of 256 Gaussians; a block scan of their
@@ -548,6 +586,176 @@ __global__ __launch_bounds__(256) void k_scan_emit(EmitArgs a) {
         base += total;
         __syncthreads();
     }
+}
+
+// Two-level binning, first level: the emission writes every instance straight
+// into its tile column's run (the first LSD pass of the tile sort, digit = x),
+// stable — instances of one column in emission (depth) order.  Each block's
+// column runs start at the scanned k_scan_reduce counts; the round's instances
+// are expanded in batches of kEmitBatch, ranked per column with 64-lane ballots
+// and per-wave counters (waves own consecutive stretches of the batch, as in
+// k_radix_scatter), staged in LDS in column-major order and stored with
+// consecutive lanes on consecutive positions of each column run.  The key
+// written is y << 7 | x (the row pass's digit and the tile's column).
+constexpr int kEmitEPT = 8, kEmitBatch = 256 * kEmitEPT;
+__global__ __launch_bounds__(256) void k_scan_emit_x(EmitArgs a) {
+    __shared__ uint32_t lds4[4];
+    __shared__ uint32_t s_start[256];
+    __shared__ uint32_t s_gauss[256];
+    __shared__ int4 s_rect[256];
+    __shared__ uint32_t s_dpos[kXDigits];   // global position of the block's next instance per column
+    __shared__ uint32_t s_gbase[kXDigits];  // the batch's column run: global position - staged position
+    __shared__ uint16_t cnt[4][kXDigits];   // per-wave column counters, then the staged run starts
+    __shared__ uint16_t s_key[kEmitBatch];
+    __shared__ uint2 s_pair[kEmitBatch];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    if (blockIdx.x == 0)
+        for (int t = tid; t < a.ntiles; t += 256) a.tile_count[t] = 0u;  // (the row pass counts into it)
+    uint32_t base;
+    {
+        uint32_t part = 0;
+        for (uint32_t j = tid; j < blockIdx.x; j += 256) part += a.scan_sums[j];
+        block_exclusive_scan(part, lds4, base);
+    }
+    {
+        const uint32_t tv = tid < kXDigits ? a.xtotals[tid] : 0u;
+        uint32_t all;
+        const uint32_t run = block_exclusive_scan(tv, lds4, all);
+        if (tid < kXDigits) s_dpos[tid] = run + a.xhist[(size_t)blockIdx.x * kXDigits + tid];
+    }
+    for (int i = tid; i < 4 * kXDigits; i += 256) (&cnt[0][0])[i] = 0;
+    __syncthreads();
+    const uint32_t r_block = blockIdx.x * (uint32_t)kScanTile;
+    for (int it = 0; it < kScanIPT; ++it) {
+        const uint32_t r = r_block + it * 256 + tid;
+        const uint2 gr = r < (uint32_t)a.P ? a.order[r] : make_uint2(0u, 0u);
+        const uint32_t g = gr.y;
+        const uint32_t c = rect_count(gr.x, 1);
+        uint32_t total;
+        const uint32_t off = block_exclusive_scan(c, lds4, total);
+        if (c) {
+            a.first_slot[g] = base + off;
+            s_rect[tid] = make_int4((int)(gr.x & 0xFFu), (int)((gr.x >> 8) & 0xFFu),
+                                    (int)((gr.x >> 16) & 0xFFu) - (int)(gr.x & 0xFFu), 0);
+        }
+        s_start[tid] = off;
+        s_gauss[tid] = g;
+        __syncthreads();
+        for (uint32_t j0 = 0; j0 < total; j0 += kEmitBatch) {
+            const uint32_t nb = total - j0 < (uint32_t)kEmitBatch ? total - j0 : (uint32_t)kEmitBatch;
+            uint32_t kk[kEmitEPT], loc[kEmitEPT];
+            uint2 pv[kEmitEPT];
+#pragma unroll
+            for (int e = 0; e < kEmitEPT; ++e) {
+                const uint32_t jj = (uint32_t)(w * 64 * kEmitEPT + e * 64 + lane);
+                const bool valid = jj < nb;
+                const uint64_t vm = __ballot(valid);
+                if (vm == 0) break;
+                const uint32_t j = j0 + (valid ? jj : 0u);
+                int lo = 0, hi = 255;  // owner: the last entry with start <= j (see k_scan_emit)
+                while (lo < hi) {
+                    const int mid = (lo + hi + 1) >> 1;
+                    if (s_start[mid] <= j) lo = mid;
+                    else hi = mid - 1;
+                }
+                const int4 q = s_rect[lo];
+                const uint32_t k = j - s_start[lo];
+                const uint32_t ky = (uint32_t)(((float)k + 0.5f) / (float)q.z);  // exact: k < 2^20
+                const uint32_t kx = k - ky * (uint32_t)q.z;
+                const uint32_t x = (uint32_t)q.x + kx, y = (uint32_t)q.y + ky;
+                kk[e] = y << kXBits | x;
+                pv[e] = make_uint2(s_gauss[lo], base + j);
+                if (valid && a.rec_flags32) a.rec_flags32[base + j] = 0u;  // (slot order: coalesced)
+                const uint32_t d = valid ? x : 0u;
+                const uint64_t peers = match_digit<kXBits>(d, vm);
+                const uint32_t rank = (uint32_t)__popcll(peers & lanemask_lt());
+                const uint32_t old = cnt[w][d];
+                loc[e] = old + rank;
+                if (valid && rank == 0) cnt[w][d] = (uint16_t)(old + (uint32_t)__popcll(peers));
+            }
+            __syncthreads();
+            {   // staged column runs of the batch (wave-major inside a column), their global bases
+                uint32_t c0 = 0, c1 = 0, c2 = 0, tot = 0;
+                if (tid < kXDigits) {
+                    c0 = cnt[0][tid];
+                    c1 = cnt[1][tid];
+                    c2 = cnt[2][tid];
+                    tot = c0 + c1 + c2 + cnt[3][tid];
+                }
+                uint32_t all;
+                const uint32_t run = block_exclusive_scan(tot, lds4, all);
+                if (tid < kXDigits) {
+                    cnt[0][tid] = (uint16_t)run;
+                    cnt[1][tid] = (uint16_t)(run + c0);
+                    cnt[2][tid] = (uint16_t)(run + c0 + c1);
+                    cnt[3][tid] = (uint16_t)(run + c0 + c1 + c2);
+                    s_gbase[tid] = s_dpos[tid] - run;
+                    s_dpos[tid] += tot;
+                }
+            }
+            __syncthreads();
+#pragma unroll
+            for (int e = 0; e < kEmitEPT; ++e) {
+                const uint32_t jj = (uint32_t)(w * 64 * kEmitEPT + e * 64 + lane);
+                if (jj < nb) {
+                    const uint32_t lp = cnt[w][kk[e] & (kXDigits - 1)] + loc[e];
+                    s_key[lp] = (uint16_t)kk[e];
+                    s_pair[lp] = pv[e];
+                }
+            }
+            __syncthreads();
+            for (uint32_t i = tid; i < nb; i += 256) {
+                const uint32_t kv = s_key[i];
+                const uint32_t pos = s_gbase[kv & (kXDigits - 1)] + i;
+                a.tile_key[pos] = kv;
+                a.pairs_out[pos] = s_pair[i];
+            }
+            for (int i = tid; i < 4 * kXDigits; i += 256) (&cnt[0][0])[i] = 0;
+            __syncthreads();
+        }
+        base += total;
+        __syncthreads();
+    }
+}
+
+// Tile ranges from the per-tile instance counts (one workgroup): an exclusive
+// scan in tile order — the ranges identifyTileRanges (rasterizer_impl.cu:105-125)
+// finds in the sorted keys; empty tiles keep (0, 0).
+__global__ __launch_bounds__(256) void k_ranges_counts(const uint32_t* __restrict__ count, int tiles,
+                                                       uint2* __restrict__ ranges) {
+    __shared__ uint32_t lds4[4];
+    const int per = (tiles + 255) / 256, t0 = threadIdx.x * per;
+    uint32_t s = 0;
+    for (int i = 0; i < per; ++i)
+        if (t0 + i < tiles) s += count[t0 + i];
+    uint32_t all;
+    uint32_t run = block_exclusive_scan(s, lds4, all);
+    for (int i = 0; i < per; ++i) {
+        const int t = t0 + i;
+        if (t < tiles) {
+            const uint32_t c = count[t];
+            ranges[t] = c ? make_uint2(run, run + c) : make_uint2(0u, 0u);
+            run += c;
+        }
+    }
+}
+
+void launch_emit_fused(const EmitArgs& a, hipStream_t s) {
+    if (a.P <= 0) return;
+    // first level: column totals and each block's column offsets, then the column-ordered emission
+    hipLaunchKernelGGL(k_radix_digit_scan, dim3(kXDigits / kScanDigits), dim3(1024), 0, s, a.xhist, a.scan_blocks,
+                       kXDigits, a.xtotals);
+    hipLaunchKernelGGL(k_scan_emit_x, dim3(a.scan_blocks), dim3(256), 0, s, a);
+}
+
+void launch_row_pass(const EmitArgs& a, uint32_t K, uint2* point_pairs, uint32_t* hist, int sort_blocks,
+                     uint2* ranges, hipStream_t s) {
+    if (a.P <= 0 || K == 0) return;
+    // second level: the stable row pass (digit y), counting instances per tile on the way
+    RangeOut ro{nullptr, nullptr, a.ntiles, a.tile_count, a.gx};
+    radix_pass<kXBits, kSortIPT>(a.tile_key, a.pairs_out, nullptr, point_pairs, nullptr, K, kXBits, false, kValPair,
+                                 hist, a.xtotals, sort_blocks, ro, nullptr, s);
+    hipLaunchKernelGGL(k_ranges_counts, dim3(1), dim3(256), 0, s, a.tile_count, a.ntiles, ranges);
 }
 
 void launch_scan_reduce(const EmitArgs& a, hipStream_t s) {

@@ -581,6 +581,24 @@ def test_forced_32bit_depth_keys_match_30bit_path(cuda_device, monkeypatch):
         np.testing.assert_array_equal(forced[k], base[k], err_msg=k)
 
 
+@pytest.mark.parametrize("P,W,H", [(3_000, 1920, 1080), (300_000, 1920, 1080), (200_000, 2048, 1040)])
+def test_two_level_binning_matches_two_pass_sort(cuda_device, monkeypatch, P, W, H):
+    """Grids over 2048 tiles (c4: 120 x 68) bin in two levels — the emission writes the instances in
+    tile-column order, one row pass follows, ranges come from per-tile counts; DGE_AMD_TILE_SORT=2pass
+    runs the emission + two full tile-sort passes + k_ranges instead.  Lists, ranges, the image and
+    every gradient are bitwise the same (3k Gaussians: sort blocks spanning many tile columns, whose
+    counts go through the global atomics; 2048 x 1040: the widest grid, 128 columns)."""
+    a = scene_arrays(P, seed=6, radius=2.0, scale=0.02)
+    g = np.random.default_rng(8).standard_normal((3, H, W)).astype(np.float32) * 1e-3
+    s = camera_settings(W, H, device="cuda")
+    fused = run_gpu(s, g, **_sh_kw(a))
+    monkeypatch.setenv("DGE_AMD_TILE_SORT", "2pass")
+    ref = run_gpu(s, g, **_sh_kw(a))
+    assert fused["num_rendered"] == ref["num_rendered"] > 0
+    for k in ("ranges", "point_list", "n_contrib", "color", "final_T") + tuple(GRAD_NAMES):
+        np.testing.assert_array_equal(fused[k], ref[k], err_msg=k)
+
+
 @pytest.mark.parametrize("env", [{"DGE_AMD_BWD_GRID_CAP": "3"}, {"DGE_AMD_BWD": "tile"},
                                  {"DGE_AMD_BWD": "tile", "DGE_AMD_BWD_GRID_CAP": "8"}])
 def test_backward_variants_match_default(cuda_device, tmp_path, env):
