@@ -134,6 +134,11 @@ inline GeomLayout geom_layout(int P) {
 // ckpt_base(t) = range.x / kSegLen + t (monotone and non-overlapping because
 // ranges are a prefix sum), each slot 4 quadrants x 64 pixels x float4.
 constexpr int kBlendRound = 256;  // list entries per blend round
+// Replay work items are listed by class of their blended-entry count, heaviest first (the hardware
+// dispatches workgroups in order: the longest items start first, the short ones fill the end);
+// class c holds up to item_cap items at bwd_items[c * item_cap ..), counted in bwd_count[item_count_at(c)]
+constexpr int kItemClasses = 4, kItemCount0 = 32;
+__host__ __device__ inline int item_count_at(int c) { return kItemCount0 * (1 + c); }  // u32 index, 128-B lines
 // backward segment length: checkpoints at every round boundary and mid-round, so a replay work item
 // covers at most 128 positions (half the per-item work of round-long segments: the replay's wave
 // durations pack onto the SIMDs instead of leaving a tail of long items)
@@ -167,7 +172,8 @@ inline ImgLayout img_layout(int W, int H) {
     L.ranges = o; o = align_up(o + 8 * tiles);
     L.tile_last = o; o = align_up(o + 4 * tiles);
     L.quad_last = o; o = align_up(o + 16 * tiles);
-    L.bwd_count = o; o = align_up(o + 16);  // [0] multi-segment items, [1] single
+    L.bwd_count = o; o = align_up(o + 4 * (size_t)item_count_at(kItemClasses));  // [0..3] the per-tile variant's;
+                                                                                 // [item_count_at(c)] class c items
     L.total = o;
     return L;
 }
@@ -197,7 +203,7 @@ inline BinLayout bin_layout(int K, int num_tiles) {
     L.sort_totals = o; o = align_up(o + 4 * ((size_t)1 << maxbits));
     L.nslots = ckpt_slots(k, num_tiles);
     L.ckpt = o; o = align_up(o + 16 * 64 * 4 * L.nslots);  // [slot][quadrant][64] float4 (T, C)
-    L.bwd_items = o; o = align_up(o + 8 * 4 * L.nslots);   // uint2 (tile, seg << 2 | quadrant)
+    L.bwd_items = o; o = align_up(o + 8 * 4 * L.nslots * kItemClasses);  // uint2 (tile, seg << 2 | quadrant)
     L.used = o; o = align_up(o + 8 * used_words(k, num_tiles));
     L.tile_count = o; o = align_up(o + 4 * (size_t)num_tiles);  // two-level binning: instances per tile
     L.total = o;

@@ -205,6 +205,21 @@ __global__ __launch_bounds__(1024) void k_tile_order(const uint2* __restrict__ r
     }
 }
 
+// The replay's work items of a quadrant: one per 128-position segment of its window, all in the class
+// of the quadrant's kept entries per segment (heaviest class first: the hardware dispatches
+// workgroups in order, so the longest items start first and the short ones fill the end).  One atomic
+// per wave, each class's counter on its own cache line (same-address atomics serialise).
+__device__ __forceinline__ int item_class(uint32_t kept) { return kept >= 64 ? 0 : kept >= 40 ? 1 : kept >= 20 ? 2 : 3; }
+__device__ __forceinline__ void emit_items(const RenderArgs& a, int tile, int quad, uint32_t nseg, uint32_t nkept,
+                                           int lane) {
+    const int c = item_class(nkept / nseg);
+    uint32_t base = 0;
+    if (lane == 0) base = atomicAdd(&a.bwd_count[item_count_at(c)], nseg);
+    base = __shfl(base, 0);
+    for (uint32_t k = lane; k < nseg; k += 64)
+        a.bwd_items[(size_t)c * a.item_cap + base + k] = make_uint2((uint32_t)tile, (k << 2) | (uint32_t)quad);
+}
+
 __global__ __launch_bounds__(64, 3) void k_render_fwd(RenderArgs a) {
     // XCD-aware: blocks b, b+8, b+16, b+24 (one XCD under the round-robin dealing) take the four
     // quadrants of one tile, so the tile's list and its Splat gathers are fetched into one L2;
@@ -478,18 +493,9 @@ __global__ __launch_bounds__(64, 3) void k_render_fwd(RenderArgs a) {
         a.out_depth[pix] = C2D.y;
     }
     const uint32_t m = wave_max_u32(inside ? last : 0u);
-    if (m) {  // the backward replay's work items for this quadrant: (tile, segment << 2 | quadrant)
-        const uint32_t nseg = (m + kSegLen - 1) / kSegLen;
-        if (nseg > 1) {  // multi-segment windows at the front of the list: they dispatch first
-            uint32_t base = 0;
-            if (lane == 0) base = atomicAdd(&a.bwd_count[0], nseg);
-            base = __shfl(base, 0);
-            for (uint32_t k = lane; k < nseg; k += 64) a.bwd_items[base + k] = make_uint2(tile, (k << 2) | quad);
-        } else if (lane == 0) {
-            const uint32_t b = atomicAdd(&a.bwd_count[1], 1u);
-            a.bwd_items[a.item_cap - 1 - b] = make_uint2(tile, quad);
-        }
-    }
+    // (item class from the entries the cull kept — the diagnostics' count, live anyway: a blended-entry
+    // count here pushed the kernel into spilling)
+    if (m) emit_items(a, tile, quad, (m + kSegLen - 1) / kSegLen, diag_kept, lane);
     if (lane == 0) {
         a.quad_last[qidx] = m;
         if (m) atomicMax(&a.tile_last[tile], m);
@@ -874,17 +880,9 @@ __global__ __launch_bounds__(128, 4) void k_render_fwd_pc(RenderArgs a) {
         a.out_depth[pix] = C2D.y;
     }
     const uint32_t m = wave_max_u32(inside ? last : 0u);
-    if (m) {  // the backward replay's work items for this quadrant (as k_render_fwd)
+    if (m) {  // multi-segment windows first (class 0), single segments last
         const uint32_t nseg = (m + kSegLen - 1) / kSegLen;
-        if (nseg > 1) {
-            uint32_t base = 0;
-            if (lane == 0) base = atomicAdd(&a.bwd_count[0], nseg);
-            base = __shfl(base, 0);
-            for (uint32_t k = lane; k < nseg; k += 64) a.bwd_items[base + k] = make_uint2(tile, (k << 2) | quad);
-        } else if (lane == 0) {
-            const uint32_t b = atomicAdd(&a.bwd_count[1], 1u);
-            a.bwd_items[a.item_cap - 1 - b] = make_uint2(tile, quad);
-        }
+        emit_items(a, tile, quad, nseg, nseg > 1 ? 128u * nseg : 0u, lane);
     }
     if (lane == 0) {
         a.quad_last[qidx] = m;
@@ -1094,6 +1092,10 @@ constexpr int kBwdHalf = 128;           // list positions per LDS staging unit
 constexpr int kBwdNI = kSegLen / 64;    // list positions per lane
 static_assert(kSegLen % kBwdHalf == 0, "whole staging units per segment");
 
+// 5 waves per SIMD: the 128-position items need <= 96 VGPRs (no spill)
+#ifndef GS_BWD_WAVES
+#define GS_BWD_WAVES 5
+#endif
 // One wave per work item = (8x8 quadrant, segment of its window), independent
 // 64-thread workgroups.  A segment is at most kSegLen = 128 list positions: the
 // wave loads their (Gaussian, slot) pairs and the forward's blended bits (2 per
@@ -1104,10 +1106,6 @@ static_assert(kSegLen % kBwdHalf == 0, "whole staging units per segment");
 // one record at 4*slot + quadrant (slot: the binning slot, so k_gauss_bwd reads
 // a Gaussian's records contiguously) and a flag.
 template <bool LOOP>
-// 5 waves per SIMD: the 128-position items need <= 96 VGPRs (no spill)
-#ifndef GS_BWD_WAVES
-#define GS_BWD_WAVES 5
-#endif
 __global__ __launch_bounds__(64, GS_BWD_WAVES) void k_render_bwd(RenderBwdArgs a, uint32_t first_item) {
     // kept entries of a half-segment, compacted back to front, + a group of padding
     // (one array per field: four consecutive entries' field is one 16-B read, see bwd_quad)
@@ -1119,13 +1117,25 @@ __global__ __launch_bounds__(64, GS_BWD_WAVES) void k_render_bwd(RenderBwdArgs a
     __shared__ uint32_t s_pos[kBwdHalf + kBwdGroup];
     __shared__ uint2 s_pair[kBwdHalf + kBwdGroup];  // (Gaussian, slot) of the kept entries: the record writes
     const int lane = threadIdx.x;
-    // block -> work item (quadrant, segment) of the forward's list, multi-segment windows first:
+    // block -> work item (quadrant, segment) of the forward's list, heaviest class first:
     // first_item + blockIdx.x (LOOP: then + gridDim.x while items remain); blocks past the list's end
     // exit (they dispatch after every real item; see launch_render_backward for the grid).  (A
     // persistent-wave work queue measured slower than the hardware dispatcher here.)
-    const uint32_t n_multi = a.bwd_count[0], n_items = n_multi + a.bwd_count[1];
+    uint32_t n_cls[kItemClasses], n_items = 0;
+#pragma unroll
+    for (int c = 0; c < kItemClasses; ++c) {
+        n_cls[c] = a.bwd_count[item_count_at(c)];
+        n_items += n_cls[c];
+    }
     for (uint32_t qi = first_item + blockIdx.x; qi < n_items; qi += gridDim.x) {
-    const uint2 item = qi < n_multi ? a.bwd_items[qi] : a.bwd_items[a.item_cap - 1 - (qi - n_multi)];
+    uint32_t cls = 0, idx = qi;  // class regions in order: heaviest items first
+#pragma unroll
+    for (int c = 0; c < kItemClasses - 1; ++c)
+        if (cls == (uint32_t)c && idx >= n_cls[c]) {
+            idx -= n_cls[c];
+            cls = c + 1;
+        }
+    const uint2 item = a.bwd_items[(size_t)cls * a.item_cap + idx];
     const int tile = (int)item.x, quad = (int)(item.y & 3u), seg = (int)(item.y >> 2);
     const int qidx = 4 * tile + quad;
     const int tx = tile % a.gx, ty = tile / a.gx;
