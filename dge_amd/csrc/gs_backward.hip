@@ -426,16 +426,7 @@ __global__ __launch_bounds__(kGB) void k_gauss_live(GaussBwdArgs a) {
     const uint32_t acc = a.acc;
     const int src = in && a.index ? a.index[idx] : idx;
     if (in && !live) {
-        if (a.dL_dconic)
-#pragma unroll
-            for (int k = 0; k < 3; ++k) a.dL_dconic[3 * (size_t)idx + k] = 0.f;
-        if (!(acc & GS_ACC_MEANS2D))
-#pragma unroll
-            for (int k = 0; k < 3; ++k) a.dL_dmeans2D[3 * (size_t)idx + k] = 0.f;
         if (!(acc & GS_ACC_OPACITY)) a.dL_dopacity[src] = 0.f;
-        if (a.dL_dcolors && !(acc & GS_ACC_COLORS))
-#pragma unroll
-            for (int k = 0; k < 3; ++k) a.dL_dcolors[3 * (size_t)idx + k] = 0.f;
         if (!(acc & GS_ACC_MEANS3D))
 #pragma unroll
             for (int k = 0; k < 3; ++k) a.dL_dmeans3D[3 * (size_t)src + k] = 0.f;
@@ -456,9 +447,24 @@ __global__ __launch_bounds__(kGB) void k_gauss_live(GaussBwdArgs a) {
             }
         }
     }
+    // the Gaussian-indexed 3-float outputs of the block's dead Gaussians, coalesced over the block's
+    // region (one 4-B store per lane and element instead of three strided stores per Gaussian: PMC
+    // write traffic of this kernel 60 -> ~15 MB at c2)
+    __syncthreads();  // s_live
+    {
+        float* z3[3] = {a.dL_dconic, !(acc & GS_ACC_MEANS2D) ? a.dL_dmeans2D : nullptr,
+                        !(acc & GS_ACC_COLORS) ? a.dL_dcolors : nullptr};
+#pragma unroll
+        for (int t = 0; t < 3; ++t) {
+            float* g = z3[t];
+            if (!g) continue;
+            g += 3 * (size_t)idx0;
+            for (int e = threadIdx.x; e < 3 * nrow; e += kGB)
+                if (!s_live[e / 3]) g[e] = 0.f;
+        }
+    }
     if (a.dsh.dc && !(acc & GS_ACC_SH) && a.M > 1 && !a.index) {
         // rest rows of the block's dead Gaussians, coalesced over the block's region
-        __syncthreads();  // s_live
         const int ncol = (a.M - 1) * 3;
         const int stride = a.dsh.rest_stride;
         float* g = a.dsh.rest + (size_t)idx0 * stride;
