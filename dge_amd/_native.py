@@ -15,7 +15,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("DGE_AMD_LIB") or os.path.join(_HERE, "lib", "libgs_raster.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "gs_raster.h")
 
-ABI_VERSION = 8  # GS_RASTER_ABI_VERSION of include/gs_raster.h this binding is written against
+ABI_VERSION = 9  # GS_RASTER_ABI_VERSION of include/gs_raster.h this binding is written against
 
 GS_OK = 0
 GS_ERR_INVALID_ARG = 1
@@ -135,6 +135,8 @@ SIGNATURES = {
     "gs_rasterize_forward_end": (ctypes.c_int, [ctypes.c_void_p, _fp, _fp, ALLOC_FN, ctypes.c_void_p, ctypes.c_void_p,
                                                  ctypes.POINTER(ctypes.c_int)]),
     "gs_rasterize_forward_release": (None, [ctypes.c_void_p]),
+    "gs_rasterize_forward_begin_multi": (ctypes.c_int, [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                                         ALLOC_FN, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "gs_rasterize_backward_ex": (ctypes.c_int, [ctypes.POINTER(GsSettings), ctypes.POINTER(GsParams), ctypes.c_int,
                                                  _fp, _fp, _fp, _fp, _fp, ctypes.POINTER(GsGrads), ctypes.c_void_p]),
     "gs_mark_visible": (ctypes.c_int, [ctypes.c_int, _fp, _fp, _fp, _fp, ctypes.c_void_p]),

@@ -331,13 +331,15 @@ struct FwdState {
 };
 
 // First half of the forward: buffers, preprocess, counter read-back, depth
-// sort, instance scan (rasterizer_impl.cu:179-239 up to the num_rendered copy).
-int bin_begin(FwdState& f, int copy_colors, gs_alloc_fn alloc, void* ctx, hipStream_t stream) {
+// sort, instance scan (rasterizer_impl.cu:179-239 up to the num_rendered copy),
+// in three steps so several views can share one preprocess launch
+// (gs_rasterize_forward_begin_multi): bin_prepare (buffers, counter memset,
+// the preprocess arguments), the preprocess, bin_after_preprocess.
+int bin_prepare(FwdState& f, int copy_colors, gs_alloc_fn alloc, void* ctx, hipStream_t stream) {
     const gs_settings* s = &f.s;
     const Grid& g = f.g;
     const gs_params& gp = f.gp;
     const int P = gp.P;
-    const bool debug = s->debug != 0;
     const GeomLayout gl = geom_layout(P);
     const ImgLayout il = img_layout(g.W, g.H);
     void* geom = alloc(ctx, 0, gl.total);
@@ -370,9 +372,19 @@ int bin_begin(FwdState& f, int copy_colors, gs_alloc_fn alloc, void* ctx, hipStr
     pa.rect_packed = rect_packable(g.gx, g.gy) ? 1 : 0;
     pa.counters = counters;
     pa.touched = at<uint8_t>(geom, gl.touched);
-    { StageScope sc(ST_PREPROCESS, stream); launch_preprocess(pa, stream); }
-    GS_LAUNCHED("preprocess");
+    return GS_OK;
+}
 
+int bin_after_preprocess(FwdState& f, hipStream_t stream) {
+    const gs_settings* s = &f.s;
+    const Grid& g = f.g;
+    const int P = f.gp.P;
+    const bool debug = s->debug != 0;
+    const GeomLayout gl = geom_layout(P);
+    const ImgLayout il = img_layout(g.W, g.H);
+    void* geom = f.geom;
+    uint32_t* counters = at<uint32_t>(f.img, il.counters);
+    PreprocessArgs& pa = f.pa;
     int rc = staging_acquire(&f.st);
     if (rc) return rc;
     GS_HIP(hipMemcpyAsync(f.st->host, counters, 4 * kCounterSlots * kCounterStride, hipMemcpyDeviceToHost, stream));
@@ -403,6 +415,15 @@ int bin_begin(FwdState& f, int copy_colors, gs_alloc_fn alloc, void* ctx, hipStr
     { StageScope sc(ST_SCAN, stream); launch_scan_reduce(ea, stream); }
     GS_LAUNCHED("instance scan");
     return GS_OK;
+}
+
+int bin_begin(FwdState& f, int copy_colors, gs_alloc_fn alloc, void* ctx, hipStream_t stream) {
+    const bool debug = f.s.debug != 0;
+    int rc = bin_prepare(f, copy_colors, alloc, ctx, stream);
+    if (rc) return rc;
+    { StageScope sc(ST_PREPROCESS, stream); launch_preprocess(f.pa, stream); }
+    GS_LAUNCHED("preprocess");
+    return bin_after_preprocess(f, stream);
 }
 
 // Second half: wait for the instance count (the reference's one host sync,
@@ -661,6 +682,89 @@ int gs_rasterize_forward_begin(const gs_settings* s, const gs_params* gp, int* r
             if (rc) return rc;
         }
         *state = st.release();
+        return GS_OK;
+    } catch (const std::exception& e) {
+        return set_error(GS_ERR_INVALID_ARG, "exception: %s", e.what());
+    } catch (...) {
+        return set_error(GS_ERR_INVALID_ARG, "unknown exception");
+    }
+}
+
+// Per-call events ordering the shared preprocess between the views' streams (a small pool per thread).
+hipEvent_t multi_event(int i) {
+    thread_local hipEvent_t ev[2 * kMaxViews] = {};
+    if (!ev[i] && hipEventCreateWithFlags(&ev[i], hipEventDisableTiming) != hipSuccess) return nullptr;
+    return ev[i];
+}
+
+bool same_scene(const gs_params& a, const gs_params& b) {
+    return a.P == b.P && a.M == b.M && a.means3D == b.means3D && a.sh_dc == b.sh_dc && a.sh_rest == b.sh_rest &&
+           a.sh_dc_stride == b.sh_dc_stride && a.sh_rest_stride == b.sh_rest_stride && a.sh_half == b.sh_half &&
+           a.colors_precomp == b.colors_precomp && a.opacities == b.opacities && a.scales == b.scales &&
+           a.rotations == b.rotations && a.cov3D_precomp == b.cov3D_precomp && a.index == b.index &&
+           a.activation == b.activation;
+}
+
+int gs_rasterize_forward_begin_multi(int n, const gs_settings* const* s, const gs_params* const* gp, int* const* radii,
+                                     gs_alloc_fn alloc, void* const* alloc_ctx, const gs_stream_t* streams,
+                                     gs_forward_state** states) {
+    if (n < 1 || n > kMaxViews || !s || !gp || !radii || !alloc || !alloc_ctx || !streams || !states)
+        return set_error(GS_ERR_INVALID_ARG, "begin_multi: 1 <= n <= %d views and every array are required", kMaxViews);
+    for (int v = 0; v < n; ++v) states[v] = nullptr;
+    bool shared = gp[0]->P > 0 && !gp[0]->sh_half && !gp[0]->index;
+    for (int v = 0; v < n && shared; ++v) {
+        shared = same_scene(*gp[0], *gp[v]) && !s[v]->debug;
+        if (v && (s[v]->image_width != s[0]->image_width || s[v]->image_height != s[0]->image_height)) shared = false;
+    }
+    if (!shared) {  // the per-view calls (identical outputs)
+        for (int v = 0; v < n; ++v) {
+            const int rc = gs_rasterize_forward_begin(s[v], gp[v], radii[v], alloc, alloc_ctx[v], streams[v], &states[v]);
+            if (rc) {
+                for (int u = 0; u < v; ++u) gs_rasterize_forward_release(states[u]);
+                for (int u = 0; u < n; ++u) states[u] = nullptr;
+                return rc;
+            }
+        }
+        return GS_OK;
+    }
+    try {
+        std::unique_ptr<gs_forward_state> st[kMaxViews];
+        PreprocessMulti m;
+        m.nv = n;
+        hipStream_t s0 = (hipStream_t)streams[0];
+        const bool debug = false;
+        hipStream_t stream = s0;  // (GS_LAUNCHED)
+        for (int v = 0; v < n; ++v) {
+            int rc = validate_params(s[v], gp[v]);
+            if (rc) return rc;
+            st[v].reset(new gs_forward_state());
+            FwdState& f = st[v]->f;
+            f.s = *s[v];
+            f.gp = *gp[v];
+            f.g = make_grid(s[v]);
+            f.radii = radii[v];
+            rc = bin_prepare(f, 1, alloc, alloc_ctx[v], (hipStream_t)streams[v]);
+            if (rc) return rc;
+            m.a[v] = f.pa;
+            if (v && streams[v] != streams[0]) {  // the shared pass writes view v's buffers after their zeroing
+                hipEvent_t e = multi_event(v);
+                if (!e) return set_error(GS_ERR_HIP, "begin_multi: event");
+                GS_HIP(hipEventRecord(e, (hipStream_t)streams[v]));
+                GS_HIP(hipStreamWaitEvent(s0, e, 0));
+            }
+        }
+        { StageScope sc(ST_PREPROCESS, s0); launch_preprocess_multi(m, s0); }
+        GS_LAUNCHED("preprocess (views)");
+        hipEvent_t done = multi_event(kMaxViews);
+        if (!done) return set_error(GS_ERR_HIP, "begin_multi: event");
+        GS_HIP(hipEventRecord(done, s0));
+        for (int v = 0; v < n; ++v) {
+            hipStream_t sv = (hipStream_t)streams[v];
+            if (sv != s0) GS_HIP(hipStreamWaitEvent(sv, done, 0));
+            const int rc = bin_after_preprocess(st[v]->f, sv);
+            if (rc) return rc;
+        }
+        for (int v = 0; v < n; ++v) states[v] = st[v].release();
         return GS_OK;
     } catch (const std::exception& e) {
         return set_error(GS_ERR_INVALID_ARG, "exception: %s", e.what());

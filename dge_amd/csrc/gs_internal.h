@@ -251,6 +251,13 @@ struct PreprocessArgs {
     uint8_t* touched;    // zeroed here: k_render_fwd sets the bytes of Gaussians some pixel blends
 };
 void launch_preprocess(const PreprocessArgs& a, hipStream_t s);
+// several views of one scene, the shared inputs read once (fp32 SH rows, no index): gs_rasterize_forward_begin_multi
+constexpr int kMaxViews = 4;
+struct PreprocessMulti {
+    PreprocessArgs a[kMaxViews];
+    int nv;
+};
+void launch_preprocess_multi(const PreprocessMulti& m, hipStream_t s);
 void launch_depth_keys32(int P, const uint32_t* rect, const Splat* splat, uint32_t* key, hipStream_t s);
 void launch_mark_visible(int P, const float* means3D, const float* view, uint8_t* present, hipStream_t s);
 

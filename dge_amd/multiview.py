@@ -24,6 +24,8 @@ from typing import Sequence
 
 import ctypes
 
+import os
+
 import torch
 import torch.distributed as dist
 
@@ -284,6 +286,13 @@ def _touched_rows(prep):
     return geom[off:off + prep.P]
 
 
+# DGE_AMD_MULTI_BEGIN=1: every view's first half from ONE gs_rasterize_forward_begin_multi call (the scene read
+# once by a shared preprocess pass).  Opt-in: bitwise the same outputs, but measured no faster at c2
+# (2130-2164 vs 2195-2218 renders/s, profiles/r02/ab_multi_begin.log) — the three per-view preprocess
+# kernels overlap each other, the shared pass delays every view's depth sort behind all three projections.
+_MULTI_BEGIN = os.environ.get("DGE_AMD_MULTI_BEGIN", "0") == "1"
+
+
 def render_views(cameras, pc, pipe, bg_color, streams: int = 2, threads: bool = False, stagger: bool = False,
                  **kw):
     """render() of every camera, the views spread round-robin over `streams` HIP streams.
@@ -327,7 +336,17 @@ def render_views(cameras, pc, pipe, bg_color, streams: int = 2, threads: bool = 
     # standard models: every view's first half (preprocess, depth sort, instance scan) is enqueued before
     # the host waits for any view's instance count; then each view is finished in turn
     begun = None
-    if _fused_ok(pc, pipe):
+    if (_fused_ok(pc, pipe) and not stagger and len(cameras) <= len(pool) and not threads and _MULTI_BEGIN
+            and kw.get("override_color") is None):
+        # one native call for every view's first half: the scene's parameters are read once by a shared
+        # preprocess pass (gs_rasterize_forward_begin_multi), each view's sort and scan on its own stream
+        from .gaussian_renderer import _fused_begin_multi
+
+        vs = pool[:len(cameras)]
+        for s in vs:
+            s.wait_event(ready)
+        begun = _fused_begin_multi(cameras, pc, pipe, bg_color, vs, kw.get("scaling_modifier", 1.0))
+    elif _fused_ok(pc, pipe):
         begun = []
         prev = ready
         for i, cam in enumerate(cameras):

@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define GS_RASTER_ABI_VERSION 8
+#define GS_RASTER_ABI_VERSION 9
 
 #define GS_OK 0
 #define GS_ERR_INVALID_ARG 1   /* AT_ERROR / std::runtime_error in the reference */
@@ -204,6 +204,18 @@ int gs_rasterize_forward_begin(const gs_settings *s, const gs_params *g, int *ra
 int gs_rasterize_forward_end(gs_forward_state *state, float *out_color, float *out_depth, gs_alloc_fn alloc,
                              void *alloc_ctx, gs_stream_t stream, int *num_rendered);
 void gs_rasterize_forward_release(gs_forward_state *state);
+/* The first halves of n <= 4 views of ONE scene (g[v] name the same parameter tensors; only
+ * g[v]->visible_out may differ), view v on streams[v], one state per view for _end: the views'
+ * buffers are allocated and their counters zeroed on their streams, one preprocess pass reads
+ * every Gaussian's parameters once and projects it into all n views (on streams[0], ordered after
+ * the other streams' zeroing; they wait for it), then each view's counter read-back, depth sort
+ * and instance scan go on its own stream.  alloc_ctx[v] is passed to alloc for view v's buffers.
+ * Per-view outputs are bit-identical to n gs_rasterize_forward_begin calls; inputs the shared
+ * pass does not take (fp16 SH, an index, differing parameters) fall back to those calls.
+ * (Beyond the reference: DGE renders a batch of views of one scene per step, DGE.py:170-239.) */
+int gs_rasterize_forward_begin_multi(int n, const gs_settings *const *s, const gs_params *const *g,
+                                     int *const *radii, gs_alloc_fn alloc, void *const *alloc_ctx,
+                                     const gs_stream_t *streams, gs_forward_state **states);
 
 int gs_rasterize_backward_ex(const gs_settings *s, const gs_params *g, int R, const int *radii,
                              const void *geom_buffer, const void *binning_buffer, const void *img_buffer,

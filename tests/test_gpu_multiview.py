@@ -187,3 +187,36 @@ def test_multiview_step_batched_streams_hinted_one_rank(cuda_device):
     assert torch.equal(r0, r1)
     torch.testing.assert_close(v1, v0, rtol=1e-5, atol=1e-9)
     torch.testing.assert_close(g1, g0, rtol=1e-5, atol=1e-9)
+
+
+@pytest.mark.parametrize("V", [2, 3])
+def test_render_views_shared_preprocess_matches_per_view(cuda_device, monkeypatch, V):
+    """render_views on several streams takes every view's first half from ONE native call whose preprocess
+    reads the scene once for all views (gs_rasterize_forward_begin_multi); DGE_AMD_MULTI_BEGIN=0's per-view
+    begin calls give bitwise the same images, radii, visibility, view-space and parameter gradients."""
+    import dge_amd.multiview as MV
+    from dge_amd.cameras import orbit_camera
+    from dge_amd.gaussian_renderer import PipelineParams
+    from dge_amd.scene import synthetic_scene
+
+    dev = torch.device("cuda")
+    W, H = 320, 256
+    cams = [orbit_camera(k, 5, W, H, device=dev) for k in range(V)]
+    g = torch.Generator().manual_seed(3)
+    seeds = [(torch.randn(3, H, W, generator=g) * 1e-3).to(dev) for _ in range(V)]
+
+    def run(multi):
+        monkeypatch.setattr(MV, "_MULTI_BEGIN", multi)
+        sc = synthetic_scene(150_000, sh_degree=3, seed=4, device=dev).requires_grad_(True)
+        outs = MV.render_views(cams, sc, PipelineParams(), torch.zeros(3, device=dev), streams=V)
+        torch.autograd.backward([o["render"] for o in outs], seeds)
+        torch.cuda.synchronize()
+        res = {f"{k}{i}": o[k].detach().cpu().numpy() for i, o in enumerate(outs)
+               for k in ("render", "radii", "visibility_filter")}
+        res.update({f"vs{i}": o["viewspace_points"].grad.cpu().numpy() for i, o in enumerate(outs)})
+        res.update({f"p{i}": p.grad.cpu().numpy() for i, p in enumerate(sc.parameters())})
+        return res
+
+    a, b = run(True), run(False)
+    for k in b:
+        np.testing.assert_array_equal(a[k], b[k], err_msg=k)
