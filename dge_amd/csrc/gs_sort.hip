@@ -63,6 +63,25 @@ __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* l
     return wbase + x - v;
 }
 
+// 256-thread exclusive max-scan (0 for thread 0).
+__device__ __forceinline__ uint32_t block_exclusive_max(uint32_t v, uint32_t* lds4) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint32_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)x, o);
+        if (lane >= o) x = max(x, y);
+    }
+    if (lane == 63) lds4[w] = x;
+    __syncthreads();
+    uint32_t pre = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) pre = i < w ? max(pre, lds4[i]) : pre;
+    __syncthreads();
+    const uint32_t ex = (uint32_t)__shfl_up((int)x, 1);
+    return max(pre, lane > 0 ? ex : 0u);
+}
+
 // The depth sort's bias: the minimum visible key, kept as ~min in the preprocess counter slots
 // (max over the slots; kCounterStride apart).
 __device__ __forceinline__ uint32_t key_bias(const uint32_t* __restrict__ bias_not) {
@@ -608,6 +627,8 @@ __global__ __launch_bounds__(256) void k_scan_emit_x(EmitArgs a) {
     __shared__ uint16_t cnt[4][kXDigits];   // per-wave column counters, then the staged run starts
     __shared__ uint16_t s_key[kEmitBatch];
     __shared__ uint2 s_pair[kEmitBatch];
+    __shared__ uint16_t s_own[kEmitBatch];  // the batch's owners (+1): marks at the entries' starts, prefix max
+    __shared__ uint32_t s_carry;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     if (blockIdx.x == 0)
         for (int t = tid; t < a.ntiles; t += 256) a.tile_count[t] = 0u;  // (the row pass counts into it)
@@ -645,6 +666,38 @@ __global__ __launch_bounds__(256) void k_scan_emit_x(EmitArgs a) {
             const uint32_t nb = total - j0 < (uint32_t)kEmitBatch ? total - j0 : (uint32_t)kEmitBatch;
             uint32_t kk[kEmitEPT], loc[kEmitEPT];
             uint2 pv[kEmitEPT];
+            // owner of every instance of the batch (the last entry with start <= j, see k_scan_emit) as a
+            // prefix max over the batch of the entries' marks at their starts: one LDS read per instance
+            // instead of a binary search of eight dependent reads
+            {
+                uint32_t carry = 0;  // owner of j0 (+1), from a search over the round's starts
+                if (tid == 0) {
+                    int lo = 0, hi = 255;
+                    while (lo < hi) {
+                        const int mid = (lo + hi + 1) >> 1;
+                        if (s_start[mid] <= j0) lo = mid;
+                        else hi = mid - 1;
+                    }
+                    s_carry = (uint32_t)lo + 1u;
+                }
+#pragma unroll
+                for (int i = 0; i < kEmitEPT; ++i) s_own[tid * kEmitEPT + i] = 0;
+                __syncthreads();
+                const uint32_t st = s_start[tid];
+                if (c && st >= j0 && st < j0 + nb) s_own[st - j0] = (uint16_t)(tid + 1);  // (starts of c > 0: distinct)
+                carry = s_carry;
+                __syncthreads();
+                uint32_t run = 0;
+#pragma unroll
+                for (int i = 0; i < kEmitEPT; ++i) run = max(run, (uint32_t)s_own[tid * kEmitEPT + i]);
+                run = max(carry, block_exclusive_max(run, lds4));
+#pragma unroll
+                for (int i = 0; i < kEmitEPT; ++i) {
+                    run = max(run, (uint32_t)s_own[tid * kEmitEPT + i]);
+                    s_own[tid * kEmitEPT + i] = (uint16_t)run;
+                }
+                __syncthreads();
+            }
 #pragma unroll
             for (int e = 0; e < kEmitEPT; ++e) {
                 const uint32_t jj = (uint32_t)(w * 64 * kEmitEPT + e * 64 + lane);
@@ -652,12 +705,7 @@ __global__ __launch_bounds__(256) void k_scan_emit_x(EmitArgs a) {
                 const uint64_t vm = __ballot(valid);
                 if (vm == 0) break;
                 const uint32_t j = j0 + (valid ? jj : 0u);
-                int lo = 0, hi = 255;  // owner: the last entry with start <= j (see k_scan_emit)
-                while (lo < hi) {
-                    const int mid = (lo + hi + 1) >> 1;
-                    if (s_start[mid] <= j) lo = mid;
-                    else hi = mid - 1;
-                }
+                const int lo = (int)s_own[valid ? jj : 0u] - 1;
                 const int4 q = s_rect[lo];
                 const uint32_t k = j - s_start[lo];
                 const uint32_t ky = (uint32_t)(((float)k + 0.5f) / (float)q.z);  // exact: k < 2^20
