@@ -61,19 +61,13 @@ def parse():
                          "backward of the summed loss -- the reference's order, DGE.py:170-239, 617-699)")
     ap.add_argument("--batch-backward", dest="batch_backward", action="store_true", help=argparse.SUPPRESS)
     ap.set_defaults(batch_backward=True)
-    ap.add_argument("--stagger", action="store_true",
-                    help="start each view's first half after the previous view's (render_views(stagger=True))")
-    ap.add_argument("--view-threads", action="store_true",
-                    help="issue each view's forward from its own host thread (dge_amd.multiview.render_views("
-                         "threads=True); measured no faster and far noisier at c2)")
+    ap.add_argument("--exact", dest="speculate", action="store_false",
+                    help="size every view's binning buffer from its instance count read back to the host (the "
+                         "reference's per-view sync, rasterizer_impl.cu:236-239) instead of from the counts seen "
+                         "before (render_views(speculate=True), checked once per step)")
     ap.add_argument("--scan-live", action="store_true",
                     help="N > 1: find the all-reduce's live rows by reading the gradient bucket after the backward "
                          "(GradBucket.allreduce) instead of agreeing on the forwards' blended Gaussians before it")
-    ap.add_argument("--overlap-zero", dest="serial_zero", action="store_false",
-                    help="zero the gradient bucket after enqueueing the forwards, only the gradient writes waiting "
-                         "for it (GradBucket.zero(overlap=True)); measured no faster than zeroing first (default)")
-    ap.add_argument("--serial-zero", dest="serial_zero", action="store_true", help=argparse.SUPPRESS)
-    ap.set_defaults(serial_zero=True)
     ap.add_argument("--cpu-baseline-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -156,10 +150,6 @@ def main():
         # durations are taken from -- on several streams an event pair also times the other streams' work
         run_views(args, cams, scene, pipe, bg, seeds, bucket, streams=1)
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-
     # instance counts of this rank's views (deterministic; outside the timed region)
     Ks, Kbs, lives = [], [], []
     with torch.no_grad():
@@ -194,6 +184,8 @@ def main():
     calib = {}
     blend = ["render_fwd", "render_bwd"]
     if not args.no_profile:
+        for _ in range(2):  # (first launches load code objects: keep them out of the stage times)
+            step_one_stream()
         _native.profile_stages(None)
         _native.profile_enable(True)
         _native.profile_collect()  # reset
@@ -202,17 +194,35 @@ def main():
         torch.cuda.synchronize()
         calib = {n: (ms, c) for n, (ms, c) in _native.profile_collect().items() if c}
         _native.profile_enable(False)
-    if distributed:
-        dist.barrier()
-    torch.cuda.synchronize()
-    m0 = torch.cuda.memory_stats(dev)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
+    # the W warmup steps run right before the timed region (after the calibration above), so the timed
+    # steps start in the steady state the warmup built: the caching allocator's per-stream pools, the
+    # staging slots, the clocks
+    for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
     if distributed:
         dist.barrier()
+    torch.cuda.synchronize()
+    m0 = torch.cuda.memory_stats(dev)
+    main_stream = torch.cuda.current_stream(dev)
+    # per-step timing: one timing event on the main stream after each step (every view stream and the
+    # backward join it there) and the host clock when each step's issue returns
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
+    host_t = []
+    wait0 = _native.lib().gs_host_wait_ns()
+    t0 = time.perf_counter()
+    evs[0].record(main_stream)
+    for i in range(args.steps):
+        step()
+        evs[i + 1].record(main_stream)
+        host_t.append(time.perf_counter())
+    torch.cuda.synchronize()
+    if distributed:
+        dist.barrier()
     dt = time.perf_counter() - t0
+    host_wait_s = (_native.lib().gs_host_wait_ns() - wait0) * 1e-9
+    step_ms = [evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps)]
+    host_ms = [1e3 * (b - a) for a, b in zip([t0] + host_t[:-1], host_t)]
     m1 = torch.cuda.memory_stats(dev)
     # caching-allocator activity inside the timed region (device allocations there cost a hipMalloc each)
     alloc_stats = {k: int(m1.get(k, 0) - m0.get(k, 0)) for k in ("num_device_alloc", "num_device_free",
@@ -327,6 +337,13 @@ def main():
             # the leg the rooflines and stages_ms come from: the same step with the views on one stream
             "roofline_leg": iso,
             "allocator_timed_region": alloc_stats,
+            # per-step GPU time between main-stream events (the step's views and backward joined), its spread,
+            # and the host's issue time per step with the part spent blocked on the instance-count read-back
+            "step_ms": _spread(step_ms),
+            "host_ms_per_step": {"issue": round(1e3 * (host_t[-1] - t0) / args.steps, 4),
+                                 "wait": round(1e3 * host_wait_s / args.steps, 4),
+                                 "busy": round((1e3 * (host_t[-1] - t0) - 1e3 * host_wait_s) / args.steps, 4),
+                                 "per_step": _spread(host_ms)},
             "legs": legs,
             "cpu_baseline": cpu,
         }
@@ -335,28 +352,39 @@ def main():
         dist.destroy_process_group()
 
 
+def _spread(xs):
+    """p50 / p90 / max (and the index of the max) of per-step milliseconds."""
+    a = np.asarray(xs, dtype=np.float64)
+    if a.size == 0:
+        return None
+    return {"p50": round(float(np.percentile(a, 50)), 4), "p90": round(float(np.percentile(a, 90)), 4),
+            "min": round(float(a.min()), 4), "max": round(float(a.max()), 4), "argmax": int(a.argmax()),
+            "max_over_p50": round(float(a.max() / max(np.percentile(a, 50), 1e-9)), 3)}
+
+
 def run_views(args, cams, scene, pipe, bg, seeds, bucket, streams=None, min_world=None):
     """One step's renders: zero the bucket, forward every view, backward (see the module docstring).
     min_world (distributed steps): the sparse all-reduce's union of live rows is agreed on between the
-    forwards and the backward (GradBucket.allreduce_begin; the caller runs allreduce_end)."""
+    forwards and the backward (GradBucket.allreduce_begin; the caller runs allreduce_end).  With
+    speculated binning capacities the step ends with the batch's check (its one host wait, on the
+    views' preprocess) and runs again in the rare case a view overflowed its capacity."""
     from dge_amd.multiview import render_backward_views, render_views
 
     streams = args.streams if streams is None else streams
-    # the overlapped zero (fused path only: its gradient writes wait for the fill in-kernel) is issued after
-    # the forwards are enqueued on the side streams, so they do not queue behind the 236-MB fill
-    overlap = (not args.serial_zero and args.batch_backward and streams > 1
-               and os.environ.get("DGE_AMD_FUSED", "1") != "0")
-    if not overlap:
+    if not args.batch_backward:
         bucket.zero()
-    if args.batch_backward:
-        outs = render_views(cams, scene, pipe, bg, streams=streams, threads=args.view_threads, stagger=args.stagger)
-        if overlap:
-            bucket.zero(overlap=True)
+        render_backward_views(cams, scene, pipe, bg, seeds, streams=streams)
+        return
+    for _ in range(2):
+        bucket.zero()
+        outs = render_views(cams, scene, pipe, bg, streams=streams, speculate=args.speculate)
         if min_world is not None and not args.scan_live:
             bucket.allreduce_begin([o.get("_live_rows") for o in outs], min_world=min_world)
         torch.autograd.backward([o["render"] for o in outs], seeds)
-    else:
-        render_backward_views(cams, scene, pipe, bg, seeds, streams=streams)
+        if outs.check():
+            return
+        # a view's instance count outgrew its speculated capacity: the step again (the capacity grew)
+    raise RuntimeError("render_views: the binning capacity check failed twice")
 
 
 def _time(fn, steps):

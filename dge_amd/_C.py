@@ -73,14 +73,10 @@ _EMPTY_U8 = {}  # device -> empty uint8 tensor (placeholder for buffers never al
 
 
 def _alloc_cb(ctx, which, nbytes):
-    # ctx: 0 = this thread's current allocator; v + 1 = view v of a multi-view begin, whose buffers belong to
-    # that view's stream (the caching allocator must not hand them out while it still uses them)
-    a = _TLS.allocs[ctx - 1] if ctx else _TLS.alloc
-    if a.stream is not None:
-        with torch.cuda.stream(a.stream):
-            buf = torch.empty(int(nbytes), dtype=torch.uint8, device=a.device)
-    else:
-        buf = torch.empty(int(nbytes), dtype=torch.uint8, device=a.device)
+    # this thread's current allocator (the C call that receives the callback runs on this thread); the
+    # buffer is allocated on the current stream
+    a = _TLS.alloc
+    buf = torch.empty(int(nbytes), dtype=torch.uint8, device=a.device)
     a.buffers[which] = buf
     return buf.data_ptr() if nbytes else None
 
@@ -92,9 +88,8 @@ class _Allocator:
     """gs_alloc_fn backed by the torch caching allocator.  The C call that receives `fn` runs on this
     thread right after construction; the shared callback finds this object through a thread-local."""
 
-    def __init__(self, device, stream=None):
+    def __init__(self, device):
         self.device = device
-        self.stream = stream
         e = _EMPTY_U8.get(device)
         if e is None:
             e = _EMPTY_U8[device] = torch.empty(0, dtype=torch.uint8, device=device)
@@ -379,57 +374,6 @@ def rasterize_gaussians_fused_begin(background, xyz, f_dc, f_rest, colors, raw_o
                                                 _stream(dev), ctypes.byref(h))
         N.check(rc, "rasterize_gaussians_fused")
         return Prepared(h.value, alloc, radii, keep, H, W, P, dev)
-
-
-def rasterize_gaussians_fused_begin_multi(views, streams):
-    """gs_rasterize_forward_begin_multi: the first halves of several views of one scene, the scene's
-    parameters read once by a shared preprocess pass.  views: one tuple of rasterize_gaussians_fused_begin's
-    arguments per view (the same parameter tensors in each, index None); streams: view v's stream (torch
-    streams, each already ordered after whatever produced the inputs).  -> one Prepared per view, each to
-    be ended on its own stream."""
-    n = len(views)
-    dev = views[0][1].device
-    N.require_gpu(views[0][1])
-    with torch.cuda.device(dev):
-        ss, gs, radii_l, allocs, keeps = [], [], [], [], []
-        first = None
-        for v, (background, xyz, f_dc, f_rest, colors, raw_opacity, raw_scaling, raw_rotation, scale_modifier,
-                viewmatrix, projmatrix, tan_fovx, tan_fovy, image_height, image_width, degree, campos, prefiltered,
-                debug, index, visible) in enumerate(views):
-            H, W = int(image_height), int(image_width)
-            if first is None:
-                xyz = _f32(xyz, "xyz")
-                f_dc, f_rest = _features(f_dc, "features_dc"), _features(f_rest, "features_rest")
-                colors = _f32(colors, "colors")
-                raw_opacity, raw_scaling = _f32(raw_opacity, "opacity"), _f32(raw_scaling, "scaling")
-                raw_rotation = _f32(raw_rotation, "rotation")
-                first = (xyz, f_dc, f_rest, colors, raw_opacity, raw_scaling, raw_rotation)
-            xyz, f_dc, f_rest, colors, raw_opacity, raw_scaling, raw_rotation = first
-            P = xyz.size(0)
-            with torch.cuda.stream(streams[v]):
-                radii = torch.empty((P,), dtype=torch.int32, device=dev)
-            g = _params(P, xyz, f_dc, f_rest, colors, raw_opacity, raw_scaling, raw_rotation, None, visible)
-            s, keep = _settings(background, viewmatrix, projmatrix, campos, tan_fovx, tan_fovy, H, W, degree,
-                                scale_modifier, prefiltered, debug)
-            keep += [xyz, f_dc, f_rest, colors, raw_opacity, raw_scaling, raw_rotation, visible]
-            ss.append(s)
-            gs.append(g)
-            radii_l.append(radii)
-            allocs.append(_Allocator(dev, streams[v]))
-            keeps.append((keep, H, W, P))
-        _TLS.allocs = allocs
-        s_arr = (ctypes.c_void_p * n)(*[ctypes.addressof(x) for x in ss])
-        g_arr = (ctypes.c_void_p * n)(*[ctypes.addressof(x) for x in gs])
-        r_arr = (ctypes.c_void_p * n)(*[r.data_ptr() for r in radii_l])
-        c_arr = (ctypes.c_void_p * n)(*range(1, n + 1))
-        st_arr = (ctypes.c_void_p * n)(*[st.cuda_stream for st in streams])
-        h_arr = (ctypes.c_void_p * n)()
-        rc = N.lib().gs_rasterize_forward_begin_multi(n, ctypes.addressof(s_arr), ctypes.addressof(g_arr),
-                                                      ctypes.addressof(r_arr), allocs[0].fn, ctypes.addressof(c_arr),
-                                                      ctypes.addressof(st_arr), ctypes.addressof(h_arr))
-        N.check(rc, "rasterize_gaussians_fused (views)")
-        return [Prepared(h_arr[v], allocs[v], radii_l[v], keeps[v][0], keeps[v][1], keeps[v][2], keeps[v][3], dev)
-                for v in range(n)]
 
 
 def rasterize_gaussians_fused_end(prep):

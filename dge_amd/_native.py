@@ -15,7 +15,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("DGE_AMD_LIB") or os.path.join(_HERE, "lib", "libgs_raster.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "gs_raster.h")
 
-ABI_VERSION = 9  # GS_RASTER_ABI_VERSION of include/gs_raster.h this binding is written against
+ABI_VERSION = 10  # GS_RASTER_ABI_VERSION of include/gs_raster.h this binding is written against
 
 GS_OK = 0
 GS_ERR_INVALID_ARG = 1
@@ -23,6 +23,10 @@ GS_ERR_HIP = 2
 GS_ERR_ALLOC = 3
 GS_ERR_PREFILTERED = 4
 GS_ERR_UNSUPPORTED = 5
+GS_ERR_RETRY = 6
+
+MAX_VIEWS = 8  # GS_MAX_VIEWS
+VIEWS_EXACT, VIEWS_SPECULATE = 0, 1
 
 _fp = ctypes.c_void_p  # device pointers travel as opaque addresses
 
@@ -135,10 +139,17 @@ SIGNATURES = {
     "gs_rasterize_forward_end": (ctypes.c_int, [ctypes.c_void_p, _fp, _fp, ALLOC_FN, ctypes.c_void_p, ctypes.c_void_p,
                                                  ctypes.POINTER(ctypes.c_int)]),
     "gs_rasterize_forward_release": (None, [ctypes.c_void_p]),
-    "gs_rasterize_forward_begin_multi": (ctypes.c_int, [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
-                                                         ALLOC_FN, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "gs_rasterize_backward_ex": (ctypes.c_int, [ctypes.POINTER(GsSettings), ctypes.POINTER(GsParams), ctypes.c_int,
                                                  _fp, _fp, _fp, _fp, _fp, ctypes.POINTER(GsGrads), ctypes.c_void_p]),
+    "gs_views_forward": (ctypes.c_int, [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ALLOC_FN, ctypes.c_void_p,
+                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p)]),
+    "gs_views_check": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    "gs_views_backward": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                          ctypes.c_void_p, ctypes.c_void_p]),
+    "gs_views_buffer": (ctypes.c_void_p, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]),
+    "gs_views_layout": (ctypes.c_longlong, [ctypes.c_void_p, ctypes.c_int]),
+    "gs_views_release": (None, [ctypes.c_void_p]),
     "gs_mark_visible": (ctypes.c_int, [ctypes.c_int, _fp, _fp, _fp, _fp, ctypes.c_void_p]),
     "gs_apply_weights": (ctypes.c_int, [ctypes.POINTER(GsSettings), ctypes.c_int, ctypes.c_int, _fp, _fp, ctypes.c_int]
                          + [_fp] * 7 + [ALLOC_FN, ctypes.c_void_p, ctypes.c_void_p]),
@@ -152,6 +163,7 @@ SIGNATURES = {
     "gs_profile_num_stages": (ctypes.c_int, []),
     "gs_profile_stage_name": (ctypes.c_char_p, [ctypes.c_int]),
     "gs_profile_collect": (ctypes.c_int, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int), ctypes.c_int]),
+    "gs_host_wait_ns": (ctypes.c_longlong, []),
     "gs_profile_diag_enable": (ctypes.c_int, [ctypes.c_int]),
     "gs_profile_diag_read": (ctypes.c_longlong, [ctypes.c_int, ctypes.POINTER(ctypes.c_uint64), ctypes.c_longlong]),
     "gs_adam_step": (ctypes.c_int, [ctypes.POINTER(AdamSegment), ctypes.c_int, ctypes.c_double, ctypes.c_double,

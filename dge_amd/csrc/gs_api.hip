@@ -20,6 +20,7 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <chrono>
 #include <limits>
 #include <memory>
 #include <atomic>
@@ -37,6 +38,7 @@ using namespace gs;
 namespace {
 
 thread_local std::string g_last_error;
+std::atomic<long long> g_host_wait_ns{0};  // gs_host_wait_ns
 
 int set_error(int code, const char* fmt, ...) {
     char buf[512];
@@ -142,8 +144,11 @@ int staging_acquire(Staging** out) {
     return GS_OK;
 }
 
-void staging_release(Staging* s) {
+void staging_release(Staging* s, bool synced = false) {
     if (!s) return;
+    // a slot dropped before its forward's _end may still have the counters' D2H copy in flight:
+    // the next forward to take it must not see that late copy land over its own counters
+    if (!synced) (void)hipEventSynchronize(s->ev);
     StagingPool& p = staging_pool();
     std::lock_guard<std::mutex> g(p.mu);
     p.free[s->dev].push_back(s);
@@ -331,20 +336,16 @@ struct FwdState {
 };
 
 // First half of the forward: buffers, preprocess, counter read-back, depth
-// sort, instance scan (rasterizer_impl.cu:179-239 up to the num_rendered copy),
-// in three steps so several views can share one preprocess launch
-// (gs_rasterize_forward_begin_multi): bin_prepare (buffers, counter memset,
-// the preprocess arguments), the preprocess, bin_after_preprocess.
-int bin_prepare(FwdState& f, int copy_colors, gs_alloc_fn alloc, void* ctx, hipStream_t stream) {
+// sort, instance scan (rasterizer_impl.cu:179-239 up to the num_rendered copy):
+// bin_prepare_in (counter memset, the preprocess arguments), the preprocess,
+// bin_after_preprocess.
+int bin_prepare_in(FwdState& f, int copy_colors, void* geom, void* img, hipStream_t stream) {
     const gs_settings* s = &f.s;
     const Grid& g = f.g;
     const gs_params& gp = f.gp;
     const int P = gp.P;
     const GeomLayout gl = geom_layout(P);
     const ImgLayout il = img_layout(g.W, g.H);
-    void* geom = alloc(ctx, 0, gl.total);
-    void* img = alloc(ctx, 2, il.total);
-    if (!geom || !img) return set_error(GS_ERR_ALLOC, "allocator returned NULL for the geometry/image buffer");
     f.geom = geom;
     f.img = img;
 
@@ -373,6 +374,13 @@ int bin_prepare(FwdState& f, int copy_colors, gs_alloc_fn alloc, void* ctx, hipS
     pa.counters = counters;
     pa.touched = at<uint8_t>(geom, gl.touched);
     return GS_OK;
+}
+
+int bin_prepare(FwdState& f, int copy_colors, gs_alloc_fn alloc, void* ctx, hipStream_t stream) {
+    void* geom = alloc(ctx, 0, geom_layout(f.gp.P).total);
+    void* img = alloc(ctx, 2, img_layout(f.g.W, f.g.H).total);
+    if (!geom || !img) return set_error(GS_ERR_ALLOC, "allocator returned NULL for the geometry/image buffer");
+    return bin_prepare_in(f, copy_colors, geom, img, stream);
 }
 
 int bin_after_preprocess(FwdState& f, hipStream_t stream) {
@@ -426,38 +434,143 @@ int bin_begin(FwdState& f, int copy_colors, gs_alloc_fn alloc, void* ctx, hipStr
     return bin_after_preprocess(f, stream);
 }
 
-// Second half: wait for the instance count (the reference's one host sync,
-// rasterizer_impl.cu:236-239), then emission, tile sort and tile ranges.  On
-// success *bin_out holds the binning buffer and *K_out the instance count.
-int bin_end(FwdState& f, gs_alloc_fn alloc, void* ctx, hipStream_t stream, void** bin_out, int* K_out) {
-    const gs_settings* s = &f.s;
-    const Grid& g = f.g;
-    const int P = f.gp.P;
-    const bool debug = s->debug != 0;
-    const GeomLayout gl = geom_layout(P);
-    const ImgLayout il = img_layout(g.W, g.H);
-    void* geom = f.geom;
-    void* img = f.img;
-    Staging* st = f.st;
-    PreprocessArgs& pa = f.pa;
-    EmitArgs& ea = f.ea;
+// Instance counts seen per (P, W, H): the capacity a speculative forward sizes
+// its binning buffer by (gs_views_forward), and the configurations whose depth
+// keys needed the 32-bit sort (never speculated).
+struct CountHistory {
+    std::mutex mu;
+    std::unordered_map<uint64_t, uint32_t> max_k;
+    std::unordered_map<uint64_t, bool> wide;
+};
+CountHistory& count_history() {
+    static CountHistory h;
+    return h;
+}
+uint64_t config_key(int P, int W, int H) {
+    return ((uint64_t)(uint32_t)P << 32) ^ ((uint64_t)(uint32_t)W << 16) ^ (uint64_t)(uint32_t)H;
+}
+void note_count(int P, int W, int H, uint64_t K, bool wide) {
+    CountHistory& h = count_history();
+    std::lock_guard<std::mutex> g(h.mu);
+    uint32_t& m = h.max_k[config_key(P, W, H)];
+    const uint32_t k = K > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)K;
+    m = k > m ? k : m;
+    if (wide) h.wide[config_key(P, W, H)] = true;
+}
+// a speculative binning buffer's capacity: the largest count seen x 1.25 + 64k (0: no history, or
+// a configuration that needed the 32-bit depth sort)
+uint32_t spec_capacity(int P, int W, int H) {
+    CountHistory& h = count_history();
+    std::lock_guard<std::mutex> g(h.mu);
+    const uint64_t k = config_key(P, W, H);
+    auto it = h.max_k.find(k);
+    if (it == h.max_k.end() || h.wide.count(k)) return 0;
+    const uint64_t c = (uint64_t)it->second + it->second / 4 + 65536;
+    return c > (uint64_t)std::numeric_limits<int>::max() ? 0u : (uint32_t)c;
+}
 
+// The host's copy of a forward's preprocess counters, after its event: the
+// instance count, whether the visible depth keys span more bits than the short
+// depth sort orders, the prefiltered error.  Releases the staging slot.
+struct Counts {
+    uint64_t K = 0;
+    bool wide = false, prefilter_fail = false;
+};
+int read_counts(FwdState& f, Counts& c) {
+    Staging* st = f.st;
+    const auto t0 = std::chrono::steady_clock::now();
     GS_HIP(hipEventSynchronize(st->ev));
+    g_host_wait_ns.fetch_add(
+        (long long)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count(),
+        std::memory_order_relaxed);
     uint64_t K64 = 0;
     uint32_t kmax = 0, kmin_not = 0;
     for (int i = 0; i < kCounterSlots; ++i) {
-        const uint32_t* c = st->host + kCounterStride * i;
-        K64 += c[0];
-        kmax = c[1] > kmax ? c[1] : kmax;
-        kmin_not = c[2] > kmin_not ? c[2] : kmin_not;
+        const uint32_t* q = st->host + kCounterStride * i;
+        K64 += q[0];
+        kmax = q[1] > kmax ? q[1] : kmax;
+        kmin_not = q[2] > kmin_not ? q[2] : kmin_not;
     }
-    const bool prefilter_fail = st->host[3] != 0;
-    staging_release(st);
+    c.K = K64;
+    c.prefilter_fail = st->host[3] != 0;
+    c.wide = K64 && kmax - ~kmin_not >= (1u << depth_sort_bits());
+    staging_release(st, true);
     f.st = nullptr;
-    if (prefilter_fail) return set_error(GS_ERR_PREFILTERED, "Point is filtered although prefiltered is set. This shouldn't happen!");
-    if (K64 > (uint64_t)std::numeric_limits<int>::max()) return set_error(GS_ERR_INVALID_ARG, "too many tile instances (%llu)", (unsigned long long)K64);
-    const uint32_t K = (uint32_t)K64;
-    if ((K && kmax - ~kmin_not >= (1u << depth_sort_bits())) || force_depth_keys32()) {
+    note_count(f.gp.P, f.g.W, f.g.H, c.K, c.wide);
+    return GS_OK;
+}
+
+// The emission, tile sort and tile ranges into the binning buffer `bin`, laid out for `K_layout`
+// instances.  n_dev == nullptr: K_layout is the instance count; else (a speculative forward) the
+// count is read on the device from the preprocess counters and capped at K_layout.
+int bin_emit(FwdState& f, void* bin, uint32_t K_layout, const uint32_t* n_dev, hipStream_t stream) {
+    const Grid& g = f.g;
+    const bool debug = f.s.debug != 0;
+    const ImgLayout il = img_layout(g.W, g.H);
+    void* img = f.img;
+    EmitArgs& ea = f.ea;
+    const BinLayout bl = bin_layout((int)K_layout, g.tiles);
+    ea.cap = n_dev ? K_layout : 0xFFFFFFFFu;
+    const TileSortPlan plan = tile_sort_plan(g.tiles);
+    if (ea.xhist) {  // two-level binning (tile_sort_fused): column-ordered emission, row pass, ranges
+        ea.tile_key = at<uint32_t>(bin, bl.key1);
+        ea.pairs_out = at<uint2>(bin, bl.pair1);
+        ea.xtotals = at<uint32_t>(bin, bl.sort_totals);
+        ea.tile_count = at<uint32_t>(bin, bl.tile_count);
+        ea.ntiles = g.tiles;
+        ea.rec_flags32 = at<uint32_t>(bin, bl.rec_flags);
+        { StageScope sc(ST_EMIT, stream); launch_emit_fused(ea, stream); }
+        { StageScope sc(ST_TILE_SORT, stream);
+        launch_row_pass(ea, K_layout, at<uint2>(bin, bl.point_pairs), at<uint32_t>(bin, bl.sort_hist), bl.sort_blocks,
+                        at<uint2>(img, il.ranges), stream, n_dev); }
+        GS_LAUNCHED("two-level binning");
+        return GS_OK;
+    }
+    ea.tile_key = at<uint32_t>(bin, bl.key0);
+    ea.slot_gauss = at<uint32_t>(bin, bl.slot_gauss);
+    ea.rec_flags32 = at<uint32_t>(bin, bl.rec_flags);
+    { StageScope sc(ST_EMIT, stream); launch_scan_emit(ea, stream); }
+    GS_LAUNCHED("emit");
+
+    int tc;
+    { StageScope sc(ST_TILE_SORT, stream);
+    tc = tile_sort(at<uint32_t>(bin, bl.key0), at<uint32_t>(bin, bl.key1), at<uint2>(bin, bl.pair0),
+                   at<uint2>(bin, bl.pair1), at<uint32_t>(bin, bl.slot_gauss), K_layout, plan.bits,
+                   at<uint32_t>(bin, bl.sort_hist), at<uint32_t>(bin, bl.sort_totals), bl.sort_blocks, stream,
+                   at<uint2>(img, il.ranges), at<uint32_t>(img, il.tile_order), g.tiles, n_dev); }
+    GS_LAUNCHED("tile sort");
+    if (!tile_sort_writes_ranges(g.tiles)) {
+        StageScope sc(ST_RANGES, stream);
+        launch_ranges(at<uint32_t>(bin, tc ? bl.key1 : bl.key0), (int)K_layout, at<uint2>(img, il.ranges), nullptr,
+                      stream);
+        GS_LAUNCHED("ranges");
+    }
+    return GS_OK;
+}
+
+// Second half: wait for the instance count (the reference's one host sync,
+// rasterizer_impl.cu:236-239), then emission, tile sort and tile ranges.  On
+// success *bin_out holds the binning buffer and *K_out the instance count.
+// which_bin: the allocator's `which` for the binning buffer.
+int bin_end(FwdState& f, gs_alloc_fn alloc, void* ctx, hipStream_t stream, void** bin_out, int* K_out,
+            int which_bin = 1) {
+    const Grid& g = f.g;
+    const int P = f.gp.P;
+    const bool debug = f.s.debug != 0;
+    const GeomLayout gl = geom_layout(P);
+    void* geom = f.geom;
+    PreprocessArgs& pa = f.pa;
+    EmitArgs& ea = f.ea;
+
+    Counts c;
+    int rc = read_counts(f, c);
+    if (rc) return rc;
+    if (c.prefilter_fail)
+        return set_error(GS_ERR_PREFILTERED, "Point is filtered although prefiltered is set. This shouldn't happen!");
+    if (c.K > (uint64_t)std::numeric_limits<int>::max())
+        return set_error(GS_ERR_INVALID_ARG, "too many tile instances (%llu)", (unsigned long long)c.K);
+    const uint32_t K = (uint32_t)c.K;
+    if (c.wide || force_depth_keys32()) {
         // the visible depth keys span more bits than the short sort covered: redo the depth order
         // on the full 32-bit keys
         int cur;
@@ -473,45 +586,46 @@ int bin_end(FwdState& f, gs_alloc_fn alloc, void* ctx, hipStream_t stream, void*
     }
     *K_out = (int)K;
 
-    const BinLayout bl = bin_layout((int)K, g.tiles);
-    void* bin = alloc(ctx, 1, bl.total);
+    void* bin = alloc(ctx, which_bin, bin_layout((int)K, g.tiles).total);
     if (!bin) return set_error(GS_ERR_ALLOC, "allocator returned NULL for the binning buffer");
     *bin_out = bin;
     if (K == 0) return GS_OK;
+    return bin_emit(f, bin, K, nullptr, stream);
+}
 
-    const TileSortPlan plan = tile_sort_plan(g.tiles);
-    if (ea.xhist) {  // two-level binning (tile_sort_fused): column-ordered emission, row pass, ranges
-        ea.tile_key = at<uint32_t>(bin, bl.key1);
-        ea.pairs_out = at<uint2>(bin, bl.pair1);
-        ea.xtotals = at<uint32_t>(bin, bl.sort_totals);
-        ea.tile_count = at<uint32_t>(bin, bl.tile_count);
-        ea.ntiles = g.tiles;
-        ea.rec_flags32 = at<uint32_t>(bin, bl.rec_flags);
-        { StageScope sc(ST_EMIT, stream); launch_emit_fused(ea, stream); }
-        { StageScope sc(ST_TILE_SORT, stream);
-        launch_row_pass(ea, K, at<uint2>(bin, bl.point_pairs), at<uint32_t>(bin, bl.sort_hist), bl.sort_blocks,
-                        at<uint2>(img, il.ranges), stream); }
-        GS_LAUNCHED("two-level binning");
-        return GS_OK;
-    }
-    ea.tile_key = at<uint32_t>(bin, bl.key0);
-    ea.slot_gauss = at<uint32_t>(bin, bl.slot_gauss);
-    ea.rec_flags32 = at<uint32_t>(bin, bl.rec_flags);
-    { StageScope sc(ST_EMIT, stream); launch_scan_emit(ea, stream); }
-    GS_LAUNCHED("emit");
-
-    int tc;
-    { StageScope sc(ST_TILE_SORT, stream);
-    tc = tile_sort(at<uint32_t>(bin, bl.key0), at<uint32_t>(bin, bl.key1), at<uint2>(bin, bl.pair0),
-                   at<uint2>(bin, bl.pair1), at<uint32_t>(bin, bl.slot_gauss), K, plan.bits,
-                   at<uint32_t>(bin, bl.sort_hist), at<uint32_t>(bin, bl.sort_totals), bl.sort_blocks, stream,
-                   at<uint2>(img, il.ranges), at<uint32_t>(img, il.tile_order), g.tiles); }
-    GS_LAUNCHED("tile sort");
-    if (!tile_sort_writes_ranges(g.tiles)) {
-        StageScope sc(ST_RANGES, stream);
-        launch_ranges(at<uint32_t>(bin, tc ? bl.key1 : bl.key0), (int)K, at<uint2>(img, il.ranges), nullptr, stream);
-        GS_LAUNCHED("ranges");
-    }
+// The blend (k_render_fwd) over a finished binning laid out for K_layout instances.
+int render_launch(FwdState& f, void* bin, uint32_t K_layout, int order_ready, float* out_color, float* out_depth,
+                  hipStream_t stream) {
+    const Grid& g = f.g;
+    const bool debug = f.s.debug != 0;
+    const GeomLayout gl = geom_layout(f.gp.P);
+    const ImgLayout il = img_layout(g.W, g.H);
+    const BinLayout bl = bin_layout((int)K_layout, g.tiles);
+    void* geom = f.geom;
+    void* img = f.img;
+    RenderArgs ra;
+    ra.W = g.W; ra.H = g.H; ra.gx = g.gx; ra.gy = g.gy;
+    ra.ranges = at<uint2>(img, il.ranges);
+    ra.tile_order = at<uint32_t>(img, il.tile_order);
+    ra.order_ready = order_ready;
+    ra.point_pairs = at<uint2>(bin, bl.point_pairs);
+    ra.bwd_items = at<uint2>(bin, bl.bwd_items);
+    ra.bwd_count = at<uint32_t>(img, il.bwd_count);
+    ra.item_cap = (uint32_t)(4 * bl.nslots);
+    ra.splat = at<Splat>(geom, gl.splat);
+    ra.bg = f.s.bg;
+    ra.final_T = at<float>(img, il.final_T);
+    ra.n_contrib = at<uint32_t>(img, il.n_contrib);
+    ra.tile_last = at<uint32_t>(img, il.tile_last);
+    ra.quad_last = at<uint32_t>(img, il.quad_last);
+    ra.ckpt = at<float4>(bin, bl.ckpt);
+    ra.used = at<uint64_t>(bin, bl.used);
+    ra.out_color = out_color;
+    ra.out_depth = out_depth;
+    ra.touched = at<uint8_t>(geom, gl.touched);
+    ra.diag = diag_buffer(0, kDiagWords * (size_t)g.tiles * 4);
+    { StageScope sc(ST_RENDER_FWD, stream); launch_render_forward(ra, stream); }
+    GS_LAUNCHED("render");
     return GS_OK;
 }
 
@@ -529,6 +643,88 @@ int bin_forward(const gs_settings* s, const Grid& g, const gs_params& gp, int* r
     *img_out = f.img;
     if (rc) return rc;
     return bin_end(f, alloc, ctx, stream, bin_out, K_out);
+}
+
+// One view's backward (gs_rasterize_backward_ex): the replay, then the per-Gaussian pass, whose
+// accumulated writes wait for writes_after.  R: the binning layout's instance count; slot_cap: a
+// speculative forward's capacity (its slots end there), else ~0.
+int backward_view(const gs_settings* s, const gs_params* gp, int R, const int* radii, const void* geom,
+                  const void* binning, const void* img, const float* dL_dpix, const gs_grads* o, hipStream_t stream,
+                  hipEvent_t writes_after, uint32_t slot_cap) {
+    const int P = gp->P;
+    if (P == 0) return GS_OK;
+    const bool debug = s->debug != 0;
+    const Grid g = make_grid(s);
+    const GeomLayout gl = geom_layout(P);
+    const ImgLayout il = img_layout(g.W, g.H);
+    const BinLayout bl = bin_layout(R, g.tiles);
+    float4* records = R > 0 ? at<float4>(const_cast<void*>(binning), bl.records) : nullptr;
+    uint8_t* rec_flags = R > 0 ? at<uint8_t>(const_cast<void*>(binning), bl.rec_flags) : nullptr;
+    // per-Gaussian "has a record" bytes: k_gauss_bwd skips every Gaussian without one (all of
+    // its gradients are zero), which is most of them (occluded behind saturated pixels)
+    // (both zeroed by the forward: `touched` in preprocess, the flags with the tile ranges.  A
+    // second backward of the same forward finds the bytes of the first, which it sets again: the
+    // entries that get records depend on the forward alone)
+    uint8_t* touched = at<uint8_t>(const_cast<void*>(geom), gl.touched);
+    if (R > 0) {
+        uint32_t* bwd_count = at<uint32_t>(const_cast<void*>(img), il.bwd_count);
+        RenderBwdArgs rb;
+        rb.W = g.W; rb.H = g.H; rb.gx = g.gx; rb.gy = g.gy;
+        rb.ranges = at<uint2>(img, il.ranges);
+        rb.point_pairs = at<uint2>(binning, bl.point_pairs);
+        rb.bwd_items = at<uint2>(binning, bl.bwd_items);
+        rb.bwd_count = bwd_count;
+        rb.tile_last = at<uint32_t>(img, il.tile_last);
+        rb.item_cap = (uint32_t)(4 * bl.nslots);
+        rb.quad_last = at<uint32_t>(img, il.quad_last);
+        rb.ckpt = at<float4>(binning, bl.ckpt);
+        rb.used = at<uint64_t>(binning, bl.used);
+        rb.splat = at<Splat>(geom, gl.splat);
+        rb.bg = s->bg;
+        rb.final_T = at<float>(img, il.final_T);
+        rb.n_contrib = at<uint32_t>(img, il.n_contrib);
+        rb.dL_dpix = dL_dpix;
+        rb.records = records;
+        rb.rec_flags = rec_flags;
+        rb.diag = diag_buffer(1, kDiagWords * 4 * bl.nslots);
+        { StageScope sc(ST_RENDER_BWD, stream); launch_render_backward(rb, stream); }
+        GS_LAUNCHED("render backward");
+    }
+    GaussBwdArgs ga;
+    ga.P = P; ga.D = s->sh_degree; ga.M = gp->M; ga.W = g.W; ga.H = g.H; ga.gx = g.gx; ga.gy = g.gy;
+    ga.means3D = gp->means3D; ga.scales = gp->scales; ga.rotations = gp->rotations;
+    ga.cov3D_precomp = gp->cov3D_precomp; ga.opacities = gp->opacities;
+    ga.index = gp->index;
+    ga.sh = sh_view(*gp);
+    ga.dsh.dc = o->dL_dsh_dc;
+    ga.dsh.rest = o->dL_dsh_rest ? o->dL_dsh_rest : o->dL_dsh_dc;
+    ga.dsh.dc_stride = o->dsh_dc_stride;
+    ga.dsh.rest_stride = o->dsh_rest_stride;
+    ga.activation = gp->activation;
+    ga.view = s->viewmatrix; ga.proj = s->projmatrix; ga.campos = s->campos;
+    ga.tanfovx = s->tanfovx; ga.tanfovy = s->tanfovy; ga.fx = g.fx; ga.fy = g.fy;
+    ga.scale_modifier = s->scale_modifier;
+    ga.radii = radii;
+    ga.tiles_touched = at<uint32_t>(geom, gl.tiles_touched);
+    ga.first_slot = at<uint32_t>(geom, gl.first_slot);
+    ga.clamped = at<uint8_t>(geom, gl.clamped);
+    ga.rec_flags = rec_flags;
+    ga.touched = touched;
+    ga.live_count = at<uint32_t>(const_cast<void*>(geom), gl.live_count);
+    ga.live_list = at<uint32_t>(const_cast<void*>(geom), gl.live_list);
+    ga.records = records;
+    ga.dL_dmeans2D = o->dL_dmeans2D; ga.dL_dcolors = o->dL_dcolors; ga.dL_dopacity = o->dL_dopacity;
+    ga.dL_dmeans3D = o->dL_dmeans3D; ga.dL_dcov3D = o->dL_dcov3D;
+    ga.dL_dscales = o->dL_dscales; ga.dL_drot = o->dL_drotations;
+    ga.acc = o->accumulate;
+    ga.slot_cap = slot_cap;
+    ga.grad_mask = o->grad_mask;
+    ga.mask_bits = o->grad_mask ? o->mask_bits : 0u;
+    ga.dL_dconic = o->dL_dconic;
+    ga.diag = diag_buffer(2, kDiagWords * 4 * (size_t)(P / 256 + 1));
+    { StageScope sc(ST_GAUSS_BWD, stream); launch_gauss_backward(ga, stream, writes_after); }
+    GS_LAUNCHED("gaussian backward");
+    return GS_OK;
 }
 
 }  // namespace
@@ -583,6 +779,8 @@ int gs_profile_set_stages(unsigned int mask) {
     profiler().mask.store(mask);
     return GS_OK;
 }
+
+long long gs_host_wait_ns(void) { return g_host_wait_ns.load(std::memory_order_relaxed); }
 
 int gs_profile_num_stages(void) { return ST_COUNT; }
 const char* gs_profile_stage_name(int i) { return (i >= 0 && i < ST_COUNT) ? kStageNames[i] : ""; }
@@ -690,89 +888,6 @@ int gs_rasterize_forward_begin(const gs_settings* s, const gs_params* gp, int* r
     }
 }
 
-// Per-call events ordering the shared preprocess between the views' streams (a small pool per thread).
-hipEvent_t multi_event(int i) {
-    thread_local hipEvent_t ev[2 * kMaxViews] = {};
-    if (!ev[i] && hipEventCreateWithFlags(&ev[i], hipEventDisableTiming) != hipSuccess) return nullptr;
-    return ev[i];
-}
-
-bool same_scene(const gs_params& a, const gs_params& b) {
-    return a.P == b.P && a.M == b.M && a.means3D == b.means3D && a.sh_dc == b.sh_dc && a.sh_rest == b.sh_rest &&
-           a.sh_dc_stride == b.sh_dc_stride && a.sh_rest_stride == b.sh_rest_stride && a.sh_half == b.sh_half &&
-           a.colors_precomp == b.colors_precomp && a.opacities == b.opacities && a.scales == b.scales &&
-           a.rotations == b.rotations && a.cov3D_precomp == b.cov3D_precomp && a.index == b.index &&
-           a.activation == b.activation;
-}
-
-int gs_rasterize_forward_begin_multi(int n, const gs_settings* const* s, const gs_params* const* gp, int* const* radii,
-                                     gs_alloc_fn alloc, void* const* alloc_ctx, const gs_stream_t* streams,
-                                     gs_forward_state** states) {
-    if (n < 1 || n > kMaxViews || !s || !gp || !radii || !alloc || !alloc_ctx || !streams || !states)
-        return set_error(GS_ERR_INVALID_ARG, "begin_multi: 1 <= n <= %d views and every array are required", kMaxViews);
-    for (int v = 0; v < n; ++v) states[v] = nullptr;
-    bool shared = gp[0]->P > 0 && !gp[0]->sh_half && !gp[0]->index;
-    for (int v = 0; v < n && shared; ++v) {
-        shared = same_scene(*gp[0], *gp[v]) && !s[v]->debug;
-        if (v && (s[v]->image_width != s[0]->image_width || s[v]->image_height != s[0]->image_height)) shared = false;
-    }
-    if (!shared) {  // the per-view calls (identical outputs)
-        for (int v = 0; v < n; ++v) {
-            const int rc = gs_rasterize_forward_begin(s[v], gp[v], radii[v], alloc, alloc_ctx[v], streams[v], &states[v]);
-            if (rc) {
-                for (int u = 0; u < v; ++u) gs_rasterize_forward_release(states[u]);
-                for (int u = 0; u < n; ++u) states[u] = nullptr;
-                return rc;
-            }
-        }
-        return GS_OK;
-    }
-    try {
-        std::unique_ptr<gs_forward_state> st[kMaxViews];
-        PreprocessMulti m;
-        m.nv = n;
-        hipStream_t s0 = (hipStream_t)streams[0];
-        const bool debug = false;
-        hipStream_t stream = s0;  // (GS_LAUNCHED)
-        for (int v = 0; v < n; ++v) {
-            int rc = validate_params(s[v], gp[v]);
-            if (rc) return rc;
-            st[v].reset(new gs_forward_state());
-            FwdState& f = st[v]->f;
-            f.s = *s[v];
-            f.gp = *gp[v];
-            f.g = make_grid(s[v]);
-            f.radii = radii[v];
-            rc = bin_prepare(f, 1, alloc, alloc_ctx[v], (hipStream_t)streams[v]);
-            if (rc) return rc;
-            m.a[v] = f.pa;
-            if (v && streams[v] != streams[0]) {  // the shared pass writes view v's buffers after their zeroing
-                hipEvent_t e = multi_event(v);
-                if (!e) return set_error(GS_ERR_HIP, "begin_multi: event");
-                GS_HIP(hipEventRecord(e, (hipStream_t)streams[v]));
-                GS_HIP(hipStreamWaitEvent(s0, e, 0));
-            }
-        }
-        { StageScope sc(ST_PREPROCESS, s0); launch_preprocess_multi(m, s0); }
-        GS_LAUNCHED("preprocess (views)");
-        hipEvent_t done = multi_event(kMaxViews);
-        if (!done) return set_error(GS_ERR_HIP, "begin_multi: event");
-        GS_HIP(hipEventRecord(done, s0));
-        for (int v = 0; v < n; ++v) {
-            hipStream_t sv = (hipStream_t)streams[v];
-            if (sv != s0) GS_HIP(hipStreamWaitEvent(sv, done, 0));
-            const int rc = bin_after_preprocess(st[v]->f, sv);
-            if (rc) return rc;
-        }
-        for (int v = 0; v < n; ++v) states[v] = st[v].release();
-        return GS_OK;
-    } catch (const std::exception& e) {
-        return set_error(GS_ERR_INVALID_ARG, "exception: %s", e.what());
-    } catch (...) {
-        return set_error(GS_ERR_INVALID_ARG, "unknown exception");
-    }
-}
-
 int gs_rasterize_forward_end(gs_forward_state* state, float* out_color, float* out_depth, gs_alloc_fn alloc,
                              void* alloc_ctx, gs_stream_t stream_, int* num_rendered) {
     std::unique_ptr<gs_forward_state> own(state);
@@ -783,48 +898,20 @@ int gs_rasterize_forward_end(gs_forward_state* state, float* out_color, float* o
             return set_error(GS_ERR_INVALID_ARG, "num_rendered, alloc, out_color and out_depth are required");
         *num_rendered = 0;
         FwdState& f = state->f;
-        const gs_settings* s = &f.s;
-        const int P = f.gp.P;
-        const bool debug = s->debug != 0;
         const Grid g = f.g;
-        if (P == 0) {  // rasterize_points.cu:57-72: zero outputs, empty buffers, no render
+        if (f.gp.P == 0) {  // rasterize_points.cu:57-72: zero outputs, empty buffers, no render
             alloc(alloc_ctx, 1, 0);
             GS_HIP(hipMemsetAsync(out_color, 0, sizeof(float) * 3 * (size_t)g.W * g.H, stream));
             GS_HIP(hipMemsetAsync(out_depth, 0, sizeof(float) * (size_t)g.W * g.H, stream));
             return GS_OK;
         }
-        void* geom = f.geom;
-        void* img = f.img;
         void* bin = nullptr;
         int K = 0;
         int rc = bin_end(f, alloc, alloc_ctx, stream, &bin, &K);
         if (rc) return rc;
-        const GeomLayout gl = geom_layout(P);
-        const ImgLayout il = img_layout(g.W, g.H);
-        const BinLayout bl = bin_layout(K, g.tiles);
-        RenderArgs ra;
-        ra.W = g.W; ra.H = g.H; ra.gx = g.gx; ra.gy = g.gy;
-        ra.ranges = at<uint2>(img, il.ranges);
-        ra.tile_order = at<uint32_t>(img, il.tile_order);
-        ra.order_ready = K > 0 && tile_sort_writes_ranges(g.tiles) ? 1 : 0;
-        ra.point_pairs = at<uint2>(bin, bl.point_pairs);
-        ra.bwd_items = at<uint2>(bin, bl.bwd_items);
-        ra.bwd_count = at<uint32_t>(img, il.bwd_count);
-        ra.item_cap = (uint32_t)(4 * bl.nslots);
-        ra.splat = at<Splat>(geom, gl.splat);
-        ra.bg = s->bg;
-        ra.final_T = at<float>(img, il.final_T);
-        ra.n_contrib = at<uint32_t>(img, il.n_contrib);
-        ra.tile_last = at<uint32_t>(img, il.tile_last);
-        ra.quad_last = at<uint32_t>(img, il.quad_last);
-        ra.ckpt = at<float4>(bin, bl.ckpt);
-        ra.used = at<uint64_t>(bin, bl.used);
-        ra.out_color = out_color;
-        ra.out_depth = out_depth;
-        ra.touched = at<uint8_t>(geom, gl.touched);
-        ra.diag = diag_buffer(0, kDiagWords * (size_t)g.tiles * 4);
-        { StageScope sc(ST_RENDER_FWD, stream); launch_render_forward(ra, stream); }
-        GS_LAUNCHED("render");
+        rc = render_launch(f, bin, (uint32_t)K, K > 0 && tile_sort_writes_ranges(g.tiles) ? 1 : 0, out_color,
+                           out_depth, stream);
+        if (rc) return rc;
         *num_rendered = K;
         return GS_OK;
     } catch (const std::exception& e) {
@@ -871,104 +958,229 @@ int gs_rasterize_backward(const gs_settings* s, int P, int M, int R, const float
     return gs_rasterize_backward_ex(s, &g2, R, radii, geom, binning, img, dL_dpix, &o, stream);
 }
 
+// the argument checks of a backward (gs_rasterize_backward_ex, gs_views_backward)
+static int validate_backward(const gs_settings* s, const gs_params* gp, int R, const int* radii, const void* geom,
+                      const void* binning, const void* img, const float* dL_dpix, const gs_grads* o) {
+    if (!s || !gp || !o) return set_error(GS_ERR_INVALID_ARG, "settings, params and grads are required");
+    const int P = gp->P;
+    if (P < 0) return set_error(GS_ERR_INVALID_ARG, "P must be >= 0");
+    if (P == 0) return GS_OK;
+    if (s->image_width <= 0 || s->image_height <= 0) return set_error(GS_ERR_INVALID_ARG, "image size must be positive");
+    if (!gp->means3D || !s->viewmatrix || !s->projmatrix || !s->bg || !s->campos)
+        return set_error(GS_ERR_INVALID_ARG, "means3D, viewmatrix, projmatrix, bg and campos are required");
+    if (gp->sh_dc && gp->M < sh_coeffs_needed(s->sh_degree))
+        return set_error(GS_ERR_INVALID_ARG, "sh has %d coefficients per channel, degree %d needs %d", gp->M,
+                         s->sh_degree, sh_coeffs_needed(s->sh_degree));
+    if (!gp->cov3D_precomp && (!gp->scales || !gp->rotations))
+        return set_error(GS_ERR_INVALID_ARG, "scales/rotations or cov3D_precomp are required");
+    if (gp->activation && !gp->opacities)
+        return set_error(GS_ERR_INVALID_ARG, "activation = 1 needs the raw opacities in the backward");
+    if (!geom || !img || !radii || !dL_dpix)
+        return set_error(GS_ERR_INVALID_ARG, "geometry/image buffers, radii and dL_dpix are required");
+    if (!o->dL_dmeans2D || !o->dL_dopacity || !o->dL_dmeans3D || !o->dL_dscales || !o->dL_drotations ||
+        (gp->M > 1 && o->dL_dsh_dc && !o->dL_dsh_rest))
+        return set_error(GS_ERR_INVALID_ARG, "gradient outputs are required");
+    if (R > 0 && !binning) return set_error(GS_ERR_INVALID_ARG, "binning buffer is required when num_rendered > 0");
+    return GS_OK;
+}
+
 int gs_rasterize_backward_ex(const gs_settings* s, const gs_params* gp, int R, const int* radii, const void* geom,
                              const void* binning, const void* img, const float* dL_dpix, const gs_grads* o,
                              gs_stream_t stream_) {
     try {
-        hipStream_t stream = (hipStream_t)stream_;
-        if (!s || !gp || !o) return set_error(GS_ERR_INVALID_ARG, "settings, params and grads are required");
-        const int P = gp->P;
-        if (P < 0) return set_error(GS_ERR_INVALID_ARG, "P must be >= 0");
-        if (P == 0) return GS_OK;
-        if (s->image_width <= 0 || s->image_height <= 0) return set_error(GS_ERR_INVALID_ARG, "image size must be positive");
-        if (!gp->means3D || !s->viewmatrix || !s->projmatrix || !s->bg || !s->campos)
-            return set_error(GS_ERR_INVALID_ARG, "means3D, viewmatrix, projmatrix, bg and campos are required");
-        if (gp->sh_dc && gp->M < sh_coeffs_needed(s->sh_degree))
-            return set_error(GS_ERR_INVALID_ARG, "sh has %d coefficients per channel, degree %d needs %d", gp->M,
-                             s->sh_degree, sh_coeffs_needed(s->sh_degree));
-        if (!gp->cov3D_precomp && (!gp->scales || !gp->rotations))
-            return set_error(GS_ERR_INVALID_ARG, "scales/rotations or cov3D_precomp are required");
-        if (gp->activation && !gp->opacities)
-            return set_error(GS_ERR_INVALID_ARG, "activation = 1 needs the raw opacities in the backward");
-        if (!geom || !img || !radii || !dL_dpix)
-            return set_error(GS_ERR_INVALID_ARG, "geometry/image buffers, radii and dL_dpix are required");
-        if (!o->dL_dmeans2D || !o->dL_dopacity || !o->dL_dmeans3D || !o->dL_dscales ||
-            !o->dL_drotations || (gp->M > 1 && o->dL_dsh_dc && !o->dL_dsh_rest))
-            return set_error(GS_ERR_INVALID_ARG, "gradient outputs are required");
-        if (R > 0 && !binning) return set_error(GS_ERR_INVALID_ARG, "binning buffer is required when num_rendered > 0");
-        const bool debug = s->debug != 0;
-        const Grid g = make_grid(s);
-        const GeomLayout gl = geom_layout(P);
-        const ImgLayout il = img_layout(g.W, g.H);
-        const BinLayout bl = bin_layout(R, g.tiles);
-        float4* records = R > 0 ? at<float4>(const_cast<void*>(binning), bl.records) : nullptr;
-        uint8_t* rec_flags = R > 0 ? at<uint8_t>(const_cast<void*>(binning), bl.rec_flags) : nullptr;
-        // per-Gaussian "has a record" bytes: k_gauss_bwd skips every Gaussian without one (all of
-        // its gradients are zero), which is most of them (occluded behind saturated pixels)
-        // (both zeroed by the forward: `touched` in preprocess, the flags with the tile ranges.  A
-        // second backward of the same forward finds the bytes of the first, which it sets again: the
-        // entries that get records depend on the forward alone)
-        uint8_t* touched = at<uint8_t>(const_cast<void*>(geom), gl.touched);
-        if (R > 0) {
-            uint32_t* bwd_count = at<uint32_t>(const_cast<void*>(img), il.bwd_count);
-            RenderBwdArgs rb;
-            rb.W = g.W; rb.H = g.H; rb.gx = g.gx; rb.gy = g.gy;
-            rb.ranges = at<uint2>(img, il.ranges);
-            rb.point_pairs = at<uint2>(binning, bl.point_pairs);
-            rb.bwd_items = at<uint2>(binning, bl.bwd_items);
-            rb.bwd_count = bwd_count;
-            rb.tile_last = at<uint32_t>(img, il.tile_last);
-            rb.item_cap = (uint32_t)(4 * bl.nslots);
-            rb.quad_last = at<uint32_t>(img, il.quad_last);
-            rb.ckpt = at<float4>(binning, bl.ckpt);
-            rb.used = at<uint64_t>(binning, bl.used);
-            rb.splat = at<Splat>(geom, gl.splat);
-            rb.bg = s->bg;
-            rb.final_T = at<float>(img, il.final_T);
-            rb.n_contrib = at<uint32_t>(img, il.n_contrib);
-            rb.dL_dpix = dL_dpix;
-            rb.records = records;
-            rb.rec_flags = rec_flags;
-            rb.touched = touched;
-            rb.diag = diag_buffer(1, kDiagWords * 4 * bl.nslots);
-            { StageScope sc(ST_RENDER_BWD, stream); launch_render_backward(rb, stream); }
-            GS_LAUNCHED("render backward");
+        const int rc = validate_backward(s, gp, R, radii, geom, binning, img, dL_dpix, o);
+        if (rc || gp->P == 0) return rc;
+        return backward_view(s, gp, R, radii, geom, binning, img, dL_dpix, o, (hipStream_t)stream_,
+                             (hipEvent_t)o->writes_after, 0xFFFFFFFFu);
+    } catch (const std::exception& e) {
+        return set_error(GS_ERR_INVALID_ARG, "exception: %s", e.what());
+    } catch (...) {
+        return set_error(GS_ERR_INVALID_ARG, "unknown exception");
+    }
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------
+// gs_views: the forwards and backwards of a batch of views of one scene
+// (DGE renders a batch of edited views per step, threestudio/systems/DGE.py:170-239)
+// ---------------------------------------------------------------------
+namespace {
+// ordering events of the views' backward calls, reused across batches
+struct EventPool {
+    std::mutex mu;
+    std::vector<hipEvent_t> free;
+    hipEvent_t get() {
+        {
+            std::lock_guard<std::mutex> g(mu);
+            if (!free.empty()) {
+                hipEvent_t e = free.back();
+                free.pop_back();
+                return e;
+            }
         }
-        GaussBwdArgs ga;
-        ga.P = P; ga.D = s->sh_degree; ga.M = gp->M; ga.W = g.W; ga.H = g.H; ga.gx = g.gx; ga.gy = g.gy;
-        ga.means3D = gp->means3D; ga.scales = gp->scales; ga.rotations = gp->rotations;
-        ga.cov3D_precomp = gp->cov3D_precomp; ga.opacities = gp->opacities;
-        ga.index = gp->index;
-        ga.sh = sh_view(*gp);
-        ga.dsh.dc = o->dL_dsh_dc;
-        ga.dsh.rest = o->dL_dsh_rest ? o->dL_dsh_rest : o->dL_dsh_dc;
-        ga.dsh.dc_stride = o->dsh_dc_stride;
-        ga.dsh.rest_stride = o->dsh_rest_stride;
-        ga.activation = gp->activation;
-        ga.view = s->viewmatrix; ga.proj = s->projmatrix; ga.campos = s->campos;
-        ga.tanfovx = s->tanfovx; ga.tanfovy = s->tanfovy; ga.fx = g.fx; ga.fy = g.fy;
-        ga.scale_modifier = s->scale_modifier;
-        ga.radii = radii;
-        ga.tiles_touched = at<uint32_t>(geom, gl.tiles_touched);
-        ga.first_slot = at<uint32_t>(geom, gl.first_slot);
-        ga.clamped = at<uint8_t>(geom, gl.clamped);
-        ga.rec_flags = rec_flags;
-        ga.touched = touched;
-        ga.live_count = at<uint32_t>(const_cast<void*>(geom), gl.live_count);
-        ga.live_list = at<uint32_t>(const_cast<void*>(geom), gl.live_list);
-        ga.records = records;
-        ga.merged = render_backward_merged();
-        ga.dL_dmeans2D = o->dL_dmeans2D; ga.dL_dcolors = o->dL_dcolors; ga.dL_dopacity = o->dL_dopacity;
-        ga.dL_dmeans3D = o->dL_dmeans3D; ga.dL_dcov3D = o->dL_dcov3D;
-        ga.dL_dscales = o->dL_dscales; ga.dL_drot = o->dL_drotations;
-        ga.acc = o->accumulate;
-        ga.grad_mask = o->grad_mask;
-        ga.mask_bits = o->grad_mask ? o->mask_bits : 0u;
-        ga.dL_dconic = o->dL_dconic;
-        ga.diag = diag_buffer(2, kDiagWords * 4 * (size_t)(P / 256 + 1));
-        { StageScope sc(ST_GAUSS_BWD, stream);
-        launch_gauss_backward(ga, stream, (hipEvent_t)o->writes_after); }
-        GS_LAUNCHED("gaussian backward");
+        hipEvent_t e = nullptr;
+        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return nullptr;
+        return e;
+    }
+    void put(hipEvent_t e) {
+        if (!e) return;
+        std::lock_guard<std::mutex> g(mu);
+        free.push_back(e);
+    }
+};
+EventPool& event_pool() {
+    static EventPool p;
+    return p;
+}
+
+bool can_speculate(const FwdState& f) {
+    const Grid& g = f.g;
+    if (f.s.debug || force_depth_keys32()) return false;
+    if (tile_sort_writes_ranges(g.tiles)) return true;  // single-pass tile sort
+    return tile_sort_fused(g.gx, g.gy) && rect_packable(g.gx, g.gy) && !tile_sort_unfused();  // two-level binning
+}
+}  // namespace
+
+struct gs_views {
+    int n = 0;
+    FwdState f[GS_MAX_VIEWS];
+    void* bin[GS_MAX_VIEWS] = {};
+    uint32_t layout[GS_MAX_VIEWS] = {};  // instances the binning buffer is laid out for
+    int spec[GS_MAX_VIEWS] = {};         // 1: capacity-sized, count checked by gs_views_check
+    long long K[GS_MAX_VIEWS] = {};      // instance count, -1 until the host knows it
+    hipEvent_t ev[GS_MAX_VIEWS] = {};    // the end of each view's work (forward, or per-Gaussian backward pass)
+    hipEvent_t fork = nullptr;           // the caller's stream, before the views' work
+    ~gs_views() {
+        for (int v = 0; v < GS_MAX_VIEWS; ++v) event_pool().put(ev[v]);
+        event_pool().put(fork);
+    }
+};
+
+namespace {
+// the views' streams wait for the caller's stream `join` (nullptr: none)
+int fork_from(gs_views* h, hipStream_t join, const gs_stream_t* streams) {
+    if (!join) return GS_OK;
+    bool other = false;
+    for (int v = 0; v < h->n; ++v) other |= (hipStream_t)streams[v] != join;
+    if (!other) return GS_OK;
+    if (!h->fork && !(h->fork = event_pool().get())) return set_error(GS_ERR_HIP, "could not create an event");
+    GS_HIP(hipEventRecord(h->fork, join));
+    for (int v = 0; v < h->n; ++v) {
+        bool seen = (hipStream_t)streams[v] == join;
+        for (int u = 0; u < v && !seen; ++u) seen = streams[u] == streams[v];
+        if (!seen) GS_HIP(hipStreamWaitEvent((hipStream_t)streams[v], h->fork, 0));
+    }
+    return GS_OK;
+}
+// `join` waits for every view stream's work so far
+int join_into(gs_views* h, hipStream_t join, const gs_stream_t* streams) {
+    if (!join) return GS_OK;
+    for (int v = 0; v < h->n; ++v) {
+        bool seen = (hipStream_t)streams[v] == join;
+        for (int u = 0; u < v && !seen; ++u) seen = streams[u] == streams[v];
+        if (seen) continue;
+        if (!h->ev[v] && !(h->ev[v] = event_pool().get())) return set_error(GS_ERR_HIP, "could not create an event");
+        GS_HIP(hipEventRecord(h->ev[v], (hipStream_t)streams[v]));
+        GS_HIP(hipStreamWaitEvent(join, h->ev[v], 0));
+    }
+    return GS_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int gs_views_forward(int n, const gs_settings* const* s, const gs_params* const* gp, float* const* out_color,
+                     float* const* out_depth, int* const* radii, int mode, gs_alloc_fn alloc, void* alloc_ctx,
+                     const gs_stream_t* streams, gs_stream_t join_, gs_views** out) {
+    try {
+        if (!out) return set_error(GS_ERR_INVALID_ARG, "out is required");
+        *out = nullptr;
+        if (n < 1 || n > GS_MAX_VIEWS || !s || !gp || !out_color || !out_depth || !radii || !alloc || !streams)
+            return set_error(GS_ERR_INVALID_ARG, "gs_views_forward: 1 <= n <= %d views and every array are required",
+                             GS_MAX_VIEWS);
+        if (mode != GS_VIEWS_EXACT && mode != GS_VIEWS_SPECULATE)
+            return set_error(GS_ERR_INVALID_ARG, "gs_views_forward: unknown mode %d", mode);
+        std::unique_ptr<gs_views> h(new gs_views());
+        h->n = n;
+        // one buffer for every view's geometry and image state (and the binning of the speculated views)
+        size_t off_geom[GS_MAX_VIEWS] = {}, off_img[GS_MAX_VIEWS] = {}, off_bin[GS_MAX_VIEWS] = {};
+        size_t total = 0;
+        for (int v = 0; v < n; ++v) {
+            int rc = validate_params(s[v], gp[v]);
+            if (rc) return rc;
+            if (!out_color[v] || !out_depth[v]) return set_error(GS_ERR_INVALID_ARG, "out_color/out_depth are required");
+            FwdState& f = h->f[v];
+            f.s = *s[v];
+            f.gp = *gp[v];
+            f.g = make_grid(s[v]);
+            f.radii = radii[v];
+            h->K[v] = -1;
+            const int P = f.gp.P;
+            if (P == 0) continue;
+            off_geom[v] = total;
+            total = align_up(total + geom_layout(P).total);
+            off_img[v] = total;
+            total = align_up(total + img_layout(f.g.W, f.g.H).total);
+            const uint32_t cap = mode == GS_VIEWS_SPECULATE && can_speculate(f) ? spec_capacity(P, f.g.W, f.g.H) : 0u;
+            if (cap) {
+                h->spec[v] = 1;
+                h->layout[v] = cap;
+                off_bin[v] = total;
+                total = align_up(total + bin_layout((int)cap, f.g.tiles).total);
+            }
+        }
+        char* base = static_cast<char*>(alloc(alloc_ctx, 0, total));
+        if (total && !base) return set_error(GS_ERR_ALLOC, "allocator returned NULL for the views' buffers");
+        hipStream_t join = (hipStream_t)join_;
+        int rc = fork_from(h.get(), join, streams);  // the views' streams start after the caller's work
+        if (rc) return rc;
+        // first halves on every view's stream: nothing waits for any count yet
+        for (int v = 0; v < n; ++v) {
+            FwdState& f = h->f[v];
+            if (f.gp.P == 0) continue;
+            hipStream_t stream = (hipStream_t)streams[v];
+            const bool debug = f.s.debug != 0;
+            rc = bin_prepare_in(f, 1, base + off_geom[v], base + off_img[v], stream);
+            if (rc) return rc;
+            { StageScope sc(ST_PREPROCESS, stream); launch_preprocess(f.pa, stream); }
+            GS_LAUNCHED("preprocess");
+            rc = bin_after_preprocess(f, stream);
+            if (rc) return rc;
+        }
+        // second halves: a speculated view's binning runs on the device count, capped at its capacity;
+        // the others wait for their count here (the reference's sync, rasterizer_impl.cu:236-239)
+        for (int v = 0; v < n; ++v) {
+            FwdState& f = h->f[v];
+            hipStream_t stream = (hipStream_t)streams[v];
+            const Grid& g = f.g;
+            if (f.gp.P == 0) {  // rasterize_points.cu:57-72
+                GS_HIP(hipMemsetAsync(out_color[v], 0, sizeof(float) * 3 * (size_t)g.W * g.H, stream));
+                GS_HIP(hipMemsetAsync(out_depth[v], 0, sizeof(float) * (size_t)g.W * g.H, stream));
+                h->K[v] = 0;
+                continue;
+            }
+            if (h->spec[v]) {
+                h->bin[v] = base + off_bin[v];
+                const uint32_t* counters = at<uint32_t>(f.img, img_layout(g.W, g.H).counters);
+                rc = bin_emit(f, h->bin[v], h->layout[v], counters, stream);
+                if (rc) return rc;
+                rc = render_launch(f, h->bin[v], h->layout[v], tile_sort_writes_ranges(g.tiles) ? 1 : 0, out_color[v],
+                                   out_depth[v], stream);
+            } else {
+                int K = 0;
+                rc = bin_end(f, alloc, alloc_ctx, stream, &h->bin[v], &K, 16 + v);
+                if (rc) return rc;
+                h->K[v] = K;
+                h->layout[v] = (uint32_t)K;
+                rc = render_launch(f, h->bin[v], (uint32_t)K, K > 0 && tile_sort_writes_ranges(g.tiles) ? 1 : 0,
+                                   out_color[v], out_depth[v], stream);
+            }
+            if (rc) return rc;
+        }
+        rc = join_into(h.get(), join, streams);
+        if (rc) return rc;
+        *out = h.release();
         return GS_OK;
     } catch (const std::exception& e) {
         return set_error(GS_ERR_INVALID_ARG, "exception: %s", e.what());
@@ -976,6 +1188,82 @@ int gs_rasterize_backward_ex(const gs_settings* s, const gs_params* gp, int R, c
         return set_error(GS_ERR_INVALID_ARG, "unknown exception");
     }
 }
+
+int gs_views_check(gs_views* h, int* num_rendered) {
+    if (!h) return set_error(GS_ERR_INVALID_ARG, "gs_views_check: handle is NULL");
+    int rc = GS_OK;
+    int first_bad = -1;
+    for (int v = 0; v < h->n; ++v) {
+        FwdState& f = h->f[v];
+        if (h->K[v] < 0 && f.st) {
+            Counts c;
+            const int r = read_counts(f, c);
+            if (r) return r;
+            h->K[v] = (long long)c.K;
+            if (c.prefilter_fail && rc != GS_ERR_PREFILTERED)
+                rc = set_error(GS_ERR_PREFILTERED, "Point is filtered although prefiltered is set. This shouldn't happen!");
+            if ((c.K > h->layout[v] || c.wide) && first_bad < 0) first_bad = v;
+        }
+        if (num_rendered) num_rendered[v] = (int)(h->K[v] < 0 ? 0 : std::min<long long>(h->K[v], 0x7FFFFFFF));
+    }
+    if (rc) return rc;
+    if (first_bad >= 0)
+        return set_error(GS_ERR_RETRY, "view %d: %lld tile instances exceed the speculative binning capacity %u (or "
+                         "its depth keys need the 32-bit sort): render the views again", first_bad,
+                         h->K[first_bad], h->layout[first_bad]);
+    return GS_OK;
+}
+
+int gs_views_backward(gs_views* h, const float* const* dL_dpix, const gs_grads* const* grads,
+                      const gs_stream_t* streams, void* writes_after, gs_stream_t join_) {
+    try {
+        if (!h || !dL_dpix || !grads || !streams)
+            return set_error(GS_ERR_INVALID_ARG, "gs_views_backward: handle, dL_dpix, grads and streams are required");
+        hipStream_t join = (hipStream_t)join_;
+        int rc0 = fork_from(h, join, streams);  // (the image gradients come from the caller's stream)
+        if (rc0) return rc0;
+        int prev = -1;
+        for (int v = 0; v < h->n; ++v) {
+            FwdState& f = h->f[v];
+            int rc = validate_backward(&f.s, &f.gp, (int)h->layout[v], f.radii, f.geom, h->bin[v], f.img, dL_dpix[v],
+                                       grads[v]);
+            if (rc) return rc;
+            if (f.gp.P == 0) continue;
+            hipStream_t sv = (hipStream_t)streams[v];
+            // accumulated writes in view order: view v's per-Gaussian pass after view prev's
+            hipEvent_t wa = prev < 0 ? (hipEvent_t)writes_after
+                                     : (streams[prev] != streams[v] ? h->ev[prev] : nullptr);
+            rc = backward_view(&f.s, &f.gp, (int)h->layout[v], f.radii, f.geom, h->bin[v], f.img, dL_dpix[v],
+                               grads[v], sv, wa, h->spec[v] ? h->layout[v] : 0xFFFFFFFFu);
+            if (rc) return rc;
+            if (!h->ev[v] && !(h->ev[v] = event_pool().get())) return set_error(GS_ERR_HIP, "could not create an event");
+            GS_HIP(hipEventRecord(h->ev[v], sv));
+            prev = v;
+        }
+        if (join)
+            for (int v = 0; v < h->n; ++v)
+                if (h->ev[v] && streams[v] != join_) GS_HIP(hipStreamWaitEvent(join, h->ev[v], 0));
+        return GS_OK;
+    } catch (const std::exception& e) {
+        return set_error(GS_ERR_INVALID_ARG, "exception: %s", e.what());
+    } catch (...) {
+        return set_error(GS_ERR_INVALID_ARG, "unknown exception");
+    }
+}
+
+void* gs_views_buffer(const gs_views* h, int v, int which) {
+    if (!h || v < 0 || v >= h->n) return nullptr;
+    switch (which) {
+        case 0: return h->f[v].geom;
+        case 1: return h->bin[v];
+        case 2: return h->f[v].img;
+        default: return nullptr;
+    }
+}
+
+long long gs_views_layout(const gs_views* h, int v) { return (!h || v < 0 || v >= h->n) ? -1 : (long long)h->layout[v]; }
+
+void gs_views_release(gs_views* h) { delete h; }
 
 int gs_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix, uint8_t* present,
                     gs_stream_t stream_) {

@@ -526,8 +526,10 @@ __global__ __launch_bounds__(kGB) void k_gauss_bwd_live(GaussBwdArgs a) {
         const int src = ok && a.index ? a.index[idx] : idx;  // parameter row
         s_gid[threadIdx.x] = (uint32_t)src;  // (SH rows are parameter rows)
         if (ok) gin = load_gauss_in(a, idx, src);
-        const uint32_t n = ok ? a.tiles_touched[idx] : 0u;
+        uint32_t n = ok ? a.tiles_touched[idx] : 0u;
         const uint32_t first = ok ? a.first_slot[idx] : 0u;  // (a live Gaussian has slots)
+        // (a speculative forward that overflowed its capacity is re-rendered; its slots stop at the capacity)
+        n = first < a.slot_cap ? min(n, a.slot_cap - first) : 0u;
         const uint32_t* flags = reinterpret_cast<const uint32_t*>(a.rec_flags);
         uint32_t fl[8];
 #pragma unroll
@@ -572,18 +574,11 @@ __global__ __launch_bounds__(kGB) void k_gauss_bwd_live(GaussBwdArgs a) {
                 for (int u = 0; u < 8; ++u) fl[u] = k0 + u < n ? flags[first + k0 + u] : 0u;
             }
             uint32_t m = 0;
-            const float4* recs;
-            if (a.merged) {  // one record per flagged slot
 #pragma unroll
-                for (int u = 0; u < 8; ++u) m |= fl[u] ? 1u << u : 0u;
-                recs = a.records + 3 * (size_t)(first + k0);
-            } else {
+            for (int u = 0; u < 8; ++u)
 #pragma unroll
-                for (int u = 0; u < 8; ++u)
-#pragma unroll
-                    for (int qd = 0; qd < 4; ++qd) m |= ((fl[u] >> (8 * qd)) & 0xFFu) ? 1u << (4 * u + qd) : 0u;
-                recs = a.records + 3 * (4 * (size_t)(first + k0));
-            }
+                for (int qd = 0; qd < 4; ++qd) m |= ((fl[u] >> (8 * qd)) & 0xFFu) ? 1u << (4 * u + qd) : 0u;
+            const float4* recs = a.records + 3 * (4 * (size_t)(first + k0));
             while (m) {
                 int bi[4];
                 bool use[4];

@@ -45,6 +45,7 @@ constexpr size_t kAlign = 256;
 
 __host__ __device__ inline size_t align_up(size_t x, size_t a = kAlign) { return (x + a - 1) / a * a; }
 inline int div_up(long long a, long long b) { return (int)((a + b - 1) / b); }
+__host__ __device__ inline uint32_t div_up_u(uint32_t a, uint32_t b) { return (a + b - 1) / b; }
 
 inline int ceil_log2(uint32_t n) {
     int b = 0;
@@ -251,13 +252,6 @@ struct PreprocessArgs {
     uint8_t* touched;    // zeroed here: k_render_fwd sets the bytes of Gaussians some pixel blends
 };
 void launch_preprocess(const PreprocessArgs& a, hipStream_t s);
-// several views of one scene, the shared inputs read once (fp32 SH rows, no index): gs_rasterize_forward_begin_multi
-constexpr int kMaxViews = 4;
-struct PreprocessMulti {
-    PreprocessArgs a[kMaxViews];
-    int nv;
-};
-void launch_preprocess_multi(const PreprocessMulti& m, hipStream_t s);
 void launch_depth_keys32(int P, const uint32_t* rect, const Splat* splat, uint32_t* key, hipStream_t s);
 void launch_mark_visible(int P, const float* means3D, const float* view, uint8_t* present, hipStream_t s);
 
@@ -269,7 +263,7 @@ void launch_mark_visible(int P, const float* means3D, const float* view, uint8_t
 int radix_sort_aux(uint32_t* key0, uint32_t* key1, uint2* pair0, uint2* pair1, const uint32_t* aux, uint32_t n,
                    int bits, int max_pass_bits, int ipt, uint32_t* hist, uint32_t* totals, int nblocks, hipStream_t s,
                    uint2* ranges = nullptr, const uint32_t* key_bias_not = nullptr, uint32_t* tile_order = nullptr,
-                   int ntiles = 0);
+                   int ntiles = 0, const uint32_t* n_dev = nullptr);
 // key_bias_not: the preprocess counter slots' ~min key (kCounterStride apart); the first pass sorts
 // (and writes) key - min
 // Stable sort of the K emitted instances on their tile id (key0 in slot
@@ -277,7 +271,8 @@ int radix_sort_aux(uint32_t* key0, uint32_t* key1, uint2* pair0, uint2* pair1, c
 // gauss_by_slot.  Returns the buffer index (0/1) holding keys and pairs.
 int tile_sort(uint32_t* key0, uint32_t* key1, uint2* pair0, uint2* pair1, const uint32_t* gauss_by_slot, uint32_t n,
               int bits, uint32_t* hist, uint32_t* totals, int nblocks, hipStream_t s, uint2* ranges,
-              uint32_t* tile_order, int ntiles);  // tile_order: the forward's dispatch order (single pass only)
+              uint32_t* tile_order, int ntiles,  // tile_order: the forward's dispatch order (single pass only)
+              const uint32_t* n_dev = nullptr);  // n_dev: preprocess counters, n = min(count, n) read on the device
 // the single-pass tile sort writes the tile ranges itself (and no sorted keys); two passes need k_ranges
 inline bool tile_sort_writes_ranges(int num_tiles) { return tile_sort_plan(num_tiles).passes == 1; }
 
@@ -305,6 +300,7 @@ struct EmitArgs {
     uint32_t* slot_gauss;        // K
     uint32_t* rec_flags32 = nullptr;  // K: zeroed by the emission (the backward's per-slot record flags)
     int scan_blocks;
+    uint32_t cap = 0xFFFFFFFFu;  // binning capacity: slots at or past it are not written (speculative forward)
     // two-level binning (tile_sort_fused): per-block column counts (k_scan_reduce), their scanned
     // form and totals, the column-ordered (Gaussian, slot) pairs, per-tile counts zeroed by block 0
     uint32_t* xhist = nullptr;
@@ -319,7 +315,7 @@ void launch_scan_emit(const EmitArgs& a, hipStream_t s);
 // (pairs_out/tile_key -> point_pairs, per-tile counts), ranges from the counts
 void launch_emit_fused(const EmitArgs& a, hipStream_t s);
 void launch_row_pass(const EmitArgs& a, uint32_t K, uint2* point_pairs, uint32_t* hist, int sort_blocks,
-                     uint2* ranges, hipStream_t s);
+                     uint2* ranges, hipStream_t s, const uint32_t* n_dev = nullptr);
 
 // tile ranges; also zeroes the backward's per-slot record flags (u32 per slot)
 void launch_ranges(const uint32_t* sorted_tile, int K, uint2* ranges, uint32_t* rec_flags32, hipStream_t s);
@@ -379,11 +375,9 @@ struct RenderBwdArgs {
     const float* dL_dpix;
     float4* records;     // [4*K][3] float4: one record per (slot, quadrant), kept entries only
     uint8_t* rec_flags;  // [4*K] set to 1 with each record (zeroed before the launch)
-    uint8_t* touched;    // [P] set to 1 for every Gaussian that got a record, or NULL: the forward set them
     uint64_t* diag;   // optional [item_cap][kDiagWords], by queue position (see diag_buffer)
 };
 void launch_render_backward(const RenderBwdArgs& a, hipStream_t s);
-int render_backward_merged();  // 1: one record per slot (k_render_bwd_tile), 0: per (slot, quadrant)
 
 struct GaussBwdArgs {
     int P, D, M, W, H, gx, gy;
@@ -402,11 +396,10 @@ struct GaussBwdArgs {
     const uint8_t* touched;    // [P] nonzero: the Gaussian has at least one record
     uint32_t* live_list;       // [P] k_gauss_live: block b's live Gaussians at [256 b, 256 b + live_count[b])
     uint32_t* live_count;      // [P/256] live Gaussians per 256-Gaussian block
-    const float4* records;     // [4*K][3] float4 by slot
-    int merged;                // records per slot (k_render_bwd_tile: flag u32 != 0, record at 3*slot) instead of
-                               // per (slot, quadrant) (k_render_bwd: flag byte 4*slot + q, record 3*(4*slot + q))
+    const float4* records;     // [4*K][3] float4: (slot, quadrant) record at 3*(4*slot + q), flag byte 4*slot + q
     float *dL_dmeans2D, *dL_dcolors, *dL_dopacity, *dL_dmeans3D, *dL_dcov3D, *dL_dscales, *dL_drot;
     uint32_t acc;  // GS_ACC_* bits: add into the output instead of overwriting
+    uint32_t slot_cap = 0xFFFFFFFFu;  // binning capacity (a speculative forward's slots end there)
     const uint8_t* grad_mask;  // optional [P]: outputs in mask_bits are multiplied by it
     uint32_t mask_bits;
     float* dL_dconic;          // optional [P,3]: the summed conic gradient (parity tests)

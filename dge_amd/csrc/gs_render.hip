@@ -513,411 +513,11 @@ __global__ __launch_bounds__(64, 3) void k_render_fwd(RenderArgs a) {
     }
 }
 
-// =====================================================================
-// forward, pipelined: one 128-thread workgroup (two waves) per 8x8 quadrant
-// =====================================================================
-// The blend of a quadrant is sequential only in its per-pixel transmittance
-// chain; the cull and the alpha test of an entry (~60% of k_render_fwd's VALU
-// work per kept entry) are independent of it.  A lone wave running all of it
-// spends ~260 cycles per kept entry (tools/probes/chain_latency.hip: a
-// dependent VALU result costs ~10 cycles, and every VALU -> SALU hand-off —
-// a ballot vote read by scalar code, a readfirstlane, a branch on __any — ~40),
-// so the heaviest quadrants (~650 kept entries over ~2800 list positions at
-// c2) set k_render_fwd's span while most of the chip idles.  Here the work of
-// one quadrant is split over two waves (on two SIMDs), stepped by one block
-// barrier per chunk of <= kPcChunk kept entries of one 256-position segment:
-//   wave 1 (producer): turns the previous chunk's votes into the backward's
-//                      blended-bit words (LDS atomics, list order), runs the
-//                      alpha test of chunk t for the 64 pixels, a' = ok ? alpha
-//                      : 0 into an LDS buffer (pixel_alpha4, the identical
-//                      instruction sequence, hence identical bits), then
-//                      gathers, culls against the quadrant and compacts the list
-//                      into the chunk ring (rounds of 128 positions, gathers one
-//                      round and ids two rounds ahead) until chunk t+1 is closed;
-//   wave 0 (chain):    blend_chain over chunk t-1 — T, colour, depth,
-//                      n_contrib, the checkpoint of every finished segment —
-//                      with no scalar hand-off per entry: the per-entry votes
-//                      stay in a lane mask, OR-reduced once per chunk.
-// Outputs are those of k_render_fwd bit for bit (same arithmetic per entry,
-// same entry order).  Checkpoints and blended-bit words are written for every
-// segment/word up to the last chained chunk (the backward reads none past the
-// last contributor).  ~20 KB of LDS and <= 128 VGPRs: 8 workgroups per CU
-// (2048 quadrants in flight chip-wide).
-constexpr int kPcChunk = 16;                  // kept entries per chunk (one pipeline step)
-constexpr int kPcCull = 128;                  // list positions per cull round (2 per lane)
-constexpr int kPcChunks = 16;                 // chunk slots in the ring
-constexpr int kPcRing = kPcChunk * kPcChunks;
-constexpr int kPcWords = 32;                  // blended-bit words being assembled (window)
-static_assert(kSegLen % kPcCull == 0, "a cull round lies inside one segment");
-// live chunk slots: chain t-1 .. producer t+1 plus one cull round's overshoot (<= 9 chunks)
-static_assert(kPcChunks >= 3 + (kPcChunk - 1 + kPcCull) / kPcChunk + 1, "chunk ring size");
-
-__device__ __forceinline__ uint32_t hw_simd_id() { return (__builtin_amdgcn_s_getreg(4 | (31 << 11)) >> 4) & 3u; }
-
-// OR over the 64 lanes with DPP row ops (the wave_sum_to_lane63 pattern); the result lands in lane 63
-template <int CTRL, int ROW_MASK>
-__device__ __forceinline__ uint32_t dpp_u32(uint32_t v) {
-    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROW_MASK, 0xF, false);
-}
-__device__ __forceinline__ uint32_t wave_or_to_lane63(uint32_t v) {
-    v |= dpp_u32<0xB1, 0xF>(v);
-    v |= dpp_u32<0x4E, 0xF>(v);
-    v |= dpp_u32<0x141, 0xF>(v);
-    v |= dpp_u32<0x140, 0xF>(v);
-    v |= dpp_u32<0x142, 0xA>(v);
-    v |= dpp_u32<0x143, 0xC>(v);
-    return v;
-}
-
-__global__ __launch_bounds__(128, 4) void k_render_fwd_pc(RenderArgs a) {
-    __shared__ __attribute__((aligned(16))) float r_x[kPcRing], r_y[kPcRing], r_cx[kPcRing], r_cy[kPcRing],
-        r_cz[kPcRing], r_op[kPcRing];
-    __shared__ float4 r_rgbd[kPcRing];
-    __shared__ __attribute__((aligned(16))) uint32_t r_pos[kPcRing];  // 1-based list position
-    __shared__ uint32_t s_meta[kPcChunks];        // chunk slot: entries | segment << 5
-    __shared__ uint32_t s_votes[kPcChunks];       // chunk slot: bit e = some pixel blended entry e
-    __shared__ f4v s_alpha[2][kPcChunk / 4][64];  // [chunk parity][group of 4 entries][pixel]
-    __shared__ unsigned long long s_words[kPcWords];
-    __shared__ uint32_t s_count[2];               // [step parity]: chunks closed | list culled << 31
-    __shared__ uint32_t s_stop[2];                // [step parity]: every pixel saturated
-    __shared__ uint32_t s_simd[2];
-    __shared__ uint64_t s_pstat;
-
-    // (wave index made uniform for the compiler: the role branches below are scalar branches)
-    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)), lane = (int)(threadIdx.x & 63);
-    // XCD-aware as k_render_fwd: blocks b, b+8, b+16, b+24 take the four quadrants of one tile
-    const int x8 = blockIdx.x & 7, j8 = blockIdx.x >> 3;
-    const int quad = j8 & 3, rank = (j8 >> 2) * 8 + x8;
-    if (rank >= a.gx * a.gy) return;
-    const int tile = (int)a.tile_order[rank];
-    const int qidx = 4 * tile + quad;
-    const int tx = tile % a.gx, ty = tile / a.gx;
-    const int bx0 = tx * kTile + (quad & 1) * kQuad, by0 = ty * kTile + (quad >> 1) * kQuad;
-    const int px = bx0 + (lane & 7), py = by0 + (lane >> 3);
-    const bool inside = px < a.W && py < a.H;
-    const float pfx = (float)px, pfy = (float)py;
-    const uint2 range = a.ranges[tile];
-    const bool list_empty = range.y <= range.x;
-    const uint32_t k_last = list_empty ? 0u : range.y - 1;
-#ifdef GS_FWD_PRIO_RANKS
-    if (rank < GS_FWD_PRIO_RANKS) __builtin_amdgcn_s_setprio(3);
-#endif
-    if (a.diag && lane == 0) s_simd[wave] = hw_simd_id();
-    const uint64_t t_entry = a.diag ? __builtin_amdgcn_s_memrealtime() : 0;
-
-    if (threadIdx.x < 2) s_stop[threadIdx.x] = 0u;
-    // Step control, evaluated identically by both waves after each barrier (the published words are
-    // double-buffered by step parity, so no wave can see a later step's value): the loop ends when
-    // the chain wave saw every pixel saturate, or when the list is culled and its last chunk chained.
-    // Each role runs its own loop (disjoint register live ranges) with one barrier per step.
-    const auto step_go = [&](int t, uint32_t& nch, bool& done) {
-        const uint32_t cw = s_count[t & 1];
-        nch = cw & 0x7FFFFFFFu;
-        done = (cw >> 31) != 0;
-        return !(s_stop[t & 1] || (done && t - 1 >= (int)nch));
-    };
-
-    if (wave == 1) {
-        // ================= producer =================
-        if (lane < kPcWords) s_words[lane] = 0ull;
-        uint32_t cb = range.x;    // first list position of the next cull round
-        uint32_t n_closed = 0;    // chunks closed (their entries and meta are final)
-        uint32_t fill = 0;        // entries of the open chunk (index n_closed)
-        uint32_t open_seg = 0;    // segment of the open chunk
-        uint32_t ids[2];
-        Entry cur[2], nxt[2];  // gathered entries of the round being culled and of the next one
-        const auto load_ids = [&](uint32_t b) {
-#pragma unroll
-            for (int i = 0; i < 2; ++i) {
-                const uint32_t k = b + 64 * i + lane;
-                ids[i] = list_empty ? 0u : a.point_pairs[k < range.y ? k : k_last].x;
-            }
-        };
-        const auto close_open = [&]() {  // a partial chunk: its pad slots blend nothing (zero opacity, colour)
-            const uint32_t cs = n_closed % kPcChunks;
-            if (lane == 0) s_meta[cs] = fill | open_seg << 5;
-            if (lane >= (int)fill && lane < kPcChunk) {
-                const uint32_t slot = cs * kPcChunk + lane;
-                r_x[slot] = r_y[slot] = r_cx[slot] = r_cy[slot] = r_cz[slot] = r_op[slot] = 0.f;
-                r_rgbd[slot] = make_float4(0.f, 0.f, 0.f, 0.f);
-                r_pos[slot] = 0u;
-            }
-            ++n_closed;
-            fill = 0;
-        };
-        const auto cull_round = [&]() {
-            const uint32_t seg = (cb - range.x) / kSegLen;
-            if (fill > 0 && seg != open_seg) close_open();  // a chunk holds one segment's entries
-            open_seg = seg;
-            uint32_t nk = 0;
-#pragma unroll
-            for (int i = 0; i < 2; ++i) {
-                const uint32_t k = cb + 64 * i + lane;
-                const bool keep = k < range.y && cull_keep(cur[i].xy, cur[i].co, (float)bx0, (float)by0);
-                const uint64_t km = __ballot(keep);
-                if (keep) {
-                    const uint32_t j = fill + nk + __popcll(km & lanemask_lt());
-                    const uint32_t slot = ((n_closed + j / kPcChunk) % kPcChunks) * kPcChunk + j % kPcChunk;
-                    r_x[slot] = cur[i].xy.x;
-                    r_y[slot] = cur[i].xy.y;
-                    r_cx[slot] = cur[i].co.x;
-                    r_cy[slot] = -cur[i].co.y;  // (negated: pixel_alpha4)
-                    r_cz[slot] = cur[i].co.z;
-                    r_op[slot] = cur[i].co.w;
-                    r_rgbd[slot] = cur[i].f;
-                    r_pos[slot] = k - range.x + 1;  // 1-based contributor index (forward.cu:331)
-                }
-                nk += (uint32_t)__popcll(km);
-            }
-            const uint32_t total = fill + nk, full = total / kPcChunk;
-            if (lane < (int)full) s_meta[(n_closed + lane) % kPcChunks] = kPcChunk | seg << 5;
-            n_closed += full;
-            fill = total % kPcChunk;
-#pragma unroll
-            for (int i = 0; i < 2; ++i) {
-                cur[i] = nxt[i];
-                nxt[i] = gather_entry(a.splat, ids[i]);
-            }
-            load_ids(cb + 3 * kPcCull);
-            cb += kPcCull;
-            if (cb >= range.y && fill > 0) close_open();
-        };
-        const auto cull_until = [&](uint32_t target) {
-            while (n_closed < target && cb < range.y) cull_round();
-        };
-        const auto publish = [&](int slot) {
-            if (lane == 0) s_count[slot] = n_closed | (cb >= range.y ? 0x80000000u : 0u);
-        };
-        // blended-bit words: those below word `wnew` are final (later chunks lie past them)
-        uint32_t wlo = 0, w_end = 0;  // first unwritten word; one past the last word owed
-        uint64_t* used = a.used + (size_t)used_base(range.x, tile) * 4 + quad;
-        const auto flush_below = [&](uint32_t wnew) {
-            for (; wlo < wnew; wlo += kPcWords) {
-                const uint32_t w = wlo + (uint32_t)lane;
-                if (lane < kPcWords && w < wnew) {
-                    used[(size_t)w * 4] = s_words[w % kPcWords];
-                    s_words[w % kPcWords] = 0ull;
-                }
-            }
-            wlo = wnew;
-        };
-        const auto convert = [&](int c) {  // the chain's votes of chunk c -> words
-            const int cs = c % kPcChunks;
-            const uint32_t nc = s_meta[cs] & 31u, votes = s_votes[cs];
-            const uint32_t p_first = __builtin_amdgcn_readfirstlane(r_pos[cs * kPcChunk]) - 1u;
-            const uint32_t p_last = __builtin_amdgcn_readfirstlane(r_pos[cs * kPcChunk + nc - 1]) - 1u;
-            flush_below(p_first >> 6);
-            if (lane < (int)nc && ((votes >> lane) & 1u)) {
-                const uint32_t p = r_pos[cs * kPcChunk + lane] - 1u;
-                atomicOr(&s_words[(p >> 6) % kPcWords], 1ull << (p & 63u));
-            }
-            w_end = (p_last >> 6) + 1;
-        };
-        if (!list_empty) {  // gathers two rounds ahead, ids three
-            load_ids(range.x);
-#pragma unroll
-            for (int i = 0; i < 2; ++i) cur[i] = gather_entry(a.splat, ids[i]);
-            load_ids(range.x + kPcCull);
-#pragma unroll
-            for (int i = 0; i < 2; ++i) nxt[i] = gather_entry(a.splat, ids[i]);
-            load_ids(range.x + 2 * kPcCull);
-        }
-        // a quadrant without a pixel inside the image blends nothing (k_render_fwd's first-round exit)
-        if (__any(inside)) cull_until(1);
-        else cb = range.y;
-        publish(0);
-        __syncthreads();
-        uint64_t p_alpha = 0, p_cull = 0;
-        int pending = -1;  // the chunk the chain wave took in the previous step: its votes are final
-        for (int t = 0;; ++t) {
-            uint32_t nch;
-            bool done;
-            if (!step_go(t, nch, done)) break;
-            const uint64_t q0 = a.diag ? __builtin_amdgcn_s_memtime() : 0;
-            if (pending >= 0) convert(pending);
-            pending = (t >= 1 && t - 1 < (int)nch) ? t - 1 : -1;  // (the chain wave's test, same words)
-            const uint64_t q1 = a.diag ? __builtin_amdgcn_s_memtime() : 0;
-            if (t < (int)nch) {          // alpha test of chunk t: a' = ok ? alpha : 0 (blend_chain's operand)
-                const int cs = t % kPcChunks;
-                const int nc = (int)(s_meta[cs] & 31u);
-                // two groups of four at a time (four independent packed streams); a group past the chunk's
-                // end computes an unused slot
-                for (int g = 0; 4 * g < nc; g += 2) {
-                    f4v ap[2];
-#pragma unroll
-                    for (int h = 0; h < 2; ++h) {
-                        const int ri = cs * kPcChunk + 4 * (g + h);
-                        const auto ld4 = [&](const float* f) { return *reinterpret_cast<const f4v*>(f + ri); };
-                        f4v dx4, dy4, G4, al;
-                        bool ok[4];
-                        pixel_alpha4(ld4(r_x), ld4(r_y), ld4(r_cx), ld4(r_cy), ld4(r_cz), ld4(r_op), -pfx, -pfy,
-                                     dx4, dy4, G4, al, ok);
-#pragma unroll
-                        for (int u = 0; u < 4; ++u) ap[h][u] = ok[u] ? al[u] : 0.0f;
-                    }
-                    s_alpha[t & 1][g][lane] = ap[0];
-                    s_alpha[t & 1][g + 1][lane] = ap[1];
-                }
-            }
-            const uint64_t q2 = a.diag ? __builtin_amdgcn_s_memtime() : 0;
-            if (!done) cull_until((uint32_t)(t + 2));  // chunk t+1 closed for the next step
-            publish((t + 1) & 1);
-            if (a.diag) {
-                p_alpha += q2 - q1;
-                p_cull += __builtin_amdgcn_s_memtime() - q2;
-            }
-            __syncthreads();
-        }
-        if (pending >= 0) convert(pending);  // the last chunk the chain wave took
-        flush_below(w_end);
-        if (a.diag) {  // (diagnostics) the producer's cycles in the alpha tests and the cull, for wave 0's record
-            if (lane == 0) s_pstat = p_alpha | p_cull << 32;
-            __syncthreads();
-        }
-        return;
-    }
-    __syncthreads();  // (the producer's prologue)
-
-    // ================= chain wave (wave 0) =================
-    float Ts = inside ? 1.0f : -1.0f;  // signed transmittance (blend_chain)
-    f2v C01 = {0.f, 0.f}, C2D = {0.f, 0.f}, L01 = {0.f, 0.f};
-    float L2 = 0.f;
-    uint32_t last = 0;
-    uint32_t cur_seg = 0;  // segment of the chain position (its checkpoint is owed)
-    bool chained = false;  // any chunk chained
-    uint32_t diag_kept = 0;
-    float4* ckpt = a.ckpt + ((size_t)ckpt_base(range.x, tile) * 4 + quad) * 64;
-    const uint64_t t_start = a.diag ? __builtin_amdgcn_s_memrealtime() : 0;
-    const uint64_t c_start = a.diag ? __builtin_amdgcn_s_memtime() : 0;
-    uint64_t c_chain = 0;
-    struct Ops {  // a group's operands: alpha of this lane's pixel, colours, positions
-        f4v a4;
-        float4 f[4];
-        uint4 p4;
-    };
-    for (int t = 0;; ++t) {
-        uint32_t nch;
-        bool done;
-        if (!step_go(t, nch, done)) break;
-        const int c = t - 1;
-        if (c >= 0 && c < (int)nch) {
-            const uint64_t c0 = a.diag ? __builtin_amdgcn_s_memtime() : 0;
-            const int cs = c % kPcChunks;
-            const uint32_t meta = __builtin_amdgcn_readfirstlane(s_meta[cs]);
-            const int nc = (int)(meta & 31u);
-            const uint32_t seg = meta >> 5;
-            if (!__any(Ts > 0.0f)) {  // every pixel saturated: nothing more to blend
-                if (lane == 0) {
-                    s_stop[(t + 1) & 1] = 1u;
-                    s_votes[cs] = 0u;
-                }
-            } else {
-                if (seg != cur_seg) {  // the checkpoints of the segments before this chunk's
-                    ckpt[(size_t)cur_seg * 256 + lane] = make_float4(fabsf(Ts), L01.x, L01.y, L2);
-                    L01 = f2v{0.f, 0.f};
-                    L2 = 0.f;
-                    for (uint32_t s2 = cur_seg + 1; s2 < seg; ++s2)
-                        ckpt[(size_t)s2 * 256 + lane] = make_float4(fabsf(Ts), 0.f, 0.f, 0.f);
-                    cur_seg = seg;
-                }
-                const f4v* al = s_alpha[c & 1][0];
-                const auto load_ops = [&](int g, Ops& o) {
-                    const int ri = cs * kPcChunk + 4 * g;
-                    o.a4 = al[g * 64 + lane];
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) o.f[u] = r_rgbd[ri + u];
-                    o.p4 = *reinterpret_cast<const uint4*>(&r_pos[ri]);
-                };
-                uint32_t lv = 0;  // this pixel's votes: bit e = entry e of the chunk blended here
-                // four entries: the transmittance chain first (the critical path), then the sums, which
-                // only need each entry's Tw; pad entries (a' = 0, zero colour) change nothing
-                const auto group = [&](int g, const Ops& o) {
-                    const uint32_t pu[4] = {o.p4.x, o.p4.y, o.p4.z, o.p4.w};
-                    float tw[4];
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) tw[u] = blend_t(o.a4[u], Ts);
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) {
-                        const float w = blend_sums(o.a4[u], tw[u], o.f[u], pu[u], C01, C2D, L01, L2, last);
-                        lv |= w > 0.0f ? 1u << (4 * g + u) : 0u;
-                    }
-                };
-                Ops oa, ob;  // ping-pong: a group's operands are read while the previous group blends
-                load_ops(0, oa);
-                if (4 < nc) load_ops(1, ob);
-                group(0, oa);
-                if (4 < nc) {
-                    if (8 < nc) load_ops(2, oa);
-                    group(1, ob);
-                    if (8 < nc) {
-                        if (12 < nc) load_ops(3, ob);
-                        group(2, oa);
-                        if (12 < nc) group(3, ob);
-                    }
-                }
-                const uint32_t votes = wave_or_to_lane63(lv);
-                if (lane == 63) s_votes[cs] = votes;
-                chained = true;
-                diag_kept += nc;
-            }
-            if (a.diag) c_chain += __builtin_amdgcn_s_memtime() - c0;
-        }
-        __syncthreads();
-    }
-
-    if (a.diag) __syncthreads();  // (diagnostics: the producer's s_pstat)
-    // the owed checkpoint of the last chained segment
-    const float T = fabsf(Ts);
-    if (chained) ckpt[(size_t)cur_seg * 256 + lane] = make_float4(T, L01.x, L01.y, L2);
-    if (inside) {
-        const size_t pix = (size_t)a.W * py + px;
-        const size_t HW = (size_t)a.W * a.H;
-        a.final_T[pix] = T;
-        a.n_contrib[pix] = last;
-        a.out_color[pix] = __builtin_fmaf(T, a.bg[0], C01.x);
-        a.out_color[HW + pix] = __builtin_fmaf(T, a.bg[1], C01.y);
-        a.out_color[2 * HW + pix] = __builtin_fmaf(T, a.bg[2], C2D.x);
-        a.out_depth[pix] = C2D.y;
-    }
-    const uint32_t m = wave_max_u32(inside ? last : 0u);
-    if (m) {  // multi-segment windows first (class 0), single segments last
-        const uint32_t nseg = (m + kSegLen - 1) / kSegLen;
-        emit_items(a, tile, quad, nseg, nseg > 1 ? 128u * nseg : 0u, lane);
-    }
-    if (lane == 0) {
-        a.quad_last[qidx] = m;
-        if (m) atomicMax(&a.tile_last[tile], m);
-        if (a.diag) {
-            uint64_t* d = a.diag + kDiagWords * (size_t)qidx;
-            d[0] = t_entry;
-            d[1] = __builtin_amdgcn_s_memrealtime();
-            d[2] = diag_kept;
-            d[3] = s_pstat;  // producer cycles: alpha tests | cull << 32
-            d[4] = c_chain;
-            d[5] = __builtin_amdgcn_s_memtime() - c_start;
-            d[6] = s_simd[0] | s_simd[1] << 2 | (uint64_t)(t_start - t_entry) << 8 | (uint64_t)rank << 40;
-            d[7] = wave_location();
-        }
-    }
-}
-
-static int fwd_variant() {
-    static int v = -1;
-    if (v < 0) {
-        const char* e = getenv("DGE_AMD_FWD");
-        v = (e && e[0] == '1') ? 1 : 0;  // 0: one wave per quadrant (k_render_fwd), 1: pipelined (experiment)
-    }
-    return v;
-}
-
 void launch_render_forward(const RenderArgs& a, hipStream_t s) {
     const int tiles = a.gx * a.gy;
     if (tiles <= 0) return;
     if (!a.order_ready) hipLaunchKernelGGL(k_tile_order, dim3(1), dim3(1024), 0, s, a.ranges, tiles, a.tile_order);
-    if (fwd_variant() == 1)
-        hipLaunchKernelGGL(k_render_fwd_pc, dim3(div_up(tiles, 8) * 32), dim3(128), 0, s, a);
-    else
-        hipLaunchKernelGGL(k_render_fwd, dim3(div_up(tiles, 8) * 32), dim3(64), 0, s, a);
+    hipLaunchKernelGGL(k_render_fwd, dim3(div_up(tiles, 8) * 32), dim3(64), 0, s, a);
 }
 
 // =====================================================================
@@ -1105,8 +705,7 @@ static_assert(kSegLen % kBwdHalf == 0, "whole staging units per segment");
 // sums are reduce-scattered across the wave (quad_reduce).  Each kept entry gets
 // one record at 4*slot + quadrant (slot: the binning slot, so k_gauss_bwd reads
 // a Gaussian's records contiguously) and a flag.
-template <bool LOOP>
-__global__ __launch_bounds__(64, GS_BWD_WAVES) void k_render_bwd(RenderBwdArgs a, uint32_t first_item) {
+__global__ __launch_bounds__(64, GS_BWD_WAVES) void k_render_bwd(RenderBwdArgs a) {
     // kept entries of a half-segment, compacted back to front, + a group of padding
     // (one array per field: four consecutive entries' field is one 16-B read, see bwd_quad)
     __shared__ __attribute__((aligned(16))) float s_x[kBwdHalf + kBwdGroup], s_y[kBwdHalf + kBwdGroup];
@@ -1117,17 +716,17 @@ __global__ __launch_bounds__(64, GS_BWD_WAVES) void k_render_bwd(RenderBwdArgs a
     __shared__ uint32_t s_pos[kBwdHalf + kBwdGroup];
     __shared__ uint2 s_pair[kBwdHalf + kBwdGroup];  // (Gaussian, slot) of the kept entries: the record writes
     const int lane = threadIdx.x;
-    // block -> work item (quadrant, segment) of the forward's list, heaviest class first:
-    // first_item + blockIdx.x (LOOP: then + gridDim.x while items remain); blocks past the list's end
-    // exit (they dispatch after every real item; see launch_render_backward for the grid).  (A
-    // persistent-wave work queue measured slower than the hardware dispatcher here.)
+    // block -> work item (quadrant, segment) of the forward's list, heaviest class first; blocks past
+    // the list's end exit (they dispatch after every real item; see launch_render_backward for the
+    // grid).  (A persistent-wave work queue measured slower than the hardware dispatcher here.)
     uint32_t n_cls[kItemClasses], n_items = 0;
 #pragma unroll
     for (int c = 0; c < kItemClasses; ++c) {
         n_cls[c] = a.bwd_count[item_count_at(c)];
         n_items += n_cls[c];
     }
-    for (uint32_t qi = first_item + blockIdx.x; qi < n_items; qi += gridDim.x) {
+    const uint32_t qi = blockIdx.x;
+    if (qi >= n_items) return;
     uint32_t cls = 0, idx = qi;  // class regions in order: heaviest items first
 #pragma unroll
     for (int c = 0; c < kItemClasses - 1; ++c)
@@ -1271,7 +870,6 @@ __global__ __launch_bounds__(64, GS_BWD_WAVES) void k_render_bwd(RenderBwdArgs a
                 finish_record(make_float4(s_cx[kw], -s_cy[kw], s_cz[kw], s_op[kw]), S, ddelx_dx, ddely_dy,
                               a.records + 3 * rec);
                 a.rec_flags[rec] = 1;
-                if (a.touched) a.touched[pr.x] = 1;
             }
         }
         if (a.diag) c_replay += __builtin_amdgcn_s_memtime() - c0;
@@ -1288,272 +886,14 @@ __global__ __launch_bounds__(64, GS_BWD_WAVES) void k_render_bwd(RenderBwdArgs a
         d[6] = (uint64_t)seg << 32 | (uint32_t)qidx;
         d[7] = wave_location();
     }
-    if (!LOOP) break;
-    }
-}
-
-// =====================================================================
-// backward, merged per tile: one 256-thread workgroup per (tile, segment)
-// =====================================================================
-// The four quadrant waves of a tile replay the same 256 list positions (each
-// its own window, pixel state and blended bits, exactly as k_render_bwd), in
-// quarters of 64 positions.  A wave's finished per-(entry, quadrant) record
-// goes to an LDS table instead of HBM; after each quarter one wave adds the
-// tile's four quadrant records of every kept position in quadrant order and
-// writes ONE record per (slot) with a u32 flag: a quarter of k_render_bwd's
-// record and flag stores, whole-record writes, one (Gaussian, slot) list read
-// and one Splat gather per position for the tile instead of one per quadrant,
-// and k_gauss_bwd reads a quarter of the records.  Fixed summation order:
-// bitwise reproducible.  Work items (tile, segment << 2) come from
-// k_bwd_tile_items (multi-segment tiles first).
-constexpr int kBwdQuarter = 64;  // list positions per replay round
-
-__global__ __launch_bounds__(1024) void k_bwd_tile_items(RenderBwdArgs a, int tiles) {
-    __shared__ uint32_t cnt[2];
-    if (threadIdx.x < 2) cnt[threadIdx.x] = 0u;
-    __syncthreads();
-    uint2* items = const_cast<uint2*>(a.bwd_items);
-    for (int t = threadIdx.x; t < tiles; t += 1024) {
-        const uint32_t last = a.tile_last[t];
-        const uint32_t nseg = (last + kSegLen - 1) / kSegLen;
-        if (nseg > 1) {  // multi-segment tiles at the front: they dispatch first
-            const uint32_t b = atomicAdd(&cnt[0], nseg);
-            for (uint32_t k = 0; k < nseg; ++k) items[b + k] = make_uint2((uint32_t)t, k << 2);
-        } else if (nseg == 1) {
-            const uint32_t b = atomicAdd(&cnt[1], 1u);
-            items[a.item_cap - 1 - b] = make_uint2((uint32_t)t, 0u);
-        }
-    }
-    __syncthreads();
-    if (threadIdx.x < 2) const_cast<uint32_t*>(a.bwd_count)[2 + threadIdx.x] = cnt[threadIdx.x];
-}
-
-template <bool LOOP>
-__global__ __launch_bounds__(256, 3) void k_render_bwd_tile(RenderBwdArgs a, uint32_t first_item) {
-    constexpr int QS = kBwdQuarter + kBwdGroup;  // staged entries per wave (+ a group of padding)
-    __shared__ __attribute__((aligned(16))) float s_x[4][QS], s_y[4][QS], s_cx[4][QS], s_cy[4][QS], s_cz[4][QS],
-        s_op[4][QS];
-    __shared__ float4 s_rgb[4][QS];
-    __shared__ uint32_t s_pos[4][QS];
-    __shared__ float s_rec[4][kSegLen][9];  // finished quadrant records by position in the segment
-    __shared__ uint64_t s_kept[4][4];       // kept positions of each quadrant, per quarter
-    const int q = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const uint32_t n_multi = a.bwd_count[2], n_items = n_multi + a.bwd_count[3];
-    for (uint32_t qi = first_item + blockIdx.x; qi < n_items; qi += gridDim.x) {
-    const uint2 item = qi < n_multi ? a.bwd_items[qi] : a.bwd_items[a.item_cap - 1 - (qi - n_multi)];
-    const int tile = (int)item.x, seg = (int)(item.y >> 2);
-    const int qidx = 4 * tile + q;
-    const int tx = tile % a.gx, ty = tile / a.gx;
-    const int bx0 = tx * kTile + (q & 1) * kQuad, by0 = ty * kTile + (q >> 1) * kQuad;
-    const int px = bx0 + (lane & 7), py = by0 + (lane >> 3);
-    const bool inside = px < a.W && py < a.H;
-    const float pfx = (float)px, pfy = (float)py;
-
-    const uint2 range = a.ranges[tile];
-    const int lo = seg * kSegLen;
-    const int tile_n = min(kSegLen, (int)a.tile_last[tile] - lo);  // the tile's positions in this segment
-    const int window = (int)a.quad_last[qidx];
-    const int nseg_q = (window + kSegLen - 1) / kSegLen;
-    // this quadrant's part [lo, limit) of the segment (empty when its window ends before it)
-    const int limit = seg >= nseg_q ? lo : seg == nseg_q - 1 ? window : lo + kSegLen;
-    const int n = limit - lo;
-
-    const uint32_t* used32 = reinterpret_cast<const uint32_t*>(a.used + (size_t)used_base(range.x, tile) * 4 + q);
-    uint2 pairs[4];
-    uint32_t kb = 0u;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int j = 64 * i + lane, k = lo + j;
-        pairs[i] = j < tile_n ? a.point_pairs[range.x + k] : make_uint2(0u, 0u);
-        const uint32_t ub = j < n ? used32[(size_t)(k >> 6) * 8 + ((k >> 5) & 1)] : 0u;
-        kb |= ((ub >> (k & 31)) & 1u) << i;
-    }
-    // the kept entries' Splats one quarter ahead: quarter i-1's gathers are in flight during quarter i
-    Entry cur = gather_entry(a.splat, (kb >> 3) & 1u ? pairs[3].x : 0u);
-
-    const size_t HW = (size_t)a.W * a.H;
-    const size_t pix = inside ? (size_t)a.W * py + px : 0;
-    const float T_final = inside && n > 0 ? a.final_T[pix] : 0.f;
-    const uint32_t last_contributor = inside && n > 0 ? a.n_contrib[pix] : 0u;
-    float dp0 = 0.f, dp1 = 0.f, dp2 = 0.f;
-    if (inside && n > 0) {
-        dp0 = a.dL_dpix[pix];
-        dp1 = a.dL_dpix[HW + pix];
-        dp2 = a.dL_dpix[2 * HW + pix];
-    }
-    const float nbg = -T_final * (a.bg[0] * dp0 + a.bg[1] * dp1 + a.bg[2] * dp2);
-    float T = T_final, D0 = 0.f, D1 = 0.f, D2 = 0.f;
-    if (n > 0 && limit < window) {  // start inside the window (see k_render_bwd)
-        const float4* ck = a.ckpt + ((size_t)ckpt_base(range.x, tile) * 4 + q) * 64;
-        T = ck[(size_t)seg * 256 + lane].x;
-        float S0 = 0.f, S1 = 0.f, S2 = 0.f;
-        for (int k = nseg_q - 1; k > seg; --k) {
-            const float4 c = ck[(size_t)k * 256 + lane];
-            S0 += c.y;
-            S1 += c.z;
-            S2 += c.w;
-        }
-        const float inv = 1.0f / T;
-        D0 = S0 * inv;
-        D1 = S1 * inv;
-        D2 = S2 * inv;
-    }
-    const float ddelx_dx = (float)(0.5 * a.W), ddely_dy = (float)(0.5 * a.H);
-    const int row = lane >> 4;
-    const int row_entry = row == 1 ? 2 : row == 2 ? 1 : row;
-    const bool row_writer = (lane & 15) == 0;
-    float* xs = s_x[q];
-    float* ys = s_y[q];
-    float* cxs = s_cx[q];
-    float* cys = s_cy[q];
-    float* czs = s_cz[q];
-    float* ops = s_op[q];
-
-#pragma unroll
-    for (int i = 3; i >= 0; --i) {  // quarters back to front
-        const int qlo = lo + 64 * i;
-        const bool keep = 64 * i + lane < n && ((kb >> i) & 1u);
-        const uint64_t km = __ballot(keep);
-        const int nk = __popcll(km);
-        if (keep) {  // compacted back to front
-            const int slot = __popcll(km & ~lanemask_lt() & ~(1ull << lane));
-            xs[slot] = cur.xy.x;
-            ys[slot] = cur.xy.y;
-            cxs[slot] = cur.co.x;
-            cys[slot] = -cur.co.y;  // (negated: pixel_alpha4; finish_record negates back)
-            czs[slot] = cur.co.z;
-            ops[slot] = cur.co.w;
-            s_rgb[q][slot] = cur.f;
-            s_pos[q][slot] = (uint32_t)(qlo + lane);
-            if (a.touched) a.touched[pairs[i].x] = 1;
-        }
-        if (i > 0) cur = gather_entry(a.splat, (kb >> (i - 1)) & 1u ? pairs[i - 1].x : 0u);
-        if (lane < kBwdGroup) {  // padding: alpha = 0 everywhere, never in a pixel's list
-            xs[nk + lane] = 0.f;
-            ys[nk + lane] = 0.f;
-            cxs[nk + lane] = 0.f;
-            cys[nk + lane] = 0.f;
-            czs[nk + lane] = 0.f;
-            ops[nk + lane] = 0.f;
-            s_rgb[q][nk + lane] = make_float4(0.f, 0.f, 0.f, 0.f);
-            s_pos[q][nk + lane] = 0xFFFFFFFFu;
-        }
-        if (lane == 0) s_kept[q][i] = km;
-        // (the staging is this wave's own: a wave-level barrier, not a block one)
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        for (int k = 0; k < nk; k += kBwdGroup) {
-            float g[kBwdGroup][9];
-            {
-                const auto ld4 = [&](const float* f) { return *reinterpret_cast<const f4v*>(f + k); };
-                const float4 c4[4] = {s_rgb[q][k], s_rgb[q][k + 1], s_rgb[q][k + 2], s_rgb[q][k + 3]};
-                const bool in4[4] = {s_pos[q][k] < last_contributor, s_pos[q][k + 1] < last_contributor,
-                                     s_pos[q][k + 2] < last_contributor, s_pos[q][k + 3] < last_contributor};
-                bwd_quad(ld4(xs), ld4(ys), ld4(cxs), ld4(cys), ld4(czs), ld4(ops), c4, in4, pfx, pfy, dp0, dp1,
-                         dp2, nbg, T, D0, D1, D2, g);
-            }
-            __builtin_amdgcn_sched_barrier(0);  // (every product first: the lane swaps clobber their operands)
-            float S[9];
-#pragma unroll
-            for (int f = 0; f < 9; ++f) S[f] = quad_reduce(g[0][f], g[1][f], g[2][f], g[3][f]);
-            __builtin_amdgcn_sched_barrier(0);
-            const int kw = k + row_entry;
-            if (row_writer && kw < nk) {
-                float4 r[3];
-                finish_record(make_float4(cxs[kw], -cys[kw], czs[kw], ops[kw]), S, ddelx_dx, ddely_dy, r);
-                float* t = s_rec[q][s_pos[q][kw] - (uint32_t)lo];
-                t[0] = r[0].x; t[1] = r[0].y; t[2] = r[0].z; t[3] = r[0].w;
-                t[4] = r[1].x; t[5] = r[1].y; t[6] = r[1].z; t[7] = r[1].w;
-                t[8] = r[2].x;
-            }
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // (the next quarter restages)
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    }
-    __syncthreads();
-    {   // the tile's record of each kept position of the segment: quadrants added in order
-        const int p = threadIdx.x, i = p >> 6;
-        const uint64_t bit = 1ull << (p & 63);
-        const bool kk[4] = {(s_kept[0][i] & bit) != 0, (s_kept[1][i] & bit) != 0, (s_kept[2][i] & bit) != 0,
-                            (s_kept[3][i] & bit) != 0};
-        if (p < tile_n && (kk[0] | kk[1] | kk[2] | kk[3])) {
-            float acc[9];
-#pragma unroll
-            for (int f = 0; f < 9; ++f) acc[f] = 0.f;
-#pragma unroll
-            for (int qq = 0; qq < 4; ++qq) {
-                if (kk[qq]) {
-#pragma unroll
-                    for (int f = 0; f < 9; ++f) acc[f] += s_rec[qq][p][f];
-                }
-            }
-            const size_t rec = a.point_pairs[range.x + lo + p].y;
-            float4* dst = a.records + 3 * rec;
-            dst[0] = make_float4(acc[0], acc[1], acc[2], acc[3]);
-            dst[1] = make_float4(acc[4], acc[5], acc[6], acc[7]);
-            dst[2] = make_float4(acc[8], 0.f, 0.f, 0.f);
-            reinterpret_cast<uint32_t*>(a.rec_flags)[rec] = 1u;
-        }
-    }
-    __syncthreads();  // (a next item reuses the table)
-    if (!LOOP) break;
-    }
 }
 
 // One workgroup per possible item (the bound, 4 x checkpoint slots, is ~7x the c2 count): the surplus
-// workgroups exit at once and cost nothing measurable (render_bwd 104 us either way), while capping the
-// grid needs a second, looping launch for the overflow whose empty dispatch alone measured ~5 us.
-// DGE_AMD_BWD_GRID_CAP=n caps it anyway (the test of the looping path).
-constexpr unsigned kBwdLoopGrid = 2048;  // the looping grid over items beyond a cap
-
-static unsigned bwd_grid_cap() {
-    static unsigned v = 0;
-    if (!v) {
-        const char* e = getenv("DGE_AMD_BWD_GRID_CAP");
-        const long c = e ? atol(e) : 0;
-        v = c > 0 ? (unsigned)c : 0xFFFFFFFFu;
-    }
-    return v;
-}
-
-// DGE_AMD_BWD=tile: k_render_bwd_tile (one record per slot), else k_render_bwd (one per quadrant).  The
-// per-tile merge cuts the record traffic and gauss_bwd (65 -> 59 us at c2) but its four quadrant waves
-// wait for one another (render_bwd 105 -> 122 us): measured 2113-2130 vs 2155-2175 renders/s, off by default.
-int render_backward_merged() {
-    static int v = -1;
-    if (v < 0) {
-        const char* e = getenv("DGE_AMD_BWD");
-        v = (e && !strcmp(e, "tile")) ? 1 : 0;
-    }
-    return v;
-}
-
+// workgroups exit at once and cost nothing measurable (render_bwd 104 us either way).
 void launch_render_backward(const RenderBwdArgs& a, hipStream_t s) {
     const int tiles = a.gx * a.gy;
-    if (tiles <= 0) return;
-    RenderBwdArgs b = a;
-    if (fwd_variant() == 0) b.touched = nullptr;  // k_render_fwd set them (the pipelined variant does not)
-    if (render_backward_merged()) {
-        hipLaunchKernelGGL(k_bwd_tile_items, dim3(1), dim3(1024), 0, s, b, tiles);
-        const unsigned items = a.item_cap / 4;  // per-tile segments <= slots
-        const unsigned cap = bwd_grid_cap() / 4 > 0 ? bwd_grid_cap() / 4 : 1u;
-        hipLaunchKernelGGL(k_render_bwd_tile<false>, dim3(items < cap ? items : cap), dim3(256), 0, s, b, 0u);
-        if (items > cap) {
-            const unsigned rest = items - cap;
-            hipLaunchKernelGGL(k_render_bwd_tile<true>, dim3(rest < kBwdLoopGrid / 4 ? rest : kBwdLoopGrid / 4),
-                               dim3(256), 0, s, b, cap);
-        }
-        return;
-    }
-    const unsigned cap = bwd_grid_cap();
-    const unsigned grid = a.item_cap < cap ? a.item_cap : cap;
-    hipLaunchKernelGGL(k_render_bwd<false>, dim3(grid), dim3(64), 0, s, b, 0u);
-    if (a.item_cap > cap) {
-        const unsigned rest = a.item_cap - cap;
-        hipLaunchKernelGGL(k_render_bwd<true>, dim3(rest < kBwdLoopGrid ? rest : kBwdLoopGrid), dim3(64), 0, s, b, cap);
-    }
+    if (tiles <= 0 || a.item_cap == 0) return;
+    hipLaunchKernelGGL(k_render_bwd, dim3(a.item_cap), dim3(64), 0, s, a);
 }
 
 }  // namespace gs

@@ -92,6 +92,18 @@ __device__ __forceinline__ uint32_t key_bias(const uint32_t* __restrict__ bias_n
     return ~m;
 }
 
+// The instance count of a forward whose binning was enqueued before the host read it back
+// (gs_views_forward, speculative capacity): the sum of the preprocess counter slots, capped at the
+// binning buffer's capacity `cap` (an overflow is detected by the host later, gs_views_check).
+// n_dev == nullptr: the host-known count `cap` itself.
+__device__ __forceinline__ uint32_t dev_count(const uint32_t* __restrict__ n_dev, uint32_t cap) {
+    if (!n_dev) return cap;
+    uint32_t k = 0;
+#pragma unroll
+    for (int i = 0; i < kCounterSlots; ++i) k += n_dev[i * kCounterStride];
+    return k < cap ? k : cap;
+}
+
 // ---------------------------------------------------------------------
 // radix sort: histogram -> per-digit scan -> stable scatter
 // ---------------------------------------------------------------------
@@ -107,13 +119,16 @@ __host__ __device__ __forceinline__ size_t hist_at(int bm, uint32_t b, uint32_t 
 template <int BITS, int IPT>
 __global__ __launch_bounds__(256) void k_radix_hist(const uint32_t* __restrict__ keys, uint32_t n, int shift,
                                                     uint32_t* __restrict__ hist, int nb, int bm,
-                                                    const uint32_t* __restrict__ bias_not) {
+                                                    const uint32_t* __restrict__ bias_not,
+                                                    const uint32_t* __restrict__ n_dev) {
     constexpr int NDIG = 1 << BITS;
     __shared__ uint32_t cnt[NDIG];
     const int tid = threadIdx.x;
+    n = dev_count(n_dev, n);
+    const uint32_t base = blockIdx.x * (uint32_t)(256 * IPT);
+    if (base >= n && blockIdx.x) return;  // (a capacity-sized grid: rows past the count are never read)
     for (int i = tid; i < NDIG; i += 256) cnt[i] = 0;
     __syncthreads();
-    const uint32_t base = blockIdx.x * (uint32_t)(256 * IPT);
     const uint32_t bias = key_bias(bias_not);
     uint32_t key[IPT];
 #pragma unroll
@@ -138,8 +153,11 @@ __global__ __launch_bounds__(256) void k_radix_hist(const uint32_t* __restrict__
 constexpr int kScanDigits = 16, kScanGroups = 64, kScanRegs = 16;
 constexpr int kScanBmRows = kScanGroups * kScanRegs;  // block-major tables up to this many blocks
 __global__ __launch_bounds__(1024) void k_radix_digit_scan(uint32_t* __restrict__ hist, int nb, int ndig,
-                                                           uint32_t* __restrict__ totals) {
+                                                           uint32_t* __restrict__ totals,
+                                                           const uint32_t* __restrict__ n_dev, uint32_t cap,
+                                                           int tile) {
     __shared__ uint32_t part[kScanGroups][kScanDigits];
+    if (n_dev) nb = max(1, div_up_u(dev_count(n_dev, cap), (uint32_t)tile));  // rows the histogram wrote
     const int dl = threadIdx.x & (kScanDigits - 1), g = threadIdx.x / kScanDigits;
     const int d = blockIdx.x * kScanDigits + dl;
     const int per = (nb + kScanGroups - 1) / kScanGroups;
@@ -193,9 +211,12 @@ __global__ __launch_bounds__(1024) void k_radix_digit_scan(uint32_t* __restrict_
 // One workgroup per digit (digit-major table): exclusive scan of hist[d][0..nb)
 // in place, totals[d] = digit count.
 __global__ __launch_bounds__(256) void k_radix_digit_scan_dm(uint32_t* __restrict__ hist, int nb,
-                                                             uint32_t* __restrict__ totals) {
+                                                             uint32_t* __restrict__ totals,
+                                                             const uint32_t* __restrict__ n_dev, uint32_t cap,
+                                                             int tile) {
     __shared__ uint32_t lds4[4];
-    uint32_t* row = hist + (size_t)blockIdx.x * nb;
+    uint32_t* row = hist + (size_t)blockIdx.x * nb;  // (digit-major: the row pitch stays the grid's nb)
+    if (n_dev) nb = max(1, div_up_u(dev_count(n_dev, cap), (uint32_t)tile));
     const int per = (nb + 255) / 256;
     const int beg = threadIdx.x * per;
     uint32_t s = 0;
@@ -247,8 +268,10 @@ __global__ __launch_bounds__(256) void k_radix_scatter(const uint32_t* __restric
                                                        int shift, const uint32_t* __restrict__ hist,
                                                        const uint32_t* __restrict__ totals, int nb, int bm,
                                                        RangeOut ro,
-                                                       const uint32_t* __restrict__ bias_not) {
+                                                       const uint32_t* __restrict__ bias_not,
+                                                       const uint32_t* __restrict__ n_dev) {
     using V = typename std::conditional<VM == kValU32, uint32_t, uint2>::type;
+    n = dev_count(n_dev, n);
     const uint32_t* vals_in = static_cast<const uint32_t*>(vals_in_);
     const uint2* pairs_in = static_cast<const uint2*>(vals_in_);
     V* vals_out = static_cast<V*>(vals_out_);
@@ -314,6 +337,8 @@ __global__ __launch_bounds__(256) void k_radix_scatter(const uint32_t* __restric
         }
     }
     __syncthreads();
+    // a capacity-sized grid (n_dev): blocks past the count leave after block 0 wrote the ranges
+    if (blockIdx.x * (uint32_t)(256 * IPT) >= n) return;
     const uint32_t base = blockIdx.x * (uint32_t)(256 * IPT) + w * 64u * IPT;
     const uint32_t bias = key_bias(bias_not);
     uint32_t key[IPT], loc[IPT];
@@ -411,24 +436,26 @@ __global__ __launch_bounds__(256) void k_radix_scatter(const uint32_t* __restric
 template <int BITS, int IPT>
 static void radix_pass(const uint32_t* kin, const void* vin, uint32_t* kout, void* vout, const uint32_t* gauss_by_slot,
                        uint32_t n, int shift, bool idv, int vm, uint32_t* hist, uint32_t* totals, int nb,
-                       RangeOut ro, const uint32_t* bias_not, hipStream_t s) {
+                       RangeOut ro, const uint32_t* bias_not, hipStream_t s, const uint32_t* n_dev = nullptr) {
+    // n_dev: the element count is read on the device (capped at n, the capacity the grid nb covers)
     constexpr int NDIG = 1 << BITS;
     const int bm = nb <= kScanBmRows ? 1 : 0;
-    hipLaunchKernelGGL((k_radix_hist<BITS, IPT>), dim3(nb), dim3(256), 0, s, kin, n, shift, hist, nb, bm, bias_not);
+    hipLaunchKernelGGL((k_radix_hist<BITS, IPT>), dim3(nb), dim3(256), 0, s, kin, n, shift, hist, nb, bm, bias_not,
+                       n_dev);
     if (bm)
         hipLaunchKernelGGL(k_radix_digit_scan, dim3(div_up(NDIG, kScanDigits)), dim3(1024), 0, s, hist, nb, NDIG,
-                           totals);
+                           totals, n_dev, n, 256 * IPT);
     else
-        hipLaunchKernelGGL(k_radix_digit_scan_dm, dim3(NDIG), dim3(256), 0, s, hist, nb, totals);
+        hipLaunchKernelGGL(k_radix_digit_scan_dm, dim3(NDIG), dim3(256), 0, s, hist, nb, totals, n_dev, n, 256 * IPT);
 #define GS_SCATTER(IDV, VM)                                                                                   \
     hipLaunchKernelGGL((k_radix_scatter<BITS, IPT, IDV, VM>), dim3(nb), dim3(256), 0, s, kin, vin, kout, vout,  \
-                       gauss_by_slot, n, shift, hist, totals, nb, bm, ro, bias_not)
+                       gauss_by_slot, n, shift, hist, totals, nb, bm, ro, bias_not, n_dev)
     if (vm == kValPair && !kout)  // the two-level binning's row pass: no sorted keys
         hipLaunchKernelGGL((k_radix_scatter<BITS, IPT, false, kValPair, false, true>), dim3(nb), dim3(256), 0, s, kin,
-                           vin, kout, vout, gauss_by_slot, n, shift, hist, totals, nb, bm, ro, bias_not);
+                           vin, kout, vout, gauss_by_slot, n, shift, hist, totals, nb, bm, ro, bias_not, n_dev);
     else if (vm == kValPairFirst && !kout)  // the last tile-sort pass: no sorted keys
         hipLaunchKernelGGL((k_radix_scatter<BITS, IPT, true, kValPairFirst, false>), dim3(nb), dim3(256), 0, s, kin,
-                           vin, kout, vout, gauss_by_slot, n, shift, hist, totals, nb, bm, ro, bias_not);
+                           vin, kout, vout, gauss_by_slot, n, shift, hist, totals, nb, bm, ro, bias_not, n_dev);
     else if (vm == kValPairFirst) GS_SCATTER(true, kValPairFirst);
     else if (vm == kValPair) GS_SCATTER(false, kValPair);
     else if (idv) GS_SCATTER(true, kValU32);
@@ -438,13 +465,14 @@ static void radix_pass(const uint32_t* kin, const void* vin, uint32_t* kout, voi
 
 static void radix_pass_bits(int bits, int ipt, const uint32_t* kin, const void* vin, uint32_t* kout, void* vout,
                             const uint32_t* gauss_by_slot, uint32_t n, int shift, bool idv, int vm, uint32_t* hist,
-                            uint32_t* totals, int nb, RangeOut ro, const uint32_t* bias_not, hipStream_t s) {
+                            uint32_t* totals, int nb, RangeOut ro, const uint32_t* bias_not, hipStream_t s,
+                            const uint32_t* n_dev) {
 #define GS_CASE(B)                                                                                              \
     case B:                                                                                                     \
         if (ipt == kDepthSortIPT)                                                                               \
-            radix_pass<B, kDepthSortIPT>(kin, vin, kout, vout, gauss_by_slot, n, shift, idv, vm, hist, totals, nb, ro, bias_not, s); \
+            radix_pass<B, kDepthSortIPT>(kin, vin, kout, vout, gauss_by_slot, n, shift, idv, vm, hist, totals, nb, ro, bias_not, s, n_dev); \
         else                                                                                                    \
-            radix_pass<B, kSortIPT>(kin, vin, kout, vout, gauss_by_slot, n, shift, idv, vm, hist, totals, nb, ro, bias_not, s); \
+            radix_pass<B, kSortIPT>(kin, vin, kout, vout, gauss_by_slot, n, shift, idv, vm, hist, totals, nb, ro, bias_not, s, n_dev); \
         break;
     switch (bits) {
         GS_CASE(1) GS_CASE(2) GS_CASE(3) GS_CASE(4) GS_CASE(5) GS_CASE(6)
@@ -464,7 +492,8 @@ static int pass_bits(int begin_bit, int end_bit, int max_pass_bits, int p, int& 
 
 int radix_sort_aux(uint32_t* key0, uint32_t* key1, uint2* pair0, uint2* pair1, const uint32_t* aux, uint32_t n,
                    int bits, int max_pass_bits, int ipt, uint32_t* hist, uint32_t* totals, int nblocks, hipStream_t s,
-                   uint2* ranges, const uint32_t* key_bias_not, uint32_t* tile_order, int ntiles) {
+                   uint2* ranges, const uint32_t* key_bias_not, uint32_t* tile_order, int ntiles,
+                   const uint32_t* n_dev) {
     uint32_t* k[2] = {key0, key1};
     uint2* v[2] = {pair0, pair1};
     int cur = 0;
@@ -481,7 +510,7 @@ int radix_sort_aux(uint32_t* key0, uint32_t* key1, uint2* pair0, uint2* pair1, c
         radix_pass_bits(b, ipt, k[cur], v[cur], ranges_here ? nullptr : k[cur ^ 1], v[cur ^ 1], aux, n, shift,
                         p == 0, p == 0 ? kValPairFirst : kValPair, hist, totals, nblocks,
                         RangeOut{ranges_here ? ranges : nullptr, ranges_here ? tile_order : nullptr, ntiles},
-                        p == 0 ? key_bias_not : nullptr, s);
+                        p == 0 ? key_bias_not : nullptr, s, n_dev);
         cur ^= 1;
         shift += b;
     }
@@ -490,9 +519,9 @@ int radix_sort_aux(uint32_t* key0, uint32_t* key1, uint2* pair0, uint2* pair1, c
 
 int tile_sort(uint32_t* key0, uint32_t* key1, uint2* pair0, uint2* pair1, const uint32_t* gauss_by_slot, uint32_t n,
               int bits, uint32_t* hist, uint32_t* totals, int nblocks, hipStream_t s, uint2* ranges,
-              uint32_t* tile_order, int ntiles) {
+              uint32_t* tile_order, int ntiles, const uint32_t* n_dev) {
     return radix_sort_aux(key0, key1, pair0, pair1, gauss_by_slot, n, bits, kMaxSinglePassBits, kSortIPT, hist, totals,
-                          nblocks, s, ranges, nullptr, tile_order, ntiles);
+                          nblocks, s, ranges, nullptr, tile_order, ntiles, n_dev);
 }
 
 // ---------------------------------------------------------------------
@@ -598,6 +627,7 @@ __global__ __launch_bounds__(256) void k_scan_emit(EmitArgs a) {
             const uint32_t k = j - s_start[lo];
             const uint32_t ky = (uint32_t)(((float)k + 0.5f) / (float)q.z);  // exact: k < 2^20, margin 0.5/width
             const uint32_t kx = k - ky * (uint32_t)q.z;
+            if (base + j >= a.cap) break;  // speculative capacity exceeded (gs_views_check reports it)
             a.tile_key[base + j] = (uint32_t)((q.y + (int)ky) * a.gx + q.x + (int)kx);
             a.slot_gauss[base + j] = s_gauss[lo];
             if (a.rec_flags32) a.rec_flags32[base + j] = 0u;  // slot's four quadrant flags (no memset launch)
@@ -713,7 +743,7 @@ __global__ __launch_bounds__(256) void k_scan_emit_x(EmitArgs a) {
                 const uint32_t x = (uint32_t)q.x + kx, y = (uint32_t)q.y + ky;
                 kk[e] = y << kXBits | x;
                 pv[e] = make_uint2(s_gauss[lo], base + j);
-                if (valid && a.rec_flags32) a.rec_flags32[base + j] = 0u;  // (slot order: coalesced)
+                if (valid && a.rec_flags32 && base + j < a.cap) a.rec_flags32[base + j] = 0u;  // (slot order: coalesced)
                 const uint32_t d = valid ? x : 0u;
                 const uint64_t peers = match_digit<kXBits>(d, vm);
                 const uint32_t rank = (uint32_t)__popcll(peers & lanemask_lt());
@@ -755,8 +785,10 @@ __global__ __launch_bounds__(256) void k_scan_emit_x(EmitArgs a) {
             for (uint32_t i = tid; i < nb; i += 256) {
                 const uint32_t kv = s_key[i];
                 const uint32_t pos = s_gbase[kv & (kXDigits - 1)] + i;
-                a.tile_key[pos] = kv;
-                a.pairs_out[pos] = s_pair[i];
+                if (pos < a.cap) {  // (speculative capacity: gs_views_check reports an overflow)
+                    a.tile_key[pos] = kv;
+                    a.pairs_out[pos] = s_pair[i];
+                }
             }
             for (int i = tid; i < 4 * kXDigits; i += 256) (&cnt[0][0])[i] = 0;
             __syncthreads();
@@ -792,17 +824,17 @@ void launch_emit_fused(const EmitArgs& a, hipStream_t s) {
     if (a.P <= 0) return;
     // first level: column totals and each block's column offsets, then the column-ordered emission
     hipLaunchKernelGGL(k_radix_digit_scan, dim3(kXDigits / kScanDigits), dim3(1024), 0, s, a.xhist, a.scan_blocks,
-                       kXDigits, a.xtotals);
+                       kXDigits, a.xtotals, (const uint32_t*)nullptr, 0u, 1);
     hipLaunchKernelGGL(k_scan_emit_x, dim3(a.scan_blocks), dim3(256), 0, s, a);
 }
 
 void launch_row_pass(const EmitArgs& a, uint32_t K, uint2* point_pairs, uint32_t* hist, int sort_blocks,
-                     uint2* ranges, hipStream_t s) {
+                     uint2* ranges, hipStream_t s, const uint32_t* n_dev) {
     if (a.P <= 0 || K == 0) return;
     // second level: the stable row pass (digit y), counting instances per tile on the way
     RangeOut ro{nullptr, nullptr, a.ntiles, a.tile_count, a.gx};
     radix_pass<kXBits, kSortIPT>(a.tile_key, a.pairs_out, nullptr, point_pairs, nullptr, K, kXBits, false, kValPair,
-                                 hist, a.xtotals, sort_blocks, ro, nullptr, s);
+                                 hist, a.xtotals, sort_blocks, ro, nullptr, s, n_dev);
     hipLaunchKernelGGL(k_ranges_counts, dim3(1), dim3(256), 0, s, a.tile_count, a.ntiles, ranges);
 }
 

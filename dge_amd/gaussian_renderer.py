@@ -186,38 +186,6 @@ def _fused_begin(viewpoint_camera, pc, pipe, bg_color, scaling_modifier=1.0, ove
     return st
 
 
-def _fused_begin_multi(cameras, pc, pipe, bg_color, streams, scaling_modifier=1.0):
-    """_fused_begin of several views at once (view v on streams[v], each already ordered after the caller's
-    inputs): one native call whose preprocess reads the scene's parameters once for all views
-    (gs_rasterize_forward_begin_multi).  Views it cannot share (debug mode, a localize index) take
-    _fused_begin one by one."""
-    from . import _C
-
-    if getattr(pc, "localize", False) or getattr(pipe, "debug", False) or len(cameras) > 4:
-        out = []
-        for cam, s in zip(cameras, streams):
-            with torch.cuda.stream(s):
-                out.append(_fused_begin(cam, pc, pipe, bg_color, scaling_modifier))
-        return out
-    xyz = pc._xyz
-    n = xyz.shape[0]
-    f_dc, f_rest = pc._features_dc, pc._features_rest
-    empty = torch.empty(0, dtype=torch.float32, device=xyz.device)
-    sts, views = [], []
-    for cam, s in zip(cameras, streams):
-        rs = _settings(cam, bg_color, scaling_modifier, pc.active_sh_degree, False)
-        with torch.cuda.stream(s):
-            visible = torch.empty(n, dtype=torch.bool, device=xyz.device)
-        sts.append({"rs": rs, "index": None, "n": n, "f_dc": f_dc, "f_rest": f_rest, "colors": None,
-                    "visible": visible, "prepared": None})
-        views.append((rs.bg, xyz, f_dc, f_rest, empty, pc._opacity, pc._scaling, pc._rotation, rs.scale_modifier,
-                      rs.viewmatrix, rs.projmatrix, rs.tanfovx, rs.tanfovy, rs.image_height, rs.image_width,
-                      rs.sh_degree, rs.campos, rs.prefiltered, rs.debug, None, visible))
-    for st, prep in zip(sts, _C.rasterize_gaussians_fused_begin_multi(views, streams)):
-        st["prepared"] = prep
-    return sts
-
-
 def _fused_end(st, pc):
     """The second half: the autograd node over the native forward's second half; render()'s dict."""
     xyz = pc._xyz

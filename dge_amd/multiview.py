@@ -258,112 +258,38 @@ def stream_pool(device, n: int):
     return pool
 
 
-_THREAD_POOLS = {}
-
-
-def _host_pool(n: int):
-    """n host threads, created once: each view's forward is issued from its own thread."""
-    from concurrent.futures import ThreadPoolExecutor
-
-    pool = _THREAD_POOLS.get(n)
-    if pool is None:
-        pool = _THREAD_POOLS[n] = ThreadPoolExecutor(max_workers=n, thread_name_prefix="dge_amd_view")
-    return pool
-
-
-def _render_on(stream, ready, grad_enabled, render, cam, pc, pipe, bg_color, kw):
-    with torch.cuda.device(stream.device), torch.cuda.stream(stream), torch.set_grad_enabled(grad_enabled):
-        stream.wait_event(ready)
-        return render(cam, pc, pipe, bg_color, **kw)
-
-
-def _touched_rows(prep):
-    """uint8 [P] view of a finished forward's `touched` bytes (the Gaussians some pixel blended)."""
-    from . import _native as N
-
-    geom = prep.alloc.buffers[0]
-    off = N.lib().gs_buffer_offset(b"geometry", b"touched", prep.P, prep.W, prep.H, 0)
-    return geom[off:off + prep.P]
-
-
-# DGE_AMD_MULTI_BEGIN=1: every view's first half from ONE gs_rasterize_forward_begin_multi call (the scene read
-# once by a shared preprocess pass).  Opt-in: bitwise the same outputs, but measured no faster at c2
-# (2130-2164 vs 2195-2218 renders/s, profiles/r02/ab_multi_begin.log) — the three per-view preprocess
-# kernels overlap each other, the shared pass delays every view's depth sort behind all three projections.
-_MULTI_BEGIN = os.environ.get("DGE_AMD_MULTI_BEGIN", "0") == "1"
-
-
-def render_views(cameras, pc, pipe, bg_color, streams: int = 2, threads: bool = False, stagger: bool = False,
-                 **kw):
+def render_views(cameras, pc, pipe, bg_color, streams: int = 2, speculate: bool = False, **kw):
     """render() of every camera, the views spread round-robin over `streams` HIP streams.
 
     The reference renders a batch's views one after another (threestudio/systems/DGE.py:179-239) on
-    one stream; here consecutive views run on different streams, so one view's latency-bound phases
-    (binning launches, the blend tail) overlap the other views' work.  threads: each view's forward
-    is issued from its own host thread (a persistent pool), so the one host wait of a forward — the
-    instance count read back after the preprocess (rasterizer_impl.cu:236-239), which sizes the
-    binning buffer — blocks only that view's thread while the others keep the GPU fed (the C calls
-    release the GIL).  Off by default: at c2 it measured no faster than one issuing thread and far
-    noisier (1413-2274 vs 1902-2052 renders/s over repeated runs).  Outputs are the same dicts render() returns, usable on the caller's stream (it
-    waits for every view); autograd runs each view's backward on that view's stream and the in-kernel
-    gradient accumulation orders itself across them (diff_gaussian_rasterization._order_grad_writes_*).
-    stagger: view i's first half (preprocess, depth sort, instance scan) starts after view i-1's, so the
-    views reach their HBM-bound and latency-bound phases at different times instead of all at once."""
-    from .gaussian_renderer import render
+    one stream.  Here, for a standard GaussianModel (the fused raw-parameter path) and up to
+    GS_MAX_VIEWS views, the batch goes through ONE autograd node over one native forward and one native
+    backward (dge_amd.views): every view's first half is enqueued before any second half, consecutive
+    views run on different streams (one view's latency-bound blend tail overlaps the others' work), and
+    the backward chains the views' gradient accumulation in view order.  speculate: the views' binning
+    buffers are sized from the instance counts seen before, without the per-view host wait for the count
+    (rasterizer_impl.cu:236-239); the caller must then call `.check()` on the returned list before using
+    the results (False: a view overflowed its capacity — render the batch again).  Other models: one
+    render() per view on the pool's streams.  Returns a list (RenderedViews) of render()'s dicts,
+    usable on the caller's stream."""
+    from .gaussian_renderer import _fused_ok, render
+    from .views import RenderedViews, render_views_batched
 
-    if streams <= 1 or len(cameras) <= 1:
-        return [render(c, pc, pipe, bg_color, **kw) for c in cameras]
     dev = bg_color.device
     main = torch.cuda.current_stream(dev)
-    pool = stream_pool(dev, streams)
-    ready = main.record_event()
-    if threads:
-        hp = _host_pool(streams)
-        grad = torch.is_grad_enabled()
-        futs = [hp.submit(_render_on, pool[i % len(pool)], ready, grad, render, cam, pc, pipe, bg_color, kw)
-                for i, cam in enumerate(cameras)]
-        outs = [f.result() for f in futs]
-        for out in outs:
-            for v in out.values():
-                if isinstance(v, torch.Tensor) and v.is_cuda:
-                    v.record_stream(main)
-        for s in pool[:min(len(pool), len(cameras))]:
-            main.wait_stream(s)
+    pool = stream_pool(dev, streams) if streams > 1 else [main]
+    if _fused_ok(pc, pipe) and 1 <= len(cameras) <= _native_max_views():
+        return render_views_batched(cameras, pc, pipe, bg_color, pool, speculate=speculate, **kw)
+    outs = RenderedViews()
+    if len(pool) == 1:
+        outs.extend(render(c, pc, pipe, bg_color, **kw) for c in cameras)
         return outs
-    from .gaussian_renderer import _fused_begin, _fused_end, _fused_ok
-
-    outs = []
-    # standard models: every view's first half (preprocess, depth sort, instance scan) is enqueued before
-    # the host waits for any view's instance count; then each view is finished in turn
-    begun = None
-    if (_fused_ok(pc, pipe) and not stagger and len(cameras) <= len(pool) and not threads and _MULTI_BEGIN
-            and kw.get("override_color") is None):
-        # one native call for every view's first half: the scene's parameters are read once by a shared
-        # preprocess pass (gs_rasterize_forward_begin_multi), each view's sort and scan on its own stream
-        from .gaussian_renderer import _fused_begin_multi
-
-        vs = pool[:len(cameras)]
-        for s in vs:
-            s.wait_event(ready)
-        begun = _fused_begin_multi(cameras, pc, pipe, bg_color, vs, kw.get("scaling_modifier", 1.0))
-    elif _fused_ok(pc, pipe):
-        begun = []
-        prev = ready
-        for i, cam in enumerate(cameras):
-            s = pool[i % len(pool)]
-            s.wait_event(prev)
-            with torch.cuda.stream(s):
-                begun.append(_fused_begin(cam, pc, pipe, bg_color, **kw))
-            if stagger:
-                prev = s.record_event()
+    ready = main.record_event()
     for i, cam in enumerate(cameras):
         s = pool[i % len(pool)]
-        if begun is None:
-            s.wait_event(ready)
+        s.wait_event(ready)
         with torch.cuda.stream(s):
-            out = render(cam, pc, pipe, bg_color, **kw) if begun is None else _fused_end(begun[i], pc)
-            if begun is not None and begun[i]["index"] is None and begun[i]["prepared"] is not None:
-                out["_live_rows"] = _touched_rows(begun[i]["prepared"])
+            out = render(cam, pc, pipe, bg_color, **kw)
         for v in out.values():
             if isinstance(v, torch.Tensor) and v.is_cuda:
                 v.record_stream(main)
@@ -371,6 +297,12 @@ def render_views(cameras, pc, pipe, bg_color, streams: int = 2, threads: bool = 
     for s in pool[:min(len(pool), len(cameras))]:
         main.wait_stream(s)
     return outs
+
+
+def _native_max_views() -> int:
+    from . import _native as N
+
+    return N.MAX_VIEWS
 
 
 def render_backward_views(cameras, pc, pipe, bg_color, grads, streams: int = 2, **kw):
@@ -426,7 +358,8 @@ def found_inf_allreduce(bucket: GradBucket, group=None) -> torch.Tensor:
 
 def multiview_step(scene, cameras, render_fn, pipe, bg, bucket: GradBucket, total_views: int, targets=None,
                    gt_images=None, masks=None, lambda_l1: float = 1.0, loss_scale: float = 1.0,
-                   semantic: bool = False, group=None, streams: int = 1, bucket_zeroed: bool = False):
+                   semantic: bool = False, group=None, streams: int = 1, bucket_zeroed: bool = False,
+                   min_world: int = 2):
     """One data-parallel step of DGE's edit loop over this rank's views (threestudio/systems/DGE.py
     forward :170-239, training_step :617-699, on_before_optimizer_step :266-296).
 
@@ -439,17 +372,22 @@ def multiview_step(scene, cameras, render_fn, pipe, bg, bucket: GradBucket, tota
     mask render per view (:198-204, override_color = the Gaussian mask) — gradient-free, so here
     without autograd, its boolean ``norm > 0.8`` map returned in ``masks``.
 
-    Then one (sparse-row) SUM all-reduce of the gradient bucket, the overflow flag MAX-reduced before it
-    (found_inf_allreduce), and the densification statistics: the SUM of the view-space gradients and the
-    MAX of the radii across views and ranks.  Returns a dict: viewspace_grad_sum [P,3], radii_max [P],
-    found_inf (float tensor [1]), semantic_masks (list of [H,W] bool, when ``semantic``).
+    Then one (sparse-row) SUM all-reduce of the gradient bucket, the overflow flag (any non-finite
+    gradient, taken on the reduced bucket: the SUM carries an inf/NaN of any rank to every rank, and rows
+    it does not carry are zero everywhere, so every rank reaches the same decision), and the
+    densification statistics: the SUM of the view-space gradients and the MAX of the radii across views
+    and ranks.  Returns a dict: viewspace_grad_sum [P,3], radii_max [P], found_inf (float tensor [1]),
+    semantic_masks (list of [H,W] bool, when ``semantic``).
 
     streams > 1 with this package's render (dge_amd.gaussian_renderer.render): the views are rendered
-    together on that many HIP streams (render_views) and ONE backward of their summed loss follows — the
-    reference's order (DGE.py renders the batch, then back-propagates); with ``bucket_zeroed`` (the caller
-    zeroed the bucket this step and these losses are the only gradient source) the all-reduce's union of
+    together (render_views: one autograd node, the views on that many HIP streams) and ONE backward of
+    their summed loss follows — the reference's order (DGE.py renders the batch, then back-propagates).
+    With ``bucket_zeroed`` (the caller zeroed the bucket this step and these losses are the only gradient
+    source): the views' binning buffers are speculated (no per-view host wait; the batch is checked after
+    the backward and the step redone in the rare case a view overflowed), and the all-reduce's union of
     live rows is agreed on between the forwards and that backward (GradBucket.allreduce_begin), so the
-    host does not wait for the backward before the collective is shaped.
+    host does not wait for the backward before the collective is shaped.  The semantic renders are issued
+    after the collective, so they overlap it.
     """
     from .gaussian_renderer import render as _render
 
@@ -459,44 +397,58 @@ def multiview_step(scene, cameras, render_fn, pipe, bg, bucket: GradBucket, tota
     radii_max = torch.zeros((P,), dtype=torch.int32, device=dev)
     sem = []
     batched = streams > 1 and render_fn is _render and len(cameras) > 1
-    pkgs = render_views(cameras, scene, pipe, bg, streams=streams) if batched else None
-    losses = []
-    for i, cam in enumerate(cameras):
-        pkg = pkgs[i] if batched else render_fn(cam, scene, pipe, bg)
-        img = pkg["render"]
-        if targets is not None:
-            loss = (img * targets[i]).sum()
-        else:
-            m = masks[i] if masks is not None else torch.ones_like(img[:1])
-            loss = torch.abs(img * m - gt_images[i] * m).sum() * (lambda_l1 / (total_views * img.numel()))
-        if loss_scale != 1.0:
-            loss = loss * loss_scale
-        if batched:
-            losses.append(loss)
-            continue
-        loss.backward()
-        vs_sum += pkg["viewspace_points"].grad
-        radii_max = torch.maximum(radii_max, pkg["radii"])
-    hinted = batched and bucket_zeroed and all("_live_rows" in pkg for pkg in pkgs)
+
+    def losses_of(pkgs, first=0):
+        out = []
+        for i, pkg in enumerate(pkgs, first):
+            img = pkg["render"]
+            if targets is not None:
+                loss = (img * targets[i]).sum()
+            else:
+                m = masks[i] if masks is not None else torch.ones_like(img[:1])
+                loss = torch.abs(img * m - gt_images[i] * m).sum() * (lambda_l1 / (total_views * img.numel()))
+            out.append(loss * loss_scale if loss_scale != 1.0 else loss)
+        return out
+
+    hinted = False
     if batched:
-        if hinted:
-            bucket.allreduce_begin([pkg["_live_rows"] for pkg in pkgs], group)
-        torch.autograd.backward(losses)
+        for attempt in range(2):
+            if attempt:
+                bucket.zero()  # (speculated only with bucket_zeroed: the failed attempt's sums go)
+            pkgs = render_views(cameras, scene, pipe, bg, streams=streams, speculate=bucket_zeroed)
+            hinted = bucket_zeroed and all("_live_rows" in pkg for pkg in pkgs)
+            if hinted:
+                bucket.allreduce_begin([pkg["_live_rows"] for pkg in pkgs], group, min_world=min_world)
+            torch.autograd.backward(losses_of(pkgs))
+            if pkgs.check():
+                break
+        else:
+            raise RuntimeError("multiview_step: the binning capacity check failed twice")
         for pkg in pkgs:
             vs_sum += pkg["viewspace_points"].grad
             radii_max = torch.maximum(radii_max, pkg["radii"])
-    for i, cam in enumerate(cameras):
-        if semantic:
-            with torch.no_grad():
-                gm = getattr(scene, "mask", None)
-                gm = gm if gm is not None else torch.ones(P, dtype=torch.bool, device=dev)
-                sm = render_fn(cam, scene, pipe, bg, override_color=gm[..., None].float().repeat(1, 3))["render"]
-                sem.append(torch.norm(sm, dim=0) > 0.8)
-    found_inf = found_inf_allreduce(bucket, group)
+    else:
+        for i, cam in enumerate(cameras):
+            pkg = render_fn(cam, scene, pipe, bg)
+            losses_of([pkg], i)[0].backward()
+            vs_sum += pkg["viewspace_points"].grad
+            radii_max = torch.maximum(radii_max, pkg["radii"])
     if hinted:
         bucket.allreduce_end()
     else:
-        bucket.allreduce(group)
+        bucket.allreduce(group, min_world=min_world)
+    if semantic:  # gradient-free: enqueued behind the collective, which runs beside them
+        with torch.no_grad():
+            gm = getattr(scene, "mask", None)
+            gm = gm if gm is not None else torch.ones(P, dtype=torch.bool, device=dev)
+            colors = gm[..., None].float().repeat(1, 3)
+            if batched:
+                sms = [o["render"] for o in render_views(cameras, scene, pipe, bg, streams=streams,
+                                                         override_color=colors)]
+            else:
+                sms = [render_fn(cam, scene, pipe, bg, override_color=colors)["render"] for cam in cameras]
+            sem = [torch.norm(sm, dim=0) > 0.8 for sm in sms]
+    found_inf = (~torch.isfinite(bucket.flat)).any().to(torch.float32).reshape(1)
     reduce_view_stats(vs_sum, radii_max, group)
     out = {"viewspace_grad_sum": vs_sum, "radii_max": radii_max, "found_inf": found_inf}
     if semantic:

@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define GS_RASTER_ABI_VERSION 9
+#define GS_RASTER_ABI_VERSION 10
 
 #define GS_OK 0
 #define GS_ERR_INVALID_ARG 1   /* AT_ERROR / std::runtime_error in the reference */
@@ -56,6 +56,7 @@ extern "C" {
 #define GS_ERR_ALLOC 3         /* allocator callback returned NULL */
 #define GS_ERR_PREFILTERED 4   /* prefiltered set but a point was culled (auxiliary.h:156-160) */
 #define GS_ERR_UNSUPPORTED 5   /* e.g. apply_weights channel count (apply_weights.cu:377-380) */
+#define GS_ERR_RETRY 6         /* gs_views_check: a speculative binning capacity was exceeded */
 
 typedef void *gs_stream_t; /* hipStream_t */
 
@@ -204,22 +205,53 @@ int gs_rasterize_forward_begin(const gs_settings *s, const gs_params *g, int *ra
 int gs_rasterize_forward_end(gs_forward_state *state, float *out_color, float *out_depth, gs_alloc_fn alloc,
                              void *alloc_ctx, gs_stream_t stream, int *num_rendered);
 void gs_rasterize_forward_release(gs_forward_state *state);
-/* The first halves of n <= 4 views of ONE scene (g[v] name the same parameter tensors; only
- * g[v]->visible_out may differ), view v on streams[v], one state per view for _end: the views'
- * buffers are allocated and their counters zeroed on their streams, one preprocess pass reads
- * every Gaussian's parameters once and projects it into all n views (on streams[0], ordered after
- * the other streams' zeroing; they wait for it), then each view's counter read-back, depth sort
- * and instance scan go on its own stream.  alloc_ctx[v] is passed to alloc for view v's buffers.
- * Per-view outputs are bit-identical to n gs_rasterize_forward_begin calls; inputs the shared
- * pass does not take (fp16 SH, an index, differing parameters) fall back to those calls.
- * (Beyond the reference: DGE renders a batch of views of one scene per step, DGE.py:170-239.) */
-int gs_rasterize_forward_begin_multi(int n, const gs_settings *const *s, const gs_params *const *g,
-                                     int *const *radii, gs_alloc_fn alloc, void *const *alloc_ctx,
-                                     const gs_stream_t *streams, gs_forward_state **states);
-
 int gs_rasterize_backward_ex(const gs_settings *s, const gs_params *g, int R, const int *radii,
                              const void *geom_buffer, const void *binning_buffer, const void *img_buffer,
                              const float *dL_dpix, const gs_grads *out, gs_stream_t stream);
+
+/* A batch of views of ONE scene (DGE renders a batch of edited views per step,
+ * threestudio/systems/DGE.py:170-239): view v on streams[v], its outputs
+ * out_color[v] [3,H,W], out_depth[v] [1,H,W], radii[v] [P] (and
+ * g[v]->visible_out).  Every view's first half (preprocess, depth sort,
+ * instance scan) is enqueued before any view's second half.
+ *   mode GS_VIEWS_EXACT: each view's second half waits for its instance count
+ *     (the reference's host sync, rasterizer_impl.cu:236-239) and sizes its
+ *     binning buffer exactly (alloc which = 16 + v);
+ *   mode GS_VIEWS_SPECULATE: a view whose (P, W, H) this library has rendered
+ *     before gets a binning buffer of 1.25 x the largest count seen + 64k
+ *     instances; its emission, tile sort and blend read the count on the
+ *     device and no host wait happens.  gs_views_check then reads the counts:
+ *     GS_ERR_RETRY means some view exceeded its capacity (its outputs and any
+ *     backward of it are invalid; a second forward of the batch fits, the
+ *     capacity having grown).  Views without history are rendered exactly.
+ * All buffers but the exact binning ones come from ONE alloc(alloc_ctx, 0, bytes).
+ * join (optional): the caller's stream — the views' streams start after its
+ * work so far, and it waits for all of the views' work before the call returns. 
+ * The outputs of a speculated batch are bit-identical to the exact ones when
+ * gs_views_check returns GS_OK. */
+#define GS_MAX_VIEWS 8
+#define GS_VIEWS_EXACT 0
+#define GS_VIEWS_SPECULATE 1
+typedef struct gs_views gs_views;
+int gs_views_forward(int n, const gs_settings *const *s, const gs_params *const *g, float *const *out_color,
+                     float *const *out_depth, int *const *radii, int mode, gs_alloc_fn alloc, void *alloc_ctx,
+                     const gs_stream_t *streams, gs_stream_t join, gs_views **out);
+/* Waits for the speculated views' counts (already on the host for exact ones);
+ * num_rendered [n] (optional) receives them.  GS_OK, GS_ERR_RETRY, GS_ERR_PREFILTERED. */
+int gs_views_check(gs_views *h, int *num_rendered);
+/* The backward of every view, view v on streams[v] with grads[v] (dL_dmeans2D
+ * per view; the parameter gradients usually shared, GS_ACC_* set from the
+ * second view on).  The views' per-Gaussian passes are chained in view order
+ * (the first after `writes_after`, an optional hipEvent_t), so accumulated
+ * gradients add up in a fixed order; `join` (optional): the views start after
+ * its work so far (the image gradients) and it waits for all of them. */
+int gs_views_backward(gs_views *h, const float *const *dL_dpix, const gs_grads *const *grads,
+                      const gs_stream_t *streams, void *writes_after, gs_stream_t join);
+/* View v's buffers (which: 0 geometry, 1 binning, 2 image; gs_buffer_offset
+ * addresses their fields with num_rendered = gs_views_layout(h, v)). */
+void *gs_views_buffer(const gs_views *h, int v, int which);
+long long gs_views_layout(const gs_views *h, int v);
+void gs_views_release(gs_views *h);
 
 /* present[i] = (view * means3D[i]).z > 0.2 (rasterizer_impl.cu:53-63). */
 int gs_mark_visible(int P, const float *means3D, const float *viewmatrix, const float *projmatrix,
@@ -308,6 +340,10 @@ int gs_profile_set_stages(unsigned int mask);
 int gs_profile_num_stages(void);
 const char *gs_profile_stage_name(int i);
 int gs_profile_collect(double *total_ms, int *counts, int n);
+/* Host time (ns, process total since load) the forward's second half spent
+ * blocked on its instance-count read-back (the reference's one host sync,
+ * rasterizer_impl.cu:236-239): the bench reports it per step. */
+long long gs_host_wait_ns(void);
 
 /* Blend-kernel diagnostics: when enabled, the forward blend and the backward
  * replay record per wave (8 u64) {start, end (s_memrealtime, 100 MHz), kept

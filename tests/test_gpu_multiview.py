@@ -189,14 +189,17 @@ def test_multiview_step_batched_streams_hinted_one_rank(cuda_device):
     torch.testing.assert_close(g1, g0, rtol=1e-5, atol=1e-9)
 
 
-@pytest.mark.parametrize("V", [2, 3])
-def test_render_views_shared_preprocess_matches_per_view(cuda_device, monkeypatch, V):
-    """render_views on several streams takes every view's first half from ONE native call whose preprocess
-    reads the scene once for all views (gs_rasterize_forward_begin_multi); DGE_AMD_MULTI_BEGIN=0's per-view
-    begin calls give bitwise the same images, radii, visibility, view-space and parameter gradients."""
-    import dge_amd.multiview as MV
+@pytest.mark.parametrize("V", [1, 3])
+@pytest.mark.parametrize("speculate", [False, True])
+def test_render_views_batched_matches_per_view_loop(cuda_device, V, speculate):
+    """render_views (one autograd node over gs_views_forward / gs_views_backward, the views on V streams)
+    against the reference's per-view loop of render() + backward: images, radii, visibility, depth,
+    view-space gradients and the accumulated parameter gradients are bitwise equal (the views' per-Gaussian
+    passes add into .grad in view order, as the loop's backward calls do); speculate: the binning buffers
+    sized from the counts seen before (no host wait), checked afterwards."""
     from dge_amd.cameras import orbit_camera
-    from dge_amd.gaussian_renderer import PipelineParams
+    from dge_amd.gaussian_renderer import PipelineParams, render
+    from dge_amd.multiview import render_views
     from dge_amd.scene import synthetic_scene
 
     dev = torch.device("cuda")
@@ -205,18 +208,56 @@ def test_render_views_shared_preprocess_matches_per_view(cuda_device, monkeypatc
     g = torch.Generator().manual_seed(3)
     seeds = [(torch.randn(3, H, W, generator=g) * 1e-3).to(dev) for _ in range(V)]
 
-    def run(multi):
-        monkeypatch.setattr(MV, "_MULTI_BEGIN", multi)
-        sc = synthetic_scene(150_000, sh_degree=3, seed=4, device=dev).requires_grad_(True)
-        outs = MV.render_views(cams, sc, PipelineParams(), torch.zeros(3, device=dev), streams=V)
-        torch.autograd.backward([o["render"] for o in outs], seeds)
+    def collect(outs, sc):
         torch.cuda.synchronize()
         res = {f"{k}{i}": o[k].detach().cpu().numpy() for i, o in enumerate(outs)
-               for k in ("render", "radii", "visibility_filter")}
+               for k in ("render", "radii", "visibility_filter", "depth_3dgs")}
         res.update({f"vs{i}": o["viewspace_points"].grad.cpu().numpy() for i, o in enumerate(outs)})
         res.update({f"p{i}": p.grad.cpu().numpy() for i, p in enumerate(sc.parameters())})
         return res
 
-    a, b = run(True), run(False)
-    for k in b:
-        np.testing.assert_array_equal(a[k], b[k], err_msg=k)
+    sc = synthetic_scene(150_000, sh_degree=3, seed=4, device=dev).requires_grad_(True)
+    outs = []
+    for c, s in zip(cams, seeds):
+        o = render(c, sc, PipelineParams(), torch.zeros(3, device=dev))
+        o["render"].backward(s)
+        outs.append(o)
+    ref = collect(outs, sc)  # (the loop's forwards also seed the capacity history)
+    for rep in range(2):
+        sc = synthetic_scene(150_000, sh_degree=3, seed=4, device=dev).requires_grad_(True)
+        outs = render_views(cams, sc, PipelineParams(), torch.zeros(3, device=dev), streams=V, speculate=speculate)
+        torch.autograd.backward([o["render"] for o in outs], seeds)
+        assert outs.check()
+        got = collect(outs, sc)
+        for k in ref:
+            np.testing.assert_array_equal(got[k], ref[k], err_msg=f"{k} (repeat {rep})")
+
+
+def test_render_views_speculated_overflow_is_reported(cuda_device):
+    """A batch whose instance count outgrows the speculated capacity (the history of this image size holds
+    a far smaller scene of the same Gaussian count) is reported by check(); rendered again, it fits and
+    equals the exact render."""
+    from dge_amd.cameras import orbit_camera
+    from dge_amd.gaussian_renderer import PipelineParams
+    from dge_amd.multiview import render_views
+    from dge_amd.scene import synthetic_scene
+
+    dev = torch.device("cuda")
+    W, H, P = 272, 176, 40_000  # (an image size no other test renders: a fresh count history)
+    cams = [orbit_camera(k, 4, W, H, device=dev) for k in range(2)]
+    small = synthetic_scene(P, sh_degree=1, seed=2, scale=0.002, device=dev)
+    big = synthetic_scene(P, sh_degree=1, seed=2, scale=0.08, device=dev)
+    bg = torch.zeros(3, device=dev)
+    with torch.no_grad():
+        assert render_views(cams, small, PipelineParams(), bg, streams=2).check()  # exact: seeds the history
+        spec = render_views(cams, big, PipelineParams(), bg, streams=2, speculate=True)
+        assert not spec.check(), "the overflow must be reported"
+        again = render_views(cams, big, PipelineParams(), bg, streams=2, speculate=True)
+        assert again.check()
+        ref = render_views(cams, big, PipelineParams(), bg, streams=2)
+        assert ref.check()
+    torch.cuda.synchronize()
+    assert again.batch.num_rendered == ref.batch.num_rendered
+    for o, r in zip(again, ref):
+        for k in ("render", "radii", "depth_3dgs"):
+            assert torch.equal(o[k], r[k]), k

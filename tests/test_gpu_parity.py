@@ -599,36 +599,3 @@ def test_two_level_binning_matches_two_pass_sort(cuda_device, monkeypatch, P, W,
         np.testing.assert_array_equal(fused[k], ref[k], err_msg=k)
 
 
-@pytest.mark.parametrize("env", [{"DGE_AMD_BWD_GRID_CAP": "3"}, {"DGE_AMD_BWD": "tile"},
-                                 {"DGE_AMD_BWD": "tile", "DGE_AMD_BWD_GRID_CAP": "8"}])
-def test_backward_variants_match_default(cuda_device, tmp_path, env):
-    """Backward launch variants, each in a child process (the switches are read once per process):
-    the work items beyond the per-item grid (kBwdGridCap; c4-sized item counts) run on a looping grid —
-    with the cap forced down to 3 items every gradient is bitwise the default launch's; the per-tile
-    merged replay (DGE_AMD_BWD=tile, opt-in) adds the quadrant records in another order: within 1e-4."""
-    import subprocess
-    import sys
-
-    script = tmp_path / "bwd_cap.py"
-    script.write_text(f'''
-import sys, numpy as np
-sys.path.insert(0, {repr(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))})
-sys.path.insert(0, {repr(os.path.dirname(os.path.abspath(__file__)))})
-from helpers import scene_arrays, camera_settings, run_gpu, GRAD_NAMES
-from test_gpu_parity import _sh_kw
-a = scene_arrays(200_000, seed=5, radius=2.0, scale=0.02)
-g = np.random.default_rng(7).standard_normal((3, 256, 384)).astype(np.float32)
-r = run_gpu(camera_settings(384, 256, device="cuda"), g, intermediates=False, **_sh_kw(a))
-np.savez(sys.argv[1], **{{n: r[n] for n in GRAD_NAMES}})
-''')
-    out = tmp_path / "capped.npz"
-    subprocess.run([sys.executable, str(script), str(out)], env=dict(os.environ, **env), check=True, timeout=300)
-    a = scene_arrays(200_000, seed=5, radius=2.0, scale=0.02)
-    g = np.random.default_rng(7).standard_normal((3, 256, 384)).astype(np.float32)
-    ref = run_gpu(camera_settings(384, 256, device="cuda"), g, intermediates=False, **_sh_kw(a))
-    got = np.load(out)
-    for n in GRAD_NAMES:
-        if "DGE_AMD_BWD" in env:
-            assert_close(got[n], ref[n], f"{n} ({env})", 1e-4)
-        else:
-            np.testing.assert_array_equal(got[n], ref[n], err_msg=f"{n} differs with the looping grid")

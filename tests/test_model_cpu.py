@@ -82,6 +82,44 @@ def test_expon_lr_schedule_known_answers():
     assert math.isclose(g(5), (0.5 + 0.5 * math.sin(0.25 * math.pi)) * 1e-3 ** 0.95 * 1e-5 ** 0.05, rel_tol=1e-12)
 
 
+def test_expon_lr_schedule_matches_reference_outputs():
+    """get_expon_lr_func / inverse_sigmoid against the reference's own functions
+    (gaussiansplatting/utils/general_utils.py:18-19, 29-62) evaluated by tools/make_golden.py lr:
+    DGE's position schedule, a delayed one, a disabled one and a short one, at steps before, at and past
+    every breakpoint -- equal to the last bit (the same numpy double operations)."""
+    import os
+
+    d = np.load(os.path.join(os.path.dirname(__file__), "golden", "lr_schedule_ref.npz"))
+    for i, (lr_init, lr_final, delay, mult, max_steps) in enumerate(d["cases"]):
+        f = get_expon_lr_func(lr_init=float(lr_init), lr_final=float(lr_final), lr_delay_steps=int(delay),
+                              lr_delay_mult=float(mult), max_steps=int(max_steps))
+        got = np.array([float(f(int(s))) for s in d["steps"]])
+        np.testing.assert_array_equal(got, d[f"lr_{i}"], err_msg=f"case {i}")
+    x = torch.from_numpy(d["inv_sigmoid_x"])
+    np.testing.assert_array_equal(inverse_sigmoid(x).numpy(), d["inv_sigmoid"])
+
+
+def test_model_learning_rate_follows_reference_schedule():
+    """GaussianModel.update_learning_rate sets the xyz group's lr to the reference schedule's value
+    (gaussian_model.py:382-389) at each step."""
+    import os
+
+    d = np.load(os.path.join(os.path.dirname(__file__), "golden", "lr_schedule_ref.npz"))
+    m = GaussianModel(3, device="cpu")
+    m.set_parameters(*[torch.zeros(4, *s) for s in ((3,), (1, 3), (15, 3), (1,), (3,), (4,))])
+    opt = OptimizationParams(max_steps=30_000)
+    m.spatial_lr_scale = 2.5
+    m.training_setup(opt, optimizer_cls=torch.optim.Adam)
+    lr_init, lr_final, delay, mult, max_steps = d["cases"][0]
+    assert math.isclose(opt.position_lr_init * 2.5, lr_init) and math.isclose(opt.position_lr_final * 2.5, lr_final)
+    for s, ref in zip(d["steps"], d["lr_0"]):
+        if s < 0:
+            continue
+        m.update_learning_rate(int(s))
+        xyz_group = next(g for g in m.optimizer.param_groups if g["name"] == "xyz")
+        assert xyz_group["lr"] == ref
+
+
 def _setup(m):
     m.training_setup(OptimizationParams(max_steps=1000), optimizer_cls=torch.optim.Adam)
     # one optimizer step so every group has state

@@ -18,7 +18,6 @@ from dge_amd.gaussian_renderer import PipelineParams, render  # noqa: E402
 from dge_amd.scene import synthetic_scene  # noqa: E402
 
 
-PIPELINED = os.environ.get("DGE_AMD_FWD", "0") == "1"  # k_render_fwd_pc: word 6 = SIMD of each wave
 
 
 def summarize(name, d, nquads=None):
@@ -46,8 +45,7 @@ def summarize(name, d, nquads=None):
     order = np.argsort(-dur)[:6]
     for i in order:
         extra = f" seg {int(d[i, 6]) >> 32} quad {int(d[i, 6]) & 0xFFFFFFFF}" if nquads else \
-            (f" simds {[(int(d[i, 6]) >> (2 * w)) & 3 for w in range(2)]}" if PIPELINED else
-             f" cull+wait share {d[i, 6] / max(1, cyc_total[i]):.2f}")
+            f" cull+wait share {d[i, 6] / max(1, cyc_total[i]):.2f}"
         print(f"   slowest: wave {ids[i]} dur {dur[i]:.1f} us kept {kept[i]} rounds {rounds[i]} loop cyc/kept "
               f"{cyc_loop[i] / max(1, kept[i]):.0f} loop share {cyc_loop[i] / max(1, cyc_total[i]):.2f} "
               f"start {(start[i] - t0) * 10e-3:.1f}{extra}")
@@ -65,25 +63,6 @@ def summarize(name, d, nquads=None):
             ov = [min(end[i], end[j]) - max(start[i], start[j]) for j in mates]
             print(f"   slowest wave {ids[i]}: {len(mates)} SIMD mates, overlap-us {[round(o * 10e-3, 1) for o in ov]}, "
                   f"their durations {[round(float(dur[j]), 1) for j in mates]}")
-    if PIPELINED and not nquads:
-        sm = np.stack([(d[:, 6] >> (2 * w)) & 3 for w in range(2)], 1)
-        distinct = np.mean([len(set(r)) == 2 for r in sm])
-        print(f"   pipelined workgroups: 2 waves on 2 distinct SIMDs in {distinct:.3f}; chain-wave SIMD histogram "
-              f"{np.bincount(sm[:, 0], minlength=4).tolist()}")
-        pro = ((d[:, 6] >> 8) & 0xFFFFFFFF) * 10e-3  # (chain wave: entry -> after the prologue)
-        pa, pc = (d[:, 3] & 0xFFFFFFFF), (d[:, 3] >> 32)
-        for i in order[:4]:
-            print(f"   wave {ids[i]}: producer cycles/kept alpha {pa[i] / max(1, kept[i]):.0f} cull {pc[i] / max(1, kept[i]):.0f}; "
-                  f"chain {cyc_loop[i] / max(1, kept[i]):.0f}; total {cyc_total[i] / max(1, kept[i]):.0f}")
-        rk = d[:, 6] >> 40
-        print(f"   prologue (first cull) us: p50 {np.percentile(pro, 50):.2f} p99 {np.percentile(pro, 99):.2f} "
-              f"max {pro.max():.2f}")
-        for lo, hi in ((0, 32), (32, 128), (128, 512), (512, 4096)):
-            m = (rk >= lo) & (rk < hi)
-            if m.any():
-                print(f"   tile ranks [{lo},{hi}): start us mean {((start[m] - t0) * 10e-3).mean():.1f} "
-                      f"max {((start[m] - t0) * 10e-3).max():.1f}; dur mean {dur[m].mean():.1f} max {dur[m].max():.1f}; "
-                      f"kept mean {kept[m].mean():.0f}")
     ts = np.linspace(0, span, 11)
     alive = [int(((start - t0) * 10e-3 <= t).sum() - ((end - t0) * 10e-3 <= t).sum()) for t in ts]
     print("   waves running over time:", " ".join(f"{t:.0f}:{a}" for t, a in zip(ts, alive)))

@@ -7,13 +7,17 @@
                     oracle's and the kernels' SH->RGB (forward.cu:20-71 restates it).
   cameras_ref.npz   the REFERENCE's getWorld2View2 / getProjectionMatrix outputs (and the
                     Simple_Camera composition) for the c1-c5 cameras and random poses.
+  lr_schedule_ref.npz  the REFERENCE's get_expon_lr_func schedules (the optimizer's position
+                    learning rate, gaussian_model.py:373-380) and inverse_sigmoid
+                    (gaussiansplatting/utils/general_utils.py:18-19, 29-62), imported read-only.
   multiview_3views.npz  the oracle's 3-view step reductions (summed parameter and view-space
                     gradients, max radii) for the F1 multi-view step test.
   scene_*.npz       seeded scenes (inputs) with the oracle's outputs and gradients:
                     the GPU parity tests compare the HIP path against them.
 
 Only data is written (no reference source).  Run from the repo root:
-    python tools/make_golden.py
+    python tools/make_golden.py            (all fixtures)
+    python tools/make_golden.py lr sh ...  (only those)
 """
 from __future__ import annotations
 
@@ -194,15 +198,49 @@ def multiview_fixture():
     print("multiview_3views", os.path.getsize(os.path.join(OUT, "multiview_3views.npz")))
 
 
+# (lr_init, lr_final, lr_delay_steps, lr_delay_mult, max_steps): DGE's position schedule (the optimizer
+# defaults of arguments/__init__.py:71-89 x spatial_lr_scale, gaussian_model.py:373-380), a delayed one,
+# a disabled one (both rates 0) and a short one
+LR_CASES = [(0.00016 * 2.5, 0.000016 * 2.5, 0, 0.01, 30_000), (1e-3, 1e-5, 500, 0.01, 10_000),
+            (0.0, 0.0, 0, 1.0, 1000), (5e-2, 5e-4, 10, 0.1, 100)]
+LR_STEPS = [-1, 0, 1, 2, 5, 9, 10, 11, 50, 99, 100, 101, 499, 500, 501, 1000, 5000, 9999, 10000, 10001, 15000,
+            29_999, 30_000, 30_001, 100_000]
+
+
+def lr_fixture():
+    sys.dont_write_bytecode = True
+    sys.path.insert(0, "/root/reference")
+    from gaussiansplatting.utils.general_utils import get_expon_lr_func, inverse_sigmoid  # the reference's own
+
+    out = {"cases": np.array(LR_CASES, dtype=np.float64), "steps": np.array(LR_STEPS, dtype=np.int64)}
+    for i, c in enumerate(LR_CASES):
+        f = get_expon_lr_func(lr_init=c[0], lr_final=c[1], lr_delay_steps=int(c[2]), lr_delay_mult=c[3],
+                              max_steps=int(c[4]))
+        out[f"lr_{i}"] = np.array([float(f(s)) for s in LR_STEPS], dtype=np.float64)
+    x = torch.linspace(0.001, 0.999, 257)
+    out["inv_sigmoid_x"] = x.numpy()
+    out["inv_sigmoid"] = inverse_sigmoid(x).numpy()
+    np.savez_compressed(os.path.join(OUT, "lr_schedule_ref.npz"), **out)
+    sys.path.remove("/root/reference")
+
+
+FIXTURES = {
+    "sh": sh_fixture,
+    "cameras": camera_fixture,
+    "lr": lr_fixture,
+    "scenes": lambda: [
+        scene_fixture("sh3_96x80", 1500, 96, 80, seed=11),
+        scene_fixture("sh1_bg_64", 800, 64, 64, seed=12, sh_degree=1, bg=(0.2, 0.5, 0.9), scale=0.08),
+        scene_fixture("colors_120x72", 1000, 120, 72, seed=13, mode="colors", scale=0.06, view=1, nviews=3),
+        scene_fixture("cov3d_mod_80", 900, 80, 80, seed=14, mode="cov3d", scale_modifier=0.8, scale=0.07)],
+    "multiview": lambda: multiview_fixture(),
+}
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
-    sh_fixture()
-    camera_fixture()
-    scene_fixture("sh3_96x80", 1500, 96, 80, seed=11)
-    scene_fixture("sh1_bg_64", 800, 64, 64, seed=12, sh_degree=1, bg=(0.2, 0.5, 0.9), scale=0.08)
-    scene_fixture("colors_120x72", 1000, 120, 72, seed=13, mode="colors", scale=0.06, view=1, nviews=3)
-    scene_fixture("cov3d_mod_80", 900, 80, 80, seed=14, mode="cov3d", scale_modifier=0.8, scale=0.07)
-    multiview_fixture()
+    for name in sys.argv[1:] or list(FIXTURES):
+        FIXTURES[name]()
 
 
 if __name__ == "__main__":
