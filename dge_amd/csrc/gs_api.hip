@@ -1058,9 +1058,8 @@ struct gs_views {
 };
 
 namespace {
-// the views' streams wait for the caller's stream `join` (nullptr: none)
+// the views' streams wait for the caller's stream `join` (a null handle is the legacy default stream)
 int fork_from(gs_views* h, hipStream_t join, const gs_stream_t* streams) {
-    if (!join) return GS_OK;
     bool other = false;
     for (int v = 0; v < h->n; ++v) other |= (hipStream_t)streams[v] != join;
     if (!other) return GS_OK;
@@ -1075,7 +1074,6 @@ int fork_from(gs_views* h, hipStream_t join, const gs_stream_t* streams) {
 }
 // `join` waits for every view stream's work so far
 int join_into(gs_views* h, hipStream_t join, const gs_stream_t* streams) {
-    if (!join) return GS_OK;
     for (int v = 0; v < h->n; ++v) {
         bool seen = (hipStream_t)streams[v] == join;
         for (int u = 0; u < v && !seen; ++u) seen = streams[u] == streams[v];
@@ -1240,9 +1238,8 @@ int gs_views_backward(gs_views* h, const float* const* dL_dpix, const gs_grads* 
             GS_HIP(hipEventRecord(h->ev[v], sv));
             prev = v;
         }
-        if (join)
-            for (int v = 0; v < h->n; ++v)
-                if (h->ev[v] && streams[v] != join_) GS_HIP(hipStreamWaitEvent(join, h->ev[v], 0));
+        for (int v = 0; v < h->n; ++v)
+            if (h->ev[v] && streams[v] != join_) GS_HIP(hipStreamWaitEvent(join, h->ev[v], 0));
         return GS_OK;
     } catch (const std::exception& e) {
         return set_error(GS_ERR_INVALID_ARG, "exception: %s", e.what());

@@ -150,29 +150,6 @@ __device__ __forceinline__ float blend_chain(float a, float4 fe, uint32_t pos, f
     return w;
 }
 
-// blend_chain split at Tw (identical operations): the transmittance step, then the sums
-__device__ __forceinline__ float blend_t(float a, float& Ts) {
-#pragma clang fp contract(off)
-    const float tT = Ts * (1.0f - a);
-    const bool go = tT >= 0.0001f;
-    const float Tw = go ? Ts : 0.0f;
-    Ts = go ? tT : -fabsf(Ts);
-    return Tw;
-}
-__device__ __forceinline__ float blend_sums(float a, float Tw, float4 fe, uint32_t pos, f2v& C01, f2v& C2D, f2v& L01,
-                                            float& L2, uint32_t& last) {
-#pragma clang fp contract(off)
-    const f2v a2 = {a, a}, T2 = {Tw, Tw};
-    const f2v fa01 = f2v{fe.x, fe.y} * a2, fa2d = f2v{fe.z, fe.w} * a2;
-    C01 = __builtin_elementwise_fma(fa01, T2, C01);
-    C2D = __builtin_elementwise_fma(fa2d, T2, C2D);
-    L01 = __builtin_elementwise_fma(fa01, T2, L01);
-    L2 = __builtin_fmaf(fa2d.x, Tw, L2);
-    const float w = a * Tw;
-    last = w > 0.0f ? pos : last;
-    return w;
-}
-
 // Dispatch order of the blend: tiles by list length, longest first (coarse
 // log-scale classes; the order inside a class is whatever the LDS atomics give
 // — it only decides placement).  The longest lists are then dealt first, one
@@ -290,8 +267,15 @@ __global__ __launch_bounds__(64, 3) void k_render_fwd(RenderArgs a) {
     }
     load_ids(range.x + kRound, ids);
 
-    // checkpoint of segment k of this quadrant: slot ckpt_base + k, quadrant `quad`
-    float4* ckpt = a.ckpt + ((size_t)ckpt_base(range.x, tile) * 4 + quad) * 64;
+    // checkpoint of segment k of this quadrant: slot ckpt_base + k, quadrant `quad`: (T after it, its own
+    // colour sum), then 64 float4 further (one address, an immediate offset) the colour composited so far
+    float4* ckpt = a.ckpt + ((size_t)ckpt_base(range.x, tile) * 4 + quad) * kCkptPer + lane;
+    const auto put_ckpt = [&](int k) {
+        ckpt[(size_t)k * 4 * kCkptPer] = make_float4(fabsf(Ts), L01.x, L01.y, L2);
+        ckpt[(size_t)k * 4 * kCkptPer + 64] = make_float4(C01.x, C01.y, C2D.x, 0.f);
+        L01 = f2v{0.f, 0.f};
+        L2 = 0.f;
+    };
     int seg_done = -1;  // last segment whose checkpoint is pending (the round just blended)
     uint64_t c_cull = 0;
     // The round's global stores (checkpoint, the previous round's blended bits) are issued after
@@ -368,20 +352,14 @@ __global__ __launch_bounds__(64, 3) void k_render_fwd(RenderArgs a) {
             cid[i] = ids[i];
         }
         load_ids(b + 2 * kRound, ids);
-        if (seg_done >= 0) {  // the previous segment's (T after it, own colour sum): the replay's start
-            ckpt[(size_t)seg_done * 256 + lane] = make_float4(fabsf(Ts), L01.x, L01.y, L2);
-            L01 = f2v{0.f, 0.f};
-            L2 = 0.f;
-        }
+        if (seg_done >= 0) put_ckpt(seg_done);  // the previous segment's: the replay's start
         seg_done = (int)((b - range.x) / kSegLen);  // the round's first segment
         // the round's second segment exists: its checkpoint follows the first one's at n_mid (-1: none,
         // or taken)
         const int n_mid_slot = n_mid;
         if (range.y - b <= (uint32_t)kSegLen) n_mid = -1;
         const auto take_mid = [&]() {
-            ckpt[(size_t)seg_done * 256 + lane] = make_float4(fabsf(Ts), L01.x, L01.y, L2);
-            L01 = f2v{0.f, 0.f};
-            L2 = 0.f;
+            put_ckpt(seg_done);
             ++seg_done;
             n_mid = -1;
         };
@@ -480,7 +458,7 @@ __global__ __launch_bounds__(64, 3) void k_render_fwd(RenderArgs a) {
 
     // the last blended segment's checkpoint (an empty tile's range is (0, 0): no slot, no replay)
     const float T = fabsf(Ts);
-    if (seg_done >= 0) ckpt[(size_t)seg_done * 256 + lane] = make_float4(T, L01.x, L01.y, L2);
+    if (seg_done >= 0) put_ckpt(seg_done);
     if (inside) {
         const size_t pix = (size_t)a.W * py + px;
         const size_t HW = (size_t)a.W * a.H;
@@ -784,21 +762,31 @@ __global__ __launch_bounds__(64, GS_BWD_WAVES) void k_render_bwd(RenderBwdArgs a
     float T = T_final, D0 = 0.f, D1 = 0.f, D2 = 0.f;
     if (limit < window) {
         // start inside the window: T after this segment (its checkpoint) and the colour composited
-        // behind position `limit`, D = (S_{seg+1} + ... + S_last) / T from the later segments' own
-        // colour sums (summed back to front)
-        const float4* ck = a.ckpt + ((size_t)ckpt_base(range.x, tile) * 4 + quad) * 64;
-        T = ck[(size_t)seg * 256 + lane].x;
-        float S0 = 0.f, S1 = 0.f, S2 = 0.f;
-        for (int k = nseg_q - 1; k > seg; --k) {
-            const float4 c = ck[(size_t)k * 256 + lane];
-            S0 += c.y;
-            S1 += c.z;
-            S2 += c.w;
+        // behind position `limit`, D = B / T.  B = C_last - C_seg, the difference of the colour sums
+        // after the window's last segment (no pixel of the quadrant blends past it) and after this one:
+        // two reads whatever the segment's place in the window — used where it keeps its precision,
+        // B >= C_last / 8 in every channel (the prefixes' rounding, relative to C_last, is then at most
+        // 8x that relative to B).  Elsewhere (the window's tail, close to saturation: few later
+        // segments) B is the sum of the later segments' own colour sums, back to front.
+        const float4* ck = a.ckpt + ((size_t)ckpt_base(range.x, tile) * 4 + quad) * kCkptPer + lane;
+        const float4 cs = ck[(size_t)seg * 4 * kCkptPer];
+        const float4 ps = ck[(size_t)seg * 4 * kCkptPer + 64];
+        const float4 pl = ck[(size_t)(nseg_q - 1) * 4 * kCkptPer + 64];
+        T = cs.x;
+        float B0 = pl.x - ps.x, B1 = pl.y - ps.y, B2 = pl.z - ps.z;
+        if (!(B0 >= 0.125f * pl.x && B1 >= 0.125f * pl.y && B2 >= 0.125f * pl.z)) {
+            B0 = 0.f, B1 = 0.f, B2 = 0.f;
+            for (int k = nseg_q - 1; k > seg; --k) {
+                const float4 c = ck[(size_t)k * 4 * kCkptPer];
+                B0 += c.y;
+                B1 += c.z;
+                B2 += c.w;
+            }
         }
         const float inv = 1.0f / T;
-        D0 = S0 * inv;
-        D1 = S1 * inv;
-        D2 = S2 * inv;
+        D0 = B0 * inv;
+        D1 = B1 * inv;
+        D2 = B2 * inv;
     }
     const float ddelx_dx = (float)(0.5 * a.W), ddely_dy = (float)(0.5 * a.H);
     const uint64_t t_start = a.diag ? __builtin_amdgcn_s_memrealtime() : 0;

@@ -150,7 +150,7 @@ __global__ __launch_bounds__(256) void k_radix_hist(const uint32_t* __restrict__
 // digit dl) sums rows [g*per, (g+1)*per) of its digit (a wave load covers 4 rows
 // x 64 B), the 64 row-group sums are scanned in LDS, then the rows are
 // rewritten.  (c2: 880 tile-sort rows -> 14 per thread.)
-constexpr int kScanDigits = 16, kScanGroups = 64, kScanRegs = 16;
+constexpr int kScanDigits = 16, kScanGroups = 64, kScanRegs = 32;
 constexpr int kScanBmRows = kScanGroups * kScanRegs;  // block-major tables up to this many blocks
 __global__ __launch_bounds__(1024) void k_radix_digit_scan(uint32_t* __restrict__ hist, int nb, int ndig,
                                                            uint32_t* __restrict__ totals,

@@ -225,8 +225,9 @@ int gs_rasterize_backward_ex(const gs_settings *s, const gs_params *g, int R, co
  *     backward of it are invalid; a second forward of the batch fits, the
  *     capacity having grown).  Views without history are rendered exactly.
  * All buffers but the exact binning ones come from ONE alloc(alloc_ctx, 0, bytes).
- * join (optional): the caller's stream — the views' streams start after its
- * work so far, and it waits for all of the views' work before the call returns. 
+ * join: the caller's stream (a null handle is the legacy default stream) — the
+ * views' streams start after its work so far, and it waits for all of the
+ * views' work before the call returns. 
  * The outputs of a speculated batch are bit-identical to the exact ones when
  * gs_views_check returns GS_OK. */
 #define GS_MAX_VIEWS 8
@@ -243,8 +244,9 @@ int gs_views_check(gs_views *h, int *num_rendered);
  * per view; the parameter gradients usually shared, GS_ACC_* set from the
  * second view on).  The views' per-Gaussian passes are chained in view order
  * (the first after `writes_after`, an optional hipEvent_t), so accumulated
- * gradients add up in a fixed order; `join` (optional): the views start after
- * its work so far (the image gradients) and it waits for all of them. */
+ * gradients add up in a fixed order; `join` (the caller's stream, null = the
+ * legacy default stream): the views start after its work so far (the image
+ * gradients) and it waits for all of them. */
 int gs_views_backward(gs_views *h, const float *const *dL_dpix, const gs_grads *const *grads,
                       const gs_stream_t *streams, void *writes_after, gs_stream_t join);
 /* View v's buffers (which: 0 geometry, 1 binning, 2 image; gs_buffer_offset

@@ -223,6 +223,6 @@ def test_render_views_on_streams_matches_sequential(cuda_device, grads_exist):
     torch.cuda.synchronize()
     for mode in ("streams", "interleaved", "bucket"):
         for a, b in zip(res["sequential"][1], res[mode][1]):
-            torch.testing.assert_close(a, b, rtol=0, atol=0)
-        for a, b in zip(res["sequential"][0], res[mode][0]):
-            torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-7)
+            torch.testing.assert_close(a, b, rtol=0, atol=0, msg=f"image ({mode})")
+        for i, (a, b) in enumerate(zip(res["sequential"][0], res[mode][0])):
+            torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-7, msg=lambda m: f"parameter {i} ({mode}): {m}")
