@@ -68,6 +68,9 @@ def parse():
     ap.add_argument("--scan-live", action="store_true",
                     help="N > 1: find the all-reduce's live rows by reading the gradient bucket after the backward "
                          "(GradBucket.allreduce) instead of agreeing on the forwards' blended Gaussians before it")
+    ap.add_argument("--serial-zero", action="store_true",
+                    help="zero the gradient bucket on the default stream before the forwards (default: on the first "
+                         "view's stream beside the forwards, GradBucket.zero(stream=...))")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -376,8 +379,19 @@ def run_views(args, cams, scene, pipe, bg, seeds, bucket, streams=None, min_worl
         render_backward_views(cams, scene, pipe, bg, seeds, streams=streams)
         return
     for _ in range(2):
-        bucket.zero()
+        # the bucket's fill runs on the first view's stream behind that view's forward, beside the others'
+        # (only the backward's gradient writes wait for it: GradBucket.zero(stream=...))
+        side = streams > 1 and not args.serial_zero
+        if side:
+            main = torch.cuda.current_stream()
+            ready = main.record_event()
+        else:
+            bucket.zero()
         outs = render_views(cams, scene, pipe, bg, streams=streams, speculate=args.speculate)
+        if side:
+            from dge_amd.multiview import stream_pool
+
+            bucket.zero(stream=stream_pool(main.device, streams)[0], after=ready)
         if min_world is not None and not args.scan_live:
             bucket.allreduce_begin([o.get("_live_rows") for o in outs], min_world=min_world)
         torch.autograd.backward([o["render"] for o in outs], seeds)

@@ -645,51 +645,55 @@ int bin_forward(const gs_settings* s, const Grid& g, const gs_params& gp, int* r
     return bin_end(f, alloc, ctx, stream, bin_out, K_out);
 }
 
-// One view's backward (gs_rasterize_backward_ex): the replay, then the per-Gaussian pass, whose
-// accumulated writes wait for writes_after.  R: the binning layout's instance count; slot_cap: a
-// speculative forward's capacity (its slots end there), else ~0.
-int backward_view(const gs_settings* s, const gs_params* gp, int R, const int* radii, const void* geom,
-                  const void* binning, const void* img, const float* dL_dpix, const gs_grads* o, hipStream_t stream,
-                  hipEvent_t writes_after, uint32_t slot_cap) {
+// One view's backward, in two parts: the gradient replay (k_render_bwd: the per-(slot, quadrant)
+// records), then the per-Gaussian pass over those records, whose accumulated writes wait for
+// writes_after.  R: the binning layout's instance count; slot_cap: a speculative forward's capacity
+// (its slots end there), else ~0.
+int replay_view(const gs_settings* s, const gs_params* gp, int R, const void* geom, const void* binning,
+                const void* img, const float* dL_dpix, hipStream_t stream) {
     const int P = gp->P;
-    if (P == 0) return GS_OK;
+    if (P == 0 || R <= 0) return GS_OK;
     const bool debug = s->debug != 0;
     const Grid g = make_grid(s);
     const GeomLayout gl = geom_layout(P);
     const ImgLayout il = img_layout(g.W, g.H);
     const BinLayout bl = bin_layout(R, g.tiles);
-    float4* records = R > 0 ? at<float4>(const_cast<void*>(binning), bl.records) : nullptr;
-    uint8_t* rec_flags = R > 0 ? at<uint8_t>(const_cast<void*>(binning), bl.rec_flags) : nullptr;
-    // per-Gaussian "has a record" bytes: k_gauss_bwd skips every Gaussian without one (all of
-    // its gradients are zero), which is most of them (occluded behind saturated pixels)
-    // (both zeroed by the forward: `touched` in preprocess, the flags with the tile ranges.  A
-    // second backward of the same forward finds the bytes of the first, which it sets again: the
-    // entries that get records depend on the forward alone)
-    uint8_t* touched = at<uint8_t>(const_cast<void*>(geom), gl.touched);
-    if (R > 0) {
-        uint32_t* bwd_count = at<uint32_t>(const_cast<void*>(img), il.bwd_count);
-        RenderBwdArgs rb;
-        rb.W = g.W; rb.H = g.H; rb.gx = g.gx; rb.gy = g.gy;
-        rb.ranges = at<uint2>(img, il.ranges);
-        rb.point_pairs = at<uint2>(binning, bl.point_pairs);
-        rb.bwd_items = at<uint2>(binning, bl.bwd_items);
-        rb.bwd_count = bwd_count;
-        rb.tile_last = at<uint32_t>(img, il.tile_last);
-        rb.item_cap = (uint32_t)(4 * bl.nslots);
-        rb.quad_last = at<uint32_t>(img, il.quad_last);
-        rb.ckpt = at<float4>(binning, bl.ckpt);
-        rb.used = at<uint64_t>(binning, bl.used);
-        rb.splat = at<Splat>(geom, gl.splat);
-        rb.bg = s->bg;
-        rb.final_T = at<float>(img, il.final_T);
-        rb.n_contrib = at<uint32_t>(img, il.n_contrib);
-        rb.dL_dpix = dL_dpix;
-        rb.records = records;
-        rb.rec_flags = rec_flags;
-        rb.diag = diag_buffer(1, kDiagWords * 4 * bl.nslots);
-        { StageScope sc(ST_RENDER_BWD, stream); launch_render_backward(rb, stream); }
-        GS_LAUNCHED("render backward");
-    }
+    RenderBwdArgs rb;
+    rb.W = g.W; rb.H = g.H; rb.gx = g.gx; rb.gy = g.gy;
+    rb.ranges = at<uint2>(img, il.ranges);
+    rb.point_pairs = at<uint2>(binning, bl.point_pairs);
+    rb.bwd_items = at<uint2>(binning, bl.bwd_items);
+    rb.bwd_count = at<uint32_t>(const_cast<void*>(img), il.bwd_count);
+    rb.tile_last = at<uint32_t>(img, il.tile_last);
+    rb.item_cap = (uint32_t)(4 * bl.nslots);
+    rb.quad_last = at<uint32_t>(img, il.quad_last);
+    rb.ckpt = at<float4>(binning, bl.ckpt);
+    rb.used = at<uint64_t>(binning, bl.used);
+    rb.splat = at<Splat>(geom, gl.splat);
+    rb.bg = s->bg;
+    rb.final_T = at<float>(img, il.final_T);
+    rb.n_contrib = at<uint32_t>(img, il.n_contrib);
+    rb.dL_dpix = dL_dpix;
+    rb.records = at<float4>(const_cast<void*>(binning), bl.records);
+    rb.rec_flags = at<uint8_t>(const_cast<void*>(binning), bl.rec_flags);
+    rb.diag = diag_buffer(1, kDiagWords * 4 * bl.nslots);
+    { StageScope sc(ST_RENDER_BWD, stream); launch_render_backward(rb, stream); }
+    GS_LAUNCHED("render backward");
+    return GS_OK;
+}
+
+// the per-Gaussian pass's arguments for one view
+// (the per-Gaussian "has a record" bytes: k_gauss_bwd skips every Gaussian without one (all of
+// its gradients are zero), which is most of them (occluded behind saturated pixels); both zeroed by
+// the forward: `touched` in preprocess, the flags with the tile ranges.  A second backward of the
+// same forward finds the bytes of the first, which it sets again: the entries that get records
+// depend on the forward alone)
+GaussBwdArgs gauss_args(const gs_settings* s, const gs_params* gp, int R, const int* radii, const void* geom,
+                        const void* binning, const gs_grads* o, uint32_t slot_cap) {
+    const int P = gp->P;
+    const Grid g = make_grid(s);
+    const GeomLayout gl = geom_layout(P);
+    const BinLayout bl = bin_layout(R, g.tiles);
     GaussBwdArgs ga;
     ga.P = P; ga.D = s->sh_degree; ga.M = gp->M; ga.W = g.W; ga.H = g.H; ga.gx = g.gx; ga.gy = g.gy;
     ga.means3D = gp->means3D; ga.scales = gp->scales; ga.rotations = gp->rotations;
@@ -708,11 +712,11 @@ int backward_view(const gs_settings* s, const gs_params* gp, int R, const int* r
     ga.tiles_touched = at<uint32_t>(geom, gl.tiles_touched);
     ga.first_slot = at<uint32_t>(geom, gl.first_slot);
     ga.clamped = at<uint8_t>(geom, gl.clamped);
-    ga.rec_flags = rec_flags;
-    ga.touched = touched;
+    ga.rec_flags = R > 0 ? at<uint8_t>(const_cast<void*>(binning), bl.rec_flags) : nullptr;
+    ga.touched = at<uint8_t>(const_cast<void*>(geom), gl.touched);
     ga.live_count = at<uint32_t>(const_cast<void*>(geom), gl.live_count);
     ga.live_list = at<uint32_t>(const_cast<void*>(geom), gl.live_list);
-    ga.records = records;
+    ga.records = R > 0 ? at<float4>(const_cast<void*>(binning), bl.records) : nullptr;
     ga.dL_dmeans2D = o->dL_dmeans2D; ga.dL_dcolors = o->dL_dcolors; ga.dL_dopacity = o->dL_dopacity;
     ga.dL_dmeans3D = o->dL_dmeans3D; ga.dL_dcov3D = o->dL_dcov3D;
     ga.dL_dscales = o->dL_dscales; ga.dL_drot = o->dL_drotations;
@@ -722,6 +726,17 @@ int backward_view(const gs_settings* s, const gs_params* gp, int R, const int* r
     ga.mask_bits = o->grad_mask ? o->mask_bits : 0u;
     ga.dL_dconic = o->dL_dconic;
     ga.diag = diag_buffer(2, kDiagWords * 4 * (size_t)(P / 256 + 1));
+    return ga;
+}
+
+int backward_view(const gs_settings* s, const gs_params* gp, int R, const int* radii, const void* geom,
+                  const void* binning, const void* img, const float* dL_dpix, const gs_grads* o, hipStream_t stream,
+                  hipEvent_t writes_after, uint32_t slot_cap) {
+    if (gp->P == 0) return GS_OK;
+    const bool debug = s->debug != 0;
+    int rc = replay_view(s, gp, R, geom, binning, img, dL_dpix, stream);
+    if (rc) return rc;
+    const GaussBwdArgs ga = gauss_args(s, gp, R, radii, geom, binning, o, slot_cap);
     { StageScope sc(ST_GAUSS_BWD, stream); launch_gauss_backward(ga, stream, writes_after); }
     GS_LAUNCHED("gaussian backward");
     return GS_OK;
@@ -1212,27 +1227,92 @@ int gs_views_check(gs_views* h, int* num_rendered) {
     return GS_OK;
 }
 
+// the views' per-Gaussian passes can run as one (launch_gauss_backward_views): one scene (same P, rows,
+// SH layout), the same parameter-shaped outputs, every view after the first adding into all of them
+bool views_mergeable(const gs_views* h, const gs_grads* const* o) {
+    const uint32_t params = GS_ACC_OPACITY | GS_ACC_MEANS3D | GS_ACC_SCALES | GS_ACC_ROTATIONS;
+    const gs_params& p0 = h->f[0].gp;
+    const gs_grads* g0 = o[0];
+    if (p0.P == 0 || g0->dL_dcov3D || p0.cov3D_precomp) return false;
+    for (int v = 1; v < h->n; ++v) {
+        const gs_params& p = h->f[v].gp;
+        const gs_grads* g = o[v];
+        if (p.P != p0.P || p.index != p0.index || p.M != p0.M || p.sh_dc != p0.sh_dc || p.sh_rest != p0.sh_rest ||
+            p.means3D != p0.means3D || p.opacities != p0.opacities || p.scales != p0.scales ||
+            p.rotations != p0.rotations || p.activation != p0.activation || p.sh_half != p0.sh_half ||
+            h->f[v].s.sh_degree != h->f[0].s.sh_degree)
+            return false;
+        if (g->dL_dopacity != g0->dL_dopacity || g->dL_dmeans3D != g0->dL_dmeans3D ||
+            g->dL_dscales != g0->dL_dscales || g->dL_drotations != g0->dL_drotations ||
+            g->dL_dsh_dc != g0->dL_dsh_dc || g->dL_dsh_rest != g0->dL_dsh_rest || g->dL_dcov3D || g->grad_mask != g0->grad_mask ||
+            g->mask_bits != g0->mask_bits)
+            return false;
+        if ((g->accumulate & params) != params || (g0->dL_dsh_dc && !(g->accumulate & GS_ACC_SH))) return false;
+    }
+    return true;
+}
+
 int gs_views_backward(gs_views* h, const float* const* dL_dpix, const gs_grads* const* grads,
                       const gs_stream_t* streams, void* writes_after, gs_stream_t join_) {
     try {
         if (!h || !dL_dpix || !grads || !streams)
             return set_error(GS_ERR_INVALID_ARG, "gs_views_backward: handle, dL_dpix, grads and streams are required");
         hipStream_t join = (hipStream_t)join_;
+        for (int v = 0; v < h->n; ++v) {
+            FwdState& f = h->f[v];
+            const int rc = validate_backward(&f.s, &f.gp, (int)h->layout[v], f.radii, f.geom, h->bin[v], f.img,
+                                             dL_dpix[v], grads[v]);
+            if (rc) return rc;
+        }
         int rc0 = fork_from(h, join, streams);  // (the image gradients come from the caller's stream)
         if (rc0) return rc0;
+        if (h->n > 1 && views_mergeable(h, grads)) {
+            // every view's replay on its stream, then ONE per-Gaussian pass over all of them (chunks of
+            // gauss_backward_max_views() views, in view order) on the first view's stream
+            hipStream_t s0 = (hipStream_t)streams[0];
+            const bool debug = h->f[0].s.debug != 0;
+            hipStream_t stream = s0;  // (GS_LAUNCHED)
+            for (int v = 0; v < h->n; ++v) {
+                FwdState& f = h->f[v];
+                hipStream_t sv = (hipStream_t)streams[v];
+                int rc = replay_view(&f.s, &f.gp, (int)h->layout[v], f.geom, h->bin[v], f.img, dL_dpix[v], sv);
+                if (rc) return rc;
+                if (sv != s0) {
+                    if (!h->ev[v] && !(h->ev[v] = event_pool().get())) return set_error(GS_ERR_HIP, "could not create an event");
+                    GS_HIP(hipEventRecord(h->ev[v], sv));
+                    GS_HIP(hipStreamWaitEvent(s0, h->ev[v], 0));
+                }
+            }
+            const int chunk = gauss_backward_max_views();
+            for (int v0 = 0; v0 < h->n; v0 += chunk) {
+                GaussBwdArgs ga[GS_MAX_VIEWS];
+                const int nv = std::min(chunk, h->n - v0);
+                for (int v = 0; v < nv; ++v) {
+                    FwdState& f = h->f[v0 + v];
+                    ga[v] = gauss_args(&f.s, &f.gp, (int)h->layout[v0 + v], f.radii, f.geom, h->bin[v0 + v],
+                                       grads[v0 + v], h->spec[v0 + v] ? h->layout[v0 + v] : 0xFFFFFFFFu);
+                }
+                { StageScope sc(ST_GAUSS_BWD, s0);
+                launch_gauss_backward_views(ga, nv, s0, v0 == 0 ? (hipEvent_t)writes_after : nullptr); }
+                GS_LAUNCHED("gaussian backward (views)");
+            }
+            if (s0 != join) {
+                if (!h->ev[0] && !(h->ev[0] = event_pool().get())) return set_error(GS_ERR_HIP, "could not create an event");
+                GS_HIP(hipEventRecord(h->ev[0], s0));
+                GS_HIP(hipStreamWaitEvent(join, h->ev[0], 0));
+            }
+            return GS_OK;
+        }
         int prev = -1;
         for (int v = 0; v < h->n; ++v) {
             FwdState& f = h->f[v];
-            int rc = validate_backward(&f.s, &f.gp, (int)h->layout[v], f.radii, f.geom, h->bin[v], f.img, dL_dpix[v],
-                                       grads[v]);
-            if (rc) return rc;
             if (f.gp.P == 0) continue;
             hipStream_t sv = (hipStream_t)streams[v];
             // accumulated writes in view order: view v's per-Gaussian pass after view prev's
             hipEvent_t wa = prev < 0 ? (hipEvent_t)writes_after
                                      : (streams[prev] != streams[v] ? h->ev[prev] : nullptr);
-            rc = backward_view(&f.s, &f.gp, (int)h->layout[v], f.radii, f.geom, h->bin[v], f.img, dL_dpix[v],
-                               grads[v], sv, wa, h->spec[v] ? h->layout[v] : 0xFFFFFFFFu);
+            int rc = backward_view(&f.s, &f.gp, (int)h->layout[v], f.radii, f.geom, h->bin[v], f.img, dL_dpix[v],
+                                   grads[v], sv, wa, h->spec[v] ? h->layout[v] : 0xFFFFFFFFu);
             if (rc) return rc;
             if (!h->ev[v] && !(h->ev[v] = event_pool().get())) return set_error(GS_ERR_HIP, "could not create an event");
             GS_HIP(hipEventRecord(h->ev[v], sv));

@@ -394,21 +394,46 @@ __device__ __forceinline__ void commit_outputs(const GaussBwdArgs& a, int idx, i
 }
 
 // ---------------------------------------------------------------------
-// Pass 1 (all P, coalesced): the live set = visible Gaussians with at least
-// one gradient record.  Every other Gaussian has exactly zero gradients: its
-// overwritten outputs get zeros here, its accumulated ones are left alone.
-// Each 256-Gaussian block compacts its live indices in place (no atomics):
-// live_list[256 b + i], i < live_count[b].
+// Several views in one pass (gs_views_backward): the views of a batch share the
+// parameters and their gradient outputs, view v >= 1 adding into them (GS_ACC_*
+// set for every parameter-shaped output), so the per-Gaussian work of all views
+// runs as ONE pass over the union of their live sets — each live Gaussian's
+// parameters and SH row read once, its views' gradients added into the outputs
+// in view order by the same thread (the later views' read-modify-writes hit L2),
+// bitwise the sums of consecutive per-view passes — instead of one pass per view
+// chained across the views' streams.  One view is the n = 1 case.
 // ---------------------------------------------------------------------
-__global__ __launch_bounds__(kGB) void k_gauss_live(GaussBwdArgs a) {
+constexpr int kMaxBwdViews = 4;
+static_assert(kMaxBwdViews <= 4, "view masks live in the top 4 bits of a live-list entry");
+constexpr uint32_t kLiveIdMask = 0x0FFFFFFFu;  // live-list entry: Gaussian | view mask << 28
+struct GaussBwdViews {
+    GaussBwdArgs v[kMaxBwdViews];
+    int n;
+};
+
+// ---------------------------------------------------------------------
+// Pass 1 (all P, coalesced): the live set = visible Gaussians with at least
+// one gradient record, in some view.  Every other Gaussian has exactly zero
+// gradients: its overwritten outputs get zeros here, its accumulated ones are
+// left alone (the parameter-shaped outputs of a Gaussian dead in view 0 are
+// zeroed per view 0's GS_ACC_* bits; a later view that has it live adds to the
+// zero, as its own pass would).  Each 256-Gaussian block compacts its live
+// entries in place (no atomics): live_list[256 b + i], i < live_count[b], in
+// view 0's geometry buffer.
+// ---------------------------------------------------------------------
+__global__ __launch_bounds__(kGB) void k_gauss_live(GaussBwdViews m) {
+    const GaussBwdArgs& a = m.v[0];
     __shared__ uint32_t s_wave[kGB / 64];
-    __shared__ uint8_t s_live[kGB];
+    __shared__ uint8_t s_live[kGB];  // view mask per Gaussian of the block
     const int idx0 = blockIdx.x * kGB;
     const int idx = idx0 + threadIdx.x;
     const int nrow = a.P - idx0 < kGB ? a.P - idx0 : kGB;
     const bool in = idx < a.P;
-    const bool live = in && a.touched[idx] && a.radii[idx] > 0;
-    s_live[threadIdx.x] = live;
+    uint32_t mask = 0;
+    for (int v = 0; v < m.n; ++v)
+        if (in && m.v[v].touched[idx] && m.v[v].radii[idx] > 0) mask |= 1u << v;
+    const bool live = mask != 0;
+    s_live[threadIdx.x] = (uint8_t)mask;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint64_t bm = __ballot(live);
     if (lane == 0) s_wave[wave] = (uint32_t)__popcll(bm);
@@ -419,13 +444,13 @@ __global__ __launch_bounds__(kGB) void k_gauss_live(GaussBwdArgs a) {
         off += w < wave ? s_wave[w] : 0u;
         total += s_wave[w];
     }
-    if (live) a.live_list[idx0 + off + (uint32_t)__popcll(bm & lanemask_lt())] = (uint32_t)idx;
+    if (live) a.live_list[idx0 + off + (uint32_t)__popcll(bm & lanemask_lt())] = (uint32_t)idx | mask << 28;
     if (threadIdx.x == 0) a.live_count[blockIdx.x] = total;
 
-    // zeros for the overwritten outputs of the dead Gaussians (parameter-shaped ones at row src)
+    // zeros for the overwritten outputs of the Gaussians dead in view 0 (parameter-shaped ones at row src)
     const uint32_t acc = a.acc;
     const int src = in && a.index ? a.index[idx] : idx;
-    if (in && !live) {
+    if (in && !(mask & 1u)) {
         if (!(acc & GS_ACC_OPACITY)) a.dL_dopacity[src] = 0.f;
         if (!(acc & GS_ACC_MEANS3D))
 #pragma unroll
@@ -447,31 +472,32 @@ __global__ __launch_bounds__(kGB) void k_gauss_live(GaussBwdArgs a) {
             }
         }
     }
-    // the Gaussian-indexed 3-float outputs of the block's dead Gaussians, coalesced over the block's
+    // each view's Gaussian-indexed 3-float outputs of its dead Gaussians, coalesced over the block's
     // region (one 4-B store per lane and element instead of three strided stores per Gaussian: PMC
     // write traffic of this kernel 60 -> ~15 MB at c2)
     __syncthreads();  // s_live
-    {
-        float* z3[3] = {a.dL_dconic, !(acc & GS_ACC_MEANS2D) ? a.dL_dmeans2D : nullptr,
-                        !(acc & GS_ACC_COLORS) ? a.dL_dcolors : nullptr};
+    for (int v = 0; v < m.n; ++v) {
+        const GaussBwdArgs& b = m.v[v];
+        float* z3[3] = {b.dL_dconic, !(b.acc & GS_ACC_MEANS2D) ? b.dL_dmeans2D : nullptr,
+                        !(b.acc & GS_ACC_COLORS) ? b.dL_dcolors : nullptr};
 #pragma unroll
         for (int t = 0; t < 3; ++t) {
             float* g = z3[t];
             if (!g) continue;
             g += 3 * (size_t)idx0;
             for (int e = threadIdx.x; e < 3 * nrow; e += kGB)
-                if (!s_live[e / 3]) g[e] = 0.f;
+                if (!((s_live[e / 3] >> v) & 1u)) g[e] = 0.f;
         }
     }
     if (a.dsh.dc && !(acc & GS_ACC_SH) && a.M > 1 && !a.index) {
-        // rest rows of the block's dead Gaussians, coalesced over the block's region
+        // rest rows of the block's Gaussians dead in view 0, coalesced over the block's region
         const int ncol = (a.M - 1) * 3;
         const int stride = a.dsh.rest_stride;
         float* g = a.dsh.rest + (size_t)idx0 * stride;
         const int total_f = (nrow - 1) * stride + ncol;
         for (int e = threadIdx.x; e < total_f; e += kGB) {
             const int row = e / stride, col = e - row * stride;
-            if (col < ncol && !s_live[row]) g[e] = 0.f;
+            if (col < ncol && !(s_live[row] & 1u)) g[e] = 0.f;
         }
     }
 }
@@ -480,18 +506,151 @@ __global__ __launch_bounds__(kGB) void k_gauss_live(GaussBwdArgs a) {
 // Pass 2: the live Gaussians of `group` consecutive pass-1 blocks (group =
 // ceil(blocks / 512), at most 8: about 512 workgroups whatever P is, so a small
 // or densely visible scene is not funnelled through a few workgroups), one per
-// thread, in batches of 256.  Their rows are scattered, so the SH rows move
-// through LDS with a flat block-wide index (consecutive lanes touch
+// thread, in batches of 256; per batch, each view in turn (a Gaussian's threads
+// idle through the views it is dead in).  Their rows are scattered, so the SH
+// rows move through LDS with a flat block-wide index (consecutive lanes touch
 // consecutive floats of one or two rows) instead of one 180-B row per lane,
 // and every read-modify-write batch issues its loads before its stores.
 // ---------------------------------------------------------------------
 constexpr int kLiveGroup = 8;    // most pass-1 blocks per workgroup
 constexpr int kLiveGrid = 512;   // target workgroups (2 per CU at 190 VGPRs)
+constexpr uint32_t kNoRow = 0xFFFFFFFFu;
 
-__global__ __launch_bounds__(kGB) void k_gauss_bwd_live(GaussBwdArgs a) {
+// One view's work on one batch of live Gaussians (every thread of the block calls it: it has
+// barriers).  ok: this thread's Gaussian is live in the view; src: its parameter row.
+__device__ __forceinline__ void bwd_view_batch(const GaussBwdArgs& a, bool ok, int idx, int src, int nrow, int ncol,
+                                               float inv_ncol, float* s_sh, uint32_t* s_gid, uint64_t* st) {
+    float* const my_sh = s_sh + threadIdx.x * kShPitch;
+    const bool ash = a.acc & GS_ACC_SH;
+    s_gid[threadIdx.x] = ok ? (uint32_t)src : kNoRow;  // (SH rows are parameter rows)
+    // independent loads first: parameters (a later view's from L2), slot range, the first 8 record flags
+    GaussIn gin{};
+    if (ok) gin = load_gauss_in(a, idx, src);
+    uint32_t n = ok ? a.tiles_touched[idx] : 0u;
+    const uint32_t first = ok ? a.first_slot[idx] : 0u;  // (a live Gaussian has slots)
+    // (a speculative forward that overflowed its capacity is re-rendered; its slots stop at the capacity)
+    n = first < a.slot_cap ? min(n, a.slot_cap - first) : 0u;
+    const uint32_t* flags = reinterpret_cast<const uint32_t*>(a.rec_flags);
+    uint32_t fl[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) fl[u] = (uint32_t)u < n ? flags[first + u] : 0u;
+    __syncthreads();  // s_gid
+    if (st) st[1] = __builtin_amdgcn_s_memrealtime();
+    const int total = nrow * ncol;
+    constexpr int kV = 12;
+    if (a.sh.dc && ncol > 0) {
+        for (int b = 0; b < total; b += kV * kGB) {
+            float v[kV];
+#pragma unroll
+            for (int u = 0; u < kV; ++u) {
+                const int e = b + u * kGB + (int)threadIdx.x;
+                const int row = (int)(((float)e + 0.5f) * inv_ncol), col = e - row * ncol;
+                const uint32_t gid = e < total ? s_gid[row] : kNoRow;
+                const size_t off = (size_t)gid * a.sh.rest_stride + col;
+                v[u] = gid == kNoRow ? 0.f
+                       : a.sh.half ? __half2float(reinterpret_cast<const __half*>(a.sh.rest)[off])
+                                   : a.sh.rest[off];
+            }
+#pragma unroll
+            for (int u = 0; u < kV; ++u) {
+                const int e = b + u * kGB + (int)threadIdx.x;
+                const int row = (int)(((float)e + 0.5f) * inv_ncol), col = e - row * ncol;
+                if (e < total) s_sh[row * kShPitch + col] = v[u];
+            }
+        }
+    }
+    // sum of this Gaussian's records: one per (slot, quadrant) the backward
+    // replay kept, flagged per slot; slots in emission order = tile order,
+    // quadrants in order within a slot.  The flagged records are taken four at
+    // a time from a bit mask (bit 4u + quadrant), all twelve loads of a batch
+    // issued before its sums: one memory round trip per four records instead
+    // of one per record (a batch's unused places re-read its first record and
+    // add nothing; acc is never -0, so the skipped +0 changes no bit).
+    float acc[9];
+#pragma unroll
+    for (int f = 0; f < 9; ++f) acc[f] = 0.f;
+    for (uint32_t k0 = 0; k0 < n; k0 += 8) {
+        if (k0) {
+#pragma unroll
+            for (int u = 0; u < 8; ++u) fl[u] = k0 + u < n ? flags[first + k0 + u] : 0u;
+        }
+        uint32_t m = 0;
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+#pragma unroll
+            for (int qd = 0; qd < 4; ++qd) m |= ((fl[u] >> (8 * qd)) & 0xFFu) ? 1u << (4 * u + qd) : 0u;
+        const float4* recs = a.records + 3 * (4 * (size_t)(first + k0));
+        while (m) {
+            int bi[4];
+            bool use[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                use[i] = m != 0u;
+                bi[i] = use[i] ? __builtin_ctz(m) : bi[0];
+                m &= m - 1u;
+            }
+            float4 r[4][3];
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int c = 0; c < 3; ++c) r[i][c] = recs[3 * bi[i] + c];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                if (use[i]) {
+                    acc[0] += r[i][0].x; acc[1] += r[i][0].y; acc[2] += r[i][0].z; acc[3] += r[i][0].w;
+                    acc[4] += r[i][1].x; acc[5] += r[i][1].y; acc[6] += r[i][1].z; acc[7] += r[i][1].w;
+                    acc[8] += r[i][2].x;
+                }
+            }
+        }
+    }
+    if (st) st[2] = __builtin_amdgcn_s_memrealtime();
+    __syncthreads();  // SH staged
+    if (st) st[3] = __builtin_amdgcn_s_memrealtime();
+
+    float ddc[3] = {0.f, 0.f, 0.f};
+    float dop = acc[5];  // w.r.t. opacity; chained through the sigmoid when activation = 1
+    GaussOut o;
+    if (ok) {
+        const float gm = a.grad_mask ? (a.grad_mask[src] ? 1.f : 0.f) : 1.f;
+        // (each thread reads and then overwrites only its own LDS row: no barrier in between)
+        gauss_bwd_visible(a, gin, acc, dop, my_sh, ncol, (a.mask_bits & GS_ACC_SH) ? gm : 1.f, ddc, o);
+        if (a.grad_mask) apply_grad_mask(a, gm, acc, dop, o);
+    }
+    if (st) st[4] = __builtin_amdgcn_s_memrealtime();
+    if (ok) commit_outputs(a, idx, src, acc, dop, ddc, o);
+    if (st) st[5] = __builtin_amdgcn_s_memrealtime();
+    // dL_dsh rest rows: through LDS (in place), flat block-wide batches, loads before stores
+    if (a.dsh.dc && ncol > 0) {
+        __syncthreads();
+        for (int b = 0; b < total; b += kV * kGB) {
+            float old[kV];
+#pragma unroll
+            for (int u = 0; u < kV; ++u) {
+                const int e = b + u * kGB + (int)threadIdx.x;
+                const int row = (int)(((float)e + 0.5f) * inv_ncol), col = e - row * ncol;
+                const uint32_t gid = e < total ? s_gid[row] : kNoRow;
+                old[u] = ash && gid != kNoRow ? a.dsh.rest[(size_t)gid * a.dsh.rest_stride + col] : 0.f;
+            }
+#pragma unroll
+            for (int u = 0; u < kV; ++u) {
+                const int e = b + u * kGB + (int)threadIdx.x;
+                const int row = (int)(((float)e + 0.5f) * inv_ncol), col = e - row * ncol;
+                const uint32_t gid = e < total ? s_gid[row] : kNoRow;
+                if (gid != kNoRow) a.dsh.rest[(size_t)gid * a.dsh.rest_stride + col] = old[u] + s_sh[row * kShPitch + col];
+            }
+        }
+    }
+    __syncthreads();  // s_gid / s_sh reused by the next view or batch
+}
+
+__global__ __launch_bounds__(kGB) void k_gauss_bwd_live(GaussBwdViews m) {
+    const GaussBwdArgs& a = m.v[0];
     __shared__ float s_sh[kGB * kShPitch];
     __shared__ uint32_t s_gid[kGB];
     __shared__ uint32_t s_pre[kLiveGroup + 1];
+    __shared__ uint32_t s_vlist[kGB];  // the batch's Gaussians live in the view being processed, compacted
+    __shared__ uint32_t s_wave[kGB / 64];
     const int nsrc = (a.P + kGB - 1) / kGB;
     const int group = (nsrc + kLiveGrid - 1) / kLiveGrid < kLiveGroup ? (nsrc + kLiveGrid - 1) / kLiveGrid : kLiveGroup;
     const int sb0 = blockIdx.x * group;
@@ -506,140 +665,42 @@ __global__ __launch_bounds__(kGB) void k_gauss_bwd_live(GaussBwdArgs a) {
     __syncthreads();
     const uint32_t count = s_pre[kLiveGroup];
     // (diagnostics) per wave, s_memrealtime at: start, the ids/params barrier, records summed, SH staged,
-    // chain computed, outputs committed; then the workgroup's live count and the end
+    // chain computed, outputs committed (view 0 of the first batch); then the workgroup's live count and the end
     uint64_t st[8] = {a.diag ? __builtin_amdgcn_s_memrealtime() : 0, 0, 0, 0, 0, 0, 0, 0};
     // rest floats staged per Gaussian: coefficients 1..15 (degree <= 3 never reads more)
     const int ncol = (a.M - 1) * 3 < kShPitch ? (a.M - 1) * 3 : kShPitch;
     const float inv_ncol = ncol > 0 ? 1.0f / (float)ncol : 0.f;
-    float* const my_sh = s_sh + threadIdx.x * kShPitch;
-    const bool ash = a.acc & GS_ACC_SH;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     for (uint32_t base = 0; base < count; base += kGB) {
         const uint32_t j = base + threadIdx.x;
-        const int nrow = count - base < (uint32_t)kGB ? (int)(count - base) : kGB;
-        const bool ok = j < count;
+        const bool in = j < count;
         int g = 0;
 #pragma unroll
         for (int q = 1; q < kLiveGroup; ++q) g += j >= s_pre[q] ? 1 : 0;
-        const int idx = ok ? (int)a.live_list[(size_t)(sb0 + g) * kGB + (j - s_pre[g])] : 0;
-        // independent loads first: parameters, slot range, the first 8 record flags
-        GaussIn gin{};
-        const int src = ok && a.index ? a.index[idx] : idx;  // parameter row
-        s_gid[threadIdx.x] = (uint32_t)src;  // (SH rows are parameter rows)
-        if (ok) gin = load_gauss_in(a, idx, src);
-        uint32_t n = ok ? a.tiles_touched[idx] : 0u;
-        const uint32_t first = ok ? a.first_slot[idx] : 0u;  // (a live Gaussian has slots)
-        // (a speculative forward that overflowed its capacity is re-rendered; its slots stop at the capacity)
-        n = first < a.slot_cap ? min(n, a.slot_cap - first) : 0u;
-        const uint32_t* flags = reinterpret_cast<const uint32_t*>(a.rec_flags);
-        uint32_t fl[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) fl[u] = (uint32_t)u < n ? flags[first + u] : 0u;
-        __syncthreads();  // s_gid
-        if (a.diag && base == 0) st[1] = __builtin_amdgcn_s_memrealtime();
-        const int total = nrow * ncol;
-        constexpr int kV = 12;
-        if (a.sh.dc && ncol > 0) {
-            for (int b = 0; b < total; b += kV * kGB) {
-                float v[kV];
-#pragma unroll
-                for (int u = 0; u < kV; ++u) {
-                    const int e = b + u * kGB + (int)threadIdx.x;
-                    const int row = (int)(((float)e + 0.5f) * inv_ncol), col = e - row * ncol;
-                    const size_t off = (size_t)s_gid[row] * a.sh.rest_stride + col;
-                    v[u] = e >= total ? 0.f
-                           : a.sh.half ? __half2float(reinterpret_cast<const __half*>(a.sh.rest)[off])
-                                       : a.sh.rest[off];
-                }
-#pragma unroll
-                for (int u = 0; u < kV; ++u) {
-                    const int e = b + u * kGB + (int)threadIdx.x;
-                    const int row = (int)(((float)e + 0.5f) * inv_ncol), col = e - row * ncol;
-                    if (e < total) s_sh[row * kShPitch + col] = v[u];
-                }
-            }
-        }
-        // sum of this Gaussian's records: one per (slot, quadrant) the backward
-        // replay kept, flagged per slot; slots in emission order = tile order,
-        // quadrants in order within a slot.  The flagged records are taken four at
-        // a time from a bit mask (bit 4u + quadrant), all twelve loads of a batch
-        // issued before its sums: one memory round trip per four records instead
-        // of one per record (a batch's unused places re-read its first record and
-        // add nothing; acc is never -0, so the skipped +0 changes no bit).
-        float acc[9];
-#pragma unroll
-        for (int f = 0; f < 9; ++f) acc[f] = 0.f;
-        for (uint32_t k0 = 0; k0 < n; k0 += 8) {
-            if (k0) {
-#pragma unroll
-                for (int u = 0; u < 8; ++u) fl[u] = k0 + u < n ? flags[first + k0 + u] : 0u;
-            }
-            uint32_t m = 0;
-#pragma unroll
-            for (int u = 0; u < 8; ++u)
-#pragma unroll
-                for (int qd = 0; qd < 4; ++qd) m |= ((fl[u] >> (8 * qd)) & 0xFFu) ? 1u << (4 * u + qd) : 0u;
-            const float4* recs = a.records + 3 * (4 * (size_t)(first + k0));
-            while (m) {
-                int bi[4];
-                bool use[4];
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    use[i] = m != 0u;
-                    bi[i] = use[i] ? __builtin_ctz(m) : bi[0];
-                    m &= m - 1u;
-                }
-                float4 r[4][3];
-#pragma unroll
-                for (int i = 0; i < 4; ++i)
-#pragma unroll
-                    for (int c = 0; c < 3; ++c) r[i][c] = recs[3 * bi[i] + c];
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    if (use[i]) {
-                        acc[0] += r[i][0].x; acc[1] += r[i][0].y; acc[2] += r[i][0].z; acc[3] += r[i][0].w;
-                        acc[4] += r[i][1].x; acc[5] += r[i][1].y; acc[6] += r[i][1].z; acc[7] += r[i][1].w;
-                        acc[8] += r[i][2].x;
-                    }
-                }
-            }
-        }
-        if (a.diag && base == 0) st[2] = __builtin_amdgcn_s_memrealtime();
-        __syncthreads();  // SH staged
-        if (a.diag && base == 0) st[3] = __builtin_amdgcn_s_memrealtime();
-
-        float ddc[3] = {0.f, 0.f, 0.f};
-        float dop = acc[5];  // w.r.t. opacity; chained through the sigmoid when activation = 1
-        GaussOut o;
-        if (ok) {
-            const float gm = a.grad_mask ? (a.grad_mask[src] ? 1.f : 0.f) : 1.f;
-            // (each thread reads and then overwrites only its own LDS row: no barrier in between)
-            gauss_bwd_visible(a, gin, acc, dop, my_sh, ncol, (a.mask_bits & GS_ACC_SH) ? gm : 1.f, ddc, o);
-            if (a.grad_mask) apply_grad_mask(a, gm, acc, dop, o);
-        }
-        if (a.diag && base == 0) st[4] = __builtin_amdgcn_s_memrealtime();
-        if (ok) commit_outputs(a, idx, src, acc, dop, ddc, o);
-        if (a.diag && base == 0) st[5] = __builtin_amdgcn_s_memrealtime();
-        // dL_dsh rest rows: through LDS (in place), flat block-wide batches, loads before stores
-        if (a.dsh.dc && ncol > 0) {
+        const uint32_t entry = in ? a.live_list[(size_t)(sb0 + g) * kGB + (j - s_pre[g])] : 0u;
+        // each view in turn over the batch's Gaussians live in it, compacted to the front of the block (the
+        // waves past them skip the view's work); a Gaussian's views in view order, one barrier apart
+#pragma unroll 1
+        for (int v = 0; v < m.n; ++v) {
+            const bool has = in && ((entry >> (28 + v)) & 1u);
+            const uint64_t bm = __ballot(has);
+            if (lane == 0) s_wave[wave] = (uint32_t)__popcll(bm);
             __syncthreads();
-            for (int b = 0; b < total; b += kV * kGB) {
-                float old[kV];
+            uint32_t off = 0, nv = 0;
 #pragma unroll
-                for (int u = 0; u < kV; ++u) {
-                    const int e = b + u * kGB + (int)threadIdx.x;
-                    const int row = (int)(((float)e + 0.5f) * inv_ncol), col = e - row * ncol;
-                    old[u] = ash && e < total ? a.dsh.rest[(size_t)s_gid[row] * a.dsh.rest_stride + col] : 0.f;
-                }
-#pragma unroll
-                for (int u = 0; u < kV; ++u) {
-                    const int e = b + u * kGB + (int)threadIdx.x;
-                    const int row = (int)(((float)e + 0.5f) * inv_ncol), col = e - row * ncol;
-                    if (e < total)
-                        a.dsh.rest[(size_t)s_gid[row] * a.dsh.rest_stride + col] = old[u] + s_sh[row * kShPitch + col];
-                }
+            for (int w = 0; w < kGB / 64; ++w) {
+                off += w < wave ? s_wave[w] : 0u;
+                nv += s_wave[w];
             }
+            if (has) s_vlist[off + (uint32_t)__popcll(bm & lanemask_lt())] = entry & kLiveIdMask;
+            __syncthreads();  // s_vlist (and s_wave, read by every thread, before its next write)
+            if (nv == 0) continue;
+            const bool ok = threadIdx.x < nv;
+            const int idx = ok ? (int)s_vlist[threadIdx.x] : 0;
+            const int src = ok && a.index ? a.index[idx] : idx;  // parameter row
+            bwd_view_batch(m.v[v], ok, idx, src, (int)nv, ncol, inv_ncol, s_sh, s_gid,
+                           a.diag && base == 0 && v == 0 ? st : nullptr);
         }
-        __syncthreads();  // s_gid / s_sh reused by the next batch
     }
     if (a.diag && (threadIdx.x & 63) == 0) {
         st[7] = __builtin_amdgcn_s_memrealtime();
@@ -650,14 +711,24 @@ __global__ __launch_bounds__(kGB) void k_gauss_bwd_live(GaussBwdArgs a) {
     }
 }
 
-void launch_gauss_backward(const GaussBwdArgs& a, hipStream_t s, hipEvent_t writes_after) {
-    if (a.P <= 0) return;
+void launch_gauss_backward_views(const GaussBwdArgs* views, int n, hipStream_t s, hipEvent_t writes_after) {
+    const GaussBwdArgs& a = views[0];
+    if (a.P <= 0 || n <= 0) return;
+    GaussBwdViews m;
+    m.n = n < kMaxBwdViews ? n : kMaxBwdViews;
+    for (int v = 0; v < m.n; ++v) m.v[v] = views[v];
     const int blocks = div_up(a.P, kGB);
-    hipLaunchKernelGGL(k_gauss_live, dim3(blocks), dim3(kGB), 0, s, a);
+    hipLaunchKernelGGL(k_gauss_live, dim3(blocks), dim3(kGB), 0, s, m);
     // k_gauss_live writes only overwritten (per-call) outputs; the accumulated ones start here
     if (writes_after) (void)hipStreamWaitEvent(s, writes_after, 0);
     const int group = std::min(div_up(blocks, kLiveGrid), kLiveGroup);  // (the kernel derives the same)
-    hipLaunchKernelGGL(k_gauss_bwd_live, dim3(div_up(blocks, group)), dim3(kGB), 0, s, a);
+    hipLaunchKernelGGL(k_gauss_bwd_live, dim3(div_up(blocks, group)), dim3(kGB), 0, s, m);
 }
+
+void launch_gauss_backward(const GaussBwdArgs& a, hipStream_t s, hipEvent_t writes_after) {
+    launch_gauss_backward_views(&a, 1, s, writes_after);
+}
+
+int gauss_backward_max_views() { return kMaxBwdViews; }
 
 }  // namespace gs

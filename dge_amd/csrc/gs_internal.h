@@ -415,6 +415,11 @@ struct GaussBwdArgs {
     uint64_t* diag;            // optional per-wave phase stamps of k_gauss_bwd_live (see diag_buffer)
 };
 void launch_gauss_backward(const GaussBwdArgs& a, hipStream_t s, hipEvent_t writes_after = nullptr);
+// n views' per-Gaussian passes as one (views[0] names the live-list scratch; the parameter-shaped
+// outputs are shared, GS_ACC_* set on them for every view but the first): at most
+// gauss_backward_max_views() views per call
+void launch_gauss_backward_views(const GaussBwdArgs* views, int n, hipStream_t s, hipEvent_t writes_after = nullptr);
+int gauss_backward_max_views();
 
 // diagnostics (gs_profile_diag_*): per-wave records of the blend kernels,
 // kDiagWords u64 each: start, end (s_memrealtime, 100 MHz), kept entries,

@@ -57,17 +57,31 @@ class GradBucket:
         for p, v in zip(self.params, self.views):
             p.grad = v
 
-    def zero(self, overlap: bool = False):
-        """Zero the bucket on the current stream.  overlap (GPU buckets): the in-kernel gradient writes of
-        later backward calls on OTHER streams wait for this fill (gs_grads.writes_after), not their whole
-        work — so a step that enqueues its forwards on side streams first and zeroes after them
-        (dge_amd.multiview.render_views, then zero, then backward) overlaps the 236-MB fill with the
-        forwards.  (No stream of its own: a fifth stream beside the three view streams and the default one
-        exceeds the 4 hardware queues and serialises unrelated work — measured 13% slower.)  For models on
-        the fused raw-parameter path, whose gradients go into .grad in-kernel; a backward that hands its
-        gradients to autograd's own accumulation must follow a plain zero()."""
-        self.flat.zero_()
+    def zero(self, overlap: bool = False, stream=None, after=None):
+        """Zero the bucket.  Default: on the current stream.  stream (GPU buckets): on that stream instead,
+        after the event `after` (record it on the bucket's last user's stream — e.g. the default stream
+        before the step's forwards are enqueued): the fused gradient writes of the next backward wait for
+        the fill (gs_grads.writes_after), nothing else does, so the fill runs beside the step's forwards
+        (dge_amd.multiview.render_views: pass one of the views' streams).  overlap: the round-2 form of the
+        same, the fill on the current stream (measured no faster; with render_views the current stream
+        already waits for the forwards).  For models on the fused raw-parameter path, whose gradients go
+        into .grad in-kernel; a backward that hands its gradients to autograd's own accumulation must
+        follow a plain zero()."""
         self._zero_event = None
+        if stream is not None and self.flat.is_cuda:
+            from . import diff_gaussian_rasterization as _r
+
+            dev = self.flat.device
+            with torch.cuda.stream(stream):
+                if after is not None:
+                    stream.wait_event(after)
+                self.flat.zero_()
+                self._zero_event = stream.record_event()
+            _r._SIDE_STREAMS = True
+            _r._GRAD_WRITES[dev.index] = (stream, self._zero_event)
+            self.attach()
+            return
+        self.flat.zero_()
         if overlap and self.flat.is_cuda:
             from . import diff_gaussian_rasterization as _r
 
