@@ -124,25 +124,16 @@ inline GeomLayout geom_layout(int P) {
 
 // Segment-parallel backward replay: for every segment k = [k*kSegLen,
 // (k+1)*kSegLen) of a tile list it blends, the forward stores per quadrant pixel
-// slot k = (T after the segment, S_k = the segment's own colour sum sum f alpha T,
-// a separate accumulator reset per segment) and, in a second array, C_k = the
-// colour composited up to the segment's end.  The backward replays each segment
-// of a quadrant window as its own work item, starting from T = slot k.T and the
-// colour composited behind the segment D = B / T, B = C_last - C_k (C_last: slot
-// nseg-1, the window's last segment: no pixel of the quadrant blends past it) —
-// two reads per item — where that difference keeps its precision (B >= C_last / 8
-// per channel: early segments, far from saturation, the ones with many later
-// segments), else B = S_{k+1} + ... + S_last (its rounding relative to B itself;
-// the window's tail has few later segments).  (Round 2 summed the S_j for every
-// item: O(segments^2) reads per quadrant, render_bwd's excess traffic; the plain
-// difference for every item broke the 1e-4 raster-sum bar near saturation.)
-// Checkpoint slots are allocated per
-// gradient.)  Checkpoint slots are allocated per
+// slot k = (T after the segment, S_k), S_k = the segment's own colour sum
+// sum f alpha T (a separate accumulator, reset per segment).  The backward
+// replays each segment of a quadrant window as its own work item, starting
+// from T = slot k.T and the colour composited behind the segment
+// D = (S_{k+1} + ... + S_last) / T: a sum of later segments' local sums, so its
+// rounding is relative to D itself (a difference of prefix sums,
+// (C_final - C_k) / T_k, would carry the whole prefix's rounding / T_k).  Checkpoint slots are allocated per
 // tile from its list: tile t owns slots [ckpt_base(t), ckpt_base(t) + ceil(len/kSegLen)),
 // ckpt_base(t) = range.x / kSegLen + t (monotone and non-overlapping because
-// ranges are a prefix sum), each slot 4 quadrants x kCkptPer float4: the 64
-// pixels' (T, S_k), then their (C_k, -).
-constexpr int kCkptPer = 128;
+// ranges are a prefix sum), each slot 4 quadrants x 64 pixels x float4.
 constexpr int kBlendRound = 256;  // list entries per blend round
 // Replay work items are listed by class of their blended-entry count, heaviest first (the hardware
 // dispatches workgroups in order: the longest items start first, the short ones fill the end);
@@ -212,7 +203,7 @@ inline BinLayout bin_layout(int K, int num_tiles) {
     L.sort_hist = o; o = align_up(o + 4 * ((size_t)1 << maxbits) * (size_t)L.sort_blocks);
     L.sort_totals = o; o = align_up(o + 4 * ((size_t)1 << maxbits));
     L.nslots = ckpt_slots(k, num_tiles);
-    L.ckpt = o; o = align_up(o + 16 * kCkptPer * 4 * L.nslots);  // [slot][quadrant][kCkptPer] float4
+    L.ckpt = o; o = align_up(o + 16 * 64 * 4 * L.nslots);  // [slot][quadrant][64] float4 (T, own colour sum)
     L.bwd_items = o; o = align_up(o + 8 * 4 * L.nslots * kItemClasses);  // uint2 (tile, seg << 2 | quadrant)
     L.used = o; o = align_up(o + 8 * used_words(k, num_tiles));
     L.tile_count = o; o = align_up(o + 4 * (size_t)num_tiles);  // two-level binning: instances per tile
@@ -341,7 +332,7 @@ struct RenderArgs {
     uint32_t* n_contrib;
     uint32_t* tile_last;
     uint32_t* quad_last;  // [tiles*4] max n_contrib per 8x8 quadrant
-    float4* ckpt;         // checkpoints for the segmented backward (see ckpt_base, kCkptPer)
+    float4* ckpt;         // (T, own colour sum) checkpoints for the segmented backward (see ckpt_base)
     uint64_t* used;       // per (quadrant, position) blended bits (see used_base)
     uint2* bwd_items;     // backward work list (4 * nslots) and its counters
     uint32_t* bwd_count;
@@ -371,7 +362,7 @@ struct RenderBwdArgs {
     const uint2* ranges;
     const uint2* point_pairs;  // per-tile lists: (Gaussian, binning slot)
     const uint32_t* quad_last;  // [tiles*4] the replay window of each quadrant wave
-    const float4* ckpt;         // the forward's checkpoints (see ckpt_base, kCkptPer)
+    const float4* ckpt;         // the forward's (T, own colour sum) checkpoints
     const uint64_t* used;       // the forward's blended bits: the backward's exact cull
     const uint2* bwd_items;     // the forward's work list (capacity item_cap)
     const uint32_t* bwd_count;  // [0] multi, [1] single items; [2], [3] the per-tile list's (k_bwd_tile_items)

@@ -268,11 +268,10 @@ __global__ __launch_bounds__(64, 3) void k_render_fwd(RenderArgs a) {
     load_ids(range.x + kRound, ids);
 
     // checkpoint of segment k of this quadrant: slot ckpt_base + k, quadrant `quad`: (T after it, its own
-    // colour sum), then 64 float4 further (one address, an immediate offset) the colour composited so far
-    float4* ckpt = a.ckpt + ((size_t)ckpt_base(range.x, tile) * 4 + quad) * kCkptPer + lane;
+    // colour sum)
+    float4* ckpt = a.ckpt + ((size_t)ckpt_base(range.x, tile) * 4 + quad) * 64 + lane;
     const auto put_ckpt = [&](int k) {
-        ckpt[(size_t)k * 4 * kCkptPer] = make_float4(fabsf(Ts), L01.x, L01.y, L2);
-        ckpt[(size_t)k * 4 * kCkptPer + 64] = make_float4(C01.x, C01.y, C2D.x, 0.f);
+        ckpt[(size_t)k * 256] = make_float4(fabsf(Ts), L01.x, L01.y, L2);
         L01 = f2v{0.f, 0.f};
         L2 = 0.f;
     };
@@ -762,26 +761,18 @@ __global__ __launch_bounds__(64, GS_BWD_WAVES) void k_render_bwd(RenderBwdArgs a
     float T = T_final, D0 = 0.f, D1 = 0.f, D2 = 0.f;
     if (limit < window) {
         // start inside the window: T after this segment (its checkpoint) and the colour composited
-        // behind position `limit`, D = B / T.  B = C_last - C_seg, the difference of the colour sums
-        // after the window's last segment (no pixel of the quadrant blends past it) and after this one:
-        // two reads whatever the segment's place in the window — used where it keeps its precision,
-        // B >= C_last / 8 in every channel (the prefixes' rounding, relative to C_last, is then at most
-        // 8x that relative to B).  Elsewhere (the window's tail, close to saturation: few later
-        // segments) B is the sum of the later segments' own colour sums, back to front.
-        const float4* ck = a.ckpt + ((size_t)ckpt_base(range.x, tile) * 4 + quad) * kCkptPer + lane;
-        const float4 cs = ck[(size_t)seg * 4 * kCkptPer];
-        const float4 ps = ck[(size_t)seg * 4 * kCkptPer + 64];
-        const float4 pl = ck[(size_t)(nseg_q - 1) * 4 * kCkptPer + 64];
-        T = cs.x;
-        float B0 = pl.x - ps.x, B1 = pl.y - ps.y, B2 = pl.z - ps.z;
-        if (!(B0 >= 0.125f * pl.x && B1 >= 0.125f * pl.y && B2 >= 0.125f * pl.z)) {
-            B0 = 0.f, B1 = 0.f, B2 = 0.f;
-            for (int k = nseg_q - 1; k > seg; --k) {
-                const float4 c = ck[(size_t)k * 4 * kCkptPer];
-                B0 += c.y;
-                B1 += c.z;
-                B2 += c.w;
-            }
+        // behind position `limit`, D = (S_{seg+1} + ... + S_last) / T from the later segments' own
+        // colour sums (summed back to front: the rounding stays relative to D itself; round 3 measured a
+        // prefix difference (C_last - C_seg) in its place for the early segments: +17 MB of checkpoint
+        // writes in the forward, no faster replay — these reads are a small part of its traffic)
+        const float4* ck = a.ckpt + ((size_t)ckpt_base(range.x, tile) * 4 + quad) * 64 + lane;
+        T = ck[(size_t)seg * 256].x;
+        float B0 = 0.f, B1 = 0.f, B2 = 0.f;
+        for (int k = nseg_q - 1; k > seg; --k) {
+            const float4 c = ck[(size_t)k * 256];
+            B0 += c.y;
+            B1 += c.z;
+            B2 += c.w;
         }
         const float inv = 1.0f / T;
         D0 = B0 * inv;
