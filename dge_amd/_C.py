@@ -290,11 +290,14 @@ def apply_weights(background, means3D, weights, opacity, scales, rotations, scal
 # fused path: raw GaussianModel parameters, activations and SH split in-kernel
 # (gs_rasterize_forward_ex / gs_rasterize_backward_ex)
 # ---------------------------------------------------------------------------
-def _params(P, xyz, f_dc, f_rest, colors, raw_opacity, raw_scaling, raw_rotation, index=None, visible=None):
+def _params(P, xyz, f_dc, f_rest, colors, raw_opacity, raw_scaling, raw_rotation, index=None, visible=None,
+            forward_only=False):
     """gs_params of the raw-parameter path; `index` (int32 [P], ascending): the localize subset's rows
-    (gathered in-kernel); fp16 features are read as such (sh_half)."""
+    (gathered in-kernel); fp16 features are read as such (sh_half); forward_only: no backward will follow
+    (the kernels skip the backward's scratch)."""
     g = N.GsParams()
     g.P = P
+    g.forward_only = 1 if forward_only else 0
     g.index = _ptr(index)
     g.sh_half = 1 if f_dc is not None and f_dc.dtype == torch.float16 else 0
     have_sh = f_dc is not None and f_dc.numel() != 0
@@ -346,7 +349,8 @@ class Prepared:
 
 def rasterize_gaussians_fused_begin(background, xyz, f_dc, f_rest, colors, raw_opacity, raw_scaling, raw_rotation,
                                     scale_modifier, viewmatrix, projmatrix, tan_fovx, tan_fovy, image_height,
-                                    image_width, degree, campos, prefiltered, debug, index=None, visible=None):
+                                    image_width, degree, campos, prefiltered, debug, index=None, visible=None,
+                                    forward_only=False):
     """First half of rasterize_gaussians_fused (gs_rasterize_forward_begin): enqueues the preprocess, the
     depth sort and the instance scan on the current stream without waiting; returns a Prepared for
     rasterize_gaussians_fused_end.  Rendering several views, begin them all first, then end each: the
@@ -364,7 +368,8 @@ def rasterize_gaussians_fused_begin(background, xyz, f_dc, f_rest, colors, raw_o
         raw_opacity, raw_scaling = _f32(raw_opacity, "opacity"), _f32(raw_scaling, "scaling")
         raw_rotation = _f32(raw_rotation, "rotation")
         radii = torch.empty((P,), dtype=torch.int32, device=dev)
-        g = _params(P, xyz, f_dc, f_rest, colors, raw_opacity, raw_scaling, raw_rotation, index, visible)
+        g = _params(P, xyz, f_dc, f_rest, colors, raw_opacity, raw_scaling, raw_rotation, index, visible,
+                    forward_only)
         s, keep = _settings(background, viewmatrix, projmatrix, campos, tan_fovx, tan_fovy, H, W, degree,
                             scale_modifier, prefiltered, debug)
         keep += [xyz, f_dc, f_rest, colors, raw_opacity, raw_scaling, raw_rotation, index, visible]

@@ -282,6 +282,7 @@ gs_params make_params(int P, int M, const float* means3D, const float* shs, cons
     g.sh_half = 0;
     g.index = nullptr;
     g.visible_out = nullptr;
+    g.forward_only = 0;
     return g;
 }
 
@@ -509,7 +510,8 @@ int bin_emit(FwdState& f, void* bin, uint32_t K_layout, const uint32_t* n_dev, h
     const ImgLayout il = img_layout(g.W, g.H);
     void* img = f.img;
     EmitArgs& ea = f.ea;
-    const BinLayout bl = bin_layout((int)K_layout, g.tiles);
+    const bool bwd = !f.gp.forward_only;
+    const BinLayout bl = bin_layout((int)K_layout, g.tiles, bwd);
     ea.cap = n_dev ? K_layout : 0xFFFFFFFFu;
     const TileSortPlan plan = tile_sort_plan(g.tiles);
     if (ea.xhist) {  // two-level binning (tile_sort_fused): column-ordered emission, row pass, ranges
@@ -518,7 +520,7 @@ int bin_emit(FwdState& f, void* bin, uint32_t K_layout, const uint32_t* n_dev, h
         ea.xtotals = at<uint32_t>(bin, bl.sort_totals);
         ea.tile_count = at<uint32_t>(bin, bl.tile_count);
         ea.ntiles = g.tiles;
-        ea.rec_flags32 = at<uint32_t>(bin, bl.rec_flags);
+        ea.rec_flags32 = bwd ? at<uint32_t>(bin, bl.rec_flags) : nullptr;
         { StageScope sc(ST_EMIT, stream); launch_emit_fused(ea, stream); }
         { StageScope sc(ST_TILE_SORT, stream);
         launch_row_pass(ea, K_layout, at<uint2>(bin, bl.point_pairs), at<uint32_t>(bin, bl.sort_hist), bl.sort_blocks,
@@ -528,7 +530,7 @@ int bin_emit(FwdState& f, void* bin, uint32_t K_layout, const uint32_t* n_dev, h
     }
     ea.tile_key = at<uint32_t>(bin, bl.key0);
     ea.slot_gauss = at<uint32_t>(bin, bl.slot_gauss);
-    ea.rec_flags32 = at<uint32_t>(bin, bl.rec_flags);
+    ea.rec_flags32 = bwd ? at<uint32_t>(bin, bl.rec_flags) : nullptr;
     { StageScope sc(ST_EMIT, stream); launch_scan_emit(ea, stream); }
     GS_LAUNCHED("emit");
 
@@ -586,7 +588,7 @@ int bin_end(FwdState& f, gs_alloc_fn alloc, void* ctx, hipStream_t stream, void*
     }
     *K_out = (int)K;
 
-    void* bin = alloc(ctx, which_bin, bin_layout((int)K, g.tiles).total);
+    void* bin = alloc(ctx, which_bin, bin_layout((int)K, g.tiles, !f.gp.forward_only).total);
     if (!bin) return set_error(GS_ERR_ALLOC, "allocator returned NULL for the binning buffer");
     *bin_out = bin;
     if (K == 0) return GS_OK;
@@ -600,10 +602,11 @@ int render_launch(FwdState& f, void* bin, uint32_t K_layout, int order_ready, fl
     const bool debug = f.s.debug != 0;
     const GeomLayout gl = geom_layout(f.gp.P);
     const ImgLayout il = img_layout(g.W, g.H);
-    const BinLayout bl = bin_layout((int)K_layout, g.tiles);
+    const BinLayout bl = bin_layout((int)K_layout, g.tiles, !f.gp.forward_only);
     void* geom = f.geom;
     void* img = f.img;
     RenderArgs ra;
+    ra.bwd = f.gp.forward_only ? 0 : 1;
     ra.W = g.W; ra.H = g.H; ra.gx = g.gx; ra.gy = g.gy;
     ra.ranges = at<uint2>(img, il.ranges);
     ra.tile_order = at<uint32_t>(img, il.tile_order);
@@ -1140,7 +1143,7 @@ int gs_views_forward(int n, const gs_settings* const* s, const gs_params* const*
                 h->spec[v] = 1;
                 h->layout[v] = cap;
                 off_bin[v] = total;
-                total = align_up(total + bin_layout((int)cap, f.g.tiles).total);
+                total = align_up(total + bin_layout((int)cap, f.g.tiles, !f.gp.forward_only).total);
             }
         }
         char* base = static_cast<char*>(alloc(alloc_ctx, 0, total));
@@ -1260,6 +1263,8 @@ int gs_views_backward(gs_views* h, const float* const* dL_dpix, const gs_grads* 
         hipStream_t join = (hipStream_t)join_;
         for (int v = 0; v < h->n; ++v) {
             FwdState& f = h->f[v];
+            if (f.gp.forward_only && f.gp.P > 0)
+                return set_error(GS_ERR_INVALID_ARG, "gs_views_backward: view %d was rendered forward_only", v);
             const int rc = validate_backward(&f.s, &f.gp, (int)h->layout[v], f.radii, f.geom, h->bin[v], f.img,
                                              dL_dpix[v], grads[v]);
             if (rc) return rc;
@@ -1365,7 +1370,8 @@ int gs_apply_weights(const gs_settings* s, int P, int M, const float* means3D, f
             return set_error(GS_ERR_UNSUPPORTED, "Unsupported number of channels: %d", num_channels);
         if (!alloc || !weights || !image_weights || !cnt)
             return set_error(GS_ERR_INVALID_ARG, "alloc, weights, image_weights and cnt are required");
-        const gs_params gp = make_params(P, M, means3D, shs, weights, opacities, scales, rotations, cov3D_precomp);
+        gs_params gp = make_params(P, M, means3D, shs, weights, opacities, scales, rotations, cov3D_precomp);
+        gp.forward_only = 1;  // (no blend, no backward: the binning only)
         int rc = validate_params(s, &gp);
         if (rc) return rc;
         if (P == 0) return GS_OK;
@@ -1378,7 +1384,7 @@ int gs_apply_weights(const gs_settings* s, int P, int M, const float* means3D, f
         if (K == 0) return GS_OK;
         const GeomLayout gl = geom_layout(P);
         const ImgLayout il = img_layout(g.W, g.H);
-        const BinLayout bl = bin_layout(K, g.tiles);
+        const BinLayout bl = bin_layout(K, g.tiles, false);
         ApplyWeightsArgs aw;
         aw.W = g.W; aw.H = g.H; aw.gx = g.gx; aw.gy = g.gy; aw.C = num_channels;
         aw.ranges = at<uint2>(img, il.ranges);

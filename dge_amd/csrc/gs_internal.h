@@ -185,7 +185,9 @@ struct BinLayout {
     int sort_blocks;
     size_t nslots;  // checkpoint slots = work-item capacity / 4
 };
-inline BinLayout bin_layout(int K, int num_tiles) {
+// bwd: with the backward's scratch (records, flags, checkpoints, work list, blended bits); a forward-only
+// binning (gs_params.forward_only) leaves them out (zero-sized, at the end)
+inline BinLayout bin_layout(int K, int num_tiles, bool bwd = true) {
     BinLayout L;
     size_t o = 0;
     size_t k = (size_t)(K > 0 ? K : 1);
@@ -198,15 +200,16 @@ inline BinLayout bin_layout(int K, int num_tiles) {
     L.pair1 = o; o = align_up(o + 8 * k);
     L.point_pairs = plan.passes & 1 ? L.pair1 : L.pair0;  // where tile_sort leaves (Gaussian, slot)
     L.slot_gauss = o; o = align_up(o + 4 * k);
-    L.records = o; o = align_up(o + 4 * 48 * k);  // one record per (slot, quadrant)
-    L.rec_flags = o; o = align_up(o + 4 * k);
     L.sort_hist = o; o = align_up(o + 4 * ((size_t)1 << maxbits) * (size_t)L.sort_blocks);
     L.sort_totals = o; o = align_up(o + 4 * ((size_t)1 << maxbits));
-    L.nslots = ckpt_slots(k, num_tiles);
+    L.tile_count = o; o = align_up(o + 4 * (size_t)num_tiles);  // two-level binning: instances per tile
+    const size_t kb = bwd ? k : 0;
+    L.nslots = bwd ? ckpt_slots(k, num_tiles) : 0;
+    L.records = o; o = align_up(o + 4 * 48 * kb);  // one record per (slot, quadrant)
+    L.rec_flags = o; o = align_up(o + 4 * kb);
     L.ckpt = o; o = align_up(o + 16 * 64 * 4 * L.nslots);  // [slot][quadrant][64] float4 (T, own colour sum)
     L.bwd_items = o; o = align_up(o + 8 * 4 * L.nslots * kItemClasses);  // uint2 (tile, seg << 2 | quadrant)
-    L.used = o; o = align_up(o + 8 * used_words(k, num_tiles));
-    L.tile_count = o; o = align_up(o + 4 * (size_t)num_tiles);  // two-level binning: instances per tile
+    L.used = o; o = align_up(o + (bwd ? 8 * used_words(k, num_tiles) : 0));
     L.total = o;
     return L;
 }
@@ -342,6 +345,7 @@ struct RenderArgs {
     uint8_t* touched;     // [P] set to 1 for every Gaussian some pixel blends (zeroed by the preprocess):
                           // exactly the Gaussians the backward gives a record, known after the forward
     uint64_t* diag;       // optional [tiles*4][kDiagWords] (see diag_buffer)
+    int bwd = 1;          // 0: a forward-only render (gs_params.forward_only): no backward bookkeeping
 };
 void launch_render_forward(const RenderArgs& a, hipStream_t s);
 

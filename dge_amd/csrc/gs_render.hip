@@ -132,6 +132,7 @@ __device__ __forceinline__ void pixel_alpha4(f4v x, f4v y, f4v cx, f4v ncy, f4v 
 // skipped entry adds (f * 0) * T = 0, a stopped or saturated one f a' * 0.
 // T, the sums and `last` are bit-identical to the oracle's.  Returns
 // w = a' Tw, > 0 exactly when the entry is blended (the caller's vote).
+template <bool SEG = true>
 __device__ __forceinline__ float blend_chain(float a, float4 fe, uint32_t pos, float& Ts, f2v& C01, f2v& C2D,
                                            f2v& L01, float& L2, uint32_t& last) {
 #pragma clang fp contract(off)
@@ -143,8 +144,10 @@ __device__ __forceinline__ float blend_chain(float a, float4 fe, uint32_t pos, f
     const f2v fa01 = f2v{fe.x, fe.y} * a2, fa2d = f2v{fe.z, fe.w} * a2;
     C01 = __builtin_elementwise_fma(fa01, T2, C01);
     C2D = __builtin_elementwise_fma(fa2d, T2, C2D);
-    L01 = __builtin_elementwise_fma(fa01, T2, L01);  // the segment's own colour sum (backward start)
-    L2 = __builtin_fmaf(fa2d.x, Tw, L2);
+    if constexpr (SEG) {
+        L01 = __builtin_elementwise_fma(fa01, T2, L01);  // the segment's own colour sum (backward start)
+        L2 = __builtin_fmaf(fa2d.x, Tw, L2);
+    }
     const float w = a * Tw;
     last = w > 0.0f ? pos : last;
     return w;
@@ -197,6 +200,9 @@ __device__ __forceinline__ void emit_items(const RenderArgs& a, int tile, int qu
         a.bwd_items[(size_t)c * a.item_cap + base + k] = make_uint2((uint32_t)tile, (k << 2) | (uint32_t)quad);
 }
 
+// BWD: the backward's bookkeeping (checkpoints, blended bits, touched bytes, the replay's work list);
+// a forward no backward follows (gs_params.forward_only) runs without it
+template <bool BWD>
 __global__ __launch_bounds__(64, 3) void k_render_fwd(RenderArgs a) {
     // XCD-aware: blocks b, b+8, b+16, b+24 (one XCD under the round-robin dealing) take the four
     // quadrants of one tile, so the tile's list and its Splat gathers are fetched into one L2;
@@ -271,9 +277,11 @@ __global__ __launch_bounds__(64, 3) void k_render_fwd(RenderArgs a) {
     // colour sum)
     float4* ckpt = a.ckpt + ((size_t)ckpt_base(range.x, tile) * 4 + quad) * 64 + lane;
     const auto put_ckpt = [&](int k) {
-        ckpt[(size_t)k * 256] = make_float4(fabsf(Ts), L01.x, L01.y, L2);
-        L01 = f2v{0.f, 0.f};
-        L2 = 0.f;
+        if constexpr (BWD) {
+            ckpt[(size_t)k * 256] = make_float4(fabsf(Ts), L01.x, L01.y, L2);
+            L01 = f2v{0.f, 0.f};
+            L2 = 0.f;
+        }
     };
     int seg_done = -1;  // last segment whose checkpoint is pending (the round just blended)
     uint64_t c_cull = 0;
@@ -283,7 +291,7 @@ __global__ __launch_bounds__(64, 3) void k_render_fwd(RenderArgs a) {
     uint64_t pend_word = 0;    // lane i < 4: word i of the previous round's blended bits
     int pend_rel = -1;         // that round's first list position (-1: none)
     auto store_words = [&]() {
-        if (pend_rel >= 0 && lane < kRound / 64 && pend_rel + 64 * lane < (int)(range.y - range.x))
+        if (BWD && pend_rel >= 0 && lane < kRound / 64 && pend_rel + 64 * lane < (int)(range.y - range.x))
             used[(size_t)(pend_rel / 64 + lane) * 4] = pend_word;  // (the list's own words only)
     };
     for (uint32_t b = range.x; b < range.y; b += kRound) {
@@ -363,8 +371,10 @@ __global__ __launch_bounds__(64, 3) void k_render_fwd(RenderArgs a) {
             n_mid = -1;
         };
         store_words();
-        s_gused[lane] = 0u;  // (groups past an early exit stay 0)
-        if (lane < kRoundLds / kGroup - 64) s_gused[64 + lane] = 0u;
+        if (BWD) {
+            s_gused[lane] = 0u;  // (groups past an early exit stay 0)
+            if (lane < kRoundLds / kGroup - 64) s_gused[64 + lane] = 0u;
+        }
         __syncthreads();
 
         const uint64_t c0 = a.diag ? __builtin_amdgcn_s_memtime() : 0;
@@ -398,11 +408,14 @@ __global__ __launch_bounds__(64, 3) void k_render_fwd(RenderArgs a) {
             uint64_t vm[kGroup];  // per entry: the lanes that blended it (uniform masks, SALU)
 #pragma unroll
             for (int u = 0; u < kGroup; ++u) {
-                const float w = blend_chain(ok[u] ? al[u] : 0.0f, c.rgbd[u], c.pos[u], Ts, C01, C2D, L01, L2, last);
-                vm[u] = __builtin_amdgcn_fcmpf(w, 0.0f, kFcmpOGT);
+                const float w = blend_chain<BWD>(ok[u] ? al[u] : 0.0f, c.rgbd[u], c.pos[u], Ts, C01, C2D, L01, L2,
+                                                 last);
+                if (BWD) vm[u] = __builtin_amdgcn_fcmpf(w, 0.0f, kFcmpOGT);
             }
-            const uint32_t gm = (vm[0] ? 1u : 0u) | (vm[1] ? 2u : 0u) | (vm[2] ? 4u : 0u) | (vm[3] ? 8u : 0u);
-            s_gused[j / kGroup] = __builtin_amdgcn_readfirstlane(gm);
+            if (BWD) {
+                const uint32_t gm = (vm[0] ? 1u : 0u) | (vm[1] ? 2u : 0u) | (vm[2] ? 4u : 0u) | (vm[3] ? 8u : 0u);
+                s_gused[j / kGroup] = __builtin_amdgcn_readfirstlane(gm);
+            }
         };
         AlphaOps ga, gb;
         ColourOps cc;
@@ -441,15 +454,17 @@ __global__ __launch_bounds__(64, 3) void k_render_fwd(RenderArgs a) {
         }
         if (a.diag) c_blend += __builtin_amdgcn_s_memtime() - c0;
         __syncthreads();
-        // the round's blended bits in list order, one ballot per word (words of rounds the wave
-        // never reaches stay unwritten: past every pixel's last contributor, outside every replay)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int sl = kslot[i];
-            const bool blended = sl >= 0 && ((s_gused[sl / kGroup] >> (sl % kGroup)) & 1u);
-            const uint64_t wd = __ballot(blended);
-            pend_word = lane == i ? wd : pend_word;
-            if (blended) a.touched[s_id[sl]] = 1;  // (same-value byte stores: no atomics needed)
+        if (BWD) {
+            // the round's blended bits in list order, one ballot per word (words of rounds the wave
+            // never reaches stay unwritten: past every pixel's last contributor, outside every replay)
+    #pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int sl = kslot[i];
+                const bool blended = sl >= 0 && ((s_gused[sl / kGroup] >> (sl % kGroup)) & 1u);
+                const uint64_t wd = __ballot(blended);
+                pend_word = lane == i ? wd : pend_word;
+                if (blended) a.touched[s_id[sl]] = 1;  // (same-value byte stores: no atomics needed)
+            }
         }
         pend_rel = (int)(b - range.x);
     }
@@ -472,7 +487,7 @@ __global__ __launch_bounds__(64, 3) void k_render_fwd(RenderArgs a) {
     const uint32_t m = wave_max_u32(inside ? last : 0u);
     // (item class from the entries the cull kept — the diagnostics' count, live anyway: a blended-entry
     // count here pushed the kernel into spilling)
-    if (m) emit_items(a, tile, quad, (m + kSegLen - 1) / kSegLen, diag_kept, lane);
+    if (BWD && m) emit_items(a, tile, quad, (m + kSegLen - 1) / kSegLen, diag_kept, lane);
     if (lane == 0) {
         a.quad_last[qidx] = m;
         if (m) atomicMax(&a.tile_last[tile], m);
@@ -494,7 +509,10 @@ void launch_render_forward(const RenderArgs& a, hipStream_t s) {
     const int tiles = a.gx * a.gy;
     if (tiles <= 0) return;
     if (!a.order_ready) hipLaunchKernelGGL(k_tile_order, dim3(1), dim3(1024), 0, s, a.ranges, tiles, a.tile_order);
-    hipLaunchKernelGGL(k_render_fwd, dim3(div_up(tiles, 8) * 32), dim3(64), 0, s, a);
+    if (a.bwd)
+        hipLaunchKernelGGL(k_render_fwd<true>, dim3(div_up(tiles, 8) * 32), dim3(64), 0, s, a);
+    else
+        hipLaunchKernelGGL(k_render_fwd<false>, dim3(div_up(tiles, 8) * 32), dim3(64), 0, s, a);
 }
 
 // =====================================================================

@@ -159,6 +159,13 @@ def _render_fused(viewpoint_camera, pc, pipe, bg_color, scaling_modifier=1.0, ov
     return _fused_end(_fused_begin(viewpoint_camera, pc, pipe, bg_color, scaling_modifier, override_color), pc)
 
 
+def _may_backward(*tensors) -> bool:
+    """Whether autograd can run a backward of a forward of these inputs (grad mode on and one of them
+    requires grad): else the kernels skip the backward's scratch (gs_params.forward_only).  The view-space
+    placeholder render() adds is a fresh leaf that requires grad, so it does not count."""
+    return torch.is_grad_enabled() and any(t is not None and t.requires_grad for t in tensors)
+
+
 def _fused_begin(viewpoint_camera, pc, pipe, bg_color, scaling_modifier=1.0, override_color=None):
     """The first half of _render_fused: settings, the visibility output and the native forward's first half
     (preprocess, depth sort, instance scan) enqueued on the current stream without a host wait."""
@@ -182,7 +189,8 @@ def _fused_begin(viewpoint_camera, pc, pipe, bg_color, scaling_modifier=1.0, ove
         rs.bg, xyz, empty if f_dc is None else f_dc, empty if f_rest is None else f_rest,
         empty if colors is None else colors, pc._opacity, pc._scaling, pc._rotation, rs.scale_modifier,
         rs.viewmatrix, rs.projmatrix, rs.tanfovx, rs.tanfovy, rs.image_height, rs.image_width, rs.sh_degree,
-        rs.campos, rs.prefiltered, rs.debug, index=index, visible=visible)
+        rs.campos, rs.prefiltered, rs.debug, index=index, visible=visible,
+        forward_only=not _may_backward(xyz, f_dc, f_rest, colors, pc._opacity, pc._scaling, pc._rotation))
     return st
 
 

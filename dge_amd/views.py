@@ -115,7 +115,7 @@ class _RasterizeViews(torch.autograd.Function):
             s, k = _fill_settings(rs, dev)
             keep += k
             g = _C._params(P, xyz, f_dc, f_rest, colors, raw_opacity, raw_scaling, raw_rotation, index,
-                           visible[v] if visible is not None else None)
+                           visible[v] if visible is not None else None, meta["forward_only"])
             ss.append(s)
             gs.append(g)
         s_arr = (ctypes.c_void_p * n)(*[ctypes.addressof(x) for x in ss])
@@ -281,8 +281,11 @@ def render_views_batched(cameras, pc, pipe, bg_color, streams, scaling_modifier=
         f_dc, f_rest, colors = None, None, _C._f32(override_color.float(), "colors")
     empty = torch.empty(0, dtype=torch.float32, device=dev)
     means2D = [_viewspace_zeros(n_pts, xyz.dtype, dev) for _ in range(n)]
+    from .gaussian_renderer import _may_backward
+
     meta = {"settings": settings, "streams": [streams[v % len(streams)] for v in range(n)], "speculate": speculate,
-            "index": None if index is None else _C._index32(index), "visible": visible}
+            "index": None if index is None else _C._index32(index), "visible": visible,
+            "forward_only": not _may_backward(xyz, f_dc, f_rest, colors, pc._opacity, pc._scaling, pc._rotation)}
     res = _RasterizeViews.apply(meta, _C._f32(xyz, "xyz"),
                                 empty if f_dc is None else _C._features(f_dc, "features_dc"),
                                 empty if f_rest is None else _C._features(f_rest, "features_rest"),

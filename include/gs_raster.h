@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define GS_RASTER_ABI_VERSION 10
+#define GS_RASTER_ABI_VERSION 11
 
 #define GS_OK 0
 #define GS_ERR_INVALID_ARG 1   /* AT_ERROR / std::runtime_error in the reference */
@@ -139,6 +139,11 @@ typedef struct gs_params {
                                      those rows only; means2D / colors / radii stay [P]. */
     uint8_t *visible_out;         /* forward only: NULL, or [P] bytes set to (radii > 0) — render()'s
                                      visibility_filter as a bool tensor, without a separate pass */
+    int forward_only;             /* forward only: 1 = no backward will follow (a render without autograd,
+                                     e.g. torch.no_grad): the binning and blend skip the backward's
+                                     scratch (gradient-record flags, checkpoints, blended bits, the
+                                     replay's work list, the touched bytes) and the binning buffer
+                                     leaves it out; a backward of such a forward is an error */
 } gs_params;
 
 /* gs_grads.accumulate bits: output i is ADDED to (out += grad) instead of

@@ -261,3 +261,35 @@ def test_render_views_speculated_overflow_is_reported(cuda_device):
     for o, r in zip(again, ref):
         for k in ("render", "radii", "depth_3dgs"):
             assert torch.equal(o[k], r[k]), k
+
+
+def test_forward_only_renders_equal_training_renders(cuda_device):
+    """Renders under no_grad (or of a scene without gradients) set gs_params.forward_only: the kernels skip
+    the backward's scratch (checkpoints, binning flags, per-Gaussian work lists) and the blend's backward
+    bookkeeping.  Image, depth, radii and the instance count equal the training render's, for render() and
+    the batched render_views."""
+    from dge_amd.cameras import orbit_camera
+    from dge_amd.gaussian_renderer import PipelineParams, render
+    from dge_amd.multiview import render_views
+    from dge_amd.scene import synthetic_scene
+
+    dev = torch.device("cuda")
+    W, H = 320, 256
+    cams = [orbit_camera(k, 3, W, H, device=dev) for k in range(3)]
+    bg = torch.tensor([0.1, 0.2, 0.3], device=dev)
+    sc = synthetic_scene(120_000, sh_degree=3, seed=6, device=dev).requires_grad_(True)
+    train = [render(c, sc, PipelineParams(), bg) for c in cams]
+    train_views = render_views(cams, sc, PipelineParams(), bg, streams=3)
+    with torch.no_grad():
+        fwd = [render(c, sc, PipelineParams(), bg) for c in cams]
+        fwd_views = render_views(cams, sc, PipelineParams(), bg, streams=3)
+        colors = torch.rand(sc.num_points(), 3, generator=torch.Generator().manual_seed(1)).to(dev)
+        sem = [render(c, sc, PipelineParams(), bg, override_color=colors) for c in cams]
+    sem_train = [render(c, sc, PipelineParams(), bg, override_color=colors.requires_grad_(True)) for c in cams]
+    assert fwd_views.check() and train_views.check()
+    torch.cuda.synchronize()
+    for pairs in ((train, fwd), (train_views, fwd_views), (train, fwd_views), (sem_train, sem)):
+        for a, b in zip(*pairs):
+            for k in ("render", "radii", "depth_3dgs"):
+                assert torch.equal(a[k].detach(), b[k]), k
+    assert train_views.batch.num_rendered == fwd_views.batch.num_rendered
