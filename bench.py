@@ -389,9 +389,9 @@ def run_views(args, cams, scene, pipe, bg, seeds, bucket, streams=None, min_worl
             bucket.zero()
         outs = render_views(cams, scene, pipe, bg, streams=streams, speculate=args.speculate)
         if side:
-            from dge_amd.multiview import stream_pool
+            from dge_amd.multiview import view_streams
 
-            bucket.zero(stream=stream_pool(main.device, streams)[0], after=ready)
+            bucket.zero(stream=view_streams(main.device, streams)[1], after=ready)
         if min_world is not None and not args.scan_live:
             bucket.allreduce_begin([o.get("_live_rows") for o in outs], min_world=min_world)
         torch.autograd.backward([o["render"] for o in outs], seeds)

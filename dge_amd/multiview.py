@@ -272,6 +272,17 @@ def stream_pool(device, n: int):
     return pool
 
 
+def view_streams(device, n: int):
+    """The streams a batch of views runs on: the caller's current stream first (the first view, and the
+    batch's merged per-Gaussian pass, need no cross-stream hop to or from the caller), then n - 1 pool
+    streams.  (Three pool streams instead, the caller joining and forking around them: 2390 against 2500
+    renders/s at c2, profiles/r03/bench_caller_first.txt.)"""
+    main = torch.cuda.current_stream(device)
+    if n <= 1:
+        return [main]
+    return [main] + stream_pool(device, n - 1)
+
+
 def render_views(cameras, pc, pipe, bg_color, streams: int = 2, speculate: bool = False, **kw):
     """render() of every camera, the views spread round-robin over `streams` HIP streams.
 
@@ -293,7 +304,8 @@ def render_views(cameras, pc, pipe, bg_color, streams: int = 2, speculate: bool 
     main = torch.cuda.current_stream(dev)
     pool = stream_pool(dev, streams) if streams > 1 else [main]
     if _fused_ok(pc, pipe) and 1 <= len(cameras) <= _native_max_views():
-        return render_views_batched(cameras, pc, pipe, bg_color, pool, speculate=speculate, **kw)
+        return render_views_batched(cameras, pc, pipe, bg_color, view_streams(dev, streams), speculate=speculate,
+                                    **kw)
     outs = RenderedViews()
     if len(pool) == 1:
         outs.extend(render(c, pc, pipe, bg_color, **kw) for c in cameras)
