@@ -35,6 +35,18 @@
 
 using namespace gs;
 
+#ifdef GS_ABLATE
+// (probe builds only, never the shipped library: DGE_AMD_ABLATE=a,b,... skips those stages, to measure
+// each stage's marginal cost inside the concurrent multi-view step; outputs are then meaningless)
+#include <cstring>
+static bool ablate(const char* what) {
+    const char* e = getenv("DGE_AMD_ABLATE");
+    return e && strstr(e, what);
+}
+#define GS_SKIP(what) if (!ablate(what))
+#else
+#define GS_SKIP(what)
+#endif
 namespace {
 
 thread_local std::string g_last_error;
@@ -400,8 +412,8 @@ int bin_after_preprocess(FwdState& f, hipStream_t stream) {
     GS_HIP(hipEventRecord(f.st->ev, stream));
 
     // depth order of the Gaussians (stable: ties keep index order)
-    int cur;
-    { StageScope sc(ST_DEPTH_SORT, stream);
+    int cur = 0;
+    GS_SKIP("depth") { StageScope sc(ST_DEPTH_SORT, stream);
     cur = radix_sort_aux(at<uint32_t>(geom, gl.key0), at<uint32_t>(geom, gl.key1), at<uint2>(geom, gl.val0),
                          at<uint2>(geom, gl.val1), pa.rect, (uint32_t)P, depth_sort_bits(), depth_pass_bits(),
                          kDepthSortIPT, at<uint32_t>(geom, gl.sort_hist), at<uint32_t>(geom, gl.sort_totals),
@@ -627,7 +639,7 @@ int render_launch(FwdState& f, void* bin, uint32_t K_layout, int order_ready, fl
     ra.out_depth = out_depth;
     ra.touched = at<uint8_t>(geom, gl.touched);
     ra.diag = diag_buffer(0, kDiagWords * (size_t)g.tiles * 4);
-    { StageScope sc(ST_RENDER_FWD, stream); launch_render_forward(ra, stream); }
+    GS_SKIP("fwd") { StageScope sc(ST_RENDER_FWD, stream); launch_render_forward(ra, stream); }
     GS_LAUNCHED("render");
     return GS_OK;
 }
@@ -680,7 +692,7 @@ int replay_view(const gs_settings* s, const gs_params* gp, int R, const void* ge
     rb.records = at<float4>(const_cast<void*>(binning), bl.records);
     rb.rec_flags = at<uint8_t>(const_cast<void*>(binning), bl.rec_flags);
     rb.diag = diag_buffer(1, kDiagWords * 4 * bl.nslots);
-    { StageScope sc(ST_RENDER_BWD, stream); launch_render_backward(rb, stream); }
+    GS_SKIP("rbwd") { StageScope sc(ST_RENDER_BWD, stream); launch_render_backward(rb, stream); }
     GS_LAUNCHED("render backward");
     return GS_OK;
 }
@@ -1159,7 +1171,7 @@ int gs_views_forward(int n, const gs_settings* const* s, const gs_params* const*
             const bool debug = f.s.debug != 0;
             rc = bin_prepare_in(f, 1, base + off_geom[v], base + off_img[v], stream);
             if (rc) return rc;
-            { StageScope sc(ST_PREPROCESS, stream); launch_preprocess(f.pa, stream); }
+            GS_SKIP("pre") { StageScope sc(ST_PREPROCESS, stream); launch_preprocess(f.pa, stream); }
             GS_LAUNCHED("preprocess");
             rc = bin_after_preprocess(f, stream);
             if (rc) return rc;
@@ -1297,7 +1309,7 @@ int gs_views_backward(gs_views* h, const float* const* dL_dpix, const gs_grads* 
                     ga[v] = gauss_args(&f.s, &f.gp, (int)h->layout[v0 + v], f.radii, f.geom, h->bin[v0 + v],
                                        grads[v0 + v], h->spec[v0 + v] ? h->layout[v0 + v] : 0xFFFFFFFFu);
                 }
-                { StageScope sc(ST_GAUSS_BWD, s0);
+                GS_SKIP("gauss") { StageScope sc(ST_GAUSS_BWD, s0);
                 launch_gauss_backward_views(ga, nv, s0, v0 == 0 ? (hipEvent_t)writes_after : nullptr); }
                 GS_LAUNCHED("gaussian backward (views)");
             }

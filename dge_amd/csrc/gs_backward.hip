@@ -513,7 +513,7 @@ __global__ __launch_bounds__(kGB) void k_gauss_live(GaussBwdViews m) {
 // and every read-modify-write batch issues its loads before its stores.
 // ---------------------------------------------------------------------
 constexpr int kLiveGroup = 8;    // most pass-1 blocks per workgroup
-constexpr int kLiveGrid = 512;   // target workgroups (2 per CU at 190 VGPRs)
+constexpr int kLiveGrid = 768;   // target workgroups (3 per CU: 166 VGPRs, 48 KB of LDS each)
 constexpr uint32_t kNoRow = 0xFFFFFFFFu;
 
 // One view's work on one batch of live Gaussians (every thread of the block calls it: it has
@@ -538,7 +538,21 @@ __device__ __forceinline__ void bwd_view_batch(const GaussBwdArgs& a, bool ok, i
     if (st) st[1] = __builtin_amdgcn_s_memrealtime();
     const int total = nrow * ncol;
     constexpr int kV = 12;
-    if (a.sh.dc && ncol > 0) {
+    if (a.sh.dc && ncol > 0 && !a.sh.half && ncol == kShPitch) {
+        // fp32 rows of the full pitch: the LDS image is the flat index itself, so each wave-instruction's
+        // 64 floats land contiguously — direct global->LDS loads (no registers, all in flight at once;
+        // the barrier below waits for them)
+        const uint32_t wave_base = __builtin_amdgcn_readfirstlane(threadIdx.x & ~63u);
+        for (int b = 0; b < total; b += kGB) {
+            const int e = b + (int)threadIdx.x;
+            if (e < total) {
+                const int row = (int)(((float)e + 0.5f) * inv_ncol), col = e - row * ncol;
+                const float* src = a.sh.rest + (size_t)s_gid[row] * a.sh.rest_stride + col;
+                __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)src,
+                                                 (__attribute__((address_space(3))) void*)(s_sh + b + wave_base), 4, 0, 0);
+            }
+        }
+    } else if (a.sh.dc && ncol > 0) {
         for (int b = 0; b < total; b += kV * kGB) {
             float v[kV];
 #pragma unroll
@@ -649,7 +663,7 @@ __global__ __launch_bounds__(kGB) void k_gauss_bwd_live(GaussBwdViews m) {
     __shared__ float s_sh[kGB * kShPitch];
     __shared__ uint32_t s_gid[kGB];
     __shared__ uint32_t s_pre[kLiveGroup + 1];
-    __shared__ uint32_t s_vlist[kGB];  // the batch's Gaussians live in the view being processed, compacted
+    __shared__ uint32_t s_vlist[2 * kGB];  // Gaussians live in the view being processed, compacted (+ a chunk's overflow)
     __shared__ uint32_t s_wave[kGB / 64];
     const int nsrc = (a.P + kGB - 1) / kGB;
     const int group = (nsrc + kLiveGrid - 1) / kLiveGrid < kLiveGroup ? (nsrc + kLiveGrid - 1) / kLiveGrid : kLiveGroup;
@@ -671,17 +685,21 @@ __global__ __launch_bounds__(kGB) void k_gauss_bwd_live(GaussBwdViews m) {
     const int ncol = (a.M - 1) * 3 < kShPitch ? (a.M - 1) * 3 : kShPitch;
     const float inv_ncol = ncol > 0 ? 1.0f / (float)ncol : 0.f;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    for (uint32_t base = 0; base < count; base += kGB) {
-        const uint32_t j = base + threadIdx.x;
-        const bool in = j < count;
-        int g = 0;
-#pragma unroll
-        for (int q = 1; q < kLiveGroup; ++q) g += j >= s_pre[q] ? 1 : 0;
-        const uint32_t entry = in ? a.live_list[(size_t)(sb0 + g) * kGB + (j - s_pre[g])] : 0u;
-        // each view in turn over the batch's Gaussians live in it, compacted to the front of the block (the
-        // waves past them skip the view's work); a Gaussian's views in view order, one barrier apart
+    // view-major: for each view in turn, the workgroup's Gaussians live in it, compacted into batches of
+    // up to 256 (a Gaussian's views one after another, in view order).  Most live Gaussians are live in
+    // one view only, so a batch per (union batch, view) would run mostly idle threads through the pass's
+    // latency-bound phases once per view; this runs each view's Gaussians of the whole workgroup together.
+    bool first = true;
 #pragma unroll 1
-        for (int v = 0; v < m.n; ++v) {
+    for (int v = 0; v < m.n; ++v) {
+        uint32_t filled = 0;  // compacted entries pending in s_vlist (< kGB between batches)
+        for (uint32_t base = 0; base < count; base += kGB) {
+            const uint32_t j = base + threadIdx.x;
+            const bool in = j < count;
+            int g = 0;
+#pragma unroll
+            for (int q = 1; q < kLiveGroup; ++q) g += j >= s_pre[q] ? 1 : 0;
+            const uint32_t entry = in ? a.live_list[(size_t)(sb0 + g) * kGB + (j - s_pre[g])] : 0u;
             const bool has = in && ((entry >> (28 + v)) & 1u);
             const uint64_t bm = __ballot(has);
             if (lane == 0) s_wave[wave] = (uint32_t)__popcll(bm);
@@ -692,14 +710,24 @@ __global__ __launch_bounds__(kGB) void k_gauss_bwd_live(GaussBwdViews m) {
                 off += w < wave ? s_wave[w] : 0u;
                 nv += s_wave[w];
             }
-            if (has) s_vlist[off + (uint32_t)__popcll(bm & lanemask_lt())] = entry & kLiveIdMask;
+            if (has) s_vlist[filled + off + (uint32_t)__popcll(bm & lanemask_lt())] = entry & kLiveIdMask;
+            filled += nv;
             __syncthreads();  // s_vlist (and s_wave, read by every thread, before its next write)
-            if (nv == 0) continue;
-            const bool ok = threadIdx.x < nv;
-            const int idx = ok ? (int)s_vlist[threadIdx.x] : 0;
-            const int src = ok && a.index ? a.index[idx] : idx;  // parameter row
-            bwd_view_batch(m.v[v], ok, idx, src, (int)nv, ncol, inv_ncol, s_sh, s_gid,
-                           a.diag && base == 0 && v == 0 ? st : nullptr);
+            if (filled < (uint32_t)kGB && base + kGB < count) continue;  // (fill the batch further)
+            while (filled > 0) {
+                const uint32_t nb = filled < (uint32_t)kGB ? filled : (uint32_t)kGB;
+                const bool ok = threadIdx.x < nb;
+                const int idx = ok ? (int)s_vlist[threadIdx.x] : 0;
+                const int src = ok && a.index ? a.index[idx] : idx;  // parameter row
+                bwd_view_batch(m.v[v], ok, idx, src, (int)nb, ncol, inv_ncol, s_sh, s_gid, a.diag && first ? st : nullptr);
+                first = false;
+                // (bwd_view_batch ends on a barrier: every thread has read its entry) the rest to the front
+                const uint32_t rest = filled - nb;
+                if (threadIdx.x < rest) s_vlist[threadIdx.x] = s_vlist[kGB + threadIdx.x];
+                __syncthreads();
+                filled = rest;
+                if (base + kGB < count) break;  // (a partial batch waits for the next chunk)
+            }
         }
     }
     if (a.diag && (threadIdx.x & 63) == 0) {

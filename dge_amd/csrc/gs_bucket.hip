@@ -120,57 +120,66 @@ __global__ __launch_bounds__(256) void k_rows_move(RowsLaunch a, const long long
 }
 
 // rows = ascending indices r with live[r] != 0, count = their number, without a host round trip
-// (torch.nonzero reads the count back): per-1024-row block counts, then each block adds up the
-// counts before it (at most ~1k words from L2, as the emission does) and writes its rows in order.
-constexpr int kCompactRows = 1024;  // rows per workgroup (4 per thread)
+// (torch.nonzero reads the count back): per-block counts, then each block adds up the counts before
+// it and writes its rows in order.  At most kCompactMaxBlocks blocks (each takes `chunks` runs of 1024
+// rows), so that prefix stays at most ~1k words from L2 per block whatever n is.
+constexpr int kCompactRows = 1024;        // rows per chunk (4 per thread)
+constexpr int kCompactMaxBlocks = 1024;
 
-__global__ __launch_bounds__(256) void k_compact_count(const uint8_t* __restrict__ live, long long n,
+__global__ __launch_bounds__(256) void k_compact_count(const uint8_t* __restrict__ live, long long n, int chunks,
                                                        long long* __restrict__ sums) {
     __shared__ uint32_t part[4];
-    const long long r0 = (long long)blockIdx.x * kCompactRows + 4 * threadIdx.x;
     uint32_t c = 0;
+    for (int k = 0; k < chunks; ++k) {
+        const long long r0 = ((long long)blockIdx.x * chunks + k) * kCompactRows + 4 * threadIdx.x;
 #pragma unroll
-    for (int u = 0; u < 4; ++u) c += (r0 + u < n && live[r0 + u]) ? 1u : 0u;
+        for (int u = 0; u < 4; ++u) c += (r0 + u < n && live[r0 + u]) ? 1u : 0u;
+    }
     c = __reduce_add_sync(~0ull, c);
     if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = c;
     __syncthreads();
     if (threadIdx.x == 0) sums[blockIdx.x] = part[0] + part[1] + part[2] + part[3];
 }
 
-__global__ __launch_bounds__(256) void k_compact_write(const uint8_t* __restrict__ live, long long n,
+__global__ __launch_bounds__(256) void k_compact_write(const uint8_t* __restrict__ live, long long n, int chunks,
                                                        const long long* __restrict__ sums, long long* __restrict__ rows,
                                                        long long* __restrict__ count) {
     __shared__ long long s_part[4];
-    __shared__ uint32_t s_wave[4];
+    __shared__ uint32_t s_wave[2][4];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     long long before = 0;  // rows of the blocks before this one
     for (int b = tid; b < (int)blockIdx.x; b += 256) before += sums[b];
     for (int o = 32; o >= 1; o >>= 1) before += __shfl_xor(before, o);
     if (lane == 0) s_part[w] = before;
-    const long long r0 = (long long)blockIdx.x * kCompactRows + 4 * tid;
-    bool l[4];
-    uint32_t c = 0;
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-        l[u] = r0 + u < n && live[r0 + u];
-        c += l[u] ? 1u : 0u;
-    }
-    // exclusive prefix of c over the block (thread order = row order)
-    uint32_t x = c;
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = (uint32_t)__shfl_up((int)x, o);
-        if (lane >= o) x += y;
-    }
-    if (lane == 63) s_wave[w] = x;
     __syncthreads();
-    const long long base = s_part[0] + s_part[1] + s_part[2] + s_part[3];
-    uint32_t off = x - c;
-    for (int k = 0; k < w; ++k) off += s_wave[k];
-    long long at = base + off;
+    long long base = s_part[0] + s_part[1] + s_part[2] + s_part[3];
+    for (int k = 0; k < chunks; ++k) {
+        const long long r0 = ((long long)blockIdx.x * chunks + k) * kCompactRows + 4 * tid;
+        bool l[4];
+        uint32_t c = 0;
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
-        if (l[u]) rows[at++] = r0 + u;
-    if (blockIdx.x == gridDim.x - 1 && tid == 255) *count = base + off + c;
+        for (int u = 0; u < 4; ++u) {
+            l[u] = r0 + u < n && live[r0 + u];
+            c += l[u] ? 1u : 0u;
+        }
+        // exclusive prefix of c over the chunk (thread order = row order)
+        uint32_t x = c;
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = (uint32_t)__shfl_up((int)x, o);
+            if (lane >= o) x += y;
+        }
+        uint32_t* sw = s_wave[k & 1];  // (double-buffered: one barrier per chunk)
+        if (lane == 63) sw[w] = x;
+        __syncthreads();
+        uint32_t off = x - c;
+        for (int q = 0; q < w; ++q) off += sw[q];
+        long long at = base + off;
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            if (l[u]) rows[at++] = r0 + u;
+        base += sw[0] + sw[1] + sw[2] + sw[3];
+    }
+    if (blockIdx.x == gridDim.x - 1 && tid == 0) *count = base;
 }
 
 static int rows_launch(const gs_rows_region* regions, int nreg, RowsLaunch& a, const char* fn) {
@@ -250,11 +259,13 @@ extern "C" int gs_rows_compact(const uint8_t* live, long long n, long long* rows
         return report_error(GS_ERR_INVALID_ARG, "gs_rows_compact: bad arguments");
     if (n == 0) return hipMemsetAsync(count_scratch, 0, sizeof(long long), (hipStream_t)stream) == hipSuccess
                            ? GS_OK : report_error(GS_ERR_HIP, "gs_rows_compact: memset failed");
-    const long long blocks = (n + kCompactRows - 1) / kCompactRows;
-    if (blocks > 0x7FFFFFFF) return report_error(GS_ERR_INVALID_ARG, "gs_rows_compact: n too large");
-    hipLaunchKernelGGL(k_compact_count, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, live, n,
+    const long long runs = (n + kCompactRows - 1) / kCompactRows;  // (<= the scratch's ceil(n / 1024))
+    if (runs > 0x7FFFFFFF) return report_error(GS_ERR_INVALID_ARG, "gs_rows_compact: n too large");
+    const long long per = (runs + kCompactMaxBlocks - 1) / kCompactMaxBlocks;  // chunks per block
+    const long long blocks = (runs + per - 1) / per;
+    hipLaunchKernelGGL(k_compact_count, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, live, n, (int)per,
                        count_scratch + 1);
-    hipLaunchKernelGGL(k_compact_write, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, live, n,
+    hipLaunchKernelGGL(k_compact_write, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, live, n, (int)per,
                        count_scratch + 1, rows, count_scratch);
     return launched();
 }

@@ -61,7 +61,8 @@ def test_rows_live_gather_scatter_match_torch(cuda_device, n, widths, density):
         assert torch.equal(m2.cpu().nan_to_num(7.0), exp.nan_to_num(7.0))
 
 
-@pytest.mark.parametrize("n,density", [(1_000_003, 0.1), (1, 1.0), (2047, 0.0), (4096, 1.0), (70_000, 0.5)])
+@pytest.mark.parametrize("n,density", [(1_000_003, 0.1), (1, 1.0), (2047, 0.0), (4096, 1.0), (70_000, 0.5),
+                                       (3_100_000, 0.3)])  # (the last: blocks of several 1024-row runs)
 def test_rows_compact_matches_nonzero(cuda_device, n, density):
     """gs_rows_compact: the ascending live rows and their count, no host round trip (vs torch.nonzero)."""
     from dge_amd import _native as N

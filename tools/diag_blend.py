@@ -73,14 +73,24 @@ def main():
     P = int(sys.argv[1]) if len(sys.argv) > 1 else 1_000_000
     W = H = int(sys.argv[2]) if len(sys.argv) > 2 else 512
     scene = synthetic_scene(P, sh_degree=3, seed=0, device=dev).requires_grad_(True)
-    cam = orbit_camera(0, 3, W, H, device=dev)
-    g = (torch.randn(3, H, W, generator=torch.Generator().manual_seed(1)) * 1e-3).to(dev)
+    V = int(sys.argv[3]) if len(sys.argv) > 3 else 1  # V > 1: the bench's batch (render_views, one merged pass)
+    cams = [orbit_camera(k, 3, W, H, device=dev) for k in range(V)]
+    gs = [(torch.randn(3, H, W, generator=torch.Generator().manual_seed(1 + k)) * 1e-3).to(dev) for k in range(V)]
     bg = torch.zeros(3, device=dev)
+
+    def once():
+        if V == 1:
+            render(cams[0], scene, PipelineParams(), bg)["render"].backward(gs[0])
+        else:
+            from dge_amd.multiview import render_views
+            outs = render_views(cams, scene, PipelineParams(), bg, streams=V)
+            torch.autograd.backward([o["render"] for o in outs], gs)
+
     for _ in range(3):
-        render(cam, scene, PipelineParams(), bg)["render"].backward(g)
+        once()
     torch.cuda.synchronize()
     _native.diag_enable(True)
-    render(cam, scene, PipelineParams(), bg)["render"].backward(g)
+    once()
     torch.cuda.synchronize()
     _native.diag_enable(False)
     summarize("render_fwd", _native.diag_read(0))
