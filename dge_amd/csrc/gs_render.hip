@@ -803,9 +803,9 @@ __global__ __launch_bounds__(64, GS_BWD_WAVES) void k_render_bwd(RenderBwdArgs a
     uint64_t c_replay = 0;
     uint32_t diag_kept = 0;
 
-    // the lane-row -> entry map of quad_reduce's result (rows hold e0, e0+2, e0+1, e0+3)
+    // the lane-row -> entry map of quad_reduce's result (row r holds entry e0 + r)
     const int row = lane >> 4;
-    const int row_entry = row == 1 ? 2 : row == 2 ? 1 : row;
+    const int row_entry = row;
     const bool row_writer = (lane & 15) == 0;
 
 #pragma unroll
@@ -858,7 +858,10 @@ __global__ __launch_bounds__(64, GS_BWD_WAVES) void k_render_bwd(RenderBwdArgs a
             __builtin_amdgcn_sched_barrier(0);  // (every product first: the lane swaps clobber their operands)
             float S[9];
 #pragma unroll
-            for (int f = 0; f < 9; ++f) S[f] = quad_reduce(g[0][f], g[1][f], g[2][f], g[3][f]);
+            // (entries 0 and 2, 1 and 3 swapped together: the operands of each lane swap then sit in
+            // different register pairs of the packed products — no copy before the swap — and row r
+            // holds entry r; the per-entry sums are the same adds in the same order)
+            for (int f = 0; f < 9; ++f) S[f] = quad_reduce(g[0][f], g[2][f], g[1][f], g[3][f]);
             __builtin_amdgcn_sched_barrier(0);
             const int kw = k + row_entry;
             if (row_writer && kw < nk) {
