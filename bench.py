@@ -416,7 +416,10 @@ def side_legs(args, scene, cams, seeds, bg, pipe, bucket, step, dev):
       (gaussian_renderer/__init__.py:90-140: the torch getters, torch.cat of the SH, GaussianRasterizer /
       _RasterizeGaussians) -- reproduced by render() with the fused raw-parameter path off;
     * c2_high_live: c2 with raw opacity N(-2, 1) instead of N(0, 1.5): most Gaussians translucent, so far
-      more of them reach the backward (the live-set backward is not only judged at ~7% live)."""
+      more of them reach the backward (the live-set backward is not only judged at ~7% live);
+    * dge_semantic_forward: DGE's second, gradient-free render of every view (DGE.py:198-204: the edit
+      mask as override_color, thresholded norm), batched like the training renders, forward only;
+    * dge_step_with_semantic: the c2 step plus those semantic renders (the DGE loop's per-view work)."""
     from dge_amd.cameras import orbit_camera
     from dge_amd.multiview import GradBucket, render_backward_views
     from dge_amd.scene import synthetic_scene
@@ -463,6 +466,33 @@ def side_legs(args, scene, cams, seeds, bg, pipe, bucket, step, dev):
     legs["c2_high_live"] = {"value": round(steps * V / dt, 3), "unit": "renders/s", "live_fraction": round(live, 4),
                             "opacity": "raw N(-2, 1)", "stages_ms": st}
     del hl, hb
+
+    # DGE's semantic render (gradient-free, override_color = the Gaussian mask, DGE.py:198-204): a 20%
+    # mask, the views batched on the step's streams, no autograd (forward-only kernels)
+    from dge_amd.multiview import render_views
+    gm = torch.rand(args.points, generator=torch.Generator().manual_seed(5)) < 0.2
+    colors = gm.to(dev)[:, None].float().repeat(1, 3)
+
+    def sem():
+        with torch.no_grad():
+            outs = render_views(cams, scene, pipe, bg, streams=args.streams, override_color=colors)
+            return [torch.norm(o["render"], dim=0) > 0.8 for o in outs]
+
+    for _ in range(3):
+        sem()
+    dt = _time(sem, steps)
+    legs["dge_semantic_forward"] = {"value": round(steps * V / dt, 3), "unit": "renders/s",
+                                    "path": "render_views(override_color=mask), no_grad, forward only"}
+
+    def step_sem():
+        step()
+        sem()
+
+    for _ in range(3):
+        step_sem()
+    dt = _time(step_sem, steps)
+    legs["dge_step_with_semantic"] = {"value": round(steps * V / dt, 3), "unit": "views/s",
+                                      "path": "the c2 step (fwd+bwd renders) + the semantic forward of each view"}
     return legs
 
 

@@ -137,8 +137,12 @@ class GradBucket:
         pinned.copy_(cs[:1], non_blocking=True)
         self._pending = ("hint", group, idx, pinned, stream.record_event(), n, mats)
 
-    def allreduce_end(self):
-        """Second half of allreduce_begin (after the backward): the packed SUM of the agreed rows."""
+    def allreduce_end(self, stream=None):
+        """Second half of allreduce_begin (after the backward): the packed SUM of the agreed rows.
+        stream (GPU buckets): run the pack, the collective and the unpack on that stream instead, behind the
+        work the current stream has enqueued so far (the backward), and return at once — the current stream
+        is then free for work that does not read the gradients (DGE's gradient-free semantic renders,
+        DGE.py:198-204) while RCCL runs; allreduce_join() makes the current stream wait for the result."""
         pend, self._pending = getattr(self, "_pending", None), None
         if pend is None:
             return None
@@ -153,13 +157,33 @@ class GradBucket:
                 if p.grad is not None and p.grad.data_ptr() != v.data_ptr():
                     v.copy_(p.grad)
             self.attach()
-        if 2 * m > n:  # mostly dense: packing would not pay
-            return dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=group)
-        rows = idx[:m]
-        packed = _rows_gather(mats, rows)
-        dist.all_reduce(packed, op=dist.ReduceOp.SUM, group=group)
-        _rows_scatter(mats, rows, packed)
+        side = stream is not None and self.flat.is_cuda
+        if side:
+            main = torch.cuda.current_stream(self.flat.device)
+            stream.wait_stream(main)
+            ctx = torch.cuda.stream(stream)
+        else:
+            import contextlib
+
+            ctx = contextlib.nullcontext()
+        with ctx:
+            if 2 * m > n:  # mostly dense: packing would not pay
+                dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=group)
+            else:
+                rows = idx[:m]
+                packed = _rows_gather(mats, rows)
+                dist.all_reduce(packed, op=dist.ReduceOp.SUM, group=group)
+                _rows_scatter(mats, rows, packed)
+                if side:  # (allocated on the side stream, freed by the caching allocator at once)
+                    rows.record_stream(stream)
+        self._reduced = stream.record_event() if side else None
         return None
+
+    def allreduce_join(self):
+        """Make the current stream wait for an allreduce_end(stream=...) (no-op otherwise)."""
+        ev, self._reduced = getattr(self, "_reduced", None), None
+        if ev is not None:
+            torch.cuda.current_stream(self.flat.device).wait_event(ev)
 
     def check_attached(self) -> bool:
         return all(p.grad is not None and p.grad.data_ptr() == v.data_ptr() for p, v in zip(self.params, self.views))
@@ -325,6 +349,18 @@ def render_views(cameras, pc, pipe, bg_color, streams: int = 2, speculate: bool 
     return outs
 
 
+_COLLECTIVE_STREAMS = {}
+
+
+def _collective_stream(device):
+    """The side stream a step's gradient collective runs on (one per device, reused)."""
+    dev = torch.device(device)
+    s = _COLLECTIVE_STREAMS.get(dev.index)
+    if s is None:
+        s = _COLLECTIVE_STREAMS[dev.index] = torch.cuda.Stream(device=dev)
+    return s
+
+
 def _native_max_views() -> int:
     from . import _native as N
 
@@ -459,11 +495,15 @@ def multiview_step(scene, cameras, render_fn, pipe, bg, bucket: GradBucket, tota
             losses_of([pkg], i)[0].backward()
             vs_sum += pkg["viewspace_points"].grad
             radii_max = torch.maximum(radii_max, pkg["radii"])
+    side = None
     if hinted:
-        bucket.allreduce_end()
+        # the collective on a side stream behind the backward; the semantic renders (which read no
+        # gradient) go on the caller's stream meanwhile, and the caller's stream joins the collective after
+        side = _collective_stream(dev) if semantic and dev.type == "cuda" else None
+        bucket.allreduce_end(stream=side)
     else:
         bucket.allreduce(group, min_world=min_world)
-    if semantic:  # gradient-free: enqueued behind the collective, which runs beside them
+    if semantic:  # gradient-free: beside the collective (hinted steps) or behind it
         with torch.no_grad():
             gm = getattr(scene, "mask", None)
             gm = gm if gm is not None else torch.ones(P, dtype=torch.bool, device=dev)
@@ -474,6 +514,7 @@ def multiview_step(scene, cameras, render_fn, pipe, bg, bucket: GradBucket, tota
             else:
                 sms = [render_fn(cam, scene, pipe, bg, override_color=colors)["render"] for cam in cameras]
             sem = [torch.norm(sm, dim=0) > 0.8 for sm in sms]
+    bucket.allreduce_join()
     found_inf = (~torch.isfinite(bucket.flat)).any().to(torch.float32).reshape(1)
     reduce_view_stats(vs_sum, radii_max, group)
     out = {"viewspace_grad_sum": vs_sum, "radii_max": radii_max, "found_inf": found_inf}

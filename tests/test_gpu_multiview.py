@@ -154,9 +154,10 @@ def test_c3_two_ranks_share_one_card(cuda_device):
 
 
 def test_multiview_step_batched_streams_hinted_one_rank(cuda_device):
-    """multiview_step(streams=3, bucket_zeroed=True) on a one-rank RCCL group — views rendered together on
-    3 streams, one backward of the summed loss, the all-reduce's live rows agreed on before it — gives the
-    per-view loop's gradients, view-space sums and radii."""
+    """multiview_step(streams=3, bucket_zeroed=True, min_world=1, semantic=True) on a one-rank RCCL group —
+    views rendered together on 3 streams, one backward of the summed loss, the all-reduce's live rows agreed
+    on before it and the whole protocol run (pack, SUM on the collective's side stream beside the semantic
+    renders, unpack) — gives the per-view loop's gradients, view-space sums, radii and semantic masks."""
     import torch.distributed as dist
 
     from dge_amd.gaussian_renderer import PipelineParams, render
@@ -173,17 +174,20 @@ def test_multiview_step_batched_streams_hinted_one_rank(cuda_device):
             sc, cams, seeds = _c3_setup(dev, P, V, W, H)
             bucket = GradBucket(sc.parameters())
             bucket.zero()
+            sc.mask = torch.arange(P, device=dev) % 5 == 0  # (the semantic render's colours)
             if mode == "loop":
                 out = multiview_step(sc, cams, render, PipelineParams(), torch.zeros(3, device=dev), bucket, V,
-                                     targets=seeds)
+                                     targets=seeds, semantic=True)
             else:
                 out = multiview_step(sc, cams, render, PipelineParams(), torch.zeros(3, device=dev), bucket, V,
-                                     targets=seeds, streams=3, bucket_zeroed=True)
+                                     targets=seeds, streams=3, bucket_zeroed=True, min_world=1, semantic=True)
             torch.cuda.synchronize()
-            res[mode] = (bucket.flat.clone(), out["viewspace_grad_sum"].clone(), out["radii_max"].clone())
+            res[mode] = (bucket.flat.clone(), out["viewspace_grad_sum"].clone(), out["radii_max"].clone(),
+                         [m.clone() for m in out["semantic_masks"]])
     finally:
         dist.destroy_process_group()
-    (g0, v0, r0), (g1, v1, r1) = res["loop"], res["batched"]
+    (g0, v0, r0, m0), (g1, v1, r1, m1) = res["loop"], res["batched"]
+    assert len(m0) == V and all(torch.equal(a, b) for a, b in zip(m0, m1)) and any(bool(m.any()) for m in m0)
     assert torch.equal(r0, r1)
     torch.testing.assert_close(v1, v0, rtol=1e-5, atol=1e-9)
     torch.testing.assert_close(g1, g0, rtol=1e-5, atol=1e-9)
@@ -293,3 +297,83 @@ def test_forward_only_renders_equal_training_renders(cuda_device):
             for k in ("render", "radii", "depth_3dgs"):
                 assert torch.equal(a[k].detach(), b[k]), k
     assert train_views.batch.num_rendered == fwd_views.batch.num_rendered
+
+
+def _hinted_worker(rank, world, port, P, V, W, H, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    try:
+        torch.cuda.set_device(0)
+        dev = torch.device("cuda", 0)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from dge_amd.gaussian_renderer import PipelineParams, render
+        from dge_amd.multiview import GradBucket, multiview_step, shard_views
+
+        sc, cams, seeds = _c3_setup(dev, P, V, W, H)
+        sc.mask = torch.arange(P, device=dev) % 5 == 0
+        mine = list(shard_views(V, world, rank))
+        bucket = GradBucket(sc.parameters())
+        bucket.zero()
+        out = multiview_step(sc, [cams[i] for i in mine], render, PipelineParams(), torch.zeros(3, device=dev),
+                             bucket, V, targets=[seeds[i] for i in mine], streams=3, bucket_zeroed=True,
+                             semantic=True)
+        torch.cuda.synchronize()
+        # this rank's own rows: the Gaussians its views blend (the rows only this rank touches must arrive)
+        q.put((rank, bucket.flat.cpu().numpy(), [m.cpu().numpy() for m in out["semantic_masks"]], None))
+    except Exception as e:  # report instead of hanging the parent
+        q.put((rank, None, None, repr(e)))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def test_hinted_sparse_allreduce_two_ranks(cuda_device):
+    """The agreed-before-backward sparse all-reduce (GradBucket.allreduce_begin/_end, the collective on a
+    side stream beside the semantic renders) with two ranks on one card (gloo, CUDA tensors), 2 views
+    each: both ranks hold the single-process 4-view step's summed gradients — including rows only one
+    rank's views touch — and each rank's semantic masks are its views' masks in the single-process step."""
+    from dge_amd.gaussian_renderer import PipelineParams, render
+    from dge_amd.multiview import GradBucket, multiview_step
+
+    P, V, W, H = 60_000, 4, 160, 128
+    dev = torch.device("cuda", 0)
+    sc, cams, seeds = _c3_setup(dev, P, V, W, H)
+    sc.mask = torch.arange(P, device=dev) % 5 == 0
+    bucket = GradBucket(sc.parameters())
+    out = multiview_step(sc, cams, render, PipelineParams(), torch.zeros(3, device=dev), bucket, V, targets=seeds,
+                         semantic=True)
+    torch.cuda.synchronize()
+    ref = bucket.flat.cpu().numpy()
+    masks = [m.cpu().numpy() for m in out["semantic_masks"]]
+    # each rank's own contribution (its two views alone): the elements only one rank's views make nonzero
+    half = []
+    for idx in ((0, 1), (2, 3)):
+        b2 = GradBucket(sc.parameters())
+        multiview_step(sc, [cams[i] for i in idx], render, PipelineParams(), torch.zeros(3, device=dev), b2, V,
+                       targets=[seeds[i] for i in idx])
+        torch.cuda.synchronize()
+        half.append(b2.flat.cpu().numpy())
+        del b2
+    del sc, bucket, out
+    torch.cuda.empty_cache()
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_hinted_worker, args=(r, 2, port, P, V, W, H, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    only0 = (half[0] != 0) & (half[1] == 0)
+    only1 = (half[1] != 0) & (half[0] == 0)
+    assert only0.any() and only1.any()
+    for rank, flat, sems, err in res:
+        assert err is None, f"rank {rank}: {err}"
+        np.testing.assert_allclose(flat, ref, rtol=1e-5, atol=1e-6 * np.abs(ref).max())
+        assert np.array_equal(flat[only0] != 0, ref[only0] != 0) and np.array_equal(flat[only1] != 0, ref[only1] != 0)
+        mine = (0, 1) if rank == 0 else (2, 3)
+        assert all(np.array_equal(a, masks[i]) for a, i in zip(sems, mine))
+    for p in procs:
+        assert p.exitcode == 0
