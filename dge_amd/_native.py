@@ -15,7 +15,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("DGE_AMD_LIB") or os.path.join(_HERE, "lib", "libgs_raster.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "gs_raster.h")
 
-ABI_VERSION = 11  # GS_RASTER_ABI_VERSION of include/gs_raster.h this binding is written against
+ABI_VERSION = 12  # GS_RASTER_ABI_VERSION of include/gs_raster.h this binding is written against
 
 GS_OK = 0
 GS_ERR_INVALID_ARG = 1
@@ -99,6 +99,7 @@ class GsGrads(ctypes.Structure):
         ("mask_bits", ctypes.c_uint),
         ("dL_dconic", _fp),
         ("writes_after", ctypes.c_void_p),
+        ("zeroed", ctypes.c_uint),
     ]
 
 

@@ -736,6 +736,7 @@ GaussBwdArgs gauss_args(const gs_settings* s, const gs_params* gp, int R, const 
     ga.dL_dmeans3D = o->dL_dmeans3D; ga.dL_dcov3D = o->dL_dcov3D;
     ga.dL_dscales = o->dL_dscales; ga.dL_drot = o->dL_drotations;
     ga.acc = o->accumulate;
+    ga.zeroed = o->zeroed & o->accumulate;
     ga.slot_cap = slot_cap;
     ga.grad_mask = o->grad_mask;
     ga.mask_bits = o->grad_mask ? o->mask_bits : 0u;
@@ -983,6 +984,7 @@ int gs_rasterize_backward(const gs_settings* s, int P, int M, int R, const float
     o.mask_bits = 0;
     o.dL_dconic = nullptr;
     o.writes_after = nullptr;
+    o.zeroed = 0;
     gs_params g2 = g;
     g2.M = M;  // dL_dsh is [P,M,3] even when shs is absent (then all zero)
     return gs_rasterize_backward_ex(s, &g2, R, radii, geom, binning, img, dL_dpix, &o, stream);

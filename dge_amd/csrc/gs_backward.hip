@@ -335,9 +335,10 @@ __device__ __forceinline__ void apply_grad_mask(const GaussBwdArgs& a, float m, 
 // all loads of the accumulated ones first, then all stores, so the ~20
 // scattered read-modify-writes overlap instead of forming a dependent chain.
 // (means2D and colors are per rendered Gaussian `idx`; the parameter-shaped outputs go to row `src`)
-__device__ __forceinline__ void commit_outputs(const GaussBwdArgs& a, int idx, int src, const float (&acc)[9],
-                                               float dop, const float (&ddc)[3], const GaussOut& o) {
-    const uint32_t f = a.acc;
+// f: the GS_ACC_* bits this Gaussian's outputs are added into (a.acc, less gs_grads.zeroed's on its first write)
+__device__ __forceinline__ void commit_outputs(const GaussBwdArgs& a, uint32_t f, int idx, int src,
+                                               const float (&acc)[9], float dop, const float (&ddc)[3],
+                                               const GaussOut& o) {
     const size_t i3 = 3 * (size_t)idx, s3 = 3 * (size_t)src;
     float* d0 = a.dsh.dc ? a.dsh.dc + (size_t)src * a.dsh.dc_stride : nullptr;
     float4* r4 = reinterpret_cast<float4*>(a.dL_drot + 4 * (size_t)src);
@@ -517,12 +518,15 @@ constexpr int kLiveGrid = 768;   // target workgroups (3 per CU: 166 VGPRs, 48 K
 constexpr uint32_t kNoRow = 0xFFFFFFFFu;
 
 // One view's work on one batch of live Gaussians (every thread of the block calls it: it has
-// barriers).  ok: this thread's Gaussian is live in the view; src: its parameter row.
-__device__ __forceinline__ void bwd_view_batch(const GaussBwdArgs& a, bool ok, int idx, int src, int nrow, int ncol,
-                                               float inv_ncol, float* s_sh, uint32_t* s_gid, uint64_t* st) {
+// barriers).  ok: this thread's Gaussian is live in the view; src: its parameter row; vfirst: no earlier
+// view of the batch has it live (zeroed outputs are stored, not added, on its first write).
+__device__ __forceinline__ void bwd_view_batch(const GaussBwdArgs& a, bool ok, int idx, int src, bool vfirst,
+                                               uint32_t zeroed, int nrow, int ncol, float inv_ncol, float* s_sh,
+                                               uint32_t* s_gid, uint8_t* s_shacc, uint64_t* st) {
     float* const my_sh = s_sh + threadIdx.x * kShPitch;
-    const bool ash = a.acc & GS_ACC_SH;
+    const uint32_t facc = a.acc & ~(vfirst ? zeroed : 0u);
     s_gid[threadIdx.x] = ok ? (uint32_t)src : kNoRow;  // (SH rows are parameter rows)
+    s_shacc[threadIdx.x] = (facc & GS_ACC_SH) ? 1 : 0;  // (the SH rows' read-modify-write, by row)
     // independent loads first: parameters (a later view's from L2), slot range, the first 8 record flags
     GaussIn gin{};
     if (ok) gin = load_gauss_in(a, idx, src);
@@ -632,7 +636,7 @@ __device__ __forceinline__ void bwd_view_batch(const GaussBwdArgs& a, bool ok, i
         if (a.grad_mask) apply_grad_mask(a, gm, acc, dop, o);
     }
     if (st) st[4] = __builtin_amdgcn_s_memrealtime();
-    if (ok) commit_outputs(a, idx, src, acc, dop, ddc, o);
+    if (ok) commit_outputs(a, facc, idx, src, acc, dop, ddc, o);
     if (st) st[5] = __builtin_amdgcn_s_memrealtime();
     // dL_dsh rest rows: through LDS (in place), flat block-wide batches, loads before stores
     if (a.dsh.dc && ncol > 0) {
@@ -644,7 +648,7 @@ __device__ __forceinline__ void bwd_view_batch(const GaussBwdArgs& a, bool ok, i
                 const int e = b + u * kGB + (int)threadIdx.x;
                 const int row = (int)(((float)e + 0.5f) * inv_ncol), col = e - row * ncol;
                 const uint32_t gid = e < total ? s_gid[row] : kNoRow;
-                old[u] = ash && gid != kNoRow ? a.dsh.rest[(size_t)gid * a.dsh.rest_stride + col] : 0.f;
+                old[u] = gid != kNoRow && s_shacc[row] ? a.dsh.rest[(size_t)gid * a.dsh.rest_stride + col] : 0.f;
             }
 #pragma unroll
             for (int u = 0; u < kV; ++u) {
@@ -662,6 +666,7 @@ __global__ __launch_bounds__(kGB) void k_gauss_bwd_live(GaussBwdViews m) {
     const GaussBwdArgs& a = m.v[0];
     __shared__ float s_sh[kGB * kShPitch];
     __shared__ uint32_t s_gid[kGB];
+    __shared__ uint8_t s_shacc[kGB];
     __shared__ uint32_t s_pre[kLiveGroup + 1];
     __shared__ uint32_t s_vlist[2 * kGB];  // Gaussians live in the view being processed, compacted (+ a chunk's overflow)
     __shared__ uint32_t s_wave[kGB / 64];
@@ -710,16 +715,19 @@ __global__ __launch_bounds__(kGB) void k_gauss_bwd_live(GaussBwdViews m) {
                 off += w < wave ? s_wave[w] : 0u;
                 nv += s_wave[w];
             }
-            if (has) s_vlist[filled + off + (uint32_t)__popcll(bm & lanemask_lt())] = entry & kLiveIdMask;
+            if (has) s_vlist[filled + off + (uint32_t)__popcll(bm & lanemask_lt())] = entry;  // (with the view mask)
             filled += nv;
             __syncthreads();  // s_vlist (and s_wave, read by every thread, before its next write)
             if (filled < (uint32_t)kGB && base + kGB < count) continue;  // (fill the batch further)
             while (filled > 0) {
                 const uint32_t nb = filled < (uint32_t)kGB ? filled : (uint32_t)kGB;
                 const bool ok = threadIdx.x < nb;
-                const int idx = ok ? (int)s_vlist[threadIdx.x] : 0;
+                const uint32_t ent = ok ? s_vlist[threadIdx.x] : 0u;
+                const int idx = (int)(ent & kLiveIdMask);
                 const int src = ok && a.index ? a.index[idx] : idx;  // parameter row
-                bwd_view_batch(m.v[v], ok, idx, src, (int)nb, ncol, inv_ncol, s_sh, s_gid, a.diag && first ? st : nullptr);
+                const bool vfirst = ((ent >> 28) & ((1u << v) - 1u)) == 0u;  // no earlier view has it live
+                bwd_view_batch(m.v[v], ok, idx, src, vfirst, a.zeroed, (int)nb, ncol, inv_ncol, s_sh, s_gid, s_shacc,
+                               a.diag && first ? st : nullptr);
                 first = false;
                 // (bwd_view_batch ends on a barrier: every thread has read its entry) the rest to the front
                 const uint32_t rest = filled - nb;

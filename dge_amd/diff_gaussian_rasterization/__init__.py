@@ -192,6 +192,7 @@ class _RasterizeGaussiansFused(torch.autograd.Function):
                 rs.viewmatrix, rs.projmatrix, rs.tanfovx, rs.tanfovy, grad_out_color, rs.sh_degree, rs.campos,
                 geomBuffer, ctx.num_rendered, binningBuffer, imgBuffer, rs.debug)
         _serialize_scratch(ctx, xyz.device)
+        _ZEROED.pop(xyz.device.index, None)  # (this backward writes .grad: the buffer is no longer all zeros)
         ordered = bool(into) and _SIDE_STREAMS
         stream, after = _order_grad_writes_begin(xyz.device) if ordered else (None, None)
         d_m2, d_xyz, d_dc, d_rest, d_col, d_op, d_sc, d_rot = _call_with_snapshot(
@@ -226,6 +227,27 @@ _FUSED_GRAD_ACCUM = os.environ.get("DGE_AMD_FUSED_GRAD_ACCUM", "1") != "0"
 # all-reduce issued there sees the gradients.  Backward calls on the default stream need nothing.
 _GRAD_WRITES = {}  # device index -> (stream, event) of the last side-stream .grad write
 _SIDE_STREAMS = False  # set once dge_amd.multiview.stream_pool hands out streams
+# device index -> (flat gradient buffer, its version counter right after GradBucket.zero()): the buffer
+# holds zeros until a backward writes into it (the native backward calls take the entry; a torch
+# in-place write shows as a version change).  A batched backward whose .grad targets all lie in it stores
+# each Gaussian's first gradient instead of adding it (gs_grads.zeroed: the zeros are never read).
+_ZEROED = {}
+
+
+def zeroed_bits(dev, tensors, bits: int) -> int:
+    """`bits` if every tensor lies in the buffer GradBucket.zero() registered for `dev` and nothing has
+    written into that buffer since (the entry is taken: the caller's backward is the next writer), else 0."""
+    ent = _ZEROED.pop(dev.index, None)
+    if ent is None or not bits or os.environ.get("DGE_AMD_ZEROED", "1") == "0":  # (=0: A/B against the add path)
+        return 0
+    flat, version = ent
+    if flat._version != version:
+        return 0
+    lo, hi = flat.data_ptr(), flat.data_ptr() + 4 * flat.numel()
+    for t in tensors:
+        if t is None or t.dtype != torch.float32 or not (lo <= t.data_ptr() and t.data_ptr() + 4 * t.numel() <= hi):
+            return 0
+    return bits
 
 
 def _order_grad_writes_begin(dev):

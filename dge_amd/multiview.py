@@ -79,9 +79,14 @@ class GradBucket:
                 self._zero_event = stream.record_event()
             _r._SIDE_STREAMS = True
             _r._GRAD_WRITES[dev.index] = (stream, self._zero_event)
+            _r._ZEROED[dev.index] = (self.flat, self.flat._version)
             self.attach()
             return
         self.flat.zero_()
+        if self.flat.is_cuda:
+            from . import diff_gaussian_rasterization as _r
+
+            _r._ZEROED[self.flat.device.index] = (self.flat, self.flat._version)
         if overlap and self.flat.is_cuda:
             from . import diff_gaussian_rasterization as _r
 

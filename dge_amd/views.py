@@ -209,6 +209,7 @@ class _RasterizeViews(torch.autograd.Function):
                 returned[k] = t
         if not ctx.has_sh:
             targets["colors"] = torch.empty_like(colors) if colors is not None and colors.numel() else None
+        zeroed = _R.zeroed_bits(dev, [targets[k] for k, (p, _, bit) in params.items() if acc0 & bit], acc0)
         acc_all = N.ACC_MEANS3D | N.ACC_OPACITY | N.ACC_SCALES | N.ACC_ROTATIONS | (N.ACC_SH if ctx.has_sh else 0)
         if not ctx.has_sh and targets.get("colors") is not None:
             acc_all |= N.ACC_COLORS
@@ -228,8 +229,11 @@ class _RasterizeViews(torch.autograd.Function):
                 o.dsh_rest_stride = 3 * (f_rest.size(1) if f_rest is not None and f_rest.numel() else 0)
             o.dL_dscales = targets["scaling"].data_ptr()
             o.dL_drotations = targets["rotation"].data_ptr()
-            # the first view writes (or adds into an existing .grad), the others add
+            # the first view writes (or adds into an existing .grad), the others add; into a .grad buffer
+            # zeroed this step, a Gaussian's first gradient is stored, not added (gs_grads.zeroed)
             o.accumulate = acc0 if v == 0 else acc_all
+            if v == 0:
+                o.zeroed = zeroed
             if grad_mask is not None:
                 o.grad_mask = grad_mask.data_ptr()
                 o.mask_bits = mask_bits

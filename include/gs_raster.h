@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define GS_RASTER_ABI_VERSION 11
+#define GS_RASTER_ABI_VERSION 12
 
 #define GS_OK 0
 #define GS_ERR_INVALID_ARG 1   /* AT_ERROR / std::runtime_error in the reference */
@@ -186,6 +186,14 @@ typedef struct gs_grads {         /* backward outputs, every element written */
      * into the same .grad buffers from different streams are ordered by it
      * while the replay of one overlaps the per-Gaussian pass of the other. */
     void *writes_after;
+    /* GS_ACC_* bits of accumulated outputs that hold exactly zero for every
+     * Gaussian before this call (the caller cleared them this step, e.g. a
+     * gradient bucket filled with zeros): the first write this call makes for
+     * a Gaussian stores its gradient instead of adding it, so the zeros are
+     * never read.  gs_views_backward honours view 0's bits for the batch: the
+     * first view that has a Gaussian live stores, later views add.  0: plain
+     * accumulation (ABI 12). */
+    unsigned int zeroed;
 } gs_grads;
 
 int gs_rasterize_forward_ex(const gs_settings *s, const gs_params *g, float *out_color, float *out_depth,

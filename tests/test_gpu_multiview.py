@@ -377,3 +377,40 @@ def test_hinted_sparse_allreduce_two_ranks(cuda_device):
         assert all(np.array_equal(a, masks[i]) for a, i in zip(sems, mine))
     for p in procs:
         assert p.exitcode == 0
+
+
+def test_zeroed_bucket_stores_first_gradient(cuda_device):
+    """GradBucket.zero() registers the cleared buffer, and the next batched backward into it stores each
+    Gaussian's first gradient instead of adding it to the zeros (gs_grads.zeroed: no read of the zeros).
+    The bucket equals the read-modify-write path's (registration dropped) bit for bit, and the registration
+    is taken by that backward: a second backward without a zero adds (twice the first sums, up to the
+    order of the additions)."""
+    from dge_amd import diff_gaussian_rasterization as R
+    from dge_amd.gaussian_renderer import PipelineParams
+    from dge_amd.multiview import GradBucket, render_views
+
+    dev = torch.device("cuda", 0)
+    P, V, W, H = 60_000, 3, 160, 128
+    sc, cams, seeds = _c3_setup(dev, P, V, W, H)
+    bucket = GradBucket(sc.parameters())
+    bg = torch.zeros(3, device=dev)
+
+    def step():
+        outs = render_views(cams, sc, PipelineParams(), bg, streams=3)
+        torch.autograd.backward([o["render"] for o in outs], seeds)
+        torch.cuda.synchronize()
+
+    res = {}
+    for mode in ("add", "store"):
+        bucket.zero()
+        if mode == "add":
+            R._ZEROED.clear()
+        else:
+            assert dev.index in R._ZEROED
+        step()
+        assert dev.index not in R._ZEROED
+        res[mode] = bucket.flat.clone()
+    assert torch.equal(res["store"], res["add"]) and bool(res["store"].abs().sum() > 0)
+    step()  # no zero in between: adds
+    # (a store would leave the first sums: half of these; the views' terms cancel in a few elements)
+    torch.testing.assert_close(bucket.flat, 2 * res["store"], rtol=1e-5, atol=1e-6 * float(res["store"].abs().max()))
