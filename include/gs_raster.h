@@ -255,9 +255,12 @@ int gs_views_forward(int n, const gs_settings *const *s, const gs_params *const 
 int gs_views_check(gs_views *h, int *num_rendered);
 /* The backward of every view, view v on streams[v] with grads[v] (dL_dmeans2D
  * per view; the parameter gradients usually shared, GS_ACC_* set from the
- * second view on).  The views' per-Gaussian passes are chained in view order
- * (the first after `writes_after`, an optional hipEvent_t), so accumulated
- * gradients add up in a fixed order; `join` (the caller's stream, null = the
+ * second view on).  Each view's gradient replay runs on its stream; when the
+ * views share their parameter-gradient outputs, ONE per-Gaussian pass on
+ * streams[0] then adds every view's gradients in view order (else the views'
+ * passes are chained in view order) — the first write after `writes_after`,
+ * an optional hipEvent_t — so accumulated gradients add up in a fixed order,
+ * bitwise those of per-view calls; `join` (the caller's stream, null = the
  * legacy default stream): the views start after its work so far (the image
  * gradients) and it waits for all of them. */
 int gs_views_backward(gs_views *h, const float *const *dL_dpix, const gs_grads *const *grads,
