@@ -345,6 +345,8 @@ struct FwdState {
     Staging* st = nullptr;
     PreprocessArgs pa;
     EmitArgs ea;
+    bool ids_ok = true;     // a forward-only render may bin Gaussian ids alone (not apply_weights' binning)
+    bool ids_only = false;  // this binning did (EmitArgs::ids_only)
     ~FwdState() { staging_release(st); }
 };
 
@@ -527,6 +529,7 @@ int bin_emit(FwdState& f, void* bin, uint32_t K_layout, const uint32_t* n_dev, h
     ea.cap = n_dev ? K_layout : 0xFFFFFFFFu;
     const TileSortPlan plan = tile_sort_plan(g.tiles);
     if (ea.xhist) {  // two-level binning (tile_sort_fused): column-ordered emission, row pass, ranges
+        ea.ids_only = f.ids_only = !bwd && f.ids_ok;
         ea.tile_key = at<uint32_t>(bin, bl.key1);
         ea.pairs_out = at<uint2>(bin, bl.pair1);
         ea.xtotals = at<uint32_t>(bin, bl.sort_totals);
@@ -624,6 +627,7 @@ int render_launch(FwdState& f, void* bin, uint32_t K_layout, int order_ready, fl
     ra.tile_order = at<uint32_t>(img, il.tile_order);
     ra.order_ready = order_ready;
     ra.point_pairs = at<uint2>(bin, bl.point_pairs);
+    ra.point_ids = f.ids_only ? at<uint32_t>(bin, bl.point_pairs) : nullptr;
     ra.bwd_items = at<uint2>(bin, bl.bwd_items);
     ra.bwd_count = at<uint32_t>(img, il.bwd_count);
     ra.item_cap = (uint32_t)(4 * bl.nslots);
@@ -649,6 +653,7 @@ int bin_forward(const gs_settings* s, const Grid& g, const gs_params& gp, int* r
                 gs_alloc_fn alloc, void* ctx, hipStream_t stream, void** geom_out, void** img_out, void** bin_out,
                 int* K_out) {
     FwdState f;
+    f.ids_ok = false;  // (apply_weights reads the (Gaussian, slot) lists)
     f.s = *s;
     f.gp = gp;
     f.g = g;

@@ -311,6 +311,9 @@ struct EmitArgs {
     uint2* pairs_out = nullptr;
     uint32_t* tile_count = nullptr;
     int ntiles = 0;
+    // ids_only (a forward-only render's two-level binning): the lists carry the Gaussian id alone (u32 at
+    // pairs_out / the point list) — the binning slot is only the backward's record address
+    int ids_only = 0;
 };
 void launch_scan_reduce(const EmitArgs& a, hipStream_t s);
 void launch_scan_emit(const EmitArgs& a, hipStream_t s);
@@ -329,6 +332,7 @@ struct RenderArgs {
     uint32_t* tile_order;      // tiles longest list first: by the single-pass tile sort, else k_tile_order
     int order_ready;           // tile_order already written (the single-pass tile sort did it)
     const uint2* point_pairs;  // per-tile lists: (Gaussian, binning slot)
+    const uint32_t* point_ids = nullptr;  // ... or the Gaussian ids alone (EmitArgs::ids_only)
     const Splat* splat;
     const float* bg;
     float* final_T;

@@ -453,6 +453,9 @@ static void radix_pass(const uint32_t* kin, const void* vin, uint32_t* kout, voi
     if (vm == kValPair && !kout)  // the two-level binning's row pass: no sorted keys
         hipLaunchKernelGGL((k_radix_scatter<BITS, IPT, false, kValPair, false, true>), dim3(nb), dim3(256), 0, s, kin,
                            vin, kout, vout, gauss_by_slot, n, shift, hist, totals, nb, bm, ro, bias_not, n_dev);
+    else if (vm == kValU32 && !kout && ro.tile_count)  // the same over Gaussian ids alone (ids_only)
+        hipLaunchKernelGGL((k_radix_scatter<BITS, IPT, false, kValU32, false, true>), dim3(nb), dim3(256), 0, s, kin,
+                           vin, kout, vout, gauss_by_slot, n, shift, hist, totals, nb, bm, ro, bias_not, n_dev);
     else if (vm == kValPairFirst && !kout)  // the last tile-sort pass: no sorted keys
         hipLaunchKernelGGL((k_radix_scatter<BITS, IPT, true, kValPairFirst, false>), dim3(nb), dim3(256), 0, s, kin,
                            vin, kout, vout, gauss_by_slot, n, shift, hist, totals, nb, bm, ro, bias_not, n_dev);
@@ -646,8 +649,11 @@ __global__ __launch_bounds__(256) void k_scan_emit(EmitArgs a) {
 // k_radix_scatter), staged in LDS in column-major order and stored with
 // consecutive lanes on consecutive positions of each column run.  The key
 // written is y << 7 | x (the row pass's digit and the tile's column).
+// IDS: the (Gaussian, slot) pair's Gaussian alone (EmitArgs::ids_only)
 constexpr int kEmitEPT = 8, kEmitBatch = 256 * kEmitEPT;
+template <bool IDS>
 __global__ __launch_bounds__(256) void k_scan_emit_x(EmitArgs a) {
+    using PV = typename std::conditional<IDS, uint32_t, uint2>::type;
     __shared__ uint32_t lds4[4];
     __shared__ uint32_t s_start[256];
     __shared__ uint32_t s_gauss[256];
@@ -656,7 +662,7 @@ __global__ __launch_bounds__(256) void k_scan_emit_x(EmitArgs a) {
     __shared__ uint32_t s_gbase[kXDigits];  // the batch's column run: global position - staged position
     __shared__ uint16_t cnt[4][kXDigits];   // per-wave column counters, then the staged run starts
     __shared__ uint16_t s_key[kEmitBatch];
-    __shared__ uint2 s_pair[kEmitBatch];
+    __shared__ PV s_pair[kEmitBatch];
     __shared__ uint16_t s_own[kEmitBatch];  // the batch's owners (+1): marks at the entries' starts, prefix max
     __shared__ uint32_t s_carry;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -695,7 +701,7 @@ __global__ __launch_bounds__(256) void k_scan_emit_x(EmitArgs a) {
         for (uint32_t j0 = 0; j0 < total; j0 += kEmitBatch) {
             const uint32_t nb = total - j0 < (uint32_t)kEmitBatch ? total - j0 : (uint32_t)kEmitBatch;
             uint32_t kk[kEmitEPT], loc[kEmitEPT];
-            uint2 pv[kEmitEPT];
+            PV pv[kEmitEPT];
             // owner of every instance of the batch (the last entry with start <= j, see k_scan_emit) as a
             // prefix max over the batch of the entries' marks at their starts: one LDS read per instance
             // instead of a binary search of eight dependent reads
@@ -742,7 +748,8 @@ __global__ __launch_bounds__(256) void k_scan_emit_x(EmitArgs a) {
                 const uint32_t kx = k - ky * (uint32_t)q.z;
                 const uint32_t x = (uint32_t)q.x + kx, y = (uint32_t)q.y + ky;
                 kk[e] = y << kXBits | x;
-                pv[e] = make_uint2(s_gauss[lo], base + j);
+                if constexpr (IDS) pv[e] = s_gauss[lo];
+                else pv[e] = make_uint2(s_gauss[lo], base + j);
                 if (valid && a.rec_flags32 && base + j < a.cap) a.rec_flags32[base + j] = 0u;  // (slot order: coalesced)
                 const uint32_t d = valid ? x : 0u;
                 const uint64_t peers = match_digit<kXBits>(d, vm);
@@ -787,7 +794,8 @@ __global__ __launch_bounds__(256) void k_scan_emit_x(EmitArgs a) {
                 const uint32_t pos = s_gbase[kv & (kXDigits - 1)] + i;
                 if (pos < a.cap) {  // (speculative capacity: gs_views_check reports an overflow)
                     a.tile_key[pos] = kv;
-                    a.pairs_out[pos] = s_pair[i];
+                    if constexpr (IDS) reinterpret_cast<uint32_t*>(a.pairs_out)[pos] = s_pair[i];
+                    else a.pairs_out[pos] = s_pair[i];
                 }
             }
             for (int i = tid; i < 4 * kXDigits; i += 256) (&cnt[0][0])[i] = 0;
@@ -825,7 +833,10 @@ void launch_emit_fused(const EmitArgs& a, hipStream_t s) {
     // first level: column totals and each block's column offsets, then the column-ordered emission
     hipLaunchKernelGGL(k_radix_digit_scan, dim3(kXDigits / kScanDigits), dim3(1024), 0, s, a.xhist, a.scan_blocks,
                        kXDigits, a.xtotals, (const uint32_t*)nullptr, 0u, 1);
-    hipLaunchKernelGGL(k_scan_emit_x, dim3(a.scan_blocks), dim3(256), 0, s, a);
+    if (a.ids_only)
+        hipLaunchKernelGGL(k_scan_emit_x<true>, dim3(a.scan_blocks), dim3(256), 0, s, a);
+    else
+        hipLaunchKernelGGL(k_scan_emit_x<false>, dim3(a.scan_blocks), dim3(256), 0, s, a);
 }
 
 void launch_row_pass(const EmitArgs& a, uint32_t K, uint2* point_pairs, uint32_t* hist, int sort_blocks,
@@ -833,8 +844,8 @@ void launch_row_pass(const EmitArgs& a, uint32_t K, uint2* point_pairs, uint32_t
     if (a.P <= 0 || K == 0) return;
     // second level: the stable row pass (digit y), counting instances per tile on the way
     RangeOut ro{nullptr, nullptr, a.ntiles, a.tile_count, a.gx};
-    radix_pass<kXBits, kSortIPT>(a.tile_key, a.pairs_out, nullptr, point_pairs, nullptr, K, kXBits, false, kValPair,
-                                 hist, a.xtotals, sort_blocks, ro, nullptr, s, n_dev);
+    radix_pass<kXBits, kSortIPT>(a.tile_key, a.pairs_out, nullptr, point_pairs, nullptr, K, kXBits, false,
+                                 a.ids_only ? kValU32 : kValPair, hist, a.xtotals, sort_blocks, ro, nullptr, s, n_dev);
     hipLaunchKernelGGL(k_ranges_counts, dim3(1), dim3(256), 0, s, a.tile_count, a.ntiles, ranges);
 }
 

@@ -267,21 +267,22 @@ def test_render_views_speculated_overflow_is_reported(cuda_device):
             assert torch.equal(o[k], r[k]), k
 
 
-def test_forward_only_renders_equal_training_renders(cuda_device):
+@pytest.mark.parametrize("W,H,P", [(320, 256, 120_000), (1920, 1080, 300_000)])
+def test_forward_only_renders_equal_training_renders(cuda_device, W, H, P):
     """Renders under no_grad (or of a scene without gradients) set gs_params.forward_only: the kernels skip
     the backward's scratch (checkpoints, binning flags, per-Gaussian work lists) and the blend's backward
-    bookkeeping.  Image, depth, radii and the instance count equal the training render's, for render() and
-    the batched render_views."""
+    bookkeeping; on grids over 2048 tiles (1080p: the two-level binning) their lists also carry the Gaussian
+    ids alone (no binning slots).  Image, depth, radii and the instance count equal the training render's,
+    for render() and the batched render_views."""
     from dge_amd.cameras import orbit_camera
     from dge_amd.gaussian_renderer import PipelineParams, render
     from dge_amd.multiview import render_views
     from dge_amd.scene import synthetic_scene
 
     dev = torch.device("cuda")
-    W, H = 320, 256
     cams = [orbit_camera(k, 3, W, H, device=dev) for k in range(3)]
     bg = torch.tensor([0.1, 0.2, 0.3], device=dev)
-    sc = synthetic_scene(120_000, sh_degree=3, seed=6, device=dev).requires_grad_(True)
+    sc = synthetic_scene(P, sh_degree=3, seed=6, device=dev).requires_grad_(True)
     train = [render(c, sc, PipelineParams(), bg) for c in cams]
     train_views = render_views(cams, sc, PipelineParams(), bg, streams=3)
     with torch.no_grad():
