@@ -93,6 +93,11 @@ bool tile_sort_unfused() {
     const char* e = getenv("DGE_AMD_TILE_SORT");
     return e && !strcmp(e, "2pass");
 }
+// the two-level binning (column-ordered emission, row pass) for a gx x gy grid (grids over 2048 tiles:
+// at c2's 1024 it measured slower than the single-pass tile sort, emit 32 -> 52 us)
+bool two_level(int gx, int gy) {
+    return tile_sort_fused(gx, gy) && rect_packable(gx, gy) && !tile_sort_unfused();
+}
 
 // depth-sort bits (three passes of kDepthPassBits; DGE_AMD_DEPTH_SORT_BITS overrides, for probes)
 int depth_sort_bits() {
@@ -433,8 +438,7 @@ int bin_after_preprocess(FwdState& f, hipStream_t stream) {
     ea.scan_sums = at<uint32_t>(geom, gl.scan_sums);
     ea.first_slot = at<uint32_t>(geom, gl.first_slot);
     ea.scan_blocks = gl.scan_blocks;
-    ea.xhist = tile_sort_fused(g.gx, g.gy) && pa.rect_packed && !tile_sort_unfused() ? at<uint32_t>(geom, gl.emit_hist)
-                                                                                    : nullptr;
+    ea.xhist = two_level(g.gx, g.gy) && pa.rect_packed ? at<uint32_t>(geom, gl.emit_hist) : nullptr;
     { StageScope sc(ST_SCAN, stream); launch_scan_reduce(ea, stream); }
     GS_LAUNCHED("instance scan");
     return GS_OK;
@@ -531,7 +535,7 @@ int bin_emit(FwdState& f, void* bin, uint32_t K_layout, const uint32_t* n_dev, h
     if (ea.xhist) {  // two-level binning (tile_sort_fused): column-ordered emission, row pass, ranges
         ea.ids_only = f.ids_only = !bwd && f.ids_ok;
         ea.tile_key = at<uint32_t>(bin, bl.key1);
-        ea.pairs_out = at<uint2>(bin, bl.pair1);
+        ea.pairs_out = at<uint2>(bin, bl.point_pairs == bl.pair1 ? bl.pair0 : bl.pair1);  // (not the row pass's output)
         ea.xtotals = at<uint32_t>(bin, bl.sort_totals);
         ea.tile_count = at<uint32_t>(bin, bl.tile_count);
         ea.ntiles = g.tiles;
@@ -539,7 +543,7 @@ int bin_emit(FwdState& f, void* bin, uint32_t K_layout, const uint32_t* n_dev, h
         { StageScope sc(ST_EMIT, stream); launch_emit_fused(ea, stream); }
         { StageScope sc(ST_TILE_SORT, stream);
         launch_row_pass(ea, K_layout, at<uint2>(bin, bl.point_pairs), at<uint32_t>(bin, bl.sort_hist), bl.sort_blocks,
-                        at<uint2>(img, il.ranges), stream, n_dev); }
+                        at<uint2>(img, il.ranges), at<uint32_t>(img, il.tile_order), stream, n_dev); }
         GS_LAUNCHED("two-level binning");
         return GS_OK;
     }
@@ -945,8 +949,8 @@ int gs_rasterize_forward_end(gs_forward_state* state, float* out_color, float* o
         int K = 0;
         int rc = bin_end(f, alloc, alloc_ctx, stream, &bin, &K);
         if (rc) return rc;
-        rc = render_launch(f, bin, (uint32_t)K, K > 0 && tile_sort_writes_ranges(g.tiles) ? 1 : 0, out_color,
-                           out_depth, stream);
+        rc = render_launch(f, bin, (uint32_t)K, K > 0 && (tile_sort_writes_ranges(g.tiles) || f.ea.xhist) ? 1 : 0,
+                           out_color, out_depth, stream);
         if (rc) return rc;
         *num_rendered = K;
         return GS_OK;
@@ -1075,7 +1079,7 @@ bool can_speculate(const FwdState& f) {
     const Grid& g = f.g;
     if (f.s.debug || force_depth_keys32()) return false;
     if (tile_sort_writes_ranges(g.tiles)) return true;  // single-pass tile sort
-    return tile_sort_fused(g.gx, g.gy) && rect_packable(g.gx, g.gy) && !tile_sort_unfused();  // two-level binning
+    return two_level(g.gx, g.gy);  // two-level binning
 }
 }  // namespace
 
@@ -1200,16 +1204,17 @@ int gs_views_forward(int n, const gs_settings* const* s, const gs_params* const*
                 const uint32_t* counters = at<uint32_t>(f.img, img_layout(g.W, g.H).counters);
                 rc = bin_emit(f, h->bin[v], h->layout[v], counters, stream);
                 if (rc) return rc;
-                rc = render_launch(f, h->bin[v], h->layout[v], tile_sort_writes_ranges(g.tiles) ? 1 : 0, out_color[v],
-                                   out_depth[v], stream);
+                rc = render_launch(f, h->bin[v], h->layout[v], tile_sort_writes_ranges(g.tiles) || f.ea.xhist ? 1 : 0,
+                                   out_color[v], out_depth[v], stream);
             } else {
                 int K = 0;
                 rc = bin_end(f, alloc, alloc_ctx, stream, &h->bin[v], &K, 16 + v);
                 if (rc) return rc;
                 h->K[v] = K;
                 h->layout[v] = (uint32_t)K;
-                rc = render_launch(f, h->bin[v], (uint32_t)K, K > 0 && tile_sort_writes_ranges(g.tiles) ? 1 : 0,
-                                   out_color[v], out_depth[v], stream);
+                rc = render_launch(f, h->bin[v], (uint32_t)K,
+                                   K > 0 && (tile_sort_writes_ranges(g.tiles) || f.ea.xhist) ? 1 : 0, out_color[v],
+                                   out_depth[v], stream);
             }
             if (rc) return rc;
         }

@@ -320,8 +320,9 @@ void launch_scan_emit(const EmitArgs& a, hipStream_t s);
 // two-level binning after the instance count is known: column scan + k_scan_emit_x, the row pass
 // (pairs_out/tile_key -> point_pairs, per-tile counts), ranges from the counts
 void launch_emit_fused(const EmitArgs& a, hipStream_t s);
+// (tile_order: also the forward's longest-list-first dispatch order, from the same counts)
 void launch_row_pass(const EmitArgs& a, uint32_t K, uint2* point_pairs, uint32_t* hist, int sort_blocks,
-                     uint2* ranges, hipStream_t s, const uint32_t* n_dev = nullptr);
+                     uint2* ranges, uint32_t* tile_order, hipStream_t s, const uint32_t* n_dev = nullptr);
 
 // tile ranges; also zeroes the backward's per-slot record flags (u32 per slot)
 void launch_ranges(const uint32_t* sorted_tile, int K, uint2* ranges, uint32_t* rec_flags32, hipStream_t s);

@@ -165,10 +165,22 @@ __global__ __launch_bounds__(1024) void k_tile_order(const uint2* __restrict__ r
     if (tid < kClasses) cnt[tid] = 0u;
     __syncthreads();
     auto cls = [](uint32_t len) { return min(kClasses - 1, (int)(__log2f((float)len + 1.0f) * 3.0f)); };
-    for (int t = tid; t < tiles; t += 1024) {
+    // (each thread's ranges loaded at once: grids up to 16 x 1024 tiles in one round trip)
+    constexpr int kPer = 16;
+    uint32_t len[kPer];
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+        const int t = tid + 1024 * i;
+        const uint2 r = t < tiles ? ranges[t] : make_uint2(0u, 0u);
+        len[i] = r.y - r.x;
+    }
+    for (int t = tid + 1024 * kPer; t < tiles; t += 1024) {  // (larger grids)
         const uint2 r = ranges[t];
         atomicAdd(&cnt[cls(r.y - r.x)], 1u);
     }
+#pragma unroll
+    for (int i = 0; i < kPer; ++i)
+        if (tid + 1024 * i < tiles) atomicAdd(&cnt[cls(len[i])], 1u);
     __syncthreads();
     if (tid == 0) {  // start of each class, longest class first
         uint32_t run = 0;
@@ -179,7 +191,12 @@ __global__ __launch_bounds__(1024) void k_tile_order(const uint2* __restrict__ r
         }
     }
     __syncthreads();
-    for (int t = tid; t < tiles; t += 1024) {
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+        const int t = tid + 1024 * i;
+        if (t < tiles) order[atomicAdd(&cnt[cls(len[i])], 1u)] = (uint32_t)t;
+    }
+    for (int t = tid + 1024 * kPer; t < tiles; t += 1024) {
         const uint2 r = ranges[t];
         order[atomicAdd(&cnt[cls(r.y - r.x)], 1u)] = (uint32_t)t;
     }

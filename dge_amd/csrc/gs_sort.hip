@@ -217,21 +217,52 @@ __global__ __launch_bounds__(256) void k_radix_digit_scan_dm(uint32_t* __restric
     __shared__ uint32_t lds4[4];
     uint32_t* row = hist + (size_t)blockIdx.x * nb;  // (digit-major: the row pitch stays the grid's nb)
     if (n_dev) nb = max(1, div_up_u(dev_count(n_dev, cap), (uint32_t)tile));
-    const int per = (nb + 255) / 256;
-    const int beg = threadIdx.x * per;
+    // each wave scans a contiguous quarter of the row in coalesced 64-element chunks (loads issued
+    // kB chunks at a time): the wave's sum, the waves' prefix through LDS, then each chunk's
+    // 64-lane scan carried from chunk to chunk (c4's row pass: 10.4k rows per digit)
+    constexpr int kB = 16;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int nchunk = (nb + 63) / 64, cpw = (nchunk + 3) / 4;  // chunks per wave
+    const int c0 = w * cpw, c1 = min(nchunk, c0 + cpw);
     uint32_t s = 0;
-    for (int i = 0; i < per; ++i) {
-        const int j = beg + i;
-        if (j < nb) s += row[j];
+    for (int cb = c0; cb < c1; cb += kB) {
+        uint32_t v[kB];
+#pragma unroll
+        for (int i = 0; i < kB; ++i) {
+            const int j = (cb + i) * 64 + lane;
+            v[i] = cb + i < c1 && j < nb ? row[j] : 0u;
+        }
+#pragma unroll
+        for (int i = 0; i < kB; ++i) s += v[i];
     }
-    uint32_t total;
-    uint32_t run = block_exclusive_scan(s, lds4, total);
-    for (int i = 0; i < per; ++i) {
-        const int j = beg + i;
-        if (j < nb) {
-            const uint32_t c = row[j];
-            row[j] = run;
-            run += c;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) s += (uint32_t)__shfl_xor((int)s, o);
+    if (lane == 0) lds4[w] = s;
+    __syncthreads();
+    uint32_t run = 0, total = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        run += i < w ? lds4[i] : 0u;
+        total += lds4[i];
+    }
+    for (int cb = c0; cb < c1; cb += kB) {
+        uint32_t v[kB];
+#pragma unroll
+        for (int i = 0; i < kB; ++i) {
+            const int j = (cb + i) * 64 + lane;
+            v[i] = cb + i < c1 && j < nb ? row[j] : 0u;
+        }
+#pragma unroll
+        for (int i = 0; i < kB; ++i) {
+            uint32_t x = v[i];
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t y = (uint32_t)__shfl_up((int)x, o);
+                if (lane >= o) x += y;
+            }
+            const int j = (cb + i) * 64 + lane;
+            if (cb + i < c1 && j < nb) row[j] = run + x - v[i];
+            run += (uint32_t)__shfl((int)x, 63);
         }
     }
     if (threadIdx.x == 0) totals[blockIdx.x] = total;
@@ -809,22 +840,50 @@ __global__ __launch_bounds__(256) void k_scan_emit_x(EmitArgs a) {
 // Tile ranges from the per-tile instance counts (one workgroup): an exclusive
 // scan in tile order — the ranges identifyTileRanges (rasterizer_impl.cu:105-125)
 // finds in the sorted keys; empty tiles keep (0, 0).
+// Each thread's run of counts is loaded at once into registers (one memory round trip instead of one
+// per count).  Two-level grids have at most 128 x 128 tiles.  Also the forward's dispatch order
+// (k_tile_order's: tiles by list length, longest first) from the same counts, when tile_order is set.
+constexpr int kRangesPer = kXDigits * kXDigits / 256;
 __global__ __launch_bounds__(256) void k_ranges_counts(const uint32_t* __restrict__ count, int tiles,
-                                                       uint2* __restrict__ ranges) {
+                                                       uint2* __restrict__ ranges, uint32_t* __restrict__ tile_order) {
     __shared__ uint32_t lds4[4];
+    constexpr int kClasses = 64;
+    __shared__ uint32_t s_cls[kClasses];
+    auto cls = [](uint32_t len) { return min(kClasses - 1, (int)(__log2f((float)len + 1.0f) * 3.0f)); };
+    if (threadIdx.x < kClasses) s_cls[threadIdx.x] = 0u;
     const int per = (tiles + 255) / 256, t0 = threadIdx.x * per;
+    uint32_t c[kRangesPer];
     uint32_t s = 0;
-    for (int i = 0; i < per; ++i)
-        if (t0 + i < tiles) s += count[t0 + i];
+#pragma unroll
+    for (int i = 0; i < kRangesPer; ++i) c[i] = i < per && t0 + i < tiles ? count[t0 + i] : 0u;
+#pragma unroll
+    for (int i = 0; i < kRangesPer; ++i) s += c[i];
     uint32_t all;
     uint32_t run = block_exclusive_scan(s, lds4, all);
-    for (int i = 0; i < per; ++i) {
+#pragma unroll
+    for (int i = 0; i < kRangesPer; ++i) {
         const int t = t0 + i;
-        if (t < tiles) {
-            const uint32_t c = count[t];
-            ranges[t] = c ? make_uint2(run, run + c) : make_uint2(0u, 0u);
-            run += c;
+        if (i < per && t < tiles) {
+            ranges[t] = c[i] ? make_uint2(run, run + c[i]) : make_uint2(0u, 0u);
+            run += c[i];
+            if (tile_order) atomicAdd(&s_cls[cls(c[i])], 1u);
         }
+    }
+    if (!tile_order) return;
+    __syncthreads();
+    if (threadIdx.x == 0) {  // start of each class, longest class first
+        uint32_t acc = 0;
+        for (int k = kClasses - 1; k >= 0; --k) {
+            const uint32_t m = s_cls[k];
+            s_cls[k] = acc;
+            acc += m;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < kRangesPer; ++i) {
+        const int t = t0 + i;
+        if (i < per && t < tiles) tile_order[atomicAdd(&s_cls[cls(c[i])], 1u)] = (uint32_t)t;
     }
 }
 
@@ -840,13 +899,13 @@ void launch_emit_fused(const EmitArgs& a, hipStream_t s) {
 }
 
 void launch_row_pass(const EmitArgs& a, uint32_t K, uint2* point_pairs, uint32_t* hist, int sort_blocks,
-                     uint2* ranges, hipStream_t s, const uint32_t* n_dev) {
+                     uint2* ranges, uint32_t* tile_order, hipStream_t s, const uint32_t* n_dev) {
     if (a.P <= 0 || K == 0) return;
     // second level: the stable row pass (digit y), counting instances per tile on the way
     RangeOut ro{nullptr, nullptr, a.ntiles, a.tile_count, a.gx};
     radix_pass<kXBits, kSortIPT>(a.tile_key, a.pairs_out, nullptr, point_pairs, nullptr, K, kXBits, false,
                                  a.ids_only ? kValU32 : kValPair, hist, a.xtotals, sort_blocks, ro, nullptr, s, n_dev);
-    hipLaunchKernelGGL(k_ranges_counts, dim3(1), dim3(256), 0, s, a.tile_count, a.ntiles, ranges);
+    hipLaunchKernelGGL(k_ranges_counts, dim3(1), dim3(256), 0, s, a.tile_count, a.ntiles, ranges, tile_order);
 }
 
 void launch_scan_reduce(const EmitArgs& a, hipStream_t s) {
