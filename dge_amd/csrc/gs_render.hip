@@ -278,7 +278,9 @@ __global__ __launch_bounds__(64, 3) void k_render_fwd(RenderArgs a) {
         for (int i = 0; i < 4; ++i) {
             const uint32_t k = b + 64 * i + lane;
             const uint32_t kc = k < range.y ? k : k_last;
-            ids[i] = list_empty ? 0u : a.point_ids ? a.point_ids[kc] : a.point_pairs[kc].x;
+            // (id-only lists come from forward-only binnings: only the !BWD blend reads them)
+            if constexpr (BWD) ids[i] = list_empty ? 0u : a.point_pairs[kc].x;
+            else ids[i] = list_empty ? 0u : a.point_ids ? a.point_ids[kc] : a.point_pairs[kc].x;
         }
     };
     uint32_t ids[4], cid[4];  // cid: the ids of the entries in `cur` (the touched bytes at the round's end)
