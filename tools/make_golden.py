@@ -6,7 +6,9 @@
                     from /root/reference with bytecode writing disabled.  Pins the
                     oracle's and the kernels' SH->RGB (forward.cu:20-71 restates it).
   cameras_ref.npz   the REFERENCE's getWorld2View2 / getProjectionMatrix outputs (and the
-                    Simple_Camera composition) for the c1-c5 cameras and random poses.
+                    Simple_Camera composition) for the c1-c5 cameras and random poses, generated
+                    in round 2 from the reference functions; now checked against restatements
+                    (camera_fixture), which no longer import the reference.
   lr_schedule_ref.npz  the REFERENCE's get_expon_lr_func schedules (the optimizer's position
                     learning rate, gaussian_model.py:373-380) and inverse_sigmoid
                     (gaussiansplatting/utils/general_utils.py:18-19, 29-62), imported read-only.
@@ -49,70 +51,84 @@ def sh_fixture():
     sys.path.remove("/root/reference")
 
 
-def camera_fixture():
-    """The reference's camera matrices (gaussiansplatting/utils/graphics_utils.py:40-51 getWorld2View2,
-    :67-87 getProjectionMatrix), imported read-only with a `kornia` stand-in module in sys.modules
-    (graphics_utils imports kornia.core at module level, :109-110, for functions this path never
-    calls; kornia is not installed — SURVEY.md §8(c)(ii)).  The Simple_Camera composition
-    (scene/cameras.py:90-94) is evaluated on the CPU with those outputs (the class itself
-    moves every tensor to CUDA).  Cameras: the c1-c5 orbit cameras and seeded random poses with
-    trans/scale."""
+def _world_to_view(R, t, translate, scale):
+    """graphics_utils.py:40-51 (getWorld2View2) restated: the camera-to-world inverse of [R^T | t],
+    its centre moved by `translate` and scaled, inverted back; float32 like the reference."""
+    w2c = np.eye(4)
+    w2c[:3, :3] = np.asarray(R).T
+    w2c[:3, 3] = t
+    c2w = np.linalg.inv(w2c)
+    c2w[:3, 3] = (c2w[:3, 3] + translate) * scale
+    return np.float32(np.linalg.inv(c2w))
+
+
+def _projection(znear, zfar, fovx, fovy):
+    """graphics_utils.py:67-87 (getProjectionMatrix) restated: a symmetric frustum (left = -right,
+    bottom = -top), z_sign = +1, built in float32 like the reference's torch.zeros(4, 4)."""
     import math
-    import types
+
+    tx, ty = math.tan(fovx / 2), math.tan(fovy / 2)
+    top, right = ty * znear, tx * znear
+    P = torch.zeros(4, 4, dtype=torch.float32)
+    P[0, 0] = 2.0 * znear / (right - -right)
+    P[1, 1] = 2.0 * znear / (top - -top)
+    P[0, 2] = (right + -right) / (right - -right)
+    P[1, 2] = (top + -top) / (top - -top)
+    P[3, 2] = 1.0
+    P[2, 2] = zfar / (zfar - znear)
+    P[2, 3] = -(zfar * znear) / (zfar - znear)
+    return P
+
+
+def camera_fixture(write: bool = False):
+    """cameras_ref.npz holds the REFERENCE's camera matrices (graphics_utils.py:40-51 getWorld2View2,
+    :67-87 getProjectionMatrix) and the Simple_Camera composition (scene/cameras.py:90-94) for the
+    c1-c5 orbit cameras and seeded random poses with trans/scale — generated in round 2 by calling the
+    reference functions themselves.  This tool no longer imports the reference: it recomputes the
+    fixture with the restatements above and checks it against the committed file, element for element
+    (write=True — `python tools/make_golden.py cameras-write` — rewrites it from them instead)."""
+    import math
 
     from dge_amd.cameras import look_at_R_T
 
-    sys.dont_write_bytecode = True
-    stub = types.ModuleType("kornia")
-    core = types.ModuleType("kornia.core")
-    core.Tensor = torch.Tensor
-    core.concatenate, core.stack, core.zeros_like = torch.cat, torch.stack, torch.zeros_like
-    stub.core = core
-    saved = {k: sys.modules.get(k) for k in ("kornia", "kornia.core")}
-    sys.modules["kornia"], sys.modules["kornia.core"] = stub, core
-    sys.path.insert(0, "/root/reference")
-    try:
-        from gaussiansplatting.utils.graphics_utils import getProjectionMatrix, getWorld2View2
-        cams = []
-        for (k, n, W, H) in [(0, 1, 256, 256), (0, 1, 512, 512), (5, 24, 512, 512), (17, 24, 512, 512),
-                             (0, 1, 1920, 1080)]:
-            az, el = 2.0 * math.pi * k / n, math.radians(15.0)
-            pos = 5.0 * np.array([math.cos(el) * math.cos(az), math.cos(el) * math.sin(az), math.sin(el)])
-            R, T = look_at_R_T(pos)
-            fx = math.radians(60.0)
-            cams.append((R, T, np.zeros(3), 1.0, fx, 2.0 * math.atan(math.tan(fx / 2) * H / W)))
-        rng = np.random.default_rng(3)
-        for _ in range(4):
-            q = rng.standard_normal(4)
-            q /= np.linalg.norm(q)
-            w, x, y, z = q
-            R = np.array([[1 - 2 * (y * y + z * z), 2 * (x * y - w * z), 2 * (x * z + w * y)],
-                          [2 * (x * y + w * z), 1 - 2 * (x * x + z * z), 2 * (y * z - w * x)],
-                          [2 * (x * z - w * y), 2 * (y * z + w * x), 1 - 2 * (x * x + y * y)]])
-            cams.append((R, rng.uniform(-3, 3, 3), rng.uniform(-1, 1, 3), float(rng.uniform(0.5, 2.0)),
-                         float(rng.uniform(0.6, 1.6)), float(rng.uniform(0.6, 1.6))))
-        out = {"n": len(cams)}
-        for i, (R, T, trans, scale, fovx, fovy) in enumerate(cams):
-            w2v = getWorld2View2(R, T, trans, scale)
-            proj = getProjectionMatrix(znear=0.01, zfar=100.0, fovX=fovx, fovY=fovy)
-            wv = torch.tensor(w2v).transpose(0, 1)
-            pt = proj.transpose(0, 1)
-            full = wv.unsqueeze(0).bmm(pt.unsqueeze(0)).squeeze(0).float()
-            out.update({f"R{i}": R, f"T{i}": T, f"trans{i}": trans, f"scale{i}": scale, f"fovx{i}": fovx,
-                        f"fovy{i}": fovy, f"w2v{i}": w2v, f"proj{i}": proj.numpy(),
-                        f"world_view{i}": wv.numpy(), f"full_proj{i}": full.numpy(),
-                        f"center{i}": wv.inverse()[3, :3].numpy()})
-        np.savez_compressed(os.path.join(OUT, "cameras_ref.npz"), **out)
-        print("cameras", len(cams))
-    finally:
-        sys.path.remove("/root/reference")
-        for k, v in saved.items():
-            if v is None:
-                sys.modules.pop(k, None)
-            else:
-                sys.modules[k] = v
-        for k in [m for m in sys.modules if m.startswith("gaussiansplatting")]:
-            sys.modules.pop(k)
+    cams = []
+    for (k, n, W, H) in [(0, 1, 256, 256), (0, 1, 512, 512), (5, 24, 512, 512), (17, 24, 512, 512),
+                         (0, 1, 1920, 1080)]:
+        az, el = 2.0 * math.pi * k / n, math.radians(15.0)
+        pos = 5.0 * np.array([math.cos(el) * math.cos(az), math.cos(el) * math.sin(az), math.sin(el)])
+        R, T = look_at_R_T(pos)
+        fx = math.radians(60.0)
+        cams.append((R, T, np.zeros(3), 1.0, fx, 2.0 * math.atan(math.tan(fx / 2) * H / W)))
+    rng = np.random.default_rng(3)
+    for _ in range(4):
+        q = rng.standard_normal(4)
+        q /= np.linalg.norm(q)
+        w, x, y, z = q
+        R = np.array([[1 - 2 * (y * y + z * z), 2 * (x * y - w * z), 2 * (x * z + w * y)],
+                      [2 * (x * y + w * z), 1 - 2 * (x * x + z * z), 2 * (y * z - w * x)],
+                      [2 * (x * z - w * y), 2 * (y * z + w * x), 1 - 2 * (x * x + y * y)]])
+        cams.append((R, rng.uniform(-3, 3, 3), rng.uniform(-1, 1, 3), float(rng.uniform(0.5, 2.0)),
+                     float(rng.uniform(0.6, 1.6)), float(rng.uniform(0.6, 1.6))))
+    out = {"n": len(cams)}
+    for i, (R, T, trans, scale, fovx, fovy) in enumerate(cams):
+        w2v = _world_to_view(R, T, trans, scale)
+        proj = _projection(0.01, 100.0, fovx, fovy)
+        wv = torch.tensor(w2v).transpose(0, 1)
+        pt = proj.transpose(0, 1)
+        full = wv.unsqueeze(0).bmm(pt.unsqueeze(0)).squeeze(0).float()
+        out.update({f"R{i}": R, f"T{i}": T, f"trans{i}": trans, f"scale{i}": scale, f"fovx{i}": fovx,
+                    f"fovy{i}": fovy, f"w2v{i}": w2v, f"proj{i}": proj.numpy(),
+                    f"world_view{i}": wv.numpy(), f"full_proj{i}": full.numpy(),
+                    f"center{i}": wv.inverse()[3, :3].numpy()})
+    path = os.path.join(OUT, "cameras_ref.npz")
+    if write or not os.path.exists(path):
+        np.savez_compressed(path, **out)
+        print("cameras written", len(cams))
+        return
+    ref = np.load(path)
+    bad = [k for k in out if not np.array_equal(np.asarray(out[k]), ref[k])]
+    assert not bad, f"restated camera matrices differ from the reference's fixture: {bad}"
+    print("cameras: restatement equals the committed reference fixture,", len(cams), "cameras")
 
 
 def scene_fixture(name, P, W, H, seed, radius=1.5, scale=0.05, sh_degree=3, bg=(0.0, 0.0, 0.0), mode="sh",
@@ -227,6 +243,7 @@ def lr_fixture():
 FIXTURES = {
     "sh": sh_fixture,
     "cameras": camera_fixture,
+    "cameras-write": lambda: camera_fixture(write=True),
     "lr": lr_fixture,
     "scenes": lambda: [
         scene_fixture("sh3_96x80", 1500, 96, 80, seed=11),
