@@ -360,9 +360,15 @@ def _spread(xs):
     a = np.asarray(xs, dtype=np.float64)
     if a.size == 0:
         return None
-    return {"p50": round(float(np.percentile(a, 50)), 4), "p90": round(float(np.percentile(a, 90)), 4),
-            "min": round(float(a.min()), 4), "max": round(float(a.max()), 4), "argmax": int(a.argmax()),
-            "max_over_p50": round(float(a.max() / max(np.percentile(a, 50), 1e-9)), 3)}
+    out = {"p50": round(float(np.percentile(a, 50)), 4), "p90": round(float(np.percentile(a, 90)), 4),
+           "min": round(float(a.min()), 4), "max": round(float(a.max()), 4), "argmax": int(a.argmax()),
+           "max_over_p50": round(float(a.max() / max(np.percentile(a, 50), 1e-9)), 3)}
+    if a.size > 2:
+        # the first timed step starts from the drained GPU the timing contract's synchronize leaves, so
+        # it also carries the host's issue time to its first launch: the spread of the others beside it
+        rest = a[1:]
+        out["max_over_p50_after_first"] = round(float(rest.max() / max(np.percentile(rest, 50), 1e-9)), 3)
+    return out
 
 
 def run_views(args, cams, scene, pipe, bg, seeds, bucket, streams=None, min_world=None):
