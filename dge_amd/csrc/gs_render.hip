@@ -231,9 +231,6 @@ __global__ __launch_bounds__(64, 3) void k_render_fwd(RenderArgs a) {
     const int qidx = 4 * tile + quad;
     const int tx = tile % a.gx, ty = tile / a.gx;
     const int lane = threadIdx.x;
-#ifdef GS_FWD_PRIO_RANKS
-    if (rank < GS_FWD_PRIO_RANKS) __builtin_amdgcn_s_setprio(3);
-#endif
     const int bx0 = tx * kTile + (quad & 1) * kQuad, by0 = ty * kTile + (quad >> 1) * kQuad;
     const int px = bx0 + (lane & 7), py = by0 + (lane >> 3);
     const bool inside = px < a.W && py < a.H;
