@@ -124,23 +124,30 @@ class GradBucket:
                 or any(h is None or h.dtype != torch.uint8 or h.shape != (n,) for h in hints)):
             self._pending = ("scan", group)  # no usable hint: allreduce() in allreduce_end
             return
-        live = hints[0].clone()
-        for h in hints[1:]:
-            live |= h
-        dist.all_reduce(live, op=dist.ReduceOp.MAX, group=group)
         from . import _native as N
 
         dev = self.flat.device
-        idx = torch.empty(n, dtype=torch.int64, device=dev)
-        cs = torch.empty(1 + (n + 1023) // 1024, dtype=torch.int64, device=dev)
-        stream = torch.cuda.current_stream(dev)
-        N.check(N.lib().gs_rows_compact(live.data_ptr(), n, idx.data_ptr(), cs.data_ptr(),
-                                        ctypes.c_void_p(stream.cuda_stream)), "gs_rows_compact")
-        pinned = getattr(self, "_count_host", None)
-        if pinned is None:
-            pinned = self._count_host = torch.empty(1, dtype=torch.int64, pin_memory=True)
-        pinned.copy_(cs[:1], non_blocking=True)
-        self._pending = ("hint", group, idx, pinned, stream.record_event(), n, mats)
+        # on a side stream behind the forwards (which set the marks): the backward the caller enqueues
+        # next on the current stream does not wait for the MAX collective and the compaction
+        main = torch.cuda.current_stream(dev)
+        side = _collective_stream(dev) if self.flat.is_cuda else main
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            live = hints[0].clone()
+            for h in hints[1:]:
+                live |= h
+            dist.all_reduce(live, op=dist.ReduceOp.MAX, group=group)
+            idx = torch.empty(n, dtype=torch.int64, device=dev)
+            cs = torch.empty(1 + (n + 1023) // 1024, dtype=torch.int64, device=dev)
+            N.check(N.lib().gs_rows_compact(live.data_ptr(), n, idx.data_ptr(), cs.data_ptr(),
+                                            ctypes.c_void_p(side.cuda_stream)), "gs_rows_compact")
+            pinned = getattr(self, "_count_host", None)
+            if pinned is None:
+                pinned = self._count_host = torch.empty(1, dtype=torch.int64, pin_memory=True)
+            pinned.copy_(cs[:1], non_blocking=True)
+            ev = side.record_event()
+        idx.record_stream(main)  # (read on the current stream by allreduce_end)
+        self._pending = ("hint", group, idx, pinned, ev, n, mats)
 
     def allreduce_end(self, stream=None):
         """Second half of allreduce_begin (after the backward): the packed SUM of the agreed rows.
@@ -156,6 +163,7 @@ class GradBucket:
         _, group, idx, pinned, ev, n, mats = pend
         ev.synchronize()  # the forwards' union is agreed: no wait for the backward
         m = int(pinned.item())
+        torch.cuda.current_stream(self.flat.device).wait_event(ev)  # (idx is written on the side stream)
         self.wait_zero()
         if not self.check_attached():
             for p, v in zip(self.params, self.views):
