@@ -86,15 +86,20 @@ __global__ __launch_bounds__(kRowsBlock) void k_rows_live(RowsLaunch a, long lon
 // wave's loads are issued before its stores; no index division.
 constexpr int kRowsPerWave = 8;
 
+// m_dev (the _dev entry points): the packed buffer has m rows (the capacity), the row list only
+// min(m, *m_dev) — a gather zero-fills the packed rows past it, a scatter leaves them
 template <bool GATHER>
 __global__ __launch_bounds__(256) void k_rows_move(RowsLaunch a, const long long* __restrict__ rows, long long m,
-                                                   float* __restrict__ packed) {
+                                                   float* __restrict__ packed, const long long* __restrict__ m_dev) {
     const long long i0 = ((long long)blockIdx.x * 4 + (threadIdx.x >> 6)) * kRowsPerWave;
     if (i0 >= m) return;
-    const int nrow = m - i0 < kRowsPerWave ? (int)(m - i0) : kRowsPerWave;
+    const long long mv = m_dev ? (*m_dev < m ? *m_dev : m) : m;  // rows with a list entry
+    if (!GATHER && i0 >= mv) return;
+    const int ncap = m - i0 < kRowsPerWave ? (int)(m - i0) : kRowsPerWave;  // packed rows of this wave
+    const int nrow = mv - i0 <= 0 ? 0 : mv - i0 < kRowsPerWave ? (int)(mv - i0) : kRowsPerWave;
     long long row[kRowsPerWave];
 #pragma unroll
-    for (int u = 0; u < kRowsPerWave; ++u) row[u] = rows[i0 + (u < nrow ? u : 0)];
+    for (int u = 0; u < kRowsPerWave; ++u) row[u] = nrow ? rows[i0 + (u < nrow ? u : 0)] : 0;
     for (int c = threadIdx.x & 63; c < a.width; c += 64) {
         int k = 0;
 #pragma unroll
@@ -105,10 +110,10 @@ __global__ __launch_bounds__(256) void k_rows_move(RowsLaunch a, const long long
         float v[kRowsPerWave];
         if (GATHER) {
 #pragma unroll
-            for (int u = 0; u < kRowsPerWave; ++u) v[u] = col[row[u] * w];
+            for (int u = 0; u < kRowsPerWave; ++u) v[u] = col[row[u] * w];  // (row[u] is a valid row)
 #pragma unroll
             for (int u = 0; u < kRowsPerWave; ++u)
-                if (u < nrow) out[(long long)u * a.width] = v[u];
+                if (u < ncap) out[(long long)u * a.width] = u < nrow ? v[u] : 0.f;
         } else {
 #pragma unroll
             for (int u = 0; u < kRowsPerWave; ++u) v[u] = out[(long long)(u < nrow ? u : 0) * a.width];
@@ -224,7 +229,7 @@ extern "C" int gs_rows_live(const gs_rows_region* regions, int nreg, long long n
 }
 
 static int rows_move(const gs_rows_region* regions, int nreg, const long long* rows, long long m, float* packed,
-                     gs_stream_t stream, bool gather, const char* fn) {
+                     gs_stream_t stream, bool gather, const char* fn, const long long* m_dev = nullptr) {
     using namespace gs;
     RowsLaunch a;
     if (int rc = rows_launch(regions, nreg, a, fn)) return rc;
@@ -234,10 +239,10 @@ static int rows_move(const gs_rows_region* regions, int nreg, const long long* r
     if (blocks > 0x7FFFFFFF) return report_error(GS_ERR_INVALID_ARG, fn);
     if (gather)
         hipLaunchKernelGGL(k_rows_move<true>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, a, rows, m,
-                           packed);
+                           packed, m_dev);
     else
         hipLaunchKernelGGL(k_rows_move<false>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, a, rows, m,
-                           packed);
+                           packed, m_dev);
     return launched();
 }
 
@@ -250,6 +255,19 @@ extern "C" int gs_rows_scatter(const gs_rows_region* regions, int nreg, const lo
                                const float* packed, gs_stream_t stream) {
     return rows_move(regions, nreg, rows, m, const_cast<float*>(packed), stream, false,
                      "gs_rows_scatter: bad arguments");
+}
+
+extern "C" int gs_rows_gather_dev(const gs_rows_region* regions, int nreg, const long long* rows, long long cap,
+                                  const long long* count, float* packed, gs_stream_t stream) {
+    if (!count) return gs::report_error(GS_ERR_INVALID_ARG, "gs_rows_gather_dev: count is required");
+    return rows_move(regions, nreg, rows, cap, packed, stream, true, "gs_rows_gather_dev: bad arguments", count);
+}
+
+extern "C" int gs_rows_scatter_dev(const gs_rows_region* regions, int nreg, const long long* rows, long long cap,
+                                   const long long* count, const float* packed, gs_stream_t stream) {
+    if (!count) return gs::report_error(GS_ERR_INVALID_ARG, "gs_rows_scatter_dev: count is required");
+    return rows_move(regions, nreg, rows, cap, const_cast<float*>(packed), stream, false,
+                     "gs_rows_scatter_dev: bad arguments", count);
 }
 
 extern "C" int gs_rows_compact(const uint8_t* live, long long n, long long* rows, long long* count_scratch,

@@ -147,7 +147,8 @@ class GradBucket:
             pinned.copy_(cs[:1], non_blocking=True)
             ev = side.record_event()
         idx.record_stream(main)  # (read on the current stream by allreduce_end)
-        self._pending = ("hint", group, idx, pinned, ev, n, mats)
+        cs.record_stream(main)
+        self._pending = ("hint", group, idx, pinned, ev, n, mats, cs)
 
     def allreduce_end(self, stream=None):
         """Second half of allreduce_begin (after the backward): the packed SUM of the agreed rows.
@@ -160,10 +161,9 @@ class GradBucket:
             return None
         if pend[0] == "scan":
             return self.allreduce(pend[1], min_world=1)
-        _, group, idx, pinned, ev, n, mats = pend
-        ev.synchronize()  # the forwards' union is agreed: no wait for the backward
-        m = int(pinned.item())
-        torch.cuda.current_stream(self.flat.device).wait_event(ev)  # (idx is written on the side stream)
+        _, group, idx, pinned, ev, n, mats, cs = pend
+        main = torch.cuda.current_stream(self.flat.device)
+        main.wait_event(ev)  # (idx and its count are written on the collective stream)
         self.wait_zero()
         if not self.check_attached():
             for p, v in zip(self.params, self.views):
@@ -172,23 +172,46 @@ class GradBucket:
             self.attach()
         side = stream is not None and self.flat.is_cuda
         if side:
-            main = torch.cuda.current_stream(self.flat.device)
             stream.wait_stream(main)
             ctx = torch.cuda.stream(stream)
         else:
             import contextlib
 
             ctx = contextlib.nullcontext()
+        # Speculative capacity: the union's size m shapes the packed collective, and reading it on the host
+        # waits for the forwards (0.5 ms at the one-rank c2 step, the GPU that far behind).  With last
+        # step's size as a capacity (+1/8), the gather / SUM / scatter of the first min(cap, m) rows is
+        # enqueued with the count read on the device (gs_rows_gather_dev: zero rows past it, the same on
+        # every rank), and only then does the host read m — the GPU has the backward and the collective
+        # queued meanwhile.  m > cap (the union grew past the margin): the rows [cap, m) follow in a
+        # second, exact packed SUM.  m is identical on every rank (the MAX-agreed union), so is cap.
+        cap = getattr(self, "_rows_cap", 0)
+        spec = 0 < cap and 2 * cap <= n
         with ctx:
-            if 2 * m > n:  # mostly dense: packing would not pay
+            if spec:
+                packed = _rows_gather(mats, idx, cap=cap, count=cs)
+                dist.all_reduce(packed, op=dist.ReduceOp.SUM, group=group)
+                _rows_scatter(mats, idx, packed, cap=cap, count=cs)
+            ev.synchronize()
+            m = int(pinned.item())
+            if spec:
+                if m > cap:
+                    rows = idx[cap:m]
+                    packed = _rows_gather(mats, rows)
+                    dist.all_reduce(packed, op=dist.ReduceOp.SUM, group=group)
+                    _rows_scatter(mats, rows, packed)
+            elif 2 * m > n:  # mostly dense: packing would not pay
                 dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=group)
             else:
                 rows = idx[:m]
                 packed = _rows_gather(mats, rows)
                 dist.all_reduce(packed, op=dist.ReduceOp.SUM, group=group)
                 _rows_scatter(mats, rows, packed)
-                if side:  # (allocated on the side stream, freed by the caching allocator at once)
-                    rows.record_stream(stream)
+            if side:  # (allocated on the side stream, freed by the caching allocator at once)
+                idx.record_stream(stream)
+                cs.record_stream(stream)
+        self._rows_cap = m + m // 8 + 4096 if _native_ok(mats) and os.environ.get("DGE_AMD_ROWS_SPEC", "1") != "0" \
+            else 0
         self._reduced = stream.record_event() if side else None
         return None
 
@@ -264,8 +287,15 @@ def _rows_live(mats, n):
     return live
 
 
-def _rows_gather(mats, idx):
-    """[len(idx), sum(widths)]: the rows idx of every matrix, side by side."""
+def _rows_gather(mats, idx, cap=None, count=None):
+    """[len(idx), sum(widths)]: the rows idx of every matrix, side by side.  cap/count (GPU): [cap, ...]
+    holding the rows idx[:min(cap, count[0])] (count read on the device), zero rows after them."""
+    if count is not None:
+        N, regs, stream = _native_rows(mats)
+        packed = torch.empty((cap, sum(m.shape[1] for m in mats)), dtype=torch.float32, device=mats[0].device)
+        N.check(N.lib().gs_rows_gather_dev(regs, len(mats), idx.data_ptr(), cap, count.data_ptr(),
+                                           packed.data_ptr(), stream), "gs_rows_gather_dev")
+        return packed
     if _native_ok(mats):
         N, regs, stream = _native_rows(mats)
         packed = torch.empty((idx.numel(), sum(m.shape[1] for m in mats)), dtype=torch.float32,
@@ -277,8 +307,13 @@ def _rows_gather(mats, idx):
     return torch.cat([m.index_select(0, idx) for m in mats], 1)
 
 
-def _rows_scatter(mats, idx, packed):
+def _rows_scatter(mats, idx, packed, cap=None, count=None):
     """The inverse of _rows_gather: rows idx of every matrix = their columns of packed."""
+    if count is not None:
+        N, regs, stream = _native_rows(mats)
+        N.check(N.lib().gs_rows_scatter_dev(regs, len(mats), idx.data_ptr(), cap, count.data_ptr(),
+                                            packed.data_ptr(), stream), "gs_rows_scatter_dev")
+        return
     if _native_ok(mats):
         N, regs, stream = _native_rows(mats)
         idx = idx.to(torch.int64).contiguous()

@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define GS_RASTER_ABI_VERSION 12
+#define GS_RASTER_ABI_VERSION 13
 
 #define GS_OK 0
 #define GS_ERR_INVALID_ARG 1   /* AT_ERROR / std::runtime_error in the reference */
@@ -330,6 +330,14 @@ int gs_rows_scatter(const gs_rows_region *regions, int nreg, const long long *ro
  * runs: dge_amd/multiview.py GradBucket.allreduce_begin).  count_scratch holds 1 + ceil(n / 1024)
  * int64 (the rest is scratch); rows holds up to n. */
 int gs_rows_compact(const uint8_t *live, long long n, long long *rows, long long *count_scratch, gs_stream_t stream);
+/* gs_rows_gather / _scatter over a packed buffer of `cap` rows whose row list holds *count rows, the
+ * count read on the device (gs_rows_compact's count_scratch[0]): the gather zero-fills the packed rows
+ * past min(cap, *count), the scatter moves only the first min(cap, *count) — a collective shaped by a
+ * capacity instead of a host read of the count (ABI 13); rows past the capacity are the caller's. */
+int gs_rows_gather_dev(const gs_rows_region *regions, int nreg, const long long *rows, long long cap,
+                       const long long *count, float *packed, gs_stream_t stream);
+int gs_rows_scatter_dev(const gs_rows_region *regions, int nreg, const long long *rows, long long cap,
+                        const long long *count, const float *packed, gs_stream_t stream);
 
 /* Byte sizes of the opaque buffers (host arithmetic, no device work). */
 size_t gs_geometry_buffer_size(int P);

@@ -1,5 +1,5 @@
 """GPU tests of the sparse-row gradient exchange kernels (gs_rows_live / gs_rows_gather /
-gs_rows_scatter, dge_amd/csrc/gs_bucket.hip) against the torch formulation GradBucket uses on CPU:
+gs_rows_scatter and their device-count forms, dge_amd/csrc/gs_bucket.hip) against the torch formulation GradBucket uses on CPU:
 bit-exact (pure data movement and a != 0 test)."""
 import pytest
 import torch
@@ -58,6 +58,37 @@ def test_rows_live_gather_scatter_match_torch(cuda_device, n, widths, density):
     for m, m2 in zip(mats, mats2):
         exp = torch.zeros(n, m.shape[1])
         exp[idx.cpu()] = m.cpu()[idx.cpu()] * 2
+        assert torch.equal(m2.cpu().nan_to_num(7.0), exp.nan_to_num(7.0))
+
+
+@pytest.mark.parametrize("cap_over", [-1000, 0, 1, 5000, None])
+def test_rows_gather_scatter_device_count(cuda_device, cap_over):
+    """gs_rows_gather_dev / gs_rows_scatter_dev (the speculative-capacity collective): a packed buffer of
+    `cap` rows from a row list whose count is read on the device — rows past min(cap, count) packed as
+    zeros, the scatter writing back only the first min(cap, count) rows."""
+    n, widths = 200_003, (3, 45, 1, 4)
+    flat, mats = _mats(n, widths, 0.2, seed=11, device="cuda")
+    idx = torch.nonzero(mv._rows_live(mats, n)).squeeze(1)
+    m = idx.numel()
+    count = m if cap_over is not None else 0
+    cap = max(1, m + (cap_over or 0))
+    idx_pad = torch.cat([idx, torch.full((max(0, cap - m) + 7,), -5, dtype=torch.int64, device="cuda")])
+    cnt = torch.tensor([count], dtype=torch.int64, device="cuda")
+    packed = mv._rows_gather(mats, idx_pad, cap=cap, count=cnt)
+    k = min(cap, count)
+    ref = torch.zeros(cap, sum(widths))
+    ref[:k] = torch.cat([mm.cpu().index_select(0, idx[:k].cpu()) for mm in mats], 1)
+    assert torch.equal(packed.cpu().view(torch.int32), ref.view(torch.int32))
+    flat2 = torch.zeros_like(flat)
+    mats2, off = [], 0
+    for w in widths:
+        mats2.append(flat2[off:off + n * w].view(n, w))
+        off += n * w
+    mv._rows_scatter(mats2, idx_pad, packed + 1.0, cap=cap, count=cnt)
+    torch.cuda.synchronize()
+    for mm, m2 in zip(mats, mats2):
+        exp = torch.zeros(n, mm.shape[1])
+        exp[idx[:k].cpu()] = mm.cpu()[idx[:k].cpu()] + 1.0
         assert torch.equal(m2.cpu().nan_to_num(7.0), exp.nan_to_num(7.0))
 
 
@@ -120,5 +151,21 @@ def test_allreduce_begin_end_one_rank(cuda_device):
         bucket.allreduce_end()
         torch.cuda.synchronize()
         assert torch.equal(bucket.flat, before)
+        m = int(union.sum())
+        assert bucket._rows_cap > m  # the next step's speculative capacity
+        # later steps: the packed SUM at a speculative capacity (above the union, then below it: the
+        # rows past the capacity follow in the exact fix-up collective) leaves the bucket unchanged too
+        for cap in (bucket._rows_cap, m // 3):
+            bucket.zero(overlap=True)
+            outs = mv.render_views(cams, sc, PipelineParams(), torch.zeros(3, device=cuda_device), streams=3)
+            bucket.allreduce_begin([o["_live_rows"] for o in outs], min_world=1)
+            torch.autograd.backward([o["render"] for o in outs], G)
+            bucket._rows_cap = cap
+            torch.cuda.synchronize()
+            before = bucket.flat.clone()
+            assert int((mv._rows_live(mats, n) != 0).sum()) == m
+            bucket.allreduce_end()
+            torch.cuda.synchronize()
+            assert torch.equal(bucket.flat, before)
     finally:
         dist.destroy_process_group()
