@@ -99,15 +99,17 @@ __device__ __forceinline__ Entry gather_entry(const Splat* splat, uint32_t id) {
 // pixel_alpha for four consecutive entries: two packed streams (f4v ops split
 // into pairs of v_pk_* instructions), bit-identical to four pixel_alpha calls.
 // Operands arrive pre-negated where a subtraction would otherwise not pack
-// (v_pk_add_f32 has no subtract form): ncy = -conic.y, (npx, npy) = -pixel, and
-//   x + npx == x - px,   (-0.5 (a dx^2 + c dy^2)) + (ncy dx) dy == ... - (b dx) dy
-// exactly (negation is exact, a - b == a + (-b) in IEEE arithmetic).
-__device__ __forceinline__ void pixel_alpha4(f4v x, f4v y, f4v cx, f4v ncy, f4v cz, f4v op, float npx, float npy,
+// (v_pk_add_f32 has no subtract form): (nca, ncb, ncc) = -conic, (npx, npy) = -pixel, and
+//   x + npx == x - px,   0.5 ((nca dx) dx + (ncc dy) dy) + (ncb dx) dy == -0.5 (a dx^2 + c dy^2) - (b dx) dy
+// exactly (negation is exact and commutes with rounding, a - b == a + (-b) in IEEE arithmetic; the
+// one sign difference, +0 for -0 when a dx^2 == -c dy^2, gives the same G and the same tests).  With
+// +conic.x/z the compiler turned -0.5 * s + t into t - 0.5 * s: four unpacked subtractions per group.
+__device__ __forceinline__ void pixel_alpha4(f4v x, f4v y, f4v ncx, f4v ncy, f4v ncz, f4v op, float npx, float npy,
                                              f4v& dx, f4v& dy, f4v& G, f4v& alpha, bool (&ok)[4]) {
 #pragma clang fp contract(off)
     dx = x + npx;
     dy = y + npy;
-    const f4v power = -0.5f * (cx * dx * dx + cz * dy * dy) + ncy * dx * dy;
+    const f4v power = 0.5f * (ncx * dx * dx + ncz * dy * dy) + ncy * dx * dy;
     G = gs_exp4(power);
     const f4v oG = op * G;
 #pragma unroll
@@ -345,9 +347,9 @@ __global__ __launch_bounds__(64, 3) void k_render_fwd(RenderArgs a) {
                 const int slot = kslot[i];
                 s_x[slot] = cur[i].xy.x;
                 s_y[slot] = cur[i].xy.y;
-                s_cx[slot] = cur[i].co.x;
+                s_cx[slot] = -cur[i].co.x;  // (negated: pixel_alpha4)
                 s_cy[slot] = -cur[i].co.y;  // (negated: pixel_alpha4)
-                s_cz[slot] = cur[i].co.z;
+                s_cz[slot] = -cur[i].co.z;
                 s_op[slot] = cur[i].co.w;
                 s_rgbd[slot] = cur[i].f;
                 s_pos[slot] = k - range.x + 1;  // 1-based contributor index (forward.cu:331)
@@ -838,9 +840,9 @@ __global__ __launch_bounds__(64, GS_BWD_WAVES) void k_render_bwd(RenderBwdArgs a
                 const int slot = nk + __popcll(km & ~lanemask_lt() & ~(1ull << lane));
                 s_x[slot] = cur[i].xy.x;
                 s_y[slot] = cur[i].xy.y;
-                s_cx[slot] = cur[i].co.x;
-                s_cy[slot] = -cur[i].co.y;  // (negated: pixel_alpha4; finish_record negates back)
-                s_cz[slot] = cur[i].co.z;
+                s_cx[slot] = -cur[i].co.x;  // (negated: pixel_alpha4)
+                s_cy[slot] = -cur[i].co.y;  // (finish_record negates the three back)
+                s_cz[slot] = -cur[i].co.z;
                 s_op[slot] = cur[i].co.w;
                 s_rgb[slot] = cur[i].f;
                 s_pos[slot] = (uint32_t)(lo + j);
@@ -884,7 +886,7 @@ __global__ __launch_bounds__(64, GS_BWD_WAVES) void k_render_bwd(RenderBwdArgs a
             if (row_writer && kw < nk) {
                 const uint2 pr = s_pair[kw];
                 const size_t rec = 4 * (size_t)pr.y + quad;
-                finish_record(make_float4(s_cx[kw], -s_cy[kw], s_cz[kw], s_op[kw]), S, ddelx_dx, ddely_dy,
+                finish_record(make_float4(-s_cx[kw], -s_cy[kw], -s_cz[kw], s_op[kw]), S, ddelx_dx, ddely_dy,
                               a.records + 3 * rec);
                 a.rec_flags[rec] = 1;
             }
