@@ -68,6 +68,9 @@ def parse():
     ap.add_argument("--scan-live", action="store_true",
                     help="N > 1: find the all-reduce's live rows by reading the gradient bucket after the backward "
                          "(GradBucket.allreduce) instead of agreeing on the forwards' blended Gaussians before it")
+    ap.add_argument("--sync-union", action="store_true",
+                    help="distributed step: wait for the union's size inside allreduce_end (GradBucket's default) "
+                         "instead of deferring that check to the next step")
     ap.add_argument("--serial-zero", action="store_true",
                     help="zero the gradient bucket on the default stream before the forwards (default: on the first "
                          "view's stream beside the forwards, GradBucket.zero(stream=...))")
@@ -115,6 +118,17 @@ def main():
     # to rehearse the RCCL path on a one-GPU box under torch.distributed.run --nproc-per-node 1
     rehearse = os.environ.get("DGE_AMD_BENCH_DIST") == "1"
     distributed = world > 1 or rehearse
+    # the views' and the collective's streams before RCCL creates its own: HIP deals the process's
+    # GPU_MAX_HW_QUEUES hardware queues to streams round-robin, and a view stream sharing the caller's
+    # queue runs that view behind the first one (measured on the one-rank RCCL rehearsal)
+    from dge_amd.multiview import _collective_stream, view_streams
+    if distributed:
+        # (the step off the null stream: under RCCL the null stream shared its hardware queue with the first
+        # pool stream, and the second view then ran behind the first one)
+        torch.cuda.set_stream(torch.cuda.Stream(device=dev))
+    view_streams(dev, args.streams)
+    if distributed:
+        _collective_stream(dev)
     if distributed:
         backend = os.environ.get("DGE_AMD_BENCH_BACKEND", "nccl")  # nccl = RCCL on ROCm; gloo for rehearsals
         if backend == "nccl":
@@ -144,7 +158,9 @@ def main():
         run_views(args, cams, scene, pipe, bg, seeds, bucket, min_world=min_world if distributed else None)
         if distributed:
             if args.batch_backward and not args.scan_live:
-                bucket.allreduce_end()
+                # the union-size check waits for the forwards: deferred to the next step's run_views, after
+                # that step's forwards are issued (GradBucket.allreduce_finalize; the timed region ends with it)
+                bucket.allreduce_end(defer_check=not args.sync_union)
             else:
                 bucket.allreduce(min_world=min_world)
 
@@ -219,6 +235,7 @@ def main():
         step()
         evs[i + 1].record(main_stream)
         host_t.append(time.perf_counter())
+    bucket.allreduce_finalize()  # (the last step's deferred union check, inside the timed region)
     torch.cuda.synchronize()
     if distributed:
         dist.barrier()
@@ -397,6 +414,8 @@ def run_views(args, cams, scene, pipe, bg, seeds, bucket, streams=None, min_worl
         if side:
             from dge_amd.multiview import view_streams
 
+            # (zero() first runs the previous step's deferred union check, its forwards done by now; a fix-up
+            # it enqueues writes the bucket, so the fill then also waits for it)
             bucket.zero(stream=view_streams(main.device, streams)[1], after=ready)
         if min_world is not None and not args.scan_live:
             bucket.allreduce_begin([o.get("_live_rows") for o in outs], min_world=min_world)

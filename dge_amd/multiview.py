@@ -51,6 +51,8 @@ class GradBucket:
             v = self.flat[off:off + p.numel()].view_as(p)
             self.views.append(v)
             off += p.numel()
+        self._rows_cap = 0       # speculated packed rows of the next sparse all-reduce (0: none yet)
+        self._deferred = None    # an allreduce_end(defer_check=True) awaiting allreduce_finalize()
         self.attach()
 
     def attach(self):
@@ -67,6 +69,7 @@ class GradBucket:
         already waits for the forwards).  For models on the fused raw-parameter path, whose gradients go
         into .grad in-kernel; a backward that hands its gradients to autograd's own accumulation must
         follow a plain zero()."""
+        fixed = self.allreduce_finalize()  # (a deferred union check's fix-up writes the bucket: before the fill)
         self._zero_event = None
         if stream is not None and self.flat.is_cuda:
             from . import diff_gaussian_rasterization as _r
@@ -75,6 +78,8 @@ class GradBucket:
             with torch.cuda.stream(stream):
                 if after is not None:
                     stream.wait_event(after)
+                if fixed:
+                    stream.wait_stream(torch.cuda.current_stream(dev))
                 self.flat.zero_()
                 self._zero_event = stream.record_event()
             _r._SIDE_STREAMS = True
@@ -113,6 +118,7 @@ class GradBucket:
         the backward gives a nonzero gradient row.  Valid only when the bucket was zeroed this step and
         these views' fused backward is the only writer of the gradients (the multi-view step); otherwise
         use allreduce(), which finds the nonzero rows by reading the bucket."""
+        self.allreduce_finalize()
         self._pending = None
         if not dist.is_available() or not dist.is_initialized() or dist.get_world_size(group) < min_world:
             return
@@ -150,12 +156,17 @@ class GradBucket:
         cs.record_stream(main)
         self._pending = ("hint", group, idx, pinned, ev, n, mats, cs)
 
-    def allreduce_end(self, stream=None):
+    def allreduce_end(self, stream=None, defer_check: bool = False):
         """Second half of allreduce_begin (after the backward): the packed SUM of the agreed rows.
         stream (GPU buckets): run the pack, the collective and the unpack on that stream instead, behind the
         work the current stream has enqueued so far (the backward), and return at once — the current stream
         is then free for work that does not read the gradients (DGE's gradient-free semantic renders,
-        DGE.py:198-204) while RCCL runs; allreduce_join() makes the current stream wait for the result."""
+        DGE.py:198-204) while RCCL runs; allreduce_join() makes the current stream wait for the result.
+        defer_check (speculated capacity only): do not wait here for the union's size; the check (and the
+        exact fix-up of rows past the capacity, in the rare step whose union outgrew it) runs in
+        allreduce_finalize(), which the next zero() / allreduce_begin() / allreduce() / allreduce_join()
+        call first — the caller finalizes before anything reads the gradients (an optimizer step)."""
+        self.allreduce_finalize()
         pend, self._pending = getattr(self, "_pending", None), None
         if pend is None:
             return None
@@ -192,14 +203,18 @@ class GradBucket:
                 packed = _rows_gather(mats, idx, cap=cap, count=cs)
                 dist.all_reduce(packed, op=dist.ReduceOp.SUM, group=group)
                 _rows_scatter(mats, idx, packed, cap=cap, count=cs)
+            if side:  # (allocated on the side stream, freed by the caching allocator at once)
+                idx.record_stream(stream)
+                cs.record_stream(stream)
+            if spec and defer_check:
+                self._deferred = (ev, pinned, cap, idx, group, mats, stream if side else None)
+                self._reduced = stream.record_event() if side else None
+                return None
             ev.synchronize()
             m = int(pinned.item())
             if spec:
                 if m > cap:
-                    rows = idx[cap:m]
-                    packed = _rows_gather(mats, rows)
-                    dist.all_reduce(packed, op=dist.ReduceOp.SUM, group=group)
-                    _rows_scatter(mats, rows, packed)
+                    _rows_fixup(mats, idx, cap, m, group)
             elif 2 * m > n:  # mostly dense: packing would not pay
                 dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=group)
             else:
@@ -207,16 +222,38 @@ class GradBucket:
                 packed = _rows_gather(mats, rows)
                 dist.all_reduce(packed, op=dist.ReduceOp.SUM, group=group)
                 _rows_scatter(mats, rows, packed)
-            if side:  # (allocated on the side stream, freed by the caching allocator at once)
-                idx.record_stream(stream)
-                cs.record_stream(stream)
-        self._rows_cap = m + m // 8 + 4096 if _native_ok(mats) and os.environ.get("DGE_AMD_ROWS_SPEC", "1") != "0" \
-            else 0
+        self._set_rows_cap(m, mats)
         self._reduced = stream.record_event() if side else None
         return None
 
+    def _set_rows_cap(self, m, mats):
+        self._rows_cap = m + m // 8 + 4096 if _native_ok(mats) and os.environ.get("DGE_AMD_ROWS_SPEC", "1") != "0" \
+            else 0
+
+    def allreduce_finalize(self) -> bool:
+        """The deferred check of an allreduce_end(defer_check=True): wait for the union's size (the forwards'
+        marks, long done by the next step), and when it exceeded the speculated capacity all-reduce the rows
+        past it (exact; on the stream the packed SUM ran on).  Returns True when it enqueued that fix-up."""
+        d, self._deferred = getattr(self, "_deferred", None), None
+        if d is None:
+            return False
+        ev, pinned, cap, idx, group, mats, stream = d
+        ev.synchronize()
+        m = int(pinned.item())
+        self._set_rows_cap(m, mats)
+        if m <= cap:
+            return False
+        import contextlib
+
+        with torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext():
+            _rows_fixup(mats, idx, cap, m, group)
+            if stream is not None:
+                self._reduced = stream.record_event()
+        return True
+
     def allreduce_join(self):
         """Make the current stream wait for an allreduce_end(stream=...) (no-op otherwise)."""
+        self.allreduce_finalize()
         ev, self._reduced = getattr(self, "_reduced", None), None
         if ev is not None:
             torch.cuda.current_stream(self.flat.device).wait_event(ev)
@@ -234,6 +271,7 @@ class GradBucket:
         result is the dense all-reduce's up to the float summation order inside RCCL.
         min_world: smallest group that communicates (1 runs the whole protocol on a one-rank group: the
         bench's RCCL rehearsal on a one-GPU box)."""
+        self.allreduce_finalize()
         if not dist.is_available() or not dist.is_initialized() or dist.get_world_size(group) < min_world:
             return None
         self.wait_zero()  # (a view whose backward wrote nothing still sees a zeroed bucket)
@@ -256,6 +294,14 @@ class GradBucket:
         dist.all_reduce(packed, op=dist.ReduceOp.SUM, group=group)
         _rows_scatter(mats, idx, packed)
         return None
+
+
+def _rows_fixup(mats, idx, cap, m, group):
+    """The union's rows [cap, m) past a speculated capacity: their own exact packed SUM."""
+    rows = idx[cap:m]
+    packed = _rows_gather(mats, rows)
+    dist.all_reduce(packed, op=dist.ReduceOp.SUM, group=group)
+    _rows_scatter(mats, rows, packed)
 
 
 # Sparse-row bookkeeping: one gfx950 kernel each on the GPU (gs_rows_live / gs_rows_gather /
@@ -374,10 +420,12 @@ def render_views(cameras, pc, pipe, bg_color, streams: int = 2, speculate: bool 
 
     dev = bg_color.device
     main = torch.cuda.current_stream(dev)
-    pool = stream_pool(dev, streams) if streams > 1 else [main]
     if _fused_ok(pc, pipe) and 1 <= len(cameras) <= _native_max_views():
         return render_views_batched(cameras, pc, pipe, bg_color, view_streams(dev, streams), speculate=speculate,
                                     **kw)
+    # (created only here: every stream takes one of the process's few hardware queues round-robin, and an
+    # unused one can put a view's stream on the same queue as another's, serialising them)
+    pool = stream_pool(dev, streams) if streams > 1 else [main]
     outs = RenderedViews()
     if len(pool) == 1:
         outs.extend(render(c, pc, pipe, bg_color, **kw) for c in cameras)

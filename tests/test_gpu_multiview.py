@@ -415,3 +415,70 @@ def test_zeroed_bucket_stores_first_gradient(cuda_device):
     step()  # no zero in between: adds
     # (a store would leave the first sums: half of these; the views' terms cancel in a few elements)
     torch.testing.assert_close(bucket.flat, 2 * res["store"], rtol=1e-5, atol=1e-6 * float(res["store"].abs().max()))
+
+
+def _deferred_worker(rank, world, port, P, V, W, H, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    try:
+        torch.cuda.set_device(0)
+        dev = torch.device("cuda", 0)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from dge_amd.gaussian_renderer import PipelineParams
+        from dge_amd.multiview import GradBucket, render_views, shard_views
+
+        sc, cams, seeds = _c3_setup(dev, P, V, W, H)
+        mine = list(shard_views(V, world, rank))
+        bucket = GradBucket(sc.parameters())
+        bg = torch.zeros(3, device=dev)
+        errs = []
+        # step 0 sets the speculated capacity; step 1 runs under it, step 2 under a third of the union (the
+        # deferred check finds the overflow and all-reduces the rows past the capacity)
+        for k, cap in enumerate((None, None, "third")):
+            bucket.zero()
+            outs = render_views([cams[i] for i in mine], sc, PipelineParams(), bg, streams=3, speculate=True)
+            bucket.allreduce_begin([o["_live_rows"] for o in outs], min_world=2)
+            torch.autograd.backward([o["render"] for o in outs], [seeds[i] for i in mine])
+            assert outs.check()
+            torch.cuda.synchronize()
+            dense = bucket.flat.clone()
+            dist.all_reduce(dense, op=dist.ReduceOp.SUM)
+            if cap == "third":
+                bucket._rows_cap = max(1, (bucket._rows_cap - 4096) * 8 // 9 // 3)  # (cap = m + m // 8 + 4096)
+            spec = bucket._rows_cap > 0
+            bucket.allreduce_end(defer_check=True)
+            deferred = getattr(bucket, "_deferred", None) is not None
+            fixed = bucket.allreduce_finalize()
+            torch.cuda.synchronize()
+            errs.append((k, spec, deferred, fixed, bool(torch.equal(bucket.flat, dense)),
+                         int((dense != 0).sum())))
+        q.put((rank, errs, None))
+    except Exception as e:  # report instead of hanging the parent
+        q.put((rank, None, repr(e)))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def test_deferred_union_check_two_ranks(cuda_device):
+    """allreduce_end(defer_check=True) + allreduce_finalize() (the bench's distributed step): with two
+    ranks on one card (gloo, CUDA tensors), the bucket after the packed SUM at a speculated capacity equals
+    the dense all-reduce of the ranks' buckets, bit for bit — also when the capacity is a third of the union
+    and the deferred check all-reduces the rows past it."""
+    P, V, W, H = 300_000, 4, 160, 128  # (a union under half the rows: the packed path)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_deferred_worker, args=(r, 2, port, P, V, W, H, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    for rank, steps, err in res:
+        assert err is None, f"rank {rank}: {err}"
+        print(f"[deferred] rank {rank}: (step, speculated, deferred, fix-up, equal, nonzero) {steps}")
+        (k0, s0, d0, f0, e0, _), (k1, s1, d1, f1, e1, _), (k2, s2, d2, f2, e2, _) = steps
+        assert not s0 and not d0 and e0          # first step: exact (no capacity yet)
+        assert s1 and d1 and not f1 and e1       # speculated, deferred, no overflow
+        assert s2 and d2 and f2 and e2           # capacity below the union: the deferred fix-up ran

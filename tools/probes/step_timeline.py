@@ -1,0 +1,16 @@
+import csv, sys
+rows=list(csv.DictReader(open(sys.argv[1])))
+rows.sort(key=lambda r:int(r['Start_Timestamp']))
+gb=[i for i,r in enumerate(rows) if r['Kernel_Name'].startswith('k_gauss_bwd_live')]
+a,b=gb[-6],gb[-5]
+t0=int(rows[a]['Start_Timestamp'])
+busy=[]
+for r in rows[a:b+1]:
+    s=(int(r['Start_Timestamp'])-t0)/1e3; e=(int(r['End_Timestamp'])-t0)/1e3
+    busy.append((s,e))
+    print(f"{s:8.1f} {e:8.1f} {e-s:6.1f} q{r['Queue_Id']:>2} s{r['Stream_Id']:>2} {r['Kernel_Name'][:60]}")
+busy.sort(); cur=busy[0][1]; idle=0
+for s,e in busy[1:]:
+    if s>cur: idle+=s-cur
+    cur=max(cur,e)
+print("span",busy[-1][0],"idle",idle)
