@@ -75,7 +75,8 @@ def parse():
                     help="zero the gradient bucket on the default stream before the forwards (default: on the first "
                          "view's stream beside the forwards, GradBucket.zero(stream=...))")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=10.0)
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="OpenMP threads of the CPU baseline (default 0: every core this process may use)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
     ap.add_argument("--no-side-legs", action="store_true",
@@ -103,8 +104,58 @@ def stage_bytes(stage, P, M, K, Kb, HW, tiles, live=None):
     return None
 
 
+def _free_port() -> int:
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(args, argv=None, child_cmd=None) -> int:
+    """`--gpus N` (N > 1) without a launcher: start N rank processes of this script, one per GPU, over a
+    127.0.0.1 rendezvous (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* in their environment, as
+    torch.distributed.run sets them), and return the first nonzero exit code (0 when all succeed).
+    Nothing here touches the GPU (torch.cuda.device_count() does not initialise HIP on this image): the
+    parent never creates a HIP context, so the ranks own their devices.  Rank 0 prints the JSON line.
+    A rank that fails ends the others (their exact PIDs) instead of leaving them in a collective."""
+    import subprocess
+
+    n = args.gpus
+    ndev = torch.cuda.device_count()
+    env0 = dict(os.environ)
+    env0.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), WORLD_SIZE=str(n),
+                DGE_AMD_BENCH_SPAWNED="1")
+    if ndev < n and "DGE_AMD_BENCH_BACKEND" not in env0:
+        # (a rehearsal of N ranks on fewer cards: RCCL refuses two ranks on one device, gloo does not)
+        print(f"[bench] {n} ranks on {ndev} visible GPU(s): gloo backend (rehearsal)", file=sys.stderr)
+        env0["DGE_AMD_BENCH_BACKEND"] = "gloo"
+    cmd = child_cmd or [sys.executable, os.path.abspath(__file__)] + list(sys.argv[1:] if argv is None else argv)
+    procs = []
+    for r in range(n):
+        env = dict(env0, RANK=str(r), LOCAL_RANK=str(r))
+        procs.append(subprocess.Popen(cmd, env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in live:  # (a failed rank leaves the others waiting in a collective)
+                    q.terminate()
+        if live:
+            time.sleep(0.05)
+    return rc
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -154,15 +205,24 @@ def main():
 
     min_world = 1 if rehearse else 2
 
-    def step():
+    coll_evs = []  # (start, end) events around each timed step's gradient collective, on the main stream
+
+    def step(timed=False):
         run_views(args, cams, scene, pipe, bg, seeds, bucket, min_world=min_world if distributed else None)
         if distributed:
+            if timed:
+                a = torch.cuda.Event(enable_timing=True)
+                a.record()
             if args.batch_backward and not args.scan_live:
                 # the union-size check waits for the forwards: deferred to the next step's run_views, after
                 # that step's forwards are issued (GradBucket.allreduce_finalize; the timed region ends with it)
                 bucket.allreduce_end(defer_check=not args.sync_union)
             else:
                 bucket.allreduce(min_world=min_world)
+            if timed:
+                b = torch.cuda.Event(enable_timing=True)
+                b.record()
+                coll_evs.append((a, b))
 
     def step_one_stream():
         # the kernels in isolation (one stream, nothing concurrent): what the per-stage and roofline
@@ -232,7 +292,7 @@ def main():
     t0 = time.perf_counter()
     evs[0].record(main_stream)
     for i in range(args.steps):
-        step()
+        step(timed=True)
         evs[i + 1].record(main_stream)
         host_t.append(time.perf_counter())
     bucket.allreduce_finalize()  # (the last step's deferred union check, inside the timed region)
@@ -242,6 +302,8 @@ def main():
     dt = time.perf_counter() - t0
     host_wait_s = (_native.lib().gs_host_wait_ns() - wait0) * 1e-9
     step_ms = [evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps)]
+    # the packed SUM (gather, RCCL all-reduce, scatter) on the main stream behind each step's backward
+    coll_ms = [a.elapsed_time(b) for a, b in coll_evs]
     host_ms = [1e3 * (b - a) for a, b in zip([t0] + host_t[:-1], host_t)]
     m1 = torch.cuda.memory_stats(dev)
     # caching-allocator activity inside the timed region (device allocations there cost a hipMalloc each)
@@ -265,10 +327,16 @@ def main():
         prof = _native.profile_collect()
         _native.profile_enable(False)
         _native.profile_stages(None)
+    rank_dt = dt
     if distributed:
         t = torch.tensor([dt], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
+        # every rank's own time (rank 0 reports them beside the max the value is taken from)
+        allt = torch.zeros(world, device=dev, dtype=torch.float64)
+        allt[rank] = rank_dt
+        dist.all_reduce(allt, op=dist.ReduceOp.SUM)
+        rank_times = [round(float(x), 5) for x in allt.tolist()]
 
     renders = args.steps * V * world
     value = renders / dt
@@ -367,6 +435,16 @@ def main():
             "legs": legs,
             "cpu_baseline": cpu,
         }
+        if distributed:
+            c50 = float(np.percentile(coll_ms, 50)) if coll_ms else 0.0
+            s50 = float(np.percentile(step_ms, 50))
+            line["distributed"] = {
+                "backend": os.environ.get("DGE_AMD_BENCH_BACKEND", "nccl").replace("nccl", "RCCL"),
+                "launch": "bench.py spawned its ranks" if os.environ.get("DGE_AMD_BENCH_SPAWNED") else
+                          "external launcher (torch.distributed.run)",
+                "rank_seconds": rank_times, "max_rank_seconds": round(dt, 5),
+                # the gradient collective of a step (pack, SUM, unpack on the main stream), its share of the step
+                "collective_ms": _spread(coll_ms), "collective_share_p50": round(c50 / max(s50, 1e-9), 4)}
         print(json.dumps(line), flush=True)
     if distributed:
         dist.destroy_process_group()
@@ -401,7 +479,7 @@ def run_views(args, cams, scene, pipe, bg, seeds, bucket, streams=None, min_worl
         bucket.zero()
         render_backward_views(cams, scene, pipe, bg, seeds, streams=streams)
         return
-    for _ in range(2):
+    for attempt in range(2):
         # the bucket's fill runs on the first view's stream behind that view's forward, beside the others'
         # (only the backward's gradient writes wait for it: GradBucket.zero(stream=...))
         side = streams > 1 and not args.serial_zero
@@ -417,12 +495,14 @@ def run_views(args, cams, scene, pipe, bg, seeds, bucket, streams=None, min_worl
             # (zero() first runs the previous step's deferred union check, its forwards done by now; a fix-up
             # it enqueues writes the bucket, so the fill then also waits for it)
             bucket.zero(stream=view_streams(main.device, streams)[1], after=ready)
-        if min_world is not None and not args.scan_live:
-            bucket.allreduce_begin([o.get("_live_rows") for o in outs], min_world=min_world)
+        if attempt == 0 and min_world is not None and not args.scan_live:
+            # (the union's MAX also carries this batch's overflow flag: a re-render below is agreed on)
+            bucket.allreduce_begin([o.get("_live_rows") for o in outs], min_world=min_world, views=outs)
         torch.autograd.backward([o["render"] for o in outs], seeds)
         if outs.check():
             return
-        # a view's instance count outgrew its speculated capacity: the step again (the capacity grew)
+        # a view's instance count outgrew its speculated capacity: the step again, locally (the capacity
+        # grew); the other ranks learn it from the flag and re-agree on the rows in allreduce_end
     raise RuntimeError("render_views: the binning capacity check failed twice")
 
 
@@ -527,7 +607,8 @@ def cpu_baseline(scene, cam, seed, bg, args):
         from oracle import oracle as O
     except Exception as e:  # pragma: no cover
         return {"error": f"oracle unavailable: {e}"}
-    threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+    usable = _usable_cpus()
+    threads = max(1, args.cpu_threads if args.cpu_threads > 0 else usable["usable"])
     O.set_threads(threads)
     from dge_amd.gaussian_renderer import _settings
     s = _settings(cam, bg, 1.0, scene.active_sh_degree)
@@ -553,7 +634,23 @@ def cpu_baseline(scene, cam, seed, bg, args):
     except OSError:
         pass
     return {"value": round(n / el, 4), "unit": "renders/s", "cores": threads, "kind": "port", "cpu_model": model,
+            "affinity_cpus": usable["affinity"], "os_cpu_count": usable["cpu_count"], "cgroup_cpus": usable["cgroup"],
             "sample": f"{n} fwd+bwd render(s) of the c2 scene, view 0, oracle/gs_oracle.c with {threads} OpenMP threads"}
+
+
+def _usable_cpus():
+    """The host cores this process may use: its CPU affinity set, capped by a cgroup CPU quota (cpu.max)
+    when one is set; os.cpu_count() (the whole machine) beside them."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) // int(per)))
+    except (OSError, ValueError):
+        pass
+    return {"usable": min(aff, quota) if quota else aff, "affinity": aff, "cpu_count": os.cpu_count(),
+            "cgroup": quota}
 
 
 if __name__ == "__main__":

@@ -1357,6 +1357,24 @@ int gs_views_backward(gs_views* h, const float* const* dL_dpix, const gs_grads* 
     }
 }
 
+int gs_views_overflow(const gs_views* h, uint8_t* flag, gs_stream_t stream_) {
+    hipStream_t stream = (hipStream_t)stream_;
+    if (!h || !flag) return set_error(GS_ERR_INVALID_ARG, "gs_views_overflow: handle and flag are required");
+    OverflowArgs a;
+    a.n = h->n;
+    a.bits = depth_sort_bits();
+    for (int v = 0; v < h->n; ++v) {
+        const FwdState& f = h->f[v];
+        if (!h->spec[v] || f.gp.P == 0) continue;
+        a.counters[v] = at<uint32_t>(f.img, img_layout(f.g.W, f.g.H).counters);
+        a.cap[v] = h->layout[v];
+    }
+    launch_views_overflow(a, flag, stream);
+    const bool debug = false;
+    GS_LAUNCHED("views overflow flag");
+    return GS_OK;
+}
+
 void* gs_views_buffer(const gs_views* h, int v, int which) {
     if (!h || v < 0 || v >= h->n) return nullptr;
     switch (which) {

@@ -324,6 +324,16 @@ void launch_emit_fused(const EmitArgs& a, hipStream_t s);
 void launch_row_pass(const EmitArgs& a, uint32_t K, uint2* point_pairs, uint32_t* hist, int sort_blocks,
                      uint2* ranges, uint32_t* tile_order, hipStream_t s, const uint32_t* n_dev = nullptr);
 
+// One byte on the device: 1 when some speculated view of a batch overflowed its binning capacity (the
+// sum of its preprocess counter slots > cap) or its visible depth keys span more than `bits` bits — the
+// host's gs_views_check decision, made where a collective can carry it (GradBucket.allreduce_begin)
+struct OverflowArgs {
+    int n = 0, bits = 0;
+    const uint32_t* counters[8] = {};  // (GS_MAX_VIEWS)
+    uint32_t cap[8] = {};  // 0: an exact view (never overflows)
+};
+void launch_views_overflow(const OverflowArgs& a, uint8_t* flag, hipStream_t s);
+
 // tile ranges; also zeroes the backward's per-slot record flags (u32 per slot)
 void launch_ranges(const uint32_t* sorted_tile, int K, uint2* ranges, uint32_t* rec_flags32, hipStream_t s);
 

@@ -944,4 +944,29 @@ void launch_ranges(const uint32_t* sorted_tile, int K, uint2* ranges, uint32_t* 
     hipLaunchKernelGGL(k_ranges, dim3(div_up(K, 256)), dim3(256), 0, s, sorted_tile, K, ranges, rec_flags32);
 }
 
+// The speculated views' overflow decision on the device (the same test as gs_views_check's on the
+// host copy of the counters): one wave, lane v < n reads view v's counter slots.
+__global__ __launch_bounds__(64) void k_views_overflow(OverflowArgs a, uint8_t* __restrict__ flag) {
+    const int v = threadIdx.x;
+    bool bad = false;
+    if (v < a.n && a.cap[v]) {
+        const uint32_t* __restrict__ c = a.counters[v];
+        uint64_t k = 0;
+        uint32_t kmax = 0u, kmin_not = 0u;
+#pragma unroll
+        for (int i = 0; i < kCounterSlots; ++i) {
+            k += c[i * kCounterStride];
+            kmax = max(kmax, c[i * kCounterStride + 1]);
+            kmin_not = max(kmin_not, c[i * kCounterStride + 2]);
+        }
+        bad = k > a.cap[v] || (k && kmax - ~kmin_not >= (1u << a.bits));
+    }
+    const uint64_t any = __ballot(bad);
+    if (v == 0) flag[0] = any ? 1 : 0;
+}
+
+void launch_views_overflow(const OverflowArgs& a, uint8_t* flag, hipStream_t s) {
+    hipLaunchKernelGGL(k_views_overflow, dim3(1), dim3(64), 0, s, a, flag);
+}
+
 }  // namespace gs

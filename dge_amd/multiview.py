@@ -70,6 +70,8 @@ class GradBucket:
         into .grad in-kernel; a backward that hands its gradients to autograd's own accumulation must
         follow a plain zero()."""
         fixed = self.allreduce_finalize()  # (a deferred union check's fix-up writes the bucket: before the fill)
+        # the previous step's packed scatter (or its fix-up) on a side stream still writes the bucket
+        reduced, self._reduced = getattr(self, "_reduced", None), None
         self._zero_event = None
         if stream is not None and self.flat.is_cuda:
             from . import diff_gaussian_rasterization as _r
@@ -80,6 +82,8 @@ class GradBucket:
                     stream.wait_event(after)
                 if fixed:
                     stream.wait_stream(torch.cuda.current_stream(dev))
+                if reduced is not None:
+                    stream.wait_event(reduced)
                 self.flat.zero_()
                 self._zero_event = stream.record_event()
             _r._SIDE_STREAMS = True
@@ -87,6 +91,8 @@ class GradBucket:
             _r._ZEROED[dev.index] = (self.flat, self.flat._version)
             self.attach()
             return
+        if reduced is not None:
+            torch.cuda.current_stream(self.flat.device).wait_event(reduced)
         self.flat.zero_()
         if self.flat.is_cuda:
             from . import diff_gaussian_rasterization as _r
@@ -107,7 +113,7 @@ class GradBucket:
         if ev is not None:
             torch.cuda.current_stream(self.flat.device).wait_event(ev)
 
-    def allreduce_begin(self, live_hint, group=None, min_world: int = 2):
+    def allreduce_begin(self, live_hint, group=None, min_world: int = 2, views=None):
         """First half of a sparse allreduce() whose union of live rows is agreed on BEFORE the backward runs,
         so the one host wait of the protocol (the union's size, which shapes the packed collective) waits
         for the forwards, not for the backward: call it after the views' forwards are enqueued and before
@@ -117,7 +123,14 @@ class GradBucket:
         the Gaussians some pixel of the view blends (set by the forward kernel), which are exactly the ones
         the backward gives a nonzero gradient row.  Valid only when the bucket was zeroed this step and
         these views' fused backward is the only writer of the gradients (the multi-view step); otherwise
-        use allreduce(), which finds the nonzero rows by reading the bucket."""
+        use allreduce(), which finds the nonzero rows by reading the bucket.
+
+        views: the speculated batch these hints come from (render_views(speculate=True)'s list).  Its
+        overflow flag (gs_views_overflow: some view outgrew its binning capacity, so its marks are not
+        the re-rendered step's rows) travels with the marks in the same MAX, so every rank learns that
+        SOME rank is re-rendering; allreduce_end then moves nothing at the agreed union and every rank
+        runs the scanning allreduce() instead.  The rank that overflowed re-renders locally (no
+        collective) between this call and allreduce_end — the same collectives on every rank."""
         self.allreduce_finalize()
         self._pending = None
         if not dist.is_available() or not dist.is_initialized() or dist.get_world_size(group) < min_world:
@@ -138,23 +151,36 @@ class GradBucket:
         main = torch.cuda.current_stream(dev)
         side = _collective_stream(dev) if self.flat.is_cuda else main
         side.wait_stream(main)
+        for h in hints:  # (read on the side stream; the caller may free the batch meanwhile)
+            h.record_stream(side)
+        batch = getattr(views, "batch", None)
         with torch.cuda.stream(side):
-            live = hints[0].clone()
+            live = torch.empty(n + 1, dtype=torch.uint8, device=dev)  # the rows' marks + the overflow flag
+            live[:n].copy_(hints[0])
             for h in hints[1:]:
-                live |= h
+                live[:n] |= h
+            if batch is not None:
+                N.check(N.lib().gs_views_overflow(batch.handle, live[n:].data_ptr(), ctypes.c_void_p(side.cuda_stream)),
+                        "gs_views_overflow")
+            else:
+                live[n:].zero_()
             dist.all_reduce(live, op=dist.ReduceOp.MAX, group=group)
             idx = torch.empty(n, dtype=torch.int64, device=dev)
             cs = torch.empty(1 + (n + 1023) // 1024, dtype=torch.int64, device=dev)
             N.check(N.lib().gs_rows_compact(live.data_ptr(), n, idx.data_ptr(), cs.data_ptr(),
                                             ctypes.c_void_p(side.cuda_stream)), "gs_rows_compact")
+            # (count, agreed overflow flag); the device-side count of the packed collective is 0 when some
+            # rank overflowed, so the speculated SUM moves nothing and the scanning allreduce() follows
+            info = torch.cat([cs[:1], live[n:].to(torch.int64)])
+            cdev = cs[:1] * (1 - info[1:])
             pinned = getattr(self, "_count_host", None)
             if pinned is None:
-                pinned = self._count_host = torch.empty(1, dtype=torch.int64, pin_memory=True)
-            pinned.copy_(cs[:1], non_blocking=True)
+                pinned = self._count_host = torch.empty(2, dtype=torch.int64, pin_memory=True)
+            pinned.copy_(info, non_blocking=True)
             ev = side.record_event()
         idx.record_stream(main)  # (read on the current stream by allreduce_end)
-        cs.record_stream(main)
-        self._pending = ("hint", group, idx, pinned, ev, n, mats, cs)
+        cdev.record_stream(main)
+        self._pending = ("hint", group, idx, pinned, ev, n, mats, cdev)
 
     def allreduce_end(self, stream=None, defer_check: bool = False):
         """Second half of allreduce_begin (after the backward): the packed SUM of the agreed rows.
@@ -211,8 +237,10 @@ class GradBucket:
                 self._reduced = stream.record_event() if side else None
                 return None
             ev.synchronize()
-            m = int(pinned.item())
-            if spec:
+            m, overflow = int(pinned[0]), int(pinned[1])
+            if overflow:  # some rank re-rendered its views after the marks: every rank scans its bucket
+                self.allreduce(group, min_world=1)
+            elif spec:
                 if m > cap:
                     _rows_fixup(mats, idx, cap, m, group)
             elif 2 * m > n:  # mostly dense: packing would not pay
@@ -239,14 +267,17 @@ class GradBucket:
             return False
         ev, pinned, cap, idx, group, mats, stream = d
         ev.synchronize()
-        m = int(pinned.item())
+        m, overflow = int(pinned[0]), int(pinned[1])
         self._set_rows_cap(m, mats)
-        if m <= cap:
+        if m <= cap and not overflow:
             return False
         import contextlib
 
         with torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext():
-            _rows_fixup(mats, idx, cap, m, group)
+            if overflow:  # (the packed SUM moved nothing: the agreed flag zeroed its device count)
+                self.allreduce(group, min_world=1)
+            else:
+                _rows_fixup(mats, idx, cap, m, group)
             if stream is not None:
                 self._reduced = stream.record_event()
         return True
@@ -508,7 +539,7 @@ def found_inf_allreduce(bucket: GradBucket, group=None) -> torch.Tensor:
     skips the optimizer step on overflow, and every replica must skip the same steps or their
     parameters diverge.  (The SUM all-reduce would spread an inf/NaN to every rank anyway — for the
     rows it carries; this flag makes the decision explicit and independent of the sparse packing.)"""
-    flag = (~torch.isfinite(bucket.flat)).any().to(torch.float32).reshape(1)
+    flag = (~torch.isfinite(bucket.flat)).any().to(torch.float32).reshape(1)  # (after or before the SUM)
     if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
         dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=group)
     return flag
@@ -531,8 +562,7 @@ def multiview_step(scene, cameras, render_fn, pipe, bg, bucket: GradBucket, tota
     without autograd, its boolean ``norm > 0.8`` map returned in ``masks``.
 
     Then one (sparse-row) SUM all-reduce of the gradient bucket, the overflow flag (any non-finite
-    gradient, taken on the reduced bucket: the SUM carries an inf/NaN of any rank to every rank, and rows
-    it does not carry are zero everywhere, so every rank reaches the same decision), and the
+    gradient of the reduced bucket on some rank: one MAX all-reduce, found_inf_allreduce), and the
     densification statistics: the SUM of the view-space gradients and the MAX of the radii across views
     and ranks.  Returns a dict: viewspace_grad_sum [P,3], radii_max [P], found_inf (float tensor [1]),
     semantic_masks (list of [H,W] bool, when ``semantic``).
@@ -570,18 +600,23 @@ def multiview_step(scene, cameras, render_fn, pipe, bg, bucket: GradBucket, tota
 
     hinted = False
     if batched:
-        for attempt in range(2):
-            if attempt:
-                bucket.zero()  # (speculated only with bucket_zeroed: the failed attempt's sums go)
+        def attempt(begin):
             pkgs = render_views(cameras, scene, pipe, bg, streams=streams, speculate=bucket_zeroed)
-            hinted = bucket_zeroed and all("_live_rows" in pkg for pkg in pkgs)
-            if hinted:
-                bucket.allreduce_begin([pkg["_live_rows"] for pkg in pkgs], group, min_world=min_world)
+            ok = bucket_zeroed and all("_live_rows" in pkg for pkg in pkgs)
+            if begin and ok:
+                bucket.allreduce_begin([pkg["_live_rows"] for pkg in pkgs], group, min_world=min_world, views=pkgs)
             torch.autograd.backward(losses_of(pkgs))
-            if pkgs.check():
-                break
-        else:
-            raise RuntimeError("multiview_step: the binning capacity check failed twice")
+            return pkgs, ok
+
+        pkgs, hinted = attempt(True)
+        if not pkgs.check():
+            # this rank's speculated capacity overflowed (speculated only with bucket_zeroed): render and
+            # back-propagate again locally, no collective — the overflow flag the union's MAX carried makes
+            # every rank's allreduce_end re-agree on the rows by scanning the buckets
+            bucket.zero()
+            pkgs, _ = attempt(False)
+            if not pkgs.check():
+                raise RuntimeError("multiview_step: the binning capacity check failed twice")
         for pkg in pkgs:
             vs_sum += pkg["viewspace_points"].grad
             radii_max = torch.maximum(radii_max, pkg["radii"])
@@ -611,7 +646,9 @@ def multiview_step(scene, cameras, render_fn, pipe, bg, bucket: GradBucket, tota
                 sms = [render_fn(cam, scene, pipe, bg, override_color=colors)["render"] for cam in cameras]
             sem = [torch.norm(sm, dim=0) > 0.8 for sm in sms]
     bucket.allreduce_join()
-    found_inf = (~torch.isfinite(bucket.flat)).any().to(torch.float32).reshape(1)
+    # (the explicit MAX of every rank's flag: a non-finite element outside the all-reduced rows still
+    # makes every rank skip the step)
+    found_inf = found_inf_allreduce(bucket, group)
     reduce_view_stats(vs_sum, radii_max, group)
     out = {"viewspace_grad_sum": vs_sum, "radii_max": radii_max, "found_inf": found_inf}
     if semantic:

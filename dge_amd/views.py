@@ -301,7 +301,7 @@ def render_views_batched(cameras, pc, pipe, bg_color, streams, scaling_modifier=
     for v in range(n):
         d = {"render": res[v], "viewspace_points": means2D[v], "visibility_filter": visible[v], "radii": res[n + v],
              "depth_3dgs": res[2 * n + v]}
-        if index is None:
+        if index is None and not meta["forward_only"]:  # (a forward-only render writes no marks)
             d["_live_rows"] = batch.touched(v)
         outs.append(d)
     return outs

@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define GS_RASTER_ABI_VERSION 13
+#define GS_RASTER_ABI_VERSION 14
 
 #define GS_OK 0
 #define GS_ERR_INVALID_ARG 1   /* AT_ERROR / std::runtime_error in the reference */
@@ -267,6 +267,11 @@ int gs_views_backward(gs_views *h, const float *const *dL_dpix, const gs_grads *
                       const gs_stream_t *streams, void *writes_after, gs_stream_t join);
 /* View v's buffers (which: 0 geometry, 1 binning, 2 image; gs_buffer_offset
  * addresses their fields with num_rendered = gs_views_layout(h, v)). */
+/* flag[0] (one device byte) = 1 when some speculated view of the batch overflowed its capacity (or
+ * needs the 32-bit depth sort) — gs_views_check's GS_ERR_RETRY decision, computed on the device on
+ * `stream` (which must be ordered after the views' forwards) without a host wait, so a collective can
+ * carry it: every rank of a view-sharded step then agrees on the recovery (ABI 14). */
+int gs_views_overflow(const gs_views *h, uint8_t *flag, gs_stream_t stream);
 void *gs_views_buffer(const gs_views *h, int v, int which);
 long long gs_views_layout(const gs_views *h, int v);
 void gs_views_release(gs_views *h);

@@ -154,6 +154,40 @@ def run_gpu(settings, dL_dpix=None, means3D=None, opacities=None, shs=None, colo
     return out
 
 
+def views_forward_dict(batch, v, color, depth, radii):
+    """run_gpu's forward dict (outputs + intermediates) for view v of a render_views batch (ViewBatch),
+    its fields read at the batch's binning layout (a speculated view's capacity, not its count)."""
+    from dge_amd import _native
+
+    L = _native.lib()
+    P, W, H = batch.P, batch.W, batch.H
+    K = int(batch.num_rendered[v])
+    R = int(L.gs_views_layout(batch.handle, v))
+    bufs = {"geometry": batch.buffer(v, 0), "binning": batch.buffer(v, 1), "image": batch.buffer(v, 2)}
+
+    def view(which, field, dtype, count):
+        off = L.gs_buffer_offset(which.encode(), field.encode(), P, W, H, R)
+        assert off >= 0, field
+        t, base = bufs[which]
+        nbytes = np.dtype(dtype).itemsize * count
+        return t[base + off:base + off + nbytes].cpu().numpy().view(dtype).copy()
+
+    tiles = ((W + 15) // 16) * ((H + 15) // 16)
+    out = dict(num_rendered=K, color=color.detach().cpu().numpy(), depth=depth.detach().cpu().numpy(),
+               radii=radii.cpu().numpy())
+    sp = view("geometry", "splat", np.float32, 16 * P).reshape(P, 16)
+    out["means2D"] = np.ascontiguousarray(sp[:, 0:2])
+    out["conic_opacity"] = np.ascontiguousarray(sp[:, 4:8])
+    out["rgbd"] = np.ascontiguousarray(sp[:, 8:12])
+    out["tiles_touched"] = view("geometry", "tiles_touched", np.uint32, P)
+    out["clamped"] = view("geometry", "clamped", np.uint8, P)
+    out["final_T"] = view("image", "final_T", np.float32, W * H)
+    out["n_contrib"] = view("image", "n_contrib", np.uint32, W * H)
+    out["ranges"] = view("image", "ranges", np.uint32, 2 * tiles)
+    out["point_list"] = view("binning", "point_pairs", np.uint32, 2 * K)[0::2] if K else np.zeros(0, np.uint32)
+    return out
+
+
 def run_oracle(O, settings, dL_dpix=None, **kw):
     nr, color, depth, radii, st = O.forward(settings, **kw)
     out = dict(num_rendered=nr, color=color, depth=depth, radii=radii, state=st)

@@ -482,3 +482,240 @@ def test_deferred_union_check_two_ranks(cuda_device):
         assert not s0 and not d0 and e0          # first step: exact (no capacity yet)
         assert s1 and d1 and not f1 and e1       # speculated, deferred, no overflow
         assert s2 and d2 and f2 and e2           # capacity below the union: the deferred fix-up ran
+
+
+def _seed_history(dev, P, cams, sc, small):
+    """Render `cams` exactly once (no gradients) to seed this process's speculated-capacity history for
+    their (P, W, H): with the scene itself, or (small) with the same number of Gaussians moved out of
+    every frustum — a capacity of 64k instances, far below the scene's count."""
+    from dge_amd.gaussian_renderer import PipelineParams
+    from dge_amd.multiview import render_views
+    from dge_amd.scene import synthetic_scene
+
+    if small:
+        sc = synthetic_scene(P, seed=1, device=dev)
+        sc._xyz += 1000.0
+    with torch.no_grad():
+        assert render_views(cams, sc, PipelineParams(), torch.zeros(3, device=dev), streams=3).check()
+
+
+def _overflow_worker(rank, world, port, P, V, sizes, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    try:
+        torch.cuda.set_device(0)
+        dev = torch.device("cuda", 0)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from dge_amd.gaussian_renderer import PipelineParams, render
+        from dge_amd.multiview import GradBucket, multiview_step, render_views, shard_views
+
+        mine = list(shard_views(V, world, rank))
+        bg = torch.zeros(3, device=dev)
+        out = {}
+        # (1) multiview_step (hinted, the check inside allreduce_end) at sizes[0]; (2) the bench's step —
+        # a speculated packed SUM whose union check is deferred — at sizes[2], after a first step at
+        # sizes[1] that sets the packed capacity.  Only rank 1's history is seeded with the small scene.
+        W, H = sizes[0]
+        sc, cams, seeds = _c3_setup(dev, P, V, W, H)
+        _seed_history(dev, P, [cams[i] for i in mine], sc, small=rank == 1)
+        bucket = GradBucket(sc.parameters())
+        bucket.zero()
+        multiview_step(sc, [cams[i] for i in mine], render, PipelineParams(), bg, bucket, V,
+                       targets=[seeds[i] for i in mine], streams=3, bucket_zeroed=True)
+        torch.cuda.synchronize()
+        out["step"] = bucket.flat.cpu().numpy()
+        del bucket
+        for k, (W, H) in enumerate(sizes[1:]):
+            sc, cams, seeds = _c3_setup(dev, P, V, W, H)
+            if k == 0:
+                bucket = GradBucket(sc.parameters())
+            else:
+                bucket.params = sc.parameters()
+                _seed_history(dev, P, [cams[i] for i in mine], sc, small=rank == 1)
+            bucket.zero()
+            retried = False
+            outs = render_views([cams[i] for i in mine], sc, PipelineParams(), bg, streams=3, speculate=True)
+            bucket.allreduce_begin([o["_live_rows"] for o in outs], views=outs)
+            torch.autograd.backward([o["render"] for o in outs], [seeds[i] for i in mine])
+            if not outs.check():
+                retried = True
+                bucket.zero()
+                outs = render_views([cams[i] for i in mine], sc, PipelineParams(), bg, streams=3, speculate=True)
+                torch.autograd.backward([o["render"] for o in outs], [seeds[i] for i in mine])
+                assert outs.check()
+            spec = bucket._rows_cap > 0
+            bucket.allreduce_end(defer_check=True)
+            deferred = getattr(bucket, "_deferred", None) is not None
+            fixed = bucket.allreduce_finalize()
+            torch.cuda.synchronize()
+            out[f"deferred{k}"] = (bucket.flat.cpu().numpy() if k else None, retried, spec, deferred, fixed)
+        q.put((rank, out, None))
+    except Exception as e:  # report instead of hanging the parent
+        import traceback
+
+        q.put((rank, None, traceback.format_exc()))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def test_overflow_on_one_rank_is_agreed(cuda_device):
+    """A speculated batch that overflows its binning capacity on ONE rank only (that rank's capacity
+    history holds a scene with no visible Gaussian): the overflowing rank re-renders locally, the overflow
+    flag rides the union's MAX collective, and every rank runs the same collectives — no hang, no
+    mismatched reduction — ending with the single-process step's summed gradients, in multiview_step and
+    in the bench's deferred-check step.  Two ranks on one card (gloo, CUDA tensors)."""
+    from dge_amd.gaussian_renderer import PipelineParams, render
+    from dge_amd.multiview import GradBucket, multiview_step
+
+    P, V = 300_000, 4
+    sizes = [(176, 128), (160, 128), (192, 128)]
+    dev = torch.device("cuda", 0)
+    refs = {}
+    for key, (W, H) in (("step", sizes[0]), ("deferred1", sizes[2])):
+        sc, cams, seeds = _c3_setup(dev, P, V, W, H)
+        bucket = GradBucket(sc.parameters())
+        multiview_step(sc, cams, render, PipelineParams(), torch.zeros(3, device=dev), bucket, V, targets=seeds)
+        torch.cuda.synchronize()
+        refs[key] = bucket.flat.cpu().numpy()
+        del sc, bucket
+    torch.cuda.empty_cache()
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_overflow_worker, args=(r, 2, port, P, V, sizes, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    for rank, out, err in res:
+        assert err is None, f"rank {rank}: {err}"
+        ref = refs["step"]
+        np.testing.assert_allclose(out["step"], ref, rtol=1e-5, atol=1e-6 * np.abs(ref).max())
+        _, r0, s0, d0, f0 = out["deferred0"]
+        flat, r1, s1, d1, f1 = out["deferred1"]
+        print(f"[overflow] rank {rank}: first step (retried, spec, deferred, fix-up) {(r0, s0, d0, f0)}, "
+              f"overflow step {(r1, s1, d1, f1)}")
+        assert not r0
+        assert r1 == (rank == 1), "only rank 1's capacity is too small"
+        assert s1 and d1 and f1, "the agreed flag must turn the deferred check into the scanning all-reduce"
+        ref = refs["deferred1"]
+        np.testing.assert_allclose(flat, ref, rtol=1e-5, atol=1e-6 * np.abs(ref).max())
+    for p in procs:
+        assert p.exitcode == 0
+
+
+def _c2_bench_setup(dev, P=1_000_000, W=512, H=512, V=3):
+    """bench.py's c2 workload: the seeded 1M scene, the 3 orbit views of a one-rank run, its seeds."""
+    from dge_amd.cameras import orbit_camera
+    from dge_amd.scene import synthetic_scene
+
+    sc = synthetic_scene(P, sh_degree=3, seed=0, device=dev).requires_grad_(True)
+    cams = [orbit_camera(k, V, W, H, device=dev) for k in range(V)]
+    gen = torch.Generator(device="cpu").manual_seed(1)
+    seeds = [(torch.randn(3, H, W, generator=gen) * 1e-3).to(dev) for _ in range(V)]
+    return sc, cams, seeds
+
+
+def test_c2_timed_path_matches_per_view_loop(cuda_device, oracle):
+    """The path bench.py times, at the timed size (c2: 1M Gaussians, 512x512, 3 orbit views): render_views
+    on 3 streams with speculated binning capacities (capacity-sized tile-sort grids, the count read on the
+    device), the bucket zeroed on a view stream beside the forwards (GradBucket.zero(stream=...): the
+    backward stores each Gaussian's first gradient), one backward of the summed loss — against the
+    reference's per-view loop of render() + backward (exact binning: the host waits for each count,
+    rasterizer_impl.cu:236-270): images, depths, radii, view-space gradients and the whole gradient bucket
+    bit for bit, twice; view 0's forward bit-identical to the oracle's (lists, ranges, n_contrib, T)."""
+    from dge_amd import _native as N
+    from dge_amd.gaussian_renderer import PipelineParams, _settings, render
+    from dge_amd.multiview import GradBucket, render_views, view_streams
+    from helpers import compare_forward, run_oracle, views_forward_dict
+
+    dev = torch.device("cuda", 0)
+    P, W, H, V = 1_000_000, 512, 512, 3
+    sc, cams, seeds = _c2_bench_setup(dev, P, W, H, V)
+    bg = torch.zeros(3, device=dev)
+    bucket = GradBucket(sc.parameters())
+    bucket.zero()
+    ref_outs = []
+    for c, s in zip(cams, seeds):  # (also seeds the capacity history of this (P, W, H))
+        o = render(c, sc, PipelineParams(), bg)
+        o["render"].backward(s)
+        ref_outs.append(o)
+    torch.cuda.synchronize()
+    keys = ("render", "depth_3dgs", "radii", "visibility_filter")
+    ref = {f"{k}{v}": o[k].detach().clone() for v, o in enumerate(ref_outs) for k in keys}
+    ref.update({f"vs{v}": o["viewspace_points"].grad.clone() for v, o in enumerate(ref_outs)})
+    ref["bucket"] = bucket.flat.clone()
+    del ref_outs
+    for rep in range(2):
+        main = torch.cuda.current_stream(dev)
+        ready = main.record_event()
+        outs = render_views(cams, sc, PipelineParams(), bg, streams=3, speculate=True)
+        bucket.zero(stream=view_streams(dev, 3)[1], after=ready)
+        torch.autograd.backward([o["render"] for o in outs], seeds)
+        assert outs.check()
+        torch.cuda.synchronize()
+        layout = [int(N.lib().gs_views_layout(outs.batch.handle, v)) for v in range(V)]
+        print(f"[c2 timed path] rep {rep}: num_rendered {outs.batch.num_rendered}, capacity {layout}")
+        assert all(0 < k < c for k, c in zip(outs.batch.num_rendered, layout)), "speculated, capacity-sized"
+        got = {f"{k}{v}": o[k].detach() for v, o in enumerate(outs) for k in keys}
+        got.update({f"vs{v}": o["viewspace_points"].grad for v, o in enumerate(outs)})
+        got["bucket"] = bucket.flat
+        for k in ref:
+            assert torch.equal(got[k], ref[k]), f"{k} (repeat {rep})"
+    assert bool(ref["bucket"].abs().sum() > 0)
+    # view 0 of the last batch against the oracle (its speculated binning, read at the capacity layout)
+    fwd = views_forward_dict(outs.batch, 0, outs[0]["render"], outs[0]["depth_3dgs"], outs[0]["radii"])
+    with torch.no_grad():
+        kw = dict(means3D=sc.get_xyz.cpu().numpy(), opacities=sc.get_opacity.cpu().numpy(),
+                  shs=sc.get_features.cpu().numpy(), scales=sc.get_scaling.cpu().numpy(),
+                  rotations=sc.get_rotation.cpu().numpy())
+    from dge_amd.cameras import orbit_camera
+
+    rs = _settings(orbit_camera(0, V, W, H, device="cpu"), torch.zeros(3), 1.0, 3)
+    compare_forward(fwd, run_oracle(oracle, rs, **kw), label="c2 timed path, view 0")
+
+
+def test_c2_speculated_overflow_at_full_size(cuda_device):
+    """A forced overflow at c2 size: the capacity history of this (P, W, H) holds a scene of the same
+    Gaussian count with none in view (a 64k-instance capacity against ~3.6M instances).  check() reports
+    it; the batch rendered again fits and equals the exact render (images, depths, radii, num_rendered)
+    and its backward equals the exact batch's bucket, bit for bit."""
+    from dge_amd.gaussian_renderer import PipelineParams
+    from dge_amd.multiview import GradBucket, render_views
+    from dge_amd.scene import synthetic_scene
+
+    dev = torch.device("cuda", 0)
+    P, W, H, V = 1_000_003, 512, 512, 3  # (a Gaussian count no other test renders: a fresh history)
+    sc, cams, seeds = _c2_bench_setup(dev, P, W, H, V)
+    bg = torch.zeros(3, device=dev)
+    far = synthetic_scene(P, sh_degree=3, seed=1, device=dev)
+    far._xyz += 1000.0
+    with torch.no_grad():
+        first = render_views(cams, far, PipelineParams(), bg, streams=3)
+        assert first.check() and max(first.batch.num_rendered) == 0
+    del far
+    bucket = GradBucket(sc.parameters())
+    res = {}
+    for mode in ("spec", "exact"):
+        bucket.zero()
+        outs = render_views(cams, sc, PipelineParams(), bg, streams=3, speculate=mode == "spec")
+        if mode == "spec":
+            torch.autograd.backward([o["render"] for o in outs], seeds)
+            assert not outs.check(), "the overflow must be reported"
+            print(f"[c2 overflow] reported: num_rendered {outs.batch.num_rendered}")
+            bucket.zero()
+            outs = render_views(cams, sc, PipelineParams(), bg, streams=3, speculate=True)
+        torch.autograd.backward([o["render"] for o in outs], seeds)
+        assert outs.check()
+        torch.cuda.synchronize()
+        res[mode] = ([{k: o[k].detach().clone() for k in ("render", "depth_3dgs", "radii")} for o in outs],
+                     list(outs.batch.num_rendered), bucket.flat.clone())
+    (a, ka, ga), (b, kb, gb) = res["spec"], res["exact"]
+    assert ka == kb and min(ka) > 1_000_000
+    for x, y in zip(a, b):
+        for k in x:
+            assert torch.equal(x[k], y[k]), k
+    assert torch.equal(ga, gb)
