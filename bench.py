@@ -589,6 +589,63 @@ def side_legs(args, scene, cams, seeds, bg, pipe, bucket, step, dev):
     legs["dge_semantic_forward"] = {"value": round(steps * V / dt, 3), "unit": "renders/s",
                                     "path": "render_views(override_color=mask), no_grad, forward only"}
 
+    # DGE's own loop, unchanged, on the render() that install_alias(fused_render=True) gives it:
+    # threestudio/systems/DGE.py forward() :170-239 per view (training render, radii max, the semantic
+    # render with the mask as override_color, its norm > 0.8 map, the masked visualisation — a boolean
+    # index, i.e. a host sync per view — the stacks), then the masked l1 of training_step (:672) and ONE
+    # backward; .grad set to None first (the optimizer's zero_grad).  No edit of DGE's code: its per-view
+    # host sync is part of what it costs.
+    from dge_amd.gaussian_renderer import render as fused_render
+    gts = [torch.rand(H_, W_, 3, generator=torch.Generator().manual_seed(50 + i)).to(dev)
+           for i, (H_, W_) in enumerate([(args.height, args.width)] * V)]
+    gm_dev = gm.to(dev)
+
+    def dge_loop():
+        for p in scene.parameters():
+            p.grad = None
+        prev_mask, scene.mask = scene.mask, gm_dev
+        try:
+            images, masks = [], []
+            radii = None
+            for i, cam in enumerate(cams):
+                pkg = fused_render(cam, scene, pipe, bg)
+                image, r = pkg["render"], pkg["radii"]
+                radii = r if i == 0 else torch.max(r, radii)
+                pkg["depth_3dgs"].permute(1, 2, 0)
+                sm = fused_render(cam, scene, pipe, bg, override_color=scene.mask[..., None].float().repeat(1, 3))["render"]
+                sm = torch.norm(sm, dim=0) > 0.8
+                viz = image.detach().clone().permute(1, 2, 0)
+                viz[sm] = 0.40 * viz[sm] + 0.60 * torch.tensor([1.0, 0.0, 0.0], device=dev)
+                masks.append(sm)
+                images.append(image.permute(1, 2, 0))
+            images = torch.stack(images, 0)
+            m = torch.stack(masks, 0)[..., None].float()
+            loss = torch.nn.functional.l1_loss(images * m, torch.stack(gts, 0) * m)
+            loss.backward()
+        finally:
+            scene.mask = prev_mask
+
+    for _ in range(3):
+        dge_loop()
+    dt = _time(dge_loop, steps)
+    from dge_amd import gaussian_renderer as GR
+    lazy = GR._LAZY_OVERRIDE
+    GR._LAZY_OVERRIDE = False
+    try:
+        for _ in range(2):
+            dge_loop()
+        dt_eager = _time(dge_loop, steps)
+    finally:
+        GR._LAZY_OVERRIDE = lazy
+    legs["dge_loop_unchanged"] = {
+        "value": round(steps * V / dt, 3), "unit": "views/s",
+        "path": "DGE.py forward() per view (fused render(), semantic render, boolean-mask viz: a host sync per "
+                "view) + masked l1 + one backward, install_alias(fused_render=True), no code edit",
+        "semantic_eager_value": round(steps * V / dt_eager, 3)}
+    for p in scene.parameters():
+        p.grad = None
+    bucket.attach()
+
     def step_sem():
         step()
         sem()

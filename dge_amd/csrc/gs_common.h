@@ -264,28 +264,36 @@ __device__ __forceinline__ bool cull_keep(float2 xy, float4 co, float bx0, float
     if (o < 1.0f / 255.0f) return false;  // alpha <= o*G <= o   (NaN falls through: keep)
     const float a = co.x, b = co.y, c = co.z;
     if (!(a > 0.f && c > 0.f && a * c - b * b > 0.f)) return true;  // not positive definite: no bound
-    const float thr = 2.0f * __logf(255.0f * o);  // the slack below absorbs __logf's error
+    // (v_log_f32: 255 o >= 1 here, no denormal; the slack below absorbs its ~1-ulp error)
+    const float thr = (2.0f * 0.693147182f) * __builtin_amdgcn_logf(255.0f * o);
     const float X0 = xy.x - (bx0 + 7.0f), X1 = xy.x - bx0;
     const float Y0 = xy.y - (by0 + 7.0f), Y1 = xy.y - by0;
     if (X0 <= 0.f && X1 >= 0.f && Y0 <= 0.f && Y1 >= 0.f) return true;
     const float slack = 2e-3f * (1.0f + fabsf(thr));
-    bool keep = false;
+    // the minimisers below only choose WHERE the quadratic is evaluated: a 1-ulp reciprocal moves them by
+    // ~1e-7 relative, which changes the evaluated value at second order, far inside the slack (an IEEE
+    // division here was ~40 of the cull's ~136 VALU per 64 list positions)
+    const float rc = __builtin_amdgcn_rcpf(c), ra = __builtin_amdgcn_rcpf(a);
+    // the smallest of the four edge minima against the level (fminf drops a NaN edge, which could
+    // not pass its own comparison either)
+    float qmin;
     // edges dx = X: minimise over dy
 #pragma unroll
     for (int e = 0; e < 2; ++e) {
         const float X = e ? X1 : X0;
-        const float dy = fminf(Y1, fmaxf(Y0, __fdividef(-b * X, c)));
+        const float dy = fminf(Y1, fmaxf(Y0, (-b * X) * rc));
         const float t1 = a * X * X, t2 = 2.f * b * X * dy, t3 = c * dy * dy;
-        keep |= (t1 + t2 + t3) - 1e-5f * (t1 + fabsf(t2) + t3) <= thr + slack;
+        const float q = (t1 + t2 + t3) - 1e-5f * (t1 + fabsf(t2) + t3);
+        qmin = e ? fminf(qmin, q) : q;
     }
 #pragma unroll
     for (int e = 0; e < 2; ++e) {
         const float Y = e ? Y1 : Y0;
-        const float dx = fminf(X1, fmaxf(X0, __fdividef(-b * Y, a)));
+        const float dx = fminf(X1, fmaxf(X0, (-b * Y) * ra));
         const float t1 = a * dx * dx, t2 = 2.f * b * dx * Y, t3 = c * Y * Y;
-        keep |= (t1 + t2 + t3) - 1e-5f * (t1 + fabsf(t2) + t3) <= thr + slack;
+        qmin = fminf(qmin, (t1 + t2 + t3) - 1e-5f * (t1 + fabsf(t2) + t3));
     }
-    return keep;
+    return qmin <= thr + slack;
 }
 
 // =====================================================================

@@ -112,9 +112,11 @@ class _RasterizeGaussiansFused(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, xyz, means2D, f_dc, f_rest, colors, raw_opacity, raw_scaling, raw_rotation, raster_settings,
-                index=None, visible=None, prepared=None):
+                index=None, visible=None, prepared=None, recompute=False):
         # prepared: the first half of this very forward, already enqueued by rasterize_gaussians_fused_begin
-        # with these inputs (dge_amd.multiview.render_views begins every view before ending any)
+        # with these inputs (dge_amd.multiview.render_views begins every view before ending any).
+        # recompute: `prepared` is a forward_only render (no backward bookkeeping in its buffers); a
+        # backward, if one comes, first renders the same inputs again with it
         rs = raster_settings
         if prepared is not None:
             num_rendered, color, depth, radii, geomBuffer, binningBuffer, imgBuffer = \
@@ -129,6 +131,7 @@ class _RasterizeGaussiansFused(torch.autograd.Function):
         ctx.raster_settings = rs
         ctx.index = index
         ctx.num_rendered = num_rendered
+        ctx.recompute = bool(recompute)
         ctx.has_sh = f_dc is not None and f_dc.numel() != 0
         ctx.save_for_backward(xyz, f_dc, f_rest, colors, raw_opacity, raw_scaling, raw_rotation, radii, geomBuffer,
                               binningBuffer, imgBuffer)
@@ -138,10 +141,20 @@ class _RasterizeGaussiansFused(torch.autograd.Function):
     @staticmethod
     def backward(ctx, grad_out_color, grad_radii, grad_depth):
         if grad_out_color is None:
-            return (None,) * 12
+            return (None,) * 13
         rs = ctx.raster_settings
         (xyz, f_dc, f_rest, colors, raw_opacity, raw_scaling, raw_rotation, radii, geomBuffer, binningBuffer,
          imgBuffer) = ctx.saved_tensors
+        if ctx.recompute:  # (a lazy forward-only render: its buffers hold no backward bookkeeping)
+            fa = (rs.bg, xyz, f_dc, f_rest, colors, raw_opacity, raw_scaling, raw_rotation, rs.scale_modifier,
+                  rs.viewmatrix, rs.projmatrix, rs.tanfovx, rs.tanfovy, rs.image_height, rs.image_width,
+                  rs.sh_degree, rs.campos, rs.prefiltered, rs.debug)
+            ctx.num_rendered, _, _, radii, geomBuffer, binningBuffer, imgBuffer = _C.rasterize_gaussians_fused(
+                *fa, index=ctx.index)
+            ctx.recompute = False
+            ctx.lazy_buffers = (radii, geomBuffer, binningBuffer, imgBuffer)  # (a second backward reuses them)
+        elif getattr(ctx, "lazy_buffers", None) is not None:
+            radii, geomBuffer, binningBuffer, imgBuffer = ctx.lazy_buffers
         # Fused gradient accumulation: where autograd would add this gradient into a parameter's .grad
         # itself, the kernel writes (or adds) it there directly and autograd receives None — saving the
         # separate read-modify-write pass over every parameter.
@@ -216,7 +229,7 @@ class _RasterizeGaussiansFused(torch.autograd.Function):
             d_rot = None
         if "sh" in into:
             d_dc = d_rest = None
-        return d_xyz, d_m2, d_dc, d_rest, d_col, d_op, d_sc, d_rot, None, None, None, None
+        return d_xyz, d_m2, d_dc, d_rest, d_col, d_op, d_sc, d_rot, None, None, None, None, None
 
 
 _FUSED_GRAD_ACCUM = os.environ.get("DGE_AMD_FUSED_GRAD_ACCUM", "1") != "0"
@@ -339,7 +352,7 @@ def _into_target(p, mode, direct, zero=False):
 
 
 def rasterize_gaussian_model(xyz, means2D, features_dc, features_rest, colors_precomp, raw_opacity, raw_scaling,
-                             raw_rotation, raster_settings, index=None, visible=None, prepared=None):
+                             raw_rotation, raster_settings, index=None, visible=None, prepared=None, recompute=False):
     """(color, radii, depth) of a GaussianModel given its raw tensors (_xyz, _features_dc, _features_rest or
     colors_precomp, _opacity, _scaling, _rotation); activations are applied in-kernel.  `index` (int32,
     ascending): render only those rows — the model's `localize` subset pc[mask] — gathering them
@@ -349,7 +362,7 @@ def rasterize_gaussian_model(xyz, means2D, features_dc, features_rest, colors_pr
     return _RasterizeGaussiansFused.apply(
         xyz, means2D, empty if features_dc is None else features_dc, empty if features_rest is None else features_rest,
         empty if colors_precomp is None else colors_precomp, raw_opacity, raw_scaling, raw_rotation, raster_settings,
-        index, visible, prepared)
+        index, visible, prepared, recompute)
 
 
 class GaussianRasterizationSettings(NamedTuple):

@@ -159,6 +159,9 @@ def _render_fused(viewpoint_camera, pc, pipe, bg_color, scaling_modifier=1.0, ov
     return _fused_end(_fused_begin(viewpoint_camera, pc, pipe, bg_color, scaling_modifier, override_color), pc)
 
 
+_LAZY_OVERRIDE = os.environ.get("DGE_AMD_LAZY_OVERRIDE", "1") != "0"
+
+
 def _may_backward(*tensors) -> bool:
     """Whether autograd can run a backward of a forward of these inputs (grad mode on and one of them
     requires grad): else the kernels skip the backward's scratch (gs_params.forward_only).  The view-space
@@ -180,8 +183,13 @@ def _fused_begin(viewpoint_camera, pc, pipe, bg_color, scaling_modifier=1.0, ove
     else:
         f_dc, f_rest, colors = None, None, override_color.float()
     visible = torch.empty(n, dtype=torch.bool, device=xyz.device)  # radii > 0, written by the preprocess
+    may_bwd = _may_backward(xyz, f_dc, f_rest, colors, pc._opacity, pc._scaling, pc._rotation)
+    # DGE's semantic render (DGE.py:198-204: override_color = the edit mask, grad mode on, its image only
+    # thresholded) never receives a gradient: render it with the forward-only kernels and, should a
+    # backward come after all, recompute the forward with the backward's bookkeeping then (lazy)
+    lazy = may_bwd and colors is not None and not colors.requires_grad and _LAZY_OVERRIDE
     st = {"rs": rs, "index": index, "n": n, "f_dc": f_dc, "f_rest": f_rest, "colors": colors, "visible": visible,
-          "prepared": None}
+          "prepared": None, "lazy": lazy}
     if rs.debug:  # debug mode: the one-call forward, which keeps the reference's failure snapshot
         return st
     empty = torch.empty(0, dtype=torch.float32, device=xyz.device)
@@ -189,8 +197,7 @@ def _fused_begin(viewpoint_camera, pc, pipe, bg_color, scaling_modifier=1.0, ove
         rs.bg, xyz, empty if f_dc is None else f_dc, empty if f_rest is None else f_rest,
         empty if colors is None else colors, pc._opacity, pc._scaling, pc._rotation, rs.scale_modifier,
         rs.viewmatrix, rs.projmatrix, rs.tanfovx, rs.tanfovy, rs.image_height, rs.image_width, rs.sh_degree,
-        rs.campos, rs.prefiltered, rs.debug, index=index, visible=visible,
-        forward_only=not _may_backward(xyz, f_dc, f_rest, colors, pc._opacity, pc._scaling, pc._rotation))
+        rs.campos, rs.prefiltered, rs.debug, index=index, visible=visible, forward_only=lazy or not may_bwd)
     return st
 
 
@@ -200,7 +207,7 @@ def _fused_end(st, pc):
     screenspace_points = _viewspace_zeros(st["n"], xyz.dtype, xyz.device)
     rendered_image, radii, depth = rasterize_gaussian_model(
         xyz, screenspace_points, st["f_dc"], st["f_rest"], st["colors"], pc._opacity, pc._scaling, pc._rotation,
-        st["rs"], st["index"], st["visible"], prepared=st["prepared"])
+        st["rs"], st["index"], st["visible"], prepared=st["prepared"], recompute=st["lazy"] and st["prepared"] is not None)
     return {
         "render": rendered_image,
         "viewspace_points": screenspace_points,

@@ -669,7 +669,14 @@ def test_c2_timed_path_matches_per_view_loop(cuda_device, oracle):
     # view 0 of the last batch against the oracle (its speculated binning, read at the capacity layout)
     fwd = views_forward_dict(outs.batch, 0, outs[0]["render"], outs[0]["depth_3dgs"], outs[0]["radii"])
     with torch.no_grad():
-        kw = dict(means3D=sc.get_xyz.cpu().numpy(), opacities=sc.get_opacity.cpu().numpy(),
+        # the oracle takes activated parameters; the kernels activate the raw ones in-kernel (sigmoid /
+        # exp / normalize on the device's libm), so the activated opacity the blend used — the Splat's
+        # conic_opacity.w, for every Gaussian in view — is what the oracle gets (torch's CPU sigmoid
+        # differs from the device's in the last bit for ~1/3 of the Gaussians)
+        op = sc.get_opacity.cpu().numpy().copy()
+        vis = fwd["radii"] > 0
+        op[vis, 0] = fwd["conic_opacity"][vis, 3]
+        kw = dict(means3D=sc.get_xyz.cpu().numpy(), opacities=op,
                   shs=sc.get_features.cpu().numpy(), scales=sc.get_scaling.cpu().numpy(),
                   rotations=sc.get_rotation.cpu().numpy())
     from dge_amd.cameras import orbit_camera
@@ -719,3 +726,38 @@ def test_c2_speculated_overflow_at_full_size(cuda_device):
         for k in x:
             assert torch.equal(x[k], y[k]), k
     assert torch.equal(ga, gb)
+
+
+def test_lazy_override_color_render(cuda_device, monkeypatch):
+    """DGE's semantic render (render(..., override_color=mask colours) with grad mode on, DGE.py:198-204)
+    runs the forward-only kernels; its image, depth and radii equal the eager training render's, and a
+    backward through it (which DGE never runs) recomputes the forward with the backward's bookkeeping and
+    gives the eager render's gradients bit for bit — also a second backward (retain_graph)."""
+    from dge_amd import gaussian_renderer as GR
+    from dge_amd.cameras import orbit_camera
+    from dge_amd.gaussian_renderer import PipelineParams, render
+    from dge_amd.scene import synthetic_scene
+
+    dev = torch.device("cuda", 0)
+    W, H = 256, 192
+    cam = orbit_camera(1, 4, W, H, device=dev)
+    G = torch.randn(3, H, W, generator=torch.Generator().manual_seed(4)).to(dev)
+    colors = torch.rand(50_000, 3, generator=torch.Generator().manual_seed(5)).to(dev)
+    res = {}
+    for lazy in (True, False):
+        monkeypatch.setattr(GR, "_LAZY_OVERRIDE", lazy)
+        sc = synthetic_scene(50_000, seed=9, device=dev).requires_grad_(True)
+        pkg = render(cam, sc, PipelineParams(), torch.zeros(3, device=dev), override_color=colors)
+        out = [pkg[k].detach().clone() for k in ("render", "depth_3dgs", "radii")]
+        (pkg["render"] * G).sum().backward(retain_graph=True)
+        g1 = [p.grad.clone() for p in (sc._xyz, sc._opacity, sc._scaling, sc._rotation)]
+        (pkg["render"] * G).sum().backward()
+        g2 = [p.grad.clone() for p in (sc._xyz, sc._opacity, sc._scaling, sc._rotation)]
+        torch.cuda.synchronize()
+        res[lazy] = (out, g1, g2, pkg["viewspace_points"].grad.clone())
+    (oa, ga1, ga2, va), (ob, gb1, gb2, vb) = res[True], res[False]
+    for x, y in zip(oa, ob):
+        assert torch.equal(x, y)
+    assert torch.equal(va, vb) and bool(va.abs().sum() > 0)
+    for x, y in zip(ga1 + ga2, gb1 + gb2):
+        assert torch.equal(x, y)
