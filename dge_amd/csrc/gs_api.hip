@@ -120,6 +120,13 @@ int depth_pass_bits() {
     return bits;
 }
 
+// DGE_AMD_VIEWS_BWD=merged: a batch's per-Gaussian passes as one launch after every replay (round 3's
+// form) instead of staggered per-view passes (read per call: A/B)
+bool views_bwd_merged() {
+    const char* e = getenv("DGE_AMD_VIEWS_BWD");
+    return e && !strcmp(e, "merged");
+}
+
 // Pinned read-back slot of one forward's preprocess counters + its event.  A
 // pool per device: several forwards may be between begin and end at once
 // (gs_rasterize_forward_begin / _end), each holding its own slot.
@@ -1091,9 +1098,11 @@ struct gs_views {
     int spec[GS_MAX_VIEWS] = {};         // 1: capacity-sized, count checked by gs_views_check
     long long K[GS_MAX_VIEWS] = {};      // instance count, -1 until the host knows it
     hipEvent_t ev[GS_MAX_VIEWS] = {};    // the end of each view's work (forward, or per-Gaussian backward pass)
+    hipEvent_t ev_r[GS_MAX_VIEWS] = {};  // the end of each view's gradient replay (staggered backward)
     hipEvent_t fork = nullptr;           // the caller's stream, before the views' work
     ~gs_views() {
         for (int v = 0; v < GS_MAX_VIEWS; ++v) event_pool().put(ev[v]);
+        for (int v = 0; v < GS_MAX_VIEWS; ++v) event_pool().put(ev_r[v]);
         event_pool().put(fork);
     }
 };
@@ -1295,6 +1304,35 @@ int gs_views_backward(gs_views* h, const float* const* dL_dpix, const gs_grads* 
         }
         int rc0 = fork_from(h, join, streams);  // (the image gradients come from the caller's stream)
         if (rc0) return rc0;
+        if (h->n > 1 && views_mergeable(h, grads) && !views_bwd_merged()) {
+            // staggered: view v's replay on its stream after view v-1's replay, then its own per-Gaussian
+            // pass there after view v-1's pass (the accumulation in view order, bitwise the per-view
+            // calls') — so view v-1's pass runs beside view v's replay instead of every pass queueing
+            // behind the last replay (round 3's merged pass: a ~165-us serial tail per step)
+            for (int v = 0; v < h->n; ++v) {
+                FwdState& f = h->f[v];
+                hipStream_t sv = (hipStream_t)streams[v];
+                const bool debug = f.s.debug != 0;
+                hipStream_t stream = sv;  // (GS_LAUNCHED)
+                if (v > 0 && streams[v - 1] != streams[v]) GS_HIP(hipStreamWaitEvent(sv, h->ev_r[v - 1], 0));
+                int rc = replay_view(&f.s, &f.gp, (int)h->layout[v], f.geom, h->bin[v], f.img, dL_dpix[v], sv);
+                if (rc) return rc;
+                if (!h->ev_r[v] && !(h->ev_r[v] = event_pool().get())) return set_error(GS_ERR_HIP, "could not create an event");
+                GS_HIP(hipEventRecord(h->ev_r[v], sv));
+                hipEvent_t wa = v == 0 ? (hipEvent_t)writes_after
+                                       : (streams[v - 1] != streams[v] ? h->ev[v - 1] : nullptr);
+                const GaussBwdArgs ga = gauss_args(&f.s, &f.gp, (int)h->layout[v], f.radii, f.geom, h->bin[v], grads[v],
+                                                   h->spec[v] ? h->layout[v] : 0xFFFFFFFFu);
+                GS_SKIP("gauss") { StageScope sc(ST_GAUSS_BWD, sv); launch_gauss_backward(ga, sv, wa); }
+                GS_LAUNCHED("gaussian backward (staggered)");
+                if (!h->ev[v] && !(h->ev[v] = event_pool().get())) return set_error(GS_ERR_HIP, "could not create an event");
+                GS_HIP(hipEventRecord(h->ev[v], sv));
+            }
+            // the last pass waited for every earlier one (and each for its replay): join on it
+            hipStream_t sl = (hipStream_t)streams[h->n - 1];
+            if (sl != join) GS_HIP(hipStreamWaitEvent(join, h->ev[h->n - 1], 0));
+            return GS_OK;
+        }
         if (h->n > 1 && views_mergeable(h, grads)) {
             // every view's replay on its stream, then ONE per-Gaussian pass over all of them (chunks of
             // gauss_backward_max_views() views, in view order) on the first view's stream
