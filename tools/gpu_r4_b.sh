@@ -8,7 +8,7 @@ timeout -k 10 600 python -u -m pytest -x -q -s --timeout 300 --timeout-method th
 tail -3 $O/pytest_gpu.log
 grep -E "^\[(c2|overflow|deferred|parity c2)" $O/pytest_gpu.log | head -20
 timeout -k 10 120 tools/probes/rocprim_sort_time > $O/rocprim_sort.txt 2>&1; cat $O/rocprim_sort.txt
-DGE_AMD_VIEWS_BWD=merged NOTESTS=1 ROUNDS=2 bash tools/gpu_ab.sh || exit 1
+DGE_AMD_VIEWS_BWD=merged VARS="base wfma" NOTESTS=1 ROUNDS=2 bash tools/gpu_ab.sh || exit 1
 VAR=DGE_AMD_VIEWS_BWD VALS="merged stagger" NOTESTS=1 ROUNDS=2 bash tools/gpu_env_ab.sh || exit 1
 timeout -k 10 300 python tools/warn_trace.py --steps 5 --warmup 3 --no-cpu-baseline > $O/warn.json 2> $O/warn.err || { tail -20 $O/warn.err; exit 1; }
 grep -A25 "warn-trace" $O/warn.err | head -40
