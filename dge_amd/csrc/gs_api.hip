@@ -439,6 +439,7 @@ int bin_after_preprocess(FwdState& f, hipStream_t stream) {
     ea.P = P; ea.gx = g.gx; ea.gy = g.gy;
     ea.order = at<uint2>(geom, cur ? gl.val1 : gl.val0);
     ea.rect_packed = pa.rect_packed;
+    ea.qmask = qmask_enabled(P) ? 1 : 0;
     ea.tiles_touched = pa.tiles_touched;
     ea.splat = pa.splat;
     ea.radii = pa.radii;
@@ -654,6 +655,8 @@ int render_launch(FwdState& f, void* bin, uint32_t K_layout, int order_ready, fl
     ra.out_depth = out_depth;
     ra.touched = at<uint8_t>(geom, gl.touched);
     ra.diag = diag_buffer(0, kDiagWords * (size_t)g.tiles * 4);
+    ra.qmask = qmask_enabled(f.gp.P) ? 1 : 0;
+    ra.id_mask = id_mask_for(f.gp.P);
     GS_SKIP("fwd") { StageScope sc(ST_RENDER_FWD, stream); launch_render_forward(ra, stream); }
     GS_LAUNCHED("render");
     return GS_OK;
@@ -693,6 +696,7 @@ int replay_view(const gs_settings* s, const gs_params* gp, int R, const void* ge
     rb.W = g.W; rb.H = g.H; rb.gx = g.gx; rb.gy = g.gy;
     rb.ranges = at<uint2>(img, il.ranges);
     rb.point_pairs = at<uint2>(binning, bl.point_pairs);
+    rb.id_mask = id_mask_for(P);
     rb.bwd_items = at<uint2>(binning, bl.bwd_items);
     rb.bwd_count = at<uint32_t>(const_cast<void*>(img), il.bwd_count);
     rb.tile_last = at<uint32_t>(img, il.tile_last);
@@ -783,6 +787,14 @@ struct gs_forward_state {
 namespace gs {
 int report_error(int code, const char* msg) { return set_error(code, "%s", msg); }
 
+bool qmask_enabled(int P) {
+    static const bool on = [] {
+        const char* e = getenv("DGE_AMD_QMASK");
+        return !(e && !strcmp(e, "0"));
+    }();
+    return on && P >= 0 && P < (1 << kIdBits);
+}
+
 uint64_t* diag_buffer(int which, size_t n_u64) {
     Diag& d = diag();
     if (!d.on.load()) return nullptr;
@@ -860,6 +872,17 @@ int gs_blend_exp(long long n, const float* x, float* y, gs_stream_t stream) {
     gs::launch_blend_exp(n, x, y, (hipStream_t)stream);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? GS_OK : set_error(GS_ERR_HIP, "gs_blend_exp launch failed: %s", hipGetErrorString(e));
+}
+
+int gs_activate_params(int P, const float* raw_opacity, const float* raw_scaling, const float* raw_rotation,
+                       float* opacity, float* scaling, float* rotation, gs_stream_t stream) {
+    if (P < 0 || (opacity && !raw_opacity) || (scaling && !raw_scaling) || (rotation && !raw_rotation))
+        return set_error(GS_ERR_INVALID_ARG, "gs_activate_params: bad arguments");
+    if (P == 0) return GS_OK;
+    gs::launch_activate_params(P, raw_opacity, raw_scaling, raw_rotation, opacity, scaling, rotation,
+                               (hipStream_t)stream);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? GS_OK : set_error(GS_ERR_HIP, "gs_activate_params launch failed: %s", hipGetErrorString(e));
 }
 
 size_t gs_geometry_buffer_size(int P) { return geom_layout(P).total; }
@@ -1473,6 +1496,8 @@ int gs_apply_weights(const gs_settings* s, int P, int M, const float* means3D, f
         aw.image_weights = image_weights;
         aw.weights = weights;
         aw.cnt = cnt;
+        aw.qmask = qmask_enabled(P) ? 1 : 0;
+        aw.id_mask = id_mask_for(P);
         { StageScope sc(ST_APPLY_WEIGHTS, stream); launch_render_apply_weights(aw, stream); }
         GS_LAUNCHED("apply_weights render");
         return GS_OK;

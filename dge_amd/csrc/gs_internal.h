@@ -25,6 +25,8 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include "gs_qmask.h"
+
 namespace gs {
 
 constexpr int kSortIPT = 16;                    // keys per thread in the tile-key radix kernels
@@ -257,6 +259,9 @@ struct PreprocessArgs {
 void launch_preprocess(const PreprocessArgs& a, hipStream_t s);
 void launch_depth_keys32(int P, const uint32_t* rect, const Splat* splat, uint32_t* key, hipStream_t s);
 void launch_mark_visible(int P, const float* means3D, const float* view, uint8_t* present, hipStream_t s);
+// (test hook gs_activate_params) the fused path's in-kernel activations over P rows
+void launch_activate_params(int P, const float* raw_opacity, const float* raw_scaling, const float* raw_rotation,
+                            float* opacity, float* scaling, float* rotation, hipStream_t s);
 
 // LSD radix sort of (u32 key, u32 value).  Returns the buffer index (0/1)
 // holding the result.  identity_vals: values of the first pass are the
@@ -314,7 +319,14 @@ struct EmitArgs {
     // ids_only (a forward-only render's two-level binning): the lists carry the Gaussian id alone (u32 at
     // pairs_out / the point list) — the binning slot is only the backward's record address
     int ids_only = 0;
+    // qmask: every emitted id carries its quadrant mask in bits kIdBits.. (gs_qmask.h; qmask_enabled)
+    int qmask = 0;
 };
+// The emission's per-instance quadrant masks (gs_qmask.h) for a P-Gaussian render: on unless
+// DGE_AMD_QMASK=0 (A/B: the blend's per-wave cull_keep instead), and only while ids fit kIdBits.
+// id_mask_for(P): what strips the mask from a list's id (all ones when there is none).
+bool qmask_enabled(int P);
+inline uint32_t id_mask_for(int P) { return qmask_enabled(P) ? kIdMask : 0xFFFFFFFFu; }
 void launch_scan_reduce(const EmitArgs& a, hipStream_t s);
 void launch_scan_emit(const EmitArgs& a, hipStream_t s);
 // two-level binning after the instance count is known: column scan + k_scan_emit_x, the row pass
@@ -361,6 +373,8 @@ struct RenderArgs {
                           // exactly the Gaussians the backward gives a record, known after the forward
     uint64_t* diag;       // optional [tiles*4][kDiagWords] (see diag_buffer)
     int bwd = 1;          // 0: a forward-only render (gs_params.forward_only): no backward bookkeeping
+    int qmask = 0;        // the list ids carry the emission's quadrant masks (else: cull_keep per wave)
+    uint32_t id_mask = 0xFFFFFFFFu;
 };
 void launch_render_forward(const RenderArgs& a, hipStream_t s);
 
@@ -372,6 +386,8 @@ struct ApplyWeightsArgs {
     const float* image_weights;
     float* weights;
     int* cnt;
+    int qmask = 0;  // (as RenderArgs)
+    uint32_t id_mask = 0xFFFFFFFFu;
 };
 void launch_render_apply_weights(const ApplyWeightsArgs& a, hipStream_t s);
 void launch_blend_exp(long long n, const float* x, float* y, hipStream_t s);
@@ -395,6 +411,7 @@ struct RenderBwdArgs {
     float4* records;     // [4*K][3] float4: one record per (slot, quadrant), kept entries only
     uint8_t* rec_flags;  // [4*K] set to 1 with each record (zeroed before the launch)
     uint64_t* diag;   // optional [item_cap][kDiagWords], by queue position (see diag_buffer)
+    uint32_t id_mask = 0xFFFFFFFFu;  // strips the emission's quadrant masks from the list ids
 };
 void launch_render_backward(const RenderBwdArgs& a, hipStream_t s);
 

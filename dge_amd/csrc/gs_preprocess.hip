@@ -290,6 +290,36 @@ void launch_depth_keys32(int P, const uint32_t* rect, const Splat* splat, uint32
     hipLaunchKernelGGL(k_depth_keys32, dim3(div_up(P, 256)), dim3(256), 0, s, P, rect, splat, key);
 }
 
+// test hook: the activations k_preprocess applies to raw parameters (gs_params.activation), same device
+// functions, so the oracle can be handed exactly the values the fused path used
+__global__ __launch_bounds__(256) void k_activate_params(int P, const float* __restrict__ raw_opacity,
+                                                         const float* __restrict__ raw_scaling,
+                                                         const float* __restrict__ raw_rotation,
+                                                         float* __restrict__ opacity, float* __restrict__ scaling,
+                                                         float* __restrict__ rotation) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= P) return;
+    if (opacity) opacity[i] = act_sigmoid(raw_opacity[i]);
+    if (scaling) {
+        const f3 sc = ld3(raw_scaling + 3 * (size_t)i);
+        scaling[3 * (size_t)i] = expf(sc.x);
+        scaling[3 * (size_t)i + 1] = expf(sc.y);
+        scaling[3 * (size_t)i + 2] = expf(sc.z);
+    }
+    if (rotation) {
+        float len;
+        const float4 q = act_normalize(*reinterpret_cast<const float4*>(raw_rotation + 4 * (size_t)i), len);
+        *reinterpret_cast<float4*>(rotation + 4 * (size_t)i) = q;
+    }
+}
+
+void launch_activate_params(int P, const float* raw_opacity, const float* raw_scaling, const float* raw_rotation,
+                            float* opacity, float* scaling, float* rotation, hipStream_t s) {
+    if (P <= 0) return;
+    hipLaunchKernelGGL(k_activate_params, dim3(div_up(P, 256)), dim3(256), 0, s, P, raw_opacity, raw_scaling,
+                       raw_rotation, opacity, scaling, rotation);
+}
+
 // checkFrustum (rasterizer_impl.cu:53-63)
 __global__ __launch_bounds__(256) void k_mark_visible(int P, const float* __restrict__ means3D,
                                                       const float* __restrict__ view, uint8_t* __restrict__ present) {

@@ -617,6 +617,7 @@ __global__ __launch_bounds__(256) void k_scan_emit(EmitArgs a) {
     __shared__ uint32_t s_start[256];
     __shared__ uint32_t s_gauss[256];
     __shared__ int4 s_rect[256];  // x0, y0, width, -
+    __shared__ QuadCull s_qc[256];  // qmask: the round's Gaussians' ellipse bounds (gs_qmask.h)
     // the block's first slot: the sum of the block sums before it (k_scan_reduce's, read from L2:
     // at most scan_blocks words; this replaced a one-workgroup top-level scan launch)
     uint32_t base;
@@ -644,6 +645,12 @@ __global__ __launch_bounds__(256) void k_scan_emit(EmitArgs a) {
                 q = tile_rect(xy.x, xy.y, a.radii[g], a.gx, a.gy);
             }
             s_rect[threadIdx.x] = make_int4(q.x0, q.y0, q.x1 - q.x0, 0);
+            if (a.qmask) {
+                const Splat* sp = a.splat + g;
+                const float2 xy = sp->xy;
+                const float4 co = sp->co;
+                s_qc[threadIdx.x] = quad_cull_setup(xy.x, xy.y, co.x, co.y, co.z, co.w);
+            }
         }
         s_start[threadIdx.x] = off;
         s_gauss[threadIdx.x] = g;
@@ -662,8 +669,11 @@ __global__ __launch_bounds__(256) void k_scan_emit(EmitArgs a) {
             const uint32_t ky = (uint32_t)(((float)k + 0.5f) / (float)q.z);  // exact: k < 2^20, margin 0.5/width
             const uint32_t kx = k - ky * (uint32_t)q.z;
             if (base + j >= a.cap) break;  // speculative capacity exceeded (gs_views_check reports it)
-            a.tile_key[base + j] = (uint32_t)((q.y + (int)ky) * a.gx + q.x + (int)kx);
-            a.slot_gauss[base + j] = s_gauss[lo];
+            const int tx = q.x + (int)kx, ty = q.y + (int)ky;
+            a.tile_key[base + j] = (uint32_t)(ty * a.gx + tx);
+            uint32_t gv = s_gauss[lo];
+            if (a.qmask) gv |= quad_mask(s_qc[lo], (float)(16 * tx), (float)(16 * ty)) << kIdBits;
+            a.slot_gauss[base + j] = gv;
             if (a.rec_flags32) a.rec_flags32[base + j] = 0u;  // slot's four quadrant flags (no memset launch)
         }
         base += total;
@@ -696,6 +706,7 @@ __global__ __launch_bounds__(256) void k_scan_emit_x(EmitArgs a) {
     __shared__ PV s_pair[kEmitBatch];
     __shared__ uint16_t s_own[kEmitBatch];  // the batch's owners (+1): marks at the entries' starts, prefix max
     __shared__ uint32_t s_carry;
+    __shared__ QuadCull s_qc[256];  // qmask: the round's Gaussians' ellipse bounds (gs_qmask.h)
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     if (blockIdx.x == 0)
         for (int t = tid; t < a.ntiles; t += 256) a.tile_count[t] = 0u;  // (the row pass counts into it)
@@ -725,6 +736,12 @@ __global__ __launch_bounds__(256) void k_scan_emit_x(EmitArgs a) {
             a.first_slot[g] = base + off;
             s_rect[tid] = make_int4((int)(gr.x & 0xFFu), (int)((gr.x >> 8) & 0xFFu),
                                     (int)((gr.x >> 16) & 0xFFu) - (int)(gr.x & 0xFFu), 0);
+            if (a.qmask) {
+                const Splat* sp = a.splat + g;
+                const float2 xy = sp->xy;
+                const float4 co = sp->co;
+                s_qc[tid] = quad_cull_setup(xy.x, xy.y, co.x, co.y, co.z, co.w);
+            }
         }
         s_start[tid] = off;
         s_gauss[tid] = g;
@@ -779,8 +796,10 @@ __global__ __launch_bounds__(256) void k_scan_emit_x(EmitArgs a) {
                 const uint32_t kx = k - ky * (uint32_t)q.z;
                 const uint32_t x = (uint32_t)q.x + kx, y = (uint32_t)q.y + ky;
                 kk[e] = y << kXBits | x;
-                if constexpr (IDS) pv[e] = s_gauss[lo];
-                else pv[e] = make_uint2(s_gauss[lo], base + j);
+                uint32_t gv = s_gauss[lo];
+                if (a.qmask && valid) gv |= quad_mask(s_qc[lo], (float)(16 * x), (float)(16 * y)) << kIdBits;
+                if constexpr (IDS) pv[e] = gv;
+                else pv[e] = make_uint2(gv, base + j);
                 if (valid && a.rec_flags32 && base + j < a.cap) a.rec_flags32[base + j] = 0u;  // (slot order: coalesced)
                 const uint32_t d = valid ? x : 0u;
                 const uint64_t peers = match_digit<kXBits>(d, vm);

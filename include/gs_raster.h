@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define GS_RASTER_ABI_VERSION 14
+#define GS_RASTER_ABI_VERSION 15
 
 #define GS_OK 0
 #define GS_ERR_INVALID_ARG 1   /* AT_ERROR / std::runtime_error in the reference */
@@ -389,6 +389,14 @@ long long gs_profile_diag_read(int which, uint64_t *host, long long max_u64);
  * device, evaluated exactly as the blend kernels do (packed pairs); bit-identical
  * to the oracle's gs_expf.  Returns GS_OK or an error code. */
 int gs_blend_exp(long long n, const float *x, float *y, gs_stream_t stream);
+
+/* Test hook: the raw-parameter activations the fused path applies in-kernel
+ * (gs_params.activation; gaussian_model.py:42-57 get_opacity / get_scaling /
+ * get_rotation: sigmoid, exp, F.normalize), over P rows on the device with the
+ * preprocess's own device functions — what the oracle must be given to see the
+ * values the kernels used.  Any output may be NULL (its input is then not read). */
+int gs_activate_params(int P, const float *raw_opacity, const float *raw_scaling, const float *raw_rotation,
+                       float *opacity, float *scaling, float *rotation, gs_stream_t stream);
 
 const char *gs_last_error(void);
 int gs_abi_version(void);

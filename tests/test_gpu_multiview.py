@@ -3,6 +3,7 @@ the 3-view step reductions against the oracle fixture, and the view-sharded step
 sharing one card (gloo) against the single-process loop."""
 from __future__ import annotations
 
+import ctypes
 import os
 import socket
 
@@ -670,15 +671,18 @@ def test_c2_timed_path_matches_per_view_loop(cuda_device, oracle):
     fwd = views_forward_dict(outs.batch, 0, outs[0]["render"], outs[0]["depth_3dgs"], outs[0]["radii"])
     with torch.no_grad():
         # the oracle takes activated parameters; the kernels activate the raw ones in-kernel (sigmoid /
-        # exp / normalize on the device's libm), so the activated opacity the blend used — the Splat's
-        # conic_opacity.w, for every Gaussian in view — is what the oracle gets (torch's CPU sigmoid
-        # differs from the device's in the last bit for ~1/3 of the Gaussians)
-        op = sc.get_opacity.cpu().numpy().copy()
-        vis = fwd["radii"] > 0
-        op[vis, 0] = fwd["conic_opacity"][vis, 3]
-        kw = dict(means3D=sc.get_xyz.cpu().numpy(), opacities=op,
-                  shs=sc.get_features.cpu().numpy(), scales=sc.get_scaling.cpu().numpy(),
-                  rotations=sc.get_rotation.cpu().numpy())
+        # exp / normalize on the device's libm, which differ from torch's in the last bit for a third of
+        # the rows): the oracle gets the device's activations (gs_activate_params: the preprocess's own
+        # device functions)
+        op = torch.empty(P, 1, device=dev)
+        scl = torch.empty(P, 3, device=dev)
+        rot = torch.empty(P, 4, device=dev)
+        N.check(N.lib().gs_activate_params(P, sc._opacity.data_ptr(), sc._scaling.data_ptr(), sc._rotation.data_ptr(),
+                                           op.data_ptr(), scl.data_ptr(), rot.data_ptr(),
+                                           ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)),
+                "gs_activate_params")
+        kw = dict(means3D=sc.get_xyz.cpu().numpy(), opacities=op.cpu().numpy(),
+                  shs=sc.get_features.cpu().numpy(), scales=scl.cpu().numpy(), rotations=rot.cpu().numpy())
     from dge_amd.cameras import orbit_camera
 
     rs = _settings(orbit_camera(0, V, W, H, device="cpu"), torch.zeros(3), 1.0, 3)
