@@ -625,23 +625,36 @@ def side_legs(args, scene, cams, seeds, bg, pipe, bucket, step, dev):
         finally:
             scene.mask = prev_mask
 
+    from dge_amd import gaussian_renderer as GR
+    hits0 = GR._RECOLOR_HITS
     for _ in range(3):
         dge_loop()
     dt = _time(dge_loop, steps)
-    from dge_amd import gaussian_renderer as GR
-    lazy = GR._LAZY_OVERRIDE
-    GR._LAZY_OVERRIDE = False
+    hits = GR._RECOLOR_HITS - hits0
+    dt_lazy = None
+    recolor = GR._RECOLOR
+    GR._RECOLOR = False  # (the semantic render in full: lazy forward-only kernels, its own binning)
     try:
         for _ in range(2):
             dge_loop()
-        dt_eager = _time(dge_loop, steps)
+        dt_full = _time(dge_loop, steps)
     finally:
-        GR._LAZY_OVERRIDE = lazy
+        GR._RECOLOR = recolor
+    lazy = GR._LAZY_OVERRIDE
+    GR._LAZY_OVERRIDE, GR._RECOLOR = False, False  # (and with the backward's bookkeeping: the round-3 path)
+    try:
+        for _ in range(2):
+            dge_loop()
+        dt_lazy = _time(dge_loop, steps)
+    finally:
+        GR._LAZY_OVERRIDE, GR._RECOLOR = lazy, recolor
     legs["dge_loop_unchanged"] = {
         "value": round(steps * V / dt, 3), "unit": "views/s",
         "path": "DGE.py forward() per view (fused render(), semantic render, boolean-mask viz: a host sync per "
                 "view) + masked l1 + one backward, install_alias(fused_render=True), no code edit",
-        "semantic_eager_value": round(steps * V / dt_eager, 3)}
+        "semantic_recolor_hits": hits,
+        "semantic_full_render_value": round(steps * V / dt_full, 3),
+        "semantic_eager_value": round(steps * V / dt_lazy, 3)}
     for p in scene.parameters():
         p.grad = None
     bucket.attach()

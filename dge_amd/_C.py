@@ -401,6 +401,31 @@ def rasterize_gaussians_fused_end(prep):
         return nr.value, out_color, out_depth, radii, geom, binning, img
 
 
+def render_recolor(background, colors, viewmatrix, projmatrix, campos, tan_fovx, tan_fovy, image_height, image_width,
+                   degree, scale_modifier, prefiltered, P, num_rendered, geomBuffer, binningBuffer, imgBuffer):
+    """gs_render_recolor: the blend of a finished forward (its geometry/binning/image buffers, num_rendered
+    instances, with backward bookkeeping) again with colours `colors` [P,3] in place of its own -> (color
+    [3,H,W], depth [1,H,W]), bit-identical to a full forward with colors_precomp = colors, on the current
+    stream (which must be ordered after that forward)."""
+    dev = colors.device
+    H, W = int(image_height), int(image_width)
+    with torch.cuda.device(dev):
+        colors = _f32(colors, "colors")
+        if colors.numel() < 3 * P:
+            raise RuntimeError("colors must hold P x 3 values")
+        s, keep = _settings(background, viewmatrix, projmatrix, campos, tan_fovx, tan_fovy, H, W, degree,
+                            scale_modifier, prefiltered, False)
+        out_color = torch.empty((3, H, W), dtype=torch.float32, device=dev)
+        out_depth = torch.empty((1, H, W), dtype=torch.float32, device=dev)
+        img_out = torch.empty(int(N.lib().gs_image_buffer_size(W, H)), dtype=torch.uint8, device=dev)
+        rc = N.lib().gs_render_recolor(ctypes.byref(s), int(P), int(num_rendered), _ptr(geomBuffer),
+                                       _ptr(binningBuffer), _ptr(imgBuffer), _ptr(colors), _ptr(img_out),
+                                       _ptr(out_color), _ptr(out_depth), _stream(dev))
+        N.check(rc, "render_recolor")
+        del keep
+        return out_color, out_depth
+
+
 def rasterize_gaussians_fused(background, xyz, f_dc, f_rest, colors, raw_opacity, raw_scaling, raw_rotation,
                               scale_modifier, viewmatrix, projmatrix, tan_fovx, tan_fovy, image_height, image_width,
                               degree, campos, prefiltered, debug, index=None, visible=None):

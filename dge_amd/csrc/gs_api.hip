@@ -120,13 +120,6 @@ int depth_pass_bits() {
     return bits;
 }
 
-// DGE_AMD_VIEWS_BWD=merged: a batch's per-Gaussian passes as one launch after every replay (round 3's
-// form) instead of staggered per-view passes (read per call: A/B)
-bool views_bwd_merged() {
-    const char* e = getenv("DGE_AMD_VIEWS_BWD");
-    return e && !strcmp(e, "merged");
-}
-
 // Pinned read-back slot of one forward's preprocess counters + its event.  A
 // pool per device: several forwards may be between begin and end at once
 // (gs_rasterize_forward_begin / _end), each holding its own slot.
@@ -400,6 +393,7 @@ int bin_prepare_in(FwdState& f, int copy_colors, void* geom, void* img, hipStrea
     pa.rect_packed = rect_packable(g.gx, g.gy) ? 1 : 0;
     pa.counters = counters;
     pa.touched = at<uint8_t>(geom, gl.touched);
+    pa.qmask_words = qmask_enabled(P) ? at<uint32_t>(geom, gl.qmask) : nullptr;
     return GS_OK;
 }
 
@@ -439,7 +433,7 @@ int bin_after_preprocess(FwdState& f, hipStream_t stream) {
     ea.P = P; ea.gx = g.gx; ea.gy = g.gy;
     ea.order = at<uint2>(geom, cur ? gl.val1 : gl.val0);
     ea.rect_packed = pa.rect_packed;
-    ea.qmask = qmask_enabled(P) ? 1 : 0;
+    ea.qmask_words = pa.qmask_words;
     ea.tiles_touched = pa.tiles_touched;
     ea.splat = pa.splat;
     ea.radii = pa.radii;
@@ -993,6 +987,61 @@ int gs_rasterize_forward_end(gs_forward_state* state, float* out_color, float* o
 
 void gs_rasterize_forward_release(gs_forward_state* state) { delete state; }
 
+int gs_render_recolor(const gs_settings* s, int P, int num_rendered, const void* geom, const void* binning,
+                      const void* img, const float* colors, void* img_out, float* out_color, float* out_depth,
+                      gs_stream_t stream_) {
+    try {
+        hipStream_t stream = (hipStream_t)stream_;
+        if (!s || P < 0 || num_rendered < 0 || !geom || !img || !img_out || !out_color || !out_depth ||
+            (P > 0 && !colors) || (num_rendered > 0 && !binning))
+            return set_error(GS_ERR_INVALID_ARG, "gs_render_recolor: bad arguments");
+        const bool debug = s->debug != 0;
+        const Grid g = make_grid(s);
+        if (g.W <= 0 || g.H <= 0) return set_error(GS_ERR_INVALID_ARG, "gs_render_recolor: bad image size");
+        const ImgLayout il = img_layout(g.W, g.H);
+        // the blend's per-pixel/per-tile outputs into img_out (the source render's backward still reads
+        // its own); tile_last is accumulated by atomicMax: zeroed with the rest of the tail
+        GS_HIP(hipMemsetAsync(at<uint8_t>(img_out, il.counters), 0, il.total - il.counters, stream));
+        if (P == 0 || num_rendered == 0) {
+            // no list: every pixel is T = 1 over the background (the blend of empty ranges)
+            GS_HIP(hipMemsetAsync(at<uint8_t>(img_out, il.ranges), 0, 8 * (size_t)g.tiles, stream));
+        }
+        const GeomLayout gl = geom_layout(P);
+        const BinLayout bl = bin_layout(num_rendered, g.tiles, true);
+        RenderArgs ra;
+        ra.bwd = 0;
+        ra.W = g.W; ra.H = g.H; ra.gx = g.gx; ra.gy = g.gy;
+        const bool empty = P == 0 || num_rendered == 0;
+        ra.ranges = at<uint2>(empty ? img_out : img, il.ranges);
+        // (read only: the empty case's own order goes to img_out)
+        ra.tile_order = at<uint32_t>(empty ? img_out : const_cast<void*>(img), il.tile_order);
+        ra.order_ready = empty ? 0 : 1;  // (the source forward left its dispatch order; an empty one gets one)
+        ra.point_pairs = empty ? nullptr : at<uint2>(binning, bl.point_pairs);
+        ra.point_ids = nullptr;
+        ra.splat = at<Splat>(geom, gl.splat);
+        ra.bg = s->bg;
+        ra.final_T = at<float>(img_out, il.final_T);
+        ra.n_contrib = at<uint32_t>(img_out, il.n_contrib);
+        ra.tile_last = at<uint32_t>(img_out, il.tile_last);
+        ra.quad_last = at<uint32_t>(img_out, il.quad_last);
+        ra.ckpt = nullptr; ra.used = nullptr; ra.bwd_items = nullptr; ra.bwd_count = nullptr; ra.item_cap = 0;
+        ra.out_color = out_color;
+        ra.out_depth = out_depth;
+        ra.touched = nullptr;
+        ra.diag = nullptr;
+        ra.qmask = qmask_enabled(P) ? 1 : 0;
+        ra.id_mask = id_mask_for(P);
+        ra.colors = colors;
+        GS_SKIP("fwd") { StageScope sc(ST_RENDER_FWD, stream); launch_render_forward(ra, stream); }
+        GS_LAUNCHED("recolor render");
+        return GS_OK;
+    } catch (const std::exception& e) {
+        return set_error(GS_ERR_INVALID_ARG, "exception: %s", e.what());
+    } catch (...) {
+        return set_error(GS_ERR_INVALID_ARG, "unknown exception");
+    }
+}
+
 int gs_rasterize_forward_ex(const gs_settings* s, const gs_params* gp, float* out_color, float* out_depth, int* radii,
                             gs_alloc_fn alloc, void* alloc_ctx, gs_stream_t stream, int* num_rendered) {
     if (num_rendered) *num_rendered = 0;
@@ -1121,11 +1170,9 @@ struct gs_views {
     int spec[GS_MAX_VIEWS] = {};         // 1: capacity-sized, count checked by gs_views_check
     long long K[GS_MAX_VIEWS] = {};      // instance count, -1 until the host knows it
     hipEvent_t ev[GS_MAX_VIEWS] = {};    // the end of each view's work (forward, or per-Gaussian backward pass)
-    hipEvent_t ev_r[GS_MAX_VIEWS] = {};  // the end of each view's gradient replay (staggered backward)
     hipEvent_t fork = nullptr;           // the caller's stream, before the views' work
     ~gs_views() {
         for (int v = 0; v < GS_MAX_VIEWS; ++v) event_pool().put(ev[v]);
-        for (int v = 0; v < GS_MAX_VIEWS; ++v) event_pool().put(ev_r[v]);
         event_pool().put(fork);
     }
 };
@@ -1327,35 +1374,6 @@ int gs_views_backward(gs_views* h, const float* const* dL_dpix, const gs_grads* 
         }
         int rc0 = fork_from(h, join, streams);  // (the image gradients come from the caller's stream)
         if (rc0) return rc0;
-        if (h->n > 1 && views_mergeable(h, grads) && !views_bwd_merged()) {
-            // staggered: view v's replay on its stream after view v-1's replay, then its own per-Gaussian
-            // pass there after view v-1's pass (the accumulation in view order, bitwise the per-view
-            // calls') — so view v-1's pass runs beside view v's replay instead of every pass queueing
-            // behind the last replay (round 3's merged pass: a ~165-us serial tail per step)
-            for (int v = 0; v < h->n; ++v) {
-                FwdState& f = h->f[v];
-                hipStream_t sv = (hipStream_t)streams[v];
-                const bool debug = f.s.debug != 0;
-                hipStream_t stream = sv;  // (GS_LAUNCHED)
-                if (v > 0 && streams[v - 1] != streams[v]) GS_HIP(hipStreamWaitEvent(sv, h->ev_r[v - 1], 0));
-                int rc = replay_view(&f.s, &f.gp, (int)h->layout[v], f.geom, h->bin[v], f.img, dL_dpix[v], sv);
-                if (rc) return rc;
-                if (!h->ev_r[v] && !(h->ev_r[v] = event_pool().get())) return set_error(GS_ERR_HIP, "could not create an event");
-                GS_HIP(hipEventRecord(h->ev_r[v], sv));
-                hipEvent_t wa = v == 0 ? (hipEvent_t)writes_after
-                                       : (streams[v - 1] != streams[v] ? h->ev[v - 1] : nullptr);
-                const GaussBwdArgs ga = gauss_args(&f.s, &f.gp, (int)h->layout[v], f.radii, f.geom, h->bin[v], grads[v],
-                                                   h->spec[v] ? h->layout[v] : 0xFFFFFFFFu);
-                GS_SKIP("gauss") { StageScope sc(ST_GAUSS_BWD, sv); launch_gauss_backward(ga, sv, wa); }
-                GS_LAUNCHED("gaussian backward (staggered)");
-                if (!h->ev[v] && !(h->ev[v] = event_pool().get())) return set_error(GS_ERR_HIP, "could not create an event");
-                GS_HIP(hipEventRecord(h->ev[v], sv));
-            }
-            // the last pass waited for every earlier one (and each for its replay): join on it
-            hipStream_t sl = (hipStream_t)streams[h->n - 1];
-            if (sl != join) GS_HIP(hipStreamWaitEvent(join, h->ev[h->n - 1], 0));
-            return GS_OK;
-        }
         if (h->n > 1 && views_mergeable(h, grads)) {
             // every view's replay on its stream, then ONE per-Gaussian pass over all of them (chunks of
             // gauss_backward_max_views() views, in view order) on the first view's stream

@@ -92,7 +92,7 @@ struct alignas(64) Splat {
 };
 
 struct GeomLayout {
-    size_t splat, tiles_touched, clamped, touched, live_count, live_list, radii, first_slot;
+    size_t splat, tiles_touched, clamped, touched, live_count, live_list, radii, first_slot, qmask;
     // live_count: one u32 per 256-Gaussian block (k_gauss_live); live_list: block-local compacted ids
     size_t key0, key1, val0, val1, rect, sort_hist, sort_totals, scan_sums, emit_hist, total;
     int sort_blocks, scan_blocks;
@@ -111,6 +111,7 @@ inline GeomLayout geom_layout(int P) {
     L.live_list = o; o = align_up(o + 4 * p);
     L.radii = o; o = align_up(o + 4 * p);
     L.first_slot = o; o = align_up(o + 4 * p);
+    L.qmask = o; o = align_up(o + 4 * p);  // the quadrant masks of each Gaussian's rect (gs_qmask.h)
     L.key0 = o; o = align_up(o + 4 * p);
     L.key1 = o; o = align_up(o + 4 * p);
     L.val0 = o; o = align_up(o + 8 * p);  // depth sort values: uint2 (rect-or-count, Gaussian)
@@ -255,6 +256,7 @@ struct PreprocessArgs {
     int rect_packed;
     uint32_t* counters;  // kCounterSlots x kCounterStride (ImgLayout)
     uint8_t* touched;    // zeroed here: k_render_fwd sets the bytes of Gaussians some pixel blends
+    uint32_t* qmask_words = nullptr;  // [P] rect_quad_masks of every Gaussian with a tile (qmask_enabled)
 };
 void launch_preprocess(const PreprocessArgs& a, hipStream_t s);
 void launch_depth_keys32(int P, const uint32_t* rect, const Splat* splat, uint32_t* key, hipStream_t s);
@@ -319,8 +321,9 @@ struct EmitArgs {
     // ids_only (a forward-only render's two-level binning): the lists carry the Gaussian id alone (u32 at
     // pairs_out / the point list) — the binning slot is only the backward's record address
     int ids_only = 0;
-    // qmask: every emitted id carries its quadrant mask in bits kIdBits.. (gs_qmask.h; qmask_enabled)
-    int qmask = 0;
+    // qmask_words (the preprocess's per-Gaussian rect masks): every emitted id carries its instance's
+    // quadrant mask in bits kIdBits.. (gs_qmask.h; qmask_enabled)
+    const uint32_t* qmask_words = nullptr;
 };
 // The emission's per-instance quadrant masks (gs_qmask.h) for a P-Gaussian render: on unless
 // DGE_AMD_QMASK=0 (A/B: the blend's per-wave cull_keep instead), and only while ids fit kIdBits.
@@ -375,6 +378,7 @@ struct RenderArgs {
     int bwd = 1;          // 0: a forward-only render (gs_params.forward_only): no backward bookkeeping
     int qmask = 0;        // the list ids carry the emission's quadrant masks (else: cull_keep per wave)
     uint32_t id_mask = 0xFFFFFFFFu;
+    const float* colors = nullptr;  // forward-only: blend these [P,3] colours instead of the Splats' (recolor)
 };
 void launch_render_forward(const RenderArgs& a, hipStream_t s);
 

@@ -1,8 +1,9 @@
 // gs_qmask.h — the per-instance quadrant mask: which 8x8 quadrants of a 16x16 tile a Gaussian can
-// reach with alpha >= 1/255 (forward.cu:336-348's skip tests), computed ONCE per (Gaussian, tile)
-// instance by the emission instead of by each of the four quadrant waves of the blend for every list
-// position it walks (the blend's cull_keep: ~136 VALU per lane and position, 14-21% of the heaviest
-// waves' cycles, plus the gathers of entries it then drops).
+// reach with alpha >= 1/255 (forward.cu:336-348's skip tests), computed ONCE per (Gaussian, tile) by
+// the preprocess (a 32-bit word per Gaussian: 4 bits per tile of its rect, rects of up to 8 tiles)
+// instead of by each of the four quadrant waves of the blend for every list position it walks (the
+// blend's cull_keep: ~136 VALU per lane and position, 14-21% of the heaviest waves' cycles, plus the
+// gathers of entries it then drops); the emission copies each instance's 4 bits into its list id.
 //
 // Host + device: the CPU suite checks the bound against the blend's own per-pixel test
 // (tests/qmask_check.cpp, brute force over the 64 pixels of every quadrant).
@@ -38,6 +39,30 @@
 
 namespace gs {
 
+// On the device the hardware's approximate square root, reciprocal and log2 (~1 ulp: far inside the
+// 1e-3 margins below); the host check uses the libm forms
+GS_QM_HD inline float qm_sqrt(float x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_sqrtf(x);
+#else
+    return sqrtf(x);
+#endif
+}
+GS_QM_HD inline float qm_rcp(float x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_rcpf(x);
+#else
+    return 1.0f / x;
+#endif
+}
+GS_QM_HD inline float qm_ln(float x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return 0.693147182f * __builtin_amdgcn_logf(x);
+#else
+    return logf(x);
+#endif
+}
+
 // Gaussian ids in the per-tile lists carry the mask in their top bits (bit 28 + quadrant) when the
 // scene has fewer than 2^28 Gaussians; id_mask() strips it
 constexpr int kIdBits = 28;
@@ -64,20 +89,21 @@ GS_QM_HD inline QuadCull quad_cull_setup(float gx, float gy, float a, float b, f
     // D = ac - b^2 with b^2 split exactly (fma): ~1 ulp of D however elongated the ellipse
     const float bb = b * b, bb_err = fmaf(b, b, -bb);
     const float D = fmaf(a, c, -bb) - bb_err;
-    const float k = (a * c) / D;  // conditioning (>= 1): the blend's own rounding of power grows with it
-    const float thr = 2.0f * logf(255.0f * o);
+    const float rD = qm_rcp(D);
+    const float k = (a * c) * rD;  // conditioning (>= 1): the blend's own rounding of power grows with it
+    const float thr = 2.0f * qm_ln(255.0f * o);
     const float T = thr + (1.0f + fabsf(thr)) * (4e-3f + 1e-5f * k);
     if (!(a > 0.0f && c > 0.0f && D > 0.0f && k < 1e6f && T >= 0.0f && T < 1e30f && fabsf(gx) < 1e7f &&
           fabsf(gy) < 1e7f)) {
         q.all = 1;  // not positive definite, degenerate, NaN or huge: no bound
         return q;
     }
-    const float dxE = sqrtf(c * T / D), dyE = sqrtf(a * T / D);
-    q.s = 1.0f / a;
+    const float dxE = qm_sqrt(c * T * rD), dyE = qm_sqrt(a * T * rD);
+    q.s = qm_rcp(a);
     q.bs = b * q.s;
     q.aT = a * T;
     q.D = D;
-    q.yr = -b * dxE / c;
+    q.yr = -b * dxE * qm_rcp(c);
     q.dxE = dxE + (1e-3f * dxE + 1e-3f);
     q.dyE = dyE + (1e-3f * dyE + 1e-3f);
     return q;
@@ -96,8 +122,8 @@ GS_QM_HD inline uint32_t quad_mask(const QuadCull& q, float tx0, float ty0) {
         const float Y1 = (q.gy - (ty0 + (float)(8 * j))) + my;
         const float lo = fmaxf(Y0, -q.dyE), hi = fminf(Y1, q.dyE);
         if (!(lo <= hi)) continue;  // the band misses the ellipse
-        const float sl = sqrtf(fmaxf(0.0f, q.aT - q.D * lo * lo));
-        const float sh = sqrtf(fmaxf(0.0f, q.aT - q.D * hi * hi));
+        const float sl = qm_sqrt(fmaxf(0.0f, q.aT - q.D * lo * lo));
+        const float sh = qm_sqrt(fmaxf(0.0f, q.aT - q.D * hi * hi));
         const float cl = -q.bs * lo, ch = -q.bs * hi;
         float xmax = fmaxf(cl + q.s * sl, ch + q.s * sh);
         float xmin = fminf(cl - q.s * sl, ch - q.s * sh);
@@ -109,6 +135,38 @@ GS_QM_HD inline uint32_t quad_mask(const QuadCull& q, float tx0, float ty0) {
         for (int i = 0; i < 2; ++i) {
             const float X0 = q.gx - (tx0 + (float)(8 * i + 7)), X1 = q.gx - (tx0 + (float)(8 * i));
             if (X0 <= xmax && X1 >= xmin) m |= 1u << (2 * j + i);
+        }
+    }
+    return m;
+}
+
+// The masks of a Gaussian's whole tile rect [x0, x0 + w) x [y0, y0 + h), w h <= kRectMaskTiles: tile
+// (x0 + i, y0 + j)'s 4 bits at 4 (j w + i) — the emission's instance order (row-major over the rect).
+// Each of the 2h pixel-row bands is bounded once (its extent turned into a range of quadrant columns),
+// not once per tile; the bits equal quad_mask's tile by tile.  Larger rects: all ones (every quadrant).
+constexpr int kRectMaskTiles = 8;
+GS_QM_HD inline uint32_t rect_quad_masks(const QuadCull& q, int x0, int y0, int w, int h) {
+    if (q.all || w * h > kRectMaskTiles) return 0xFFFFFFFFu;
+    uint32_t m = 0u;
+    const float mx = 1e-3f * q.dxE + 1e-3f, my = 1e-3f * q.dyE + 1e-3f;
+    for (int j = 0; j < 2 * h; ++j) {  // band j: pixel rows 16 y0 + 8 j .. + 7
+        const float py0 = (float)(16 * y0 + 8 * j);
+        const float Y0 = (q.gy - (py0 + 7.0f)) - my, Y1 = (q.gy - py0) + my;
+        const float lo = fmaxf(Y0, -q.dyE), hi = fminf(Y1, q.dyE);
+        if (!(lo <= hi)) continue;
+        const float sl = qm_sqrt(fmaxf(0.0f, q.aT - q.D * lo * lo));
+        const float sh = qm_sqrt(fmaxf(0.0f, q.aT - q.D * hi * hi));
+        const float cl = -q.bs * lo, ch = -q.bs * hi;
+        float xmax = fmaxf(cl + q.s * sl, ch + q.s * sh);
+        float xmin = fminf(cl - q.s * sl, ch - q.s * sh);
+        if (lo <= q.yr && q.yr <= hi) xmax = q.dxE;
+        if (lo <= -q.yr && -q.yr <= hi) xmin = -q.dxE;
+        xmax += mx;
+        xmin -= mx;
+        for (int c = 0; c < 2 * w; ++c) {  // quadrant column c: pixels 16 x0 + 8 c .. + 7
+            const float px0 = (float)(16 * x0 + 8 * c);
+            const float X0 = q.gx - (px0 + 7.0f), X1 = q.gx - px0;
+            if (X0 <= xmax && X1 >= xmin) m |= 1u << (4 * ((j >> 1) * w + (c >> 1)) + 2 * (j & 1) + (c & 1));
         }
     }
     return m;

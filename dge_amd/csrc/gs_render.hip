@@ -307,10 +307,22 @@ __global__ __launch_bounds__(64, 3) void k_render_fwd(RenderArgs a) {
     // quadrant drops gathers Gaussian 0 (one shared line) instead of its Splat
     const uint32_t qbit = a.qmask ? 1u << (kIdBits + quad) : 0u;
     const auto gather_id = [&](uint32_t id) { return a.qmask && !(id & qbit) ? 0u : id & a.id_mask; };
+    // (gs_render_recolor: a forward-only blend over another render's binning with its own colours)
+    const auto gather = [&](uint32_t id) {
+        Entry e = gather_entry(a.splat, id);
+        if constexpr (!BWD) {
+            if (a.colors) {
+                e.f.x = a.colors[3 * (size_t)id];
+                e.f.y = a.colors[3 * (size_t)id + 1];
+                e.f.z = a.colors[3 * (size_t)id + 2];
+            }
+        }
+        return e;
+    };
     load_ids(range.x, ids);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        cur[i] = gather_entry(a.splat, gather_id(ids[i]));
+        cur[i] = gather(gather_id(ids[i]));
         cid[i] = ids[i];
     }
     load_ids(range.x + kRound, ids);
@@ -398,7 +410,7 @@ __global__ __launch_bounds__(64, 3) void k_render_fwd(RenderArgs a) {
         // next round's gathers and the round after's ids, in flight during the blend
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            cur[i] = gather_entry(a.splat, gather_id(ids[i]));
+            cur[i] = gather(gather_id(ids[i]));
             cid[i] = ids[i];
         }
         load_ids(b + 2 * kRound, ids);

@@ -567,6 +567,12 @@ __device__ __forceinline__ uint32_t rect_count(uint32_t v, int packed) {
     return ((v >> 16 & 0xFFu) - (v & 0xFFu)) * ((v >> 24) - (v >> 8 & 0xFFu));
 }
 
+// Instance k (row-major over the Gaussian's rect) of a rect_quad_masks word: its tile's 4 bits (rects of
+// more than kRectMaskTiles tiles carry all ones)
+__device__ __forceinline__ uint32_t inst_mask(uint32_t word, uint32_t k) {
+    return k < (uint32_t)kRectMaskTiles ? (word >> (4 * k)) & 0xFu : 0xFu;
+}
+
 // Block sums of the instance counts in depth order (k_scan_emit derives each
 // block's first slot from them).
 __global__ __launch_bounds__(256) void k_scan_reduce(EmitArgs a) {
@@ -616,8 +622,7 @@ __global__ __launch_bounds__(256) void k_scan_emit(EmitArgs a) {
     __shared__ uint32_t lds4[4];
     __shared__ uint32_t s_start[256];
     __shared__ uint32_t s_gauss[256];
-    __shared__ int4 s_rect[256];  // x0, y0, width, -
-    __shared__ QuadCull s_qc[256];  // qmask: the round's Gaussians' ellipse bounds (gs_qmask.h)
+    __shared__ int4 s_rect[256];  // x0, y0, width, the rect's quadrant masks (qmask_words)
     // the block's first slot: the sum of the block sums before it (k_scan_reduce's, read from L2:
     // at most scan_blocks words; this replaced a one-workgroup top-level scan launch)
     uint32_t base;
@@ -644,13 +649,7 @@ __global__ __launch_bounds__(256) void k_scan_emit(EmitArgs a) {
                 const float2 xy = a.splat[g].xy;
                 q = tile_rect(xy.x, xy.y, a.radii[g], a.gx, a.gy);
             }
-            s_rect[threadIdx.x] = make_int4(q.x0, q.y0, q.x1 - q.x0, 0);
-            if (a.qmask) {
-                const Splat* sp = a.splat + g;
-                const float2 xy = sp->xy;
-                const float4 co = sp->co;
-                s_qc[threadIdx.x] = quad_cull_setup(xy.x, xy.y, co.x, co.y, co.z, co.w);
-            }
+            s_rect[threadIdx.x] = make_int4(q.x0, q.y0, q.x1 - q.x0, a.qmask_words ? (int)a.qmask_words[g] : 0);
         }
         s_start[threadIdx.x] = off;
         s_gauss[threadIdx.x] = g;
@@ -672,7 +671,7 @@ __global__ __launch_bounds__(256) void k_scan_emit(EmitArgs a) {
             const int tx = q.x + (int)kx, ty = q.y + (int)ky;
             a.tile_key[base + j] = (uint32_t)(ty * a.gx + tx);
             uint32_t gv = s_gauss[lo];
-            if (a.qmask) gv |= quad_mask(s_qc[lo], (float)(16 * tx), (float)(16 * ty)) << kIdBits;
+            if (a.qmask_words) gv |= inst_mask((uint32_t)q.w, k) << kIdBits;
             a.slot_gauss[base + j] = gv;
             if (a.rec_flags32) a.rec_flags32[base + j] = 0u;  // slot's four quadrant flags (no memset launch)
         }
@@ -706,7 +705,6 @@ __global__ __launch_bounds__(256) void k_scan_emit_x(EmitArgs a) {
     __shared__ PV s_pair[kEmitBatch];
     __shared__ uint16_t s_own[kEmitBatch];  // the batch's owners (+1): marks at the entries' starts, prefix max
     __shared__ uint32_t s_carry;
-    __shared__ QuadCull s_qc[256];  // qmask: the round's Gaussians' ellipse bounds (gs_qmask.h)
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     if (blockIdx.x == 0)
         for (int t = tid; t < a.ntiles; t += 256) a.tile_count[t] = 0u;  // (the row pass counts into it)
@@ -735,13 +733,8 @@ __global__ __launch_bounds__(256) void k_scan_emit_x(EmitArgs a) {
         if (c) {
             a.first_slot[g] = base + off;
             s_rect[tid] = make_int4((int)(gr.x & 0xFFu), (int)((gr.x >> 8) & 0xFFu),
-                                    (int)((gr.x >> 16) & 0xFFu) - (int)(gr.x & 0xFFu), 0);
-            if (a.qmask) {
-                const Splat* sp = a.splat + g;
-                const float2 xy = sp->xy;
-                const float4 co = sp->co;
-                s_qc[tid] = quad_cull_setup(xy.x, xy.y, co.x, co.y, co.z, co.w);
-            }
+                                    (int)((gr.x >> 16) & 0xFFu) - (int)(gr.x & 0xFFu),
+                                    a.qmask_words ? (int)a.qmask_words[g] : 0);
         }
         s_start[tid] = off;
         s_gauss[tid] = g;
@@ -797,7 +790,7 @@ __global__ __launch_bounds__(256) void k_scan_emit_x(EmitArgs a) {
                 const uint32_t x = (uint32_t)q.x + kx, y = (uint32_t)q.y + ky;
                 kk[e] = y << kXBits | x;
                 uint32_t gv = s_gauss[lo];
-                if (a.qmask && valid) gv |= quad_mask(s_qc[lo], (float)(16 * x), (float)(16 * y)) << kIdBits;
+                if (a.qmask_words) gv |= inst_mask((uint32_t)q.w, k) << kIdBits;
                 if constexpr (IDS) pv[e] = gv;
                 else pv[e] = make_uint2(gv, base + j);
                 if (valid && a.rec_flags32 && base + j < a.cap) a.rec_flags32[base + j] = 0u;  // (slot order: coalesced)

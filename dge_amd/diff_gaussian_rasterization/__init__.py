@@ -103,6 +103,14 @@ class _RasterizeGaussians(torch.autograd.Function):
                 grad_cov3Ds_precomp, None)
 
 
+class RecolorPrepared:
+    """`prepared` of _RasterizeGaussiansFused for a render that is already finished: the recolor of an earlier
+    forward's buffers with other colours (dge_amd.gaussian_renderer, DGE's semantic render)."""
+
+    def __init__(self, num_rendered, color, depth, radii):
+        self.num_rendered, self.color, self.depth, self.radii = num_rendered, color, depth, radii
+
+
 class _RasterizeGaussiansFused(torch.autograd.Function):
     """Rasterize straight from a GaussianModel's raw tensors (not part of the
     reference API; used by dge_amd.gaussian_renderer.render when the model has
@@ -118,9 +126,14 @@ class _RasterizeGaussiansFused(torch.autograd.Function):
         # recompute: `prepared` is a forward_only render (no backward bookkeeping in its buffers); a
         # backward, if one comes, first renders the same inputs again with it
         rs = raster_settings
-        if prepared is not None:
+        if isinstance(prepared, RecolorPrepared):  # (finished already: gs_render_recolor over another forward)
+            num_rendered, color, depth, radii = prepared.num_rendered, prepared.color, prepared.depth, prepared.radii
+            geomBuffer = binningBuffer = imgBuffer = torch.empty(0, dtype=torch.uint8, device=xyz.device)
+        elif prepared is not None:
             num_rendered, color, depth, radii, geomBuffer, binningBuffer, imgBuffer = \
                 _C.rasterize_gaussians_fused_end(prepared)
+            if not recompute:  # (a forward with backward bookkeeping: a recolor may reuse its buffers)
+                prepared.finished = (num_rendered, geomBuffer, binningBuffer, imgBuffer)
         else:
             args = (rs.bg, xyz, f_dc, f_rest, colors, raw_opacity, raw_scaling, raw_rotation, rs.scale_modifier,
                     rs.viewmatrix, rs.projmatrix, rs.tanfovx, rs.tanfovy, rs.image_height, rs.image_width,

@@ -18,7 +18,8 @@ import weakref
 import torch
 import torch.nn.functional as F
 
-from .diff_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer, rasterize_gaussian_model
+from .diff_gaussian_rasterization import (GaussianRasterizationSettings, GaussianRasterizer, RecolorPrepared,
+                                         rasterize_gaussian_model)
 from .sh_utils import eval_sh
 
 
@@ -160,6 +161,50 @@ def _render_fused(viewpoint_camera, pc, pipe, bg_color, scaling_modifier=1.0, ov
 
 
 _LAZY_OVERRIDE = os.environ.get("DGE_AMD_LAZY_OVERRIDE", "1") != "0"
+_RECOLOR = os.environ.get("DGE_AMD_RECOLOR", "1") != "0"
+
+# The last fused forward with backward bookkeeping per device: DGE renders each view for training, then
+# the same camera and Gaussians again with the edit mask as override_color (DGE.py:181, 198-204) —
+# identical preprocess, depth order and tile lists, only the colours differ.  A gradient-free recolor
+# render whose geometry inputs are the ones of that forward (the same tensors at the same versions, the
+# same camera matrices, image size, fields of view, scale modifier, localize rows) reuses its buffers:
+# only the blend runs again (gs_render_recolor), bit-identical to the full forward.  Weak references: an
+# entry never keeps a forward's buffers alive (its autograd graph does, until its backward).
+_LAST_FORWARD = {}  # device index -> _ForwardEntry
+_RECOLOR_HITS = 0  # recolor renders served from a cached forward (tests, bench)
+
+
+def _tensor_key(t):
+    return None if t is None else (id(t), t._version)
+
+
+class _ForwardEntry:
+    def __init__(self, key, refs, num_rendered, P, stream, radii, visible):
+        self.key, self.refs, self.num_rendered, self.P = key, refs, num_rendered, P
+        self.stream, self.radii, self.visible = stream, radii, visible
+
+    def buffers(self):
+        bufs = [r() for r in self.refs]
+        return None if any(b is None for b in bufs) else bufs
+
+
+def _geometry_key(pc, rs, index):
+    return (_tensor_key(pc._xyz), _tensor_key(pc._opacity), _tensor_key(pc._scaling), _tensor_key(pc._rotation),
+            _tensor_key(index), _tensor_key(rs.viewmatrix), _tensor_key(rs.projmatrix), int(rs.image_height),
+            int(rs.image_width), float(rs.tanfovx), float(rs.tanfovy), float(rs.scale_modifier), bool(rs.prefiltered))
+
+
+def _recolor_source(pc, rs, index):
+    """The cached forward a recolor render of these inputs may reuse, or None."""
+    if not _RECOLOR:
+        return None
+    ent = _LAST_FORWARD.get(pc._xyz.device.index)
+    if ent is None or ent.key != _geometry_key(pc, rs, index):
+        return None
+    # (ids and versions match; the weak references confirm the very tensors are alive, not recycled ids)
+    if any(r() is None for r in ent.tensor_refs) or ent.buffers() is None:
+        return None
+    return ent
 
 
 def _may_backward(*tensors) -> bool:
@@ -192,6 +237,23 @@ def _fused_begin(viewpoint_camera, pc, pipe, bg_color, scaling_modifier=1.0, ove
           "prepared": None, "lazy": lazy}
     if rs.debug:  # debug mode: the one-call forward, which keeps the reference's failure snapshot
         return st
+    if colors is not None and not colors.requires_grad and (lazy or not may_bwd):
+        src = _recolor_source(pc, rs, index)
+        if src is not None:  # the same geometry as the last forward: only its blend again, other colours
+            global _RECOLOR_HITS
+            _RECOLOR_HITS += 1
+            geom, binning, img = src.buffers()
+            cur = torch.cuda.current_stream(xyz.device)
+            if src.stream != cur:
+                cur.wait_stream(src.stream)
+            color, depth = _C.render_recolor(rs.bg, colors, rs.viewmatrix, rs.projmatrix, rs.campos, rs.tanfovx,
+                                             rs.tanfovy, rs.image_height, rs.image_width, rs.sh_degree,
+                                             rs.scale_modifier, rs.prefiltered, n, src.num_rendered, geom, binning,
+                                             img)
+            st["visible"] = src.visible.clone()
+            st["prepared"] = RecolorPrepared(src.num_rendered, color, depth, src.radii.clone())
+            st["lazy"] = may_bwd  # (a backward, should one come, renders these inputs in full first)
+            return st
     empty = torch.empty(0, dtype=torch.float32, device=xyz.device)
     st["prepared"] = _C.rasterize_gaussians_fused_begin(
         rs.bg, xyz, empty if f_dc is None else f_dc, empty if f_rest is None else f_rest,
@@ -205,9 +267,21 @@ def _fused_end(st, pc):
     """The second half: the autograd node over the native forward's second half; render()'s dict."""
     xyz = pc._xyz
     screenspace_points = _viewspace_zeros(st["n"], xyz.dtype, xyz.device)
+    prep = st["prepared"]
     rendered_image, radii, depth = rasterize_gaussian_model(
         xyz, screenspace_points, st["f_dc"], st["f_rest"], st["colors"], pc._opacity, pc._scaling, pc._rotation,
-        st["rs"], st["index"], st["visible"], prepared=st["prepared"], recompute=st["lazy"] and st["prepared"] is not None)
+        st["rs"], st["index"], st["visible"], prepared=prep, recompute=st["lazy"] and prep is not None)
+    fin = getattr(prep, "finished", None)
+    if fin is not None and _RECOLOR:  # a forward with backward bookkeeping: later recolor renders may reuse it
+        nr, geom, binning, img = fin
+        prep.finished = None
+        ent = _ForwardEntry(_geometry_key(pc, st["rs"], st["index"]), [weakref.ref(geom), weakref.ref(binning),
+                            weakref.ref(img)], nr, st["n"], torch.cuda.current_stream(xyz.device), radii, st["visible"])
+        ent.tensor_refs = [weakref.ref(t) for t in (pc._xyz, pc._opacity, pc._scaling, pc._rotation,
+                                                    st["rs"].viewmatrix, st["rs"].projmatrix) if t is not None]
+        if st["index"] is not None:
+            ent.tensor_refs.append(weakref.ref(st["index"]))
+        _LAST_FORWARD[xyz.device.index] = ent
     return {
         "render": rendered_image,
         "viewspace_points": screenspace_points,

@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define GS_RASTER_ABI_VERSION 15
+#define GS_RASTER_ABI_VERSION 16
 
 #define GS_OK 0
 #define GS_ERR_INVALID_ARG 1   /* AT_ERROR / std::runtime_error in the reference */
@@ -218,6 +218,23 @@ int gs_rasterize_forward_begin(const gs_settings *s, const gs_params *g, int *ra
 int gs_rasterize_forward_end(gs_forward_state *state, float *out_color, float *out_depth, gs_alloc_fn alloc,
                              void *alloc_ctx, gs_stream_t stream, int *num_rendered);
 void gs_rasterize_forward_release(gs_forward_state *state);
+
+/* The same render with other colours: the forward-only blend over a finished
+ * raw-parameter or precomputed-colour forward's buffers (geom/binning/img of
+ * num_rendered instances, a forward WITH backward bookkeeping — not
+ * forward_only), the Gaussians' colours replaced by colors [P,3] (the
+ * colors_precomp of rasterize_points.cu:45 — DGE's semantic render,
+ * threestudio/systems/DGE.py:198-204, uses the same camera and Gaussians as
+ * the training render just before it, so their preprocess, depth order and
+ * tile lists are identical and only the blend differs).  out_color/out_depth
+ * are bit-identical to a full forward with colors_precomp = colors; img_out
+ * (gs_image_buffer_size) receives that blend's per-pixel state, the source
+ * buffers are only read.  s must describe the source forward (image size,
+ * grid); its bg is the one blended.  Enqueued on `stream`, which must be
+ * ordered after the source forward. */
+int gs_render_recolor(const gs_settings *s, int P, int num_rendered, const void *geom_buffer,
+                      const void *binning_buffer, const void *img_buffer, const float *colors, void *img_out,
+                      float *out_color, float *out_depth, gs_stream_t stream);
 int gs_rasterize_backward_ex(const gs_settings *s, const gs_params *g, int R, const int *radii,
                              const void *geom_buffer, const void *binning_buffer, const void *img_buffer,
                              const float *dL_dpix, const gs_grads *out, gs_stream_t stream);

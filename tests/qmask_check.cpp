@@ -97,6 +97,29 @@ int main(int argc, char** argv) {
             }
         }
     }
+    // the per-rect form (the preprocess's word) against quad_mask tile by tile
+    long rect_cases = 0, rect_diff = 0;
+    for (long n = 0; n < cases / 4; ++n) {
+        const int w = 1 + (int)(U(rng) * 4.0f), h = 1 + (int)(U(rng) * 4.0f);
+        if (w * h > gs::kRectMaskTiles) continue;
+        const int x0 = (int)(U(rng) * 100.0f), y0 = (int)(U(rng) * 60.0f);
+        const float s1 = expf(logf(0.3f) + U(rng) * logf(100.0f)), s2 = expf(logf(0.3f) + U(rng) * logf(100.0f));
+        const float th = 6.2831853f * U(rng), cs = cosf(th), sn = sinf(th);
+        const float c00 = s1 * s1 * cs * cs + s2 * s2 * sn * sn + 0.3f, c11 = s1 * s1 * sn * sn + s2 * s2 * cs * cs + 0.3f;
+        const float c01 = (s1 * s1 - s2 * s2) * cs * sn, det = c00 * c11 - c01 * c01;
+        if (!(det > 0.0f)) continue;
+        const float gx = 16.0f * x0 + U(rng) * 16.0f * w, gy = 16.0f * y0 + U(rng) * 16.0f * h;
+        const gs::QuadCull qc = gs::quad_cull_setup(gx, gy, c11 / det, -c01 / det, c00 / det, 0.004f + U(rng));
+        const uint32_t word = gs::rect_quad_masks(qc, x0, y0, w, h);
+        for (int j = 0; j < h; ++j)
+            for (int i = 0; i < w; ++i) {
+                const uint32_t t = gs::quad_mask(qc, 16.0f * (x0 + i), 16.0f * (y0 + j));
+                rect_diff += ((word >> (4 * (j * w + i))) & 0xFu) != t;
+            }
+        ++rect_cases;
+    }
+    printf("rect_cases %ld rect_mismatches %ld\n", rect_cases, rect_diff);
+    if (rect_diff) misses += rect_diff;
     printf("cases %ld degenerate %ld quadrants_needed %ld bits_set %ld misses %ld overkept %.4f (cull_keep: %ld kept, "
            "overkept %.4f, misses %ld)\n", cases, degenerate, needed, set, misses, set ? (double)(set - needed) / (double)set : 0.0,
            cull_set, cull_set ? (double)(cull_set - needed) / (double)cull_set : 0.0, cull_miss);

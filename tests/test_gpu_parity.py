@@ -599,3 +599,80 @@ def test_two_level_binning_matches_two_pass_sort(cuda_device, monkeypatch, P, W,
         np.testing.assert_array_equal(fused[k], ref[k], err_msg=k)
 
 
+
+
+@pytest.mark.parametrize("localize", [False, True])
+def test_semantic_render_reuses_the_training_forward(cuda_device, localize):
+    """DGE's semantic render (DGE.py:198-204: the same camera and Gaussians right after the training render,
+    the edit mask as override_color, grad mode on) reuses the training forward's preprocess, depth order and
+    tile lists (gs_render_recolor: only the blend again): image, depth, radii and visibility bit-identical to
+    the full semantic render; a backward through it still works (a full re-render first) and equals the full
+    path's; a parameter changed in place (optimizer step) or another camera is never served from the cache.
+    localize: the local-edit path (pc[mask] rows, override_color full-P as DGE passes it)."""
+    from dge_amd import gaussian_renderer as GR
+    from dge_amd.cameras import orbit_camera
+    from dge_amd.gaussian_renderer import PipelineParams, render
+    from dge_amd.scene import synthetic_scene
+
+    dev = torch.device("cuda")
+    P, W, H = 60_000, 240, 176
+    pipe, bg = PipelineParams(), torch.tensor([0.1, 0.0, 0.2], device=dev)
+    cams = [orbit_camera(k, 4, W, H, device=dev) for k in range(2)]
+    G = torch.randn(3, H, W, generator=torch.Generator().manual_seed(4)).to(dev)
+
+    def scene():
+        sc = synthetic_scene(P, seed=31, radius=1.5, scale=0.03, device=dev).requires_grad_(True)
+        m = torch.zeros(P, dtype=torch.bool, device=dev)
+        m[torch.argsort(sc._xyz[:, 1])[: P // 3]] = True
+        sc.mask = m
+        sc.localize = localize
+        return sc
+
+    def run(reuse):
+        GR._RECOLOR = reuse
+        sc = scene()
+        colors = sc.mask[..., None].float().repeat(1, 3)
+        out, hits = [], []
+        for cam in cams:
+            tr = render(cam, sc, pipe, bg)  # the training render (its buffers stay alive: the graph holds them)
+            h0 = GR._RECOLOR_HITS
+            sem = render(cam, sc, pipe, bg, override_color=colors)
+            hits.append(GR._RECOLOR_HITS - h0)
+            out.append({k: sem[k].detach().clone() for k in ("render", "depth_3dgs", "radii", "visibility_filter")})
+            out[-1]["train"] = tr["render"].detach().clone()
+        # the semantic render of camera 0 after camera 1's forward: not the cached geometry, a full render
+        h0 = GR._RECOLOR_HITS
+        sem0 = render(cams[0], sc, pipe, bg, override_color=colors)
+        hits.append(GR._RECOLOR_HITS - h0)
+        # a backward through a (reused) semantic render: the lazy node re-renders in full, then backpropagates
+        tr = render(cams[1], sc, pipe, bg)
+        sem = render(cams[1], sc, pipe, bg, override_color=colors)
+        (sem["render"] * G).sum().backward()
+        grads = [p.grad.clone() for p in (sc._xyz, sc._opacity, sc._scaling, sc._rotation)]
+        # an in-place parameter update (what an optimizer step is) invalidates the cached forward
+        tr = render(cams[0], sc, pipe, bg)
+        with torch.no_grad():
+            sc._xyz.add_(0.001)
+        h0 = GR._RECOLOR_HITS
+        sem_after = render(cams[0], sc, pipe, bg, override_color=colors)["render"].detach().clone()
+        hits.append(GR._RECOLOR_HITS - h0)
+        del tr
+        return out, sem0["render"].detach().clone(), grads, sem_after, hits
+
+    prev = GR._RECOLOR
+    try:
+        got = run(True)
+        ref = run(False)
+    finally:
+        GR._RECOLOR = prev
+    assert got[4] == [1, 1, 0, 0], f"recolor hits {got[4]}"
+    assert ref[4] == [0, 0, 0, 0]
+    for v, (a, b) in enumerate(zip(got[0], ref[0])):
+        for k in a:
+            assert torch.equal(a[k], b[k]), f"camera {v}: {k}"
+        assert not torch.equal(a["render"], a["train"])  # (the mask colours differ from the SH colours)
+    assert torch.equal(got[1], ref[1])
+    for a, b in zip(got[2], ref[2]):
+        assert torch.equal(a, b)
+    assert bool(got[2][0].abs().sum() > 0)
+    assert torch.equal(got[3], ref[3])
