@@ -622,7 +622,8 @@ __global__ __launch_bounds__(256) void k_scan_emit(EmitArgs a) {
     __shared__ uint32_t lds4[4];
     __shared__ uint32_t s_start[256];
     __shared__ uint32_t s_gauss[256];
-    __shared__ int4 s_rect[256];  // x0, y0, width, the rect's quadrant masks (qmask_words)
+    __shared__ int4 s_rect[256];  // x0, y0, width | big << 16, the rect's quadrant masks (qmask_words)
+    __shared__ QuadCull s_qc[256];  // (rects of more than kRectMaskTiles tiles: the bound itself)
     // the block's first slot: the sum of the block sums before it (k_scan_reduce's, read from L2:
     // at most scan_blocks words; this replaced a one-workgroup top-level scan launch)
     uint32_t base;
@@ -632,9 +633,22 @@ __global__ __launch_bounds__(256) void k_scan_emit(EmitArgs a) {
         block_exclusive_scan(part, lds4, base);
     }
     const uint32_t r_block = blockIdx.x * (uint32_t)kScanTile;
+    // every round's (rect, Gaussian) and quadrant-mask word loaded up front: one memory round trip
+    // instead of two dependent ones per round
+    uint2 grs[kScanIPT];
+    uint32_t qws[kScanIPT];
+#pragma unroll
     for (int it = 0; it < kScanIPT; ++it) {
         const uint32_t r = r_block + it * 256 + threadIdx.x;
-        const uint2 gr = r < (uint32_t)a.P ? a.order[r] : make_uint2(0u, 0u);
+        grs[it] = r < (uint32_t)a.P ? a.order[r] : make_uint2(0u, 0u);
+    }
+#pragma unroll
+    for (int it = 0; it < kScanIPT; ++it) {
+        const uint32_t c = rect_count(grs[it].x, a.rect_packed);
+        qws[it] = a.qmask_words && c && c <= (uint32_t)kRectMaskTiles ? a.qmask_words[grs[it].y] : 0u;
+    }
+    for (int it = 0; it < kScanIPT; ++it) {
+        const uint2 gr = grs[it];
         const uint32_t g = gr.y;
         const uint32_t c = rect_count(gr.x, a.rect_packed);
         uint32_t total;
@@ -649,7 +663,14 @@ __global__ __launch_bounds__(256) void k_scan_emit(EmitArgs a) {
                 const float2 xy = a.splat[g].xy;
                 q = tile_rect(xy.x, xy.y, a.radii[g], a.gx, a.gy);
             }
-            s_rect[threadIdx.x] = make_int4(q.x0, q.y0, q.x1 - q.x0, a.qmask_words ? (int)a.qmask_words[g] : 0);
+            const bool big = a.qmask_words && c > (uint32_t)kRectMaskTiles;
+            if (big) {
+                const Splat* sp = a.splat + g;
+                const float2 xy = sp->xy;
+                const float4 co = sp->co;
+                s_qc[threadIdx.x] = quad_cull_setup(xy.x, xy.y, co.x, co.y, co.z, co.w);
+            }
+            s_rect[threadIdx.x] = make_int4(q.x0, q.y0, (q.x1 - q.x0) | (big ? 1 << 16 : 0), (int)qws[it]);
         }
         s_start[threadIdx.x] = off;
         s_gauss[threadIdx.x] = g;
@@ -664,14 +685,17 @@ __global__ __launch_bounds__(256) void k_scan_emit(EmitArgs a) {
                 else hi = mid - 1;
             }
             const int4 q = s_rect[lo];
+            const int w = q.z & 0xFFFF;
             const uint32_t k = j - s_start[lo];
-            const uint32_t ky = (uint32_t)(((float)k + 0.5f) / (float)q.z);  // exact: k < 2^20, margin 0.5/width
-            const uint32_t kx = k - ky * (uint32_t)q.z;
+            const uint32_t ky = (uint32_t)(((float)k + 0.5f) / (float)w);  // exact: k < 2^20, margin 0.5/width
+            const uint32_t kx = k - ky * (uint32_t)w;
             if (base + j >= a.cap) break;  // speculative capacity exceeded (gs_views_check reports it)
             const int tx = q.x + (int)kx, ty = q.y + (int)ky;
             a.tile_key[base + j] = (uint32_t)(ty * a.gx + tx);
             uint32_t gv = s_gauss[lo];
-            if (a.qmask_words) gv |= inst_mask((uint32_t)q.w, k) << kIdBits;
+            if (a.qmask_words)
+                gv |= (q.z >> 16 ? quad_mask(s_qc[lo], (float)(16 * tx), (float)(16 * ty))
+                                 : inst_mask((uint32_t)q.w, k)) << kIdBits;
             a.slot_gauss[base + j] = gv;
             if (a.rec_flags32) a.rec_flags32[base + j] = 0u;  // slot's four quadrant flags (no memset launch)
         }
@@ -705,6 +729,7 @@ __global__ __launch_bounds__(256) void k_scan_emit_x(EmitArgs a) {
     __shared__ PV s_pair[kEmitBatch];
     __shared__ uint16_t s_own[kEmitBatch];  // the batch's owners (+1): marks at the entries' starts, prefix max
     __shared__ uint32_t s_carry;
+    __shared__ QuadCull s_qc[256];  // (rects of more than kRectMaskTiles tiles: the bound itself)
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     if (blockIdx.x == 0)
         for (int t = tid; t < a.ntiles; t += 256) a.tile_count[t] = 0u;  // (the row pass counts into it)
@@ -732,9 +757,16 @@ __global__ __launch_bounds__(256) void k_scan_emit_x(EmitArgs a) {
         const uint32_t off = block_exclusive_scan(c, lds4, total);
         if (c) {
             a.first_slot[g] = base + off;
+            const bool big = a.qmask_words && c > (uint32_t)kRectMaskTiles;
+            if (big) {
+                const Splat* sp = a.splat + g;
+                const float2 xy = sp->xy;
+                const float4 co = sp->co;
+                s_qc[tid] = quad_cull_setup(xy.x, xy.y, co.x, co.y, co.z, co.w);
+            }
             s_rect[tid] = make_int4((int)(gr.x & 0xFFu), (int)((gr.x >> 8) & 0xFFu),
-                                    (int)((gr.x >> 16) & 0xFFu) - (int)(gr.x & 0xFFu),
-                                    a.qmask_words ? (int)a.qmask_words[g] : 0);
+                                    ((int)((gr.x >> 16) & 0xFFu) - (int)(gr.x & 0xFFu)) | (big ? 1 << 16 : 0),
+                                    a.qmask_words && !big ? (int)a.qmask_words[g] : 0);
         }
         s_start[tid] = off;
         s_gauss[tid] = g;
@@ -784,13 +816,16 @@ __global__ __launch_bounds__(256) void k_scan_emit_x(EmitArgs a) {
                 const uint32_t j = j0 + (valid ? jj : 0u);
                 const int lo = (int)s_own[valid ? jj : 0u] - 1;
                 const int4 q = s_rect[lo];
+                const int qw = q.z & 0xFFFF;
                 const uint32_t k = j - s_start[lo];
-                const uint32_t ky = (uint32_t)(((float)k + 0.5f) / (float)q.z);  // exact: k < 2^20
-                const uint32_t kx = k - ky * (uint32_t)q.z;
+                const uint32_t ky = (uint32_t)(((float)k + 0.5f) / (float)qw);  // exact: k < 2^20
+                const uint32_t kx = k - ky * (uint32_t)qw;
                 const uint32_t x = (uint32_t)q.x + kx, y = (uint32_t)q.y + ky;
                 kk[e] = y << kXBits | x;
                 uint32_t gv = s_gauss[lo];
-                if (a.qmask_words) gv |= inst_mask((uint32_t)q.w, k) << kIdBits;
+                if (a.qmask_words)
+                    gv |= (q.z >> 16 ? quad_mask(s_qc[lo], (float)(16 * x), (float)(16 * y)) : inst_mask((uint32_t)q.w, k))
+                          << kIdBits;
                 if constexpr (IDS) pv[e] = gv;
                 else pv[e] = make_uint2(gv, base + j);
                 if (valid && a.rec_flags32 && base + j < a.cap) a.rec_flags32[base + j] = 0u;  // (slot order: coalesced)
