@@ -393,7 +393,7 @@ int bin_prepare_in(FwdState& f, int copy_colors, void* geom, void* img, hipStrea
     pa.rect_packed = rect_packable(g.gx, g.gy) ? 1 : 0;
     pa.counters = counters;
     pa.touched = at<uint8_t>(geom, gl.touched);
-    pa.qmask_words = qmask_enabled(P) ? at<uint32_t>(geom, gl.qmask) : nullptr;
+    pa.qmask_words = qmask_enabled(P) ? at<uint64_t>(geom, gl.qmask) : nullptr;
     return GS_OK;
 }
 
@@ -651,7 +651,6 @@ int render_launch(FwdState& f, void* bin, uint32_t K_layout, int order_ready, fl
     ra.diag = diag_buffer(0, kDiagWords * (size_t)g.tiles * 4);
     ra.qmask = qmask_enabled(f.gp.P) ? 1 : 0;
     ra.id_mask = id_mask_for(f.gp.P);
-    ra.xcd_items = bwd_xcd_items() ? 1 : 0;
     GS_SKIP("fwd") { StageScope sc(ST_RENDER_FWD, stream); launch_render_forward(ra, stream); }
     GS_LAUNCHED("render");
     return GS_OK;
@@ -706,7 +705,7 @@ int replay_view(const gs_settings* s, const gs_params* gp, int R, const void* ge
     rb.dL_dpix = dL_dpix;
     rb.records = at<float4>(const_cast<void*>(binning), bl.records);
     rb.rec_flags = at<uint8_t>(const_cast<void*>(binning), bl.rec_flags);
-    rb.diag = diag_buffer(1, kDiagWords * (4 * bl.nslots + kItemXcds));  // (by block: the grid, whole XCD rounds)
+    rb.diag = diag_buffer(1, kDiagWords * 4 * bl.nslots);
     GS_SKIP("rbwd") { StageScope sc(ST_RENDER_BWD, stream); launch_render_backward(rb, stream); }
     GS_LAUNCHED("render backward");
     return GS_OK;
@@ -781,14 +780,6 @@ struct gs_forward_state {
 
 namespace gs {
 int report_error(int code, const char* msg) { return set_error(code, "%s", msg); }
-
-bool bwd_xcd_items() {
-    static const bool on = [] {
-        const char* e = getenv("DGE_AMD_BWD_XCD");
-        return !(e && !strcmp(e, "0"));
-    }();
-    return on;
-}
 
 bool qmask_enabled(int P) {
     static const bool on = [] {

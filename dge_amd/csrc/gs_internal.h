@@ -111,7 +111,7 @@ inline GeomLayout geom_layout(int P) {
     L.live_list = o; o = align_up(o + 4 * p);
     L.radii = o; o = align_up(o + 4 * p);
     L.first_slot = o; o = align_up(o + 4 * p);
-    L.qmask = o; o = align_up(o + 4 * p);  // the quadrant masks of each Gaussian's rect (gs_qmask.h)
+    L.qmask = o; o = align_up(o + 8 * p);  // each Gaussian's rect bound (rect_band_ranges, gs_qmask.h)
     L.key0 = o; o = align_up(o + 4 * p);
     L.key1 = o; o = align_up(o + 4 * p);
     L.val0 = o; o = align_up(o + 8 * p);  // depth sort values: uint2 (rect-or-count, Gaussian)
@@ -140,14 +140,9 @@ inline GeomLayout geom_layout(int P) {
 constexpr int kBlendRound = 256;  // list entries per blend round
 // Replay work items are listed by class of their blended-entry count, heaviest first (the hardware
 // dispatches workgroups in order: the longest items start first, the short ones fill the end);
-// class c holds up to item_cap items per XCD list, counted in bwd_count[item_count_at(c, x)]
-// XCD-aware: each class is split in kItemXcds lists by tile (tile & 7): the backward's block b takes items of
-// list b & 7 only, and the hardware deals block b to XCD b mod 8 — every item of a tile (its quadrants and
-// segments) replays on one XCD, whose L2 then fetches the tile's list, Splats and pixel state once
-constexpr int kItemClasses = 4, kItemCount0 = 32, kItemXcds = 8;
-__host__ __device__ inline int item_count_at(int c, int x = 0) {  // u32 index, 128-B lines
-    return kItemCount0 * (1 + c * kItemXcds + x);
-}
+// class c holds up to item_cap items at bwd_items[c * item_cap ..), counted in bwd_count[item_count_at(c)]
+constexpr int kItemClasses = 4, kItemCount0 = 32;
+__host__ __device__ inline int item_count_at(int c) { return kItemCount0 * (1 + c); }  // u32 index, 128-B lines
 // backward segment length: checkpoints at every round boundary and mid-round, so a replay work item
 // covers at most 128 positions (half the per-item work of round-long segments: the replay's wave
 // durations pack onto the SIMDs instead of leaving a tail of long items)
@@ -181,8 +176,8 @@ inline ImgLayout img_layout(int W, int H) {
     L.ranges = o; o = align_up(o + 8 * tiles);
     L.tile_last = o; o = align_up(o + 4 * tiles);
     L.quad_last = o; o = align_up(o + 16 * tiles);
-    L.bwd_count = o; o = align_up(o + 4 * (size_t)item_count_at(kItemClasses));  // [item_count_at(c, x)]: the
-                                                                                 // items of class c, XCD list x
+    L.bwd_count = o; o = align_up(o + 4 * (size_t)item_count_at(kItemClasses));  // [0..3] the per-tile variant's;
+                                                                                 // [item_count_at(c)] class c items
     L.total = o;
     return L;
 }
@@ -216,9 +211,7 @@ inline BinLayout bin_layout(int K, int num_tiles, bool bwd = true) {
     L.records = o; o = align_up(o + 4 * 48 * kb);  // one record per (slot, quadrant)
     L.rec_flags = o; o = align_up(o + 4 * kb);
     L.ckpt = o; o = align_up(o + 16 * 64 * 4 * L.nslots);  // [slot][quadrant][64] float4 (T, own colour sum)
-    // uint2 (tile, seg << 2 | quadrant): list (c, x) at ((c * kItemXcds + x) * item_cap ..) — each at the full
-    // item bound (a list may hold every item of a step; the untouched rest costs address space only)
-    L.bwd_items = o; o = align_up(o + 8 * 4 * L.nslots * kItemClasses * kItemXcds);
+    L.bwd_items = o; o = align_up(o + 8 * 4 * L.nslots * kItemClasses);  // uint2 (tile, seg << 2 | quadrant)
     L.used = o; o = align_up(o + (bwd ? 8 * used_words(k, num_tiles) : 0));
     L.total = o;
     return L;
@@ -263,7 +256,7 @@ struct PreprocessArgs {
     int rect_packed;
     uint32_t* counters;  // kCounterSlots x kCounterStride (ImgLayout)
     uint8_t* touched;    // zeroed here: k_render_fwd sets the bytes of Gaussians some pixel blends
-    uint32_t* qmask_words = nullptr;  // [P] rect_quad_masks of every Gaussian with a tile (qmask_enabled)
+    uint64_t* qmask_words = nullptr;  // [P] rect_band_ranges of every Gaussian with a tile (qmask_enabled)
 };
 void launch_preprocess(const PreprocessArgs& a, hipStream_t s);
 void launch_depth_keys32(int P, const uint32_t* rect, const Splat* splat, uint32_t* key, hipStream_t s);
@@ -330,7 +323,7 @@ struct EmitArgs {
     int ids_only = 0;
     // qmask_words (the preprocess's per-Gaussian rect masks): every emitted id carries its instance's
     // quadrant mask in bits kIdBits.. (gs_qmask.h; qmask_enabled)
-    const uint32_t* qmask_words = nullptr;
+    const uint64_t* qmask_words = nullptr;
 };
 // The emission's per-instance quadrant masks (gs_qmask.h) for a P-Gaussian render: on unless
 // DGE_AMD_QMASK=0 (A/B: the blend's per-wave cull_keep instead), and only while ids fit kIdBits.
@@ -386,9 +379,7 @@ struct RenderArgs {
     int qmask = 0;        // the list ids carry the emission's quadrant masks (else: cull_keep per wave)
     uint32_t id_mask = 0xFFFFFFFFu;
     const float* colors = nullptr;  // forward-only: blend these [P,3] colours instead of the Splats' (recolor)
-    int xcd_items = 1;    // the backward's work lists by tile (kItemXcds); 0: by quadrant (A/B)
 };
-bool bwd_xcd_items();  // DGE_AMD_BWD_XCD (default on)
 void launch_render_forward(const RenderArgs& a, hipStream_t s);
 
 struct ApplyWeightsArgs {

@@ -1,6 +1,7 @@
 // gs_qmask.h — the per-instance quadrant mask: which 8x8 quadrants of a 16x16 tile a Gaussian can
 // reach with alpha >= 1/255 (forward.cu:336-348's skip tests), computed ONCE per (Gaussian, tile) by
-// the preprocess (a 32-bit word per Gaussian: 4 bits per tile of its rect, rects of up to 8 tiles)
+// the preprocess (a 64-bit word per Gaussian: each pixel-row band's range of quadrant columns, rects of up
+// to 8 x 4 tiles; the emission bounds larger ones per instance)
 // instead of by each of the four quadrant waves of the blend for every list position it walks (the
 // blend's cull_keep: ~136 VALU per lane and position, 14-21% of the heaviest waves' cycles, plus the
 // gathers of entries it then drops); the emission copies each instance's 4 bits into its list id.
@@ -140,16 +141,20 @@ GS_QM_HD inline uint32_t quad_mask(const QuadCull& q, float tx0, float ty0) {
     return m;
 }
 
-// The masks of a Gaussian's whole tile rect [x0, x0 + w) x [y0, y0 + h), w h <= kRectMaskTiles: tile
-// (x0 + i, y0 + j)'s 4 bits at 4 (j w + i) — the emission's instance order (row-major over the rect).
-// Each of the 2h pixel-row bands is bounded once (its extent turned into a range of quadrant columns),
-// not once per tile; the bits equal quad_mask's tile by tile.  Larger rects: all ones (every quadrant).
-constexpr int kRectMaskTiles = 8;
-GS_QM_HD inline uint32_t rect_quad_masks(const QuadCull& q, int x0, int y0, int w, int h) {
-    if (q.all || w * h > kRectMaskTiles) return 0xFFFFFFFFu;
-    uint32_t m = 0u;
+// The bound of a Gaussian's whole tile rect [x0, x0 + w) x [y0, y0 + h) (w <= kBandMaxW, h <= kBandMaxH) in
+// one 64-bit word: for each of its 2h pixel-row bands (band b: rows 16 y0 + 8 b .. + 7) the range of
+// quadrant columns c (pixels 16 x0 + 8 c .. + 7, c < 2w) the ellipse reaches — contiguous, the ellipse
+// being convex — as byte b = cmin << 4 | cmax (0xF0: none).  Each band is bounded once, not once per
+// tile; band_inst_mask() gives the instance's 4 bits, equal to quad_mask's tile by tile.  Larger rects
+// (huge footprints): the emission bounds each instance with quad_mask.
+constexpr int kBandMaxW = 8, kBandMaxH = 4;
+constexpr uint64_t kBandsAll = 0x0F0F0F0F0F0F0F0Full, kBandsNone = 0xF0F0F0F0F0F0F0F0ull;
+GS_QM_HD inline bool band_rect_fits(int w, int h) { return w <= kBandMaxW && h <= kBandMaxH; }
+GS_QM_HD inline uint64_t rect_band_ranges(const QuadCull& q, int x0, int y0, int w, int h) {
+    if (q.all) return kBandsAll;
+    uint64_t word = kBandsNone;
     const float mx = 1e-3f * q.dxE + 1e-3f, my = 1e-3f * q.dyE + 1e-3f;
-    for (int j = 0; j < 2 * h; ++j) {  // band j: pixel rows 16 y0 + 8 j .. + 7
+    for (int j = 0; j < 2 * h; ++j) {
         const float py0 = (float)(16 * y0 + 8 * j);
         const float Y0 = (q.gy - (py0 + 7.0f)) - my, Y1 = (q.gy - py0) + my;
         const float lo = fmaxf(Y0, -q.dyE), hi = fminf(Y1, q.dyE);
@@ -163,10 +168,33 @@ GS_QM_HD inline uint32_t rect_quad_masks(const QuadCull& q, int x0, int y0, int 
         if (lo <= -q.yr && -q.yr <= hi) xmin = -q.dxE;
         xmax += mx;
         xmin -= mx;
-        for (int c = 0; c < 2 * w; ++c) {  // quadrant column c: pixels 16 x0 + 8 c .. + 7
+        int cmin = 15, cmax = -1;
+        for (int c = 0; c < 2 * w; ++c) {
             const float px0 = (float)(16 * x0 + 8 * c);
             const float X0 = q.gx - (px0 + 7.0f), X1 = q.gx - px0;
-            if (X0 <= xmax && X1 >= xmin) m |= 1u << (4 * ((j >> 1) * w + (c >> 1)) + 2 * (j & 1) + (c & 1));
+            if (X0 <= xmax && X1 >= xmin) {
+                cmin = c < cmin ? c : cmin;
+                cmax = c;
+            }
+        }
+        if (cmax >= 0) {
+            word &= ~(0xFFull << (8 * j));
+            word |= (uint64_t)(cmin << 4 | cmax) << (8 * j);
+        }
+    }
+    return word;
+}
+// tile (x0 + i, y0 + j) of such a rect: its quadrant bits q = (qy << 1) | qx
+GS_QM_HD inline uint32_t band_inst_mask(uint64_t word, int i, int j) {
+    uint32_t m = 0u;
+#pragma unroll
+    for (int qy = 0; qy < 2; ++qy) {
+        const uint32_t band = (uint32_t)(word >> (8 * (2 * j + qy))) & 0xFFu;
+        const int cmin = (int)(band >> 4), cmax = (int)(band & 15u);
+#pragma unroll
+        for (int qx = 0; qx < 2; ++qx) {
+            const int c = 2 * i + qx;
+            if (cmin <= c && c <= cmax) m |= 1u << (2 * qy + qx);
         }
     }
     return m;

@@ -230,14 +230,12 @@ __global__ __launch_bounds__(1024) void k_tile_order(const uint2* __restrict__ r
 __device__ __forceinline__ int item_class(uint32_t kept) { return kept >= 64 ? 0 : kept >= 40 ? 1 : kept >= 20 ? 2 : 3; }
 __device__ __forceinline__ void emit_items(const RenderArgs& a, int tile, int quad, uint32_t nseg, uint32_t nkept,
                                            int lane) {
-    // (xcd_items 0, A/B: the quadrants of a tile spread over the lists, as before the XCD lists)
-    const int c = item_class(nkept / nseg), x = (a.xcd_items ? tile : 4 * tile + quad) & (kItemXcds - 1);
+    const int c = item_class(nkept / nseg);
     uint32_t base = 0;
-    if (lane == 0) base = atomicAdd(&a.bwd_count[item_count_at(c, x)], nseg);
+    if (lane == 0) base = atomicAdd(&a.bwd_count[item_count_at(c)], nseg);
     base = __shfl(base, 0);
     for (uint32_t k = lane; k < nseg; k += 64)
-        a.bwd_items[(size_t)(c * kItemXcds + x) * a.item_cap + base + k] =
-            make_uint2((uint32_t)tile, (k << 2) | (uint32_t)quad);
+        a.bwd_items[(size_t)c * a.item_cap + base + k] = make_uint2((uint32_t)tile, (k << 2) | (uint32_t)quad);
 }
 
 // BWD: the backward's bookkeeping (checkpoints, blended bits, touched bytes, the replay's work list);
@@ -745,10 +743,9 @@ constexpr int kBwdHalf = 128;           // list positions per LDS staging unit
 constexpr int kBwdNI = kSegLen / 64;    // list positions per lane
 static_assert(kSegLen % kBwdHalf == 0, "whole staging units per segment");
 
-// 4 waves per SIMD: <= 128 VGPRs (108; the item loop over an XCD list no longer fits 96, and 4 waves
-// measured as fast as 5 in round 2)
+// 5 waves per SIMD: the 128-position items need <= 96 VGPRs (no spill)
 #ifndef GS_BWD_WAVES
-#define GS_BWD_WAVES 4
+#define GS_BWD_WAVES 5
 #endif
 // One wave per work item = (8x8 quadrant, segment of its window), independent
 // 64-thread workgroups.  A segment is at most kSegLen = 128 list positions: the
@@ -770,20 +767,17 @@ __global__ __launch_bounds__(64, GS_BWD_WAVES) void k_render_bwd(RenderBwdArgs a
     __shared__ uint32_t s_pos[kBwdHalf + kBwdGroup];
     __shared__ uint2 s_pair[kBwdHalf + kBwdGroup];  // (Gaussian, slot) of the kept entries: the record writes
     const int lane = threadIdx.x;
-    // block -> work items (quadrant, segment) of its XCD's list x = b & 7, heaviest class first: block b
-    // takes items j, j + G/8, ... (j = b >> 3, G the grid), so every item runs (normally one per block,
-    // G being ~7x the items; several only if one list holds most of a step's items); blocks past the
-    // list's end exit (they dispatch after every real item).  (A persistent-wave work queue measured
-    // slower than the hardware dispatcher here.)
-    const int xl = (int)(blockIdx.x & (kItemXcds - 1));
+    // block -> work item (quadrant, segment) of the forward's list, heaviest class first; blocks past
+    // the list's end exit (they dispatch after every real item; see launch_render_backward for the
+    // grid).  (A persistent-wave work queue measured slower than the hardware dispatcher here.)
     uint32_t n_cls[kItemClasses], n_items = 0;
 #pragma unroll
     for (int c = 0; c < kItemClasses; ++c) {
-        n_cls[c] = a.bwd_count[item_count_at(c, xl)];
+        n_cls[c] = a.bwd_count[item_count_at(c)];
         n_items += n_cls[c];
     }
-    const uint32_t stride = gridDim.x / kItemXcds;
-    for (uint32_t qi = blockIdx.x / kItemXcds; qi < n_items; qi += stride) {
+    const uint32_t qi = blockIdx.x;
+    if (qi >= n_items) return;
     uint32_t cls = 0, idx = qi;  // class regions in order: heaviest items first
 #pragma unroll
     for (int c = 0; c < kItemClasses - 1; ++c)
@@ -791,7 +785,7 @@ __global__ __launch_bounds__(64, GS_BWD_WAVES) void k_render_bwd(RenderBwdArgs a
             idx -= n_cls[c];
             cls = c + 1;
         }
-    const uint2 item = a.bwd_items[(size_t)(cls * kItemXcds + xl) * a.item_cap + idx];
+    const uint2 item = a.bwd_items[(size_t)cls * a.item_cap + idx];
     const int tile = (int)item.x, quad = (int)(item.y & 3u), seg = (int)(item.y >> 2);
     const int qidx = 4 * tile + quad;
     const int tx = tile % a.gx, ty = tile / a.gx;
@@ -938,7 +932,7 @@ __global__ __launch_bounds__(64, GS_BWD_WAVES) void k_render_bwd(RenderBwdArgs a
         __syncthreads();
     }
     if (a.diag && lane == 0) {
-        uint64_t* d = a.diag + kDiagWords * (size_t)blockIdx.x;  // (a block's later items overwrite its first)
+        uint64_t* d = a.diag + kDiagWords * (size_t)qi;
         d[0] = t_start;
         d[1] = __builtin_amdgcn_s_memrealtime();
         d[2] = diag_kept;
@@ -948,7 +942,6 @@ __global__ __launch_bounds__(64, GS_BWD_WAVES) void k_render_bwd(RenderBwdArgs a
         d[6] = (uint64_t)seg << 32 | (uint32_t)qidx;
         d[7] = wave_location();
     }
-    }  // (items of this block)
 }
 
 // One workgroup per possible item (the bound, 4 x checkpoint slots, is ~7x the c2 count): the surplus
@@ -956,8 +949,7 @@ __global__ __launch_bounds__(64, GS_BWD_WAVES) void k_render_bwd(RenderBwdArgs a
 void launch_render_backward(const RenderBwdArgs& a, hipStream_t s) {
     const int tiles = a.gx * a.gy;
     if (tiles <= 0 || a.item_cap == 0) return;
-    const uint32_t grid = (a.item_cap + kItemXcds - 1) / kItemXcds * kItemXcds;  // (whole XCD rounds)
-    hipLaunchKernelGGL(k_render_bwd, dim3(grid), dim3(64), 0, s, a);
+    hipLaunchKernelGGL(k_render_bwd, dim3(a.item_cap), dim3(64), 0, s, a);
 }
 
 }  // namespace gs

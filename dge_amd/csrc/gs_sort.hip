@@ -567,12 +567,6 @@ __device__ __forceinline__ uint32_t rect_count(uint32_t v, int packed) {
     return ((v >> 16 & 0xFFu) - (v & 0xFFu)) * ((v >> 24) - (v >> 8 & 0xFFu));
 }
 
-// Instance k (row-major over the Gaussian's rect) of a rect_quad_masks word: its tile's 4 bits (rects of
-// more than kRectMaskTiles tiles carry all ones)
-__device__ __forceinline__ uint32_t inst_mask(uint32_t word, uint32_t k) {
-    return k < (uint32_t)kRectMaskTiles ? (word >> (4 * k)) & 0xFu : 0xFu;
-}
-
 // Block sums of the instance counts in depth order (k_scan_emit derives each
 // block's first slot from them).
 __global__ __launch_bounds__(256) void k_scan_reduce(EmitArgs a) {
@@ -622,8 +616,9 @@ __global__ __launch_bounds__(256) void k_scan_emit(EmitArgs a) {
     __shared__ uint32_t lds4[4];
     __shared__ uint32_t s_start[256];
     __shared__ uint32_t s_gauss[256];
-    __shared__ int4 s_rect[256];  // x0, y0, width | big << 16, the rect's quadrant masks (qmask_words)
-    __shared__ QuadCull s_qc[256];  // (rects of more than kRectMaskTiles tiles: the bound itself)
+    __shared__ int4 s_rect[256];  // x0, y0, width | big << 16
+    __shared__ uint2 s_qw[256];     // the rect's band word (qmask_words)
+    __shared__ QuadCull s_qc[256];  // (rects past band_rect_fits: the bound itself)
     // the block's first slot: the sum of the block sums before it (k_scan_reduce's, read from L2:
     // at most scan_blocks words; this replaced a one-workgroup top-level scan launch)
     uint32_t base;
@@ -636,7 +631,7 @@ __global__ __launch_bounds__(256) void k_scan_emit(EmitArgs a) {
     // every round's (rect, Gaussian) and quadrant-mask word loaded up front: one memory round trip
     // instead of two dependent ones per round
     uint2 grs[kScanIPT];
-    uint32_t qws[kScanIPT];
+    uint64_t qws[kScanIPT];
 #pragma unroll
     for (int it = 0; it < kScanIPT; ++it) {
         const uint32_t r = r_block + it * 256 + threadIdx.x;
@@ -645,7 +640,7 @@ __global__ __launch_bounds__(256) void k_scan_emit(EmitArgs a) {
 #pragma unroll
     for (int it = 0; it < kScanIPT; ++it) {
         const uint32_t c = rect_count(grs[it].x, a.rect_packed);
-        qws[it] = a.qmask_words && c && c <= (uint32_t)kRectMaskTiles ? a.qmask_words[grs[it].y] : 0u;
+        qws[it] = a.qmask_words && c ? a.qmask_words[grs[it].y] : 0ull;  // (unused past band_rect_fits)
     }
     for (int it = 0; it < kScanIPT; ++it) {
         const uint2 gr = grs[it];
@@ -663,14 +658,15 @@ __global__ __launch_bounds__(256) void k_scan_emit(EmitArgs a) {
                 const float2 xy = a.splat[g].xy;
                 q = tile_rect(xy.x, xy.y, a.radii[g], a.gx, a.gy);
             }
-            const bool big = a.qmask_words && c > (uint32_t)kRectMaskTiles;
+            const bool big = a.qmask_words && !band_rect_fits(q.x1 - q.x0, q.y1 - q.y0);
             if (big) {
                 const Splat* sp = a.splat + g;
                 const float2 xy = sp->xy;
                 const float4 co = sp->co;
                 s_qc[threadIdx.x] = quad_cull_setup(xy.x, xy.y, co.x, co.y, co.z, co.w);
             }
-            s_rect[threadIdx.x] = make_int4(q.x0, q.y0, (q.x1 - q.x0) | (big ? 1 << 16 : 0), (int)qws[it]);
+            s_rect[threadIdx.x] = make_int4(q.x0, q.y0, (q.x1 - q.x0) | (big ? 1 << 16 : 0), 0);
+            s_qw[threadIdx.x] = make_uint2((uint32_t)qws[it], (uint32_t)(qws[it] >> 32));
         }
         s_start[threadIdx.x] = off;
         s_gauss[threadIdx.x] = g;
@@ -693,9 +689,11 @@ __global__ __launch_bounds__(256) void k_scan_emit(EmitArgs a) {
             const int tx = q.x + (int)kx, ty = q.y + (int)ky;
             a.tile_key[base + j] = (uint32_t)(ty * a.gx + tx);
             uint32_t gv = s_gauss[lo];
-            if (a.qmask_words)
+            if (a.qmask_words) {
+                const uint2 qw = s_qw[lo];
                 gv |= (q.z >> 16 ? quad_mask(s_qc[lo], (float)(16 * tx), (float)(16 * ty))
-                                 : inst_mask((uint32_t)q.w, k)) << kIdBits;
+                                 : band_inst_mask((uint64_t)qw.y << 32 | qw.x, (int)kx, (int)ky)) << kIdBits;
+            }
             a.slot_gauss[base + j] = gv;
             if (a.rec_flags32) a.rec_flags32[base + j] = 0u;  // slot's four quadrant flags (no memset launch)
         }
@@ -729,7 +727,8 @@ __global__ __launch_bounds__(256) void k_scan_emit_x(EmitArgs a) {
     __shared__ PV s_pair[kEmitBatch];
     __shared__ uint16_t s_own[kEmitBatch];  // the batch's owners (+1): marks at the entries' starts, prefix max
     __shared__ uint32_t s_carry;
-    __shared__ QuadCull s_qc[256];  // (rects of more than kRectMaskTiles tiles: the bound itself)
+    __shared__ QuadCull s_qc[256];  // (rects past band_rect_fits: the bound itself)
+    __shared__ uint2 s_qw[256];     // the rect's band word (qmask_words)
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     if (blockIdx.x == 0)
         for (int t = tid; t < a.ntiles; t += 256) a.tile_count[t] = 0u;  // (the row pass counts into it)
@@ -757,16 +756,20 @@ __global__ __launch_bounds__(256) void k_scan_emit_x(EmitArgs a) {
         const uint32_t off = block_exclusive_scan(c, lds4, total);
         if (c) {
             a.first_slot[g] = base + off;
-            const bool big = a.qmask_words && c > (uint32_t)kRectMaskTiles;
+            const int rw = (int)((gr.x >> 16) & 0xFFu) - (int)(gr.x & 0xFFu);
+            const int rh = (int)(gr.x >> 24) - (int)((gr.x >> 8) & 0xFFu);
+            const bool big = a.qmask_words && !band_rect_fits(rw, rh);
+            uint64_t qw = 0ull;
             if (big) {
                 const Splat* sp = a.splat + g;
                 const float2 xy = sp->xy;
                 const float4 co = sp->co;
                 s_qc[tid] = quad_cull_setup(xy.x, xy.y, co.x, co.y, co.z, co.w);
+            } else if (a.qmask_words) {
+                qw = a.qmask_words[g];
             }
-            s_rect[tid] = make_int4((int)(gr.x & 0xFFu), (int)((gr.x >> 8) & 0xFFu),
-                                    ((int)((gr.x >> 16) & 0xFFu) - (int)(gr.x & 0xFFu)) | (big ? 1 << 16 : 0),
-                                    a.qmask_words && !big ? (int)a.qmask_words[g] : 0);
+            s_rect[tid] = make_int4((int)(gr.x & 0xFFu), (int)((gr.x >> 8) & 0xFFu), rw | (big ? 1 << 16 : 0), 0);
+            s_qw[tid] = make_uint2((uint32_t)qw, (uint32_t)(qw >> 32));
         }
         s_start[tid] = off;
         s_gauss[tid] = g;
@@ -823,9 +826,12 @@ __global__ __launch_bounds__(256) void k_scan_emit_x(EmitArgs a) {
                 const uint32_t x = (uint32_t)q.x + kx, y = (uint32_t)q.y + ky;
                 kk[e] = y << kXBits | x;
                 uint32_t gv = s_gauss[lo];
-                if (a.qmask_words)
-                    gv |= (q.z >> 16 ? quad_mask(s_qc[lo], (float)(16 * x), (float)(16 * y)) : inst_mask((uint32_t)q.w, k))
+                if (a.qmask_words) {
+                    const uint2 qw = s_qw[lo];
+                    gv |= (q.z >> 16 ? quad_mask(s_qc[lo], (float)(16 * x), (float)(16 * y))
+                                     : band_inst_mask((uint64_t)qw.y << 32 | qw.x, (int)kx, (int)ky))
                           << kIdBits;
+                }
                 if constexpr (IDS) pv[e] = gv;
                 else pv[e] = make_uint2(gv, base + j);
                 if (valid && a.rec_flags32 && base + j < a.cap) a.rec_flags32[base + j] = 0u;  // (slot order: coalesced)

@@ -100,8 +100,7 @@ int main(int argc, char** argv) {
     // the per-rect form (the preprocess's word) against quad_mask tile by tile
     long rect_cases = 0, rect_diff = 0;
     for (long n = 0; n < cases / 4; ++n) {
-        const int w = 1 + (int)(U(rng) * 4.0f), h = 1 + (int)(U(rng) * 4.0f);
-        if (w * h > gs::kRectMaskTiles) continue;
+        const int w = 1 + (int)(U(rng) * gs::kBandMaxW), h = 1 + (int)(U(rng) * gs::kBandMaxH);
         const int x0 = (int)(U(rng) * 100.0f), y0 = (int)(U(rng) * 60.0f);
         const float s1 = expf(logf(0.3f) + U(rng) * logf(100.0f)), s2 = expf(logf(0.3f) + U(rng) * logf(100.0f));
         const float th = 6.2831853f * U(rng), cs = cosf(th), sn = sinf(th);
@@ -110,11 +109,11 @@ int main(int argc, char** argv) {
         if (!(det > 0.0f)) continue;
         const float gx = 16.0f * x0 + U(rng) * 16.0f * w, gy = 16.0f * y0 + U(rng) * 16.0f * h;
         const gs::QuadCull qc = gs::quad_cull_setup(gx, gy, c11 / det, -c01 / det, c00 / det, 0.004f + U(rng));
-        const uint32_t word = gs::rect_quad_masks(qc, x0, y0, w, h);
+        const uint64_t word = gs::rect_band_ranges(qc, x0, y0, w, h);
         for (int j = 0; j < h; ++j)
             for (int i = 0; i < w; ++i) {
                 const uint32_t t = gs::quad_mask(qc, 16.0f * (x0 + i), 16.0f * (y0 + j));
-                rect_diff += ((word >> (4 * (j * w + i))) & 0xFu) != t;
+                rect_diff += gs::band_inst_mask(word, i, j) != t;
             }
         ++rect_cases;
     }
