@@ -628,10 +628,14 @@ __global__ __launch_bounds__(256) void k_scan_emit(EmitArgs a) {
         block_exclusive_scan(part, lds4, base);
     }
     const uint32_t r_block = blockIdx.x * (uint32_t)kScanTile;
-    // every round's (rect, Gaussian) and quadrant-mask word loaded up front: one memory round trip
-    // instead of two dependent ones per round
+    // every round's inputs loaded up front (one memory round trip instead of dependent ones per round):
+    // (rect, Gaussian), its quadrant-mask word, and the Splat's 2D mean + conic where the rect itself or a
+    // bound too large for a word needs them
     uint2 grs[kScanIPT];
     uint64_t qws[kScanIPT];
+    float2 xys[kScanIPT];
+    float4 cos_[kScanIPT];
+    int rads[kScanIPT];
 #pragma unroll
     for (int it = 0; it < kScanIPT; ++it) {
         const uint32_t r = r_block + it * 256 + threadIdx.x;
@@ -639,9 +643,16 @@ __global__ __launch_bounds__(256) void k_scan_emit(EmitArgs a) {
     }
 #pragma unroll
     for (int it = 0; it < kScanIPT; ++it) {
-        const uint32_t c = rect_count(grs[it].x, a.rect_packed);
-        qws[it] = a.qmask_words && c ? a.qmask_words[grs[it].y] : 0ull;  // (unused past band_rect_fits)
+        const uint32_t c = rect_count(grs[it].x, a.rect_packed), g = grs[it].y;
+        const bool fits = a.rect_packed && band_rect_fits((int)((grs[it].x >> 16) & 0xFFu) - (int)(grs[it].x & 0xFFu),
+                                                          (int)(grs[it].x >> 24) - (int)((grs[it].x >> 8) & 0xFFu));
+        const bool need_splat = c && (!a.rect_packed || (a.qmask_words && !fits));
+        qws[it] = a.qmask_words && c && (fits || !a.rect_packed) ? a.qmask_words[g] : 0ull;
+        xys[it] = need_splat ? a.splat[g].xy : make_float2(0.f, 0.f);
+        cos_[it] = need_splat && a.qmask_words ? a.splat[g].co : make_float4(0.f, 0.f, 0.f, 0.f);
+        rads[it] = c && !a.rect_packed ? a.radii[g] : 0;
     }
+#pragma unroll  // (the prefetched arrays stay in registers)
     for (int it = 0; it < kScanIPT; ++it) {
         const uint2 gr = grs[it];
         const uint32_t g = gr.y;
@@ -655,16 +666,12 @@ __global__ __launch_bounds__(256) void k_scan_emit(EmitArgs a) {
                 q.x0 = (int)(gr.x & 0xFFu); q.y0 = (int)((gr.x >> 8) & 0xFFu);
                 q.x1 = (int)((gr.x >> 16) & 0xFFu); q.y1 = (int)(gr.x >> 24);
             } else {
-                const float2 xy = a.splat[g].xy;
-                q = tile_rect(xy.x, xy.y, a.radii[g], a.gx, a.gy);
+                q = tile_rect(xys[it].x, xys[it].y, rads[it], a.gx, a.gy);
             }
             const bool big = a.qmask_words && !band_rect_fits(q.x1 - q.x0, q.y1 - q.y0);
-            if (big) {
-                const Splat* sp = a.splat + g;
-                const float2 xy = sp->xy;
-                const float4 co = sp->co;
-                s_qc[threadIdx.x] = quad_cull_setup(xy.x, xy.y, co.x, co.y, co.z, co.w);
-            }
+            if (big)
+                s_qc[threadIdx.x] = quad_cull_setup(xys[it].x, xys[it].y, cos_[it].x, cos_[it].y, cos_[it].z,
+                                                    cos_[it].w);
             s_rect[threadIdx.x] = make_int4(q.x0, q.y0, (q.x1 - q.x0) | (big ? 1 << 16 : 0), 0);
             s_qw[threadIdx.x] = make_uint2((uint32_t)qws[it], (uint32_t)(qws[it] >> 32));
         }
@@ -747,9 +754,30 @@ __global__ __launch_bounds__(256) void k_scan_emit_x(EmitArgs a) {
     for (int i = tid; i < 4 * kXDigits; i += 256) (&cnt[0][0])[i] = 0;
     __syncthreads();
     const uint32_t r_block = blockIdx.x * (uint32_t)kScanTile;
+    // every round's inputs up front (as k_scan_emit): (rect, Gaussian), the mask word or, for a rect too
+    // large for one, the Splat's 2D mean + conic
+    uint2 grs[kScanIPT];
+    uint64_t qws[kScanIPT];
+    float2 xys[kScanIPT];
+    float4 cos_[kScanIPT];
+#pragma unroll
     for (int it = 0; it < kScanIPT; ++it) {
         const uint32_t r = r_block + it * 256 + tid;
-        const uint2 gr = r < (uint32_t)a.P ? a.order[r] : make_uint2(0u, 0u);
+        grs[it] = r < (uint32_t)a.P ? a.order[r] : make_uint2(0u, 0u);
+    }
+#pragma unroll
+    for (int it = 0; it < kScanIPT; ++it) {
+        const uint2 gr = grs[it];
+        const bool c = rect_count(gr.x, 1) != 0u;
+        const bool fits = band_rect_fits((int)((gr.x >> 16) & 0xFFu) - (int)(gr.x & 0xFFu),
+                                         (int)(gr.x >> 24) - (int)((gr.x >> 8) & 0xFFu));
+        qws[it] = a.qmask_words && c && fits ? a.qmask_words[gr.y] : 0ull;
+        xys[it] = a.qmask_words && c && !fits ? a.splat[gr.y].xy : make_float2(0.f, 0.f);
+        cos_[it] = a.qmask_words && c && !fits ? a.splat[gr.y].co : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll  // (the prefetched arrays stay in registers)
+    for (int it = 0; it < kScanIPT; ++it) {
+        const uint2 gr = grs[it];
         const uint32_t g = gr.y;
         const uint32_t c = rect_count(gr.x, 1);
         uint32_t total;
@@ -759,17 +787,10 @@ __global__ __launch_bounds__(256) void k_scan_emit_x(EmitArgs a) {
             const int rw = (int)((gr.x >> 16) & 0xFFu) - (int)(gr.x & 0xFFu);
             const int rh = (int)(gr.x >> 24) - (int)((gr.x >> 8) & 0xFFu);
             const bool big = a.qmask_words && !band_rect_fits(rw, rh);
-            uint64_t qw = 0ull;
-            if (big) {
-                const Splat* sp = a.splat + g;
-                const float2 xy = sp->xy;
-                const float4 co = sp->co;
-                s_qc[tid] = quad_cull_setup(xy.x, xy.y, co.x, co.y, co.z, co.w);
-            } else if (a.qmask_words) {
-                qw = a.qmask_words[g];
-            }
+            if (big)
+                s_qc[tid] = quad_cull_setup(xys[it].x, xys[it].y, cos_[it].x, cos_[it].y, cos_[it].z, cos_[it].w);
             s_rect[tid] = make_int4((int)(gr.x & 0xFFu), (int)((gr.x >> 8) & 0xFFu), rw | (big ? 1 << 16 : 0), 0);
-            s_qw[tid] = make_uint2((uint32_t)qw, (uint32_t)(qw >> 32));
+            s_qw[tid] = make_uint2((uint32_t)qws[it], (uint32_t)(qws[it] >> 32));
         }
         s_start[tid] = off;
         s_gauss[tid] = g;
