@@ -42,7 +42,7 @@ int main(int argc, char** argv) {
     const long cases = argc > 1 ? atol(argv[1]) : 200000;
     std::mt19937_64 rng(argc > 2 ? atoll(argv[2]) : 1);
     std::uniform_real_distribution<float> U(0.0f, 1.0f);
-    long misses = 0, set = 0, needed = 0, degenerate = 0, cull_set = 0, cull_miss = 0;
+    long misses = 0, set = 0, needed = 0, degenerate = 0, cull_set = 0, cull_miss = 0, aabb_set = 0;
     float pw[256], G[256];
     for (long n = 0; n < cases; ++n) {
         // tile origin: small and large image coordinates (c4: 1920 x 1080)
@@ -89,6 +89,12 @@ int main(int argc, char** argv) {
             set += bit;
             const bool ck = cull_keep_host(gx, gy, a, b, c, o, tx0 + 8.0f * (float)(q & 1), ty0 + 8.0f * (float)(q >> 1));
             cull_set += ck;
+            {  // (comparison only) the ellipse's bounding box against the quadrant box
+                const float bx0 = tx0 + 8.0f * (float)(q & 1), by0 = ty0 + 8.0f * (float)(q >> 1);
+                const bool ab = qc.all || (qc.dyE >= 0.0f && gx + qc.dxE >= bx0 && gx - qc.dxE <= bx0 + 7.0f &&
+                                           gy + qc.dyE >= by0 && gy - qc.dyE <= by0 + 7.0f);
+                aabb_set += ab;
+            }
             cull_miss += any && !ck;
             if (any && !bit) {
                 if (++misses <= 10)
@@ -120,7 +126,7 @@ int main(int argc, char** argv) {
     printf("rect_cases %ld rect_mismatches %ld\n", rect_cases, rect_diff);
     if (rect_diff) misses += rect_diff;
     printf("cases %ld degenerate %ld quadrants_needed %ld bits_set %ld misses %ld overkept %.4f (cull_keep: %ld kept, "
-           "overkept %.4f, misses %ld)\n", cases, degenerate, needed, set, misses, set ? (double)(set - needed) / (double)set : 0.0,
-           cull_set, cull_set ? (double)(cull_set - needed) / (double)cull_set : 0.0, cull_miss);
+           "overkept %.4f, misses %ld) (bounding box: %ld kept)\n", cases, degenerate, needed, set, misses, set ? (double)(set - needed) / (double)set : 0.0,
+           cull_set, cull_set ? (double)(cull_set - needed) / (double)cull_set : 0.0, cull_miss, aabb_set);
     return misses ? 1 : 0;
 }
