@@ -120,6 +120,16 @@ int depth_pass_bits() {
     return bits;
 }
 
+// DGE_AMD_VIEWS_ISSUE=view: a batch's first halves enqueued view by view (round 3) instead of every
+// preprocess first (A/B)
+bool views_issue_by_view() {
+    static const bool on = [] {
+        const char* e = getenv("DGE_AMD_VIEWS_ISSUE");
+        return e && !strcmp(e, "view");
+    }();
+    return on;
+}
+
 // Pinned read-back slot of one forward's preprocess counters + its event.  A
 // pool per device: several forwards may be between begin and end at once
 // (gs_rasterize_forward_begin / _end), each holding its own slot.
@@ -393,7 +403,6 @@ int bin_prepare_in(FwdState& f, int copy_colors, void* geom, void* img, hipStrea
     pa.rect_packed = rect_packable(g.gx, g.gy) ? 1 : 0;
     pa.counters = counters;
     pa.touched = at<uint8_t>(geom, gl.touched);
-    pa.qmask_words = qmask_enabled(P) ? at<uint64_t>(geom, gl.qmask) : nullptr;
     return GS_OK;
 }
 
@@ -433,7 +442,6 @@ int bin_after_preprocess(FwdState& f, hipStream_t stream) {
     ea.P = P; ea.gx = g.gx; ea.gy = g.gy;
     ea.order = at<uint2>(geom, cur ? gl.val1 : gl.val0);
     ea.rect_packed = pa.rect_packed;
-    ea.qmask_words = pa.qmask_words;
     ea.tiles_touched = pa.tiles_touched;
     ea.splat = pa.splat;
     ea.radii = pa.radii;
@@ -649,8 +657,6 @@ int render_launch(FwdState& f, void* bin, uint32_t K_layout, int order_ready, fl
     ra.out_depth = out_depth;
     ra.touched = at<uint8_t>(geom, gl.touched);
     ra.diag = diag_buffer(0, kDiagWords * (size_t)g.tiles * 4);
-    ra.qmask = qmask_enabled(f.gp.P) ? 1 : 0;
-    ra.id_mask = id_mask_for(f.gp.P);
     GS_SKIP("fwd") { StageScope sc(ST_RENDER_FWD, stream); launch_render_forward(ra, stream); }
     GS_LAUNCHED("render");
     return GS_OK;
@@ -690,7 +696,6 @@ int replay_view(const gs_settings* s, const gs_params* gp, int R, const void* ge
     rb.W = g.W; rb.H = g.H; rb.gx = g.gx; rb.gy = g.gy;
     rb.ranges = at<uint2>(img, il.ranges);
     rb.point_pairs = at<uint2>(binning, bl.point_pairs);
-    rb.id_mask = id_mask_for(P);
     rb.bwd_items = at<uint2>(binning, bl.bwd_items);
     rb.bwd_count = at<uint32_t>(const_cast<void*>(img), il.bwd_count);
     rb.tile_last = at<uint32_t>(img, il.tile_last);
@@ -781,13 +786,6 @@ struct gs_forward_state {
 namespace gs {
 int report_error(int code, const char* msg) { return set_error(code, "%s", msg); }
 
-bool qmask_enabled(int P) {
-    static const bool on = [] {
-        const char* e = getenv("DGE_AMD_QMASK");
-        return !(e && !strcmp(e, "0"));
-    }();
-    return on && P >= 0 && P < (1 << kIdBits);
-}
 
 uint64_t* diag_buffer(int which, size_t n_u64) {
     Diag& d = diag();
@@ -1029,8 +1027,6 @@ int gs_render_recolor(const gs_settings* s, int P, int num_rendered, const void*
         ra.out_depth = out_depth;
         ra.touched = nullptr;
         ra.diag = nullptr;
-        ra.qmask = qmask_enabled(P) ? 1 : 0;
-        ra.id_mask = id_mask_for(P);
         ra.colors = colors;
         GS_SKIP("fwd") { StageScope sc(ST_RENDER_FWD, stream); launch_render_forward(ra, stream); }
         GS_LAUNCHED("recolor render");
@@ -1253,7 +1249,10 @@ int gs_views_forward(int n, const gs_settings* const* s, const gs_params* const*
         hipStream_t join = (hipStream_t)join_;
         int rc = fork_from(h.get(), join, streams);  // the views' streams start after the caller's work
         if (rc) return rc;
-        // first halves on every view's stream: nothing waits for any count yet
+        // first halves on every view's stream: nothing waits for any count yet.  Breadth first: every
+        // view's preprocess is enqueued before any view's depth sort, so the views' chains start together
+        // (view by view, the last view's preprocess started ~200 us of host issue after the first's and
+        // the forward phase ended with that view)
         for (int v = 0; v < n; ++v) {
             FwdState& f = h->f[v];
             if (f.gp.P == 0) continue;
@@ -1263,7 +1262,15 @@ int gs_views_forward(int n, const gs_settings* const* s, const gs_params* const*
             if (rc) return rc;
             GS_SKIP("pre") { StageScope sc(ST_PREPROCESS, stream); launch_preprocess(f.pa, stream); }
             GS_LAUNCHED("preprocess");
-            rc = bin_after_preprocess(f, stream);
+            if (views_issue_by_view()) {  // (A/B: round 3's order)
+                rc = bin_after_preprocess(f, stream);
+                if (rc) return rc;
+            }
+        }
+        for (int v = 0; v < n && !views_issue_by_view(); ++v) {
+            FwdState& f = h->f[v];
+            if (f.gp.P == 0) continue;
+            rc = bin_after_preprocess(f, (hipStream_t)streams[v]);
             if (rc) return rc;
         }
         // second halves: a speculated view's binning runs on the device count, capped at its capacity;
@@ -1514,8 +1521,6 @@ int gs_apply_weights(const gs_settings* s, int P, int M, const float* means3D, f
         aw.image_weights = image_weights;
         aw.weights = weights;
         aw.cnt = cnt;
-        aw.qmask = qmask_enabled(P) ? 1 : 0;
-        aw.id_mask = id_mask_for(P);
         { StageScope sc(ST_APPLY_WEIGHTS, stream); launch_render_apply_weights(aw, stream); }
         GS_LAUNCHED("apply_weights render");
         return GS_OK;

@@ -25,8 +25,6 @@
 #include <stddef.h>
 #include <stdint.h>
 
-#include "gs_qmask.h"
-
 namespace gs {
 
 constexpr int kSortIPT = 16;                    // keys per thread in the tile-key radix kernels
@@ -92,7 +90,7 @@ struct alignas(64) Splat {
 };
 
 struct GeomLayout {
-    size_t splat, tiles_touched, clamped, touched, live_count, live_list, radii, first_slot, qmask;
+    size_t splat, tiles_touched, clamped, touched, live_count, live_list, radii, first_slot;
     // live_count: one u32 per 256-Gaussian block (k_gauss_live); live_list: block-local compacted ids
     size_t key0, key1, val0, val1, rect, sort_hist, sort_totals, scan_sums, emit_hist, total;
     int sort_blocks, scan_blocks;
@@ -111,7 +109,6 @@ inline GeomLayout geom_layout(int P) {
     L.live_list = o; o = align_up(o + 4 * p);
     L.radii = o; o = align_up(o + 4 * p);
     L.first_slot = o; o = align_up(o + 4 * p);
-    L.qmask = o; o = align_up(o + 8 * p);  // each Gaussian's rect bound (rect_band_ranges, gs_qmask.h)
     L.key0 = o; o = align_up(o + 4 * p);
     L.key1 = o; o = align_up(o + 4 * p);
     L.val0 = o; o = align_up(o + 8 * p);  // depth sort values: uint2 (rect-or-count, Gaussian)
@@ -256,7 +253,6 @@ struct PreprocessArgs {
     int rect_packed;
     uint32_t* counters;  // kCounterSlots x kCounterStride (ImgLayout)
     uint8_t* touched;    // zeroed here: k_render_fwd sets the bytes of Gaussians some pixel blends
-    uint64_t* qmask_words = nullptr;  // [P] rect_band_ranges of every Gaussian with a tile (qmask_enabled)
 };
 void launch_preprocess(const PreprocessArgs& a, hipStream_t s);
 void launch_depth_keys32(int P, const uint32_t* rect, const Splat* splat, uint32_t* key, hipStream_t s);
@@ -321,15 +317,7 @@ struct EmitArgs {
     // ids_only (a forward-only render's two-level binning): the lists carry the Gaussian id alone (u32 at
     // pairs_out / the point list) — the binning slot is only the backward's record address
     int ids_only = 0;
-    // qmask_words (the preprocess's per-Gaussian rect masks): every emitted id carries its instance's
-    // quadrant mask in bits kIdBits.. (gs_qmask.h; qmask_enabled)
-    const uint64_t* qmask_words = nullptr;
 };
-// The emission's per-instance quadrant masks (gs_qmask.h) for a P-Gaussian render: on unless
-// DGE_AMD_QMASK=0 (A/B: the blend's per-wave cull_keep instead), and only while ids fit kIdBits.
-// id_mask_for(P): what strips the mask from a list's id (all ones when there is none).
-bool qmask_enabled(int P);
-inline uint32_t id_mask_for(int P) { return qmask_enabled(P) ? kIdMask : 0xFFFFFFFFu; }
 void launch_scan_reduce(const EmitArgs& a, hipStream_t s);
 void launch_scan_emit(const EmitArgs& a, hipStream_t s);
 // two-level binning after the instance count is known: column scan + k_scan_emit_x, the row pass
@@ -376,8 +364,6 @@ struct RenderArgs {
                           // exactly the Gaussians the backward gives a record, known after the forward
     uint64_t* diag;       // optional [tiles*4][kDiagWords] (see diag_buffer)
     int bwd = 1;          // 0: a forward-only render (gs_params.forward_only): no backward bookkeeping
-    int qmask = 0;        // the list ids carry the emission's quadrant masks (else: cull_keep per wave)
-    uint32_t id_mask = 0xFFFFFFFFu;
     const float* colors = nullptr;  // forward-only: blend these [P,3] colours instead of the Splats' (recolor)
 };
 void launch_render_forward(const RenderArgs& a, hipStream_t s);
@@ -390,8 +376,6 @@ struct ApplyWeightsArgs {
     const float* image_weights;
     float* weights;
     int* cnt;
-    int qmask = 0;  // (as RenderArgs)
-    uint32_t id_mask = 0xFFFFFFFFu;
 };
 void launch_render_apply_weights(const ApplyWeightsArgs& a, hipStream_t s);
 void launch_blend_exp(long long n, const float* x, float* y, hipStream_t s);
@@ -415,7 +399,6 @@ struct RenderBwdArgs {
     float4* records;     // [4*K][3] float4: one record per (slot, quadrant), kept entries only
     uint8_t* rec_flags;  // [4*K] set to 1 with each record (zeroed before the launch)
     uint64_t* diag;   // optional [item_cap][kDiagWords], by queue position (see diag_buffer)
-    uint32_t id_mask = 0xFFFFFFFFu;  // strips the emission's quadrant masks from the list ids
 };
 void launch_render_backward(const RenderBwdArgs& a, hipStream_t s);
 

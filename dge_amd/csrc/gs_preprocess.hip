@@ -183,10 +183,6 @@ __global__ __launch_bounds__(256) void k_preprocess(PreprocessArgs a) {
                 const Rect r = tile_rect(pix.x, pix.y, (int)rad, a.gx, a.gy);
                 const uint32_t area = (uint32_t)((r.y1 - r.y0) * (r.x1 - r.x0));
                 if (area != 0) {
-                    if (a.qmask_words && band_rect_fits(r.x1 - r.x0, r.y1 - r.y0))  // (the blend's cull, per band)
-                        a.qmask_words[idx] = rect_band_ranges(quad_cull_setup(pix.x, pix.y, conic.x, conic.y, conic.z,
-                                                                              conic.w),
-                                                              r.x0, r.y0, r.x1 - r.x0, r.y1 - r.y0);
                     rect = a.rect_packed ? pack_rect(r.x0, r.y0, r.x1, r.y1) : area;
                     radius_out = (int)rad;
                     touched = area;

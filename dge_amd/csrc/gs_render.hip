@@ -303,10 +303,6 @@ __global__ __launch_bounds__(64, 3) void k_render_fwd(RenderArgs a) {
     };
     uint32_t ids[4], cid[4];  // cid: the ids of the entries in `cur` (the touched bytes at the round's end)
     Entry cur[4];
-    // qmask: the list ids carry the emission's quadrant masks — the cull is one bit, and an entry this
-    // quadrant drops gathers Gaussian 0 (one shared line) instead of its Splat
-    const uint32_t qbit = a.qmask ? 1u << (kIdBits + quad) : 0u;
-    const auto gather_id = [&](uint32_t id) { return a.qmask && !(id & qbit) ? 0u : id & a.id_mask; };
     // (gs_render_recolor: a forward-only blend over another render's binning with its own colours)
     const auto gather = [&](uint32_t id) {
         Entry e = gather_entry(a.splat, id);
@@ -322,7 +318,7 @@ __global__ __launch_bounds__(64, 3) void k_render_fwd(RenderArgs a) {
     load_ids(range.x, ids);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        cur[i] = gather(gather_id(ids[i]));
+        cur[i] = gather(ids[i]);
         cid[i] = ids[i];
     }
     load_ids(range.x + kRound, ids);
@@ -375,8 +371,7 @@ __global__ __launch_bounds__(64, 3) void k_render_fwd(RenderArgs a) {
                 nk = n_mid;
             }
             const uint32_t k = b + 64 * i + lane;
-            const bool keep = k < range.y && (a.qmask ? (cid[i] & qbit) != 0u
-                                                      : cull_keep(cur[i].xy, cur[i].co, (float)bx0, (float)by0));
+            const bool keep = k < range.y && cull_keep(cur[i].xy, cur[i].co, (float)bx0, (float)by0);
             const uint64_t km = __ballot(keep);
             kslot[i] = keep ? nk + __popcll(km & lanemask_lt()) : -1;
             if (keep) {
@@ -389,7 +384,7 @@ __global__ __launch_bounds__(64, 3) void k_render_fwd(RenderArgs a) {
                 s_op[slot] = cur[i].co.w;
                 s_rgbd[slot] = cur[i].f;
                 s_pos[slot] = k - range.x + 1;  // 1-based contributor index (forward.cu:331)
-                s_id[slot] = cid[i] & a.id_mask;
+                s_id[slot] = cid[i];
             }
             nk += __popcll(km);
         }
@@ -410,7 +405,7 @@ __global__ __launch_bounds__(64, 3) void k_render_fwd(RenderArgs a) {
         // next round's gathers and the round after's ids, in flight during the blend
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            cur[i] = gather(gather_id(ids[i]));
+            cur[i] = gather(ids[i]);
             cid[i] = ids[i];
         }
         load_ids(b + 2 * kRound, ids);
@@ -603,11 +598,10 @@ __global__ __launch_bounds__(64) void k_render_apply_weights(ApplyWeightsArgs a)
         float4 co = make_float4(0.f, 0.f, 0.f, 0.f);
         uint32_t id = 0;
         if (k < range.y) {
-            const uint32_t v = a.point_pairs[k].x;
-            id = v & a.id_mask;
+            id = a.point_pairs[k].x;
             xy = a.splat[id].xy;
             co = a.splat[id].co;
-            keep = a.qmask ? ((v >> (kIdBits + quad)) & 1u) != 0u : cull_keep(xy, co, (float)bx0, (float)by0);
+            keep = cull_keep(xy, co, (float)bx0, (float)by0);
         }
         const uint64_t km = __ballot(keep);
         if (keep) {
@@ -819,7 +813,7 @@ __global__ __launch_bounds__(64, GS_BWD_WAVES) void k_render_bwd(RenderBwdArgs a
     Entry cur[kBwdNI];
 #pragma unroll
     for (int i = 0; i < kBwdNI; ++i)  // (dropped entries gather Gaussian 0: one shared line)
-        cur[i] = gather_entry(a.splat, (kb >> i) & 1u ? pairs[i].x & a.id_mask : 0u);
+        cur[i] = gather_entry(a.splat, (kb >> i) & 1u ? pairs[i].x : 0u);
 
     const size_t HW = (size_t)a.W * a.H;
     const size_t pix = inside ? (size_t)a.W * py + px : 0;

@@ -616,9 +616,7 @@ __global__ __launch_bounds__(256) void k_scan_emit(EmitArgs a) {
     __shared__ uint32_t lds4[4];
     __shared__ uint32_t s_start[256];
     __shared__ uint32_t s_gauss[256];
-    __shared__ int4 s_rect[256];  // x0, y0, width | big << 16
-    __shared__ uint2 s_qw[256];     // the rect's band word (qmask_words)
-    __shared__ QuadCull s_qc[256];  // (rects past band_rect_fits: the bound itself)
+    __shared__ int4 s_rect[256];  // x0, y0, width, -
     // the block's first slot: the sum of the block sums before it (k_scan_reduce's, read from L2:
     // at most scan_blocks words; this replaced a one-workgroup top-level scan launch)
     uint32_t base;
@@ -629,12 +627,9 @@ __global__ __launch_bounds__(256) void k_scan_emit(EmitArgs a) {
     }
     const uint32_t r_block = blockIdx.x * (uint32_t)kScanTile;
     // every round's inputs loaded up front (one memory round trip instead of dependent ones per round):
-    // (rect, Gaussian), its quadrant-mask word, and the Splat's 2D mean + conic where the rect itself or a
-    // bound too large for a word needs them
+    // (rect, Gaussian), and where the rect is not packed the Splat's 2D mean and the radius it comes from
     uint2 grs[kScanIPT];
-    uint64_t qws[kScanIPT];
     float2 xys[kScanIPT];
-    float4 cos_[kScanIPT];
     int rads[kScanIPT];
 #pragma unroll
     for (int it = 0; it < kScanIPT; ++it) {
@@ -644,12 +639,7 @@ __global__ __launch_bounds__(256) void k_scan_emit(EmitArgs a) {
 #pragma unroll
     for (int it = 0; it < kScanIPT; ++it) {
         const uint32_t c = rect_count(grs[it].x, a.rect_packed), g = grs[it].y;
-        const bool fits = a.rect_packed && band_rect_fits((int)((grs[it].x >> 16) & 0xFFu) - (int)(grs[it].x & 0xFFu),
-                                                          (int)(grs[it].x >> 24) - (int)((grs[it].x >> 8) & 0xFFu));
-        const bool need_splat = c && (!a.rect_packed || (a.qmask_words && !fits));
-        qws[it] = a.qmask_words && c && (fits || !a.rect_packed) ? a.qmask_words[g] : 0ull;
-        xys[it] = need_splat ? a.splat[g].xy : make_float2(0.f, 0.f);
-        cos_[it] = need_splat && a.qmask_words ? a.splat[g].co : make_float4(0.f, 0.f, 0.f, 0.f);
+        xys[it] = c && !a.rect_packed ? a.splat[g].xy : make_float2(0.f, 0.f);
         rads[it] = c && !a.rect_packed ? a.radii[g] : 0;
     }
 #pragma unroll  // (the prefetched arrays stay in registers)
@@ -668,12 +658,7 @@ __global__ __launch_bounds__(256) void k_scan_emit(EmitArgs a) {
             } else {
                 q = tile_rect(xys[it].x, xys[it].y, rads[it], a.gx, a.gy);
             }
-            const bool big = a.qmask_words && !band_rect_fits(q.x1 - q.x0, q.y1 - q.y0);
-            if (big)
-                s_qc[threadIdx.x] = quad_cull_setup(xys[it].x, xys[it].y, cos_[it].x, cos_[it].y, cos_[it].z,
-                                                    cos_[it].w);
-            s_rect[threadIdx.x] = make_int4(q.x0, q.y0, (q.x1 - q.x0) | (big ? 1 << 16 : 0), 0);
-            s_qw[threadIdx.x] = make_uint2((uint32_t)qws[it], (uint32_t)(qws[it] >> 32));
+            s_rect[threadIdx.x] = make_int4(q.x0, q.y0, q.x1 - q.x0, 0);
         }
         s_start[threadIdx.x] = off;
         s_gauss[threadIdx.x] = g;
@@ -688,20 +673,12 @@ __global__ __launch_bounds__(256) void k_scan_emit(EmitArgs a) {
                 else hi = mid - 1;
             }
             const int4 q = s_rect[lo];
-            const int w = q.z & 0xFFFF;
             const uint32_t k = j - s_start[lo];
-            const uint32_t ky = (uint32_t)(((float)k + 0.5f) / (float)w);  // exact: k < 2^20, margin 0.5/width
-            const uint32_t kx = k - ky * (uint32_t)w;
+            const uint32_t ky = (uint32_t)(((float)k + 0.5f) / (float)q.z);  // exact: k < 2^20, margin 0.5/width
+            const uint32_t kx = k - ky * (uint32_t)q.z;
             if (base + j >= a.cap) break;  // speculative capacity exceeded (gs_views_check reports it)
-            const int tx = q.x + (int)kx, ty = q.y + (int)ky;
-            a.tile_key[base + j] = (uint32_t)(ty * a.gx + tx);
-            uint32_t gv = s_gauss[lo];
-            if (a.qmask_words) {
-                const uint2 qw = s_qw[lo];
-                gv |= (q.z >> 16 ? quad_mask(s_qc[lo], (float)(16 * tx), (float)(16 * ty))
-                                 : band_inst_mask((uint64_t)qw.y << 32 | qw.x, (int)kx, (int)ky)) << kIdBits;
-            }
-            a.slot_gauss[base + j] = gv;
+            a.tile_key[base + j] = (uint32_t)((q.y + (int)ky) * a.gx + q.x + (int)kx);
+            a.slot_gauss[base + j] = s_gauss[lo];
             if (a.rec_flags32) a.rec_flags32[base + j] = 0u;  // slot's four quadrant flags (no memset launch)
         }
         base += total;
@@ -734,8 +711,6 @@ __global__ __launch_bounds__(256) void k_scan_emit_x(EmitArgs a) {
     __shared__ PV s_pair[kEmitBatch];
     __shared__ uint16_t s_own[kEmitBatch];  // the batch's owners (+1): marks at the entries' starts, prefix max
     __shared__ uint32_t s_carry;
-    __shared__ QuadCull s_qc[256];  // (rects past band_rect_fits: the bound itself)
-    __shared__ uint2 s_qw[256];     // the rect's band word (qmask_words)
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     if (blockIdx.x == 0)
         for (int t = tid; t < a.ntiles; t += 256) a.tile_count[t] = 0u;  // (the row pass counts into it)
@@ -754,26 +729,11 @@ __global__ __launch_bounds__(256) void k_scan_emit_x(EmitArgs a) {
     for (int i = tid; i < 4 * kXDigits; i += 256) (&cnt[0][0])[i] = 0;
     __syncthreads();
     const uint32_t r_block = blockIdx.x * (uint32_t)kScanTile;
-    // every round's inputs up front (as k_scan_emit): (rect, Gaussian), the mask word or, for a rect too
-    // large for one, the Splat's 2D mean + conic
-    uint2 grs[kScanIPT];
-    uint64_t qws[kScanIPT];
-    float2 xys[kScanIPT];
-    float4 cos_[kScanIPT];
+    uint2 grs[kScanIPT];  // every round's (rect, Gaussian) up front (as k_scan_emit)
 #pragma unroll
     for (int it = 0; it < kScanIPT; ++it) {
         const uint32_t r = r_block + it * 256 + tid;
         grs[it] = r < (uint32_t)a.P ? a.order[r] : make_uint2(0u, 0u);
-    }
-#pragma unroll
-    for (int it = 0; it < kScanIPT; ++it) {
-        const uint2 gr = grs[it];
-        const bool c = rect_count(gr.x, 1) != 0u;
-        const bool fits = band_rect_fits((int)((gr.x >> 16) & 0xFFu) - (int)(gr.x & 0xFFu),
-                                         (int)(gr.x >> 24) - (int)((gr.x >> 8) & 0xFFu));
-        qws[it] = a.qmask_words && c && fits ? a.qmask_words[gr.y] : 0ull;
-        xys[it] = a.qmask_words && c && !fits ? a.splat[gr.y].xy : make_float2(0.f, 0.f);
-        cos_[it] = a.qmask_words && c && !fits ? a.splat[gr.y].co : make_float4(0.f, 0.f, 0.f, 0.f);
     }
 #pragma unroll  // (the prefetched arrays stay in registers)
     for (int it = 0; it < kScanIPT; ++it) {
@@ -784,13 +744,8 @@ __global__ __launch_bounds__(256) void k_scan_emit_x(EmitArgs a) {
         const uint32_t off = block_exclusive_scan(c, lds4, total);
         if (c) {
             a.first_slot[g] = base + off;
-            const int rw = (int)((gr.x >> 16) & 0xFFu) - (int)(gr.x & 0xFFu);
-            const int rh = (int)(gr.x >> 24) - (int)((gr.x >> 8) & 0xFFu);
-            const bool big = a.qmask_words && !band_rect_fits(rw, rh);
-            if (big)
-                s_qc[tid] = quad_cull_setup(xys[it].x, xys[it].y, cos_[it].x, cos_[it].y, cos_[it].z, cos_[it].w);
-            s_rect[tid] = make_int4((int)(gr.x & 0xFFu), (int)((gr.x >> 8) & 0xFFu), rw | (big ? 1 << 16 : 0), 0);
-            s_qw[tid] = make_uint2((uint32_t)qws[it], (uint32_t)(qws[it] >> 32));
+            s_rect[tid] = make_int4((int)(gr.x & 0xFFu), (int)((gr.x >> 8) & 0xFFu),
+                                    (int)((gr.x >> 16) & 0xFFu) - (int)(gr.x & 0xFFu), 0);
         }
         s_start[tid] = off;
         s_gauss[tid] = g;
@@ -840,21 +795,13 @@ __global__ __launch_bounds__(256) void k_scan_emit_x(EmitArgs a) {
                 const uint32_t j = j0 + (valid ? jj : 0u);
                 const int lo = (int)s_own[valid ? jj : 0u] - 1;
                 const int4 q = s_rect[lo];
-                const int qw = q.z & 0xFFFF;
                 const uint32_t k = j - s_start[lo];
-                const uint32_t ky = (uint32_t)(((float)k + 0.5f) / (float)qw);  // exact: k < 2^20
-                const uint32_t kx = k - ky * (uint32_t)qw;
+                const uint32_t ky = (uint32_t)(((float)k + 0.5f) / (float)q.z);  // exact: k < 2^20
+                const uint32_t kx = k - ky * (uint32_t)q.z;
                 const uint32_t x = (uint32_t)q.x + kx, y = (uint32_t)q.y + ky;
                 kk[e] = y << kXBits | x;
-                uint32_t gv = s_gauss[lo];
-                if (a.qmask_words) {
-                    const uint2 qw = s_qw[lo];
-                    gv |= (q.z >> 16 ? quad_mask(s_qc[lo], (float)(16 * x), (float)(16 * y))
-                                     : band_inst_mask((uint64_t)qw.y << 32 | qw.x, (int)kx, (int)ky))
-                          << kIdBits;
-                }
-                if constexpr (IDS) pv[e] = gv;
-                else pv[e] = make_uint2(gv, base + j);
+                if constexpr (IDS) pv[e] = s_gauss[lo];
+                else pv[e] = make_uint2(s_gauss[lo], base + j);
                 if (valid && a.rec_flags32 && base + j < a.cap) a.rec_flags32[base + j] = 0u;  // (slot order: coalesced)
                 const uint32_t d = valid ? x : 0u;
                 const uint64_t peers = match_digit<kXBits>(d, vm);

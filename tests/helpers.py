@@ -20,8 +20,6 @@ import numpy as np
 import torch
 
 RTOL = 1e-4
-# the per-tile lists' Gaussian ids carry the emission's quadrant masks in bits 28.. (gs_qmask.h)
-ID_MASK = np.uint32((1 << 28) - 1)
 GRAD_NAMES = ["dL_dmeans2D", "dL_dcolors", "dL_dopacity", "dL_dmeans3D", "dL_dcov3D", "dL_dsh", "dL_dscales",
               "dL_drotations"]
 
@@ -139,8 +137,7 @@ def run_gpu(settings, dL_dpix=None, means3D=None, opacities=None, shs=None, colo
         out["n_contrib"] = view(img, "image", "n_contrib", np.uint32, W * H)
         out["ranges"] = view(img, "image", "ranges", np.uint32, 2 * tiles)
         # per-tile lists: (Gaussian, slot) pairs; the Gaussian ids are the reference's point_list
-        out["point_list"] = (view(binning, "binning", "point_pairs", np.uint32, 2 * K)[0::2] & ID_MASK
-                             if K else np.zeros(0, np.uint32))
+        out["point_list"] = view(binning, "binning", "point_pairs", np.uint32, 2 * K)[0::2] if K else np.zeros(0, np.uint32)
     if dL_dpix is not None:
         g = torch.as_tensor(np.asarray(dL_dpix, np.float32)).to(dev)
         dconic = torch.empty((P, 3), dtype=torch.float32, device=dev) if conic_grad else None
@@ -187,7 +184,7 @@ def views_forward_dict(batch, v, color, depth, radii):
     out["final_T"] = view("image", "final_T", np.float32, W * H)
     out["n_contrib"] = view("image", "n_contrib", np.uint32, W * H)
     out["ranges"] = view("image", "ranges", np.uint32, 2 * tiles)
-    out["point_list"] = view("binning", "point_pairs", np.uint32, 2 * K)[0::2] & ID_MASK if K else np.zeros(0, np.uint32)
+    out["point_list"] = view("binning", "point_pairs", np.uint32, 2 * K)[0::2] if K else np.zeros(0, np.uint32)
     return out
 
 

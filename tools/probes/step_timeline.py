@@ -1,7 +1,8 @@
 import csv, sys
-rows=list(csv.DictReader(open(sys.argv[1])))
+import gzip
+rows=list(csv.DictReader((gzip.open(sys.argv[1], 'rt') if sys.argv[1].endswith('.gz') else open(sys.argv[1]))))
 rows.sort(key=lambda r:int(r['Start_Timestamp']))
-gb=[i for i,r in enumerate(rows) if r['Kernel_Name'].startswith('k_gauss_bwd_live')]
+gb=[i for i,r in enumerate(rows) if 'k_gauss_bwd_live' in r['Kernel_Name']]
 a,b=gb[-6],gb[-5]
 t0=int(rows[a]['Start_Timestamp'])
 busy=[]
