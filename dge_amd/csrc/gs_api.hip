@@ -130,6 +130,16 @@ bool views_issue_by_view() {
     return on;
 }
 
+// DGE_AMD_VIEWS_PRE=1: a batch's views preprocessed in one pass (k_preprocess_views) when they share their
+// inputs (A/B; round 3 measured it no faster with the view-by-view issue order)
+bool views_shared_preprocess() {
+    static const bool on = [] {
+        const char* e = getenv("DGE_AMD_VIEWS_PRE");
+        return e && !strcmp(e, "1");
+    }();
+    return on;
+}
+
 // Pinned read-back slot of one forward's preprocess counters + its event.  A
 // pool per device: several forwards may be between begin and end at once
 // (gs_rasterize_forward_begin / _end), each holding its own slot.
@@ -1167,9 +1177,11 @@ struct gs_views {
     long long K[GS_MAX_VIEWS] = {};      // instance count, -1 until the host knows it
     hipEvent_t ev[GS_MAX_VIEWS] = {};    // the end of each view's work (forward, or per-Gaussian backward pass)
     hipEvent_t fork = nullptr;           // the caller's stream, before the views' work
+    hipEvent_t pre = nullptr;            // the end of the views' shared preprocess (k_preprocess_views)
     ~gs_views() {
         for (int v = 0; v < GS_MAX_VIEWS; ++v) event_pool().put(ev[v]);
         event_pool().put(fork);
+        event_pool().put(pre);
     }
 };
 
@@ -1253,7 +1265,42 @@ int gs_views_forward(int n, const gs_settings* const* s, const gs_params* const*
         // view's preprocess is enqueued before any view's depth sort, so the views' chains start together
         // (view by view, the last view's preprocess started ~200 us of host issue after the first's and
         // the forward phase ended with that view)
-        for (int v = 0; v < n; ++v) {
+        // one preprocess for every view (k_preprocess_views: the scene read once) when the views share
+        // their inputs, on the first view's stream, which the others then wait for
+        bool shared = views_shared_preprocess() && !views_issue_by_view() && n >= 2;
+        for (int v = 0; v < n && shared; ++v) shared = h->f[v].gp.P > 0 && h->f[v].s.debug == 0;
+        if (shared) {
+            hipStream_t s0 = (hipStream_t)streams[0];
+            const PreprocessArgs* pas[GS_MAX_VIEWS];
+            for (int v = 0; v < n; ++v) {
+                rc = bin_prepare_in(h->f[v], 1, base + off_geom[v], base + off_img[v], s0);
+                if (rc) return rc;
+                pas[v] = &h->f[v].pa;
+            }
+            shared = preprocess_views_ok(pas, n);
+            if (shared) {
+                const bool debug = false;
+                hipStream_t stream = s0;  // (GS_LAUNCHED)
+                GS_SKIP("pre") { StageScope sc(ST_PREPROCESS, s0); launch_preprocess_views(pas, n, s0); }
+                GS_LAUNCHED("preprocess (views)");
+                if (!h->pre && !(h->pre = event_pool().get())) return set_error(GS_ERR_HIP, "could not create an event");
+                GS_HIP(hipEventRecord(h->pre, s0));
+                for (int v = 1; v < n; ++v)
+                    if ((hipStream_t)streams[v] != s0) GS_HIP(hipStreamWaitEvent((hipStream_t)streams[v], h->pre, 0));
+            } else {  // (the buffers are prepared on the first stream: the others wait for it)
+                if (!h->pre && !(h->pre = event_pool().get())) return set_error(GS_ERR_HIP, "could not create an event");
+                GS_HIP(hipEventRecord(h->pre, s0));
+                for (int v = 0; v < n; ++v) {
+                    hipStream_t stream = (hipStream_t)streams[v];
+                    const bool debug = h->f[v].s.debug != 0;
+                    if (stream != s0) GS_HIP(hipStreamWaitEvent(stream, h->pre, 0));
+                    GS_SKIP("pre") { StageScope sc(ST_PREPROCESS, stream); launch_preprocess(h->f[v].pa, stream); }
+                    GS_LAUNCHED("preprocess");
+                }
+                shared = true;  // (every view's preprocess is enqueued)
+            }
+        }
+        for (int v = 0; v < n && !shared; ++v) {
             FwdState& f = h->f[v];
             if (f.gp.P == 0) continue;
             hipStream_t stream = (hipStream_t)streams[v];
