@@ -11,3 +11,5 @@ timeout -k 10 300 python tools/warn_trace.py --steps 5 --warmup 3 --no-cpu-basel
 grep -A30 "warn-trace" $O/warn.err | head -45
 DGE_AMD_BENCH_BACKEND=gloo timeout -k 10 300 python bench.py --gpus 2 --steps 10 --warmup 3 --no-side-legs --no-cpu-baseline > $O/bench_gloo2.json 2> $O/bench_gloo2.err || { tail -20 $O/bench_gloo2.err; exit 1; }
 python -c "import json; d=json.loads(open('$O/bench_gloo2.json').read().strip().splitlines()[-1]); print(d['value'], d['n_gpus'], d.get('distributed'))"
+timeout -k 10 300 python tools/probes/dge_loop_profile.py > $O/dge_loop_profile.txt 2>&1 || { tail -20 $O/dge_loop_profile.txt; exit 1; }
+head -60 $O/dge_loop_profile.txt | cut -c1-150
