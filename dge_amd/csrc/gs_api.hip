@@ -130,6 +130,16 @@ bool views_issue_by_view() {
     return on;
 }
 
+// DGE_AMD_VIEWS_FWD=streams: each view's blend launched on its own stream (round 3) instead of one launch
+// for the batch (A/B)
+bool views_batch_forward() {
+    static const bool on = [] {
+        const char* e = getenv("DGE_AMD_VIEWS_FWD");
+        return !(e && !strcmp(e, "streams"));
+    }();
+    return on;
+}
+
 // DGE_AMD_VIEWS_PRE=1: a batch's views preprocessed in one pass (k_preprocess_views) when they share their
 // inputs (A/B; round 3 measured it no faster with the view-by-view issue order)
 bool views_shared_preprocess() {
@@ -635,10 +645,9 @@ int bin_end(FwdState& f, gs_alloc_fn alloc, void* ctx, hipStream_t stream, void*
 }
 
 // The blend (k_render_fwd) over a finished binning laid out for K_layout instances.
-int render_launch(FwdState& f, void* bin, uint32_t K_layout, int order_ready, float* out_color, float* out_depth,
-                  hipStream_t stream) {
+RenderArgs render_args(FwdState& f, void* bin, uint32_t K_layout, int order_ready, float* out_color,
+                       float* out_depth) {
     const Grid& g = f.g;
-    const bool debug = f.s.debug != 0;
     const GeomLayout gl = geom_layout(f.gp.P);
     const ImgLayout il = img_layout(g.W, g.H);
     const BinLayout bl = bin_layout((int)K_layout, g.tiles, !f.gp.forward_only);
@@ -667,6 +676,13 @@ int render_launch(FwdState& f, void* bin, uint32_t K_layout, int order_ready, fl
     ra.out_depth = out_depth;
     ra.touched = at<uint8_t>(geom, gl.touched);
     ra.diag = diag_buffer(0, kDiagWords * (size_t)g.tiles * 4);
+    return ra;
+}
+
+int render_launch(FwdState& f, void* bin, uint32_t K_layout, int order_ready, float* out_color, float* out_depth,
+                  hipStream_t stream) {
+    const bool debug = f.s.debug != 0;
+    const RenderArgs ra = render_args(f, bin, K_layout, order_ready, out_color, out_depth);
     GS_SKIP("fwd") { StageScope sc(ST_RENDER_FWD, stream); launch_render_forward(ra, stream); }
     GS_LAUNCHED("render");
     return GS_OK;
@@ -1321,7 +1337,13 @@ int gs_views_forward(int n, const gs_settings* const* s, const gs_params* const*
             if (rc) return rc;
         }
         // second halves: a speculated view's binning runs on the device count, capped at its capacity;
-        // the others wait for their count here (the reference's sync, rasterizer_impl.cu:236-239)
+        // the others wait for their count here (the reference's sync, rasterizer_impl.cu:236-239).  The
+        // blends: one batched launch (views_batch_forward) when every view renders (same kind, <= 4)
+        bool batch_fwd = views_batch_forward() && n >= 2 && n <= kRenderBatch;
+        for (int v = 0; v < n && batch_fwd; ++v)
+            batch_fwd = h->f[v].gp.P > 0 && h->f[v].s.debug == 0 && h->f[v].gp.forward_only == h->f[0].gp.forward_only;
+        RenderArgs ras[kRenderBatch];
+        int nras = 0;
         for (int v = 0; v < n; ++v) {
             FwdState& f = h->f[v];
             hipStream_t stream = (hipStream_t)streams[v];
@@ -1332,24 +1354,52 @@ int gs_views_forward(int n, const gs_settings* const* s, const gs_params* const*
                 h->K[v] = 0;
                 continue;
             }
+            uint32_t layout = 0;
+            int order_ready = 0;
             if (h->spec[v]) {
                 h->bin[v] = base + off_bin[v];
                 const uint32_t* counters = at<uint32_t>(f.img, img_layout(g.W, g.H).counters);
                 rc = bin_emit(f, h->bin[v], h->layout[v], counters, stream);
                 if (rc) return rc;
-                rc = render_launch(f, h->bin[v], h->layout[v], tile_sort_writes_ranges(g.tiles) || f.ea.xhist ? 1 : 0,
-                                   out_color[v], out_depth[v], stream);
+                layout = h->layout[v];
+                order_ready = tile_sort_writes_ranges(g.tiles) || f.ea.xhist ? 1 : 0;
             } else {
                 int K = 0;
                 rc = bin_end(f, alloc, alloc_ctx, stream, &h->bin[v], &K, 16 + v);
                 if (rc) return rc;
                 h->K[v] = K;
                 h->layout[v] = (uint32_t)K;
-                rc = render_launch(f, h->bin[v], (uint32_t)K,
-                                   K > 0 && (tile_sort_writes_ranges(g.tiles) || f.ea.xhist) ? 1 : 0, out_color[v],
-                                   out_depth[v], stream);
+                layout = (uint32_t)K;
+                order_ready = K > 0 && (tile_sort_writes_ranges(g.tiles) || f.ea.xhist) ? 1 : 0;
             }
-            if (rc) return rc;
+            if (batch_fwd) {
+                ras[nras++] = render_args(f, h->bin[v], layout, order_ready, out_color[v], out_depth[v]);
+            } else {
+                rc = render_launch(f, h->bin[v], layout, order_ready, out_color[v], out_depth[v], stream);
+                if (rc) return rc;
+            }
+        }
+        if (nras) {
+            // the views' blends as ONE launch on the first view's stream, once every view's binning is done
+            // (their heaviest quadrants' tails then overlap in one grid instead of three contending ones)
+            hipStream_t s0 = (hipStream_t)streams[0];
+            for (int v = 1; v < n; ++v) {
+                hipStream_t sv = (hipStream_t)streams[v];
+                if (sv == s0) continue;
+                if (!h->ev[v] && !(h->ev[v] = event_pool().get())) return set_error(GS_ERR_HIP, "could not create an event");
+                GS_HIP(hipEventRecord(h->ev[v], sv));
+                GS_HIP(hipStreamWaitEvent(s0, h->ev[v], 0));
+            }
+            {
+                const bool debug = false;
+                hipStream_t stream = s0;  // (GS_LAUNCHED)
+                GS_SKIP("fwd") { StageScope sc(ST_RENDER_FWD, s0); launch_render_forward_views(ras, nras, s0); }
+                GS_LAUNCHED("render (views)");
+            }
+            if (!h->pre && !(h->pre = event_pool().get())) return set_error(GS_ERR_HIP, "could not create an event");
+            GS_HIP(hipEventRecord(h->pre, s0));
+            for (int v = 1; v < n; ++v)
+                if ((hipStream_t)streams[v] != s0) GS_HIP(hipStreamWaitEvent((hipStream_t)streams[v], h->pre, 0));
         }
         rc = join_into(h.get(), join, streams);
         if (rc) return rc;

@@ -371,6 +371,14 @@ struct RenderArgs {
     const float* colors = nullptr;  // forward-only: blend these [P,3] colours instead of the Splats' (recolor)
 };
 void launch_render_forward(const RenderArgs& a, hipStream_t s);
+// n views' blends in one launch (the views' tiles of one rank interleaved, every view's longest lists
+// first); every view must be a training (bwd) render or every one forward-only
+constexpr int kRenderBatch = 4;
+struct RenderBatch {
+    RenderArgs v[kRenderBatch];
+    int n;
+};
+void launch_render_forward_views(const RenderArgs* v, int n, hipStream_t s);
 
 struct ApplyWeightsArgs {
     int W, H, gx, gy, C;

@@ -241,12 +241,16 @@ __device__ __forceinline__ void emit_items(const RenderArgs& a, int tile, int qu
 // BWD: the backward's bookkeeping (checkpoints, blended bits, touched bytes, the replay's work list);
 // a forward no backward follows (gs_params.forward_only) runs without it
 template <bool BWD>
-__global__ __launch_bounds__(64, 3) void k_render_fwd(RenderArgs a) {
+__global__ __launch_bounds__(64, 3) void k_render_fwd(RenderBatch rb) {
     // XCD-aware: blocks b, b+8, b+16, b+24 (one XCD under the round-robin dealing) take the four
     // quadrants of one tile, so the tile's list and its Splat gathers are fetched into one L2;
-    // tiles in k_tile_order's order, longest list first
+    // tiles in k_tile_order's order, longest list first.  A batch of views (one launch for a step's
+    // views, gs_views_forward): the views' tiles of one rank follow each other, so every view's
+    // longest lists start first
     const int x8 = blockIdx.x & 7, j8 = blockIdx.x >> 3;
-    const int quad = j8 & 3, rank = (j8 >> 2) * 8 + x8;
+    const int quad = j8 & 3, r2 = j8 >> 2;
+    const int view = r2 % rb.n, rank = (r2 / rb.n) * 8 + x8;
+    const RenderArgs& a = rb.v[view];
     if (rank >= a.gx * a.gy) return;
     const int tile = (int)a.tile_order[rank];
     const int qidx = 4 * tile + quad;
@@ -555,15 +559,27 @@ __global__ __launch_bounds__(64, 3) void k_render_fwd(RenderArgs a) {
     }
 }
 
-void launch_render_forward(const RenderArgs& a, hipStream_t s) {
-    const int tiles = a.gx * a.gy;
-    if (tiles <= 0) return;
-    if (!a.order_ready) hipLaunchKernelGGL(k_tile_order, dim3(1), dim3(1024), 0, s, a.ranges, tiles, a.tile_order);
-    if (a.bwd)
-        hipLaunchKernelGGL(k_render_fwd<true>, dim3(div_up(tiles, 8) * 32), dim3(64), 0, s, a);
+void launch_render_forward_views(const RenderArgs* v, int n, hipStream_t s) {
+    RenderBatch rb;
+    rb.n = 0;
+    int tiles = 0;
+    for (int i = 0; i < n; ++i) {
+        const int t = v[i].gx * v[i].gy;
+        if (t <= 0) continue;
+        if (!v[i].order_ready)
+            hipLaunchKernelGGL(k_tile_order, dim3(1), dim3(1024), 0, s, v[i].ranges, t, v[i].tile_order);
+        rb.v[rb.n++] = v[i];
+        tiles = t > tiles ? t : tiles;
+    }
+    if (rb.n == 0) return;
+    const dim3 grid(div_up(tiles, 8) * 32 * rb.n);
+    if (rb.v[0].bwd)
+        hipLaunchKernelGGL(k_render_fwd<true>, grid, dim3(64), 0, s, rb);
     else
-        hipLaunchKernelGGL(k_render_fwd<false>, dim3(div_up(tiles, 8) * 32), dim3(64), 0, s, a);
+        hipLaunchKernelGGL(k_render_fwd<false>, grid, dim3(64), 0, s, rb);
 }
+
+void launch_render_forward(const RenderArgs& a, hipStream_t s) { launch_render_forward_views(&a, 1, s); }
 
 // =====================================================================
 // apply_weights: same traversal, per blended pair add image weights

@@ -1,0 +1,10 @@
+#!/bin/bash
+# round 4, GPU call j: the batched blend launch (one k_render_fwd for a step's views): the GPU suite, A/B
+# against per-view launches on the views' streams, and with the shared preprocess on top
+cd "$GRAFT_REPO_ROOT" 2>/dev/null || cd /root/repo
+O=gpurun_out/r4j
+mkdir -p $O
+timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu -p no:cacheprovider tests > $O/pytest_gpu.log 2>&1 || { tail -60 $O/pytest_gpu.log; exit 1; }
+tail -2 $O/pytest_gpu.log
+VAR=DGE_AMD_VIEWS_FWD VALS="batch streams" NOTESTS=1 ROUNDS=3 bash tools/gpu_env_ab.sh || exit 1
+VAR=DGE_AMD_VIEWS_PRE VALS="1 0" NOTESTS=1 ROUNDS=2 bash tools/gpu_env_ab.sh || exit 1
