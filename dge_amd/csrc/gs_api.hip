@@ -761,11 +761,9 @@ int bin_forward(const gs_settings* s, const Grid& g, const gs_params& gp, int* r
 // records), then the per-Gaussian pass over those records, whose accumulated writes wait for
 // writes_after.  R: the binning layout's instance count; slot_cap: a speculative forward's capacity
 // (its slots end there), else ~0.
-int replay_view(const gs_settings* s, const gs_params* gp, int R, const void* geom, const void* binning,
-                const void* img, const float* dL_dpix, hipStream_t stream) {
+RenderBwdArgs replay_args(const gs_settings* s, const gs_params* gp, int R, const void* geom, const void* binning,
+                          const void* img, const float* dL_dpix) {
     const int P = gp->P;
-    if (P == 0 || R <= 0) return GS_OK;
-    const bool debug = s->debug != 0;
     const Grid g = make_grid(s);
     const GeomLayout gl = geom_layout(P);
     const ImgLayout il = img_layout(g.W, g.H);
@@ -789,6 +787,14 @@ int replay_view(const gs_settings* s, const gs_params* gp, int R, const void* ge
     rb.records = at<float4>(const_cast<void*>(binning), bl.records);
     rb.rec_flags = at<uint8_t>(const_cast<void*>(binning), bl.rec_flags);
     rb.diag = diag_buffer(1, kDiagWords * 4 * bl.nslots);
+    return rb;
+}
+
+int replay_view(const gs_settings* s, const gs_params* gp, int R, const void* geom, const void* binning,
+                const void* img, const float* dL_dpix, hipStream_t stream) {
+    if (gp->P == 0 || R <= 0) return GS_OK;
+    const bool debug = s->debug != 0;
+    const RenderBwdArgs rb = replay_args(s, gp, R, geom, binning, img, dL_dpix);
     GS_SKIP("rbwd") { StageScope sc(ST_RENDER_BWD, stream); launch_render_backward(rb, stream); }
     GS_LAUNCHED("render backward");
     return GS_OK;
@@ -1594,7 +1600,19 @@ int gs_views_backward(gs_views* h, const float* const* dL_dpix, const gs_grads* 
             hipStream_t s0 = (hipStream_t)streams[0];
             const bool debug = h->f[0].s.debug != 0;
             hipStream_t stream = s0;  // (GS_LAUNCHED)
-            for (int v = 0; v < h->n; ++v) {
+            // the replays: one batched launch on the first stream (views_forward_mode 2), or one per stream
+            bool batch = views_forward_mode() == 2 && h->n <= kRenderBatch && !debug;
+            for (int v = 0; v < h->n && batch; ++v) batch = h->f[v].gp.P > 0 && h->layout[v] > 0;
+            if (batch) {
+                RenderBwdArgs rbs[kRenderBatch];
+                for (int v = 0; v < h->n; ++v) {
+                    FwdState& f = h->f[v];
+                    rbs[v] = replay_args(&f.s, &f.gp, (int)h->layout[v], f.geom, h->bin[v], f.img, dL_dpix[v]);
+                }
+                GS_SKIP("rbwd") { StageScope sc(ST_RENDER_BWD, s0); launch_render_backward_views(rbs, h->n, s0); }
+                GS_LAUNCHED("render backward (views)");
+            }
+            for (int v = 0; v < h->n && !batch; ++v) {
                 FwdState& f = h->f[v];
                 hipStream_t sv = (hipStream_t)streams[v];
                 int rc = replay_view(&f.s, &f.gp, (int)h->layout[v], f.geom, h->bin[v], f.img, dL_dpix[v], sv);

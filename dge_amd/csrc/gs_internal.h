@@ -422,6 +422,12 @@ struct RenderBwdArgs {
     uint64_t* diag;   // optional [item_cap][kDiagWords], by queue position (see diag_buffer)
 };
 void launch_render_backward(const RenderBwdArgs& a, hipStream_t s);
+// n views' replays in one launch (their items interleaved, every view's heaviest first)
+struct RenderBwdBatch {
+    RenderBwdArgs v[kRenderBatch];
+    int n;
+};
+void launch_render_backward_views(const RenderBwdArgs* v, int n, hipStream_t s);
 
 struct GaussBwdArgs {
     int P, D, M, W, H, gx, gy;

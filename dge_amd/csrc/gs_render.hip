@@ -766,7 +766,7 @@ static_assert(kSegLen % kBwdHalf == 0, "whole staging units per segment");
 // sums are reduce-scattered across the wave (quad_reduce).  Each kept entry gets
 // one record at 4*slot + quadrant (slot: the binning slot, so k_gauss_bwd reads
 // a Gaussian's records contiguously) and a flag.
-__global__ __launch_bounds__(64, GS_BWD_WAVES) void k_render_bwd(RenderBwdArgs a) {
+__global__ __launch_bounds__(64, GS_BWD_WAVES) void k_render_bwd(RenderBwdBatch rbb) {
     // kept entries of a half-segment, compacted back to front, + a group of padding
     // (one array per field: four consecutive entries' field is one 16-B read, see bwd_quad)
     __shared__ __attribute__((aligned(16))) float s_x[kBwdHalf + kBwdGroup], s_y[kBwdHalf + kBwdGroup];
@@ -780,13 +780,16 @@ __global__ __launch_bounds__(64, GS_BWD_WAVES) void k_render_bwd(RenderBwdArgs a
     // block -> work item (quadrant, segment) of the forward's list, heaviest class first; blocks past
     // the list's end exit (they dispatch after every real item; see launch_render_backward for the
     // grid).  (A persistent-wave work queue measured slower than the hardware dispatcher here.)
+    // (a batch of views in one launch: block b takes item b / n of view b % n — the views' heaviest
+    // items first, interleaved)
+    const RenderBwdArgs& a = rbb.v[blockIdx.x % rbb.n];
     uint32_t n_cls[kItemClasses], n_items = 0;
 #pragma unroll
     for (int c = 0; c < kItemClasses; ++c) {
         n_cls[c] = a.bwd_count[item_count_at(c)];
         n_items += n_cls[c];
     }
-    const uint32_t qi = blockIdx.x;
+    const uint32_t qi = blockIdx.x / rbb.n;
     if (qi >= n_items) return;
     uint32_t cls = 0, idx = qi;  // class regions in order: heaviest items first
 #pragma unroll
@@ -956,10 +959,19 @@ __global__ __launch_bounds__(64, GS_BWD_WAVES) void k_render_bwd(RenderBwdArgs a
 
 // One workgroup per possible item (the bound, 4 x checkpoint slots, is ~7x the c2 count): the surplus
 // workgroups exit at once and cost nothing measurable (render_bwd 104 us either way).
-void launch_render_backward(const RenderBwdArgs& a, hipStream_t s) {
-    const int tiles = a.gx * a.gy;
-    if (tiles <= 0 || a.item_cap == 0) return;
-    hipLaunchKernelGGL(k_render_bwd, dim3(a.item_cap), dim3(64), 0, s, a);
+void launch_render_backward_views(const RenderBwdArgs* v, int n, hipStream_t s) {
+    RenderBwdBatch rbb;
+    rbb.n = 0;
+    uint32_t cap = 0;
+    for (int i = 0; i < n; ++i) {
+        if (v[i].gx * v[i].gy <= 0 || v[i].item_cap == 0) continue;
+        rbb.v[rbb.n++] = v[i];
+        cap = v[i].item_cap > cap ? v[i].item_cap : cap;
+    }
+    if (rbb.n == 0) return;
+    hipLaunchKernelGGL(k_render_bwd, dim3(cap * (uint32_t)rbb.n), dim3(64), 0, s, rbb);
 }
+
+void launch_render_backward(const RenderBwdArgs& a, hipStream_t s) { launch_render_backward_views(&a, 1, s); }
 
 }  // namespace gs
