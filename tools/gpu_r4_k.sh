@@ -2,7 +2,7 @@
 # round 4, GPU call k: the "half" batched mode (one preprocess, depth sort and scan for the views, per-view second halves)
 # against per-view launches on the views' streams, and with the shared preprocess on top
 cd "$GRAFT_REPO_ROOT" 2>/dev/null || cd /root/repo
-O=gpurun_out/r4j
+O=gpurun_out/r4k
 mkdir -p $O
 timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu -p no:cacheprovider tests > $O/pytest_gpu.log 2>&1 || { tail -60 $O/pytest_gpu.log; exit 1; }
 tail -2 $O/pytest_gpu.log
