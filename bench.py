@@ -354,7 +354,8 @@ def main():
     pmc_path = os.path.join(HERE, "profiles", "pmc_traffic.json")
     if os.path.exists(pmc_path):
         try:
-            pmc = json.load(open(pmc_path))
+            with open(pmc_path) as fh:
+                pmc = json.load(fh)
         except Exception:
             pmc = {}
     for name in blend:  # both blend kernels, timed live in the one-stream roofline leg

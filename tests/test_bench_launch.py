@@ -34,7 +34,7 @@ def test_spawn_ranks_environment(monkeypatch, tmp_path):
     monkeypatch.setenv("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     rc = bench.spawn_ranks(SimpleNamespace(gpus=3), argv=[], child_cmd=[sys.executable, "-c", code])
     assert rc == 0
-    envs = [json.load(open(tmp_path / f"rank{r}")) for r in range(3)]
+    envs = [json.loads((tmp_path / f"rank{r}").read_text()) for r in range(3)]
     assert [e["RANK"] for e in envs] == ["0", "1", "2"] and [e["LOCAL_RANK"] for e in envs] == ["0", "1", "2"]
     assert {e["WORLD_SIZE"] for e in envs} == {"3"} and {e["MASTER_ADDR"] for e in envs} == {"127.0.0.1"}
     assert len({e["MASTER_PORT"] for e in envs}) == 1 and {e["DGE_AMD_BENCH_SPAWNED"] for e in envs} == {"1"}
