@@ -535,17 +535,24 @@ def side_legs(args, scene, cams, seeds, bg, pipe, bucket, step, dev):
     V = len(cams)
     prev = os.environ.get("DGE_AMD_FUSED")
     os.environ["DGE_AMD_FUSED"] = "0"
+
+    def unchanged():
+        # DGE renders its views one after another on the caller's stream (DGE.py:179-222).  (On the views'
+        # streams each view's torch getter nodes would run on its own stream while feeding the one
+        # AccumulateGrad node per parameter: autograd's stream-mismatch warning, round 3's stderr.)
+        run_views(args, cams, scene, pipe, bg, seeds, bucket, streams=1)
+
     try:
         for _ in range(3):
-            step()
-        dt = _time(step, steps)
+            unchanged()
+        dt = _time(unchanged, steps)
     finally:
         if prev is None:
             os.environ.pop("DGE_AMD_FUSED", None)
         else:
             os.environ["DGE_AMD_FUSED"] = prev
     legs["dge_unchanged_render"] = {"value": round(steps * V / dt, 3), "unit": "renders/s",
-                                    "path": "torch getters + cat + _RasterizeGaussians (fused path off)"}
+                                    "path": "torch getters + cat + _RasterizeGaussians (fused path off), one stream"}
 
     hl = synthetic_scene(args.points, sh_degree=args.sh_degree, seed=0, device=dev, opacity_mean=-2.0,
                          opacity_std=1.0).requires_grad_(True)

@@ -120,14 +120,6 @@ int depth_pass_bits() {
     return bits;
 }
 
-// DGE_AMD_SEG_CAP (tests; read per forward): the longest tile run k_tile_depth_sort orders in LDS
-// (shorter: more runs take the chunked global-memory passes of k_tile_depth_sort_long)
-uint32_t seg_cap() {
-    const char* e = getenv("DGE_AMD_SEG_CAP");
-    const long v = e ? atol(e) : 0;
-    return v >= 1 && v < kSegCap ? (uint32_t)v : (uint32_t)kSegCap;
-}
-
 // DGE_AMD_VIEWS_ISSUE=view: a batch's first halves enqueued view by view (round 3) instead of every
 // preprocess first (A/B)
 bool views_issue_by_view() {
@@ -466,10 +458,9 @@ int bin_after_preprocess_views(FwdState* const* fs, int n, size_t vstride, hipSt
     }
     const ViewBatch vb{n, vstride};
 
-    // depth order of the Gaussians (stable: ties keep index order); tile-first binning: none (the
-    // emission walks Gaussian order, each tile's run is depth-sorted after the tile sort)
+    // depth order of the Gaussians (stable: ties keep index order)
     int cur = 0;
-    if (!tile_first()) GS_SKIP("depth") { StageScope sc(ST_DEPTH_SORT, stream);
+    GS_SKIP("depth") { StageScope sc(ST_DEPTH_SORT, stream);
     cur = radix_sort_aux(at<uint32_t>(geom, gl.key0), at<uint32_t>(geom, gl.key1), at<uint2>(geom, gl.val0),
                          at<uint2>(geom, gl.val1), pa.rect, (uint32_t)P, depth_sort_bits(), depth_pass_bits(),
                          kDepthSortIPT, at<uint32_t>(geom, gl.sort_hist), at<uint32_t>(geom, gl.sort_totals),
@@ -482,8 +473,7 @@ int bin_after_preprocess_views(FwdState* const* fs, int n, size_t vstride, hipSt
         EmitArgs& ea = fv.ea;
         void* gv = fv.geom;
         ea.P = P; ea.gx = g.gx; ea.gy = g.gy;
-        ea.order = tile_first() ? nullptr : at<uint2>(gv, cur ? gl.val1 : gl.val0);
-        ea.rect = fv.pa.rect;
+        ea.order = at<uint2>(gv, cur ? gl.val1 : gl.val0);
         ea.rect_packed = fv.pa.rect_packed;
         ea.tiles_touched = fv.pa.tiles_touched;
         ea.splat = fv.pa.splat;
@@ -503,30 +493,6 @@ int bin_after_preprocess_views(FwdState* const* fs, int n, size_t vstride, hipSt
 int bin_after_preprocess(FwdState& f, hipStream_t stream) {
     FwdState* fs[1] = {&f};
     return bin_after_preprocess_views(fs, 1, 0, stream);
-}
-
-// Tile-first binning's last step: every tile's run (the binned lists, Gaussian order) sorted on the
-// depth key into the point lists (n views vstride bytes apart: grid.y).  order_ready: the binning wrote
-// the longest-first tile order, which then also orders this launch's workgroups.
-void tile_depth_sort(FwdState& f, void* bin, uint32_t K_layout, bool order_ready, int n, size_t vstride,
-                     hipStream_t stream) {
-    const Grid& g = f.g;
-    const ImgLayout il = img_layout(g.W, g.H);
-    const BinLayout bl = bin_layout((int)K_layout, g.tiles, !f.gp.forward_only);
-    SegSortArgs sa;
-    sa.ranges = at<uint2>(f.img, il.ranges);
-    sa.tile_order = order_ready ? at<uint32_t>(f.img, il.tile_order) : nullptr;
-    sa.ntiles = g.tiles;
-    sa.depth_key = f.pa.depth_key;
-    sa.in = at<uint2>(bin, bl.binned);
-    sa.out = at<uint2>(bin, bl.point_pairs);
-    sa.kscratch0 = at<uint32_t>(bin, bl.key0);
-    sa.kscratch1 = at<uint32_t>(bin, bl.key1);
-    sa.cap = seg_cap();
-    sa.ids_only = f.ids_only ? 1 : 0;
-    sa.vstride = vstride;
-    StageScope sc(ST_DEPTH_SORT, stream);
-    launch_tile_depth_sort(sa, stream, n);
 }
 
 // The single-pass binning (emission + tile sort with ranges) of n speculated views laid out alike, vstride
@@ -559,10 +525,6 @@ int bin_emit_views(FwdState* const* fs, int n, size_t vstride, void* const* bins
               at<uint32_t>(bins[0], bl.sort_hist), at<uint32_t>(bins[0], bl.sort_totals), bl.sort_blocks, stream,
               at<uint2>(f.img, il.ranges), at<uint32_t>(f.img, il.tile_order), g.tiles, n_dev, ViewBatch{n, vstride}); }
     GS_LAUNCHED("tile sort (views)");
-    if (tile_first()) {
-        tile_depth_sort(f, bins[0], K_layout, true, n, vstride, stream);
-        GS_LAUNCHED("tile depth sort (views)");
-    }
     return GS_OK;
 }
 
@@ -634,7 +596,7 @@ int read_counts(FwdState& f, Counts& c) {
     }
     c.K = K64;
     c.prefilter_fail = st->host[3] != 0;
-    c.wide = !tile_first() && K64 && kmax - ~kmin_not >= (1u << depth_sort_bits());
+    c.wide = K64 && kmax - ~kmin_not >= (1u << depth_sort_bits());
     staging_release(st, true);
     f.st = nullptr;
     note_count(f.gp.P, f.g.W, f.g.H, c.K, c.wide);
@@ -657,20 +619,16 @@ int bin_emit(FwdState& f, void* bin, uint32_t K_layout, const uint32_t* n_dev, h
     if (ea.xhist) {  // two-level binning (tile_sort_fused): column-ordered emission, row pass, ranges
         ea.ids_only = f.ids_only = !bwd && f.ids_ok;
         ea.tile_key = at<uint32_t>(bin, bl.key1);
-        ea.pairs_out = at<uint2>(bin, bl.binned == bl.pair1 ? bl.pair0 : bl.pair1);  // (not the row pass's output)
+        ea.pairs_out = at<uint2>(bin, bl.point_pairs == bl.pair1 ? bl.pair0 : bl.pair1);  // (not the row pass's output)
         ea.xtotals = at<uint32_t>(bin, bl.sort_totals);
         ea.tile_count = at<uint32_t>(bin, bl.tile_count);
         ea.ntiles = g.tiles;
         ea.rec_flags32 = bwd ? at<uint32_t>(bin, bl.rec_flags) : nullptr;
         { StageScope sc(ST_EMIT, stream); launch_emit_fused(ea, stream); }
         { StageScope sc(ST_TILE_SORT, stream);
-        launch_row_pass(ea, K_layout, at<uint2>(bin, bl.binned), at<uint32_t>(bin, bl.sort_hist), bl.sort_blocks,
+        launch_row_pass(ea, K_layout, at<uint2>(bin, bl.point_pairs), at<uint32_t>(bin, bl.sort_hist), bl.sort_blocks,
                         at<uint2>(img, il.ranges), at<uint32_t>(img, il.tile_order), stream, n_dev); }
         GS_LAUNCHED("two-level binning");
-        if (tile_first()) {
-            tile_depth_sort(f, bin, K_layout, true, 1, 0, stream);
-            GS_LAUNCHED("tile depth sort");
-        }
         return GS_OK;
     }
     ea.tile_key = at<uint32_t>(bin, bl.key0);
@@ -691,10 +649,6 @@ int bin_emit(FwdState& f, void* bin, uint32_t K_layout, const uint32_t* n_dev, h
         launch_ranges(at<uint32_t>(bin, tc ? bl.key1 : bl.key0), (int)K_layout, at<uint2>(img, il.ranges), nullptr,
                       stream);
         GS_LAUNCHED("ranges");
-    }
-    if (tile_first()) {
-        tile_depth_sort(f, bin, K_layout, tile_sort_writes_ranges(g.tiles), 1, 0, stream);
-        GS_LAUNCHED("tile depth sort");
     }
     return GS_OK;
 }
@@ -721,7 +675,7 @@ int bin_end(FwdState& f, gs_alloc_fn alloc, void* ctx, hipStream_t stream, void*
     if (c.K > (uint64_t)std::numeric_limits<int>::max())
         return set_error(GS_ERR_INVALID_ARG, "too many tile instances (%llu)", (unsigned long long)c.K);
     const uint32_t K = (uint32_t)c.K;
-    if (!tile_first() && (c.wide || force_depth_keys32())) {
+    if (c.wide || force_depth_keys32()) {
         // the visible depth keys span more bits than the short sort covered: redo the depth order
         // on the full 32-bit keys
         int cur;
@@ -917,15 +871,6 @@ struct gs_forward_state {
 
 namespace gs {
 int report_error(int code, const char* msg) { return set_error(code, "%s", msg); }
-
-// DGE_AMD_BINNING=depth: the depth-first binning (global depth sort, emission in depth order; A/B)
-bool tile_first() {
-    static const bool on = [] {
-        const char* e = getenv("DGE_AMD_BINNING");
-        return !(e && !strcmp(e, "depth"));
-    }();
-    return on;
-}
 
 
 uint64_t* diag_buffer(int which, size_t n_u64) {
@@ -1740,7 +1685,7 @@ int gs_views_overflow(const gs_views* h, uint8_t* flag, gs_stream_t stream_) {
     if (!h || !flag) return set_error(GS_ERR_INVALID_ARG, "gs_views_overflow: handle and flag are required");
     OverflowArgs a;
     a.n = h->n;
-    a.bits = tile_first() ? 0 : depth_sort_bits();
+    a.bits = depth_sort_bits();
     for (int v = 0; v < h->n; ++v) {
         const FwdState& f = h->f[v];
         if (!h->spec[v] || f.gp.P == 0) continue;

@@ -179,16 +179,9 @@ inline ImgLayout img_layout(int W, int H) {
     return L;
 }
 
-// Tile-first binning (the default; DGE_AMD_BINNING=depth selects the round-3 depth-first one): the
-// instances are emitted in Gaussian order, sorted stably on the tile alone, and each tile's run is then
-// sorted on the depth key by one workgroup (k_tile_depth_sort) — no global depth sort.  The binned runs
-// (Gaussian order) and the depth-ordered lists live in the two pair buffers.
-bool tile_first();
-
 struct BinLayout {
     size_t key0, key1, pair0, pair1, slot_gauss, point_pairs, records, rec_flags, sort_hist, sort_totals, ckpt,
         bwd_items, used, tile_count, total;
-    size_t binned;  // where the binning leaves the per-tile runs (== point_pairs unless tile_first())
     int sort_blocks;
     size_t nslots;  // checkpoint slots = work-item capacity / 4
 };
@@ -205,8 +198,7 @@ inline BinLayout bin_layout(int K, int num_tiles, bool bwd = true) {
     L.key1 = o; o = align_up(o + 4 * k);
     L.pair0 = o; o = align_up(o + 8 * k);
     L.pair1 = o; o = align_up(o + 8 * k);
-    L.binned = plan.passes & 1 ? L.pair1 : L.pair0;  // where tile_sort leaves (Gaussian, slot)
-    L.point_pairs = !tile_first() ? L.binned : L.binned == L.pair1 ? L.pair0 : L.pair1;
+    L.point_pairs = plan.passes & 1 ? L.pair1 : L.pair0;  // where tile_sort leaves (Gaussian, slot)
     L.slot_gauss = o; o = align_up(o + 4 * k);
     L.sort_hist = o; o = align_up(o + 4 * ((size_t)1 << maxbits) * (size_t)L.sort_blocks);
     L.sort_totals = o; o = align_up(o + 4 * ((size_t)1 << maxbits));
@@ -316,8 +308,7 @@ __host__ __device__ inline uint32_t pack_rect(int x0, int y0, int x1, int y1) {
 struct EmitArgs {
     int P, gx, gy;
     int rect_packed;
-    const uint2* order;          // by depth rank: (packed rect or tiles_touched, Gaussian id); nullptr:
-    const uint32_t* rect;        // Gaussian order (tile_first()), entry i = (rect[i], i)
+    const uint2* order;          // by depth rank: (packed rect or tiles_touched, Gaussian id)
     const uint32_t* tiles_touched;
     const Splat* splat;
     const int* radii;
@@ -358,25 +349,6 @@ struct OverflowArgs {
     uint32_t cap[8] = {};  // 0: an exact view (never overflows)
 };
 void launch_views_overflow(const OverflowArgs& a, uint8_t* flag, hipStream_t s);
-
-// Tile-first binning's per-tile depth order: one workgroup per tile sorts the tile's run of `in`
-// (Gaussian order) stably on depth_key[Gaussian] into `out`.  Runs longer than `cap` (<= kSegCap) take a
-// chunked global-memory LSD sort through kscratch0/1 (u32 per instance; `in` is overwritten then).
-constexpr int kSegCap = 16384;
-struct SegSortArgs {
-    const uint2* ranges;
-    const uint32_t* tile_order = nullptr;  // dispatch order (longest list first), or nullptr: block = tile
-    int ntiles = 0;
-    const uint32_t* depth_key;  // per Gaussian: the bits of its (positive) view depth
-    void* in;                   // uint2 (Gaussian, slot) pairs, or u32 ids (ids_only)
-    void* out;
-    uint32_t* kscratch0;
-    uint32_t* kscratch1;
-    uint32_t cap = kSegCap;
-    int ids_only = 0;
-    size_t vstride = 0;  // a batch of views (grid.y), see ViewBatch
-};
-void launch_tile_depth_sort(const SegSortArgs& a, hipStream_t s, int nviews = 1);
 
 // tile ranges; also zeroes the backward's per-slot record flags (u32 per slot)
 void launch_ranges(const uint32_t* sorted_tile, int K, uint2* ranges, uint32_t* rec_flags32, hipStream_t s);

@@ -606,7 +606,6 @@ __device__ __forceinline__ void emit_view(EmitArgs& a) {
     const size_t vs = a.vstride;
     if (!vs) return;
     a.order = vview(a.order, vs);
-    a.rect = vview(a.rect, vs);
     a.tiles_touched = vview(a.tiles_touched, vs);
     a.splat = vview(a.splat, vs);
     a.radii = vview(a.radii, vs);
@@ -632,8 +631,7 @@ __global__ __launch_bounds__(256) void k_scan_reduce(EmitArgs a) {
 #pragma unroll
     for (int it = 0; it < kScanIPT; ++it) {
         const uint32_t r = base + it * 256 + threadIdx.x;
-        const uint32_t rc = r < (uint32_t)a.P ? r : (uint32_t)a.P - 1u;
-        v[it] = a.order ? a.order[rc].x : a.rect[rc];
+        v[it] = a.order[r < (uint32_t)a.P ? r : (uint32_t)a.P - 1u].x;
     }
 #pragma unroll
     for (int it = 0; it < kScanIPT; ++it) {
@@ -689,7 +687,7 @@ __global__ __launch_bounds__(256) void k_scan_emit(EmitArgs a) {
 #pragma unroll
     for (int it = 0; it < kScanIPT; ++it) {
         const uint32_t r = r_block + it * 256 + threadIdx.x;
-        grs[it] = r >= (uint32_t)a.P ? make_uint2(0u, 0u) : a.order ? a.order[r] : make_uint2(a.rect[r], r);
+        grs[it] = r < (uint32_t)a.P ? a.order[r] : make_uint2(0u, 0u);
     }
 #pragma unroll
     for (int it = 0; it < kScanIPT; ++it) {
@@ -789,7 +787,7 @@ __global__ __launch_bounds__(256) void k_scan_emit_x(EmitArgs a) {
 #pragma unroll
     for (int it = 0; it < kScanIPT; ++it) {
         const uint32_t r = r_block + it * 256 + tid;
-        grs[it] = r >= (uint32_t)a.P ? make_uint2(0u, 0u) : a.order ? a.order[r] : make_uint2(a.rect[r], r);
+        grs[it] = r < (uint32_t)a.P ? a.order[r] : make_uint2(0u, 0u);
     }
 #pragma unroll  // (the prefetched arrays stay in registers)
     for (int it = 0; it < kScanIPT; ++it) {
@@ -996,296 +994,6 @@ void launch_scan_emit(const EmitArgs& a, hipStream_t s, int nviews) {
 }
 
 // ---------------------------------------------------------------------
-// Tile-first binning: per-tile depth order
-// ---------------------------------------------------------------------
-// The reference sorts (tile << 32 | depth bits) keys emitted in Gaussian order with a stable radix
-// sort (rasterizer_impl.cu:67-100, :253-261): per tile, instances by depth bits, ties by Gaussian
-// index.  Here the emission walks Gaussian order and the stable tile sort leaves each tile's run in
-// Gaussian order, so a STABLE sort of every run on its 32-bit depth key alone yields the same lists.
-// One 1024-thread workgroup per tile: the run's keys (biased by the run's minimum, so only the bits
-// that differ are sorted) and local indices stay in registers, 8-bit LSD passes rank them with 64-lane
-// ballots and per-wave digit counters (as k_radix_scatter, no atomics) and exchange them through LDS;
-// the sorted indices then gather the run's entries (L2-hot: the workgroup just read them).  A run
-// longer than the LDS holds takes the same passes chunk by chunk through global scratch.
-constexpr int kSegThreads = 1024, kSegWaves = kSegThreads / 64, kSegIPT = kSegCap / kSegThreads;
-constexpr int kSegBits = 8, kSegDigits = 1 << kSegBits;
-static_assert(kSegIPT * 64 <= 65535 && kSegCap <= 65536, "u16 counters and local indices");
-
-// exclusive scan over a 1024-thread workgroup (16 waves); lds16: 16 words
-__device__ __forceinline__ uint32_t block1024_exclusive_scan(uint32_t v, uint32_t* lds16) {
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    uint32_t x = v;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = (uint32_t)__shfl_up((int)x, o);
-        if (lane >= o) x += y;
-    }
-    if (lane == 63) lds16[w] = x;
-    __syncthreads();
-    uint32_t wbase = 0;
-#pragma unroll
-    for (int i = 0; i < kSegWaves; ++i) wbase += i < w ? lds16[i] : 0u;
-    __syncthreads();
-    return wbase + x - v;
-}
-
-// min and max over the workgroup; lds: 2 * kSegWaves words
-__device__ __forceinline__ void block1024_minmax(uint32_t& mn, uint32_t& mx, uint32_t* lds) {
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) {
-        mn = min(mn, (uint32_t)__shfl_xor((int)mn, o));
-        mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
-    }
-    if (lane == 0) {
-        lds[w] = mn;
-        lds[kSegWaves + w] = mx;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < kSegWaves; ++i) {
-        mn = min(mn, lds[i]);
-        mx = max(mx, lds[kSegWaves + i]);
-    }
-    __syncthreads();
-}
-
-template <class V>
-__device__ __forceinline__ uint32_t seg_gauss(const V& v) {
-    if constexpr (std::is_same<V, uint2>::value) return v.x;
-    else return v;
-}
-
-// Stable rank of this wave's elements (element e = w * 64 * IPT + it * 64 + lane, in order) by the
-// digit at `shift`: loc[it] = the element's place among the wave's elements of its digit; cnt[w][d]
-// ends as the wave's count of digit d.
-template <int IPT>
-__device__ __forceinline__ void seg_rank(const uint32_t (&key)[IPT], uint32_t (&loc)[IPT], uint32_t n_w, int shift,
-                                         uint16_t (*cnt)[kSegDigits]) {
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-#pragma unroll
-    for (int it = 0; it < IPT; ++it) {
-        const uint32_t e = (uint32_t)(it * 64 + lane);
-        const bool valid = e < n_w;
-        const uint64_t vm = __ballot(valid);
-        if (vm == 0) break;
-        const uint32_t d = (key[it] >> shift) & (kSegDigits - 1);
-        const uint64_t peers = match_digit<kSegBits>(valid ? d : 0u, vm);
-        const uint32_t rank = (uint32_t)__popcll(peers & lanemask_lt());
-        const uint32_t old = cnt[w][d];
-        loc[it] = old + rank;
-        if (valid && rank == 0) cnt[w][d] = (uint16_t)(old + (uint32_t)__popcll(peers));
-    }
-}
-
-// The workgroup's tile run: [r.x, r.y) of the view's lists
-__device__ __forceinline__ uint2 seg_run(const SegSortArgs& a) {
-    const uint32_t* tile_order = vview(a.tile_order, a.vstride);
-    const int tile = tile_order ? (int)tile_order[blockIdx.x] : (int)blockIdx.x;
-    return vview(a.ranges, a.vstride)[tile];
-}
-
-// Runs longer than a.cap: chunked LSD passes through global memory (a separate kernel: sharing one
-// with the LDS path pushed the latter's registers into scratch)
-template <bool IDS>
-__global__ __launch_bounds__(kSegThreads) void k_tile_depth_sort_long(SegSortArgs a) {
-    using V = typename std::conditional<IDS, uint32_t, uint2>::type;
-    const size_t vs = a.vstride;
-    const uint2 r = seg_run(a);
-    const uint32_t n = r.y > r.x ? r.y - r.x : 0u;
-    if (n <= a.cap) return;
-    const uint32_t* depth_key = vview(a.depth_key, vs);
-    V* in = static_cast<V*>(vview(a.in, vs)) + r.x;
-    V* out = static_cast<V*>(vview(a.out, vs)) + r.x;
-    __shared__ uint16_t cnt[kSegWaves][kSegDigits];
-    __shared__ uint32_t s_red[2 * kSegWaves];
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    for (int i = tid; i < kSegWaves * kSegDigits; i += kSegThreads) (&cnt[0][0])[i] = 0;
-    {
-        // pass p writes (key, value) buffer p & 1 and reads the other (pass 0 reads `in` = value buffer 1)
-        uint32_t* const k0 = vview(a.kscratch0, vs) + r.x;
-        uint32_t* const k1 = vview(a.kscratch1, vs) + r.x;
-        __shared__ uint32_t s_hist[kSegDigits], s_dof[kSegDigits];
-        uint32_t mn = 0xFFFFFFFFu, mx = 0u;
-        for (uint32_t e = tid; e < n; e += kSegThreads) {
-            const uint32_t k = depth_key[seg_gauss(in[e])];
-            mn = min(mn, k);
-            mx = max(mx, k);
-        }
-        block1024_minmax(mn, mx, s_red);
-        const int bits = mx > mn ? 32 - __clz((int)(mx - mn)) : 0;
-        const int passes = (bits + kSegBits - 1) / kSegBits;
-        for (int p = 0; p < passes; ++p) {
-            const int shift = p * kSegBits;
-            const bool odd = p & 1;
-            const V* vsrc = odd ? out : in;
-            const uint32_t* ksrc = odd ? k0 : k1;
-            V* vdst = odd ? in : out;
-            uint32_t* kdst = odd ? k1 : k0;
-            for (int i = tid; i < kSegDigits; i += kSegThreads) s_hist[i] = 0u;
-            __syncthreads();
-            for (uint32_t e = tid; e < n; e += kSegThreads) {
-                const uint32_t k = p == 0 ? depth_key[seg_gauss(in[e])] - mn : ksrc[e];
-                atomicAdd(&s_hist[(k >> shift) & (kSegDigits - 1)], 1u);
-            }
-            __syncthreads();
-            {
-                const uint32_t hv = tid < kSegDigits ? s_hist[tid] : 0u;
-                const uint32_t ex = block1024_exclusive_scan(hv, s_red);
-                if (tid < kSegDigits) s_dof[tid] = ex;
-            }
-            __syncthreads();
-            constexpr int kLongIPT = kSegIPT / 2;  // (half the registers of the LDS path: no spill)
-            for (uint32_t c0 = 0; c0 < n; c0 += kSegThreads * kLongIPT) {
-                const uint32_t base = c0 + (uint32_t)(w * 64 * kLongIPT);
-                const uint32_t n_w = n > base ? min(n - base, (uint32_t)(64 * kLongIPT)) : 0u;
-                uint32_t key[kLongIPT], loc[kLongIPT];
-#pragma unroll
-                for (int it = 0; it < kLongIPT; ++it) {
-                    const uint32_t e = (uint32_t)(it * 64 + lane);
-                    key[it] = e >= n_w ? 0u : p == 0 ? depth_key[seg_gauss(in[base + e])] - mn : ksrc[base + e];
-                }
-                seg_rank(key, loc, n_w, shift, cnt);
-                __syncthreads();
-                if (tid < kSegDigits) {  // wave prefix per digit; the chunk's digit totals into s_hist
-                    uint32_t run = 0;
-#pragma unroll
-                    for (int ww = 0; ww < kSegWaves; ++ww) {
-                        const uint32_t c = cnt[ww][tid];
-                        cnt[ww][tid] = (uint16_t)run;
-                        run += c;
-                    }
-                    s_hist[tid] = run;
-                }
-                __syncthreads();
-#pragma unroll
-                for (int it = 0; it < kLongIPT; ++it) {
-                    const uint32_t e = (uint32_t)(it * 64 + lane);
-                    if (e < n_w) {
-                        const uint32_t d = (key[it] >> shift) & (kSegDigits - 1);
-                        const uint32_t pos = s_dof[d] + cnt[w][d] + loc[it];
-                        kdst[pos] = key[it];
-                        vdst[pos] = vsrc[base + e];  // (re-read from L2 rather than held: no spill)
-                    }
-                }
-                __syncthreads();
-                if (tid < kSegDigits) s_dof[tid] += s_hist[tid];
-                for (int i = tid; i < kSegWaves * kSegDigits; i += kSegThreads) (&cnt[0][0])[i] = 0;
-                __syncthreads();
-            }
-        }
-        if (!(passes & 1))  // (even: the result is back in `in`; none: the run is already ordered)
-            for (uint32_t e = tid; e < n; e += kSegThreads) out[e] = in[e];
-    }
-}
-
-// Runs of up to a.cap entries: keys and local indices in registers, LDS exchange between passes
-template <bool IDS>
-__global__ __launch_bounds__(kSegThreads) void k_tile_depth_sort(SegSortArgs a) {
-    using V = typename std::conditional<IDS, uint32_t, uint2>::type;
-    const size_t vs = a.vstride;
-    const uint2 r = seg_run(a);
-    const uint32_t n = r.y > r.x ? r.y - r.x : 0u;
-    if (n == 0 || n > a.cap) return;
-    const uint32_t* depth_key = vview(a.depth_key, vs);
-    const V* in = static_cast<const V*>(vview(a.in, vs)) + r.x;
-    V* out = static_cast<V*>(vview(a.out, vs)) + r.x;
-    __shared__ uint32_t s_key[kSegCap];
-    __shared__ uint16_t s_idx[kSegCap];
-    __shared__ uint16_t cnt[kSegWaves][kSegDigits];
-    __shared__ uint32_t s_red[2 * kSegWaves];
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    for (int i = tid; i < kSegWaves * kSegDigits; i += kSegThreads) (&cnt[0][0])[i] = 0;
-    const uint32_t base = (uint32_t)(w * 64 * kSegIPT);
-    const uint32_t n_w = n > base ? min(n - base, (uint32_t)(64 * kSegIPT)) : 0u;
-    uint32_t key[kSegIPT], idx[kSegIPT], loc[kSegIPT];
-#pragma unroll
-    for (int it = 0; it < kSegIPT; ++it) {
-        const uint32_t e = (uint32_t)(it * 64 + lane);
-        idx[it] = e < n_w ? seg_gauss(in[base + e]) : 0u;  // (the Gaussian first; its key next)
-    }
-    uint32_t mn = 0xFFFFFFFFu, mx = 0u;
-#pragma unroll
-    for (int it = 0; it < kSegIPT; ++it) {
-        const uint32_t e = (uint32_t)(it * 64 + lane);
-        key[it] = e < n_w ? depth_key[idx[it]] : 0u;
-        if (e < n_w) {
-            mn = min(mn, key[it]);
-            mx = max(mx, key[it]);
-        }
-        idx[it] = base + e;
-    }
-    block1024_minmax(mn, mx, s_red);  // (its barriers also order the counter zeroing above)
-    const int bits = mx > mn ? 32 - __clz((int)(mx - mn)) : 0;
-    if (bits == 0) {  // one key: the run is already in order
-        for (uint32_t e = tid; e < n; e += kSegThreads) out[e] = in[e];
-        return;
-    }
-#pragma unroll
-    for (int it = 0; it < kSegIPT; ++it) key[it] -= mn;
-    const int passes = (bits + kSegBits - 1) / kSegBits;
-    for (int p = 0; p < passes; ++p) {
-        const int shift = p * kSegBits;
-        seg_rank(key, loc, n_w, shift, cnt);
-        __syncthreads();
-        {  // digit-major starts: digit d's run, then wave w's share of it after waves < w
-            uint32_t c[kSegWaves];
-            uint32_t tot = 0;
-            if (tid < kSegDigits) {
-#pragma unroll
-                for (int ww = 0; ww < kSegWaves; ++ww) {
-                    c[ww] = cnt[ww][tid];
-                    tot += c[ww];
-                }
-            }
-            uint32_t run = block1024_exclusive_scan(tot, s_red);
-            if (tid < kSegDigits) {
-#pragma unroll
-                for (int ww = 0; ww < kSegWaves; ++ww) {
-                    cnt[ww][tid] = (uint16_t)run;
-                    run += c[ww];
-                }
-            }
-        }
-        __syncthreads();
-#pragma unroll
-        for (int it = 0; it < kSegIPT; ++it) {
-            const uint32_t e = (uint32_t)(it * 64 + lane);
-            if (e < n_w) {
-                const uint32_t pos = cnt[w][(key[it] >> shift) & (kSegDigits - 1)] + loc[it];
-                s_key[pos] = key[it];
-                s_idx[pos] = (uint16_t)idx[it];
-            }
-        }
-        __syncthreads();
-        if (p + 1 == passes) break;
-#pragma unroll
-        for (int it = 0; it < kSegIPT; ++it) {
-            const uint32_t e = (uint32_t)(it * 64 + lane);
-            if (e < n_w) {
-                key[it] = s_key[base + e];
-                idx[it] = s_idx[base + e];
-            }
-        }
-        for (int i = tid; i < kSegWaves * kSegDigits; i += kSegThreads) (&cnt[0][0])[i] = 0;
-        __syncthreads();
-    }
-    for (uint32_t e = tid; e < n; e += kSegThreads) out[e] = in[s_idx[e]];
-}
-
-void launch_tile_depth_sort(const SegSortArgs& a, hipStream_t s, int nviews) {
-    if (a.ntiles <= 0 || nviews <= 0) return;
-    const dim3 grid(a.ntiles, nviews);
-    if (a.ids_only) {
-        hipLaunchKernelGGL(k_tile_depth_sort<true>, grid, dim3(kSegThreads), 0, s, a);
-        hipLaunchKernelGGL(k_tile_depth_sort_long<true>, grid, dim3(kSegThreads), 0, s, a);
-    } else {
-        hipLaunchKernelGGL(k_tile_depth_sort<false>, grid, dim3(kSegThreads), 0, s, a);
-        hipLaunchKernelGGL(k_tile_depth_sort_long<false>, grid, dim3(kSegThreads), 0, s, a);
-    }
-}
-
-// ---------------------------------------------------------------------
 // identifyTileRanges (rasterizer_impl.cu:105-125) + instance maps
 // ---------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_ranges(const uint32_t* __restrict__ tile, int K, uint2* __restrict__ ranges,
@@ -1326,7 +1034,7 @@ __global__ __launch_bounds__(64) void k_views_overflow(OverflowArgs a, uint8_t* 
             kmax = max(kmax, c[i * kCounterStride + 1]);
             kmin_not = max(kmin_not, c[i * kCounterStride + 2]);
         }
-        bad = k > a.cap[v] || (a.bits && k && kmax - ~kmin_not >= (1u << a.bits));  // (bits 0: no depth sort)
+        bad = k > a.cap[v] || (k && kmax - ~kmin_not >= (1u << a.bits));
     }
     const uint64_t any = __ballot(bad);
     if (v == 0) flag[0] = any ? 1 : 0;

@@ -569,24 +569,16 @@ def test_depth_beyond_30bit_key_range_keeps_reference_order(cuda_device, oracle)
     compare_grads(got, ref, O=oracle, label="far-depth")
 
 
-@pytest.mark.parametrize("cap", [1, 100, 1000])
-def test_long_tile_runs_take_the_global_passes(cuda_device, monkeypatch, oracle, cap):
-    """Tile-first binning: a tile run longer than the LDS holds (16384 entries; DGE_AMD_SEG_CAP lowers the
-    limit so most runs here exceed it) is depth-sorted by k_tile_depth_sort_long's chunked global-memory
-    passes.  Lists, ranges and image equal the oracle's (the reference's stable (tile, depth) order) with the
-    backward on top; cap 1: every run of two or more entries, cap 1000: a mix of both kernels."""
+def test_forced_32bit_depth_keys_match_30bit_path(cuda_device, monkeypatch):
+    """The 32-bit fallback (DGE_AMD_DEPTH_KEYS32=1) and the 30-bit path give the same lists and images."""
     a = scene_arrays(100_000, seed=4, radius=2.0, scale=0.02)
     kw = _sh_kw(a)
-    g = np.random.default_rng(9).standard_normal((3, 160, 192)).astype(np.float32) * 1e-3
-    ref = run_oracle(oracle, camera_settings(192, 160), g, **kw)
-    monkeypatch.setenv("DGE_AMD_SEG_CAP", str(cap))
-    got = run_gpu(camera_settings(192, 160, device="cuda"), g, **kw)
-    lens = ref["ranges"].reshape(-1, 2) @ np.array([-1, 1])
-    assert (lens > cap).sum() > 0 and got["num_rendered"] == ref["num_rendered"]
-    np.testing.assert_array_equal(got["ranges"], ref["ranges"])
-    np.testing.assert_array_equal(got["point_list"], ref["point_list"])
-    compare_forward(got, ref, label=f"seg cap {cap}")
-    compare_grads(got, ref, O=oracle, label=f"seg cap {cap}")
+    s = camera_settings(256, 256, device="cuda")
+    base = run_gpu(s, **kw)
+    monkeypatch.setenv("DGE_AMD_DEPTH_KEYS32", "1")
+    forced = run_gpu(s, **kw)
+    for k in ("radii", "ranges", "point_list", "n_contrib", "color", "final_T"):
+        np.testing.assert_array_equal(forced[k], base[k], err_msg=k)
 
 
 @pytest.mark.parametrize("P,W,H", [(3_000, 1920, 1080), (300_000, 1920, 1080), (200_000, 2048, 1040)])
