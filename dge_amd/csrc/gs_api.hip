@@ -131,13 +131,11 @@ bool views_issue_by_view() {
 }
 
 // DGE_AMD_VIEWS_FWD (A/B): "streams" — each view's chain on its own stream (round 3); "render" — the same,
-// the blends as one launch; "batch" — the whole batch as one chain of batched launches (and one batched
-// replay); "half" — the first halves batched (one preprocess, depth sort and scan for every view), then
-// each view's second half on its own stream
+// the blends as one launch; default — the whole batch as one chain of batched launches
 int views_forward_mode() {
     static const int m = [] {
         const char* e = getenv("DGE_AMD_VIEWS_FWD");
-        return !e ? 0 : !strcmp(e, "streams") ? 0 : !strcmp(e, "render") ? 1 : !strcmp(e, "batch") ? 2 : 3;
+        return e && !strcmp(e, "streams") ? 0 : e && !strcmp(e, "render") ? 1 : 2;
     }();
     return m;
 }
@@ -1337,15 +1335,13 @@ int gs_views_forward(int n, const gs_settings* const* s, const gs_params* const*
         hipStream_t join = (hipStream_t)join_;
         int rc = fork_from(h.get(), join, streams);  // the views' streams start after the caller's work
         if (rc) return rc;
-        bool first_halves_done = false;
         // The whole batch as ONE chain of launches on the first view's stream, each kernel over every view
         // (grid.y or interleaved blocks): one preprocess reading the scene once, one depth sort, one scan,
         // one emission, one tile sort, one blend — ~20 launches, each with n times the workgroups, instead
         // of n contending chains of small launches.  When every view is speculated, alike (P, image size,
         // kind) and laid out at one stride in the allocation, on the single-pass tile sort.
         {
-            const int fmode = views_forward_mode();
-            bool batched = fmode >= 2 && n >= 2 && n <= kRenderBatch && mode == GS_VIEWS_SPECULATE;
+            bool batched = views_forward_mode() == 2 && n >= 2 && n <= kRenderBatch && mode == GS_VIEWS_SPECULATE;
             const size_t stride = n >= 2 ? off_geom[1] - off_geom[0] : 0;
             for (int v = 0; v < n && batched; ++v) {
                 const FwdState& f = h->f[v];
@@ -1379,13 +1375,6 @@ int gs_views_forward(int n, const gs_settings* const* s, const gs_params* const*
                 GS_LAUNCHED("preprocess (views)");
                 rc = bin_after_preprocess_views(fs, n, stride, s0);
                 if (rc) return rc;
-                if (fmode == 3) {  // ("half": the second halves on the views' streams, behind the batch's first)
-                    if (!h->pre && !(h->pre = event_pool().get())) return set_error(GS_ERR_HIP, "could not create an event");
-                    GS_HIP(hipEventRecord(h->pre, s0));
-                    for (int v = 1; v < n; ++v)
-                        if ((hipStream_t)streams[v] != s0) GS_HIP(hipStreamWaitEvent((hipStream_t)streams[v], h->pre, 0));
-                    first_halves_done = true;
-                } else {
                 rc = bin_emit_views(fs, n, stride, bins, h->layout[0], s0);
                 if (rc) return rc;
                 RenderArgs ras[kRenderBatch];
@@ -1402,7 +1391,6 @@ int gs_views_forward(int n, const gs_settings* const* s, const gs_params* const*
                 if (rc) return rc;
                 *out = h.release();
                 return GS_OK;
-                }
             }
         }
         // first halves on every view's stream: nothing waits for any count yet.  Breadth first: every
@@ -1411,7 +1399,7 @@ int gs_views_forward(int n, const gs_settings* const* s, const gs_params* const*
         // the forward phase ended with that view)
         // one preprocess for every view (k_preprocess_views: the scene read once) when the views share
         // their inputs, on the first view's stream, which the others then wait for
-        bool shared = !first_halves_done && views_shared_preprocess() && !views_issue_by_view() && n >= 2;
+        bool shared = views_shared_preprocess() && !views_issue_by_view() && n >= 2;
         for (int v = 0; v < n && shared; ++v) shared = h->f[v].gp.P > 0 && h->f[v].s.debug == 0;
         if (shared) {
             hipStream_t s0 = (hipStream_t)streams[0];
@@ -1444,7 +1432,7 @@ int gs_views_forward(int n, const gs_settings* const* s, const gs_params* const*
                 shared = true;  // (every view's preprocess is enqueued)
             }
         }
-        for (int v = 0; v < n && !shared && !first_halves_done; ++v) {
+        for (int v = 0; v < n && !shared; ++v) {
             FwdState& f = h->f[v];
             if (f.gp.P == 0) continue;
             hipStream_t stream = (hipStream_t)streams[v];
@@ -1458,7 +1446,7 @@ int gs_views_forward(int n, const gs_settings* const* s, const gs_params* const*
                 if (rc) return rc;
             }
         }
-        for (int v = 0; v < n && !views_issue_by_view() && !first_halves_done; ++v) {
+        for (int v = 0; v < n && !views_issue_by_view(); ++v) {
             FwdState& f = h->f[v];
             if (f.gp.P == 0) continue;
             rc = bin_after_preprocess(f, (hipStream_t)streams[v]);
@@ -1467,7 +1455,7 @@ int gs_views_forward(int n, const gs_settings* const* s, const gs_params* const*
         // second halves: a speculated view's binning runs on the device count, capped at its capacity;
         // the others wait for their count here (the reference's sync, rasterizer_impl.cu:236-239).  The
         // blends: one batched launch (views_batch_forward) when every view renders (same kind, <= 4)
-        bool batch_fwd = views_forward_mode() == 1 && n >= 2 && n <= kRenderBatch;
+        bool batch_fwd = views_forward_mode() >= 1 && n >= 2 && n <= kRenderBatch;
         for (int v = 0; v < n && batch_fwd; ++v)
             batch_fwd = h->f[v].gp.P > 0 && h->f[v].s.debug == 0 && h->f[v].gp.forward_only == h->f[0].gp.forward_only;
         RenderArgs ras[kRenderBatch];
