@@ -130,16 +130,6 @@ bool views_issue_by_view() {
     return on;
 }
 
-// DGE_AMD_VIEWS_FWD (A/B): "streams" — each view's chain on its own stream (round 3); "render" — the same,
-// the blends as one launch; default — the whole batch as one chain of batched launches
-int views_forward_mode() {
-    static const int m = [] {
-        const char* e = getenv("DGE_AMD_VIEWS_FWD");
-        return e && !strcmp(e, "streams") ? 0 : e && !strcmp(e, "render") ? 1 : 2;
-    }();
-    return m;
-}
-
 // DGE_AMD_VIEWS_PRE=1: a batch's views preprocessed in one pass (k_preprocess_views) when they share their
 // inputs (A/B; round 3 measured it no faster with the view-by-view issue order)
 bool views_shared_preprocess() {
@@ -433,10 +423,7 @@ int bin_prepare(FwdState& f, int copy_colors, gs_alloc_fn alloc, void* ctx, hipS
     return bin_prepare_in(f, copy_colors, geom, img, stream);
 }
 
-// After the preprocess of n views whose buffers sit vstride bytes apart (n = 1: one view): each view's
-// counter read-back, then ONE depth sort and ONE instance scan over all of them (grid.y = view)
-int bin_after_preprocess_views(FwdState* const* fs, int n, size_t vstride, hipStream_t stream) {
-    FwdState& f = *fs[0];
+int bin_after_preprocess(FwdState& f, hipStream_t stream) {
     const gs_settings* s = &f.s;
     const Grid& g = f.g;
     const int P = f.gp.P;
@@ -446,15 +433,10 @@ int bin_after_preprocess_views(FwdState* const* fs, int n, size_t vstride, hipSt
     void* geom = f.geom;
     uint32_t* counters = at<uint32_t>(f.img, il.counters);
     PreprocessArgs& pa = f.pa;
-    for (int v = 0; v < n; ++v) {
-        FwdState& fv = *fs[v];
-        int rc = staging_acquire(&fv.st);
-        if (rc) return rc;
-        GS_HIP(hipMemcpyAsync(fv.st->host, at<uint32_t>(fv.img, il.counters), 4 * kCounterSlots * kCounterStride,
-                              hipMemcpyDeviceToHost, stream));
-        GS_HIP(hipEventRecord(fv.st->ev, stream));
-    }
-    const ViewBatch vb{n, vstride};
+    int rc = staging_acquire(&f.st);
+    if (rc) return rc;
+    GS_HIP(hipMemcpyAsync(f.st->host, counters, 4 * kCounterSlots * kCounterStride, hipMemcpyDeviceToHost, stream));
+    GS_HIP(hipEventRecord(f.st->ev, stream));
 
     // depth order of the Gaussians (stable: ties keep index order)
     int cur = 0;
@@ -462,67 +444,23 @@ int bin_after_preprocess_views(FwdState* const* fs, int n, size_t vstride, hipSt
     cur = radix_sort_aux(at<uint32_t>(geom, gl.key0), at<uint32_t>(geom, gl.key1), at<uint2>(geom, gl.val0),
                          at<uint2>(geom, gl.val1), pa.rect, (uint32_t)P, depth_sort_bits(), depth_pass_bits(),
                          kDepthSortIPT, at<uint32_t>(geom, gl.sort_hist), at<uint32_t>(geom, gl.sort_totals),
-                         gl.sort_blocks, stream, nullptr, counters + 2, nullptr, 0, nullptr, vb); }
+                         gl.sort_blocks, stream, nullptr, counters + 2); }
     if (cur < 0) return set_error(GS_ERR_INVALID_ARG, "depth sort: bad digit layout");
     GS_LAUNCHED("depth sort");
 
-    for (int v = 0; v < n; ++v) {
-        FwdState& fv = *fs[v];
-        EmitArgs& ea = fv.ea;
-        void* gv = fv.geom;
-        ea.P = P; ea.gx = g.gx; ea.gy = g.gy;
-        ea.order = at<uint2>(gv, cur ? gl.val1 : gl.val0);
-        ea.rect_packed = fv.pa.rect_packed;
-        ea.tiles_touched = fv.pa.tiles_touched;
-        ea.splat = fv.pa.splat;
-        ea.radii = fv.pa.radii;
-        ea.scan_sums = at<uint32_t>(gv, gl.scan_sums);
-        ea.first_slot = at<uint32_t>(gv, gl.first_slot);
-        ea.scan_blocks = gl.scan_blocks;
-        ea.xhist = two_level(g.gx, g.gy) && fv.pa.rect_packed ? at<uint32_t>(gv, gl.emit_hist) : nullptr;
-    }
-    EmitArgs ea = f.ea;
-    ea.vstride = vstride;
-    { StageScope sc(ST_SCAN, stream); launch_scan_reduce(ea, stream, n); }
+    EmitArgs& ea = f.ea;
+    ea.P = P; ea.gx = g.gx; ea.gy = g.gy;
+    ea.order = at<uint2>(geom, cur ? gl.val1 : gl.val0);
+    ea.rect_packed = pa.rect_packed;
+    ea.tiles_touched = pa.tiles_touched;
+    ea.splat = pa.splat;
+    ea.radii = pa.radii;
+    ea.scan_sums = at<uint32_t>(geom, gl.scan_sums);
+    ea.first_slot = at<uint32_t>(geom, gl.first_slot);
+    ea.scan_blocks = gl.scan_blocks;
+    ea.xhist = two_level(g.gx, g.gy) && pa.rect_packed ? at<uint32_t>(geom, gl.emit_hist) : nullptr;
+    { StageScope sc(ST_SCAN, stream); launch_scan_reduce(ea, stream); }
     GS_LAUNCHED("instance scan");
-    return GS_OK;
-}
-
-int bin_after_preprocess(FwdState& f, hipStream_t stream) {
-    FwdState* fs[1] = {&f};
-    return bin_after_preprocess_views(fs, 1, 0, stream);
-}
-
-// The single-pass binning (emission + tile sort with ranges) of n speculated views laid out alike, vstride
-// bytes apart, in ONE emission and ONE tile sort (grid.y = view): bins[v] their binning buffers, each laid
-// out for K_layout instances, the counts read on the device
-int bin_emit_views(FwdState* const* fs, int n, size_t vstride, void* const* bins, uint32_t K_layout,
-                   hipStream_t stream) {
-    FwdState& f = *fs[0];
-    const Grid& g = f.g;
-    const bool debug = f.s.debug != 0;
-    const ImgLayout il = img_layout(g.W, g.H);
-    const bool bwd = !f.gp.forward_only;
-    const BinLayout bl = bin_layout((int)K_layout, g.tiles, bwd);
-    const TileSortPlan plan = tile_sort_plan(g.tiles);
-    for (int v = 0; v < n; ++v) {
-        EmitArgs& ea = fs[v]->ea;
-        ea.cap = K_layout;
-        ea.tile_key = at<uint32_t>(bins[v], bl.key0);
-        ea.slot_gauss = at<uint32_t>(bins[v], bl.slot_gauss);
-        ea.rec_flags32 = bwd ? at<uint32_t>(bins[v], bl.rec_flags) : nullptr;
-    }
-    EmitArgs ea = f.ea;
-    ea.vstride = vstride;
-    { StageScope sc(ST_EMIT, stream); launch_scan_emit(ea, stream, n); }
-    GS_LAUNCHED("emit (views)");
-    const uint32_t* n_dev = at<uint32_t>(f.img, il.counters);
-    { StageScope sc(ST_TILE_SORT, stream);
-    tile_sort(at<uint32_t>(bins[0], bl.key0), at<uint32_t>(bins[0], bl.key1), at<uint2>(bins[0], bl.pair0),
-              at<uint2>(bins[0], bl.pair1), at<uint32_t>(bins[0], bl.slot_gauss), K_layout, plan.bits,
-              at<uint32_t>(bins[0], bl.sort_hist), at<uint32_t>(bins[0], bl.sort_totals), bl.sort_blocks, stream,
-              at<uint2>(f.img, il.ranges), at<uint32_t>(f.img, il.tile_order), g.tiles, n_dev, ViewBatch{n, vstride}); }
-    GS_LAUNCHED("tile sort (views)");
     return GS_OK;
 }
 
@@ -697,9 +635,10 @@ int bin_end(FwdState& f, gs_alloc_fn alloc, void* ctx, hipStream_t stream, void*
 }
 
 // The blend (k_render_fwd) over a finished binning laid out for K_layout instances.
-RenderArgs render_args(FwdState& f, void* bin, uint32_t K_layout, int order_ready, float* out_color,
-                       float* out_depth) {
+int render_launch(FwdState& f, void* bin, uint32_t K_layout, int order_ready, float* out_color, float* out_depth,
+                  hipStream_t stream) {
     const Grid& g = f.g;
+    const bool debug = f.s.debug != 0;
     const GeomLayout gl = geom_layout(f.gp.P);
     const ImgLayout il = img_layout(g.W, g.H);
     const BinLayout bl = bin_layout((int)K_layout, g.tiles, !f.gp.forward_only);
@@ -728,13 +667,6 @@ RenderArgs render_args(FwdState& f, void* bin, uint32_t K_layout, int order_read
     ra.out_depth = out_depth;
     ra.touched = at<uint8_t>(geom, gl.touched);
     ra.diag = diag_buffer(0, kDiagWords * (size_t)g.tiles * 4);
-    return ra;
-}
-
-int render_launch(FwdState& f, void* bin, uint32_t K_layout, int order_ready, float* out_color, float* out_depth,
-                  hipStream_t stream) {
-    const bool debug = f.s.debug != 0;
-    const RenderArgs ra = render_args(f, bin, K_layout, order_ready, out_color, out_depth);
     GS_SKIP("fwd") { StageScope sc(ST_RENDER_FWD, stream); launch_render_forward(ra, stream); }
     GS_LAUNCHED("render");
     return GS_OK;
@@ -761,9 +693,11 @@ int bin_forward(const gs_settings* s, const Grid& g, const gs_params& gp, int* r
 // records), then the per-Gaussian pass over those records, whose accumulated writes wait for
 // writes_after.  R: the binning layout's instance count; slot_cap: a speculative forward's capacity
 // (its slots end there), else ~0.
-RenderBwdArgs replay_args(const gs_settings* s, const gs_params* gp, int R, const void* geom, const void* binning,
-                          const void* img, const float* dL_dpix) {
+int replay_view(const gs_settings* s, const gs_params* gp, int R, const void* geom, const void* binning,
+                const void* img, const float* dL_dpix, hipStream_t stream) {
     const int P = gp->P;
+    if (P == 0 || R <= 0) return GS_OK;
+    const bool debug = s->debug != 0;
     const Grid g = make_grid(s);
     const GeomLayout gl = geom_layout(P);
     const ImgLayout il = img_layout(g.W, g.H);
@@ -787,14 +721,6 @@ RenderBwdArgs replay_args(const gs_settings* s, const gs_params* gp, int R, cons
     rb.records = at<float4>(const_cast<void*>(binning), bl.records);
     rb.rec_flags = at<uint8_t>(const_cast<void*>(binning), bl.rec_flags);
     rb.diag = diag_buffer(1, kDiagWords * 4 * bl.nslots);
-    return rb;
-}
-
-int replay_view(const gs_settings* s, const gs_params* gp, int R, const void* geom, const void* binning,
-                const void* img, const float* dL_dpix, hipStream_t stream) {
-    if (gp->P == 0 || R <= 0) return GS_OK;
-    const bool debug = s->debug != 0;
-    const RenderBwdArgs rb = replay_args(s, gp, R, geom, binning, img, dL_dpix);
     GS_SKIP("rbwd") { StageScope sc(ST_RENDER_BWD, stream); launch_render_backward(rb, stream); }
     GS_LAUNCHED("render backward");
     return GS_OK;
@@ -1335,64 +1261,6 @@ int gs_views_forward(int n, const gs_settings* const* s, const gs_params* const*
         hipStream_t join = (hipStream_t)join_;
         int rc = fork_from(h.get(), join, streams);  // the views' streams start after the caller's work
         if (rc) return rc;
-        // The whole batch as ONE chain of launches on the first view's stream, each kernel over every view
-        // (grid.y or interleaved blocks): one preprocess reading the scene once, one depth sort, one scan,
-        // one emission, one tile sort, one blend — ~20 launches, each with n times the workgroups, instead
-        // of n contending chains of small launches.  When every view is speculated, alike (P, image size,
-        // kind) and laid out at one stride in the allocation, on the single-pass tile sort.
-        {
-            bool batched = views_forward_mode() == 2 && n >= 2 && n <= kRenderBatch && mode == GS_VIEWS_SPECULATE;
-            const size_t stride = n >= 2 ? off_geom[1] - off_geom[0] : 0;
-            for (int v = 0; v < n && batched; ++v) {
-                const FwdState& f = h->f[v];
-                const FwdState& f0 = h->f[0];
-                batched = f.gp.P > 0 && f.gp.P == f0.gp.P && f.g.W == f0.g.W && f.g.H == f0.g.H && f.s.debug == 0 &&
-                          h->spec[v] && h->layout[v] == h->layout[0] && f.gp.forward_only == f0.gp.forward_only &&
-                          !two_level(f.g.gx, f.g.gy) && tile_sort_writes_ranges(f.g.tiles) &&
-                          off_geom[v] == off_geom[0] + v * stride && off_img[v] == off_img[0] + v * stride &&
-                          off_bin[v] == off_bin[0] + v * stride;
-            }
-            if (batched) {
-                hipStream_t s0 = (hipStream_t)streams[0];
-                const bool debug = false;
-                hipStream_t stream = s0;  // (GS_LAUNCHED)
-                FwdState* fs[GS_MAX_VIEWS];
-                const PreprocessArgs* pas[GS_MAX_VIEWS];
-                void* bins[GS_MAX_VIEWS];
-                for (int v = 0; v < n; ++v) {
-                    fs[v] = &h->f[v];
-                    rc = bin_prepare_in(h->f[v], 1, base + off_geom[v], base + off_img[v], s0);
-                    if (rc) return rc;
-                    pas[v] = &h->f[v].pa;
-                    bins[v] = h->bin[v] = base + off_bin[v];
-                }
-                if (preprocess_views_ok(pas, n)) {
-                    GS_SKIP("pre") { StageScope sc(ST_PREPROCESS, s0); launch_preprocess_views(pas, n, s0); }
-                } else {
-                    GS_SKIP("pre") { StageScope sc(ST_PREPROCESS, s0);
-                        for (int v = 0; v < n; ++v) launch_preprocess(h->f[v].pa, s0); }
-                }
-                GS_LAUNCHED("preprocess (views)");
-                rc = bin_after_preprocess_views(fs, n, stride, s0);
-                if (rc) return rc;
-                rc = bin_emit_views(fs, n, stride, bins, h->layout[0], s0);
-                if (rc) return rc;
-                RenderArgs ras[kRenderBatch];
-                for (int v = 0; v < n; ++v)
-                    ras[v] = render_args(h->f[v], bins[v], h->layout[v], 1, out_color[v], out_depth[v]);
-                GS_SKIP("fwd") { StageScope sc(ST_RENDER_FWD, s0); launch_render_forward_views(ras, n, s0); }
-                GS_LAUNCHED("render (views)");
-                // the views' streams (the backward's) start after the batch
-                if (!h->pre && !(h->pre = event_pool().get())) return set_error(GS_ERR_HIP, "could not create an event");
-                GS_HIP(hipEventRecord(h->pre, s0));
-                for (int v = 1; v < n; ++v)
-                    if ((hipStream_t)streams[v] != s0) GS_HIP(hipStreamWaitEvent((hipStream_t)streams[v], h->pre, 0));
-                rc = join_into(h.get(), join, streams);
-                if (rc) return rc;
-                *out = h.release();
-                return GS_OK;
-            }
-        }
         // first halves on every view's stream: nothing waits for any count yet.  Breadth first: every
         // view's preprocess is enqueued before any view's depth sort, so the views' chains start together
         // (view by view, the last view's preprocess started ~200 us of host issue after the first's and
@@ -1453,13 +1321,7 @@ int gs_views_forward(int n, const gs_settings* const* s, const gs_params* const*
             if (rc) return rc;
         }
         // second halves: a speculated view's binning runs on the device count, capped at its capacity;
-        // the others wait for their count here (the reference's sync, rasterizer_impl.cu:236-239).  The
-        // blends: one batched launch (views_batch_forward) when every view renders (same kind, <= 4)
-        bool batch_fwd = views_forward_mode() >= 1 && n >= 2 && n <= kRenderBatch;
-        for (int v = 0; v < n && batch_fwd; ++v)
-            batch_fwd = h->f[v].gp.P > 0 && h->f[v].s.debug == 0 && h->f[v].gp.forward_only == h->f[0].gp.forward_only;
-        RenderArgs ras[kRenderBatch];
-        int nras = 0;
+        // the others wait for their count here (the reference's sync, rasterizer_impl.cu:236-239)
         for (int v = 0; v < n; ++v) {
             FwdState& f = h->f[v];
             hipStream_t stream = (hipStream_t)streams[v];
@@ -1470,52 +1332,24 @@ int gs_views_forward(int n, const gs_settings* const* s, const gs_params* const*
                 h->K[v] = 0;
                 continue;
             }
-            uint32_t layout = 0;
-            int order_ready = 0;
             if (h->spec[v]) {
                 h->bin[v] = base + off_bin[v];
                 const uint32_t* counters = at<uint32_t>(f.img, img_layout(g.W, g.H).counters);
                 rc = bin_emit(f, h->bin[v], h->layout[v], counters, stream);
                 if (rc) return rc;
-                layout = h->layout[v];
-                order_ready = tile_sort_writes_ranges(g.tiles) || f.ea.xhist ? 1 : 0;
+                rc = render_launch(f, h->bin[v], h->layout[v], tile_sort_writes_ranges(g.tiles) || f.ea.xhist ? 1 : 0,
+                                   out_color[v], out_depth[v], stream);
             } else {
                 int K = 0;
                 rc = bin_end(f, alloc, alloc_ctx, stream, &h->bin[v], &K, 16 + v);
                 if (rc) return rc;
                 h->K[v] = K;
                 h->layout[v] = (uint32_t)K;
-                layout = (uint32_t)K;
-                order_ready = K > 0 && (tile_sort_writes_ranges(g.tiles) || f.ea.xhist) ? 1 : 0;
+                rc = render_launch(f, h->bin[v], (uint32_t)K,
+                                   K > 0 && (tile_sort_writes_ranges(g.tiles) || f.ea.xhist) ? 1 : 0, out_color[v],
+                                   out_depth[v], stream);
             }
-            if (batch_fwd) {
-                ras[nras++] = render_args(f, h->bin[v], layout, order_ready, out_color[v], out_depth[v]);
-            } else {
-                rc = render_launch(f, h->bin[v], layout, order_ready, out_color[v], out_depth[v], stream);
-                if (rc) return rc;
-            }
-        }
-        if (nras) {
-            // the views' blends as ONE launch on the first view's stream, once every view's binning is done
-            // (their heaviest quadrants' tails then overlap in one grid instead of three contending ones)
-            hipStream_t s0 = (hipStream_t)streams[0];
-            for (int v = 1; v < n; ++v) {
-                hipStream_t sv = (hipStream_t)streams[v];
-                if (sv == s0) continue;
-                if (!h->ev[v] && !(h->ev[v] = event_pool().get())) return set_error(GS_ERR_HIP, "could not create an event");
-                GS_HIP(hipEventRecord(h->ev[v], sv));
-                GS_HIP(hipStreamWaitEvent(s0, h->ev[v], 0));
-            }
-            {
-                const bool debug = false;
-                hipStream_t stream = s0;  // (GS_LAUNCHED)
-                GS_SKIP("fwd") { StageScope sc(ST_RENDER_FWD, s0); launch_render_forward_views(ras, nras, s0); }
-                GS_LAUNCHED("render (views)");
-            }
-            if (!h->pre && !(h->pre = event_pool().get())) return set_error(GS_ERR_HIP, "could not create an event");
-            GS_HIP(hipEventRecord(h->pre, s0));
-            for (int v = 1; v < n; ++v)
-                if ((hipStream_t)streams[v] != s0) GS_HIP(hipStreamWaitEvent((hipStream_t)streams[v], h->pre, 0));
+            if (rc) return rc;
         }
         rc = join_into(h.get(), join, streams);
         if (rc) return rc;
@@ -1600,19 +1434,7 @@ int gs_views_backward(gs_views* h, const float* const* dL_dpix, const gs_grads* 
             hipStream_t s0 = (hipStream_t)streams[0];
             const bool debug = h->f[0].s.debug != 0;
             hipStream_t stream = s0;  // (GS_LAUNCHED)
-            // the replays: one batched launch on the first stream (views_forward_mode 2), or one per stream
-            bool batch = views_forward_mode() == 2 && h->n <= kRenderBatch && !debug;
-            for (int v = 0; v < h->n && batch; ++v) batch = h->f[v].gp.P > 0 && h->layout[v] > 0;
-            if (batch) {
-                RenderBwdArgs rbs[kRenderBatch];
-                for (int v = 0; v < h->n; ++v) {
-                    FwdState& f = h->f[v];
-                    rbs[v] = replay_args(&f.s, &f.gp, (int)h->layout[v], f.geom, h->bin[v], f.img, dL_dpix[v]);
-                }
-                GS_SKIP("rbwd") { StageScope sc(ST_RENDER_BWD, s0); launch_render_backward_views(rbs, h->n, s0); }
-                GS_LAUNCHED("render backward (views)");
-            }
-            for (int v = 0; v < h->n && !batch; ++v) {
+            for (int v = 0; v < h->n; ++v) {
                 FwdState& f = h->f[v];
                 hipStream_t sv = (hipStream_t)streams[v];
                 int rc = replay_view(&f.s, &f.gp, (int)h->layout[v], f.geom, h->bin[v], f.img, dL_dpix[v], sv);

@@ -265,13 +265,6 @@ void launch_mark_visible(int P, const float* means3D, const float* view, uint8_t
 void launch_activate_params(int P, const float* raw_opacity, const float* raw_scaling, const float* raw_rotation,
                             float* opacity, float* scaling, float* rotation, hipStream_t s);
 
-// A batch of views whose buffers sit `stride` bytes apart (gs_views_forward: one allocation of equal
-// per-view layouts): the kernels run grid.y = n over them, offsetting view 0's pointers
-struct ViewBatch {
-    int n = 1;
-    size_t stride = 0;
-};
-
 // LSD radix sort of (u32 key, u32 value).  Returns the buffer index (0/1)
 // holding the result.  identity_vals: values of the first pass are the
 // element indices (val0 is not read).
@@ -280,7 +273,7 @@ struct ViewBatch {
 int radix_sort_aux(uint32_t* key0, uint32_t* key1, uint2* pair0, uint2* pair1, const uint32_t* aux, uint32_t n,
                    int bits, int max_pass_bits, int ipt, uint32_t* hist, uint32_t* totals, int nblocks, hipStream_t s,
                    uint2* ranges = nullptr, const uint32_t* key_bias_not = nullptr, uint32_t* tile_order = nullptr,
-                   int ntiles = 0, const uint32_t* n_dev = nullptr, const ViewBatch& vb = ViewBatch());
+                   int ntiles = 0, const uint32_t* n_dev = nullptr);
 // key_bias_not: the preprocess counter slots' ~min key (kCounterStride apart); the first pass sorts
 // (and writes) key - min
 // Stable sort of the K emitted instances on their tile id (key0 in slot
@@ -289,8 +282,7 @@ int radix_sort_aux(uint32_t* key0, uint32_t* key1, uint2* pair0, uint2* pair1, c
 int tile_sort(uint32_t* key0, uint32_t* key1, uint2* pair0, uint2* pair1, const uint32_t* gauss_by_slot, uint32_t n,
               int bits, uint32_t* hist, uint32_t* totals, int nblocks, hipStream_t s, uint2* ranges,
               uint32_t* tile_order, int ntiles,  // tile_order: the forward's dispatch order (single pass only)
-              const uint32_t* n_dev = nullptr,  // n_dev: preprocess counters, n = min(count, n) read on the device
-              const ViewBatch& vb = ViewBatch());
+              const uint32_t* n_dev = nullptr);  // n_dev: preprocess counters, n = min(count, n) read on the device
 // the single-pass tile sort writes the tile ranges itself (and no sorted keys); two passes need k_ranges
 inline bool tile_sort_writes_ranges(int num_tiles) { return tile_sort_plan(num_tiles).passes == 1; }
 
@@ -329,10 +321,9 @@ struct EmitArgs {
     // ids_only (a forward-only render's two-level binning): the lists carry the Gaussian id alone (u32 at
     // pairs_out / the point list) — the binning slot is only the backward's record address
     int ids_only = 0;
-    size_t vstride = 0;  // a batch of views (grid.y): view v's buffers at + v * vstride (see ViewBatch)
 };
-void launch_scan_reduce(const EmitArgs& a, hipStream_t s, int nviews = 1);
-void launch_scan_emit(const EmitArgs& a, hipStream_t s, int nviews = 1);
+void launch_scan_reduce(const EmitArgs& a, hipStream_t s);
+void launch_scan_emit(const EmitArgs& a, hipStream_t s);
 // two-level binning after the instance count is known: column scan + k_scan_emit_x, the row pass
 // (pairs_out/tile_key -> point_pairs, per-tile counts), ranges from the counts
 void launch_emit_fused(const EmitArgs& a, hipStream_t s);
@@ -380,14 +371,6 @@ struct RenderArgs {
     const float* colors = nullptr;  // forward-only: blend these [P,3] colours instead of the Splats' (recolor)
 };
 void launch_render_forward(const RenderArgs& a, hipStream_t s);
-// n views' blends in one launch (the views' tiles of one rank interleaved, every view's longest lists
-// first); every view must be a training (bwd) render or every one forward-only
-constexpr int kRenderBatch = 4;
-struct RenderBatch {
-    RenderArgs v[kRenderBatch];
-    int n;
-};
-void launch_render_forward_views(const RenderArgs* v, int n, hipStream_t s);
 
 struct ApplyWeightsArgs {
     int W, H, gx, gy, C;
@@ -422,12 +405,6 @@ struct RenderBwdArgs {
     uint64_t* diag;   // optional [item_cap][kDiagWords], by queue position (see diag_buffer)
 };
 void launch_render_backward(const RenderBwdArgs& a, hipStream_t s);
-// n views' replays in one launch (their items interleaved, every view's heaviest first)
-struct RenderBwdBatch {
-    RenderBwdArgs v[kRenderBatch];
-    int n;
-};
-void launch_render_backward_views(const RenderBwdArgs* v, int n, hipStream_t s);
 
 struct GaussBwdArgs {
     int P, D, M, W, H, gx, gy;

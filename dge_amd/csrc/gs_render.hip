@@ -241,16 +241,12 @@ __device__ __forceinline__ void emit_items(const RenderArgs& a, int tile, int qu
 // BWD: the backward's bookkeeping (checkpoints, blended bits, touched bytes, the replay's work list);
 // a forward no backward follows (gs_params.forward_only) runs without it
 template <bool BWD>
-__global__ __launch_bounds__(64, 3) void k_render_fwd(RenderBatch rb) {
+__global__ __launch_bounds__(64, 3) void k_render_fwd(RenderArgs a) {
     // XCD-aware: blocks b, b+8, b+16, b+24 (one XCD under the round-robin dealing) take the four
     // quadrants of one tile, so the tile's list and its Splat gathers are fetched into one L2;
-    // tiles in k_tile_order's order, longest list first.  A batch of views (one launch for a step's
-    // views, gs_views_forward): the views' tiles of one rank follow each other, so every view's
-    // longest lists start first
+    // tiles in k_tile_order's order, longest list first
     const int x8 = blockIdx.x & 7, j8 = blockIdx.x >> 3;
-    const int quad = j8 & 3, r2 = j8 >> 2;
-    const int view = r2 % rb.n, rank = (r2 / rb.n) * 8 + x8;
-    const RenderArgs& a = rb.v[view];
+    const int quad = j8 & 3, rank = (j8 >> 2) * 8 + x8;
     if (rank >= a.gx * a.gy) return;
     const int tile = (int)a.tile_order[rank];
     const int qidx = 4 * tile + quad;
@@ -559,27 +555,15 @@ __global__ __launch_bounds__(64, 3) void k_render_fwd(RenderBatch rb) {
     }
 }
 
-void launch_render_forward_views(const RenderArgs* v, int n, hipStream_t s) {
-    RenderBatch rb;
-    rb.n = 0;
-    int tiles = 0;
-    for (int i = 0; i < n; ++i) {
-        const int t = v[i].gx * v[i].gy;
-        if (t <= 0) continue;
-        if (!v[i].order_ready)
-            hipLaunchKernelGGL(k_tile_order, dim3(1), dim3(1024), 0, s, v[i].ranges, t, v[i].tile_order);
-        rb.v[rb.n++] = v[i];
-        tiles = t > tiles ? t : tiles;
-    }
-    if (rb.n == 0) return;
-    const dim3 grid(div_up(tiles, 8) * 32 * rb.n);
-    if (rb.v[0].bwd)
-        hipLaunchKernelGGL(k_render_fwd<true>, grid, dim3(64), 0, s, rb);
+void launch_render_forward(const RenderArgs& a, hipStream_t s) {
+    const int tiles = a.gx * a.gy;
+    if (tiles <= 0) return;
+    if (!a.order_ready) hipLaunchKernelGGL(k_tile_order, dim3(1), dim3(1024), 0, s, a.ranges, tiles, a.tile_order);
+    if (a.bwd)
+        hipLaunchKernelGGL(k_render_fwd<true>, dim3(div_up(tiles, 8) * 32), dim3(64), 0, s, a);
     else
-        hipLaunchKernelGGL(k_render_fwd<false>, grid, dim3(64), 0, s, rb);
+        hipLaunchKernelGGL(k_render_fwd<false>, dim3(div_up(tiles, 8) * 32), dim3(64), 0, s, a);
 }
-
-void launch_render_forward(const RenderArgs& a, hipStream_t s) { launch_render_forward_views(&a, 1, s); }
 
 // =====================================================================
 // apply_weights: same traversal, per blended pair add image weights
@@ -766,7 +750,7 @@ static_assert(kSegLen % kBwdHalf == 0, "whole staging units per segment");
 // sums are reduce-scattered across the wave (quad_reduce).  Each kept entry gets
 // one record at 4*slot + quadrant (slot: the binning slot, so k_gauss_bwd reads
 // a Gaussian's records contiguously) and a flag.
-__global__ __launch_bounds__(64, GS_BWD_WAVES) void k_render_bwd(RenderBwdBatch rbb) {
+__global__ __launch_bounds__(64, GS_BWD_WAVES) void k_render_bwd(RenderBwdArgs a) {
     // kept entries of a half-segment, compacted back to front, + a group of padding
     // (one array per field: four consecutive entries' field is one 16-B read, see bwd_quad)
     __shared__ __attribute__((aligned(16))) float s_x[kBwdHalf + kBwdGroup], s_y[kBwdHalf + kBwdGroup];
@@ -780,16 +764,13 @@ __global__ __launch_bounds__(64, GS_BWD_WAVES) void k_render_bwd(RenderBwdBatch 
     // block -> work item (quadrant, segment) of the forward's list, heaviest class first; blocks past
     // the list's end exit (they dispatch after every real item; see launch_render_backward for the
     // grid).  (A persistent-wave work queue measured slower than the hardware dispatcher here.)
-    // (a batch of views in one launch: block b takes item b / n of view b % n — the views' heaviest
-    // items first, interleaved)
-    const RenderBwdArgs& a = rbb.v[blockIdx.x % rbb.n];
     uint32_t n_cls[kItemClasses], n_items = 0;
 #pragma unroll
     for (int c = 0; c < kItemClasses; ++c) {
         n_cls[c] = a.bwd_count[item_count_at(c)];
         n_items += n_cls[c];
     }
-    const uint32_t qi = blockIdx.x / rbb.n;
+    const uint32_t qi = blockIdx.x;
     if (qi >= n_items) return;
     uint32_t cls = 0, idx = qi;  // class regions in order: heaviest items first
 #pragma unroll
@@ -959,19 +940,10 @@ __global__ __launch_bounds__(64, GS_BWD_WAVES) void k_render_bwd(RenderBwdBatch 
 
 // One workgroup per possible item (the bound, 4 x checkpoint slots, is ~7x the c2 count): the surplus
 // workgroups exit at once and cost nothing measurable (render_bwd 104 us either way).
-void launch_render_backward_views(const RenderBwdArgs* v, int n, hipStream_t s) {
-    RenderBwdBatch rbb;
-    rbb.n = 0;
-    uint32_t cap = 0;
-    for (int i = 0; i < n; ++i) {
-        if (v[i].gx * v[i].gy <= 0 || v[i].item_cap == 0) continue;
-        rbb.v[rbb.n++] = v[i];
-        cap = v[i].item_cap > cap ? v[i].item_cap : cap;
-    }
-    if (rbb.n == 0) return;
-    hipLaunchKernelGGL(k_render_bwd, dim3(cap * (uint32_t)rbb.n), dim3(64), 0, s, rbb);
+void launch_render_backward(const RenderBwdArgs& a, hipStream_t s) {
+    const int tiles = a.gx * a.gy;
+    if (tiles <= 0 || a.item_cap == 0) return;
+    hipLaunchKernelGGL(k_render_bwd, dim3(a.item_cap), dim3(64), 0, s, a);
 }
-
-void launch_render_backward(const RenderBwdArgs& a, hipStream_t s) { launch_render_backward_views(&a, 1, s); }
 
 }  // namespace gs

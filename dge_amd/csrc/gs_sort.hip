@@ -28,12 +28,6 @@ namespace gs {
 // ---------------------------------------------------------------------
 // helpers
 // ---------------------------------------------------------------------
-// A batch of views (gs_views_forward): view blockIdx.y's buffers sit vstride bytes after view 0's (one
-// allocation, equal per-view layouts), so a kernel takes view 0's pointers and offsets them
-template <class T>
-__device__ __forceinline__ T* vview(T* p, size_t vstride) {
-    return p ? reinterpret_cast<T*>(reinterpret_cast<uintptr_t>(p) + (size_t)blockIdx.y * vstride) : p;
-}
 template <int BITS>
 __device__ __forceinline__ uint64_t match_digit(uint32_t d, uint64_t valid_mask) {
     uint64_t m = valid_mask;
@@ -126,12 +120,8 @@ template <int BITS, int IPT>
 __global__ __launch_bounds__(256) void k_radix_hist(const uint32_t* __restrict__ keys, uint32_t n, int shift,
                                                     uint32_t* __restrict__ hist, int nb, int bm,
                                                     const uint32_t* __restrict__ bias_not,
-                                                    const uint32_t* __restrict__ n_dev, size_t vstride) {
+                                                    const uint32_t* __restrict__ n_dev) {
     constexpr int NDIG = 1 << BITS;
-    keys = vview(keys, vstride);
-    hist = vview(hist, vstride);
-    bias_not = vview(bias_not, vstride);
-    n_dev = vview(n_dev, vstride);
     __shared__ uint32_t cnt[NDIG];
     const int tid = threadIdx.x;
     n = dev_count(n_dev, n);
@@ -165,11 +155,8 @@ constexpr int kScanBmRows = kScanGroups * kScanRegs;  // block-major tables up t
 __global__ __launch_bounds__(1024) void k_radix_digit_scan(uint32_t* __restrict__ hist, int nb, int ndig,
                                                            uint32_t* __restrict__ totals,
                                                            const uint32_t* __restrict__ n_dev, uint32_t cap,
-                                                           int tile, size_t vstride) {
+                                                           int tile) {
     __shared__ uint32_t part[kScanGroups][kScanDigits];
-    hist = vview(hist, vstride);
-    totals = vview(totals, vstride);
-    n_dev = vview(n_dev, vstride);
     if (n_dev) nb = max(1, div_up_u(dev_count(n_dev, cap), (uint32_t)tile));  // rows the histogram wrote
     const int dl = threadIdx.x & (kScanDigits - 1), g = threadIdx.x / kScanDigits;
     const int d = blockIdx.x * kScanDigits + dl;
@@ -226,11 +213,8 @@ __global__ __launch_bounds__(1024) void k_radix_digit_scan(uint32_t* __restrict_
 __global__ __launch_bounds__(256) void k_radix_digit_scan_dm(uint32_t* __restrict__ hist, int nb,
                                                              uint32_t* __restrict__ totals,
                                                              const uint32_t* __restrict__ n_dev, uint32_t cap,
-                                                             int tile, size_t vstride) {
+                                                             int tile) {
     __shared__ uint32_t lds4[4];
-    hist = vview(hist, vstride);
-    totals = vview(totals, vstride);
-    n_dev = vview(n_dev, vstride);
     uint32_t* row = hist + (size_t)blockIdx.x * nb;  // (digit-major: the row pitch stays the grid's nb)
     if (n_dev) nb = max(1, div_up_u(dev_count(n_dev, cap), (uint32_t)tile));
     // each wave scans a contiguous quarter of the row in coalesced 64-element chunks (loads issued
@@ -316,20 +300,8 @@ __global__ __launch_bounds__(256) void k_radix_scatter(const uint32_t* __restric
                                                        const uint32_t* __restrict__ totals, int nb, int bm,
                                                        RangeOut ro,
                                                        const uint32_t* __restrict__ bias_not,
-                                                       const uint32_t* __restrict__ n_dev, size_t vstride) {
+                                                       const uint32_t* __restrict__ n_dev) {
     using V = typename std::conditional<VM == kValU32, uint32_t, uint2>::type;
-    keys_in = vview(keys_in, vstride);
-    vals_in_ = vview(vals_in_, vstride);
-    keys_out = vview(keys_out, vstride);
-    vals_out_ = vview(vals_out_, vstride);
-    gauss_by_slot = vview(gauss_by_slot, vstride);
-    hist = vview(hist, vstride);
-    totals = vview(totals, vstride);
-    ro.ranges = vview(ro.ranges, vstride);
-    ro.tile_order = vview(ro.tile_order, vstride);
-    ro.tile_count = vview(ro.tile_count, vstride);
-    bias_not = vview(bias_not, vstride);
-    n_dev = vview(n_dev, vstride);
     n = dev_count(n_dev, n);
     const uint32_t* vals_in = static_cast<const uint32_t*>(vals_in_);
     const uint2* pairs_in = static_cast<const uint2*>(vals_in_);
@@ -495,33 +467,29 @@ __global__ __launch_bounds__(256) void k_radix_scatter(const uint32_t* __restric
 template <int BITS, int IPT>
 static void radix_pass(const uint32_t* kin, const void* vin, uint32_t* kout, void* vout, const uint32_t* gauss_by_slot,
                        uint32_t n, int shift, bool idv, int vm, uint32_t* hist, uint32_t* totals, int nb,
-                       RangeOut ro, const uint32_t* bias_not, hipStream_t s, const uint32_t* n_dev = nullptr,
-                       const ViewBatch& vb = ViewBatch()) {
+                       RangeOut ro, const uint32_t* bias_not, hipStream_t s, const uint32_t* n_dev = nullptr) {
     // n_dev: the element count is read on the device (capped at n, the capacity the grid nb covers)
-    // vb: the same pass over vb.n views' buffers, vb.stride bytes apart (grid.y = view)
     constexpr int NDIG = 1 << BITS;
     const int bm = nb <= kScanBmRows ? 1 : 0;
-    const size_t vs = vb.stride;
-    hipLaunchKernelGGL((k_radix_hist<BITS, IPT>), dim3(nb, vb.n), dim3(256), 0, s, kin, n, shift, hist, nb, bm,
-                       bias_not, n_dev, vs);
+    hipLaunchKernelGGL((k_radix_hist<BITS, IPT>), dim3(nb), dim3(256), 0, s, kin, n, shift, hist, nb, bm, bias_not,
+                       n_dev);
     if (bm)
-        hipLaunchKernelGGL(k_radix_digit_scan, dim3(div_up(NDIG, kScanDigits), vb.n), dim3(1024), 0, s, hist, nb, NDIG,
-                           totals, n_dev, n, 256 * IPT, vs);
+        hipLaunchKernelGGL(k_radix_digit_scan, dim3(div_up(NDIG, kScanDigits)), dim3(1024), 0, s, hist, nb, NDIG,
+                           totals, n_dev, n, 256 * IPT);
     else
-        hipLaunchKernelGGL(k_radix_digit_scan_dm, dim3(NDIG, vb.n), dim3(256), 0, s, hist, nb, totals, n_dev, n,
-                           256 * IPT, vs);
+        hipLaunchKernelGGL(k_radix_digit_scan_dm, dim3(NDIG), dim3(256), 0, s, hist, nb, totals, n_dev, n, 256 * IPT);
 #define GS_SCATTER(IDV, VM)                                                                                   \
-    hipLaunchKernelGGL((k_radix_scatter<BITS, IPT, IDV, VM>), dim3(nb, vb.n), dim3(256), 0, s, kin, vin, kout,  \
-                       vout, gauss_by_slot, n, shift, hist, totals, nb, bm, ro, bias_not, n_dev, vs)
+    hipLaunchKernelGGL((k_radix_scatter<BITS, IPT, IDV, VM>), dim3(nb), dim3(256), 0, s, kin, vin, kout, vout,  \
+                       gauss_by_slot, n, shift, hist, totals, nb, bm, ro, bias_not, n_dev)
     if (vm == kValPair && !kout)  // the two-level binning's row pass: no sorted keys
-        hipLaunchKernelGGL((k_radix_scatter<BITS, IPT, false, kValPair, false, true>), dim3(nb, vb.n), dim3(256), 0, s,
-                           kin, vin, kout, vout, gauss_by_slot, n, shift, hist, totals, nb, bm, ro, bias_not, n_dev, vs);
+        hipLaunchKernelGGL((k_radix_scatter<BITS, IPT, false, kValPair, false, true>), dim3(nb), dim3(256), 0, s, kin,
+                           vin, kout, vout, gauss_by_slot, n, shift, hist, totals, nb, bm, ro, bias_not, n_dev);
     else if (vm == kValU32 && !kout && ro.tile_count)  // the same over Gaussian ids alone (ids_only)
-        hipLaunchKernelGGL((k_radix_scatter<BITS, IPT, false, kValU32, false, true>), dim3(nb, vb.n), dim3(256), 0, s,
-                           kin, vin, kout, vout, gauss_by_slot, n, shift, hist, totals, nb, bm, ro, bias_not, n_dev, vs);
+        hipLaunchKernelGGL((k_radix_scatter<BITS, IPT, false, kValU32, false, true>), dim3(nb), dim3(256), 0, s, kin,
+                           vin, kout, vout, gauss_by_slot, n, shift, hist, totals, nb, bm, ro, bias_not, n_dev);
     else if (vm == kValPairFirst && !kout)  // the last tile-sort pass: no sorted keys
-        hipLaunchKernelGGL((k_radix_scatter<BITS, IPT, true, kValPairFirst, false>), dim3(nb, vb.n), dim3(256), 0, s,
-                           kin, vin, kout, vout, gauss_by_slot, n, shift, hist, totals, nb, bm, ro, bias_not, n_dev, vs);
+        hipLaunchKernelGGL((k_radix_scatter<BITS, IPT, true, kValPairFirst, false>), dim3(nb), dim3(256), 0, s, kin,
+                           vin, kout, vout, gauss_by_slot, n, shift, hist, totals, nb, bm, ro, bias_not, n_dev);
     else if (vm == kValPairFirst) GS_SCATTER(true, kValPairFirst);
     else if (vm == kValPair) GS_SCATTER(false, kValPair);
     else if (idv) GS_SCATTER(true, kValU32);
@@ -532,13 +500,13 @@ static void radix_pass(const uint32_t* kin, const void* vin, uint32_t* kout, voi
 static void radix_pass_bits(int bits, int ipt, const uint32_t* kin, const void* vin, uint32_t* kout, void* vout,
                             const uint32_t* gauss_by_slot, uint32_t n, int shift, bool idv, int vm, uint32_t* hist,
                             uint32_t* totals, int nb, RangeOut ro, const uint32_t* bias_not, hipStream_t s,
-                            const uint32_t* n_dev, const ViewBatch& vb) {
+                            const uint32_t* n_dev) {
 #define GS_CASE(B)                                                                                              \
     case B:                                                                                                     \
         if (ipt == kDepthSortIPT)                                                                               \
-            radix_pass<B, kDepthSortIPT>(kin, vin, kout, vout, gauss_by_slot, n, shift, idv, vm, hist, totals, nb, ro, bias_not, s, n_dev, vb); \
+            radix_pass<B, kDepthSortIPT>(kin, vin, kout, vout, gauss_by_slot, n, shift, idv, vm, hist, totals, nb, ro, bias_not, s, n_dev); \
         else                                                                                                    \
-            radix_pass<B, kSortIPT>(kin, vin, kout, vout, gauss_by_slot, n, shift, idv, vm, hist, totals, nb, ro, bias_not, s, n_dev, vb); \
+            radix_pass<B, kSortIPT>(kin, vin, kout, vout, gauss_by_slot, n, shift, idv, vm, hist, totals, nb, ro, bias_not, s, n_dev); \
         break;
     switch (bits) {
         GS_CASE(1) GS_CASE(2) GS_CASE(3) GS_CASE(4) GS_CASE(5) GS_CASE(6)
@@ -559,7 +527,7 @@ static int pass_bits(int begin_bit, int end_bit, int max_pass_bits, int p, int& 
 int radix_sort_aux(uint32_t* key0, uint32_t* key1, uint2* pair0, uint2* pair1, const uint32_t* aux, uint32_t n,
                    int bits, int max_pass_bits, int ipt, uint32_t* hist, uint32_t* totals, int nblocks, hipStream_t s,
                    uint2* ranges, const uint32_t* key_bias_not, uint32_t* tile_order, int ntiles,
-                   const uint32_t* n_dev, const ViewBatch& vb) {
+                   const uint32_t* n_dev) {
     uint32_t* k[2] = {key0, key1};
     uint2* v[2] = {pair0, pair1};
     int cur = 0;
@@ -576,7 +544,7 @@ int radix_sort_aux(uint32_t* key0, uint32_t* key1, uint2* pair0, uint2* pair1, c
         radix_pass_bits(b, ipt, k[cur], v[cur], ranges_here ? nullptr : k[cur ^ 1], v[cur ^ 1], aux, n, shift,
                         p == 0, p == 0 ? kValPairFirst : kValPair, hist, totals, nblocks,
                         RangeOut{ranges_here ? ranges : nullptr, ranges_here ? tile_order : nullptr, ntiles},
-                        p == 0 ? key_bias_not : nullptr, s, n_dev, vb);
+                        p == 0 ? key_bias_not : nullptr, s, n_dev);
         cur ^= 1;
         shift += b;
     }
@@ -585,9 +553,9 @@ int radix_sort_aux(uint32_t* key0, uint32_t* key1, uint2* pair0, uint2* pair1, c
 
 int tile_sort(uint32_t* key0, uint32_t* key1, uint2* pair0, uint2* pair1, const uint32_t* gauss_by_slot, uint32_t n,
               int bits, uint32_t* hist, uint32_t* totals, int nblocks, hipStream_t s, uint2* ranges,
-              uint32_t* tile_order, int ntiles, const uint32_t* n_dev, const ViewBatch& vb) {
+              uint32_t* tile_order, int ntiles, const uint32_t* n_dev) {
     return radix_sort_aux(key0, key1, pair0, pair1, gauss_by_slot, n, bits, kMaxSinglePassBits, kSortIPT, hist, totals,
-                          nblocks, s, ranges, nullptr, tile_order, ntiles, n_dev, vb);
+                          nblocks, s, ranges, nullptr, tile_order, ntiles, n_dev);
 }
 
 // ---------------------------------------------------------------------
@@ -601,28 +569,8 @@ __device__ __forceinline__ uint32_t rect_count(uint32_t v, int packed) {
 
 // Block sums of the instance counts in depth order (k_scan_emit derives each
 // block's first slot from them).
-// (a batch of views: EmitArgs::vstride, grid.y = view)
-__device__ __forceinline__ void emit_view(EmitArgs& a) {
-    const size_t vs = a.vstride;
-    if (!vs) return;
-    a.order = vview(a.order, vs);
-    a.tiles_touched = vview(a.tiles_touched, vs);
-    a.splat = vview(a.splat, vs);
-    a.radii = vview(a.radii, vs);
-    a.scan_sums = vview(a.scan_sums, vs);
-    a.first_slot = vview(a.first_slot, vs);
-    a.tile_key = vview(a.tile_key, vs);
-    a.slot_gauss = vview(a.slot_gauss, vs);
-    a.rec_flags32 = vview(a.rec_flags32, vs);
-    a.xhist = vview(a.xhist, vs);
-    a.xtotals = vview(a.xtotals, vs);
-    a.pairs_out = vview(a.pairs_out, vs);
-    a.tile_count = vview(a.tile_count, vs);
-}
-
 __global__ __launch_bounds__(256) void k_scan_reduce(EmitArgs a) {
     __shared__ uint32_t lds4[4];
-    emit_view(a);
     uint32_t s = 0;
     const uint32_t base = blockIdx.x * (uint32_t)kScanTile;
     // (clamped loads, all issued before the first use: a guarded load per iteration was waited
@@ -666,7 +614,6 @@ __global__ __launch_bounds__(256) void k_scan_reduce(EmitArgs a) {
 // per Gaussian instead).
 __global__ __launch_bounds__(256) void k_scan_emit(EmitArgs a) {
     __shared__ uint32_t lds4[4];
-    emit_view(a);
     __shared__ uint32_t s_start[256];
     __shared__ uint32_t s_gauss[256];
     __shared__ int4 s_rect[256];  // x0, y0, width, -
@@ -754,7 +701,6 @@ template <bool IDS>
 __global__ __launch_bounds__(256) void k_scan_emit_x(EmitArgs a) {
     using PV = typename std::conditional<IDS, uint32_t, uint2>::type;
     __shared__ uint32_t lds4[4];
-    emit_view(a);
     __shared__ uint32_t s_start[256];
     __shared__ uint32_t s_gauss[256];
     __shared__ int4 s_rect[256];
@@ -966,7 +912,7 @@ void launch_emit_fused(const EmitArgs& a, hipStream_t s) {
     if (a.P <= 0) return;
     // first level: column totals and each block's column offsets, then the column-ordered emission
     hipLaunchKernelGGL(k_radix_digit_scan, dim3(kXDigits / kScanDigits), dim3(1024), 0, s, a.xhist, a.scan_blocks,
-                       kXDigits, a.xtotals, (const uint32_t*)nullptr, 0u, 1, (size_t)0);
+                       kXDigits, a.xtotals, (const uint32_t*)nullptr, 0u, 1);
     if (a.ids_only)
         hipLaunchKernelGGL(k_scan_emit_x<true>, dim3(a.scan_blocks), dim3(256), 0, s, a);
     else
@@ -983,14 +929,14 @@ void launch_row_pass(const EmitArgs& a, uint32_t K, uint2* point_pairs, uint32_t
     hipLaunchKernelGGL(k_ranges_counts, dim3(1), dim3(256), 0, s, a.tile_count, a.ntiles, ranges, tile_order);
 }
 
-void launch_scan_reduce(const EmitArgs& a, hipStream_t s, int nviews) {
+void launch_scan_reduce(const EmitArgs& a, hipStream_t s) {
     if (a.P <= 0) return;
-    hipLaunchKernelGGL(k_scan_reduce, dim3(a.scan_blocks, nviews), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_scan_reduce, dim3(a.scan_blocks), dim3(256), 0, s, a);
 }
 
-void launch_scan_emit(const EmitArgs& a, hipStream_t s, int nviews) {
+void launch_scan_emit(const EmitArgs& a, hipStream_t s) {
     if (a.P <= 0) return;
-    hipLaunchKernelGGL(k_scan_emit, dim3(a.scan_blocks, nviews), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_scan_emit, dim3(a.scan_blocks), dim3(256), 0, s, a);
 }
 
 // ---------------------------------------------------------------------
