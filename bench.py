@@ -705,10 +705,11 @@ def cpu_baseline(scene, cam, seed, bg, args):
             break
     model = ""
     try:
-        for ln in open("/proc/cpuinfo"):
-            if ln.startswith("model name"):
-                model = ln.split(":", 1)[1].strip()
-                break
+        with open("/proc/cpuinfo") as fh:
+            for ln in fh:
+                if ln.startswith("model name"):
+                    model = ln.split(":", 1)[1].strip()
+                    break
     except OSError:
         pass
     return {"value": round(n / el, 4), "unit": "renders/s", "cores": threads, "kind": "port", "cpu_model": model,
@@ -722,7 +723,8 @@ def _usable_cpus():
     aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
     quota = None
     try:
-        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        with open("/sys/fs/cgroup/cpu.max") as fh:
+            q, per = fh.read().split()[:2]
         if q != "max":
             quota = max(1, int(int(q) // int(per)))
     except (OSError, ValueError):
