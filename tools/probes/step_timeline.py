@@ -2,7 +2,8 @@ import csv, sys
 import gzip
 rows=list(csv.DictReader((gzip.open(sys.argv[1], 'rt') if sys.argv[1].endswith('.gz') else open(sys.argv[1]))))
 rows.sort(key=lambda r:int(r['Start_Timestamp']))
-gb=[i for i,r in enumerate(rows) if 'k_gauss_bwd_live' in r['Kernel_Name']]
+marker = sys.argv[2] if len(sys.argv) > 2 else 'k_gauss_bwd_live'  # (one launch per step)
+gb=[i for i,r in enumerate(rows) if marker in r['Kernel_Name'] and 'k_gauss_bwd_live' not in r['Kernel_Name'].replace(marker, '', 1) or (marker == 'k_gauss_bwd_live' and 'k_gauss_bwd_live' in r['Kernel_Name'])]
 a,b=gb[-6],gb[-5]
 t0=int(rows[a]['Start_Timestamp'])
 busy=[]
