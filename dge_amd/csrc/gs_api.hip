@@ -1178,13 +1178,10 @@ struct gs_views {
     hipEvent_t ev[GS_MAX_VIEWS] = {};    // the end of each view's work (forward, or per-Gaussian backward pass)
     hipEvent_t fork = nullptr;           // the caller's stream, before the views' work
     hipEvent_t pre = nullptr;            // the end of the views' shared preprocess (k_preprocess_views)
-    int nchunks = 0;                     // gs_views_set_row_chunks: the per-Gaussian pass in row chunks
-    hipEvent_t chunk_ev[kMaxRowChunks] = {};  // chunk c's rows final (recorded by gs_views_backward)
     ~gs_views() {
         for (int v = 0; v < GS_MAX_VIEWS; ++v) event_pool().put(ev[v]);
         event_pool().put(fork);
         event_pool().put(pre);
-        for (int c = 0; c < kMaxRowChunks; ++c) event_pool().put(chunk_ev[c]);
     }
 };
 
@@ -1449,9 +1446,6 @@ int gs_views_backward(gs_views* h, const float* const* dL_dpix, const gs_grads* 
                 }
             }
             const int chunk = gauss_backward_max_views();
-            // row chunks (gs_views_set_row_chunks) split the batch's one pass; a batch of more views than
-            // one pass takes records them after its last pass
-            const bool rows_split = h->nchunks > 0 && h->n <= chunk;
             for (int v0 = 0; v0 < h->n; v0 += chunk) {
                 GaussBwdArgs ga[GS_MAX_VIEWS];
                 const int nv = std::min(chunk, h->n - v0);
@@ -1461,12 +1455,9 @@ int gs_views_backward(gs_views* h, const float* const* dL_dpix, const gs_grads* 
                                        grads[v0 + v], h->spec[v0 + v] ? h->layout[v0 + v] : 0xFFFFFFFFu);
                 }
                 GS_SKIP("gauss") { StageScope sc(ST_GAUSS_BWD, s0);
-                launch_gauss_backward_views(ga, nv, s0, v0 == 0 ? (hipEvent_t)writes_after : nullptr,
-                                            rows_split ? h->nchunks : 0, h->chunk_ev); }
+                launch_gauss_backward_views(ga, nv, s0, v0 == 0 ? (hipEvent_t)writes_after : nullptr); }
                 GS_LAUNCHED("gaussian backward (views)");
             }
-            if (!rows_split)
-                for (int c = 0; c < h->nchunks; ++c) GS_HIP(hipEventRecord(h->chunk_ev[c], s0));
             if (s0 != join) {
                 if (!h->ev[0] && !(h->ev[0] = event_pool().get())) return set_error(GS_ERR_HIP, "could not create an event");
                 GS_HIP(hipEventRecord(h->ev[0], s0));
@@ -1491,31 +1482,12 @@ int gs_views_backward(gs_views* h, const float* const* dL_dpix, const gs_grads* 
         }
         for (int v = 0; v < h->n; ++v)
             if (h->ev[v] && streams[v] != join_) GS_HIP(hipStreamWaitEvent(join, h->ev[v], 0));
-        for (int c = 0; c < h->nchunks; ++c) GS_HIP(hipEventRecord(h->chunk_ev[c], join));  // (every row at once)
         return GS_OK;
     } catch (const std::exception& e) {
         return set_error(GS_ERR_INVALID_ARG, "exception: %s", e.what());
     } catch (...) {
         return set_error(GS_ERR_INVALID_ARG, "unknown exception");
     }
-}
-
-int gs_views_set_row_chunks(gs_views* h, int n, long long* rows) {
-    if (!h || n < 0 || n > kMaxRowChunks || (n > 0 && !rows))
-        return set_error(GS_ERR_INVALID_ARG, "gs_views_set_row_chunks: handle, 0 <= n <= %d and rows[n + 1] required",
-                         kMaxRowChunks);
-    for (int c = 0; c < n; ++c)
-        if (!h->chunk_ev[c] && !(h->chunk_ev[c] = event_pool().get())) return set_error(GS_ERR_HIP, "could not create an event");
-    h->nchunks = n;
-    const int P = h->n > 0 ? h->f[0].gp.P : 0;
-    for (int c = 0; n > 0 && c <= n; ++c) rows[c] = gauss_backward_chunk_row(P, n, c);
-    return GS_OK;
-}
-
-int gs_views_chunk_wait(const gs_views* h, int c, gs_stream_t stream) {
-    if (!h || c < 0 || c >= h->nchunks) return set_error(GS_ERR_INVALID_ARG, "gs_views_chunk_wait: no chunk %d", c);
-    GS_HIP(hipStreamWaitEvent((hipStream_t)stream, h->chunk_ev[c], 0));
-    return GS_OK;
 }
 
 int gs_views_overflow(const gs_views* h, uint8_t* flag, gs_stream_t stream_) {

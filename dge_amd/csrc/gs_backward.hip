@@ -410,7 +410,6 @@ constexpr uint32_t kLiveIdMask = 0x0FFFFFFFu;  // live-list entry: Gaussian | vi
 struct GaussBwdViews {
     GaussBwdArgs v[kMaxBwdViews];
     int n;
-    int wg0 = 0;  // first workgroup of this launch (a row chunk of k_gauss_bwd_live, see launch_gauss_backward_views)
 };
 
 // ---------------------------------------------------------------------
@@ -673,8 +672,7 @@ __global__ __launch_bounds__(kGB) void k_gauss_bwd_live(GaussBwdViews m) {
     __shared__ uint32_t s_wave[kGB / 64];
     const int nsrc = (a.P + kGB - 1) / kGB;
     const int group = (nsrc + kLiveGrid - 1) / kLiveGrid < kLiveGroup ? (nsrc + kLiveGrid - 1) / kLiveGrid : kLiveGroup;
-    const int wg = (int)blockIdx.x + m.wg0;  // (a row chunk's launch starts at workgroup wg0)
-    const int sb0 = wg * group;
+    const int sb0 = blockIdx.x * group;
     if (threadIdx.x < kLiveGroup)
         s_pre[threadIdx.x + 1] = (int)threadIdx.x < group && sb0 + (int)threadIdx.x < nsrc ? a.live_count[sb0 + threadIdx.x] : 0u;
     __syncthreads();
@@ -743,31 +741,15 @@ __global__ __launch_bounds__(kGB) void k_gauss_bwd_live(GaussBwdViews m) {
     if (a.diag && (threadIdx.x & 63) == 0) {
         st[7] = __builtin_amdgcn_s_memrealtime();
         st[6] = count;  // live Gaussians of the workgroup
-        uint64_t* d = a.diag + kDiagWords * ((size_t)wg * 4 + (threadIdx.x >> 6));
+        uint64_t* d = a.diag + kDiagWords * ((size_t)blockIdx.x * 4 + (threadIdx.x >> 6));
 #pragma unroll
         for (int i = 0; i < 8; ++i) d[i] = st[i];
     }
 }
 
-// Workgroups of k_gauss_bwd_live for P Gaussians, and the rows workgroup w starts at
-static int gauss_bwd_group(int P) { return std::min(div_up(div_up(P, kGB), kLiveGrid), kLiveGroup); }
-static int gauss_bwd_workgroups(int P) { return div_up(div_up(P, kGB), gauss_bwd_group(P)); }
-
-// Row chunk c of nchunks: workgroups [c W / n, (c + 1) W / n) of the pass, rows from the first one's
-long long gauss_backward_chunk_row(int P, int nchunks, int c) {
-    if (P <= 0 || nchunks <= 0 || c <= 0) return 0;
-    if (c >= nchunks) return P;
-    const long long w = (long long)gauss_bwd_workgroups(P) * c / nchunks;
-    return std::min((long long)P, w * gauss_bwd_group(P) * kGB);
-}
-
-void launch_gauss_backward_views(const GaussBwdArgs* views, int n, hipStream_t s, hipEvent_t writes_after,
-                                 int nchunks, const hipEvent_t* chunk_done) {
+void launch_gauss_backward_views(const GaussBwdArgs* views, int n, hipStream_t s, hipEvent_t writes_after) {
     const GaussBwdArgs& a = views[0];
-    if (a.P <= 0 || n <= 0) {
-        for (int c = 0; c < nchunks; ++c) (void)hipEventRecord(chunk_done[c], s);
-        return;
-    }
+    if (a.P <= 0 || n <= 0) return;
     GaussBwdViews m;
     m.n = n < kMaxBwdViews ? n : kMaxBwdViews;
     for (int v = 0; v < m.n; ++v) m.v[v] = views[v];
@@ -775,23 +757,12 @@ void launch_gauss_backward_views(const GaussBwdArgs* views, int n, hipStream_t s
     hipLaunchKernelGGL(k_gauss_live, dim3(blocks), dim3(kGB), 0, s, m);
     // k_gauss_live writes only overwritten (per-call) outputs; the accumulated ones start here
     if (writes_after) (void)hipStreamWaitEvent(s, writes_after, 0);
-    const int nwg = gauss_bwd_workgroups(a.P);
-    if (nchunks <= 0) {
-        hipLaunchKernelGGL(k_gauss_bwd_live, dim3(nwg), dim3(kGB), 0, s, m);
-        return;
-    }
-    // row chunks: one launch per consecutive workgroup range, an event after each, so a consumer of the
-    // finished rows (the multi-GPU gradient SUM) starts while the later chunks run
-    for (int c = 0; c < nchunks; ++c) {
-        const int w0 = (int)((long long)nwg * c / nchunks), w1 = (int)((long long)nwg * (c + 1) / nchunks);
-        m.wg0 = w0;
-        if (w1 > w0) hipLaunchKernelGGL(k_gauss_bwd_live, dim3(w1 - w0), dim3(kGB), 0, s, m);
-        (void)hipEventRecord(chunk_done[c], s);
-    }
+    const int group = std::min(div_up(blocks, kLiveGrid), kLiveGroup);  // (the kernel derives the same)
+    hipLaunchKernelGGL(k_gauss_bwd_live, dim3(div_up(blocks, group)), dim3(kGB), 0, s, m);
 }
 
 void launch_gauss_backward(const GaussBwdArgs& a, hipStream_t s, hipEvent_t writes_after) {
-    launch_gauss_backward_views(&a, 1, s, writes_after, 0, nullptr);
+    launch_gauss_backward_views(&a, 1, s, writes_after);
 }
 
 int gauss_backward_max_views() { return kMaxBwdViews; }

@@ -87,15 +87,12 @@ __global__ __launch_bounds__(kRowsBlock) void k_rows_live(RowsLaunch a, long lon
 constexpr int kRowsPerWave = 8;
 
 // m_dev (the _dev entry points): the packed buffer has m rows (the capacity), the row list only
-// min(m, *m_dev) — a gather zero-fills the packed rows past it, a scatter leaves them.  off_dev (the _at
-// entry points, a row chunk): the list starts at rows + *off_dev
+// min(m, *m_dev) — a gather zero-fills the packed rows past it, a scatter leaves them
 template <bool GATHER>
 __global__ __launch_bounds__(256) void k_rows_move(RowsLaunch a, const long long* __restrict__ rows, long long m,
-                                                   float* __restrict__ packed, const long long* __restrict__ m_dev,
-                                                   const long long* __restrict__ off_dev) {
+                                                   float* __restrict__ packed, const long long* __restrict__ m_dev) {
     const long long i0 = ((long long)blockIdx.x * 4 + (threadIdx.x >> 6)) * kRowsPerWave;
     if (i0 >= m) return;
-    if (off_dev) rows += *off_dev;
     const long long mv = m_dev ? (*m_dev < m ? *m_dev : m) : m;  // rows with a list entry
     if (!GATHER && i0 >= mv) return;
     const int ncap = m - i0 < kRowsPerWave ? (int)(m - i0) : kRowsPerWave;  // packed rows of this wave
@@ -210,35 +207,6 @@ static int rows_launch(const gs_rows_region* regions, int nreg, RowsLaunch& a, c
     return GS_OK;
 }
 
-// Row chunks of an ascending row list of *count entries: one lane per chunk bound, a binary search
-// (lower bound) of the bound in the list; info[2c] = the chunk's first entry, info[2c + 1] = its entries
-constexpr int kMaxChunkBounds = 17;  // 16 chunks
-struct ChunkBounds {
-    long long b[kMaxChunkBounds];
-};
-__global__ __launch_bounds__(64) void k_rows_chunk_info(const long long* __restrict__ rows,
-                                                        const long long* __restrict__ count, int nchunks,
-                                                        ChunkBounds bounds, long long* __restrict__ info) {
-    __shared__ long long s_pos[kMaxChunkBounds];
-    const int c = threadIdx.x;
-    const long long n = *count;
-    if (c <= nchunks) {
-        const long long key = bounds.b[c];
-        long long lo = 0, hi = n;  // first entry >= key
-        while (lo < hi) {
-            const long long mid = (lo + hi) >> 1;
-            if (rows[mid] < key) lo = mid + 1;
-            else hi = mid;
-        }
-        s_pos[c] = lo;
-    }
-    __syncthreads();
-    if (c < nchunks) {
-        info[2 * c] = s_pos[c];
-        info[2 * c + 1] = s_pos[c + 1] - s_pos[c];
-    }
-}
-
 static int launched() {
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? GS_OK : report_error(GS_ERR_HIP, hipGetErrorString(e));
@@ -261,8 +229,7 @@ extern "C" int gs_rows_live(const gs_rows_region* regions, int nreg, long long n
 }
 
 static int rows_move(const gs_rows_region* regions, int nreg, const long long* rows, long long m, float* packed,
-                     gs_stream_t stream, bool gather, const char* fn, const long long* m_dev = nullptr,
-                     const long long* off_dev = nullptr) {
+                     gs_stream_t stream, bool gather, const char* fn, const long long* m_dev = nullptr) {
     using namespace gs;
     RowsLaunch a;
     if (int rc = rows_launch(regions, nreg, a, fn)) return rc;
@@ -272,10 +239,10 @@ static int rows_move(const gs_rows_region* regions, int nreg, const long long* r
     if (blocks > 0x7FFFFFFF) return report_error(GS_ERR_INVALID_ARG, fn);
     if (gather)
         hipLaunchKernelGGL(k_rows_move<true>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, a, rows, m,
-                           packed, m_dev, off_dev);
+                           packed, m_dev);
     else
         hipLaunchKernelGGL(k_rows_move<false>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, a, rows, m,
-                           packed, m_dev, off_dev);
+                           packed, m_dev);
     return launched();
 }
 
@@ -301,33 +268,6 @@ extern "C" int gs_rows_scatter_dev(const gs_rows_region* regions, int nreg, cons
     if (!count) return gs::report_error(GS_ERR_INVALID_ARG, "gs_rows_scatter_dev: count is required");
     return rows_move(regions, nreg, rows, cap, const_cast<float*>(packed), stream, false,
                      "gs_rows_scatter_dev: bad arguments", count);
-}
-
-extern "C" int gs_rows_gather_at(const gs_rows_region* regions, int nreg, const long long* rows, long long cap,
-                                 const long long* info, float* packed, gs_stream_t stream) {
-    if (!info) return gs::report_error(GS_ERR_INVALID_ARG, "gs_rows_gather_at: info is required");
-    return rows_move(regions, nreg, rows, cap, packed, stream, true, "gs_rows_gather_at: bad arguments", info + 1,
-                     info);
-}
-
-extern "C" int gs_rows_scatter_at(const gs_rows_region* regions, int nreg, const long long* rows, long long cap,
-                                  const long long* info, const float* packed, gs_stream_t stream) {
-    if (!info) return gs::report_error(GS_ERR_INVALID_ARG, "gs_rows_scatter_at: info is required");
-    return rows_move(regions, nreg, rows, cap, const_cast<float*>(packed), stream, false,
-                     "gs_rows_scatter_at: bad arguments", info + 1, info);
-}
-
-extern "C" int gs_rows_chunk_info(const long long* rows, const long long* count, int nchunks, const long long* bounds,
-                                  long long* info, gs_stream_t stream) {
-    using namespace gs;
-    if (!rows || !count || !bounds || !info || nchunks < 1 || nchunks + 1 > kMaxChunkBounds)
-        return report_error(GS_ERR_INVALID_ARG, "gs_rows_chunk_info: bad arguments (1 <= nchunks <= 16)");
-    ChunkBounds b;
-    for (int c = 0; c < kMaxChunkBounds; ++c) b.b[c] = c <= nchunks ? bounds[c] : 0;
-    for (int c = 0; c < nchunks; ++c)
-        if (b.b[c] > b.b[c + 1]) return report_error(GS_ERR_INVALID_ARG, "gs_rows_chunk_info: bounds must ascend");
-    hipLaunchKernelGGL(k_rows_chunk_info, dim3(1), dim3(64), 0, (hipStream_t)stream, rows, count, nchunks, b, info);
-    return launched();
 }
 
 extern "C" int gs_rows_compact(const uint8_t* live, long long n, long long* rows, long long* count_scratch,

@@ -437,12 +437,7 @@ void launch_gauss_backward(const GaussBwdArgs& a, hipStream_t s, hipEvent_t writ
 // n views' per-Gaussian passes as one (views[0] names the live-list scratch; the parameter-shaped
 // outputs are shared, GS_ACC_* set on them for every view but the first): at most
 // gauss_backward_max_views() views per call
-// nchunks > 0: the pass as nchunks launches over consecutive row ranges (gauss_backward_chunk_row), event
-// chunk_done[c] recorded after chunk c (every event recorded also when there is nothing to do)
-void launch_gauss_backward_views(const GaussBwdArgs* views, int n, hipStream_t s, hipEvent_t writes_after = nullptr,
-                                 int nchunks = 0, const hipEvent_t* chunk_done = nullptr);
-long long gauss_backward_chunk_row(int P, int nchunks, int c);  // first row of chunk c (c = nchunks: P)
-constexpr int kMaxRowChunks = 16;
+void launch_gauss_backward_views(const GaussBwdArgs* views, int n, hipStream_t s, hipEvent_t writes_after = nullptr);
 int gauss_backward_max_views();
 
 // diagnostics (gs_profile_diag_*): per-wave records of the blend kernels,

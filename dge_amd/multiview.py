@@ -173,32 +173,14 @@ class GradBucket:
             # rank overflowed, so the speculated SUM moves nothing and the scanning allreduce() follows
             info = torch.cat([cs[:1], live[n:].to(torch.int64)])
             cdev = cs[:1] * (1 - info[1:])
-            # row chunks: the batch's per-Gaussian pass runs as consecutive row ranges, and
-            # allreduce_end starts each range's SUM as soon as the pass has finished it; each chunk's place
-            # in the union's row list and its size found on the device (identical on every rank)
-            chunks = None
-            nch = _row_chunks()
-            if nch > 1 and batch is not None and not getattr(batch, "indexed", True) and batch.P == n:
-                bounds = batch.set_row_chunks(nch)
-                cinfo = torch.empty(2 * nch, dtype=torch.int64, device=dev)
-                barr = (ctypes.c_longlong * (nch + 1))(*bounds)
-                N.check(N.lib().gs_rows_chunk_info(idx.data_ptr(), cdev.data_ptr(), nch, barr, cinfo.data_ptr(),
-                                                   ctypes.c_void_p(side.cuda_stream)), "gs_rows_chunk_info")
-                chunks = (batch, cinfo, nch)
-                info = torch.cat([info, cinfo])
-            pinned = self._pinned(info.numel())
+            pinned = getattr(self, "_count_host", None)
+            if pinned is None:
+                pinned = self._count_host = torch.empty(2, dtype=torch.int64, pin_memory=True)
             pinned.copy_(info, non_blocking=True)
             ev = side.record_event()
         idx.record_stream(main)  # (read on the current stream by allreduce_end)
         cdev.record_stream(main)
-        self._pending = ("hint", group, idx, pinned, ev, n, mats, cdev, chunks)
-
-    def _pinned(self, k):
-        """The pinned host words the step's counts are copied into (one buffer per size, reused)."""
-        bufs = self.__dict__.setdefault("_count_host", {})
-        if k not in bufs:
-            bufs[k] = torch.empty(k, dtype=torch.int64, pin_memory=True)
-        return bufs[k]
+        self._pending = ("hint", group, idx, pinned, ev, n, mats, cdev)
 
     def allreduce_end(self, stream=None, defer_check: bool = False):
         """Second half of allreduce_begin (after the backward): the packed SUM of the agreed rows.
@@ -216,12 +198,8 @@ class GradBucket:
             return None
         if pend[0] == "scan":
             return self.allreduce(pend[1], min_world=1)
-        _, group, idx, pinned, ev, n, mats, cs, chunks = pend
+        _, group, idx, pinned, ev, n, mats, cs = pend
         main = torch.cuda.current_stream(self.flat.device)
-        ccaps = getattr(self, "_chunk_caps", None)
-        if (chunks is not None and ccaps is not None and len(ccaps) == chunks[2] and 0 < 2 * sum(ccaps) <= n
-                and self.check_attached()):
-            return self._allreduce_chunks(group, idx, pinned, ev, mats, chunks, ccaps, stream, defer_check)
         main.wait_event(ev)  # (idx and its count are written on the collective stream)
         self.wait_zero()
         if not self.check_attached():
@@ -255,12 +233,11 @@ class GradBucket:
                 idx.record_stream(stream)
                 cs.record_stream(stream)
             if spec and defer_check:
-                self._deferred = (ev, pinned, cap, idx, group, mats, stream if side else None, None)
+                self._deferred = (ev, pinned, cap, idx, group, mats, stream if side else None)
                 self._reduced = stream.record_event() if side else None
                 return None
             ev.synchronize()
             m, overflow = int(pinned[0]), int(pinned[1])
-            self._set_chunk_caps(pinned, chunks, mats)
             if overflow:  # some rank re-rendered its views after the marks: every rank scans its bucket
                 self.allreduce(group, min_world=1)
             elif spec:
@@ -281,48 +258,6 @@ class GradBucket:
         self._rows_cap = m + m // 8 + 4096 if _native_ok(mats) and os.environ.get("DGE_AMD_ROWS_SPEC", "1") != "0" \
             else 0
 
-    def _set_chunk_caps(self, pinned, chunks, mats):
-        """Next step's per-chunk capacities from this step's chunk sizes (host copy, after the event)."""
-        if chunks is None:
-            return
-        nch = chunks[2]
-        ms = [int(pinned[3 + 2 * c]) for c in range(nch)]
-        self._chunk_caps = [m + m // 8 + 1024 for m in ms] if _native_ok(mats) and \
-            os.environ.get("DGE_AMD_ROWS_SPEC", "1") != "0" else None
-
-    def _allreduce_chunks(self, group, idx, pinned, ev, mats, chunks, ccaps, stream, defer_check):
-        """The packed SUM in row chunks, each behind its rows' part of the per-Gaussian pass:
-        chunk c's gather / SUM / scatter wait for gs_views_chunk_wait(c) only, so they run on the collective
-        stream (or `stream`) while the pass computes the later chunks.  Each chunk has a speculated capacity
-        (last step's size + 1/8); its size, read on the device, shapes nothing the host must know; the check
-        (and the exact SUM of a chunk's rows past its capacity) follows in allreduce_finalize, deferred or
-        here.  Every rank issues the same collectives: the union, its chunks and the capacities are agreed."""
-        batch, cinfo, nch = chunks
-        dev = self.flat.device
-        main = torch.cuda.current_stream(dev)
-        side = stream is not None and self.flat.is_cuda
-        coll = stream if side else _collective_stream(dev)
-        coll.wait_event(ev)  # (the union's rows and their chunks; written on the collective stream)
-        for c in range(nch):
-            batch.chunk_wait(c, coll)  # (after the pass, which waited for the bucket's zero fill)
-            with torch.cuda.stream(coll):
-                at = cinfo[2 * c:2 * c + 2]
-                packed = _rows_gather_at(mats, idx, ccaps[c], at)
-                dist.all_reduce(packed, op=dist.ReduceOp.SUM, group=group)
-                _rows_scatter_at(mats, idx, packed, ccaps[c], at)
-        idx.record_stream(coll)
-        cinfo.record_stream(coll)
-        done = coll.record_event()
-        if side:
-            self._reduced = done
-        else:
-            main.wait_event(done)
-        self._deferred = (ev, pinned, None, idx, group, mats, coll if side else None, (nch, list(ccaps)))
-        self._chunked = True
-        if not defer_check:
-            self.allreduce_finalize()
-        return None
-
     def allreduce_finalize(self) -> bool:
         """The deferred check of an allreduce_end(defer_check=True): wait for the union's size (the forwards'
         marks, long done by the next step), and when it exceeded the speculated capacity all-reduce the rows
@@ -330,27 +265,17 @@ class GradBucket:
         d, self._deferred = getattr(self, "_deferred", None), None
         if d is None:
             return False
-        ev, pinned, cap, idx, group, mats, stream, chunked = d
+        ev, pinned, cap, idx, group, mats, stream = d
         ev.synchronize()
         m, overflow = int(pinned[0]), int(pinned[1])
         self._set_rows_cap(m, mats)
-        if chunked is not None:  # per chunk: its rows past its capacity
-            nch, used = chunked
-            self._set_chunk_caps(pinned, (None, None, nch), mats)
-            over = [(int(pinned[2 + 2 * c]), int(pinned[3 + 2 * c]), used[c]) for c in range(nch)]
-            over = [(s0 + cp, s0 + mc) for s0, mc, cp in over if mc > cp]
-            if not over and not overflow:
-                return False
-        elif m <= cap and not overflow:
+        if m <= cap and not overflow:
             return False
         import contextlib
 
         with torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext():
             if overflow:  # (the packed SUM moved nothing: the agreed flag zeroed its device count)
                 self.allreduce(group, min_world=1)
-            elif chunked is not None:
-                for a, b in over:
-                    _rows_fixup(mats, idx, a, b, group)
             else:
                 _rows_fixup(mats, idx, cap, m, group)
             if stream is not None:
@@ -400,30 +325,6 @@ class GradBucket:
         dist.all_reduce(packed, op=dist.ReduceOp.SUM, group=group)
         _rows_scatter(mats, idx, packed)
         return None
-
-
-def _row_chunks() -> int:
-    """Row chunks of the multi-GPU gradient SUM (DGE_AMD_ROWS_CHUNKS, default 4; 0 or 1: one SUM after
-    the whole backward)."""
-    try:
-        return max(0, min(16, int(os.environ.get("DGE_AMD_ROWS_CHUNKS", "4"))))
-    except ValueError:
-        return 4
-
-
-def _rows_gather_at(mats, idx, cap, at):
-    """[cap, sum(widths)]: the rows idx[at[0] : at[0] + min(cap, at[1])] (read on the device), zero rows after."""
-    N, regs, stream = _native_rows(mats)
-    packed = torch.empty((cap, sum(m.shape[1] for m in mats)), dtype=torch.float32, device=mats[0].device)
-    N.check(N.lib().gs_rows_gather_at(regs, len(mats), idx.data_ptr(), cap, at.data_ptr(), packed.data_ptr(), stream),
-            "gs_rows_gather_at")
-    return packed
-
-
-def _rows_scatter_at(mats, idx, packed, cap, at):
-    N, regs, stream = _native_rows(mats)
-    N.check(N.lib().gs_rows_scatter_at(regs, len(mats), idx.data_ptr(), cap, at.data_ptr(), packed.data_ptr(),
-                                       stream), "gs_rows_scatter_at")
 
 
 def _rows_fixup(mats, idx, cap, m, group):

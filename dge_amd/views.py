@@ -55,7 +55,6 @@ class ViewBatch:
     def __init__(self, handle, bufs, n, P, W, H, dev, keep):
         self.handle, self.bufs, self.n, self.P, self.W, self.H, self.dev = handle, bufs, n, P, W, H, dev
         self.keep = keep
-        self.indexed = False
         self.status = None
         self.num_rendered = None
         self._fin = weakref.finalize(self, N.lib().gs_views_release, handle)
@@ -71,17 +70,6 @@ class ViewBatch:
                 N.check(rc, "render_views")
             self.status = rc
         return self.status == N.GS_OK
-
-    def set_row_chunks(self, n: int):
-        """Split the coming backward's per-Gaussian pass into n row chunks (gs_views_set_row_chunks; 0: off):
-        returns the n + 1 row bounds.  chunk_wait(c, stream) then orders `stream` after chunk c's rows."""
-        rows = (ctypes.c_longlong * (n + 1))()
-        N.check(N.lib().gs_views_set_row_chunks(self.handle, n, rows), "gs_views_set_row_chunks")
-        return list(rows) if n > 0 else []
-
-    def chunk_wait(self, c: int, stream):
-        N.check(N.lib().gs_views_chunk_wait(self.handle, c, ctypes.c_void_p(stream.cuda_stream)),
-                "gs_views_chunk_wait")
 
     def buffer(self, v: int, which: int):
         """(torch byte tensor, offset) of view v's buffer (0 geometry, 1 binning, 2 image)."""
@@ -146,7 +134,6 @@ class _RasterizeViews(torch.autograd.Function):
                                       join, ctypes.byref(h))
         N.check(rc, "render_views")
         batch = ViewBatch(h.value, bufs, n, P, W, H, dev, keep)
-        batch.indexed = index is not None  # (gradient rows = index[i]: no row chunks)
         if P == 0:
             radii.zero_()
         meta["batch"] = batch

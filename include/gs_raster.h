@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define GS_RASTER_ABI_VERSION 17
+#define GS_RASTER_ABI_VERSION 16
 
 #define GS_OK 0
 #define GS_ERR_INVALID_ARG 1   /* AT_ERROR / std::runtime_error in the reference */
@@ -289,16 +289,6 @@ int gs_views_backward(gs_views *h, const float *const *dL_dpix, const gs_grads *
  * `stream` (which must be ordered after the views' forwards) without a host wait, so a collective can
  * carry it: every rank of a view-sharded step then agrees on the recovery (ABI 14). */
 int gs_views_overflow(const gs_views *h, uint8_t *flag, gs_stream_t stream);
-/* Row chunks of the batch's gradients (ABI 17; SURVEY.md §8(e): the multi-GPU gradient SUM starts on the
- * rows the backward has finished while it computes the rest).  After gs_views_set_row_chunks(h, n, rows)
- * (0 < n <= 16; n = 0 turns it off) the next gs_views_backward runs its merged per-Gaussian pass as n
- * launches over consecutive row ranges [rows[c], rows[c + 1]) (rows[0] = 0, rows[n] = P, written here)
- * and records an event after each; gs_views_chunk_wait(h, c, stream) makes `stream` wait until chunk c's
- * gradient rows are final (every row of the batch's parameter-shaped outputs in the range).  A backward
- * that cannot split (more views than one pass takes, or views whose passes chain) records every chunk's
- * event at its end. */
-int gs_views_set_row_chunks(gs_views *h, int n, long long *rows);
-int gs_views_chunk_wait(const gs_views *h, int c, gs_stream_t stream);
 void *gs_views_buffer(const gs_views *h, int v, int which);
 long long gs_views_layout(const gs_views *h, int v);
 void gs_views_release(gs_views *h);
@@ -370,17 +360,6 @@ int gs_rows_gather_dev(const gs_rows_region *regions, int nreg, const long long 
                        const long long *count, float *packed, gs_stream_t stream);
 int gs_rows_scatter_dev(const gs_rows_region *regions, int nreg, const long long *rows, long long cap,
                         const long long *count, const float *packed, gs_stream_t stream);
-/* A row chunk of a compacted row list (ABI 17): info[2c] = the position in `rows` of the first entry
- * >= bounds[c], info[2c + 1] = the entries in [bounds[c], bounds[c + 1]) — of the first *count entries
- * of the ascending list, found on the device (nchunks <= 16, bounds[nchunks] = the end). */
-int gs_rows_chunk_info(const long long *rows, const long long *count, int nchunks, const long long *bounds,
-                       long long *info, gs_stream_t stream);
-/* gs_rows_gather_dev / _scatter_dev over the list entries rows[info[0] ..) with info[1] of them (a chunk
- * of gs_rows_chunk_info), both read on the device. */
-int gs_rows_gather_at(const gs_rows_region *regions, int nreg, const long long *rows, long long cap,
-                      const long long *info, float *packed, gs_stream_t stream);
-int gs_rows_scatter_at(const gs_rows_region *regions, int nreg, const long long *rows, long long cap,
-                       const long long *info, const float *packed, gs_stream_t stream);
 
 /* Byte sizes of the opaque buffers (host arithmetic, no device work). */
 size_t gs_geometry_buffer_size(int P);

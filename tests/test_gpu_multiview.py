@@ -485,81 +485,6 @@ def test_deferred_union_check_two_ranks(cuda_device):
         assert s2 and d2 and f2 and e2           # capacity below the union: the deferred fix-up ran
 
 
-def _chunked_worker(rank, world, port, P, V, W, H, q):
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    try:
-        torch.cuda.set_device(0)
-        dev = torch.device("cuda", 0)
-        dist.init_process_group("gloo", rank=rank, world_size=world)
-        from dge_amd.gaussian_renderer import PipelineParams
-        from dge_amd.multiview import GradBucket, render_views, shard_views
-
-        sc, cams, seeds = _c3_setup(dev, P, V, W, H)
-        mine = list(shard_views(V, world, rank))
-        bucket = GradBucket(sc.parameters())
-        bg = torch.zeros(3, device=dev)
-        errs = []
-        # step 0: exact (sets the capacities); step 1: the SUM in row chunks behind the per-Gaussian pass;
-        # step 2: every chunk's capacity a third of its rows (the deferred check SUMs the rest of each chunk)
-        for k, cap in enumerate((None, None, "third")):
-            bucket.zero()
-            outs = render_views([cams[i] for i in mine], sc, PipelineParams(), bg, streams=3, speculate=True)
-            bucket.allreduce_begin([o["_live_rows"] for o in outs], min_world=2, views=outs)
-            torch.autograd.backward([o["render"] for o in outs], [seeds[i] for i in mine])
-            assert outs.check()
-            if cap == "third":
-                bucket._chunk_caps = [max(1, c // 3) for c in bucket._chunk_caps]
-            bucket._chunked = False
-            bucket.allreduce_end(defer_check=True)  # (enqueued while the backward may still run)
-            chunked = bucket._chunked
-            fixed = bucket.allreduce_finalize()
-            torch.cuda.synchronize()
-            got = bucket.flat.clone()
-            # the same step again (deterministic), its bucket all-reduced densely once the backward is done
-            bucket.zero()
-            outs = render_views([cams[i] for i in mine], sc, PipelineParams(), bg, streams=3, speculate=True)
-            torch.autograd.backward([o["render"] for o in outs], [seeds[i] for i in mine])
-            assert outs.check()
-            torch.cuda.synchronize()
-            dense = bucket.flat.clone()
-            dist.all_reduce(dense, op=dist.ReduceOp.SUM)
-            torch.cuda.synchronize()
-            errs.append((k, chunked, fixed, bool(torch.equal(got, dense)), int((dense != 0).sum())))
-        q.put((rank, errs, None))
-    except Exception as e:  # report instead of hanging the parent
-        import traceback
-        q.put((rank, None, repr(e) + traceback.format_exc()))
-    finally:
-        if dist.is_initialized():
-            dist.destroy_process_group()
-
-
-def test_row_chunked_sum_two_ranks(cuda_device):
-    """the multi-GPU gradient SUM in row chunks, chunk c's pack / SUM / unpack behind
-    gs_views_chunk_wait(c) — the part of the merged per-Gaussian pass that finishes its rows — instead of
-    after the whole backward.  Two ranks on one card (gloo, CUDA tensors): the bucket equals the dense
-    all-reduce of the ranks' buckets bit for bit, with the chunks' SUMs enqueued before the backward is
-    known to be done, and with every chunk's capacity below its rows (the deferred fix-ups)."""
-    P, V, W, H = 300_000, 4, 160, 128
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_chunked_worker, args=(r, 2, port, P, V, W, H, q)) for r in range(2)]
-    for p in procs:
-        p.start()
-    res = [q.get(timeout=240) for _ in procs]
-    for p in procs:
-        p.join(timeout=60)
-    for rank, steps, err in res:
-        assert err is None, f"rank {rank}: {err}"
-        print(f"[row chunks] rank {rank}: (step, chunked, fix-up, equal, nonzero) {steps}")
-        (k0, c0, f0, e0, nz0), (k1, c1, f1, e1, _), (k2, c2, f2, e2, _) = steps
-        assert not c0 and e0 and nz0 > 0   # first step: exact, no capacities yet
-        assert c1 and not f1 and e1        # chunked under the speculated capacities
-        assert c2 and f2 and e2            # chunk capacities below the rows: the fix-ups ran
-
-
 def _seed_history(dev, P, cams, sc, small):
     """Render `cams` exactly once (no gradients) to seed this process's speculated-capacity history for
     their (P, W, H): with the scene itself, or (small) with the same number of Gaussians moved out of
