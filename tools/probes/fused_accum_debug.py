@@ -37,28 +37,29 @@ def run(fused, pre_grad, batched):
         set_fused_grad_accumulation(prev)
 
 
-for spec in (False, True):
-    GR._SPEC_RENDER = spec
-    for pre_grad in (False, True):
-        for batched in (False, True):
-            a, b = run(True, pre_grad, batched), run(False, pre_grad, batched)
-            bad = [(n, int((x != y).sum()), float((x - y).abs().max())) for n, x, y in zip(names, a, b)
-                   if not torch.equal(x, y)]
-            print(f"spec {spec} pre_grad {pre_grad} batched {batched}: {bad}")
-# the speculated render against the exact one, per view, forward and per-view backward alone
-for spec in (True, False):
-    GR._SPEC_RENDER = spec
-    sc = synthetic_scene(15_000, seed=5, radius=1.5, scale=0.03, device=dev).requires_grad_(True)
-    res = []
-    for c, g in zip(cams, Gs):
-        pkg = render(c, sc, PipelineParams(), bg)
-        (pkg["render"] * g).sum().backward()
-        res.append((pkg["render"].detach().clone(), [p.grad.clone() for p in sc.parameters()]))
-        for p in sc.parameters():
-            p.grad = None
-    if spec:
-        got = res
-    else:
-        for v, ((ia, ga), (ib, gb)) in enumerate(zip(got, res)):
-            print(f"view {v}: image equal {torch.equal(ia, ib)}",
-                  [(n, int((x != y).sum())) for n, x, y in zip(names, ga, gb) if not torch.equal(x, y)])
+if __name__ == "__main__":
+    for spec in (False, True):
+      GR._SPEC_RENDER = spec
+      for pre_grad in (False, True):
+          for batched in (False, True):
+              a, b = run(True, pre_grad, batched), run(False, pre_grad, batched)
+              bad = [(n, int((x != y).sum()), float((x - y).abs().max())) for n, x, y in zip(names, a, b)
+                     if not torch.equal(x, y)]
+              print(f"spec {spec} pre_grad {pre_grad} batched {batched}: {bad}")
+  # the speculated render against the exact one, per view, forward and per-view backward alone
+  for spec in (True, False):
+      GR._SPEC_RENDER = spec
+      sc = synthetic_scene(15_000, seed=5, radius=1.5, scale=0.03, device=dev).requires_grad_(True)
+      res = []
+      for c, g in zip(cams, Gs):
+          pkg = render(c, sc, PipelineParams(), bg)
+          (pkg["render"] * g).sum().backward()
+          res.append((pkg["render"].detach().clone(), [p.grad.clone() for p in sc.parameters()]))
+          for p in sc.parameters():
+              p.grad = None
+      if spec:
+          got = res
+      else:
+          for v, ((ia, ga), (ib, gb)) in enumerate(zip(got, res)):
+              print(f"view {v}: image equal {torch.equal(ia, ib)}",
+                    [(n, int((x != y).sum())) for n, x, y in zip(names, ga, gb) if not torch.equal(x, y)])
