@@ -133,6 +133,9 @@ class _RasterizeViews(torch.autograd.Function):
                                       N.VIEWS_SPECULATE if speculate else N.VIEWS_EXACT, bufs.fn, None, st_arr,
                                       join, ctypes.byref(h))
         N.check(rc, "render_views")
+        # (the backward reads the radii through the handle: kept alive with the batch, not only by the
+        # caller's outputs — DGE's loop drops a view's radii dict once it has taken their max)
+        keep.append(radii)
         batch = ViewBatch(h.value, bufs, n, P, W, H, dev, keep)
         if P == 0:
             radii.zero_()
