@@ -634,11 +634,11 @@ def side_legs(args, scene, cams, seeds, bg, pipe, bucket, step, dev):
             scene.mask = prev_mask
 
     from dge_amd import gaussian_renderer as GR
-    hits0, spec0 = GR._RECOLOR_HITS, GR._SPEC_RENDERS
+    hits0 = GR._RECOLOR_HITS
     for _ in range(3):
         dge_loop()
     dt = _time(dge_loop, steps)
-    hits, spec = GR._RECOLOR_HITS - hits0, GR._SPEC_RENDERS - spec0
+    hits = GR._RECOLOR_HITS - hits0
     dt_lazy = None
     recolor = GR._RECOLOR
     GR._RECOLOR = False  # (the semantic render in full: lazy forward-only kernels, its own binning)
@@ -661,7 +661,6 @@ def side_legs(args, scene, cams, seeds, bg, pipe, bucket, step, dev):
         "path": "DGE.py forward() per view (fused render(), semantic render, boolean-mask viz: a host sync per "
                 "view) + masked l1 + one backward, install_alias(fused_render=True), no code edit",
         "semantic_recolor_hits": hits,
-        "speculated_training_renders": spec,
         "semantic_full_render_value": round(steps * V / dt_full, 3),
         "semantic_eager_value": round(steps * V / dt_lazy, 3)}
     for p in scene.parameters():

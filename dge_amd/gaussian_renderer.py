@@ -157,58 +157,7 @@ def _render_fused(viewpoint_camera, pc, pipe, bg_color, scaling_modifier=1.0, ov
     """render() for a standard GaussianModel without the getters' torch kernels:
     the rasterizer consumes _xyz, _features_dc, _features_rest, _opacity,
     _scaling, _rotation directly and returns their gradients."""
-    if override_color is None and _SPEC_RENDER and not getattr(pipe, "debug", False):
-        out = _render_speculated(viewpoint_camera, pc, pipe, bg_color, scaling_modifier)
-        if out is not None:
-            return out
     return _fused_end(_fused_begin(viewpoint_camera, pc, pipe, bg_color, scaling_modifier, override_color), pc)
-
-
-# DGE's training render per view (DGE.py:181) with a speculated binning capacity (round 4): the view as a batch
-# of one through gs_views_forward(GS_VIEWS_SPECULATE) — the whole forward enqueued at once, no host wait
-# for the instance count between its halves (rasterizer_impl.cu:236-239) — then the count checked while
-# the GPU runs the rest; a view that outgrew the capacity is rendered again the exact way.  Bitwise the
-# exact render (tests).  DGE_AMD_SPEC_RENDER=0: always the exact per-view forward.
-_SPEC_RENDER = os.environ.get("DGE_AMD_SPEC_RENDER", "1") != "0"
-_SPEC_RETRIES = 0  # speculated renders that overflowed and were rendered again (tests)
-_SPEC_RENDERS = 0  # renders served by the batch-of-one path (tests, bench)
-
-
-def _render_speculated(viewpoint_camera, pc, pipe, bg_color, scaling_modifier):
-    from .views import render_views_batched
-
-    global _SPEC_RETRIES
-    dev = pc._xyz.device
-    cur = torch.cuda.current_stream(dev)
-    outs = render_views_batched([viewpoint_camera], pc, pipe, bg_color, [cur], scaling_modifier, None,
-                                speculate=True)
-    if not outs.check():
-        _SPEC_RETRIES += 1
-        return None
-    global _SPEC_RENDERS
-    _SPEC_RENDERS += 1
-    d = outs[0]
-    d.pop("_live_rows", None)
-    batch = outs.batch
-    if _RECOLOR and _may_backward(pc._xyz, pc._features_dc, pc._features_rest, None, pc._opacity, pc._scaling,
-                                  pc._rotation):  # (a forward with backward bookkeeping: the semantic render may reuse it)
-        refs, offs = [], []
-        for which in range(3):
-            t, off = batch.buffer(0, which)
-            refs.append(weakref.ref(t))
-            offs.append(off)
-        from . import _native as N
-
-        index = _mask_rows(pc.mask) if getattr(pc, "localize", False) else None
-        rs = _settings(viewpoint_camera, bg_color, scaling_modifier, pc.active_sh_degree, False)
-        ent = _ForwardEntry(_geometry_key(pc, rs, index), refs, int(N.lib().gs_views_layout(batch.handle, 0)),
-                            batch.P, cur, d["radii"], d["visibility_filter"], offs)
-        ent.tensor_refs = [weakref.ref(t) for t in (pc._xyz, pc._opacity, pc._scaling, pc._rotation,
-                                                    rs.viewmatrix, rs.projmatrix) if t is not None]
-        if index is not None:
-            ent.tensor_refs.append(weakref.ref(index))
-        _LAST_FORWARD[dev.index] = ent
-    return d
 
 
 _LAZY_OVERRIDE = os.environ.get("DGE_AMD_LAZY_OVERRIDE", "1") != "0"

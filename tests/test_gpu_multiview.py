@@ -765,3 +765,36 @@ def test_lazy_override_color_render(cuda_device, monkeypatch):
     assert torch.equal(va, vb) and bool(va.abs().sum() > 0)
     for x, y in zip(ga1 + ga2, gb1 + gb2):
         assert torch.equal(x, y)
+
+
+def test_views_backward_after_outputs_dropped(cuda_device):
+    """The batch keeps what its backward reads: a caller that keeps only the images (DGE's loop drops a
+    view's dict once it has taken the radii max) and allocates in between gets the same gradients, bit for
+    bit, as one that keeps every output (the radii block was once handed to other tensors meanwhile)."""
+    from dge_amd.cameras import orbit_camera
+    from dge_amd.gaussian_renderer import PipelineParams
+    from dge_amd.multiview import render_views
+    from dge_amd.scene import synthetic_scene
+
+    dev = torch.device("cuda")
+    P, W, H = 40_000, 176, 144
+    cams = [orbit_camera(k, 4, W, H, device=dev) for k in range(3)]
+    Gs = [torch.randn(3, H, W, generator=torch.Generator().manual_seed(60 + k)).to(dev) for k in range(3)]
+
+    def run(keep):
+        sc = synthetic_scene(P, seed=21, radius=1.5, scale=0.03, device=dev).requires_grad_(True)
+        outs = render_views(cams, sc, PipelineParams(), torch.zeros(3, device=dev), streams=3, speculate=True)
+        assert outs.check()
+        imgs = [o["render"] for o in outs]
+        if not keep:
+            del outs
+            junk = [torch.full((len(cams), P), -7, dtype=torch.int32, device=dev) for _ in range(4)]
+            del junk
+        torch.autograd.backward(imgs, Gs)
+        torch.cuda.synchronize()
+        return [p.grad.clone() for p in sc.parameters()]
+
+    ref = run(True)
+    got = run(False)
+    for i, (a, b) in enumerate(zip(got, ref)):
+        assert torch.equal(a, b), f"parameter {i}"

@@ -676,58 +676,3 @@ def test_semantic_render_reuses_the_training_forward(cuda_device, localize):
         assert torch.equal(a, b)
     assert bool(got[2][0].abs().sum() > 0)
     assert torch.equal(got[3], ref[3])
-
-
-@pytest.mark.parametrize("localize", [False, True])
-def test_speculated_render_matches_exact(cuda_device, localize):
-    """render()'s training render with a speculated binning capacity (the view as a batch of one through
-    gs_views_forward(GS_VIEWS_SPECULATE): no host wait for the instance count between its halves,
-    rasterizer_impl.cu:236-239, the count checked afterwards) equals the exact per-view forward bit for
-    bit: image, depth, radii, visibility, dL/dmeans2D and every parameter gradient of DGE's per-view loop
-    (two views, one backward of the summed loss), the semantic render served from it included."""
-    from dge_amd import gaussian_renderer as GR
-    from dge_amd.cameras import orbit_camera
-    from dge_amd.gaussian_renderer import PipelineParams, render
-    from dge_amd.scene import synthetic_scene
-
-    dev = torch.device("cuda")
-    P, W, H = 80_000, 208, 160
-    pipe, bg = PipelineParams(), torch.tensor([0.0, 0.1, 0.2], device=dev)
-    cams = [orbit_camera(k, 5, W, H, device=dev) for k in range(2)]
-    Gs = [torch.randn(3, H, W, generator=torch.Generator().manual_seed(7 + k)).to(dev) for k in range(2)]
-
-    def run(spec):
-        GR._SPEC_RENDER = spec
-        sc = synthetic_scene(P, seed=12, radius=1.5, scale=0.03, device=dev).requires_grad_(True)
-        m = torch.zeros(P, dtype=torch.bool, device=dev)
-        m[torch.argsort(sc._xyz[:, 0])[: P // 2]] = True
-        sc.mask, sc.localize = m, localize
-        n0 = GR._SPEC_RENDERS
-        outs, loss = [], 0.0
-        for cam, G in zip(cams, Gs):
-            pkg = render(cam, sc, pipe, bg)
-            sem = render(cam, sc, pipe, bg, override_color=sc.mask[..., None].float().repeat(1, 3))["render"]
-            outs.append((pkg, sem.detach().clone()))
-            loss = loss + (pkg["render"] * G).sum()
-        loss.backward()
-        torch.cuda.synchronize()
-        res = [{k: (v.detach().clone() if k != "viewspace_points" else v.grad.clone()) for k, v in pkg.items()}
-               | {"semantic": sem} for pkg, sem in outs]
-        grads = [p.grad.clone() for p in (sc._xyz, sc._features_dc, sc._features_rest, sc._opacity, sc._scaling,
-                                          sc._rotation)]
-        return res, grads, GR._SPEC_RENDERS - n0
-
-    prev = GR._SPEC_RENDER
-    try:
-        run(True)  # (seeds the capacity history of this (P, W, H))
-        got = run(True)
-        ref = run(False)
-    finally:
-        GR._SPEC_RENDER = prev
-    assert got[2] == 2 and ref[2] == 0, (got[2], ref[2])
-    for v, (a, b) in enumerate(zip(got[0], ref[0])):
-        for k in a:
-            assert torch.equal(a[k], b[k]), f"view {v}: {k}"
-    for i, (a, b) in enumerate(zip(got[1], ref[1])):
-        assert torch.equal(a, b), f"gradient {i}"
-    assert bool(got[1][0].abs().sum() > 0)
