@@ -116,8 +116,9 @@ __device__ __forceinline__ uint32_t dev_count(const uint32_t* __restrict__ n_dev
 __host__ __device__ __forceinline__ size_t hist_at(int bm, uint32_t b, uint32_t d, int nb, int ndig) {
     return bm ? (size_t)b * ndig + d : (size_t)d * nb + b;
 }
-template <int BITS, int IPT>
-__global__ __launch_bounds__(256) void k_radix_hist(const uint32_t* __restrict__ keys, uint32_t n, int shift,
+// KT: the key type (u16 for the two-level binning's row pass: its keys are y << 7 | x)
+template <int BITS, int IPT, class KT = uint32_t>
+__global__ __launch_bounds__(256) void k_radix_hist(const KT* __restrict__ keys, uint32_t n, int shift,
                                                     uint32_t* __restrict__ hist, int nb, int bm,
                                                     const uint32_t* __restrict__ bias_not,
                                                     const uint32_t* __restrict__ n_dev) {
@@ -134,7 +135,7 @@ __global__ __launch_bounds__(256) void k_radix_hist(const uint32_t* __restrict__
 #pragma unroll
     for (int it = 0; it < IPT; ++it) {
         const uint32_t idx = base + it * 256 + tid;
-        key[it] = idx < n ? keys[idx] - bias : 0u;
+        key[it] = idx < n ? (uint32_t)keys[idx] - bias : 0u;
     }
 #pragma unroll
     for (int it = 0; it < IPT; ++it) {
@@ -291,8 +292,8 @@ enum ValMode { kValU32 = 0, kValPairFirst = 1, kValPair = 2 };
 // WK: the sorted keys are written (every pass but the last tile-sort pass).  Without them the block
 // stages only the digit (u16), and the per-wave digit counters are u16 throughout (<= 256*IPT), so
 // the single-pass tile sort fits three workgroups per CU (52 KB of LDS instead of 68).
-template <int BITS, int IPT, bool IDV, int VM, bool WK = true, bool TC = false>
-__global__ __launch_bounds__(256) void k_radix_scatter(const uint32_t* __restrict__ keys_in,
+template <int BITS, int IPT, bool IDV, int VM, bool WK = true, bool TC = false, class KT = uint32_t>
+__global__ __launch_bounds__(256) void k_radix_scatter(const KT* __restrict__ keys_in,
                                                        const void* __restrict__ vals_in_,
                                                        uint32_t* __restrict__ keys_out, void* __restrict__ vals_out_,
                                                        const uint32_t* __restrict__ gauss_by_slot, uint32_t n,
@@ -378,7 +379,7 @@ __global__ __launch_bounds__(256) void k_radix_scatter(const uint32_t* __restric
     for (int it = 0; it < IPT; ++it) {
         const uint32_t idx = base + it * 64 + lane;
         const bool valid = idx < n;
-        key[it] = valid ? keys_in[idx] - bias : 0u;
+        key[it] = valid ? (uint32_t)keys_in[idx] - bias : 0u;
         if constexpr (VM == kValU32) val[it] = IDV ? idx : (valid ? vals_in[idx] : 0u);
         else if constexpr (VM == kValPairFirst) val[it] = make_uint2(valid ? gauss_by_slot[idx] : 0u, idx);
         else val[it] = valid ? pairs_in[idx] : make_uint2(0u, 0u);
@@ -432,7 +433,7 @@ __global__ __launch_bounds__(256) void k_radix_scatter(const uint32_t* __restric
     __shared__ SK s_key[256 * IPT];
     __shared__ V s_val[256 * IPT];
     const uint32_t b0 = blockIdx.x * (uint32_t)(256 * IPT);
-    const uint32_t x_first = TC ? keys_in[b0] & (kXDigits - 1) : 0u;  // the block's first column
+    const uint32_t x_first = TC ? (uint32_t)keys_in[b0] & (kXDigits - 1) : 0u;  // the block's first column
 #pragma unroll
     for (int it = 0; it < IPT; ++it) {
         const uint32_t idx = base + it * 64 + lane;
@@ -481,13 +482,7 @@ static void radix_pass(const uint32_t* kin, const void* vin, uint32_t* kout, voi
 #define GS_SCATTER(IDV, VM)                                                                                   \
     hipLaunchKernelGGL((k_radix_scatter<BITS, IPT, IDV, VM>), dim3(nb), dim3(256), 0, s, kin, vin, kout, vout,  \
                        gauss_by_slot, n, shift, hist, totals, nb, bm, ro, bias_not, n_dev)
-    if (vm == kValPair && !kout)  // the two-level binning's row pass: no sorted keys
-        hipLaunchKernelGGL((k_radix_scatter<BITS, IPT, false, kValPair, false, true>), dim3(nb), dim3(256), 0, s, kin,
-                           vin, kout, vout, gauss_by_slot, n, shift, hist, totals, nb, bm, ro, bias_not, n_dev);
-    else if (vm == kValU32 && !kout && ro.tile_count)  // the same over Gaussian ids alone (ids_only)
-        hipLaunchKernelGGL((k_radix_scatter<BITS, IPT, false, kValU32, false, true>), dim3(nb), dim3(256), 0, s, kin,
-                           vin, kout, vout, gauss_by_slot, n, shift, hist, totals, nb, bm, ro, bias_not, n_dev);
-    else if (vm == kValPairFirst && !kout)  // the last tile-sort pass: no sorted keys
+    if (vm == kValPairFirst && !kout)  // the last tile-sort pass: no sorted keys
         hipLaunchKernelGGL((k_radix_scatter<BITS, IPT, true, kValPairFirst, false>), dim3(nb), dim3(256), 0, s, kin,
                            vin, kout, vout, gauss_by_slot, n, shift, hist, totals, nb, bm, ro, bias_not, n_dev);
     else if (vm == kValPairFirst) GS_SCATTER(true, kValPairFirst);
@@ -845,7 +840,7 @@ __global__ __launch_bounds__(256) void k_scan_emit_x(EmitArgs a) {
                 const uint32_t kv = s_key[i];
                 const uint32_t pos = s_gbase[kv & (kXDigits - 1)] + i;
                 if (pos < a.cap) {  // (speculative capacity: gs_views_check reports an overflow)
-                    a.tile_key[pos] = kv;
+                    reinterpret_cast<uint16_t*>(a.tile_key)[pos] = (uint16_t)kv;  // (the row pass reads u16 keys)
                     if constexpr (IDS) reinterpret_cast<uint32_t*>(a.pairs_out)[pos] = s_pair[i];
                     else a.pairs_out[pos] = s_pair[i];
                 }
@@ -923,9 +918,26 @@ void launch_row_pass(const EmitArgs& a, uint32_t K, uint2* point_pairs, uint32_t
                      uint2* ranges, uint32_t* tile_order, hipStream_t s, const uint32_t* n_dev) {
     if (a.P <= 0 || K == 0) return;
     // second level: the stable row pass (digit y), counting instances per tile on the way
+    // (u16 keys: y << 7 | x fits; half the key bytes of the emission's writes and of the pass's reads)
     RangeOut ro{nullptr, nullptr, a.ntiles, a.tile_count, a.gx};
-    radix_pass<kXBits, kSortIPT>(a.tile_key, a.pairs_out, nullptr, point_pairs, nullptr, K, kXBits, false,
-                                 a.ids_only ? kValU32 : kValPair, hist, a.xtotals, sort_blocks, ro, nullptr, s, n_dev);
+    const uint16_t* keys = reinterpret_cast<const uint16_t*>(a.tile_key);
+    constexpr int NDIG = kXDigits;
+    const int nb = sort_blocks, bm = nb <= kScanBmRows ? 1 : 0;
+    hipLaunchKernelGGL((k_radix_hist<kXBits, kSortIPT, uint16_t>), dim3(nb), dim3(256), 0, s, keys, K, kXBits, hist, nb,
+                       bm, (const uint32_t*)nullptr, n_dev);
+    if (bm)
+        hipLaunchKernelGGL(k_radix_digit_scan, dim3(div_up(NDIG, kScanDigits)), dim3(1024), 0, s, hist, nb, NDIG,
+                           a.xtotals, n_dev, K, kSortTile);
+    else
+        hipLaunchKernelGGL(k_radix_digit_scan_dm, dim3(NDIG), dim3(256), 0, s, hist, nb, a.xtotals, n_dev, K, kSortTile);
+    if (a.ids_only)
+        hipLaunchKernelGGL((k_radix_scatter<kXBits, kSortIPT, false, kValU32, false, true, uint16_t>), dim3(nb), dim3(256),
+                           0, s, keys, a.pairs_out, nullptr, point_pairs, nullptr, K, kXBits, hist, a.xtotals, nb, bm, ro,
+                           (const uint32_t*)nullptr, n_dev);
+    else
+        hipLaunchKernelGGL((k_radix_scatter<kXBits, kSortIPT, false, kValPair, false, true, uint16_t>), dim3(nb), dim3(256),
+                           0, s, keys, a.pairs_out, nullptr, point_pairs, nullptr, K, kXBits, hist, a.xtotals, nb, bm, ro,
+                           (const uint32_t*)nullptr, n_dev);
     hipLaunchKernelGGL(k_ranges_counts, dim3(1), dim3(256), 0, s, a.tile_count, a.ntiles, ranges, tile_order);
 }
 
