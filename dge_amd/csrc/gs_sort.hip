@@ -691,7 +691,10 @@ __global__ __launch_bounds__(256) void k_scan_emit(EmitArgs a) {
 // consecutive lanes on consecutive positions of each column run.  The key
 // written is y << 7 | x (the row pass's digit and the tile's column).
 // IDS: the (Gaussian, slot) pair's Gaussian alone (EmitArgs::ids_only)
-constexpr int kEmitEPT = 8, kEmitBatch = 256 * kEmitEPT;
+#ifndef GS_EMIT_EPT
+#define GS_EMIT_EPT 8  // instances per thread of an emission batch (A/B: -DGS_EMIT_EPT=...)
+#endif
+constexpr int kEmitEPT = GS_EMIT_EPT, kEmitBatch = 256 * kEmitEPT;
 template <bool IDS>
 __global__ __launch_bounds__(256) void k_scan_emit_x(EmitArgs a) {
     using PV = typename std::conditional<IDS, uint32_t, uint2>::type;
