@@ -917,6 +917,10 @@ void launch_emit_fused(const EmitArgs& a, hipStream_t s) {
         hipLaunchKernelGGL(k_scan_emit_x<false>, dim3(a.scan_blocks), dim3(256), 0, s, a);
 }
 
+#ifndef GS_ROW_IPT
+#define GS_ROW_IPT 16  // elements per thread of the row pass (A/B: -DGS_ROW_IPT=32)
+#endif
+constexpr int kRowIPT = GS_ROW_IPT;
 void launch_row_pass(const EmitArgs& a, uint32_t K, uint2* point_pairs, uint32_t* hist, int sort_blocks,
                      uint2* ranges, uint32_t* tile_order, hipStream_t s, const uint32_t* n_dev) {
     if (a.P <= 0 || K == 0) return;
@@ -924,21 +928,23 @@ void launch_row_pass(const EmitArgs& a, uint32_t K, uint2* point_pairs, uint32_t
     // (u16 keys: y << 7 | x fits; half the key bytes of the emission's writes and of the pass's reads)
     RangeOut ro{nullptr, nullptr, a.ntiles, a.tile_count, a.gx};
     const uint16_t* keys = reinterpret_cast<const uint16_t*>(a.tile_key);
-    constexpr int NDIG = kXDigits;
-    const int nb = sort_blocks, bm = nb <= kScanBmRows ? 1 : 0;
-    hipLaunchKernelGGL((k_radix_hist<kXBits, kSortIPT, uint16_t>), dim3(nb), dim3(256), 0, s, keys, K, kXBits, hist, nb,
+    constexpr int NDIG = kXDigits, IPT = kRowIPT, TILE = 256 * kRowIPT;
+    static_assert(TILE >= kSortTile, "the histogram table is sized for kSortTile-row blocks");
+    const int nb = (int)div_up_u(K, (uint32_t)TILE), bm = nb <= kScanBmRows ? 1 : 0;
+    (void)sort_blocks;
+    hipLaunchKernelGGL((k_radix_hist<kXBits, IPT, uint16_t>), dim3(nb), dim3(256), 0, s, keys, K, kXBits, hist, nb,
                        bm, (const uint32_t*)nullptr, n_dev);
     if (bm)
         hipLaunchKernelGGL(k_radix_digit_scan, dim3(div_up(NDIG, kScanDigits)), dim3(1024), 0, s, hist, nb, NDIG,
-                           a.xtotals, n_dev, K, kSortTile);
+                           a.xtotals, n_dev, K, TILE);
     else
-        hipLaunchKernelGGL(k_radix_digit_scan_dm, dim3(NDIG), dim3(256), 0, s, hist, nb, a.xtotals, n_dev, K, kSortTile);
+        hipLaunchKernelGGL(k_radix_digit_scan_dm, dim3(NDIG), dim3(256), 0, s, hist, nb, a.xtotals, n_dev, K, TILE);
     if (a.ids_only)
-        hipLaunchKernelGGL((k_radix_scatter<kXBits, kSortIPT, false, kValU32, false, true, uint16_t>), dim3(nb), dim3(256),
+        hipLaunchKernelGGL((k_radix_scatter<kXBits, IPT, false, kValU32, false, true, uint16_t>), dim3(nb), dim3(256),
                            0, s, keys, a.pairs_out, nullptr, point_pairs, nullptr, K, kXBits, hist, a.xtotals, nb, bm, ro,
                            (const uint32_t*)nullptr, n_dev);
     else
-        hipLaunchKernelGGL((k_radix_scatter<kXBits, kSortIPT, false, kValPair, false, true, uint16_t>), dim3(nb), dim3(256),
+        hipLaunchKernelGGL((k_radix_scatter<kXBits, IPT, false, kValPair, false, true, uint16_t>), dim3(nb), dim3(256),
                            0, s, keys, a.pairs_out, nullptr, point_pairs, nullptr, K, kXBits, hist, a.xtotals, nb, bm, ro,
                            (const uint32_t*)nullptr, n_dev);
     hipLaunchKernelGGL(k_ranges_counts, dim3(1), dim3(256), 0, s, a.tile_count, a.ntiles, ranges, tile_order);
