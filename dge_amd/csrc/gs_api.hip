@@ -1434,20 +1434,38 @@ int gs_views_backward(gs_views* h, const float* const* dL_dpix, const gs_grads* 
             hipStream_t s0 = (hipStream_t)streams[0];
             const bool debug = h->f[0].s.debug != 0;
             hipStream_t stream = s0;  // (GS_LAUNCHED)
+            const int chunk = gauss_backward_max_views();
+            // one pass for the batch: its first half (the live set from the forwards' touched bytes) runs
+            // on s0 right behind view 0's replay, beside the other views' replays, not after all of them
+            const bool split = h->n <= chunk;
+            GaussBwdArgs ga[GS_MAX_VIEWS];
+            if (split)
+                for (int v = 0; v < h->n; ++v) {
+                    FwdState& f = h->f[v];
+                    ga[v] = gauss_args(&f.s, &f.gp, (int)h->layout[v], f.radii, f.geom, h->bin[v], grads[v],
+                                       h->spec[v] ? h->layout[v] : 0xFFFFFFFFu);
+                }
             for (int v = 0; v < h->n; ++v) {
                 FwdState& f = h->f[v];
                 hipStream_t sv = (hipStream_t)streams[v];
                 int rc = replay_view(&f.s, &f.gp, (int)h->layout[v], f.geom, h->bin[v], f.img, dL_dpix[v], sv);
                 if (rc) return rc;
+                if (split && v == 0) {
+                    GS_SKIP("gauss") { StageScope sc(ST_GAUSS_BWD, s0); launch_gauss_live_views(ga, h->n, s0); }
+                    GS_LAUNCHED("gaussian live set (views)");
+                }
                 if (sv != s0) {
                     if (!h->ev[v] && !(h->ev[v] = event_pool().get())) return set_error(GS_ERR_HIP, "could not create an event");
                     GS_HIP(hipEventRecord(h->ev[v], sv));
                     GS_HIP(hipStreamWaitEvent(s0, h->ev[v], 0));
                 }
             }
-            const int chunk = gauss_backward_max_views();
-            for (int v0 = 0; v0 < h->n; v0 += chunk) {
-                GaussBwdArgs ga[GS_MAX_VIEWS];
+            if (split) {
+                GS_SKIP("gauss") { StageScope sc(ST_GAUSS_BWD, s0);
+                launch_gauss_bwd_live_views(ga, h->n, s0, (hipEvent_t)writes_after); }
+                GS_LAUNCHED("gaussian backward (views)");
+            }
+            for (int v0 = 0; !split && v0 < h->n; v0 += chunk) {
                 const int nv = std::min(chunk, h->n - v0);
                 for (int v = 0; v < nv; ++v) {
                     FwdState& f = h->f[v0 + v];

@@ -747,18 +747,33 @@ __global__ __launch_bounds__(kGB) void k_gauss_bwd_live(GaussBwdViews m) {
     }
 }
 
-void launch_gauss_backward_views(const GaussBwdArgs* views, int n, hipStream_t s, hipEvent_t writes_after) {
-    const GaussBwdArgs& a = views[0];
-    if (a.P <= 0 || n <= 0) return;
+static GaussBwdViews gauss_views(const GaussBwdArgs* views, int n) {
     GaussBwdViews m;
     m.n = n < kMaxBwdViews ? n : kMaxBwdViews;
     for (int v = 0; v < m.n; ++v) m.v[v] = views[v];
-    const int blocks = div_up(a.P, kGB);
-    hipLaunchKernelGGL(k_gauss_live, dim3(blocks), dim3(kGB), 0, s, m);
+    return m;
+}
+
+// Pass 1 alone: it reads only what the forwards left (touched bytes, radii), so it may run before the
+// views' gradient replays end (gs_views_backward: behind view 0's replay, beside the others')
+void launch_gauss_live_views(const GaussBwdArgs* views, int n, hipStream_t s) {
+    if (views[0].P <= 0 || n <= 0) return;
+    hipLaunchKernelGGL(k_gauss_live, dim3(div_up(views[0].P, kGB)), dim3(kGB), 0, s, gauss_views(views, n));
+}
+
+// Pass 2 (after launch_gauss_live_views on an ordered stream, and after every view's replay)
+void launch_gauss_bwd_live_views(const GaussBwdArgs* views, int n, hipStream_t s, hipEvent_t writes_after) {
+    if (views[0].P <= 0 || n <= 0) return;
     // k_gauss_live writes only overwritten (per-call) outputs; the accumulated ones start here
     if (writes_after) (void)hipStreamWaitEvent(s, writes_after, 0);
+    const int blocks = div_up(views[0].P, kGB);
     const int group = std::min(div_up(blocks, kLiveGrid), kLiveGroup);  // (the kernel derives the same)
-    hipLaunchKernelGGL(k_gauss_bwd_live, dim3(div_up(blocks, group)), dim3(kGB), 0, s, m);
+    hipLaunchKernelGGL(k_gauss_bwd_live, dim3(div_up(blocks, group)), dim3(kGB), 0, s, gauss_views(views, n));
+}
+
+void launch_gauss_backward_views(const GaussBwdArgs* views, int n, hipStream_t s, hipEvent_t writes_after) {
+    launch_gauss_live_views(views, n, s);
+    launch_gauss_bwd_live_views(views, n, s, writes_after);
 }
 
 void launch_gauss_backward(const GaussBwdArgs& a, hipStream_t s, hipEvent_t writes_after) {

@@ -438,6 +438,9 @@ void launch_gauss_backward(const GaussBwdArgs& a, hipStream_t s, hipEvent_t writ
 // outputs are shared, GS_ACC_* set on them for every view but the first): at most
 // gauss_backward_max_views() views per call
 void launch_gauss_backward_views(const GaussBwdArgs* views, int n, hipStream_t s, hipEvent_t writes_after = nullptr);
+// the same in its two passes (the first needs only the forwards' outputs)
+void launch_gauss_live_views(const GaussBwdArgs* views, int n, hipStream_t s);
+void launch_gauss_bwd_live_views(const GaussBwdArgs* views, int n, hipStream_t s, hipEvent_t writes_after);
 int gauss_backward_max_views();
 
 // diagnostics (gs_profile_diag_*): per-wave records of the blend kernels,
