@@ -197,10 +197,11 @@ void staging_release(Staging* s, bool synced = false) {
 // ---------------------------------------------------------------------
 enum Stage {
     ST_PREPROCESS = 0, ST_DEPTH_SORT, ST_SCAN, ST_EMIT, ST_TILE_SORT, ST_RANGES, ST_RENDER_FWD,
-    ST_RENDER_BWD, ST_GAUSS_BWD, ST_APPLY_WEIGHTS, ST_COUNT
+    ST_RENDER_BWD, ST_GAUSS_BWD, ST_APPLY_WEIGHTS, ST_GAUSS_LIVE, ST_COUNT
 };
+// (gauss_live: a batch's live-set pass when it runs apart from the rest of gauss_bwd, gs_views_backward)
 const char* kStageNames[ST_COUNT] = {"preprocess", "depth_sort", "scan", "emit", "tile_sort", "ranges",
-                                     "render_fwd", "render_bwd", "gauss_bwd", "apply_weights"};
+                                     "render_fwd", "render_bwd", "gauss_bwd", "apply_weights", "gauss_live"};
 struct ProfRecord {
     int stage;
     hipEvent_t a, b;
@@ -1451,7 +1452,7 @@ int gs_views_backward(gs_views* h, const float* const* dL_dpix, const gs_grads* 
                 int rc = replay_view(&f.s, &f.gp, (int)h->layout[v], f.geom, h->bin[v], f.img, dL_dpix[v], sv);
                 if (rc) return rc;
                 if (split && v == 0) {
-                    GS_SKIP("gauss") { StageScope sc(ST_GAUSS_BWD, s0); launch_gauss_live_views(ga, h->n, s0); }
+                    GS_SKIP("gauss") { StageScope sc(ST_GAUSS_LIVE, s0); launch_gauss_live_views(ga, h->n, s0); }
                     GS_LAUNCHED("gaussian live set (views)");
                 }
                 if (sv != s0) {
