@@ -306,7 +306,7 @@ struct EmitArgs {
     const int* radii;
     uint32_t* scan_sums;         // [scan_blocks + 1]
     uint32_t* first_slot;
-    uint32_t* tile_key;          // K
+    uint32_t* tile_key;          // K (two-level binning: u16 keys y << 7 | x in the same buffer)
     uint32_t* slot_gauss;        // K
     uint32_t* rec_flags32 = nullptr;  // K: zeroed by the emission (the backward's per-slot record flags)
     int scan_blocks;

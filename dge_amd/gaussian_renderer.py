@@ -179,18 +179,15 @@ def _tensor_key(t):
 
 
 class _ForwardEntry:
-    """num_rendered: the binning layout's instance count (a speculated forward's capacity); offs: each
-    buffer's byte offset in its tensor (a batch of views keeps its buffers in one allocation)."""
+    """num_rendered: the binning layout's instance count."""
 
-    def __init__(self, key, refs, num_rendered, P, stream, radii, visible, offs=(0, 0, 0)):
+    def __init__(self, key, refs, num_rendered, P, stream, radii, visible):
         self.key, self.refs, self.num_rendered, self.P = key, refs, num_rendered, P
-        self.stream, self.radii, self.visible, self.offs = stream, radii, visible, tuple(offs)
+        self.stream, self.radii, self.visible = stream, radii, visible
 
     def buffers(self):
         bufs = [r() for r in self.refs]
-        if any(b is None for b in bufs):
-            return None
-        return [b[o:] if o else b for b, o in zip(bufs, self.offs)]
+        return None if any(b is None for b in bufs) else bufs
 
 
 def _geometry_key(pc, rs, index):
