@@ -35,18 +35,6 @@
 
 using namespace gs;
 
-#ifdef GS_ABLATE
-// (probe builds only, never the shipped library: DGE_AMD_ABLATE=a,b,... skips those stages, to measure
-// each stage's marginal cost inside the concurrent multi-view step; outputs are then meaningless)
-#include <cstring>
-static bool ablate(const char* what) {
-    const char* e = getenv("DGE_AMD_ABLATE");
-    return e && strstr(e, what);
-}
-#define GS_SKIP(what) if (!ablate(what))
-#else
-#define GS_SKIP(what)
-#endif
 namespace {
 
 thread_local std::string g_last_error;
@@ -97,47 +85,6 @@ bool tile_sort_unfused() {
 // at c2's 1024 it measured slower than the single-pass tile sort, emit 32 -> 52 us)
 bool two_level(int gx, int gy) {
     return tile_sort_fused(gx, gy) && rect_packable(gx, gy) && !tile_sort_unfused();
-}
-
-// depth-sort bits (three passes of kDepthPassBits; DGE_AMD_DEPTH_SORT_BITS overrides, for probes)
-int depth_sort_bits() {
-    static const int bits = [] {
-        const char* e = getenv("DGE_AMD_DEPTH_SORT_BITS");
-        const int b = e ? atoi(e) : 0;
-        return (b >= 3 && b <= 30) ? b : kDepthSortBits;
-    }();
-    return bits;
-}
-
-// per-pass digit bits of the depth sort (DGE_AMD_DEPTH_PASS_BITS overrides; negative: low passes of
-// that width, the remainder in the last)
-int depth_pass_bits() {
-    static const int bits = [] {
-        const char* e = getenv("DGE_AMD_DEPTH_PASS_BITS");
-        const int b = e ? atoi(e) : 0;
-        return (b != 0 && b >= -10 && b <= 11) ? b : kDepthPassBits;
-    }();
-    return bits;
-}
-
-// DGE_AMD_VIEWS_ISSUE=view: a batch's first halves enqueued view by view (round 3) instead of every
-// preprocess first (A/B)
-bool views_issue_by_view() {
-    static const bool on = [] {
-        const char* e = getenv("DGE_AMD_VIEWS_ISSUE");
-        return e && !strcmp(e, "view");
-    }();
-    return on;
-}
-
-// DGE_AMD_VIEWS_PRE=1: a batch's views preprocessed in one pass (k_preprocess_views) when they share their
-// inputs (A/B; round 3 measured it no faster with the view-by-view issue order)
-bool views_shared_preprocess() {
-    static const bool on = [] {
-        const char* e = getenv("DGE_AMD_VIEWS_PRE");
-        return e && !strcmp(e, "1");
-    }();
-    return on;
 }
 
 // Pinned read-back slot of one forward's preprocess counters + its event.  A
@@ -441,9 +388,9 @@ int bin_after_preprocess(FwdState& f, hipStream_t stream) {
 
     // depth order of the Gaussians (stable: ties keep index order)
     int cur = 0;
-    GS_SKIP("depth") { StageScope sc(ST_DEPTH_SORT, stream);
+    { StageScope sc(ST_DEPTH_SORT, stream);
     cur = radix_sort_aux(at<uint32_t>(geom, gl.key0), at<uint32_t>(geom, gl.key1), at<uint2>(geom, gl.val0),
-                         at<uint2>(geom, gl.val1), pa.rect, (uint32_t)P, depth_sort_bits(), depth_pass_bits(),
+                         at<uint2>(geom, gl.val1), pa.rect, (uint32_t)P, kDepthSortBits, kDepthPassBits,
                          kDepthSortIPT, at<uint32_t>(geom, gl.sort_hist), at<uint32_t>(geom, gl.sort_totals),
                          gl.sort_blocks, stream, nullptr, counters + 2); }
     if (cur < 0) return set_error(GS_ERR_INVALID_ARG, "depth sort: bad digit layout");
@@ -533,7 +480,7 @@ int read_counts(FwdState& f, Counts& c) {
     }
     c.K = K64;
     c.prefilter_fail = st->host[3] != 0;
-    c.wide = K64 && kmax - ~kmin_not >= (1u << depth_sort_bits());
+    c.wide = K64 && kmax - ~kmin_not >= (1u << kDepthSortBits);
     staging_release(st, true);
     f.st = nullptr;
     note_count(f.gp.P, f.g.W, f.g.H, c.K, c.wide);
@@ -668,7 +615,7 @@ int render_launch(FwdState& f, void* bin, uint32_t K_layout, int order_ready, fl
     ra.out_depth = out_depth;
     ra.touched = at<uint8_t>(geom, gl.touched);
     ra.diag = diag_buffer(0, kDiagWords * (size_t)g.tiles * 4);
-    GS_SKIP("fwd") { StageScope sc(ST_RENDER_FWD, stream); launch_render_forward(ra, stream); }
+    { StageScope sc(ST_RENDER_FWD, stream); launch_render_forward(ra, stream); }
     GS_LAUNCHED("render");
     return GS_OK;
 }
@@ -722,7 +669,7 @@ int replay_view(const gs_settings* s, const gs_params* gp, int R, const void* ge
     rb.records = at<float4>(const_cast<void*>(binning), bl.records);
     rb.rec_flags = at<uint8_t>(const_cast<void*>(binning), bl.rec_flags);
     rb.diag = diag_buffer(1, kDiagWords * 4 * bl.nslots);
-    GS_SKIP("rbwd") { StageScope sc(ST_RENDER_BWD, stream); launch_render_backward(rb, stream); }
+    { StageScope sc(ST_RENDER_BWD, stream); launch_render_backward(rb, stream); }
     GS_LAUNCHED("render backward");
     return GS_OK;
 }
@@ -1039,7 +986,7 @@ int gs_render_recolor(const gs_settings* s, int P, int num_rendered, const void*
         ra.touched = nullptr;
         ra.diag = nullptr;
         ra.colors = colors;
-        GS_SKIP("fwd") { StageScope sc(ST_RENDER_FWD, stream); launch_render_forward(ra, stream); }
+        { StageScope sc(ST_RENDER_FWD, stream); launch_render_forward(ra, stream); }
         GS_LAUNCHED("recolor render");
         return GS_OK;
     } catch (const std::exception& e) {
@@ -1178,11 +1125,9 @@ struct gs_views {
     long long K[GS_MAX_VIEWS] = {};      // instance count, -1 until the host knows it
     hipEvent_t ev[GS_MAX_VIEWS] = {};    // the end of each view's work (forward, or per-Gaussian backward pass)
     hipEvent_t fork = nullptr;           // the caller's stream, before the views' work
-    hipEvent_t pre = nullptr;            // the end of the views' shared preprocess (k_preprocess_views)
     ~gs_views() {
         for (int v = 0; v < GS_MAX_VIEWS; ++v) event_pool().put(ev[v]);
         event_pool().put(fork);
-        event_pool().put(pre);
     }
 };
 
@@ -1266,56 +1211,17 @@ int gs_views_forward(int n, const gs_settings* const* s, const gs_params* const*
         // view's preprocess is enqueued before any view's depth sort, so the views' chains start together
         // (view by view, the last view's preprocess started ~200 us of host issue after the first's and
         // the forward phase ended with that view)
-        // one preprocess for every view (k_preprocess_views: the scene read once) when the views share
-        // their inputs, on the first view's stream, which the others then wait for
-        bool shared = views_shared_preprocess() && !views_issue_by_view() && n >= 2;
-        for (int v = 0; v < n && shared; ++v) shared = h->f[v].gp.P > 0 && h->f[v].s.debug == 0;
-        if (shared) {
-            hipStream_t s0 = (hipStream_t)streams[0];
-            const PreprocessArgs* pas[GS_MAX_VIEWS];
-            for (int v = 0; v < n; ++v) {
-                rc = bin_prepare_in(h->f[v], 1, base + off_geom[v], base + off_img[v], s0);
-                if (rc) return rc;
-                pas[v] = &h->f[v].pa;
-            }
-            shared = preprocess_views_ok(pas, n);
-            if (shared) {
-                const bool debug = false;
-                hipStream_t stream = s0;  // (GS_LAUNCHED)
-                GS_SKIP("pre") { StageScope sc(ST_PREPROCESS, s0); launch_preprocess_views(pas, n, s0); }
-                GS_LAUNCHED("preprocess (views)");
-                if (!h->pre && !(h->pre = event_pool().get())) return set_error(GS_ERR_HIP, "could not create an event");
-                GS_HIP(hipEventRecord(h->pre, s0));
-                for (int v = 1; v < n; ++v)
-                    if ((hipStream_t)streams[v] != s0) GS_HIP(hipStreamWaitEvent((hipStream_t)streams[v], h->pre, 0));
-            } else {  // (the buffers are prepared on the first stream: the others wait for it)
-                if (!h->pre && !(h->pre = event_pool().get())) return set_error(GS_ERR_HIP, "could not create an event");
-                GS_HIP(hipEventRecord(h->pre, s0));
-                for (int v = 0; v < n; ++v) {
-                    hipStream_t stream = (hipStream_t)streams[v];
-                    const bool debug = h->f[v].s.debug != 0;
-                    if (stream != s0) GS_HIP(hipStreamWaitEvent(stream, h->pre, 0));
-                    GS_SKIP("pre") { StageScope sc(ST_PREPROCESS, stream); launch_preprocess(h->f[v].pa, stream); }
-                    GS_LAUNCHED("preprocess");
-                }
-                shared = true;  // (every view's preprocess is enqueued)
-            }
-        }
-        for (int v = 0; v < n && !shared; ++v) {
+        for (int v = 0; v < n; ++v) {
             FwdState& f = h->f[v];
             if (f.gp.P == 0) continue;
             hipStream_t stream = (hipStream_t)streams[v];
             const bool debug = f.s.debug != 0;
             rc = bin_prepare_in(f, 1, base + off_geom[v], base + off_img[v], stream);
             if (rc) return rc;
-            GS_SKIP("pre") { StageScope sc(ST_PREPROCESS, stream); launch_preprocess(f.pa, stream); }
+            { StageScope sc(ST_PREPROCESS, stream); launch_preprocess(f.pa, stream); }
             GS_LAUNCHED("preprocess");
-            if (views_issue_by_view()) {  // (A/B: round 3's order)
-                rc = bin_after_preprocess(f, stream);
-                if (rc) return rc;
-            }
         }
-        for (int v = 0; v < n && !views_issue_by_view(); ++v) {
+        for (int v = 0; v < n; ++v) {
             FwdState& f = h->f[v];
             if (f.gp.P == 0) continue;
             rc = bin_after_preprocess(f, (hipStream_t)streams[v]);
@@ -1452,7 +1358,7 @@ int gs_views_backward(gs_views* h, const float* const* dL_dpix, const gs_grads* 
                 int rc = replay_view(&f.s, &f.gp, (int)h->layout[v], f.geom, h->bin[v], f.img, dL_dpix[v], sv);
                 if (rc) return rc;
                 if (split && v == 0) {
-                    GS_SKIP("gauss") { StageScope sc(ST_GAUSS_LIVE, s0); launch_gauss_live_views(ga, h->n, s0); }
+                    { StageScope sc(ST_GAUSS_LIVE, s0); launch_gauss_live_views(ga, h->n, s0); }
                     GS_LAUNCHED("gaussian live set (views)");
                 }
                 if (sv != s0) {
@@ -1462,7 +1368,7 @@ int gs_views_backward(gs_views* h, const float* const* dL_dpix, const gs_grads* 
                 }
             }
             if (split) {
-                GS_SKIP("gauss") { StageScope sc(ST_GAUSS_BWD, s0);
+                { StageScope sc(ST_GAUSS_BWD, s0);
                 launch_gauss_bwd_live_views(ga, h->n, s0, (hipEvent_t)writes_after); }
                 GS_LAUNCHED("gaussian backward (views)");
             }
@@ -1473,7 +1379,7 @@ int gs_views_backward(gs_views* h, const float* const* dL_dpix, const gs_grads* 
                     ga[v] = gauss_args(&f.s, &f.gp, (int)h->layout[v0 + v], f.radii, f.geom, h->bin[v0 + v],
                                        grads[v0 + v], h->spec[v0 + v] ? h->layout[v0 + v] : 0xFFFFFFFFu);
                 }
-                GS_SKIP("gauss") { StageScope sc(ST_GAUSS_BWD, s0);
+                { StageScope sc(ST_GAUSS_BWD, s0);
                 launch_gauss_backward_views(ga, nv, s0, v0 == 0 ? (hipEvent_t)writes_after : nullptr); }
                 GS_LAUNCHED("gaussian backward (views)");
             }
@@ -1514,7 +1420,7 @@ int gs_views_overflow(const gs_views* h, uint8_t* flag, gs_stream_t stream_) {
     if (!h || !flag) return set_error(GS_ERR_INVALID_ARG, "gs_views_overflow: handle and flag are required");
     OverflowArgs a;
     a.n = h->n;
-    a.bits = depth_sort_bits();
+    a.bits = kDepthSortBits;
     for (int v = 0; v < h->n; ++v) {
         const FwdState& f = h->f[v];
         if (!h->spec[v] || f.gp.P == 0) continue;

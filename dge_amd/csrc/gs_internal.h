@@ -255,10 +255,6 @@ struct PreprocessArgs {
     uint8_t* touched;    // zeroed here: k_render_fwd sets the bytes of Gaussians some pixel blends
 };
 void launch_preprocess(const PreprocessArgs& a, hipStream_t s);
-// a batch's views of one scene in one pass (k_preprocess_views): when preprocess_views_ok (2..4 views, the
-// same inputs, fp32 SH rows of the full pitch, no index, no precomputed colours or covariances)
-bool preprocess_views_ok(const PreprocessArgs* const* v, int n);
-void launch_preprocess_views(const PreprocessArgs* const* v, int n, hipStream_t s);
 void launch_depth_keys32(int P, const uint32_t* rect, const Splat* splat, uint32_t* key, hipStream_t s);
 void launch_mark_visible(int P, const float* means3D, const float* view, uint8_t* present, hipStream_t s);
 // (test hook gs_activate_params) the fused path's in-kernel activations over P rows

@@ -267,169 +267,6 @@ __global__ __launch_bounds__(256) void k_preprocess(PreprocessArgs a) {
     }
 }
 
-// Several views of one scene in one pass (gs_views_forward: DGE renders a batch of views of the same
-// Gaussians, threestudio/systems/DGE.py:170-239): every per-Gaussian input — position, scale, rotation,
-// opacity, coefficient 0 and the block's 15 SH rows staged through LDS — is read once and projected into
-// each view in turn with k_preprocess<false>'s operations (every view's outputs bit-identical to its
-// own k_preprocess), instead of once per view: at c2 236 of the ~334 B per Gaussian and view.  fp32 rows
-// of the full pitch without an index only (the two-half staging cannot stay resident across views).
-constexpr int kPreViews = 4;
-struct PreprocessViews {
-    PreprocessArgs a[kPreViews];
-    int n;
-};
-__global__ __launch_bounds__(256) void k_preprocess_views(PreprocessViews m) {
-    const PreprocessArgs& a = m.a[0];  // the inputs every view shares
-    __shared__ float s_sh[256 * kShPitch];
-    __shared__ uint32_t part[4][3];
-    const int idx0 = blockIdx.x * 256;
-    const int idx = idx0 + threadIdx.x;
-    const int ncol = (a.M - 1) * 3 < kShPitch ? (a.M - 1) * 3 : kShPitch;
-    const bool stage_sh = a.copy_colors && !a.colors_precomp && a.sh.dc && ncol > 0;
-    const int nrow = a.P - idx0 < 256 ? a.P - idx0 : 256;
-    if (stage_sh) sh_rows_load<256>(a.sh.rest + (size_t)idx0 * a.sh.rest_stride, a.sh.rest_stride, s_sh, nrow, ncol);
-    f3 p = mk3(0, 0, 0), sc_in = mk3(0.f, 0.f, 0.f), c0 = mk3(0.f, 0.f, 0.f);
-    float4 q_in = make_float4(0.f, 0.f, 0.f, 0.f);
-    float op_in = 0.f;
-    if (idx < a.P) {
-        p = ld3(a.means3D + 3 * (size_t)idx);
-        q_in = *reinterpret_cast<const float4*>(a.rotations + 4 * (size_t)idx);
-        sc_in = ld3(a.scales + 3 * (size_t)idx);
-        op_in = a.opacities[idx];
-        if (a.sh.dc && !a.colors_precomp) c0 = sh_dc3(a.sh.dc, a.sh.half, (size_t)idx * a.sh.dc_stride);
-    }
-    if (stage_sh) __syncthreads();  // rows staged
-    for (int vi = 0; vi < m.n; ++vi) {
-        const PreprocessArgs& b = m.a[vi];
-        uint32_t touched = 0, rect = 0, key = 0xFFFFFFFFu;
-        int radius_out = 0;
-        uint8_t clamp_bits = 0;
-        f3 rgb = mk3(0, 0, 0);
-        float2 pix = make_float2(0.f, 0.f);
-        float4 conic = make_float4(0.f, 0.f, 0.f, 0.f);
-        float depth = 0.f;
-        if (idx < a.P) {
-            const float* v = b.view;
-            const float* pm = b.proj;
-            float cov3[6];
-            float4 q = q_in;
-            f3 sc = sc_in;
-            const float4 ph = proj_point(pm, p);
-            const float pw = 1.0f / (ph.w + 0.0000001f);
-            const f3 pv = view_point(v, p);
-            const bool visible = pv.z > 0.2f;
-            if (!visible && b.prefiltered) atomicOr(&b.counters[3], 1u);
-            if (visible) {
-                if (a.activation) {
-                    float len;
-                    q = act_normalize(q, len);
-                    sc = mk3(expf(sc.x), expf(sc.y), expf(sc.z));
-                }
-                cov3d_from_scale_rot(sc, b.scale_modifier, q, cov3);
-                Ewa e;
-                ewa_setup(p, b.fx, b.fy, b.tanfovx, b.tanfovy, cov3, v, e);
-                float ca, cb, cc;
-                ewa_cov2d(e, ca, cb, cc);
-                const float det = ca * cc - cb * cb;
-                if (det != 0.0f) {
-                    const float det_inv = 1.f / det;
-                    const float op = a.activation ? act_sigmoid(op_in) : op_in;
-                    conic = make_float4(cc * det_inv, -cb * det_inv, ca * det_inv, op);
-                    const float mid = 0.5f * (ca + cc);
-                    const float l1 = mid + sqrtf(fmaxf(0.1f, mid * mid - det));
-                    const float l2 = mid - sqrtf(fmaxf(0.1f, mid * mid - det));
-                    const float rad = ceilf(3.f * sqrtf(fmaxf(l1, l2)));
-                    pix = make_float2(ndc_to_pixel(ph.x * pw, b.W), ndc_to_pixel(ph.y * pw, b.H));
-                    const Rect r = tile_rect(pix.x, pix.y, (int)rad, b.gx, b.gy);
-                    const uint32_t area = (uint32_t)((r.y1 - r.y0) * (r.x1 - r.x0));
-                    if (area != 0) {
-                        rect = b.rect_packed ? pack_rect(r.x0, r.y0, r.x1, r.y1) : area;
-                        radius_out = (int)rad;
-                        touched = area;
-                        depth = pv.z;
-                        key = __float_as_uint(pv.z);
-                    }
-                }
-            }
-        }
-        const bool sh_color = touched && a.copy_colors && !a.colors_precomp;
-        if (touched && a.copy_colors && a.colors_precomp) rgb = ld3(a.colors_precomp + 3 * (size_t)idx);
-        if (sh_color) {
-            const f3 dir = sh_dir(p, ld3(b.campos));
-            const f3 head = sh_rgb_head(b.D, dir, c0, s_sh + threadIdx.x * kShPitch);
-            rgb = sh_rgb_tail(b.D, dir, head, s_sh + threadIdx.x * kShPitch + kShA, clamp_bits);
-        }
-        if (idx < a.P) {
-            if (touched) {
-                Splat sp;
-                sp.xy = pix;
-                sp.pad0 = make_float2(0.f, 0.f);
-                sp.co = conic;
-                sp.rgbd = make_float4(rgb.x, rgb.y, rgb.z, depth);
-                sp.pad1 = make_float4(0.f, 0.f, 0.f, 0.f);
-                b.splat[idx] = sp;
-            }
-            if (!b.rect_packed || !b.radii_out) b.radii[idx] = radius_out;
-            if (b.radii_out) b.radii_out[idx] = radius_out;
-            if (b.visible_out) b.visible_out[idx] = radius_out > 0;
-            b.tiles_touched[idx] = touched;
-            b.clamped[idx] = clamp_bits;
-            b.depth_key[idx] = key;
-            b.rect[idx] = rect;
-            if (b.touched) b.touched[idx] = 0;
-        }
-        uint32_t s = touched, kmax = touched ? key : 0u, kmin_n = touched ? ~key : 0u;
-#pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) {
-            s += (uint32_t)__shfl_xor((int)s, o);
-            kmax = max(kmax, (uint32_t)__shfl_xor((int)kmax, o));
-            kmin_n = max(kmin_n, (uint32_t)__shfl_xor((int)kmin_n, o));
-        }
-        if ((threadIdx.x & 63) == 0) {
-            part[threadIdx.x >> 6][0] = s;
-            part[threadIdx.x >> 6][1] = kmax;
-            part[threadIdx.x >> 6][2] = kmin_n;
-        }
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            const uint32_t t = part[0][0] + part[1][0] + part[2][0] + part[3][0];
-            if (t) {
-                uint32_t* c = b.counters + kCounterStride * (blockIdx.x % kCounterSlots);
-                atomicAdd(&c[0], t);
-                atomicMax(&c[1], max(max(part[0][1], part[1][1]), max(part[2][1], part[3][1])));
-                atomicMax(&c[2], max(max(part[0][2], part[1][2]), max(part[2][2], part[3][2])));
-            }
-        }
-        __syncthreads();  // (part is reused by the next view)
-    }
-}
-
-bool preprocess_views_ok(const PreprocessArgs* const* v, int n) {
-    if (n < 2 || n > kPreViews) return false;
-    const PreprocessArgs& a = *v[0];
-    const int ncol = (a.M - 1) * 3;
-    if (a.P <= 0 || a.index || a.sh.half || a.cov3D_precomp || !a.copy_colors || a.colors_precomp || !a.sh.dc ||
-        (a.M > 1 && ncol != kShPitch) || (a.M > 1 && a.sh.rest_stride != kShPitch))
-        return false;
-    for (int i = 1; i < n; ++i) {
-        const PreprocessArgs& b = *v[i];
-        if (b.P != a.P || b.means3D != a.means3D || b.scales != a.scales || b.rotations != a.rotations ||
-            b.opacities != a.opacities || b.sh.dc != a.sh.dc || b.sh.rest != a.sh.rest || b.M != a.M ||
-            b.D != a.D || b.activation != a.activation || b.index || b.cov3D_precomp || b.colors_precomp ||
-            b.copy_colors != a.copy_colors || b.sh.half || b.sh.dc_stride != a.sh.dc_stride ||
-            b.sh.rest_stride != a.sh.rest_stride)
-            return false;
-    }
-    return true;
-}
-
-void launch_preprocess_views(const PreprocessArgs* const* v, int n, hipStream_t s) {
-    PreprocessViews m;
-    m.n = n;
-    for (int i = 0; i < n; ++i) m.a[i] = *v[i];
-    hipLaunchKernelGGL(k_preprocess_views, dim3(div_up(v[0]->P, 256)), dim3(256), 0, s, m);
-}
-
 void launch_preprocess(const PreprocessArgs& a, hipStream_t s) {
     if (a.P <= 0) return;
     if (a.sh.half || a.index)  // (the one-pass staging needs the block's rows contiguous)

@@ -109,14 +109,7 @@ __device__ __forceinline__ void pixel_alpha4(f4v x, f4v y, f4v ncx, f4v ncy, f4v
 #pragma clang fp contract(off)
     dx = x + npx;
     dy = y + npy;
-#ifdef GS_POWER_FMA
-    // (contracted as nvcc's default -fmad=true would: two fused steps instead of two adds and a scale)
-    const f4v half = {0.5f, 0.5f, 0.5f, 0.5f};
-    const f4v power = __builtin_elementwise_fma(
-        half, __builtin_elementwise_fma(ncz * dy, dy, ncx * dx * dx), ncy * dx * dy);
-#else
     const f4v power = 0.5f * (ncx * dx * dx + ncz * dy * dy) + ncy * dx * dy;
-#endif
     G = gs_exp4(power);
     const f4v oG = op * G;
 #pragma unroll
@@ -149,17 +142,6 @@ __device__ __forceinline__ float blend_chain(float a, float4 fe, uint32_t pos, f
     const bool go = tT >= 0.0001f;
     const float Tw = go ? Ts : 0.0f;
     Ts = go ? tT : -fabsf(Ts);
-#ifdef GS_BLEND_W
-    // f * (alpha T): the blend weight w = a' Tw once, every sum one fma with it
-    const float w = a * Tw;
-    const f2v w2 = {w, w};
-    C01 = __builtin_elementwise_fma(f2v{fe.x, fe.y}, w2, C01);
-    C2D = __builtin_elementwise_fma(f2v{fe.z, fe.w}, w2, C2D);
-    if constexpr (SEG) {
-        L01 = __builtin_elementwise_fma(f2v{fe.x, fe.y}, w2, L01);  // the segment's own colour sum (backward start)
-        L2 = __builtin_fmaf(fe.z, w, L2);
-    }
-#else
     const f2v a2 = {a, a}, T2 = {Tw, Tw};
     const f2v fa01 = f2v{fe.x, fe.y} * a2, fa2d = f2v{fe.z, fe.w} * a2;
     C01 = __builtin_elementwise_fma(fa01, T2, C01);
@@ -169,7 +151,6 @@ __device__ __forceinline__ float blend_chain(float a, float4 fe, uint32_t pos, f
         L2 = __builtin_fmaf(fa2d.x, Tw, L2);
     }
     const float w = a * Tw;
-#endif
     last = w > 0.0f ? pos : last;
     return w;
 }

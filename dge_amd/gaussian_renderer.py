@@ -235,11 +235,14 @@ def _fused_begin(viewpoint_camera, pc, pipe, bg_color, scaling_modifier=1.0, ove
     # thresholded) never receives a gradient: render it with the forward-only kernels and, should a
     # backward come after all, recompute the forward with the backward's bookkeeping then (lazy)
     lazy = may_bwd and colors is not None and not colors.requires_grad and _LAZY_OVERRIDE
+    # forward_only: the kernels skip the backward's bookkeeping, and a two-level binning then keeps the
+    # Gaussian ids alone (gs_raster.h gs_render_recolor): such a forward is never a recolor source
+    forward_only = lazy or not may_bwd
     st = {"rs": rs, "index": index, "n": n, "f_dc": f_dc, "f_rest": f_rest, "colors": colors, "visible": visible,
-          "prepared": None, "lazy": lazy}
+          "prepared": None, "lazy": lazy, "forward_only": forward_only}
     if rs.debug:  # debug mode: the one-call forward, which keeps the reference's failure snapshot
         return st
-    if colors is not None and not colors.requires_grad and (lazy or not may_bwd):
+    if colors is not None and not colors.requires_grad and forward_only:
         src = _recolor_source(pc, rs, index)
         if src is not None:  # the same geometry as the last forward: only its blend again, other colours
             global _RECOLOR_HITS
@@ -248,6 +251,9 @@ def _fused_begin(viewpoint_camera, pc, pipe, bg_color, scaling_modifier=1.0, ove
             cur = torch.cuda.current_stream(xyz.device)
             if src.stream != cur:
                 cur.wait_stream(src.stream)
+                # (the source's graph may be freed on its stream while this blend still reads its buffers)
+                for t in (geom, binning, img):
+                    t.record_stream(cur)
             color, depth = _C.render_recolor(rs.bg, colors, rs.viewmatrix, rs.projmatrix, rs.campos, rs.tanfovx,
                                              rs.tanfovy, rs.image_height, rs.image_width, rs.sh_degree,
                                              rs.scale_modifier, rs.prefiltered, n, src.num_rendered, geom, binning,
@@ -261,7 +267,7 @@ def _fused_begin(viewpoint_camera, pc, pipe, bg_color, scaling_modifier=1.0, ove
         rs.bg, xyz, empty if f_dc is None else f_dc, empty if f_rest is None else f_rest,
         empty if colors is None else colors, pc._opacity, pc._scaling, pc._rotation, rs.scale_modifier,
         rs.viewmatrix, rs.projmatrix, rs.tanfovx, rs.tanfovy, rs.image_height, rs.image_width, rs.sh_degree,
-        rs.campos, rs.prefiltered, rs.debug, index=index, visible=visible, forward_only=lazy or not may_bwd)
+        rs.campos, rs.prefiltered, rs.debug, index=index, visible=visible, forward_only=forward_only)
     return st
 
 
@@ -274,7 +280,8 @@ def _fused_end(st, pc):
         xyz, screenspace_points, st["f_dc"], st["f_rest"], st["colors"], pc._opacity, pc._scaling, pc._rotation,
         st["rs"], st["index"], st["visible"], prepared=prep, recompute=st["lazy"] and prep is not None)
     fin = getattr(prep, "finished", None)
-    if fin is not None and _RECOLOR:  # a forward with backward bookkeeping: later recolor renders may reuse it
+    if fin is not None and _RECOLOR and not st.get("forward_only", True):
+        # a forward with backward bookkeeping: later recolor renders may reuse it
         nr, geom, binning, img = fin
         prep.finished = None
         ent = _ForwardEntry(_geometry_key(pc, st["rs"], st["index"]), [weakref.ref(geom), weakref.ref(binning),

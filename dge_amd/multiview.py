@@ -250,7 +250,8 @@ class GradBucket:
                 packed = _rows_gather(mats, rows)
                 dist.all_reduce(packed, op=dist.ReduceOp.SUM, group=group)
                 _rows_scatter(mats, rows, packed)
-        self._set_rows_cap(m, mats)
+        if not overflow:  # (an overflowed step's marks were abandoned: allreduce() set the cap from its scan)
+            self._set_rows_cap(m, mats)
         self._reduced = stream.record_event() if side else None
         return None
 
@@ -268,7 +269,8 @@ class GradBucket:
         ev, pinned, cap, idx, group, mats, stream = d
         ev.synchronize()
         m, overflow = int(pinned[0]), int(pinned[1])
-        self._set_rows_cap(m, mats)
+        if not overflow:  # (else allreduce() below sets the cap from the union it scans)
+            self._set_rows_cap(m, mats)
         if m <= cap and not overflow:
             return False
         import contextlib
@@ -319,6 +321,7 @@ class GradBucket:
         live = _rows_live(mats, n)
         dist.all_reduce(live, op=dist.ReduceOp.MAX, group=group)
         idx = torch.nonzero(live).squeeze(1)
+        self._set_rows_cap(int(idx.numel()), mats)  # (the next hinted step's speculated capacity)
         if 2 * idx.numel() > n:  # mostly dense: packing would not pay
             return dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=group)
         packed = _rows_gather(mats, idx)

@@ -887,6 +887,225 @@ int go_backward_chain(go_state *st, const go_settings *s, const go_inputs *in, c
     return GO_OK;
 }
 
+/* ------------------------------------------------------------------ */
+/* Magnitude of the chain's terms (test infrastructure for the per-    */
+/* element gradient bar): gauss_chain evaluated in absolute arithmetic */
+/* ------------------------------------------------------------------ */
+/* Every output of the chain is a sum of products (forward-state coefficient) x (a rasterizer sum).
+ * go_backward_chain_mag evaluates the same chain with each coefficient's absolute value, each
+ * subtraction as an addition and the inputs replaced by per-sum magnitudes m9 (the oracle's mag9:
+ * sums of |sub-term| over the contributing pixels), in double: the result bounds |chain(g)| for any
+ * |g| <= m9, so it is the scale against which both a reordered rasterizer sum and the chain's own
+ * float rounding (whose error is u x the terms it adds, cancelled or not) are measured.  Coefficients
+ * (T, V, W, the SH direction terms, R, S, ...) are computed exactly as the float chain computes them:
+ * they are forward state, identical wherever the forward is. */
+#define FA(x) fabs((double)(x))
+static void cov2d_bwd_mag(v3 mean, float fx, float fy, float tanfovx, float tanfovy, const float *cov3D,
+                          const float *view, const double mcon[3], double mcov[6], double mgm[3]) {
+    ewa_ctx e;
+    ewa_setup(mean, fx, fy, tanfovx, tanfovy, cov3D, view, &e);
+    const double xm = e.txtz < -e.limx || e.txtz > e.limx ? 0 : 1;
+    const double ym = e.tytz < -e.limy || e.tytz > e.limy ? 0 : 1;
+    const cm3 *T = &e.T, *W = &e.W, *V = &e.V;
+    cm3 Tt = cm3T(T), Vt = cm3T(V);
+    cm3 TtV = cm3mul(&Tt, &Vt);
+    cm3 cov2D = cm3mul(&TtV, T);
+    float a = cov2D.c[0][0] += 0.3f;
+    float b = cov2D.c[0][1];
+    float c = cov2D.c[1][1] += 0.3f;
+    float denom = a * c - b * b;
+    float denom2inv = 1.0f / ((denom * denom) + 0.0000001f);
+    double ma = 0, mb = 0, mc = 0;
+#define Tm(i, j) (T->c[i][j])
+#define Vm(i, j) (V->c[i][j])
+    for (int i = 0; i < 6; ++i) mcov[i] = 0;
+    if (denom2inv != 0) {
+        ma = FA(denom2inv) * (FA(c * c) * mcon[0] + FA(2 * b * c) * mcon[1] + FA(denom - a * c) * mcon[2]);
+        mc = FA(denom2inv) * (FA(a * a) * mcon[2] + FA(2 * a * b) * mcon[1] + FA(denom - a * c) * mcon[0]);
+        mb = FA(denom2inv) * 2 * (FA(b * c) * mcon[0] + FA(denom + 2 * b * b) * mcon[1] + FA(a * b) * mcon[2]);
+        mcov[0] = FA(Tm(0, 0) * Tm(0, 0)) * ma + FA(Tm(0, 0) * Tm(1, 0)) * mb + FA(Tm(1, 0) * Tm(1, 0)) * mc;
+        mcov[3] = FA(Tm(0, 1) * Tm(0, 1)) * ma + FA(Tm(0, 1) * Tm(1, 1)) * mb + FA(Tm(1, 1) * Tm(1, 1)) * mc;
+        mcov[5] = FA(Tm(0, 2) * Tm(0, 2)) * ma + FA(Tm(0, 2) * Tm(1, 2)) * mb + FA(Tm(1, 2) * Tm(1, 2)) * mc;
+        mcov[1] = FA(2 * Tm(0, 0) * Tm(0, 1)) * ma + (FA(Tm(0, 0) * Tm(1, 1)) + FA(Tm(0, 1) * Tm(1, 0))) * mb +
+                  FA(2 * Tm(1, 0) * Tm(1, 1)) * mc;
+        mcov[2] = FA(2 * Tm(0, 0) * Tm(0, 2)) * ma + (FA(Tm(0, 0) * Tm(1, 2)) + FA(Tm(0, 2) * Tm(1, 0))) * mb +
+                  FA(2 * Tm(1, 0) * Tm(1, 2)) * mc;
+        mcov[4] = FA(2 * Tm(0, 2) * Tm(0, 1)) * ma + (FA(Tm(0, 1) * Tm(1, 2)) + FA(Tm(0, 2) * Tm(1, 1))) * mb +
+                  FA(2 * Tm(1, 1) * Tm(1, 2)) * mc;
+    }
+    double mT[2][3];
+    for (int k = 0; k < 3; ++k) {  /* dL_dT0k, dL_dT1k (backward.cu:230-241), terms kept separate */
+        double tv0 = 0, tv1 = 0;
+        for (int j = 0; j < 3; ++j) { tv0 += FA(Tm(0, j) * Vm(k, j)); tv1 += FA(Tm(1, j) * Vm(k, j)); }
+        mT[0][k] = 2 * tv0 * ma + tv1 * mb;
+        mT[1][k] = 2 * tv1 * mc + tv0 * mb;
+    }
+#undef Tm
+#undef Vm
+#define Wm(i, j) FA(W->c[i][j])
+    double mJ00 = Wm(0, 0) * mT[0][0] + Wm(0, 1) * mT[0][1] + Wm(0, 2) * mT[0][2];
+    double mJ02 = Wm(2, 0) * mT[0][0] + Wm(2, 1) * mT[0][1] + Wm(2, 2) * mT[0][2];
+    double mJ11 = Wm(1, 0) * mT[1][0] + Wm(1, 1) * mT[1][1] + Wm(1, 2) * mT[1][2];
+    double mJ12 = Wm(2, 0) * mT[1][0] + Wm(2, 1) * mT[1][1] + Wm(2, 2) * mT[1][2];
+#undef Wm
+    const v3 t = e.t;
+    float tz = 1.f / t.z, tz2 = tz * tz, tz3 = tz2 * tz;
+    double mtx = xm * FA(fx * tz2) * mJ02;
+    double mty = ym * FA(fy * tz2) * mJ12;
+    double mtz = FA(fx * tz2) * mJ00 + FA(fy * tz2) * mJ11 + FA((2 * fx * t.x) * tz3) * mJ02 + FA((2 * fy * t.y) * tz3) * mJ12;
+    /* xform_vec43_T with |view| */
+    mgm[0] = FA(view[0]) * mtx + FA(view[1]) * mty + FA(view[2]) * mtz;
+    mgm[1] = FA(view[4]) * mtx + FA(view[5]) * mty + FA(view[6]) * mtz;
+    mgm[2] = FA(view[8]) * mtx + FA(view[9]) * mty + FA(view[10]) * mtz;
+}
+
+/* sh_bwd in absolute arithmetic: |dL_dsh| bounds and the view-direction mean-gradient magnitude */
+static void sh_bwd_mag(int deg, v3 pos, v3 campos, const float *sh_g, const unsigned char *clamped,
+                       const double mcol[3], double *msh, double mdir[3]) {
+    v3 dir_orig = v3sub(pos, campos);
+    float len = sqrtf(v3dot(dir_orig, dir_orig));
+    float x = dir_orig.x / len, y = dir_orig.y / len, z = dir_orig.z / len;
+    const double mg[3] = {clamped[0] ? 0 : mcol[0], clamped[1] ? 0 : mcol[1], clamped[2] ? 0 : mcol[2]};
+    /* basis coefficient of each SH row (the DSH scalars of sh_bwd) */
+    float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
+    float basis[16] = {kC0, -kC1 * y, kC1 * z, -kC1 * x, kC2[0] * xy, kC2[1] * yz, kC2[2] * (2.f * zz - xx - yy),
+                       kC2[3] * xz, kC2[4] * (xx - yy), kC3[0] * y * (3.f * xx - yy), kC3[1] * xy * z,
+                       kC3[2] * y * (4.f * zz - xx - yy), kC3[3] * z * (2.f * zz - 3.f * xx - 3.f * yy),
+                       kC3[4] * x * (4.f * zz - xx - yy), kC3[5] * z * (xx - yy), kC3[6] * x * (xx - 3.f * yy)};
+    const int n = deg == 0 ? 1 : deg == 1 ? 4 : deg == 2 ? 9 : 16;
+    for (int k = 0; k < n; ++k)
+        for (int ch = 0; ch < 3; ++ch) msh[3 * k + ch] = FA(basis[k]) * mg[ch];
+    /* dL_ddir = (dx.g, dy.g, dz.g): dx, dy, dz do not depend on g (forward state), recomputed here with
+     * sh_bwd's sums */
+    double mdd[3] = {0, 0, 0};
+    if (deg > 0) {
+#define SH(k) v3ld(sh_g + 3 * (k))
+        v3 dx = v3scale(SH(3), -kC1), dy = v3scale(SH(1), -kC1), dz = v3scale(SH(2), kC1);
+        if (deg > 1) {
+            v3 sx = v3add(v3add(v3add(v3scale(SH(4), kC2[0] * y), v3scale(SH(6), kC2[2] * 2.f * -x)), v3scale(SH(7), kC2[3] * z)),
+                          v3scale(SH(8), kC2[4] * 2.f * x));
+            v3 sy = v3add(v3add(v3add(v3scale(SH(4), kC2[0] * x), v3scale(SH(5), kC2[1] * z)), v3scale(SH(6), kC2[2] * 2.f * -y)),
+                          v3scale(SH(8), kC2[4] * 2.f * -y));
+            v3 sz = v3add(v3add(v3scale(SH(5), kC2[1] * y), v3scale(SH(6), kC2[2] * 2.f * 2.f * z)), v3scale(SH(7), kC2[3] * x));
+            dx = v3add(dx, sx); dy = v3add(dy, sy); dz = v3add(dz, sz);
+            if (deg > 2) {
+                v3 tx = v3scale(SH(9), kC3[0] * 3.f * 2.f * xy);
+                tx = v3add(tx, v3scale(SH(10), kC3[1] * yz));
+                tx = v3add(tx, v3scale(SH(11), kC3[2] * -2.f * xy));
+                tx = v3add(tx, v3scale(SH(12), kC3[3] * -3.f * 2.f * xz));
+                tx = v3add(tx, v3scale(SH(13), kC3[4] * (-3.f * xx + 4.f * zz - yy)));
+                tx = v3add(tx, v3scale(SH(14), kC3[5] * 2.f * xz));
+                tx = v3add(tx, v3scale(SH(15), kC3[6] * 3.f * (xx - yy)));
+                v3 ty = v3scale(SH(9), kC3[0] * 3.f * (xx - yy));
+                ty = v3add(ty, v3scale(SH(10), kC3[1] * xz));
+                ty = v3add(ty, v3scale(SH(11), kC3[2] * (-3.f * yy + 4.f * zz - xx)));
+                ty = v3add(ty, v3scale(SH(12), kC3[3] * -3.f * 2.f * yz));
+                ty = v3add(ty, v3scale(SH(13), kC3[4] * -2.f * xy));
+                ty = v3add(ty, v3scale(SH(14), kC3[5] * -2.f * yz));
+                ty = v3add(ty, v3scale(SH(15), kC3[6] * -3.f * 2.f * xy));
+                v3 tzv = v3scale(SH(10), kC3[1] * xy);
+                tzv = v3add(tzv, v3scale(SH(11), kC3[2] * 4.f * 2.f * yz));
+                tzv = v3add(tzv, v3scale(SH(12), kC3[3] * 3.f * (2.f * zz - xx - yy)));
+                tzv = v3add(tzv, v3scale(SH(13), kC3[4] * 4.f * 2.f * xz));
+                tzv = v3add(tzv, v3scale(SH(14), kC3[5] * (xx - yy)));
+                dx = v3add(dx, tx); dy = v3add(dy, ty); dz = v3add(dz, tzv);
+            }
+        }
+#undef SH
+        mdd[0] = FA(dx.x) * mg[0] + FA(dx.y) * mg[1] + FA(dx.z) * mg[2];
+        mdd[1] = FA(dy.x) * mg[0] + FA(dy.y) * mg[1] + FA(dy.z) * mg[2];
+        mdd[2] = FA(dz.x) * mg[0] + FA(dz.y) * mg[1] + FA(dz.z) * mg[2];
+    }
+    /* dnormvdv3 with absolute coefficients */
+    v3 v = dir_orig;
+    float sum2 = v.x * v.x + v.y * v.y + v.z * v.z;
+    float invsum32 = 1.0f / sqrtf(sum2 * sum2 * sum2);
+    mdir[0] = (FA(sum2 - v.x * v.x) * mdd[0] + FA(v.y * v.x) * mdd[1] + FA(v.z * v.x) * mdd[2]) * FA(invsum32);
+    mdir[1] = (FA(v.x * v.y) * mdd[0] + FA(sum2 - v.y * v.y) * mdd[1] + FA(v.z * v.y) * mdd[2]) * FA(invsum32);
+    mdir[2] = (FA(v.x * v.z) * mdd[0] + FA(v.y * v.z) * mdd[1] + FA(sum2 - v.z * v.z) * mdd[2]) * FA(invsum32);
+}
+
+/* cov3d_bwd in absolute arithmetic */
+static void cov3d_bwd_mag(const float *scale, float mod, const float *rot, const double mcov[6], double mscale[3],
+                          double mrot[4]) {
+    float r = rot[0], x = rot[1], y = rot[2], z = rot[3];
+    cm3 R = cm3cols(1.f - 2.f * (y * y + z * z), 2.f * (x * y - r * z), 2.f * (x * z + r * y),
+                    2.f * (x * y + r * z), 1.f - 2.f * (x * x + z * z), 2.f * (y * z - r * x),
+                    2.f * (x * z - r * y), 2.f * (y * z + r * x), 1.f - 2.f * (x * x + y * y));
+    cm3 S = cm3cols(1, 0, 0, 0, 1, 0, 0, 0, 1);
+    v3 s = v3make(mod * scale[0], mod * scale[1], mod * scale[2]);
+    S.c[0][0] = s.x; S.c[1][1] = s.y; S.c[2][2] = s.z;
+    cm3 M = cm3mul(&S, &R);
+    /* dSig (col-major, symmetric) magnitudes */
+    double dS[3][3] = {{mcov[0], 0.5 * mcov[1], 0.5 * mcov[2]}, {0.5 * mcov[1], mcov[3], 0.5 * mcov[4]},
+                       {0.5 * mcov[2], 0.5 * mcov[4], mcov[5]}};
+    double dM[3][3];  /* dM = (2M) * dSig, glm order: dM[c][r] = sum_k 2M[k][r] dSig[c][k] */
+    for (int c = 0; c < 3; ++c)
+        for (int rr = 0; rr < 3; ++rr)
+            dM[c][rr] = FA(2.0f * M.c[0][rr]) * dS[c][0] + FA(2.0f * M.c[1][rr]) * dS[c][1] + FA(2.0f * M.c[2][rr]) * dS[c][2];
+    /* Rt.c[i][k] = R.c[k][i]; dMt.c[i][k] = dM[k][i] */
+    for (int i = 0; i < 3; ++i) mscale[i] = FA(R.c[0][i]) * dM[0][i] + FA(R.c[1][i]) * dM[1][i] + FA(R.c[2][i]) * dM[2][i];
+    double D[3][3];
+    const double sv[3] = {FA(s.x), FA(s.y), FA(s.z)};
+    for (int i = 0; i < 3; ++i)
+        for (int k = 0; k < 3; ++k) D[i][k] = dM[k][i] * sv[i];
+    mrot[0] = FA(2 * z) * (D[0][1] + D[1][0]) + FA(2 * y) * (D[2][0] + D[0][2]) + FA(2 * x) * (D[1][2] + D[2][1]);
+    mrot[1] = FA(2 * y) * (D[1][0] + D[0][1]) + FA(2 * z) * (D[2][0] + D[0][2]) + FA(2 * r) * (D[1][2] + D[2][1]) +
+              FA(4 * x) * (D[2][2] + D[1][1]);
+    mrot[2] = FA(2 * x) * (D[1][0] + D[0][1]) + FA(2 * r) * (D[2][0] + D[0][2]) + FA(2 * z) * (D[1][2] + D[2][1]) +
+              FA(4 * y) * (D[2][2] + D[0][0]);
+    mrot[3] = FA(2 * r) * (D[0][1] + D[1][0]) + FA(2 * x) * (D[2][0] + D[0][2]) + FA(2 * y) * (D[1][2] + D[2][1]) +
+              FA(4 * z) * (D[1][1] + D[0][0]);
+}
+
+/* gauss_chain in absolute arithmetic from magnitudes m9 [P,9] (same layout as g9); outputs as gauss_chain's
+ * (dL_dmeans3D [P,3], dL_dcov3D [P,6], dL_dsh [P,M,3], dL_dscales [P,3], dL_drotations [P,4]) in double. */
+int go_backward_chain_mag(go_state *st, const go_settings *s, const go_inputs *in, const float *m9, double *m_means3D,
+                          double *m_cov3D, double *m_sh, double *m_scales, double *m_rotations) {
+    const int P = in->P, M = in->M;
+    if (P == 0) return GO_OK;
+    memset(m_means3D, 0, 3 * (size_t)P * sizeof(double));
+    memset(m_cov3D, 0, 6 * (size_t)P * sizeof(double));
+    if (M > 0 && m_sh) memset(m_sh, 0, (size_t)P * M * 3 * sizeof(double));
+    memset(m_scales, 0, 3 * (size_t)P * sizeof(double));
+    memset(m_rotations, 0, 4 * (size_t)P * sizeof(double));
+    const float fy = s->image_height / (2.0f * s->tanfovy);
+    const float fx = s->image_width / (2.0f * s->tanfovx);
+    const float *proj = s->projmatrix;
+#pragma omp parallel for schedule(static)
+    for (int i = 0; i < P; ++i) {
+        if (!(st->radii[i] > 0)) continue;
+        const float *g = m9 + 9 * (size_t)i;
+        const double mcon[3] = {FA(g[2]), FA(g[3]), FA(g[4])};
+        v3 m = v3ld(in->means3D + 3 * (size_t)i);
+        const float *cov3 = in->cov3D_precomp ? in->cov3D_precomp + 6 * (size_t)i : st->cov3D + 6 * (size_t)i;
+        double mgm[3];
+        cov2d_bwd_mag(m, fx, fy, s->tanfovx, s->tanfovy, cov3, s->viewmatrix, mcon, m_cov3D + 6 * (size_t)i, mgm);
+        float mh[4];
+        xform_point44(m, proj, mh);
+        float m_w = 1.0f / (mh[3] + 0.0000001f);
+        float mul1 = (proj[0] * m.x + proj[4] * m.y + proj[8] * m.z + proj[12]) * m_w * m_w;
+        float mul2 = (proj[1] * m.x + proj[5] * m.y + proj[9] * m.z + proj[13]) * m_w * m_w;
+        const double g2x = FA(g[0]), g2y = FA(g[1]);
+        mgm[0] += FA(proj[0] * m_w - proj[3] * mul1) * g2x + FA(proj[1] * m_w - proj[3] * mul2) * g2y;
+        mgm[1] += FA(proj[4] * m_w - proj[7] * mul1) * g2x + FA(proj[5] * m_w - proj[7] * mul2) * g2y;
+        mgm[2] += FA(proj[8] * m_w - proj[11] * mul1) * g2x + FA(proj[9] * m_w - proj[11] * mul2) * g2y;
+        if (in->shs && m_sh) {
+            const double mcol[3] = {FA(g[6]), FA(g[7]), FA(g[8])};
+            double mdir[3];
+            sh_bwd_mag(s->sh_degree, m, v3ld(s->campos), in->shs + (size_t)i * M * 3, st->clamped + 3 * (size_t)i,
+                       mcol, m_sh + (size_t)i * M * 3, mdir);
+            for (int k = 0; k < 3; ++k) mgm[k] += mdir[k];
+        }
+        for (int k = 0; k < 3; ++k) m_means3D[3 * (size_t)i + k] = mgm[k];
+        if (in->scales)
+            cov3d_bwd_mag(in->scales + 3 * (size_t)i, s->scale_modifier, in->rotations + 4 * (size_t)i,
+                          m_cov3D + 6 * (size_t)i, m_scales + 3 * (size_t)i, m_rotations + 4 * (size_t)i);
+    }
+    return GO_OK;
+}
+#undef FA
+
 /* rasterizer_impl.cu:53-63 */
 void go_mark_visible(int P, const float *means3D, const float *viewmatrix, const float *projmatrix,
                      unsigned char *present) {

@@ -82,6 +82,12 @@ int go_backward_chain(go_state *st, const go_settings *s, const go_inputs *in, c
                       float *dL_dmeans3D, float *dL_dcov3D, float *dL_dsh, float *dL_dscales,
                       float *dL_drotations);
 
+/* The chain in absolute arithmetic (test infrastructure): from per-sum magnitudes m9 [P,9] (the
+ * layout of g9, e.g. go_backward's mag9), the magnitude of the terms every chain output is made of,
+ * in double (|chain(g)| <= chain_mag(m9) whenever |g| <= m9 elementwise). */
+int go_backward_chain_mag(go_state *st, const go_settings *s, const go_inputs *in, const float *m9,
+                          double *m_means3D, double *m_cov3D, double *m_sh, double *m_scales, double *m_rotations);
+
 /* Access an intermediate array by name; returns element count or -1. */
 long go_state_get(go_state *st, const char *name, void **ptr);
 void go_free(go_state *st);

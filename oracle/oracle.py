@@ -80,6 +80,10 @@ def lib():
         L.go_backward_chain.restype = ctypes.c_int
         L.go_backward_chain.argtypes = [ctypes.c_void_p, ctypes.POINTER(_Settings), ctypes.POINTER(_Inputs),
                                         _f32p] + [_f32p] * 5
+        _f64p = ctypes.POINTER(ctypes.c_double)
+        L.go_backward_chain_mag.restype = ctypes.c_int
+        L.go_backward_chain_mag.argtypes = [ctypes.c_void_p, ctypes.POINTER(_Settings), ctypes.POINTER(_Inputs),
+                                            _f32p] + [_f64p] * 5
         L.go_state_get.restype = ctypes.c_long
         L.go_state_get.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_void_p)]
         L.go_free.argtypes = [ctypes.c_void_p]
@@ -304,6 +308,30 @@ def backward_chain(state: State, g9):
         ("dL_dmeans3D", "dL_dcov3D", "dL_dsh", "dL_dscales", "dL_drotations")])
     if rc != 0:
         raise RuntimeError(f"oracle backward_chain failed with code {rc}")
+    return out
+
+
+def backward_chain_mag(state: State, m9):
+    """The chain in absolute arithmetic (gs_oracle.c go_backward_chain_mag): from per-sum magnitudes m9
+    [P,9] (backward()'s "mag9"), the float64 magnitude of the terms each chain output is made of — the
+    scale of a per-element gradient bar that holds for cancelled elements too."""
+    s, inp = state.settings, state.inputs
+    P, M = inp.P, inp.M
+    g = np.ascontiguousarray(np.asarray(m9, np.float32).reshape(P, 9))
+    out = {
+        "dL_dmeans3D": np.zeros((P, 3), np.float64),
+        "dL_dcov3D": np.zeros((P, 6), np.float64),
+        "dL_dsh": np.zeros((P, M, 3), np.float64),
+        "dL_dscales": np.zeros((P, 3), np.float64),
+        "dL_drotations": np.zeros((P, 4), np.float64),
+    }
+    f64 = ctypes.POINTER(ctypes.c_double)
+    cs, ci = s.c(), inp.c()
+    rc = lib().go_backward_chain_mag(state.handle, ctypes.byref(cs), ctypes.byref(ci), _ptr(g), *[
+        _ptr(out[k], f64) if out[k].size else None for k in
+        ("dL_dmeans3D", "dL_dcov3D", "dL_dsh", "dL_dscales", "dL_drotations")])
+    if rc != 0:
+        raise RuntimeError(f"oracle backward_chain_mag failed with code {rc}")
     return out
 
 

@@ -21,7 +21,7 @@ import numpy as np
 import pytest
 import torch
 
-from helpers import GRAD_NAMES, assert_close, camera_settings, compare_forward, compare_grads, golden_inputs, \
+from helpers import GRAD_NAMES, RTOL, assert_close, camera_settings, compare_forward, compare_grads, golden_inputs, \
     run_gpu, run_oracle, scene_arrays, settings_from_golden
 
 pytestmark = pytest.mark.gpu
@@ -280,6 +280,94 @@ def test_c2_full_size_vs_oracle(cuda_device, oracle):
     got = run_gpu(camera_settings(512, 512, device="cuda"), g, **kw)
     compare_forward(got, ref, label="c2")
     compare_grads(got, ref, O=oracle, label="c2")
+
+
+def test_c2_render_raw_parameter_grads_per_element(cuda_device, oracle):
+    """The gradients DGE consumes, at the timed size: render()'s fused raw-parameter path (c2: 1M Gaussians,
+    512x512, view 0 of the bench's 3-view orbit; activations and their derivatives in-kernel, gradients
+    written straight into _xyz.grad ... _rotation.grad) against the oracle's activated-parameter gradients
+    chained through the reference getters (sigmoid / exp / normalize, gaussian_model.py:221-258) by torch
+    autograd on the CPU.
+
+    Per element, no max-floor: |got - ref| <= 1e-4 (|ref| + m), where m is the magnitude of the terms the
+    element is made of — the oracle's per-Gaussian raster-sum magnitudes (mag9: sums of |sub-term| over the
+    contributing pixels) carried through the per-Gaussian chain in absolute arithmetic (every coefficient
+    |c|, every subtraction an addition: oracle.backward_chain_mag, backward.cu:144-396) and through |J| of
+    the getter.  A reordered sum, and the chain's own float rounding, can move an element by a fraction of
+    m, never of its own value, so this is the bar a cancelling element can be held to (a scale gradient
+    along a Gaussian axis seen end-on is such an element: terms of ~1e-5 cancelling to ~1e-11).  Printed: the worst err / (1e-4 (|ref| + m)) and the worst relative error |got-ref|/|ref|
+    over the elements above the floor |ref| >= m / 100 (a sum cancelled by less than 100x); asserted <= 1e-4.
+    The oracle runs on the device's activations (gs_activate_params) so the forward — and with it every
+    blend decision — is bit-identical (asserted), as in the timed-path test."""
+    import ctypes
+
+    from dge_amd import _native as N
+    from dge_amd.cameras import orbit_camera
+    from dge_amd.gaussian_renderer import PipelineParams, _fused_ok, _settings, render
+    from dge_amd.scene import synthetic_scene
+
+    dev = torch.device("cuda")
+    P, W, H, V = 1_000_000, 512, 512, 3
+    sc = synthetic_scene(P, sh_degree=3, seed=0, device=dev).requires_grad_(True)
+    assert _fused_ok(sc, PipelineParams())
+    G = (torch.randn(3, H, W, generator=torch.Generator().manual_seed(1)) * 1e-3).to(dev)
+    pkg = render(orbit_camera(0, V, W, H, device=dev), sc, PipelineParams(), torch.zeros(3, device=dev))
+    pkg["render"].backward(G)
+    torch.cuda.synchronize()
+    got = {n: p.grad.cpu().numpy().astype(np.float64) for n, p in
+           zip(["_xyz", "_features_dc", "_features_rest", "_opacity", "_scaling", "_rotation"], sc.parameters())}
+    got["viewspace"] = pkg["viewspace_points"].grad.cpu().numpy()[:, :2].astype(np.float64)
+    with torch.no_grad():
+        op, scl, rot = (torch.empty(P, k, device=dev) for k in (1, 3, 4))
+        N.check(N.lib().gs_activate_params(P, sc._opacity.data_ptr(), sc._scaling.data_ptr(), sc._rotation.data_ptr(),
+                                           op.data_ptr(), scl.data_ptr(), rot.data_ptr(),
+                                           ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)),
+                "gs_activate_params")
+        torch.cuda.synchronize()
+        op, scl, rot = op.cpu().numpy(), scl.cpu().numpy(), rot.cpu().numpy()
+    s = _settings(orbit_camera(0, V, W, H, device="cpu"), torch.zeros(3), 1.0, 3)
+    nr, color, _, radii, st = oracle.forward(s, means3D=sc._xyz.detach().cpu().numpy(), opacities=op,
+                                             shs=torch.cat([sc._features_dc, sc._features_rest], 1).detach().cpu().numpy(),
+                                             scales=scl, rotations=rot)
+    np.testing.assert_array_equal(pkg["radii"].cpu().numpy(), radii)
+    np.testing.assert_array_equal(pkg["render"].detach().cpu().numpy(), color)  # every blend decision the oracle's
+    ref = oracle.backward(st, G.cpu().numpy())
+    mag9 = ref["mag9"].astype(np.float64)
+    # the chain in absolute arithmetic over the 9 sums' magnitudes (oracle go_backward_chain_mag)
+    cm = oracle.backward_chain_mag(st, ref["mag9"])
+    # the getters (CPU torch autograd) for the reference values, |J| of each getter for the magnitudes
+    cpu = synthetic_scene(P, sh_degree=3, seed=0).requires_grad_(True)
+    torch.autograd.backward([cpu.get_xyz, cpu.get_opacity, cpu.get_features, cpu.get_scaling, cpu.get_rotation],
+                            [torch.from_numpy(ref[k]) for k in
+                             ("dL_dmeans3D", "dL_dopacity", "dL_dsh", "dL_dscales", "dL_drotations")])
+    refs = {n: p.grad.numpy().astype(np.float64) for n, p in
+            zip(["_xyz", "_features_dc", "_features_rest", "_opacity", "_scaling", "_rotation"], cpu.parameters())}
+    refs["viewspace"] = ref["dL_dmeans2D"][:, :2].astype(np.float64)
+    q = cpu._rotation.detach().numpy().astype(np.float64)
+    qn = np.linalg.norm(q, axis=1, keepdims=True)
+    y = q / qn
+    jrot = np.abs((np.eye(4)[None] - y[:, :, None] * y[:, None, :]) / qn[:, :, None])  # d normalize / dq
+    o = op.astype(np.float64)
+    mags = {"_xyz": cm["dL_dmeans3D"], "_features_dc": cm["dL_dsh"][:, :1], "_features_rest": cm["dL_dsh"][:, 1:],
+            "_opacity": mag9[:, 5:6] * o * (1 - o), "_scaling": cm["dL_dscales"] * scl.astype(np.float64),
+            "_rotation": np.einsum("pij,pj->pi", jrot, cm["dL_drotations"]), "viewspace": mag9[:, 0:2]}
+    worst = {}
+    for n, r in refs.items():
+        g, m = got[n], mags[n]
+        assert g.shape == r.shape == m.shape, n
+        err = np.abs(g - r)
+        bound = RTOL * (np.abs(r) + m)
+        ratio = np.where(bound > 0, err / np.maximum(bound, 1e-300), np.where(err > 0, np.inf, 0.0))
+        above = (np.abs(r) >= m / 100) & (r != 0)
+        rel = float((err[above] / np.abs(r[above])).max()) if above.any() else 0.0
+        i = np.unravel_index(np.argmax(ratio), r.shape)
+        worst[n] = (float(ratio.max()), rel, int(above.sum()), int(r.size), int((ratio > 1).sum()),
+                    f"worst at {i}: got {g[i]:.6e} ref {r[i]:.6e} m {m[i]:.3e}")
+    print("[parity c2 raw grads] per tensor (worst err/bound, worst rel err where |ref| >= m/100, "
+          f"elements above the floor, elements, elements beyond the bound, worst element): {worst}")
+    for n, w in worst.items():
+        assert w[0] <= 1.0, f"{n}: worst err / (1e-4 (|ref| + m)) = {w[0]:.3g}, {w[4]} beyond; {w[5]}"
+        assert w[1] <= RTOL, f"{n}: worst relative error {w[1]:.3g} above the floor"
 
 
 def test_c4_hd_forward_vs_oracle(cuda_device, oracle):
@@ -676,3 +764,40 @@ def test_semantic_render_reuses_the_training_forward(cuda_device, localize):
         assert torch.equal(a, b)
     assert bool(got[2][0].abs().sum() > 0)
     assert torch.equal(got[3], ref[3])
+
+
+def test_recolor_never_reuses_a_forward_only_render(cuda_device):
+    """A training-shaped render of frozen parameters with grad mode on (the view-space placeholder keeps the
+    graph, hence the buffers, alive) runs the forward-only kernels; on a grid over 2048 tiles (1024x768:
+    two-level binning) its lists hold Gaussian ids only.  A later override_color render of the same camera
+    must not be served from it (gs_render_recolor reads (Gaussian, slot) pairs): no recolor hit, and the
+    image, depth and radii are bit-identical to the full render's."""
+    from dge_amd import gaussian_renderer as GR
+    from dge_amd.cameras import orbit_camera
+    from dge_amd.gaussian_renderer import PipelineParams, render
+    from dge_amd.scene import synthetic_scene
+
+    dev = torch.device("cuda")
+    P, W, H = 200_000, 1024, 768
+    cam = orbit_camera(0, 1, W, H, device=dev)
+    pipe, bg = PipelineParams(), torch.tensor([0.1, 0.0, 0.2], device=dev)
+    sc = synthetic_scene(P, seed=13, radius=1.5, scale=0.03, device=dev)  # frozen: requires_grad False
+    colors = (torch.arange(P, device=dev) % 3 == 0)[:, None].float().repeat(1, 3)
+    prev = GR._RECOLOR
+    try:
+        outs = []
+        for reuse in (True, False):
+            GR._RECOLOR = reuse
+            GR._LAST_FORWARD.clear()
+            tr = render(cam, sc, pipe, bg)  # grad mode on, nothing trainable: forward_only
+            assert tr["viewspace_points"].requires_grad
+            h0 = GR._RECOLOR_HITS
+            sem = render(cam, sc, pipe, bg, override_color=colors)
+            assert GR._RECOLOR_HITS == h0, "a forward-only render was reused"
+            outs.append({k: sem[k].detach().clone() for k in ("render", "depth_3dgs", "radii")})
+            del tr
+        for k in outs[0]:
+            assert torch.equal(outs[0][k], outs[1][k]), k
+        assert bool(outs[0]["render"].abs().sum() > 0)
+    finally:
+        GR._RECOLOR = prev

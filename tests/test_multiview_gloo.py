@@ -124,12 +124,14 @@ def _free_port():
 
 
 @pytest.mark.slow
+@pytest.mark.parametrize("world,V", [(2, 4), (4, 10)], ids=["2ranks_4views", "4ranks_10views"])
 @pytest.mark.parametrize("mode", ["seed", "l1"])
-def test_sharded_step_equals_single_process(mode):
-    """2 ranks x 2 views == 1 process x 4 views: the summed parameter gradients (sparse-row bucket
-    all-reduce), the view-space gradient sum and the radii max; for DGE's masked l1 (a mean over all
-    views, DGE.py:672) through the B_local / B share of each rank.  found_inf is collective."""
-    P, V = 60, 4
+def test_sharded_step_equals_single_process(mode, world, V):
+    """world ranks x their shard_views shards == 1 process x V views (2 x 2 = 4; 4 ranks over 10 views: the
+    uneven 3/3/2/2 shards): the summed parameter gradients (sparse-row bucket all-reduce), the view-space
+    gradient sum and the radii max; for DGE's masked l1 (a mean over all views, DGE.py:672) through the
+    B_local / B share of each rank.  found_inf is collective (a NaN on rank 1 only)."""
+    P = 60
     pc = _Scene(P, seed=4)
     cams, targets = _setup(P, V)
     if mode == "l1":
@@ -142,7 +144,7 @@ def test_sharded_step_equals_single_process(mode):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, P, V, mode, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, P, V, mode, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=300) for _ in procs]

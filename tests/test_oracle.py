@@ -255,3 +255,29 @@ def test_apply_weights_counts(oracle):
                                   np.zeros((1,), np.int32), iw, scales=sc["scales"], rotations=sc["rotations"])
     _, alpha = _analytic_single(W, H, 2.0, 0.05, 0.8, (1, 1, 1), s)
     assert cnt[0] == int((alpha > 0).sum()) and abs(w[0, 0] - (alpha > 0).sum()) < 1e-3
+
+
+def test_chain_magnitudes_bound_the_chain(oracle):
+    """oracle.backward_chain_mag (the chain in absolute arithmetic, the scale of the per-element gradient bar
+    of test_c2_render_raw_parameter_grads_per_element) bounds the float chain for any sums within the
+    magnitudes: for random g with |g| <= m9, |chain(g)| <= chain_mag(m9) (to the chain's own rounding);
+    it is zero for the Gaussians that are not rendered."""
+    a = scene_arrays(3000, seed=12, radius=4.0, scale=0.05)
+    s = camera_settings(160, 120)
+    nr, _, _, radii, st = oracle.forward(s, means3D=a["means3D"], opacities=a["opacities"], shs=a["shs"],
+                                         scales=a["scales"], rotations=a["rotations"])
+    g = np.random.default_rng(3).standard_normal((3, 120, 160)).astype(np.float32)
+    ref = oracle.backward(st, g)
+    m9 = ref["mag9"]
+    mag = oracle.backward_chain_mag(st, m9)
+    rng = np.random.default_rng(4)
+    for _ in range(4):
+        g9 = (m9 * rng.uniform(-1, 1, m9.shape)).astype(np.float32)
+        ch = oracle.backward_chain(st, g9)
+        for n in ("dL_dmeans3D", "dL_dcov3D", "dL_dsh", "dL_dscales", "dL_drotations"):
+            assert np.all(np.abs(ch[n]) <= mag[n] * (1 + 1e-5) + 1e-30), n
+    dead = radii == 0
+    assert dead.any() and (~dead).any()
+    for n in ("dL_dmeans3D", "dL_dscales", "dL_drotations"):
+        assert not mag[n][dead].any()
+        assert (mag[n][~dead & (m9.max(1) > 0)] > 0).any()
