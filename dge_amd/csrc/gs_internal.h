@@ -193,6 +193,10 @@ inline BinLayout bin_layout(int K, int num_tiles, bool bwd = true) {
     size_t k = (size_t)(K > 0 ? K : 1);
     TileSortPlan plan = tile_sort_plan(num_tiles);
     int maxbits = plan.bits0 > plan.bits1 ? plan.bits0 : plan.bits1;
+    // the two-level binning (grids over 2048 tiles: tile_sort_fused) keeps kXDigits column / row digits in
+    // these tables (its column totals, the row pass's histogram): a 2049..4096-tile grid's two 6-bit passes
+    // would size them for 64
+    if (num_tiles > (1 << kMaxSinglePassBits) && maxbits < kXBits) maxbits = kXBits;
     L.sort_blocks = div_up((long long)k, kSortTile);
     L.key0 = o; o = align_up(o + 4 * k);
     L.key1 = o; o = align_up(o + 4 * k);

@@ -669,13 +669,16 @@ def test_forced_32bit_depth_keys_match_30bit_path(cuda_device, monkeypatch):
         np.testing.assert_array_equal(forced[k], base[k], err_msg=k)
 
 
-@pytest.mark.parametrize("P,W,H", [(3_000, 1920, 1080), (300_000, 1920, 1080), (200_000, 2048, 1040)])
+@pytest.mark.parametrize("P,W,H", [(3_000, 1920, 1080), (300_000, 1920, 1080), (200_000, 2048, 1040),
+                                   (300_000, 1280, 720), (200_000, 1024, 768)])
 def test_two_level_binning_matches_two_pass_sort(cuda_device, monkeypatch, P, W, H):
     """Grids over 2048 tiles (c4: 120 x 68) bin in two levels — the emission writes the instances in
     tile-column order, one row pass follows, ranges come from per-tile counts; DGE_AMD_TILE_SORT=2pass
     runs the emission + two full tile-sort passes + k_ranges instead.  Lists, ranges, the image and
     every gradient are bitwise the same (3k Gaussians: sort blocks spanning many tile columns, whose
-    counts go through the global atomics; 2048 x 1040: the widest grid, 128 columns)."""
+    counts go through the global atomics; 2048 x 1040: the widest grid, 128 columns; 1280 x 720 and
+    1024 x 768: 2049..4096 tiles, whose two-pass plan has 6-bit digits while the two-level tables hold
+    128 — round 5 found those tables sized for 64, and fixed it)."""
     a = scene_arrays(P, seed=6, radius=2.0, scale=0.02)
     g = np.random.default_rng(8).standard_normal((3, H, W)).astype(np.float32) * 1e-3
     s = camera_settings(W, H, device="cuda")
