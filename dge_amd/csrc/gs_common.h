@@ -164,19 +164,29 @@ __device__ __forceinline__ void ewa_cov2d(const Ewa& e, float& a, float& b, floa
 // NVIDIA GPU); the skip / stop decisions of the blend (alpha >= 1/255,
 // T (1 - alpha) >= 1e-4) and therefore n_contrib, the per-pixel lists and the
 // whole T chain depend on the last bit of every G.  So the exp here is a fixed
-// sequence of IEEE single operations — clamp, round-to-integer by the 1.5*2^23
-// shifter, one-constant Cody-Waite reduction, degree-7 Taylor/Horner with
-// fma, exponent built from the shifter's bits — that the CPU oracle
-// (oracle/gs_oracle.c gs_expf) evaluates identically: G, alpha, T and every
-// blend decision are bit-identical between the two.  Accuracy: <= 0.97 ulp
-// against exp over [-10, 1] (99.67% correctly rounded).  NaN -> NaN (the
-// reference then blends the entry at alpha = min(0.99, NaN) = 0.99, and so
-// do we); -inf -> -inf (alpha < 1/255: skipped, as exp(-inf) = 0 is).
+// sequence of IEEE single operations that the CPU oracle (oracle/gs_oracle.c
+// gs_expf) evaluates identically: G, alpha, T and every blend decision are
+// bit-identical between the two.
+//   u = fma(x, log2e, S)        S = 1.5 * 2^23: u = S + rint(x log2e), the product unrounded (round 5:
+//                               one fma where a multiply and an add were: 2 VALU less per group of four)
+//   u = clamp(u, S - 120, S + 120)
+//   n = u - S;  r = fma(n, -ln2, x)            (|r| <= ln2 / 2 for |x log2e| <= 120)
+//   p = degree-7 Taylor/Horner in fma;  result = p * 2^n  (2^n from u's bits)
+// Accuracy: <= 0.86 ulp against exp on [-6, 0] (every float), <= 0.97 ulp on [-10, 1].  NaN -> NaN (r is
+// NaN: the reference then blends the entry at alpha = min(0.99, NaN) = 0.99, and so do we); -inf and
+// x << -83 (u clamped, r huge and negative) give p -> -inf or a negative value (odd degree), alpha < 1/255:
+// skipped, as exp's 0 is.  The clamp keeps 2^n a normal number, so p * 2^n is exact.
+// Why not a 2^(j/64) table + a short polynomial (round-4 verdict): the Horner steps are packed (v_pk_fma_f32:
+// half an instruction per entry each), so a degree-3 polynomial saves 2 VALU per entry while the table costs
+// the index arithmetic (2), an LDS read per entry in a loop already bound by LDS reads of its operands, and a
+// second reduction constant (2 fma: |n| grows 64x) — no fewer instructions, and a longer dependency chain.
+// A degree-6 minimax polynomial (one packed step less) loses the odd-degree sign for x << -83.
 // ---------------------------------------------------------------------
 typedef float f2v __attribute__((ext_vector_type(2)));  // two entries per packed instruction
 
 constexpr float kExpLog2e = 1.44269504f;
-constexpr float kExpShifter = 12582912.0f;  // 1.5 * 2^23: t + S rounds t to an integer (ties to even)
+constexpr float kExpShifter = 12582912.0f;  // 1.5 * 2^23: x log2e + S rounds to S + an integer (ties to even)
+constexpr float kExpLo = kExpShifter - 120.0f, kExpHi = kExpShifter + 120.0f;
 constexpr float kExpLn2 = 0.693147182f;
 constexpr float kExpC7 = 1.98412698e-4f, kExpC6 = 1.38888889e-3f, kExpC5 = 8.33333377e-3f,
                 kExpC4 = 4.16666679e-2f, kExpC3 = 1.66666672e-1f;
@@ -187,9 +197,8 @@ __device__ __forceinline__ float exp_scale(float u) {  // 2^n from the shifter s
 
 __device__ __forceinline__ float gs_exp(float x) {
 #pragma clang fp contract(off)
-    float t = x * kExpLog2e;
-    t = fminf(fmaxf(t, -120.0f), 120.0f);
-    const float u = t + kExpShifter;
+    float u = __builtin_fmaf(x, kExpLog2e, kExpShifter);
+    u = fminf(fmaxf(u, kExpLo), kExpHi);
     const float n = u - kExpShifter;
     const float r = __builtin_fmaf(n, -kExpLn2, x);
     float p = __builtin_fmaf(kExpC7, r, kExpC6);
@@ -208,14 +217,13 @@ __device__ __forceinline__ float gs_exp(float x) {
 typedef float f4v __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ f4v gs_exp4(f4v x) {
 #pragma clang fp contract(off)
-    f4v t = x * kExpLog2e;
-    t.x = fminf(fmaxf(t.x, -120.0f), 120.0f);
-    t.y = fminf(fmaxf(t.y, -120.0f), 120.0f);
-    t.z = fminf(fmaxf(t.z, -120.0f), 120.0f);
-    t.w = fminf(fmaxf(t.w, -120.0f), 120.0f);
-    const f4v u = t + kExpShifter;
-    const f4v n = u - kExpShifter;
     const f4v c = {1.0f, 1.0f, 1.0f, 1.0f};
+    f4v u = __builtin_elementwise_fma(x, kExpLog2e * c, kExpShifter * c);
+    u.x = fminf(fmaxf(u.x, kExpLo), kExpHi);
+    u.y = fminf(fmaxf(u.y, kExpLo), kExpHi);
+    u.z = fminf(fmaxf(u.z, kExpLo), kExpHi);
+    u.w = fminf(fmaxf(u.w, kExpLo), kExpHi);
+    const f4v n = u - kExpShifter;
     const f4v r = __builtin_elementwise_fma(n, -kExpLn2 * c, x);
     f4v p = __builtin_elementwise_fma(kExpC7 * c, r, kExpC6 * c);
     p = __builtin_elementwise_fma(p, r, kExpC5 * c);

@@ -102,14 +102,13 @@ static v3 xform_vec43_T(v3 p, const float *m) {
 /* The blend's exp (forward.cu:345, backward.cu:495, apply_weights.cu): the
  * reference calls CUDA's expf (<= 2 ulp, unavailable here).  The oracle fixes
  * ONE exp as a sequence of IEEE single operations (<= 0.97 ulp vs exp over
- * [-10, 1], 99.67% correctly rounded; NaN -> NaN, -inf -> -inf) that the HIP
+ * [-10, 1], <= 0.86 ulp over every float of [-6, 0]; NaN -> NaN) that the HIP
  * path (dge_amd/csrc/gs_common.h gs_exp) evaluates identically, so every
  * alpha, every skip/stop decision, T and n_contrib can be compared bit for
  * bit.  fmaf is the correctly rounded fused multiply-add (built -mfma). */
 static float gs_expf(float x) {
-    float t = x * 1.44269504f;
-    t = fminf(fmaxf(t, -120.0f), 120.0f);
-    const float u = t + 12582912.0f; /* 1.5 * 2^23: rounds t to an integer, ties to even */
+    float u = fmaf(x, 1.44269504f, 12582912.0f); /* 1.5 * 2^23 + rint(x log2e), the product unrounded */
+    u = fminf(fmaxf(u, 12582912.0f - 120.0f), 12582912.0f + 120.0f);
     const float n = u - 12582912.0f;
     const float r = fmaf(n, -0.693147182f, x);
     float p = fmaf(1.98412698e-4f, r, 1.38888889e-3f);

@@ -68,8 +68,10 @@ def test_blend_exp_bitwise_vs_oracle(cuda_device, oracle):
     print(f"[parity] blend exp: {int((~same).sum())} of {xs.size} differ")
     assert same.all(), xs[~same][:10]
     live = (xs > -10) & (xs < 1)
-    rel = np.abs(got[live].astype(np.float64) - np.exp(xs[live].astype(np.float64))) / np.exp(xs[live].astype(np.float64))
-    assert rel.max() < 1.2e-7  # <= ~1 ulp (the oracle's header quotes 0.97 ulp max)
+    ref64 = np.exp(xs[live].astype(np.float64))
+    ulps = np.abs(got[live].astype(np.float64) - ref64) / np.spacing(ref64.astype(np.float32)).astype(np.float64)
+    print(f"[parity] blend exp: max {ulps.max():.3f} ulp against fp64 exp on [-10, 1]")
+    assert ulps.max() <= 1.5  # (the oracle restatement: <= 0.86 ulp on every float of [-6, 0], 0.97 on [-10, 1])
 
 
 def test_c1_scene_vs_oracle(cuda_device, oracle):
