@@ -386,14 +386,13 @@ int bin_after_preprocess(FwdState& f, hipStream_t stream) {
     GS_HIP(hipMemcpyAsync(f.st->host, counters, 4 * kCounterSlots * kCounterStride, hipMemcpyDeviceToHost, stream));
     GS_HIP(hipEventRecord(f.st->ev, stream));
 
-    // depth order of the Gaussians (stable: ties keep index order)
+    // depth order of the Gaussians (stable: ties keep index order), any key range: MSD buckets + local sorts
     int cur = 0;
     { StageScope sc(ST_DEPTH_SORT, stream);
-    cur = radix_sort_aux(at<uint32_t>(geom, gl.key0), at<uint32_t>(geom, gl.key1), at<uint2>(geom, gl.val0),
-                         at<uint2>(geom, gl.val1), pa.rect, (uint32_t)P, kDepthSortBits, kDepthPassBits,
-                         kDepthSortIPT, at<uint32_t>(geom, gl.sort_hist), at<uint32_t>(geom, gl.sort_totals),
-                         gl.sort_blocks, stream, nullptr, counters + 2); }
-    if (cur < 0) return set_error(GS_ERR_INVALID_ARG, "depth sort: bad digit layout");
+    cur = depth_sort_msd(at<uint32_t>(geom, gl.key0), at<uint32_t>(geom, gl.key1), at<uint2>(geom, gl.val0),
+                         at<uint2>(geom, gl.val1), pa.rect, (uint32_t)P, at<uint32_t>(geom, gl.sort_hist),
+                         at<uint32_t>(geom, gl.sort_totals), gl.sort_blocks, at<uint2>(geom, gl.msd_ranges),
+                         counters + 2, stream); }
     GS_LAUNCHED("depth sort");
 
     EmitArgs& ea = f.ea;
@@ -480,7 +479,10 @@ int read_counts(FwdState& f, Counts& c) {
     }
     c.K = K64;
     c.prefilter_fail = st->host[3] != 0;
-    c.wide = K64 && kmax - ~kmin_not >= (1u << kDepthSortBits);
+    // (the MSD depth sort orders any key range: no 32-bit redo; `wide` stays for the forced fallback test)
+    c.wide = false;
+    (void)kmax;
+    (void)kmin_not;
     staging_release(st, true);
     f.st = nullptr;
     note_count(f.gp.P, f.g.W, f.g.H, c.K, c.wide);
@@ -1420,7 +1422,6 @@ int gs_views_overflow(const gs_views* h, uint8_t* flag, gs_stream_t stream_) {
     if (!h || !flag) return set_error(GS_ERR_INVALID_ARG, "gs_views_overflow: handle and flag are required");
     OverflowArgs a;
     a.n = h->n;
-    a.bits = kDepthSortBits;
     for (int v = 0; v < h->n; ++v) {
         const FwdState& f = h->f[v];
         if (!h->spec[v] || f.gp.P == 0) continue;

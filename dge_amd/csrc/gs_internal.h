@@ -33,14 +33,15 @@ constexpr int kDepthSortIPT = 8;                // depth sort: smaller tiles, >=
 constexpr int kDepthSortTile = 256 * kDepthSortIPT;
 constexpr int kScanIPT = 4;
 constexpr int kScanTile = 256 * kScanIPT;
-// Depth sort: keys are the bits of the view depth (d > 0.2), sorted as key - min(visible keys) on
-// kDepthSortBits bits in three passes — a depth ratio up to 2^(27-23) = 65536 between the farthest
-// and nearest visible Gaussian; wider (or NaN) ranges take the full 32-bit sort (4 x 8 bits).
+// Depth sort: keys are the bits of the view depth (d > 0.2), relative to the visible minimum; since round 5
+// one MSD bucketing pass + a per-bucket local sort (depth_sort_msd) orders any range.  The 3-pass LSD form
+// (kDepthSortBits) is kept as the 32-bit fallback's pass width only (DGE_AMD_DEPTH_KEYS32, a test switch).
 constexpr int kCounterSlots = 16;   // preprocess counters: copies in separate 64-B lines
 constexpr int kCounterStride = 16;  // u32 per slot
 constexpr int kDepthPassBits = 9;
 constexpr int kDepthSortBits = 3 * kDepthPassBits;
 constexpr int kMaxSinglePassBits = 11;          // tile keys up to 2048 tiles sort in one pass
+constexpr int kMsdBits = 11, kMsdBuckets = 1 << kMsdBits, kMsdCulled = kMsdBuckets - 1;  // depth_sort_msd
 constexpr size_t kAlign = 256;
 
 __host__ __device__ inline size_t align_up(size_t x, size_t a = kAlign) { return (x + a - 1) / a * a; }
@@ -92,7 +93,7 @@ struct alignas(64) Splat {
 struct GeomLayout {
     size_t splat, tiles_touched, clamped, touched, live_count, live_list, radii, first_slot;
     // live_count: one u32 per 256-Gaussian block (k_gauss_live); live_list: block-local compacted ids
-    size_t key0, key1, val0, val1, rect, sort_hist, sort_totals, scan_sums, emit_hist, total;
+    size_t key0, key1, val0, val1, rect, sort_hist, sort_totals, scan_sums, emit_hist, msd_ranges, total;
     int sort_blocks, scan_blocks;
 };
 inline GeomLayout geom_layout(int P) {
@@ -118,6 +119,7 @@ inline GeomLayout geom_layout(int P) {
     L.sort_totals = o; o = align_up(o + 4 * (1u << kMaxSinglePassBits));
     L.scan_sums = o; o = align_up(o + 4 * (size_t)(L.scan_blocks + 1));
     L.emit_hist = o; o = align_up(o + 4 * (size_t)kXDigits * L.scan_blocks);  // two-level binning: columns per block
+    L.msd_ranges = o; o = align_up(o + 8 * (size_t)kMsdBuckets);  // depth_sort_msd: each bucket's (start, end)
     L.total = o;
     return L;
 }
@@ -279,6 +281,12 @@ int radix_sort_aux(uint32_t* key0, uint32_t* key1, uint2* pair0, uint2* pair1, c
 // Stable sort of the K emitted instances on their tile id (key0 in slot
 // order); the values are (Gaussian, slot) pairs built on the first pass from
 // gauss_by_slot.  Returns the buffer index (0/1) holding keys and pairs.
+// The depth order (depth bits, index) of the P Gaussians for any key range: one stable 11-bit MSD pass
+// into depth buckets (keys relative to the visible minimum, read with the range from the preprocess counters
+// at bias_not) and a per-bucket local sort; the (rect, Gaussian) values end in pair0 (returns 0).
+int depth_sort_msd(uint32_t* key0, uint32_t* key1, uint2* pair0, uint2* pair1, const uint32_t* rect, uint32_t n,
+                   uint32_t* hist, uint32_t* totals, int nblocks, uint2* bucket_ranges, const uint32_t* bias_not,
+                   hipStream_t s);
 int tile_sort(uint32_t* key0, uint32_t* key1, uint2* pair0, uint2* pair1, const uint32_t* gauss_by_slot, uint32_t n,
               int bits, uint32_t* hist, uint32_t* totals, int nblocks, hipStream_t s, uint2* ranges,
               uint32_t* tile_order, int ntiles,  // tile_order: the forward's dispatch order (single pass only)
@@ -335,7 +343,7 @@ void launch_row_pass(const EmitArgs& a, uint32_t K, uint2* point_pairs, uint32_t
 // sum of its preprocess counter slots > cap) or its visible depth keys span more than `bits` bits — the
 // host's gs_views_check decision, made where a collective can carry it (GradBucket.allreduce_begin)
 struct OverflowArgs {
-    int n = 0, bits = 0;
+    int n = 0;
     const uint32_t* counters[8] = {};  // (GS_MAX_VIEWS)
     uint32_t cap[8] = {};  // 0: an exact view (never overflows)
 };

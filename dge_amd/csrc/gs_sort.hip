@@ -104,6 +104,32 @@ __device__ __forceinline__ uint32_t dev_count(const uint32_t* __restrict__ n_dev
     return k < cap ? k : cap;
 }
 
+// The depth sort's MSD bucketing (depth_sort_msd): the visible keys' range [kmin, kmax] (the preprocess
+// counter slots: [1] max key, [2] ~min key) split into at most kMsdBuckets - 1 buckets of 2^s keys each,
+// bucket = (key - kmin) >> s with s the smallest shift that keeps the top bucket below kMsdCulled; culled
+// keys (0xFFFFFFFF, whose relative key is ~kmin) in bucket kMsdCulled.  Within a bucket only the low s
+// bits of key - kmin differ: k_depth_bucket_sort orders them.
+struct MsdParams {
+    uint32_t kmin, s;
+};
+__device__ __forceinline__ MsdParams msd_params(const uint32_t* __restrict__ bias_not) {
+    uint32_t mn = 0u, mx = 0u;
+#pragma unroll
+    for (int i = 0; i < kCounterSlots; ++i) {
+        mn = max(mn, bias_not[i * kCounterStride]);
+        mx = max(mx, bias_not[i * kCounterStride - 1]);
+    }
+    MsdParams m;
+    m.kmin = ~mn;
+    const uint32_t range = mx >= m.kmin ? mx - m.kmin : 0u;  // (no visible key: kmin = ~0, range 0)
+    const uint32_t q = range / (uint32_t)(kMsdBuckets - 1);
+    m.s = q ? 32u - (uint32_t)__clz(q) : 0u;  // range < (kMsdBuckets - 1) << s
+    return m;
+}
+__device__ __forceinline__ uint32_t msd_digit(uint32_t krel, const MsdParams& m) {
+    return krel == ~m.kmin ? (uint32_t)kMsdCulled : krel >> m.s;
+}
+
 // ---------------------------------------------------------------------
 // radix sort: histogram -> per-digit scan -> stable scatter
 // ---------------------------------------------------------------------
@@ -117,7 +143,8 @@ __host__ __device__ __forceinline__ size_t hist_at(int bm, uint32_t b, uint32_t 
     return bm ? (size_t)b * ndig + d : (size_t)d * nb + b;
 }
 // KT: the key type (u16 for the two-level binning's row pass: its keys are y << 7 | x)
-template <int BITS, int IPT, class KT = uint32_t>
+// DM: the digit is the MSD depth bucket (msd_digit) instead of (key >> shift) & mask
+template <int BITS, int IPT, class KT = uint32_t, bool DM = false>
 __global__ __launch_bounds__(256) void k_radix_hist(const KT* __restrict__ keys, uint32_t n, int shift,
                                                     uint32_t* __restrict__ hist, int nb, int bm,
                                                     const uint32_t* __restrict__ bias_not,
@@ -131,6 +158,8 @@ __global__ __launch_bounds__(256) void k_radix_hist(const KT* __restrict__ keys,
     for (int i = tid; i < NDIG; i += 256) cnt[i] = 0;
     __syncthreads();
     const uint32_t bias = key_bias(bias_not);
+    MsdParams msd{0u, 0u};
+    if constexpr (DM) msd = msd_params(bias_not);
     // counts do not depend on which thread sees which key: each thread takes VEC consecutive keys per 16-B
     // load (a wave reads 1 KB per instruction instead of 64 scattered 2-4 B words)
     constexpr int VEC = 16 / (int)sizeof(KT);
@@ -154,7 +183,10 @@ __global__ __launch_bounds__(256) void k_radix_hist(const KT* __restrict__ keys,
         const KT* k = reinterpret_cast<const KT*>(&raw[j]);
 #pragma unroll
         for (int u = 0; u < VEC; ++u)
-            if (e0 + u < n) atomicAdd(&cnt[(((uint32_t)k[u] - bias) >> shift) & (NDIG - 1)], 1u);
+            if (e0 + u < n) {
+                const uint32_t kr = (uint32_t)k[u] - bias;
+                atomicAdd(&cnt[DM ? msd_digit(kr, msd) : (kr >> shift) & (NDIG - 1)], 1u);
+            }
     }
     __syncthreads();
     for (int d = tid; d < NDIG; d += 256) hist[hist_at(bm, blockIdx.x, d, nb, NDIG)] = cnt[d];
@@ -306,7 +338,7 @@ enum ValMode { kValU32 = 0, kValPairFirst = 1, kValPair = 2 };
 // WK: the sorted keys are written (every pass but the last tile-sort pass).  Without them the block
 // stages only the digit (u16), and the per-wave digit counters are u16 throughout (<= 256*IPT), so
 // the single-pass tile sort fits three workgroups per CU (52 KB of LDS instead of 68).
-template <int BITS, int IPT, bool IDV, int VM, bool WK = true, bool TC = false, class KT = uint32_t>
+template <int BITS, int IPT, bool IDV, int VM, bool WK = true, bool TC = false, class KT = uint32_t, bool DM = false>
 __global__ __launch_bounds__(256) void k_radix_scatter(const KT* __restrict__ keys_in,
                                                        const void* __restrict__ vals_in_,
                                                        uint32_t* __restrict__ keys_out, void* __restrict__ vals_out_,
@@ -387,6 +419,9 @@ __global__ __launch_bounds__(256) void k_radix_scatter(const KT* __restrict__ ke
     if (blockIdx.x * (uint32_t)(256 * IPT) >= n) return;
     const uint32_t base = blockIdx.x * (uint32_t)(256 * IPT) + w * 64u * IPT;
     const uint32_t bias = key_bias(bias_not);
+    MsdParams msd{0u, 0u};
+    if constexpr (DM) msd = msd_params(bias_not);
+    auto digit = [&](uint32_t k) { return DM ? msd_digit(k, msd) : (k >> shift) & (NDIG - 1); };
     uint32_t key[IPT], loc[IPT];
     V val[IPT];
 #pragma unroll
@@ -395,7 +430,7 @@ __global__ __launch_bounds__(256) void k_radix_scatter(const KT* __restrict__ ke
         const bool valid = idx < n;
         key[it] = valid ? (uint32_t)keys_in[idx] - bias : 0u;
         if constexpr (VM == kValU32) val[it] = IDV ? idx : (valid ? vals_in[idx] : 0u);
-        else if constexpr (VM == kValPairFirst) val[it] = make_uint2(valid ? gauss_by_slot[idx] : 0u, idx);
+        else if constexpr (VM == kValPairFirst) val[it] = make_uint2(0u, idx);  // (aux re-read at the store)
         else val[it] = valid ? pairs_in[idx] : make_uint2(0u, 0u);
     }
 #pragma unroll
@@ -404,7 +439,7 @@ __global__ __launch_bounds__(256) void k_radix_scatter(const KT* __restrict__ ke
         const bool valid = idx < n;
         const uint64_t vm = __ballot(valid);
         if (vm == 0) break;
-        const uint32_t d = (key[it] >> shift) & (NDIG - 1);
+        const uint32_t d = digit(key[it]);
         const uint64_t peers = match_digit<BITS>(d, vm);
         const uint32_t rank = (uint32_t)__popcll(peers & lanemask_lt());
         const uint32_t old = cnt[w][d];
@@ -444,18 +479,23 @@ __global__ __launch_bounds__(256) void k_radix_scatter(const KT* __restrict__ ke
     // stage the block in digit-major order, then store it with consecutive lanes on consecutive
     // positions of each digit run (coalesced) instead of one scattered element per lane
     using SK = typename std::conditional<WK, uint32_t, uint16_t>::type;  // staged key, or its digit
+    // kValPairFirst stages the element's position in the block (u16) instead of its 8-B (aux, index) pair and
+    // gathers aux again at the store (from L1/L2: the block's slice was just read): a quarter of the staging
+    // LDS, so more workgroups per CU (c2's single-pass tile sort: 52 -> 28 KB, 3 -> 5 per CU)
+    using SV = typename std::conditional<VM == kValPairFirst, uint16_t, V>::type;
     __shared__ SK s_key[256 * IPT];
-    __shared__ V s_val[256 * IPT];
+    __shared__ SV s_val[256 * IPT];
     const uint32_t b0 = blockIdx.x * (uint32_t)(256 * IPT);
     const uint32_t x_first = TC ? (uint32_t)keys_in[b0] & (kXDigits - 1) : 0u;  // the block's first column
 #pragma unroll
     for (int it = 0; it < IPT; ++it) {
         const uint32_t idx = base + it * 64 + lane;
         if (idx < n) {
-            const uint32_t d = (key[it] >> shift) & (NDIG - 1);
+            const uint32_t d = digit(key[it]);
             const uint32_t lp = cnt[w][d] + loc[it];
             s_key[lp] = WK ? (SK)key[it] : (SK)d;
-            s_val[lp] = val[it];
+            if constexpr (VM == kValPairFirst) s_val[lp] = (uint16_t)(idx - b0);
+            else s_val[lp] = val[it];
             if (TC) {
                 const uint32_t x = key[it] & (kXDigits - 1), y = key[it] >> kXBits, c = x - x_first;
                 if (c < (uint32_t)kTcCols) atomicAdd(&s_tc[c * kXDigits + y], 1u);
@@ -473,9 +513,14 @@ __global__ __launch_bounds__(256) void k_radix_scatter(const KT* __restrict__ ke
     const int nvalid = n - b0 < (uint32_t)(256 * IPT) ? (int)(n - b0) : 256 * IPT;
     for (int i = tid; i < nvalid; i += 256) {
         const uint32_t k = s_key[i];
-        const uint32_t pos = dbase[WK ? (k >> shift) & (NDIG - 1) : k] + (uint32_t)i;
+        const uint32_t pos = dbase[WK ? digit(k) : k] + (uint32_t)i;
         if (WK) keys_out[pos] = k;
-        vals_out[pos] = s_val[i];
+        if constexpr (VM == kValPairFirst) {
+            const uint32_t e = b0 + (uint32_t)s_val[i];
+            vals_out[pos] = make_uint2(gauss_by_slot[e], e);
+        } else {
+            vals_out[pos] = s_val[i];
+        }
     }
 }
 
@@ -565,6 +610,207 @@ int tile_sort(uint32_t* key0, uint32_t* key1, uint2* pair0, uint2* pair1, const 
               uint32_t* tile_order, int ntiles, const uint32_t* n_dev) {
     return radix_sort_aux(key0, key1, pair0, pair1, gauss_by_slot, n, bits, kMaxSinglePassBits, kSortIPT, hist, totals,
                           nblocks, s, ranges, nullptr, tile_order, ntiles, n_dev);
+}
+
+// ---------------------------------------------------------------------
+// depth sort: MSD bucketing + per-bucket local sort (round 5)
+// ---------------------------------------------------------------------
+// The reference orders the instances by (tile, depth bits, Gaussian index) with one 64-bit cub sort
+// (rasterizer_impl.cu:253-261); the emission here needs the Gaussians in (depth bits, index) order.  One
+// stable 11-bit MSD pass (histogram, digit scan, scatter: the LSD kernels with msd_digit) puts every visible
+// Gaussian into its depth bucket in index order; k_depth_bucket_sort then orders each bucket on the key
+// bits below the bucket (the s bits of msd_params) in LDS, stable, so the result is the (key, index) order of
+// a full stable sort for any key range: 4 launches where the 3-pass LSD sort took 9 (and a 32-bit fallback for
+// ranges over 27 bits).  Buckets over kBucketCap keys (a dense depth band, measured max 1.6k at c2 and 3.6k
+// at c4) take an in-kernel global-memory LSD over the bucket, one workgroup, correct at any size.
+constexpr int kBucketIPT = 16, kBucketCap = 256 * kBucketIPT;
+constexpr int kLocalBits = 7, kLocalDig = 1 << kLocalBits;
+
+// Stable digit-major positions of one chunk (<= kBucketCap elements) held in registers: element j of the chunk
+// is (wave w, it, lane) with j = w * 64 * ipt + it * 64 + lane, so the waves own consecutive stretches (the
+// per-wave counters then rank in input order).  pos[it] <- the element's position in the chunk's digit-major
+// order; s_start[d] / s_tot[d] <- digit d's run in the chunk.
+template <int IPT>
+__device__ __forceinline__ void chunk_rank(const uint32_t (&dig)[IPT], int ipt, uint32_t n, uint32_t (&pos)[IPT],
+                                           uint16_t (*cnt)[kLocalDig], uint32_t* s_start, uint32_t* s_tot,
+                                           uint32_t* lds4) {
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    for (int i = tid; i < 4 * kLocalDig; i += 256) (&cnt[0][0])[i] = 0;
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < IPT; ++it) {
+        const uint32_t j = (uint32_t)(w * 64 * ipt + it * 64 + lane);
+        const bool valid = it < ipt && j < n;
+        const uint64_t vm = __ballot(valid);
+        if (vm != 0) {  // (wave-uniform)
+            const uint32_t d = valid ? dig[it] : 0u;
+            const uint64_t peers = match_digit<kLocalBits>(d, vm);
+            const uint32_t rank = (uint32_t)__popcll(peers & lanemask_lt());
+            const uint32_t old = cnt[w][d];
+            pos[it] = old + rank;
+            if (valid && rank == 0) cnt[w][d] = (uint16_t)(old + (uint32_t)__popcll(peers));
+        }
+    }
+    __syncthreads();
+    uint32_t c0 = 0, c1 = 0, c2 = 0, tot = 0;
+    if (tid < kLocalDig) {
+        c0 = cnt[0][tid];
+        c1 = cnt[1][tid];
+        c2 = cnt[2][tid];
+        tot = c0 + c1 + c2 + cnt[3][tid];
+    }
+    uint32_t all;
+    const uint32_t run = block_exclusive_scan(tot, lds4, all);
+    if (tid < kLocalDig) {
+        cnt[0][tid] = (uint16_t)run;
+        cnt[1][tid] = (uint16_t)(run + c0);
+        cnt[2][tid] = (uint16_t)(run + c0 + c1);
+        cnt[3][tid] = (uint16_t)(run + c0 + c1 + c2);
+        s_start[tid] = run;
+        s_tot[tid] = tot;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < IPT; ++it) {
+        const uint32_t j = (uint32_t)(w * 64 * ipt + it * 64 + lane);
+        if (it < ipt && j < n) pos[it] += cnt[w][dig[it]];
+    }
+}
+
+// One workgroup per MSD bucket: keys_b / vals_b (the MSD pass's output: keys relative to kmin, (rect,
+// Gaussian) values) -> vals_a in (key, index) order.  The culled bucket and buckets of one key value are
+// copied (already in index order).
+__global__ __launch_bounds__(256) void k_depth_bucket_sort(uint32_t* __restrict__ keys_b, uint2* __restrict__ vals_b,
+                                                           uint32_t* __restrict__ keys_a, uint2* __restrict__ vals_a,
+                                                           const uint2* __restrict__ ranges,
+                                                           const uint32_t* __restrict__ bias_not) {
+    __shared__ uint32_t s_key[kBucketCap];
+    __shared__ uint2 s_val[kBucketCap];
+    __shared__ uint16_t cnt[4][kLocalDig];
+    __shared__ uint32_t s_start[kLocalDig], s_tot[kLocalDig], s_base[kLocalDig];
+    __shared__ uint32_t lds4[4];
+    const uint2 r = ranges[blockIdx.x];
+    const uint32_t n = r.y - r.x;
+    if (n == 0) return;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const MsdParams m = msd_params(bias_not);
+    const int passes = ((int)m.s + kLocalBits - 1) / kLocalBits;
+    if (blockIdx.x == (uint32_t)kMsdCulled || passes == 0 || n == 1) {
+        for (uint32_t i = tid; i < n; i += 256) vals_a[r.x + i] = vals_b[r.x + i];
+        return;
+    }
+    uint32_t key[kBucketIPT], dig[kBucketIPT], pos[kBucketIPT];
+    uint2 val[kBucketIPT];
+    if (n <= (uint32_t)kBucketCap) {  // in LDS: every pass ranks the bucket held in registers
+        const int ipt = (int)div_up_u(n, 256u);
+#pragma unroll
+        for (int it = 0; it < kBucketIPT; ++it) {
+            const uint32_t j = (uint32_t)(w * 64 * ipt + it * 64 + lane);
+            if (it < ipt && j < n) {
+                key[it] = keys_b[r.x + j];
+                val[it] = vals_b[r.x + j];
+            }
+        }
+        for (int p = 0; p < passes; ++p) {
+#pragma unroll
+            for (int it = 0; it < kBucketIPT; ++it) dig[it] = (key[it] >> (p * kLocalBits)) & (kLocalDig - 1);
+            chunk_rank<kBucketIPT>(dig, ipt, n, pos, cnt, s_start, s_tot, lds4);
+#pragma unroll
+            for (int it = 0; it < kBucketIPT; ++it) {
+                const uint32_t j = (uint32_t)(w * 64 * ipt + it * 64 + lane);
+                if (it < ipt && j < n) {
+                    s_key[pos[it]] = key[it];
+                    s_val[pos[it]] = val[it];
+                }
+            }
+            __syncthreads();
+            if (p + 1 == passes) break;
+#pragma unroll
+            for (int it = 0; it < kBucketIPT; ++it) {
+                const uint32_t j = (uint32_t)(w * 64 * ipt + it * 64 + lane);
+                if (it < ipt && j < n) {
+                    key[it] = s_key[j];
+                    val[it] = s_val[j];
+                }
+            }
+            __syncthreads();  // (the next pass's counters and staging)
+        }
+        for (uint32_t i = tid; i < n; i += 256) vals_a[r.x + i] = s_val[i];
+        return;
+    }
+    // a bucket over kBucketCap keys: LSD passes over it in global memory, chunk after chunk in input order
+    // (stable), ping-pong between the B and A copies of its range
+    uint32_t* ks = keys_b;
+    uint32_t* kd = keys_a;
+    uint2* vs = vals_b;
+    uint2* vd = vals_a;
+    for (int p = 0; p < passes; ++p) {
+        const int shift = p * kLocalBits;
+        if (tid < kLocalDig) s_base[tid] = 0u;
+        __syncthreads();
+        for (uint32_t i = tid; i < n; i += 256) atomicAdd(&s_base[(ks[r.x + i] >> shift) & (kLocalDig - 1)], 1u);
+        __syncthreads();
+        {
+            const uint32_t c = tid < kLocalDig ? s_base[tid] : 0u;
+            uint32_t all;
+            const uint32_t run = block_exclusive_scan(c, lds4, all);
+            if (tid < kLocalDig) s_base[tid] = run;
+        }
+        __syncthreads();
+        for (uint32_t c0 = 0; c0 < n; c0 += (uint32_t)kBucketCap) {
+            const uint32_t cn = n - c0 < (uint32_t)kBucketCap ? n - c0 : (uint32_t)kBucketCap;
+            const int ipt = (int)div_up_u(cn, 256u);
+#pragma unroll
+            for (int it = 0; it < kBucketIPT; ++it) {
+                const uint32_t j = (uint32_t)(w * 64 * ipt + it * 64 + lane);
+                if (it < ipt && j < cn) {
+                    key[it] = ks[r.x + c0 + j];
+                    val[it] = vs[r.x + c0 + j];
+                }
+                dig[it] = (key[it] >> shift) & (kLocalDig - 1);
+            }
+            chunk_rank<kBucketIPT>(dig, ipt, cn, pos, cnt, s_start, s_tot, lds4);
+#pragma unroll
+            for (int it = 0; it < kBucketIPT; ++it) {
+                const uint32_t j = (uint32_t)(w * 64 * ipt + it * 64 + lane);
+                if (it < ipt && j < cn) {
+                    const uint32_t g = s_base[dig[it]] + pos[it] - s_start[dig[it]];
+                    kd[r.x + g] = key[it];
+                    vd[r.x + g] = val[it];
+                }
+            }
+            __syncthreads();
+            if (tid < kLocalDig) s_base[tid] += s_tot[tid];
+            __syncthreads();
+        }
+        uint32_t* kt = ks; ks = kd; kd = kt;
+        uint2* vt = vs; vs = vd; vd = vt;
+    }
+    if (vs != vals_a)  // (an even number of passes ends in the B copy)
+        for (uint32_t i = tid; i < n; i += 256) vals_a[r.x + i] = vals_b[r.x + i];
+}
+
+int depth_sort_msd(uint32_t* key0, uint32_t* key1, uint2* pair0, uint2* pair1, const uint32_t* rect, uint32_t n,
+                   uint32_t* hist, uint32_t* totals, int nblocks, uint2* bucket_ranges, const uint32_t* bias_not,
+                   hipStream_t s) {
+    if (n == 0) return 0;
+    constexpr int IPT = kDepthSortIPT, NDIG = kMsdBuckets;
+    const int bm = nblocks <= kScanBmRows ? 1 : 0;
+    hipLaunchKernelGGL((k_radix_hist<kMsdBits, IPT, uint32_t, true>), dim3(nblocks), dim3(256), 0, s, key0, n, 0, hist,
+                       nblocks, bm, bias_not, (const uint32_t*)nullptr);
+    if (bm)
+        hipLaunchKernelGGL(k_radix_digit_scan, dim3(div_up(NDIG, kScanDigits)), dim3(1024), 0, s, hist, nblocks, NDIG,
+                           totals, (const uint32_t*)nullptr, n, 256 * IPT);
+    else
+        hipLaunchKernelGGL(k_radix_digit_scan_dm, dim3(NDIG), dim3(256), 0, s, hist, nblocks, totals,
+                           (const uint32_t*)nullptr, n, 256 * IPT);
+    // (block 0 writes every bucket's range, as a single-pass tile sort writes the tile ranges)
+    hipLaunchKernelGGL((k_radix_scatter<kMsdBits, IPT, true, kValPairFirst, true, false, uint32_t, true>), dim3(nblocks),
+                       dim3(256), 0, s, key0, nullptr, key1, pair1, rect, n, 0, hist, totals, nblocks, bm,
+                       RangeOut{bucket_ranges, nullptr, NDIG}, bias_not, (const uint32_t*)nullptr);
+    hipLaunchKernelGGL(k_depth_bucket_sort, dim3(NDIG), dim3(256), 0, s, key1, pair1, key0, pair0, bucket_ranges,
+                       bias_not);
+    return 0;  // (the (rect, Gaussian) values in depth order are in pair0)
 }
 
 // ---------------------------------------------------------------------
@@ -1015,7 +1261,9 @@ __global__ __launch_bounds__(64) void k_views_overflow(OverflowArgs a, uint8_t* 
             kmax = max(kmax, c[i * kCounterStride + 1]);
             kmin_not = max(kmin_not, c[i * kCounterStride + 2]);
         }
-        bad = k > a.cap[v] || (k && kmax - ~kmin_not >= (1u << a.bits));
+        bad = k > a.cap[v];  // (any depth-key range sorts: depth_sort_msd)
+        (void)kmax;
+        (void)kmin_not;
     }
     const uint64_t any = __ballot(bad);
     if (v == 0) flag[0] = any ? 1 : 0;

@@ -627,10 +627,9 @@ def _axis_camera(W, H, fov_deg=60.0, device="cpu"):
                          proj, (0.0, 0.0, 0.0), 3, device=device)
 
 
-def _far_depth_scene():
+def _far_depth_scene(P=4000, zlo=3.0, zhi=6.0):
     rng = np.random.default_rng(11)
-    P = 4000
-    xyz = np.stack([rng.uniform(-1, 1, P), rng.uniform(-1, 1, P), rng.uniform(3, 6, P)], 1).astype(np.float32)
+    xyz = np.stack([rng.uniform(-1, 1, P), rng.uniform(-1, 1, P), rng.uniform(zlo, zhi, P)], 1).astype(np.float32)
     # Gaussians beyond the 30-bit depth key (>= 2^125 ~ 4.25e37), on the axis (centre tile), in reverse
     # index order of depth, plus a tie: the order must still be the reference's (depth bits, index)
     far = np.array([[0, 0, 9e37], [0, 0, 6e37], [0, 0, 6e37], [0, 0, 5e37], [0.01, 0, 7e37]], np.float32)
@@ -643,10 +642,13 @@ def _far_depth_scene():
                 scales=rng.uniform(0.01, 0.05, (n, 3)).astype(np.float32), rotations=rot)
 
 
-def test_depth_beyond_30bit_key_range_keeps_reference_order(cuda_device, oracle):
-    """Depth keys are the view depth's float bits offset into 30 bits (three 10-bit radix passes); a
-    depth >= 2^125 is flagged by preprocess and the depth order is redone on the full 32-bit keys."""
-    kw = _far_depth_scene()
+@pytest.mark.parametrize("P,zlo,zhi", [(4000, 3.0, 6.0), (24000, 3.0, 3.5)], ids=["spread", "dense_band"])
+def test_depth_beyond_30bit_key_range_keeps_reference_order(cuda_device, oracle, P, zlo, zhi):
+    """Depth keys spanning ~30 bits (Gaussians beyond 5e37 beside depths 3..6): the MSD depth buckets are 2^20
+    keys wide, so the near Gaussians share a handful of buckets — 'spread': ~1000 per bucket (the in-LDS local
+    sort), 'dense_band' (24k Gaussians at depths 3..3.5): ~12k per bucket (the in-kernel global-memory LSD of
+    an oversized bucket).  The lists, ranges and every output equal the oracle's (the reference's order)."""
+    kw = _far_depth_scene(P, zlo, zhi)
     g = np.random.default_rng(3).standard_normal((3, 96, 96)).astype(np.float32) * 1e-3
     ref = run_oracle(oracle, _axis_camera(96, 96), g, **kw)
     got = run_gpu(_axis_camera(96, 96, device="cuda"), g, **kw)
@@ -660,7 +662,8 @@ def test_depth_beyond_30bit_key_range_keeps_reference_order(cuda_device, oracle)
 
 
 def test_forced_32bit_depth_keys_match_30bit_path(cuda_device, monkeypatch):
-    """The 32-bit fallback (DGE_AMD_DEPTH_KEYS32=1) and the 30-bit path give the same lists and images."""
+    """The 32-bit LSD fallback (DGE_AMD_DEPTH_KEYS32=1: four 8-bit passes over the full keys) and the MSD depth
+    sort give the same lists and images."""
     a = scene_arrays(100_000, seed=4, radius=2.0, scale=0.02)
     kw = _sh_kw(a)
     s = camera_settings(256, 256, device="cuda")
