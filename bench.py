@@ -201,7 +201,8 @@ def main():
     seeds = [(torch.randn(3, H, W, generator=gen) * 1e-3).to(dev) for _ in range(V)]
     bg = torch.zeros(3, device=dev)
     pipe = PipelineParams()
-    bucket = GradBucket(scene.parameters())
+    # (DGE_AMD_BUCKET_ROWS=0: the flat concatenated bucket instead of the row-major one — an A/B switch)
+    bucket = GradBucket(scene.parameters(), rows=None if os.environ.get("DGE_AMD_BUCKET_ROWS", "1") != "0" else False)
 
     min_world = 1 if rehearse else 2
 
@@ -536,11 +537,15 @@ def side_legs(args, scene, cams, seeds, bg, pipe, bucket, step, dev):
     prev = os.environ.get("DGE_AMD_FUSED")
     os.environ["DGE_AMD_FUSED"] = "0"
 
+    # (autograd's own accumulation here, not the fused in-kernel one: a flat bucket of contiguous .grad
+    # tensors — into the row-major bucket's strided .grad views AccumulateGrad warns about the layout)
+    flat_bucket = GradBucket(scene.parameters(), rows=False)
+
     def unchanged():
         # DGE renders its views one after another on the caller's stream (DGE.py:179-222).  (On the views'
         # streams each view's torch getter nodes would run on its own stream while feeding the one
         # AccumulateGrad node per parameter: autograd's stream-mismatch warning, round 3's stderr.)
-        run_views(args, cams, scene, pipe, bg, seeds, bucket, streams=1)
+        run_views(args, cams, scene, pipe, bg, seeds, flat_bucket, streams=1)
 
     try:
         for _ in range(3):
@@ -553,6 +558,8 @@ def side_legs(args, scene, cams, seeds, bg, pipe, bucket, step, dev):
             os.environ["DGE_AMD_FUSED"] = prev
     legs["dge_unchanged_render"] = {"value": round(steps * V / dt, 3), "unit": "renders/s",
                                     "path": "torch getters + cat + _RasterizeGaussians (fused path off), one stream"}
+    del flat_bucket
+    bucket.attach()
 
     hl = synthetic_scene(args.points, sh_degree=args.sh_degree, seed=0, device=dev, opacity_mean=-2.0,
                          opacity_std=1.0).requires_grad_(True)

@@ -439,6 +439,27 @@ def rasterize_gaussians_fused(background, xyz, f_dc, f_rest, colors, raw_opacity
         visible=visible))
 
 
+def row_pitch_ok(t) -> bool:
+    """t's rows (dim 0) may sit at any pitch, its trailing dims packed: a parameter-shaped gradient the kernels
+    can write in place (a contiguous tensor, or a column block of a row-major gradient bucket)."""
+    if t.dim() == 0 or t.stride(-1) != 1:
+        return False
+    expect = 1
+    for d in range(t.dim() - 1, 0, -1):
+        if t.size(d) > 1 and t.stride(d) != expect:
+            return False
+        expect *= t.size(d)
+    return t.size(0) <= 1 or t.stride(0) >= expect
+
+
+def set_grad_pitches(o, d_xyz, d_op, d_sc, d_rot, d_dc=None, d_rest=None):
+    """gs_grads row pitches (ABI 17) and SH strides from the output tensors' row strides."""
+    o.pitch_means3D, o.pitch_opacity = int(d_xyz.stride(0)), int(d_op.stride(0))
+    o.pitch_scales, o.pitch_rotations = int(d_sc.stride(0)), int(d_rot.stride(0))
+    o.dsh_dc_stride = int(d_dc.stride(0)) if d_dc is not None else 3
+    o.dsh_rest_stride = int(d_rest.stride(0)) if d_rest is not None else 0
+
+
 def rasterize_gaussians_fused_backward(background, xyz, f_dc, f_rest, colors, raw_opacity, raw_scaling, raw_rotation,
                                        radii, scale_modifier, viewmatrix, projmatrix, tan_fovx, tan_fovy,
                                        dL_dout_color, degree, campos, geomBuffer, R, binningBuffer, imageBuffer,
@@ -502,9 +523,8 @@ def rasterize_gaussians_fused_backward(background, xyz, f_dc, f_rest, colors, ra
         o.dL_dmeans3D, o.dL_dcov3D = _ptr(d_xyz), None
         o.dL_dsh_dc = _ptr(d_dc) if have_sh else None
         o.dL_dsh_rest = _ptr(d_rest) if d_rest is not None else None
-        o.dsh_dc_stride = 3
-        o.dsh_rest_stride = 3 * (d_rest.size(1) if d_rest is not None else 0)
         o.dL_dscales, o.dL_drotations = _ptr(d_sc), _ptr(d_rot)
+        set_grad_pitches(o, d_xyz, d_op, d_sc, d_rot, d_dc if have_sh else None, d_rest)
         o.accumulate = acc_bits
         if writes_after is not None:
             o.writes_after = writes_after.cuda_event

@@ -15,7 +15,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("DGE_AMD_LIB") or os.path.join(_HERE, "lib", "libgs_raster.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "gs_raster.h")
 
-ABI_VERSION = 16  # GS_RASTER_ABI_VERSION of include/gs_raster.h this binding is written against
+ABI_VERSION = 17  # GS_RASTER_ABI_VERSION of include/gs_raster.h this binding is written against
 
 GS_OK = 0
 GS_ERR_INVALID_ARG = 1
@@ -100,6 +100,10 @@ class GsGrads(ctypes.Structure):
         ("dL_dconic", _fp),
         ("writes_after", ctypes.c_void_p),
         ("zeroed", ctypes.c_uint),
+        ("pitch_means3D", ctypes.c_int),
+        ("pitch_opacity", ctypes.c_int),
+        ("pitch_scales", ctypes.c_int),
+        ("pitch_rotations", ctypes.c_int),
     ]
 
 
@@ -114,6 +118,8 @@ class AdamSegment(ctypes.Structure):
         ("n", ctypes.c_longlong),
         ("step_size", ctypes.c_float),
         ("bias_correction2_sqrt", ctypes.c_float),
+        ("grad_width", ctypes.c_int),
+        ("grad_pitch", ctypes.c_int),
     ]
 
 

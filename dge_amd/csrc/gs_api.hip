@@ -714,6 +714,10 @@ GaussBwdArgs gauss_args(const gs_settings* s, const gs_params* gp, int R, const 
     ga.dL_dmeans2D = o->dL_dmeans2D; ga.dL_dcolors = o->dL_dcolors; ga.dL_dopacity = o->dL_dopacity;
     ga.dL_dmeans3D = o->dL_dmeans3D; ga.dL_dcov3D = o->dL_dcov3D;
     ga.dL_dscales = o->dL_dscales; ga.dL_drot = o->dL_drotations;
+    ga.pm3 = o->pitch_means3D > 0 ? o->pitch_means3D : 3;
+    ga.pop = o->pitch_opacity > 0 ? o->pitch_opacity : 1;
+    ga.psc = o->pitch_scales > 0 ? o->pitch_scales : 3;
+    ga.prot = o->pitch_rotations > 0 ? o->pitch_rotations : 4;
     ga.acc = o->accumulate;
     ga.zeroed = o->zeroed & o->accumulate;
     ga.slot_cap = slot_cap;
@@ -1029,6 +1033,7 @@ int gs_rasterize_backward(const gs_settings* s, int P, int M, int R, const float
     o.dL_dconic = nullptr;
     o.writes_after = nullptr;
     o.zeroed = 0;
+    o.pitch_means3D = o.pitch_opacity = o.pitch_scales = o.pitch_rotations = 0;
     gs_params g2 = g;
     g2.M = M;  // dL_dsh is [P,M,3] even when shs is absent (then all zero)
     return gs_rasterize_backward_ex(s, &g2, R, radii, geom, binning, img, dL_dpix, &o, stream);
@@ -1057,6 +1062,11 @@ static int validate_backward(const gs_settings* s, const gs_params* gp, int R, c
         (gp->M > 1 && o->dL_dsh_dc && !o->dL_dsh_rest))
         return set_error(GS_ERR_INVALID_ARG, "gradient outputs are required");
     if (R > 0 && !binning) return set_error(GS_ERR_INVALID_ARG, "binning buffer is required when num_rendered > 0");
+    if (o->pitch_means3D < 0 || o->pitch_opacity < 0 || o->pitch_scales < 0 || o->pitch_rotations < 0 ||
+        (o->pitch_means3D > 0 && o->pitch_means3D < 3) || (o->pitch_scales > 0 && o->pitch_scales < 3) ||
+        (o->pitch_rotations > 0 && (o->pitch_rotations < 4 || o->pitch_rotations % 4)) ||
+        (reinterpret_cast<uintptr_t>(o->dL_drotations) & 15))
+        return set_error(GS_ERR_INVALID_ARG, "gradient row pitches: >= the row width, dL_drotations rows 16-B aligned");
     return GS_OK;
 }
 
@@ -1314,7 +1324,10 @@ bool views_mergeable(const gs_views* h, const gs_grads* const* o) {
         if (g->dL_dopacity != g0->dL_dopacity || g->dL_dmeans3D != g0->dL_dmeans3D ||
             g->dL_dscales != g0->dL_dscales || g->dL_drotations != g0->dL_drotations ||
             g->dL_dsh_dc != g0->dL_dsh_dc || g->dL_dsh_rest != g0->dL_dsh_rest || g->dL_dcov3D || g->grad_mask != g0->grad_mask ||
-            g->mask_bits != g0->mask_bits)
+            g->mask_bits != g0->mask_bits || g->pitch_means3D != g0->pitch_means3D ||
+            g->pitch_opacity != g0->pitch_opacity || g->pitch_scales != g0->pitch_scales ||
+            g->pitch_rotations != g0->pitch_rotations || g->dsh_dc_stride != g0->dsh_dc_stride ||
+            g->dsh_rest_stride != g0->dsh_rest_stride)
             return false;
         if ((g->accumulate & params) != params || (g0->dL_dsh_dc && !(g->accumulate & GS_ACC_SH))) return false;
     }

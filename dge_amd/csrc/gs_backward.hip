@@ -339,9 +339,12 @@ __device__ __forceinline__ void apply_grad_mask(const GaussBwdArgs& a, float m, 
 __device__ __forceinline__ void commit_outputs(const GaussBwdArgs& a, uint32_t f, int idx, int src,
                                                const float (&acc)[9], float dop, const float (&ddc)[3],
                                                const GaussOut& o) {
-    const size_t i3 = 3 * (size_t)idx, s3 = 3 * (size_t)src;
+    const size_t i3 = 3 * (size_t)idx;
+    float* const m3 = a.dL_dmeans3D + (size_t)src * a.pm3;
+    float* const op1 = a.dL_dopacity + (size_t)src * a.pop;
+    float* const sc3 = a.dL_dscales + (size_t)src * a.psc;
     float* d0 = a.dsh.dc ? a.dsh.dc + (size_t)src * a.dsh.dc_stride : nullptr;
-    float4* r4 = reinterpret_cast<float4*>(a.dL_drot + 4 * (size_t)src);
+    float4* r4 = reinterpret_cast<float4*>(a.dL_drot + (size_t)src * a.prot);
     float om2[2] = {0.f, 0.f}, oop = 0.f, ocol[3] = {0.f, 0.f, 0.f}, om3[3] = {0.f, 0.f, 0.f};
     float ocov[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, osc[3] = {0.f, 0.f, 0.f}, odc[3] = {0.f, 0.f, 0.f};
     float4 orot = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -349,19 +352,19 @@ __device__ __forceinline__ void commit_outputs(const GaussBwdArgs& a, uint32_t f
 #pragma unroll
         for (int k = 0; k < 3; ++k) a.dL_dconic[i3 + k] = acc[2 + k];
     if (f & GS_ACC_MEANS2D) { om2[0] = a.dL_dmeans2D[i3]; om2[1] = a.dL_dmeans2D[i3 + 1]; }
-    if (f & GS_ACC_OPACITY) oop = a.dL_dopacity[src];
+    if (f & GS_ACC_OPACITY) oop = *op1;
     if (a.dL_dcolors && (f & GS_ACC_COLORS))
 #pragma unroll
         for (int k = 0; k < 3; ++k) ocol[k] = a.dL_dcolors[i3 + k];
     if (f & GS_ACC_MEANS3D)
 #pragma unroll
-        for (int k = 0; k < 3; ++k) om3[k] = a.dL_dmeans3D[s3 + k];
+        for (int k = 0; k < 3; ++k) om3[k] = m3[k];
     if (a.dL_dcov3D && (f & GS_ACC_COV3D))
 #pragma unroll
         for (int k = 0; k < 6; ++k) ocov[k] = a.dL_dcov3D[6 * (size_t)src + k];
     if (f & GS_ACC_SCALES)
 #pragma unroll
-        for (int k = 0; k < 3; ++k) osc[k] = a.dL_dscales[s3 + k];
+        for (int k = 0; k < 3; ++k) osc[k] = sc3[k];
     if (f & GS_ACC_ROTATIONS) orot = *r4;
     if (d0 && (f & GS_ACC_SH))
 #pragma unroll
@@ -370,18 +373,18 @@ __device__ __forceinline__ void commit_outputs(const GaussBwdArgs& a, uint32_t f
     a.dL_dmeans2D[i3] = om2[0] + acc[0];
     a.dL_dmeans2D[i3 + 1] = om2[1] + acc[1];
     if (!(f & GS_ACC_MEANS2D)) a.dL_dmeans2D[i3 + 2] = 0.f;
-    a.dL_dopacity[src] = oop + dop;
+    *op1 = oop + dop;
     if (a.dL_dcolors)  // optional (the raw-parameter SH path does not need it)
 #pragma unroll
         for (int k = 0; k < 3; ++k) a.dL_dcolors[i3 + k] = ocol[k] + acc[6 + k];
-    a.dL_dmeans3D[s3] = om3[0] + o.dmean.x;
-    a.dL_dmeans3D[s3 + 1] = om3[1] + o.dmean.y;
-    a.dL_dmeans3D[s3 + 2] = om3[2] + o.dmean.z;
+    m3[0] = om3[0] + o.dmean.x;
+    m3[1] = om3[1] + o.dmean.y;
+    m3[2] = om3[2] + o.dmean.z;
     if (a.dL_dcov3D)
 #pragma unroll
         for (int k = 0; k < 6; ++k) a.dL_dcov3D[6 * (size_t)src + k] = ocov[k] + o.dcov[k];
 #pragma unroll
-    for (int k = 0; k < 3; ++k) a.dL_dscales[s3 + k] = osc[k] + o.dscale[k];
+    for (int k = 0; k < 3; ++k) sc3[k] = osc[k] + o.dscale[k];
     *r4 = make_float4(orot.x + o.drot.x, orot.y + o.drot.y, orot.z + o.drot.z, orot.w + o.drot.w);
     if (d0) {
 #pragma unroll
@@ -452,18 +455,18 @@ __global__ __launch_bounds__(kGB) void k_gauss_live(GaussBwdViews m) {
     const uint32_t acc = a.acc;
     const int src = in && a.index ? a.index[idx] : idx;
     if (in && !(mask & 1u)) {
-        if (!(acc & GS_ACC_OPACITY)) a.dL_dopacity[src] = 0.f;
+        if (!(acc & GS_ACC_OPACITY)) a.dL_dopacity[(size_t)src * a.pop] = 0.f;
         if (!(acc & GS_ACC_MEANS3D))
 #pragma unroll
-            for (int k = 0; k < 3; ++k) a.dL_dmeans3D[3 * (size_t)src + k] = 0.f;
+            for (int k = 0; k < 3; ++k) a.dL_dmeans3D[(size_t)src * a.pm3 + k] = 0.f;
         if (a.dL_dcov3D && !(acc & GS_ACC_COV3D))
 #pragma unroll
             for (int k = 0; k < 6; ++k) a.dL_dcov3D[6 * (size_t)src + k] = 0.f;
         if (!(acc & GS_ACC_SCALES))
 #pragma unroll
-            for (int k = 0; k < 3; ++k) a.dL_dscales[3 * (size_t)src + k] = 0.f;
+            for (int k = 0; k < 3; ++k) a.dL_dscales[(size_t)src * a.psc + k] = 0.f;
         if (!(acc & GS_ACC_ROTATIONS))
-            *reinterpret_cast<float4*>(a.dL_drot + 4 * (size_t)src) = make_float4(0.f, 0.f, 0.f, 0.f);
+            *reinterpret_cast<float4*>(a.dL_drot + (size_t)src * a.prot) = make_float4(0.f, 0.f, 0.f, 0.f);
         if (a.dsh.dc && !(acc & GS_ACC_SH)) {
             float* d0 = a.dsh.dc + (size_t)src * a.dsh.dc_stride;
             d0[0] = 0.f; d0[1] = 0.f; d0[2] = 0.f;

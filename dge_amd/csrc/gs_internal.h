@@ -433,6 +433,7 @@ struct GaussBwdArgs {
     uint32_t* live_count;      // [P/256] live Gaussians per 256-Gaussian block
     const float4* records;     // [4*K][3] float4: (slot, quadrant) record at 3*(4*slot + q), flag byte 4*slot + q
     float *dL_dmeans2D, *dL_dcolors, *dL_dopacity, *dL_dmeans3D, *dL_dcov3D, *dL_dscales, *dL_drot;
+    int pm3 = 3, pop = 1, psc = 3, prot = 4;  // row pitches (floats) of the parameter-shaped outputs
     uint32_t acc;  // GS_ACC_* bits: add into the output instead of overwriting
     uint32_t zeroed;  // acc bits whose outputs hold zeros: a Gaussian's first write stores (gs_grads.zeroed)
     uint32_t slot_cap = 0xFFFFFFFFu;  // binning capacity (a speculative forward's slots end there)

@@ -53,6 +53,38 @@ __global__ __launch_bounds__(kAdamThreads) void k_adam(AdamLaunch a) {
     const long long n = sg.n;
     const float nstep = -sg.step_size;
     const float bc2s = sg.bias_correction2_sqrt;
+    if (sg.grad_pitch > 0) {
+        // grad rows at a pitch (a row-major gradient bucket's column block): p, m, v packed as float4, each
+        // thread's four gradients gathered (element e of row e / w, column e % w)
+        const uint32_t w = (uint32_t)sg.grad_width, pitch = (uint32_t)sg.grad_pitch;
+        auto gat = [&](long long e) { return sg.grad[(size_t)((uint64_t)e / w) * pitch + (uint64_t)e % w]; };
+        const bool vec4 = ((reinterpret_cast<uintptr_t>(sg.param) | reinterpret_cast<uintptr_t>(sg.exp_avg) |
+                            reinterpret_cast<uintptr_t>(sg.exp_avg_sq)) & 15) == 0;
+        for (int u = 0; u < 4; ++u) {
+            const long long e4 = e0 + 4 * ((long long)u * kAdamThreads + threadIdx.x);
+            if (vec4 && e4 + 3 < n) {
+                float4 p = reinterpret_cast<float4*>(sg.param)[e4 >> 2];
+                float4 m = reinterpret_cast<float4*>(sg.exp_avg)[e4 >> 2];
+                float4 v = reinterpret_cast<float4*>(sg.exp_avg_sq)[e4 >> 2];
+                adam_one(p.x, gat(e4), m.x, v.x, a, nstep, bc2s);
+                adam_one(p.y, gat(e4 + 1), m.y, v.y, a, nstep, bc2s);
+                adam_one(p.z, gat(e4 + 2), m.z, v.z, a, nstep, bc2s);
+                adam_one(p.w, gat(e4 + 3), m.w, v.w, a, nstep, bc2s);
+                reinterpret_cast<float4*>(sg.param)[e4 >> 2] = p;
+                reinterpret_cast<float4*>(sg.exp_avg)[e4 >> 2] = m;
+                reinterpret_cast<float4*>(sg.exp_avg_sq)[e4 >> 2] = v;
+            } else {
+                for (long long e = e4; e < n && e < e4 + 4; ++e) {
+                    float pe = sg.param[e], me = sg.exp_avg[e], ve = sg.exp_avg_sq[e];
+                    adam_one(pe, gat(e), me, ve, a, nstep, bc2s);
+                    sg.param[e] = pe;
+                    sg.exp_avg[e] = me;
+                    sg.exp_avg_sq[e] = ve;
+                }
+            }
+        }
+        return;
+    }
     const bool vec = ((reinterpret_cast<uintptr_t>(sg.param) | reinterpret_cast<uintptr_t>(sg.grad) |
                        reinterpret_cast<uintptr_t>(sg.exp_avg) | reinterpret_cast<uintptr_t>(sg.exp_avg_sq)) & 15) == 0;
     if (vec) {
@@ -124,6 +156,9 @@ extern "C" int gs_adam_step(const gs_adam_segment* segs, int nseg, double beta1,
             const gs_adam_segment& sg = segs[i];
             if (sg.n < 0 || (sg.n > 0 && (!sg.param || !sg.grad || !sg.exp_avg || !sg.exp_avg_sq)))
                 return report_error(GS_ERR_INVALID_ARG, "gs_adam_step: segment with NULL tensors");
+            if (sg.grad_pitch < 0 || (sg.grad_pitch > 0 && (sg.grad_width <= 0 || sg.grad_pitch < sg.grad_width ||
+                                                            sg.n % sg.grad_width)))
+                return report_error(GS_ERR_INVALID_ARG, "gs_adam_step: grad rows need 0 < width <= pitch, n % width == 0");
             if (sg.n == 0) continue;
             a.seg[k] = sg;
             a.block0[k] = blocks;

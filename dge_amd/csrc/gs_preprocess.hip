@@ -238,8 +238,8 @@ __global__ __launch_bounds__(256) void k_preprocess(PreprocessArgs a) {
         if (a.touched) a.touched[idx] = 0;
     }
     // workgroup total of instances and the range of the visible depth keys -> three atomics
-    // (per slot: [0] instances, [1] max key, [2] ~min key: all start at 0).  The depth sort orders
-    // key - min on kDepthSortBits bits; the host redoes it on all 32 when the range is wider.
+    // (per slot: [0] instances, [1] max key, [2] ~min key: all start at 0).  The depth sort's MSD buckets
+    // split [min, max] (depth_sort_msd).
     __shared__ uint32_t part[4][3];
     uint32_t s = touched, kmax = touched ? key : 0u, kmin_n = touched ? ~key : 0u;
 #pragma unroll
@@ -276,8 +276,8 @@ void launch_preprocess(const PreprocessArgs& a, hipStream_t s) {
 }
 
 // Full 32-bit depth keys (the reference's key, rasterizer_impl.cu:86-92) from what preprocess left:
-// the fallback for scenes whose visible depth keys span more than kDepthSortBits (the 3-pass sort
-// has overwritten the originals by then).
+// the 32-bit LSD redo of the depth order that DGE_AMD_DEPTH_KEYS32=1 forces (a test of the MSD sort;
+// the MSD pass has overwritten the original keys with relative ones by then).
 __global__ __launch_bounds__(256) void k_depth_keys32(int P, const uint32_t* __restrict__ rect,
                                                       const Splat* __restrict__ splat, uint32_t* __restrict__ key) {
     const int i = blockIdx.x * 256 + threadIdx.x;

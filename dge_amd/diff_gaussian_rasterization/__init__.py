@@ -349,8 +349,9 @@ def _accumulation_mode(p, node=None):
     g = p.grad
     if g is None:
         return "new", owner
-    if (g.shape == p.shape and g.dtype == torch.float32 and g.device == p.device and g.is_contiguous()
-            and not g.requires_grad):
+    # (a contiguous .grad, or a column block of a row-major gradient bucket: rows at a pitch, written in place)
+    if (g.shape == p.shape and g.dtype == torch.float32 and g.device == p.device and not g.requires_grad
+            and (g.is_contiguous() or _C.row_pitch_ok(g))):
         return "add", owner
     return None, None
 

@@ -38,22 +38,59 @@ def shard_views(num_views: int, world: int, rank: int) -> range:
 
 
 class GradBucket:
-    """One flat gradient buffer shared by a list of parameters."""
+    """One gradient buffer shared by a list of parameters.
 
-    def __init__(self, params: Sequence[torch.Tensor]):
+    Row-major (``rows``, the default when every parameter has the same number of rows, as a GaussianModel's
+    six do): one [n, pitch] fp32 matrix, every parameter's ``.grad`` a column block of it (a strided view,
+    the parameter's shape), pitch = the summed row widths rounded up to 16 floats (59 -> 64 at SH degree 3)
+    and 4-wide parameters (the rotation) first, on 16-byte boundaries.  A Gaussian's whole gradient is then
+    one 256-B row: the per-Gaussian backward pass writes two cache lines per live Gaussian instead of one
+    or two in each of six tensors (gs_grads.pitch_*), and the sparse all-reduce packs whole rows.
+    Otherwise (``rows=False``, or parameters of different row counts) the flat concatenation."""
+
+    def __init__(self, params: Sequence[torch.Tensor], rows: bool | None = None):
         self.params = list(params)
         dev = self.params[0].device
-        total = sum(p.numel() for p in self.params)
-        self.flat = torch.zeros(total, dtype=torch.float32, device=dev)
+        n0 = {p.shape[0] if p.dim() else -1 for p in self.params}
+        if rows is None:  # (GPU parameters: the fused backward writes the rows in place; autograd's own
+            # accumulation into a strided .grad works too but warns about the layout contract)
+            rows = (len(n0) == 1 and -1 not in n0 and all(p.dim() >= 1 and p.is_cuda for p in self.params))
         self.views = []
-        off = 0
-        for p in self.params:
-            v = self.flat[off:off + p.numel()].view_as(p)
-            self.views.append(v)
-            off += p.numel()
+        self.rows = None
+        if rows:
+            n = n0.pop()
+            widths = [p[0].numel() if n else int(torch.Size(p.shape[1:]).numel()) for p in self.params]
+            order = sorted(range(len(self.params)), key=lambda i: widths[i] % 4 != 0)  # (stable: 4-wide first)
+            cols, c = {}, 0
+            for i in order:
+                if widths[i] % 4 == 0:
+                    c = (c + 3) // 4 * 4
+                cols[i] = c
+                c += widths[i]
+            pitch = max(16, (c + 15) // 16 * 16)
+            self.flat = torch.zeros(n * pitch, dtype=torch.float32, device=dev)
+            self.rows = self.flat.view(n, pitch)
+            for i, p in enumerate(self.params):
+                self.views.append(self.rows[:, cols[i]:cols[i] + widths[i]].view(p.shape))
+        else:
+            total = sum(p.numel() for p in self.params)
+            self.flat = torch.zeros(total, dtype=torch.float32, device=dev)
+            off = 0
+            for p in self.params:
+                self.views.append(self.flat[off:off + p.numel()].view_as(p))
+                off += p.numel()
         self._rows_cap = 0       # speculated packed rows of the next sparse all-reduce (0: none yet)
         self._deferred = None    # an allreduce_end(defer_check=True) awaiting allreduce_finalize()
         self.attach()
+
+    def row_matrices(self):
+        """The bucket as [n, width] matrices sharing their rows (the sparse all-reduce's regions), or None:
+        the row-major matrix itself, or each parameter's [n, -1] view of the flat layout."""
+        if self.rows is not None:
+            return [self.rows]
+        rows = {v.shape[0] if v.dim() else -1 for v in self.views}
+        n = next(iter(rows))
+        return [v.reshape(n, -1) for v in self.views] if len(rows) == 1 and n >= 0 else None
 
     def attach(self):
         for p, v in zip(self.params, self.views):
@@ -135,9 +172,8 @@ class GradBucket:
         self._pending = None
         if not dist.is_available() or not dist.is_initialized() or dist.get_world_size(group) < min_world:
             return
-        rows = {v.shape[0] if v.dim() else -1 for v in self.views}
-        n = next(iter(rows))
-        mats = [v.reshape(n, -1) for v in self.views] if len(rows) == 1 and n >= 0 else None
+        mats = self.row_matrices()
+        n = mats[0].shape[0] if mats is not None else -1
         hints = list(live_hint or [])
         if (mats is None or not hints or not _native_ok(mats)
                 or any(h is None or h.dtype != torch.uint8 or h.shape != (n,) for h in hints)):
@@ -313,11 +349,10 @@ class GradBucket:
                 if p.grad is not None and p.grad.data_ptr() != v.data_ptr():
                     v.copy_(p.grad)
             self.attach()
-        rows = {v.shape[0] if v.dim() else -1 for v in self.views}
-        if not sparse or async_op or len(rows) != 1 or -1 in rows:
+        mats = self.row_matrices()
+        if not sparse or async_op or mats is None:
             return dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=group, async_op=async_op)
-        n = rows.pop()
-        mats = [v.reshape(n, -1) for v in self.views]
+        n = mats[0].shape[0]
         live = _rows_live(mats, n)
         dist.all_reduce(live, op=dist.ReduceOp.MAX, group=group)
         idx = torch.nonzero(live).squeeze(1)

@@ -24,6 +24,7 @@ import ctypes
 
 import torch
 
+from . import _C
 from . import _native as N
 
 
@@ -61,12 +62,15 @@ class FusedAdam(torch.optim.Optimizer):
                     state["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
                     state["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
                 m, v = state["exp_avg"], state["exp_avg_sq"]
+                # (the gradient may also be a column block of a row-major gradient bucket: rows at a pitch)
+                strided = not g.is_contiguous() and _C.row_pitch_ok(g) and p.dim() >= 1
                 for name, t in (("param", p), ("grad", g), ("exp_avg", m), ("exp_avg_sq", v)):
                     if not t.is_cuda:
                         raise RuntimeError(f"FusedAdam: {name} must live on the GPU (no CPU path)")
-                    if t.dtype != torch.float32 or not t.is_contiguous() or t.shape != p.shape:
+                    if t.dtype != torch.float32 or t.shape != p.shape or not (t.is_contiguous() or
+                                                                              (t is g and strided)):
                         raise RuntimeError(f"FusedAdam: {name} must be a contiguous float32 tensor of the "
-                                           f"parameter's shape")
+                                           f"parameter's shape (the gradient: or rows at a pitch)")
                 state["step"] += 1
                 t = float(state["step"].item())
                 bias_correction1 = 1 - beta1 ** t
@@ -75,6 +79,8 @@ class FusedAdam(torch.optim.Optimizer):
                 seg.param, seg.grad = p.data_ptr(), g.data_ptr()
                 seg.exp_avg, seg.exp_avg_sq = m.data_ptr(), v.data_ptr()
                 seg.n = p.numel()
+                if strided:
+                    seg.grad_width, seg.grad_pitch = int(p[0].numel()), int(g.stride(0))
                 seg.step_size = lr / bias_correction1
                 seg.bias_correction2_sqrt = bias_correction2 ** 0.5
                 launches.setdefault((p.device, float(beta1), float(beta2), eps), []).append(seg)

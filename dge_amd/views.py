@@ -228,10 +228,12 @@ class _RasterizeViews(torch.autograd.Function):
             if ctx.has_sh:
                 o.dL_dsh_dc = targets["f_dc"].data_ptr()
                 o.dL_dsh_rest = _C._ptr(targets["f_rest"])
-                o.dsh_dc_stride = 3
-                o.dsh_rest_stride = 3 * (f_rest.size(1) if f_rest is not None and f_rest.numel() else 0)
             o.dL_dscales = targets["scaling"].data_ptr()
             o.dL_drotations = targets["rotation"].data_ptr()
+            # row pitches: a .grad that is a column block of a row-major gradient bucket is written in place
+            rest = targets["f_rest"] if ctx.has_sh and f_rest is not None and f_rest.numel() else None
+            _C.set_grad_pitches(o, targets["xyz"], targets["opacity"], targets["scaling"], targets["rotation"],
+                                targets["f_dc"] if ctx.has_sh else None, rest)
             # the first view writes (or adds into an existing .grad), the others add; into a .grad buffer
             # zeroed this step, a Gaussian's first gradient is stored, not added (gs_grads.zeroed)
             o.accumulate = acc0 if v == 0 else acc_all

@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define GS_RASTER_ABI_VERSION 16
+#define GS_RASTER_ABI_VERSION 17
 
 #define GS_OK 0
 #define GS_ERR_INVALID_ARG 1   /* AT_ERROR / std::runtime_error in the reference */
@@ -194,6 +194,14 @@ typedef struct gs_grads {         /* backward outputs, every element written */
      * first view that has a Gaussian live stores, later views add.  0: plain
      * accumulation (ABI 12). */
     unsigned int zeroed;
+    /* Row pitches (in floats) of the parameter-shaped outputs: element (i, c) of dL_dmeans3D at
+     * dL_dmeans3D[i * pitch_means3D + c], likewise dL_dopacity, dL_dscales, dL_drotations; 0 = the
+     * reference's packed [P,3] / [P] / [P,3] / [P,4].  With dsh_dc_stride / dsh_rest_stride they let every
+     * parameter gradient of a Gaussian live in ONE row of a row-major gradient bucket (the .grad tensors
+     * then strided views of it: dge_amd.multiview.GradBucket), so the per-Gaussian pass reads and writes
+     * two cache lines per live Gaussian instead of one or two in each of six arrays.  dL_drotations rows
+     * must stay 16-byte aligned (pitch a multiple of 4).  (ABI 17) */
+    int pitch_means3D, pitch_opacity, pitch_scales, pitch_rotations;
 } gs_grads;
 
 int gs_rasterize_forward_ex(const gs_settings *s, const gs_params *g, float *out_color, float *out_depth,
@@ -324,6 +332,10 @@ typedef struct gs_adam_segment {
     long long n;                  /* elements */
     float step_size;
     float bias_correction2_sqrt;
+    /* grad's rows (ABI 17): element e at grad[(e / grad_width) * grad_pitch + e % grad_width] — a .grad
+     * that is a column block of a row-major gradient bucket; grad_pitch 0: packed like param */
+    int grad_width;
+    int grad_pitch;
 } gs_adam_segment;
 int gs_adam_step(const gs_adam_segment *segs, int nseg, double beta1, double beta2, float eps,
                  gs_stream_t stream);

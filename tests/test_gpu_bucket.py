@@ -141,7 +141,7 @@ def test_allreduce_begin_end_one_rank(cuda_device):
         torch.cuda.synchronize()
         before = bucket.flat.clone()
         n = sc._xyz.shape[0]
-        mats = [v.reshape(n, -1) for v in bucket.views]
+        mats = bucket.row_matrices()
         nonzero = mv._rows_live(mats, n).bool()
         union = torch.zeros(n, dtype=torch.bool, device=cuda_device)
         for h in hints:

@@ -47,6 +47,40 @@ def test_fused_adam_matches_torch_adam_gpu_foreach(cuda_device):
     assert diff == 0
 
 
+def test_fused_adam_with_row_major_bucket_grads(cuda_device):
+    """The GaussianModel's six parameters with their .grad in a row-major GradBucket (every .grad a column
+    block of one [P, 64] matrix: rows at a pitch): FusedAdam (the gathered-gradient segments) against
+    torch.optim.Adam (foreach) stepping the same parameters with contiguous copies of the gradients,
+    bitwise, over five steps."""
+    from dge_amd.multiview import GradBucket
+    from dge_amd.optim import FusedAdam
+
+    g = torch.Generator().manual_seed(3)
+    shapes = [(1001, 3), (1001, 1, 3), (1001, 15, 3), (1001, 1), (1001, 3), (1001, 4)]
+    lrs = [1.6e-4, 0.0125, 0.0125 / 20, 0.05, 0.005, 0.001]
+    init = [torch.randn(s, generator=g) for s in shapes]
+    ref = [torch.nn.Parameter(t.clone().to(cuda_device)) for t in init]
+    dev = [torch.nn.Parameter(t.clone().to(cuda_device)) for t in init]
+    bucket = GradBucket(dev)
+    assert bucket.rows is not None and not dev[2].grad.is_contiguous()
+    mk = lambda ps: [{"params": [p], "lr": lr, "name": f"g{i}"} for i, (p, lr) in enumerate(zip(ps, lrs))]  # noqa
+    opt_ref = torch.optim.Adam(mk(ref), lr=0.0, betas=(0.9, 0.99), eps=1e-15)
+    opt_dev = FusedAdam(mk(dev), lr=0.0, betas=(0.9, 0.99), eps=1e-15)
+    for it in range(5):
+        bucket.zero()
+        for k, (a, b) in enumerate(zip(ref, dev)):
+            gr = (torch.randn(a.shape, generator=g) * (10.0 ** (k % 3 - 2))).to(cuda_device)
+            a.grad = gr.clone()
+            b.grad.copy_(gr)  # (into the bucket's strided view)
+        opt_ref.step()
+        opt_dev.step()
+    torch.cuda.synchronize()
+    for a, b in zip(ref, dev):
+        assert torch.equal(a.detach(), b.detach())
+        for key in ("exp_avg", "exp_avg_sq"):
+            assert torch.equal(opt_dev.state[b][key], opt_ref.state[a][key])
+
+
 def test_fused_adam_matches_torch_adam_cpu(cuda_device):
     from dge_amd.optim import FusedAdam
 

@@ -173,7 +173,7 @@ def test_grad_bucket_views_and_zero():
     assert vs.sum() == 6 and rm.tolist() == [1, 2]
 
 
-def _sparse_worker(rank, world, port, q):
+def _sparse_worker(rank, world, port, q, row_major=False):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -184,7 +184,8 @@ def _sparse_worker(rank, world, port, q):
             g = torch.Generator().manual_seed(100 + rank)
             ps = [torch.zeros(400, 3, requires_grad=True), torch.zeros(400, 1, 15, requires_grad=True),
                   torch.zeros(400, 1, requires_grad=True)]
-            bk = GradBucket(ps)
+            bk = GradBucket(ps, rows=row_major)
+            assert (bk.rows is not None) == row_major
             rows = torch.randperm(400, generator=g)[: 30 + 20 * rank]  # each rank: its own live rows
             for p in ps:
                 p.grad[rows] = torch.randn(p.grad[rows].shape, generator=g)
@@ -196,12 +197,14 @@ def _sparse_worker(rank, world, port, q):
 
 
 @pytest.mark.slow
-def test_sparse_bucket_allreduce_equals_dense():
-    """GradBucket.allreduce(sparse=True) (union of nonzero rows, packed) == the dense all-reduce."""
+@pytest.mark.parametrize("rows", [False, True], ids=["flat", "row_major"])
+def test_sparse_bucket_allreduce_equals_dense(rows):
+    """GradBucket.allreduce(sparse=True) (union of nonzero rows, packed) == the dense all-reduce, for the flat
+    concatenation and for the row-major bucket (one [n, pitch] matrix, each .grad a column block)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_sparse_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_sparse_worker, args=(r, 2, port, q, rows)) for r in range(2)]
     for p in procs:
         p.start()
     res = [q.get(timeout=300) for _ in procs]
@@ -212,3 +215,27 @@ def test_sparse_bucket_allreduce_equals_dense():
         np.testing.assert_array_equal(sp, de)
         assert np.count_nonzero(de) > 0
     np.testing.assert_array_equal(res[0][1], res[1][1])
+
+
+def test_row_major_bucket_layout():
+    """GradBucket(rows=True): every parameter's .grad is a column block of one [n, pitch] matrix (4-wide
+    parameters first, on 16-B boundaries; pitch a multiple of 16 floats), its shape the parameter's; writes
+    through .grad land in the right rows and columns; zero() clears every row; the GaussianModel's six
+    tensors (3 + 3 + 45 + 1 + 3 + 4 = 59 floats) get a 64-float pitch with the rotation at column 0."""
+    from dge_amd.scene import synthetic_scene
+
+    sc = synthetic_scene(10, sh_degree=3, seed=0).requires_grad_(True)
+    bk = GradBucket(sc.parameters(), rows=True)
+    assert bk.rows.shape == (10, 64) and bk.check_attached()
+    rot = sc._rotation.grad
+    assert rot.data_ptr() == bk.rows.data_ptr() and rot.stride() == (64, 1)
+    cols = {}
+    for name, p in zip(["xyz", "dc", "rest", "op", "sc", "rot"], sc.parameters()):
+        assert p.grad.shape == p.shape and p.grad.stride(0) == 64
+        cols[name] = (p.grad.data_ptr() - bk.rows.data_ptr()) // 4
+        p.grad.fill_(float(len(cols)))
+    assert cols["rot"] == 0 and sorted(cols.values()) == [0, 4, 7, 10, 55, 56]
+    assert float(bk.rows[:, :59].min()) >= 1.0 and not bk.rows[:, 59:].any()
+    assert float(bk.rows[3, 10:55].max()) == 3.0  # (the SH rest block, 45 floats of row 3)
+    bk.zero()
+    assert not bk.flat.any() and bk.check_attached()
