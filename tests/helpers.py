@@ -268,9 +268,11 @@ def raster_sums(out):
                            out["dL_dcolors"].reshape(P, 3)], 1).astype(np.float32)
 
 
-def raster_grad_mismatches(got, ref, rtol=RTOL):
+def raster_grad_mismatches(got, ref, rtol=RTOL, rows=None):
     g, r = raster_sums(got).astype(np.float64), raster_sums(ref).astype(np.float64)
     mag = ref["mag9"].astype(np.float64)
+    if rows is not None:
+        g, r, mag = g[rows], r[rows], mag[rows]
     err = np.abs(g - r)
     tol = rtol * mag + 1e-30
     res = {}
@@ -279,8 +281,8 @@ def raster_grad_mismatches(got, ref, rtol=RTOL):
     return res
 
 
-def compare_raster_grads(got, ref, rtol=RTOL, label=""):
-    res = raster_grad_mismatches(got, ref, rtol)
+def compare_raster_grads(got, ref, rtol=RTOL, label="", rows=None):
+    res = raster_grad_mismatches(got, ref, rtol, rows)
     print(f"[parity{(' ' + label) if label else ''}] raster-sum mismatches (count, max err/(rtol*mag)): {res}")
     bad = {k: v for k, v in res.items() if v[0] != 0}
     assert not bad, f"rasterizer gradient sums beyond {rtol} x magnitude: {bad}"
@@ -290,29 +292,32 @@ def compare_raster_grads(got, ref, rtol=RTOL, label=""):
 CHAIN_NAMES = ["dL_dmeans3D", "dL_dcov3D", "dL_dsh", "dL_dscales", "dL_drotations"]
 
 
-def chain_mismatches(O, got, ref):
+def chain_mismatches(O, got, ref, rows=None):
     """The per-Gaussian chain (backward.cu:144-396) fed with the GPU's own rasterizer sums on the
-    oracle: the parameter gradients must then be bit-identical to the GPU's."""
+    oracle: the parameter gradients must then be bit-identical to the GPU's (rows: only those Gaussians)."""
     chained = O.backward_chain(ref["state"], raster_sums(got))
-    return {n: _exact_mismatch(got[n], chained[n], signed_zero=False) for n in CHAIN_NAMES}
+    sel = (lambda a: a) if rows is None else (lambda a: np.asarray(a)[rows])
+    return {n: _exact_mismatch(sel(got[n]), sel(chained[n]), signed_zero=False) for n in CHAIN_NAMES}
 
 
-def compare_chain(O, got, ref, label=""):
-    c = chain_mismatches(O, got, ref)
+def compare_chain(O, got, ref, label="", rows=None):
+    c = chain_mismatches(O, got, ref, rows)
     print(f"[parity{(' ' + label) if label else ''}] chain mismatches (bitwise): {c}")
     bad = {k: v for k, v in c.items() if v != 0}
     assert not bad, f"per-Gaussian chain differs from the oracle's on the same sums: {bad}"
     return c
 
 
-def compare_grads(got, ref, rtol=RTOL, O=None, label=""):
+def compare_grads(got, ref, rtol=RTOL, O=None, label="", rows=None):
     """Backward parity in two exact stages — the rasterizer sums within rtol x their magnitude, the
     per-Gaussian chain bit-identical on the same sums (needs the GPU's dL_dconic3 and the oracle
-    state) — then the end-to-end gradients against the oracle's as a report + sanity bound."""
+    state) — then the end-to-end gradients against the oracle's as a report + sanity bound.
+    rows: a boolean mask of the Gaussians compared (None: all)."""
     if O is not None and "dL_dconic3" in got and "mag9" in ref:
-        compare_raster_grads(got, ref, rtol, label)
-        compare_chain(O, got, ref, label)
-    worst = {n: close_report(got[n], ref[n], rtol)[1] for n in GRAD_NAMES}
+        compare_raster_grads(got, ref, rtol, label, rows)
+        compare_chain(O, got, ref, label, rows)
+    sel = (lambda a: np.asarray(a)) if rows is None else (lambda a: np.asarray(a)[rows])
+    worst = {n: close_report(sel(got[n]), sel(ref[n]), rtol)[1] for n in GRAD_NAMES}
     print(f"[parity{(' ' + label) if label else ''}] end-to-end max |err|/max|ref|: {worst}")
     for n in GRAD_NAMES:
-        assert_close(got[n], ref[n], n, rtol)
+        assert_close(sel(got[n]), sel(ref[n]), n, rtol)

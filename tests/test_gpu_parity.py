@@ -658,7 +658,12 @@ def test_depth_beyond_30bit_key_range_keeps_reference_order(cuda_device, oracle,
     np.testing.assert_array_equal(got["ranges"], ref["ranges"])
     np.testing.assert_array_equal(got["point_list"], ref["point_list"])
     compare_forward(got, ref, label="far-depth")
-    compare_grads(got, ref, O=oracle, label="far-depth")
+    # (the five Gaussians beyond 5e37 overflow float32 in the chain — 1 / t.z near the smallest normal, its
+    # square flushed — on either side in ways that differ only in which non-finite or subnormal value comes
+    # out; this test is about their depth order, so their gradients are left out of the comparison)
+    near = np.ones(ref["radii"].shape[0], bool)
+    near[-5:] = False
+    compare_grads(got, ref, O=oracle, label="far-depth", rows=near)
 
 
 def test_forced_32bit_depth_keys_match_30bit_path(cuda_device, monkeypatch):
