@@ -42,6 +42,11 @@ constexpr int kDepthPassBits = 9;
 constexpr int kDepthSortBits = 3 * kDepthPassBits;
 constexpr int kMaxSinglePassBits = 11;          // tile keys up to 2048 tiles sort in one pass
 constexpr int kMsdBits = 11, kMsdBuckets = 1 << kMsdBits, kMsdCulled = kMsdBuckets - 1;  // depth_sort_msd
+#ifndef GS_MSD_IPT
+#define GS_MSD_IPT 8  // keys per thread of the MSD pass's blocks (A/B: -DGS_MSD_IPT=16)
+#endif
+constexpr int kMsdIPT = GS_MSD_IPT;
+static_assert(kMsdIPT >= kDepthSortIPT, "the depth sort's tables are sized for kDepthSortTile-key blocks");
 constexpr size_t kAlign = 256;
 
 __host__ __device__ inline size_t align_up(size_t x, size_t a = kAlign) { return (x + a - 1) / a * a; }

@@ -197,9 +197,13 @@ __global__ __launch_bounds__(256) void k_radix_hist(const KT* __restrict__ keys,
 // digit dl) sums rows [g*per, (g+1)*per) of its digit (a wave load covers 4 rows
 // x 64 B), the 64 row-group sums are scanned in LDS, then the rows are
 // rewritten.  (c2: 880 tile-sort rows -> 14 per thread.)
-constexpr int kScanDigits = 16, kScanGroups = 64, kScanRegs = 32;
+#ifndef GS_SCAN_DIGITS
+#define GS_SCAN_DIGITS 16  // digits per digit-scan workgroup (x 64 row groups = its threads; A/B: -DGS_SCAN_DIGITS=4)
+#endif
+constexpr int kScanDigits = GS_SCAN_DIGITS, kScanGroups = 64, kScanRegs = 32;
+constexpr int kScanThreads = kScanDigits * kScanGroups;
 constexpr int kScanBmRows = kScanGroups * kScanRegs;  // block-major tables up to this many blocks
-__global__ __launch_bounds__(1024) void k_radix_digit_scan(uint32_t* __restrict__ hist, int nb, int ndig,
+__global__ __launch_bounds__(kScanThreads) void k_radix_digit_scan(uint32_t* __restrict__ hist, int nb, int ndig,
                                                            uint32_t* __restrict__ totals,
                                                            const uint32_t* __restrict__ n_dev, uint32_t cap,
                                                            int tile) {
@@ -534,7 +538,7 @@ static void radix_pass(const uint32_t* kin, const void* vin, uint32_t* kout, voi
     hipLaunchKernelGGL((k_radix_hist<BITS, IPT>), dim3(nb), dim3(256), 0, s, kin, n, shift, hist, nb, bm, bias_not,
                        n_dev);
     if (bm)
-        hipLaunchKernelGGL(k_radix_digit_scan, dim3(div_up(NDIG, kScanDigits)), dim3(1024), 0, s, hist, nb, NDIG,
+        hipLaunchKernelGGL(k_radix_digit_scan, dim3(div_up(NDIG, kScanDigits)), dim3(kScanThreads), 0, s, hist, nb, NDIG,
                            totals, n_dev, n, 256 * IPT);
     else
         hipLaunchKernelGGL(k_radix_digit_scan_dm, dim3(NDIG), dim3(256), 0, s, hist, nb, totals, n_dev, n, 256 * IPT);
@@ -794,12 +798,13 @@ int depth_sort_msd(uint32_t* key0, uint32_t* key1, uint2* pair0, uint2* pair1, c
                    uint32_t* hist, uint32_t* totals, int nblocks, uint2* bucket_ranges, const uint32_t* bias_not,
                    hipStream_t s) {
     if (n == 0) return 0;
-    constexpr int IPT = kDepthSortIPT, NDIG = kMsdBuckets;
+    constexpr int IPT = kMsdIPT, NDIG = kMsdBuckets;
+    nblocks = (int)div_up_u(n, 256u * IPT);  // (<= the table's rows: sized for kDepthSortTile-key blocks)
     const int bm = nblocks <= kScanBmRows ? 1 : 0;
     hipLaunchKernelGGL((k_radix_hist<kMsdBits, IPT, uint32_t, true>), dim3(nblocks), dim3(256), 0, s, key0, n, 0, hist,
                        nblocks, bm, bias_not, (const uint32_t*)nullptr);
     if (bm)
-        hipLaunchKernelGGL(k_radix_digit_scan, dim3(div_up(NDIG, kScanDigits)), dim3(1024), 0, s, hist, nblocks, NDIG,
+        hipLaunchKernelGGL(k_radix_digit_scan, dim3(div_up(NDIG, kScanDigits)), dim3(kScanThreads), 0, s, hist, nblocks, NDIG,
                            totals, (const uint32_t*)nullptr, n, 256 * IPT);
     else
         hipLaunchKernelGGL(k_radix_digit_scan_dm, dim3(NDIG), dim3(256), 0, s, hist, nblocks, totals,
@@ -1169,7 +1174,7 @@ __global__ __launch_bounds__(256) void k_ranges_counts(const uint32_t* __restric
 void launch_emit_fused(const EmitArgs& a, hipStream_t s) {
     if (a.P <= 0) return;
     // first level: column totals and each block's column offsets, then the column-ordered emission
-    hipLaunchKernelGGL(k_radix_digit_scan, dim3(kXDigits / kScanDigits), dim3(1024), 0, s, a.xhist, a.scan_blocks,
+    hipLaunchKernelGGL(k_radix_digit_scan, dim3(kXDigits / kScanDigits), dim3(kScanThreads), 0, s, a.xhist, a.scan_blocks,
                        kXDigits, a.xtotals, (const uint32_t*)nullptr, 0u, 1);
     if (a.ids_only)
         hipLaunchKernelGGL(k_scan_emit_x<true>, dim3(a.scan_blocks), dim3(256), 0, s, a);
@@ -1195,7 +1200,7 @@ void launch_row_pass(const EmitArgs& a, uint32_t K, uint2* point_pairs, uint32_t
     hipLaunchKernelGGL((k_radix_hist<kXBits, IPT, uint16_t>), dim3(nb), dim3(256), 0, s, keys, K, kXBits, hist, nb,
                        bm, (const uint32_t*)nullptr, n_dev);
     if (bm)
-        hipLaunchKernelGGL(k_radix_digit_scan, dim3(div_up(NDIG, kScanDigits)), dim3(1024), 0, s, hist, nb, NDIG,
+        hipLaunchKernelGGL(k_radix_digit_scan, dim3(div_up(NDIG, kScanDigits)), dim3(kScanThreads), 0, s, hist, nb, NDIG,
                            a.xtotals, n_dev, K, TILE);
     else
         hipLaunchKernelGGL(k_radix_digit_scan_dm, dim3(NDIG), dim3(256), 0, s, hist, nb, a.xtotals, n_dev, K, TILE);
