@@ -342,8 +342,11 @@ enum ValMode { kValU32 = 0, kValPairFirst = 1, kValPair = 2 };
 // WK: the sorted keys are written (every pass but the last tile-sort pass).  Without them the block
 // stages only the digit (u16), and the per-wave digit counters are u16 throughout (<= 256*IPT), so
 // the single-pass tile sort fits three workgroups per CU (52 KB of LDS instead of 68).
+#ifndef GS_SCATTER_MINW
+#define GS_SCATTER_MINW 1  // minimum waves per SIMD the scatter's registers are fitted for (A/B)
+#endif
 template <int BITS, int IPT, bool IDV, int VM, bool WK = true, bool TC = false, class KT = uint32_t, bool DM = false>
-__global__ __launch_bounds__(256) void k_radix_scatter(const KT* __restrict__ keys_in,
+__global__ __launch_bounds__(256, GS_SCATTER_MINW) void k_radix_scatter(const KT* __restrict__ keys_in,
                                                        const void* __restrict__ vals_in_,
                                                        uint32_t* __restrict__ keys_out, void* __restrict__ vals_out_,
                                                        const uint32_t* __restrict__ gauss_by_slot, uint32_t n,
@@ -689,7 +692,7 @@ __global__ __launch_bounds__(256) void k_depth_bucket_sort(uint32_t* __restrict_
                                                            const uint2* __restrict__ ranges,
                                                            const uint32_t* __restrict__ bias_not) {
     __shared__ uint32_t s_key[kBucketCap];
-    __shared__ uint2 s_val[kBucketCap];
+    __shared__ uint16_t s_pos[kBucketCap];  // each staged key's position in the bucket (its value: re-read at the end)
     __shared__ uint16_t cnt[4][kLocalDig];
     __shared__ uint32_t s_start[kLocalDig], s_tot[kLocalDig], s_base[kLocalDig];
     __shared__ uint32_t lds4[4];
@@ -707,13 +710,12 @@ __global__ __launch_bounds__(256) void k_depth_bucket_sort(uint32_t* __restrict_
     uint2 val[kBucketIPT];
     if (n <= (uint32_t)kBucketCap) {  // in LDS: every pass ranks the bucket held in registers
         const int ipt = (int)div_up_u(n, 256u);
+        uint32_t src[kBucketIPT];  // the element's position in the bucket's input
 #pragma unroll
         for (int it = 0; it < kBucketIPT; ++it) {
             const uint32_t j = (uint32_t)(w * 64 * ipt + it * 64 + lane);
-            if (it < ipt && j < n) {
-                key[it] = keys_b[r.x + j];
-                val[it] = vals_b[r.x + j];
-            }
+            src[it] = j;
+            if (it < ipt && j < n) key[it] = keys_b[r.x + j];
         }
         for (int p = 0; p < passes; ++p) {
 #pragma unroll
@@ -724,7 +726,7 @@ __global__ __launch_bounds__(256) void k_depth_bucket_sort(uint32_t* __restrict_
                 const uint32_t j = (uint32_t)(w * 64 * ipt + it * 64 + lane);
                 if (it < ipt && j < n) {
                     s_key[pos[it]] = key[it];
-                    s_val[pos[it]] = val[it];
+                    s_pos[pos[it]] = (uint16_t)src[it];
                 }
             }
             __syncthreads();
@@ -734,12 +736,12 @@ __global__ __launch_bounds__(256) void k_depth_bucket_sort(uint32_t* __restrict_
                 const uint32_t j = (uint32_t)(w * 64 * ipt + it * 64 + lane);
                 if (it < ipt && j < n) {
                     key[it] = s_key[j];
-                    val[it] = s_val[j];
+                    src[it] = s_pos[j];
                 }
             }
             __syncthreads();  // (the next pass's counters and staging)
         }
-        for (uint32_t i = tid; i < n; i += 256) vals_a[r.x + i] = s_val[i];
+        for (uint32_t i = tid; i < n; i += 256) vals_a[r.x + i] = vals_b[r.x + s_pos[i]];
         return;
     }
     // a bucket over kBucketCap keys: LSD passes over it in global memory, chunk after chunk in input order
