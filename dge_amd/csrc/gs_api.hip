@@ -77,6 +77,8 @@ bool force_depth_keys32() {
 
 // DGE_AMD_TILE_SORT=2pass: the emission + two full tile-sort passes + k_ranges even where the
 // two-level binning applies (tests compare both; read per forward)
+// DGE_AMD_TILE_SORT=2pass (a test switch): the emission + radix tile sort (+ k_ranges) on every grid, in place
+// of the direct emission (<= 2048 tiles) and the two-level binning (larger grids)
 bool tile_sort_unfused() {
     const char* e = getenv("DGE_AMD_TILE_SORT");
     return e && !strcmp(e, "2pass");
@@ -406,6 +408,12 @@ int bin_after_preprocess(FwdState& f, hipStream_t stream) {
     ea.first_slot = at<uint32_t>(geom, gl.first_slot);
     ea.scan_blocks = gl.scan_blocks;
     ea.xhist = two_level(g.gx, g.gy) && pa.rect_packed ? at<uint32_t>(geom, gl.emit_hist) : nullptr;
+    // direct emission (k_emit_tiles): the scan also counts each block's instances per tile (in the depth
+    // sort's tables, free by then)
+    const bool direct = !ea.xhist && direct_emission_grid(g.gx, g.gy) && pa.rect_packed && !tile_sort_unfused();
+    ea.thist = direct ? at<uint32_t>(geom, gl.sort_hist) : nullptr;
+    ea.ttotals = direct ? at<uint32_t>(geom, gl.sort_totals) : nullptr;
+    ea.ntiles = g.tiles;
     { StageScope sc(ST_SCAN, stream); launch_scan_reduce(ea, stream); }
     GS_LAUNCHED("instance scan");
     return GS_OK;
@@ -515,6 +523,16 @@ int bin_emit(FwdState& f, void* bin, uint32_t K_layout, const uint32_t* n_dev, h
         launch_row_pass(ea, K_layout, at<uint2>(bin, bl.point_pairs), at<uint32_t>(bin, bl.sort_hist), bl.sort_blocks,
                         at<uint2>(img, il.ranges), at<uint32_t>(img, il.tile_order), stream, n_dev); }
         GS_LAUNCHED("two-level binning");
+        return GS_OK;
+    }
+    if (ea.thist) {  // direct emission: the lists, the tile ranges and the dispatch order in one launch
+        ea.ids_only = f.ids_only = !bwd && f.ids_ok;
+        ea.pairs_out = at<uint2>(bin, bl.point_pairs);
+        ea.rec_flags32 = bwd ? at<uint32_t>(bin, bl.rec_flags) : nullptr;
+        ea.ranges = at<uint2>(img, il.ranges);
+        ea.tile_order = at<uint32_t>(img, il.tile_order);
+        { StageScope sc(ST_EMIT, stream); launch_emit_tiles(ea, stream); }
+        GS_LAUNCHED("direct emission");
         return GS_OK;
     }
     ea.tile_key = at<uint32_t>(bin, bl.key0);

@@ -120,7 +120,9 @@ inline GeomLayout geom_layout(int P) {
     L.val0 = o; o = align_up(o + 8 * p);  // depth sort values: uint2 (rect-or-count, Gaussian)
     L.val1 = o; o = align_up(o + 8 * p);
     L.rect = o; o = align_up(o + 4 * p);  // packed tile rect (pack_rect) or tiles_touched
-    L.sort_hist = o; o = align_up(o + 4 * (1u << kMaxSinglePassBits) * (size_t)L.sort_blocks);  // any digit width
+    // any digit width; also the direct emission's per-block tile counts (scan_blocks rows of up to 2048 tiles)
+    const size_t hist_rows = (size_t)(L.sort_blocks > L.scan_blocks ? L.sort_blocks : L.scan_blocks);
+    L.sort_hist = o; o = align_up(o + 4 * (1u << kMaxSinglePassBits) * hist_rows);
     L.sort_totals = o; o = align_up(o + 4 * (1u << kMaxSinglePassBits));
     L.scan_sums = o; o = align_up(o + 4 * (size_t)(L.scan_blocks + 1));
     L.emit_hist = o; o = align_up(o + 4 * (size_t)kXDigits * L.scan_blocks);  // two-level binning: columns per block
@@ -334,9 +336,22 @@ struct EmitArgs {
     // ids_only (a forward-only render's two-level binning): the lists carry the Gaussian id alone (u32 at
     // pairs_out / the point list) — the binning slot is only the backward's record address
     int ids_only = 0;
+    // direct emission (direct_emission: single-pass grids with packed rects): each scan block's instances
+    // per tile (k_scan_reduce), scanned in place over the blocks by launch_scan_reduce, the tile totals;
+    // k_emit_tiles writes the lists (pairs_out), the tile ranges and the forward's dispatch order
+    uint32_t* thist = nullptr;
+    uint32_t* ttotals = nullptr;
+    uint2* ranges = nullptr;
+    uint32_t* tile_order = nullptr;
 };
+// The direct emission for a gx x gy grid: at most 2048 tiles (one digit of the tile sort) and rects packed
+// in the depth-sort payload
+inline bool direct_emission_grid(int gx, int gy) {
+    return gx * gy <= (1 << kMaxSinglePassBits) && rect_packable(gx, gy);
+}
 void launch_scan_reduce(const EmitArgs& a, hipStream_t s);
 void launch_scan_emit(const EmitArgs& a, hipStream_t s);
+void launch_emit_tiles(const EmitArgs& a, hipStream_t s);
 // two-level binning after the instance count is known: column scan + k_scan_emit_x, the row pass
 // (pairs_out/tile_key -> point_pairs, per-tile counts), ranges from the counts
 void launch_emit_fused(const EmitArgs& a, hipStream_t s);

@@ -334,6 +334,49 @@ struct RangeOut {
 };
 constexpr int kTcCols = 4;
 
+// Block 0 of a single-pass tile sort (or of the direct emission): each thread holds the counts c of tiles
+// [tid * PER, tid * PER + PER), starting at list position `run`.  Writes the tile ranges
+// (identifyTileRanges, rasterizer_impl.cu:105-125; empty tiles keep (0, 0)) and, when tile_order is set, the
+// forward's dispatch order — tiles by list length, longest first (the former k_tile_order launch).  Every
+// thread of the block calls it (barriers).
+template <int PER>
+__device__ void write_tile_ranges(const uint32_t (&c)[PER], uint32_t run, int ntiles, uint2* __restrict__ ranges,
+                                  uint32_t* __restrict__ tile_order) {
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+        const int d = tid * PER + i;
+        if (ranges && d < ntiles) ranges[d] = c[i] ? make_uint2(run, run + c[i]) : make_uint2(0u, 0u);
+        run += c[i];
+    }
+    if (!tile_order) return;
+    constexpr int kClasses = 64;
+    __shared__ uint32_t s_cls[kClasses];
+    auto cls = [](uint32_t len) { return min(kClasses - 1, (int)(__log2f((float)len + 1.0f) * 3.0f)); };
+    if (tid < kClasses) s_cls[tid] = 0u;
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+        const int d = tid * PER + i;
+        if (d < ntiles) atomicAdd(&s_cls[cls(c[i])], 1u);
+    }
+    __syncthreads();
+    if (tid == 0) {  // start of each class, longest class first
+        uint32_t acc = 0;
+        for (int k = kClasses - 1; k >= 0; --k) {
+            const uint32_t m = s_cls[k];
+            s_cls[k] = acc;
+            acc += m;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+        const int d = tid * PER + i;
+        if (d < ntiles) tile_order[atomicAdd(&s_cls[cls(c[i])], 1u)] = (uint32_t)d;
+    }
+}
+
 // Value modes of the scatter: u32 values (IDV: the element index), or a packed
 // (Gaussian, slot) pair: built from the index and a Gaussian-per-slot array on
 // the first pass of the tile sort, then carried as one 8-byte value.
@@ -382,44 +425,17 @@ __global__ __launch_bounds__(256, GS_SCATTER_MINW) void k_radix_scatter(const KT
             s += loc[i];
         }
         uint32_t tot;
-        uint32_t run = block_exclusive_scan(s, lds4, tot);
+        const uint32_t run0 = block_exclusive_scan(s, lds4, tot);
+        uint32_t run = run0;
 #pragma unroll
         for (int i = 0; i < PER; ++i) {
             const int d = tid * PER + i;
             if (d < NDIG) dbase[d] = run;
-            // single-pass tile sort: the digit is the tile, so its run is the tile's range
-            // (identifyTileRanges, rasterizer_impl.cu:105-125; empty tiles keep (0, 0))
-            if (ro.ranges && blockIdx.x == 0 && d < NDIG)
-                ro.ranges[d] = loc[i] ? make_uint2(run, run + loc[i]) : make_uint2(0u, 0u);
             run += loc[i];
         }
-        if (ro.tile_order && blockIdx.x == 0) {  // (uniform per block: the barriers below are safe)
-            constexpr int kClasses = 64;
-            __shared__ uint32_t s_cls[kClasses];
-            auto cls = [](uint32_t len) { return min(kClasses - 1, (int)(__log2f((float)len + 1.0f) * 3.0f)); };
-            if (tid < kClasses) s_cls[tid] = 0u;
-            __syncthreads();
-#pragma unroll
-            for (int i = 0; i < PER; ++i) {
-                const int d = tid * PER + i;
-                if (d < ro.ntiles) atomicAdd(&s_cls[cls(loc[i])], 1u);
-            }
-            __syncthreads();
-            if (tid == 0) {  // start of each class, longest class first
-                uint32_t acc = 0;
-                for (int c = kClasses - 1; c >= 0; --c) {
-                    const uint32_t m = s_cls[c];
-                    s_cls[c] = acc;
-                    acc += m;
-                }
-            }
-            __syncthreads();
-#pragma unroll
-            for (int i = 0; i < PER; ++i) {
-                const int d = tid * PER + i;
-                if (d < ro.ntiles) ro.tile_order[atomicAdd(&s_cls[cls(loc[i])], 1u)] = (uint32_t)d;
-            }
-        }
+        // single-pass tile sort: the digit is the tile, so its run is the tile's range
+        if (blockIdx.x == 0 && (ro.ranges || ro.tile_order))  // (uniform per block: its barriers are safe)
+            write_tile_ranges<PER>(loc, run0, ro.ntiles, ro.ranges, ro.tile_order);
     }
     __syncthreads();
     // a capacity-sized grid (n_dev): blocks past the count leave after block 0 wrote the ranges
@@ -866,6 +882,54 @@ __global__ __launch_bounds__(256) void k_scan_reduce(EmitArgs a) {
         __syncthreads();
         if (threadIdx.x < kXDigits) a.xhist[(size_t)blockIdx.x * kXDigits + threadIdx.x] = h[threadIdx.x];
     }
+    if (a.thist) {
+        // direct emission: the block's instances per tile.  A rect adds +1 at (x0, y0), -1 at (x1, y0) and
+        // (x0, y1), +1 at (x1, y1) (corners past the grid dropped); prefix sums along x, then along y, give
+        // every tile's count: four LDS atomics per Gaussian whatever its size.  Rows are gx + 1 apart (odd:
+        // the row pass's lanes, one row each, hit distinct banks); each prefix runs in registers, 16 cells
+        // loaded at a time, one thread per row (gy <= 255), then one per column (gx <= 255).
+        constexpr int kCells = (1 << kMaxSinglePassBits) + kRectPackMax;  // gx * gy + gy cells at most
+        __shared__ int s_d[kCells];
+        const int gx = a.gx, gy = a.gy, nt = a.ntiles, gp = gx + 1;
+        for (int t = threadIdx.x; t < gy * gp; t += 256) s_d[t] = 0;
+        __syncthreads();
+#pragma unroll
+        for (int it = 0; it < kScanIPT; ++it) {
+            const uint32_t r = base + it * 256 + threadIdx.x;
+            const uint32_t q = v[it];
+            const int x0 = (int)(q & 0xFFu), y0 = (int)((q >> 8) & 0xFFu), x1 = (int)((q >> 16) & 0xFFu),
+                      y1 = (int)(q >> 24);
+            if (r < (uint32_t)a.P && x1 > x0 && y1 > y0) {
+                atomicAdd(&s_d[y0 * gp + x0], 1);
+                if (x1 < gx) atomicAdd(&s_d[y0 * gp + x1], -1);
+                if (y1 < gy) {
+                    atomicAdd(&s_d[y1 * gp + x0], -1);
+                    if (x1 < gx) atomicAdd(&s_d[y1 * gp + x1], 1);
+                }
+            }
+        }
+        __syncthreads();
+        auto prefix = [&](int first, int n, int stride) {  // inclusive prefix of s_d[first + i * stride], i < n
+            int run = 0;
+            for (int i0 = 0; i0 < n; i0 += 16) {
+                int c[16];
+#pragma unroll
+                for (int i = 0; i < 16; ++i) c[i] = i0 + i < n ? s_d[first + (i0 + i) * stride] : 0;
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    run += c[i];
+                    if (i0 + i < n) s_d[first + (i0 + i) * stride] = run;
+                }
+            }
+        };
+        if ((int)threadIdx.x < gy) prefix((int)threadIdx.x * gp, gx, 1);
+        __syncthreads();
+        if ((int)threadIdx.x < gx) prefix((int)threadIdx.x, gy, gp);
+        __syncthreads();
+        const int bm = a.scan_blocks <= kScanBmRows ? 1 : 0;
+        for (int t = threadIdx.x; t < nt; t += 256)
+            a.thist[hist_at(bm, blockIdx.x, (uint32_t)t, a.scan_blocks, nt)] = (uint32_t)s_d[(t / gx) * gp + t % gx];
+    }
 }
 
 // Emission in depth order: rounds of 256 Gaussians; a block scan of their
@@ -945,6 +1009,205 @@ __global__ __launch_bounds__(256) void k_scan_emit(EmitArgs a) {
         }
         base += total;
         __syncthreads();
+    }
+}
+
+// Direct emission (round 5; single-pass grids with packed rects, direct_emission_grid): the emission writes
+// every instance straight to its place in its tile's list, so the tile sort (histogram, digit scan, scatter
+// over the K emitted keys) is gone.  k_scan_reduce counted each block's instances per tile and
+// launch_scan_reduce scanned those counts over the blocks, so block b's instances of tile t start at
+// (instances of tiles < t) + (tile t's instances in blocks < b).  Inside the block, instances are taken in
+// slot order (= depth order: the block's Gaussians by rank, each one's tiles row-major) in batches of
+// kEtBatch: the owner of every instance is a prefix max over marks at the Gaussians' first slots, each
+// instance is ranked among the batch's instances of its tile with 64-lane ballots and per-wave counters
+// (waves own consecutive stretches of the batch, so ranks follow slot order: stable), staged in LDS in
+// tile-major order and stored with consecutive lanes on consecutive positions of each tile's run.  The lists
+// are therefore the single-pass tile sort's (Gaussian, slot) pairs, bit for bit.  Block 0 also writes the
+// tile ranges and the forward's dispatch order.  IDS: the Gaussian id alone (EmitArgs::ids_only).
+#ifndef GS_EMIT_TILE_EPT
+#define GS_EMIT_TILE_EPT 16  // instances per thread of a batch (A/B)
+#endif
+constexpr int kEtEPT = GS_EMIT_TILE_EPT, kEtBatch = 256 * kEtEPT;
+static_assert(kEtBatch <= 65536 && kScanTile < 65535, "u16 staged positions and owners");
+template <int BITS, bool IDS>
+__global__ __launch_bounds__(256) void k_emit_tiles(EmitArgs a) {
+    constexpr int NDIG = 1 << BITS, PER = NDIG >= 256 ? NDIG / 256 : 1;
+    constexpr int GPT = kScanTile / 256;  // consecutive Gaussians (depth ranks) per thread
+    __shared__ uint32_t lds4[4];
+    __shared__ uint32_t s_start[kScanTile];  // each Gaussian's first instance, relative to the block's first slot
+    __shared__ uint32_t s_rect[kScanTile];   // its packed tile rect
+    __shared__ uint16_t s_own[kEtBatch];     // the batch's owners (+1): marks at the Gaussians' starts, prefix max
+    __shared__ uint16_t cnt[4][NDIG];        // per-wave tile counters, then the staged runs' starts
+    // per tile: the global position of the block's next instance; while a batch is stored, its run's global
+    // position minus its staged position
+    __shared__ uint32_t s_pos[NDIG];
+    __shared__ uint16_t s_idx[kEtBatch];     // staged, tile-major: the instance's position in the batch
+    __shared__ uint32_t s_carry;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int nt = a.ntiles;
+    const uint32_t r_block = blockIdx.x * (uint32_t)kScanTile;
+    for (int i = tid; i < 4 * NDIG; i += 256) (&cnt[0][0])[i] = 0;
+    uint32_t base;  // the block's first slot (as k_scan_emit)
+    {
+        uint32_t part = 0;
+        for (uint32_t j = tid; j < blockIdx.x; j += 256) part += a.scan_sums[j];
+        block_exclusive_scan(part, lds4, base);
+    }
+    {   // each tile's first position for this block; block 0: the ranges and the dispatch order
+        const int bm = a.scan_blocks <= kScanBmRows ? 1 : 0;
+        uint32_t c[PER];
+        uint32_t s = 0;
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const int d = tid * PER + i;
+            c[i] = d < nt ? a.ttotals[d] : 0u;
+            s += c[i];
+        }
+        uint32_t all;
+        const uint32_t run0 = block_exclusive_scan(s, lds4, all);
+        uint32_t run = run0;
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const int d = tid * PER + i;
+            s_pos[d] = d < nt ? run + a.thist[hist_at(bm, blockIdx.x, (uint32_t)d, a.scan_blocks, nt)] : 0u;
+            run += c[i];
+        }
+        if (blockIdx.x == 0) write_tile_ranges<PER>(c, run0, nt, a.ranges, a.tile_order);
+    }
+    // the block's Gaussians, GPT consecutive ranks per thread: first slots, rects
+    const uint32_t r0 = r_block + (uint32_t)(tid * GPT);
+    uint32_t gst[GPT], gc[GPT];
+    uint32_t total;
+    {
+        uint2 gr[GPT];
+#pragma unroll
+        for (int i = 0; i < GPT; ++i) gr[i] = r0 + i < (uint32_t)a.P ? a.order[r0 + i] : make_uint2(0u, 0u);
+        uint32_t s = 0;
+#pragma unroll
+        for (int i = 0; i < GPT; ++i) {
+            gc[i] = rect_count(gr[i].x, 1);
+            s += gc[i];
+        }
+        uint32_t off = block_exclusive_scan(s, lds4, total);
+#pragma unroll
+        for (int i = 0; i < GPT; ++i) {
+            gst[i] = off;
+            s_start[tid * GPT + i] = off;
+            s_rect[tid * GPT + i] = gr[i].x;
+            if (gc[i]) a.first_slot[gr[i].y] = base + off;
+            off += gc[i];
+        }
+    }
+    if (tid == 0) s_carry = 0u;
+    // instance j of the block (relative to its first slot) owned by block Gaussian o: its tile
+    auto tile_of = [&](uint32_t j, int o) {
+        const uint32_t q = s_rect[o];
+        const uint32_t x0 = q & 0xFFu, y0 = (q >> 8) & 0xFFu, wd = ((q >> 16) & 0xFFu) - x0;
+        const uint32_t k = j - s_start[o];
+        const uint32_t ky = (uint32_t)(((float)k + 0.5f) / (float)wd);  // exact: k < 2^20
+        return (y0 + ky) * (uint32_t)a.gx + x0 + (k - ky * wd);
+    };
+    for (uint32_t j0 = 0; j0 < total; j0 += (uint32_t)kEtBatch) {
+        const uint32_t nb = total - j0 < (uint32_t)kEtBatch ? total - j0 : (uint32_t)kEtBatch;
+        // owner of every instance of the batch: marks at the starts of the Gaussians starting in it (starts of
+        // Gaussians with instances are distinct), prefix max, carried in from the previous batch
+#pragma unroll
+        for (int i = 0; i < kEtEPT; ++i) s_own[tid * kEtEPT + i] = 0;
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < GPT; ++i)
+            if (gc[i] && gst[i] >= j0 && gst[i] < j0 + nb) s_own[gst[i] - j0] = (uint16_t)(tid * GPT + i + 1);
+        const uint32_t carry = s_carry;
+        __syncthreads();
+        {
+            uint32_t run = 0;
+#pragma unroll
+            for (int i = 0; i < kEtEPT; ++i) run = max(run, (uint32_t)s_own[tid * kEtEPT + i]);
+            run = max(carry, block_exclusive_max(run, lds4));
+#pragma unroll
+            for (int i = 0; i < kEtEPT; ++i) {
+                run = max(run, (uint32_t)s_own[tid * kEtEPT + i]);
+                s_own[tid * kEtEPT + i] = (uint16_t)run;
+            }
+        }
+        __syncthreads();
+        uint32_t dg[kEtEPT], loc[kEtEPT];
+#pragma unroll
+        for (int e = 0; e < kEtEPT; ++e) {
+            const uint32_t jj = (uint32_t)(w * 64 * kEtEPT + e * 64 + lane);
+            const bool valid = jj < nb;
+            const uint64_t vm = __ballot(valid);
+            dg[e] = 0u;
+            loc[e] = 0u;
+            if (vm != 0) {  // (wave-uniform; no break: the loop stays unrolled)
+                const uint32_t d = valid ? tile_of(j0 + jj, (int)s_own[jj] - 1) : 0u;
+                const uint32_t slot = base + j0 + jj;
+                if (valid && a.rec_flags32 && slot < a.cap) a.rec_flags32[slot] = 0u;  // (slot order: coalesced)
+                const uint64_t peers = match_digit<BITS>(d, vm);
+                const uint32_t rank = (uint32_t)__popcll(peers & lanemask_lt());
+                const uint32_t old = cnt[w][d];
+                dg[e] = d;
+                loc[e] = old + rank;
+                if (valid && rank == 0) cnt[w][d] = (uint16_t)(old + (uint32_t)__popcll(peers));
+            }
+        }
+        __syncthreads();
+        {   // the batch's tile runs (wave-major inside a tile) and their global bases
+            uint32_t t4[PER][4];
+            uint32_t s = 0;
+#pragma unroll
+            for (int i = 0; i < PER; ++i) {
+                const int d = tid * PER + i;
+#pragma unroll
+                for (int v = 0; v < 4; ++v) t4[i][v] = cnt[v][d];
+                s += t4[i][0] + t4[i][1] + t4[i][2] + t4[i][3];
+            }
+            uint32_t all;
+            uint32_t run = block_exclusive_scan(s, lds4, all);
+#pragma unroll
+            for (int i = 0; i < PER; ++i) {
+                const int d = tid * PER + i;
+                cnt[0][d] = (uint16_t)run;
+                cnt[1][d] = (uint16_t)(run + t4[i][0]);
+                cnt[2][d] = (uint16_t)(run + t4[i][0] + t4[i][1]);
+                cnt[3][d] = (uint16_t)(run + t4[i][0] + t4[i][1] + t4[i][2]);
+                s_pos[d] -= run;
+                run += t4[i][0] + t4[i][1] + t4[i][2] + t4[i][3];
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int e = 0; e < kEtEPT; ++e) {
+            const uint32_t jj = (uint32_t)(w * 64 * kEtEPT + e * 64 + lane);
+            if (jj < nb) s_idx[cnt[w][dg[e]] + loc[e]] = (uint16_t)jj;
+        }
+        __syncthreads();
+        // every staged instance's loads issued before the stores (fixed trip count, unrolled)
+#pragma unroll
+        for (int e = 0; e < kEtEPT; ++e) {
+            const uint32_t i = (uint32_t)(e * 256 + tid);
+            if (i < nb) {
+                const uint32_t jj = s_idx[i];
+                const int o = (int)s_own[jj] - 1;
+                const uint32_t pos = s_pos[tile_of(j0 + jj, o)] + i;
+                const uint32_t g = a.order[r_block + (uint32_t)o].y;  // (the block's own entries: L2)
+                if (pos < a.cap) {  // (speculative capacity: gs_views_check reports an overflow)
+                    if constexpr (IDS) reinterpret_cast<uint32_t*>(a.pairs_out)[pos] = g;
+                    else a.pairs_out[pos] = make_uint2(g, base + j0 + jj);
+                }
+            }
+        }
+        __syncthreads();
+        // the next batch's positions: each tile's run ends where the next tile's begins (the batch's end
+        // for the last digit)
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const int d = tid * PER + i;
+            s_pos[d] += d + 1 < NDIG ? (uint32_t)cnt[0][d + 1] : nb;
+        }
+        if (tid == 0) s_carry = s_own[nb - 1];
+        __syncthreads();
+        for (int i = tid; i < 4 * NDIG; i += 256) (&cnt[0][0])[i] = 0;
     }
 }
 
@@ -1220,6 +1483,26 @@ void launch_row_pass(const EmitArgs& a, uint32_t K, uint2* point_pairs, uint32_t
 void launch_scan_reduce(const EmitArgs& a, hipStream_t s) {
     if (a.P <= 0) return;
     hipLaunchKernelGGL(k_scan_reduce, dim3(a.scan_blocks), dim3(256), 0, s, a);
+    if (a.thist) {  // direct emission: each block's first position per tile, the tile totals
+        if (a.scan_blocks <= kScanBmRows)
+            hipLaunchKernelGGL(k_radix_digit_scan, dim3(div_up(a.ntiles, kScanDigits)), dim3(kScanThreads), 0, s, a.thist,
+                               a.scan_blocks, a.ntiles, a.ttotals, (const uint32_t*)nullptr, 0u, 1);
+        else
+            hipLaunchKernelGGL(k_radix_digit_scan_dm, dim3(a.ntiles), dim3(256), 0, s, a.thist, a.scan_blocks, a.ttotals,
+                               (const uint32_t*)nullptr, 0u, 1);
+    }
+}
+
+void launch_emit_tiles(const EmitArgs& a, hipStream_t s) {
+    if (a.P <= 0) return;
+    const int bits = ceil_log2((uint32_t)(a.ntiles > 1 ? a.ntiles : 2));
+#define GS_ET(B)                                                                                       \
+    if (a.ids_only) hipLaunchKernelGGL((k_emit_tiles<B, true>), dim3(a.scan_blocks), dim3(256), 0, s, a); \
+    else hipLaunchKernelGGL((k_emit_tiles<B, false>), dim3(a.scan_blocks), dim3(256), 0, s, a)
+    if (bits <= 8) { GS_ET(8); }
+    else if (bits <= 10) { GS_ET(10); }
+    else { GS_ET(11); }
+#undef GS_ET
 }
 
 void launch_scan_emit(const EmitArgs& a, hipStream_t s) {

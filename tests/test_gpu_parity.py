@@ -679,17 +679,23 @@ def test_forced_32bit_depth_keys_match_30bit_path(cuda_device, monkeypatch):
         np.testing.assert_array_equal(forced[k], base[k], err_msg=k)
 
 
-@pytest.mark.parametrize("P,W,H", [(3_000, 1920, 1080), (300_000, 1920, 1080), (200_000, 2048, 1040),
-                                   (300_000, 1280, 720), (200_000, 1024, 768)])
-def test_two_level_binning_matches_two_pass_sort(cuda_device, monkeypatch, P, W, H):
+@pytest.mark.parametrize("P,W,H,scale", [(3_000, 1920, 1080, 0.02), (300_000, 1920, 1080, 0.02),
+                                         (200_000, 2048, 1040, 0.02), (300_000, 1280, 720, 0.02),
+                                         (200_000, 1024, 768, 0.02), (300_000, 512, 512, 0.02),
+                                         (40_000, 160, 120, 0.02), (100_000, 720, 720, 0.02),
+                                         (3_000, 512, 512, 0.15)])
+def test_two_level_binning_matches_two_pass_sort(cuda_device, monkeypatch, P, W, H, scale):
     """Grids over 2048 tiles (c4: 120 x 68) bin in two levels — the emission writes the instances in
-    tile-column order, one row pass follows, ranges come from per-tile counts; DGE_AMD_TILE_SORT=2pass
-    runs the emission + two full tile-sort passes + k_ranges instead.  Lists, ranges, the image and
-    every gradient are bitwise the same (3k Gaussians: sort blocks spanning many tile columns, whose
-    counts go through the global atomics; 2048 x 1040: the widest grid, 128 columns; 1280 x 720 and
-    1024 x 768: 2049..4096 tiles, whose two-pass plan has 6-bit digits while the two-level tables hold
-    128 — round 5 found those tables sized for 64, and fixed it)."""
-    a = scene_arrays(P, seed=6, radius=2.0, scale=0.02)
+    tile-column order, one row pass follows, ranges come from per-tile counts; grids of at most 2048 tiles
+    (c2: 32 x 32) bin by the direct emission — every instance written straight to its place in its tile's
+    list; DGE_AMD_TILE_SORT=2pass runs the emission + the radix tile sort (+ k_ranges) instead.  Lists,
+    ranges, the image and every gradient are bitwise the same (3k Gaussians: sort blocks spanning many tile
+    columns, whose counts go through the global atomics; 2048 x 1040: the widest grid, 128 columns; 1280 x 720
+    and 1024 x 768: 2049..4096 tiles, whose two-pass plan has 6-bit digits while the two-level tables hold
+    128 — round 5 found those tables sized for 64, and fixed it; 512 x 512, 160 x 120 and 720 x 720: the
+    direct emission's 10-, 8- and 11-bit tile digits; 3k large Gaussians at 512 x 512: blocks whose instances
+    span several emission batches)."""
+    a = scene_arrays(P, seed=6, radius=2.0, scale=scale)
     g = np.random.default_rng(8).standard_normal((3, H, W)).astype(np.float32) * 1e-3
     s = camera_settings(W, H, device="cuda")
     fused = run_gpu(s, g, **_sh_kw(a))
@@ -698,6 +704,22 @@ def test_two_level_binning_matches_two_pass_sort(cuda_device, monkeypatch, P, W,
     assert fused["num_rendered"] == ref["num_rendered"] > 0
     for k in ("ranges", "point_list", "n_contrib", "color", "final_T") + tuple(GRAD_NAMES):
         np.testing.assert_array_equal(fused[k], ref[k], err_msg=k)
+
+
+@pytest.mark.parametrize("W,H", [(4128, 48), (4128, 320)], ids=["single_pass", "two_pass"])
+def test_wide_grid_unpacked_rects_vs_oracle(cuda_device, oracle, W, H):
+    """Grids more than 255 tiles wide carry tiles_touched instead of a packed rect through the depth sort
+    (the emission gathers the rect): 258 x 3 tiles bin by the emission + a single-pass radix tile sort,
+    258 x 20 by the emission + two tile-sort passes + k_ranges (too wide for the two-level binning).
+    Every forward output equals the oracle's."""
+    a = scene_arrays(20_000, seed=12, radius=2.0, scale=0.03)
+    kw = _sh_kw(a)
+    g = np.random.default_rng(2).standard_normal((3, H, W)).astype(np.float32) * 1e-3
+    ref = run_oracle(oracle, camera_settings(W, H), g, **kw)
+    got = run_gpu(camera_settings(W, H, device="cuda"), g, **kw)
+    assert got["num_rendered"] == ref["num_rendered"] > 0
+    compare_forward(got, ref, label=f"wide {W}x{H}")
+    compare_grads(got, ref, O=oracle, label=f"wide {W}x{H}")
 
 
 
