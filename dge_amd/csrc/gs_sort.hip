@@ -339,14 +339,17 @@ constexpr int kTcCols = 4;
 // (identifyTileRanges, rasterizer_impl.cu:105-125; empty tiles keep (0, 0)) and, when tile_order is set, the
 // forward's dispatch order — tiles by list length, longest first (the former k_tile_order launch).  Every
 // thread of the block calls it (barriers).
+// cap: the binning capacity of a speculative forward (the direct emission's counts are the full instance
+// counts): ranges are clamped to it, so an overflowed binning, redone later, is never read past its end
 template <int PER>
 __device__ void write_tile_ranges(const uint32_t (&c)[PER], uint32_t run, int ntiles, uint2* __restrict__ ranges,
-                                  uint32_t* __restrict__ tile_order) {
+                                  uint32_t* __restrict__ tile_order, uint32_t cap = 0xFFFFFFFFu) {
     const int tid = threadIdx.x;
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
         const int d = tid * PER + i;
-        if (ranges && d < ntiles) ranges[d] = c[i] ? make_uint2(run, run + c[i]) : make_uint2(0u, 0u);
+        if (ranges && d < ntiles)
+            ranges[d] = c[i] ? make_uint2(min(run, cap), min(run + c[i], cap)) : make_uint2(0u, 0u);
         run += c[i];
     }
     if (!tile_order) return;
@@ -1072,7 +1075,7 @@ __global__ __launch_bounds__(256) void k_emit_tiles(EmitArgs a) {
             s_pos[d] = d < nt ? run + a.thist[hist_at(bm, blockIdx.x, (uint32_t)d, a.scan_blocks, nt)] : 0u;
             run += c[i];
         }
-        if (blockIdx.x == 0) write_tile_ranges<PER>(c, run0, nt, a.ranges, a.tile_order);
+        if (blockIdx.x == 0) write_tile_ranges<PER>(c, run0, nt, a.ranges, a.tile_order, a.cap);
     }
     // the block's Gaussians, GPT consecutive ranks per thread: first slots, rects
     const uint32_t r0 = r_block + (uint32_t)(tid * GPT);
@@ -1191,9 +1194,12 @@ __global__ __launch_bounds__(256) void k_emit_tiles(EmitArgs a) {
                 const int o = (int)s_own[jj] - 1;
                 const uint32_t pos = s_pos[tile_of(j0 + jj, o)] + i;
                 const uint32_t g = a.order[r_block + (uint32_t)o].y;  // (the block's own entries: L2)
-                if (pos < a.cap) {  // (speculative capacity: gs_views_check reports an overflow)
+                // (speculative capacity: gs_views_check reports an overflow; an overflowed binning is redone,
+                // but until then its lists must stay inside the buffer: the ranges are clamped to the
+                // capacity, and so is every slot — the backward's record address)
+                if (pos < a.cap) {
                     if constexpr (IDS) reinterpret_cast<uint32_t*>(a.pairs_out)[pos] = g;
-                    else a.pairs_out[pos] = make_uint2(g, base + j0 + jj);
+                    else a.pairs_out[pos] = make_uint2(g, min(base + j0 + jj, a.cap - 1u));
                 }
             }
         }
