@@ -1390,6 +1390,8 @@ int gs_views_backward(gs_views* h, const float* const* dL_dpix, const gs_grads* 
                 hipStream_t sv = (hipStream_t)streams[v];
                 int rc = replay_view(&f.s, &f.gp, (int)h->layout[v], f.geom, h->bin[v], f.img, dL_dpix[v], sv);
                 if (rc) return rc;
+                // (before view 0's replay instead, beside the others' replays: 2861-2877 vs 2882-2898
+                // renders/s, profiles/r05/ab_scan_shape_live_first.txt)
                 if (split && v == 0) {
                     { StageScope sc(ST_GAUSS_LIVE, s0); launch_gauss_live_views(ga, h->n, s0); }
                     GS_LAUNCHED("gaussian live set (views)");

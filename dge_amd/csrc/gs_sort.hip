@@ -193,14 +193,21 @@ __global__ __launch_bounds__(256) void k_radix_hist(const KT* __restrict__ keys,
 }
 
 // Exclusive scan of every digit's column hist[0..nb)[d] in place, totals[d] =
-// digit count.  One 1024-thread workgroup per 16 digits: thread (row group g,
-// digit dl) sums rows [g*per, (g+1)*per) of its digit (a wave load covers 4 rows
-// x 64 B), the 64 row-group sums are scanned in LDS, then the rows are
-// rewritten.  (c2: 880 tile-sort rows -> 14 per thread.)
+// digit count.  One workgroup per kScanDigits digits: thread (row group g,
+// digit dl) sums rows [g*per, (g+1)*per) of its digit (a wave load covers 8 rows
+// x 32 B), the kScanGroups row-group sums are scanned in LDS, then the rows are
+// rewritten.  (c2: the direct emission's 977 block rows -> 31 per thread.)
+// Digits per digit-scan workgroup x row groups = its threads.  256-thread workgroups (8 x 32) find room on
+// CUs busy with the other streams' blends, where 1024-thread ones waited up to 70 us for a CU to drain
+// (3-stream trace): c2 2883-2898 -> 2943-2945 renders/s (one-stream scan stage 18.0 -> 20.7 us); 4 x 64
+// (16-B row segments) measured 2882 (profiles/r05/ab_scan_shape_live_first.txt)
 #ifndef GS_SCAN_DIGITS
-#define GS_SCAN_DIGITS 16  // digits per digit-scan workgroup (x 64 row groups = its threads; A/B: -DGS_SCAN_DIGITS=4)
+#define GS_SCAN_DIGITS 8
 #endif
-constexpr int kScanDigits = GS_SCAN_DIGITS, kScanGroups = 64, kScanRegs = 32;
+#ifndef GS_SCAN_GROUPS
+#define GS_SCAN_GROUPS 32
+#endif
+constexpr int kScanDigits = GS_SCAN_DIGITS, kScanGroups = GS_SCAN_GROUPS, kScanRegs = 32;
 constexpr int kScanThreads = kScanDigits * kScanGroups;
 constexpr int kScanBmRows = kScanGroups * kScanRegs;  // block-major tables up to this many blocks
 __global__ __launch_bounds__(kScanThreads) void k_radix_digit_scan(uint32_t* __restrict__ hist, int nb, int ndig,
@@ -331,6 +338,9 @@ struct RangeOut {
     // counted in LDS for the block's first kTcCols columns, global atomics beyond
     uint32_t* tile_count = nullptr;
     int gx = 0;
+    // the MSD depth pass (DM): the culled bucket's values (already final: index order, nothing to sort)
+    // go straight to the sorted output instead of through k_depth_bucket_sort
+    uint2* culled_out = nullptr;
 };
 constexpr int kTcCols = 4;
 
@@ -539,11 +549,14 @@ __global__ __launch_bounds__(256, GS_SCATTER_MINW) void k_radix_scatter(const KT
     const int nvalid = n - b0 < (uint32_t)(256 * IPT) ? (int)(n - b0) : 256 * IPT;
     for (int i = tid; i < nvalid; i += 256) {
         const uint32_t k = s_key[i];
-        const uint32_t pos = dbase[WK ? digit(k) : k] + (uint32_t)i;
+        const uint32_t dd = WK ? digit(k) : k;
+        const uint32_t pos = dbase[dd] + (uint32_t)i;
         if (WK) keys_out[pos] = k;
         if constexpr (VM == kValPairFirst) {
             const uint32_t e = b0 + (uint32_t)s_val[i];
-            vals_out[pos] = make_uint2(gauss_by_slot[e], e);
+            V* dst = vals_out;
+            if constexpr (DM) dst = dd == (uint32_t)kMsdCulled && ro.culled_out ? ro.culled_out : vals_out;
+            dst[pos] = make_uint2(gauss_by_slot[e], e);
         } else {
             vals_out[pos] = s_val[i];
         }
@@ -721,7 +734,8 @@ __global__ __launch_bounds__(256) void k_depth_bucket_sort(uint32_t* __restrict_
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const MsdParams m = msd_params(bias_not);
     const int passes = ((int)m.s + kLocalBits - 1) / kLocalBits;
-    if (blockIdx.x == (uint32_t)kMsdCulled || passes == 0 || n == 1) {
+    if (blockIdx.x == (uint32_t)kMsdCulled) return;  // (the MSD scatter wrote the culled bucket's values in place)
+    if (passes == 0 || n == 1) {
         for (uint32_t i = tid; i < n; i += 256) vals_a[r.x + i] = vals_b[r.x + i];
         return;
     }
@@ -833,7 +847,7 @@ int depth_sort_msd(uint32_t* key0, uint32_t* key1, uint2* pair0, uint2* pair1, c
     // (block 0 writes every bucket's range, as a single-pass tile sort writes the tile ranges)
     hipLaunchKernelGGL((k_radix_scatter<kMsdBits, IPT, true, kValPairFirst, true, false, uint32_t, true>), dim3(nblocks),
                        dim3(256), 0, s, key0, nullptr, key1, pair1, rect, n, 0, hist, totals, nblocks, bm,
-                       RangeOut{bucket_ranges, nullptr, NDIG}, bias_not, (const uint32_t*)nullptr);
+                       RangeOut{bucket_ranges, nullptr, NDIG, nullptr, 0, pair0}, bias_not, (const uint32_t*)nullptr);
     hipLaunchKernelGGL(k_depth_bucket_sort, dim3(NDIG), dim3(256), 0, s, key1, pair1, key0, pair0, bucket_ranges,
                        bias_not);
     return 0;  // (the (rect, Gaussian) values in depth order are in pair0)
