@@ -291,13 +291,15 @@ def apply_weights(background, means3D, weights, opacity, scales, rotations, scal
 # (gs_rasterize_forward_ex / gs_rasterize_backward_ex)
 # ---------------------------------------------------------------------------
 def _params(P, xyz, f_dc, f_rest, colors, raw_opacity, raw_scaling, raw_rotation, index=None, visible=None,
-            forward_only=False):
+            forward_only=False, aux_mask=None):
     """gs_params of the raw-parameter path; `index` (int32 [P], ascending): the localize subset's rows
     (gathered in-kernel); fp16 features are read as such (sh_half); forward_only: no backward will follow
-    (the kernels skip the backward's scratch)."""
+    (the kernels skip the backward's scratch); aux_mask: a uint8 tensor over the parameter rows whose 0/1
+    the blend composites beside the colour (gs_params.aux_mask, served to render_recolor)."""
     g = N.GsParams()
     g.P = P
     g.forward_only = 1 if forward_only else 0
+    g.aux_mask = _ptr(aux_mask)
     g.index = _ptr(index)
     g.sh_half = 1 if f_dc is not None and f_dc.dtype == torch.float16 else 0
     have_sh = f_dc is not None and f_dc.numel() != 0
@@ -350,7 +352,7 @@ class Prepared:
 def rasterize_gaussians_fused_begin(background, xyz, f_dc, f_rest, colors, raw_opacity, raw_scaling, raw_rotation,
                                     scale_modifier, viewmatrix, projmatrix, tan_fovx, tan_fovy, image_height,
                                     image_width, degree, campos, prefiltered, debug, index=None, visible=None,
-                                    forward_only=False):
+                                    forward_only=False, aux_mask=None):
     """First half of rasterize_gaussians_fused (gs_rasterize_forward_begin): enqueues the preprocess, the
     depth sort and the instance scan on the current stream without waiting; returns a Prepared for
     rasterize_gaussians_fused_end.  Rendering several views, begin them all first, then end each: the
@@ -368,11 +370,16 @@ def rasterize_gaussians_fused_begin(background, xyz, f_dc, f_rest, colors, raw_o
         raw_opacity, raw_scaling = _f32(raw_opacity, "opacity"), _f32(raw_scaling, "scaling")
         raw_rotation = _f32(raw_rotation, "rotation")
         radii = torch.empty((P,), dtype=torch.int32, device=dev)
+        if aux_mask is not None:
+            if (aux_mask.dtype not in (torch.bool, torch.uint8) or aux_mask.device != dev or aux_mask.dim() != 1
+                    or aux_mask.numel() != xyz.size(0)):
+                raise ValueError("aux_mask must be a bool or uint8 tensor over the parameter rows, on the device")
+            aux_mask = aux_mask.contiguous().view(torch.uint8)
         g = _params(P, xyz, f_dc, f_rest, colors, raw_opacity, raw_scaling, raw_rotation, index, visible,
-                    forward_only)
+                    forward_only, aux_mask)
         s, keep = _settings(background, viewmatrix, projmatrix, campos, tan_fovx, tan_fovy, H, W, degree,
                             scale_modifier, prefiltered, debug)
-        keep += [xyz, f_dc, f_rest, colors, raw_opacity, raw_scaling, raw_rotation, index, visible]
+        keep += [xyz, f_dc, f_rest, colors, raw_opacity, raw_scaling, raw_rotation, index, visible, aux_mask]
         alloc = _Allocator(dev)
         h = ctypes.c_void_p(None)
         rc = N.lib().gs_rasterize_forward_begin(ctypes.byref(s), ctypes.byref(g), _ptr(radii), alloc.fn, None,
@@ -402,11 +409,13 @@ def rasterize_gaussians_fused_end(prep):
 
 
 def render_recolor(background, colors, viewmatrix, projmatrix, campos, tan_fovx, tan_fovy, image_height, image_width,
-                   degree, scale_modifier, prefiltered, P, num_rendered, geomBuffer, binningBuffer, imgBuffer):
+                   degree, scale_modifier, prefiltered, P, num_rendered, geomBuffer, binningBuffer, imgBuffer,
+                   src_aux_mask=None):
     """gs_render_recolor: the blend of a finished forward (its geometry/binning/image buffers, num_rendered
     instances, with backward bookkeeping) again with colours `colors` [P,3] in place of its own -> (color
     [3,H,W], depth [1,H,W]), bit-identical to a full forward with colors_precomp = colors, on the current
-    stream (which must be ordered after that forward)."""
+    stream (which must be ordered after that forward).  src_aux_mask: the aux_mask that forward composited
+    (unchanged since): colours equal to its 0/1 grey are then served from that forward's sums."""
     dev = colors.device
     H, W = int(image_height), int(image_width)
     with torch.cuda.device(dev):
@@ -418,9 +427,12 @@ def render_recolor(background, colors, viewmatrix, projmatrix, campos, tan_fovx,
         out_color = torch.empty((3, H, W), dtype=torch.float32, device=dev)
         out_depth = torch.empty((1, H, W), dtype=torch.float32, device=dev)
         img_out = torch.empty(int(N.lib().gs_image_buffer_size(W, H)), dtype=torch.uint8, device=dev)
+        src = None if src_aux_mask is None else src_aux_mask.contiguous().view(torch.uint8)
+        if src is not None and src.numel() < P:
+            raise RuntimeError("src_aux_mask must cover the P Gaussians")
         rc = N.lib().gs_render_recolor(ctypes.byref(s), int(P), int(num_rendered), _ptr(geomBuffer),
                                        _ptr(binningBuffer), _ptr(imgBuffer), _ptr(colors), _ptr(img_out),
-                                       _ptr(out_color), _ptr(out_depth), _stream(dev))
+                                       _ptr(out_color), _ptr(out_depth), _ptr(src), _stream(dev))
         N.check(rc, "render_recolor")
         del keep
         return out_color, out_depth

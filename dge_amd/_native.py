@@ -15,7 +15,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("DGE_AMD_LIB") or os.path.join(_HERE, "lib", "libgs_raster.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "gs_raster.h")
 
-ABI_VERSION = 17  # GS_RASTER_ABI_VERSION of include/gs_raster.h this binding is written against
+ABI_VERSION = 18  # GS_RASTER_ABI_VERSION of include/gs_raster.h this binding is written against
 
 GS_OK = 0
 GS_ERR_INVALID_ARG = 1
@@ -71,6 +71,7 @@ class GsParams(ctypes.Structure):
         ("index", ctypes.c_void_p),
         ("visible_out", ctypes.c_void_p),
         ("forward_only", ctypes.c_int),
+        ("aux_mask", ctypes.c_void_p),
     ]
 
 
@@ -191,7 +192,7 @@ SIGNATURES = {
                                            ctypes.c_longlong, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "gs_blend_exp": (ctypes.c_int, [ctypes.c_longlong, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "gs_activate_params": (ctypes.c_int, [ctypes.c_int] + [ctypes.c_void_p] * 7),
-    "gs_render_recolor": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int] + [ctypes.c_void_p] * 8),
+    "gs_render_recolor": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int] + [ctypes.c_void_p] * 9),
     "gs_last_error": (ctypes.c_char_p, []),
     "gs_abi_version": (ctypes.c_int, []),
 }

@@ -270,6 +270,7 @@ gs_params make_params(int P, int M, const float* means3D, const float* shs, cons
     g.index = nullptr;
     g.visible_out = nullptr;
     g.forward_only = 0;
+    g.aux_mask = nullptr;
     return g;
 }
 
@@ -363,6 +364,7 @@ int bin_prepare_in(FwdState& f, int copy_colors, void* geom, void* img, hipStrea
     pa.rect_packed = rect_packable(g.gx, g.gy) ? 1 : 0;
     pa.counters = counters;
     pa.touched = at<uint8_t>(geom, gl.touched);
+    pa.aux_mask = gp.forward_only ? nullptr : gp.aux_mask;
     return GS_OK;
 }
 
@@ -635,6 +637,8 @@ int render_launch(FwdState& f, void* bin, uint32_t K_layout, int order_ready, fl
     ra.out_depth = out_depth;
     ra.touched = at<uint8_t>(geom, gl.touched);
     ra.diag = diag_buffer(0, kDiagWords * (size_t)g.tiles * 4);
+    // (gs_params.aux_mask: the grey composited beside the colour, for a later gs_render_recolor)
+    ra.aux_out = f.gp.aux_mask && !f.gp.forward_only ? at<float2>(img, il.aux) : nullptr;
     { StageScope sc(ST_RENDER_FWD, stream); launch_render_forward(ra, stream); }
     GS_LAUNCHED("render");
     return GS_OK;
@@ -969,7 +973,7 @@ void gs_rasterize_forward_release(gs_forward_state* state) { delete state; }
 
 int gs_render_recolor(const gs_settings* s, int P, int num_rendered, const void* geom, const void* binning,
                       const void* img, const float* colors, void* img_out, float* out_color, float* out_depth,
-                      gs_stream_t stream_) {
+                      const uint8_t* src_aux_mask, gs_stream_t stream_) {
     try {
         hipStream_t stream = (hipStream_t)stream_;
         if (!s || P < 0 || num_rendered < 0 || !geom || !img || !img_out || !out_color || !out_depth ||
@@ -1010,6 +1014,16 @@ int gs_render_recolor(const gs_settings* s, int P, int num_rendered, const void*
         ra.touched = nullptr;
         ra.diag = nullptr;
         ra.colors = colors;
+        if (src_aux_mask && !empty) {
+            // the colours against the source forward's aux grey, on the device (a flag word of img_out's
+            // counters, zeroed above); equal: the blend composes the image from that forward's sums
+            uint32_t* flag = at<uint32_t>(img_out, il.counters);
+            launch_aux_match(P, colors, src_aux_mask, flag, stream);
+            GS_LAUNCHED("recolor aux check");
+            ra.aux_match = flag;
+            ra.aux_src = at<float2>(const_cast<void*>(img), il.aux);
+            ra.final_T_src = at<float>(const_cast<void*>(img), il.final_T);
+        }
         { StageScope sc(ST_RENDER_FWD, stream); launch_render_forward(ra, stream); }
         GS_LAUNCHED("recolor render");
         return GS_OK;

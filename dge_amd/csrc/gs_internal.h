@@ -89,7 +89,7 @@ inline TileSortPlan tile_sort_plan(int num_tiles) {
 // 2D mean, conic + opacity, colour + depth (forward.cu:251-255 outputs).
 struct alignas(64) Splat {
     float2 xy;
-    float2 pad0;
+    float2 aux;   // x: gs_params.aux_mask as 0/1 (the grey value the blend composites beside the colour)
     float4 co;    // conic (a, b, c) + opacity
     float4 rgbd;  // colour + view depth
     float4 pad1;
@@ -166,7 +166,7 @@ __host__ __device__ inline uint32_t used_base(uint32_t range_x, int tile) { retu
 __host__ __device__ inline size_t used_words(size_t K, int tiles) { return 4 * (K / 64 + (size_t)tiles + 2); }
 
 struct ImgLayout {
-    size_t final_T, n_contrib, tile_order, counters, ranges, tile_last, quad_last, bwd_count, total;
+    size_t final_T, n_contrib, tile_order, counters, ranges, tile_last, quad_last, bwd_count, aux, total;
     // counters: kCounterSlots slots of kCounterStride u32: [0] instances, [1] max depth key,
     // [2] ~min depth key (summed / maxed over the slots by the host); slot 0 [3]: prefiltered error
 };
@@ -184,6 +184,7 @@ inline ImgLayout img_layout(int W, int H) {
     L.quad_last = o; o = align_up(o + 16 * tiles);
     L.bwd_count = o; o = align_up(o + 4 * (size_t)item_count_at(kItemClasses));  // [0..3] the per-tile variant's;
                                                                                  // [item_count_at(c)] class c items
+    L.aux = o; o = align_up(o + 8 * n);  // float2 per pixel: the aux_mask grey sum (before bg), depth
     L.total = o;
     return L;
 }
@@ -266,6 +267,7 @@ struct PreprocessArgs {
     int rect_packed;
     uint32_t* counters;  // kCounterSlots x kCounterStride (ImgLayout)
     uint8_t* touched;    // zeroed here: k_render_fwd sets the bytes of Gaussians some pixel blends
+    const uint8_t* aux_mask = nullptr;  // gs_params.aux_mask: 0/1 into the Splat's aux slot
 };
 void launch_preprocess(const PreprocessArgs& a, hipStream_t s);
 void launch_depth_keys32(int P, const uint32_t* rect, const Splat* splat, uint32_t* key, hipStream_t s);
@@ -397,8 +399,16 @@ struct RenderArgs {
     uint64_t* diag;       // optional [tiles*4][kDiagWords] (see diag_buffer)
     int bwd = 1;          // 0: a forward-only render (gs_params.forward_only): no backward bookkeeping
     const float* colors = nullptr;  // forward-only: blend these [P,3] colours instead of the Splats' (recolor)
+    float2* aux_out = nullptr;      // (bwd) gs_params.aux_mask: per pixel the grey sum and the depth
+    // (recolor) *aux_match == 0: the colours are the source forward's aux grey, so the image is composed
+    // from its aux sums (aux_src) and transmittance (final_T_src) instead of blended
+    const uint32_t* aux_match = nullptr;
+    const float2* aux_src = nullptr;
+    const float* final_T_src = nullptr;
 };
 void launch_render_forward(const RenderArgs& a, hipStream_t s);
+// flag[0] |= 1 unless colors[i] == (m, m, m) bit for bit, m = aux_mask[i] ? 1 : 0, for every i < P
+void launch_aux_match(int P, const float* colors, const uint8_t* aux_mask, uint32_t* flag, hipStream_t s);
 
 struct ApplyWeightsArgs {
     int W, H, gx, gy, C;

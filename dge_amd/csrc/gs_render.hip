@@ -134,9 +134,13 @@ __device__ __forceinline__ void pixel_alpha4(f4v x, f4v y, f4v ncx, f4v ncy, f4v
 // skipped entry adds (f * 0) * T = 0, a stopped or saturated one f a' * 0.
 // T, the sums and `last` are bit-identical to the oracle's.  Returns
 // w = a' Tw, > 0 exactly when the entry is blended (the caller's vote).
-template <bool SEG = true>
+// AUX: the aux grey m in {0, 1} (m_on: m = 1, wave-uniform) composited the same way — a recolor blend with
+// colour (m, m, m) computes fma(m a', Tw, C) on each channel, which is fma(a', Tw, C) for m = 1 and C for
+// m = 0 (C + (+0) Tw, C >= +0) — so Cm + T bg is that render's image, bit for bit.
+template <bool SEG = true, bool AUX = false>
 __device__ __forceinline__ float blend_chain(float a, float4 fe, uint32_t pos, float& Ts, f2v& C01, f2v& C2D,
-                                           f2v& L01, float& L2, uint32_t& last) {
+                                           f2v& L01, float& L2, uint32_t& last, bool m_on = false,
+                                           float* Cm = nullptr) {
 #pragma clang fp contract(off)
     const float tT = Ts * (1.0f - a);
     const bool go = tT >= 0.0001f;
@@ -146,6 +150,7 @@ __device__ __forceinline__ float blend_chain(float a, float4 fe, uint32_t pos, f
     const f2v fa01 = f2v{fe.x, fe.y} * a2, fa2d = f2v{fe.z, fe.w} * a2;
     C01 = __builtin_elementwise_fma(fa01, T2, C01);
     C2D = __builtin_elementwise_fma(fa2d, T2, C2D);
+    if constexpr (AUX) *Cm = m_on ? __builtin_fmaf(a, Tw, *Cm) : *Cm;
     if constexpr (SEG) {
         L01 = __builtin_elementwise_fma(fa01, T2, L01);  // the segment's own colour sum (backward start)
         L2 = __builtin_fmaf(fa2d.x, Tw, L2);
@@ -220,8 +225,10 @@ __device__ __forceinline__ void emit_items(const RenderArgs& a, int tile, int qu
 }
 
 // BWD: the backward's bookkeeping (checkpoints, blended bits, touched bytes, the replay's work list);
-// a forward no backward follows (gs_params.forward_only) runs without it
-template <bool BWD>
+// a forward no backward follows (gs_params.forward_only) runs without it.  AUX (with BWD): the aux grey
+// composited beside the colour (gs_params.aux_mask) into aux_out.  Without BWD, a recolor render whose
+// colours are its source forward's aux grey (*aux_match == 0) composes its image from that forward's sums.
+template <bool BWD, bool AUX = false>
 __global__ __launch_bounds__(64, 3) void k_render_fwd(RenderArgs a) {
     // XCD-aware: blocks b, b+8, b+16, b+24 (one XCD under the round-robin dealing) take the four
     // quadrants of one tile, so the tile's list and its Splat gathers are fetched into one L2;
@@ -237,6 +244,21 @@ __global__ __launch_bounds__(64, 3) void k_render_fwd(RenderArgs a) {
     const int px = bx0 + (lane & 7), py = by0 + (lane >> 3);
     const bool inside = px < a.W && py < a.H;
     const float pfx = (float)px, pfy = (float)py;
+    if constexpr (!BWD) {
+        if (a.aux_match && *a.aux_match == 0u) {  // (one flag for the whole grid: a uniform branch)
+            if (inside) {  // the bits the blend below would produce (forward.cu:376, as at the end)
+                const size_t pix = (size_t)a.W * py + px;
+                const size_t HW = (size_t)a.W * a.H;
+                const float T = a.final_T_src[pix];
+                const float2 av = a.aux_src[pix];
+                a.out_color[pix] = __builtin_fmaf(T, a.bg[0], av.x);
+                a.out_color[HW + pix] = __builtin_fmaf(T, a.bg[1], av.x);
+                a.out_color[2 * HW + pix] = __builtin_fmaf(T, a.bg[2], av.x);
+                a.out_depth[pix] = av.y;
+            }
+            return;
+        }
+    }
 
     // the round's kept entries, one array per field: a pair of consecutive entries' field is one
     // 16-B read, the operands of two packed instructions (pixel_alpha4)
@@ -246,6 +268,10 @@ __global__ __launch_bounds__(64, 3) void k_render_fwd(RenderArgs a) {
     __shared__ __attribute__((aligned(16))) float s_x[kRoundLds], s_y[kRoundLds];
     __shared__ __attribute__((aligned(16))) float s_cx[kRoundLds], s_cy[kRoundLds], s_cz[kRoundLds], s_op[kRoundLds];
     __shared__ float4 s_rgbd[kRoundLds];
+    __shared__ __attribute__((aligned(16))) uint8_t s_mb[AUX ? kRoundLds : 4];  // (AUX) kept entries' aux bit
+    // (AUX) the next round's aux values in list order, loaded global -> LDS with its gathers: no registers
+    // held across the blend (the kernel sits at its 168-VGPR bound)
+    __shared__ float s_mnext[AUX ? kRound : 64];
     __shared__ __attribute__((aligned(16))) uint32_t s_pos[kRoundLds];
     __shared__ uint32_t s_gused[kRoundLds / kGroup];  // per blend group: bit u = entry u was blended
     __shared__ uint32_t s_id[kRoundLds];              // the kept entries' Gaussians (the touched bytes)
@@ -256,6 +282,7 @@ __global__ __launch_bounds__(64, 3) void k_render_fwd(RenderArgs a) {
     f2v C01 = {0.f, 0.f}, C2D = {0.f, 0.f};  // (C0, C1), (C2, depth)
     f2v L01 = {0.f, 0.f};                    // this segment's own colour sum (C0, C1), C2
     float L2 = 0.f;
+    float Cm = 0.f;  // (AUX) the aux grey sum
     uint32_t last = 0;
     const uint64_t t_start = a.diag ? __builtin_amdgcn_s_memrealtime() : 0;
     const uint64_t c_start = a.diag ? __builtin_amdgcn_s_memtime() : 0;
@@ -296,12 +323,23 @@ __global__ __launch_bounds__(64, 3) void k_render_fwd(RenderArgs a) {
         }
         return e;
     };
+    // (AUX) entry 64 i + lane's aux value -> s_mnext[64 i + lane]
+    const auto load_aux = [&](const uint32_t (&id)[4]) {
+        if constexpr (AUX) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                __builtin_amdgcn_global_load_lds(
+                    (__attribute__((address_space(1))) void*)&a.splat[id[i]].aux.x,
+                    (__attribute__((address_space(3))) void*)(s_mnext + 64 * i), 4, 0, 0);
+        }
+    };
     load_ids(range.x, ids);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         cur[i] = gather(ids[i]);
         cid[i] = ids[i];
     }
+    load_aux(ids);
     load_ids(range.x + kRound, ids);
 
     // checkpoint of segment k of this quadrant: slot ckpt_base + k, quadrant `quad`: (T after it, its own
@@ -334,6 +372,9 @@ __global__ __launch_bounds__(64, 3) void k_render_fwd(RenderArgs a) {
         // the blend loops over them
         int nk = 0, n_mid = 0;
         int kslot[4];  // compacted slot of this lane's entry i (-1: culled)
+        // (AUX: the round's aux values came global -> LDS, which the compiler does not track: every load of
+        // the previous round done — the gathers the cull reads were issued before them anyway)
+        if constexpr (AUX) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             if (i == kSegLen / 64) {
@@ -347,6 +388,7 @@ __global__ __launch_bounds__(64, 3) void k_render_fwd(RenderArgs a) {
                     s_cz[slot] = 0.f;
                     s_op[slot] = 0.f;
                     s_rgbd[slot] = make_float4(0.f, 0.f, 0.f, 0.f);
+                    if constexpr (AUX) s_mb[slot] = 0;
                     s_pos[slot] = 0u;
                 }
                 nk = n_mid;
@@ -364,6 +406,7 @@ __global__ __launch_bounds__(64, 3) void k_render_fwd(RenderArgs a) {
                 s_cz[slot] = -cur[i].co.z;
                 s_op[slot] = cur[i].co.w;
                 s_rgbd[slot] = cur[i].f;
+                if constexpr (AUX) s_mb[slot] = s_mnext[64 * i + lane] != 0.0f ? 1 : 0;
                 s_pos[slot] = k - range.x + 1;  // 1-based contributor index (forward.cu:331)
                 s_id[slot] = cid[i];
             }
@@ -378,6 +421,7 @@ __global__ __launch_bounds__(64, 3) void k_render_fwd(RenderArgs a) {
             s_cz[nk + lane] = 0.f;
             s_op[nk + lane] = 0.f;
             s_rgbd[nk + lane] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if constexpr (AUX) s_mb[nk + lane] = 0;
             s_pos[nk + lane] = 0u;
         }
         diag_kept += nk;
@@ -389,6 +433,8 @@ __global__ __launch_bounds__(64, 3) void k_render_fwd(RenderArgs a) {
             cur[i] = gather(ids[i]);
             cid[i] = ids[i];
         }
+        if constexpr (AUX) __builtin_amdgcn_s_waitcnt(0xC07F);  // (the compaction's s_mnext reads are done)
+        load_aux(ids);
         load_ids(b + 2 * kRound, ids);
         if (seg_done >= 0) put_ckpt(seg_done);  // the previous segment's: the replay's start
         seg_done = (int)((b - range.x) / kSegLen);  // the round's first segment
@@ -435,12 +481,15 @@ __global__ __launch_bounds__(64, 3) void k_render_fwd(RenderArgs a) {
         const auto blend_group = [&](int j, const AlphaOps& g, const ColourOps& c) {
             f4v dx4, dy4, G4, al;
             bool ok[4];
+            // (AUX: the group's four aux bits, the same for every lane: one scalar word)
+            uint32_t mb = 0u;
+            if constexpr (AUX) mb = __builtin_amdgcn_readfirstlane(*reinterpret_cast<const uint32_t*>(s_mb + j));
             pixel_alpha4(g.x, g.y, g.cx, g.cy, g.cz, g.op, -pfx, -pfy, dx4, dy4, G4, al, ok);
             uint64_t vm[kGroup];  // per entry: the lanes that blended it (uniform masks, SALU)
 #pragma unroll
             for (int u = 0; u < kGroup; ++u) {
-                const float w = blend_chain<BWD>(ok[u] ? al[u] : 0.0f, c.rgbd[u], c.pos[u], Ts, C01, C2D, L01, L2,
-                                                 last);
+                const float w = blend_chain<BWD, AUX>(ok[u] ? al[u] : 0.0f, c.rgbd[u], c.pos[u], Ts, C01, C2D, L01,
+                                                      L2, last, ((mb >> (8 * u)) & 1u) != 0u, &Cm);
                 if (BWD) vm[u] = __builtin_amdgcn_fcmpf(w, 0.0f, kFcmpOGT);
             }
             if (BWD) {
@@ -514,6 +563,7 @@ __global__ __launch_bounds__(64, 3) void k_render_fwd(RenderArgs a) {
         a.out_color[HW + pix] = __builtin_fmaf(T, a.bg[1], C01.y);
         a.out_color[2 * HW + pix] = __builtin_fmaf(T, a.bg[2], C2D.x);
         a.out_depth[pix] = C2D.y;
+        if constexpr (AUX) a.aux_out[pix] = make_float2(Cm, C2D.y);
     }
     const uint32_t m = wave_max_u32(inside ? last : 0u);
     // (item class from the entries the cull kept — the diagnostics' count, live anyway: a blended-entry
@@ -540,10 +590,31 @@ void launch_render_forward(const RenderArgs& a, hipStream_t s) {
     const int tiles = a.gx * a.gy;
     if (tiles <= 0) return;
     if (!a.order_ready) hipLaunchKernelGGL(k_tile_order, dim3(1), dim3(1024), 0, s, a.ranges, tiles, a.tile_order);
-    if (a.bwd)
-        hipLaunchKernelGGL(k_render_fwd<true>, dim3(div_up(tiles, 8) * 32), dim3(64), 0, s, a);
+    if (a.bwd && a.aux_out)
+        hipLaunchKernelGGL((k_render_fwd<true, true>), dim3(div_up(tiles, 8) * 32), dim3(64), 0, s, a);
+    else if (a.bwd)
+        hipLaunchKernelGGL((k_render_fwd<true, false>), dim3(div_up(tiles, 8) * 32), dim3(64), 0, s, a);
     else
-        hipLaunchKernelGGL(k_render_fwd<false>, dim3(div_up(tiles, 8) * 32), dim3(64), 0, s, a);
+        hipLaunchKernelGGL((k_render_fwd<false, false>), dim3(div_up(tiles, 8) * 32), dim3(64), 0, s, a);
+}
+
+// Whether a recolor's colours are its source forward's aux grey: flag[0] |= 1 on any difference
+// (bits compared: the blend of equal bits gives equal bits); flag zeroed by the caller
+__global__ __launch_bounds__(256) void k_aux_match(int P, const float* __restrict__ colors,
+                                                   const uint8_t* __restrict__ aux_mask, uint32_t* __restrict__ flag) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    bool diff = false;
+    if (i < P) {
+        const uint32_t m = aux_mask[i] ? __float_as_uint(1.0f) : 0u;
+        diff = __float_as_uint(colors[3 * (size_t)i]) != m || __float_as_uint(colors[3 * (size_t)i + 1]) != m ||
+               __float_as_uint(colors[3 * (size_t)i + 2]) != m;
+    }
+    if (__any(diff) && (threadIdx.x & 63) == 0) atomicOr(flag, 1u);  // (a vector atomic, rare: only on difference)
+}
+
+void launch_aux_match(int P, const float* colors, const uint8_t* aux_mask, uint32_t* flag, hipStream_t s) {
+    if (P <= 0) return;
+    hipLaunchKernelGGL(k_aux_match, dim3(div_up(P, 256)), dim3(256), 0, s, P, colors, aux_mask, flag);
 }
 
 // =====================================================================

@@ -162,6 +162,12 @@ def _render_fused(viewpoint_camera, pc, pipe, bg_color, scaling_modifier=1.0, ov
 
 _LAZY_OVERRIDE = os.environ.get("DGE_AMD_LAZY_OVERRIDE", "1") != "0"
 _RECOLOR = os.environ.get("DGE_AMD_RECOLOR", "1") != "0"
+# A training forward of a model carrying a boolean `mask` over its Gaussians (DGE's edit mask) also
+# composites that mask as a grey colour along its own alpha / transmittance chain (gs_params.aux_mask): the
+# semantic render DGE issues right after it (override_color = mask repeated over the channels) is then
+# served from those sums — checked on the device, bit for bit — instead of a second blend.
+_AUX = os.environ.get("DGE_AMD_AUX", "1") != "0"
+_AUX_HITS = 0  # recolor renders offered a forward's aux sums (tests, bench)
 
 # The last fused forward with backward bookkeeping per device: DGE renders each view for training, then
 # the same camera and Gaussians again with the edit mask as override_color (DGE.py:181, 198-204) —
@@ -181,9 +187,18 @@ def _tensor_key(t):
 class _ForwardEntry:
     """num_rendered: the binning layout's instance count."""
 
-    def __init__(self, key, refs, num_rendered, P, stream, radii, visible):
+    def __init__(self, key, refs, num_rendered, P, stream, radii, visible, aux=None):
         self.key, self.refs, self.num_rendered, self.P = key, refs, num_rendered, P
         self.stream, self.radii, self.visible = stream, radii, visible
+        # aux: (weakref to the mask the forward composited, its version then)
+        self.aux = None if aux is None else (weakref.ref(aux), aux._version)
+
+    def aux_mask(self):
+        """The mask this forward composited (gs_params.aux_mask), if it is alive and unchanged since."""
+        if self.aux is None:
+            return None
+        m = self.aux[0]()
+        return m if m is not None and m._version == self.aux[1] else None
 
     def buffers(self):
         bufs = [r() for r in self.refs]
@@ -231,6 +246,12 @@ def _fused_begin(viewpoint_camera, pc, pipe, bg_color, scaling_modifier=1.0, ove
         f_dc, f_rest, colors = None, None, override_color.float()
     visible = torch.empty(n, dtype=torch.bool, device=xyz.device)  # radii > 0, written by the preprocess
     may_bwd = _may_backward(xyz, f_dc, f_rest, colors, pc._opacity, pc._scaling, pc._rotation)
+    aux = None
+    if _AUX and _RECOLOR and override_color is None and index is None and may_bwd:
+        m = getattr(pc, "mask", None)
+        if (isinstance(m, torch.Tensor) and m.dtype == torch.bool and m.shape == (xyz.shape[0],)
+                and m.device == xyz.device and m.is_contiguous()):
+            aux = m
     # DGE's semantic render (DGE.py:198-204: override_color = the edit mask, grad mode on, its image only
     # thresholded) never receives a gradient: render it with the forward-only kernels and, should a
     # backward come after all, recompute the forward with the backward's bookkeeping then (lazy)
@@ -239,7 +260,7 @@ def _fused_begin(viewpoint_camera, pc, pipe, bg_color, scaling_modifier=1.0, ove
     # Gaussian ids alone (gs_raster.h gs_render_recolor): such a forward is never a recolor source
     forward_only = lazy or not may_bwd
     st = {"rs": rs, "index": index, "n": n, "f_dc": f_dc, "f_rest": f_rest, "colors": colors, "visible": visible,
-          "prepared": None, "lazy": lazy, "forward_only": forward_only}
+          "prepared": None, "lazy": lazy, "forward_only": forward_only, "aux": aux}
     if rs.debug:  # debug mode: the one-call forward, which keeps the reference's failure snapshot
         return st
     if colors is not None and not colors.requires_grad and forward_only:
@@ -254,10 +275,14 @@ def _fused_begin(viewpoint_camera, pc, pipe, bg_color, scaling_modifier=1.0, ove
                 # (the source's graph may be freed on its stream while this blend still reads its buffers)
                 for t in (geom, binning, img):
                     t.record_stream(cur)
+            src_aux = src.aux_mask()
+            if src_aux is not None:
+                global _AUX_HITS
+                _AUX_HITS += 1
             color, depth = _C.render_recolor(rs.bg, colors, rs.viewmatrix, rs.projmatrix, rs.campos, rs.tanfovx,
                                              rs.tanfovy, rs.image_height, rs.image_width, rs.sh_degree,
                                              rs.scale_modifier, rs.prefiltered, n, src.num_rendered, geom, binning,
-                                             img)
+                                             img, src_aux_mask=src_aux)
             st["visible"] = src.visible.clone()
             st["prepared"] = RecolorPrepared(src.num_rendered, color, depth, src.radii.clone())
             st["lazy"] = may_bwd  # (a backward, should one come, renders these inputs in full first)
@@ -267,7 +292,7 @@ def _fused_begin(viewpoint_camera, pc, pipe, bg_color, scaling_modifier=1.0, ove
         rs.bg, xyz, empty if f_dc is None else f_dc, empty if f_rest is None else f_rest,
         empty if colors is None else colors, pc._opacity, pc._scaling, pc._rotation, rs.scale_modifier,
         rs.viewmatrix, rs.projmatrix, rs.tanfovx, rs.tanfovy, rs.image_height, rs.image_width, rs.sh_degree,
-        rs.campos, rs.prefiltered, rs.debug, index=index, visible=visible, forward_only=forward_only)
+        rs.campos, rs.prefiltered, rs.debug, index=index, visible=visible, forward_only=forward_only, aux_mask=aux)
     return st
 
 
@@ -285,7 +310,8 @@ def _fused_end(st, pc):
         nr, geom, binning, img = fin
         prep.finished = None
         ent = _ForwardEntry(_geometry_key(pc, st["rs"], st["index"]), [weakref.ref(geom), weakref.ref(binning),
-                            weakref.ref(img)], nr, st["n"], torch.cuda.current_stream(xyz.device), radii, st["visible"])
+                            weakref.ref(img)], nr, st["n"], torch.cuda.current_stream(xyz.device), radii, st["visible"],
+                            aux=st.get("aux"))
         ent.tensor_refs = [weakref.ref(t) for t in (pc._xyz, pc._opacity, pc._scaling, pc._rotation,
                                                     st["rs"].viewmatrix, st["rs"].projmatrix) if t is not None]
         if st["index"] is not None:

@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define GS_RASTER_ABI_VERSION 17
+#define GS_RASTER_ABI_VERSION 18
 
 #define GS_OK 0
 #define GS_ERR_INVALID_ARG 1   /* AT_ERROR / std::runtime_error in the reference */
@@ -144,6 +144,13 @@ typedef struct gs_params {
                                      scratch (gradient-record flags, checkpoints, blended bits, the
                                      replay's work list, the touched bytes) and the binning buffer
                                      leaves it out; a backward of such a forward is an error */
+    const uint8_t *aux_mask;      /* NULL, or [P] bytes 0/1 (a bool tensor; row index[i] with `index`): a
+                                     forward with backward bookkeeping also composites these values as a
+                                     grey colour along the same alpha / transmittance chain and keeps the
+                                     result in its image buffer — the image a recolor render with
+                                     colors[i] = (m_i, m_i, m_i) gives, which gs_render_recolor then serves
+                                     without a second blend (DGE renders the edit mask of each view right
+                                     after its training render, threestudio/systems/DGE.py:198-204) (ABI 18) */
 } gs_params;
 
 /* gs_grads.accumulate bits: output i is ADDED to (out += grad) instead of
@@ -239,10 +246,14 @@ void gs_rasterize_forward_release(gs_forward_state *state);
  * (gs_image_buffer_size) receives that blend's per-pixel state, the source
  * buffers are only read.  s must describe the source forward (image size,
  * grid); its bg is the one blended.  Enqueued on `stream`, which must be
- * ordered after the source forward. */
+ * ordered after the source forward.  src_aux_mask: NULL, or the gs_params.aux_mask
+ * the source forward composited (the same bytes, unchanged since): where colors
+ * holds exactly (m_i, m_i, m_i) for every Gaussian (checked on the device, bit for
+ * bit) the image is composed from that forward's grey sum and transmittance
+ * instead of blended again — the same bits; otherwise the blend runs (ABI 18). */
 int gs_render_recolor(const gs_settings *s, int P, int num_rendered, const void *geom_buffer,
                       const void *binning_buffer, const void *img_buffer, const float *colors, void *img_out,
-                      float *out_color, float *out_depth, gs_stream_t stream);
+                      float *out_color, float *out_depth, const uint8_t *src_aux_mask, gs_stream_t stream);
 int gs_rasterize_backward_ex(const gs_settings *s, const gs_params *g, int R, const int *radii,
                              const void *geom_buffer, const void *binning_buffer, const void *img_buffer,
                              const float *dL_dpix, const gs_grads *out, gs_stream_t stream);

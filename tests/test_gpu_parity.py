@@ -801,6 +801,53 @@ def test_semantic_render_reuses_the_training_forward(cuda_device, localize):
     assert torch.equal(got[3], ref[3])
 
 
+@pytest.mark.parametrize("bg", [(0.0, 0.0, 0.0), (0.1, 0.0, 0.2)], ids=["black", "colour"])
+def test_semantic_render_served_from_the_training_blend(cuda_device, bg):
+    """gs_params.aux_mask: the training render of a model carrying an edit mask also composites the mask as a
+    grey along its own alpha / transmittance chain; DGE's semantic render right after it (override_color = the
+    mask repeated over the channels, DGE.py:198-204) is composed from those sums after a device-side check of
+    the colours — bit-identical to the recolor blend and to a full render.  Other colours (half the mask's
+    grey) fail the check and are blended; the training render itself is unchanged by the extra channel."""
+    from dge_amd import gaussian_renderer as GR
+    from dge_amd.cameras import orbit_camera
+    from dge_amd.gaussian_renderer import PipelineParams, render
+    from dge_amd.scene import synthetic_scene
+
+    dev = torch.device("cuda")
+    P, W, H = 60_000, 240, 176
+    pipe, bgt = PipelineParams(), torch.tensor(bg, device=dev)
+    cams = [orbit_camera(k, 4, W, H, device=dev) for k in range(2)]
+
+    def run(aux, recolor):
+        GR._AUX, GR._RECOLOR = aux, recolor
+        sc = synthetic_scene(P, seed=31, radius=1.5, scale=0.03, device=dev).requires_grad_(True)
+        sc.mask = torch.zeros(P, dtype=torch.bool, device=dev)
+        sc.mask[torch.argsort(sc._xyz[:, 1])[: P // 3]] = True
+        outs = []
+        for cam in cams:
+            tr = render(cam, sc, pipe, bgt)
+            h0 = GR._AUX_HITS
+            colors = sc.mask[..., None].float().repeat(1, 3)
+            sem = render(cam, sc, pipe, bgt, override_color=colors)
+            half = render(cam, sc, pipe, bgt, override_color=colors * 0.5)
+            outs.append([t.detach().clone() for t in (tr["render"], tr["depth_3dgs"], sem["render"],
+                                                      sem["depth_3dgs"], half["render"])] + [GR._AUX_HITS - h0])
+        return outs
+
+    prev = GR._AUX, GR._RECOLOR
+    try:
+        fused, recolor, full = run(True, True), run(False, True), run(False, False)
+    finally:
+        GR._AUX, GR._RECOLOR = prev
+    names = ("training image", "training depth", "semantic image", "semantic depth", "half-grey image")
+    for v in range(len(cams)):
+        for i, name in enumerate(names):
+            assert torch.equal(fused[v][i], recolor[v][i]), f"camera {v}: {name} (aux vs recolor)"
+            assert torch.equal(fused[v][i], full[v][i]), f"camera {v}: {name} (aux vs full render)"
+        assert not torch.equal(fused[v][2], fused[v][4])
+    assert [o[5] for o in fused] == [2, 2] and [o[5] for o in recolor] == [0, 0]
+
+
 def test_recolor_never_reuses_a_forward_only_render(cuda_device):
     """A training-shaped render of frozen parameters with grad mode on (the view-space placeholder keeps the
     graph, hence the buffers, alive) runs the forward-only kernels; on a grid over 2048 tiles (1024x768:
