@@ -475,7 +475,7 @@ def set_grad_pitches(o, d_xyz, d_op, d_sc, d_rot, d_dc=None, d_rest=None):
 def rasterize_gaussians_fused_backward(background, xyz, f_dc, f_rest, colors, raw_opacity, raw_scaling, raw_rotation,
                                        radii, scale_modifier, viewmatrix, projmatrix, tan_fovx, tan_fovy,
                                        dL_dout_color, degree, campos, geomBuffer, R, binningBuffer, imageBuffer,
-                                       debug, into=None, index=None, writes_after=None):
+                                       debug, into=None, index=None, writes_after=None, defer=False):
     """-> (dL_dmeans2D [P,3], dL_dxyz, dL_dfeatures_dc, dL_dfeatures_rest, dL_dcolors, dL_dopacity_raw,
     dL_dscaling_raw, dL_drotation_raw), gradients w.r.t. the raw tensors.
 
@@ -484,7 +484,9 @@ def rasterize_gaussians_fused_backward(background, xyz, f_dc, f_rest, colors, ra
     fused gradient accumulation, gs_grads.accumulate); the returned tuple then holds `dest`.
     index: the forward's rows; the parameter-shaped gradients are then full-size, zero outside them.
     writes_after: optional torch.cuda.Event the stream waits for before the first accumulated write
-    (gs_grads.writes_after: after the replay, before the per-Gaussian pass)."""
+    (gs_grads.writes_after: after the replay, before the per-Gaussian pass).
+    defer: enqueue only the gradient replay (gs_rasterize_backward_replay) and return (out, PendingBackward):
+    the outputs are written when rasterize_backward_passes runs that pending pass (with others)."""
     N.require_gpu(xyz)
     dev = xyz.device
     index = _index32(index)
@@ -523,7 +525,7 @@ def rasterize_gaussians_fused_backward(background, xyz, f_dc, f_rest, colors, ra
         d_rot = dest("rotation", lambda: new((Pp, 4), **opts), N.ACC_ROTATIONS)
         out = (d_m2, d_xyz, d_dc, d_rest, d_col, d_op, d_sc, d_rot)
         if P == 0:
-            return out
+            return (out, None) if defer else out
         xyz = _f32(xyz, "xyz")
         f_dc, f_rest = _features(f_dc, "features_dc"), _features(f_rest, "features_rest")
         colors = _f32(colors, "colors")
@@ -549,9 +551,53 @@ def rasterize_gaussians_fused_backward(background, xyz, f_dc, f_rest, colors, ra
         grad = _f32(dL_dout_color, "dL_dout_color")
         s, keep = _settings(background, viewmatrix, projmatrix, campos, tan_fovx, tan_fovy, H, W, degree,
                             scale_modifier, False, debug)
-        rc = N.lib().gs_rasterize_backward_ex(ctypes.byref(s), ctypes.byref(g), int(R), _ptr(radii.contiguous()),
+        radii = radii.contiguous()
+        if defer:
+            rc = N.lib().gs_rasterize_backward_replay(ctypes.byref(s), ctypes.byref(g), int(R), _ptr(radii),
+                                                      _ptr(geomBuffer), _ptr(binningBuffer), _ptr(imageBuffer),
+                                                      _ptr(grad), ctypes.byref(o), _stream(dev))
+            N.check(rc, "rasterize_gaussians_fused_backward (replay)")
+            keep += [xyz, f_dc, f_rest, colors, raw_opacity, raw_scaling, raw_rotation, index, radii, grad,
+                     geomBuffer, binningBuffer, imageBuffer, into, out]
+            return out, PendingBackward(s, g, o, int(R), radii, geomBuffer, binningBuffer, keep)
+        rc = N.lib().gs_rasterize_backward_ex(ctypes.byref(s), ctypes.byref(g), int(R), _ptr(radii),
                                               _ptr(geomBuffer), _ptr(binningBuffer), _ptr(imageBuffer), _ptr(grad),
                                               ctypes.byref(o), _stream(dev))
         N.check(rc, "rasterize_gaussians_fused_backward")
         del keep
         return out
+
+
+class PendingBackward:
+    """A view's backward whose gradient replay is enqueued (gs_rasterize_backward_replay) and whose
+    per-Gaussian pass waits for rasterize_backward_passes; holds the native arguments and every tensor
+    they point at."""
+
+    def __init__(self, s, g, o, R, radii, geom, binning, keep):
+        self.s, self.g, self.o, self.R, self.radii, self.geom, self.binning = s, g, o, R, radii, geom, binning
+        self.keep = keep
+
+    def set_writes_after(self, event):
+        self.o.writes_after = event.cuda_event if event is not None else None
+
+
+def rasterize_backward_passes(pending):
+    """The per-Gaussian passes of the pending backwards (in order) on the current stream, which must be
+    ordered after each one's replay: one merged pass when they render one scene into the same gradient
+    outputs (gs_rasterize_backward_passes), else one pass per view; at most N.MAX_VIEWS per native call."""
+    if not pending:
+        return
+    dev = pending[0].radii.device
+    with torch.cuda.device(dev):
+        for c0 in range(0, len(pending), N.MAX_VIEWS):
+            chunk = pending[c0:c0 + N.MAX_VIEWS]
+            n = len(chunk)
+            sa = (ctypes.c_void_p * n)(*[ctypes.addressof(p.s) for p in chunk])
+            ga = (ctypes.c_void_p * n)(*[ctypes.addressof(p.g) for p in chunk])
+            oa = (ctypes.c_void_p * n)(*[ctypes.addressof(p.o) for p in chunk])
+            ra = (ctypes.c_int * n)(*[p.R for p in chunk])
+            rad = (ctypes.c_void_p * n)(*[_ptr(p.radii) for p in chunk])
+            geo = (ctypes.c_void_p * n)(*[_ptr(p.geom) for p in chunk])
+            binn = (ctypes.c_void_p * n)(*[_ptr(p.binning) for p in chunk])
+            rc = N.lib().gs_rasterize_backward_passes(n, sa, ga, ra, rad, geo, binn, oa, _stream(dev))
+            N.check(rc, "rasterize_backward_passes")

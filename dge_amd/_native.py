@@ -150,6 +150,9 @@ SIGNATURES = {
     "gs_rasterize_forward_release": (None, [ctypes.c_void_p]),
     "gs_rasterize_backward_ex": (ctypes.c_int, [ctypes.POINTER(GsSettings), ctypes.POINTER(GsParams), ctypes.c_int,
                                                  _fp, _fp, _fp, _fp, _fp, ctypes.POINTER(GsGrads), ctypes.c_void_p]),
+    "gs_rasterize_backward_replay": (ctypes.c_int, [ctypes.POINTER(GsSettings), ctypes.POINTER(GsParams), ctypes.c_int,
+                                                     _fp, _fp, _fp, _fp, _fp, ctypes.POINTER(GsGrads), ctypes.c_void_p]),
+    "gs_rasterize_backward_passes": (ctypes.c_int, [ctypes.c_int] + [ctypes.c_void_p] * 8),
     "gs_views_forward": (ctypes.c_int, [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ALLOC_FN, ctypes.c_void_p,
                                          ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p)]),

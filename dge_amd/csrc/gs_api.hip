@@ -1071,6 +1071,34 @@ int gs_rasterize_backward(const gs_settings* s, int P, int M, int R, const float
     return gs_rasterize_backward_ex(s, &g2, R, radii, geom, binning, img, dL_dpix, &o, stream);
 }
 
+// the views' per-Gaussian passes can run as one (launch_gauss_backward_views): one scene (same P, rows,
+// SH layout), the same parameter-shaped outputs, every view after the first adding into all of them
+static bool passes_mergeable(int n, const gs_settings* const* s, const gs_params* const* gpv, const gs_grads* const* o) {
+    const uint32_t params = GS_ACC_OPACITY | GS_ACC_MEANS3D | GS_ACC_SCALES | GS_ACC_ROTATIONS;
+    const gs_params& p0 = *gpv[0];
+    const gs_grads* g0 = o[0];
+    if (p0.P == 0 || g0->dL_dcov3D || p0.cov3D_precomp) return false;
+    for (int v = 1; v < n; ++v) {
+        const gs_params& p = *gpv[v];
+        const gs_grads* g = o[v];
+        if (p.P != p0.P || p.index != p0.index || p.M != p0.M || p.sh_dc != p0.sh_dc || p.sh_rest != p0.sh_rest ||
+            p.means3D != p0.means3D || p.opacities != p0.opacities || p.scales != p0.scales ||
+            p.rotations != p0.rotations || p.activation != p0.activation || p.sh_half != p0.sh_half ||
+            s[v]->sh_degree != s[0]->sh_degree)
+            return false;
+        if (g->dL_dopacity != g0->dL_dopacity || g->dL_dmeans3D != g0->dL_dmeans3D ||
+            g->dL_dscales != g0->dL_dscales || g->dL_drotations != g0->dL_drotations ||
+            g->dL_dsh_dc != g0->dL_dsh_dc || g->dL_dsh_rest != g0->dL_dsh_rest || g->dL_dcov3D || g->grad_mask != g0->grad_mask ||
+            g->mask_bits != g0->mask_bits || g->pitch_means3D != g0->pitch_means3D ||
+            g->pitch_opacity != g0->pitch_opacity || g->pitch_scales != g0->pitch_scales ||
+            g->pitch_rotations != g0->pitch_rotations || g->dsh_dc_stride != g0->dsh_dc_stride ||
+            g->dsh_rest_stride != g0->dsh_rest_stride)
+            return false;
+        if ((g->accumulate & params) != params || (g0->dL_dsh_dc && !(g->accumulate & GS_ACC_SH))) return false;
+    }
+    return true;
+}
+
 // the argument checks of a backward (gs_rasterize_backward_ex, gs_views_backward)
 static int validate_backward(const gs_settings* s, const gs_params* gp, int R, const int* radii, const void* geom,
                       const void* binning, const void* img, const float* dL_dpix, const gs_grads* o) {
@@ -1110,6 +1138,61 @@ int gs_rasterize_backward_ex(const gs_settings* s, const gs_params* gp, int R, c
         if (rc || gp->P == 0) return rc;
         return backward_view(s, gp, R, radii, geom, binning, img, dL_dpix, o, (hipStream_t)stream_,
                              (hipEvent_t)o->writes_after, 0xFFFFFFFFu);
+    } catch (const std::exception& e) {
+        return set_error(GS_ERR_INVALID_ARG, "exception: %s", e.what());
+    } catch (...) {
+        return set_error(GS_ERR_INVALID_ARG, "unknown exception");
+    }
+}
+
+int gs_rasterize_backward_replay(const gs_settings* s, const gs_params* gp, int R, const int* radii,
+                                 const void* geom, const void* binning, const void* img, const float* dL_dpix,
+                                 const gs_grads* o, gs_stream_t stream_) {
+    try {
+        const int rc = validate_backward(s, gp, R, radii, geom, binning, img, dL_dpix, o);
+        if (rc || gp->P == 0) return rc;
+        return replay_view(s, gp, R, geom, binning, img, dL_dpix, (hipStream_t)stream_);
+    } catch (const std::exception& e) {
+        return set_error(GS_ERR_INVALID_ARG, "exception: %s", e.what());
+    } catch (...) {
+        return set_error(GS_ERR_INVALID_ARG, "unknown exception");
+    }
+}
+
+int gs_rasterize_backward_passes(int n, const gs_settings* const* s, const gs_params* const* gp, const int* R,
+                                 const int* const* radii, const void* const* geom, const void* const* binning,
+                                 const gs_grads* const* o, gs_stream_t stream_) {
+    try {
+        if (n < 1 || n > GS_MAX_VIEWS || !s || !gp || !R || !radii || !geom || !binning || !o)
+            return set_error(GS_ERR_INVALID_ARG, "gs_rasterize_backward_passes: 1 <= n <= %d views and every array "
+                             "are required", GS_MAX_VIEWS);
+        for (int v = 0; v < n; ++v) {
+            if (!s[v] || !gp[v] || !o[v]) return set_error(GS_ERR_INVALID_ARG, "view %d: settings, params, grads", v);
+            if (gp[v]->P > 0 && (!geom[v] || !radii[v] || (R[v] > 0 && !binning[v])))
+                return set_error(GS_ERR_INVALID_ARG, "view %d: buffers and radii are required", v);
+        }
+        hipStream_t stream = (hipStream_t)stream_;
+        const bool debug = s[0]->debug != 0;
+        GaussBwdArgs ga[GS_MAX_VIEWS];
+        for (int v = 0; v < n; ++v)
+            ga[v] = gauss_args(s[v], gp[v], R[v], radii[v], geom[v], binning[v], o[v], 0xFFFFFFFFu);
+        if (n > 1 && passes_mergeable(n, s, gp, o)) {
+            const int chunk = gauss_backward_max_views();
+            for (int v0 = 0; v0 < n; v0 += chunk) {
+                const int nv = std::min(chunk, n - v0);
+                { StageScope sc(ST_GAUSS_BWD, stream);
+                launch_gauss_backward_views(ga + v0, nv, stream, v0 == 0 ? (hipEvent_t)o[0]->writes_after : nullptr); }
+                GS_LAUNCHED("gaussian backward (views)");
+            }
+            return GS_OK;
+        }
+        for (int v = 0; v < n; ++v) {  // one pass per view, in order
+            if (gp[v]->P == 0) continue;
+            { StageScope sc(ST_GAUSS_BWD, stream);
+            launch_gauss_backward(ga[v], stream, (hipEvent_t)o[v]->writes_after); }
+            GS_LAUNCHED("gaussian backward");
+        }
+        return GS_OK;
     } catch (const std::exception& e) {
         return set_error(GS_ERR_INVALID_ARG, "exception: %s", e.what());
     } catch (...) {
@@ -1340,32 +1423,14 @@ int gs_views_check(gs_views* h, int* num_rendered) {
     return GS_OK;
 }
 
-// the views' per-Gaussian passes can run as one (launch_gauss_backward_views): one scene (same P, rows,
-// SH layout), the same parameter-shaped outputs, every view after the first adding into all of them
 bool views_mergeable(const gs_views* h, const gs_grads* const* o) {
-    const uint32_t params = GS_ACC_OPACITY | GS_ACC_MEANS3D | GS_ACC_SCALES | GS_ACC_ROTATIONS;
-    const gs_params& p0 = h->f[0].gp;
-    const gs_grads* g0 = o[0];
-    if (p0.P == 0 || g0->dL_dcov3D || p0.cov3D_precomp) return false;
-    for (int v = 1; v < h->n; ++v) {
-        const gs_params& p = h->f[v].gp;
-        const gs_grads* g = o[v];
-        if (p.P != p0.P || p.index != p0.index || p.M != p0.M || p.sh_dc != p0.sh_dc || p.sh_rest != p0.sh_rest ||
-            p.means3D != p0.means3D || p.opacities != p0.opacities || p.scales != p0.scales ||
-            p.rotations != p0.rotations || p.activation != p0.activation || p.sh_half != p0.sh_half ||
-            h->f[v].s.sh_degree != h->f[0].s.sh_degree)
-            return false;
-        if (g->dL_dopacity != g0->dL_dopacity || g->dL_dmeans3D != g0->dL_dmeans3D ||
-            g->dL_dscales != g0->dL_dscales || g->dL_drotations != g0->dL_drotations ||
-            g->dL_dsh_dc != g0->dL_dsh_dc || g->dL_dsh_rest != g0->dL_dsh_rest || g->dL_dcov3D || g->grad_mask != g0->grad_mask ||
-            g->mask_bits != g0->mask_bits || g->pitch_means3D != g0->pitch_means3D ||
-            g->pitch_opacity != g0->pitch_opacity || g->pitch_scales != g0->pitch_scales ||
-            g->pitch_rotations != g0->pitch_rotations || g->dsh_dc_stride != g0->dsh_dc_stride ||
-            g->dsh_rest_stride != g0->dsh_rest_stride)
-            return false;
-        if ((g->accumulate & params) != params || (g0->dL_dsh_dc && !(g->accumulate & GS_ACC_SH))) return false;
+    const gs_settings* s[GS_MAX_VIEWS];
+    const gs_params* gp[GS_MAX_VIEWS];
+    for (int v = 0; v < h->n; ++v) {
+        s[v] = &h->f[v].s;
+        gp[v] = &h->f[v].gp;
     }
-    return true;
+    return passes_mergeable(h->n, s, gp, o);
 }
 
 int gs_views_backward(gs_views* h, const float* const* dL_dpix, const gs_grads* const* grads,

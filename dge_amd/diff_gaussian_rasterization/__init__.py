@@ -145,6 +145,7 @@ class _RasterizeGaussiansFused(torch.autograd.Function):
         ctx.index = index
         ctx.num_rendered = num_rendered
         ctx.recompute = bool(recompute)
+        ctx.means2D = means2D  # (a deferred backward hands its gradient over itself: _defer_pass)
         ctx.has_sh = f_dc is not None and f_dc.numel() != 0
         ctx.save_for_backward(xyz, f_dc, f_rest, colors, raw_opacity, raw_scaling, raw_rotation, radii, geomBuffer,
                               binningBuffer, imgBuffer)
@@ -219,6 +220,17 @@ class _RasterizeGaussiansFused(torch.autograd.Function):
                 geomBuffer, ctx.num_rendered, binningBuffer, imgBuffer, rs.debug)
         _serialize_scratch(ctx, xyz.device)
         _ZEROED.pop(xyz.device.index, None)  # (this backward writes .grad: the buffer is no longer all zeros)
+        m2 = getattr(ctx, "means2D", None)
+        m2_mode = _accumulation_mode(m2, node(1))[0] if into and _DEFER_PASSES else None
+        if (m2_mode is not None and ctx.index is None and ctx.has_sh and not rs.debug
+                and all(k in into for k in ("xyz", "opacity", "scaling", "rotation", "sh"))):
+            # every gradient goes into a .grad: enqueue the gradient replay now and this view's per-Gaussian
+            # pass at the end of the backward, merged with the other views' (_defer_pass)
+            out, pend = _C.rasterize_gaussians_fused_backward(*args, into=into, index=None, defer=True)
+            for p, t in direct:  # (written by the deferred pass; the next view's backward adds into them)
+                p.grad = t
+            _defer_pass(xyz.device, pend, m2, m2_mode, out[0], [t for _, t in direct])
+            return (None,) * 13
         ordered = bool(into) and _SIDE_STREAMS
         stream, after = _order_grad_writes_begin(xyz.device) if ordered else (None, None)
         d_m2, d_xyz, d_dc, d_rest, d_col, d_op, d_sc, d_rot = _call_with_snapshot(
@@ -246,6 +258,46 @@ class _RasterizeGaussiansFused(torch.autograd.Function):
 
 
 _FUSED_GRAD_ACCUM = os.environ.get("DGE_AMD_FUSED_GRAD_ACCUM", "1") != "0"
+
+# Deferred per-Gaussian passes.  DGE renders its views one by one and backpropagates their stacked loss once
+# (threestudio/systems/DGE.py:179-222, 672): autograd then runs the views' backward nodes one after
+# another.  When a view's gradients all go into .grad buffers (the fused accumulation above), its backward
+# enqueues only the gradient replay; the per-Gaussian passes of all such views of the backward run at its
+# end (an autograd final callback, before backward() returns) as ONE merged pass
+# (gs_rasterize_backward_passes, the pass the batched views path runs) — the same sums in the same view
+# order, bitwise.  The view-space gradients (dL/dmeans2D) are handed to their leaves there.
+_DEFER_PASSES = os.environ.get("DGE_AMD_DEFER_PASSES", "1") != "0"
+_PENDING_PASSES = {}  # device index -> [(PendingBackward, replay event, means2D leaf, mode, dL/dmeans2D, fresh)]
+
+
+def _defer_pass(dev, pend, m2, m2_mode, d_m2, fresh):
+    lst = _PENDING_PASSES.get(dev.index)
+    if lst is None:
+        lst = _PENDING_PASSES[dev.index] = []
+        torch.autograd.Variable._execution_engine.queue_callback(lambda d=dev: _run_deferred_passes(d))
+    ev = torch.cuda.current_stream(dev).record_event()
+    lst.append((pend, ev, m2, m2_mode, d_m2, fresh))
+
+
+def _run_deferred_passes(dev):
+    lst = _PENDING_PASSES.pop(dev.index, None)
+    if not lst:
+        return
+    cur = torch.cuda.current_stream(dev)
+    for _, ev, *_rest in lst:
+        cur.wait_event(ev)
+    pend = [e[0] for e in lst if e[0] is not None]
+    stream, after = _order_grad_writes_begin(dev) if _SIDE_STREAMS else (None, None)
+    if pend:
+        pend[0].set_writes_after(after)
+        _C.rasterize_backward_passes(pend)
+    if _SIDE_STREAMS:
+        _order_grad_writes_end(dev, stream, [t for e in lst for t in e[5]])
+    for _, _, m2, mode, d_m2, _ in lst:  # (what means2D's AccumulateGrad would have done)
+        if m2.grad is None:
+            m2.grad = d_m2
+        else:
+            m2.grad.add_(d_m2)
 
 # In-kernel .grad writes of backward calls that autograd runs on different streams (views rendered
 # concurrently, dge_amd.multiview.render_views: each view's backward runs on its forward's stream)

@@ -257,6 +257,23 @@ int gs_render_recolor(const gs_settings *s, int P, int num_rendered, const void 
 int gs_rasterize_backward_ex(const gs_settings *s, const gs_params *g, int R, const int *radii,
                              const void *geom_buffer, const void *binning_buffer, const void *img_buffer,
                              const float *dL_dpix, const gs_grads *out, gs_stream_t stream);
+/* gs_rasterize_backward_ex in its two halves, for a caller that defers the per-Gaussian passes of several
+ * views' backwards to the end of one autograd backward (DGE's loop renders its views one by one and
+ * backpropagates their stacked loss once, threestudio/systems/DGE.py:179-222, 672):
+ *   _replay: the gradient replay of one view (its per-(slot, quadrant) records, kept in that view's
+ *            binning buffer); the arguments are the ones gs_rasterize_backward_ex would get;
+ *   _passes: the per-Gaussian passes of n replayed views, in view order — ONE merged pass (the one
+ *            gs_views_backward runs) when the views render one scene into the same gradient outputs and
+ *            every view after the first accumulates (GS_ACC_*) into all of them, else one pass per view.
+ *            out[0]->writes_after orders the first accumulated write.  `stream` must be ordered after
+ *            every view's replay.  Bitwise the per-view gs_rasterize_backward_ex calls in that order.
+ * (ABI 18) */
+int gs_rasterize_backward_replay(const gs_settings *s, const gs_params *g, int R, const int *radii,
+                                 const void *geom_buffer, const void *binning_buffer, const void *img_buffer,
+                                 const float *dL_dpix, const gs_grads *out, gs_stream_t stream);
+int gs_rasterize_backward_passes(int n, const gs_settings *const *s, const gs_params *const *g, const int *R,
+                                 const int *const *radii, const void *const *geom_buffer,
+                                 const void *const *binning_buffer, const gs_grads *const *out, gs_stream_t stream);
 
 /* A batch of views of ONE scene (DGE renders a batch of edited views per step,
  * threestudio/systems/DGE.py:170-239): view v on streams[v], its outputs

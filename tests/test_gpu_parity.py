@@ -498,6 +498,48 @@ def test_fused_gradient_accumulation(cuda_device):
         assert torch.equal(g, p.grad)
 
 
+@pytest.mark.parametrize("views,pre_grad", [(3, False), (3, True), (10, False)])
+def test_dge_loop_backward_merges_the_views_passes(cuda_device, views, pre_grad):
+    """DGE's loop (DGE.py:179-222, 672): the views rendered one by one, their images stacked into one masked
+    l1 loss, ONE backward.  Each view's backward enqueues its gradient replay and the views' per-Gaussian passes
+    run merged at the end of the backward (an autograd final callback; DGE_AMD_DEFER_PASSES=0: one pass per
+    view inside each view's backward).  Every parameter's .grad and every view-space gradient is bitwise the
+    same; 10 views: two native calls of at most 8."""
+    from dge_amd import diff_gaussian_rasterization as R
+    from dge_amd.cameras import orbit_camera
+    from dge_amd.gaussian_renderer import PipelineParams, render
+    from dge_amd.scene import synthetic_scene
+
+    dev = torch.device("cuda")
+    W, H = 160, 120
+    cams = [orbit_camera(k, views, W, H, device=dev) for k in range(views)]
+    gts = torch.rand(views, H, W, 3, generator=torch.Generator().manual_seed(3)).to(dev)
+    bg = torch.zeros(3, device=dev)
+
+    def run(defer):
+        prev, R._DEFER_PASSES = R._DEFER_PASSES, defer
+        try:
+            sc = synthetic_scene(20_000, seed=8, radius=1.5, scale=0.03, device=dev).requires_grad_(True)
+            if pre_grad:
+                for p in sc.parameters():
+                    p.grad = torch.full_like(p, 0.125)
+            pkgs = [render(c, sc, PipelineParams(), bg) for c in cams]
+            images = torch.stack([p["render"].permute(1, 2, 0) for p in pkgs], 0)
+            m = (images.detach().mean(-1, keepdim=True) > 0.05).float()
+            torch.nn.functional.l1_loss(images * m, gts * m).backward()
+            assert not R._PENDING_PASSES  # (flushed before backward() returned)
+            return [p.grad.clone() for p in sc.parameters()], [p["viewspace_points"].grad.clone() for p in pkgs]
+        finally:
+            R._DEFER_PASSES = prev
+
+    (ga, va), (gb, vb) = run(True), run(False)
+    for x, y in zip(ga, gb):
+        assert torch.equal(x, y)
+    for x, y in zip(va, vb):
+        assert torch.equal(x, y)
+    assert all(bool(v.abs().sum() > 0) for v in va)
+
+
 def test_c5_local_edit_fp16_sh_vs_oracle(cuda_device, oracle):
     """configs[4]: 1.0M-Gaussian scene, localize=True on a fixed 200k mask (sorted by x, first 20%),
     SH stored as fp16 and upcast in-kernel, fp32 covariance inputs, 512x512 fwd+bwd.
