@@ -475,7 +475,7 @@ def set_grad_pitches(o, d_xyz, d_op, d_sc, d_rot, d_dc=None, d_rest=None):
 def rasterize_gaussians_fused_backward(background, xyz, f_dc, f_rest, colors, raw_opacity, raw_scaling, raw_rotation,
                                        radii, scale_modifier, viewmatrix, projmatrix, tan_fovx, tan_fovy,
                                        dL_dout_color, degree, campos, geomBuffer, R, binningBuffer, imageBuffer,
-                                       debug, into=None, index=None, writes_after=None, defer=False):
+                                       debug, into=None, index=None, writes_after=None, defer=False, stream=None):
     """-> (dL_dmeans2D [P,3], dL_dxyz, dL_dfeatures_dc, dL_dfeatures_rest, dL_dcolors, dL_dopacity_raw,
     dL_dscaling_raw, dL_drotation_raw), gradients w.r.t. the raw tensors.
 
@@ -486,7 +486,9 @@ def rasterize_gaussians_fused_backward(background, xyz, f_dc, f_rest, colors, ra
     writes_after: optional torch.cuda.Event the stream waits for before the first accumulated write
     (gs_grads.writes_after: after the replay, before the per-Gaussian pass).
     defer: enqueue only the gradient replay (gs_rasterize_backward_replay) and return (out, PendingBackward):
-    the outputs are written when rasterize_backward_passes runs that pending pass (with others)."""
+    the outputs are written when rasterize_backward_passes runs that pending pass (with others); `stream`
+    (a torch.cuda.Stream ordered after the current one): where the replay runs (default: the current stream;
+    the outputs are allocated on the current stream either way)."""
     N.require_gpu(xyz)
     dev = xyz.device
     index = _index32(index)
@@ -555,7 +557,8 @@ def rasterize_gaussians_fused_backward(background, xyz, f_dc, f_rest, colors, ra
         if defer:
             rc = N.lib().gs_rasterize_backward_replay(ctypes.byref(s), ctypes.byref(g), int(R), _ptr(radii),
                                                       _ptr(geomBuffer), _ptr(binningBuffer), _ptr(imageBuffer),
-                                                      _ptr(grad), ctypes.byref(o), _stream(dev))
+                                                      _ptr(grad), ctypes.byref(o),
+                                                      _stream(dev) if stream is None else stream.cuda_stream)
             N.check(rc, "rasterize_gaussians_fused_backward (replay)")
             keep += [xyz, f_dc, f_rest, colors, raw_opacity, raw_scaling, raw_rotation, index, radii, grad,
                      geomBuffer, binningBuffer, imageBuffer, into, out]

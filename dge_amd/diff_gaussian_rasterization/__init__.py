@@ -226,10 +226,14 @@ class _RasterizeGaussiansFused(torch.autograd.Function):
                 and all(k in into for k in ("xyz", "opacity", "scaling", "rotation", "sh"))):
             # every gradient goes into a .grad: enqueue the gradient replay now and this view's per-Gaussian
             # pass at the end of the backward, merged with the other views' (_defer_pass)
-            out, pend = _C.rasterize_gaussians_fused_backward(*args, into=into, index=None, defer=True)
+            # (consecutive views' replays on different streams: the latency-bound replays overlap)
+            side = _replay_stream(xyz.device)
+            if side is not None:
+                side.wait_stream(torch.cuda.current_stream(xyz.device))
+            out, pend = _C.rasterize_gaussians_fused_backward(*args, into=into, index=None, defer=True, stream=side)
             for p, t in direct:  # (written by the deferred pass; the next view's backward adds into them)
                 p.grad = t
-            _defer_pass(xyz.device, pend, m2, m2_mode, out[0], [t for _, t in direct])
+            _defer_pass(xyz.device, pend, m2, m2_mode, out[0], [t for _, t in direct], side)
             return (None,) * 13
         ordered = bool(into) and _SIDE_STREAMS
         stream, after = _order_grad_writes_begin(xyz.device) if ordered else (None, None)
@@ -268,14 +272,31 @@ _FUSED_GRAD_ACCUM = os.environ.get("DGE_AMD_FUSED_GRAD_ACCUM", "1") != "0"
 # order, bitwise.  The view-space gradients (dL/dmeans2D) are handed to their leaves there.
 _DEFER_PASSES = os.environ.get("DGE_AMD_DEFER_PASSES", "1") != "0"
 _PENDING_PASSES = {}  # device index -> [(PendingBackward, replay event, means2D leaf, mode, dL/dmeans2D, fresh)]
+_REPLAY_STREAMS = {}  # device index -> the side streams deferred replays rotate over (with the current one)
+# (2 side streams measured within the noise of one stream in DGE's loop, 1101-1171 vs 1107-1220 views/s:
+# its replays follow one another on the caller's stream by default)
+_REPLAY_SIDE = int(os.environ.get("DGE_AMD_REPLAY_STREAMS", "0"))
 
 
-def _defer_pass(dev, pend, m2, m2_mode, d_m2, fresh):
+def _replay_stream(dev):
+    """The stream the next deferred replay of this backward runs on: the current stream for the first, then
+    _REPLAY_SIDE side streams in turn (None: the current stream).  The replay reads and writes only tensors
+    its PendingBackward holds, and the deferred passes wait for it."""
+    k = len(_PENDING_PASSES.get(dev.index, ()))
+    if _REPLAY_SIDE <= 0 or k % (_REPLAY_SIDE + 1) == 0:
+        return None
+    pool = _REPLAY_STREAMS.get(dev.index)
+    if pool is None:
+        pool = _REPLAY_STREAMS[dev.index] = [torch.cuda.Stream(device=dev) for _ in range(_REPLAY_SIDE)]
+    return pool[k % (_REPLAY_SIDE + 1) - 1]
+
+
+def _defer_pass(dev, pend, m2, m2_mode, d_m2, fresh, stream=None):
     lst = _PENDING_PASSES.get(dev.index)
     if lst is None:
         lst = _PENDING_PASSES[dev.index] = []
         torch.autograd.Variable._execution_engine.queue_callback(lambda d=dev: _run_deferred_passes(d))
-    ev = torch.cuda.current_stream(dev).record_event()
+    ev = (stream if stream is not None else torch.cuda.current_stream(dev)).record_event()
     lst.append((pend, ev, m2, m2_mode, d_m2, fresh))
 
 

@@ -498,13 +498,14 @@ def test_fused_gradient_accumulation(cuda_device):
         assert torch.equal(g, p.grad)
 
 
-@pytest.mark.parametrize("views,pre_grad", [(3, False), (3, True), (10, False)])
-def test_dge_loop_backward_merges_the_views_passes(cuda_device, views, pre_grad):
+@pytest.mark.parametrize("views,pre_grad,side", [(3, False, 2), (3, True, 2), (10, False, 2), (3, False, 0)])
+def test_dge_loop_backward_merges_the_views_passes(cuda_device, views, pre_grad, side):
     """DGE's loop (DGE.py:179-222, 672): the views rendered one by one, their images stacked into one masked
     l1 loss, ONE backward.  Each view's backward enqueues its gradient replay and the views' per-Gaussian passes
     run merged at the end of the backward (an autograd final callback; DGE_AMD_DEFER_PASSES=0: one pass per
     view inside each view's backward).  Every parameter's .grad and every view-space gradient is bitwise the
-    same; 10 views: two native calls of at most 8."""
+    same; 10 views: two native calls of at most 8; side: the replays rotate over the current stream and that
+    many side streams (DGE_AMD_REPLAY_STREAMS)."""
     from dge_amd import diff_gaussian_rasterization as R
     from dge_amd.cameras import orbit_camera
     from dge_amd.gaussian_renderer import PipelineParams, render
@@ -518,6 +519,7 @@ def test_dge_loop_backward_merges_the_views_passes(cuda_device, views, pre_grad)
 
     def run(defer):
         prev, R._DEFER_PASSES = R._DEFER_PASSES, defer
+        prev_side, R._REPLAY_SIDE = R._REPLAY_SIDE, side
         try:
             sc = synthetic_scene(20_000, seed=8, radius=1.5, scale=0.03, device=dev).requires_grad_(True)
             if pre_grad:
@@ -530,7 +532,7 @@ def test_dge_loop_backward_merges_the_views_passes(cuda_device, views, pre_grad)
             assert not R._PENDING_PASSES  # (flushed before backward() returned)
             return [p.grad.clone() for p in sc.parameters()], [p["viewspace_points"].grad.clone() for p in pkgs]
         finally:
-            R._DEFER_PASSES = prev
+            R._DEFER_PASSES, R._REPLAY_SIDE = prev, prev_side
 
     (ga, va), (gb, vb) = run(True), run(False)
     for x, y in zip(ga, gb):
