@@ -1,7 +1,9 @@
 """Summarise rocprofv3 --pmc passes per kernel (dev tool).
 
-Reads gpurun_out/pmc/p*/.../*counter_collection.csv, averages every counter
-per dispatch for each kernel, prints a table and writes
+Reads gpurun_out/pmc/p*/.../*counter_collection.csv, takes every counter's median
+over a kernel's dispatches (the steady-state launches of the timed step: the bench's
+setup calls — reference-ABI backwards that overwrite every output — are outliers a mean
+would mix in), prints a table and writes
 gpurun_out/pmc/pmc_traffic.json (committed as profiles/pmc_traffic.json): per kernel the HBM bytes per launch from the
 memory-side counters, corrected as MI355X_MICROARCH.md §HBM prescribes
 (FETCH_SIZE reports half the bytes of wide coalesced reads on gfx950: x2;
@@ -16,7 +18,7 @@ import sys
 
 STAGE = {"k_preprocess": "preprocess", "k_render_fwd": "render_fwd", "k_render_bwd": "render_bwd",
          "k_gauss_live": "gauss_bwd", "k_gauss_bwd_live": "gauss_bwd", "k_render_apply_weights": "apply_weights",
-         "k_ranges": "ranges", "k_scan_emit": "emit"}
+         "k_ranges": "ranges", "k_scan_emit": "emit", "k_emit_tiles": "emit"}
 
 
 def main(root):
@@ -30,7 +32,7 @@ def main(root):
     out = {}
     keys = sorted(vals, key=lambda k: -sum(vals[k].get("SQ_WAVE_CYCLES", [0])))
     for k in keys:
-        c = {n: sum(v) / len(v) for n, v in vals[k].items()}
+        c = {n: sorted(v)[len(v) // 2] for n, v in vals[k].items()}
         line = " ".join(f"{n}={c[n]:.4g}" for n in sorted(c))
         print(f"{k}: {line}")
         if k in STAGE and "FETCH_SIZE" in c and "WRITE_SIZE" in c:
@@ -39,7 +41,8 @@ def main(root):
             e = out.setdefault(STAGE[k], {"kernel": [], "read_bytes_per_launch": 0, "write_bytes_per_launch": 0,
                                           "bytes_per_launch": 0,
                                           "method": "rocprofv3 --pmc FETCH_SIZE (x2, gfx950 correction) + "
-                                                    "WRITE_SIZE, separate passes; a stage's kernels summed"})
+                                                    "WRITE_SIZE, separate passes; median over the kernel's dispatches; "
+                                                    "a stage's kernels summed"})
             e["kernel"].append(k)
             e["read_bytes_per_launch"] += int(rd)
             e["write_bytes_per_launch"] += int(wr)
