@@ -15,7 +15,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("DGE_AMD_LIB") or os.path.join(_HERE, "lib", "libgs_raster.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "gs_raster.h")
 
-ABI_VERSION = 18  # GS_RASTER_ABI_VERSION of include/gs_raster.h this binding is written against
+ABI_VERSION = 19  # GS_RASTER_ABI_VERSION of include/gs_raster.h this binding is written against
 
 GS_OK = 0
 GS_ERR_INVALID_ARG = 1
@@ -105,6 +105,7 @@ class GsGrads(ctypes.Structure):
         ("pitch_opacity", ctypes.c_int),
         ("pitch_scales", ctypes.c_int),
         ("pitch_rotations", ctypes.c_int),
+        ("dirty_rows", ctypes.c_void_p),
     ]
 
 
@@ -187,6 +188,10 @@ SIGNATURES = {
                                       ctypes.c_void_p, ctypes.c_void_p]),
     "gs_rows_scatter": (ctypes.c_int, [ctypes.POINTER(RowsRegion), ctypes.c_int, ctypes.c_void_p, ctypes.c_longlong,
                                        ctypes.c_void_p, ctypes.c_void_p]),
+    "gs_rows_zero_dirty": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_longlong, ctypes.c_int, ctypes.c_void_p,
+                                          ctypes.c_longlong, ctypes.c_void_p]),
+    "gs_rows_mark_dirty": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_longlong, ctypes.c_void_p,
+                                          ctypes.c_void_p]),
     "gs_rows_compact": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_longlong, ctypes.c_void_p, ctypes.c_void_p,
                                        ctypes.c_void_p]),
     "gs_rows_gather_dev": (ctypes.c_int, [ctypes.POINTER(RowsRegion), ctypes.c_int, ctypes.c_void_p, ctypes.c_longlong,

@@ -745,6 +745,7 @@ GaussBwdArgs gauss_args(const gs_settings* s, const gs_params* gp, int R, const 
     ga.slot_cap = slot_cap;
     ga.grad_mask = o->grad_mask;
     ga.mask_bits = o->grad_mask ? o->mask_bits : 0u;
+    ga.dirty = o->dirty_rows;
     ga.dL_dconic = o->dL_dconic;
     ga.diag = diag_buffer(2, kDiagWords * 4 * (size_t)(P / 256 + 1));
     return ga;
@@ -1066,6 +1067,7 @@ int gs_rasterize_backward(const gs_settings* s, int P, int M, int R, const float
     o.writes_after = nullptr;
     o.zeroed = 0;
     o.pitch_means3D = o.pitch_opacity = o.pitch_scales = o.pitch_rotations = 0;
+    o.dirty_rows = nullptr;
     gs_params g2 = g;
     g2.M = M;  // dL_dsh is [P,M,3] even when shs is absent (then all zero)
     return gs_rasterize_backward_ex(s, &g2, R, radii, geom, binning, img, dL_dpix, &o, stream);

@@ -454,6 +454,7 @@ __global__ __launch_bounds__(kGB) void k_gauss_live(GaussBwdViews m) {
     // zeros for the overwritten outputs of the Gaussians dead in view 0 (parameter-shaped ones at row src)
     const uint32_t acc = a.acc;
     const int src = in && a.index ? a.index[idx] : idx;
+    if (live && a.dirty) a.dirty[src] = 1;  // (the bucket row this pass may write: its next clear zeroes it)
     if (in && !(mask & 1u)) {
         if (!(acc & GS_ACC_OPACITY)) a.dL_dopacity[(size_t)src * a.pop] = 0.f;
         if (!(acc & GS_ACC_MEANS3D))

@@ -187,6 +187,25 @@ __global__ __launch_bounds__(256) void k_compact_write(const uint8_t* __restrict
     if (blockIdx.x == gridDim.x - 1 && tid == 0) *count = base;
 }
 
+// Four rows per wave, a 16-lane group per row (float4 columns, rows wider than 64 floats loop): the dirty
+// rows of a row-major bucket zeroed, their flags cleared.
+__global__ __launch_bounds__(256) void k_rows_zero_dirty(float* __restrict__ rows, long long pitch, int width,
+                                                         uint8_t* __restrict__ dirty, long long n) {
+    const long long r = ((long long)blockIdx.x * 256 + threadIdx.x) >> 4;
+    const int c0 = 4 * (threadIdx.x & 15);
+    if (r >= n || !dirty[r]) return;
+    float4* row = reinterpret_cast<float4*>(rows + r * pitch);
+    for (int c = c0; c < width; c += 64) row[c >> 2] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (c0 == 0) dirty[r] = 0;  // (this row's group only reads its own flag: no race with the other rows)
+}
+
+__global__ __launch_bounds__(256) void k_rows_mark_dirty(uint8_t* __restrict__ dirty, const long long* __restrict__ rows,
+                                                         long long m, const long long* __restrict__ m_dev) {
+    const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+    const long long mv = m_dev ? (*m_dev < m ? *m_dev : m) : m;
+    if (i < mv) dirty[rows[i]] = 1;
+}
+
 static int rows_launch(const gs_rows_region* regions, int nreg, RowsLaunch& a, const char* fn) {
     if (nreg < 1 || nreg > GS_ROWS_MAX_REGIONS || !regions)
         return report_error(GS_ERR_INVALID_ARG, fn);
@@ -285,5 +304,31 @@ extern "C" int gs_rows_compact(const uint8_t* live, long long n, long long* rows
                        count_scratch + 1);
     hipLaunchKernelGGL(k_compact_write, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, live, n, (int)per,
                        count_scratch + 1, rows, count_scratch);
+    return launched();
+}
+
+extern "C" int gs_rows_zero_dirty(float* rows, long long pitch, int width, uint8_t* dirty, long long n,
+                                  gs_stream_t stream) {
+    using namespace gs;
+    if (n < 0 || (n > 0 && (!rows || !dirty)) || width < 0 || width > pitch || (pitch & 3) || (width & 3) ||
+        (reinterpret_cast<uintptr_t>(rows) & 15))
+        return report_error(GS_ERR_INVALID_ARG, "gs_rows_zero_dirty: bad arguments (16-B rows, 4-float pitch/width)");
+    if (n == 0 || width == 0) return GS_OK;
+    const long long blocks = (n * 16 + 255) / 256;
+    if (blocks > 0x7FFFFFFF) return report_error(GS_ERR_INVALID_ARG, "gs_rows_zero_dirty: n too large");
+    hipLaunchKernelGGL(k_rows_zero_dirty, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, rows, pitch, width,
+                       dirty, n);
+    return launched();
+}
+
+extern "C" int gs_rows_mark_dirty(uint8_t* dirty, const long long* rows, long long m, const long long* count,
+                                  gs_stream_t stream) {
+    using namespace gs;
+    if (m < 0 || (m > 0 && (!dirty || !rows))) return report_error(GS_ERR_INVALID_ARG, "gs_rows_mark_dirty: bad arguments");
+    if (m == 0) return GS_OK;
+    const long long blocks = (m + 255) / 256;
+    if (blocks > 0x7FFFFFFF) return report_error(GS_ERR_INVALID_ARG, "gs_rows_mark_dirty: m too large");
+    hipLaunchKernelGGL(k_rows_mark_dirty, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, dirty, rows, m,
+                       count);
     return launched();
 }

@@ -467,6 +467,7 @@ struct GaussBwdArgs {
     uint32_t acc;  // GS_ACC_* bits: add into the output instead of overwriting
     uint32_t zeroed;  // acc bits whose outputs hold zeros: a Gaussian's first write stores (gs_grads.zeroed)
     uint32_t slot_cap = 0xFFFFFFFFu;  // binning capacity (a speculative forward's slots end there)
+    uint8_t* dirty = nullptr;  // optional [rows] (gs_grads.dirty_rows): k_gauss_live marks the live rows
     const uint8_t* grad_mask;  // optional [P]: outputs in mask_bits are multiplied by it
     uint32_t mask_bits;
     float* dL_dconic;          // optional [P,3]: the summed conic gradient (parity tests)

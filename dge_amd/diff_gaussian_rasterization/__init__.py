@@ -220,6 +220,7 @@ class _RasterizeGaussiansFused(torch.autograd.Function):
                 geomBuffer, ctx.num_rendered, binningBuffer, imgBuffer, rs.debug)
         _serialize_scratch(ctx, xyz.device)
         _ZEROED.pop(xyz.device.index, None)  # (this backward writes .grad: the buffer is no longer all zeros)
+        _DIRTY.pop(xyz.device.index, None)   # (... at rows it does not record)
         m2 = getattr(ctx, "means2D", None)
         m2_mode = _accumulation_mode(m2, node(1))[0] if into and _DEFER_PASSES else None
         if (m2_mode is not None and ctx.index is None and ctx.has_sh and not rs.debug
@@ -331,6 +332,24 @@ _SIDE_STREAMS = False  # set once dge_amd.multiview.stream_pool hands out stream
 # in-place write shows as a version change).  A batched backward whose .grad targets all lie in it stores
 # each Gaussian's first gradient instead of adding it (gs_grads.zeroed: the zeros are never read).
 _ZEROED = {}
+# device index -> [flat, dirty, version]: a row-major GradBucket's record of the rows written since its last
+# clear (gs_grads.dirty_rows: the batched backward marks its live rows; the sparse all-reduce marks the rows
+# it scatters).  Valid while the buffer's version is unchanged and no unmarked writer ran (the per-view fused
+# backward drops it): the bucket's next zero() then clears those rows only (gs_rows_zero_dirty).
+_DIRTY = {}
+
+
+def dirty_rows(dev, tensors):
+    """The dirty-row mask (a uint8 tensor) of the tracked bucket on `dev` if every tensor lies in it, else None."""
+    rec = _DIRTY.get(dev.index)
+    if rec is None or rec[0]._version != rec[2]:
+        return None
+    flat = rec[0]
+    lo, hi = flat.data_ptr(), flat.data_ptr() + 4 * flat.numel()
+    for t in tensors:
+        if t is None or not (lo <= t.data_ptr() and t.data_ptr() + 4 * t.numel() <= hi):
+            return None
+    return rec[1]
 
 
 def zeroed_bits(dev, tensors, bits: int) -> int:

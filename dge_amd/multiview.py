@@ -23,6 +23,7 @@ from __future__ import annotations
 from typing import Sequence
 
 import ctypes
+import weakref
 
 import os
 
@@ -35,6 +36,12 @@ def shard_views(num_views: int, world: int, rank: int) -> range:
     base, extra = divmod(num_views, world)
     start = rank * base + min(rank, extra)
     return range(start, start + base + (1 if rank < extra else 0))
+
+
+# the dirty-row masks of the row-major GPU buckets, by their rows' address (the sparse all-reduce's scatter
+# marks the rows it writes: _rows_scatter); DGE_AMD_SPARSE_ZERO=0 clears the whole bucket every zero()
+_DIRTY_BY_ROWS = weakref.WeakValueDictionary()
+_SPARSE_ZERO = os.environ.get("DGE_AMD_SPARSE_ZERO", "1") != "0"
 
 
 class GradBucket:
@@ -70,6 +77,9 @@ class GradBucket:
             pitch = max(16, (c + 15) // 16 * 16)
             self.flat = torch.zeros(n * pitch, dtype=torch.float32, device=dev)
             self.rows = self.flat.view(n, pitch)
+            if self.flat.is_cuda:  # (the rows written since the last zero(): a sparse clear, gs_rows_zero_dirty)
+                self._dirty = torch.zeros(n, dtype=torch.uint8, device=dev)
+                _DIRTY_BY_ROWS[self.rows.data_ptr()] = self._dirty
             for i, p in enumerate(self.params):
                 self.views.append(self.rows[:, cols[i]:cols[i] + widths[i]].view(p.shape))
         else:
@@ -80,6 +90,8 @@ class GradBucket:
                 self.views.append(self.flat[off:off + p.numel()].view_as(p))
                 off += p.numel()
         self._rows_cap = 0       # speculated packed rows of the next sparse all-reduce (0: none yet)
+        if not hasattr(self, "_dirty"):
+            self._dirty = None
         self._deferred = None    # an allreduce_end(defer_check=True) awaiting allreduce_finalize()
         self.attach()
 
@@ -121,7 +133,7 @@ class GradBucket:
                     stream.wait_stream(torch.cuda.current_stream(dev))
                 if reduced is not None:
                     stream.wait_event(reduced)
-                self.flat.zero_()
+                self._clear()
                 self._zero_event = stream.record_event()
             _r._SIDE_STREAMS = True
             _r._GRAD_WRITES[dev.index] = (stream, self._zero_event)
@@ -130,7 +142,7 @@ class GradBucket:
             return
         if reduced is not None:
             torch.cuda.current_stream(self.flat.device).wait_event(reduced)
-        self.flat.zero_()
+        self._clear()
         if self.flat.is_cuda:
             from . import diff_gaussian_rasterization as _r
 
@@ -143,6 +155,34 @@ class GradBucket:
             _r._SIDE_STREAMS = True
             _r._GRAD_WRITES[dev.index] = (torch.cuda.current_stream(dev), self._zero_event)
         self.attach()
+
+    def _clear(self):
+        """Zero the buffer on the current stream: only the rows written since the last clear when every writer
+        since recorded them (the dirty-row record is intact: diff_gaussian_rasterization._DIRTY), else all of it;
+        then a fresh record."""
+        if self._dirty is None:
+            self.flat.zero_()
+            return
+        from . import _native as N
+        from . import diff_gaussian_rasterization as _r
+
+        dev = self.flat.device
+        rec = _r._DIRTY.get(dev.index)
+        if rec is not None and rec[0] is self.flat and rec[2] == self.flat._version and _SPARSE_ZERO:
+            n, pitch = self.rows.shape
+            N.check(N.lib().gs_rows_zero_dirty(self.flat.data_ptr(), pitch, pitch, self._dirty.data_ptr(), n,
+                                               torch.cuda.current_stream(dev).cuda_stream), "gs_rows_zero_dirty")
+        else:
+            self.flat.zero_()
+            self._dirty.zero_()
+        _r._DIRTY[dev.index] = [self.flat, self._dirty, self.flat._version]
+
+    def _drop_dirty(self):
+        """A write of every row not recorded in the dirty mask (a dense collective into the buffer)."""
+        if self._dirty is not None:
+            from . import diff_gaussian_rasterization as _r
+
+            _r._DIRTY.pop(self.flat.device.index, None)
 
     def wait_zero(self):
         """Make the current stream wait for an overlapped zero() (no-op otherwise)."""
@@ -280,6 +320,7 @@ class GradBucket:
                 if m > cap:
                     _rows_fixup(mats, idx, cap, m, group)
             elif 2 * m > n:  # mostly dense: packing would not pay
+                self._drop_dirty()  # (every row may change: the next zero() clears all of them)
                 dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=group)
             else:
                 rows = idx[:m]
@@ -351,6 +392,7 @@ class GradBucket:
             self.attach()
         mats = self.row_matrices()
         if not sparse or async_op or mats is None:
+            self._drop_dirty()
             return dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=group, async_op=async_op)
         n = mats[0].shape[0]
         live = _rows_live(mats, n)
@@ -358,6 +400,7 @@ class GradBucket:
         idx = torch.nonzero(live).squeeze(1)
         self._set_rows_cap(int(idx.numel()), mats)  # (the next hinted step's speculated capacity)
         if 2 * idx.numel() > n:  # mostly dense: packing would not pay
+            self._drop_dirty()
             return dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=group)
         packed = _rows_gather(mats, idx)
         dist.all_reduce(packed, op=dist.ReduceOp.SUM, group=group)
@@ -423,11 +466,16 @@ def _rows_gather(mats, idx, cap=None, count=None):
 
 
 def _rows_scatter(mats, idx, packed, cap=None, count=None):
-    """The inverse of _rows_gather: rows idx of every matrix = their columns of packed."""
+    """The inverse of _rows_gather: rows idx of every matrix = their columns of packed (and a row-major
+    bucket's dirty-row mask records them)."""
+    dirty = _DIRTY_BY_ROWS.get(mats[0].data_ptr()) if len(mats) == 1 and mats[0].is_cuda else None
     if count is not None:
         N, regs, stream = _native_rows(mats)
         N.check(N.lib().gs_rows_scatter_dev(regs, len(mats), idx.data_ptr(), cap, count.data_ptr(),
                                             packed.data_ptr(), stream), "gs_rows_scatter_dev")
+        if dirty is not None:
+            N.check(N.lib().gs_rows_mark_dirty(dirty.data_ptr(), idx.data_ptr(), cap, count.data_ptr(), stream),
+                    "gs_rows_mark_dirty")
         return
     if _native_ok(mats):
         N, regs, stream = _native_rows(mats)
@@ -435,6 +483,9 @@ def _rows_scatter(mats, idx, packed, cap=None, count=None):
         packed = packed.contiguous()
         N.check(N.lib().gs_rows_scatter(regs, len(mats), idx.data_ptr(), idx.numel(), packed.data_ptr(), stream),
                 "gs_rows_scatter")
+        if dirty is not None:
+            N.check(N.lib().gs_rows_mark_dirty(dirty.data_ptr(), idx.data_ptr(), idx.numel(), None, stream),
+                    "gs_rows_mark_dirty")
         return
     off = 0
     for m in mats:

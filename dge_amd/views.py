@@ -213,6 +213,7 @@ class _RasterizeViews(torch.autograd.Function):
         if not ctx.has_sh:
             targets["colors"] = torch.empty_like(colors) if colors is not None and colors.numel() else None
         zeroed = _R.zeroed_bits(dev, [targets[k] for k, (p, _, bit) in params.items() if acc0 & bit], acc0)
+        dirty = _R.dirty_rows(dev, [targets[k] for k in params])
         acc_all = N.ACC_MEANS3D | N.ACC_OPACITY | N.ACC_SCALES | N.ACC_ROTATIONS | (N.ACC_SH if ctx.has_sh else 0)
         if not ctx.has_sh and targets.get("colors") is not None:
             acc_all |= N.ACC_COLORS
@@ -237,6 +238,7 @@ class _RasterizeViews(torch.autograd.Function):
             # the first view writes (or adds into an existing .grad), the others add; into a .grad buffer
             # zeroed this step, a Gaussian's first gradient is stored, not added (gs_grads.zeroed)
             o.accumulate = acc0 if v == 0 else acc_all
+            o.dirty_rows = _C._ptr(dirty)  # (the bucket's written rows: its next zero() clears only those)
             if v == 0:
                 o.zeroed = zeroed
             if grad_mask is not None:

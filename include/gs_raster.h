@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define GS_RASTER_ABI_VERSION 18
+#define GS_RASTER_ABI_VERSION 19
 
 #define GS_OK 0
 #define GS_ERR_INVALID_ARG 1   /* AT_ERROR / std::runtime_error in the reference */
@@ -209,6 +209,11 @@ typedef struct gs_grads {         /* backward outputs, every element written */
      * two cache lines per live Gaussian instead of one or two in each of six arrays.  dL_drotations rows
      * must stay 16-byte aligned (pitch a multiple of 4).  (ABI 17) */
     int pitch_means3D, pitch_opacity, pitch_scales, pitch_rotations;
+    /* Optional [rows] bytes (NULL: none): set to 1 at the parameter row of every Gaussian whose
+     * accumulated gradients this call may write — a row-major gradient bucket's record of its nonzero rows,
+     * so its next clear zeroes only those (gs_rows_zero_dirty).  gs_views_backward / _passes take view 0's.
+     * (ABI 19) */
+    uint8_t *dirty_rows;
 } gs_grads;
 
 int gs_rasterize_forward_ex(const gs_settings *s, const gs_params *g, float *out_color, float *out_depth,
@@ -400,6 +405,14 @@ int gs_rows_gather_dev(const gs_rows_region *regions, int nreg, const long long 
                        const long long *count, float *packed, gs_stream_t stream);
 int gs_rows_scatter_dev(const gs_rows_region *regions, int nreg, const long long *rows, long long cap,
                         const long long *count, const float *packed, gs_stream_t stream);
+
+/* rows[r * pitch + c] = 0 for c < width and every r < n with dirty[r] != 0, then dirty[r] = 0: the clear of a
+ * row-major gradient bucket whose written rows the backward recorded (gs_grads.dirty_rows) — at c2 ~7% of
+ * the rows instead of a 256 MB fill.  rows 16-B aligned, pitch and width multiples of 4 (ABI 19). */
+int gs_rows_zero_dirty(float *rows, long long pitch, int width, uint8_t *dirty, long long n, gs_stream_t stream);
+/* dirty[rows[i]] = 1 for i < m (count: NULL, or m read on the device as min(m, *count)): the rows a sparse
+ * all-reduce's scatter wrote (ABI 19). */
+int gs_rows_mark_dirty(uint8_t *dirty, const long long *rows, long long m, const long long *count, gs_stream_t stream);
 
 /* Byte sizes of the opaque buffers (host arithmetic, no device work). */
 size_t gs_geometry_buffer_size(int P);

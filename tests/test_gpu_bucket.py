@@ -169,3 +169,49 @@ def test_allreduce_begin_end_one_rank(cuda_device):
             assert torch.equal(bucket.flat, before)
     finally:
         dist.destroy_process_group()
+
+
+def test_sparse_zero_clears_every_written_row(cuda_device, monkeypatch):
+    """GradBucket.zero() on a row-major GPU bucket clears only the rows written since its last clear when every
+    writer recorded them (gs_grads.dirty_rows from the batched backward's live set; the sparse all-reduce's
+    scatter), else all of it: after every step's zero() the whole bucket is 0 — with the live set moving from
+    step to step (other cameras), a torch write into a .grad in between (version change: a full clear) and a
+    per-view fused backward (an unrecorded writer: a full clear).  The step's gradients equal those of a
+    bucket cleared in full every time (DGE_AMD_SPARSE_ZERO=0)."""
+    from dge_amd.cameras import orbit_camera
+    from dge_amd.gaussian_renderer import PipelineParams, render
+    from dge_amd.scene import synthetic_scene
+
+    dev = torch.device("cuda")
+    P, W, H = 60_000, 160, 120
+    g = torch.Generator().manual_seed(2)
+    seeds = [torch.randn(3, H, W, generator=g).to(dev) for _ in range(3)]
+    bg = torch.zeros(3, device=dev)
+
+    def run(sparse):
+        monkeypatch.setattr(mv, "_SPARSE_ZERO", sparse)
+        sc = synthetic_scene(P, seed=4, radius=1.5, scale=0.03, device=dev).requires_grad_(True)
+        bucket = mv.GradBucket(sc.parameters())
+        assert bucket.rows is not None and bucket._dirty is not None
+        snaps = []
+        for step in range(5):
+            bucket.zero()
+            torch.cuda.synchronize()
+            assert int(torch.count_nonzero(bucket.flat)) == 0, f"step {step}: rows left after zero()"
+            cams = [orbit_camera(k + step, 8, W, H, device=dev) for k in range(3)]
+            if step == 3:  # a per-view fused backward: writes .grad without recording rows
+                (render(cams[0], sc, PipelineParams(), bg)["render"] * seeds[0]).sum().backward()
+            else:
+                outs = mv.render_views(cams, sc, PipelineParams(), bg, streams=3, speculate=True)
+                torch.autograd.backward([o["render"] for o in outs], seeds)
+                assert outs.check()
+            if step == 1:
+                with torch.no_grad():
+                    sc._opacity.grad.mul_(1.0)  # (a torch write: the buffer's version moves)
+            snaps.append(bucket.flat.clone())
+        return snaps
+
+    a, b = run(True), run(False)
+    for x, y in zip(a, b):
+        assert torch.equal(x, y)
+    assert any(bool(x.abs().sum() > 0) for x in a)
