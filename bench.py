@@ -185,6 +185,7 @@ def main():
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
+            os.environ.setdefault("GLOO_SOCKET_IFNAME", "lo")  # (rehearsal ranks on one host: loopback)
             dist.init_process_group(backend)
 
     from dge_amd import _native, _C

@@ -4,6 +4,7 @@ sharing one card (gloo) against the single-process loop."""
 from __future__ import annotations
 
 import ctypes
+import datetime
 import os
 import socket
 
@@ -93,11 +94,12 @@ def _c3_setup(dev, P, V, W, H):
 
 def _c3_worker(rank, world, port, P, V, W, H, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["GLOO_SOCKET_IFNAME"] = "lo"  # (gloo on loopback: the host name need not resolve)
     os.environ["MASTER_PORT"] = str(port)
     try:
         torch.cuda.set_device(0)
         dev = torch.device("cuda", 0)
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=90))
         from dge_amd.gaussian_renderer import PipelineParams, render
         from dge_amd.multiview import GradBucket, multiview_step, shard_views
 
@@ -139,7 +141,7 @@ def test_c3_two_ranks_share_one_card(cuda_device):
     procs = [ctx.Process(target=_c3_worker, args=(r, 2, port, P, V, W, H, q)) for r in range(2)]
     for p in procs:
         p.start()
-    res = [q.get(timeout=240) for _ in procs]
+    res = [q.get(timeout=150) for _ in procs]
     for p in procs:
         p.join(timeout=60)
     for rank, flat, vs, rmax, err in res:
@@ -303,11 +305,12 @@ def test_forward_only_renders_equal_training_renders(cuda_device, W, H, P):
 
 def _hinted_worker(rank, world, port, P, V, W, H, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["GLOO_SOCKET_IFNAME"] = "lo"  # (gloo on loopback: the host name need not resolve)
     os.environ["MASTER_PORT"] = str(port)
     try:
         torch.cuda.set_device(0)
         dev = torch.device("cuda", 0)
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=90))
         from dge_amd.gaussian_renderer import PipelineParams, render
         from dge_amd.multiview import GradBucket, multiview_step, shard_views
 
@@ -365,7 +368,7 @@ def test_hinted_sparse_allreduce_two_ranks(cuda_device):
     procs = [ctx.Process(target=_hinted_worker, args=(r, 2, port, P, V, W, H, q)) for r in range(2)]
     for p in procs:
         p.start()
-    res = [q.get(timeout=240) for _ in procs]
+    res = [q.get(timeout=150) for _ in procs]
     for p in procs:
         p.join(timeout=60)
     only0 = (half[0] != 0) & (half[1] == 0)
@@ -420,11 +423,12 @@ def test_zeroed_bucket_stores_first_gradient(cuda_device):
 
 def _deferred_worker(rank, world, port, P, V, W, H, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["GLOO_SOCKET_IFNAME"] = "lo"  # (gloo on loopback: the host name need not resolve)
     os.environ["MASTER_PORT"] = str(port)
     try:
         torch.cuda.set_device(0)
         dev = torch.device("cuda", 0)
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=90))
         from dge_amd.gaussian_renderer import PipelineParams
         from dge_amd.multiview import GradBucket, render_views, shard_views
 
@@ -479,7 +483,7 @@ def test_deferred_union_check_two_ranks(cuda_device, world, V):
     procs = [ctx.Process(target=_deferred_worker, args=(r, world, port, P, V, W, H, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = [q.get(timeout=240) for _ in procs]
+    res = [q.get(timeout=150) for _ in procs]
     for p in procs:
         p.join(timeout=60)
     for rank, steps, err in res:
@@ -508,11 +512,12 @@ def _seed_history(dev, P, cams, sc, small):
 
 def _overflow_worker(rank, world, port, P, V, sizes, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["GLOO_SOCKET_IFNAME"] = "lo"  # (gloo on loopback: the host name need not resolve)
     os.environ["MASTER_PORT"] = str(port)
     try:
         torch.cuda.set_device(0)
         dev = torch.device("cuda", 0)
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=90))
         from dge_amd.gaussian_renderer import PipelineParams, render
         from dge_amd.multiview import GradBucket, multiview_step, render_views, shard_views
 
@@ -596,7 +601,7 @@ def test_overflow_on_one_rank_is_agreed(cuda_device, world, V):
     procs = [ctx.Process(target=_overflow_worker, args=(r, world, port, P, V, sizes, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = [q.get(timeout=300) for _ in procs]
+    res = [q.get(timeout=150) for _ in procs]
     for p in procs:
         p.join(timeout=60)
     for rank, out, err in res:

@@ -8,6 +8,7 @@ box the same code path runs with dge_amd's render() and the nccl (RCCL)
 backend (bench.py --gpus N)."""
 from __future__ import annotations
 
+import datetime
 import os
 import socket
 import sys
@@ -96,8 +97,9 @@ def _l1_targets(V, W=32, H=32):
 
 def _worker(rank, world, port, P, V, mode, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["GLOO_SOCKET_IFNAME"] = "lo"  # (gloo on loopback: the host name need not resolve)
     os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=90))
     try:
         torch.set_num_threads(1)
         pc = _Scene(P, seed=4)
@@ -147,7 +149,7 @@ def test_sharded_step_equals_single_process(mode, world, V):
     procs = [ctx.Process(target=_worker, args=(r, world, port, P, V, mode, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = [q.get(timeout=300) for _ in procs]
+    res = [q.get(timeout=150) for _ in procs]
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -175,8 +177,9 @@ def test_grad_bucket_views_and_zero():
 
 def _sparse_worker(rank, world, port, q, row_major=False):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["GLOO_SOCKET_IFNAME"] = "lo"  # (gloo on loopback: the host name need not resolve)
     os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=90))
     try:
         torch.set_num_threads(1)
         out = {}
@@ -207,7 +210,7 @@ def test_sparse_bucket_allreduce_equals_dense(rows):
     procs = [ctx.Process(target=_sparse_worker, args=(r, 2, port, q, rows)) for r in range(2)]
     for p in procs:
         p.start()
-    res = [q.get(timeout=300) for _ in procs]
+    res = [q.get(timeout=150) for _ in procs]
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
