@@ -187,16 +187,23 @@ __global__ __launch_bounds__(256) void k_compact_write(const uint8_t* __restrict
     if (blockIdx.x == gridDim.x - 1 && tid == 0) *count = base;
 }
 
-// Four rows per wave, a 16-lane group per row (float4 columns, rows wider than 64 floats loop): the dirty
-// rows of a row-major bucket zeroed, their flags cleared.
+// One thread per row reads its flag (coalesced) and clears it; each wave then zeroes its dirty rows one after
+// another, all 64 lanes on one row (one 256-B store per 64 floats) — a grid of n / 256 workgroups, not one
+// thread per float: the clean rows cost a byte read.
 __global__ __launch_bounds__(256) void k_rows_zero_dirty(float* __restrict__ rows, long long pitch, int width,
                                                          uint8_t* __restrict__ dirty, long long n) {
-    const long long r = ((long long)blockIdx.x * 256 + threadIdx.x) >> 4;
-    const int c0 = 4 * (threadIdx.x & 15);
-    if (r >= n || !dirty[r]) return;
-    float4* row = reinterpret_cast<float4*>(rows + r * pitch);
-    for (int c = c0; c < width; c += 64) row[c >> 2] = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (c0 == 0) dirty[r] = 0;  // (this row's group only reads its own flag: no race with the other rows)
+    const long long r = (long long)blockIdx.x * 256 + threadIdx.x;
+    const int lane = threadIdx.x & 63;
+    const bool d = r < n && dirty[r];
+    if (d) dirty[r] = 0;
+    uint64_t m = __ballot(d);
+    const long long wbase = r - lane;  // the wave's first row
+    while (m) {  // (wave-uniform)
+        const int k = __ffsll((unsigned long long)m) - 1;
+        m &= m - 1;
+        float* row = rows + (wbase + k) * pitch;
+        for (int c = lane; c < width; c += 64) row[c] = 0.f;
+    }
 }
 
 __global__ __launch_bounds__(256) void k_rows_mark_dirty(uint8_t* __restrict__ dirty, const long long* __restrict__ rows,
@@ -314,7 +321,7 @@ extern "C" int gs_rows_zero_dirty(float* rows, long long pitch, int width, uint8
         (reinterpret_cast<uintptr_t>(rows) & 15))
         return report_error(GS_ERR_INVALID_ARG, "gs_rows_zero_dirty: bad arguments (16-B rows, 4-float pitch/width)");
     if (n == 0 || width == 0) return GS_OK;
-    const long long blocks = (n * 16 + 255) / 256;
+    const long long blocks = (n + 255) / 256;
     if (blocks > 0x7FFFFFFF) return report_error(GS_ERR_INVALID_ARG, "gs_rows_zero_dirty: n too large");
     hipLaunchKernelGGL(k_rows_zero_dirty, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, rows, pitch, width,
                        dirty, n);
