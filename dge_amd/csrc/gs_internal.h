@@ -145,10 +145,13 @@ inline GeomLayout geom_layout(int P) {
 // ranges are a prefix sum), each slot 4 quadrants x 64 pixels x float4.
 constexpr int kBlendRound = 256;  // list entries per blend round
 // Replay work items are listed by class of their blended-entry count, heaviest first (the hardware
-// dispatches workgroups in order: the longest items start first, the short ones fill the end);
-// class c holds up to item_cap items at bwd_items[c * item_cap ..), counted in bwd_count[item_count_at(c)]
-constexpr int kItemClasses = 4, kItemCount0 = 32;
-__host__ __device__ inline int item_count_at(int c) { return kItemCount0 * (1 + c); }  // u32 index, 128-B lines
+// dispatches workgroups in order: the longest items start first, the short ones fill the end).  Each
+// class keeps one list per XCD group of the forward (kItemXcds: the forward's rank & 7, the XCD its
+// tile's four quadrant waves ran on): list (c, x) holds up to item_cap items at
+// bwd_items[(c * kItemXcds + x) * item_cap ..), counted in bwd_count[item_count_at(c, x)], and the
+// replay runs list x on one XCD, so a tile's four quadrants gather its list and Splats into one L2
+constexpr int kItemClasses = 4, kItemXcds = 8, kItemCount0 = 32;
+__host__ __device__ inline int item_count_at(int c, int x) { return kItemCount0 * (1 + c * kItemXcds + x); }  // 128-B lines
 // backward segment length: checkpoints at every round boundary and mid-round, so a replay work item
 // covers at most 128 positions (half the per-item work of round-long segments: the replay's wave
 // durations pack onto the SIMDs instead of leaving a tail of long items)
@@ -182,8 +185,7 @@ inline ImgLayout img_layout(int W, int H) {
     L.ranges = o; o = align_up(o + 8 * tiles);
     L.tile_last = o; o = align_up(o + 4 * tiles);
     L.quad_last = o; o = align_up(o + 16 * tiles);
-    L.bwd_count = o; o = align_up(o + 4 * (size_t)item_count_at(kItemClasses));  // [0..3] the per-tile variant's;
-                                                                                 // [item_count_at(c)] class c items
+    L.bwd_count = o; o = align_up(o + 4 * (size_t)item_count_at(kItemClasses, 0));  // [item_count_at(c, x)]
     L.aux = o; o = align_up(o + 8 * n);  // float2 per pixel: the aux_mask grey sum (before bg), depth
     L.total = o;
     return L;
@@ -222,7 +224,7 @@ inline BinLayout bin_layout(int K, int num_tiles, bool bwd = true) {
     L.records = o; o = align_up(o + 4 * 48 * kb);  // one record per (slot, quadrant)
     L.rec_flags = o; o = align_up(o + 4 * kb);
     L.ckpt = o; o = align_up(o + 16 * 64 * 4 * L.nslots);  // [slot][quadrant][64] float4 (T, own colour sum)
-    L.bwd_items = o; o = align_up(o + 8 * 4 * L.nslots * kItemClasses);  // uint2 (tile, seg << 2 | quadrant)
+    L.bwd_items = o; o = align_up(o + 8 * 4 * L.nslots * kItemClasses * kItemXcds);  // uint2 (tile, seg << 2 | quadrant)
     L.used = o; o = align_up(o + (bwd ? 8 * used_words(k, num_tiles) : 0));
     L.total = o;
     return L;

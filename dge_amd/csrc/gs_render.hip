@@ -214,14 +214,15 @@ __global__ __launch_bounds__(1024) void k_tile_order(const uint2* __restrict__ r
 // workgroups in order, so the longest items start first and the short ones fill the end).  One atomic
 // per wave, each class's counter on its own cache line (same-address atomics serialise).
 __device__ __forceinline__ int item_class(uint32_t kept) { return kept >= 64 ? 0 : kept >= 40 ? 1 : kept >= 20 ? 2 : 3; }
-__device__ __forceinline__ void emit_items(const RenderArgs& a, int tile, int quad, uint32_t nseg, uint32_t nkept,
-                                           int lane) {
+// List x (the forward's XCD group, rank & 7) keeps a tile's four quadrants together (see kItemXcds).
+__device__ __forceinline__ void emit_items(const RenderArgs& a, int tile, int quad, int x, uint32_t nseg,
+                                           uint32_t nkept, int lane) {
     const int c = item_class(nkept / nseg);
     uint32_t base = 0;
-    if (lane == 0) base = atomicAdd(&a.bwd_count[item_count_at(c)], nseg);
+    if (lane == 0) base = atomicAdd(&a.bwd_count[item_count_at(c, x)], nseg);
     base = __shfl(base, 0);
-    for (uint32_t k = lane; k < nseg; k += 64)
-        a.bwd_items[(size_t)c * a.item_cap + base + k] = make_uint2((uint32_t)tile, (k << 2) | (uint32_t)quad);
+    uint2* list = a.bwd_items + (size_t)(c * kItemXcds + x) * a.item_cap;
+    for (uint32_t k = lane; k < nseg; k += 64) list[base + k] = make_uint2((uint32_t)tile, (k << 2) | (uint32_t)quad);
 }
 
 // BWD: the backward's bookkeeping (checkpoints, blended bits, touched bytes, the replay's work list);
@@ -568,7 +569,7 @@ __global__ __launch_bounds__(64, 3) void k_render_fwd(RenderArgs a) {
     const uint32_t m = wave_max_u32(inside ? last : 0u);
     // (item class from the entries the cull kept — the diagnostics' count, live anyway: a blended-entry
     // count here pushed the kernel into spilling)
-    if (BWD && m) emit_items(a, tile, quad, (m + kSegLen - 1) / kSegLen, diag_kept, lane);
+    if (BWD && m) emit_items(a, tile, quad, x8, (m + kSegLen - 1) / kSegLen, diag_kept, lane);
     if (lane == 0) {
         a.quad_last[qidx] = m;
         if (m) atomicMax(&a.tile_last[tile], m);
@@ -813,25 +814,57 @@ __global__ __launch_bounds__(64, GS_BWD_WAVES) void k_render_bwd(RenderBwdArgs a
     __shared__ uint32_t s_pos[kBwdHalf + kBwdGroup];
     __shared__ uint2 s_pair[kBwdHalf + kBwdGroup];  // (Gaussian, slot) of the kept entries: the record writes
     const int lane = threadIdx.x;
-    // block -> work item (quadrant, segment) of the forward's list, heaviest class first; blocks past
-    // the list's end exit (they dispatch after every real item; see launch_render_backward for the
-    // grid).  (A persistent-wave work queue measured slower than the hardware dispatcher here.)
-    uint32_t n_cls[kItemClasses], n_items = 0;
+    // block -> work item (quadrant, segment) of the forward's lists, heaviest class first.  Class c's
+    // region is 8 x (its longest XCD list) blocks; block b of it (b & 7 = its XCD under the round-robin
+    // dealing) takes item b >> 3 of list (c, b & 7), so a tile's quadrants replay on one XCD and share
+    // its L2.  Should the regions outgrow the grid (lists far out of balance; the grid bounds only their
+    // total), the blocks take the lists one after another instead.  Blocks past the end exit (they
+    // dispatch after every real item; see launch_render_backward for the grid).  (A persistent-wave
+    // work queue measured slower than the hardware dispatcher here.)
+    const uint32_t nl = lane < kItemClasses * kItemXcds ? a.bwd_count[item_count_at(lane >> 3, lane & 7)] : 0u;
+    // (list l's count: readlane(nl, l), a block-uniform lane select — no indexed array, no scratch)
+    const auto n_list = [&](int l) { return (uint32_t)__builtin_amdgcn_readlane((int)nl, l); };
+    uint32_t region[kItemClasses], need = 0, total = 0;
 #pragma unroll
     for (int c = 0; c < kItemClasses; ++c) {
-        n_cls[c] = a.bwd_count[item_count_at(c)];
-        n_items += n_cls[c];
+        uint32_t m = 0;
+#pragma unroll
+        for (int x = 0; x < kItemXcds; ++x) {
+            const uint32_t v = n_list(c * kItemXcds + x);
+            m = v > m ? v : m;
+            total += v;
+        }
+        region[c] = kItemXcds * m;
+        need += region[c];
     }
     const uint32_t qi = blockIdx.x;
-    if (qi >= n_items) return;
-    uint32_t cls = 0, idx = qi;  // class regions in order: heaviest items first
+    int list = -1;
+    uint32_t idx = 0;
+    if (need <= gridDim.x) {
+        uint32_t o = qi;
 #pragma unroll
-    for (int c = 0; c < kItemClasses - 1; ++c)
-        if (cls == (uint32_t)c && idx >= n_cls[c]) {
-            idx -= n_cls[c];
-            cls = c + 1;
+        for (int c = 0; c < kItemClasses; ++c) {
+            if (list < 0 && o < region[c]) {
+                const int x = (int)(o & (kItemXcds - 1));
+                idx = o / kItemXcds;
+                list = idx < n_list(c * kItemXcds + x) ? c * kItemXcds + x : kItemClasses * kItemXcds;
+            }
+            if (list < 0) o -= region[c];
         }
-    const uint2 item = a.bwd_items[(size_t)cls * a.item_cap + idx];
+    } else if (qi < total) {
+        uint32_t o = qi;
+#pragma unroll
+        for (int l = 0; l < kItemClasses * kItemXcds; ++l) {
+            const uint32_t v = n_list(l);
+            if (list < 0 && o < v) {
+                list = l;
+                idx = o;
+            }
+            if (list < 0) o -= v;
+        }
+    }
+    if (list < 0 || list >= kItemClasses * kItemXcds) return;
+    const uint2 item = a.bwd_items[(size_t)list * a.item_cap + idx];
     const int tile = (int)item.x, quad = (int)(item.y & 3u), seg = (int)(item.y >> 2);
     const int qidx = 4 * tile + quad;
     const int tx = tile % a.gx, ty = tile / a.gx;
