@@ -151,7 +151,11 @@ constexpr int kBlendRound = 256;  // list entries per blend round
 // bwd_items[(c * kItemXcds + x) * item_cap ..), counted in bwd_count[item_count_at(c, x)], and the
 // replay runs list x on one XCD, so a tile's four quadrants gather its list and Splats into one L2
 constexpr int kItemClasses = 4, kItemXcds = 8, kItemCount0 = 32;
-__host__ __device__ inline int item_count_at(int c, int x) { return kItemCount0 * (1 + c * kItemXcds + x); }  // 128-B lines
+// (count (c, x) on XCD group x's 128-B line; each class's longest list on line 0, an atomicMax beside each
+// list's atomicAdd: a replay workgroup reads the four maxima and its own list's count, 5 scalar loads —
+// the ~100k surplus workgroups of a speculated grid exit after the first four)
+__host__ __device__ inline int item_count_at(int c, int x) { return kItemCount0 * (2 + x) + c; }
+__host__ __device__ inline int item_max_at(int c) { return kItemCount0 + c; }
 // backward segment length: checkpoints at every round boundary and mid-round, so a replay work item
 // covers at most 128 positions (half the per-item work of round-long segments: the replay's wave
 // durations pack onto the SIMDs instead of leaving a tail of long items)
@@ -185,7 +189,7 @@ inline ImgLayout img_layout(int W, int H) {
     L.ranges = o; o = align_up(o + 8 * tiles);
     L.tile_last = o; o = align_up(o + 4 * tiles);
     L.quad_last = o; o = align_up(o + 16 * tiles);
-    L.bwd_count = o; o = align_up(o + 4 * (size_t)item_count_at(kItemClasses, 0));  // [item_count_at(c, x)]
+    L.bwd_count = o; o = align_up(o + 4 * (size_t)item_count_at(0, kItemXcds));  // [item_max_at(c)], [item_count_at(c, x)]
     L.aux = o; o = align_up(o + 8 * n);  // float2 per pixel: the aux_mask grey sum (before bg), depth
     L.total = o;
     return L;

@@ -219,7 +219,10 @@ __device__ __forceinline__ void emit_items(const RenderArgs& a, int tile, int qu
                                            uint32_t nkept, int lane) {
     const int c = item_class(nkept / nseg);
     uint32_t base = 0;
-    if (lane == 0) base = atomicAdd(&a.bwd_count[item_count_at(c, x)], nseg);
+    if (lane == 0) {
+        base = atomicAdd(&a.bwd_count[item_count_at(c, x)], nseg);
+        atomicMax(&a.bwd_count[item_max_at(c)], base + nseg);
+    }
     base = __shfl(base, 0);
     uint2* list = a.bwd_items + (size_t)(c * kItemXcds + x) * a.item_cap;
     for (uint32_t k = lane; k < nseg; k += 64) list[base + k] = make_uint2((uint32_t)tile, (k << 2) | (uint32_t)quad);
@@ -821,49 +824,48 @@ __global__ __launch_bounds__(64, GS_BWD_WAVES) void k_render_bwd(RenderBwdArgs a
     // total), the blocks take the lists one after another instead.  Blocks past the end exit (they
     // dispatch after every real item; see launch_render_backward for the grid).  (A persistent-wave
     // work queue measured slower than the hardware dispatcher here.)
-    const uint32_t nl = lane < kItemClasses * kItemXcds ? a.bwd_count[item_count_at(lane >> 3, lane & 7)] : 0u;
-    // (list l's count: readlane(nl, l), a block-uniform lane select — no indexed array, no scratch)
-    const auto n_list = [&](int l) { return (uint32_t)__builtin_amdgcn_readlane((int)nl, l); };
-    uint32_t region[kItemClasses], need = 0, total = 0;
+    const uint32_t qi = blockIdx.x;
+    uint32_t region[kItemClasses], need = 0;
 #pragma unroll
     for (int c = 0; c < kItemClasses; ++c) {
-        uint32_t m = 0;
-#pragma unroll
-        for (int x = 0; x < kItemXcds; ++x) {
-            const uint32_t v = n_list(c * kItemXcds + x);
-            m = v > m ? v : m;
-            total += v;
-        }
-        region[c] = kItemXcds * m;
+        region[c] = kItemXcds * a.bwd_count[item_max_at(c)];
         need += region[c];
     }
-    const uint32_t qi = blockIdx.x;
-    int list = -1;
-    uint32_t idx = 0;
+    int list;
+    uint32_t idx;
     if (need <= gridDim.x) {
+        if (qi >= need) return;
         uint32_t o = qi;
+        int c = 0;
 #pragma unroll
-        for (int c = 0; c < kItemClasses; ++c) {
-            if (list < 0 && o < region[c]) {
-                const int x = (int)(o & (kItemXcds - 1));
-                idx = o / kItemXcds;
-                list = idx < n_list(c * kItemXcds + x) ? c * kItemXcds + x : kItemClasses * kItemXcds;
+        for (int k = 0; k < kItemClasses - 1; ++k)
+            if (c == k && o >= region[k]) {
+                o -= region[k];
+                c = k + 1;
             }
-            if (list < 0) o -= region[c];
-        }
-    } else if (qi < total) {
+        const int x = (int)(o % kItemXcds);
+        idx = o / kItemXcds;
+        if (idx >= a.bwd_count[item_count_at(c, x)]) return;
+        list = c * kItemXcds + x;
+    } else {
+        // (lane c * 8 + x loads count (c, x); readlane(nl, l) is list l's count: a block-uniform lane
+        // select, no indexed array)
+        const uint32_t nl =
+            lane < kItemClasses * kItemXcds ? a.bwd_count[item_count_at(lane / kItemXcds, lane % kItemXcds)] : 0u;
         uint32_t o = qi;
+        list = -1;
+        idx = 0;
 #pragma unroll
         for (int l = 0; l < kItemClasses * kItemXcds; ++l) {
-            const uint32_t v = n_list(l);
+            const uint32_t v = (uint32_t)__builtin_amdgcn_readlane((int)nl, l);
             if (list < 0 && o < v) {
                 list = l;
                 idx = o;
             }
             if (list < 0) o -= v;
         }
+        if (list < 0) return;
     }
-    if (list < 0 || list >= kItemClasses * kItemXcds) return;
     const uint2 item = a.bwd_items[(size_t)list * a.item_cap + idx];
     const int tile = (int)item.x, quad = (int)(item.y & 3u), seg = (int)(item.y >> 2);
     const int qidx = 4 * tile + quad;

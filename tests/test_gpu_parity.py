@@ -156,6 +156,30 @@ def test_known_answer_single_gaussian(cuda_device, oracle):
     assert got["num_rendered"] == 4 and got["radii"][0] == 5
 
 
+@pytest.mark.parametrize("W,H", [(16, 16), (32, 16)], ids=["one_tile", "two_tiles"])
+def test_replay_lists_out_of_balance(cuda_device, oracle, W, H):
+    """The replay's work lists are per forward XCD group (kItemXcds, gs_internal.h): one tile puts every
+    item in one of the eight lists, so 8 x the longest list outgrows the grid (4 x checkpoint slots) and
+    k_render_bwd takes the lists one after another; two tiles leave six lists empty (the XCD mapping's
+    regions mostly holes).  Faint Gaussians: no pixel saturates, every quadrant's window is its whole list."""
+    a = scene_arrays(3000, seed=17, radius=0.4, scale=0.05)
+    kw = _sh_kw(a)
+    kw["opacities"] = np.full_like(a["opacities"], 0.02)
+    g = np.random.default_rng(9).standard_normal((3, H, W)).astype(np.float32)
+    ref = run_oracle(oracle, camera_settings(W, H), g, **kw)
+    got = run_gpu(camera_settings(W, H, device="cuda"), g, **kw)
+    compare_forward(got, ref, label=f"lists {W}x{H}")
+    compare_grads(got, ref, O=oracle, label=f"lists {W}x{H}")
+    # the fallback's condition, from the forward's windows: a tile's items sit in one list, whose longest
+    # class holds at least a quarter of them
+    tiles = (W // 16) * (H // 16)
+    nc = got["n_contrib"].reshape(H // 16, 2, 8, W // 16, 2, 8)
+    items = np.ceil(nc.max(axis=(2, 5)) / 128).reshape(H // 16, 2, W // 16, 2).sum(axis=(1, 3)).ravel()
+    grid = 4 * (got["num_rendered"] // 128 + tiles + 2)
+    print(f"[parity] replay lists: items per tile {items.tolist()}, grid {grid}")
+    assert (8 * np.ceil(items.max() / 4) > grid) == (tiles == 1)
+
+
 def test_prefiltered_error_is_reported(cuda_device):
     from dge_amd._native import NativeError
 

@@ -63,6 +63,11 @@ def summarize(name, d, nquads=None):
             ov = [min(end[i], end[j]) - max(start[i], start[j]) for j in mates]
             print(f"   slowest wave {ids[i]}: {len(mates)} SIMD mates, overlap-us {[round(o * 10e-3, 1) for o in ov]}, "
                   f"their durations {[round(float(dur[j]), 1) for j in mates]}")
+    if loc.any():  # per XCD: its last wave's end, summed wave time and waves (balance across the 8 L2s)
+        xcc = loc >> 32
+        print("   per XCD end/us, wave-us, waves:", " ".join(
+            f"{int(x)}:{(end[xcc == x].max() - t0) * 10e-3:.0f}/{dur[xcc == x].sum():.0f}/{int((xcc == x).sum())}"
+            for x in np.unique(xcc)))
     ts = np.linspace(0, span, 11)
     alive = [int(((start - t0) * 10e-3 <= t).sum() - ((end - t0) * 10e-3 <= t).sum()) for t in ts]
     print("   waves running over time:", " ".join(f"{t:.0f}:{a}" for t, a in zip(ts, alive)))
