@@ -89,9 +89,12 @@ inline TileSortPlan tile_sort_plan(int num_tiles) {
 // 2D mean, conic + opacity, colour + depth (forward.cu:251-255 outputs).
 struct alignas(64) Splat {
     float2 xy;
-    float2 aux;   // x: gs_params.aux_mask as 0/1 (the grey value the blend composites beside the colour)
+    float2 pad0;
     float4 co;    // conic (a, b, c) + opacity
-    float4 rgbd;  // colour + view depth
+    // colour + view depth; the depth NEGATED where gs_params.aux_mask marks the Gaussian (the grey value 1 the
+    // blend composites beside the colour): a touched Gaussian's depth is > 0.2, so its sign is a free bit the
+    // gather brings along, and every reader takes |w|
+    float4 rgbd;
     float4 pad1;
 };
 
@@ -185,12 +188,13 @@ inline ImgLayout img_layout(int W, int H) {
     L.final_T = o; o = align_up(o + 4 * n);
     L.n_contrib = o; o = align_up(o + 4 * n);
     L.tile_order = o; o = align_up(o + 4 * tiles);  // tiles by list length, longest first
+    // (before the counters: every pixel is written by the blend that fills it, the memset skips its 8 B/pixel)
+    L.aux = o; o = align_up(o + 8 * n);  // float2 per pixel: the aux_mask grey sum (before bg), depth
     L.counters = o; o = align_up(o + 4 * kCounterSlots * kCounterStride);  // counters.. zeroed per forward (one memset)
     L.ranges = o; o = align_up(o + 8 * tiles);
     L.tile_last = o; o = align_up(o + 4 * tiles);
     L.quad_last = o; o = align_up(o + 16 * tiles);
     L.bwd_count = o; o = align_up(o + 4 * (size_t)item_count_at(0, kItemXcds));  // [item_max_at(c)], [item_count_at(c, x)]
-    L.aux = o; o = align_up(o + 8 * n);  // float2 per pixel: the aux_mask grey sum (before bg), depth
     L.total = o;
     return L;
 }
@@ -273,7 +277,7 @@ struct PreprocessArgs {
     int rect_packed;
     uint32_t* counters;  // kCounterSlots x kCounterStride (ImgLayout)
     uint8_t* touched;    // zeroed here: k_render_fwd sets the bytes of Gaussians some pixel blends
-    const uint8_t* aux_mask = nullptr;  // gs_params.aux_mask: 0/1 into the Splat's aux slot
+    const uint8_t* aux_mask = nullptr;  // gs_params.aux_mask: the sign of the Splat's depth
 };
 void launch_preprocess(const PreprocessArgs& a, hipStream_t s);
 void launch_depth_keys32(int P, const uint32_t* rect, const Splat* splat, uint32_t* key, hipStream_t s);

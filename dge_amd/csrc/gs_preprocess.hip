@@ -87,7 +87,7 @@ __global__ __launch_bounds__(256) void k_preprocess(PreprocessArgs a) {
     float2 pix = make_float2(0.f, 0.f);
     float4 conic = make_float4(0.f, 0.f, 0.f, 0.f);
     float depth = 0.f;
-    float auxv = 0.f;  // gs_params.aux_mask as 0/1
+    bool auxv = false;  // gs_params.aux_mask
     // SH rows of the whole block staged first, in flight together with the per-Gaussian loads below
     // (one memory phase instead of geometry -> compute -> SH rows); rows of Gaussians that turn out
     // culled are read needlessly (180 B each), which object-centric views hardly have
@@ -152,7 +152,7 @@ __global__ __launch_bounds__(256) void k_preprocess(PreprocessArgs a) {
             sc = ld3(a.scales + 3 * (size_t)src);
         }
         const float op_in = a.opacities[src];
-        if (a.aux_mask) auxv = a.aux_mask[src] ? 1.0f : 0.0f;
+        if (a.aux_mask) auxv = a.aux_mask[src] != 0;
         // in_frustum (auxiliary.h:139-164): only the near test is live
         const float4 ph = proj_point(pm, p);
         const float pw = 1.0f / (ph.w + 0.0000001f);
@@ -222,9 +222,9 @@ __global__ __launch_bounds__(256) void k_preprocess(PreprocessArgs a) {
         if (touched) {  // (whole 64-B records: writing only the used 40 B measured slower — partial lines)
             Splat sp;
             sp.xy = pix;
-            sp.aux = make_float2(auxv, 0.f);
+            sp.pad0 = make_float2(0.f, 0.f);
             sp.co = conic;
-            sp.rgbd = make_float4(rgb.x, rgb.y, rgb.z, depth);
+            sp.rgbd = make_float4(rgb.x, rgb.y, rgb.z, auxv ? -depth : depth);  // (Splat: the aux bit)
             sp.pad1 = make_float4(0.f, 0.f, 0.f, 0.f);
             a.splat[idx] = sp;
         }
@@ -284,7 +284,7 @@ __global__ __launch_bounds__(256) void k_depth_keys32(int P, const uint32_t* __r
                                                       const Splat* __restrict__ splat, uint32_t* __restrict__ key) {
     const int i = blockIdx.x * 256 + threadIdx.x;
     if (i >= P) return;
-    key[i] = rect[i] ? __float_as_uint(splat[i].rgbd.w) : 0xFFFFFFFFu;
+    key[i] = rect[i] ? __float_as_uint(fabsf(splat[i].rgbd.w)) : 0xFFFFFFFFu;
 }
 
 void launch_depth_keys32(int P, const uint32_t* rect, const Splat* splat, uint32_t* key, hipStream_t s) {

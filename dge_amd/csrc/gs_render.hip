@@ -272,10 +272,8 @@ __global__ __launch_bounds__(64, 3) void k_render_fwd(RenderArgs a) {
     __shared__ __attribute__((aligned(16))) float s_x[kRoundLds], s_y[kRoundLds];
     __shared__ __attribute__((aligned(16))) float s_cx[kRoundLds], s_cy[kRoundLds], s_cz[kRoundLds], s_op[kRoundLds];
     __shared__ float4 s_rgbd[kRoundLds];
-    __shared__ __attribute__((aligned(16))) uint8_t s_mb[AUX ? kRoundLds : 4];  // (AUX) kept entries' aux bit
-    // (AUX) the next round's aux values in list order, loaded global -> LDS with its gathers: no registers
-    // held across the blend (the kernel sits at its 168-VGPR bound)
-    __shared__ float s_mnext[AUX ? kRound : 64];
+    // (AUX) kept entries' aux bit: the sign of the gathered depth (Splat), no load of its own
+    __shared__ __attribute__((aligned(16))) uint8_t s_mb[AUX ? kRoundLds : 4];
     __shared__ __attribute__((aligned(16))) uint32_t s_pos[kRoundLds];
     __shared__ uint32_t s_gused[kRoundLds / kGroup];  // per blend group: bit u = entry u was blended
     __shared__ uint32_t s_id[kRoundLds];              // the kept entries' Gaussians (the touched bytes)
@@ -327,23 +325,12 @@ __global__ __launch_bounds__(64, 3) void k_render_fwd(RenderArgs a) {
         }
         return e;
     };
-    // (AUX) entry 64 i + lane's aux value -> s_mnext[64 i + lane]
-    const auto load_aux = [&](const uint32_t (&id)[4]) {
-        if constexpr (AUX) {
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-                __builtin_amdgcn_global_load_lds(
-                    (__attribute__((address_space(1))) void*)&a.splat[id[i]].aux.x,
-                    (__attribute__((address_space(3))) void*)(s_mnext + 64 * i), 4, 0, 0);
-        }
-    };
     load_ids(range.x, ids);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         cur[i] = gather(ids[i]);
         cid[i] = ids[i];
     }
-    load_aux(ids);
     load_ids(range.x + kRound, ids);
 
     // checkpoint of segment k of this quadrant: slot ckpt_base + k, quadrant `quad`: (T after it, its own
@@ -376,9 +363,6 @@ __global__ __launch_bounds__(64, 3) void k_render_fwd(RenderArgs a) {
         // the blend loops over them
         int nk = 0, n_mid = 0;
         int kslot[4];  // compacted slot of this lane's entry i (-1: culled)
-        // (AUX: the round's aux values came global -> LDS, which the compiler does not track: every load of
-        // the previous round done — the gathers the cull reads were issued before them anyway)
-        if constexpr (AUX) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             if (i == kSegLen / 64) {
@@ -409,8 +393,10 @@ __global__ __launch_bounds__(64, 3) void k_render_fwd(RenderArgs a) {
                 s_cy[slot] = -cur[i].co.y;  // (negated: pixel_alpha4)
                 s_cz[slot] = -cur[i].co.z;
                 s_op[slot] = cur[i].co.w;
-                s_rgbd[slot] = cur[i].f;
-                if constexpr (AUX) s_mb[slot] = s_mnext[64 * i + lane] != 0.0f ? 1 : 0;
+                // (|depth|: the sign is the aux bit, Splat; every variant strips it — a recolor may blend
+                // the lists of a forward that had an aux mask)
+                s_rgbd[slot] = make_float4(cur[i].f.x, cur[i].f.y, cur[i].f.z, fabsf(cur[i].f.w));
+                if constexpr (AUX) s_mb[slot] = cur[i].f.w < 0.0f ? 1 : 0;
                 s_pos[slot] = k - range.x + 1;  // 1-based contributor index (forward.cu:331)
                 s_id[slot] = cid[i];
             }
@@ -437,8 +423,6 @@ __global__ __launch_bounds__(64, 3) void k_render_fwd(RenderArgs a) {
             cur[i] = gather(ids[i]);
             cid[i] = ids[i];
         }
-        if constexpr (AUX) __builtin_amdgcn_s_waitcnt(0xC07F);  // (the compaction's s_mnext reads are done)
-        load_aux(ids);
         load_ids(b + 2 * kRound, ids);
         if (seg_done >= 0) put_ckpt(seg_done);  // the previous segment's: the replay's start
         seg_done = (int)((b - range.x) / kSegLen);  // the round's first segment
@@ -465,7 +449,9 @@ __global__ __launch_bounds__(64, 3) void k_render_fwd(RenderArgs a) {
         // waiting for them does not wait for the prefetch.  Reads past nk land in the padding or
         // stale slots (index < kRound + kGroup) and are never used.
         struct AlphaOps { f4v x, y, cx, cy, cz, op; };
-        struct ColourOps { float4 rgbd[kGroup]; uint32_t pos[kGroup]; };
+        // (AUX: mb, the group's four aux bits, read with the colours — before the next group's alpha
+        // prefetch, so the wait for it is the colours' wait and does not drain the prefetch)
+        struct ColourOps { float4 rgbd[kGroup]; uint32_t pos[kGroup]; uint32_t mb; };
         const auto load_alpha = [&](int j, AlphaOps& g) {
             const auto ld4 = [&](const float* f) { return *reinterpret_cast<const f4v*>(f + j); };
             g.x = ld4(s_x);
@@ -476,6 +462,8 @@ __global__ __launch_bounds__(64, 3) void k_render_fwd(RenderArgs a) {
             g.op = ld4(s_op);
         };
         const auto load_colour = [&](int j, ColourOps& c) {
+            // (mb first: the first entry's chain needs it, and LDS reads retire in order)
+            if constexpr (AUX) c.mb = *reinterpret_cast<const uint32_t*>(s_mb + j);
 #pragma unroll
             for (int u = 0; u < kGroup; ++u) {
                 c.rgbd[u] = s_rgbd[j + u];
@@ -487,7 +475,7 @@ __global__ __launch_bounds__(64, 3) void k_render_fwd(RenderArgs a) {
             bool ok[4];
             // (AUX: the group's four aux bits, the same for every lane: one scalar word)
             uint32_t mb = 0u;
-            if constexpr (AUX) mb = __builtin_amdgcn_readfirstlane(*reinterpret_cast<const uint32_t*>(s_mb + j));
+            if constexpr (AUX) mb = __builtin_amdgcn_readfirstlane(c.mb);
             pixel_alpha4(g.x, g.y, g.cx, g.cy, g.cz, g.op, -pfx, -pfy, dx4, dy4, G4, al, ok);
             uint64_t vm[kGroup];  // per entry: the lanes that blended it (uniform masks, SALU)
 #pragma unroll
