@@ -48,11 +48,15 @@ _t_entry = [0.0]
 
 def _render_marked(*a, **k):
     _t_entry[0] = time.perf_counter()
-    return render(*a, **k)
+    try:
+        return render(*a, **k)
+    finally:
+        _t_entry[0] = 0.0
 
 
 def _begin_marked(*a):
     t = time.perf_counter()
+    _t_entry[0] = 0.0
     acc["render() entry -> native begin"] += t - _t_entry[0]
     cnt["render() entry -> native begin"] += 1
     try:
@@ -63,6 +67,27 @@ def _begin_marked(*a):
 
 
 _lib.gs_rasterize_forward_begin = _begin_marked
+# the timeline of the pre-launch path: time since render() entry at the entry of each step (training renders)
+_marks = collections.defaultdict(float)
+_mark_n = collections.defaultdict(int)
+
+
+def _marked(name, mod, attr):
+    f = getattr(mod, attr)
+
+    def w(*a, **k):
+        if _t_entry[0]:
+            _marks[name] += time.perf_counter() - _t_entry[0]
+            _mark_n[name] += 1
+        return f(*a, **k)
+    setattr(mod, attr, w)
+
+
+for _name, _mod, _attr in (("GR._fused_ok", GR, "_fused_ok"), ("GR._render_fused", GR, "_render_fused"),
+                           ("GR._settings", GR, "_settings"), ("GR._may_backward", GR, "_may_backward"),
+                           ("_C._index32", _C, "_index32"), ("_C._params", _C, "_params"),
+                           ("_C._settings", _C, "_settings"), ("_C._stream", _C, "_stream")):
+    _marked(_name, _mod, _attr)
 
 dev = torch.device("cuda", 0)
 P, W, H, V = 1_000_000, 512, 512, 3
@@ -116,6 +141,9 @@ for k in sorted(acc, key=lambda k: -acc[k]):
     print(f"  {k:42s} {acc[k] / n * 1e6:8.0f} us per iteration, {acc[k] / cnt[k] * 1e6:7.1f} us per call x {cnt[k] // n}")
 for k, v in extra.items():
     print(f"  {k:42s} {v / n * 1e6:8.0f} us per iteration")
+print("  pre-launch timeline (us since render() entry, training renders):")
+for k in sorted(_marks, key=lambda k: _marks[k] / max(1, _mark_n[k])):
+    print(f"    {k:40s} {_marks[k] / max(1, _mark_n[k]) * 1e6:8.1f}")
 
 if os.environ.get("PROFILE"):
     import cProfile
