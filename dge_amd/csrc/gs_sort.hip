@@ -1408,60 +1408,39 @@ __global__ __launch_bounds__(256) void k_scan_emit_x(EmitArgs a) {
 
 // Tile ranges from the per-tile instance counts (one workgroup): an exclusive
 // scan in tile order — the ranges identifyTileRanges (rasterizer_impl.cu:105-125)
-// finds in the sorted keys; empty tiles keep (0, 0).  Two-level grids have at most 128 x 128 tiles.  Also
-// the forward's dispatch order (k_tile_order's: tiles by list length, longest first) from the same counts,
-// when tile_order is set.
-// The counts come in and the ranges go out coalesced, through LDS (each thread scans a run of
-// consecutive tiles: rows padded by one word per 32, so a wave's runs sit in distinct banks), and the
-// class counters take one LDS atomic per (wave, class) present (lanes of a class found by ballots): the
-// strided per-thread loads and stores and the per-tile atomics on 64 counters took 16 us at c4's 8160 tiles.
+// finds in the sorted keys; empty tiles keep (0, 0).
+// Each thread's run of counts is loaded at once into registers (one memory round trip instead of one
+// per count).  Two-level grids have at most 128 x 128 tiles.  Also the forward's dispatch order
+// (k_tile_order's: tiles by list length, longest first) from the same counts, when tile_order is set.
 constexpr int kRangesPer = kXDigits * kXDigits / 256;
-__device__ __forceinline__ int ranges_lds(int t) { return t + (t >> 5); }
 __global__ __launch_bounds__(256) void k_ranges_counts(const uint32_t* __restrict__ count, int tiles,
                                                        uint2* __restrict__ ranges, uint32_t* __restrict__ tile_order) {
     __shared__ uint32_t lds4[4];
     constexpr int kClasses = 64;
     __shared__ uint32_t s_cls[kClasses];
-    __shared__ uint32_t s_c[kXDigits * kXDigits + kXDigits * kXDigits / 32 + 1];  // counts, then exclusive starts
     auto cls = [](uint32_t len) { return min(kClasses - 1, (int)(__log2f((float)len + 1.0f) * 3.0f)); };
-    const int tid = threadIdx.x, lane = tid & 63;
-    if (tid < kClasses) s_cls[tid] = 0u;
-    for (int t = tid; t < tiles; t += 256) s_c[ranges_lds(t)] = count[t];
-    __syncthreads();
-    const int per = (tiles + 255) / 256, t0 = tid * per;
+    if (threadIdx.x < kClasses) s_cls[threadIdx.x] = 0u;
+    const int per = (tiles + 255) / 256, t0 = threadIdx.x * per;
     uint32_t c[kRangesPer];
-    uint32_t sum = 0;
+    uint32_t s = 0;
 #pragma unroll
-    for (int i = 0; i < kRangesPer; ++i) {
-        c[i] = i < per && t0 + i < tiles ? s_c[ranges_lds(t0 + i)] : 0u;
-        sum += c[i];
-    }
+    for (int i = 0; i < kRangesPer; ++i) c[i] = i < per && t0 + i < tiles ? count[t0 + i] : 0u;
+#pragma unroll
+    for (int i = 0; i < kRangesPer; ++i) s += c[i];
     uint32_t all;
-    uint32_t run = block_exclusive_scan(sum, lds4, all);  // (its barriers order the reads above)
+    uint32_t run = block_exclusive_scan(s, lds4, all);
 #pragma unroll
     for (int i = 0; i < kRangesPer; ++i) {
-        if (i < per && t0 + i < tiles) s_c[ranges_lds(t0 + i)] = run;
-        run += c[i];
-    }
-    if (tid == 0) s_c[ranges_lds(tiles)] = all;
-    __syncthreads();
-    for (int t = tid; t < tiles; t += 256) {
-        const uint32_t a = s_c[ranges_lds(t)], b = s_c[ranges_lds(t + 1)];
-        ranges[t] = b > a ? make_uint2(a, b) : make_uint2(0u, 0u);
+        const int t = t0 + i;
+        if (i < per && t < tiles) {
+            ranges[t] = c[i] ? make_uint2(run, run + c[i]) : make_uint2(0u, 0u);
+            run += c[i];
+            if (tile_order) atomicAdd(&s_cls[cls(c[i])], 1u);
+        }
     }
     if (!tile_order) return;
-    // classes: tile t = t1 * 256 + tid, each thread's tiles strided (the order inside a class is free)
-    const int n1 = (tiles + 255) / 256;
-    for (int t1 = 0; t1 < n1; ++t1) {
-        const int t = t1 * 256 + tid;
-        const bool valid = t < tiles;
-        const uint64_t vm = __ballot(valid);
-        const uint32_t k = valid ? (uint32_t)cls(s_c[ranges_lds(t + 1)] - s_c[ranges_lds(t)]) : 0u;
-        const uint64_t peers = match_digit<6>(k, vm);
-        if (valid && __popcll(peers & lanemask_lt()) == 0) atomicAdd(&s_cls[k], (uint32_t)__popcll(peers));
-    }
     __syncthreads();
-    if (tid == 0) {  // start of each class, longest class first
+    if (threadIdx.x == 0) {  // start of each class, longest class first
         uint32_t acc = 0;
         for (int k = kClasses - 1; k >= 0; --k) {
             const uint32_t m = s_cls[k];
@@ -1470,21 +1449,11 @@ __global__ __launch_bounds__(256) void k_ranges_counts(const uint32_t* __restric
         }
     }
     __syncthreads();
-    for (int t1 = 0; t1 < n1; ++t1) {
-        const int t = t1 * 256 + tid;
-        const bool valid = t < tiles;
-        const uint64_t vm = __ballot(valid);
-        const uint32_t k = valid ? (uint32_t)cls(s_c[ranges_lds(t + 1)] - s_c[ranges_lds(t)]) : 0u;
-        const uint64_t peers = match_digit<6>(k, vm);
-        const uint32_t rank = (uint32_t)__popcll(peers & lanemask_lt());
-        uint32_t b0 = 0;
-        if (valid && rank == 0) b0 = atomicAdd(&s_cls[k], (uint32_t)__popcll(peers));
-        // the leader's base to its peers: the lowest lane of `peers`
-        const int leader = valid ? __ffsll((unsigned long long)peers) - 1 : lane;
-        b0 = (uint32_t)__shfl((int)b0, leader);
-        if (valid) tile_order[b0 + rank] = (uint32_t)t;
+#pragma unroll
+    for (int i = 0; i < kRangesPer; ++i) {
+        const int t = t0 + i;
+        if (i < per && t < tiles) tile_order[atomicAdd(&s_cls[cls(c[i])], 1u)] = (uint32_t)t;
     }
-    (void)lane;
 }
 
 void launch_emit_fused(const EmitArgs& a, hipStream_t s) {
