@@ -421,7 +421,8 @@ size_t gs_binning_buffer_size(int num_rendered, int num_tiles);
 
 /* Offsets (bytes) of the per-Gaussian arrays inside the geometry buffer, for
  * field-by-field parity tests.  Names: "splat" (64-B records: "means2D" float2
- * at +0, "conic_opacity" float4 at +16, "rgbd" float4 = r,g,b,depth at +32),
+ * at +0, "conic_opacity" float4 at +16, "rgbd" float4 = r,g,b,depth at +32 — the depth negated for
+ * the Gaussians a forward's gs_params.aux_mask marks: the blend's aux bit, |depth| is the depth),
  * "tiles_touched" (u32), "clamped" (u8, bit c = channel c clamped), "radii"
  * (int32; a copy of the caller's radii, kept only when the caller passes none
  * or the tile grid exceeds 255 x 255).
