@@ -869,20 +869,23 @@ def test_semantic_render_reuses_the_training_forward(cuda_device, localize):
     assert torch.equal(got[3], ref[3])
 
 
-@pytest.mark.parametrize("bg", [(0.0, 0.0, 0.0), (0.1, 0.0, 0.2)], ids=["black", "colour"])
-def test_semantic_render_served_from_the_training_blend(cuda_device, bg):
+@pytest.mark.parametrize("bg,W,H", [((0.0, 0.0, 0.0), 240, 176), ((0.1, 0.0, 0.2), 240, 176),
+                                    ((0.1, 0.0, 0.2), 1024, 768)], ids=["black", "colour", "colour_two_level"])
+def test_semantic_render_served_from_the_training_blend(cuda_device, bg, W, H):
     """gs_params.aux_mask: the training render of a model carrying an edit mask also composites the mask as a
     grey along its own alpha / transmittance chain; DGE's semantic render right after it (override_color = the
     mask repeated over the channels, DGE.py:198-204) is composed from those sums after a device-side check of
     the colours — bit-identical to the recolor blend and to a full render.  Other colours (half the mask's
-    grey) fail the check and are blended; the training render itself is unchanged by the extra channel."""
+    grey) fail the check and are blended; the training render itself is unchanged by the extra channel.  The
+    mask rides as the sign of the Splat depth: every blend, depth and recolor must read |depth| (1024x768: the
+    two-level binning's grid)."""
     from dge_amd import gaussian_renderer as GR
     from dge_amd.cameras import orbit_camera
     from dge_amd.gaussian_renderer import PipelineParams, render
     from dge_amd.scene import synthetic_scene
 
     dev = torch.device("cuda")
-    P, W, H = 60_000, 240, 176
+    P = 60_000
     pipe, bgt = PipelineParams(), torch.tensor(bg, device=dev)
     cams = [orbit_camera(k, 4, W, H, device=dev) for k in range(2)]
 
