@@ -460,15 +460,21 @@ __global__ __launch_bounds__(256, GS_SCATTER_MINW) void k_radix_scatter(const KT
     auto digit = [&](uint32_t k) { return DM ? msd_digit(k, msd) : (k >> shift) & (NDIG - 1); };
     uint32_t key[IPT], loc[IPT];
     V val[IPT];
+    // unconditional loads, clamped into the array (base < n here): all of them in flight at once.  (Loads
+    // under `valid` with the bias applied in the same branch waited for each key in turn — 16 memory round
+    // trips per block: c4's row pass 221 us.)
 #pragma unroll
     for (int it = 0; it < IPT; ++it) {
         const uint32_t idx = base + it * 64 + lane;
-        const bool valid = idx < n;
-        key[it] = valid ? (uint32_t)keys_in[idx] - bias : 0u;
-        if constexpr (VM == kValU32) val[it] = IDV ? idx : (valid ? vals_in[idx] : 0u);
+        const uint32_t ci = idx < n ? idx : n - 1;
+        key[it] = (uint32_t)keys_in[ci];
+        if constexpr (VM == kValU32) val[it] = IDV ? idx : vals_in[ci];
         else if constexpr (VM == kValPairFirst) val[it] = make_uint2(0u, idx);  // (aux re-read at the store)
-        else val[it] = valid ? pairs_in[idx] : make_uint2(0u, 0u);
+        else val[it] = pairs_in[ci];
     }
+    __builtin_amdgcn_sched_barrier(0);  // (keeps the bias below from being hoisted between the loads)
+#pragma unroll
+    for (int it = 0; it < IPT; ++it) key[it] = base + it * 64 + lane < n ? key[it] - bias : 0u;
 #pragma unroll
     for (int it = 0; it < IPT; ++it) {
         const uint32_t idx = base + it * 64 + lane;
