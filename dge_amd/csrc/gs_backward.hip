@@ -561,23 +561,29 @@ __device__ __forceinline__ void bwd_view_batch(const GaussBwdArgs& a, bool ok, i
             }
         }
     } else if (a.sh.dc && ncol > 0) {
+        // (raw bits first, converted once the batch's loads are all issued: a conversion beside its load made
+        // each fp16 load wait in turn)
+        const bool half = a.sh.half != 0;
         for (int b = 0; b < total; b += kV * kGB) {
-            float v[kV];
+            uint32_t v[kV];
 #pragma unroll
             for (int u = 0; u < kV; ++u) {
                 const int e = b + u * kGB + (int)threadIdx.x;
                 const int row = (int)(((float)e + 0.5f) * inv_ncol), col = e - row * ncol;
                 const uint32_t gid = e < total ? s_gid[row] : kNoRow;
                 const size_t off = (size_t)gid * a.sh.rest_stride + col;
-                v[u] = gid == kNoRow ? 0.f
-                       : a.sh.half ? __half2float(reinterpret_cast<const __half*>(a.sh.rest)[off])
-                                   : a.sh.rest[off];
+                v[u] = gid == kNoRow ? 0u
+                       : half ? (uint32_t)reinterpret_cast<const uint16_t*>(a.sh.rest)[off]
+                              : __float_as_uint(a.sh.rest[off]);
             }
+            __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int u = 0; u < kV; ++u) {
                 const int e = b + u * kGB + (int)threadIdx.x;
                 const int row = (int)(((float)e + 0.5f) * inv_ncol), col = e - row * ncol;
-                if (e < total) s_sh[row * kShPitch + col] = v[u];
+                if (e < total)
+                    s_sh[row * kShPitch + col] = half ? __half2float(__ushort_as_half((unsigned short)v[u]))
+                                                      : __uint_as_float(v[u]);
             }
         }
     }

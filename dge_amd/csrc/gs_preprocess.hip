@@ -87,7 +87,8 @@ __global__ __launch_bounds__(256) void k_preprocess(PreprocessArgs a) {
     float2 pix = make_float2(0.f, 0.f);
     float4 conic = make_float4(0.f, 0.f, 0.f, 0.f);
     float depth = 0.f;
-    bool auxv = false;  // gs_params.aux_mask
+    uint32_t auxv = 0;  // gs_params.aux_mask byte, compared at the Splat store (a compare beside the load,
+                        // in a branch of its own, waited for every load in flight)
     // SH rows of the whole block staged first, in flight together with the per-Gaussian loads below
     // (one memory phase instead of geometry -> compute -> SH rows); rows of Gaussians that turn out
     // culled are read needlessly (180 B each), which object-centric views hardly have
@@ -112,27 +113,36 @@ __global__ __launch_bounds__(256) void k_preprocess(PreprocessArgs a) {
         const float invA = 1.0f / (float)ncolA, invB = ncolB > 0 ? 1.0f / (float)ncolB : 0.f;
         const int rbase = a.index ? 0 : idx0;  // rows: s_src[row] (gathered) or idx0 + row
         const float* baseF = a.sh.rest + (size_t)rbase * stride;
-        const __half* baseH = reinterpret_cast<const __half*>(a.sh.rest) + (size_t)rbase * stride;
-        auto ld = [&](uint32_t off) { return a.sh.half ? __half2float(baseH[off]) : baseF[off]; };
+        const uint16_t* baseH = reinterpret_cast<const uint16_t*>(a.sh.rest) + (size_t)rbase * stride;
+        // raw bits first, converted once every load is issued (a conversion next to its load made each
+        // fp16 load wait in turn: c5's 45 rows of round trips)
+        const bool half = a.sh.half != 0;
+        auto ld = [&](uint32_t off) { return half ? (uint32_t)baseH[off] : __float_as_uint(baseF[off]); };
+        auto cvt = [&](uint32_t r) {
+            return half ? __half2float(__ushort_as_half((unsigned short)r)) : __uint_as_float(r);
+        };
         auto srow = [&](int row) { return a.index ? s_src[row] : row; };
-        float shA[kShA];
+        uint32_t rawA[kShA], rawB[kShBPer];
 #pragma unroll
         for (int i = 0; i < kShA; ++i) {
             const int f = threadIdx.x + 256 * i;
             const int row = (int)(((float)f + 0.5f) * invA), col = f - row * ncolA;
-            shA[i] = row < nrow ? ld((uint32_t)(srow(row) * stride + col)) : 0.f;
+            rawA[i] = row < nrow ? ld((uint32_t)(srow(row) * stride + col)) : 0u;
         }
 #pragma unroll
         for (int i = 0; i < kShBPer; ++i) {
             const int f = threadIdx.x + 256 * i;
             const int row = (int)(((float)f + 0.5f) * invB), col = f - row * ncolB;
-            shB[i] = ncolB > 0 && row < nrow ? ld((uint32_t)(srow(row) * stride + kShA + col)) : 0.f;
+            rawB[i] = ncolB > 0 && row < nrow ? ld((uint32_t)(srow(row) * stride + kShA + col)) : 0u;
         }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < kShBPer; ++i) shB[i] = cvt(rawB[i]);
 #pragma unroll
         for (int i = 0; i < kShA; ++i) {
             const int f = threadIdx.x + 256 * i;
             const int row = (int)(((float)f + 0.5f) * invA), col = f - row * ncolA;
-            if (row < nrow) s_sh[row * kShPitchAB + col] = shA[i];
+            if (row < nrow) s_sh[row * kShPitchAB + col] = cvt(rawA[i]);
         }
     }
     if (idx < a.P) {
@@ -152,7 +162,8 @@ __global__ __launch_bounds__(256) void k_preprocess(PreprocessArgs a) {
             sc = ld3(a.scales + 3 * (size_t)src);
         }
         const float op_in = a.opacities[src];
-        if (a.aux_mask) auxv = a.aux_mask[src] != 0;
+        // (no branch: without a mask the load reads the opacities' bytes, a valid address, and is ignored)
+        auxv = (a.aux_mask ? a.aux_mask : reinterpret_cast<const uint8_t*>(a.opacities))[src];
         // in_frustum (auxiliary.h:139-164): only the near test is live
         const float4 ph = proj_point(pm, p);
         const float pw = 1.0f / (ph.w + 0.0000001f);
@@ -224,7 +235,7 @@ __global__ __launch_bounds__(256) void k_preprocess(PreprocessArgs a) {
             sp.xy = pix;
             sp.pad0 = make_float2(0.f, 0.f);
             sp.co = conic;
-            sp.rgbd = make_float4(rgb.x, rgb.y, rgb.z, auxv ? -depth : depth);  // (Splat: the aux bit)
+            sp.rgbd = make_float4(rgb.x, rgb.y, rgb.z, a.aux_mask && auxv != 0u ? -depth : depth);  // (Splat: the aux bit)
             sp.pad1 = make_float4(0.f, 0.f, 0.f, 0.f);
             a.splat[idx] = sp;
         }

@@ -40,6 +40,21 @@ __device__ __forceinline__ uint64_t match_digit(uint32_t d, uint64_t valid_mask)
     return m;
 }
 
+// This thread's part of the sum of sums[0 .. n): elements tid, tid + 256, ... loaded four at a time, clamped
+// and unconditional, so their loads are in flight together (a loop adding each load as it came waited for
+// every one in turn).
+__device__ __forceinline__ uint32_t strided_part(const uint32_t* __restrict__ sums, uint32_t n) {
+    uint32_t part = 0;
+    for (uint32_t j0 = threadIdx.x; j0 < n; j0 += 1024) {
+        uint32_t v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = sums[min(j0 + 256u * u, n - 1)];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) part += j0 + 256u * u < n ? v[u] : 0u;
+    }
+    return part;
+}
+
 // 256-thread exclusive scan; `total` receives the workgroup sum.
 __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* lds4, uint32_t& total) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -971,7 +986,7 @@ __global__ __launch_bounds__(256) void k_scan_emit(EmitArgs a) {
     uint32_t base;
     {
         uint32_t part = 0;
-        for (uint32_t j = threadIdx.x; j < blockIdx.x; j += 256) part += a.scan_sums[j];
+        part = strided_part(a.scan_sums, blockIdx.x);
         block_exclusive_scan(part, lds4, base);
     }
     const uint32_t r_block = blockIdx.x * (uint32_t)kScanTile;
@@ -1073,17 +1088,24 @@ __global__ __launch_bounds__(256) void k_emit_tiles(EmitArgs a) {
     uint32_t base;  // the block's first slot (as k_scan_emit)
     {
         uint32_t part = 0;
-        for (uint32_t j = tid; j < blockIdx.x; j += 256) part += a.scan_sums[j];
+        part = strided_part(a.scan_sums, blockIdx.x);
         block_exclusive_scan(part, lds4, base);
     }
     {   // each tile's first position for this block; block 0: the ranges and the dispatch order
         const int bm = a.scan_blocks <= kScanBmRows ? 1 : 0;
-        uint32_t c[PER];
+        uint32_t c[PER], h[PER];
         uint32_t s = 0;
+        // (totals and this block's row loaded together, clamped: no load waits alone)
 #pragma unroll
         for (int i = 0; i < PER; ++i) {
-            const int d = tid * PER + i;
-            c[i] = d < nt ? a.ttotals[d] : 0u;
+            const int d = min(tid * PER + i, nt - 1);
+            c[i] = a.ttotals[d];
+            h[i] = a.thist[hist_at(bm, blockIdx.x, (uint32_t)d, a.scan_blocks, nt)];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            if (tid * PER + i >= nt) c[i] = 0u;
             s += c[i];
         }
         uint32_t all;
@@ -1092,7 +1114,7 @@ __global__ __launch_bounds__(256) void k_emit_tiles(EmitArgs a) {
 #pragma unroll
         for (int i = 0; i < PER; ++i) {
             const int d = tid * PER + i;
-            s_pos[d] = d < nt ? run + a.thist[hist_at(bm, blockIdx.x, (uint32_t)d, a.scan_blocks, nt)] : 0u;
+            s_pos[d] = d < nt ? run + h[i] : 0u;
             run += c[i];
         }
         if (blockIdx.x == 0) write_tile_ranges<PER>(c, run0, nt, a.ranges, a.tile_order, a.cap);
@@ -1104,7 +1126,11 @@ __global__ __launch_bounds__(256) void k_emit_tiles(EmitArgs a) {
     {
         uint2 gr[GPT];
 #pragma unroll
-        for (int i = 0; i < GPT; ++i) gr[i] = r0 + i < (uint32_t)a.P ? a.order[r0 + i] : make_uint2(0u, 0u);
+        for (int i = 0; i < GPT; ++i) gr[i] = a.order[min(r0 + i, (uint32_t)a.P - 1)];  // (clamped: loads together)
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < GPT; ++i)
+            if (r0 + i >= (uint32_t)a.P) gr[i] = make_uint2(0u, 0u);
         uint32_t s = 0;
 #pragma unroll
         for (int i = 0; i < GPT; ++i) {
@@ -1205,7 +1231,30 @@ __global__ __launch_bounds__(256) void k_emit_tiles(EmitArgs a) {
             if (jj < nb) s_idx[cnt[w][dg[e]] + loc[e]] = (uint16_t)jj;
         }
         __syncthreads();
-        // every staged instance's loads issued before the stores (fixed trip count, unrolled)
+        // every staged instance's loads issued before the stores (fixed trip count, unrolled; the scheduling
+        // barrier keeps the ids-only build from storing each id as its load returns: 16 round trips a batch)
+        if constexpr (IDS) {  // (the pairs build batches its loads by itself, and this form measured slower there)
+        uint32_t st_pos[kEtEPT], st_g[kEtEPT], st_j[kEtEPT];
+#pragma unroll
+        for (int e = 0; e < kEtEPT; ++e) {
+            const uint32_t i = (uint32_t)(e * 256 + tid);
+            const uint32_t jj = i < nb ? s_idx[i] : 0u;
+            const int o = i < nb ? (int)s_own[jj] - 1 : 0;
+            st_pos[e] = i < nb ? s_pos[tile_of(j0 + jj, o)] + i : 0xFFFFFFFFu;
+            st_g[e] = a.order[r_block + (uint32_t)o].y;  // (the block's own entries: L2; o valid either way)
+            st_j[e] = jj;
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int e = 0; e < kEtEPT; ++e) {
+            // (speculative capacity: gs_views_check reports an overflow; an overflowed binning is redone,
+            // but until then its lists must stay inside the buffer: the ranges are clamped to the
+            // capacity, and so is every slot — the backward's record address)
+            const uint32_t pos = st_pos[e];
+            if (pos < a.cap) reinterpret_cast<uint32_t*>(a.pairs_out)[pos] = st_g[e];
+        }
+        (void)st_j;
+        } else {
 #pragma unroll
         for (int e = 0; e < kEtEPT; ++e) {
             const uint32_t i = (uint32_t)(e * 256 + tid);
@@ -1217,11 +1266,9 @@ __global__ __launch_bounds__(256) void k_emit_tiles(EmitArgs a) {
                 // (speculative capacity: gs_views_check reports an overflow; an overflowed binning is redone,
                 // but until then its lists must stay inside the buffer: the ranges are clamped to the
                 // capacity, and so is every slot — the backward's record address)
-                if (pos < a.cap) {
-                    if constexpr (IDS) reinterpret_cast<uint32_t*>(a.pairs_out)[pos] = g;
-                    else a.pairs_out[pos] = make_uint2(g, min(base + j0 + jj, a.cap - 1u));
-                }
+                if (pos < a.cap) a.pairs_out[pos] = make_uint2(g, min(base + j0 + jj, a.cap - 1u));
             }
+        }
         }
         __syncthreads();
         // the next batch's positions: each tile's run ends where the next tile's begins (the batch's end
@@ -1271,7 +1318,7 @@ __global__ __launch_bounds__(256) void k_scan_emit_x(EmitArgs a) {
     uint32_t base;
     {
         uint32_t part = 0;
-        for (uint32_t j = tid; j < blockIdx.x; j += 256) part += a.scan_sums[j];
+        part = strided_part(a.scan_sums, blockIdx.x);
         block_exclusive_scan(part, lds4, base);
     }
     {
