@@ -433,9 +433,22 @@ __global__ __launch_bounds__(kGB) void k_gauss_live(GaussBwdViews m) {
     const int idx = idx0 + threadIdx.x;
     const int nrow = a.P - idx0 < kGB ? a.P - idx0 : kGB;
     const bool in = idx < a.P;
+    // (every view's touched byte and radius loaded together, clamped; `a && b` per view loaded them one by
+    // one, each waited for)
+    const int ci = in ? idx : 0;
+    uint32_t tb[kMaxBwdViews];
+    int rv[kMaxBwdViews];
+#pragma unroll
+    for (int v = 0; v < kMaxBwdViews; ++v) {
+        const GaussBwdArgs& b = m.v[v < m.n ? v : 0];
+        tb[v] = b.touched[ci];
+        rv[v] = b.radii[ci];
+    }
+    __builtin_amdgcn_sched_barrier(0);
     uint32_t mask = 0;
-    for (int v = 0; v < m.n; ++v)
-        if (in && m.v[v].touched[idx] && m.v[v].radii[idx] > 0) mask |= 1u << v;
+#pragma unroll
+    for (int v = 0; v < kMaxBwdViews; ++v)
+        if (v < m.n && in && tb[v] && rv[v] > 0) mask |= 1u << v;
     const bool live = mask != 0;
     s_live[threadIdx.x] = (uint8_t)mask;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -534,6 +547,9 @@ __device__ __forceinline__ void bwd_view_batch(const GaussBwdArgs& a, bool ok, i
     // independent loads first: parameters (a later view's from L2), slot range, the first 8 record flags
     GaussIn gin{};
     if (ok) gin = load_gauss_in(a, idx, src);
+    // (the grad-mask byte with the other inputs: read where it is used, it waited for itself alone)
+    // (no branch: without a mask the load reads the means' bytes, a valid address, and is ignored)
+    const uint32_t gmb_raw = (a.grad_mask ? a.grad_mask : reinterpret_cast<const uint8_t*>(a.means3D))[ok ? src : 0];
     uint32_t n = ok ? a.tiles_touched[idx] : 0u;
     const uint32_t first = ok ? a.first_slot[idx] : 0u;  // (a live Gaussian has slots)
     // (a speculative forward that overflowed its capacity is re-rendered; its slots stop at the capacity)
@@ -640,7 +656,7 @@ __device__ __forceinline__ void bwd_view_batch(const GaussBwdArgs& a, bool ok, i
     float dop = acc[5];  // w.r.t. opacity; chained through the sigmoid when activation = 1
     GaussOut o;
     if (ok) {
-        const float gm = a.grad_mask ? (a.grad_mask[src] ? 1.f : 0.f) : 1.f;
+        const float gm = !a.grad_mask || gmb_raw ? 1.f : 0.f;
         // (each thread reads and then overwrites only its own LDS row: no barrier in between)
         gauss_bwd_visible(a, gin, acc, dop, my_sh, ncol, (a.mask_bits & GS_ACC_SH) ? gm : 1.f, ddc, o);
         if (a.grad_mask) apply_grad_mask(a, gm, acc, dop, o);

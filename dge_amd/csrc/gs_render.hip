@@ -255,9 +255,10 @@ __global__ __launch_bounds__(64, 3) void k_render_fwd(RenderArgs a) {
                 const size_t HW = (size_t)a.W * a.H;
                 const float T = a.final_T_src[pix];
                 const float2 av = a.aux_src[pix];
-                a.out_color[pix] = __builtin_fmaf(T, a.bg[0], av.x);
-                a.out_color[HW + pix] = __builtin_fmaf(T, a.bg[1], av.x);
-                a.out_color[2 * HW + pix] = __builtin_fmaf(T, a.bg[2], av.x);
+                const float bg0 = a.bg[0], bg1 = a.bg[1], bg2 = a.bg[2];  // (all three before the stores)
+                a.out_color[pix] = __builtin_fmaf(T, bg0, av.x);
+                a.out_color[HW + pix] = __builtin_fmaf(T, bg1, av.x);
+                a.out_color[2 * HW + pix] = __builtin_fmaf(T, bg2, av.x);
                 a.out_depth[pix] = av.y;
             }
             return;
@@ -551,9 +552,12 @@ __global__ __launch_bounds__(64, 3) void k_render_fwd(RenderArgs a) {
         a.final_T[pix] = T;
         a.n_contrib[pix] = last;
         // forward.cu:376 `C + T * bg`, contracted (as the oracle): fma(T, bg, C)
-        a.out_color[pix] = __builtin_fmaf(T, a.bg[0], C01.x);
-        a.out_color[HW + pix] = __builtin_fmaf(T, a.bg[1], C01.y);
-        a.out_color[2 * HW + pix] = __builtin_fmaf(T, a.bg[2], C2D.x);
+        // (the background read before the first store: loaded between the stores, each load waited, the
+        // compiler unable to tell out_color from bg — three round trips at every wave's end)
+        const float bg0 = a.bg[0], bg1 = a.bg[1], bg2 = a.bg[2];
+        a.out_color[pix] = __builtin_fmaf(T, bg0, C01.x);
+        a.out_color[HW + pix] = __builtin_fmaf(T, bg1, C01.y);
+        a.out_color[2 * HW + pix] = __builtin_fmaf(T, bg2, C2D.x);
         a.out_depth[pix] = C2D.y;
         if constexpr (AUX) a.aux_out[pix] = make_float2(Cm, C2D.y);
     }
