@@ -40,6 +40,18 @@ __device__ __forceinline__ uint64_t match_digit(uint32_t d, uint64_t valid_mask)
     return m;
 }
 
+// k div w for the instance index k < 2^16 inside a rect w <= 255 tiles wide, without a division: a table of
+// magic multipliers M[w] = ceil(2^32 / w) (one integer division per thread, filled before the block's first
+// barrier), k div w = umulhi(k, M[w]) — exact since k (M - 2^32 / w) < 2^32 / w for k < 2^16 (and w = 1 is k).
+// (The IEEE float quotient (k + 0.5) / w it replaces cost ~16 VALU and a reciprocal per instance.)
+__device__ __forceinline__ void fill_div_magic(uint32_t* s_magic) {
+    const uint32_t w = threadIdx.x;  // (256 threads: one entry each)
+    s_magic[w] = w > 1 ? 0xFFFFFFFFu / w + 1u : 0u;
+}
+__device__ __forceinline__ uint32_t div_small(uint32_t k, uint32_t w, const uint32_t* s_magic) {
+    return w == 1 ? k : __umulhi(k, s_magic[w]);
+}
+
 // This thread's part of the sum of sums[0 .. n): elements tid, tid + 256, ... loaded four at a time, clamped
 // and unconditional, so their loads are in flight together (a loop adding each load as it came waited for
 // every one in turn).
@@ -1081,6 +1093,8 @@ __global__ __launch_bounds__(256) void k_emit_tiles(EmitArgs a) {
     __shared__ uint32_t s_pos[NDIG];
     __shared__ uint16_t s_idx[kEtBatch];     // staged, tile-major: the instance's position in the batch
     __shared__ uint32_t s_carry;
+    __shared__ uint32_t s_magic[256];
+    fill_div_magic(s_magic);
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int nt = a.ntiles;
     const uint32_t r_block = blockIdx.x * (uint32_t)kScanTile;
@@ -1153,7 +1167,7 @@ __global__ __launch_bounds__(256) void k_emit_tiles(EmitArgs a) {
         const uint32_t q = s_rect[o];
         const uint32_t x0 = q & 0xFFu, y0 = (q >> 8) & 0xFFu, wd = ((q >> 16) & 0xFFu) - x0;
         const uint32_t k = j - s_start[o];
-        const uint32_t ky = (uint32_t)(((float)k + 0.5f) / (float)wd);  // exact: k < 2^20
+        const uint32_t ky = div_small(k, wd, s_magic);
         return (y0 + ky) * (uint32_t)a.gx + x0 + (k - ky * wd);
     };
     for (uint32_t j0 = 0; j0 < total; j0 += (uint32_t)kEtBatch) {
@@ -1312,6 +1326,8 @@ __global__ __launch_bounds__(256) void k_scan_emit_x(EmitArgs a) {
     __shared__ PV s_pair[kEmitBatch];
     __shared__ uint16_t s_own[kEmitBatch];  // the batch's owners (+1): marks at the entries' starts, prefix max
     __shared__ uint32_t s_carry;
+    __shared__ uint32_t s_magic[256];
+    fill_div_magic(s_magic);
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     if (blockIdx.x == 0)
         for (int t = tid; t < a.ntiles; t += 256) a.tile_count[t] = 0u;  // (the row pass counts into it)
@@ -1397,7 +1413,7 @@ __global__ __launch_bounds__(256) void k_scan_emit_x(EmitArgs a) {
                 const int lo = (int)s_own[valid ? jj : 0u] - 1;
                 const int4 q = s_rect[lo];
                 const uint32_t k = j - s_start[lo];
-                const uint32_t ky = (uint32_t)(((float)k + 0.5f) / (float)q.z);  // exact: k < 2^20
+                const uint32_t ky = div_small(k, (uint32_t)q.z, s_magic);
                 const uint32_t kx = k - ky * (uint32_t)q.z;
                 const uint32_t x = (uint32_t)q.x + kx, y = (uint32_t)q.y + ky;
                 kk[e] = y << kXBits | x;
