@@ -721,16 +721,23 @@ __global__ __launch_bounds__(kGB) void k_gauss_bwd_live(GaussBwdViews m) {
     // one view only, so a batch per (union batch, view) would run mostly idle threads through the pass's
     // latency-bound phases once per view; this runs each view's Gaussians of the whole workgroup together.
     bool first = true;
+    // this thread's entry of chunk `base` (the union list with every view's bit: the same for all views)
+    const auto load_entry = [&](uint32_t base) {
+        const uint32_t j = base + threadIdx.x;
+        int g = 0;
+#pragma unroll
+        for (int q = 1; q < kLiveGroup; ++q) g += j >= s_pre[q] ? 1 : 0;
+        return j < count ? a.live_list[(size_t)(sb0 + g) * kGB + (j - s_pre[g])] : 0u;
+    };
+    // (chunk 0 loaded once for every view: most workgroups have one chunk, and each view's reload of it was a
+    // round trip on the pass's latency-bound path)
+    const uint32_t entry0 = load_entry(0);
 #pragma unroll 1
     for (int v = 0; v < m.n; ++v) {
         uint32_t filled = 0;  // compacted entries pending in s_vlist (< kGB between batches)
         for (uint32_t base = 0; base < count; base += kGB) {
-            const uint32_t j = base + threadIdx.x;
-            const bool in = j < count;
-            int g = 0;
-#pragma unroll
-            for (int q = 1; q < kLiveGroup; ++q) g += j >= s_pre[q] ? 1 : 0;
-            const uint32_t entry = in ? a.live_list[(size_t)(sb0 + g) * kGB + (j - s_pre[g])] : 0u;
+            const bool in = base + threadIdx.x < count;
+            const uint32_t entry = base == 0 ? entry0 : load_entry(base);
             const bool has = in && ((entry >> (28 + v)) & 1u);
             const uint64_t bm = __ballot(has);
             if (lane == 0) s_wave[wave] = (uint32_t)__popcll(bm);
