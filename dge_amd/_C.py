@@ -136,8 +136,34 @@ def _settings(bg, viewmatrix, projmatrix, campos, tanfovx, tanfovy, H, W, sh_deg
     return s, keep
 
 
+_RAW_STREAM = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+
+
 def _stream(device):
+    """The device's current stream as a hipStream_t (the raw query: no Stream object per call)."""
+    if _RAW_STREAM is not None:
+        idx = device.index if device.index is not None else torch.cuda.current_device()
+        return ctypes.c_void_p(_RAW_STREAM(idx))
     return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+class _Same:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        return False
+
+
+_SAME = _Same()
+
+
+def _on(dev):
+    """torch.cuda.device(dev), or nothing when dev is already the current device (the common case: a context
+    switch costs a device query and two sets per call)."""
+    if dev.index is None or torch.cuda.current_device() == dev.index:
+        return _SAME
+    return torch.cuda.device(dev)
 
 
 def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations, scale_modifier, cov3D_precomp,
@@ -149,7 +175,7 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
     dev = means3D.device
     P = means3D.size(0)
     H, W = int(image_height), int(image_width)
-    with torch.cuda.device(dev):
+    with _on(dev):
         means3D = _f32(means3D, "means3D")
         colors, opacity = _f32(colors, "colors"), _f32(opacity, "opacity")
         scales, rotations = _f32(scales, "scales"), _f32(rotations, "rotations")
@@ -190,7 +216,7 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
     P = means3D.size(0)
     H, W = int(dL_dout_color.size(1)), int(dL_dout_color.size(2))
     M = sh.size(1) if sh is not None and sh.numel() != 0 else 0
-    with torch.cuda.device(dev):
+    with _on(dev):
         opts = dict(dtype=torch.float32, device=dev)
         out = (torch.empty((P, 3), **opts), torch.empty((P, 3), **opts), torch.empty((P, 1), **opts),
                torch.empty((P, 3), **opts), torch.empty((P, 6), **opts), torch.empty((P, M, 3), **opts),
@@ -242,7 +268,7 @@ def mark_visible(means3D, viewmatrix, projmatrix):
     N.require_gpu(means3D)
     dev = means3D.device
     P = means3D.size(0)
-    with torch.cuda.device(dev):
+    with _on(dev):
         present = torch.zeros((P,), dtype=torch.bool, device=dev)
         if P == 0:
             return present
@@ -269,7 +295,7 @@ def apply_weights(background, means3D, weights, opacity, scales, rotations, scal
         raise RuntimeError("apply_weights updates weights and cnt in place: they must be contiguous")
     if weights.dtype != torch.float32 or cnt.dtype != torch.int32:
         raise RuntimeError("weights must be float32 and cnt int32")
-    with torch.cuda.device(dev):
+    with _on(dev):
         means3D, opacity = _f32(means3D, "means3D"), _f32(opacity, "opacity")
         scales, rotations = _f32(scales, "scales"), _f32(rotations, "rotations")
         cov3D_precomp, sh = _f32(cov3D_precomp, "cov3D_precomp"), _f32(sh, "sh")
@@ -363,7 +389,7 @@ def rasterize_gaussians_fused_begin(background, xyz, f_dc, f_rest, colors, raw_o
     index = _index32(index)
     P = index.numel() if index is not None else xyz.size(0)
     H, W = int(image_height), int(image_width)
-    with torch.cuda.device(dev):
+    with _on(dev):
         xyz = _f32(xyz, "xyz")
         f_dc, f_rest = _features(f_dc, "features_dc"), _features(f_rest, "features_rest")
         colors = _f32(colors, "colors")
@@ -392,7 +418,7 @@ def rasterize_gaussians_fused_end(prep):
     """Second half (gs_rasterize_forward_end) on the current stream (the begin stream or one ordered after
     it): -> the (num_rendered, color, depth, radii, geom, binning, img) of rasterize_gaussians_fused."""
     dev = prep.dev
-    with torch.cuda.device(dev):
+    with _on(dev):
         out_color = torch.empty((3, prep.H, prep.W), dtype=torch.float32, device=dev)
         out_depth = torch.empty((1, prep.H, prep.W), dtype=torch.float32, device=dev)
         _TLS.alloc = prep.alloc  # the binning buffer joins the geometry/image buffers of the begin
@@ -418,7 +444,7 @@ def render_recolor(background, colors, viewmatrix, projmatrix, campos, tan_fovx,
     (unchanged since): colours equal to its 0/1 grey are then served from that forward's sums."""
     dev = colors.device
     H, W = int(image_height), int(image_width)
-    with torch.cuda.device(dev):
+    with _on(dev):
         colors = _f32(colors, "colors")
         if colors.numel() < 3 * P:
             raise RuntimeError("colors must hold P x 3 values")
@@ -495,7 +521,7 @@ def rasterize_gaussians_fused_backward(background, xyz, f_dc, f_rest, colors, ra
     Pp = xyz.size(0)  # parameter rows
     P = index.numel() if index is not None else Pp
     H, W = int(dL_dout_color.size(1)), int(dL_dout_color.size(2))
-    with torch.cuda.device(dev):
+    with _on(dev):
         opts = dict(dtype=torch.float32, device=dev)
         have_sh = f_dc is not None and f_dc.numel() != 0
         into = into or {}
@@ -591,7 +617,7 @@ def rasterize_backward_passes(pending):
     if not pending:
         return
     dev = pending[0].radii.device
-    with torch.cuda.device(dev):
+    with _on(dev):
         for c0 in range(0, len(pending), N.MAX_VIEWS):
             chunk = pending[c0:c0 + N.MAX_VIEWS]
             n = len(chunk)
