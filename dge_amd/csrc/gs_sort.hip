@@ -1629,21 +1629,23 @@ void launch_ranges(const uint32_t* sorted_tile, int K, uint2* ranges, uint32_t* 
 // host copy of the counters): one wave, lane v < n reads view v's counter slots.
 __global__ __launch_bounds__(64) void k_views_overflow(OverflowArgs a, uint8_t* __restrict__ flag) {
     const int v = threadIdx.x;
-    bool bad = false;
-    if (v < a.n && a.cap[v]) {
-        const uint32_t* __restrict__ c = a.counters[v];
-        uint64_t k = 0;
-        uint32_t kmax = 0u, kmin_not = 0u;
+    // a speculated view's (cap != 0; exact views and views of no Gaussians have no counters) slot counts,
+    // loaded together under the lane's condition and summed after it: the summing loop inside the condition
+    // waited for each load in turn
+    const bool act = v < a.n && a.cap[v] != 0u && a.counters[v] != nullptr;
+    uint32_t cs[kCounterSlots];
 #pragma unroll
-        for (int i = 0; i < kCounterSlots; ++i) {
-            k += c[i * kCounterStride];
-            kmax = max(kmax, c[i * kCounterStride + 1]);
-            kmin_not = max(kmin_not, c[i * kCounterStride + 2]);
-        }
-        bad = k > a.cap[v];  // (any depth-key range sorts: depth_sort_msd)
-        (void)kmax;
-        (void)kmin_not;
+    for (int i = 0; i < kCounterSlots; ++i) cs[i] = 0u;
+    if (act) {
+        const uint32_t* __restrict__ c = a.counters[v];
+#pragma unroll
+        for (int i = 0; i < kCounterSlots; ++i) cs[i] = c[i * kCounterStride];
     }
+    __builtin_amdgcn_sched_barrier(0);
+    uint64_t k = 0;
+#pragma unroll
+    for (int i = 0; i < kCounterSlots; ++i) k += cs[i];
+    const bool bad = act && k > a.cap[v];  // (any depth-key range sorts: depth_sort_msd)
     const uint64_t any = __ballot(bad);
     if (v == 0) flag[0] = any ? 1 : 0;
 }
