@@ -279,10 +279,23 @@ _REPLAY_STREAMS = {}  # device index -> the side streams deferred replays rotate
 _REPLAY_SIDE = int(os.environ.get("DGE_AMD_REPLAY_STREAMS", "0"))
 
 
+_PENDING_TASK = {}  # device index -> the autograd graph task whose final callback runs _PENDING_PASSES
+
+
+def _flush_stale_passes(dev):
+    """Run the deferred passes a previous backward left behind.  A backward that raised after a view was
+    deferred (OOM, anomaly mode, an interrupt) never ran its final callback; its pending list is tied to that
+    graph task, so the next backward sees another task id, runs the stale passes first (the .grad buffers
+    they target are then fully written, never left as uninitialised memory) and queues its own callback."""
+    if dev.index in _PENDING_PASSES and _PENDING_TASK.get(dev.index) != torch._C._current_graph_task_id():
+        _run_deferred_passes(dev)
+
+
 def _replay_stream(dev):
     """The stream the next deferred replay of this backward runs on: the current stream for the first, then
     _REPLAY_SIDE side streams in turn (None: the current stream).  The replay reads and writes only tensors
     its PendingBackward holds, and the deferred passes wait for it."""
+    _flush_stale_passes(dev)
     k = len(_PENDING_PASSES.get(dev.index, ()))
     if _REPLAY_SIDE <= 0 or k % (_REPLAY_SIDE + 1) == 0:
         return None
@@ -293,9 +306,11 @@ def _replay_stream(dev):
 
 
 def _defer_pass(dev, pend, m2, m2_mode, d_m2, fresh, stream=None):
+    _flush_stale_passes(dev)
     lst = _PENDING_PASSES.get(dev.index)
     if lst is None:
         lst = _PENDING_PASSES[dev.index] = []
+        _PENDING_TASK[dev.index] = torch._C._current_graph_task_id()
         torch.autograd.Variable._execution_engine.queue_callback(lambda d=dev: _run_deferred_passes(d))
     ev = (stream if stream is not None else torch.cuda.current_stream(dev)).record_event()
     lst.append((pend, ev, m2, m2_mode, d_m2, fresh))
@@ -303,6 +318,7 @@ def _defer_pass(dev, pend, m2, m2_mode, d_m2, fresh, stream=None):
 
 def _run_deferred_passes(dev):
     lst = _PENDING_PASSES.pop(dev.index, None)
+    _PENDING_TASK.pop(dev.index, None)
     if not lst:
         return
     cur = torch.cuda.current_stream(dev)
@@ -444,6 +460,10 @@ def _accumulation_mode(p, node=None):
     # (a contiguous .grad, or a column block of a row-major gradient bucket: rows at a pitch, written in place)
     if (g.shape == p.shape and g.dtype == torch.float32 and g.device == p.device and not g.requires_grad
             and (g.is_contiguous() or _C.row_pitch_ok(g))):
+        # the kernels store a rotation gradient row as one float4: its rows 16-B aligned, the pitch a multiple
+        # of 4 (what gs_rasterize_backward_ex validates); any other .grad of that shape goes back to autograd
+        if g.dim() == 2 and g.shape[1] == 4 and (g.stride(0) % 4 or g.data_ptr() % 16):
+            return None, None
         return "add", owner
     return None, None
 

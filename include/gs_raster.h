@@ -248,14 +248,20 @@ void gs_rasterize_forward_release(gs_forward_state *state);
  * the training render just before it, so their preprocess, depth order and
  * tile lists are identical and only the blend differs).  out_color/out_depth
  * are bit-identical to a full forward with colors_precomp = colors; img_out
- * (gs_image_buffer_size) receives that blend's per-pixel state, the source
- * buffers are only read.  s must describe the source forward (image size,
- * grid); its bg is the one blended.  Enqueued on `stream`, which must be
- * ordered after the source forward.  src_aux_mask: NULL, or the gs_params.aux_mask
- * the source forward composited (the same bytes, unchanged since): where colors
- * holds exactly (m_i, m_i, m_i) for every Gaussian (checked on the device, bit for
- * bit) the image is composed from that forward's grey sum and transmittance
- * instead of blended again — the same bits; otherwise the blend runs (ABI 18). */
+ * (gs_image_buffer_size) receives that blend's per-pixel state (final T,
+ * n_contrib, the tile / quadrant windows) when the blend runs, and is scratch
+ * whose per-pixel state is UNDEFINED when the aux match below serves the image
+ * (only out_color / out_depth are written then); the source buffers are only
+ * read.  s must describe the source forward (image size, grid); its bg is the
+ * one blended.  Enqueued on `stream`, which must be ordered after the source
+ * forward.  src_aux_mask: NULL, or the gs_params.aux_mask the source forward
+ * composited (the same bytes, unchanged since), addressed like colors: byte i
+ * belongs to colors[i].  It is unsupported with a source forward that used
+ * gs_params.index (that forward read aux_mask[index[i]]); pass NULL there, or
+ * the mask gathered by the index.  Where colors holds exactly (m_i, m_i, m_i)
+ * for every Gaussian (checked on the device, bit for bit) the image is composed
+ * from that forward's grey sum and transmittance instead of blended again — the
+ * same bits; otherwise the blend runs (ABI 18). */
 int gs_render_recolor(const gs_settings *s, int P, int num_rendered, const void *geom_buffer,
                       const void *binning_buffer, const void *img_buffer, const float *colors, void *img_out,
                       float *out_color, float *out_depth, const uint8_t *src_aux_mask, gs_stream_t stream);

@@ -13,6 +13,7 @@
  *   - stable (tile, depth) key sort: equal keys keep Gaussian-index order.
  */
 #include "gs_oracle.h"
+#include "gs_oracle_internal.h"
 
 #include <math.h>
 #include <stdint.h>
@@ -22,8 +23,6 @@
 #include <omp.h>
 #endif
 
-#define TILE_X 16
-#define TILE_Y 16
 
 /* auxiliary.h:22-39 */
 static const float kC0 = 0.28209479177387814f;
@@ -106,7 +105,8 @@ static v3 xform_vec43_T(v3 p, const float *m) {
  * path (dge_amd/csrc/gs_common.h gs_exp) evaluates identically, so every
  * alpha, every skip/stop decision, T and n_contrib can be compared bit for
  * bit.  fmaf is the correctly rounded fused multiply-add (built -mfma). */
-static float gs_expf(float x) {
+GO_EXACT static float gs_expf(float x) {
+    GO_EXACT_BODY
     float u = fmaf(x, 1.44269504f, 12582912.0f); /* 1.5 * 2^23 + rint(x log2e), the product unrounded */
     u = fminf(fmaxf(u, 12582912.0f - 120.0f), 12582912.0f + 120.0f);
     const float n = u - 12582912.0f;
@@ -124,6 +124,17 @@ static float gs_expf(float x) {
     float sc;
     memcpy(&sc, &sb, 4);
     return p * sc;
+}
+
+float go_expf1(float x) { return gs_expf(x); }
+
+GO_EXACT int go_pixel_alpha(const float *co, float dx, float dy, float *G, float *alpha) {
+    GO_EXACT_BODY
+    const float power = -0.5f * (co[0] * dx * dx + co[2] * dy * dy) - co[1] * dx * dy;
+    if (power > 0.0f) return 0;
+    *G = gs_expf(power);
+    *alpha = fminf(0.99f, co[3] * *G);
+    return !(*alpha < 1.0f / 255.0f);
 }
 
 /* Test hook: gs_expf over an array (bit-compared with the GPU's gs_exp). */
@@ -146,25 +157,7 @@ static void tile_rect(float px, float py, int r, int gx, int gy, int *x0, int *y
 /* ------------------------------------------------------------------ */
 /* state                                                                */
 /* ------------------------------------------------------------------ */
-struct go_state {
-    int P, W, H, gx, gy, K;
-    float *depths;         /* P */
-    unsigned char *clamped; /* 3P */
-    int *radii;            /* P */
-    float *means2D;        /* 2P */
-    float *cov3D;          /* 6P */
-    float *conic_opacity;  /* 4P */
-    float *rgb;            /* 3P */
-    uint32_t *tiles_touched; /* P */
-    uint32_t *point_offsets; /* P, inclusive scan */
-    uint64_t *point_keys;    /* K sorted */
-    uint32_t *point_list;    /* K sorted */
-    uint32_t *ranges;        /* 2 * tiles */
-    float *final_T;          /* HW */
-    uint32_t *n_contrib;     /* HW */
-    uint32_t *n_visited;     /* HW: list entries visited before stopping (diagnostic) */
-    const float *features;   /* rgb or colors_precomp (borrowed) */
-};
+/* struct go_state: gs_oracle_internal.h */
 
 void go_free(go_state *st) {
     if (!st) return;
@@ -228,8 +221,9 @@ typedef struct {
     cm3 J, W, T, V;
 } ewa_ctx;
 
-static void ewa_setup(v3 mean, float fx, float fy, float tanfovx, float tanfovy, const float *cov3D,
-                      const float *view, ewa_ctx *e) {
+GO_EXACT static void ewa_setup(v3 mean, float fx, float fy, float tanfovx, float tanfovy, const float *cov3D,
+                               const float *view, ewa_ctx *e) {
+    GO_EXACT_BODY
     v3 t = xform_point43(mean, view);
     e->limx = 1.3f * tanfovx;
     e->limy = 1.3f * tanfovy;
@@ -515,8 +509,21 @@ go_state *go_forward(const go_settings *s, const go_inputs *in, float *out_color
  * gradient term is bounded by the absolute values of the products it adds:
  * dL_dalpha by sum_ch (|c| + |accum|) |dL_dch| T + |T_final/(1-alpha) bg.dL_dpix|,
  * dG/d(delx) by |G dx a| + |G dy b|, and so on. */
+/* em (nullable): every (pixel, instance) term set appended as (Gaussian id, 9 float terms), in the order this
+ * pixel computes them (go_backward_truth sums them in float in several admissible atomic arrival orders). */
+static void emit_terms(go_emit *em, uint32_t id, const float t[9]) {
+    if (em->n == em->cap) {
+        em->cap = em->cap ? 2 * em->cap : 4096;
+        em->ids = (uint32_t *)realloc(em->ids, em->cap * sizeof(uint32_t));
+        em->terms = (float *)realloc(em->terms, em->cap * 9 * sizeof(float));
+    }
+    em->ids[em->n] = id;
+    memcpy(em->terms + 9 * em->n, t, 9 * sizeof(float));
+    em->n++;
+}
+
 static void render_pixel_bwd(const go_state *st, const float *colors, const float *bg, const float *dL_dpix, int tile,
-                             int px, int py, double *rec, double *mag) {
+                             int px, int py, double *rec, double *mag, go_emit *em) {
     const uint32_t r0 = st->ranges[2 * tile], r1 = st->ranges[2 * tile + 1];
     const float pfx = (float)px, pfy = (float)py;
     const size_t pix = (size_t)st->W * py + px, HW = (size_t)st->W * st->H;
@@ -533,22 +540,19 @@ static void render_pixel_bwd(const go_state *st, const float *colors, const floa
         uint32_t id = st->point_list[k];
         float dx = st->means2D[2 * (size_t)id] - pfx, dy = st->means2D[2 * (size_t)id + 1] - pfy;
         const float *co = st->conic_opacity + 4 * (size_t)id;
-        float power = -0.5f * (co[0] * dx * dx + co[2] * dy * dy) - co[1] * dx * dy;
-        if (power > 0.0f) continue;
-        float G = gs_expf(power);
-        float alpha = fminf(0.99f, co[3] * G);
-        if (alpha < 1.0f / 255.0f) continue;
+        float G, alpha;
+        if (!go_pixel_alpha(co, dx, dy, &G, &alpha)) continue;
         T = T / (1.f - alpha);
         float dchannel_dcolor = alpha * T;
         float dL_dalpha = 0.0f;
-        double *r = rec + 9 * (size_t)k;
+        float t9[9];
         for (int ch = 0; ch < 3; ++ch) {
             float c = colors[3 * (size_t)id + ch];
             accum_rec[ch] = last_alpha * last_color[ch] + (1.f - last_alpha) * accum_rec[ch];
             last_color[ch] = c;
             float dL_dch = dL_dpixel[ch];
             dL_dalpha += (c - accum_rec[ch]) * dL_dch;
-            r[6 + ch] += (double)(dchannel_dcolor * dL_dch);
+            t9[6 + ch] = dchannel_dcolor * dL_dch;
         }
         dL_dalpha *= T;
         last_alpha = alpha;
@@ -559,12 +563,17 @@ static void render_pixel_bwd(const go_state *st, const float *colors, const floa
         float gdx = G * dx, gdy = G * dy;
         float dG_ddelx = -gdx * co[0] - gdy * co[1];
         float dG_ddely = -gdy * co[2] - gdx * co[1];
-        r[0] += (double)(dL_dG * dG_ddelx * ddelx_dx);
-        r[1] += (double)(dL_dG * dG_ddely * ddely_dy);
-        r[2] += (double)(-0.5f * gdx * dx * dL_dG);
-        r[3] += (double)(-0.5f * gdx * dy * dL_dG);
-        r[4] += (double)(-0.5f * gdy * dy * dL_dG);
-        r[5] += (double)(G * dL_dalpha);
+        t9[0] = dL_dG * dG_ddelx * ddelx_dx;
+        t9[1] = dL_dG * dG_ddely * ddely_dy;
+        t9[2] = -0.5f * gdx * dx * dL_dG;
+        t9[3] = -0.5f * gdx * dy * dL_dG;
+        t9[4] = -0.5f * gdy * dy * dL_dG;
+        t9[5] = G * dL_dalpha;
+        if (rec) {
+            double *r = rec + 9 * (size_t)k;
+            for (int j = 0; j < 9; ++j) r[j] += (double)t9[j];
+        }
+        if (em) emit_terms(em, id, t9);
         if (mag) {
             double ma = 0, bgm = 0;
             for (int ch = 0; ch < 3; ++ch) {
@@ -584,6 +593,11 @@ static void render_pixel_bwd(const go_state *st, const float *colors, const floa
             for (int ch = 0; ch < 3; ++ch) m[6 + ch] += fabs((double)dchannel_dcolor * dL_dpixel[ch]);
         }
     }
+}
+
+void go_render_pixel_terms(const go_state *st, const float *colors, const float *bg, const float *dL_dpix, int tile,
+                           int px, int py, go_emit *em) {
+    render_pixel_bwd(st, colors, bg, dL_dpix, tile, px, py, NULL, NULL, em);
 }
 
 /* backward.cu:144-274: writes dL_dcov (6) and returns the cov-path mean grad */
@@ -830,7 +844,7 @@ int go_backward(go_state *st, const go_settings *s, const go_inputs *in, const f
         for (int yy = 0; yy < TILE_Y; ++yy)
             for (int xx = 0; xx < TILE_X; ++xx) {
                 int px = tx * TILE_X + xx, py = ty * TILE_Y + yy;
-                if (px < W && py < H) render_pixel_bwd(st, colors, s->bg, dL_dpix, t, px, py, rec, mrec);
+                if (px < W && py < H) render_pixel_bwd(st, colors, s->bg, dL_dpix, t, px, py, rec, mrec, NULL);
             }
     }
     /* per-Gaussian sums over its instances, in sorted order (deterministic) */

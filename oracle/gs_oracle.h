@@ -88,6 +88,20 @@ int go_backward_chain(go_state *st, const go_settings *s, const go_inputs *in, c
 int go_backward_chain_mag(go_state *st, const go_settings *s, const go_inputs *in, const float *m9,
                           double *m_means3D, double *m_cov3D, double *m_sh, double *m_scales, double *m_rotations);
 
+/* The fp64 truth for the per-element gradient bar (gs_truth.c; test infrastructure):
+ * go_backward_truth: sums_d [P,9] (layout of g9; NULL: not computed) — backward.cu's per-pixel formulas in double at the float
+ * forward's state, summed in double; sums_f [n_orders,P,9] (n_orders <= 4) — the oracle's float per-pixel
+ * terms summed in float one by one, as the reference's float atomics add them, in n_orders admissible
+ * arrival orders (0: tiles ascending / pixels row-major / entries back to front, 1: its reverse, 2: the
+ * even-numbered terms then the odd ones, 3: a seeded pseudo-random permutation).
+ * go_backward_chain_f64: the per-Gaussian chain (backward.cu:20-396) in double from double sums, the
+ * forward quantities recomputed in double from the float inputs, the decisions the float forward's. */
+int go_backward_truth(go_state *st, const go_settings *s, const go_inputs *in, const float *dL_dpix, int n_orders,
+                      float *sums_f, double *sums_d);
+int go_backward_chain_f64(go_state *st, const go_settings *s, const go_inputs *in, const double *g9,
+                          double *dL_dmeans3D, double *dL_dcov3D, double *dL_dsh, double *dL_dscales,
+                          double *dL_drotations);
+
 /* Access an intermediate array by name; returns element count or -1. */
 long go_state_get(go_state *st, const char *name, void **ptr);
 void go_free(go_state *st);

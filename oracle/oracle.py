@@ -23,6 +23,10 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB_PATH = os.path.join(_HERE, "liboracle.so")
 _lib = None
+# contraction models of the oracle's backward (oracle/Makefile): "off" is THE oracle; the fma builds are further
+# admissible fp32 evaluations of the reference's arithmetic (nvcc's default -fmad=true) for the fp64-truth bar
+MODELS = {"off": "liboracle.so", "fma_gcc": "liboracle_fma_gcc.so", "fma_clang": "liboracle_fma_clang.so"}
+_models = {}
 
 _f32p = ctypes.POINTER(ctypes.c_float)
 _i32p = ctypes.POINTER(ctypes.c_int)
@@ -61,40 +65,60 @@ class _Inputs(ctypes.Structure):
 
 def build(force: bool = False) -> str:
     """Compile liboracle.so with the committed Makefile (gcc, OpenMP)."""
-    src = os.path.join(_HERE, "gs_oracle.c")
-    if force or not os.path.exists(_LIB_PATH) or os.path.getmtime(_LIB_PATH) < os.path.getmtime(src):
+    srcs = [os.path.join(_HERE, f) for f in ("gs_oracle.c", "gs_truth.c", "gs_oracle.h", "gs_oracle_internal.h",
+                                             "Makefile")]
+    libs = [os.path.join(_HERE, f) for f in MODELS.values()]
+    if force or not all(map(os.path.exists, libs)) or \
+            min(map(os.path.getmtime, libs)) < max(map(os.path.getmtime, srcs)):
         subprocess.run(["make", "-s", "-C", _HERE], check=True)
     return _LIB_PATH
 
 
-def lib():
+def lib(model: str = "off"):
+    """The oracle library of a contraction model (MODELS; "off": the oracle itself)."""
     global _lib
+    if model != "off":
+        if model not in _models:
+            path = os.path.join(_HERE, MODELS[model])
+            if not os.path.exists(path):
+                build()
+            _models[model] = _bind(ctypes.CDLL(path))
+        return _models[model]
     if _lib is None:
         if not os.path.exists(_LIB_PATH):
             build()
-        L = ctypes.CDLL(_LIB_PATH)
-        L.go_forward.restype = ctypes.c_void_p
-        L.go_forward.argtypes = [ctypes.POINTER(_Settings), ctypes.POINTER(_Inputs), _f32p, _f32p, _i32p, _i32p, _i32p]
-        L.go_backward.restype = ctypes.c_int
-        L.go_backward.argtypes = [ctypes.c_void_p, ctypes.POINTER(_Settings), ctypes.POINTER(_Inputs), _f32p] + [_f32p] * 10
-        L.go_backward_chain.restype = ctypes.c_int
-        L.go_backward_chain.argtypes = [ctypes.c_void_p, ctypes.POINTER(_Settings), ctypes.POINTER(_Inputs),
-                                        _f32p] + [_f32p] * 5
-        _f64p = ctypes.POINTER(ctypes.c_double)
-        L.go_backward_chain_mag.restype = ctypes.c_int
-        L.go_backward_chain_mag.argtypes = [ctypes.c_void_p, ctypes.POINTER(_Settings), ctypes.POINTER(_Inputs),
-                                            _f32p] + [_f64p] * 5
-        L.go_state_get.restype = ctypes.c_long
-        L.go_state_get.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_void_p)]
-        L.go_free.argtypes = [ctypes.c_void_p]
-        L.go_mark_visible.argtypes = [ctypes.c_int, _f32p, _f32p, _f32p, _u8p]
-        L.go_apply_weights.restype = ctypes.c_int
-        L.go_apply_weights.argtypes = [ctypes.POINTER(_Settings), ctypes.POINTER(_Inputs), ctypes.c_int, _f32p, _f32p, _i32p]
-        L.go_set_threads.argtypes = [ctypes.c_int]
-        L.go_sh_to_rgb.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, _f32p, _f32p, _f32p, _f32p, _u8p]
-        L.go_expf.argtypes = [ctypes.c_int, _f32p, _f32p]
-        _lib = L
+        _lib = _bind(ctypes.CDLL(_LIB_PATH))
     return _lib
+
+
+def _bind(L):
+    L.go_forward.restype = ctypes.c_void_p
+    L.go_forward.argtypes = [ctypes.POINTER(_Settings), ctypes.POINTER(_Inputs), _f32p, _f32p, _i32p, _i32p, _i32p]
+    L.go_backward.restype = ctypes.c_int
+    L.go_backward.argtypes = [ctypes.c_void_p, ctypes.POINTER(_Settings), ctypes.POINTER(_Inputs), _f32p] + [_f32p] * 10
+    L.go_backward_chain.restype = ctypes.c_int
+    L.go_backward_chain.argtypes = [ctypes.c_void_p, ctypes.POINTER(_Settings), ctypes.POINTER(_Inputs),
+                                    _f32p] + [_f32p] * 5
+    _f64p = ctypes.POINTER(ctypes.c_double)
+    L.go_backward_chain_mag.restype = ctypes.c_int
+    L.go_backward_chain_mag.argtypes = [ctypes.c_void_p, ctypes.POINTER(_Settings), ctypes.POINTER(_Inputs),
+                                        _f32p] + [_f64p] * 5
+    L.go_backward_truth.restype = ctypes.c_int
+    L.go_backward_truth.argtypes = [ctypes.c_void_p, ctypes.POINTER(_Settings), ctypes.POINTER(_Inputs), _f32p,
+                                    ctypes.c_int, _f32p, _f64p]
+    L.go_backward_chain_f64.restype = ctypes.c_int
+    L.go_backward_chain_f64.argtypes = [ctypes.c_void_p, ctypes.POINTER(_Settings), ctypes.POINTER(_Inputs),
+                                        _f64p] + [_f64p] * 5
+    L.go_state_get.restype = ctypes.c_long
+    L.go_state_get.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_void_p)]
+    L.go_free.argtypes = [ctypes.c_void_p]
+    L.go_mark_visible.argtypes = [ctypes.c_int, _f32p, _f32p, _f32p, _u8p]
+    L.go_apply_weights.restype = ctypes.c_int
+    L.go_apply_weights.argtypes = [ctypes.POINTER(_Settings), ctypes.POINTER(_Inputs), ctypes.c_int, _f32p, _f32p, _i32p]
+    L.go_set_threads.argtypes = [ctypes.c_int]
+    L.go_sh_to_rgb.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, _f32p, _f32p, _f32p, _f32p, _u8p]
+    L.go_expf.argtypes = [ctypes.c_int, _f32p, _f32p]
+    return L
 
 
 def set_threads(n: int) -> None:
@@ -259,7 +283,7 @@ def forward(settings, means3D, opacities, shs=None, colors_precomp=None, scales=
     return nr.value, color, depth, radii, State(h, s, inp, nr.value)
 
 
-def backward(state: State, dL_dpix, magnitudes: bool = True):
+def backward(state: State, dL_dpix, magnitudes: bool = True, model: str = "off"):
     """rasterize_points.cu:97-157 semantics -> dict of the 8 reference grads (+ dL_dconic, and with
     `magnitudes` "mag9" [P,9]: the per-Gaussian sum of absolute sub-terms of (dL_dmean2D x, y,
     dL_dconic x, y, w, dL_dopacity, dL_dcolor r, g, b), the cancellation-aware scale of each sum)."""
@@ -280,7 +304,7 @@ def backward(state: State, dL_dpix, magnitudes: bool = True):
     if magnitudes:
         out["mag9"] = np.zeros((P, 9), np.float32)
     cs, ci = s.c(), inp.c()
-    rc = lib().go_backward(state.handle, ctypes.byref(cs), ctypes.byref(ci), _ptr(g), *[
+    rc = lib(model).go_backward(state.handle, ctypes.byref(cs), ctypes.byref(ci), _ptr(g), *[
         _ptr(out[k]) if out[k].size else None for k in
         ("dL_dmeans2D", "dL_dcolors", "dL_dopacity", "dL_dmeans3D", "dL_dcov3D", "dL_dsh", "dL_dscales",
          "dL_drotations", "dL_dconic")], _ptr(out["mag9"]) if magnitudes and P else None)
@@ -289,7 +313,7 @@ def backward(state: State, dL_dpix, magnitudes: bool = True):
     return out
 
 
-def backward_chain(state: State, g9):
+def backward_chain(state: State, g9, model: str = "off"):
     """The per-Gaussian chain of the backward (backward.cu:144-396) from float rasterizer sums
     g9 [P,9] = (dL_dmean2D x, y, dL_dconic x, y, w, dL_dopacity, dL_dcolor r, g, b)."""
     s, inp = state.settings, state.inputs
@@ -303,7 +327,7 @@ def backward_chain(state: State, g9):
         "dL_drotations": np.zeros((P, 4), np.float32),
     }
     cs, ci = s.c(), inp.c()
-    rc = lib().go_backward_chain(state.handle, ctypes.byref(cs), ctypes.byref(ci), _ptr(g), *[
+    rc = lib(model).go_backward_chain(state.handle, ctypes.byref(cs), ctypes.byref(ci), _ptr(g), *[
         _ptr(out[k]) if out[k].size else None for k in
         ("dL_dmeans3D", "dL_dcov3D", "dL_dsh", "dL_dscales", "dL_drotations")])
     if rc != 0:
@@ -332,6 +356,52 @@ def backward_chain_mag(state: State, m9):
         ("dL_dmeans3D", "dL_dcov3D", "dL_dsh", "dL_dscales", "dL_drotations")])
     if rc != 0:
         raise RuntimeError(f"oracle backward_chain_mag failed with code {rc}")
+    return out
+
+
+TRUTH_ORDERS = 4
+
+
+def backward_truth(state: State, dL_dpix, n_orders: int = TRUTH_ORDERS, model: str = "off", double: bool = True):
+    """The rasterizer sums for the fp64-truth bar (gs_truth.c go_backward_truth): {"sums_d": [P,9] float64 —
+    backward.cu's per-pixel formulas in double at the float forward's state; "sums_f": [n_orders,P,9] float32
+    — the oracle's float per-pixel terms summed one by one in float, as the reference's float atomics add
+    them, in n_orders admissible arrival orders}.  Layout of each row: (dL_dmean2D x, y, dL_dconic x, y, w,
+    dL_dopacity, dL_dcolor r, g, b).  model: whose float terms (MODELS); double=False: no sums_d (None)."""
+    s, inp = state.settings, state.inputs
+    P = inp.P
+    g = _np(dL_dpix).reshape(3, s.image_height, s.image_width)
+    sums_f = np.zeros((n_orders, P, 9), np.float32)
+    sums_d = np.zeros((P, 9), np.float64) if double else None
+    cs, ci = s.c(), inp.c()
+    rc = lib(model).go_backward_truth(state.handle, ctypes.byref(cs), ctypes.byref(ci), _ptr(g), int(n_orders),
+                                      _ptr(sums_f), _ptr(sums_d, ctypes.POINTER(ctypes.c_double)))
+    if rc != 0:
+        raise RuntimeError(f"oracle backward_truth failed with code {rc}")
+    return {"sums_d": sums_d, "sums_f": sums_f}
+
+
+def backward_chain_f64(state: State, g9):
+    """The per-Gaussian chain (backward.cu:20-396) in double (gs_truth.c go_backward_chain_f64) from float64
+    sums g9 [P,9]: the truth's parameter gradients w.r.t. the activated parameters (dL_dscales w.r.t.
+    scale_modifier * scale, dL_drotations w.r.t. the unnormalised quaternion), all float64."""
+    s, inp = state.settings, state.inputs
+    P, M = inp.P, inp.M
+    g = np.ascontiguousarray(np.asarray(g9, np.float64).reshape(P, 9))
+    out = {
+        "dL_dmeans3D": np.zeros((P, 3), np.float64),
+        "dL_dcov3D": np.zeros((P, 6), np.float64),
+        "dL_dsh": np.zeros((P, M, 3), np.float64),
+        "dL_dscales": np.zeros((P, 3), np.float64),
+        "dL_drotations": np.zeros((P, 4), np.float64),
+    }
+    f64 = ctypes.POINTER(ctypes.c_double)
+    cs, ci = s.c(), inp.c()
+    rc = lib().go_backward_chain_f64(state.handle, ctypes.byref(cs), ctypes.byref(ci), _ptr(g, f64), *[
+        _ptr(out[k], f64) if out[k].size else None for k in
+        ("dL_dmeans3D", "dL_dcov3D", "dL_dsh", "dL_dscales", "dL_drotations")])
+    if rc != 0:
+        raise RuntimeError(f"oracle backward_chain_f64 failed with code {rc}")
     return out
 
 

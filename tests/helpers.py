@@ -321,3 +321,163 @@ def compare_grads(got, ref, rtol=RTOL, O=None, label="", rows=None):
     print(f"[parity{(' ' + label) if label else ''}] end-to-end max |err|/max|ref|: {worst}")
     for n in GRAD_NAMES:
         assert_close(sel(got[n]), sel(ref[n]), n, rtol)
+
+
+# ---------------------------------------------------------------------------
+# The fp64-truth bar for the gradients DGE consumes (round 6)
+# ---------------------------------------------------------------------------
+# truth: backward.cu's formulas in double at the float forward's state (oracle/gs_truth.c): the rasterizer
+# sums (go_backward_truth sums_d) through the per-Gaussian chain in double (go_backward_chain_f64) and the
+# reference getters' derivatives in double.  The reference's own fp32 arithmetic: the oracle's float
+# per-pixel terms summed one by one in float as its float atomics add them, in TRUTH_ORDERS admissible
+# arrival orders (sums_f), plus the oracle's float rounding of the double sum (go_backward), each through the
+# float chain (go_backward_chain, backward.cu:144-396) and torch's fp32 getters (gaussian_model.py:221-258).
+# Per element:  |got - truth| <= TRUTH_MULT * E_ref + TRUTH_REL * |truth|,  E_ref = max over those fp32
+# evaluations of |ref - truth|; the elements the second term alone admits are counted and capped.
+TRUTH_MULT = 4.0
+TRUTH_REL = 1e-4
+TRUTH_ONLY_REL_MAX = 0.01
+PARAM_NAMES = ["_xyz", "_features_dc", "_features_rest", "_opacity", "_scaling", "_rotation"]
+
+
+def getter_grads_fp32(raw, act, half_sh=False):
+    """The reference getters' backward in torch fp32 on the CPU (gaussian_model.py:221-258: get_features =
+    cat(dc, rest), get_opacity = sigmoid, get_scaling = exp, get_rotation = F.normalize): raw [n, ...] CPU
+    float32 tensors of the six parameters, act the activated-parameter gradients (dL_dmeans3D, dL_dsh,
+    dL_dopacity, dL_dscales, dL_drotations).  half_sh: SH stored fp16, its gradient cast to fp16 (autograd's
+    cast back to the half leaf)."""
+    import torch.nn.functional as F
+
+    leaves = {k: raw[k].detach().clone().float().requires_grad_(True) for k in PARAM_NAMES}
+    outs = [leaves["_xyz"], torch.cat([leaves["_features_dc"], leaves["_features_rest"]], 1),
+            torch.sigmoid(leaves["_opacity"]), torch.exp(leaves["_scaling"]), F.normalize(leaves["_rotation"])]
+    gs = [act["dL_dmeans3D"], act["dL_dsh"], act["dL_dopacity"], act["dL_dscales"], act["dL_drotations"]]
+    torch.autograd.backward(outs, [torch.as_tensor(np.asarray(g, np.float32)).reshape(o.shape) for o, g in
+                                   zip(outs, gs)])
+    res = {k: leaves[k].grad.numpy().astype(np.float64) for k in PARAM_NAMES}
+    if half_sh:
+        for k in ("_features_dc", "_features_rest"):
+            res[k] = res[k].astype(np.float16).astype(np.float64)
+    return res
+
+
+def getter_grads_f64(raw, act):
+    """The same derivatives in float64 (numpy) from the raw parameters."""
+    r = {k: np.asarray(raw[k].detach().float().cpu().numpy() if hasattr(raw[k], "detach") else raw[k], np.float64)
+         for k in PARAM_NAMES}
+    sh = np.asarray(act["dL_dsh"], np.float64)
+    s = 1.0 / (1.0 + np.exp(-r["_opacity"]))
+    q = r["_rotation"]
+    qn = np.maximum(np.linalg.norm(q, axis=1, keepdims=True), 1e-12)
+    y = q / qn
+    gq = np.asarray(act["dL_drotations"], np.float64)
+    return {"_xyz": np.asarray(act["dL_dmeans3D"], np.float64), "_features_dc": sh[:, :1], "_features_rest": sh[:, 1:],
+            "_opacity": np.asarray(act["dL_dopacity"], np.float64).reshape(s.shape) * s * (1.0 - s),
+            "_scaling": np.asarray(act["dL_dscales"], np.float64) * np.exp(r["_scaling"]),
+            "_rotation": (gq - y * np.sum(y * gq, axis=1, keepdims=True)) / qn}
+
+
+def truth_case(O, st, dL_dpix, raw, half_sh=False, n_orders=None, models=None):
+    """(truth, refs, names, rows) for a forward whose oracle state is `st` and whose raw parameter rows are
+    `raw` (CPU tensors): the truth and every fp32 evaluation of the reference's backward as {parameter:
+    [rows, ...] float64, "viewspace": [rows, 2]} over `rows`, the Gaussians with a nonzero rasterizer sum in the
+    truth (every other Gaussian's gradients are exactly zero in the truth and in every evaluation: the chain
+    of zero sums).  names labels the refs "<model>:<sums>": the contraction model of the float arithmetic —
+    "off", or fma contraction as gcc / clang apply it, two admissible models of nvcc's default -fmad=true —
+    and the sums' arrival order, or "rounded" for the double sum rounded to float."""
+    n_orders = O.TRUTH_ORDERS if n_orders is None else n_orders
+    models = list(O.MODELS) if models is None else models
+    truth = rows = None
+    refs, names = [], []
+    for model in models:
+        tb = O.backward_truth(st, dL_dpix, n_orders, model=model, double=truth is None)
+        if truth is None:
+            sd = tb["sums_d"]
+            rows = np.flatnonzero(np.any(sd != 0, axis=1))
+            ch = O.backward_chain_f64(st, sd)
+            t = getter_grads_f64(raw, dict(ch, dL_dopacity=sd[:, 5:6]))
+            t["viewspace"] = sd[:, 0:2]
+            truth = {k: v[rows] for k, v in t.items()}
+        base = O.backward(st, dL_dpix, magnitudes=False, model=model)
+        cands = [("rounded", raster_sums(base))] + [(f"order{o}", tb["sums_f"][o]) for o in range(n_orders)]
+        for name, s9 in cands:
+            c = O.backward_chain(st, s9, model=model)
+            r = getter_grads_fp32(raw, dict(c, dL_dopacity=s9[:, 5:6]), half_sh)
+            r["viewspace"] = np.asarray(s9[:, 0:2], np.float64)
+            refs.append({k: v[rows] for k, v in r.items()})
+            names.append(f"{model}:{name}")
+    return truth, refs, names, rows
+
+
+def _bar_counts(err, E, t, nz, mult, rel):
+    bound = mult * E + rel * np.abs(t)
+    held = nz & (err <= mult * E)
+    only = nz & ~held & (err <= bound)
+    beyond = nz & (err > bound)
+    ratio = np.where(bound > 0, err / np.maximum(bound, 1e-300), np.where(err > 0, np.inf, 0.0))
+    return held, only, beyond, ratio
+
+
+def truth_bar(got, truth, refs, label="", mult=TRUTH_MULT, rel=TRUTH_REL, max_only_rel=TRUTH_ONLY_REL_MAX,
+              dump=None, names=None, check=True):
+    """Per tensor: |got - truth| <= mult * E_ref + rel * |truth| per element (E_ref: the largest error of the
+    fp32 evaluations `refs` against the truth), at most max_only_rel of the nonzero elements admitted by the
+    rel * |truth| term alone, and no more elements beyond the bound than the reference's own evaluations show
+    when each contraction model's evaluations are held to the other models' E_ref (a model of the reference's
+    arithmetic that is not the reference's own misses this per-element bar at a few elements per million —
+    heavily cancelled sums — so that count, measured here on the same case, is the allowance).  Prints per
+    tensor: nonzero elements, held by mult * E_ref, admitted only by rel |truth| (%), beyond, the worst err /
+    bound, then [the reference's own: worst only-rel %, most elements beyond, worst err/bound]."""
+    names = names or [f"ref{k}" for k in range(len(refs))]
+    groups = {}
+    for k, nm in enumerate(names):
+        groups.setdefault(nm.split(":")[0], []).append(k)
+    stats = {}
+    for n, t in truth.items():
+        g = np.asarray(got[n], np.float64)
+        t = np.asarray(t, np.float64)
+        assert g.shape == t.shape, f"{n}: {g.shape} vs {t.shape}"
+        err = np.abs(g - t)
+        errs = np.stack([np.abs(np.asarray(r[n], np.float64) - t) for r in refs])
+        nz = (t != 0) | (g != 0)
+        held, only, beyond, ratio = _bar_counts(err, errs.max(0), t, nz, mult, rel)
+        i = np.unravel_index(int(np.argmax(ratio)), t.shape) if ratio.size else None
+        row = dict(nonzero=int(nz.sum()), held=int(held.sum()), only_rel=int(only.sum()), beyond=int(beyond.sum()),
+                   worst=float(ratio.max()) if ratio.size else 0.0,
+                   note="" if i is None else f"got {g[i]:.6e} truth {t[i]:.6e} E_ref {errs.max(0)[i]:.3e}")
+        self_only, self_beyond, self_worst = 0.0, 0, 0.0
+        if len(groups) > 1:  # each model's evaluations against the other models' envelope
+            gmax = {m: errs[idx].max(0) for m, idx in groups.items()}
+            for m, idx in groups.items():
+                E_other = np.max([e for mm, e in gmax.items() if mm != m], axis=0)
+                for k in idx:
+                    rnz = (t != 0) | (np.asarray(refs[k][n]) != 0)
+                    _, o_k, b_k, r_k = _bar_counts(errs[k], E_other, t, rnz, mult, rel)
+                    self_only = max(self_only, float(o_k.sum()) / max(int(rnz.sum()), 1))
+                    self_beyond = max(self_beyond, int(b_k.sum()))
+                    self_worst = max(self_worst, float(r_k.max()) if r_k.size else 0.0)
+        row.update(self_only=self_only, self_beyond=self_beyond, self_worst=self_worst)
+        stats[n] = row
+    print(f"[truth bar{(' ' + label) if label else ''}] per tensor: nonzero / held by {mult:g} x E_ref / "
+          f"admitted only by {rel:g} |truth| / beyond (allowed) / worst err/bound — E_ref over {len(refs)} fp32 "
+          f"evaluations ({', '.join(f'{m} x{len(v)}' for m, v in groups.items())}); [the reference's own models held "
+          "to each other: worst only-rel %, most beyond, worst err/bound]")
+    for n, a in stats.items():
+        frac = a["only_rel"] / max(a["nonzero"], 1)
+        print(f"  {n:15s} {a['nonzero']:9d} {a['held']:9d} {a['only_rel']:7d} ({100 * frac:.3f}%) {a['beyond']:4d} "
+              f"({a['self_beyond']}) worst {a['worst']:.3g}  [{100 * a['self_only']:.3f}%, {a['self_beyond']}, "
+              f"{a['self_worst']:.3g}]  {a['note']}")
+    if dump:  # (offline analysis: at most 10k of the compared rows, float32 except the truth)
+        nrow = len(next(iter(truth.values())))
+        sel = np.arange(nrow) if nrow <= 10000 else np.sort(np.random.default_rng(0).choice(nrow, 10000, replace=False))
+        np.savez(dump, sel=sel, names=np.array(names), **{f"got_{n}": np.asarray(got[n], np.float32)[sel] for n in truth},
+                 **{f"truth_{n}": np.asarray(t)[sel] for n, t in truth.items()},
+                 **{f"ref{k}_{n}": np.asarray(r[n], np.float32)[sel] for k, r in enumerate(refs) for n in truth})
+    if check:
+        for n, a in stats.items():
+            assert a["beyond"] <= a["self_beyond"], \
+                f"{label} {n}: {a['beyond']} elements beyond {mult:g} E_ref + {rel:g}|truth| (the reference's own " \
+                f"models: {a['self_beyond']}); {a['note']}"
+            assert a["only_rel"] <= max_only_rel * a["nonzero"], \
+                f"{label} {n}: {a['only_rel']} of {a['nonzero']} nonzero elements admitted only by the {rel:g}|truth| term"
+    return stats

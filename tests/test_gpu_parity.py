@@ -396,6 +396,116 @@ def test_c2_render_raw_parameter_grads_per_element(cuda_device, oracle):
         assert w[1] <= RTOL, f"{n}: worst relative error {w[1]:.3g} above the floor"
 
 
+def _fused_truth_check(O, sc, pkg, G, cam_cpu, label, index=None, half_sh=False):
+    """render()'s fused raw-parameter gradients (already in sc's .grad, pkg its outputs) against the fp64
+    truth (tests/helpers.py truth_bar).  The oracle runs on the device's own activations of the rendered rows
+    (gs_activate_params: the device functions the fused kernels apply, so the forward — every blend decision —
+    is bit-identical, asserted) with SH as stored (fp16 upcast when half_sh); the truth and the reference's fp32
+    evaluations (five: the oracle's float sums and four atomic arrival orders) chain through the getters of
+    the raw rows.  DGE_AMD_TRUTH_DUMP=<dir>: the compared rows are saved there (offline analysis)."""
+    import ctypes
+    import os
+
+    from dge_amd import _native as N
+    from dge_amd.gaussian_renderer import _settings
+    from helpers import PARAM_NAMES, truth_bar, truth_case
+
+    dev = sc._xyz.device
+    params = dict(zip(PARAM_NAMES, sc.parameters()))
+    rows = None if index is None else index.to(dev).long()
+    raw = {k: (p.detach() if rows is None else p.detach()[rows]).contiguous() for k, p in params.items()}
+    n = raw["_xyz"].shape[0]
+    with torch.no_grad():
+        op, scl, rot = (torch.empty(n, k, device=dev) for k in (1, 3, 4))
+        N.check(N.lib().gs_activate_params(n, raw["_opacity"].data_ptr(), raw["_scaling"].data_ptr(),
+                                           raw["_rotation"].data_ptr(), op.data_ptr(), scl.data_ptr(), rot.data_ptr(),
+                                           ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)),
+                "gs_activate_params")
+        torch.cuda.synchronize()
+    s = _settings(cam_cpu, torch.zeros(3), 1.0, sc.active_sh_degree)
+    shs = torch.cat([raw["_features_dc"], raw["_features_rest"]], 1).float().cpu().numpy()
+    _, color, _, radii, st = O.forward(s, means3D=raw["_xyz"].cpu().numpy(), opacities=op.cpu().numpy(), shs=shs,
+                                       scales=scl.cpu().numpy(), rotations=rot.cpu().numpy())
+    np.testing.assert_array_equal(pkg["radii"].cpu().numpy(), radii)
+    np.testing.assert_array_equal(pkg["render"].detach().cpu().numpy(), color)  # every blend decision the oracle's
+    truth, refs, names, live = truth_case(O, st, G.detach().cpu().numpy(), {k: v.cpu() for k, v in raw.items()},
+                                          half_sh)
+    got = {k: (p.grad if rows is None else p.grad[rows]).float().cpu().numpy().astype(np.float64)
+           for k, p in params.items()}
+    got["viewspace"] = pkg["viewspace_points"].grad.cpu().numpy()[:, :2].astype(np.float64)
+    dead = np.ones(n, bool)
+    dead[live] = False
+    for k, v in got.items():  # a Gaussian with all-zero rasterizer sums has exactly zero gradients
+        assert not np.any(v[dead]), f"{label} {k}: nonzero gradient at a Gaussian no pixel blended"
+    got = {k: v[live] for k, v in got.items()}
+    d = os.environ.get("DGE_AMD_TRUTH_DUMP")
+    return truth_bar(got, truth, refs, label, dump=os.path.join(d, f"truth_{label}.npz") if d else None, names=names)
+
+
+def test_c2_render_raw_grads_vs_fp64_truth(cuda_device, oracle):
+    """The gradients DGE consumes, at the timed size (c2: 1M Gaussians, 512x512, view 0 of the bench's 3-view
+    orbit; render()'s fused raw-parameter path: activations in-kernel, gradients written into _xyz.grad ...
+    _rotation.grad), held per element to the fp64 truth: |got - truth| <= 4 E_ref + 1e-4 |truth|, E_ref the
+    largest error of the reference's fp32 evaluations, at most 1% of a tensor's nonzero elements admitted by
+    the second term alone (tests/helpers.py truth_bar; backward.cu:144-557, gaussian_model.py:221-258)."""
+    from dge_amd.cameras import orbit_camera
+    from dge_amd.gaussian_renderer import PipelineParams, _fused_ok, render
+    from dge_amd.scene import synthetic_scene
+
+    dev = torch.device("cuda")
+    P, W, H, V = 1_000_000, 512, 512, 3
+    sc = synthetic_scene(P, sh_degree=3, seed=0, device=dev).requires_grad_(True)
+    assert _fused_ok(sc, PipelineParams())
+    G = (torch.randn(3, H, W, generator=torch.Generator().manual_seed(1)) * 1e-3).to(dev)
+    pkg = render(orbit_camera(0, V, W, H, device=dev), sc, PipelineParams(), torch.zeros(3, device=dev))
+    pkg["render"].backward(G)
+    torch.cuda.synchronize()
+    _fused_truth_check(oracle, sc, pkg, G, orbit_camera(0, V, W, H, device="cpu"), "c2")
+
+
+def test_c5_render_fp16_sh_local_edit_vs_fp64_truth(cuda_device, oracle):
+    """configs[4] through render(): 1M-Gaussian scene, localize on a 200k mask, SH stored fp16 (upcast
+    in-kernel, gradients written back as fp16), the fused index path — its subset-row gradients against the
+    fp64 truth with the same bar as c2 (the reference's fp32 evaluations' SH gradients cast to fp16, as
+    autograd casts them back to the half leaf)."""
+    from dge_amd.cameras import orbit_camera
+    from dge_amd.gaussian_renderer import PipelineParams, render
+    from dge_amd.scene import synthetic_scene
+
+    dev = torch.device("cuda")
+    P, Psub, W, H = 1_000_000, 200_000, 512, 512
+    sc = synthetic_scene(P, seed=0, device=dev)
+    sc._features_dc = sc._features_dc.half()
+    sc._features_rest = sc._features_rest.half()
+    order = torch.argsort(sc._xyz[:, 0])
+    mask = torch.zeros(P, dtype=torch.bool, device=dev)
+    mask[order[:Psub]] = True
+    sc.mask, sc.localize = mask, True
+    sc.requires_grad_(True)
+    G = (torch.randn(3, H, W, generator=torch.Generator().manual_seed(1)) * 1e-3).to(dev)
+    pkg = render(orbit_camera(0, 1, W, H, device=dev), sc, PipelineParams(), torch.zeros(3, device=dev))
+    (pkg["render"] * G).sum().backward()
+    torch.cuda.synchronize()
+    assert sc._features_dc.grad.dtype == torch.float16
+    _fused_truth_check(oracle, sc, pkg, G, orbit_camera(0, 1, W, H, device="cpu"), "c5",
+                       index=torch.nonzero(mask).flatten(), half_sh=True)
+
+
+def test_render_dropin_autograd_vs_fp64_truth(cuda_device, oracle):
+    """test_render_dropin_autograd's render() (5000 Gaussians, 160x120) held to the fp64 truth bar."""
+    from dge_amd.cameras import orbit_camera
+    from dge_amd.gaussian_renderer import PipelineParams, render
+    from dge_amd.scene import synthetic_scene
+
+    dev = torch.device("cuda")
+    sc = synthetic_scene(5000, seed=77, radius=1.5, scale=0.04, device=dev).requires_grad_(True)
+    G = torch.randn(3, 120, 160, generator=torch.Generator().manual_seed(9)).to(dev)
+    pkg = render(orbit_camera(1, 4, 160, 120, device=dev), sc, PipelineParams(), torch.zeros(3, device=dev))
+    (pkg["render"] * G).sum().backward()
+    torch.cuda.synchronize()
+    _fused_truth_check(oracle, sc, pkg, G, orbit_camera(1, 4, 160, 120, device="cpu"), "dropin")
+
+
 def test_c4_hd_forward_vs_oracle(cuda_device, oracle):
     """configs[3]: 2.5M Gaussians, 1920x1080 forward (8160 tiles -> two-pass tile sort), bit-identical."""
     from dge_amd.gaussian_renderer import _settings
@@ -564,6 +674,58 @@ def test_dge_loop_backward_merges_the_views_passes(cuda_device, views, pre_grad,
     for x, y in zip(va, vb):
         assert torch.equal(x, y)
     assert all(bool(v.abs().sum() > 0) for v in va)
+
+
+def test_deferred_passes_survive_a_failed_backward(cuda_device):
+    """A backward that raises after a view's per-Gaussian pass was deferred never runs its final callback.
+    The next backward must still run its own deferred passes (its .grad fully written, equal to a backward
+    that never deferred) — the pending list is tied to the graph task that queued its callback, and a stale
+    list is flushed (its passes run into the failed backward's buffers) before the next one starts."""
+    from dge_amd import diff_gaussian_rasterization as R
+    from dge_amd.cameras import orbit_camera
+    from dge_amd.gaussian_renderer import PipelineParams, render
+    from dge_amd.scene import synthetic_scene
+
+    dev = torch.device("cuda")
+    W, H = 160, 120
+    cams = [orbit_camera(k, 2, W, H, device=dev) for k in range(2)]
+    G = torch.randn(3, H, W, generator=torch.Generator().manual_seed(4)).to(dev)
+    bg = torch.zeros(3, device=dev)
+
+    class Raiser(torch.autograd.Function):
+        @staticmethod
+        def forward(ctx, x):
+            return x * 1.0
+
+        @staticmethod
+        def backward(ctx, g):
+            raise RuntimeError("injected backward failure")
+
+    def loss(sc, fail):
+        leaf = torch.ones(4, device=dev, requires_grad=True)
+        side = Raiser.apply(leaf) if fail else leaf * 1.0  # (created first: autograd runs it after the renders)
+        imgs = [render(c, sc, PipelineParams(), bg)["render"] for c in cams]
+        return sum((im * G).sum() for im in imgs) + side.sum() * 0.0
+
+    sc = synthetic_scene(15_000, seed=6, radius=1.5, scale=0.03, device=dev).requires_grad_(True)
+    with pytest.raises(RuntimeError, match="injected"):
+        loss(sc, True).backward()
+    assert R._PENDING_PASSES  # the failed backward left its deferred passes behind
+    for p in sc.parameters():
+        p.grad = None
+    loss(sc, False).backward()
+    torch.cuda.synchronize()
+    assert not R._PENDING_PASSES
+    got = [p.grad.clone() for p in sc.parameters()]
+
+    prev, R._DEFER_PASSES = R._DEFER_PASSES, False
+    try:
+        ref = synthetic_scene(15_000, seed=6, radius=1.5, scale=0.03, device=dev).requires_grad_(True)
+        loss(ref, False).backward()
+    finally:
+        R._DEFER_PASSES = prev
+    for g, p in zip(got, ref.parameters()):
+        assert torch.equal(g, p.grad)
 
 
 def test_c5_local_edit_fp16_sh_vs_oracle(cuda_device, oracle):

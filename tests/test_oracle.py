@@ -296,3 +296,83 @@ def test_blend_exp_accuracy(oracle):
     assert ulps[: -1_000_000].max() <= 0.86 and ulps.max() <= 1.0, ulps.max()
     odd = oracle.expf(np.array([np.nan, -np.inf, -1e30, -200.0, -90.0, -83.5], np.float32))
     assert np.isnan(odd[0]) and np.all(odd[1:] < 1.0 / 255.0)
+
+
+# ---------------------------------------------------------------------------
+# the fp64 truth of the per-element gradient bar (oracle/gs_truth.c, tests/helpers.py truth_bar)
+# ---------------------------------------------------------------------------
+def test_truth_matches_dense_float64_autograd(oracle):
+    """The truth (backward.cu's formulas in double at the float forward's state) against autograd of the
+    independent dense float64 formulation (tests/torch_ref.py, which also recomputes the forward in double):
+    equal to the forward state's float rounding, <= 1e-5 x (|autograd| + the terms' magnitude) per element
+    (measured ~1.5e-6); the double sums agree with the oracle's double sums of its float terms to the terms'
+    own float rounding (<= 1e-5 x magnitude)."""
+    import torch_ref as TR
+
+    P, W, H = 300, 64, 64
+    a, s = _pin_scene(P, 3, "sh", W, H)
+    G = np.random.default_rng(2).standard_normal((3, H, W)).astype(np.float32)
+    kw = dict(shs=a["shs"], scales=a["scales"], rotations=a["rotations"])
+    ref = run_oracle(oracle, s, G, means3D=a["means3D"], opacities=a["opacities"], **kw)
+    st = ref["state"]
+    tb = oracle.backward_truth(st, G)
+    from helpers import raster_sums
+
+    mag9 = ref["mag9"].astype(np.float64)
+    assert np.all(np.abs(tb["sums_d"] - raster_sums(ref)) <= 1e-5 * mag9 + 1e-30)
+    ch = oracle.backward_chain_f64(st, tb["sums_d"])
+    leaf = {k: torch.tensor(v, dtype=torch.float64, requires_grad=True) for k, v in kw.items()}
+    m3 = torch.tensor(a["means3D"], dtype=torch.float64, requires_grad=True)
+    op = torch.tensor(a["opacities"], dtype=torch.float64, requires_grad=True)
+    m2 = torch.zeros(P, 3, dtype=torch.float64, requires_grad=True)
+    c, _, _, _ = TR.dense_render(m3, op, s, means2D=m2, **leaf)
+    (c * torch.as_tensor(G, dtype=torch.float64)).sum().backward()
+    mag = oracle.backward_chain_mag(st, ref["mag9"])
+    for name, t, ag, m in [("dL_dmeans3D", ch["dL_dmeans3D"], m3.grad, mag["dL_dmeans3D"]),
+                           ("dL_dsh", ch["dL_dsh"], leaf["shs"].grad, mag["dL_dsh"]),
+                           ("dL_dscales", ch["dL_dscales"], leaf["scales"].grad, mag["dL_dscales"]),
+                           ("dL_drotations", ch["dL_drotations"], leaf["rotations"].grad, mag["dL_drotations"]),
+                           ("dL_dopacity", tb["sums_d"][:, 5], op.grad.reshape(-1), mag9[:, 5]),
+                           ("dL_dmeans2D", tb["sums_d"][:, :2], m2.grad[:, :2], mag9[:, :2])]:
+        ag = ag.numpy()
+        worst = float((np.abs(t - ag) / (np.abs(ag) + m + 1e-300)).max())
+        assert worst <= 1e-5, f"{name}: truth vs dense float64 autograd {worst:.3g}"
+
+
+def test_truth_bar_admits_the_references_arithmetic_and_catches_an_error(oracle):
+    """Every fp32 evaluation of the reference's backward (3 contraction models x (the double sum rounded + 4
+    atomic arrival orders)) lies within 1e-4 x magnitude of the truth's rasterizer sums; the bar admits one of
+    them as `got`, and rejects it once 5% of its elements carry a relative error of 5e-4."""
+    from dge_amd.gaussian_renderer import _settings
+    from dge_amd.cameras import orbit_camera
+    from dge_amd.scene import synthetic_scene
+    from helpers import PARAM_NAMES, truth_bar, truth_case
+
+    W, H = 128, 128
+    sc = synthetic_scene(20_000, seed=3, radius=1.5, scale=0.03)
+    raw = dict(zip(PARAM_NAMES, [p.detach() for p in sc.parameters()]))
+    with torch.no_grad():
+        op, scl, rot = sc.get_opacity, sc.get_scaling, sc.get_rotation
+    s = _settings(orbit_camera(0, 1, W, H, device="cpu"), torch.zeros(3), 1.0, 3)
+    shs = torch.cat([raw["_features_dc"], raw["_features_rest"]], 1).numpy()
+    _, _, _, _, st = oracle.forward(s, means3D=raw["_xyz"].numpy(), opacities=op.numpy(), shs=shs,
+                                    scales=scl.numpy(), rotations=rot.numpy())
+    G = np.random.default_rng(5).standard_normal((3, H, W)).astype(np.float32)
+    base = oracle.backward(st, G)
+    tb = oracle.backward_truth(st, G)
+    mag9 = base["mag9"].astype(np.float64)
+    for model in oracle.MODELS:
+        t = oracle.backward_truth(st, G, model=model, double=False)
+        for o in range(oracle.TRUTH_ORDERS):
+            assert np.all(np.abs(t["sums_f"][o] - tb["sums_d"]) <= 1e-4 * mag9 + 1e-30), (model, o)
+    truth, refs, names, rows = truth_case(oracle, st, G, raw)
+    assert len(refs) == 3 * (1 + oracle.TRUTH_ORDERS) and len(rows) > 1000
+    k = names.index("fma_clang:order3")
+    got = refs[k]
+    others = [r for j, r in enumerate(refs) if j != k]
+    onames = [n for j, n in enumerate(names) if j != k]
+    truth_bar(got, truth, others, "self", names=onames)
+    rng = np.random.default_rng(0)
+    bad = {n: v * np.where(rng.random(v.shape) < 0.05, 1 + 5e-4, 1.0) for n, v in got.items()}
+    with pytest.raises(AssertionError):
+        truth_bar(bad, truth, others, "perturbed", names=onames)
