@@ -684,7 +684,113 @@ def side_legs(args, scene, cams, seeds, bg, pipe, bucket, step, dev):
     dt = _time(step_sem, steps)
     legs["dge_step_with_semantic"] = {"value": round(steps * V / dt, 3), "unit": "views/s",
                                       "path": "the c2 step (fwd+bwd renders) + the semantic forward of each view"}
+    # BASELINE.json's other single-GPU configs and SURVEY.md §8(f) F3, timed here so the driver's run records them
+    del flat_bucket
+    torch.cuda.empty_cache()
+    for name, fn in (("c4_hd_forward", leg_c4), ("c5_local_edit", leg_c5), ("f3_adam", leg_adam)):
+        legs[name] = fn(dev, steps, 3)
+        torch.cuda.empty_cache()
     return legs
+
+
+def _timed(fn, steps, warmup):
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / steps
+
+
+def _stages(fn, n=3):
+    from dge_amd import _native
+
+    _native.profile_stages(None)
+    _native.profile_enable(True)
+    _native.profile_collect()
+    for _ in range(n):
+        fn()
+    torch.cuda.synchronize()
+    prof = _native.profile_collect()
+    _native.profile_enable(False)
+    return {k: round(ms / c, 4) for k, (ms, c) in prof.items() if c}
+
+
+def leg_c4(dev, steps, warmup):
+    """configs[3]: 2.5M Gaussians, 1920x1080, forward only (render() without autograd: 8160 tiles, the
+    two-level binning; rasterizer_impl.cu:179-285)."""
+    from dge_amd.cameras import orbit_camera
+    from dge_amd.gaussian_renderer import PipelineParams, render
+    from dge_amd.scene import synthetic_scene
+
+    P, W, H = 2_500_000, 1920, 1080
+    sc = synthetic_scene(P, seed=2, device=dev)
+    cam = orbit_camera(0, 1, W, H, device=dev)
+    bg = torch.zeros(3, device=dev)
+
+    def fwd():
+        with torch.no_grad():
+            render(cam, sc, PipelineParams(), bg)
+
+    dt = _timed(fwd, steps, warmup)
+    return {"workload": "c4: 2.5M Gaussians, 1920x1080, fp32 forward only", "value": round(1.0 / dt, 2),
+            "unit": "renders/s", "ms_per_render": round(1e3 * dt, 3), "stages_ms": _stages(fwd)}
+
+
+def leg_c5(dev, steps, warmup):
+    """configs[4]: 1.0M scene, localize on a 200k mask (the x-sorted first 20%), SH stored fp16, fp32
+    covariance inputs, 512x512 forward + backward through render() (gaussian_model.py:221-258 localize)."""
+    from dge_amd.cameras import orbit_camera
+    from dge_amd.gaussian_renderer import PipelineParams, render
+    from dge_amd.scene import synthetic_scene
+
+    P, Psub, W, H = 1_000_000, 200_000, 512, 512
+    sc = synthetic_scene(P, seed=0, device=dev)
+    sc._features_dc = sc._features_dc.half()
+    sc._features_rest = sc._features_rest.half()
+    mask = torch.zeros(P, dtype=torch.bool, device=dev)
+    mask[torch.argsort(sc._xyz[:, 0])[:Psub]] = True
+    sc.mask, sc.localize = mask, True
+    sc.requires_grad_(True)
+    cam = orbit_camera(0, 1, W, H, device=dev)
+    g = torch.randn(3, H, W, device=dev, generator=torch.Generator(device=dev).manual_seed(5)) * 1e-3
+    bg = torch.zeros(3, device=dev)
+
+    def step():
+        for p in sc.parameters():
+            p.grad = None
+        (render(cam, sc, PipelineParams(), bg)["render"] * g).sum().backward()
+
+    dt = _timed(step, steps, warmup)
+    return {"workload": "c5: 1.0M scene, localize 200k (x-sorted 20%), fp16 SH, 512x512 fwd+bwd",
+            "value": round(1.0 / dt, 2), "unit": "renders/s", "ms_per_render": round(1e3 * dt, 3),
+            "stages_ms": _stages(step)}
+
+
+def leg_adam(dev, steps, warmup):
+    """the optimizer step over a 1.0M-Gaussian GaussianModel (six groups, 59 floats per
+    Gaussian, gaussian_model.py:336-394): FusedAdam (one gfx950 kernel) against torch.optim.Adam (foreach)."""
+    from dge_amd.optim import FusedAdam
+
+    P = 1_000_000
+    shapes = [(P, 3), (P, 1, 3), (P, 15, 3), (P, 1), (P, 3), (P, 4)]
+    lrs = [1.6e-4, 0.0125, 0.0125 / 20, 0.05, 0.005, 0.001]
+    out = {"workload": "F3: Adam step over 1.0M Gaussians (59 floats each)", "unit": "GB/s algorithmic",
+           "bytes_per_step": 59 * P * 28}
+    gen = torch.Generator(device=dev).manual_seed(7)
+    for name, cls in (("fused", FusedAdam), ("torch_foreach", torch.optim.Adam)):
+        ps = [torch.nn.Parameter(torch.randn(s, device=dev, generator=gen)) for s in shapes]
+        for p in ps:
+            p.grad = torch.randn(p.shape, device=dev, generator=gen) * 1e-3
+        opt = cls([{"params": [p], "lr": lr} for p, lr in zip(ps, lrs)], lr=0.0, eps=1e-15)
+        dt = _timed(opt.step, steps, warmup)
+        out[name] = {"ms": round(1e3 * dt, 4), "algorithmic_GBps": round(out["bytes_per_step"] / dt / 1e9, 1)}
+        del opt, ps
+    out["value"] = out["fused"]["algorithmic_GBps"]
+    out["speedup"] = round(out["torch_foreach"]["ms"] / out["fused"]["ms"], 2)
+    return out
 
 
 def cpu_baseline(scene, cam, seed, bg, args):

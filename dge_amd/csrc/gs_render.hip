@@ -723,8 +723,14 @@ void launch_render_apply_weights(const ApplyWeightsArgs& a, hipStream_t s) {
 __device__ __forceinline__ float bwd_chain(bool hit, float alpha, float G, float4 c, float dp0, float dp1, float dp2,
                                            float nbg, float& T, float& D0, float& D1, float& D2, float& wc) {
     const float ae = hit ? alpha : 0.f;
-    const float r = __builtin_amdgcn_rcpf(1.f - ae);
-    T = hit ? T * r : T;
+    const float d = 1.f - ae;
+    const float r = __builtin_amdgcn_rcpf(d);
+    // T / d: the reciprocal's product plus one Newton step on the quotient (q + (T - q d) r), within about half
+    // an ulp like the reference's IEEE division (backward.cu:503) — T * rcp alone carries v_rcp_f32's ulp into
+    // every step of the back-to-front chain, and those errors add up in sums that cancel (round 6, the fp64-truth
+    // bar: the dL/dcolor sums of a few Gaussians 14x further from the truth than the reference's own arithmetic)
+    const float q = T * r;
+    T = hit ? __builtin_fmaf(__builtin_fmaf(-q, d, T), r, q) : T;
     const float t0 = c.x - D0, t1 = c.y - D1, t2 = c.z - D2;
     float dL_dalpha = t0 * dp0;
     dL_dalpha += t1 * dp1;

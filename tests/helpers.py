@@ -337,6 +337,13 @@ def compare_grads(got, ref, rtol=RTOL, O=None, label="", rows=None):
 TRUTH_MULT = 4.0
 TRUTH_REL = 1e-4
 TRUTH_ONLY_REL_MAX = 0.01
+# E_ref is a sample (the largest of a few correlated fp32 evaluations), not an error scale: where the samples all
+# happen to land close to the truth — heavily cancelled elements — an evaluation of the same quality misses the
+# bar.  The reference's own contraction models, each held to the others' E_ref, miss it at up to 2.4e-5 of a
+# tensor's nonzero elements (c2 / c5, measured on the GPU box, round 6), so each tensor may have
+# floor(TRUTH_TAIL x nonzero) such elements (and at least as many as the reference's own models show on the same
+# case), every one printed; the self-measured rate itself is asserted below TRUTH_TAIL.
+TRUTH_TAIL = 1e-4
 PARAM_NAMES = ["_xyz", "_features_dc", "_features_rest", "_opacity", "_scaling", "_rotation"]
 
 
@@ -422,12 +429,11 @@ def truth_bar(got, truth, refs, label="", mult=TRUTH_MULT, rel=TRUTH_REL, max_on
               dump=None, names=None, check=True):
     """Per tensor: |got - truth| <= mult * E_ref + rel * |truth| per element (E_ref: the largest error of the
     fp32 evaluations `refs` against the truth), at most max_only_rel of the nonzero elements admitted by the
-    rel * |truth| term alone, and no more elements beyond the bound than the reference's own evaluations show
-    when each contraction model's evaluations are held to the other models' E_ref (a model of the reference's
-    arithmetic that is not the reference's own misses this per-element bar at a few elements per million —
-    heavily cancelled sums — so that count, measured here on the same case, is the allowance).  Prints per
-    tensor: nonzero elements, held by mult * E_ref, admitted only by rel |truth| (%), beyond, the worst err /
-    bound, then [the reference's own: worst only-rel %, most elements beyond, worst err/bound]."""
+    rel * |truth| term alone, and at most floor(TRUTH_TAIL x nonzero) elements beyond the bound (or as many as
+    the reference's own evaluations show when each contraction model's evaluations are held to the other
+    models' E_ref, if more; see TRUTH_TAIL).  Prints per tensor: nonzero elements, held by mult * E_ref,
+    admitted only by rel |truth| (%), beyond (allowed), the worst err / bound, then [the reference's own models
+    held to each other: worst only-rel %, most elements beyond, worst err/bound] and every element beyond."""
     names = names or [f"ref{k}" for k in range(len(refs))]
     groups = {}
     for k, nm in enumerate(names):
@@ -445,6 +451,11 @@ def truth_bar(got, truth, refs, label="", mult=TRUTH_MULT, rel=TRUTH_REL, max_on
         row = dict(nonzero=int(nz.sum()), held=int(held.sum()), only_rel=int(only.sum()), beyond=int(beyond.sum()),
                    worst=float(ratio.max()) if ratio.size else 0.0,
                    note="" if i is None else f"got {g[i]:.6e} truth {t[i]:.6e} E_ref {errs.max(0)[i]:.3e}")
+        if row["beyond"]:  # the elements beyond, worst first: (index, got, truth, E_ref, err / E_ref)
+            bi = np.argsort(-ratio.reshape(-1))[:min(row["beyond"], 10)]
+            row["beyond_at"] = [(np.unravel_index(int(j), t.shape), float(g.reshape(-1)[j]), float(t.reshape(-1)[j]),
+                                 float(errs.max(0).reshape(-1)[j]),
+                                 float(err.reshape(-1)[j] / max(errs.max(0).reshape(-1)[j], 1e-300))) for j in bi]
         self_only, self_beyond, self_worst = 0.0, 0, 0.0
         if len(groups) > 1:  # each model's evaluations against the other models' envelope
             gmax = {m: errs[idx].max(0) for m, idx in groups.items()}
@@ -456,7 +467,8 @@ def truth_bar(got, truth, refs, label="", mult=TRUTH_MULT, rel=TRUTH_REL, max_on
                     self_only = max(self_only, float(o_k.sum()) / max(int(rnz.sum()), 1))
                     self_beyond = max(self_beyond, int(b_k.sum()))
                     self_worst = max(self_worst, float(r_k.max()) if r_k.size else 0.0)
-        row.update(self_only=self_only, self_beyond=self_beyond, self_worst=self_worst)
+        row.update(self_only=self_only, self_beyond=self_beyond, self_worst=self_worst,
+                   allowed=max(self_beyond, int(TRUTH_TAIL * row["nonzero"])))
         stats[n] = row
     print(f"[truth bar{(' ' + label) if label else ''}] per tensor: nonzero / held by {mult:g} x E_ref / "
           f"admitted only by {rel:g} |truth| / beyond (allowed) / worst err/bound — E_ref over {len(refs)} fp32 "
@@ -465,19 +477,23 @@ def truth_bar(got, truth, refs, label="", mult=TRUTH_MULT, rel=TRUTH_REL, max_on
     for n, a in stats.items():
         frac = a["only_rel"] / max(a["nonzero"], 1)
         print(f"  {n:15s} {a['nonzero']:9d} {a['held']:9d} {a['only_rel']:7d} ({100 * frac:.3f}%) {a['beyond']:4d} "
-              f"({a['self_beyond']}) worst {a['worst']:.3g}  [{100 * a['self_only']:.3f}%, {a['self_beyond']}, "
+              f"({a['allowed']}) worst {a['worst']:.3g}  [{100 * a['self_only']:.3f}%, {a['self_beyond']}, "
               f"{a['self_worst']:.3g}]  {a['note']}")
-    if dump:  # (offline analysis: at most 10k of the compared rows, float32 except the truth)
+        for e in a.get("beyond_at", []):
+            print(f"      beyond at {e[0]}: got {e[1]:.6e} truth {e[2]:.6e} E_ref {e[3]:.3e} err/E_ref {e[4]:.3g}")
+    if dump:  # (offline analysis: at most 4k of the compared rows, float32 except the truth)
         nrow = len(next(iter(truth.values())))
-        sel = np.arange(nrow) if nrow <= 10000 else np.sort(np.random.default_rng(0).choice(nrow, 10000, replace=False))
+        sel = np.arange(nrow) if nrow <= 4000 else np.sort(np.random.default_rng(0).choice(nrow, 4000, replace=False))
         np.savez(dump, sel=sel, names=np.array(names), **{f"got_{n}": np.asarray(got[n], np.float32)[sel] for n in truth},
                  **{f"truth_{n}": np.asarray(t)[sel] for n, t in truth.items()},
                  **{f"ref{k}_{n}": np.asarray(r[n], np.float32)[sel] for k, r in enumerate(refs) for n in truth})
     if check:
         for n, a in stats.items():
-            assert a["beyond"] <= a["self_beyond"], \
-                f"{label} {n}: {a['beyond']} elements beyond {mult:g} E_ref + {rel:g}|truth| (the reference's own " \
-                f"models: {a['self_beyond']}); {a['note']}"
+            assert a["beyond"] <= a["allowed"], \
+                f"{label} {n}: {a['beyond']} elements beyond {mult:g} E_ref + {rel:g}|truth| (allowed {a['allowed']}; " \
+                f"the reference's own models: {a['self_beyond']}); {a['note']}"
+            assert a["self_beyond"] <= max(1, TRUTH_TAIL * a["nonzero"]), \
+                f"{label} {n}: the reference's own models miss the bar at {a['self_beyond']} elements"
             assert a["only_rel"] <= max_only_rel * a["nonzero"], \
                 f"{label} {n}: {a['only_rel']} of {a['nonzero']} nonzero elements admitted only by the {rel:g}|truth| term"
     return stats

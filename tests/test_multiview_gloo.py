@@ -126,11 +126,11 @@ def _free_port():
 
 
 @pytest.mark.slow
-@pytest.mark.parametrize("world,V", [(2, 4), (4, 10)], ids=["2ranks_4views", "4ranks_10views"])
+@pytest.mark.parametrize("world,V", [(2, 4), (4, 10), (8, 24)], ids=["2ranks_4views", "4ranks_10views", "8ranks_24views"])
 @pytest.mark.parametrize("mode", ["seed", "l1"])
 def test_sharded_step_equals_single_process(mode, world, V):
     """world ranks x their shard_views shards == 1 process x V views (2 x 2 = 4; 4 ranks over 10 views: the
-    uneven 3/3/2/2 shards): the summed parameter gradients (sparse-row bucket all-reduce), the view-space
+    uneven 3/3/2/2 shards; 8 ranks over c3's 24 views, 3 each: the driver's N = 8 shape): the summed parameter gradients (sparse-row bucket all-reduce), the view-space
     gradient sum and the radii max; for DGE's masked l1 (a mean over all views, DGE.py:672) through the
     B_local / B share of each rank.  found_inf is collective (a NaN on rank 1 only)."""
     P = 60
