@@ -685,7 +685,6 @@ def side_legs(args, scene, cams, seeds, bg, pipe, bucket, step, dev):
     legs["dge_step_with_semantic"] = {"value": round(steps * V / dt, 3), "unit": "views/s",
                                       "path": "the c2 step (fwd+bwd renders) + the semantic forward of each view"}
     # BASELINE.json's other single-GPU configs and SURVEY.md §8(f) F3, timed here so the driver's run records them
-    del flat_bucket
     torch.cuda.empty_cache()
     for name, fn in (("c4_hd_forward", leg_c4), ("c5_local_edit", leg_c5), ("f3_adam", leg_adam)):
         legs[name] = fn(dev, steps, 3)
