@@ -24,7 +24,6 @@
 //    quadrant) with plain stores.  No float atomics: the per-Gaussian sum
 //    happens in gs_backward.hip in a fixed order, so the backward is bitwise
 //    reproducible.
-#include <stdlib.h>
 #include <string.h>
 
 #include "gs_common.h"
@@ -583,23 +582,16 @@ __global__ __launch_bounds__(64, 3) void k_render_fwd(RenderArgs a) {
     }
 }
 
-static int env_int(const char* name) {
-    const char* e = getenv(name);
-    return e ? atoi(e) : 0;
-}
-
 void launch_render_forward(const RenderArgs& a, hipStream_t s) {
     const int tiles = a.gx * a.gy;
     if (tiles <= 0) return;
-    // (experiment: DGE_AMD_FWD_LDS bytes of dynamic LDS per workgroup reserved, which bounds the waves per CU)
-    static const size_t lds = (size_t)env_int("DGE_AMD_FWD_LDS");
     if (!a.order_ready) hipLaunchKernelGGL(k_tile_order, dim3(1), dim3(1024), 0, s, a.ranges, tiles, a.tile_order);
     if (a.bwd && a.aux_out)
-        hipLaunchKernelGGL((k_render_fwd<true, true>), dim3(div_up(tiles, 8) * 32), dim3(64), lds, s, a);
+        hipLaunchKernelGGL((k_render_fwd<true, true>), dim3(div_up(tiles, 8) * 32), dim3(64), 0, s, a);
     else if (a.bwd)
-        hipLaunchKernelGGL((k_render_fwd<true, false>), dim3(div_up(tiles, 8) * 32), dim3(64), lds, s, a);
+        hipLaunchKernelGGL((k_render_fwd<true, false>), dim3(div_up(tiles, 8) * 32), dim3(64), 0, s, a);
     else
-        hipLaunchKernelGGL((k_render_fwd<false, false>), dim3(div_up(tiles, 8) * 32), dim3(64), lds, s, a);
+        hipLaunchKernelGGL((k_render_fwd<false, false>), dim3(div_up(tiles, 8) * 32), dim3(64), 0, s, a);
 }
 
 // Whether a recolor's colours are its source forward's aux grey: flag[0] |= 1 on any difference
@@ -1036,8 +1028,7 @@ __global__ __launch_bounds__(64, GS_BWD_WAVES) void k_render_bwd(RenderBwdArgs a
 void launch_render_backward(const RenderBwdArgs& a, hipStream_t s) {
     const int tiles = a.gx * a.gy;
     if (tiles <= 0 || a.item_cap == 0) return;
-    static const size_t lds = (size_t)env_int("DGE_AMD_BWD_LDS");  // (experiment, as DGE_AMD_FWD_LDS)
-    hipLaunchKernelGGL(k_render_bwd, dim3(a.item_cap), dim3(64), lds, s, a);
+    hipLaunchKernelGGL(k_render_bwd, dim3(a.item_cap), dim3(64), 0, s, a);
 }
 
 }  // namespace gs
