@@ -74,6 +74,9 @@ def parse():
     ap.add_argument("--serial-zero", action="store_true",
                     help="zero the gradient bucket on the default stream before the forwards (default: on the first "
                          "view's stream beside the forwards, GradBucket.zero(stream=...))")
+    ap.add_argument("--opacity-mean", type=float, default=0.0,
+                    help="raw opacity N(mean, std) of the synthetic scene (profiling: -2 / 1 is the c2_high_live leg's)")
+    ap.add_argument("--opacity-std", type=float, default=1.5)
     ap.add_argument("--cpu-baseline-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="OpenMP threads of the CPU baseline (default 0: every core this process may use)")
@@ -195,7 +198,8 @@ def main():
     from dge_amd.scene import synthetic_scene
 
     P, W, H, V = args.points, args.width, args.height, args.views_per_rank
-    scene = synthetic_scene(P, sh_degree=args.sh_degree, seed=0, device=dev).requires_grad_(True)
+    scene = synthetic_scene(P, sh_degree=args.sh_degree, seed=0, device=dev,
+                            opacity_mean=args.opacity_mean, opacity_std=args.opacity_std).requires_grad_(True)
     n_total = V * world
     cams = [orbit_camera(k, n_total, W, H, device=dev) for k in range(rank * V, (rank + 1) * V)]
     gen = torch.Generator(device="cpu").manual_seed(1)

@@ -195,6 +195,15 @@ __device__ __forceinline__ float exp_scale(float u) {  // 2^n from the shifter s
     return __uint_as_float((__float_as_uint(u) << 23) + 0x3F800000u);
 }
 
+#ifdef GS_HW_EXP
+// (A/B measurement only, tools/probes/exp_flips.py: the hardware v_exp_f32 on x log2e, __expf's sequence — not
+// reproducible on the CPU, so the oracle's blend decisions become flips)
+__device__ __forceinline__ float gs_exp(float x) { return __builtin_amdgcn_exp2f(x * kExpLog2e); }
+typedef float f4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ f4v gs_exp4(f4v x) {
+    return f4v{gs_exp(x.x), gs_exp(x.y), gs_exp(x.z), gs_exp(x.w)};
+}
+#else
 __device__ __forceinline__ float gs_exp(float x) {
 #pragma clang fp contract(off)
     float u = __builtin_fmaf(x, kExpLog2e, kExpShifter);
@@ -234,6 +243,7 @@ __device__ __forceinline__ f4v gs_exp4(f4v x) {
     p = __builtin_elementwise_fma(p, r, c);
     return p * f4v{exp_scale(u.x), exp_scale(u.y), exp_scale(u.z), exp_scale(u.w)};
 }
+#endif
 
 // GaussianModel activations (gaussian_model.py:42-57): sigmoid, exp,
 // F.normalize(q, dim=1, eps=1e-12) and their derivatives (what torch's
