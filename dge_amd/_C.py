@@ -17,6 +17,7 @@ functors, rasterize_points.cu:27-33) on the caller's current stream.
 from __future__ import annotations
 
 import ctypes
+import os
 import threading
 import weakref
 
@@ -137,6 +138,39 @@ def _settings(bg, viewmatrix, projmatrix, campos, tanfovx, tanfovy, H, W, sh_deg
 
 
 _RAW_STREAM = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+
+# The compiled binding (dge_amd/csrc/gs_torch.cpp -> dge_amd/lib/_gs_torch*.so) of the calls DGE's loop makes per
+# view: the raw-parameter forward's halves and the recolor.  It drives the library instance loaded above (its
+# entry points handed over as addresses); DGE_AMD_BINDING=ctypes keeps every call on the ctypes path below.
+_GT = None
+
+
+def _load_binding():
+    global _GT
+    if os.environ.get("DGE_AMD_BINDING", "torch") == "ctypes" or _RAW_STREAM is None:
+        return None
+    import glob
+    import importlib.machinery
+    import importlib.util
+
+    found = glob.glob(os.path.join(os.path.dirname(N.LIB_PATH), "_gs_torch*.so")) or \
+        glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "_gs_torch*.so"))
+    if not found:
+        return None
+    loader = importlib.machinery.ExtensionFileLoader("_gs_torch", found[0])
+    spec = importlib.util.spec_from_file_location("_gs_torch", found[0], loader=loader)
+    mod = importlib.util.module_from_spec(spec)
+    loader.exec_module(mod)
+    L = N.lib()
+    mod.bind({n: ctypes.cast(getattr(L, n), ctypes.c_void_p).value for n in (
+        "gs_rasterize_forward_begin", "gs_rasterize_forward_end", "gs_rasterize_forward_release",
+        "gs_render_recolor", "gs_image_buffer_size")})
+    _GT = mod
+    return mod
+
+
+def _raw_stream(device) -> int:
+    return _RAW_STREAM(device.index if device.index is not None else torch.cuda.current_device())
 
 
 def _stream(device):
@@ -386,6 +420,14 @@ def rasterize_gaussians_fused_begin(background, xyz, f_dc, f_rest, colors, raw_o
     idle behind it."""
     N.require_gpu(xyz)
     dev = xyz.device
+    if _GT is not None:
+        p = _GT.fused_begin(background, xyz, f_dc, f_rest, colors, raw_opacity, raw_scaling, raw_rotation,
+                            float(scale_modifier), viewmatrix, projmatrix, float(tan_fovx), float(tan_fovy),
+                            int(image_height), int(image_width), int(degree), campos, bool(prefiltered), bool(debug),
+                            index, visible, bool(forward_only), aux_mask, _raw_stream(dev))
+        if p.rc:
+            N.check(p.rc, "rasterize_gaussians_fused")
+        return p
     index = _index32(index)
     P = index.numel() if index is not None else xyz.size(0)
     H, W = int(image_height), int(image_width)
@@ -417,6 +459,11 @@ def rasterize_gaussians_fused_begin(background, xyz, f_dc, f_rest, colors, raw_o
 def rasterize_gaussians_fused_end(prep):
     """Second half (gs_rasterize_forward_end) on the current stream (the begin stream or one ordered after
     it): -> the (num_rendered, color, depth, radii, geom, binning, img) of rasterize_gaussians_fused."""
+    if _GT is not None and isinstance(prep, _GT.Prepared):
+        rc, nr, color, depth, radii, geom, binning, img = _GT.fused_end(prep, _raw_stream(prep.radii.device))
+        if rc:
+            N.check(rc, "rasterize_gaussians_fused")
+        return nr, color, depth, radii, geom, binning, img
     dev = prep.dev
     with _on(dev):
         out_color = torch.empty((3, prep.H, prep.W), dtype=torch.float32, device=dev)
@@ -443,6 +490,14 @@ def render_recolor(background, colors, viewmatrix, projmatrix, campos, tan_fovx,
     stream (which must be ordered after that forward).  src_aux_mask: the aux_mask that forward composited
     (unchanged since): colours equal to its 0/1 grey are then served from that forward's sums."""
     dev = colors.device
+    if _GT is not None:
+        rc, color, depth = _GT.render_recolor(background, colors, viewmatrix, projmatrix, campos, float(tan_fovx),
+                                              float(tan_fovy), int(image_height), int(image_width), int(degree),
+                                              float(scale_modifier), bool(prefiltered), int(P), int(num_rendered),
+                                              geomBuffer, binningBuffer, imgBuffer, src_aux_mask, _raw_stream(dev))
+        if rc:
+            N.check(rc, "render_recolor")
+        return color, depth
     H, W = int(image_height), int(image_width)
     with _on(dev):
         colors = _f32(colors, "colors")
@@ -630,3 +685,9 @@ def rasterize_backward_passes(pending):
             binn = (ctypes.c_void_p * n)(*[_ptr(p.binning) for p in chunk])
             rc = N.lib().gs_rasterize_backward_passes(n, sa, ga, ra, rad, geo, binn, oa, _stream(dev))
             N.check(rc, "rasterize_backward_passes")
+
+
+try:
+    _load_binding()
+except ImportError:  # (no libgs_raster.so yet: every native call raises when it is made; tests/test_c_abi.py)
+    _GT = None

@@ -87,3 +87,16 @@ def test_product_package_never_imports_the_oracle():
     for f in root.rglob("*.py"):
         src = f.read_text()
         assert not re.search(r"^\s*(from|import)\s+oracle", src, flags=re.M), f
+
+
+def test_compiled_binding_is_built_and_bound():
+    """The compiled torch binding of render()'s per-view calls (dge_amd/csrc/gs_torch.cpp) is in-tree next to
+    libgs_raster.so, loads, and drives the library instance dge_amd._native loaded (its entry points bound)."""
+    import os
+
+    from dge_amd import _C
+
+    assert _C._GT is not None, "dge_amd/lib/_gs_torch*.so missing: make -C dge_amd/csrc"
+    assert os.path.dirname(_C._GT.__file__) == os.path.dirname(N.LIB_PATH)
+    for f in ("fused_begin", "fused_end", "render_recolor", "bind", "Prepared"):
+        assert hasattr(_C._GT, f), f

@@ -25,6 +25,7 @@ from helpers import GRAD_NAMES, RTOL, assert_close, camera_settings, compare_for
     run_gpu, run_oracle, scene_arrays, settings_from_golden
 
 pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 
@@ -674,6 +675,46 @@ def test_dge_loop_backward_merges_the_views_passes(cuda_device, views, pre_grad,
     for x, y in zip(va, vb):
         assert torch.equal(x, y)
     assert all(bool(v.abs().sum() > 0) for v in va)
+
+
+@pytest.mark.parametrize("localize", [False, True])
+def test_compiled_binding_matches_ctypes_path(cuda_device, localize):
+    """render()'s per-view calls through the compiled binding (dge_amd/csrc/gs_torch.cpp: the forward's halves and
+    the recolor) against the ctypes path on the same inputs: image, depth, radii, visibility, the semantic recolor
+    render (the edit mask as override_color, served from the training blend's aux sums) and every raw-parameter
+    gradient bitwise; the binding is the one loaded (in-tree .so)."""
+    from dge_amd import _C
+    from dge_amd import gaussian_renderer as GR
+    from dge_amd.cameras import orbit_camera
+    from dge_amd.gaussian_renderer import PipelineParams, render
+    from dge_amd.scene import synthetic_scene
+
+    GT = _C._GT
+    assert GT is not None and os.path.dirname(GT.__file__) == os.path.join(ROOT, "dge_amd", "lib")
+    dev = torch.device("cuda")
+    cam = orbit_camera(1, 3, 200, 136, device=dev)
+    G = torch.randn(3, 136, 200, generator=torch.Generator().manual_seed(12)).to(dev)
+    outs = []
+    try:
+        for gt in (GT, None):
+            _C._GT = gt
+            sc = synthetic_scene(20_000, seed=22, radius=1.5, scale=0.03, device=dev).requires_grad_(True)
+            sc.mask = (torch.rand(20_000, generator=torch.Generator().manual_seed(3)) < 0.3).to(dev)
+            sc.localize = localize
+            hits = GR._RECOLOR_HITS
+            pkg = render(cam, sc, PipelineParams(), torch.tensor([0.1, 0.0, 0.2], device=dev))
+            n = int(sc.mask.sum()) if localize else 20_000
+            sem = render(cam, sc, PipelineParams(), torch.tensor([0.1, 0.0, 0.2], device=dev),
+                         override_color=torch.ones(n, 3, device=dev))["render"]
+            assert GR._RECOLOR_HITS == hits + 1  # (the semantic render took the recolor path)
+            (pkg["render"] * G).sum().backward()
+            torch.cuda.synchronize()
+            outs.append([pkg["render"], pkg["depth_3dgs"], pkg["radii"], pkg["visibility_filter"], sem,
+                         pkg["viewspace_points"].grad] + [p.grad for p in sc.parameters()])
+    finally:
+        _C._GT = GT
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
 
 
 def test_deferred_passes_survive_a_failed_backward(cuda_device):
