@@ -26,7 +26,7 @@ bg = torch.zeros(3, device=dev)
 pipe = GR.PipelineParams()
 mask = (torch.rand(P, generator=torch.Generator().manual_seed(5)) < 0.2).to(dev)
 gts = [torch.rand(H, W, 3, generator=torch.Generator().manual_seed(50 + i)).to(dev) for i in range(V)]
-pre = []
+pre, native = [], []
 _begin = _C.rasterize_gaussians_fused_begin
 _entry = [0.0]
 
@@ -39,6 +39,26 @@ def begin_timed(*a, **k):
 
 
 _C.rasterize_gaussians_fused_begin = begin_timed
+
+
+class _Proxy:
+    """the binding with its fused_begin timed: the Python before the native call (render() entry -> the call)
+    and the call itself (structs, allocations and the native first half's HIP calls)"""
+
+    def __getattr__(self, n):
+        return getattr(GT, n)
+
+    def fused_begin(self, *a):
+        t = time.perf_counter()
+        if _entry[0]:
+            native.append(t - _entry[0])  # (replaced by the call's own time below)
+        r = GT.fused_begin(*a)
+        if _entry[0]:
+            native[-1] = (t - _entry[0], time.perf_counter() - t)
+        return r
+
+
+PROXY = _Proxy()
 
 
 def render(*a, **k):
@@ -68,13 +88,15 @@ def loop():
 
 res = {"torch": [], "ctypes": []}
 pres = {"torch": [], "ctypes": []}
+split = []
 for rnd in range(4):
     for mode in ("torch", "ctypes"):
-        _C._GT = GT if mode == "torch" else None
+        _C._GT = PROXY if mode == "torch" else None
         for _ in range(3):
             loop()
         torch.cuda.synchronize()
         pre.clear()
+        native.clear()
         n = 20
         t0 = time.perf_counter()
         for _ in range(n):
@@ -82,6 +104,10 @@ for rnd in range(4):
         torch.cuda.synchronize()
         res[mode].append(n * V / (time.perf_counter() - t0))
         pres[mode].append(statistics.median(pre) * 1e6)
+        if mode == "torch":
+            split.append((statistics.median(x[0] for x in native) * 1e6, statistics.median(x[1] for x in native) * 1e6))
 _C._GT = GT
 print(json.dumps({"dge_loop_views_per_s": {k: [round(x, 1) for x in v] for k, v in res.items()},
-                  "render_prelaunch_us_median": {k: [round(x, 1) for x in v] for k, v in pres.items()}}))
+                  "render_entry_to_first_half_enqueued_us_median": {k: [round(x, 1) for x in v] for k, v in pres.items()},
+                  "binding_python_before_native_call_us": [round(a, 1) for a, _ in split],
+                  "binding_native_first_half_call_us": [round(b, 1) for _, b in split]}))
