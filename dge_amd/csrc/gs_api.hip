@@ -88,6 +88,13 @@ bool tile_sort_unfused() {
 bool two_level(int gx, int gy) {
     return tile_sort_fused(gx, gy) && rect_packable(gx, gy) && !tile_sort_unfused();
 }
+// the region emission (launch_region_emit) for a gx x gy grid, opt-in: DGE_AMD_BINNING=region (an A/B and test
+// switch).  It measured slower than the two-level binning at c4 (emit 574 vs 423 us), which stays
+// the default there
+bool region_emission(int gx, int gy) {
+    const char* e = getenv("DGE_AMD_BINNING");
+    return region_emission_grid(gx, gy) && !tile_sort_unfused() && e && !strcmp(e, "region");
+}
 
 // Pinned read-back slot of one forward's preprocess counters + its event.  A
 // pool per device: several forwards may be between begin and end at once
@@ -414,6 +421,10 @@ int bin_after_preprocess(FwdState& f, hipStream_t stream) {
     // sort's tables, free by then)
     const bool direct = !ea.xhist && direct_emission_grid(g.gx, g.gy) && pa.rect_packed && !tile_sort_unfused();
     ea.thist = direct ? at<uint32_t>(geom, gl.sort_hist) : nullptr;
+    // region emission (grids of 2049..kRegionMaxTiles tiles): chosen in bin_emit when its count table fits the
+    // binning buffer (the two-level binning's column counts above stay the fallback)
+    ea.chunks = pa.rect_packed && region_emission(g.gx, g.gy) ? region_chunks(P) : 0;
+    ea.region_rows = region_rows(g.gx, g.gy);
     ea.ttotals = direct ? at<uint32_t>(geom, gl.sort_totals) : nullptr;
     ea.ntiles = g.tiles;
     { StageScope sc(ST_SCAN, stream); launch_scan_reduce(ea, stream); }
@@ -512,6 +523,22 @@ int bin_emit(FwdState& f, void* bin, uint32_t K_layout, const uint32_t* n_dev, h
     const BinLayout bl = bin_layout((int)K_layout, g.tiles, bwd);
     ea.cap = n_dev ? K_layout : 0xFFFFFFFFu;
     const TileSortPlan plan = tile_sort_plan(g.tiles);
+    if (ea.chunks && region_table_fits(bl, f.gp.P, g.tiles)) {
+        // region emission: count table, scan, ranges + dispatch order, the lists (every store bounded by the
+        // layout's instance count, exact binning or not: the counts come from the rects, not from K)
+        ea.cap = K_layout;
+        ea.ids_only = f.ids_only = !bwd && f.ids_ok;
+        ea.pairs_out = at<uint2>(bin, bl.point_pairs);
+        ea.rec_flags32 = bwd ? at<uint32_t>(bin, bl.rec_flags) : nullptr;
+        ea.chunk_hist = at<uint32_t>(bin, bl.key0);
+        ea.tile_start = at<uint32_t>(bin, bl.slot_gauss);
+        ea.ttotals = at<uint32_t>(bin, bl.tile_count);
+        ea.ranges = at<uint2>(img, il.ranges);
+        ea.tile_order = at<uint32_t>(img, il.tile_order);
+        { StageScope sc(ST_EMIT, stream); launch_region_emit(ea, stream); }
+        GS_LAUNCHED("region emission");
+        return GS_OK;
+    }
     if (ea.xhist) {  // two-level binning (tile_sort_fused): column-ordered emission, row pass, ranges
         ea.ids_only = f.ids_only = !bwd && f.ids_ok;
         ea.tile_key = at<uint32_t>(bin, bl.key1);

@@ -355,12 +355,54 @@ struct EmitArgs {
     uint32_t* ttotals = nullptr;
     uint2* ranges = nullptr;
     uint32_t* tile_order = nullptr;
+    // region emission (region_emission_grid): each depth chunk's instances per tile, scanned in place over the
+    // chunks (chunks rows of ntiles, block-major), every tile's first list position (unclamped), the rows of a
+    // region
+    uint32_t* chunk_hist = nullptr;
+    uint32_t* tile_start = nullptr;
+    int chunks = 0;
+    int region_rows = 0;
 };
 // The direct emission for a gx x gy grid: at most 2048 tiles (one digit of the tile sort) and rects packed
 // in the depth-sort payload
 inline bool direct_emission_grid(int gx, int gy) {
     return gx * gy <= (1 << kMaxSinglePassBits) && rect_packable(gx, gy);
 }
+// The region emission (round 6) for grids of 2049..kRegionMaxTiles tiles with packed rects (c4's 120 x 68): the
+// depth order is cut into chunks of kChunkG Gaussians and the grid into regions of region_rows(gx) tile rows.
+// Each chunk counts its instances per tile (k_chunk_count), a scan over the chunks gives each chunk's first
+// position in every tile's list, and one workgroup per (chunk, region) picks the chunk's Gaussians that reach its
+// region, expands their instances there in depth order, ranks them per tile, stages them tile-major in LDS and
+// stores each tile's run (about kChunkG x 17 / 8160 = 34 ids at c4) coalesced.  Every instance is written once,
+// into its final place — the two-level binning wrote it twice (column emission, row pass) and read it back once.
+// Opt-in (DGE_AMD_BINNING=region): it measured slower than the two-level binning at c4, 574 vs 423 us — its
+// per-batch ranking, scans and barriers leave the CUs waiting.
+#ifndef GS_CHUNK_G
+#define GS_CHUNK_G 16384
+#endif
+constexpr int kChunkG = GS_CHUNK_G, kRegionMaxTiles = 12288;
+static_assert(kChunkG % kScanTile == 0, "a chunk is whole scan blocks");
+inline int region_chunks(int P) { return div_up((long long)(P > 0 ? P : 1), kChunkG); }
+// tile rows per region: about GS_REGION_TILES tiles (a region's per-tile counters fit 10 bits of tile index;
+// the emit time at c4 by region size in the comment below)
+#ifndef GS_REGION_TILES
+#define GS_REGION_TILES 512  // (c4: 1024 -> 764 us, 512 -> 574, 256 -> 621, 128 -> 791)
+#endif
+static_assert(GS_REGION_TILES <= 1024, "region tiles fit 10 bits");
+inline int region_rows(int gx, int gy) {
+    const int r = GS_REGION_TILES / (gx > 0 ? gx : 1);
+    return r < 1 ? 1 : (r > gy ? gy : r);
+}
+inline bool region_emission_grid(int gx, int gy) {
+    return gx * gy > (1 << kMaxSinglePassBits) && gx * gy <= kRegionMaxTiles && rect_packable(gx, gy);
+}
+// the count table (chunks x tiles u32) goes where the tile sort's keys would be ([key0, pair0)), the tile starts
+// where its slot map would be: both unused by the region emission
+inline bool region_table_fits(const BinLayout& L, int P, int tiles) {
+    return (size_t)4 * region_chunks(P) * (size_t)tiles <= L.pair0 - L.key0 &&
+           (size_t)4 * (size_t)tiles <= L.sort_hist - L.slot_gauss;
+}
+void launch_region_emit(const EmitArgs& a, hipStream_t s);
 void launch_scan_reduce(const EmitArgs& a, hipStream_t s);
 void launch_scan_emit(const EmitArgs& a, hipStream_t s);
 void launch_emit_tiles(const EmitArgs& a, hipStream_t s);

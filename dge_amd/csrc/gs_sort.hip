@@ -1482,8 +1482,12 @@ __global__ __launch_bounds__(256) void k_scan_emit_x(EmitArgs a) {
 // per count).  Two-level grids have at most 128 x 128 tiles.  Also the forward's dispatch order
 // (k_tile_order's: tiles by list length, longest first) from the same counts, when tile_order is set.
 constexpr int kRangesPer = kXDigits * kXDigits / 256;
+// cap: a speculative forward's binning capacity (the band emission's counts are the full instance counts:
+// ranges clamped to it, as write_tile_ranges does); starts: every tile's first position, unclamped (the band
+// emission's bases), when set
 __global__ __launch_bounds__(256) void k_ranges_counts(const uint32_t* __restrict__ count, int tiles,
-                                                       uint2* __restrict__ ranges, uint32_t* __restrict__ tile_order) {
+                                                       uint2* __restrict__ ranges, uint32_t* __restrict__ tile_order,
+                                                       uint32_t cap, uint32_t* __restrict__ starts) {
     __shared__ uint32_t lds4[4];
     constexpr int kClasses = 64;
     __shared__ uint32_t s_cls[kClasses];
@@ -1502,7 +1506,8 @@ __global__ __launch_bounds__(256) void k_ranges_counts(const uint32_t* __restric
     for (int i = 0; i < kRangesPer; ++i) {
         const int t = t0 + i;
         if (i < per && t < tiles) {
-            ranges[t] = c[i] ? make_uint2(run, run + c[i]) : make_uint2(0u, 0u);
+            ranges[t] = c[i] ? make_uint2(min(run, cap), min(run + c[i], cap)) : make_uint2(0u, 0u);
+            if (starts) starts[t] = run;
             run += c[i];
             if (tile_order) atomicAdd(&s_cls[cls(c[i])], 1u);
         }
@@ -1523,6 +1528,362 @@ __global__ __launch_bounds__(256) void k_ranges_counts(const uint32_t* __restric
         const int t = t0 + i;
         if (i < per && t < tiles) tile_order[atomicAdd(&s_cls[cls(c[i])], 1u)] = (uint32_t)t;
     }
+}
+
+// ---------------------------------------------------------------------
+// region emission (round 6; region_emission_grid: 2049..kRegionMaxTiles tiles, packed rects — c4's 120 x 68)
+// ---------------------------------------------------------------------
+// The direct emission's idea (every instance written once, straight to its place in its tile's list) for grids
+// too large for its per-(1024-Gaussian block, tile) tables.  The depth order is cut into chunks of kChunkG
+// Gaussians, the grid into regions of region_rows tile rows (~1024 tiles):
+//   k_chunk_count  the chunk's instances per tile (a rect adds +-1 at its four corners in LDS, then prefix sums
+//                  along x and y), one table row per chunk; also every Gaussian's first slot (emission order) and,
+//                  for a training binning, the zeroed record flags of the chunk's slots;
+//   digit scan     over the chunks per tile (in place: each chunk's first position relative to its tile's
+//                  start) and the tile totals; k_ranges_counts: ranges, dispatch order, the tiles' starts;
+//   k_region_emit  one workgroup per (chunk, region): the chunk's Gaussians that reach the region are appended
+//                  in depth order to an LDS list (one block scan per 1024 ranks), and the list's instances inside
+//                  the region are expanded in batches as in k_emit_tiles — owner = prefix max over marks at the
+//                  entries' first instances, rank among the batch's instances of the tile by 64-lane ballots and
+//                  per-wave counters (stable), staged tile-major in LDS — and stored as per-tile runs (~32 ids
+//                  at c4: coalesced, where one store per instance at its final place measured 5x slower).
+// Per tile the instances come chunk by chunk, Gaussian by Gaussian in depth order: the lists are the tile sort's,
+// bit for bit (and the (Gaussian, slot) pairs carry the emission-order slot, first slot + the instance's
+// row-major index in its rect).
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ uint32_t dpp_u32(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROW_MASK, 0xF, false);
+}
+// 64-lane inclusive scan with DPP row shifts and row broadcasts (no LDS crossbar trip per step)
+__device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t v) {
+    v += dpp_u32<0x111, 0xF>(v);  // row_shr:1
+    v += dpp_u32<0x112, 0xF>(v);  // row_shr:2
+    v += dpp_u32<0x114, 0xF>(v);  // row_shr:4
+    v += dpp_u32<0x118, 0xF>(v);  // row_shr:8
+    v += dpp_u32<0x142, 0xA>(v);  // row_bcast:15 into rows 1, 3
+    v += dpp_u32<0x143, 0xC>(v);  // row_bcast:31 into rows 2, 3
+    return v;
+}
+// NT-thread exclusive scan; `total` receives the workgroup sum
+template <int NT>
+__device__ __forceinline__ uint32_t block_excl_scan_n(uint32_t v, uint32_t* lds, uint32_t& total) {
+    constexpr int NW = NT / 64;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint32_t x = wave_incl_scan_u32(v);
+    if (lane == 63) lds[w] = x;
+    __syncthreads();
+    uint32_t base = 0, t = 0;
+#pragma unroll
+    for (int i = 0; i < NW; ++i) {
+        const uint32_t c = lds[i];
+        base += i < w ? c : 0u;
+        t += c;
+    }
+    __syncthreads();
+    total = t;
+    return base + x - v;
+}
+
+constexpr int kCcThreads = 1024;
+__global__ __launch_bounds__(kCcThreads) void k_chunk_count(EmitArgs a) {
+    extern __shared__ int s_d[];  // gy rows of gx + 1 cells
+    __shared__ uint32_t lds16[kCcThreads / 64];
+    const int gx = a.gx, gy = a.gy, nt = a.ntiles, gp = gx + 1, tid = threadIdx.x;
+    const uint32_t d = blockIdx.x, P = (uint32_t)a.P;
+    constexpr uint32_t SBC = kChunkG / kScanTile;  // scan blocks per chunk
+    constexpr int IT = kChunkG / kCcThreads, HI = IT < 8 ? IT : 8;  // rounds of kCcThreads ranks, HI at a time
+    static_assert(IT % HI == 0, "whole halves");
+    const uint32_t r0 = d * (uint32_t)kChunkG;
+    __shared__ uint32_t s_tot[HI][kCcThreads / 64];  // per (round, wave): its instances
+    uint32_t cbase;  // the chunk's first slot: the scan's block sums before it
+    {
+        uint32_t part = 0;
+        for (uint32_t i = (uint32_t)tid; i < d * SBC; i += kCcThreads) part += a.scan_sums[i];
+        block_excl_scan_n<kCcThreads>(part, lds16, cbase);
+    }
+    for (int t = tid; t < gy * gp; t += kCcThreads) s_d[t] = 0;
+    __syncthreads();
+    const int lane = tid & 63, w = tid >> 6;
+    uint32_t run = cbase;
+    for (int h0 = 0; h0 < IT; h0 += HI) {
+        uint2 gr[HI];  // (every load of the part in flight at once)
+#pragma unroll
+        for (int it = 0; it < HI; ++it) {
+            const uint32_t r = r0 + (uint32_t)((h0 + it) * kCcThreads + tid);
+            gr[it] = r < P ? a.order[r] : make_uint2(0u, 0u);
+        }
+        uint32_t c[HI], incl[HI];
+#pragma unroll
+        for (int it = 0; it < HI; ++it) {
+            const uint32_t q = gr[it].x;
+            const int x0 = (int)(q & 0xFFu), y0 = (int)((q >> 8) & 0xFFu), x1 = (int)((q >> 16) & 0xFFu),
+                      y1 = (int)(q >> 24);
+            const bool any = x1 > x0 && y1 > y0;
+            if (any) {
+                atomicAdd(&s_d[y0 * gp + x0], 1);
+                if (x1 < gx) atomicAdd(&s_d[y0 * gp + x1], -1);
+                if (y1 < gy) {
+                    atomicAdd(&s_d[y1 * gp + x0], -1);
+                    if (x1 < gx) atomicAdd(&s_d[y1 * gp + x1], 1);
+                }
+            }
+            c[it] = any ? (uint32_t)((x1 - x0) * (y1 - y0)) : 0u;
+            incl[it] = wave_incl_scan_u32(c[it]);
+            if (lane == 63) s_tot[it][w] = incl[it];
+        }
+        __syncthreads();
+        // first slots in depth order (rank r0 + round * kCcThreads + tid): the rounds before, the waves before
+#pragma unroll
+        for (int it = 0; it < HI; ++it) {
+            uint32_t wb = 0, rt = 0;
+            for (int v = 0; v < kCcThreads / 64; ++v) {
+                const uint32_t t = s_tot[it][v];
+                wb += v < w ? t : 0u;
+                rt += t;
+            }
+            if (c[it]) a.first_slot[gr[it].y] = run + wb + incl[it] - c[it];
+            run += rt;
+        }
+        __syncthreads();
+    }
+    if (a.rec_flags32)  // the chunk's slots' four quadrant flags (slot order: coalesced; no memset launch)
+        for (uint32_t sl = cbase + (uint32_t)tid; sl < run; sl += kCcThreads)
+            if (sl < a.cap) a.rec_flags32[sl] = 0u;
+    __syncthreads();
+    auto prefix = [&](int first, int n, int stride) {  // inclusive prefix of s_d[first + i * stride], i < n
+        int acc = 0;
+        for (int i0 = 0; i0 < n; i0 += 16) {
+            int c[16];
+#pragma unroll
+            for (int i = 0; i < 16; ++i) c[i] = i0 + i < n ? s_d[first + (i0 + i) * stride] : 0;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                acc += c[i];
+                if (i0 + i < n) s_d[first + (i0 + i) * stride] = acc;
+            }
+        }
+    };
+    if (tid < gy) prefix(tid * gp, gx, 1);
+    __syncthreads();
+    if (tid < gx) prefix(tid, gy, gp);
+    __syncthreads();
+    uint32_t* __restrict__ row = a.chunk_hist + (size_t)d * nt;  // (block-major: one coalesced row)
+    for (int t = tid; t < nt; t += kCcThreads) row[t] = (uint32_t)s_d[(t / gx) * gp + t % gx];
+}
+
+constexpr int kReEPT = 16, kReBatch = 256 * kReEPT, kReList = 2048, kReSub = 1024;
+static_assert(kReList < 65535 && kReBatch <= 65536, "u16 owners and staged positions");
+// BITS: bits of a tile's index inside its region (region_rows x gx <= 1024 tiles)
+template <int BITS, bool IDS>
+__global__ __launch_bounds__(256) void k_region_emit(EmitArgs a) {
+    constexpr int NDIG = 1 << BITS, PER = NDIG >= 256 ? NDIG / 256 : 1;
+    __shared__ uint32_t lds4[4];
+    __shared__ uint32_t s_magic[256];
+    __shared__ uint32_t s_pos[NDIG];      // per region tile: global position of the next instance (see k_emit_tiles)
+    __shared__ uint16_t cnt[4][NDIG];     // per-wave tile counters, then the staged runs' starts
+    __shared__ uint16_t s_own[kReBatch];  // the batch's owners (+1): marks at the entries' first instances, prefix max
+    __shared__ uint16_t s_idx[kReBatch];  // staged, tile-major: the instance's position in the batch
+    __shared__ uint32_t s_lrect[kReList], s_lstart[kReList], s_lid[kReList];  // the list: rect, first instance, id
+    __shared__ uint32_t s_lsf[IDS ? 1 : kReList];                             // first slot (pairs)
+    __shared__ uint32_t s_carry;
+    fill_div_magic(s_magic);
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int gx = a.gx, gy = a.gy, nt = a.ntiles, RH = a.region_rows;
+    const uint32_t P = (uint32_t)a.P;
+    // (chunk, region): consecutive (chunk-major) on one XCD (workgroups go to the XCDs round-robin), so a chunk's
+    // depth-order entries, read by each of its regions, stay in that XCD's L2
+    const uint32_t nreg = (uint32_t)div_up_u((uint32_t)gy, (uint32_t)RH), N = (uint32_t)a.chunks * nreg;
+    const uint32_t per_x = div_up_u(N, 8u);
+    const uint32_t logical = (blockIdx.x & 7u) * per_x + (blockIdx.x >> 3);
+    if (logical >= N) return;  // (workgroup-uniform, before any barrier)
+    const uint32_t d = logical / nreg, reg = logical - d * nreg;
+    const uint32_t ry0 = reg * (uint32_t)RH, ry1 = min((uint32_t)gy, ry0 + (uint32_t)RH);
+    const uint32_t t0 = ry0 * (uint32_t)gx, RT = (ry1 - ry0) * (uint32_t)gx;
+    for (int i = tid; i < NDIG; i += 256)
+        s_pos[i] = (uint32_t)i < RT ? a.tile_start[t0 + i] + a.chunk_hist[(size_t)d * nt + t0 + i] : 0u;
+    for (int i = tid; i < 4 * NDIG; i += 256) (&cnt[0][0])[i] = 0;
+    // region-local tile of instance j (relative to the list's first) owned by list entry o; y, x and the
+    // instance's row-major index in its whole rect on the side
+    auto place = [&](uint32_t j, uint32_t o, uint32_t& y, uint32_t& x, uint32_t& kr) {
+        const uint32_t q = s_lrect[o];
+        const uint32_t x0 = q & 0xFFu, y0 = (q >> 8) & 0xFFu, wd = ((q >> 16) & 0xFFu) - x0;
+        const uint32_t ya = max(y0, ry0);
+        const uint32_t k = j - s_lstart[o];
+        const uint32_t ky = div_small(k, wd, s_magic), kx = k - ky * wd;
+        y = ya + ky;
+        x = x0 + kx;
+        kr = (y - y0) * wd + kx;
+        return (y - ry0) * (uint32_t)gx + x;
+    };
+    // expand the list's n_inst instances (n_list entries): batches of kReBatch, ranked, staged, stored
+    auto expand = [&](uint32_t n_list, uint32_t n_inst) {
+        for (uint32_t j0 = 0; j0 < n_inst; j0 += (uint32_t)kReBatch) {
+            const uint32_t nb = n_inst - j0 < (uint32_t)kReBatch ? n_inst - j0 : (uint32_t)kReBatch;
+#pragma unroll
+            for (int i = 0; i < kReEPT; ++i) s_own[tid * kReEPT + i] = 0;
+            __syncthreads();
+            for (uint32_t i = (uint32_t)tid; i < n_list; i += 256) {
+                const uint32_t st = s_lstart[i];
+                if (st >= j0 && st < j0 + nb) s_own[st - j0] = (uint16_t)(i + 1u);  // (list entries: distinct starts)
+            }
+            const uint32_t carry = j0 ? s_carry : 0u;
+            __syncthreads();
+            {
+                uint32_t run = 0;
+#pragma unroll
+                for (int i = 0; i < kReEPT; ++i) run = max(run, (uint32_t)s_own[tid * kReEPT + i]);
+                run = max(carry, block_exclusive_max(run, lds4));
+#pragma unroll
+                for (int i = 0; i < kReEPT; ++i) {
+                    run = max(run, (uint32_t)s_own[tid * kReEPT + i]);
+                    s_own[tid * kReEPT + i] = (uint16_t)run;
+                }
+            }
+            __syncthreads();
+            uint32_t dg[kReEPT], loc[kReEPT];
+#pragma unroll
+            for (int e = 0; e < kReEPT; ++e) {
+                const uint32_t jj = (uint32_t)(w * 64 * kReEPT + e * 64 + lane);
+                const bool valid = jj < nb;
+                const uint64_t vm = __ballot(valid);
+                dg[e] = 0u;
+                loc[e] = 0u;
+                if (vm != 0) {  // (wave-uniform; no break: the loop stays unrolled)
+                    uint32_t y, x, kr;
+                    const uint32_t t = valid ? place(j0 + jj, (uint32_t)s_own[jj] - 1u, y, x, kr) : 0u;
+                    const uint64_t peers = match_digit<BITS>(t, vm);
+                    const uint32_t rank = (uint32_t)__popcll(peers & lanemask_lt());
+                    const uint32_t old = cnt[w][t];
+                    dg[e] = t;
+                    loc[e] = old + rank;
+                    if (valid && rank == 0) cnt[w][t] = (uint16_t)(old + (uint32_t)__popcll(peers));
+                }
+            }
+            __syncthreads();
+            {   // the batch's tile runs (wave-major inside a tile) and their global bases
+                uint32_t t4[PER][4];
+                uint32_t sum = 0;
+#pragma unroll
+                for (int i = 0; i < PER; ++i) {
+                    const int t = tid * PER + i;
+#pragma unroll
+                    for (int v = 0; v < 4; ++v) t4[i][v] = t < NDIG ? cnt[v][t] : 0u;
+                    sum += t4[i][0] + t4[i][1] + t4[i][2] + t4[i][3];
+                }
+                uint32_t all;
+                uint32_t run = block_exclusive_scan(sum, lds4, all);
+#pragma unroll
+                for (int i = 0; i < PER; ++i) {
+                    const int t = tid * PER + i;
+                    if (t < NDIG) {
+                        cnt[0][t] = (uint16_t)run;
+                        cnt[1][t] = (uint16_t)(run + t4[i][0]);
+                        cnt[2][t] = (uint16_t)(run + t4[i][0] + t4[i][1]);
+                        cnt[3][t] = (uint16_t)(run + t4[i][0] + t4[i][1] + t4[i][2]);
+                        s_pos[t] -= run;
+                    }
+                    run += t4[i][0] + t4[i][1] + t4[i][2] + t4[i][3];
+                }
+            }
+            __syncthreads();
+#pragma unroll
+            for (int e = 0; e < kReEPT; ++e) {
+                const uint32_t jj = (uint32_t)(w * 64 * kReEPT + e * 64 + lane);
+                if (jj < nb) s_idx[cnt[w][dg[e]] + loc[e]] = (uint16_t)jj;
+            }
+            __syncthreads();
+#pragma unroll
+            for (int e = 0; e < kReEPT; ++e) {
+                const uint32_t i = (uint32_t)(e * 256 + tid);
+                if (i < nb) {
+                    const uint32_t jj = s_idx[i];
+                    const uint32_t o = (uint32_t)s_own[jj] - 1u;
+                    uint32_t y, x, kr;
+                    const uint32_t t = place(j0 + jj, o, y, x, kr);
+                    const uint32_t pos = s_pos[t] + i;
+                    if (pos < a.cap) {  // (bounded by the layout: see bin_emit)
+                        if constexpr (IDS) reinterpret_cast<uint32_t*>(a.pairs_out)[pos] = s_lid[o];
+                        else a.pairs_out[pos] = make_uint2(s_lid[o], min(s_lsf[o] + kr, a.cap - 1u));
+                    }
+                }
+            }
+            __syncthreads();
+            // the next batch's positions: each tile's run ends where the next tile's begins (the batch's end for
+            // the last)
+#pragma unroll
+            for (int i = 0; i < PER; ++i) {
+                const int t = tid * PER + i;
+                if (t < NDIG) s_pos[t] += t + 1 < NDIG ? (uint32_t)cnt[0][t + 1] : nb;
+            }
+            if (tid == 0) s_carry = s_own[nb - 1];
+            __syncthreads();
+            for (int i = tid; i < 4 * NDIG; i += 256) (&cnt[0][0])[i] = 0;
+        }
+    };
+    const uint32_t r0 = d * (uint32_t)kChunkG;
+    uint32_t n_list = 0, n_inst = 0;
+    for (uint32_t sb = 0; sb < (uint32_t)kChunkG && r0 + sb < P; sb += (uint32_t)kReSub) {
+        // four consecutive depth ranks per thread; an entry of the list if its rect reaches the region's rows
+        uint2 gr[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const uint32_t r = r0 + sb + (uint32_t)(tid * 4 + i);
+            gr[i] = r < P ? a.order[r] : make_uint2(0u, 0u);
+        }
+        uint32_t cr[4], nsel = 0, ninst = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const uint32_t q = gr[i].x;
+            const uint32_t x0 = q & 0xFFu, y0 = (q >> 8) & 0xFFu, x1 = (q >> 16) & 0xFFu, y1 = q >> 24;
+            const uint32_t ya = max(y0, ry0), yb = min(y1, ry1);
+            cr[i] = x1 > x0 && yb > ya ? (yb - ya) * (x1 - x0) : 0u;  // (<= 1024: the region's tiles)
+            nsel += cr[i] ? 1u : 0u;
+            ninst += cr[i];
+        }
+        // one scan for both: entries (< 2^11) above instances (<= 1024 x 1024 = 2^20 per 1024 ranks)
+        uint32_t tot;
+        const uint32_t ex = block_exclusive_scan(nsel << 21 | ninst, lds4, tot);
+        uint32_t lp = n_list + (ex >> 21), io = n_inst + (ex & 0x1FFFFFu);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            if (cr[i]) {
+                s_lrect[lp] = gr[i].x;
+                s_lstart[lp] = io;
+                s_lid[lp] = gr[i].y;
+                if constexpr (!IDS) s_lsf[lp] = a.first_slot[gr[i].y];
+                ++lp;
+                io += cr[i];
+            }
+        n_list += tot >> 21;
+        n_inst += tot & 0x1FFFFFu;
+        const bool last = sb + (uint32_t)kReSub >= (uint32_t)kChunkG || r0 + sb + (uint32_t)kReSub >= P;
+        if (n_list > (uint32_t)(kReList - kReSub) || (last && n_list)) {
+            __syncthreads();
+            expand(n_list, n_inst);
+            __syncthreads();
+            n_list = 0;
+            n_inst = 0;
+        }
+    }
+}
+
+void launch_region_emit(const EmitArgs& a, hipStream_t s) {
+    if (a.P <= 0) return;
+    const int nt = a.ntiles, nc = a.chunks;
+    hipLaunchKernelGGL(k_chunk_count, dim3(nc), dim3(kCcThreads), (size_t)4 * a.gy * (a.gx + 1), s, a);
+    hipLaunchKernelGGL(k_radix_digit_scan, dim3(div_up(nt, kScanDigits)), dim3(kScanThreads), 0, s, a.chunk_hist, nc, nt,
+                       a.ttotals, (const uint32_t*)nullptr, 0u, 1);
+    hipLaunchKernelGGL(k_ranges_counts, dim3(1), dim3(256), 0, s, a.ttotals, nt, a.ranges, a.tile_order, a.cap,
+                       a.tile_start);
+    const int nreg = div_up(a.gy, a.region_rows), grid = 8 * div_up((long long)nc * nreg, 8);
+    const int bits = ceil_log2((uint32_t)(a.region_rows * a.gx));
+#define GS_RE(B)                                                                                   \
+    if (a.ids_only) hipLaunchKernelGGL((k_region_emit<B, true>), dim3(grid), dim3(256), 0, s, a); \
+    else hipLaunchKernelGGL((k_region_emit<B, false>), dim3(grid), dim3(256), 0, s, a)
+    if (bits <= 8) { GS_RE(8); }
+    else if (bits <= 9) { GS_RE(9); }
+    else { GS_RE(10); }
+#undef GS_RE
 }
 
 void launch_emit_fused(const EmitArgs& a, hipStream_t s) {
@@ -1566,7 +1927,8 @@ void launch_row_pass(const EmitArgs& a, uint32_t K, uint2* point_pairs, uint32_t
         hipLaunchKernelGGL((k_radix_scatter<kXBits, IPT, false, kValPair, false, true, uint16_t>), dim3(nb), dim3(256),
                            0, s, keys, a.pairs_out, nullptr, point_pairs, nullptr, K, kXBits, hist, a.xtotals, nb, bm, ro,
                            (const uint32_t*)nullptr, n_dev);
-    hipLaunchKernelGGL(k_ranges_counts, dim3(1), dim3(256), 0, s, a.tile_count, a.ntiles, ranges, tile_order);
+    hipLaunchKernelGGL(k_ranges_counts, dim3(1), dim3(256), 0, s, a.tile_count, a.ntiles, ranges, tile_order,
+                       0xFFFFFFFFu, (uint32_t*)nullptr);
 }
 
 void launch_scan_reduce(const EmitArgs& a, hipStream_t s) {

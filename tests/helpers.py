@@ -137,7 +137,8 @@ def run_gpu(settings, dL_dpix=None, means3D=None, opacities=None, shs=None, colo
         out["n_contrib"] = view(img, "image", "n_contrib", np.uint32, W * H)
         out["ranges"] = view(img, "image", "ranges", np.uint32, 2 * tiles)
         # per-tile lists: (Gaussian, slot) pairs; the Gaussian ids are the reference's point_list
-        out["point_list"] = view(binning, "binning", "point_pairs", np.uint32, 2 * K)[0::2] if K else np.zeros(0, np.uint32)
+        out["point_pairs"] = view(binning, "binning", "point_pairs", np.uint32, 2 * K) if K else np.zeros(0, np.uint32)
+        out["point_list"] = out["point_pairs"][0::2]
     if dL_dpix is not None:
         g = torch.as_tensor(np.asarray(dL_dpix, np.float32)).to(dev)
         dconic = torch.empty((P, 3), dtype=torch.float32, device=dev) if conic_grad else None

@@ -977,6 +977,46 @@ def test_two_level_binning_matches_two_pass_sort(cuda_device, monkeypatch, P, W,
         np.testing.assert_array_equal(fused[k], ref[k], err_msg=k)
 
 
+@pytest.mark.parametrize("P,W,H,scale", [(300_000, 1920, 1080, 0.02), (2_000, 1920, 1080, 0.02),
+                                         (200_000, 1280, 720, 0.02), (200_000, 1024, 768, 0.02),
+                                         (150_000, 2048, 1536, 0.02), (4_000, 1920, 1080, 0.3),
+                                         (60_000, 4000, 400, 0.05)])
+def test_region_emission_matches_two_level_binning(cuda_device, monkeypatch, P, W, H, scale):
+    """DGE_AMD_BINNING=region (opt-in; slower than the two-level binning at c4) bins grids of 2049..12288 tiles by
+    the region emission — per-chunk tile counts, a scan over the chunks, then one workgroup per (depth chunk,
+    band of tile rows) expands the chunk's instances in its rows and stores each tile's run straight into the
+    lists.  Against the default (two-level binning: column emission + row pass) the (Gaussian, slot) pairs,
+    ranges, image and every gradient are bitwise the same, and so is a forward-only render's image (Gaussian ids
+    alone in the lists).  2k Gaussians at 1080p: a count table larger than the tile-sort key space it borrows
+    (falls back to the two-level binning); 2048 x 1536: 12288 tiles, the largest grid; 4k Gaussians of scale
+    0.3: rects spanning many regions and lists of more than one batch; 4000 x 400: 250 tiles wide, beyond the
+    two-level binning's 128 columns (the default there is the emission + two-pass tile sort)."""
+    from dge_amd.cameras import orbit_camera
+    from dge_amd.gaussian_renderer import PipelineParams, render
+    from dge_amd.scene import synthetic_scene
+
+    a = scene_arrays(P, seed=6, radius=2.0, scale=scale)
+    g = np.random.default_rng(8).standard_normal((3, H, W)).astype(np.float32) * 1e-3
+    s = camera_settings(W, H, device="cuda")
+    ref = run_gpu(s, g, **_sh_kw(a))
+    monkeypatch.setenv("DGE_AMD_BINNING", "region")
+    band = run_gpu(s, g, **_sh_kw(a))
+    assert band["num_rendered"] == ref["num_rendered"] > 0
+    for k in ("ranges", "point_pairs", "n_contrib", "color", "final_T") + tuple(GRAD_NAMES):
+        np.testing.assert_array_equal(band[k], ref[k], err_msg=k)
+    dev = torch.device("cuda")
+    sc = synthetic_scene(P, sh_degree=3, seed=6, scale=scale, device=dev)
+    cam = orbit_camera(1, 3, W, H, device=dev)
+    bg = torch.tensor([0.1, 0.2, 0.3], device=dev)
+    with torch.no_grad():
+        one = render(cam, sc, PipelineParams(), bg)
+        monkeypatch.delenv("DGE_AMD_BINNING")
+        two = render(cam, sc, PipelineParams(), bg)
+    torch.cuda.synchronize()
+    for k in ("render", "radii", "depth_3dgs"):
+        assert torch.equal(one[k], two[k]), k
+
+
 @pytest.mark.parametrize("W,H", [(4128, 48), (4128, 320)], ids=["single_pass", "two_pass"])
 def test_wide_grid_unpacked_rects_vs_oracle(cuda_device, oracle, W, H):
     """Grids more than 255 tiles wide carry tiles_touched instead of a packed rect through the depth sort
