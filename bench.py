@@ -389,6 +389,10 @@ def main():
             r["limit"] = "hbm" if r["frac"] > 0.5 else "valu" if vf > 0.5 else "latency"
         if tr.get("build"):
             r["pmc_build"] = tr["build"]
+            # the PMC pass measured the kernel sources this run was built from (else the traffic is stale)
+            from dge_amd._native import source_stamp
+
+            r["pmc_build_current"] = tr["build"] == source_stamp()
         rooflines[name] = r
     roofline = max(rooflines.values(), key=lambda r: r["avg_ms"]) if rooflines else None
 

@@ -17,6 +17,22 @@ HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "gs_raster.h")
 
 ABI_VERSION = 19  # GS_RASTER_ABI_VERSION of include/gs_raster.h this binding is written against
 
+
+def source_stamp() -> str:
+    """A stamp of the kernel sources the library is built from (sha1 of dge_amd/csrc/*.hip and *.h, by name):
+    profiles/pmc_traffic.json records the stamp of the build it measured, and bench.py reports whether the
+    running build still has it."""
+    import glob
+    import hashlib
+
+    h = hashlib.sha1()
+    csrc = os.path.join(_HERE, "csrc")
+    for f in sorted(glob.glob(os.path.join(csrc, "*.hip")) + glob.glob(os.path.join(csrc, "*.h"))):
+        h.update(os.path.basename(f).encode())
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:12]
+
 GS_OK = 0
 GS_ERR_INVALID_ARG = 1
 GS_ERR_HIP = 2

@@ -22,6 +22,10 @@ STAGE = {"k_preprocess": "preprocess", "k_render_fwd": "render_fwd", "k_render_b
 
 
 def main(root):
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+    from dge_amd._native import source_stamp  # (the kernel sources of the build that was measured)
+
+    stamp = source_stamp()
     vals = collections.defaultdict(lambda: collections.defaultdict(list))
     for f in glob.glob(os.path.join(root, "p*", "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
@@ -49,8 +53,7 @@ def main(root):
             e["bytes_per_launch"] += int(rd + wr)
             if "SQ_INSTS_VALU" in c:
                 e["valu_insts_per_launch"] = int(e.get("valu_insts_per_launch", 0) + c["SQ_INSTS_VALU"])
-            if os.environ.get("PMC_BUILD"):
-                e["build"] = os.environ["PMC_BUILD"]
+            e["build"] = os.environ.get("PMC_BUILD") or stamp
     if out:
         dst = os.path.join(root, "pmc_traffic.json")  # copied into profiles/ by hand after the run
         json.dump(out, open(dst, "w"), indent=1)
