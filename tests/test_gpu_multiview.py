@@ -474,8 +474,9 @@ def test_deferred_union_check_two_ranks(cuda_device, world, V):
     four ranks on one card (gloo, CUDA tensors; 10 views over 4 ranks: uneven 3/3/2/2 shards), the bucket
     after the packed SUM at a speculated capacity equals the dense all-reduce of the ranks' buckets (bit for
     bit with two ranks; with four, to the rounding of the collective's rank order, which depends on the
-    row's position in the buffer) — also when the capacity is a third of the union and the deferred check
-    all-reduces the rows past it."""
+    row's position in the buffer: shown on the CPU by test_allreduce_sum_order_depends_on_buffer_position,
+    where every 4-rank result is an fp32 reordering of the same sum) — also when the capacity is a third of
+    the union and the deferred check all-reduces the rows past it."""
     P, W, H = 300_000, 160, 128  # (a union under half the rows: the packed path)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()

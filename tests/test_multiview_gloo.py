@@ -242,3 +242,74 @@ def test_row_major_bucket_layout():
     assert float(bk.rows[3, 10:55].max()) == 3.0  # (the SH rest block, 45 floats of row 3)
     bk.zero()
     assert not bk.flat.any() and bk.check_attached()
+
+
+def _order_worker(rank, world, port, pad, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["GLOO_SOCKET_IFNAME"] = "lo"
+    os.environ["MASTER_PORT"] = str(port)
+    try:
+        dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=90))
+        g = torch.Generator().manual_seed(100 + rank)
+        n = 20_000
+        # magnitudes over six decades: the 4-term sums' rounding depends on the order of the terms
+        v = torch.randn(n, generator=g) * torch.pow(10.0, torch.randint(-3, 3, (n,), generator=g).float())
+        dense = v.clone()
+        dist.all_reduce(dense)
+        shifted = torch.cat([torch.zeros(pad), v])  # the same values at another offset of the buffer
+        dist.all_reduce(shifted)
+        allv = [torch.empty_like(v) for _ in range(world)]
+        dist.all_gather(allv, v)
+        q.put((rank, dense.numpy(), shifted[pad:].numpy(), torch.stack(allv).numpy(), None))
+    except Exception as e:  # report instead of hanging the parent
+        q.put((rank, None, None, None, repr(e)))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def _fp32_sums(terms):
+    """Every fp32 result of summing the four per-rank terms (columns of `terms` [4, n]) in any order: the
+    24 left folds and the 3 x 8 pairwise trees."""
+    import itertools
+
+    t = terms.astype(np.float32)
+    out = []
+    for p in itertools.permutations(range(4)):
+        s = t[p[0]]
+        for k in p[1:]:
+            s = (s + t[k]).astype(np.float32)
+        out.append(s)
+        out.append(((t[p[0]] + t[p[1]]).astype(np.float32) + (t[p[2]] + t[p[3]]).astype(np.float32)).astype(np.float32))
+    return np.stack(out)
+
+
+@pytest.mark.slow
+def test_allreduce_sum_order_depends_on_buffer_position():
+    """Why the 4-rank GPU tests compare the packed (sparse-row) all-reduce with the dense one to the rounding of
+    the sum and not bit for bit (test_gpu_multiview.py, the deferred union check): gloo's SUM over 4 ranks adds
+    an element's 4 terms in an order that depends on where the element sits in the buffer.  The same values
+    all-reduced at two offsets of a buffer give different bits for some elements, and every result is one of
+    the fp32 sums of the same 4 terms in some order — a reordering of the sum, not an error.  (With 2 ranks
+    a + b = b + a: bit for bit.)"""
+    world, pad = 4, 1237
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_order_worker, args=(r, world, port, pad, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=180) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+    for r in res:
+        assert r[4] is None, r[4]
+    _, dense, shifted, terms, _ = res[0]
+    cand = _fp32_sums(terms)
+    assert np.all((cand == dense[None, :]).any(axis=0)), "dense: not a reordering of the 4-term sum"
+    assert np.all((cand == shifted[None, :]).any(axis=0)), "shifted: not a reordering of the 4-term sum"
+    differ = int((dense != shifted).sum())
+    assert differ > 0, "the summation order did not depend on the buffer position"
+    for r in res[1:]:  # every rank holds the same result
+        np.testing.assert_array_equal(r[1], dense)
+        np.testing.assert_array_equal(r[2], shifted)
