@@ -539,13 +539,40 @@ __device__ __forceinline__ float row_sum16(float v) {
 // 3 swaps + 3 adds + 4 DPP adds for four sums instead of 4 x 6 DPP adds.
 // Result: every lane of row 0 holds sum(a), row 1 sum(c), row 2 sum(b),
 // row 3 sum(d).  Fixed summation order (deterministic).
-__device__ __forceinline__ float quad_reduce(float a, float b, float c, float d) {
+__device__ __forceinline__ float quad_reduce_rows(float a, float b, float c, float d) {  // before the row sum
     const auto p = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(b), false, false);
     const float ab = __uint_as_float(p[0]) + __uint_as_float(p[1]);  // lanes 0-31: a, 32-63: b
     const auto q = __builtin_amdgcn_permlane32_swap(__float_as_uint(c), __float_as_uint(d), false, false);
     const float cd = __uint_as_float(q[0]) + __uint_as_float(q[1]);  // lanes 0-31: c, 32-63: d
     const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(ab), __float_as_uint(cd), false, false);
-    return row_sum16(__uint_as_float(r[0]) + __uint_as_float(r[1]));  // rows: a, c, b, d
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);  // rows: a, c, b, d (each still to be summed)
+}
+__device__ __forceinline__ float quad_reduce(float a, float b, float c, float d) {
+    return row_sum16(quad_reduce_rows(a, b, c, d));
+}
+
+// row_sum16 of nine values at once, each step one v_add_f32_dpp.  (Written out: the compiler pairs the row
+// sums' adds of two values into one v_pk_add_f32, which takes no DPP operand, so each step became a
+// v_mov_b32_dpp per value plus half a packed add — 36 + 9 instructions where 36 do.)  Same adds in the same
+// order as row_sum16 on each value, so the sums are bitwise row_sum16's.  A DPP read of a VGPR needs two wait
+// states after the VALU write of it (the s_nop for the inputs); inside, a value is read again nine
+// instructions after its write.
+__device__ __forceinline__ void row_sum16_x9(float (&v)[9]) {
+#define GS_DPP9(CTRL)                                                                                  \
+    "v_add_f32_dpp %0, %0, %0 " CTRL " row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"                 \
+    "v_add_f32_dpp %1, %1, %1 " CTRL " row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"                 \
+    "v_add_f32_dpp %2, %2, %2 " CTRL " row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"                 \
+    "v_add_f32_dpp %3, %3, %3 " CTRL " row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"                 \
+    "v_add_f32_dpp %4, %4, %4 " CTRL " row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"                 \
+    "v_add_f32_dpp %5, %5, %5 " CTRL " row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"                 \
+    "v_add_f32_dpp %6, %6, %6 " CTRL " row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"                 \
+    "v_add_f32_dpp %7, %7, %7 " CTRL " row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"                 \
+    "v_add_f32_dpp %8, %8, %8 " CTRL " row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+    asm("s_nop 1\n\t" GS_DPP9("quad_perm:[1,0,3,2]") GS_DPP9("quad_perm:[2,3,0,1]") GS_DPP9("row_half_mirror")
+            GS_DPP9("row_mirror")
+        : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]), "+v"(v[7]),
+          "+v"(v[8]));
+#undef GS_DPP9
 }
 
 __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {

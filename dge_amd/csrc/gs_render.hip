@@ -996,7 +996,8 @@ __global__ __launch_bounds__(64, GS_BWD_WAVES) void k_render_bwd(RenderBwdArgs a
             // (entries 0 and 2, 1 and 3 swapped together: the operands of each lane swap then sit in
             // different register pairs of the packed products — no copy before the swap — and row r
             // holds entry r; the per-entry sums are the same adds in the same order)
-            for (int f = 0; f < 9; ++f) S[f] = quad_reduce(g[0][f], g[2][f], g[1][f], g[3][f]);
+            for (int f = 0; f < 9; ++f) S[f] = quad_reduce_rows(g[0][f], g[2][f], g[1][f], g[3][f]);
+            row_sum16_x9(S);
             __builtin_amdgcn_sched_barrier(0);
             const int kw = k + row_entry;
             if (row_writer && kw < nk) {
