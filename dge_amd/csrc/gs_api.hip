@@ -692,11 +692,9 @@ int bin_forward(const gs_settings* s, const Grid& g, const gs_params& gp, int* r
 // records), then the per-Gaussian pass over those records, whose accumulated writes wait for
 // writes_after.  R: the binning layout's instance count; slot_cap: a speculative forward's capacity
 // (its slots end there), else ~0.
-int replay_view(const gs_settings* s, const gs_params* gp, int R, const void* geom, const void* binning,
-                const void* img, const float* dL_dpix, hipStream_t stream) {
+RenderBwdArgs replay_args(const gs_settings* s, const gs_params* gp, int R, const void* geom, const void* binning,
+                          const void* img, const float* dL_dpix) {
     const int P = gp->P;
-    if (P == 0 || R <= 0) return GS_OK;
-    const bool debug = s->debug != 0;
     const Grid g = make_grid(s);
     const GeomLayout gl = geom_layout(P);
     const ImgLayout il = img_layout(g.W, g.H);
@@ -720,6 +718,14 @@ int replay_view(const gs_settings* s, const gs_params* gp, int R, const void* ge
     rb.records = at<float4>(const_cast<void*>(binning), bl.records);
     rb.rec_flags = at<uint8_t>(const_cast<void*>(binning), bl.rec_flags);
     rb.diag = diag_buffer(1, kDiagWords * 4 * bl.nslots);
+    return rb;
+}
+
+int replay_view(const gs_settings* s, const gs_params* gp, int R, const void* geom, const void* binning,
+                const void* img, const float* dL_dpix, hipStream_t stream) {
+    if (gp->P == 0 || R <= 0) return GS_OK;
+    const bool debug = s->debug != 0;
+    const RenderBwdArgs rb = replay_args(s, gp, R, geom, binning, img, dL_dpix);
     { StageScope sc(ST_RENDER_BWD, stream); launch_render_backward(rb, stream); }
     GS_LAUNCHED("render backward");
     return GS_OK;
@@ -1237,6 +1243,11 @@ int gs_rasterize_backward_passes(int n, const gs_settings* const* s, const gs_pa
 // ---------------------------------------------------------------------
 namespace {
 // ordering events of the views' backward calls, reused across batches
+// The pool's events only order streams on the device (hipStreamWaitEvent; the host never waits on them):
+// no system-scope fence, which a record otherwise pays with an L2 writeback for the host's view
+#ifndef GS_POOL_EVENT_FLAGS
+#define GS_POOL_EVENT_FLAGS (hipEventDisableTiming | hipEventDisableSystemFence)
+#endif
 struct EventPool {
     std::mutex mu;
     std::vector<hipEvent_t> free;
@@ -1250,7 +1261,7 @@ struct EventPool {
             }
         }
         hipEvent_t e = nullptr;
-        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return nullptr;
+        if (hipEventCreateWithFlags(&e, GS_POOL_EVENT_FLAGS) != hipSuccess) return nullptr;
         return e;
     }
     void put(hipEvent_t e) {
@@ -1476,17 +1487,15 @@ int gs_views_backward(gs_views* h, const float* const* dL_dpix, const gs_grads* 
                                              dL_dpix[v], grads[v]);
             if (rc) return rc;
         }
-        int rc0 = fork_from(h, join, streams);  // (the image gradients come from the caller's stream)
-        if (rc0) return rc0;
         if (h->n > 1 && views_mergeable(h, grads)) {
-            // every view's replay on its stream, then ONE per-Gaussian pass over all of them (chunks of
+            // every view's replay, then ONE per-Gaussian pass over all of them (chunks of
             // gauss_backward_max_views() views, in view order) on the first view's stream
             hipStream_t s0 = (hipStream_t)streams[0];
             const bool debug = h->f[0].s.debug != 0;
             hipStream_t stream = s0;  // (GS_LAUNCHED)
             const int chunk = gauss_backward_max_views();
             // one pass for the batch: its first half (the live set from the forwards' touched bytes) runs
-            // on s0 right behind view 0's replay, beside the other views' replays, not after all of them
+            // on s0 right behind view 0's replay (or the merged replay)
             const bool split = h->n <= chunk;
             GaussBwdArgs ga[GS_MAX_VIEWS];
             if (split)
@@ -1495,7 +1504,70 @@ int gs_views_backward(gs_views* h, const float* const* dL_dpix, const gs_grads* 
                     ga[v] = gauss_args(&f.s, &f.gp, (int)h->layout[v], f.radii, f.geom, h->bin[v], grads[v],
                                        h->spec[v] ? h->layout[v] : 0xFFFFFFFFu);
                 }
-            for (int v = 0; v < h->n; ++v) {
+            // Views on several streams: every replay in ONE launch on s0 (k_render_bwd_views), so the backward
+            // makes no cross-stream hop — the fork to the views' streams and their join back before the
+            // per-Gaussian pass each cost ~10 us of queue time (tools/probes/queue_gap.hip).  Views on one
+            // stream keep one launch per view (no hop either way; the per-launch stage times stay per view).
+            // Off with the per-wave diagnostics (their buffer is per launch) or DGE_AMD_REPLAY_MERGE=0.
+            bool merge = false;
+            for (int v = 1; v < h->n; ++v) merge |= streams[v] != streams[0];
+            if (merge) {
+                const char* e = getenv("DGE_AMD_REPLAY_MERGE");
+                merge = !(e && !strcmp(e, "0"));
+            }
+            RenderBwdArgs rbs[GS_MAX_VIEWS];
+            int nr = 0;
+            for (int v = 0; merge && v < h->n; ++v) {
+                FwdState& f = h->f[v];
+                if (f.gp.P == 0 || h->layout[v] == 0) continue;
+                rbs[nr] = replay_args(&f.s, &f.gp, (int)h->layout[v], f.geom, h->bin[v], f.img, dL_dpix[v]);
+                merge = rbs[nr++].diag == nullptr;
+            }
+            if (merge) {
+                if (s0 != join) {  // (only s0 starts after the caller's work)
+                    if (!h->fork && !(h->fork = event_pool().get())) return set_error(GS_ERR_HIP, "could not create an event");
+                    GS_HIP(hipEventRecord(h->fork, join));
+                    GS_HIP(hipStreamWaitEvent(s0, h->fork, 0));
+                }
+                // the live-set pass (it reads the forwards' outputs only) on the first other view stream, beside the
+                // merged replay instead of after it on s0: c2 3089 -> 3181 renders/s with the merge
+                // (profiles/r06/queues/ab_merged_replay.txt); DGE_AMD_LIVE_SIDE=0: after it
+                int side = -1;
+                if (split) {
+                    const char* e = getenv("DGE_AMD_LIVE_SIDE");
+                    for (int v = 1; !(e && !strcmp(e, "0")) && side < 0 && v < h->n; ++v)
+                        if (streams[v] != streams[0]) side = v;
+                }
+                if (side > 0) {
+                    hipStream_t ss = (hipStream_t)streams[side];
+                    if (!h->ev[0] && !(h->ev[0] = event_pool().get())) return set_error(GS_ERR_HIP, "could not create an event");
+                    GS_HIP(hipEventRecord(h->ev[0], s0));
+                    GS_HIP(hipStreamWaitEvent(ss, h->ev[0], 0));
+                    { StageScope sc(ST_GAUSS_LIVE, ss); launch_gauss_live_views(ga, h->n, ss, (hipEvent_t)writes_after); }
+                    hipStream_t stream = ss;  // (GS_LAUNCHED)
+                    GS_LAUNCHED("gaussian live set (views, side stream)");
+                    if (!h->ev[side] && !(h->ev[side] = event_pool().get())) return set_error(GS_ERR_HIP, "could not create an event");
+                    GS_HIP(hipEventRecord(h->ev[side], ss));
+                }
+                if (nr) {
+                    // (the grids a quarter of the item bounds: ~3.7x the real items at c2; DGE_AMD_REPLAY_GRID_DIV
+                    // forces smaller ones, so the tests run the blocks' item loop)
+                    const char* d = getenv("DGE_AMD_REPLAY_GRID_DIV");
+                    const uint32_t div = d ? (uint32_t)std::max(1, atoi(d)) : 4u;
+                    { StageScope sc(ST_RENDER_BWD, s0); launch_render_backward_views(rbs, nr, div, s0); }
+                    GS_LAUNCHED("render backward (views)");
+                }
+                if (side > 0) {
+                    GS_HIP(hipStreamWaitEvent(s0, h->ev[side], 0));
+                } else if (split) {
+                    { StageScope sc(ST_GAUSS_LIVE, s0); launch_gauss_live_views(ga, h->n, s0, (hipEvent_t)writes_after); }
+                    GS_LAUNCHED("gaussian live set (views)");
+                }
+            } else {
+                int rc0 = fork_from(h, join, streams);  // (the image gradients come from the caller's stream)
+                if (rc0) return rc0;
+            }
+            for (int v = 0; !merge && v < h->n; ++v) {
                 FwdState& f = h->f[v];
                 hipStream_t sv = (hipStream_t)streams[v];
                 int rc = replay_view(&f.s, &f.gp, (int)h->layout[v], f.geom, h->bin[v], f.img, dL_dpix[v], sv);
@@ -1503,7 +1575,7 @@ int gs_views_backward(gs_views* h, const float* const* dL_dpix, const gs_grads* 
                 // (before view 0's replay instead, beside the others' replays: 2861-2877 vs 2882-2898
                 // renders/s, profiles/r05/ab_scan_shape_live_first.txt)
                 if (split && v == 0) {
-                    { StageScope sc(ST_GAUSS_LIVE, s0); launch_gauss_live_views(ga, h->n, s0); }
+                    { StageScope sc(ST_GAUSS_LIVE, s0); launch_gauss_live_views(ga, h->n, s0, (hipEvent_t)writes_after); }
                     GS_LAUNCHED("gaussian live set (views)");
                 }
                 if (sv != s0) {
@@ -1514,7 +1586,7 @@ int gs_views_backward(gs_views* h, const float* const* dL_dpix, const gs_grads* 
             }
             if (split) {
                 { StageScope sc(ST_GAUSS_BWD, s0);
-                launch_gauss_bwd_live_views(ga, h->n, s0, (hipEvent_t)writes_after); }
+                launch_gauss_bwd_live_views(ga, h->n, s0, ga[0].dirty ? nullptr : (hipEvent_t)writes_after); }
                 GS_LAUNCHED("gaussian backward (views)");
             }
             for (int v0 = 0; !split && v0 < h->n; v0 += chunk) {
@@ -1535,6 +1607,8 @@ int gs_views_backward(gs_views* h, const float* const* dL_dpix, const gs_grads* 
             }
             return GS_OK;
         }
+        int rc0 = fork_from(h, join, streams);  // (the image gradients come from the caller's stream)
+        if (rc0) return rc0;
         int prev = -1;
         for (int v = 0; v < h->n; ++v) {
             FwdState& f = h->f[v];

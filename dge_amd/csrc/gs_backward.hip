@@ -789,8 +789,11 @@ static GaussBwdViews gauss_views(const GaussBwdArgs* views, int n) {
 
 // Pass 1 alone: it reads only what the forwards left (touched bytes, radii), so it may run before the
 // views' gradient replays end (gs_views_backward: behind view 0's replay, beside the others')
-void launch_gauss_live_views(const GaussBwdArgs* views, int n, hipStream_t s) {
+// writes_after: the pass marks the gradient bucket's dirty rows (GaussBwdArgs::dirty) — after the bucket's clear,
+// which zeroes the marked rows and resets the marks (a mark made before it would be lost, and the row never cleared)
+void launch_gauss_live_views(const GaussBwdArgs* views, int n, hipStream_t s, hipEvent_t writes_after) {
     if (views[0].P <= 0 || n <= 0) return;
+    if (writes_after && views[0].dirty) (void)hipStreamWaitEvent(s, writes_after, 0);
     hipLaunchKernelGGL(k_gauss_live, dim3(div_up(views[0].P, kGB)), dim3(kGB), 0, s, gauss_views(views, n));
 }
 
@@ -805,8 +808,8 @@ void launch_gauss_bwd_live_views(const GaussBwdArgs* views, int n, hipStream_t s
 }
 
 void launch_gauss_backward_views(const GaussBwdArgs* views, int n, hipStream_t s, hipEvent_t writes_after) {
-    launch_gauss_live_views(views, n, s);
-    launch_gauss_bwd_live_views(views, n, s, writes_after);
+    launch_gauss_live_views(views, n, s, writes_after);
+    launch_gauss_bwd_live_views(views, n, s, views[0].dirty ? nullptr : writes_after);  // (same stream: waited)
 }
 
 void launch_gauss_backward(const GaussBwdArgs& a, hipStream_t s, hipEvent_t writes_after) {

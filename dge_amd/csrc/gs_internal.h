@@ -495,6 +495,16 @@ struct RenderBwdArgs {
     uint64_t* diag;   // optional [item_cap][kDiagWords], by queue position (see diag_buffer)
 };
 void launch_render_backward(const RenderBwdArgs& a, hipStream_t s);
+// n views' replays as one launch per kMaxReplayViews views, on one stream (no diag): view v's grid is
+// grid_div-th of its item bound (rounded up to whole runs of 8 blocks), each block looping over the items
+// one grid apart
+constexpr int kMaxReplayViews = 4;
+struct RenderBwdViews {
+    int n;
+    uint32_t grid[kMaxReplayViews];
+    RenderBwdArgs v[kMaxReplayViews];
+};
+void launch_render_backward_views(const RenderBwdArgs* a, int n, uint32_t grid_div, hipStream_t s);
 
 struct GaussBwdArgs {
     int P, D, M, W, H, gx, gy;
@@ -531,7 +541,7 @@ void launch_gauss_backward(const GaussBwdArgs& a, hipStream_t s, hipEvent_t writ
 // gauss_backward_max_views() views per call
 void launch_gauss_backward_views(const GaussBwdArgs* views, int n, hipStream_t s, hipEvent_t writes_after = nullptr);
 // the same in its two passes (the first needs only the forwards' outputs)
-void launch_gauss_live_views(const GaussBwdArgs* views, int n, hipStream_t s);
+void launch_gauss_live_views(const GaussBwdArgs* views, int n, hipStream_t s, hipEvent_t writes_after);
 void launch_gauss_bwd_live_views(const GaussBwdArgs* views, int n, hipStream_t s, hipEvent_t writes_after);
 int gauss_backward_max_views();
 

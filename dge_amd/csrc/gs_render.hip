@@ -804,7 +804,8 @@ static_assert(kSegLen % kBwdHalf == 0, "whole staging units per segment");
 // sums are reduce-scattered across the wave (quad_reduce).  Each kept entry gets
 // one record at 4*slot + quadrant (slot: the binning slot, so k_gauss_bwd reads
 // a Gaussian's records contiguously) and a flag.
-__global__ __launch_bounds__(64, GS_BWD_WAVES) void k_render_bwd(RenderBwdArgs a) {
+// qi: the block's place in this view's grid of `grid` blocks (k_render_bwd: blockIdx.x, gridDim.x)
+__device__ __forceinline__ void render_bwd_block(const RenderBwdArgs& a, const uint32_t qi, const uint32_t grid) {
     // kept entries of a half-segment, compacted back to front, + a group of padding
     // (one array per field: four consecutive entries' field is one 16-B read, see bwd_quad)
     __shared__ __attribute__((aligned(16))) float s_x[kBwdHalf + kBwdGroup], s_y[kBwdHalf + kBwdGroup];
@@ -822,7 +823,6 @@ __global__ __launch_bounds__(64, GS_BWD_WAVES) void k_render_bwd(RenderBwdArgs a
     // total), the blocks take the lists one after another instead.  Blocks past the end exit (they
     // dispatch after every real item; see launch_render_backward for the grid).  (A persistent-wave
     // work queue measured slower than the hardware dispatcher here.)
-    const uint32_t qi = blockIdx.x;
     uint32_t region[kItemClasses], need = 0;
 #pragma unroll
     for (int c = 0; c < kItemClasses; ++c) {
@@ -831,7 +831,7 @@ __global__ __launch_bounds__(64, GS_BWD_WAVES) void k_render_bwd(RenderBwdArgs a
     }
     int list;
     uint32_t idx;
-    if (need <= gridDim.x) {
+    if (need <= grid) {
         if (qi >= need) return;
         uint32_t o = qi;
         int c = 0;
@@ -1024,12 +1024,57 @@ __global__ __launch_bounds__(64, GS_BWD_WAVES) void k_render_bwd(RenderBwdArgs a
     }
 }
 
+__global__ __launch_bounds__(64, GS_BWD_WAVES) void k_render_bwd(RenderBwdArgs a) {
+    render_bwd_block(a, blockIdx.x, gridDim.x);
+}
+
+// Several views' replays in one launch (one stream: no fork to the views' streams and no join back
+// before the per-Gaussian pass — each such cross-stream hop cost ~10 us of queue time on the box,
+// tools/probes/queue_gap.hip).  The views' grids are interleaved in runs of 8 blocks: block b is block
+// 8 i + (b & 7) of view (b >> 3) % n, i = (b >> 3) / n — so b & 7, the XCD under the round-robin dealing
+// that each view's item lists are grouped by, is the block's XCD in its own view's grid too, and every
+// view's heaviest items dispatch first.  A view's grid is m.grid[v] blocks (a multiple of 8), not its
+// item bound: the bound (~7x the real items at c2) dealt from ONE queue made the surplus workgroups'
+// dispatch outlast the replay (3 x 147k blocks: the step +43 us against three launches on three
+// queues); a block takes items qi, qi + grid, ... below the lists' need (once at c2), so any count is
+// replayed.
+__global__ __launch_bounds__(64, 4) void k_render_bwd_views(RenderBwdViews m) {  // (4: the item loop spilled at 96 VGPRs)
+    const uint32_t u = blockIdx.x >> 3, v = u % (uint32_t)m.n;
+    const RenderBwdArgs& a = m.v[v];
+    const uint32_t grid = m.grid[v];
+    const uint32_t q0 = (u / (uint32_t)m.n) * 8 + (blockIdx.x & 7u);
+    if (q0 >= grid) return;
+    uint32_t need = 0;
+#pragma unroll
+    for (int c = 0; c < kItemClasses; ++c) need += kItemXcds * a.bwd_count[item_max_at(c)];
+    const uint32_t lim = need < a.item_cap ? need : a.item_cap;  // (past it every block exits at once)
+    for (uint32_t qi = q0; qi < lim; qi += grid) render_bwd_block(a, qi, a.item_cap);
+}
+
 // One workgroup per possible item (the bound, 4 x checkpoint slots, is ~7x the c2 count): the surplus
 // workgroups exit at once and cost nothing measurable (render_bwd 104 us either way).
 void launch_render_backward(const RenderBwdArgs& a, hipStream_t s) {
     const int tiles = a.gx * a.gy;
     if (tiles <= 0 || a.item_cap == 0) return;
     hipLaunchKernelGGL(k_render_bwd, dim3(a.item_cap), dim3(64), 0, s, a);
+}
+
+void launch_render_backward_views(const RenderBwdArgs* a, int n, uint32_t grid_div, hipStream_t s) {
+    if (grid_div < 1) grid_div = 1;
+    for (int v0 = 0; v0 < n; v0 += kMaxReplayViews) {
+        RenderBwdViews m;
+        m.n = std::min(kMaxReplayViews, n - v0);
+        uint32_t runs = 0;  // the longest view grid, in runs of 8 blocks
+        for (int v = 0; v < m.n; ++v) {
+            m.v[v] = a[v0 + v];
+            const uint32_t cap = a[v0 + v].item_cap;
+            m.grid[v] = 8 * ((cap / grid_div + 7) / 8);
+            if (m.grid[v] == 0 && cap > 0) m.grid[v] = 8;
+            runs = std::max(runs, m.grid[v] / 8);
+        }
+        if (runs == 0) continue;
+        hipLaunchKernelGGL(k_render_bwd_views, dim3(8 * m.n * runs), dim3(64), 0, s, m);
+    }
 }
 
 }  // namespace gs

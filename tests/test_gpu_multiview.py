@@ -240,6 +240,52 @@ def test_render_views_batched_matches_per_view_loop(cuda_device, V, speculate):
             np.testing.assert_array_equal(got[k], ref[k], err_msg=f"{k} (repeat {rep})")
 
 
+@pytest.mark.parametrize("merge", ["1", "0", "loop", "side"])
+def test_merged_replay_matches_per_view_loop(cuda_device, monkeypatch, merge):
+    """Five views on three streams: the backward's replays as ONE launch on the caller's stream per four
+    views (k_render_bwd_views: 4 + 1, the views' grids interleaved; DGE_AMD_REPLAY_MERGE=1, the default),
+    the same with grids of 8 blocks per view so that every block loops over its items one grid apart
+    ("loop": DGE_AMD_REPLAY_GRID_DIV), or one launch per view on the views' streams (=0), then the
+    per-Gaussian passes in chunks — every output bitwise the per-view loop's.  "side": three views, the
+    merged replay with the live-set pass on a view stream beside it (DGE_AMD_LIVE_SIDE=1)."""
+    from dge_amd.cameras import orbit_camera
+    from dge_amd.gaussian_renderer import PipelineParams, render
+    from dge_amd.multiview import render_views
+    from dge_amd.scene import synthetic_scene
+
+    monkeypatch.setenv("DGE_AMD_REPLAY_MERGE", "0" if merge == "0" else "1")
+    if merge == "loop":
+        monkeypatch.setenv("DGE_AMD_REPLAY_GRID_DIV", "1000000")
+    monkeypatch.setenv("DGE_AMD_LIVE_SIDE", "1" if merge == "side" else "0")
+    dev = torch.device("cuda")
+    W, H, V = 288, 224, 3 if merge == "side" else 5
+    cams = [orbit_camera(k, 7, W, H, device=dev) for k in range(V)]
+    g = torch.Generator().manual_seed(9)
+    seeds = [(torch.randn(3, H, W, generator=g) * 1e-3).to(dev) for _ in range(V)]
+
+    def collect(outs, sc):
+        torch.cuda.synchronize()
+        res = {f"{k}{i}": o[k].detach().cpu().numpy() for i, o in enumerate(outs) for k in ("render", "radii")}
+        res.update({f"vs{i}": o["viewspace_points"].grad.cpu().numpy() for i, o in enumerate(outs)})
+        res.update({f"p{i}": p.grad.cpu().numpy() for i, p in enumerate(sc.parameters())})
+        return res
+
+    sc = synthetic_scene(120_000, sh_degree=3, seed=5, device=dev).requires_grad_(True)
+    outs = []
+    for c, s in zip(cams, seeds):
+        o = render(c, sc, PipelineParams(), torch.zeros(3, device=dev))
+        o["render"].backward(s)
+        outs.append(o)
+    ref = collect(outs, sc)
+    sc = synthetic_scene(120_000, sh_degree=3, seed=5, device=dev).requires_grad_(True)
+    outs = render_views(cams, sc, PipelineParams(), torch.zeros(3, device=dev), streams=3, speculate=True)
+    torch.autograd.backward([o["render"] for o in outs], seeds)
+    assert outs.check()
+    got = collect(outs, sc)
+    for k in ref:
+        np.testing.assert_array_equal(got[k], ref[k], err_msg=f"{k} (merge={merge})")
+
+
 def test_render_views_speculated_overflow_is_reported(cuda_device):
     """A batch whose instance count outgrows the speculated capacity (the history of this image size holds
     a far smaller scene of the same Gaussian count) is reported by check(); rendered again, it fits and
