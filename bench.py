@@ -292,7 +292,9 @@ def main():
     main_stream = torch.cuda.current_stream(dev)
     # per-step timing: one timing event on the main stream after each step (every view stream and the
     # backward join it there) and the host clock when each step's issue returns
-    evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
+    # (fence-free timing events, gs_timer_*: a torch event's record flushes the L2 for the host — a marker
+    # in the caller's queue between a step's last gradient writes and the next step's first kernel)
+    evs = [_native.StepTimer() for _ in range(args.steps + 1)]
     host_t = []
     wait0 = _native.lib().gs_host_wait_ns()
     t0 = time.perf_counter()
@@ -307,7 +309,7 @@ def main():
         dist.barrier()
     dt = time.perf_counter() - t0
     host_wait_s = (_native.lib().gs_host_wait_ns() - wait0) * 1e-9
-    step_ms = [evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps)]
+    step_ms = [evs[i].elapsed_ms(evs[i + 1]) for i in range(args.steps)]
     # the packed SUM (gather, RCCL all-reduce, scatter) on the main stream behind each step's backward
     coll_ms = [a.elapsed_time(b) for a, b in coll_evs]
     host_ms = [1e3 * (b - a) for a, b in zip([t0] + host_t[:-1], host_t)]
@@ -494,18 +496,18 @@ def run_views(args, cams, scene, pipe, bg, seeds, bucket, streams=None, min_worl
         # the bucket's fill runs on the first view's stream behind that view's forward, beside the others'
         # (only the backward's gradient writes wait for it: GradBucket.zero(stream=...))
         side = streams > 1 and not args.serial_zero
-        if side:
-            main = torch.cuda.current_stream()
-            ready = main.record_event()
-        else:
+        if not side:
             bucket.zero()
         outs = render_views(cams, scene, pipe, bg, streams=streams, speculate=args.speculate)
         if side:
             from dge_amd.multiview import view_streams
 
             # (zero() first runs the previous step's deferred union check, its forwards done by now; a fix-up
-            # it enqueues writes the bucket, so the fill then also waits for it)
-            bucket.zero(stream=view_streams(main.device, streams)[1], after=ready)
+            # it enqueues writes the bucket, so the fill then also waits for it.)  The view stream already waits
+            # for everything the caller's stream held before this step (the forward's fork: the previous step's
+            # gradient writes), so the fill needs no event of its own there — one system-fenced marker less in
+            # the caller's queue per step
+            bucket.zero(stream=view_streams(torch.cuda.current_stream().device, streams)[1])
         if attempt == 0 and min_world is not None and not args.scan_live:
             # (the union's MAX also carries this batch's overflow flag: a re-render below is agreed on)
             bucket.allreduce_begin([o.get("_live_rows") for o in outs], min_world=min_world, views=outs)

@@ -196,6 +196,10 @@ SIGNATURES = {
     "gs_host_wait_ns": (ctypes.c_longlong, []),
     "gs_profile_diag_enable": (ctypes.c_int, [ctypes.c_int]),
     "gs_profile_diag_read": (ctypes.c_longlong, [ctypes.c_int, ctypes.POINTER(ctypes.c_uint64), ctypes.c_longlong]),
+    "gs_timer_create": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p)]),
+    "gs_timer_record": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    "gs_timer_elapsed_ms": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_float)]),
+    "gs_timer_destroy": (ctypes.c_int, [ctypes.c_void_p]),
     "gs_adam_step": (ctypes.c_int, [ctypes.POINTER(AdamSegment), ctypes.c_int, ctypes.c_double, ctypes.c_double,
                                     ctypes.c_float, ctypes.c_void_p]),
     "gs_rows_live": (ctypes.c_int, [ctypes.POINTER(RowsRegion), ctypes.c_int, ctypes.c_longlong, ctypes.c_void_p,
@@ -278,6 +282,27 @@ def require_gpu(t) -> None:
         _gpu_ok = True
     if not getattr(t, "is_cuda", False):
         raise NativeError("dge_amd: tensors must live on the GPU")
+
+
+class StepTimer:
+    """A timing event without the system-scope fence (gs_timer_*): record(stream), elapsed_ms(end)."""
+
+    def __init__(self):
+        h = ctypes.c_void_p(None)
+        check(lib().gs_timer_create(ctypes.byref(h)), "gs_timer_create")
+        self.h = h.value
+
+    def record(self, stream) -> None:
+        check(lib().gs_timer_record(self.h, stream.cuda_stream), "gs_timer_record")
+
+    def elapsed_ms(self, end: "StepTimer") -> float:
+        ms = ctypes.c_float()
+        check(lib().gs_timer_elapsed_ms(self.h, end.h, ctypes.byref(ms)), "gs_timer_elapsed_ms")
+        return float(ms.value)
+
+    def __del__(self):
+        if getattr(self, "h", None) and _lib is not None:
+            _lib.gs_timer_destroy(self.h)
 
 
 def profile_enable(on: bool = True) -> None:

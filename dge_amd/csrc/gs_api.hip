@@ -26,6 +26,7 @@
 #include <atomic>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -96,14 +97,33 @@ bool region_emission(int gx, int gy) {
     return region_emission_grid(gx, gy) && !tile_sort_unfused() && e && !strcmp(e, "region");
 }
 
-// Pinned read-back slot of one forward's preprocess counters + its event.  A
-// pool per device: several forwards may be between begin and end at once
-// (gs_rasterize_forward_begin / _end), each holding its own slot.
+// Pinned (coherent) read-back slot of one forward's preprocess counters, written by the depth sort's first
+// kernel (CountPublish) and followed by its sequence word, which the host polls.  A pool per device: several
+// forwards may be between begin and end at once (gs_rasterize_forward_begin / _end), each holding its own slot.
+constexpr int kStagingWords = kCounterSlots * kCounterStride + 16;  // counters, the sequence word, padding
 struct Staging {
     uint32_t* host = nullptr;
-    hipEvent_t ev = nullptr;
+    uint32_t* dev_view = nullptr;  // the device's address of `host`
+    uint32_t seq = 0;              // the value this slot's publication ends with
     int dev = 0;
 };
+std::atomic<uint32_t> g_staging_seq{0};
+
+// Wait (host) until the slot's publication has landed: its sequence word equals s->seq.  A forward's
+// publication always comes (the depth sort runs for every P > 0); the bound only turns a lost device into an
+// error instead of a hang.
+bool staging_wait(const Staging* s) {
+    const volatile uint32_t* w = s->host + kCounterSlots * kCounterStride;
+    if (*w == s->seq) return true;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (unsigned spin = 0;; ++spin) {
+        if (*w == s->seq) return true;
+        if ((spin & 1023u) == 1023u) {
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(60)) return false;
+            std::this_thread::yield();
+        }
+    }
+}
 struct StagingPool {
     std::mutex mu;
     std::unordered_map<int, std::vector<Staging*>> free;
@@ -128,20 +148,37 @@ int staging_acquire(Staging** out) {
     }
     Staging* s = new Staging();
     s->dev = dev;
-    if (hipHostMalloc((void**)&s->host, 4 * kCounterSlots * kCounterStride, hipHostMallocDefault) != hipSuccess ||
-        hipEventCreateWithFlags(&s->ev, hipEventDisableTiming) != hipSuccess) {
+    if (hipHostMalloc((void**)&s->host, 4 * kStagingWords, hipHostMallocCoherent) != hipSuccess) {
         delete s;
         return set_error(GS_ERR_HIP, "could not create the counter read-back slot");
+    }
+    memset(s->host, 0, 4 * kStagingWords);
+    if (hipHostGetDevicePointer((void**)&s->dev_view, s->host, 0) != hipSuccess) {
+        (void)hipHostFree(s->host);
+        delete s;
+        return set_error(GS_ERR_HIP, "could not map the counter read-back slot");
     }
     *out = s;
     return GS_OK;
 }
 
+// the slot's next publication: a sequence value no earlier use of the slot wrote (0 is never used)
+CountPublish staging_publish(Staging* s, const uint32_t* counters) {
+    uint32_t q = ++g_staging_seq;
+    if (q == 0) q = ++g_staging_seq;
+    s->seq = q;
+    CountPublish p;
+    p.src = counters;
+    p.dst = s->dev_view;
+    p.seq = q;
+    return p;
+}
+
 void staging_release(Staging* s, bool synced = false) {
     if (!s) return;
-    // a slot dropped before its forward's _end may still have the counters' D2H copy in flight:
-    // the next forward to take it must not see that late copy land over its own counters
-    if (!synced) (void)hipEventSynchronize(s->ev);
+    // a slot dropped before its forward's _end may still have its publication in flight:
+    // the next forward to take it must not see that late write land over its own counters
+    if (!synced) (void)staging_wait(s);
     StagingPool& p = staging_pool();
     std::lock_guard<std::mutex> g(p.mu);
     p.free[s->dev].push_back(s);
@@ -394,8 +431,9 @@ int bin_after_preprocess(FwdState& f, hipStream_t stream) {
     PreprocessArgs& pa = f.pa;
     int rc = staging_acquire(&f.st);
     if (rc) return rc;
-    GS_HIP(hipMemcpyAsync(f.st->host, counters, 4 * kCounterSlots * kCounterStride, hipMemcpyDeviceToHost, stream));
-    GS_HIP(hipEventRecord(f.st->ev, stream));
+    // (read back by the depth sort's first kernel: against the round-5 D2H copy + event, c2 3217-3243 vs
+    // 3208-3230 renders/s and the host's busy time per step 0.46-0.55 vs 0.56-0.68 ms, profiles/r06/queues/)
+    const CountPublish pub = staging_publish(f.st, counters);
 
     // depth order of the Gaussians (stable: ties keep index order), any key range: MSD buckets + local sorts
     int cur = 0;
@@ -403,7 +441,7 @@ int bin_after_preprocess(FwdState& f, hipStream_t stream) {
     cur = depth_sort_msd(at<uint32_t>(geom, gl.key0), at<uint32_t>(geom, gl.key1), at<uint2>(geom, gl.val0),
                          at<uint2>(geom, gl.val1), pa.rect, (uint32_t)P, at<uint32_t>(geom, gl.sort_hist),
                          at<uint32_t>(geom, gl.sort_totals), gl.sort_blocks, at<uint2>(geom, gl.msd_ranges),
-                         counters + 2, stream); }
+                         counters + 2, stream, pub); }
     GS_LAUNCHED("depth sort");
 
     EmitArgs& ea = f.ea;
@@ -486,7 +524,8 @@ struct Counts {
 int read_counts(FwdState& f, Counts& c) {
     Staging* st = f.st;
     const auto t0 = std::chrono::steady_clock::now();
-    GS_HIP(hipEventSynchronize(st->ev));
+    if (!staging_wait(st)) return set_error(GS_ERR_HIP, "the preprocess counters were not published within 60 s");
+    std::atomic_thread_fence(std::memory_order_acquire);
     g_host_wait_ns.fetch_add(
         (long long)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count(),
         std::memory_order_relaxed);
@@ -825,6 +864,29 @@ uint64_t* diag_buffer(int which, size_t n_u64) {
 extern "C" {
 
 const char* gs_last_error(void) { return g_last_error.c_str(); }
+
+int gs_timer_create(void** event) {
+    if (!event) return set_error(GS_ERR_INVALID_ARG, "gs_timer_create: event is required");
+    hipEvent_t e = nullptr;
+    GS_HIP(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
+    *event = e;
+    return GS_OK;
+}
+int gs_timer_record(void* event, gs_stream_t stream) {
+    if (!event) return set_error(GS_ERR_INVALID_ARG, "gs_timer_record: event is required");
+    GS_HIP(hipEventRecord((hipEvent_t)event, (hipStream_t)stream));
+    return GS_OK;
+}
+int gs_timer_elapsed_ms(void* start, void* end, float* ms) {
+    if (!start || !end || !ms) return set_error(GS_ERR_INVALID_ARG, "gs_timer_elapsed_ms: start, end and ms are required");
+    GS_HIP(hipEventSynchronize((hipEvent_t)end));
+    GS_HIP(hipEventElapsedTime(ms, (hipEvent_t)start, (hipEvent_t)end));
+    return GS_OK;
+}
+int gs_timer_destroy(void* event) {
+    if (event) GS_HIP(hipEventDestroy((hipEvent_t)event));
+    return GS_OK;
+}
 
 int gs_profile_diag_enable(int on) {
     diag().on.store(on != 0);

@@ -303,9 +303,18 @@ int radix_sort_aux(uint32_t* key0, uint32_t* key1, uint2* pair0, uint2* pair1, c
 // The depth order (depth bits, index) of the P Gaussians for any key range: one stable 11-bit MSD pass
 // into depth buckets (keys relative to the visible minimum, read with the range from the preprocess counters
 // at bias_not) and a per-bucket local sort; the (rect, Gaussian) values end in pair0 (returns 0).
+// The preprocess counters published to the host by the depth sort's first kernel (block 0, at its end): the
+// kCounterSlots x kCounterStride words at src copied to dst (pinned host memory, device view), then after a
+// system-scope fence the word dst[kCounterSlots * kCounterStride] = seq — the host polls that word instead of
+// an event behind a D2H copy (the copy and the fenced marker cost each view's sort chain ~13 us of queue time)
+struct CountPublish {
+    const uint32_t* src = nullptr;
+    uint32_t* dst = nullptr;
+    uint32_t seq = 0;
+};
 int depth_sort_msd(uint32_t* key0, uint32_t* key1, uint2* pair0, uint2* pair1, const uint32_t* rect, uint32_t n,
                    uint32_t* hist, uint32_t* totals, int nblocks, uint2* bucket_ranges, const uint32_t* bias_not,
-                   hipStream_t s);
+                   hipStream_t s, CountPublish pub = CountPublish{});
 int tile_sort(uint32_t* key0, uint32_t* key1, uint2* pair0, uint2* pair1, const uint32_t* gauss_by_slot, uint32_t n,
               int bits, uint32_t* hist, uint32_t* totals, int nblocks, hipStream_t s, uint2* ranges,
               uint32_t* tile_order, int ntiles,  // tile_order: the forward's dispatch order (single pass only)

@@ -175,7 +175,7 @@ template <int BITS, int IPT, class KT = uint32_t, bool DM = false>
 __global__ __launch_bounds__(256) void k_radix_hist(const KT* __restrict__ keys, uint32_t n, int shift,
                                                     uint32_t* __restrict__ hist, int nb, int bm,
                                                     const uint32_t* __restrict__ bias_not,
-                                                    const uint32_t* __restrict__ n_dev) {
+                                                    const uint32_t* __restrict__ n_dev, CountPublish pub) {
     constexpr int NDIG = 1 << BITS;
     __shared__ uint32_t cnt[NDIG];
     const int tid = threadIdx.x;
@@ -217,6 +217,13 @@ __global__ __launch_bounds__(256) void k_radix_hist(const KT* __restrict__ keys,
     }
     __syncthreads();
     for (int d = tid; d < NDIG; d += 256) hist[hist_at(bm, blockIdx.x, d, nb, NDIG)] = cnt[d];
+    if (pub.dst && blockIdx.x == 0) {  // (CountPublish: vector stores, the sequence word last)
+        for (int i = tid; i < kCounterSlots * kCounterStride; i += 256) pub.dst[i] = pub.src[i];
+        __threadfence_system();
+        __syncthreads();
+        if (tid == 0) __hip_atomic_store(pub.dst + kCounterSlots * kCounterStride, pub.seq, __ATOMIC_RELEASE,
+                                         __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 }
 
 // Exclusive scan of every digit's column hist[0..nb)[d] in place, totals[d] =
@@ -604,7 +611,7 @@ static void radix_pass(const uint32_t* kin, const void* vin, uint32_t* kout, voi
     constexpr int NDIG = 1 << BITS;
     const int bm = nb <= kScanBmRows ? 1 : 0;
     hipLaunchKernelGGL((k_radix_hist<BITS, IPT>), dim3(nb), dim3(256), 0, s, kin, n, shift, hist, nb, bm, bias_not,
-                       n_dev);
+                       n_dev, CountPublish{});
     if (bm)
         hipLaunchKernelGGL(k_radix_digit_scan, dim3(div_up(NDIG, kScanDigits)), dim3(kScanThreads), 0, s, hist, nb, NDIG,
                            totals, n_dev, n, 256 * IPT);
@@ -864,13 +871,13 @@ __global__ __launch_bounds__(256) void k_depth_bucket_sort(uint32_t* __restrict_
 
 int depth_sort_msd(uint32_t* key0, uint32_t* key1, uint2* pair0, uint2* pair1, const uint32_t* rect, uint32_t n,
                    uint32_t* hist, uint32_t* totals, int nblocks, uint2* bucket_ranges, const uint32_t* bias_not,
-                   hipStream_t s) {
+                   hipStream_t s, CountPublish pub) {
     if (n == 0) return 0;
     constexpr int IPT = kMsdIPT, NDIG = kMsdBuckets;
     nblocks = (int)div_up_u(n, 256u * IPT);  // (<= the table's rows: sized for kDepthSortTile-key blocks)
     const int bm = nblocks <= kScanBmRows ? 1 : 0;
     hipLaunchKernelGGL((k_radix_hist<kMsdBits, IPT, uint32_t, true>), dim3(nblocks), dim3(256), 0, s, key0, n, 0, hist,
-                       nblocks, bm, bias_not, (const uint32_t*)nullptr);
+                       nblocks, bm, bias_not, (const uint32_t*)nullptr, pub);
     if (bm)
         hipLaunchKernelGGL(k_radix_digit_scan, dim3(div_up(NDIG, kScanDigits)), dim3(kScanThreads), 0, s, hist, nblocks, NDIG,
                            totals, (const uint32_t*)nullptr, n, 256 * IPT);
@@ -1913,7 +1920,7 @@ void launch_row_pass(const EmitArgs& a, uint32_t K, uint2* point_pairs, uint32_t
     const int nb = (int)div_up_u(K, (uint32_t)TILE), bm = nb <= kScanBmRows ? 1 : 0;
     (void)sort_blocks;
     hipLaunchKernelGGL((k_radix_hist<kXBits, IPT, uint16_t>), dim3(nb), dim3(256), 0, s, keys, K, kXBits, hist, nb,
-                       bm, (const uint32_t*)nullptr, n_dev);
+                       bm, (const uint32_t*)nullptr, n_dev, CountPublish{});
     if (bm)
         hipLaunchKernelGGL(k_radix_digit_scan, dim3(div_up(NDIG, kScanDigits)), dim3(kScanThreads), 0, s, hist, nb, NDIG,
                            a.xtotals, n_dev, K, TILE);

@@ -389,10 +389,20 @@ def _order_grad_writes_begin(dev):
     backward itself right before its per-Gaussian pass (gs_grads.writes_after), so this view's gradient
     replay still overlaps the previous view's gradient writes on the other stream."""
     cur = torch.cuda.current_stream(dev)
+    return cur, grad_writes_event(dev, cur)
+
+
+def grad_writes_event(dev, cur):
+    """The event `cur`'s .grad writes must wait for: the last gradient writer's, when it was another stream,
+    else None.  A writer may leave its event unrecorded (None: views' batched backward, whose stream is then
+    recorded here, on demand — after everything enqueued on it so far, a superset of its gradient writes), so
+    a step whose next writer is on the same stream puts no event (a system-fenced marker) in its queue."""
     last = _GRAD_WRITES.get(dev.index)
-    if last is not None and last[0] != cur:
-        return cur, last[1]
-    return cur, None
+    if last is None or last[0] == cur:
+        return None
+    if last[1] is None:
+        last = _GRAD_WRITES[dev.index] = (last[0], last[0].record_event())
+    return last[1]
 
 
 def _order_grad_writes_end(dev, cur, fresh):

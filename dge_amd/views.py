@@ -246,15 +246,15 @@ class _RasterizeViews(torch.autograd.Function):
                 o.mask_bits = mask_bits
             gg.append(o)
         stream = torch.cuda.current_stream(dev)
-        last = _R._GRAD_WRITES.get(dev.index)
-        after = last[1].cuda_event if last is not None and last[0] != stream else None
+        ev = _R.grad_writes_event(dev, stream)
+        after = ev.cuda_event if ev is not None else None
         dp = (ctypes.c_void_p * n)(*[g.data_ptr() for g in gpix])
         go = (ctypes.c_void_p * n)(*[ctypes.addressof(o) for o in gg])
         st_arr = (ctypes.c_void_p * n)(*[st.cuda_stream for st in ctx.meta["streams"]])
         rc = N.lib().gs_views_backward(batch.handle, dp, go, st_arr, after, stream.cuda_stream)
         N.check(rc, "render_views backward")
         if _R._SIDE_STREAMS:  # later backward calls on other streams order their .grad writes after these
-            _R._GRAD_WRITES[dev.index] = (stream, stream.record_event())
+            _R._GRAD_WRITES[dev.index] = (stream, None)  # (the event recorded by the next writer that needs it)
         for p, t in direct:
             p.grad = t
         colors_grad = None if ctx.has_sh else targets.get("colors")

@@ -462,6 +462,14 @@ long long gs_host_wait_ns(void);
 int gs_profile_diag_enable(int on);
 long long gs_profile_diag_read(int which, uint64_t *host, long long max_u64);
 
+/* Step timer (bench.py's per-step GPU times): timing events without the system-scope fence — a record is a
+ * marker in the stream's queue that writes back nothing for the host (a fenced one flushes the L2 the step's
+ * gradient writes just dirtied).  gs_timer_elapsed_ms waits for `end`.  (Not in the reference's API.) */
+int gs_timer_create(void **event);
+int gs_timer_record(void *event, gs_stream_t stream);
+int gs_timer_elapsed_ms(void *start, void *end, float *ms);
+int gs_timer_destroy(void *event);
+
 /* Test hook: the blend's exp (forward.cu:345 `exp(power)`) over n floats on the
  * device, evaluated exactly as the blend kernels do (packed pairs); bit-identical
  * to the oracle's gs_expf.  Returns GS_OK or an error code. */

@@ -711,10 +711,8 @@ def test_c2_timed_path_matches_per_view_loop(cuda_device, oracle):
     ref["bucket"] = bucket.flat.clone()
     del ref_outs
     for rep in range(2):
-        main = torch.cuda.current_stream(dev)
-        ready = main.record_event()
         outs = render_views(cams, sc, PipelineParams(), bg, streams=3, speculate=True)
-        bucket.zero(stream=view_streams(dev, 3)[1], after=ready)
+        bucket.zero(stream=view_streams(dev, 3)[1])  # (as bench.py: the view stream waits for the fork)
         torch.autograd.backward([o["render"] for o in outs], seeds)
         assert outs.check()
         torch.cuda.synchronize()
