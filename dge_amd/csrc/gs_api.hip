@@ -385,7 +385,9 @@ int bin_prepare_in(FwdState& f, int copy_colors, void* geom, void* img, hipStrea
     f.img = img;
 
     uint32_t* counters = at<uint32_t>(img, il.counters);
-    GS_HIP(hipMemsetAsync(counters, 0, il.total - il.counters, stream));  // counters, ranges, tile_last, ...
+    static_assert(kAlign % 16 == 0, "whole 16-B stores");
+    launch_zero16(counters, il.total - il.counters, stream);  // counters, ranges, tile_last, ...
+    { const bool debug = s->debug != 0; GS_LAUNCHED("zero image state"); }
 
     PreprocessArgs& pa = f.pa;
     pa.P = P; pa.D = s->sh_degree; pa.M = gp.M; pa.W = g.W; pa.H = g.H; pa.gx = g.gx; pa.gy = g.gy;

@@ -280,6 +280,7 @@ struct PreprocessArgs {
     const uint8_t* aux_mask = nullptr;  // gs_params.aux_mask: the sign of the Splat's depth
 };
 void launch_preprocess(const PreprocessArgs& a, hipStream_t s);
+void launch_zero16(void* p, size_t bytes, hipStream_t s);  // bytes: a multiple of 16, p 16-B aligned
 void launch_depth_keys32(int P, const uint32_t* rect, const Splat* splat, uint32_t* key, hipStream_t s);
 void launch_mark_visible(int P, const float* means3D, const float* view, uint8_t* present, hipStream_t s);
 // (test hook gs_activate_params) the fused path's in-kernel activations over P rows

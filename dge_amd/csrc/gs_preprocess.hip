@@ -280,6 +280,19 @@ __global__ __launch_bounds__(256) void k_preprocess(PreprocessArgs a) {
     }
 }
 
+// The image buffer's per-forward state (counters, ranges, tile windows, work-list counts: ~30 KB at 512^2)
+// zeroed before the preprocess: 16-B stores, one per thread.  (hipMemsetAsync's fill kernel took 7-8 us for it
+// at the head of every view's chain, against ~2 us.)
+__global__ __launch_bounds__(256) void k_zero16(uint4* __restrict__ p, uint32_t n16) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i < n16) p[i] = make_uint4(0u, 0u, 0u, 0u);
+}
+
+void launch_zero16(void* p, size_t bytes, hipStream_t s) {
+    const uint32_t n16 = (uint32_t)(bytes / 16);
+    if (n16) hipLaunchKernelGGL(k_zero16, dim3(div_up(n16, 256)), dim3(256), 0, s, static_cast<uint4*>(p), n16);
+}
+
 void launch_preprocess(const PreprocessArgs& a, hipStream_t s) {
     if (a.P <= 0) return;
     if (a.sh.half || a.index)  // (the one-pass staging needs the block's rows contiguous)
