@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define GS_RASTER_ABI_VERSION 19
+#define GS_RASTER_ABI_VERSION 20
 
 #define GS_OK 0
 #define GS_ERR_INVALID_ARG 1   /* AT_ERROR / std::runtime_error in the reference */
@@ -464,7 +464,7 @@ long long gs_profile_diag_read(int which, uint64_t *host, long long max_u64);
 
 /* Step timer (bench.py's per-step GPU times): timing events without the system-scope fence — a record is a
  * marker in the stream's queue that writes back nothing for the host (a fenced one flushes the L2 the step's
- * gradient writes just dirtied).  gs_timer_elapsed_ms waits for `end`.  (Not in the reference's API.) */
+ * gradient writes just dirtied).  gs_timer_elapsed_ms waits for `end`.  (Not in the reference's API; ABI 20.) */
 int gs_timer_create(void **event);
 int gs_timer_record(void *event, gs_stream_t stream);
 int gs_timer_elapsed_ms(void *start, void *end, float *ms);
