@@ -18,9 +18,6 @@
 // (num_rendered, radii, sorted tile lists) are identical, not just close.
 // These kernels are HBM-bound; the extra multiplies cost nothing measurable.
 #pragma clang fp contract(off)
-#include <stdlib.h>
-#include <string.h>
-
 #include "gs_common.h"
 #include "gs_internal.h"
 #include "gs_raster.h"  // GS_ACC_*
@@ -783,265 +780,6 @@ __global__ __launch_bounds__(kGB) void k_gauss_bwd_live(GaussBwdViews m) {
     }
 }
 
-// One batch of (Gaussian, view) pairs (k_gauss_bwd_mixed): bwd_view_batch with a view per thread.
-__device__ __forceinline__ void bwd_mixed_batch(const GaussBwdViews& m, bool ok, int idx, int src, int view,
-                                                uint32_t round, uint32_t nrounds, uint32_t zeroed, int nrow, int ncol,
-                                                float inv_ncol, float* s_sh, uint32_t* s_gid, uint8_t* s_shacc,
-                                                uint8_t* s_round) {
-    const GaussBwdArgs& a = m.v[view];  // this thread's view (the cameras, geometry, records, per-view outputs)
-    const GaussBwdArgs& a0 = m.v[0];   // the batch's scene: the SH rows in and their gradients out
-    float* const my_sh = s_sh + threadIdx.x * kShPitch;
-    const bool vfirst = round == 0;
-    const uint32_t facc = a.acc & ~(vfirst ? zeroed : 0u);
-    s_round[threadIdx.x] = ok ? (uint8_t)round : (uint8_t)0xFF;
-    s_gid[threadIdx.x] = ok ? (uint32_t)src : kNoRow;  // (SH rows are parameter rows)
-    s_shacc[threadIdx.x] = (facc & GS_ACC_SH) ? 1 : 0;  // (the SH rows' read-modify-write, by row)
-    // independent loads first: parameters (a later view's from L2), slot range, the first 8 record flags
-    GaussIn gin{};
-    if (ok) gin = load_gauss_in(a, idx, src);
-    // (the grad-mask byte with the other inputs: read where it is used, it waited for itself alone)
-    // (no branch: without a mask the load reads the means' bytes, a valid address, and is ignored)
-    const uint32_t gmb_raw = (a.grad_mask ? a.grad_mask : reinterpret_cast<const uint8_t*>(a.means3D))[ok ? src : 0];
-    uint32_t n = ok ? a.tiles_touched[idx] : 0u;
-    const uint32_t first = ok ? a.first_slot[idx] : 0u;  // (a live Gaussian has slots)
-    // (a speculative forward that overflowed its capacity is re-rendered; its slots stop at the capacity)
-    n = first < a.slot_cap ? min(n, a.slot_cap - first) : 0u;
-    const uint32_t* flags = reinterpret_cast<const uint32_t*>(a.rec_flags);
-    uint32_t fl[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) fl[u] = (uint32_t)u < n ? flags[first + u] : 0u;
-    __syncthreads();  // s_gid
-    const int total = nrow * ncol;
-    constexpr int kV = 12;
-    if (a0.sh.dc && ncol > 0 && !a0.sh.half && ncol == kShPitch) {
-        // fp32 rows of the full pitch: the LDS image is the flat index itself, so each wave-instruction's
-        // 64 floats land contiguously — direct global->LDS loads (no registers, all in flight at once;
-        // the barrier below waits for them)
-        const uint32_t wave_base = __builtin_amdgcn_readfirstlane(threadIdx.x & ~63u);
-        for (int b = 0; b < total; b += kGB) {
-            const int e = b + (int)threadIdx.x;
-            if (e < total) {
-                const int row = (int)(((float)e + 0.5f) * inv_ncol), col = e - row * ncol;
-                const float* src = a0.sh.rest + (size_t)s_gid[row] * a0.sh.rest_stride + col;
-                __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)src,
-                                                 (__attribute__((address_space(3))) void*)(s_sh + b + wave_base), 4, 0, 0);
-            }
-        }
-    } else if (a0.sh.dc && ncol > 0) {
-        // (raw bits first, converted once the batch's loads are all issued: a conversion beside its load made
-        // each fp16 load wait in turn)
-        const bool half = a0.sh.half != 0;
-        for (int b = 0; b < total; b += kV * kGB) {
-            uint32_t v[kV];
-#pragma unroll
-            for (int u = 0; u < kV; ++u) {
-                const int e = b + u * kGB + (int)threadIdx.x;
-                const int row = (int)(((float)e + 0.5f) * inv_ncol), col = e - row * ncol;
-                const uint32_t gid = e < total ? s_gid[row] : kNoRow;
-                const size_t off = (size_t)gid * a0.sh.rest_stride + col;
-                v[u] = gid == kNoRow ? 0u
-                       : half ? (uint32_t)reinterpret_cast<const uint16_t*>(a0.sh.rest)[off]
-                              : __float_as_uint(a0.sh.rest[off]);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int u = 0; u < kV; ++u) {
-                const int e = b + u * kGB + (int)threadIdx.x;
-                const int row = (int)(((float)e + 0.5f) * inv_ncol), col = e - row * ncol;
-                if (e < total)
-                    s_sh[row * kShPitch + col] = half ? __half2float(__ushort_as_half((unsigned short)v[u]))
-                                                      : __uint_as_float(v[u]);
-            }
-        }
-    }
-    // sum of this Gaussian's records: one per (slot, quadrant) the backward
-    // replay kept, flagged per slot; slots in emission order = tile order,
-    // quadrants in order within a slot.  The flagged records are taken four at
-    // a time from a bit mask (bit 4u + quadrant), all twelve loads of a batch
-    // issued before its sums: one memory round trip per four records instead
-    // of one per record (a batch's unused places re-read its first record and
-    // add nothing; acc is never -0, so the skipped +0 changes no bit).
-    float acc[9];
-#pragma unroll
-    for (int f = 0; f < 9; ++f) acc[f] = 0.f;
-    for (uint32_t k0 = 0; k0 < n; k0 += 8) {
-        if (k0) {
-#pragma unroll
-            for (int u = 0; u < 8; ++u) fl[u] = k0 + u < n ? flags[first + k0 + u] : 0u;
-        }
-        uint32_t m = 0;
-#pragma unroll
-        for (int u = 0; u < 8; ++u)
-#pragma unroll
-            for (int qd = 0; qd < 4; ++qd) m |= ((fl[u] >> (8 * qd)) & 0xFFu) ? 1u << (4 * u + qd) : 0u;
-        const float4* recs = a.records + 3 * (4 * (size_t)(first + k0));
-        while (m) {
-            int bi[4];
-            bool use[4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                use[i] = m != 0u;
-                bi[i] = use[i] ? __builtin_ctz(m) : bi[0];
-                m &= m - 1u;
-            }
-            float4 r[4][3];
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-#pragma unroll
-                for (int c = 0; c < 3; ++c) r[i][c] = recs[3 * bi[i] + c];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                if (use[i]) {
-                    acc[0] += r[i][0].x; acc[1] += r[i][0].y; acc[2] += r[i][0].z; acc[3] += r[i][0].w;
-                    acc[4] += r[i][1].x; acc[5] += r[i][1].y; acc[6] += r[i][1].z; acc[7] += r[i][1].w;
-                    acc[8] += r[i][2].x;
-                }
-            }
-        }
-    }
-    __syncthreads();  // SH staged
-
-    float ddc[3] = {0.f, 0.f, 0.f};
-    float dop = acc[5];  // w.r.t. opacity; chained through the sigmoid when activation = 1
-    GaussOut o;
-    if (ok) {
-        const float gm = !a.grad_mask || gmb_raw ? 1.f : 0.f;
-        // (each thread reads and then overwrites only its own LDS row: no barrier in between)
-        gauss_bwd_visible(a, gin, acc, dop, my_sh, ncol, (a.mask_bits & GS_ACC_SH) ? gm : 1.f, ddc, o);
-        if (a.grad_mask) apply_grad_mask(a, gm, acc, dop, o);
-    }
-    // Commits in rounds: round r = how many of the Gaussian's live views come before this pair's view, so a
-    // Gaussian's views add into its shared gradients in view order, one barrier apart (the batch's pairs of
-    // one Gaussian are in distinct rounds; a pair in an earlier batch committed before this batch began)
-    for (uint32_t r = 0; r < nrounds; ++r) {
-        if (r) __syncthreads();  // (round r-1's stores before round r's read-modify-writes)
-        if (ok && round == r) commit_outputs(a, facc, idx, src, acc, dop, ddc, o);
-        // dL_dsh rest rows of this round: through LDS (in place), flat block-wide batches, loads before stores
-        if (a0.dsh.dc && ncol > 0) {
-            __syncthreads();
-            for (int b = 0; b < total; b += kV * kGB) {
-                float old[kV];
-#pragma unroll
-                for (int u = 0; u < kV; ++u) {
-                    const int e = b + u * kGB + (int)threadIdx.x;
-                    const int row = (int)(((float)e + 0.5f) * inv_ncol), col = e - row * ncol;
-                    const uint32_t gid = e < total && s_round[row] == r ? s_gid[row] : kNoRow;
-                    old[u] = gid != kNoRow && s_shacc[row] ? a0.dsh.rest[(size_t)gid * a0.dsh.rest_stride + col] : 0.f;
-                }
-#pragma unroll
-                for (int u = 0; u < kV; ++u) {
-                    const int e = b + u * kGB + (int)threadIdx.x;
-                    const int row = (int)(((float)e + 0.5f) * inv_ncol), col = e - row * ncol;
-                    const uint32_t gid = e < total && s_round[row] == r ? s_gid[row] : kNoRow;
-                    if (gid != kNoRow)
-                        a0.dsh.rest[(size_t)gid * a0.dsh.rest_stride + col] = old[u] + s_sh[row * kShPitch + col];
-                }
-            }
-        }
-    }
-    __syncthreads();  // s_gid / s_sh / s_round reused by the next batch
-}
-
-// The same pass with each batch's 256 threads taking (Gaussian, view) pairs of any view: the workgroup's union
-// entries are expanded chunk by chunk into one pair per live view (a Gaussian's pairs in view order, next to
-// each other), and a batch is the next 256 pairs — where the view-by-view form ran one latency-bound batch per
-// view (at c2 ~104 of 256 threads busy in each of 3), this runs ~1.2.  Every thread does its own view's work
-// (cameras, records, per-view outputs through m.v[v]); the shared gradients of a Gaussian live in several views
-// of one batch are committed in view order, one round per earlier live view (bwd_mixed_batch), so the sums are
-// bitwise the view-by-view pass's.
-// A pair: Gaussian | round << 28 | view << 30 (ids < 2^28; round: the Gaussian's live views before `view`)
-__device__ __forceinline__ uint32_t expand_pairs(const GaussBwdViews& m, uint32_t entry, bool in, uint32_t* s_vlist,
-                                                 uint32_t* s_wave, uint32_t filled, int lane, int wave) {
-    // appends this chunk's pairs (entry, v) for v in order; returns the new fill
-    for (int v = 0; v < m.n; ++v) {
-        const bool has = in && ((entry >> (28 + v)) & 1u);
-        const uint64_t bm = __ballot(has);
-        if (lane == 0) s_wave[wave] = (uint32_t)__popcll(bm);
-        __syncthreads();
-        uint32_t off = 0, nv = 0;
-#pragma unroll
-        for (int w = 0; w < kGB / 64; ++w) {
-            off += w < wave ? s_wave[w] : 0u;
-            nv += s_wave[w];
-        }
-        if (has) {
-            const uint32_t round = (uint32_t)__popc((entry >> 28) & ((1u << v) - 1u));
-            s_vlist[filled + off + (uint32_t)__popcll(bm & lanemask_lt())] =
-                (entry & kLiveIdMask) | round << 28 | (uint32_t)v << 30;
-        }
-        filled += nv;
-        __syncthreads();  // (s_wave read by every thread before its next write)
-    }
-    return filled;
-}
-
-__global__ __launch_bounds__(kGB) void k_gauss_bwd_mixed(GaussBwdViews m) {
-    const GaussBwdArgs& a = m.v[0];
-    __shared__ float s_sh[kGB * kShPitch];
-    __shared__ uint32_t s_gid[kGB];
-    __shared__ uint8_t s_shacc[kGB];
-    __shared__ uint8_t s_round[kGB];
-    __shared__ uint32_t s_pre[kLiveGroup + 1];
-    __shared__ uint32_t s_vlist[kGB + kGB * kMaxBwdViews];  // pairs pending: < kGB + one chunk's (<= n per entry)
-    __shared__ uint32_t s_wave[kGB / 64];
-    __shared__ uint32_t s_nr;
-    const int nsrc = (a.P + kGB - 1) / kGB;
-    const int group = (nsrc + kLiveGrid - 1) / kLiveGrid < kLiveGroup ? (nsrc + kLiveGrid - 1) / kLiveGrid : kLiveGroup;
-    const int sb0 = blockIdx.x * group;
-    if (threadIdx.x < kLiveGroup)
-        s_pre[threadIdx.x + 1] = (int)threadIdx.x < group && sb0 + (int)threadIdx.x < nsrc ? a.live_count[sb0 + threadIdx.x] : 0u;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        s_pre[0] = 0;
-#pragma unroll
-        for (int g = 1; g <= kLiveGroup; ++g) s_pre[g] += s_pre[g - 1];
-    }
-    __syncthreads();
-    const uint32_t count = s_pre[kLiveGroup];
-    const int ncol = (a.M - 1) * 3 < kShPitch ? (a.M - 1) * 3 : kShPitch;
-    const float inv_ncol = ncol > 0 ? 1.0f / (float)ncol : 0.f;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const auto load_entry = [&](uint32_t base) {
-        const uint32_t j = base + threadIdx.x;
-        int g = 0;
-#pragma unroll
-        for (int q = 1; q < kLiveGroup; ++q) g += j >= s_pre[q] ? 1 : 0;
-        return j < count ? a.live_list[(size_t)(sb0 + g) * kGB + (j - s_pre[g])] : 0u;
-    };
-    uint32_t filled = 0;
-    for (uint32_t base = 0; base < count; base += kGB) {
-        const bool in = base + threadIdx.x < count;
-        filled = expand_pairs(m, load_entry(base), in, s_vlist, s_wave, filled, lane, wave);
-        const bool last = base + kGB >= count;
-        while (filled >= (uint32_t)kGB || (last && filled > 0)) {
-            const uint32_t nb = filled < (uint32_t)kGB ? filled : (uint32_t)kGB;
-            const bool ok = threadIdx.x < nb;
-            const uint32_t ent = ok ? s_vlist[threadIdx.x] : 0u;
-            const int v = (int)(ent >> 30);
-            const uint32_t round = (ent >> 28) & 3u;
-            const int idx = (int)(ent & kLiveIdMask);
-            const int src = ok && a.index ? a.index[idx] : idx;
-            if (threadIdx.x == 0) s_nr = 0;
-            __syncthreads();
-            if (ok) atomicMax(&s_nr, round + 1);
-            __syncthreads();
-            const uint32_t nrounds = s_nr;
-            bwd_mixed_batch(m, ok, idx, src, v, round, nrounds, a.zeroed, (int)nb, ncol, inv_ncol, s_sh, s_gid, s_shacc,
-                            s_round);
-            // (bwd_mixed_batch ends on a barrier: every thread has read its pair) the rest to the front
-            const uint32_t rest = filled - nb;  // (block-uniform: the chunked copy's barriers are reached by all)
-            for (uint32_t c = 0; c * kGB < rest; ++c) {
-                const uint32_t t = c * kGB + threadIdx.x;
-                const uint32_t e = t < rest ? s_vlist[kGB + t] : 0u;
-                __syncthreads();  // (chunk c's reads before its writes over chunk c - 1's source)
-                if (t < rest) s_vlist[t] = e;
-            }
-            __syncthreads();
-            filled = rest;
-        }
-    }
-}
-
 static GaussBwdViews gauss_views(const GaussBwdArgs* views, int n) {
     GaussBwdViews m;
     m.n = n < kMaxBwdViews ? n : kMaxBwdViews;
@@ -1066,13 +804,7 @@ void launch_gauss_bwd_live_views(const GaussBwdArgs* views, int n, hipStream_t s
     if (writes_after) (void)hipStreamWaitEvent(s, writes_after, 0);
     const int blocks = div_up(views[0].P, kGB);
     const int group = std::min(div_up(blocks, kLiveGrid), kLiveGroup);  // (the kernel derives the same)
-    // DGE_AMD_GAUSS_MIX=1, several views: batches of (Gaussian, view) pairs (k_gauss_bwd_mixed); else (one view,
-    // the per-wave diagnostics, which the view-by-view kernel stamps) view by view
-    const char* e = getenv("DGE_AMD_GAUSS_MIX");
-    if (n > 1 && !views[0].diag && e && !strcmp(e, "1"))
-        hipLaunchKernelGGL(k_gauss_bwd_mixed, dim3(div_up(blocks, group)), dim3(kGB), 0, s, gauss_views(views, n));
-    else
-        hipLaunchKernelGGL(k_gauss_bwd_live, dim3(div_up(blocks, group)), dim3(kGB), 0, s, gauss_views(views, n));
+    hipLaunchKernelGGL(k_gauss_bwd_live, dim3(div_up(blocks, group)), dim3(kGB), 0, s, gauss_views(views, n));
 }
 
 void launch_gauss_backward_views(const GaussBwdArgs* views, int n, hipStream_t s, hipEvent_t writes_after) {
