@@ -105,6 +105,7 @@ struct Staging {
     uint32_t* host = nullptr;
     uint32_t* dev_view = nullptr;  // the device's address of `host`
     uint32_t seq = 0;              // the value this slot's publication ends with
+    bool armed = false;            // the kernel that publishes it was launched (else nothing will land)
     int dev = 0;
 };
 std::atomic<uint32_t> g_staging_seq{0};
@@ -178,7 +179,8 @@ void staging_release(Staging* s, bool synced = false) {
     if (!s) return;
     // a slot dropped before its forward's _end may still have its publication in flight:
     // the next forward to take it must not see that late write land over its own counters
-    if (!synced) (void)staging_wait(s);
+    if (!synced && s->armed) (void)staging_wait(s);
+    s->armed = false;
     StagingPool& p = staging_pool();
     std::lock_guard<std::mutex> g(p.mu);
     p.free[s->dev].push_back(s);
@@ -445,6 +447,7 @@ int bin_after_preprocess(FwdState& f, hipStream_t stream) {
                          at<uint32_t>(geom, gl.sort_totals), gl.sort_blocks, at<uint2>(geom, gl.msd_ranges),
                          counters + 2, stream, pub); }
     GS_LAUNCHED("depth sort");
+    f.st->armed = true;  // (a launch that failed above publishes nothing: its slot is released without a wait)
 
     EmitArgs& ea = f.ea;
     ea.P = P; ea.gx = g.gx; ea.gy = g.gy;
@@ -526,7 +529,8 @@ struct Counts {
 int read_counts(FwdState& f, Counts& c) {
     Staging* st = f.st;
     const auto t0 = std::chrono::steady_clock::now();
-    if (!staging_wait(st)) return set_error(GS_ERR_HIP, "the preprocess counters were not published within 60 s");
+    if (!st->armed || !staging_wait(st))
+        return set_error(GS_ERR_HIP, "the preprocess counters were not published (within 60 s)");
     std::atomic_thread_fence(std::memory_order_acquire);
     g_host_wait_ns.fetch_add(
         (long long)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count(),
