@@ -15,7 +15,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("DGE_AMD_LIB") or os.path.join(_HERE, "lib", "libgs_raster.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "gs_raster.h")
 
-ABI_VERSION = 20  # GS_RASTER_ABI_VERSION of include/gs_raster.h this binding is written against
+ABI_VERSION = 21  # GS_RASTER_ABI_VERSION of include/gs_raster.h this binding is written against
 
 
 def source_stamp() -> str:
@@ -144,7 +144,7 @@ class AdamSegment(ctypes.Structure):
 class RowsRegion(ctypes.Structure):
     """struct gs_rows_region (include/gs_raster.h)."""
 
-    _fields_ = [("base", ctypes.c_void_p), ("width", ctypes.c_int)]
+    _fields_ = [("base", ctypes.c_void_p), ("width", ctypes.c_int), ("pitch", ctypes.c_int)]
 
 
 ROWS_MAX_REGIONS = 8

@@ -8,7 +8,7 @@
 // nonzero on some rank.  These kernels are its bookkeeping, each one pass at the
 // HBM roofline instead of torch's per-tensor compare / any / index_select / cat /
 // index_copy chain (~680 us at c3 on one MI355X, tools/probes/bucket_cost.py):
-//   k_rows_live    live[r] = row r of some region has an element != 0   (reads 4·W·n B)
+//   k_rows_live    live[r] = row r of some region has an element != 0   (reads 4·pitch·n B)
 //   k_rows_gather  packed[i, :] = row rows[i] of every region           (4·W·m B each way)
 //   k_rows_scatter row rows[i] of every region = packed[i, :]
 #include "gs_internal.h"
@@ -19,20 +19,29 @@ namespace gs {
 struct RowsLaunch {
     int nreg, width;                               // regions, total floats per row
     float* base[GS_ROWS_MAX_REGIONS];
-    int w[GS_ROWS_MAX_REGIONS];
+    int w[GS_ROWS_MAX_REGIONS];                    // used columns of each region
+    int p[GS_ROWS_MAX_REGIONS];                    // its row stride (>= w)
     int col0[GS_ROWS_MAX_REGIONS + 1];             // first packed column of each region
 };
 
 constexpr int kRowsBlock = 256;  // rows per workgroup of k_rows_live
 
-// One workgroup per 256 rows: each region's rows [r0, r0 + nr) are one contiguous span, read
-// coalesced (float4 when the span is 16-B aligned, four in flight per thread); a nonzero element
-// marks its row in LDS (benign same-value stores).
+// One workgroup per 256 rows: each region's rows [r0, r0 + nr) are one contiguous span of pitch-wide
+// rows, read coalesced (float4 when the span is 16-B aligned, four in flight per thread); a nonzero
+// element of the first w columns marks its row in LDS (benign same-value stores).
 __device__ __forceinline__ int row_of(int j, int w, float inv_w) {
     int r = (int)((float)j * inv_w);  // exact after the correction: j < 2^24
     r -= (r * w > j);
     r += ((r + 1) * w <= j);
     return r;
+}
+
+// element j of the span: mark its row when it is nonzero (NaN counts, as torch's `!= 0`) and a used column
+__device__ __forceinline__ void mark_elem(uint32_t* flag, float v, int j, int p, float inv_p, int w) {
+    if (v != 0.f) {
+        const int r = row_of(j, p, inv_p);
+        if (p == w || j - r * p < w) flag[r] = 1u;
+    }
 }
 
 __global__ __launch_bounds__(kRowsBlock) void k_rows_live(RowsLaunch a, long long n, uint8_t* __restrict__ live) {
@@ -42,10 +51,10 @@ __global__ __launch_bounds__(kRowsBlock) void k_rows_live(RowsLaunch a, long lon
     flag[threadIdx.x] = 0u;
     __syncthreads();
     for (int k = 0; k < a.nreg; ++k) {
-        const int w = a.w[k];
-        const float* __restrict__ src = a.base[k] + r0 * w;
-        const int span = nr * w;
-        const float inv_w = 1.f / (float)w;
+        const int w = a.w[k], p = a.p[k];
+        const float* __restrict__ src = a.base[k] + r0 * p;
+        const int span = (nr - 1) * p + w;  // (the last row's padding may lie past the allocation)
+        const float inv_p = 1.f / (float)p;
         int e = 0;  // elements below e are done
         if ((reinterpret_cast<uintptr_t>(src) & 15) == 0) {
             const float4* __restrict__ s4 = reinterpret_cast<const float4*>(src);
@@ -58,25 +67,23 @@ __global__ __launch_bounds__(kRowsBlock) void k_rows_live(RowsLaunch a, long lon
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
                     const int j = 4 * (q + u * kRowsBlock);
-                    if (v[u].x != 0.f) flag[row_of(j, w, inv_w)] = 1u;  // (NaN counts, as torch's `!= 0`)
-                    if (v[u].y != 0.f) flag[row_of(j + 1, w, inv_w)] = 1u;
-                    if (v[u].z != 0.f) flag[row_of(j + 2, w, inv_w)] = 1u;
-                    if (v[u].w != 0.f) flag[row_of(j + 3, w, inv_w)] = 1u;
+                    mark_elem(flag, v[u].x, j, p, inv_p, w);
+                    mark_elem(flag, v[u].y, j + 1, p, inv_p, w);
+                    mark_elem(flag, v[u].z, j + 2, p, inv_p, w);
+                    mark_elem(flag, v[u].w, j + 3, p, inv_p, w);
                 }
             }
             for (; q < n4; q += kRowsBlock) {
                 const float4 v = s4[q];
                 const int j = 4 * q;
-                if (v.x != 0.f) flag[row_of(j, w, inv_w)] = 1u;
-                if (v.y != 0.f) flag[row_of(j + 1, w, inv_w)] = 1u;
-                if (v.z != 0.f) flag[row_of(j + 2, w, inv_w)] = 1u;
-                if (v.w != 0.f) flag[row_of(j + 3, w, inv_w)] = 1u;
+                mark_elem(flag, v.x, j, p, inv_p, w);
+                mark_elem(flag, v.y, j + 1, p, inv_p, w);
+                mark_elem(flag, v.z, j + 2, p, inv_p, w);
+                mark_elem(flag, v.w, j + 3, p, inv_p, w);
             }
             e = n4 << 2;
         }
-        for (int j = e + threadIdx.x; j < span; j += kRowsBlock) {
-            if (src[j] != 0.f) flag[row_of(j, w, inv_w)] = 1u;
-        }
+        for (int j = e + threadIdx.x; j < span; j += kRowsBlock) mark_elem(flag, src[j], j, p, inv_p, w);
     }
     __syncthreads();
     if ((int)threadIdx.x < nr) live[r0 + threadIdx.x] = (uint8_t)flag[threadIdx.x];
@@ -105,7 +112,7 @@ __global__ __launch_bounds__(256) void k_rows_move(RowsLaunch a, const long long
 #pragma unroll
         for (int q = 1; q < GS_ROWS_MAX_REGIONS; ++q) k += (c >= a.col0[q]);
         float* __restrict__ col = a.base[k] + (c - a.col0[k]);
-        const int w = a.w[k];
+        const int w = a.p[k];  // (row stride)
         float* __restrict__ out = packed + i0 * a.width + c;
         float v[kRowsPerWave];
         if (GATHER) {
@@ -219,14 +226,17 @@ static int rows_launch(const gs_rows_region* regions, int nreg, RowsLaunch& a, c
     a.nreg = nreg;
     a.col0[0] = 0;
     for (int k = 0; k < nreg; ++k) {
-        if (!regions[k].base || regions[k].width < 1) return report_error(GS_ERR_INVALID_ARG, fn);
+        if (!regions[k].base || regions[k].width < 1 || (regions[k].pitch && regions[k].pitch < regions[k].width))
+            return report_error(GS_ERR_INVALID_ARG, fn);
         a.base[k] = regions[k].base;
         a.w[k] = regions[k].width;
+        a.p[k] = regions[k].pitch ? regions[k].pitch : regions[k].width;
         a.col0[k + 1] = a.col0[k] + regions[k].width;
     }
     for (int k = nreg; k < GS_ROWS_MAX_REGIONS; ++k) {
         a.base[k] = nullptr;
         a.w[k] = 1;
+        a.p[k] = 1;
         a.col0[k + 1] = a.col0[k];
     }
     a.width = a.col0[nreg];
@@ -246,7 +256,7 @@ extern "C" int gs_rows_live(const gs_rows_region* regions, int nreg, long long n
     if (int rc = rows_launch(regions, nreg, a, "gs_rows_live: bad region list")) return rc;
     if (n < 0 || (n > 0 && !live)) return report_error(GS_ERR_INVALID_ARG, "gs_rows_live: bad row count / mask");
     for (int k = 0; k < nreg; ++k)
-        if ((long long)kRowsBlock * a.w[k] >= (1ll << 24))
+        if ((long long)kRowsBlock * a.p[k] >= (1ll << 24))
             return report_error(GS_ERR_INVALID_ARG, "gs_rows_live: region too wide");
     if (n == 0) return GS_OK;
     hipLaunchKernelGGL(k_rows_live, dim3((unsigned)((n + kRowsBlock - 1) / kRowsBlock)), dim3(kRowsBlock), 0,

@@ -75,6 +75,7 @@ class GradBucket:
                 cols[i] = c
                 c += widths[i]
             pitch = max(16, (c + 15) // 16 * 16)
+            self._used = c  # (the columns a parameter owns: the sparse all-reduce packs only these)
             self.flat = torch.zeros(n * pitch, dtype=torch.float32, device=dev)
             self.rows = self.flat.view(n, pitch)
             if self.flat.is_cuda:  # (the rows written since the last zero(): a sparse clear, gs_rows_zero_dirty)
@@ -97,9 +98,10 @@ class GradBucket:
 
     def row_matrices(self):
         """The bucket as [n, width] matrices sharing their rows (the sparse all-reduce's regions), or None:
-        the row-major matrix itself, or each parameter's [n, -1] view of the flat layout."""
+        the row-major matrix's used columns (59 of a GaussianModel's 64-float rows: the padding never
+        travels), or each parameter's [n, -1] view of the flat layout."""
         if self.rows is not None:
-            return [self.rows]
+            return [self.rows[:, :self._used]]
         rows = {v.shape[0] if v.dim() else -1 for v in self.views}
         n = next(iter(rows))
         return [v.reshape(n, -1) for v in self.views] if len(rows) == 1 and n >= 0 else None
@@ -421,7 +423,7 @@ def _rows_fixup(mats, idx, cap, m, group):
 def _native_rows(mats):
     from . import _native as N
 
-    regs = (N.RowsRegion * len(mats))(*[N.RowsRegion(m.data_ptr(), m.shape[1]) for m in mats])
+    regs = (N.RowsRegion * len(mats))(*[N.RowsRegion(m.data_ptr(), m.shape[1], m.stride(0) if m.shape[0] > 1 else 0) for m in mats])
     return N, regs, ctypes.c_void_p(torch.cuda.current_stream(mats[0].device).cuda_stream)
 
 
@@ -429,7 +431,8 @@ def _native_ok(mats):
     from . import _native as N
 
     return (mats[0].is_cuda and len(mats) <= N.ROWS_MAX_REGIONS
-            and all(m.dtype == torch.float32 and m.is_contiguous() for m in mats))
+            and all(m.dtype == torch.float32 and m.dim() == 2 and (m.is_contiguous() or (
+                m.stride(1) == 1 and m.stride(0) >= m.shape[1] and m.stride(0) < 2**31)) for m in mats))
 
 
 def _rows_live(mats, n):

@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define GS_RASTER_ABI_VERSION 20
+#define GS_RASTER_ABI_VERSION 21
 
 #define GS_OK 0
 #define GS_ERR_INVALID_ARG 1   /* AT_ERROR / std::runtime_error in the reference */
@@ -387,10 +387,13 @@ int gs_adam_step(const gs_adam_segment *segs, int nseg, double beta1, double bet
  * GaussianModel's six .grad tensors: 3 + 3 + 45 + 1 + 3 + 4 floats per row). */
 #define GS_ROWS_MAX_REGIONS 8
 typedef struct gs_rows_region {
-    float *base;                  /* [n, width] row-major */
+    float *base;                  /* [n, width] row-major, rows `pitch` floats apart */
     int width;
+    int pitch;                    /* 0: width (dense rows); else >= width (a column block of a wider row,
+                                   * e.g. the 59 used columns of a 64-float bucket row: ABI 21) */
 } gs_rows_region;
-/* live[r] = 1 if row r of some region holds an element != 0 (NaN included), else 0. */
+/* live[r] = 1 if row r of some region holds an element != 0 (NaN included) in its first `width`
+ * columns, else 0. */
 int gs_rows_live(const gs_rows_region *regions, int nreg, long long n, uint8_t *live, gs_stream_t stream);
 /* packed[i, :] = row rows[i] of region 0, then of region 1, ... (m x sum(width)). */
 int gs_rows_gather(const gs_rows_region *regions, int nreg, const long long *rows, long long m, float *packed,

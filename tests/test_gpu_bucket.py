@@ -61,6 +61,33 @@ def test_rows_live_gather_scatter_match_torch(cuda_device, n, widths, density):
         assert torch.equal(m2.cpu().nan_to_num(7.0), exp.nan_to_num(7.0))
 
 
+@pytest.mark.parametrize("n,width,pitch", [(1_000_003, 59, 64), (257, 1, 3), (4099, 13, 16)])
+def test_rows_pitched_region_ignores_padding(cuda_device, n, width, pitch):
+    """A region that is the first `width` columns of `pitch`-float rows (GradBucket.row_matrices: the 59 used
+    columns of a GaussianModel's 64-float bucket row, ABI 21): live marks only rows nonzero in those columns
+    (the padding holds nonzeros here), the gather packs `width` columns, the scatter leaves the padding."""
+    g = torch.Generator(device="cpu").manual_seed(n)
+    full = torch.zeros(n, pitch)
+    rows = torch.rand(n, generator=g) < 0.2
+    full[rows, :width] = torch.randn(int(rows.sum()), width, generator=g)
+    full[:, width:] = 5.0  # padding: never a live mark, never moved
+    full = full.to("cuda")
+    m = full[:, :width]
+    assert mv._native_ok([m]) and not m.is_contiguous()
+    live = mv._rows_live([m], n)
+    assert torch.equal(live.cpu(), rows.to(torch.uint8))
+    idx = torch.nonzero(live).squeeze(1)
+    packed = mv._rows_gather([m], idx)
+    assert packed.shape == (idx.numel(), width)
+    assert torch.equal(packed.cpu(), full.cpu()[idx.cpu(), :width])
+    full2 = torch.full_like(full, 9.0)
+    mv._rows_scatter([full2[:, :width]], idx, packed * 2)
+    torch.cuda.synchronize()
+    exp = torch.full((n, pitch), 9.0)
+    exp[idx.cpu(), :width] = full.cpu()[idx.cpu(), :width] * 2
+    assert torch.equal(full2.cpu(), exp)
+
+
 @pytest.mark.parametrize("cap_over", [-1000, 0, 1, 5000, None])
 def test_rows_gather_scatter_device_count(cuda_device, cap_over):
     """gs_rows_gather_dev / gs_rows_scatter_dev (the speculative-capacity collective): a packed buffer of
